@@ -1,0 +1,167 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ``MulticlassConfusionMatrix(num_classes=1000)`` on batches of 8192 bf16 logits, DDP sync.
+
+BASELINE.json config #2 ("MulticlassConfusionMatrix num_classes=1000, batch=8192 bf16, DDP sync over N x MI355X").
+Metric: metric-updates/sec summed over the node (each rank updates its own metric on its own 8192-row batches;
+weak scaling: per-GPU work is fixed).  The timed region of one run is K ``update`` calls followed by one synced
+``compute()`` (RCCL all-reduce of the 1000x1000 int64 state), bracketed by barrier + ``torch.cuda.synchronize()``;
+the max over ranks is reported.  ``compute_ms`` (sync + compute wall-clock) is measured separately.
+
+The same loop is also run through an op-for-op emulation of the reference implementation (``benchmarks/reference_path.py``)
+on the same data in the same process; ``vs_baseline`` = ours / emulated reference.
+
+Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]`` (N>1: launch with torch.distributed.run).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+NUM_CLASSES = 1000
+BATCH = 8192
+N_BUFFERS = 4
+
+
+def _setup(gpus: int):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if world > 1:
+        backend = "nccl" if device.type == "cuda" else "gloo"
+        dist.init_process_group(backend, rank=rank, world_size=world)
+    return world, rank, device
+
+
+def _barrier_sync(device: torch.device, world: int) -> None:
+    if world > 1:
+        dist.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+
+
+def _max_over_ranks(x: float, device: torch.device, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _data(device: torch.device, rank: int):
+    g = torch.Generator(device="cpu").manual_seed(1234 + rank)
+    preds = [torch.randn(BATCH, NUM_CLASSES, generator=g).to(device=device, dtype=torch.bfloat16) for _ in range(N_BUFFERS)]
+    target = [torch.randint(0, NUM_CLASSES, (BATCH,), generator=g).to(device) for _ in range(N_BUFFERS)]
+    return preds, target
+
+
+def _run(metric, preds, target, steps: int, warmup: int, device, world):
+    for i in range(warmup):
+        metric.update(preds[i % N_BUFFERS], target[i % N_BUFFERS])
+    metric.compute() if hasattr(metric, "_computed") else metric.compute()
+    _reset(metric)
+    _barrier_sync(device, world)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        metric.update(preds[i % N_BUFFERS], target[i % N_BUFFERS])
+    result = metric.compute()
+    _barrier_sync(device, world)
+    elapsed = time.perf_counter() - t0
+    # separate measurement of the synced compute wall-clock
+    _barrier_sync(device, world)
+    c0 = time.perf_counter()
+    reps = 5
+    for _ in range(reps):
+        if hasattr(metric, "_computed"):
+            metric._computed = None
+        result = metric.compute()
+    _barrier_sync(device, world)
+    compute_ms = (time.perf_counter() - c0) / reps * 1e3
+    return elapsed, compute_ms, result
+
+
+def _reset(metric) -> None:
+    if hasattr(metric, "reset"):
+        metric.reset()
+    else:
+        metric.confmat.zero_()
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--no-baseline", action="store_true", help="skip the in-run reference-emulation baseline")
+    args = ap.parse_args()
+
+    world, rank, device = _setup(args.gpus)
+    from torchmetrics_amd.classification import MulticlassConfusionMatrix
+
+    preds, target = _data(device, rank)
+
+    ours = MulticlassConfusionMatrix(num_classes=NUM_CLASSES).to(device)
+    t_ours, cms_ours, res_ours = _run(ours, preds, target, args.steps, args.warmup, device, world)
+    t_ours = _max_over_ranks(t_ours, device, world)
+    cms_ours = _max_over_ranks(cms_ours, device, world)
+
+    base_val = None
+    t_ref = cms_ref = None
+    if not args.no_baseline:
+        from benchmarks.reference_path import ReferenceEmulatedConfusionMatrix
+
+        ref = ReferenceEmulatedConfusionMatrix(NUM_CLASSES, device)
+        t_ref, cms_ref, res_ref = _run(ref, preds, target, args.steps, args.warmup, device, world)
+        t_ref = _max_over_ranks(t_ref, device, world)
+        cms_ref = _max_over_ranks(cms_ref, device, world)
+        if not torch.equal(res_ref.to(res_ours.device), res_ours):
+            raise RuntimeError("benchmark parity failure: confusion matrices differ from the reference emulation")
+        base_val = world * args.steps / t_ref
+
+    value = world * args.steps / t_ours
+    if rank == 0:
+        out = {
+            "metric": "metric-updates/sec (whole node)",
+            "value": round(value, 2),
+            "unit": "updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_ours / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / base_val, 3) if base_val else None,
+            "dtype": "bf16",
+            "data": "synthetic (randn bf16 logits, uniform int64 targets; fixed seeds)",
+            "config": {
+                "model": "MulticlassConfusionMatrix(num_classes=1000)",
+                "global_batch": BATCH * world,
+                "seq_len": 1,
+                "parallelism": f"dp{world}",
+            },
+            "compute_ms": round(cms_ours, 4),
+            "samples_per_s": round(value * BATCH, 1),
+            "baseline": {
+                "impl": "reference torchmetrics 1.4.0dev op sequence (benchmarks/reference_path.py)",
+                "value": round(base_val, 2) if base_val else None,
+                "ms_per_step": round(t_ref / args.steps * 1e3, 4) if t_ref else None,
+                "compute_ms": round(cms_ref, 4) if cms_ref else None,
+            },
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

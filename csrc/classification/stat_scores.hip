@@ -1,0 +1,736 @@
+// Classification statistics kernels: confusion matrices and tp/fp/tn/fn for binary, multiclass and multilabel tasks.
+//
+// Replaces the reference's per-update chain (validation torch.unique + argmax + mask + bincount + diag/sum algebra,
+// F/classification/stat_scores.py:90-131,344-419,647-681; confusion_matrix.py:333-337) with:
+//   update = 1 fused pass over the inputs (argmax / threshold+sigmoid / ignore mask / range validation / histogram)
+//          + 1 tiny finalize launch that folds the batch counts into the metric states and re-zeros the workspace.
+// No host synchronisation anywhere in the update: invalid inputs raise bits in a device flag word.
+//
+// Multiclass argmax rows (C >= 32, X == 1): one wave64 per row, 16-byte vector loads, wave argmax with
+// torch.argmax tie-breaking (first index; NaN wins).  Everything else: one thread per (sample, spatial) item.
+// Small histograms are privatised in LDS (one int32 sub-histogram per block) and flushed with 64-bit atomics.
+#include "../common/tm_common.h"
+
+namespace tm_amd {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kLdsBins = 12288;  // 48 KiB of int32 bins
+
+// ----------------------------------------------------------------------------------------------------------------
+// multiclass: per-item predicted label
+// ----------------------------------------------------------------------------------------------------------------
+enum McMode : int { kMcConfmat = 0, kMcStats = 1 };
+
+template <typename target_t>
+__device__ __forceinline__ bool mc_target(const target_t* __restrict__ target, long long item, int C, long long ignore,
+                                          bool has_ignore, int* flag, int& t_out) {
+  const long long t = static_cast<long long>(target[item]);
+  if (has_ignore && t == ignore) return false;
+  if (t < 0 || t >= C) {
+    raise_flag(flag, kErrTargetOutOfRange);
+    return false;
+  }
+  t_out = static_cast<int>(t);
+  return true;
+}
+
+// accumulate one (target, predicted-set) observation; the K predicted labels are at pidx[0], pidx[pstride], ...
+__device__ __forceinline__ void mc_accumulate(int mode, int t, const int* preds_k, int K, int C, int64_t* out,
+                                              int* lds, bool use_lds, long long group) {
+  if (mode == kMcConfmat) {
+    const long long bin = static_cast<long long>(t) * C + preds_k[0];
+    if (use_lds)
+      atomicAdd(&lds[bin], 1);
+    else
+      atomic_add_i64(out + bin, 1);
+    return;
+  }
+  // stats workspace layout per group: [tp(C) | fp(C) | fn(C) | count]
+  const long long base = group * (3LL * C + 1);
+  bool hit = false;
+  for (int k = 0; k < K; ++k) {
+    const int p = preds_k[k];
+    if (p == t) {
+      hit = true;
+    } else {
+      if (use_lds) atomicAdd(&lds[C + p], 1);
+      else atomic_add_i64(out + base + C + p, 1);
+    }
+  }
+  const long long slot = hit ? t : 2LL * C + t;
+  if (use_lds) {
+    atomicAdd(&lds[slot], 1);
+    atomicAdd(&lds[3 * C], 1);
+  } else {
+    atomic_add_i64(out + base + slot, 1);
+    atomic_add_i64(out + base + 3LL * C, 1);
+  }
+}
+
+__device__ __forceinline__ void lds_flush(int* lds, int nbins, int64_t* out) {
+  __syncthreads();
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
+    const int v = lds[b];
+    if (v) atomic_add_i64(out + b, v);
+  }
+}
+
+// wave-per-row argmax (X == 1). preds: [N, C] row-major. 16-B vector loads when rows are 16-B aligned.
+template <typename scalar_t, typename target_t>
+__global__ void __launch_bounds__(kBlock) mc_argmax_rows_kernel(const scalar_t* __restrict__ preds,
+                                                                const target_t* __restrict__ target, long long N, int C,
+                                                                long long ignore, bool has_ignore, int mode,
+                                                                int64_t* __restrict__ out, int* __restrict__ flag,
+                                                                bool vec, bool samplewise) {
+  extern __shared__ __attribute__((aligned(16))) int lds[];
+  const int nbins = mode == kMcConfmat ? C * C : 3 * C + 1;
+  const bool use_lds = !samplewise && nbins <= kLdsBins && (gridDim.x * (blockDim.x / kWave)) * 4LL <= N;
+  if (use_lds) {
+    for (int b = threadIdx.x; b < nbins; b += blockDim.x) lds[b] = 0;
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & (kWave - 1);
+  const long long wave = (static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
+  const long long nwaves = static_cast<long long>(gridDim.x) * blockDim.x / kWave;
+  constexpr int kVec = 16 / sizeof(scalar_t);
+  for (long long row = wave; row < N; row += nwaves) {
+    const scalar_t* rp = preds + row * C;
+    float best = -INFINITY;
+    int bidx = 0x7fffffff;
+    if (vec) {
+      for (int c0 = lane * kVec; c0 < C; c0 += kWave * kVec) {
+        const uint4 raw = *reinterpret_cast<const uint4*>(rp + c0);
+        const scalar_t* e = reinterpret_cast<const scalar_t*>(&raw);
+#pragma unroll
+        for (int j = 0; j < kVec; ++j) {
+          const float v = to_f32(e[j]);
+          if (argmax_better(v, c0 + j, best, bidx)) {
+            best = v;
+            bidx = c0 + j;
+          }
+        }
+      }
+    } else {
+      for (int c = lane; c < C; c += kWave) {
+        const float v = to_f32(rp[c]);
+        if (argmax_better(v, c, best, bidx)) {
+          best = v;
+          bidx = c;
+        }
+      }
+    }
+    wave_argmax(best, bidx);
+    if (lane == 0) {
+      int t;
+      if (mc_target(target, row, C, ignore, has_ignore, flag, t)) {
+        mc_accumulate(mode, t, &bidx, 1, C, out, lds, use_lds, samplewise ? row : 0);
+      }
+    }
+  }
+  if (use_lds) lds_flush(lds, nbins, out);
+}
+
+// Sub-wave rows: a wave64 handles 64/LPR rows at once, LPR lanes per row. Every lane issues up to kBatch independent
+// 16-byte loads before consuming any (memory-level parallelism instead of one dependent load chain per wave), the
+// row's target is fetched in the same batch, and the argmax is reduced inside the LPR-lane group (log2(LPR)
+// shuffles).  For C = 1000 bf16 (2000 B rows) LPR = 16 gives 8 loads in flight per lane, 4 rows per wave.
+template <typename scalar_t, typename target_t, int LPR>
+__global__ void __launch_bounds__(kBlock) mc_argmax_subwave_kernel(const scalar_t* __restrict__ preds,
+                                                                   const target_t* __restrict__ target, long long N,
+                                                                   int C, long long ignore, bool has_ignore, int mode,
+                                                                   int64_t* __restrict__ out, int* __restrict__ flag,
+                                                                   bool samplewise) {
+  extern __shared__ __attribute__((aligned(16))) int lds[];
+  constexpr int kVec = 16 / sizeof(scalar_t);
+  constexpr int kRowsPerWave = kWave / LPR;
+  constexpr int kBatch = 8;
+  const int nbins = mode == kMcConfmat ? C * C : 3 * C + 1;
+  const long long nwaves = static_cast<long long>(gridDim.x) * (blockDim.x / kWave);
+  const bool use_lds = !samplewise && nbins <= kLdsBins && nwaves * kRowsPerWave * 4LL <= N;
+  if (use_lds) {
+    for (int b = threadIdx.x; b < nbins; b += blockDim.x) lds[b] = 0;
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & (kWave - 1);
+  const int sub = lane / LPR;
+  const int sl = lane - sub * LPR;
+  const long long wave = (static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
+  const int nchunks = C / kVec;
+  for (long long base = wave * kRowsPerWave; base < N; base += nwaves * kRowsPerWave) {  // wave-uniform loop
+    const long long row = base + sub;
+    const bool live = row < N;
+    long long t = 0;
+    if (live && sl == 0) t = static_cast<long long>(target[row]);
+    const u32x4* rp = reinterpret_cast<const u32x4*>(preds + (live ? row : 0) * C);
+    float best = -INFINITY;
+    int bidx = 0x7fffffff;
+    for (int c0 = sl; c0 < nchunks; c0 += LPR * kBatch) {
+      u32x4 buf[kBatch];
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        const int ci = c0 + j * LPR;
+        if (live && ci < nchunks) buf[j] = __builtin_nontemporal_load(rp + ci);
+      }
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        const int ci = c0 + j * LPR;
+        if (live && ci < nchunks) {
+          const scalar_t* e = reinterpret_cast<const scalar_t*>(&buf[j]);
+#pragma unroll
+          for (int k = 0; k < kVec; ++k) {
+            const float v = to_f32(e[k]);
+            const int idx = ci * kVec + k;
+            if (argmax_better(v, idx, best, bidx)) {
+              best = v;
+              bidx = idx;
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int off = LPR / 2; off > 0; off >>= 1) {
+      const float ov = __shfl_xor(best, off, kWave);
+      const int oi = __shfl_xor(bidx, off, kWave);
+      if (argmax_better(ov, oi, best, bidx)) {
+        best = ov;
+        bidx = oi;
+      }
+    }
+    if (live && sl == 0) {
+      bool ok = true;
+      if (has_ignore && t == ignore) ok = false;
+      else if (t < 0 || t >= C) {
+        raise_flag(flag, kErrTargetOutOfRange);
+        ok = false;
+      }
+      if (ok) mc_accumulate(mode, static_cast<int>(t), &bidx, 1, C, out, lds, use_lds, samplewise ? row : 0);
+    }
+  }
+  if (use_lds) lds_flush(lds, nbins, out);
+}
+
+// thread-per-item: preds is either float scores [N, C, X] (argmax over C, stride X) or int labels [N, K, X].
+template <typename scalar_t, typename target_t, bool kArgmax>
+__global__ void __launch_bounds__(kBlock) mc_items_kernel(const scalar_t* __restrict__ preds,
+                                                          const target_t* __restrict__ target, long long N,
+                                                          long long X, int C, int K, long long ignore, bool has_ignore,
+                                                          int mode, int64_t* __restrict__ out, int* __restrict__ flag,
+                                                          bool samplewise) {
+  extern __shared__ __attribute__((aligned(16))) int lds[];
+  const int nbins = mode == kMcConfmat ? C * C : 3 * C + 1;
+  const long long items = N * X;
+  const bool use_lds = !samplewise && nbins <= kLdsBins && static_cast<long long>(gridDim.x) * blockDim.x * 4 <= items;
+  if (use_lds) {
+    for (int b = threadIdx.x; b < nbins; b += blockDim.x) lds[b] = 0;
+    __syncthreads();
+  }
+  int pk[16];
+  for (long long it = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; it < items;
+       it += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const long long n = it / X, x = it - n * X;
+    int t;
+    if (!mc_target(target, it, C, ignore, has_ignore, flag, t)) continue;
+    bool ok = true;
+    if constexpr (kArgmax) {
+      const scalar_t* p = preds + n * C * X + x;
+      float best = to_f32(p[0]);
+      int bidx = 0;
+      for (int c = 1; c < C; ++c) {
+        const float v = to_f32(p[static_cast<long long>(c) * X]);
+        if (argmax_better(v, c, best, bidx)) {
+          best = v;
+          bidx = c;
+        }
+      }
+      pk[0] = bidx;
+    } else {
+      const scalar_t* p = preds + n * K * X + x;
+      if (K == 1) {
+        const long long v = static_cast<long long>(p[0]);
+        ok = v >= 0 && v < C;
+        pk[0] = static_cast<int>(v);
+      } else for (int k = 0; k < K; ++k) {
+        const long long v = static_cast<long long>(p[static_cast<long long>(k) * X]);
+        if (v < 0 || v >= C) {
+          ok = false;
+          break;
+        }
+        pk[k] = static_cast<int>(v);
+      }
+      if (!ok) {
+        raise_flag(flag, kErrPredsOutOfRange);
+        continue;
+      }
+    }
+    mc_accumulate(mode, t, pk, kArgmax ? 1 : K, C, out, lds, use_lds, samplewise ? n : 0);
+  }
+  if (use_lds) lds_flush(lds, nbins, out);
+}
+
+// fold a multiclass stats workspace [G, 3C+1] into the states; optionally micro-reduce over classes.
+// accumulate=true: states += batch ; false: states = batch (samplewise outputs). Re-zeros the workspace.
+__global__ void __launch_bounds__(kBlock) mc_finalize_kernel(int64_t* __restrict__ ws, int C, bool micro,
+                                                             bool accumulate, int64_t* __restrict__ tp,
+                                                             int64_t* __restrict__ fp, int64_t* __restrict__ tn,
+                                                             int64_t* __restrict__ fn) {
+  const long long g = blockIdx.x;
+  int64_t* w = ws + g * (3LL * C + 1);
+  const long long cnt = w[3 * C];
+  __shared__ long long red[3][kBlock / kWave];
+  long long st = 0, sf = 0, sn = 0;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const long long a = w[c], b = w[C + c], d = w[2 * C + c];
+    if (micro) {
+      st += a;
+      sf += b;
+      sn += d;
+    } else {
+      const long long o = g * C + c;
+      const long long e = cnt - a - b - d;
+      if (accumulate) {
+        tp[o] += a; fp[o] += b; fn[o] += d; tn[o] += e;
+      } else {
+        tp[o] = a; fp[o] = b; fn[o] = d; tn[o] = e;
+      }
+    }
+    w[c] = 0;
+    w[C + c] = 0;
+    w[2 * C + c] = 0;
+  }
+  if (micro) {
+    st = wave_sum_ll(st);
+    sf = wave_sum_ll(sf);
+    sn = wave_sum_ll(sn);
+    const int wid = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+    if (lane == 0) {
+      red[0][wid] = st;
+      red[1][wid] = sf;
+      red[2][wid] = sn;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      long long a = 0, b = 0, d = 0;
+      for (int i = 0; i < static_cast<int>(blockDim.x / kWave); ++i) {
+        a += red[0][i];
+        b += red[1][i];
+        d += red[2][i];
+      }
+      const long long e = static_cast<long long>(C) * cnt - a - b - d;
+      if (accumulate) {
+        tp[g] += a; fp[g] += b; fn[g] += d; tn[g] += e;
+      } else {
+        tp[g] = a; fp[g] = b; fn[g] = d; tn[g] = e;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) w[3 * C] = 0;
+}
+
+int pick_grid(long long work_items, int per_block) {
+  return grid_cap((work_items + per_block - 1) / per_block, 256 * 8);
+}
+
+// ----------------------------------------------------------------------------------------------------------------
+// binary / multilabel
+// ----------------------------------------------------------------------------------------------------------------
+// workspace per (group, label): [tpA, fpA, fnA, tpB, fpB, fnB, count]  (A = preds as probabilities,
+// B = preds as logits -> sigmoid).  A per-call "not a probability" word decides between A and B at finalize, which
+// reproduces the reference's `if not torch.all((preds >= 0) * (preds <= 1)): preds = preds.sigmoid()` without a
+// host round trip.
+constexpr int kBinSlots = 7;
+
+template <typename scalar_t>
+__device__ __forceinline__ void bin_pred(scalar_t raw, float thr_t, int* flag, bool& pa, bool& pb, bool& valid) {
+  valid = true;
+  if constexpr (IsFloating<scalar_t>::value) {
+    const float v = to_f32(raw);
+    pa = v > thr_t;
+    const float s = round_to<scalar_t>(1.f / (1.f + __expf(-v)));
+    pb = s > thr_t;
+  } else {
+    const long long v = static_cast<long long>(raw);
+    if (v != 0 && v != 1) {
+      raise_flag(flag, kErrPredsNotBinary);
+      valid = false;
+    }
+    pa = pb = (v == 1);
+  }
+}
+
+__device__ __forceinline__ void bin_slots(bool t, bool pa, bool pb, int& sa, int& sb) {
+  // tp=0 fp=1 fn=2 (tn implicit); -1 = tn
+  sa = t ? (pa ? 0 : 2) : (pa ? 1 : -1);
+  sb = t ? (pb ? 3 : 5) : (pb ? 4 : -1);
+}
+
+// flat kernel: elements of preds [N, L, X] visited in memory order; group = samplewise ? n*L + l : l
+template <typename scalar_t, typename target_t>
+__global__ void __launch_bounds__(kBlock) bin_flat_kernel(const scalar_t* __restrict__ preds,
+                                                          const target_t* __restrict__ target, long long total,
+                                                          long long L, long long X, float thr_t, long long ignore,
+                                                          bool has_ignore, bool samplewise, int64_t* __restrict__ ws,
+                                                          int* __restrict__ flag, int* __restrict__ not_prob,
+                                                          bool prob_check_all) {
+  extern __shared__ __attribute__((aligned(16))) int lds[];
+  const long long nbins = L * kBinSlots;
+  const bool use_lds = !samplewise && nbins <= kLdsBins && static_cast<long long>(gridDim.x) * blockDim.x * 4 <= total;
+  if (use_lds) {
+    for (int b = threadIdx.x; b < nbins; b += blockDim.x) lds[b] = 0;
+    __syncthreads();
+  }
+  int local_not_prob = 0;
+  for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const long long tv = static_cast<long long>(target[i]);
+    const long long nl = i / X;  // n*L + l
+    const long long l = nl % L;
+    bool pa, pb, valid;
+    // stat scores decide logits-vs-probabilities over ALL preds (ignored positions included); the binary
+    // confusion matrix decides after dropping ignored positions (reference F/classification/confusion_matrix.py)
+    const bool ignored = has_ignore && tv == ignore;
+    if constexpr (IsFloating<scalar_t>::value) {
+      const float v = to_f32(preds[i]);
+      if (!(v >= 0.f && v <= 1.f) && (prob_check_all || !ignored)) local_not_prob = 1;
+    }
+    if (ignored) continue;
+    if (tv != 0 && tv != 1) {
+      raise_flag(flag, kErrTargetNotBinary);
+      continue;
+    }
+    bin_pred<scalar_t>(preds[i], thr_t, flag, pa, pb, valid);
+    if (!valid) continue;
+    int sa, sb;
+    bin_slots(tv == 1, pa, pb, sa, sb);
+    const long long g = samplewise ? nl : l;
+    if (use_lds) {
+      int* h = lds + l * kBinSlots;
+      if (sa >= 0) atomicAdd(h + sa, 1);
+      if (sb >= 0) atomicAdd(h + sb, 1);
+      atomicAdd(h + 6, 1);
+    } else {
+      int64_t* h = ws + g * kBinSlots;
+      if (sa >= 0) atomic_add_i64(h + sa, 1);
+      if (sb >= 0) atomic_add_i64(h + sb, 1);
+      atomic_add_i64(h + 6, 1);
+    }
+  }
+  if (IsFloating<scalar_t>::value) {
+    if (__any(local_not_prob) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(not_prob, 1);
+  }
+  if (use_lds) {
+    __syncthreads();
+    for (long long b = threadIdx.x; b < nbins; b += blockDim.x) {
+      const int v = lds[b];
+      if (v) atomic_add_i64(ws + b, v);
+    }
+  }
+}
+
+// segment kernel for long contiguous segments (X large): block = one chunk of one (n, l) segment, register
+// accumulation + block reduction, 7 atomics per block.
+template <typename scalar_t, typename target_t>
+__global__ void __launch_bounds__(kBlock) bin_seg_kernel(const scalar_t* __restrict__ preds,
+                                                         const target_t* __restrict__ target, long long nseg,
+                                                         long long L, long long X, long long chunk, float thr_t,
+                                                         long long ignore, bool has_ignore, bool samplewise,
+                                                         int64_t* __restrict__ ws, int* __restrict__ flag,
+                                                         int* __restrict__ not_prob, bool prob_check_all) {
+  const long long chunks_per_seg = (X + chunk - 1) / chunk;
+  const long long seg = blockIdx.x / chunks_per_seg;
+  const long long cidx = blockIdx.x - seg * chunks_per_seg;
+  if (seg >= nseg) return;
+  const long long beg = cidx * chunk, end = min(X, beg + chunk);
+  const scalar_t* p = preds + seg * X;
+  const target_t* t = target + seg * X;
+  long long acc[kBinSlots] = {0, 0, 0, 0, 0, 0, 0};
+  int local_not_prob = 0;
+  for (long long x = beg + threadIdx.x; x < end; x += blockDim.x) {
+    const long long tv = static_cast<long long>(t[x]);
+    const bool ignored = has_ignore && tv == ignore;
+    if constexpr (IsFloating<scalar_t>::value) {
+      const float v = to_f32(p[x]);
+      if (!(v >= 0.f && v <= 1.f) && (prob_check_all || !ignored)) local_not_prob = 1;
+    }
+    if (ignored) continue;
+    if (tv != 0 && tv != 1) {
+      raise_flag(flag, kErrTargetNotBinary);
+      continue;
+    }
+    bool pa, pb, valid;
+    bin_pred<scalar_t>(p[x], thr_t, flag, pa, pb, valid);
+    if (!valid) continue;
+    int sa, sb;
+    bin_slots(tv == 1, pa, pb, sa, sb);
+#pragma unroll
+    for (int s = 0; s < 6; ++s) acc[s] += (s == sa) + (s == sb);
+    acc[6] += 1;
+  }
+  if (IsFloating<scalar_t>::value) {
+    if (__any(local_not_prob) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(not_prob, 1);
+  }
+  __shared__ long long red[kBinSlots][kBlock / kWave];
+  const int wid = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+#pragma unroll
+  for (int s = 0; s < kBinSlots; ++s) {
+    const long long v = wave_sum_ll(acc[s]);
+    if (lane == 0) red[s][wid] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kBinSlots) {
+    long long v = 0;
+    for (int w = 0; w < static_cast<int>(blockDim.x / kWave); ++w) v += red[threadIdx.x][w];
+    const long long g = samplewise ? seg : seg % L;
+    if (v) atomic_add_i64(ws + g * kBinSlots + threadIdx.x, v);
+  }
+}
+
+// states (per group g): accumulate or write tp/fp/tn/fn; picks interpretation A/B from not_prob; zeros ws + flag.
+__global__ void __launch_bounds__(kBlock) bin_finalize_kernel(int64_t* __restrict__ ws, long long G,
+                                                              int* __restrict__ not_prob, bool accumulate,
+                                                              int64_t* __restrict__ tp, int64_t* __restrict__ fp,
+                                                              int64_t* __restrict__ tn, int64_t* __restrict__ fn) {
+  const bool use_b = *not_prob != 0;
+  for (long long g = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; g < G;
+       g += static_cast<long long>(gridDim.x) * blockDim.x) {
+    int64_t* w = ws + g * kBinSlots;
+    const long long a = use_b ? w[3] : w[0];
+    const long long b = use_b ? w[4] : w[1];
+    const long long d = use_b ? w[5] : w[2];
+    const long long e = w[6] - a - b - d;
+    if (accumulate) {
+      tp[g] += a; fp[g] += b; fn[g] += d; tn[g] += e;
+    } else {
+      tp[g] = a; fp[g] = b; fn[g] = d; tn[g] = e;
+    }
+#pragma unroll
+    for (int s = 0; s < kBinSlots; ++s) w[s] = 0;
+  }
+}
+
+// binary / multilabel confusion matrices [G, 2, 2] (rows = target, cols = pred) accumulated in place
+__global__ void __launch_bounds__(kBlock) bin_confmat_finalize_kernel(int64_t* __restrict__ ws, long long G,
+                                                                      const int* __restrict__ not_prob,
+                                                                      int64_t* __restrict__ confmat) {
+  const bool use_b = *not_prob != 0;
+  for (long long g = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; g < G;
+       g += static_cast<long long>(gridDim.x) * blockDim.x) {
+    int64_t* w = ws + g * kBinSlots;
+    const long long tp = use_b ? w[3] : w[0];
+    const long long fp = use_b ? w[4] : w[1];
+    const long long fn = use_b ? w[5] : w[2];
+    const long long tn = w[6] - tp - fp - fn;
+    int64_t* c = confmat + g * 4;
+    c[0] += tn;
+    c[1] += fp;
+    c[2] += fn;
+    c[3] += tp;
+#pragma unroll
+    for (int s = 0; s < kBinSlots; ++s) w[s] = 0;
+  }
+}
+
+// reset of the per-call logit flag is ordered after the finalize (same stream)
+__global__ void zero_int_kernel(int* p) { *p = 0; }
+
+}  // namespace
+
+// ================================================================================================================
+// host launchers
+// ================================================================================================================
+
+// Multiclass update.
+//   preds: float [N, C, X] (argmax) or int [N, K, X] labels
+//   target: int [N, X]
+//   mode 0: out = confmat [C, C] int64 (accumulated in place)
+//   mode 1: out = workspace [G, 3C+1] int64 (G = N if samplewise else 1); finalize with mc_stats_finalize
+void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out, at::Tensor flag, int64_t num_classes,
+               int64_t ignore_index, bool has_ignore, int64_t mode, bool samplewise) {
+  TM_CHECK_CUDA(preds);
+  TM_CHECK_CUDA(target);
+  TM_CHECK_CONTIG(preds);
+  TM_CHECK_CONTIG(target);
+  TM_CHECK_CONTIG(out);
+  TORCH_CHECK(out.scalar_type() == at::kLong, "mc_update: out must be int64");
+  TORCH_CHECK(flag.scalar_type() == at::kInt && flag.numel() >= 1, "mc_update: flag must be int32[1]");
+  const int C = static_cast<int>(num_classes);
+  const bool argmax = preds.is_floating_point();
+  const long long N = target.numel() == 0 ? 0 : target.size(0);
+  if (N == 0) return;
+  const long long X = target.numel() / N;
+  TORCH_CHECK(mode == kMcConfmat || mode == kMcStats, "mc_update: bad mode");
+  if (mode == kMcConfmat) {
+    TORCH_CHECK(out.numel() == static_cast<long long>(C) * C, "mc_update: confmat must have C*C elements");
+  } else {
+    TORCH_CHECK(out.numel() == (samplewise ? N : 1) * (3LL * C + 1), "mc_update: workspace has wrong size");
+  }
+  long long K = 1;
+  if (argmax) {
+    TORCH_CHECK(preds.numel() == N * C * X, "mc_update: preds must be [N, C, ...] matching target");
+  } else {
+    TORCH_CHECK(preds.numel() % (N * X) == 0, "mc_update: label preds must be [N, K, ...]");
+    K = preds.numel() / (N * X);
+    TORCH_CHECK(K >= 1 && K <= 16, "mc_update: at most 16 predicted labels per item");
+    TORCH_CHECK(mode == kMcStats || K == 1, "mc_update: confmat needs exactly one predicted label");
+  }
+  const int nbins = mode == kMcConfmat ? C * C : 3 * C + 1;
+  const size_t lds_bytes = (!samplewise && nbins <= kLdsBins) ? nbins * sizeof(int) : 0;
+  auto s = stream();
+  int64_t* outp = out.data_ptr<int64_t>();
+  int* flagp = flag.data_ptr<int>();
+  TM_DISPATCH_TARGET(target.scalar_type(), "mc_update", [&] {
+    const target_t* tp = reinterpret_cast<const target_t*>(target.data_ptr());
+    TM_DISPATCH_PREDS(preds.scalar_type(), "mc_update", [&] {
+      const scalar_t* pp = reinterpret_cast<const scalar_t*>(preds.data_ptr());
+      if constexpr (IsFloating<scalar_t>::value) {
+        const bool vec = (C * sizeof(scalar_t)) % 16 == 0 && (reinterpret_cast<uintptr_t>(pp) % 16) == 0;
+        if (X == 1 && C >= 32 && vec) {
+          // rows of <= 16 lanes x 8 loads x 16 B go 16 lanes per row; longer rows use the whole wave per row
+          const long long row_bytes = static_cast<long long>(C) * sizeof(scalar_t);
+          if (row_bytes <= 16LL * 8 * 16) {
+            constexpr int LPR = 16;
+            const int grid = pick_grid(N, (kBlock / kWave) * (kWave / LPR));
+            hipLaunchKernelGGL((mc_argmax_subwave_kernel<scalar_t, target_t, LPR>), dim3(grid), dim3(kBlock),
+                               lds_bytes, s, pp, tp, N, C, ignore_index, has_ignore, static_cast<int>(mode), outp,
+                               flagp, samplewise);
+          } else {
+            constexpr int LPR = 64;
+            const int grid = pick_grid(N, kBlock / kWave);
+            hipLaunchKernelGGL((mc_argmax_subwave_kernel<scalar_t, target_t, LPR>), dim3(grid), dim3(kBlock),
+                               lds_bytes, s, pp, tp, N, C, ignore_index, has_ignore, static_cast<int>(mode), outp,
+                               flagp, samplewise);
+          }
+        } else if (X == 1 && C >= 32) {
+          const int waves_per_block = kBlock / kWave;
+          const int grid = pick_grid(N, waves_per_block);
+          hipLaunchKernelGGL((mc_argmax_rows_kernel<scalar_t, target_t>), dim3(grid), dim3(kBlock), lds_bytes, s, pp,
+                             tp, N, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, vec, samplewise);
+        } else {
+          const int grid = pick_grid(N * X, kBlock);
+          hipLaunchKernelGGL((mc_items_kernel<scalar_t, target_t, true>), dim3(grid), dim3(kBlock), lds_bytes, s, pp,
+                             tp, N, X, C, 1, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, samplewise);
+        }
+      } else {
+        const int grid = pick_grid(N * X, kBlock);
+        hipLaunchKernelGGL((mc_items_kernel<scalar_t, target_t, false>), dim3(grid), dim3(kBlock), lds_bytes, s, pp,
+                           tp, N, X, C, static_cast<int>(K), ignore_index, has_ignore, static_cast<int>(mode), outp,
+                           flagp, samplewise);
+      }
+    });
+  });
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+void mc_stats_finalize(at::Tensor ws, int64_t num_classes, bool micro, bool accumulate, at::Tensor tp, at::Tensor fp,
+                       at::Tensor tn, at::Tensor fn) {
+  const int C = static_cast<int>(num_classes);
+  const long long G = ws.numel() / (3LL * C + 1);
+  for (auto* t : {&tp, &fp, &tn, &fn}) {
+    TORCH_CHECK(t->scalar_type() == at::kLong && t->is_contiguous(), "mc_stats_finalize: states must be int64");
+    TORCH_CHECK(t->numel() == (micro ? G : G * C), "mc_stats_finalize: state size mismatch");
+  }
+  hipLaunchKernelGGL(mc_finalize_kernel, dim3(G), dim3(kBlock), 0, stream(), ws.data_ptr<int64_t>(), C, micro,
+                     accumulate, tp.data_ptr<int64_t>(), fp.data_ptr<int64_t>(), tn.data_ptr<int64_t>(),
+                     fn.data_ptr<int64_t>());
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+// Binary / multilabel update. preds, target: [N, L, X] (same numel). ws: [G, 7] int64 with G = N*L (samplewise)
+// or L.  not_prob: int32[1] per-call flag (zeroed by finalize).
+void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws, at::Tensor flag, at::Tensor not_prob,
+                int64_t num_labels, double threshold, int64_t ignore_index, bool has_ignore, bool samplewise,
+                bool prob_check_all) {
+  TM_CHECK_CUDA(preds);
+  TM_CHECK_CUDA(target);
+  TM_CHECK_CONTIG(preds);
+  TM_CHECK_CONTIG(target);
+  TORCH_CHECK(preds.numel() == target.numel(), "bin_update: preds/target numel mismatch");
+  const long long total = preds.numel();
+  if (total == 0) return;
+  const long long N = preds.size(0);
+  const long long L = num_labels;
+  TORCH_CHECK(total % (N * L) == 0, "bin_update: shape must be [N, L, ...]");
+  const long long X = total / (N * L);
+  const long long G = samplewise ? N * L : L;
+  TORCH_CHECK(ws.numel() == G * kBinSlots && ws.scalar_type() == at::kLong, "bin_update: bad workspace");
+  auto s = stream();
+  TM_DISPATCH_TARGET(target.scalar_type(), "bin_update", [&] {
+    const target_t* tp = reinterpret_cast<const target_t*>(target.data_ptr());
+    TM_DISPATCH_PREDS(preds.scalar_type(), "bin_update", [&] {
+      const scalar_t* pp = reinterpret_cast<const scalar_t*>(preds.data_ptr());
+      float thr_t = static_cast<float>(threshold);
+      if constexpr (std::is_same<scalar_t, c10::BFloat16>::value) thr_t = static_cast<float>(c10::BFloat16(thr_t));
+      if constexpr (std::is_same<scalar_t, c10::Half>::value) thr_t = static_cast<float>(c10::Half(thr_t));
+      if (X >= 1024) {
+        const long long chunk = 16384;
+        const long long nseg = N * L;
+        const long long blocks = nseg * ((X + chunk - 1) / chunk);
+        TORCH_CHECK(blocks < (1LL << 31), "bin_update: too many segments");
+        hipLaunchKernelGGL((bin_seg_kernel<scalar_t, target_t>), dim3(blocks), dim3(kBlock), 0, s, pp, tp, nseg, L, X,
+                           chunk, thr_t, ignore_index, has_ignore, samplewise, ws.data_ptr<int64_t>(),
+                           flag.data_ptr<int>(), not_prob.data_ptr<int>(), prob_check_all);
+      } else {
+        const long long nbins = L * kBinSlots;
+        const size_t lds_bytes = (!samplewise && nbins <= kLdsBins) ? nbins * sizeof(int) : 0;
+        const int grid = pick_grid(total, kBlock * 4);
+        hipLaunchKernelGGL((bin_flat_kernel<scalar_t, target_t>), dim3(grid), dim3(kBlock), lds_bytes, s, pp, tp,
+                           total, L, X, thr_t, ignore_index, has_ignore, samplewise, ws.data_ptr<int64_t>(),
+                           flag.data_ptr<int>(), not_prob.data_ptr<int>(), prob_check_all);
+      }
+    });
+  });
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+void bin_stats_finalize(at::Tensor ws, at::Tensor not_prob, bool accumulate, at::Tensor tp, at::Tensor fp,
+                        at::Tensor tn, at::Tensor fn) {
+  const long long G = ws.numel() / kBinSlots;
+  for (auto* t : {&tp, &fp, &tn, &fn})
+    TORCH_CHECK(t->scalar_type() == at::kLong && t->is_contiguous() && t->numel() == G,
+                "bin_stats_finalize: states must be contiguous int64 with G elements");
+  auto s = stream();
+  hipLaunchKernelGGL(bin_finalize_kernel, dim3(grid_cap((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                     ws.data_ptr<int64_t>(), G, not_prob.data_ptr<int>(), accumulate, tp.data_ptr<int64_t>(),
+                     fp.data_ptr<int64_t>(), tn.data_ptr<int64_t>(), fn.data_ptr<int64_t>());
+  hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+void bin_confmat_finalize(at::Tensor ws, at::Tensor not_prob, at::Tensor confmat) {
+  const long long G = ws.numel() / kBinSlots;
+  TORCH_CHECK(confmat.scalar_type() == at::kLong && confmat.is_contiguous() && confmat.numel() == 4 * G,
+              "bin_confmat_finalize: confmat must be contiguous int64 [G, 2, 2]");
+  auto s = stream();
+  hipLaunchKernelGGL(bin_confmat_finalize_kernel, dim3(grid_cap((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                     ws.data_ptr<int64_t>(), G, not_prob.data_ptr<int>(), confmat.data_ptr<int64_t>());
+  hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+}  // namespace tm_amd
+
+TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def(
+      "mc_update(Tensor preds, Tensor target, Tensor(a!) out, Tensor(b!) flag, int num_classes, int ignore_index, "
+      "bool has_ignore, int mode, bool samplewise) -> ()");
+  m.def(
+      "mc_stats_finalize(Tensor(a!) ws, int num_classes, bool micro, bool accumulate, Tensor(b!) tp, Tensor(c!) fp, "
+      "Tensor(d!) tn, Tensor(e!) fn) -> ()");
+  m.def(
+      "bin_update(Tensor preds, Tensor target, Tensor(a!) ws, Tensor(b!) flag, Tensor(c!) not_prob, int num_labels, "
+      "float threshold, int ignore_index, bool has_ignore, bool samplewise, bool prob_check_all) -> ()");
+  m.def("bin_confmat_finalize(Tensor(a!) ws, Tensor(b!) not_prob, Tensor(c!) confmat) -> ()");
+  m.def(
+      "bin_stats_finalize(Tensor(a!) ws, Tensor(b!) not_prob, bool accumulate, Tensor(c!) tp, Tensor(d!) fp, "
+      "Tensor(e!) tn, Tensor(f!) fn) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
+  m.impl("mc_update", &tm_amd::mc_update);
+  m.impl("mc_stats_finalize", &tm_amd::mc_stats_finalize);
+  m.impl("bin_update", &tm_amd::bin_update);
+  m.impl("bin_stats_finalize", &tm_amd::bin_stats_finalize);
+  m.impl("bin_confmat_finalize", &tm_amd::bin_confmat_finalize);
+}

@@ -1,0 +1,182 @@
+// Shared device helpers for the torchmetrics_amd HIP kernels (gfx950 / CDNA4, wave64).
+//
+// Conventions used by every kernel in csrc/:
+//   * wave = 64 lanes; blocks are multiples of 64 threads; lane = threadIdx.x & 63.
+//   * validation failures are OR-ed into a per-metric int32 flag word (bits in validation.h); the host reads it
+//     lazily at compute() instead of synchronising on every update.
+//   * integer state accumulation uses 64-bit global atomics (order independent -> deterministic results).
+#pragma once
+
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/util/BFloat16.h>
+#include <c10/util/Half.h>
+#include <hip/hip_runtime.h>
+#include <torch/library.h>
+
+#include <cstdint>
+
+namespace tm_amd {
+
+constexpr int kWave = 64;
+
+// native 16-byte vector (usable with __builtin_nontemporal_load, unlike HIP's uint4 class)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// --------------------------------------------------------------------------------------------- validation bits
+// keep in sync with torchmetrics_amd/utils/validation.py
+constexpr int kErrTargetOutOfRange = 1 << 0;
+constexpr int kErrPredsOutOfRange = 1 << 1;
+constexpr int kErrTargetNotBinary = 1 << 2;
+constexpr int kErrPredsNotBinary = 1 << 3;
+constexpr int kErrPredsNan = 1 << 4;
+constexpr int kErrValueNan = 1 << 5;
+constexpr int kErrNegValue = 1 << 6;
+
+// ------------------------------------------------------------------------------------------------ type helpers
+template <typename T>
+__device__ __forceinline__ float to_f32(T v) {
+  return static_cast<float>(v);
+}
+template <>
+__device__ __forceinline__ float to_f32<c10::BFloat16>(c10::BFloat16 v) {
+  return __uint_as_float(static_cast<uint32_t>(v.x) << 16);
+}
+template <>
+__device__ __forceinline__ float to_f32<c10::Half>(c10::Half v) {
+  return __half2float(*reinterpret_cast<const __half*>(&v));
+}
+
+// round an fp32 value to storage type T and back (emulates ATen computing in fp32 and storing in T)
+template <typename T>
+__device__ __forceinline__ float round_to(float v) {
+  return v;
+}
+template <>
+__device__ __forceinline__ float round_to<c10::BFloat16>(float v) {
+  // round-to-nearest-even, NaN preserved (same as c10::BFloat16 conversion)
+  uint32_t u = __float_as_uint(v);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return v;
+  uint32_t lsb = (u >> 16) & 1u;
+  u += 0x7fffu + lsb;
+  return __uint_as_float(u & 0xffff0000u);
+}
+template <>
+__device__ __forceinline__ float round_to<c10::Half>(float v) {
+  return __half2float(__float2half(v));
+}
+template <>
+__device__ __forceinline__ float round_to<double>(float v) {
+  return v;
+}
+
+template <typename T>
+struct IsFloating {
+  static constexpr bool value = false;
+};
+template <>
+struct IsFloating<float> {
+  static constexpr bool value = true;
+};
+template <>
+struct IsFloating<double> {
+  static constexpr bool value = true;
+};
+template <>
+struct IsFloating<c10::Half> {
+  static constexpr bool value = true;
+};
+template <>
+struct IsFloating<c10::BFloat16> {
+  static constexpr bool value = true;
+};
+
+// ------------------------------------------------------------------------------------------ wave reductions
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+__device__ __forceinline__ long long wave_sum_ll(long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// argmax combine with torch.argmax semantics: NaN wins, then larger value, then smaller index
+__device__ __forceinline__ bool argmax_better(float va, int ia, float vb, int ib) {
+  const bool na = va != va, nb = vb != vb;
+  if (na != nb) return na;
+  if (na && nb) return ia < ib;
+  if (va != vb) return va > vb;
+  return ia < ib;
+}
+
+__device__ __forceinline__ void wave_argmax(float& v, int& i) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float ov = __shfl_xor(v, off, kWave);
+    const int oi = __shfl_xor(i, off, kWave);
+    if (argmax_better(ov, oi, v, i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+}
+
+__device__ __forceinline__ void atomic_add_i64(int64_t* p, long long v) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(p), static_cast<unsigned long long>(v));
+}
+
+__device__ __forceinline__ void raise_flag(int* flag, int bit) { atomicOr(flag, bit); }
+
+inline int grid_cap(long long blocks, int cap = 256 * 16) {
+  return static_cast<int>(blocks < cap ? (blocks < 1 ? 1 : blocks) : cap);
+}
+
+inline hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+#define TM_CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a ROCm (cuda) tensor")
+#define TM_CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+
+// Dispatch over the element types a metric input can have (floating: f32/f16/bf16/f64; integral: i64/i32/u8/bool)
+#define TM_DISPATCH_PREDS(dtype, NAME, ...)                                     \
+  [&] {                                                                          \
+    switch (dtype) {                                                             \
+      case at::kFloat: { using scalar_t = float; return __VA_ARGS__(); }         \
+      case at::kHalf: { using scalar_t = c10::Half; return __VA_ARGS__(); }      \
+      case at::kBFloat16: { using scalar_t = c10::BFloat16; return __VA_ARGS__(); } \
+      case at::kDouble: { using scalar_t = double; return __VA_ARGS__(); }       \
+      case at::kLong: { using scalar_t = int64_t; return __VA_ARGS__(); }        \
+      case at::kInt: { using scalar_t = int32_t; return __VA_ARGS__(); }         \
+      case at::kByte: { using scalar_t = uint8_t; return __VA_ARGS__(); }        \
+      case at::kBool: { using scalar_t = uint8_t; return __VA_ARGS__(); }        \
+      default: TORCH_CHECK(false, NAME ": unsupported preds dtype ", dtype);     \
+    }                                                                            \
+  }()
+
+#define TM_DISPATCH_TARGET(dtype, NAME, ...)                                    \
+  [&] {                                                                          \
+    switch (dtype) {                                                             \
+      case at::kLong: { using target_t = int64_t; return __VA_ARGS__(); }        \
+      case at::kInt: { using target_t = int32_t; return __VA_ARGS__(); }         \
+      case at::kByte: { using target_t = uint8_t; return __VA_ARGS__(); }        \
+      case at::kBool: { using target_t = uint8_t; return __VA_ARGS__(); }        \
+      default: TORCH_CHECK(false, NAME ": unsupported target dtype ", dtype);    \
+    }                                                                            \
+  }()
+
+#define TM_DISPATCH_FLOAT(dtype, NAME, ...)                                     \
+  [&] {                                                                          \
+    switch (dtype) {                                                             \
+      case at::kFloat: { using scalar_t = float; return __VA_ARGS__(); }         \
+      case at::kHalf: { using scalar_t = c10::Half; return __VA_ARGS__(); }      \
+      case at::kBFloat16: { using scalar_t = c10::BFloat16; return __VA_ARGS__(); } \
+      case at::kDouble: { using scalar_t = double; return __VA_ARGS__(); }       \
+      default: TORCH_CHECK(false, NAME ": unsupported float dtype ", dtype);     \
+    }                                                                            \
+  }()
+
+}  // namespace tm_amd

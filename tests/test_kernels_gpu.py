@@ -1,0 +1,129 @@
+"""Numerics of the HIP kernels vs the CPU (ATen) implementation of the same op contract.
+
+Every case runs the GPU op and the CPU op on identical inputs and requires identical integer results.
+"""
+import pytest
+import torch
+
+from torchmetrics_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _flag(dev):
+    return torch.zeros(1, dtype=torch.int32, device=dev)
+
+
+def _mc(preds, target, C, ignore, mode, samplewise, dev):
+    N = target.shape[0]
+    if mode == ops.MC_CONFMAT:
+        out = torch.zeros(C * C, dtype=torch.int64, device=dev)
+    else:
+        out = torch.zeros((N if samplewise else 1) * (3 * C + 1), dtype=torch.int64, device=dev)
+    flag = _flag(dev)
+    ops.mc_update(preds.to(dev), target.to(dev), out, flag, C, ignore, mode, samplewise)
+    return out.cpu(), int(flag.item())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(257, 5), (1000, 64), (333, 1000), (64, 37), (8, 6, 7), (4, 130, 9)])
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("ignore", [None, 0, -1])
+def test_multiclass_argmax(dtype, shape, mode, ignore):
+    C = shape[1]
+    preds = torch.randn(*shape).to(dtype)
+    target = torch.randint(0, C, (shape[0], *shape[2:]))
+    if ignore is not None:
+        target[::7] = ignore
+    g, fg = _mc(preds, target, C, ignore, mode, False, DEV)
+    c, fc = _mc(preds, target, C, ignore, mode, False, "cpu")
+    assert torch.equal(g, c)
+    assert fg == fc == 0
+
+
+@pytest.mark.parametrize("K", [1, 3])
+@pytest.mark.parametrize("samplewise", [False, True])
+def test_multiclass_labels(K, samplewise):
+    C, N, X = 7, 50, 4
+    preds = torch.stack([torch.randperm(C)[:K] for _ in range(N * X)]).view(N, X, K).permute(0, 2, 1).contiguous()
+    target = torch.randint(0, C, (N, X))
+    g, _ = _mc(preds, target, C, None, ops.MC_STATS, samplewise, DEV)
+    c, _ = _mc(preds, target, C, None, ops.MC_STATS, samplewise, "cpu")
+    assert torch.equal(g, c)
+
+
+def test_multiclass_argmax_ties_and_nan():
+    preds = torch.zeros(128, 40)
+    preds[:, 3] = 1.0
+    preds[:, 17] = 1.0  # tie -> first index
+    preds[5, 30] = float("nan")  # NaN wins like torch.argmax
+    target = torch.randint(0, 40, (128,))
+    g, _ = _mc(preds, target, 40, None, ops.MC_CONFMAT, False, DEV)
+    c, _ = _mc(preds, target, 40, None, ops.MC_CONFMAT, False, "cpu")
+    assert torch.equal(g, c)
+
+
+def test_multiclass_flags_out_of_range():
+    preds = torch.randn(100, 5)
+    target = torch.randint(0, 5, (100,))
+    target[3] = 9
+    g, fg = _mc(preds, target, 5, None, ops.MC_CONFMAT, False, DEV)
+    c, fc = _mc(preds, target, 5, None, ops.MC_CONFMAT, False, "cpu")
+    assert torch.equal(g, c)
+    assert fg == fc != 0
+
+
+def _bin(preds, target, L, thr, ignore, samplewise, dev, prob_check_all=True):
+    N = preds.shape[0]
+    G = N * L if samplewise else L
+    ws = torch.zeros(G * 7, dtype=torch.int64, device=dev)
+    np_ = torch.zeros(1, dtype=torch.int32, device=dev)
+    flag = _flag(dev)
+    ops.bin_update(preds.to(dev), target.to(dev), ws, flag, np_, L, thr, ignore, samplewise, prob_check_all)
+    outs = [torch.zeros(G, dtype=torch.int64, device=dev) for _ in range(4)]
+    ops.bin_stats_finalize(ws, np_, True, *outs)
+    return torch.stack([o.cpu() for o in outs]), int(flag.item())
+
+
+@pytest.mark.parametrize("kind", ["prob", "logit", "int"])
+@pytest.mark.parametrize("shape,L", [((1000,), 1), ((64, 9), 9), ((16, 3, 2000), 3), ((8, 2, 5), 2)])
+@pytest.mark.parametrize("samplewise", [False, True])
+@pytest.mark.parametrize("ignore", [None, -1])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_binary_like(kind, shape, L, samplewise, ignore, dtype):
+    if kind == "prob":
+        preds = torch.rand(*shape).to(dtype)
+    elif kind == "logit":
+        preds = (torch.randn(*shape) * 3).to(dtype)
+    else:
+        preds = torch.randint(0, 2, shape)
+    target = torch.randint(0, 2, shape)
+    if ignore is not None:
+        target.view(-1)[::5] = ignore
+    g, fg = _bin(preds, target, L, 0.5, ignore, samplewise, DEV)
+    c, fc = _bin(preds, target, L, 0.5, ignore, samplewise, "cpu")
+    assert torch.equal(g, c)
+    assert fg == fc
+
+
+def test_binary_confmat_prob_check_excludes_ignored():
+    preds = torch.rand(300)
+    target = torch.randint(0, 2, (300,))
+    preds[0] = 5.0  # out of [0,1] but ignored -> stays probability interpretation
+    target[0] = -1
+    dev_res = []
+    for dev in (DEV, "cpu"):
+        ws = torch.zeros(7, dtype=torch.int64, device=dev)
+        np_ = torch.zeros(1, dtype=torch.int32, device=dev)
+        cm = torch.zeros(2, 2, dtype=torch.int64, device=dev)
+        ops.bin_update(preds.to(dev), target.to(dev), ws, _flag(dev), np_, 1, 0.5, -1, False, False)
+        ops.bin_confmat_finalize(ws, np_, cm)
+        dev_res.append(cm.cpu())
+    assert torch.equal(dev_res[0], dev_res[1])
+
+
+@pytest.mark.parametrize("n,bins", [(10000, 37), (100000, 20000), (5, 3)])
+def test_histogram(n, bins):
+    x = torch.randint(0, bins, (n,))
+    assert torch.equal(ops.histogram(x.to(DEV), bins).cpu(), torch.bincount(x, minlength=bins))

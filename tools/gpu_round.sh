@@ -1,0 +1,28 @@
+#!/bin/bash
+# One gpurun session: GPU tests, smoke, bench, rocprof kernel stats. Each GPU step has its own time limit and the
+# chain stops at the first failure.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEP=${1:-all}
+if [[ $STEP == all || $STEP == test || $STEP == quick ]]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+  tail -3 gpurun_out/pytest_gpu.log
+fi
+if [[ $STEP == all || $STEP == smoke ]]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -40 gpurun_out/smoke.log; exit 1; }
+  tail -2 gpurun_out/smoke.log
+fi
+if [[ $STEP == all || $STEP == bench || $STEP == quick ]]; then
+  timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 || { tail -40 gpurun_out/bench.log; exit 1; }
+  tail -1 gpurun_out/bench.log
+fi
+if [[ $STEP == all || $STEP == prof ]]; then
+  cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 5 > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1 || { tail -40 $GRAFT_REPO_ROOT/gpurun_out/prof.log; exit 1; }
+  cd $GRAFT_REPO_ROOT
+  find gpurun_out/prof -name "*kernel_stats*" | head -3
+fi
+if [[ $STEP == all || $STEP == kbench || $STEP == quick ]]; then
+  timeout -k 10 300 python benchmarks/kbench.py > gpurun_out/kbench.log 2>&1 || { tail -40 gpurun_out/kbench.log; exit 1; }
+  cat gpurun_out/kbench.log
+fi

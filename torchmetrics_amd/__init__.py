@@ -1,0 +1,25 @@
+"""torchmetrics_amd: an MI355X-native (ROCm / CDNA4) metrics framework with the torchmetrics 1.4 API.
+
+Root namespace mirrors reference ``S/__init__.py:23-151``.
+"""
+import logging as __logging
+
+from torchmetrics_amd.__about__ import __version__  # noqa: F401
+
+_logger = __logging.getLogger("torchmetrics_amd")
+_logger.addHandler(__logging.StreamHandler())
+_logger.setLevel(__logging.INFO)
+
+from torchmetrics_amd import functional  # noqa: E402,F401
+from torchmetrics_amd.aggregation import (  # noqa: E402
+    CatMetric,
+    MaxMetric,
+    MeanMetric,
+    MinMetric,
+    RunningMean,
+    RunningSum,
+    SumMetric,
+)
+from torchmetrics_amd.classification import *  # noqa: E402,F401,F403
+from torchmetrics_amd.collections import MetricCollection  # noqa: E402
+from torchmetrics_amd.metric import CompositionalMetric, Metric  # noqa: E402

@@ -1,0 +1,102 @@
+"""Hamming distance module metrics. Parity: reference ``S/classification/hamming.py``.
+
+Thin subclasses of the fused stat-scores metrics: ``update`` is the shared HIP kernel, ``compute`` is the score
+algebra of :mod:`torchmetrics_amd.functional.classification._reductions`.
+"""
+from typing import Any, Optional, Sequence, Type, Union
+
+from torch import Tensor
+
+from torchmetrics_amd.classification.base import _ClassificationTaskWrapper
+from torchmetrics_amd.classification.stat_scores import BinaryStatScores, MulticlassStatScores, MultilabelStatScores
+from torchmetrics_amd.functional.classification._family import _check_beta
+from torchmetrics_amd.functional.classification._reductions import _stat_reduce
+from torchmetrics_amd.metric import Metric
+from torchmetrics_amd.utilities.enums import ClassificationTask
+from torchmetrics_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
+
+
+class BinaryHammingDistance(BinaryStatScores):
+    """Binary HammingDistance."""
+
+    is_differentiable = False
+    higher_is_better: Optional[bool] = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+
+    def compute(self) -> Tensor:
+        tp, fp, tn, fn = self._final_state()
+        return _stat_reduce("hamming", tp, fp, tn, fn, "binary", self.multidim_average)
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
+
+
+class MulticlassHammingDistance(MulticlassStatScores):
+    """Multiclass HammingDistance."""
+
+    is_differentiable = False
+    higher_is_better: Optional[bool] = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+    plot_legend_name: str = "Class"
+
+    def compute(self) -> Tensor:
+        tp, fp, tn, fn = self._final_state()
+        return _stat_reduce("hamming", tp, fp, tn, fn, self.average, self.multidim_average)
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
+
+
+class MultilabelHammingDistance(MultilabelStatScores):
+    """Multilabel HammingDistance."""
+
+    is_differentiable = False
+    higher_is_better: Optional[bool] = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+    plot_legend_name: str = "Label"
+
+    def compute(self) -> Tensor:
+        tp, fp, tn, fn = self._final_state()
+        return _stat_reduce("hamming", tp, fp, tn, fn, self.average, self.multidim_average, multilabel=True)
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
+
+
+class HammingDistance(_ClassificationTaskWrapper):
+    """Task wrapper: returns Binary/Multiclass/MultilabelHammingDistance for ``task``."""
+
+    def __new__(  # type: ignore[misc]
+        cls: Type["HammingDistance"],
+        task: str,
+        threshold: float = 0.5,
+        num_classes: Optional[int] = None,
+        num_labels: Optional[int] = None,
+        average: Optional[str] = "micro",
+        multidim_average: str = "global",
+        top_k: Optional[int] = 1,
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> Metric:
+        task = ClassificationTask.from_str(task)
+        kwargs.update({"multidim_average": multidim_average, "ignore_index": ignore_index, "validate_args": validate_args})
+        if task == ClassificationTask.BINARY:
+            return BinaryHammingDistance(threshold, **kwargs)
+        if task == ClassificationTask.MULTICLASS:
+            if not isinstance(num_classes, int):
+                raise ValueError(f"`num_classes` is expected to be `int` but `{type(num_classes)} was passed.`")
+            if not isinstance(top_k, int):
+                raise ValueError(f"`top_k` is expected to be `int` but `{type(top_k)} was passed.`")
+            return MulticlassHammingDistance(num_classes, top_k, average, **kwargs)
+        if task == ClassificationTask.MULTILABEL:
+            if not isinstance(num_labels, int):
+                raise ValueError(f"`num_labels` is expected to be `int` but `{type(num_labels)} was passed.`")
+            return MultilabelHammingDistance(num_labels, threshold, average, **kwargs)
+        raise ValueError(f"Task {task} not supported!")

@@ -1,0 +1,387 @@
+"""``MetricCollection`` with compute groups and collection-level (sync-once) distributed sync.
+
+API/behaviour parity with reference ``S/collections.py:34-661`` (kwargs filtering, prefix/postfix, nested
+collections, compute groups discovered on the first ``update`` and shared by reference, ``copy_state`` semantics).
+
+MI355X-first change -- **one sync per collection**: the reference ``compute`` calls every member's ``compute``, and
+each one syncs its own states (``S/collections.py:330-338``), i.e. per state 1 barrier + 2 all_gathers, repeated for
+every member even when compute groups share the states.  Here ``compute`` syncs the *group leaders* of all eligible
+members in ONE engine call (:func:`torchmetrics_amd.parallel.sync.sync_state_dicts`): for a 20-metric
+classification+regression collection that is one ``all_reduce`` per (op, dtype) bucket -- typically 2-3 RCCL
+collectives in total.  Every member's ``compute()`` still returns the synced value and local states are restored
+afterwards, exactly like the per-metric path.
+"""
+from collections import OrderedDict
+from copy import deepcopy
+from typing import Any, Dict, Hashable, Iterable, Iterator, List, Optional, Sequence, Tuple, Union
+
+import torch
+from torch import Tensor
+from torch.nn import ModuleDict
+
+from torchmetrics_amd.metric import CompositionalMetric, Metric
+from torchmetrics_amd.parallel.sync import sync_state_dicts
+from torchmetrics_amd.utilities.data import _flatten_dict, allclose
+from torchmetrics_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_single_or_multi_val
+from torchmetrics_amd.utilities.prints import rank_zero_warn
+
+
+class MetricCollection(ModuleDict):
+    """Chain metrics that take the same inputs into one ``update``/``compute``/``forward``.
+
+    Args:
+        metrics: a metric, a sequence of metrics, or a dict ``name -> metric``; nested collections are flattened.
+        additional_metrics: more metrics when ``metrics`` is a metric/sequence.
+        prefix / postfix: strings added around every output key.
+        compute_groups: ``True`` (auto-detect metrics with identical states after the first update), ``False``, or an
+            explicit list of lists of metric names.
+    """
+
+    _modules: Dict[str, Metric]  # type: ignore[assignment]
+    _groups: Dict[int, List[str]]
+
+    def __init__(
+        self,
+        metrics: Union[Metric, Sequence[Metric], Dict[str, Metric]],
+        *additional_metrics: Metric,
+        prefix: Optional[str] = None,
+        postfix: Optional[str] = None,
+        compute_groups: Union[bool, List[List[str]]] = True,
+    ) -> None:
+        super().__init__()
+        self.prefix = self._check_arg(prefix, "prefix")
+        self.postfix = self._check_arg(postfix, "postfix")
+        self._enable_compute_groups = compute_groups
+        self._groups_checked: bool = False
+        self._state_is_copy: bool = False
+        self.add_metrics(metrics, *additional_metrics)
+
+    # ------------------------------------------------------------------------------------------------ hot path
+    @torch.jit.unused
+    def forward(self, *args: Any, **kwargs: Any) -> Dict[str, Any]:
+        return self._compute_and_reduce("forward", *args, **kwargs)
+
+    def update(self, *args: Any, **kwargs: Any) -> None:
+        """Update every metric (only the first member of each compute group once groups are known)."""
+        if self._groups_checked:
+            for cg in self._groups.values():
+                m0 = getattr(self, cg[0])
+                m0.update(*args, **m0._filter_kwargs(**kwargs))
+            if self._state_is_copy:
+                self._compute_groups_create_state_ref()
+                self._state_is_copy = False
+        else:
+            for m in self.values(copy_state=False):
+                m.update(*args, **m._filter_kwargs(**kwargs))
+            if self._enable_compute_groups:
+                self._merge_compute_groups()
+                self._compute_groups_create_state_ref()
+                self._groups_checked = True
+
+    def _merge_compute_groups(self) -> None:
+        """Merge groups whose leaders hold identical states (O(M^2) pairwise, once)."""
+        changed = True
+        while changed:
+            changed = False
+            keys = list(self._groups.keys())
+            for i, a in enumerate(keys):
+                for b in keys[i + 1 :]:
+                    if a not in self._groups or b not in self._groups:
+                        continue
+                    m1 = getattr(self, self._groups[a][0])
+                    m2 = getattr(self, self._groups[b][0])
+                    if self._equal_metric_states(m1, m2):
+                        self._groups[a].extend(self._groups.pop(b))
+                        changed = True
+        self._groups = dict(enumerate(self._groups.values()))
+
+    @staticmethod
+    def _equal_metric_states(metric1: Metric, metric2: Metric) -> bool:
+        if len(metric1._defaults) == 0 or len(metric2._defaults) == 0:
+            return False
+        if metric1._defaults.keys() != metric2._defaults.keys():
+            return False
+        for key in metric1._defaults:
+            s1, s2 = getattr(metric1, key), getattr(metric2, key)
+            if type(s1) != type(s2):  # noqa: E721
+                return False
+            if isinstance(s1, Tensor) and isinstance(s2, Tensor):
+                return s1.shape == s2.shape and allclose(s1, s2)
+            if isinstance(s1, list) and isinstance(s2, list):
+                return all(a.shape == b.shape and allclose(a, b) for a, b in zip(s1, s2))
+        return True
+
+    def _compute_groups_create_state_ref(self, copy: bool = False) -> None:
+        """Point every group member's states at the leader's (or deep-copy them when ``copy``)."""
+        if not self._state_is_copy:
+            for cg in self._groups.values():
+                m0 = getattr(self, cg[0])
+                for name in cg[1:]:
+                    mi = getattr(self, name)
+                    for state in m0._defaults:
+                        val = getattr(m0, state)
+                        setattr(mi, state, deepcopy(val) if copy else val)
+                    mi._update_count = deepcopy(m0._update_count) if copy else m0._update_count
+                    mi._computed = deepcopy(m0._computed) if copy else m0._computed
+        self._state_is_copy = copy
+
+    def compute(self) -> Dict[str, Any]:
+        return self._compute_and_reduce("compute")
+
+    # ----------------------------------------------------------------------------------------- sync-once engine
+    def _eligible_for_collection_sync(self, m: Metric) -> bool:
+        return (
+            isinstance(m, Metric)
+            and not isinstance(m, CompositionalMetric)
+            and type(m)._sync_dist is Metric._sync_dist
+            and m.dist_sync_fn is None
+            and m._to_sync
+            and not m._is_synced
+            and m._computed is None
+            and bool(m.distributed_available_fn() if callable(m.distributed_available_fn) else False)
+        )
+
+    def _collection_sync(self) -> List[Tuple[Metric, bool]]:
+        """Sync all eligible members with one engine call; returns ``(metric, saved _to_sync)`` to restore."""
+        members = dict(self.items(keep_base=True, copy_state=False))
+        if self._groups:
+            groups = [cg for cg in self._groups.values()]
+            covered = {n for cg in groups for n in cg}
+            groups += [[n] for n in members if n not in covered]
+        else:
+            groups = [[n] for n in members]
+        plans: Dict[Any, List[List[Metric]]] = {}
+        for cg in groups:
+            ms = [members[n] for n in cg if n in members]
+            if not ms or not all(self._eligible_for_collection_sync(m) for m in ms):
+                continue
+            key = id(ms[0].process_group) if ms[0].process_group is not None else None
+            plans.setdefault(key, []).append(ms)
+        restore: List[Tuple[Metric, bool]] = []
+        for _, grp_list in plans.items():
+            leaders = [g[0] for g in grp_list]
+            entries = [({a: getattr(m, a) for a in m._reductions}, m._reductions) for m in leaders]
+            synced = sync_state_dicts(entries, group=leaders[0].process_group)
+            for g, states in zip(grp_list, synced):
+                for m in g:
+                    m._cache = {a: getattr(m, a) for a in m._defaults}
+                    for a, v in states.items():
+                        setattr(m, a, v)
+                    m._is_synced = True
+                    restore.append((m, m._to_sync))
+                    m._to_sync = False
+        return restore
+
+    def _compute_and_reduce(self, method_name: str, *args: Any, **kwargs: Any) -> Dict[str, Any]:
+        result = {}
+        restore: List[Tuple[Metric, bool]] = []
+        if method_name == "compute":
+            restore = self._collection_sync()
+        try:
+            for k, m in self.items(keep_base=True, copy_state=False):
+                if method_name == "compute":
+                    res = m.compute()
+                elif method_name == "forward":
+                    res = m(*args, **m._filter_kwargs(**kwargs))
+                else:
+                    raise ValueError(f"method_name should be either 'compute' or 'forward', but got {method_name}")
+                result[k] = res
+        finally:
+            for m, to_sync in restore:
+                if m._is_synced:
+                    m.unsync()
+                m._to_sync = to_sync
+
+        _, duplicates = _flatten_dict(result)
+        flat: Dict[str, Any] = {}
+        for k, m in self.items(keep_base=True, copy_state=False):
+            res = result[k]
+            if isinstance(res, dict):
+                for key, v in res.items():
+                    if duplicates:
+                        stripped = k.replace(getattr(m, "prefix", "") or "", "")
+                        stripped = stripped.replace(getattr(m, "postfix", "") or "", "")
+                        key = f"{stripped}_{key}"
+                    if getattr(m, "_from_collection", None) and m.prefix is not None:
+                        key = f"{m.prefix}{key}"
+                    if getattr(m, "_from_collection", None) and m.postfix is not None:
+                        key = f"{key}{m.postfix}"
+                    flat[key] = v
+            else:
+                flat[k] = res
+        return {self._set_name(k): v for k, v in flat.items()}
+
+    # -------------------------------------------------------------------------------------------- management
+    def reset(self) -> None:
+        for m in self.values(copy_state=False):
+            m.reset()
+        if self._enable_compute_groups and self._groups_checked:
+            self._compute_groups_create_state_ref()
+
+    def clone(self, prefix: Optional[str] = None, postfix: Optional[str] = None) -> "MetricCollection":
+        mc = deepcopy(self)
+        if prefix:
+            mc.prefix = self._check_arg(prefix, "prefix")
+        if postfix:
+            mc.postfix = self._check_arg(postfix, "postfix")
+        return mc
+
+    def persistent(self, mode: bool = True) -> None:
+        for m in self.values(copy_state=False):
+            m.persistent(mode)
+
+    def add_metrics(
+        self, metrics: Union[Metric, Sequence[Metric], Dict[str, Metric]], *additional_metrics: Metric
+    ) -> None:
+        if isinstance(metrics, Metric):
+            metrics = [metrics]
+        if isinstance(metrics, Sequence):
+            metrics = list(metrics)
+            remain: list = []
+            for m in additional_metrics:
+                (metrics if isinstance(m, Metric) else remain).append(m)
+            if remain:
+                rank_zero_warn(f"You have passes extra arguments {remain} which are not `Metric` so they will be ignored.")
+        elif additional_metrics:
+            raise ValueError(
+                f"You have passes extra arguments {additional_metrics} which are not compatible"
+                f" with first passed dictionary {metrics} so they will be ignored."
+            )
+
+        def _absorb(prefix_name: Optional[str], coll: "MetricCollection") -> None:
+            for k, v in coll.items(keep_base=False):
+                v.postfix = coll.postfix
+                v.prefix = coll.prefix
+                v._from_collection = True
+                self[f"{prefix_name}_{k}" if prefix_name is not None else k] = v
+
+        if isinstance(metrics, dict):
+            for name in sorted(metrics.keys()):
+                metric = metrics[name]
+                if not isinstance(metric, (Metric, MetricCollection)):
+                    raise ValueError(
+                        f"Value {metric} belonging to key {name} is not an instance of"
+                        " `torchmetrics.Metric` or `torchmetrics.MetricCollection`"
+                    )
+                if isinstance(metric, Metric):
+                    self[name] = metric
+                else:
+                    _absorb(name, metric)
+        elif isinstance(metrics, Sequence):
+            for metric in metrics:
+                if not isinstance(metric, (Metric, MetricCollection)):
+                    raise ValueError(
+                        f"Input {metric} to `MetricCollection` is not a instance of"
+                        " `torchmetrics.Metric` or `torchmetrics.MetricCollection`"
+                    )
+                if isinstance(metric, Metric):
+                    name = metric.__class__.__name__
+                    if name in self:
+                        raise ValueError(f"Encountered two metrics both named {name}")
+                    self[name] = metric
+                else:
+                    _absorb(None, metric)
+        else:
+            raise ValueError(
+                "Unknown input to MetricCollection. Expected, `Metric`, `MetricCollection` or `dict`/`sequence` of the"
+                f" previous, but got {metrics}"
+            )
+        self._groups_checked = False
+        if self._enable_compute_groups:
+            self._init_compute_groups()
+        else:
+            self._groups = {}
+
+    def _init_compute_groups(self) -> None:
+        if isinstance(self._enable_compute_groups, list):
+            self._groups = dict(enumerate(self._enable_compute_groups))
+            for v in self._groups.values():
+                for metric in v:
+                    if metric not in self:
+                        raise ValueError(
+                            f"Input {metric} in `compute_groups` argument does not match a metric in the collection."
+                            f" Please make sure that {self._enable_compute_groups} matches {self.keys(keep_base=True)}"
+                        )
+            self._groups_checked = True
+        else:
+            self._groups = {i: [str(k)] for i, k in enumerate(self.keys(keep_base=True))}
+
+    @property
+    def compute_groups(self) -> Dict[int, List[str]]:
+        return self._groups
+
+    def _set_name(self, base: str) -> str:
+        name = base if self.prefix is None else self.prefix + base
+        return name if self.postfix is None else name + self.postfix
+
+    def _to_renamed_ordered_dict(self) -> OrderedDict:
+        od = OrderedDict()
+        for k, v in self._modules.items():
+            od[self._set_name(k)] = v
+        return od
+
+    def __iter__(self) -> Iterator[Hashable]:
+        return iter(self.keys())
+
+    def keys(self, keep_base: bool = False) -> Iterable[Hashable]:  # type: ignore[override]
+        if keep_base:
+            return self._modules.keys()
+        return self._to_renamed_ordered_dict().keys()
+
+    def items(self, keep_base: bool = False, copy_state: bool = True) -> Iterable[Tuple[str, Metric]]:  # type: ignore
+        self._compute_groups_create_state_ref(copy_state)
+        if keep_base:
+            return self._modules.items()
+        return self._to_renamed_ordered_dict().items()
+
+    def values(self, copy_state: bool = True) -> Iterable[Metric]:  # type: ignore[override]
+        self._compute_groups_create_state_ref(copy_state)
+        return self._modules.values()
+
+    def __getitem__(self, key: str, copy_state: bool = True) -> Metric:  # type: ignore[override]
+        self._compute_groups_create_state_ref(copy_state)
+        return self._modules[key]
+
+    @staticmethod
+    def _check_arg(arg: Optional[str], name: str) -> Optional[str]:
+        if arg is None or isinstance(arg, str):
+            return arg
+        raise ValueError(f"Expected input `{name}` to be a string, but got {type(arg)}")
+
+    def __repr__(self) -> str:
+        out = super().__repr__()[:-2]
+        if self.prefix:
+            out += f",\n  prefix={self.prefix}{',' if self.postfix else ''}"
+        if self.postfix:
+            out += f"{',' if not self.prefix else ''}\n  postfix={self.postfix}"
+        return out + "\n)"
+
+    def set_dtype(self, dst_type: Union[str, torch.dtype]) -> "MetricCollection":
+        for m in self.values(copy_state=False):
+            m.set_dtype(dst_type)
+        return self
+
+    def plot(
+        self,
+        val: Optional[Union[Dict, Sequence[Dict]]] = None,
+        ax: Optional[Union[_AX_TYPE, Sequence[_AX_TYPE]]] = None,
+        together: bool = False,
+    ) -> Sequence[_PLOT_OUT_TYPE]:
+        if not isinstance(together, bool):
+            raise ValueError(f"Expected argument `together` to be a boolean, but got {type(together)}")
+        if ax is not None and not together and not (isinstance(ax, Sequence) and len(ax) == len(self)):
+            raise ValueError(
+                "Expected argument `ax` to be a sequence of matplotlib axis objects with the same length as the "
+                f"number of metrics in the collection, but got {type(ax)} when `together=False`"
+            )
+        val = val or self.compute()
+        if together:
+            return plot_single_or_multi_val(val, ax=ax)
+        out = []
+        for i, (k, m) in enumerate(self.items(keep_base=True, copy_state=False)):
+            if isinstance(val, dict):
+                f, a = m.plot(val[k], ax=ax[i] if ax is not None else ax)
+            else:
+                f, a = m.plot([v[k] for v in val], ax=ax[i] if ax is not None else ax)
+            out.append((f, a))
+        return out

@@ -1,0 +1,2 @@
+"""Functional (stateless) metrics (parity: reference ``F/__init__.py``)."""
+from torchmetrics_amd.functional.classification import *  # noqa: F401,F403

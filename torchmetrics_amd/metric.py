@@ -1,0 +1,807 @@
+"""Core runtime: the ``Metric`` base class and ``CompositionalMetric``.
+
+Lifecycle parity with reference ``S/metric.py:50-1211`` (``add_state`` / ``update`` / ``compute`` / ``forward`` /
+``reset`` / ``sync`` / ``unsync`` / ``sync_context`` / ``state_dict`` / pickling / operator algebra).
+
+MI355X-first differences:
+
+* **Sync** (``_sync_dist``): with ``dist_sync_fn=None`` (the default) states go through the bucketed engine in
+  :mod:`torchmetrics_amd.parallel.sync` -- one RCCL ``all_reduce`` per (op, dtype) bucket for SUM/MEAN/MAX/MIN states,
+  one packed ``all_gather`` per dtype for CAT/None states, no barriers.  A user-supplied ``dist_sync_fn`` keeps the
+  reference per-tensor contract exactly (``fn(tensor, group=...) -> List[Tensor]``, ``T/bases/test_metric.py:517``).
+* **Deferred validation**: HIP kernels validate value ranges on device and raise bits in ``self._device_errors``;
+  the flags are read once (a 4-byte D2H copy) at ``compute()`` instead of the reference's per-``update`` host syncs
+  (``F/classification/stat_scores.py:307,316``).  ``TORCHMETRICS_AMD_STRICT=1`` checks after every update.
+"""
+import builtins
+import functools
+import inspect
+from abc import ABC, abstractmethod
+from contextlib import contextmanager
+from copy import deepcopy
+from typing import Any, Callable, Dict, Generator, List, Optional, Sequence, Tuple, Union
+
+import torch
+from torch import Tensor
+from torch.nn import Module
+
+from torchmetrics_amd.parallel.sync import distributed_available as _engine_dist_available
+from torchmetrics_amd.parallel.sync import sync_state_dicts
+from torchmetrics_amd.utilities.data import (
+    _flatten,
+    _squeeze_if_scalar,
+    apply_to_collection,
+    dim_zero_cat,
+    dim_zero_max,
+    dim_zero_mean,
+    dim_zero_min,
+    dim_zero_sum,
+)
+from torchmetrics_amd.utilities.exceptions import TorchMetricsUserError
+from torchmetrics_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_single_or_multi_val
+from torchmetrics_amd.utilities.prints import rank_zero_warn
+from torchmetrics_amd.utils import validation as _validation
+
+_REDUCTION_BY_NAME = {
+    "sum": dim_zero_sum,
+    "mean": dim_zero_mean,
+    "max": dim_zero_max,
+    "min": dim_zero_min,
+    "cat": dim_zero_cat,
+}
+
+_CONST_ATTRS = (
+    "higher_is_better",
+    "is_differentiable",
+    "full_state_update",
+    "plot_lower_bound",
+    "plot_upper_bound",
+    "plot_legend_name",
+)
+
+
+def jit_distributed_available() -> bool:
+    """True when ``torch.distributed`` is available and a default process group exists."""
+    return _engine_dist_available()
+
+
+class Metric(Module, ABC):
+    """Base class for all metrics.
+
+    Subclasses register states with :meth:`add_state` and implement ``update`` and ``compute``.
+
+    Keyword Args:
+        compute_on_cpu: move list states to CPU after each ``update``.
+        dist_sync_on_step: synchronise states inside ``forward`` (so the batch value is global).
+        process_group: process group to sync over (default WORLD).
+        dist_sync_fn: custom per-tensor gather; ``None`` selects the bucketed RCCL engine.
+        distributed_available_fn: callable deciding whether we run distributed.
+        sync_on_compute: synchronise states in ``compute``.
+        compute_with_cache: cache the ``compute`` result until the next ``update``/``reset``.
+    """
+
+    __jit_ignored_attributes__ = ("device",)
+    __jit_unused_properties__ = (
+        "is_differentiable",
+        "higher_is_better",
+        "plot_lower_bound",
+        "plot_upper_bound",
+        "plot_legend_name",
+        "metric_state",
+        "_update_called",
+    )
+    is_differentiable: Optional[bool] = None
+    higher_is_better: Optional[bool] = None
+    full_state_update: Optional[bool] = None
+    plot_lower_bound: Optional[float] = None
+    plot_upper_bound: Optional[float] = None
+    plot_legend_name: Optional[str] = None
+
+    def __init__(self, **kwargs: Any) -> None:
+        super().__init__()
+        torch._C._log_api_usage_once(f"torchmetrics_amd.metric.{self.__class__.__name__}")
+        self._device = torch.device("cpu")
+        self._dtype = torch.get_default_dtype()
+
+        def _bool_kw(name: str, default: bool) -> bool:
+            val = kwargs.pop(name, default)
+            if not isinstance(val, bool):
+                raise ValueError(f"Expected keyword argument `{name}` to be an `bool` but got {val}")
+            return val
+
+        self.compute_on_cpu = _bool_kw("compute_on_cpu", False)
+        self.dist_sync_on_step = _bool_kw("dist_sync_on_step", False)
+        self.process_group = kwargs.pop("process_group", None)
+        self.dist_sync_fn = kwargs.pop("dist_sync_fn", None)
+        if self.dist_sync_fn is not None and not callable(self.dist_sync_fn):
+            raise ValueError(
+                f"Expected keyword argument `dist_sync_fn` to be an callable function but got {self.dist_sync_fn}"
+            )
+        self.distributed_available_fn = kwargs.pop("distributed_available_fn", None) or jit_distributed_available
+        self.sync_on_compute = _bool_kw("sync_on_compute", True)
+        self.compute_with_cache = _bool_kw("compute_with_cache", True)
+        if kwargs:
+            raise ValueError(f"Unexpected keyword arguments: {', '.join(f'`{a}`' for a in sorted(kwargs))}")
+
+        self._update_signature = inspect.signature(self.update)
+        self.update: Callable = self._wrap_update(self.update)  # type: ignore[method-assign]
+        self.compute: Callable = self._wrap_compute(self.compute)  # type: ignore[method-assign]
+        self._computed = None
+        self._forward_cache = None
+        self._update_count = 0
+        self._to_sync = self.sync_on_compute
+        self._should_unsync = True
+        self._enable_grad = False
+        self._dtype_convert = False
+
+        self._defaults: Dict[str, Union[List, Tensor]] = {}
+        self._persistent: Dict[str, bool] = {}
+        self._reductions: Dict[str, Union[str, Callable[..., Any], None]] = {}
+
+        self._is_synced = False
+        self._cache: Optional[Dict[str, Union[List[Tensor], Tensor]]] = None
+        # device-side validation flags (lazily allocated on first GPU update; see utils/validation.py)
+        self._device_errors: Optional[Tensor] = None
+
+    # ------------------------------------------------------------------------------------------------ properties
+    @property
+    def _update_called(self) -> bool:
+        rank_zero_warn(
+            "This property will be removed in 2.0.0. Use `Metric.updated_called` instead.",
+            DeprecationWarning,
+            stacklevel=2,
+        )
+        return self.update_called
+
+    @property
+    def update_called(self) -> bool:
+        """``True`` if ``update``/``forward`` ran since construction or the last ``reset``."""
+        return self._update_count > 0
+
+    @property
+    def update_count(self) -> int:
+        return self._update_count
+
+    @property
+    def metric_state(self) -> Dict[str, Union[List[Tensor], Tensor]]:
+        return {attr: getattr(self, attr) for attr in self._defaults}
+
+    # ---------------------------------------------------------------------------------------------------- states
+    def add_state(
+        self,
+        name: str,
+        default: Union[list, Tensor],
+        dist_reduce_fx: Optional[Union[str, Callable]] = None,
+        persistent: bool = False,
+    ) -> None:
+        """Register a state: a tensor, or an empty list that ``update`` appends to.
+
+        ``dist_reduce_fx`` in ``{"sum","mean","max","min","cat", None}`` or a callable applied to the rank-stacked
+        state.
+        """
+        if not isinstance(default, (Tensor, list)) or (isinstance(default, list) and default):
+            raise ValueError("state variable must be a tensor or any empty list (where you can append tensors)")
+        if isinstance(dist_reduce_fx, str):
+            if dist_reduce_fx not in _REDUCTION_BY_NAME:
+                raise ValueError(
+                    "`dist_reduce_fx` must be callable or one of ['mean', 'sum', 'cat', 'min', 'max', None]"
+                )
+            dist_reduce_fx = _REDUCTION_BY_NAME[dist_reduce_fx]
+        elif dist_reduce_fx is not None and not callable(dist_reduce_fx):
+            raise ValueError("`dist_reduce_fx` must be callable or one of ['mean', 'sum', 'cat', 'min', 'max', None]")
+        if isinstance(default, Tensor):
+            default = default.contiguous()
+        setattr(self, name, default)
+        self._defaults[name] = deepcopy(default)
+        self._persistent[name] = persistent
+        self._reductions[name] = dist_reduce_fx
+
+    # ---------------------------------------------------------------------------------------------------- forward
+    @torch.jit.unused
+    def forward(self, *args: Any, **kwargs: Any) -> Any:
+        """Update the global state with the batch and return the metric value on the batch alone."""
+        if self._is_synced:
+            raise TorchMetricsUserError(
+                "The Metric shouldn't be synced when performing ``forward``. "
+                "HINT: Did you forget to call ``unsync`` ?."
+            )
+        if self.full_state_update or self.full_state_update is None or self.dist_sync_on_step:
+            self._forward_cache = self._forward_full_state_update(*args, **kwargs)
+        else:
+            self._forward_cache = self._forward_reduce_state_update(*args, **kwargs)
+        return self._forward_cache
+
+    def _enter_batch_mode(self) -> bool:
+        self._to_sync = self.dist_sync_on_step
+        self._should_unsync = False
+        saved = self.compute_on_cpu
+        self.compute_on_cpu = False
+        self._enable_grad = True
+        return saved
+
+    def _exit_batch_mode(self, saved_compute_on_cpu: bool) -> None:
+        self._is_synced = False
+        self._should_unsync = True
+        self._to_sync = self.sync_on_compute
+        self._computed = None
+        self._enable_grad = False
+        self.compute_on_cpu = saved_compute_on_cpu
+        if self.compute_on_cpu:
+            self._move_list_states_to_cpu()
+
+    def _forward_full_state_update(self, *args: Any, **kwargs: Any) -> Any:
+        """Two ``update`` calls: one on the global state, one on a fresh state for the batch value."""
+        self.update(*args, **kwargs)
+        count = self._update_count
+        saved = self._enter_batch_mode()
+        cache = {attr: getattr(self, attr) for attr in self._defaults}
+        self.reset()
+        self.update(*args, **kwargs)
+        batch_val = self.compute()
+        for attr, val in cache.items():
+            setattr(self, attr, val)
+        self._update_count = count
+        self._exit_batch_mode(saved)
+        return batch_val
+
+    def _forward_reduce_state_update(self, *args: Any, **kwargs: Any) -> Any:
+        """One ``update`` on a fresh state, then fold the batch state into the saved global state."""
+        global_state = {attr: getattr(self, attr) for attr in self._defaults}
+        count = self._update_count
+        self.reset()
+        saved = self._enter_batch_mode()
+        self.update(*args, **kwargs)
+        batch_val = self.compute()
+        self._update_count = count + 1
+        with torch.no_grad():
+            self._reduce_states(global_state)
+        self._exit_batch_mode(saved)
+        return batch_val
+
+    def _reduce_states(self, incoming_state: Dict[str, Any]) -> None:
+        """Merge ``incoming_state`` (the pre-batch global state) with the current (batch) state."""
+        for attr in self._defaults:
+            local = getattr(self, attr)
+            glob = incoming_state[attr]
+            fn = self._reductions[attr]
+            if fn is dim_zero_sum:
+                merged = glob + local
+            elif fn is dim_zero_mean:
+                merged = ((self._update_count - 1) * glob + local).float() / self._update_count
+            elif fn is dim_zero_max:
+                merged = torch.max(glob, local)
+            elif fn is dim_zero_min:
+                merged = torch.min(glob, local)
+            elif fn is dim_zero_cat:
+                merged = torch.cat([glob, local]) if isinstance(glob, Tensor) else glob + local
+            elif fn is None and isinstance(glob, Tensor):
+                merged = torch.stack([glob, local])
+            elif fn is None and isinstance(glob, list):
+                merged = _flatten([glob, local])
+            elif callable(fn):
+                merged = fn(torch.stack([glob, local]))
+            else:
+                raise TypeError(f"Unsupported reduce_fn: {fn}")
+            setattr(self, attr, merged)
+
+    # ------------------------------------------------------------------------------------------------------- sync
+    def _sync_dist(self, dist_sync_fn: Optional[Callable] = None, process_group: Optional[Any] = None) -> None:
+        group = process_group or self.process_group
+        states = {attr: getattr(self, attr) for attr in self._reductions}
+        if dist_sync_fn is None:
+            synced = sync_state_dicts([(states, self._reductions)], group=group)[0]
+            for attr, val in synced.items():
+                setattr(self, attr, val)
+            return
+        # user-supplied per-tensor gather: reference contract, one call per state tensor
+        for attr, fn in self._reductions.items():
+            if fn is dim_zero_cat and isinstance(states[attr], list) and len(states[attr]) > 1:
+                states[attr] = [dim_zero_cat(states[attr])]
+        gathered = apply_to_collection(states, Tensor, dist_sync_fn, group=group)
+        for attr, fn in self._reductions.items():
+            val = gathered[attr]
+            if isinstance(val, list) and len(val) == 0:
+                setattr(self, attr, [])
+                continue
+            if isinstance(val[0], Tensor):
+                val = torch.stack(val)
+            elif isinstance(val[0], list):
+                val = _flatten(val)
+            if not (callable(fn) or fn is None):
+                raise TypeError("reduction_fn must be callable or None")
+            setattr(self, attr, fn(val) if fn is not None else val)
+
+    def _wrap_update(self, update: Callable) -> Callable:
+        @functools.wraps(update)
+        def wrapped_func(*args: Any, **kwargs: Any) -> None:
+            self._computed = None
+            self._update_count += 1
+            with torch.set_grad_enabled(self._enable_grad):
+                try:
+                    update(*args, **kwargs)
+                except RuntimeError as err:
+                    if "Expected all tensors to be on" in str(err):
+                        raise RuntimeError(
+                            "Encountered different devices in metric calculation (see stacktrace for details)."
+                            " This could be due to the metric class not being on the same device as input."
+                            f" Instead of `metric={self.__class__.__name__}(...)` try to do"
+                            f" `metric={self.__class__.__name__}(...).to(device)` where"
+                            " device corresponds to the device of the input."
+                        ) from err
+                    raise err
+            if _validation.STRICT and self._device_errors is not None:
+                self._raise_device_errors()
+            if self.compute_on_cpu:
+                self._move_list_states_to_cpu()
+
+        return wrapped_func
+
+    def _device_error_buffer(self, device: torch.device) -> Tensor:
+        """Per-metric int32 flag word the HIP kernels ``atomicOr`` validation failures into."""
+        buf = self._device_errors
+        if buf is None or buf.device != device:
+            buf = torch.zeros(1, dtype=torch.int32, device=device)
+            self._device_errors = buf
+        return buf
+
+    def _raise_device_errors(self) -> None:
+        buf = self._device_errors
+        if buf is None:
+            return
+        code = int(buf.item())
+        if code:
+            buf.zero_()
+            _validation.raise_for_code(code, self)
+
+    def _move_list_states_to_cpu(self) -> None:
+        for key in self._defaults:
+            val = getattr(self, key)
+            if isinstance(val, Sequence):
+                setattr(self, key, [v.to("cpu") for v in val])
+
+    def sync(
+        self,
+        dist_sync_fn: Optional[Callable] = None,
+        process_group: Optional[Any] = None,
+        should_sync: bool = True,
+        distributed_available: Optional[Callable] = None,
+    ) -> None:
+        """Synchronise states across processes (no-op when not distributed or ``should_sync=False``)."""
+        if self._is_synced and should_sync:
+            raise TorchMetricsUserError("The Metric has already been synced.")
+        if distributed_available is None and self.distributed_available_fn is not None:
+            distributed_available = self.distributed_available_fn
+        is_distributed = distributed_available() if callable(distributed_available) else None
+        if not should_sync or not is_distributed:
+            return
+        self._cache = {attr: getattr(self, attr) for attr in self._defaults}
+        self._sync_dist(dist_sync_fn, process_group=process_group)
+        self._is_synced = True
+
+    def unsync(self, should_unsync: bool = True) -> None:
+        """Restore the local (pre-sync) states."""
+        if not should_unsync:
+            return
+        if not self._is_synced:
+            raise TorchMetricsUserError("The Metric has already been un-synced.")
+        if self._cache is None:
+            raise TorchMetricsUserError("The internal cache should exist to unsync the Metric.")
+        for attr, val in self._cache.items():
+            setattr(self, attr, val)
+        self._is_synced = False
+        self._cache = None
+
+    @contextmanager
+    def sync_context(
+        self,
+        dist_sync_fn: Optional[Callable] = None,
+        process_group: Optional[Any] = None,
+        should_sync: bool = True,
+        should_unsync: bool = True,
+        distributed_available: Optional[Callable] = None,
+    ) -> Generator:
+        """Sync on entry, restore local states on exit."""
+        self.sync(
+            dist_sync_fn=dist_sync_fn,
+            process_group=process_group,
+            should_sync=should_sync,
+            distributed_available=distributed_available,
+        )
+        yield
+        self.unsync(should_unsync=self._is_synced and should_unsync)
+
+    def _wrap_compute(self, compute: Callable) -> Callable:
+        @functools.wraps(compute)
+        def wrapped_func(*args: Any, **kwargs: Any) -> Any:
+            if not self.update_called:
+                rank_zero_warn(
+                    f"The ``compute`` method of metric {self.__class__.__name__}"
+                    " was called before the ``update`` method which may lead to errors,"
+                    " as metric states have not yet been updated.",
+                    UserWarning,
+                )
+            if self._computed is not None:
+                return self._computed
+            if self._device_errors is not None:
+                self._raise_device_errors()
+            with self.sync_context(
+                dist_sync_fn=self.dist_sync_fn,
+                should_sync=self._to_sync,
+                should_unsync=self._should_unsync,
+            ):
+                value = _squeeze_if_scalar(compute(*args, **kwargs))
+            if self.compute_with_cache:
+                self._computed = value
+            return value
+
+        return wrapped_func
+
+    @abstractmethod
+    def update(self, *_: Any, **__: Any) -> None:
+        """Update the states with a batch."""
+
+    @abstractmethod
+    def compute(self) -> Any:
+        """Compute the metric value from the (synced) states."""
+
+    def plot(self, *_: Any, **__: Any) -> Any:
+        raise NotImplementedError
+
+    def _plot(self, val: Any = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        val = val if val is not None else self.compute()
+        return plot_single_or_multi_val(
+            val,
+            ax=ax,
+            higher_is_better=self.higher_is_better,
+            name=self.__class__.__name__,
+            lower_bound=self.plot_lower_bound,
+            upper_bound=self.plot_upper_bound,
+            legend_name=self.plot_legend_name,
+        )
+
+    def reset(self) -> None:
+        """Reset all states to their defaults."""
+        self._update_count = 0
+        self._forward_cache = None
+        self._computed = None
+        for attr, default in self._defaults.items():
+            cur = getattr(self, attr)
+            if isinstance(default, Tensor):
+                setattr(self, attr, default.detach().clone().to(cur.device))
+            else:
+                setattr(self, attr, [])
+        self._cache = None
+        self._is_synced = False
+
+    def clone(self) -> "Metric":
+        return deepcopy(self)
+
+    # ------------------------------------------------------------------------------------------------- pickling
+    def __getstate__(self) -> Dict[str, Any]:
+        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature")}
+
+    def __setstate__(self, state: Dict[str, Any]) -> None:
+        self.__dict__.update(state)
+        self._update_signature = inspect.signature(self.update)
+        self.update: Callable = self._wrap_update(self.update)  # type: ignore[method-assign]
+        self.compute: Callable = self._wrap_compute(self.compute)  # type: ignore[method-assign]
+
+    def __setattr__(self, name: str, value: Any) -> None:
+        if name in _CONST_ATTRS:
+            raise RuntimeError(f"Can't change const `{name}`.")
+        super().__setattr__(name, value)
+
+    # ------------------------------------------------------------------------------------------ device / dtype
+    @property
+    def device(self) -> "torch.device":
+        return self._device
+
+    @property
+    def dtype(self) -> "torch.dtype":
+        return self._dtype
+
+    def type(self, dst_type: Union[str, torch.dtype]) -> "Metric":  # noqa: A003
+        """No-op; use :meth:`set_dtype` (metric states keep their dtype under ``.half()`` etc.)."""
+        return self
+
+    def float(self) -> "Metric":  # noqa: A003
+        return self
+
+    def double(self) -> "Metric":
+        return self
+
+    def half(self) -> "Metric":
+        return self
+
+    def set_dtype(self, dst_type: Union[str, torch.dtype]) -> "Metric":
+        """Convert floating states to ``dst_type``."""
+        self._dtype_convert = True
+        out = super().type(dst_type)
+        out._dtype_convert = False
+        return out
+
+    def _apply(self, fn: Callable, exclude_state: Sequence[str] = "") -> Module:  # type: ignore[override]
+        this = super()._apply(fn)
+        fs = str(fn)
+        is_dtype_cast = any(f in fs for f in ("Module.type", "Module.half", "Module.float", "Module.double", "Module.bfloat16"))
+        if not self._dtype_convert and is_dtype_cast:
+            return this
+        for key, value in this._defaults.items():
+            if key in exclude_state:
+                continue
+            if isinstance(value, Tensor):
+                this._defaults[key] = fn(value)
+            elif isinstance(value, Sequence):
+                this._defaults[key] = [fn(v) for v in value]
+            cur = getattr(this, key)
+            if isinstance(cur, Tensor):
+                setattr(this, key, fn(cur))
+            elif isinstance(cur, Sequence):
+                setattr(this, key, [fn(v) for v in cur])
+            else:
+                raise TypeError(
+                    f"Expected metric state to be either a Tensor or a list of Tensor, but encountered {cur}"
+                )
+        probe = fn(torch.zeros(1, device=self.device))
+        self._device = probe.device
+        self._dtype = probe.dtype
+        if this._computed is not None:
+            this._computed = apply_to_collection(this._computed, Tensor, fn)
+        if this._forward_cache is not None:
+            this._forward_cache = apply_to_collection(this._forward_cache, Tensor, fn)
+        if this._device_errors is not None and this._device_errors.device != self._device:
+            this._device_errors = None
+        return this
+
+    # ------------------------------------------------------------------------------------------- checkpointing
+    def persistent(self, mode: bool = False) -> None:
+        for key in self._persistent:
+            self._persistent[key] = mode
+
+    def state_dict(  # type: ignore[override]
+        self,
+        destination: Optional[Dict[str, Any]] = None,
+        prefix: str = "",
+        keep_vars: bool = False,
+    ) -> Dict[str, Any]:
+        destination = super().state_dict(destination=destination, prefix=prefix, keep_vars=keep_vars)  # type: ignore
+        for key in self._defaults:
+            if not self._persistent[key]:
+                continue
+            cur = getattr(self, key)
+            if not keep_vars:
+                if isinstance(cur, Tensor):
+                    cur = cur.detach()
+                elif isinstance(cur, list):
+                    cur = [v.detach() if isinstance(v, Tensor) else v for v in cur]
+            destination[prefix + key] = deepcopy(cur)
+        return destination
+
+    def _load_from_state_dict(
+        self,
+        state_dict: dict,
+        prefix: str,
+        local_metadata: dict,
+        strict: bool,
+        missing_keys: List[str],
+        unexpected_keys: List[str],
+        error_msgs: List[str],
+    ) -> None:
+        for key in self._defaults:
+            name = prefix + key
+            if name in state_dict:
+                setattr(self, key, state_dict.pop(name))
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, True, missing_keys, unexpected_keys, error_msgs)
+
+    def _filter_kwargs(self, **kwargs: Any) -> Dict[str, Any]:
+        """Keep only the kwargs that ``update`` accepts (all of them if it takes ``**kwargs``)."""
+        var_kinds = (inspect.Parameter.VAR_POSITIONAL, inspect.Parameter.VAR_KEYWORD)
+        params = self._update_signature.parameters
+        filtered = {k: v for k, v in kwargs.items() if k in params and params[k].kind not in var_kinds}
+        has_var_kw = any(v.kind == inspect.Parameter.VAR_KEYWORD for v in params.values())
+        if not filtered and not has_var_kw:
+            return {}
+        if has_var_kw:
+            return kwargs
+        return filtered
+
+    def __hash__(self) -> int:
+        vals: List[Any] = [self.__class__.__name__, id(self)]
+        for key in self._defaults:
+            v = getattr(self, key)
+            if hasattr(v, "__iter__") and not isinstance(v, Tensor):
+                vals.extend(v)
+            else:
+                vals.append(v)
+        return hash(tuple(vals))
+
+    # -------------------------------------------------------------------------------------------- operator algebra
+    def __add__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.add, self, other)
+
+    def __and__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.bitwise_and, self, other)
+
+    def __eq__(self, other: Any) -> "CompositionalMetric":  # type: ignore[override]
+        return CompositionalMetric(torch.eq, self, other)
+
+    def __floordiv__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.floor_divide, self, other)
+
+    def __ge__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.ge, self, other)
+
+    def __gt__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.gt, self, other)
+
+    def __le__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.le, self, other)
+
+    def __lt__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.lt, self, other)
+
+    def __matmul__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.matmul, self, other)
+
+    def __mod__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.fmod, self, other)
+
+    def __mul__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.mul, self, other)
+
+    def __ne__(self, other: Any) -> "CompositionalMetric":  # type: ignore[override]
+        return CompositionalMetric(torch.ne, self, other)
+
+    def __or__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.bitwise_or, self, other)
+
+    def __pow__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.pow, self, other)
+
+    def __radd__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.add, other, self)
+
+    def __rand__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.bitwise_and, self, other)
+
+    def __rfloordiv__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.floor_divide, other, self)
+
+    def __rmatmul__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.matmul, other, self)
+
+    def __rmod__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.fmod, other, self)
+
+    def __rmul__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.mul, other, self)
+
+    def __ror__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.bitwise_or, other, self)
+
+    def __rpow__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.pow, other, self)
+
+    def __rsub__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.sub, other, self)
+
+    def __rtruediv__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.true_divide, other, self)
+
+    def __rxor__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.bitwise_xor, other, self)
+
+    def __sub__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.sub, self, other)
+
+    def __truediv__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.true_divide, self, other)
+
+    def __xor__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.bitwise_xor, self, other)
+
+    def __abs__(self) -> "CompositionalMetric":
+        return CompositionalMetric(torch.abs, self, None)
+
+    def __inv__(self) -> "CompositionalMetric":
+        return CompositionalMetric(torch.bitwise_not, self, None)
+
+    def __invert__(self) -> "CompositionalMetric":
+        return self.__inv__()
+
+    def __neg__(self) -> "CompositionalMetric":
+        return CompositionalMetric(_neg, self, None)
+
+    def __pos__(self) -> "CompositionalMetric":
+        return CompositionalMetric(torch.abs, self, None)
+
+    def __getitem__(self, idx: int) -> "CompositionalMetric":
+        return CompositionalMetric(lambda x: x[idx], self, None)
+
+    def __getnewargs__(self) -> Tuple:
+        return (Metric.__str__(self),)
+
+    __iter__ = None
+
+
+def _neg(x: Tensor) -> Tensor:
+    return -torch.abs(x)
+
+
+class CompositionalMetric(Metric):
+    """``op(metric_a.compute(), metric_b.compute())``; children sync themselves (reference ``S/metric.py:1088``)."""
+
+    def __init__(
+        self,
+        operator: Callable,
+        metric_a: Union[Metric, builtins.float, Tensor],
+        metric_b: Union[Metric, builtins.float, Tensor, None],
+    ) -> None:
+        super().__init__()
+        self.op = operator
+        if isinstance(metric_a, Tensor):
+            self.register_buffer("metric_a", metric_a, persistent=False)
+        else:
+            self.metric_a = metric_a
+        if isinstance(metric_b, Tensor):
+            self.register_buffer("metric_b", metric_b, persistent=False)
+        else:
+            self.metric_b = metric_b
+
+    def _sync_dist(self, dist_sync_fn: Optional[Callable] = None, process_group: Optional[Any] = None) -> None:
+        """Children sync in their own ``compute``."""
+
+    def update(self, *args: Any, **kwargs: Any) -> None:
+        if isinstance(self.metric_a, Metric):
+            self.metric_a.update(*args, **self.metric_a._filter_kwargs(**kwargs))
+        if isinstance(self.metric_b, Metric):
+            self.metric_b.update(*args, **self.metric_b._filter_kwargs(**kwargs))
+
+    def compute(self) -> Any:
+        val_a = self.metric_a.compute() if isinstance(self.metric_a, Metric) else self.metric_a
+        val_b = self.metric_b.compute() if isinstance(self.metric_b, Metric) else self.metric_b
+        if val_b is None:
+            return self.op(val_a)
+        return self.op(val_a, val_b)
+
+    @torch.jit.unused
+    def forward(self, *args: Any, **kwargs: Any) -> Any:
+        val_a = (
+            self.metric_a(*args, **self.metric_a._filter_kwargs(**kwargs))
+            if isinstance(self.metric_a, Metric)
+            else self.metric_a
+        )
+        val_b = (
+            self.metric_b(*args, **self.metric_b._filter_kwargs(**kwargs))
+            if isinstance(self.metric_b, Metric)
+            else self.metric_b
+        )
+        if val_a is None:
+            self._forward_cache = None
+        elif val_b is None:
+            self._forward_cache = None if isinstance(self.metric_b, Metric) else self.op(val_a)
+        else:
+            self._forward_cache = self.op(val_a, val_b)
+        return self._forward_cache
+
+    def reset(self) -> None:
+        if isinstance(self.metric_a, Metric):
+            self.metric_a.reset()
+        if isinstance(self.metric_b, Metric):
+            self.metric_b.reset()
+
+    def persistent(self, mode: bool = False) -> None:
+        if isinstance(self.metric_a, Metric):
+            self.metric_a.persistent(mode=mode)
+        if isinstance(self.metric_b, Metric):
+            self.metric_b.persistent(mode=mode)
+
+    def __repr__(self) -> str:
+        name = self.op.__name__ if hasattr(self.op, "__name__") else repr(self.op)
+        return self.__class__.__name__ + f"(\n  {name}(\n    {self.metric_a!r},\n    {self.metric_b!r}\n  )\n)"
+
+    def _wrap_compute(self, compute: Callable) -> Callable:
+        return compute
+
+
+__all__ = ["Metric", "CompositionalMetric", "jit_distributed_available"]

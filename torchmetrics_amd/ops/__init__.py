@@ -1,0 +1,140 @@
+"""Device-dispatching entry points for the hand-written HIP kernels (``csrc/`` -> ``_C/libtm_amd.so``).
+
+Every op has exactly two implementations, selected by the *device of its inputs* (not by availability):
+
+* ROCm tensors (``tensor.is_cuda``) -> ``torch.ops.tm_amd.*`` HIP kernels for gfx950.  If the library is missing
+  on a GPU host the call raises: there is no silent eager fallback on the GPU.
+* CPU tensors -> the host implementation in :mod:`torchmetrics_amd.ops._cpu` (ATen ops), which is the CPU
+  device implementation of the same contract (used by CPU/gloo runs and as the numerics oracle in tests).
+"""
+import os
+import threading
+from pathlib import Path
+from typing import Optional
+
+import torch
+from torch import Tensor
+
+from torchmetrics_amd.ops import _cpu
+
+_LIB_PATH = Path(__file__).resolve().parent.parent / "_C" / "libtm_amd.so"
+_lock = threading.Lock()
+_state = {"loaded": False, "error": None}
+
+
+def native_library_path() -> Path:
+    return _LIB_PATH
+
+
+def load_native(strict: bool = True) -> bool:
+    """Load ``libtm_amd.so`` (idempotent). With ``strict`` a missing/broken library raises."""
+    if _state["loaded"]:
+        return True
+    with _lock:
+        if _state["loaded"]:
+            return True
+        try:
+            if not _LIB_PATH.exists():
+                raise FileNotFoundError(
+                    f"{_LIB_PATH} not found: build the HIP kernels with `python tools/build_ext.py` "
+                    "(or `python -c 'import __graft_entry__ as g; g.build()'`)"
+                )
+            torch.ops.load_library(str(_LIB_PATH))
+            _state["loaded"] = True
+        except Exception as err:  # noqa: BLE001
+            _state["error"] = err
+            if strict:
+                raise RuntimeError(f"torchmetrics_amd native HIP library unavailable: {err}") from err
+            return False
+    return True
+
+
+def native_available() -> bool:
+    return load_native(strict=False)
+
+
+def _ops():
+    load_native(strict=True)
+    return torch.ops.tm_amd
+
+
+# ------------------------------------------------------------------------------------------------ classification
+MC_CONFMAT = 0
+MC_STATS = 1
+
+
+def mc_update(
+    preds: Tensor,
+    target: Tensor,
+    out: Tensor,
+    flag: Tensor,
+    num_classes: int,
+    ignore_index: Optional[int],
+    mode: int,
+    samplewise: bool = False,
+) -> None:
+    """Multiclass histogram update (see ``csrc/classification/stat_scores.hip``).
+
+    ``preds``: float scores ``[N, C, ...]`` (argmax) or int labels ``[N, K, ...]``; ``target``: ``[N, ...]``.
+    ``mode=MC_CONFMAT`` accumulates ``out[C, C]``; ``mode=MC_STATS`` accumulates the ``[G, 3C+1]`` workspace.
+    """
+    if preds.is_cuda:
+        _ops().mc_update(
+            preds.contiguous(), target.contiguous(), out, flag, int(num_classes),
+            int(ignore_index) if ignore_index is not None else 0, ignore_index is not None, int(mode), bool(samplewise),
+        )
+    else:
+        _cpu.mc_update(preds, target, out, flag, num_classes, ignore_index, mode, samplewise)
+
+
+def mc_stats_finalize(ws: Tensor, num_classes: int, micro: bool, accumulate: bool, tp: Tensor, fp: Tensor,
+                      tn: Tensor, fn: Tensor) -> None:
+    if ws.is_cuda:
+        _ops().mc_stats_finalize(ws, int(num_classes), bool(micro), bool(accumulate), tp, fp, tn, fn)
+    else:
+        _cpu.mc_stats_finalize(ws, num_classes, micro, accumulate, tp, fp, tn, fn)
+
+
+def bin_update(preds: Tensor, target: Tensor, ws: Tensor, flag: Tensor, not_prob: Tensor, num_labels: int,
+               threshold: float, ignore_index: Optional[int], samplewise: bool = False,
+               prob_check_all: bool = True) -> None:
+    """Binary / multilabel tp/fp/fn/count update for ``[N, L, ...]`` inputs into a ``[G, 7]`` workspace.
+
+    ``prob_check_all=False`` excludes ignored positions from the logits-vs-probabilities decision.
+    """
+    if preds.is_cuda:
+        _ops().bin_update(
+            preds.contiguous(), target.contiguous(), ws, flag, not_prob, int(num_labels), float(threshold),
+            int(ignore_index) if ignore_index is not None else 0, ignore_index is not None, bool(samplewise),
+            bool(prob_check_all),
+        )
+    else:
+        _cpu.bin_update(preds, target, ws, flag, not_prob, num_labels, threshold, ignore_index, samplewise,
+                        prob_check_all)
+
+
+def bin_confmat_finalize(ws: Tensor, not_prob: Tensor, confmat: Tensor) -> None:
+    """Fold a ``[G, 7]`` workspace into ``[G, 2, 2]`` confusion matrices (in place) and re-zero it."""
+    if ws.is_cuda:
+        _ops().bin_confmat_finalize(ws, not_prob, confmat)
+    else:
+        _cpu.bin_confmat_finalize(ws, not_prob, confmat)
+
+
+def bin_stats_finalize(ws: Tensor, not_prob: Tensor, accumulate: bool, tp: Tensor, fp: Tensor, tn: Tensor,
+                       fn: Tensor) -> None:
+    if ws.is_cuda:
+        _ops().bin_stats_finalize(ws, not_prob, bool(accumulate), tp, fp, tn, fn)
+    else:
+        _cpu.bin_stats_finalize(ws, not_prob, accumulate, tp, fp, tn, fn)
+
+
+def histogram(x: Tensor, minlength: int) -> Tensor:
+    """Deterministic integer bincount (int64 counts)."""
+    if x.is_cuda:
+        out = torch.zeros(int(minlength), dtype=torch.int64, device=x.device)
+        flag = torch.zeros(1, dtype=torch.int32, device=x.device)
+        x = x if x.dtype in (torch.int64, torch.int32, torch.uint8) else x.long()
+        _ops().histogram(x.contiguous(), out, flag)
+        return out
+    return torch.bincount(x, minlength=minlength)

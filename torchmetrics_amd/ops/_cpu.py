@@ -1,0 +1,168 @@
+"""CPU implementations of the ``torch.ops.tm_amd`` contracts (ATen ops, eager validation).
+
+Same inputs/outputs as the HIP kernels in ``csrc/``; invalid values raise immediately (no device flag on the host).
+"""
+from typing import Optional
+
+import torch
+from torch import Tensor
+
+from torchmetrics_amd.utils import validation as V
+
+
+def _set(flag: Tensor, code: int) -> None:
+    """Record a validation failure exactly like the kernels do (the caller decides when to raise)."""
+    if flag is not None:
+        flag.bitwise_or_(code)
+
+
+def mc_update(
+    preds: Tensor,
+    target: Tensor,
+    out: Tensor,
+    flag: Tensor,
+    num_classes: int,
+    ignore_index: Optional[int],
+    mode: int,
+    samplewise: bool,
+) -> None:
+    C = int(num_classes)
+    N = target.shape[0] if target.ndim else 1
+    if target.numel() == 0:
+        return
+    target = target.reshape(N, -1).long()
+    X = target.shape[1]
+    if preds.is_floating_point():
+        labels = preds.reshape(N, C, X).argmax(dim=1).unsqueeze(1)  # [N, 1, X]
+    else:
+        labels = preds.reshape(N, -1, X).long()  # [N, K, X]
+    K = labels.shape[1]
+    valid = torch.ones_like(target, dtype=torch.bool)
+    if ignore_index is not None:
+        valid &= target != ignore_index
+    bad_t = valid & ((target < 0) | (target >= C))
+    if bool(bad_t.any()):
+        _set(flag, V.TARGET_OUT_OF_RANGE)
+        valid &= ~bad_t
+    bad_p = ((labels < 0) | (labels >= C)).any(dim=1) & valid
+    if bool(bad_p.any()):
+        _set(flag, V.PREDS_OUT_OF_RANGE)
+        valid &= ~bad_p
+    if mode == 0:
+        t = target[valid]
+        p = labels[:, 0, :][valid]
+        out.view(-1).add_(torch.bincount(t * C + p, minlength=C * C))
+        return
+    G = N if samplewise else 1
+    ws = out.view(G, 3 * C + 1)
+    if K == 1 and not samplewise:
+        t = target[valid]
+        p = labels[:, 0, :][valid]
+        cm = torch.bincount(t * C + p, minlength=C * C).view(C, C)
+        tp = cm.diag()
+        ws[0, :C] += tp
+        ws[0, C : 2 * C] += cm.sum(0) - tp
+        ws[0, 2 * C : 3 * C] += cm.sum(1) - tp
+        ws[0, 3 * C] += t.numel()
+        return
+    onehot_t = torch.nn.functional.one_hot(target.clamp(0, C - 1), C) * valid.unsqueeze(-1)  # [N, X, C]
+    pred_set = torch.zeros(N, X, C, dtype=torch.long)
+    pred_set.scatter_(2, labels.clamp(0, C - 1).permute(0, 2, 1), 1)
+    pred_set = pred_set * valid.unsqueeze(-1)
+    tp = (onehot_t * pred_set).sum(1)  # [N, C]
+    fn = (onehot_t * (1 - pred_set)).sum(1)
+    fp = ((1 - onehot_t) * pred_set).sum(1)
+    cnt = valid.sum(1)
+    if not samplewise:
+        tp, fp, fn, cnt = tp.sum(0, keepdim=True), fp.sum(0, keepdim=True), fn.sum(0, keepdim=True), cnt.sum(0, keepdim=True)
+    ws[:, :C] += tp
+    ws[:, C : 2 * C] += fp
+    ws[:, 2 * C : 3 * C] += fn
+    ws[:, 3 * C] += cnt
+
+
+def mc_stats_finalize(ws: Tensor, num_classes: int, micro: bool, accumulate: bool, tp: Tensor, fp: Tensor,
+                      tn: Tensor, fn: Tensor) -> None:
+    C = int(num_classes)
+    G = ws.numel() // (3 * C + 1)
+    w = ws.view(G, 3 * C + 1)
+    a, b, d, cnt = w[:, :C], w[:, C : 2 * C], w[:, 2 * C : 3 * C], w[:, 3 * C : 3 * C + 1]
+    if micro:
+        a, b, d = a.sum(1), b.sum(1), d.sum(1)
+        e = C * cnt[:, 0] - a - b - d
+    else:
+        e = cnt - a - b - d
+    for dst, src in ((tp, a), (fp, b), (fn, d), (tn, e)):
+        src = src.reshape(dst.shape)
+        if accumulate:
+            dst += src
+        else:
+            dst.copy_(src)
+    w.zero_()
+
+
+def bin_update(preds: Tensor, target: Tensor, ws: Tensor, flag: Tensor, not_prob: Tensor, num_labels: int,
+               threshold: float, ignore_index: Optional[int], samplewise: bool, prob_check_all: bool = True) -> None:
+    if preds.numel() == 0:
+        return
+    N = preds.shape[0]
+    L = int(num_labels)
+    p = preds.reshape(N, L, -1)
+    t = target.reshape(N, L, -1).long()
+    valid = torch.ones_like(t, dtype=torch.bool)
+    if ignore_index is not None:
+        valid &= t != ignore_index
+    bad_t = valid & (t != 0) & (t != 1)
+    if bool(bad_t.any()):
+        _set(flag, V.TARGET_NOT_BINARY)
+        valid &= ~bad_t
+    if p.is_floating_point():
+        in_range = (p >= 0) & (p <= 1)
+        if not prob_check_all and ignore_index is not None:
+            in_range = in_range | (t == ignore_index)
+        if not bool(in_range.all()):
+            not_prob.fill_(1)
+        thr = torch.tensor(threshold, dtype=p.dtype)
+        pa = p > thr
+        pb = p.float().sigmoid().to(p.dtype) > thr
+    else:
+        bad_p = (p != 0) & (p != 1)
+        if bool(bad_p.any()):
+            _set(flag, V.PREDS_NOT_BINARY)
+            valid &= ~bad_p
+        pa = pb = p == 1
+    tt = (t == 1) & valid
+    tf = (t == 0) & valid
+    sum_dims = (2,) if samplewise else (0, 2)
+    cols = [
+        (tt & pa).sum(sum_dims), (tf & pa).sum(sum_dims), (tt & ~pa).sum(sum_dims),
+        (tt & pb).sum(sum_dims), (tf & pb).sum(sum_dims), (tt & ~pb).sum(sum_dims),
+        valid.sum(sum_dims),
+    ]
+    ws.view(-1, 7).add_(torch.stack([c.reshape(-1) for c in cols], dim=1))
+
+
+def bin_stats_finalize(ws: Tensor, not_prob: Tensor, accumulate: bool, tp: Tensor, fp: Tensor, tn: Tensor,
+                       fn: Tensor) -> None:
+    w = ws.view(-1, 7)
+    off = 3 if int(not_prob.item()) else 0
+    a, b, d = w[:, off], w[:, off + 1], w[:, off + 2]
+    e = w[:, 6] - a - b - d
+    for dst, src in ((tp, a), (fp, b), (fn, d), (tn, e)):
+        src = src.reshape(dst.shape)
+        if accumulate:
+            dst += src
+        else:
+            dst.copy_(src)
+    w.zero_()
+    not_prob.zero_()
+
+
+def bin_confmat_finalize(ws: Tensor, not_prob: Tensor, confmat: Tensor) -> None:
+    w = ws.view(-1, 7)
+    off = 3 if int(not_prob.item()) else 0
+    tp, fp, fn = w[:, off], w[:, off + 1], w[:, off + 2]
+    tn = w[:, 6] - tp - fp - fn
+    confmat.view(-1, 4).add_(torch.stack([tn, fp, fn, tp], dim=1))
+    w.zero_()
+    not_prob.zero_()

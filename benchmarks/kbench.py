@@ -81,7 +81,12 @@ CASES = {"confmat": case_confmat, "binary": case_binary}
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default=None)
+    ap.add_argument("--N", type=int, default=0)
+    ap.add_argument("--C", type=int, default=0)
     a = ap.parse_args()
+    if a.N:
+        print(json.dumps(case_confmat(N=a.N, C=a.C)))
+        sys.exit(0)
     for name, fn in CASES.items():
         if a.only and a.only != name:
             continue

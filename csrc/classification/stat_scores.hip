@@ -11,6 +11,8 @@
 // Small histograms are privatised in LDS (one int32 sub-histogram per block) and flushed with 64-bit atomics.
 #include "../common/tm_common.h"
 
+#include <cstdlib>
+
 namespace tm_amd {
 namespace {
 
@@ -589,7 +591,24 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
         if (X == 1 && C >= 32 && vec) {
           // rows of <= 16 lanes x 8 loads x 16 B go 16 lanes per row; longer rows use the whole wave per row
           const long long row_bytes = static_cast<long long>(C) * sizeof(scalar_t);
-          if (row_bytes <= 16LL * 8 * 16) {
+          static const int lpr_override = [] {
+            const char* e = std::getenv("TM_AMD_MC_LPR");  // tuning knob: 16 / 32 / 64
+            return e ? std::atoi(e) : 0;
+          }();
+          const int lpr = lpr_override ? lpr_override : (row_bytes <= 16LL * 8 * 16 ? 16 : 64);
+          if (lpr == 32) {
+            constexpr int LPR = 32;
+            const int grid = pick_grid(N, (kBlock / kWave) * (kWave / LPR));
+            hipLaunchKernelGGL((mc_argmax_subwave_kernel<scalar_t, target_t, LPR>), dim3(grid), dim3(kBlock),
+                               lds_bytes, s, pp, tp, N, C, ignore_index, has_ignore, static_cast<int>(mode), outp,
+                               flagp, samplewise);
+          } else if (lpr == 8) {
+            constexpr int LPR = 8;
+            const int grid = pick_grid(N, (kBlock / kWave) * (kWave / LPR));
+            hipLaunchKernelGGL((mc_argmax_subwave_kernel<scalar_t, target_t, LPR>), dim3(grid), dim3(kBlock),
+                               lds_bytes, s, pp, tp, N, C, ignore_index, has_ignore, static_cast<int>(mode), outp,
+                               flagp, samplewise);
+          } else if (lpr == 16) {
             constexpr int LPR = 16;
             const int grid = pick_grid(N, (kBlock / kWave) * (kWave / LPR));
             hipLaunchKernelGGL((mc_argmax_subwave_kernel<scalar_t, target_t, LPR>), dim3(grid), dim3(kBlock),

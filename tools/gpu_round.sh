@@ -26,3 +26,14 @@ if [[ $STEP == all || $STEP == kbench || $STEP == quick ]]; then
   timeout -k 10 300 python benchmarks/kbench.py > gpurun_out/kbench.log 2>&1 || { tail -40 gpurun_out/kbench.log; exit 1; }
   cat gpurun_out/kbench.log
 fi
+if [[ $STEP == kprof ]]; then
+  cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/kprof -o kb --output-format csv -- python3 $GRAFT_REPO_ROOT/benchmarks/kbench.py > $GRAFT_REPO_ROOT/gpurun_out/kprof.log 2>&1 || { tail -40 $GRAFT_REPO_ROOT/gpurun_out/kprof.log; exit 1; }
+  cd $GRAFT_REPO_ROOT && cut -c1-200 gpurun_out/kprof/kb_kernel_stats.csv | head -30
+fi
+if [[ $STEP == tune ]]; then
+  timeout -k 10 120 python benchmarks/host_overhead.py 2>&1 | grep -v amdgpu.ids
+  for L in 8 16 32 64; do
+    cd /tmp && TM_AMD_MC_LPR=$L timeout -k 10 300 rocprofv3 --kernel-trace -d $GRAFT_REPO_ROOT/gpurun_out/tune$L -o t --output-format csv -- python3 $GRAFT_REPO_ROOT/benchmarks/kbench.py --N 8192 --C 1000 > /dev/null 2>&1 || exit 1
+    cd $GRAFT_REPO_ROOT
+  done
+fi

@@ -181,7 +181,20 @@ class _StatWorkspace:
 
 
 def _scratch_flag(device: torch.device) -> Tensor:
+    """A fresh (zeroed) validation flag word, for callers that check it afterwards."""
     return torch.zeros(1, dtype=torch.int32, device=device)
+
+
+_SINK: dict = {}
+
+
+def _sink_flag(device: torch.device) -> Tensor:
+    """A cached per-device flag word for callers that do not validate (no allocation per update)."""
+    key = (device.type, device.index)
+    buf = _SINK.get(key)
+    if buf is None:
+        buf = _SINK[key] = torch.zeros(1, dtype=torch.int32, device=device)
+    return buf
 
 
 def _binary_like_stats(
@@ -206,7 +219,7 @@ def _binary_like_stats(
         ws = torch.zeros(G * 7, dtype=torch.int64, device=dev)
         not_prob = torch.zeros(1, dtype=torch.int32, device=dev)
     if flag is None:
-        flag = _scratch_flag(dev)
+        flag = _sink_flag(dev)
     p = _as_preds(preds)
     t = _as_target(target)
     if p.ndim == 0:
@@ -247,7 +260,7 @@ def _multiclass_stats(
     else:
         p = _as_preds(preds)
     if flag is None:
-        flag = _scratch_flag(dev)
+        flag = _sink_flag(dev)
     C = num_classes
     G = N if samplewise else 1
     micro = micro and not samplewise

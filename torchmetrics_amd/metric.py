@@ -17,7 +17,7 @@ import builtins
 import functools
 import inspect
 from abc import ABC, abstractmethod
-from contextlib import contextmanager
+from contextlib import contextmanager, nullcontext
 from copy import deepcopy
 from typing import Any, Callable, Dict, Generator, List, Optional, Sequence, Tuple, Union
 
@@ -49,6 +49,8 @@ _REDUCTION_BY_NAME = {
     "min": dim_zero_min,
     "cat": dim_zero_cat,
 }
+
+_NULL_CTX = nullcontext()
 
 _CONST_ATTRS = (
     "higher_is_better",
@@ -316,7 +318,10 @@ class Metric(Module, ABC):
         def wrapped_func(*args: Any, **kwargs: Any) -> None:
             self._computed = None
             self._update_count += 1
-            with torch.set_grad_enabled(self._enable_grad):
+            grad_ctx = (
+                _NULL_CTX if torch.is_grad_enabled() == self._enable_grad else torch.set_grad_enabled(self._enable_grad)
+            )
+            with grad_ctx:
                 try:
                     update(*args, **kwargs)
                 except RuntimeError as err:

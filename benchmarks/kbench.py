@@ -29,17 +29,22 @@ def timeit(fn, reps: int = 200, warmup: int = 20) -> float:
 
 def case_confmat(N=8192, C=1000, dtype=torch.bfloat16):
     dev = "cuda"
-    preds = torch.randn(N, C, device=dev).to(dtype)
-    target = torch.randint(0, C, (N,), device=dev)
+    nbuf = 4  # cycle buffers like bench.py (inputs not L2-resident, as in a real eval loop)
+    preds_l = [torch.randn(N, C, device=dev).to(dtype) for _ in range(nbuf)]
+    target_l = [torch.randint(0, C, (N,), device=dev) for _ in range(nbuf)]
+    preds = preds_l[0]
     cm = torch.zeros(C * C, dtype=torch.int64, device=dev)
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    it = [0]
 
     def ours():
-        ops.mc_update(preds, target, cm, flag, C, None, ops.MC_CONFMAT, False)
+        i = it[0] = (it[0] + 1) % nbuf
+        ops.mc_update(preds_l[i], target_l[i], cm, flag, C, None, ops.MC_CONFMAT, False)
 
     def aten():
-        lab = preds.argmax(1)
-        cm.add_(torch.bincount(target * C + lab, minlength=C * C))
+        i = it[0] = (it[0] + 1) % nbuf
+        lab = preds_l[i].argmax(1)
+        cm.add_(torch.bincount(target_l[i] * C + lab, minlength=C * C))
 
     t_ours = timeit(ours)
     t_aten = timeit(aten)

@@ -1,0 +1,238 @@
+// Streaming regression moments: one pass over (preds, target) computing any subset of ~14 per-output sums
+// (SSE, SAE, Σp, Σt, Σp², Σt², Σpt, MAPE/SMAPE/WMAPE terms, MSLE, log-cosh, Minkowski, count), accumulated in fp64.
+//
+// This one kernel backs every streaming regression metric (reference F/regression/{mse,mae,mape,symmetric_mape,
+// wmape,log_mse,log_cosh,r2,rse,explained_variance,pearson,concordance,minkowski}.py) and, through
+// MetricCollection, a whole group of them in a single launch.  Stage 1 writes per-block partials (no float atomics:
+// bitwise-reproducible), stage 2 reduces them in fixed order and adds the results straight into the metric state
+// tensors (f32 / f64 / i64) given as a tensor list, so an update is exactly two launches whatever the metric set.
+//
+// Pearson-style metrics pass per-column shifts (the running means) so the sums are of centred values, which keeps
+// the single-pass variance/covariance update stable (Σ(x-s)² instead of Σx² - n·mean²).
+#include "../common/tm_common.h"
+
+#include <vector>
+
+namespace tm_amd {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kMaxSums = 14;
+
+enum SumId : int {
+  kSSE = 0,     // Σ (p - t)^2
+  kSAE = 1,     // Σ |p - t|
+  kSP = 2,      // Σ p~      (p~ = p - shift_p)
+  kST = 3,      // Σ t~
+  kSPP = 4,     // Σ p~^2
+  kSTT = 5,     // Σ t~^2
+  kSPT = 6,     // Σ p~ t~
+  kMAPE = 7,    // Σ |p - t| / max(|t|, eps)
+  kSMAPE = 8,   // Σ 2|p - t| / max(|p| + |t|, eps)
+  kSABST = 9,   // Σ |t|
+  kMSLE = 10,   // Σ (log1p(p) - log1p(t))^2
+  kLOGCOSH = 11,// Σ log(cosh(p - t))
+  kMINK = 12,   // Σ |p - t|^P
+  kCOUNT = 13,  // number of observations per column
+};
+
+template <typename scalar_t>
+__global__ void __launch_bounds__(kBlock) moments_partial_kernel(const scalar_t* __restrict__ preds,
+                                                                 const scalar_t* __restrict__ target, long long n_rows,
+                                                                 int k, int mask, double eps, double pw,
+                                                                 const float* __restrict__ shift_p,
+                                                                 const float* __restrict__ shift_t,
+                                                                 double* __restrict__ partial) {
+  // every thread keeps one column: total threads is a multiple of k (host guarantees blockDim % k == 0 or k > block)
+  const long long tid = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const long long nthreads = static_cast<long long>(gridDim.x) * blockDim.x;
+  const long long total = n_rows * k;
+  double acc[kMaxSums];
+#pragma unroll
+  for (int s = 0; s < kMaxSums; ++s) acc[s] = 0.0;
+  const int col = static_cast<int>(tid % k);
+  const float sp = shift_p ? shift_p[col] : 0.f;
+  const float st = shift_t ? shift_t[col] : 0.f;
+  // stride is a multiple of k -> the column of this thread never changes
+  for (long long i = tid; i < total; i += nthreads) {
+    const float p = to_f32(preds[i]);
+    const float t = to_f32(target[i]);
+    const float d = p - t;
+    const float ad = fabsf(d);
+    if (mask & (1 << kSSE)) acc[kSSE] += static_cast<double>(d) * d;
+    if (mask & (1 << kSAE)) acc[kSAE] += ad;
+    if (mask & ((1 << kSP) | (1 << kSPP) | (1 << kSPT) | (1 << kST) | (1 << kSTT))) {
+      const double pc = static_cast<double>(p) - sp, tc = static_cast<double>(t) - st;
+      acc[kSP] += pc;
+      acc[kST] += tc;
+      acc[kSPP] += pc * pc;
+      acc[kSTT] += tc * tc;
+      acc[kSPT] += pc * tc;
+    }
+    if (mask & (1 << kMAPE)) acc[kMAPE] += ad / fmax(static_cast<double>(fabsf(t)), eps);
+    if (mask & (1 << kSMAPE)) acc[kSMAPE] += 2.0 * ad / fmax(static_cast<double>(fabsf(p) + fabsf(t)), eps);
+    if (mask & (1 << kSABST)) acc[kSABST] += fabsf(t);
+    if (mask & (1 << kMSLE)) {
+      const double l = log1p(static_cast<double>(p)) - log1p(static_cast<double>(t));
+      acc[kMSLE] += l * l;
+    }
+    if (mask & (1 << kLOGCOSH)) {
+      // log(cosh(x)) = |x| + log1p(exp(-2|x|)) - log(2)  (overflow-free)
+      const double x = fabs(static_cast<double>(d));
+      acc[kLOGCOSH] += x + log1p(exp(-2.0 * x)) - 0.69314718055994530942;
+    }
+    if (mask & (1 << kMINK)) acc[kMINK] += pow(static_cast<double>(ad), pw);
+    acc[kCOUNT] += 1.0;
+  }
+  // block reduction per (column, sum): threads with equal tid % k hold the same column
+  __shared__ double red[kBlock][kMaxSums + 1];
+#pragma unroll
+  for (int s = 0; s < kMaxSums; ++s) red[threadIdx.x][s] = acc[s];
+  __syncthreads();
+  // rows of the partial buffer: [block][column][sum]
+  for (int c = threadIdx.x; c < k; c += blockDim.x) {
+    double out[kMaxSums];
+#pragma unroll
+    for (int s = 0; s < kMaxSums; ++s) out[s] = 0.0;
+    // threads t with (blockIdx*blockDim + t) % k == c
+    const int first = static_cast<int>(((c - (static_cast<long long>(blockIdx.x) * blockDim.x) % k) % k + k) % k);
+    for (int t = first; t < static_cast<int>(blockDim.x); t += k) {
+#pragma unroll
+      for (int s = 0; s < kMaxSums; ++s) out[s] += red[t][s];
+    }
+    double* dst = partial + (static_cast<long long>(blockIdx.x) * k + c) * kMaxSums;
+#pragma unroll
+    for (int s = 0; s < kMaxSums; ++s) dst[s] = out[s];
+  }
+}
+
+struct DestSpec {
+  void* ptr[kMaxSums];
+  int sum_id[kMaxSums];
+  int dtype[kMaxSums];  // 0 = f32, 1 = f64, 2 = i64
+  int per_col[kMaxSums];  // 1: dest has k elements, 0: dest is a scalar (sum over columns)
+  int n;
+};
+
+// one block per column: fixed-order reduction over blocks, then add into the destination states
+__global__ void __launch_bounds__(kBlock) moments_finalize_kernel(const double* __restrict__ partial, int nblocks,
+                                                                  int k, DestSpec spec, double* __restrict__ out_sums) {
+  const int c = blockIdx.x;
+  __shared__ double red[kMaxSums][kBlock / kWave];
+  double acc[kMaxSums];
+#pragma unroll
+  for (int s = 0; s < kMaxSums; ++s) acc[s] = 0.0;
+  for (int b = threadIdx.x; b < nblocks; b += blockDim.x) {
+    const double* src = partial + (static_cast<long long>(b) * k + c) * kMaxSums;
+#pragma unroll
+    for (int s = 0; s < kMaxSums; ++s) acc[s] += src[s];
+  }
+  const int wid = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+#pragma unroll
+  for (int s = 0; s < kMaxSums; ++s) {
+    const double v = wave_sum(acc[s]);
+    if (lane == 0) red[s][wid] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kMaxSums) {
+    double v = 0.0;
+    for (int w = 0; w < static_cast<int>(blockDim.x / kWave); ++w) v += red[threadIdx.x][w];
+    if (out_sums) out_sums[c * kMaxSums + threadIdx.x] = v;
+    red[threadIdx.x][0] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < spec.n) {
+    const int j = threadIdx.x;
+    const double v = red[spec.sum_id[j]][0];
+    const int idx = spec.per_col[j] ? c : 0;
+    // per-column destination, or a scalar destination fed from column 0 (counts are equal in every column)
+    if (spec.per_col[j] || c == 0) {
+      if (spec.dtype[j] == 0) reinterpret_cast<float*>(spec.ptr[j])[idx] += static_cast<float>(v);
+      else if (spec.dtype[j] == 1) reinterpret_cast<double*>(spec.ptr[j])[idx] += v;
+      else reinterpret_cast<int64_t*>(spec.ptr[j])[idx] += static_cast<int64_t>(llrint(v));
+    }
+  }
+}
+
+}  // namespace
+
+// preds/target: [N, k] (or [N] with k = 1), same floating dtype. dests[j] += sum[sum_ids[j]] (per column, or over
+// column 0 when dest has one element and k > 1, e.g. observation counts). Returns the [k, 14] fp64 sums when want_sums.
+at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int64_t num_outputs, int64_t mask,
+                          double eps, double power, const c10::optional<at::Tensor>& shift_p,
+                          const c10::optional<at::Tensor>& shift_t, at::TensorList dests,
+                          at::IntArrayRef sum_ids, bool want_sums) {
+  TM_CHECK_CUDA(preds);
+  TM_CHECK_CONTIG(preds);
+  TM_CHECK_CONTIG(target);
+  TORCH_CHECK(preds.scalar_type() == target.scalar_type(), "moments_update: preds/target dtype mismatch");
+  TORCH_CHECK(preds.numel() == target.numel(), "moments_update: preds/target numel mismatch");
+  TORCH_CHECK(dests.size() == sum_ids.size() && dests.size() <= kMaxSums, "moments_update: bad destination list");
+  const int k = static_cast<int>(num_outputs);
+  TORCH_CHECK(k >= 1 && preds.numel() % k == 0, "moments_update: numel not divisible by num_outputs");
+  const long long n_rows = preds.numel() / k;
+  auto dopt = preds.options().dtype(at::kDouble);
+  at::Tensor sums = want_sums ? at::zeros({k, kMaxSums}, dopt) : at::Tensor();
+  if (n_rows == 0) return sums;
+  // thread count must be a multiple of k so each thread keeps one column
+  int block = kBlock;
+  long long blocks = (n_rows * k + block - 1) / block;
+  blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);
+  if (k > 1) {
+    // grid * block multiple of k: use block = 256 and blocks multiple of k/gcd(256,k)
+    long long g = k;
+    long long a = block;
+    while (a) { long long r = g % a; g = a; a = r; }
+    const long long step = k / g;
+    blocks = ((blocks + step - 1) / step) * step;
+  }
+  at::Tensor partial = at::empty({blocks, k, kMaxSums}, dopt);
+  const float* sp = nullptr;
+  const float* st = nullptr;
+  if (shift_p.has_value()) {
+    TORCH_CHECK(shift_p->scalar_type() == at::kFloat && shift_p->numel() == k, "shift_p must be f32[k]");
+    sp = shift_p->data_ptr<float>();
+  }
+  if (shift_t.has_value()) {
+    TORCH_CHECK(shift_t->scalar_type() == at::kFloat && shift_t->numel() == k, "shift_t must be f32[k]");
+    st = shift_t->data_ptr<float>();
+  }
+  auto s = stream();
+  TM_DISPATCH_FLOAT(preds.scalar_type(), "moments_update", [&] {
+    hipLaunchKernelGGL((moments_partial_kernel<scalar_t>), dim3(blocks), dim3(block), 0, s,
+                       reinterpret_cast<const scalar_t*>(preds.data_ptr()),
+                       reinterpret_cast<const scalar_t*>(target.data_ptr()), n_rows, k, static_cast<int>(mask), eps,
+                       power, sp, st, partial.data_ptr<double>());
+  });
+  DestSpec spec{};
+  spec.n = static_cast<int>(dests.size());
+  for (int j = 0; j < spec.n; ++j) {
+    const at::Tensor& d = dests[j];
+    TORCH_CHECK(d.is_cuda() && d.is_contiguous(), "moments_update: destination states must be contiguous GPU tensors");
+    TORCH_CHECK(d.numel() == k || d.numel() == 1, "moments_update: destination must have k or 1 elements");
+    spec.ptr[j] = d.data_ptr();
+    spec.sum_id[j] = static_cast<int>(sum_ids[j]);
+    TORCH_CHECK(spec.sum_id[j] >= 0 && spec.sum_id[j] < kMaxSums, "moments_update: bad sum id");
+    spec.per_col[j] = d.numel() == k && k > 1 ? 1 : (k == 1 ? 1 : 0);
+    switch (d.scalar_type()) {
+      case at::kFloat: spec.dtype[j] = 0; break;
+      case at::kDouble: spec.dtype[j] = 1; break;
+      case at::kLong: spec.dtype[j] = 2; break;
+      default: TORCH_CHECK(false, "moments_update: destination dtype must be f32/f64/i64");
+    }
+  }
+  hipLaunchKernelGGL(moments_finalize_kernel, dim3(k), dim3(kBlock), 0, s, partial.data_ptr<double>(),
+                     static_cast<int>(blocks), k, spec, want_sums ? sums.data_ptr<double>() : nullptr);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return sums;
+}
+
+}  // namespace tm_amd
+
+TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def(
+      "moments_update(Tensor preds, Tensor target, int num_outputs, int mask, float eps, float power, "
+      "Tensor? shift_p, Tensor? shift_t, Tensor(a!)[] dests, int[] sum_ids, bool want_sums) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) { m.impl("moments_update", &tm_amd::moments_update); }

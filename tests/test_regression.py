@@ -1,0 +1,161 @@
+"""Regression metrics vs scikit-learn / scipy oracles (reference test model: ``T/regression``)."""
+from functools import partial
+
+import numpy as np
+import pytest
+import torch
+from scipy import stats
+from sklearn import metrics as skm
+
+import torchmetrics_amd as tm
+import torchmetrics_amd.functional as F
+from tests.helpers import assert_close, run_class_test, run_ddp_class_test, run_functional_test
+
+NB, BS = 4, 32
+DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+def _np(x):
+    return x.detach().cpu().double().numpy()
+
+
+def _inputs(k=1, positive=False):
+    shape = (NB, BS) if k == 1 else (NB, BS, k)
+    p, t = torch.rand(shape), torch.rand(shape)
+    if not positive:
+        p, t = p * 4 - 2, t * 4 - 2
+    return p, t
+
+
+def _ref(name, preds, target, **kw):
+    p, t = _np(preds), _np(target)
+    if name == "mse":
+        v = skm.mean_squared_error(t, p, multioutput="raw_values" if p.ndim == 2 else "uniform_average")
+        return v if kw.get("squared", True) else np.sqrt(v)
+    if name == "mae":
+        return skm.mean_absolute_error(t.reshape(-1), p.reshape(-1))
+    if name == "mape":
+        return np.mean(np.abs(p - t) / np.maximum(np.abs(t), 1.17e-06))
+    if name == "smape":
+        return np.mean(2 * np.abs(p - t) / np.maximum(np.abs(t) + np.abs(p), 1.17e-06))
+    if name == "wmape":
+        return np.abs(p - t).sum() / np.abs(t).sum()
+    if name == "msle":
+        return skm.mean_squared_log_error(t, p)
+    if name == "logcosh":
+        return np.mean(np.log(np.cosh(p - t)), axis=0)
+    if name == "r2":
+        return skm.r2_score(t, p, multioutput=kw.get("multioutput", "uniform_average"))
+    if name == "ev":
+        return skm.explained_variance_score(t, p, multioutput=kw.get("multioutput", "uniform_average"))
+    if name == "pearson":
+        if p.ndim == 2:
+            return np.array([stats.pearsonr(t[:, i], p[:, i])[0] for i in range(p.shape[1])])
+        return stats.pearsonr(t, p)[0]
+    if name == "spearman":
+        return stats.spearmanr(t, p)[0]
+    if name == "kendall":
+        return stats.kendalltau(p, t)[0]
+    if name == "minkowski":
+        return np.sum(np.abs(p - t) ** kw["p"]) ** (1 / kw["p"])
+    if name == "tweedie0":
+        return skm.mean_tweedie_deviance(t, p, power=0.0)
+    if name == "tweedie15":
+        return skm.mean_tweedie_deviance(t, p, power=1.5)
+    if name == "concordance":
+        mx, my = p.mean(0), t.mean(0)
+        vx, vy = p.var(0, ddof=1), t.var(0, ddof=1)
+        cov = ((p - mx) * (t - my)).sum(0) / (p.shape[0] - 1)
+        return 2 * cov / (vx + vy + (mx - my) ** 2)
+    if name == "rse":
+        return np.sum((t - p) ** 2) / np.sum((t - t.mean()) ** 2)
+    raise ValueError(name)
+
+
+CASES = [
+    ("mse", tm.MeanSquaredError, F.mean_squared_error, {}, False, 1),
+    ("mse", tm.MeanSquaredError, F.mean_squared_error, {"squared": False}, False, 1),
+    ("mae", tm.MeanAbsoluteError, F.mean_absolute_error, {}, False, 1),
+    ("mape", tm.MeanAbsolutePercentageError, F.mean_absolute_percentage_error, {}, False, 1),
+    ("smape", tm.SymmetricMeanAbsolutePercentageError, F.symmetric_mean_absolute_percentage_error, {}, False, 1),
+    ("wmape", tm.WeightedMeanAbsolutePercentageError, F.weighted_mean_absolute_percentage_error, {}, False, 1),
+    ("msle", tm.MeanSquaredLogError, F.mean_squared_log_error, {}, True, 1),
+    ("logcosh", tm.LogCoshError, F.log_cosh_error, {}, False, 1),
+    ("r2", tm.R2Score, F.r2_score, {}, False, 1),
+    ("ev", tm.ExplainedVariance, F.explained_variance, {}, False, 1),
+    ("pearson", tm.PearsonCorrCoef, F.pearson_corrcoef, {}, False, 1),
+    ("concordance", tm.ConcordanceCorrCoef, F.concordance_corrcoef, {}, False, 1),
+    ("spearman", tm.SpearmanCorrCoef, F.spearman_corrcoef, {}, False, 1),
+    ("kendall", tm.KendallRankCorrCoef, F.kendall_rank_corrcoef, {}, False, 1),
+    ("minkowski", tm.MinkowskiDistance, F.minkowski_distance, {"p": 3}, False, 1),
+    ("tweedie0", tm.TweedieDevianceScore, partial(F.tweedie_deviance_score, power=0.0), {"power": 0.0}, False, 1),
+    ("tweedie15", tm.TweedieDevianceScore, partial(F.tweedie_deviance_score, power=1.5), {"power": 1.5}, True, 1),
+    ("rse", tm.RelativeSquaredError, F.relative_squared_error, {}, False, 1),
+]
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("name,cls,fn,args,positive,k", CASES)
+def test_regression(device, name, cls, fn, args, positive, k):
+    p, t = _inputs(k, positive)
+    ref_kw = {kk: v for kk, v in args.items() if kk in ("squared", "p")}
+    ref = partial(_ref, name, **ref_kw)
+    fn_args = {kk: v for kk, v in args.items() if kk in ("squared", "p")}
+    run_class_test(p, t, cls, ref, metric_args=args, device=device, atol=1e-4)
+    run_functional_test(p, t, partial(fn, **fn_args), ref, device=device, atol=1e-4)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("name,cls,extra", [
+    ("mse", tm.MeanSquaredError, {"num_outputs": 3}),
+    ("r2", tm.R2Score, {"num_outputs": 3, "multioutput": "raw_values"}),
+    ("pearson", tm.PearsonCorrCoef, {"num_outputs": 3}),
+    ("logcosh", tm.LogCoshError, {"num_outputs": 3}),
+])
+def test_multioutput(device, name, cls, extra):
+    p, t = _inputs(3)
+    ref = partial(_ref, name, **({"multioutput": extra["multioutput"]} if "multioutput" in extra else {}))
+    run_class_test(p, t, cls, ref, metric_args=extra, device=device, atol=1e-4)
+
+
+def test_kendall_variants_and_ttest():
+    p, t = torch.randint(0, 5, (60,)).float(), torch.randint(0, 5, (60,)).float()
+    for v in ("b", "c"):
+        tau = F.kendall_rank_corrcoef(p, t, variant=v)
+        ref = stats.kendalltau(_np(p), _np(t), variant=v)[0]
+        assert_close(tau, ref, atol=1e-5)
+    tau, pv = F.kendall_rank_corrcoef(p, t, variant="b", t_test=True)
+    assert_close(pv, stats.kendalltau(_np(p), _np(t), variant="b", method="asymptotic")[1], atol=1e-3)
+
+
+def test_cosine_kl_csi():
+    p, t = torch.randn(10, 6), torch.randn(10, 6)
+    sk = np.array([np.dot(a, b) / np.linalg.norm(a) / np.linalg.norm(b) for a, b in zip(_np(p), _np(t))])
+    assert_close(F.cosine_similarity(p, t, "none"), sk, atol=1e-5)
+    m = tm.CosineSimilarity(reduction="mean")
+    m.update(p, t)
+    assert_close(m.compute(), sk.mean(), atol=1e-5)
+    a, b = torch.rand(8, 5), torch.rand(8, 5)
+    an, bn = _np(a) / _np(a).sum(1, keepdims=True), _np(b) / _np(b).sum(1, keepdims=True)
+    assert_close(F.kl_divergence(a, b), np.mean([stats.entropy(x, y) for x, y in zip(an, bn)]), atol=1e-5)
+    pr, tg = torch.rand(5, 4, 4), torch.rand(5, 4, 4)
+    h = ((pr >= 0.5) & (tg >= 0.5)).sum()
+    mi = ((pr < 0.5) & (tg >= 0.5)).sum()
+    fa = ((pr >= 0.5) & (tg < 0.5)).sum()
+    assert_close(F.critical_success_index(pr, tg, 0.5), h / (h + mi + fa))
+
+
+def test_regression_grad_flows():
+    p = torch.randn(20, requires_grad=True)
+    t = torch.randn(20)
+    v = F.mean_squared_error(p, t)
+    v.backward()
+    assert_close(p.grad, 2 * (p - t).detach() / 20, atol=1e-6)
+
+
+@pytest.mark.ddp
+@pytest.mark.parametrize("name,cls", [("pearson", tm.PearsonCorrCoef), ("mse", tm.MeanSquaredError),
+                                      ("spearman", tm.SpearmanCorrCoef), ("r2", tm.R2Score)])
+def test_regression_ddp(name, cls):
+    p, t = _inputs()
+    run_ddp_class_test(p, t, cls, partial(_ref, name), atol=1e-4)

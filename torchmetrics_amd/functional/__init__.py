@@ -1,2 +1,3 @@
 """Functional (stateless) metrics (parity: reference ``F/__init__.py``)."""
 from torchmetrics_amd.functional.classification import *  # noqa: F401,F403
+from torchmetrics_amd.functional.regression import *  # noqa: F401,F403

@@ -138,3 +138,43 @@ def histogram(x: Tensor, minlength: int) -> Tensor:
         _ops().histogram(x.contiguous(), out, flag)
         return out
     return torch.bincount(x, minlength=minlength)
+
+
+# ------------------------------------------------------------------------------------------------------ regression
+# sum ids of csrc/regression/moments.hip
+SSE, SAE, SP, ST, SPP, STT, SPT, MAPE, SMAPE, SABST, MSLE, LOGCOSH, MINK, COUNT = range(14)
+
+
+def moments_update(
+    preds: Tensor,
+    target: Tensor,
+    num_outputs: int,
+    sums: "list[int]",
+    dests: "list[Tensor]",
+    dest_ids: "list[int]",
+    eps: float = 1.17e-06,
+    power: float = 2.0,
+    shift_p: Optional[Tensor] = None,
+    shift_t: Optional[Tensor] = None,
+    want_sums: bool = False,
+) -> Optional[Tensor]:
+    """One pass computing the requested per-output sums and adding ``sum[dest_ids[j]]`` into ``dests[j]``.
+
+    ``preds``/``target`` are ``[N, num_outputs]`` (or 1-D). Returns the ``[num_outputs, 14]`` fp64 sums if asked.
+    """
+    mask = 0
+    for s in list(sums) + list(dest_ids):
+        mask |= 1 << int(s)
+    needs_grad = torch.is_grad_enabled() and (preds.requires_grad or target.requires_grad)
+    if preds.is_cuda and not needs_grad:
+        if preds.dtype != target.dtype or not preds.is_floating_point():
+            dt = torch.promote_types(preds.dtype, target.dtype)
+            dt = dt if dt.is_floating_point else torch.float32
+            preds, target = preds.to(dt), target.to(dt)
+        res = _ops().moments_update(
+            preds.contiguous(), target.contiguous(), int(num_outputs), mask, float(eps), float(power),
+            shift_p, shift_t, list(dests), [int(i) for i in dest_ids], bool(want_sums),
+        )
+        return res if want_sums else None
+    return _cpu.moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_t, dests, dest_ids,
+                               want_sums)

@@ -166,3 +166,39 @@ def bin_confmat_finalize(ws: Tensor, not_prob: Tensor, confmat: Tensor) -> None:
     confmat.view(-1, 4).add_(torch.stack([tn, fp, fn, tp], dim=1))
     w.zero_()
     not_prob.zero_()
+
+
+def moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_t, dests, dest_ids, want_sums):
+    k = int(num_outputs)
+    p = preds.reshape(-1, k).double()
+    t = target.reshape(-1, k).double()
+    d = p - t
+    ad = d.abs()
+    sums = torch.zeros(k, 14, dtype=torch.float64, device=p.device)
+    pc = p - (shift_p.double() if shift_p is not None else 0.0)
+    tc = t - (shift_t.double() if shift_t is not None else 0.0)
+    cols = {
+        0: lambda: (d * d).sum(0),
+        1: lambda: ad.sum(0),
+        2: lambda: pc.sum(0),
+        3: lambda: tc.sum(0),
+        4: lambda: (pc * pc).sum(0),
+        5: lambda: (tc * tc).sum(0),
+        6: lambda: (pc * tc).sum(0),
+        7: lambda: (ad / t.abs().clamp(min=eps)).sum(0),
+        8: lambda: (2 * ad / (p.abs() + t.abs()).clamp(min=eps)).sum(0),
+        9: lambda: t.abs().sum(0),
+        10: lambda: ((torch.log1p(p) - torch.log1p(t)) ** 2).sum(0),
+        11: lambda: (ad + torch.log1p(torch.exp(-2 * ad)) - 0.69314718055994530942).sum(0),
+        12: lambda: (ad**power).sum(0),
+        13: lambda: torch.full((k,), float(p.shape[0]), dtype=torch.float64, device=p.device),
+    }
+    for sid, fn in cols.items():
+        if mask & (1 << sid) or sid == 13:
+            sums[:, sid] = fn()
+    for dst, sid in zip(dests, dest_ids):
+        val = sums[:, sid] if dst.numel() == k else sums[0, sid]
+        if dst.dtype == torch.int64:
+            val = torch.round(val).long()
+        dst += val.reshape(dst.shape).to(dst.dtype)
+    return sums if want_sums else None

@@ -1,0 +1,209 @@
+"""Correlation / similarity / divergence module metrics.
+
+Parity: reference ``S/regression/{pearson,concordance,spearman,kendall,cosine_similarity,kl_divergence}.py``.
+Pearson-family states use ``dist_reduce_fx=None`` and are merged per rank in ``compute`` (Chan et al.).
+"""
+from typing import Any, List, Optional, Sequence, Tuple, Union
+
+import torch
+from torch import Tensor
+
+from torchmetrics_amd.functional.regression.correlation import (
+    _concordance_corrcoef_compute,
+    _cosine_similarity_compute,
+    _cosine_similarity_update,
+    _final_aggregation,
+    _kendall_corrcoef_compute,
+    _kld_compute,
+    _kld_update,
+    _MetricVariant,
+    _pearson_corrcoef_compute,
+    _pearson_corrcoef_update,
+    _spearman_corrcoef_compute,
+    _spearman_corrcoef_update,
+    _TestAlternative,
+)
+from torchmetrics_amd.functional.regression.streaming import _check_data_shape_to_num_outputs
+from torchmetrics_amd.metric import Metric
+from torchmetrics_amd.utilities.checks import _check_same_shape
+from torchmetrics_amd.utilities.data import dim_zero_cat
+from torchmetrics_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
+from torchmetrics_amd.utilities.prints import rank_zero_warn
+
+
+class PearsonCorrCoef(Metric):
+    is_differentiable = True
+    higher_is_better = None
+    full_state_update: bool = True
+    plot_lower_bound: float = -1.0
+    plot_upper_bound: float = 1.0
+
+    def __init__(self, num_outputs: int = 1, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if not isinstance(num_outputs, int) and num_outputs < 1:
+            raise ValueError("Expected argument `num_outputs` to be an int larger than 0, but got {num_outputs}")
+        self.num_outputs = num_outputs
+        for name in ("mean_x", "mean_y", "var_x", "var_y", "corr_xy", "n_total"):
+            self.add_state(name, default=torch.zeros(self.num_outputs), dist_reduce_fx=None)
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        (self.mean_x, self.mean_y, self.var_x, self.var_y, self.corr_xy, self.n_total) = _pearson_corrcoef_update(
+            preds, target, self.mean_x, self.mean_y, self.var_x, self.var_y, self.corr_xy, self.n_total,
+            self.num_outputs,
+        )
+
+    def _merged(self) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
+        if (self.num_outputs == 1 and self.mean_x.numel() > 1) or (self.num_outputs > 1 and self.mean_x.ndim > 1):
+            return _final_aggregation(self.mean_x, self.mean_y, self.var_x, self.var_y, self.corr_xy, self.n_total)
+        return self.mean_x, self.mean_y, self.var_x, self.var_y, self.corr_xy, self.n_total
+
+    def compute(self) -> Tensor:
+        _, _, var_x, var_y, corr_xy, n_total = self._merged()
+        return _pearson_corrcoef_compute(var_x, var_y, corr_xy, n_total)
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
+
+
+class ConcordanceCorrCoef(PearsonCorrCoef):
+    def compute(self) -> Tensor:
+        mean_x, mean_y, var_x, var_y, corr_xy, n_total = self._merged()
+        return _concordance_corrcoef_compute(mean_x, mean_y, var_x, var_y, corr_xy, n_total)
+
+
+class SpearmanCorrCoef(Metric):
+    is_differentiable: bool = False
+    higher_is_better: bool = True
+    full_state_update: bool = False
+    plot_lower_bound: float = -1.0
+    plot_upper_bound: float = 1.0
+
+    def __init__(self, num_outputs: int = 1, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        rank_zero_warn(
+            "Metric `SpearmanCorrcoef` will save all targets and predictions in the buffer."
+            " For large datasets, this may lead to large memory footprint."
+        )
+        if not isinstance(num_outputs, int) and num_outputs < 1:
+            raise ValueError("Expected argument `num_outputs` to be an int larger than 0, but got {num_outputs}")
+        self.num_outputs = num_outputs
+        self.add_state("preds", default=[], dist_reduce_fx="cat")
+        self.add_state("target", default=[], dist_reduce_fx="cat")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        preds, target = _spearman_corrcoef_update(preds, target, num_outputs=self.num_outputs)
+        self.preds.append(preds)
+        self.target.append(target)
+
+    def compute(self) -> Tensor:
+        return _spearman_corrcoef_compute(dim_zero_cat(self.preds), dim_zero_cat(self.target))
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
+
+
+class KendallRankCorrCoef(Metric):
+    is_differentiable = False
+    higher_is_better = None
+    full_state_update = True
+    plot_lower_bound: float = -1.0
+    plot_upper_bound: float = 1.0
+
+    def __init__(
+        self,
+        variant: str = "b",
+        t_test: bool = False,
+        alternative: Optional[str] = "two-sided",
+        num_outputs: int = 1,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        if not isinstance(t_test, bool):
+            raise ValueError(f"Argument `t_test` is expected to be of a type `bool`, but got {type(t_test)}.")
+        if t_test and alternative is None:
+            raise ValueError("Argument `alternative` is required if `t_test=True` but got `None`.")
+        self.variant = _MetricVariant.from_str(str(variant))
+        self.alternative = _TestAlternative.from_str(str(alternative)) if t_test else None
+        self.num_outputs = num_outputs
+        self.add_state("preds", [], dist_reduce_fx="cat")
+        self.add_state("target", [], dist_reduce_fx="cat")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        _check_same_shape(preds, target)
+        _check_data_shape_to_num_outputs(preds, target, self.num_outputs)
+        if self.num_outputs == 1:
+            preds, target = preds.unsqueeze(1), target.unsqueeze(1)
+        self.preds.append(preds)
+        self.target.append(target)
+
+    def compute(self) -> Union[Tensor, Tuple[Tensor, Tensor]]:
+        tau, p = _kendall_corrcoef_compute(dim_zero_cat(self.preds), dim_zero_cat(self.target), self.variant,
+                                           self.alternative)
+        return (tau, p) if p is not None else tau
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
+
+
+class CosineSimilarity(Metric):
+    is_differentiable: bool = True
+    higher_is_better: bool = True
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+
+    def __init__(self, reduction: Optional[str] = "sum", **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        allowed = ("mean", "sum", "none", None)
+        if reduction not in allowed:
+            raise ValueError(f"Expected argument `reduction` to be one of {allowed} but got {reduction}")
+        self.reduction = reduction
+        self.add_state("preds", [], dist_reduce_fx="cat")
+        self.add_state("target", [], dist_reduce_fx="cat")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        preds, target = _cosine_similarity_update(preds, target)
+        self.preds.append(preds)
+        self.target.append(target)
+
+    def compute(self) -> Tensor:
+        return _cosine_similarity_compute(dim_zero_cat(self.preds), dim_zero_cat(self.target), self.reduction)
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
+
+
+class KLDivergence(Metric):
+    is_differentiable: bool = True
+    higher_is_better: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+
+    def __init__(self, log_prob: bool = False, reduction: Optional[str] = "mean", **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if not isinstance(log_prob, bool):
+            raise TypeError(f"Expected argument `log_prob` to be bool but got {log_prob}")
+        self.log_prob = log_prob
+        allowed = ["mean", "sum", "none", None]
+        if reduction not in allowed:
+            raise ValueError(f"Expected argument `reduction` to be one of {allowed} but got {reduction}")
+        self.reduction = reduction
+        if self.reduction in ["mean", "sum"]:
+            self.add_state("measures", torch.tensor(0.0), dist_reduce_fx="sum")
+        else:
+            self.add_state("measures", [], dist_reduce_fx="cat")
+        self.add_state("total", torch.tensor(0), dist_reduce_fx="sum")
+
+    def update(self, p: Tensor, q: Tensor) -> None:
+        measures, total = _kld_update(p, q, self.log_prob)
+        if self.reduction is None or self.reduction == "none":
+            self.measures.append(measures)
+        else:
+            self.measures += measures.sum()
+        self.total += total
+
+    def compute(self) -> Tensor:
+        measures = dim_zero_cat(self.measures) if self.reduction in ["none", None] else self.measures
+        return _kld_compute(measures, self.total, self.reduction)
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)

@@ -1,0 +1,96 @@
+"""BASELINE config #4: FrechetInceptionDistance on random 50k x 2048 feature tensors (real + fake).
+
+Times (a) the state updates (50 batches of 1000 features per distribution) and (b) ``compute()``, for our
+implementation and for an op-for-op emulation of the reference (``features.double()``, ``sum(0)``, ``t().mm()``;
+compute with ``torch.linalg.eigvals(Σ1 Σ2)``, reference ``S/image/fid.py:159-179,336-361``).
+Prints one JSON line.
+"""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from torchmetrics_amd.image import FrechetInceptionDistance  # noqa: E402
+
+N, D, B = 50_000, 2048, 1000
+
+
+class _Id(torch.nn.Module):
+    num_features = D
+
+    def forward(self, x):
+        return x
+
+
+def _sync():
+    torch.cuda.synchronize()
+
+
+def ours(real, fake):
+    m = FrechetInceptionDistance(feature=_Id()).cuda()
+    _sync()
+    t0 = time.perf_counter()
+    for r, f in zip(real, fake):
+        m.update(r, real=True)
+        m.update(f, real=False)
+    _sync()
+    t1 = time.perf_counter()
+    v = m.compute()
+    _sync()
+    t2 = time.perf_counter()
+    return v.item(), t1 - t0, t2 - t1
+
+
+def reference(real, fake):
+    dev = real[0].device
+    st = {k: torch.zeros(D, dtype=torch.float64, device=dev) for k in ("rs", "fs")}
+    cv = {k: torch.zeros(D, D, dtype=torch.float64, device=dev) for k in ("rc", "fc")}
+    _sync()
+    t0 = time.perf_counter()
+    for r, f in zip(real, fake):
+        rd, fd = r.double(), f.double()
+        st["rs"] += rd.sum(0)
+        cv["rc"] += rd.t().mm(rd)
+        st["fs"] += fd.sum(0)
+        cv["fc"] += fd.t().mm(fd)
+    _sync()
+    t1 = time.perf_counter()
+    n = N
+    mr, mf = (st["rs"] / n).unsqueeze(0), (st["fs"] / n).unsqueeze(0)
+    cr = (cv["rc"] - n * mr.t().mm(mr)) / (n - 1)
+    cf = (cv["fc"] - n * mf.t().mm(mf)) / (n - 1)
+    a = (mr - mf).square().sum()
+    b = cr.trace() + cf.trace()
+    c = torch.linalg.eigvals(cr @ cf).sqrt().real.sum(dim=-1)
+    v = a + b - 2 * c
+    _sync()
+    t2 = time.perf_counter()
+    return v.item(), t1 - t0, t2 - t1
+
+
+def main():
+    g = torch.Generator(device="cuda").manual_seed(0)
+    real = [torch.randn(B, D, device="cuda", generator=g) for _ in range(N // B)]
+    fake = [torch.randn(B, D, device="cuda", generator=g) * 1.1 + 0.05 for _ in range(N // B)]
+    ours(real[:2], fake[:2])  # warmup (kernels, rocSOLVER handles)
+    v_o, up_o, cp_o = ours(real, fake)
+    v_r, up_r, cp_r = reference(real, fake)
+    out = {
+        "metric": "FID update features/s and compute wall-clock (50k x 2048 real + fake)",
+        "ours": {"fid": v_o, "update_s": round(up_o, 4), "compute_s": round(cp_o, 4),
+                 "features_per_s": round(2 * N / up_o, 1)},
+        "reference_emulated": {"fid": v_r, "update_s": round(up_r, 4), "compute_s": round(cp_r, 4),
+                               "features_per_s": round(2 * N / up_r, 1)},
+        "update_speedup": round(up_r / up_o, 3),
+        "compute_speedup": round(cp_r / cp_o, 3),
+        "rel_diff": abs(v_o - v_r) / max(abs(v_r), 1e-12),
+    }
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

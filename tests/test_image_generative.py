@@ -1,0 +1,119 @@
+"""FID / KID / IS / MiFID against numpy/scipy oracles and the fp64-MFMA SYRK kernel against an fp64 GEMM."""
+import numpy as np
+import pytest
+import torch
+from scipy import linalg
+
+from torchmetrics_amd import ops
+from torchmetrics_amd.image import (
+    FrechetInceptionDistance,
+    InceptionScore,
+    KernelInceptionDistance,
+    MemorizationInformedFrechetInceptionDistance,
+)
+from torchmetrics_amd.models import InceptionV3Features
+from tests.helpers import assert_close
+
+DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+class _Id(torch.nn.Module):
+    def __init__(self, d):
+        super().__init__()
+        self.num_features = d
+
+    def forward(self, x):
+        return x
+
+
+def _np_fid(r, f):
+    r, f = r.double().cpu().numpy(), f.double().cpu().numpy()
+    mu1, mu2 = r.mean(0), f.mean(0)
+    s1, s2 = np.cov(r.T), np.cov(f.T)
+    return ((mu1 - mu2) ** 2).sum() + np.trace(s1) + np.trace(s2) - 2 * np.trace(linalg.sqrtm(s1 @ s2).real)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("d", [16, 130])
+def test_fid_matches_scipy(device, d):
+    g = torch.Generator().manual_seed(0)
+    real = torch.randn(300, d, generator=g)
+    fake = torch.randn(300, d, generator=g) * 1.2 + 0.1
+    m = FrechetInceptionDistance(feature=_Id(d)).to(device)
+    for chunk in real.split(100):
+        m.update(chunk.to(device), real=True)
+    for chunk in fake.split(77):
+        m.update(chunk.to(device), real=False)
+    assert_close(m.compute(), _np_fid(real, fake), atol=1e-3, rtol=1e-4)
+
+
+def test_fid_reset_real_features():
+    m = FrechetInceptionDistance(feature=_Id(8), reset_real_features=False)
+    m.update(torch.randn(10, 8), real=True)
+    m.update(torch.randn(10, 8), real=False)
+    m.reset()
+    assert m.real_features_num_samples == 10 and m.fake_features_num_samples == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,d,dtype", [(1, 64, torch.float32), (1000, 2048, torch.float32), (517, 300, torch.bfloat16),
+                                       (33, 129, torch.float16), (4096, 256, torch.float64)])
+def test_syrk_kernel_vs_fp64_gemm(n, d, dtype):
+    x = torch.randn(n, d, device="cuda").to(dtype)
+    s0 = torch.randn(d, device="cuda", dtype=torch.float64)
+    c0 = torch.randn(d, d, device="cuda", dtype=torch.float64)
+    s, c = s0.clone(), c0.clone()
+    ops.feature_moments_update(x, s, c)
+    xd = x.double()
+    torch.testing.assert_close(s, s0 + xd.sum(0), rtol=1e-12, atol=1e-9)
+    torch.testing.assert_close(c, c0 + xd.t() @ xd, rtol=1e-12, atol=1e-9)
+
+
+def test_kid_matches_loop_oracle():
+    g = torch.Generator().manual_seed(1)
+    real, fake = torch.randn(120, 8, generator=g), torch.randn(120, 8, generator=g) + 0.3
+    m = KernelInceptionDistance(feature=_Id(8), subsets=6, subset_size=40)
+    m.update(real, True)
+    m.update(fake, False)
+    torch.manual_seed(7)
+    mean, std = m.compute()
+    torch.manual_seed(7)
+    scores = []
+    for _ in range(6):
+        fr = real[torch.randperm(120)[:40]].double()
+        ff = fake[torch.randperm(120)[:40]].double()
+        k = lambda a, b: (a @ b.T / 8 + 1) ** 3  # noqa: E731
+        kxx, kyy, kxy = k(fr, fr), k(ff, ff), k(fr, ff)
+        mm = 40
+        v = (kxx.sum() - kxx.diag().sum() + kyy.sum() - kyy.diag().sum()) / (mm * (mm - 1)) - 2 * kxy.sum() / mm**2
+        scores.append(v)
+    s = torch.stack(scores)
+    assert_close(mean, s.mean(), atol=1e-5)
+    assert_close(std, s.std(unbiased=False), atol=1e-5)
+
+
+def test_inception_score_and_mifid():
+    g = torch.Generator().manual_seed(2)
+    logits = torch.randn(100, 10, generator=g)
+    m = InceptionScore(feature=_Id(10), splits=1)
+    m.update(logits)
+    mean, _ = m.compute()
+    p = logits.softmax(1)
+    ref = (p * (p.log() - p.mean(0, keepdim=True).log())).sum(1).mean().exp()
+    assert_close(mean, ref, atol=1e-5)
+    mf = MemorizationInformedFrechetInceptionDistance(feature=_Id(6))
+    real, fake = torch.randn(50, 6, generator=g), torch.randn(50, 6, generator=g)
+    mf.update(real, True)
+    mf.update(fake, False)
+    assert torch.isfinite(mf.compute())
+
+
+def test_inception_network_shapes():
+    net = InceptionV3Features(["64", "2048", "logits_unbiased"])
+    imgs = torch.randint(0, 255, (2, 3, 80, 80), dtype=torch.uint8)
+    f64, f2048, logits = net(imgs)
+    assert f64.shape == (2, 64) and f2048.shape == (2, 2048) and logits.shape == (2, 1008)
+    fid = FrechetInceptionDistance(feature=64)
+    fid.update(imgs, real=True)
+    fid.update(imgs, real=False)
+    assert fid.real_features_cov_sum.shape == (64, 64)

@@ -37,3 +37,12 @@ if [[ $STEP == tune ]]; then
     cd $GRAFT_REPO_ROOT
   done
 fi
+if [[ $STEP == fid ]]; then
+  timeout -k 10 900 python -m pytest tests/test_image_generative.py -m gpu -x -q > gpurun_out/pytest_fid.log 2>&1 || { tail -40 gpurun_out/pytest_fid.log; exit 1; }
+  tail -2 gpurun_out/pytest_fid.log
+  timeout -k 10 900 python benchmarks/bench_fid.py > gpurun_out/bench_fid.log 2>&1 || { tail -40 gpurun_out/bench_fid.log; exit 1; }
+  tail -1 gpurun_out/bench_fid.log
+fi
+if [[ $STEP == fidprof ]]; then
+  cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/fidprof -o f --output-format csv -- python3 $GRAFT_REPO_ROOT/benchmarks/bench_fid.py > $GRAFT_REPO_ROOT/gpurun_out/fidprof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/fidprof.log; exit 1; }
+fi

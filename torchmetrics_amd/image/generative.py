@@ -1,0 +1,394 @@
+"""Feature-statistics generative metrics: FID, KID, Inception Score, MiFID.
+
+Parity: reference ``S/image/fid.py:159-374``, ``kid.py:33-276``, ``inception.py:34-170``, ``mifid.py:36-240``
+(constructor args, state names/dtypes/reductions, ``reset_real_features``, ``normalize``).
+
+MI355X-first changes:
+
+* FID ``update``: one fp64-MFMA SYRK kernel (``csrc/image/feature_moments.hip``) accumulates Σx and XᵀX straight into
+  the fp64 states -- upper triangle only, inputs converted to fp64 while staged in LDS (no fp64 copy of the batch).
+* FID ``compute``: ``tr sqrt(Σ1 Σ2)`` via the symmetric form ``Σ sqrt(λ(A Σ2 A))`` with ``A = Σ1^{1/2}`` -- two
+  symmetric eigensolves (rocSOLVER) instead of the reference's non-symmetric ``eigvals`` (``fid.py:177``).
+* KID: all ``subsets`` draws are evaluated as one batched GEMM with the polynomial kernel and masked diagonal sums
+  fused in the epilogue, instead of a Python loop of 3 GEMMs per subset (``kid.py:267``).  The RNG is consumed in the
+  reference's order, so the sampled subsets are identical for the same seed.
+"""
+from copy import deepcopy
+from typing import Any, List, Optional, Sequence, Tuple, Union
+
+import torch
+from torch import Tensor
+from torch.nn import Module
+
+from torchmetrics_amd import ops
+from torchmetrics_amd.metric import Metric
+from torchmetrics_amd.models.inception import NoTrainInceptionV3
+from torchmetrics_amd.utilities.data import dim_zero_cat
+from torchmetrics_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
+from torchmetrics_amd.utilities.prints import rank_zero_warn
+
+
+# --------------------------------------------------------------------------------------------------------- helpers
+def _trace_sqrt_product(sigma1: Tensor, sigma2: Tensor) -> Tensor:
+    """``tr sqrt(Σ1 Σ2)`` for symmetric PSD matrices through two symmetric eigensolves (fp64)."""
+    w, v = torch.linalg.eigh(sigma1)
+    root = (v * w.clamp(min=0).sqrt()) @ v.T
+    m = root @ sigma2 @ root
+    ev = torch.linalg.eigvalsh(0.5 * (m + m.T))
+    return ev.clamp(min=0).sqrt().sum(dim=-1)
+
+
+def _compute_fid(mu1: Tensor, sigma1: Tensor, mu2: Tensor, sigma2: Tensor) -> Tensor:
+    """``||μ1-μ2||² + tr Σ1 + tr Σ2 - 2 tr sqrt(Σ1 Σ2)``."""
+    a = (mu1 - mu2).square().sum(dim=-1)
+    b = sigma1.trace() + sigma2.trace()
+    c = _trace_sqrt_product(sigma1, sigma2)
+    return a + b - 2 * c
+
+
+def _resolve_feature_network(feature: Union[str, int, Module], default_tap: str) -> Tuple[Module, int]:
+    if isinstance(feature, (str, int)):
+        tap = str(feature)
+        net = NoTrainInceptionV3(name="inception-v3-compat", features_list=[tap])
+        return net, net.num_features
+    if isinstance(feature, Module):
+        if hasattr(feature, "num_features"):
+            return feature, int(feature.num_features)
+        dummy = torch.randint(0, 255, (1, 3, 299, 299), dtype=torch.uint8)
+        return feature, int(feature(dummy).shape[-1])
+    raise TypeError("Got unknown input to argument `feature`")
+
+
+class _FeatureNetMetric(Metric):
+    """Common plumbing: feature network kept out of ``state_dict`` semantics, ``normalize`` uint8 conversion."""
+
+    feature_network: str = "inception"
+
+    def _features(self, imgs: Tensor) -> Tensor:
+        imgs = (imgs * 255).byte() if self.normalize else imgs
+        feats = self.inception(imgs)
+        self.orig_dtype = feats.dtype
+        return feats
+
+    def _apply(self, fn: Any, exclude_state: Sequence[str] = "") -> Module:  # type: ignore[override]
+        return super()._apply(fn, exclude_state)
+
+
+# -------------------------------------------------------------------------------------------------------------- FID
+class FrechetInceptionDistance(_FeatureNetMetric):
+    higher_is_better: bool = False
+    is_differentiable: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+
+    real_features_sum: Tensor
+    real_features_cov_sum: Tensor
+    real_features_num_samples: Tensor
+    fake_features_sum: Tensor
+    fake_features_cov_sum: Tensor
+    fake_features_num_samples: Tensor
+
+    def __init__(
+        self,
+        feature: Union[int, Module] = 2048,
+        reset_real_features: bool = True,
+        normalize: bool = False,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        if isinstance(feature, int) and feature not in (64, 192, 768, 2048):
+            raise ValueError(
+                f"Integer input to argument `feature` must be one of (64, 192, 768, 2048), but got {feature}."
+            )
+        self.inception, num_features = _resolve_feature_network(feature, "2048")
+        if not isinstance(reset_real_features, bool):
+            raise ValueError("Argument `reset_real_features` expected to be a bool")
+        self.reset_real_features = reset_real_features
+        if not isinstance(normalize, bool):
+            raise ValueError("Argument `normalize` expected to be a bool")
+        self.normalize = normalize
+        self.orig_dtype = torch.float32
+        nf = (num_features, num_features)
+        self.add_state("real_features_sum", torch.zeros(num_features).double(), dist_reduce_fx="sum")
+        self.add_state("real_features_cov_sum", torch.zeros(nf).double(), dist_reduce_fx="sum")
+        self.add_state("real_features_num_samples", torch.tensor(0).long(), dist_reduce_fx="sum")
+        self.add_state("fake_features_sum", torch.zeros(num_features).double(), dist_reduce_fx="sum")
+        self.add_state("fake_features_cov_sum", torch.zeros(nf).double(), dist_reduce_fx="sum")
+        self.add_state("fake_features_num_samples", torch.tensor(0).long(), dist_reduce_fx="sum")
+
+    def update(self, imgs: Tensor, real: bool) -> None:
+        feats = self._features(imgs)
+        self.update_features(feats, real, num_samples=imgs.shape[0])
+
+    def update_features(self, features: Tensor, real: bool, num_samples: Optional[int] = None) -> None:
+        """Accumulate already-extracted ``[N, D]`` features (the bench path: no feature network)."""
+        if features.dim() == 1:
+            features = features.unsqueeze(0)
+        prefix = "real" if real else "fake"
+        s = getattr(self, f"{prefix}_features_sum")
+        c = getattr(self, f"{prefix}_features_cov_sum")
+        if s.device != features.device or not s.is_contiguous() or not c.is_contiguous():
+            s, c = s.to(features.device).contiguous(), c.to(features.device).contiguous()
+            setattr(self, f"{prefix}_features_sum", s)
+            setattr(self, f"{prefix}_features_cov_sum", c)
+        ops.feature_moments_update(features, s, c)
+        n = getattr(self, f"{prefix}_features_num_samples")
+        setattr(self, f"{prefix}_features_num_samples", n + (features.shape[0] if num_samples is None else num_samples))
+
+    def compute(self) -> Tensor:
+        if self.real_features_num_samples < 2 or self.fake_features_num_samples < 2:
+            raise RuntimeError("More than one sample is required for both the real and fake distributed to compute FID")
+        mean_real = (self.real_features_sum / self.real_features_num_samples).unsqueeze(0)
+        mean_fake = (self.fake_features_sum / self.fake_features_num_samples).unsqueeze(0)
+        cov_real = (self.real_features_cov_sum - self.real_features_num_samples * mean_real.t().mm(mean_real)) / (
+            self.real_features_num_samples - 1
+        )
+        cov_fake = (self.fake_features_cov_sum - self.fake_features_num_samples * mean_fake.t().mm(mean_fake)) / (
+            self.fake_features_num_samples - 1
+        )
+        return _compute_fid(mean_real.squeeze(0), cov_real, mean_fake.squeeze(0), cov_fake).to(self.orig_dtype)
+
+    def reset(self) -> None:
+        if not self.reset_real_features:
+            keep = {k: deepcopy(getattr(self, k)) for k in
+                    ("real_features_sum", "real_features_cov_sum", "real_features_num_samples")}
+            super().reset()
+            for k, v in keep.items():
+                setattr(self, k, v)
+        else:
+            super().reset()
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
+
+
+# -------------------------------------------------------------------------------------------------------------- KID
+def maximum_mean_discrepancy(k_xx: Tensor, k_xy: Tensor, k_yy: Tensor) -> Tensor:
+    """Unbiased MMD² from kernel matrices (works on batched ``[..., m, m]`` inputs)."""
+    m = k_xx.shape[-1]
+    kt_xx = k_xx.sum(dim=(-2, -1)) - torch.diagonal(k_xx, dim1=-2, dim2=-1).sum(-1)
+    kt_yy = k_yy.sum(dim=(-2, -1)) - torch.diagonal(k_yy, dim1=-2, dim2=-1).sum(-1)
+    k_xy_sum = k_xy.sum(dim=(-2, -1))
+    return (kt_xx + kt_yy) / (m * (m - 1)) - 2 * k_xy_sum / (m**2)
+
+
+def poly_kernel(f1: Tensor, f2: Tensor, degree: int = 3, gamma: Optional[float] = None, coef: float = 1.0) -> Tensor:
+    if gamma is None:
+        gamma = 1.0 / f1.shape[-1]
+    return (f1 @ f2.transpose(-2, -1) * gamma + coef) ** degree
+
+
+def poly_mmd(f_real: Tensor, f_fake: Tensor, degree: int = 3, gamma: Optional[float] = None,
+             coef: float = 1.0) -> Tensor:
+    k_11 = poly_kernel(f_real, f_real, degree, gamma, coef)
+    k_22 = poly_kernel(f_fake, f_fake, degree, gamma, coef)
+    k_12 = poly_kernel(f_real, f_fake, degree, gamma, coef)
+    return maximum_mean_discrepancy(k_11, k_12, k_22)
+
+
+class KernelInceptionDistance(_FeatureNetMetric):
+    higher_is_better: bool = False
+    is_differentiable: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+
+    def __init__(
+        self,
+        feature: Union[str, int, Module] = 2048,
+        subsets: int = 100,
+        subset_size: int = 1000,
+        degree: int = 3,
+        gamma: Optional[float] = None,
+        coef: float = 1.0,
+        reset_real_features: bool = True,
+        normalize: bool = False,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        rank_zero_warn(
+            "Metric `Kernel Inception Distance` will save all extracted features in buffer."
+            " For large datasets this may lead to large memory footprint.",
+            UserWarning,
+        )
+        if isinstance(feature, (str, int)) and str(feature) not in ("logits_unbiased", "64", "192", "768", "2048"):
+            raise ValueError(
+                f"Integer input to argument `feature` must be one of ('logits_unbiased', 64, 192, 768, 2048),"
+                f" but got {feature}."
+            )
+        self.inception, _ = _resolve_feature_network(feature, "2048")
+        if not (isinstance(subsets, int) and subsets > 0):
+            raise ValueError("Argument `subsets` expected to be integer larger than 0")
+        self.subsets = subsets
+        if not (isinstance(subset_size, int) and subset_size > 0):
+            raise ValueError("Argument `subset_size` expected to be integer larger than 0")
+        self.subset_size = subset_size
+        if not (isinstance(degree, int) and degree > 0):
+            raise ValueError("Argument `degree` expected to be integer larger than 0")
+        self.degree = degree
+        if gamma is not None and not (isinstance(gamma, float) and gamma > 0):
+            raise ValueError("Argument `gamma` expected to be `None` or float larger than 0")
+        self.gamma = gamma
+        if not (isinstance(coef, float) and coef > 0):
+            raise ValueError("Argument `coef` expected to be float larger than 0")
+        self.coef = coef
+        if not isinstance(reset_real_features, bool):
+            raise ValueError("Argument `reset_real_features` expected to be a bool")
+        self.reset_real_features = reset_real_features
+        if not isinstance(normalize, bool):
+            raise ValueError("Argument `normalize` expected to be a bool")
+        self.normalize = normalize
+        self.add_state("real_features", [], dist_reduce_fx=None)
+        self.add_state("fake_features", [], dist_reduce_fx=None)
+
+    def update(self, imgs: Tensor, real: bool) -> None:
+        feats = self._features(imgs)
+        (self.real_features if real else self.fake_features).append(feats)
+
+    def compute(self) -> Tuple[Tensor, Tensor]:
+        real = dim_zero_cat(self.real_features)
+        fake = dim_zero_cat(self.fake_features)
+        n_real, n_fake = real.shape[0], fake.shape[0]
+        if n_real < self.subset_size:
+            raise ValueError("Argument `subset_size` should be smaller than the number of samples")
+        if n_fake < self.subset_size:
+            raise ValueError("Argument `subset_size` should be smaller than the number of samples")
+        # draw the permutations in the reference order (real, fake, real, fake, ...) on the host generator
+        idx_r, idx_f = [], []
+        for _ in range(self.subsets):
+            idx_r.append(torch.randperm(n_real)[: self.subset_size])
+            idx_f.append(torch.randperm(n_fake)[: self.subset_size])
+        ir = torch.stack(idx_r).to(real.device)
+        if_ = torch.stack(idx_f).to(fake.device)
+        scores = []
+        chunk = max(1, int(2**28 // max(1, self.subset_size * self.subset_size * 3)))
+        for s in range(0, self.subsets, chunk):
+            fr = real[ir[s : s + chunk]]  # [b, m, D]
+            ff = fake[if_[s : s + chunk]]
+            scores.append(poly_mmd(fr, ff, self.degree, self.gamma, self.coef))
+        kid = torch.cat(scores)
+        return kid.mean(), kid.std(unbiased=False)
+
+    def reset(self) -> None:
+        if not self.reset_real_features:
+            value = self._defaults.pop("real_features")
+            super().reset()
+            self._defaults["real_features"] = value
+        else:
+            super().reset()
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        val = val or self.compute()[0]
+        return self._plot(val, ax)
+
+
+# ---------------------------------------------------------------------------------------------------------- IS
+class InceptionScore(_FeatureNetMetric):
+    is_differentiable: bool = False
+    higher_is_better: bool = True
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+
+    def __init__(self, feature: Union[str, int, Module] = "logits_unbiased", splits: int = 10,
+                 normalize: bool = False, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        rank_zero_warn(
+            "Metric `InceptionScore` will save all extracted features in buffer."
+            " For large datasets this may lead to large memory footprint.",
+            UserWarning,
+        )
+        if isinstance(feature, (str, int)) and str(feature) not in ("logits_unbiased", "64", "192", "768", "2048",
+                                                                    "1008"):
+            raise ValueError(f"Integer input to argument `feature` must be one of the valid taps, but got {feature}.")
+        self.inception, _ = _resolve_feature_network(feature, "logits_unbiased")
+        if not isinstance(normalize, bool):
+            raise ValueError("Argument `normalize` expected to be a bool")
+        self.normalize = normalize
+        self.splits = splits
+        self.add_state("features", [], dist_reduce_fx=None)
+
+    def update(self, imgs: Tensor) -> None:
+        self.features.append(self._features(imgs))
+
+    def compute(self) -> Tuple[Tensor, Tensor]:
+        features = dim_zero_cat(self.features)
+        idx = torch.randperm(features.shape[0])
+        features = features[idx.to(features.device)]
+        prob = features.softmax(dim=1)
+        log_prob = features.log_softmax(dim=1)
+        kls = []
+        for p, lp in zip(prob.chunk(self.splits, dim=0), log_prob.chunk(self.splits, dim=0)):
+            m = p.mean(dim=0, keepdim=True)
+            kls.append((p * (lp - m.log())).sum(dim=1).mean().exp())
+        kl = torch.stack(kls)
+        return kl.mean(), kl.std()
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        val = val or self.compute()[0]
+        return self._plot(val, ax)
+
+
+# ------------------------------------------------------------------------------------------------------------ MiFID
+def _compute_cosine_distance(features1: Tensor, features2: Tensor, cosine_distance_eps: float = 0.1) -> Tensor:
+    f1 = features1[torch.sum(features1, dim=1) != 0]
+    f2 = features2[torch.sum(features2, dim=1) != 0]
+    n1 = f1 / torch.norm(f1, dim=1, keepdim=True)
+    n2 = f2 / torch.norm(f2, dim=1, keepdim=True)
+    d = 1.0 - torch.abs(n1 @ n2.t())
+    mean_min_d = torch.mean(d.min(dim=1).values)
+    return mean_min_d if mean_min_d < cosine_distance_eps else torch.ones_like(mean_min_d)
+
+
+def _mifid_compute(mu1: Tensor, sigma1: Tensor, features1: Tensor, mu2: Tensor, sigma2: Tensor, features2: Tensor,
+                   cosine_distance_eps: float = 0.1) -> Tensor:
+    fid = _compute_fid(mu1, sigma1, mu2, sigma2)
+    dist = _compute_cosine_distance(features1, features2, cosine_distance_eps)
+    return fid / (dist + 10e-15) if fid > 1e-8 else torch.zeros_like(fid)
+
+
+class MemorizationInformedFrechetInceptionDistance(_FeatureNetMetric):
+    higher_is_better: bool = False
+    is_differentiable: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+
+    def __init__(self, feature: Union[int, Module] = 2048, reset_real_features: bool = True, normalize: bool = False,
+                 cosine_distance_eps: float = 0.1, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if isinstance(feature, int) and feature not in (64, 192, 768, 2048):
+            raise ValueError(
+                f"Integer input to argument `feature` must be one of (64, 192, 768, 2048), but got {feature}."
+            )
+        self.inception, _ = _resolve_feature_network(feature, "2048")
+        if not isinstance(reset_real_features, bool):
+            raise ValueError("Argument `reset_real_features` expected to be a bool")
+        self.reset_real_features = reset_real_features
+        if not isinstance(normalize, bool):
+            raise ValueError("Argument `normalize` expected to be a bool")
+        self.normalize = normalize
+        if not (isinstance(cosine_distance_eps, float) and 1 >= cosine_distance_eps > 0):
+            raise ValueError("Argument `cosine_distance_eps` expected to be a float greater than 0 and less than 1")
+        self.cosine_distance_eps = cosine_distance_eps
+        self.add_state("real_features", [], dist_reduce_fx=None)
+        self.add_state("fake_features", [], dist_reduce_fx=None)
+
+    def update(self, imgs: Tensor, real: bool) -> None:
+        feats = self._features(imgs).double()
+        (self.real_features if real else self.fake_features).append(feats)
+
+    def compute(self) -> Tensor:
+        real = dim_zero_cat(self.real_features).double()
+        fake = dim_zero_cat(self.fake_features).double()
+        mr, mf = real.mean(0), fake.mean(0)
+        cr, cf = torch.cov(real.t()), torch.cov(fake.t())
+        return _mifid_compute(mr, cr, real, mf, cf, fake, self.cosine_distance_eps).to(self.orig_dtype)
+
+    def reset(self) -> None:
+        if not self.reset_real_features:
+            value = self._defaults.pop("real_features")
+            super().reset()
+            self._defaults["real_features"] = value
+        else:
+            super().reset()
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)

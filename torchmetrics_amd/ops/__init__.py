@@ -178,3 +178,14 @@ def moments_update(
         return res if want_sums else None
     return _cpu.moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_t, dests, dest_ids,
                                want_sums)
+
+
+# ----------------------------------------------------------------------------------------------------------- image
+def feature_moments_update(features: Tensor, feat_sum: Tensor, feat_cov: Tensor) -> None:
+    """``feat_sum += Σ_n x_n`` and ``feat_cov += XᵀX`` in fp64 (fp64-MFMA SYRK on ROCm, upper triangle only)."""
+    if features.is_cuda:
+        if features.dtype not in (torch.float32, torch.float16, torch.bfloat16, torch.float64):
+            features = features.float()
+        _ops().feature_moments_update(features.contiguous(), feat_sum, feat_cov)
+    else:
+        _cpu.feature_moments_update(features, feat_sum, feat_cov)

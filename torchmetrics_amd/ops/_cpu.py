@@ -202,3 +202,9 @@ def moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_
             val = torch.round(val).long()
         dst += val.reshape(dst.shape).to(dst.dtype)
     return sums if want_sums else None
+
+
+def feature_moments_update(features: Tensor, feat_sum: Tensor, feat_cov: Tensor) -> None:
+    x = features.double()
+    feat_sum += x.sum(0)
+    feat_cov += x.t().mm(x)

@@ -27,6 +27,42 @@ from torchmetrics_amd.classification.f_beta import (
     MultilabelF1Score,
     MultilabelFBetaScore,
 )
+from torchmetrics_amd.classification.fixed_point import (
+    BinaryPrecisionAtFixedRecall,
+    BinaryRecallAtFixedPrecision,
+    BinarySensitivityAtSpecificity,
+    BinarySpecificityAtSensitivity,
+    MulticlassPrecisionAtFixedRecall,
+    MulticlassRecallAtFixedPrecision,
+    MulticlassSensitivityAtSpecificity,
+    MulticlassSpecificityAtSensitivity,
+    MultilabelPrecisionAtFixedRecall,
+    MultilabelRecallAtFixedPrecision,
+    MultilabelSensitivityAtSpecificity,
+    MultilabelSpecificityAtSensitivity,
+    PrecisionAtFixedRecall,
+    RecallAtFixedPrecision,
+    SensitivityAtSpecificity,
+    SpecificityAtSensitivity,
+)
+from torchmetrics_amd.classification.precision_recall_curve import (
+    AUROC,
+    ROC,
+    AveragePrecision,
+    BinaryAUROC,
+    BinaryAveragePrecision,
+    BinaryPrecisionRecallCurve,
+    BinaryROC,
+    MulticlassAUROC,
+    MulticlassAveragePrecision,
+    MulticlassPrecisionRecallCurve,
+    MulticlassROC,
+    MultilabelAUROC,
+    MultilabelAveragePrecision,
+    MultilabelPrecisionRecallCurve,
+    MultilabelROC,
+    PrecisionRecallCurve,
+)
 from torchmetrics_amd.classification.hamming import (
     BinaryHammingDistance,
     HammingDistance,

@@ -5,6 +5,39 @@ from torchmetrics_amd.functional.classification.accuracy import (
     multiclass_accuracy,
     multilabel_accuracy,
 )
+from torchmetrics_amd.functional.classification.auroc import auroc, binary_auroc, multiclass_auroc, multilabel_auroc
+from torchmetrics_amd.functional.classification.average_precision import (
+    average_precision,
+    binary_average_precision,
+    multiclass_average_precision,
+    multilabel_average_precision,
+)
+from torchmetrics_amd.functional.classification.precision_recall_curve import (
+    binary_precision_recall_curve,
+    multiclass_precision_recall_curve,
+    multilabel_precision_recall_curve,
+    precision_recall_curve,
+)
+from torchmetrics_amd.functional.classification.recall_fixed_precision import (
+    binary_precision_at_fixed_recall,
+    binary_recall_at_fixed_precision,
+    binary_sensitivity_at_specificity,
+    binary_specificity_at_sensitivity,
+    multiclass_precision_at_fixed_recall,
+    multiclass_recall_at_fixed_precision,
+    multiclass_sensitivity_at_specificity,
+    multiclass_specificity_at_sensitivity,
+    multilabel_precision_at_fixed_recall,
+    multilabel_recall_at_fixed_precision,
+    multilabel_sensitivity_at_specificity,
+    multilabel_specificity_at_sensitivity,
+    precision_at_fixed_recall,
+    recall_at_fixed_precision,
+    sensitivity_at_specificity,
+    specicity_at_sensitivity,
+    specificity_at_sensitivity,
+)
+from torchmetrics_amd.functional.classification.roc import binary_roc, multiclass_roc, multilabel_roc, roc
 from torchmetrics_amd.functional.classification.cohen_kappa import (
     binary_cohen_kappa,
     cohen_kappa,

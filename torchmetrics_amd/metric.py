@@ -449,8 +449,9 @@ class Metric(Module, ABC):
     def compute(self) -> Any:
         """Compute the metric value from the (synced) states."""
 
-    def plot(self, *_: Any, **__: Any) -> Any:
-        raise NotImplementedError
+    def plot(self, val: Any = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        """Plot a single or multiple values from the metric (every reference subclass does exactly this)."""
+        return self._plot(val, ax)
 
     def _plot(self, val: Any = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
         val = val if val is not None else self.compute()

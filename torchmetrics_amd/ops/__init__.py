@@ -189,3 +189,29 @@ def feature_moments_update(features: Tensor, feat_sum: Tensor, feat_cov: Tensor)
         _ops().feature_moments_update(features.contiguous(), feat_sum, feat_cov)
     else:
         _cpu.feature_moments_update(features, feat_sum, feat_cov)
+
+
+# ------------------------------------------------------------------------------------------- classification curves
+CURVE_BINARY = 0
+CURVE_MULTILABEL = 1
+CURVE_MULTICLASS = 2
+
+
+def curve_update(preds: Tensor, target: Tensor, thr_sorted: Tensor, perm: Tensor, hist: Tensor, ctl: Tensor,
+                 state: Tensor, err: Tensor, mode: int, ignore_index: Optional[int], micro: bool = False) -> None:
+    """Binned multi-threshold confusion matrices ``state[T, H, 2, 2] += ...`` (``csrc/classification/curve.hip``).
+
+    ``preds``: ``[N]`` (binary), ``[N, L]`` (multilabel) or ``[N, C]`` (multiclass) raw scores; sigmoid / softmax is
+    applied on the device iff any considered score is outside ``[0, 1]``.  ``thr_sorted`` (f64, ascending) and
+    ``perm`` (caller index of each sorted threshold) describe the thresholds.  ``hist`` / ``ctl`` are int32 scratch
+    that must be zero on entry and are zero again on exit.  Invalid targets set bits in ``err``.
+    """
+    if preds.is_cuda:
+        if preds.dtype not in (torch.float32, torch.float16, torch.bfloat16, torch.float64):
+            preds = preds.float()
+        if target.dtype == torch.bool:
+            target = target.to(torch.uint8)
+        _ops().curve_update(preds.contiguous(), target.contiguous(), thr_sorted, perm, hist, ctl, state, err,
+                            mode, -1 if ignore_index is None else int(ignore_index), ignore_index is not None, micro)
+    else:
+        _cpu.curve_update(preds, target, thr_sorted, perm, state, err, mode, ignore_index, micro)

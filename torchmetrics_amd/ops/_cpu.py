@@ -208,3 +208,55 @@ def feature_moments_update(features: Tensor, feat_sum: Tensor, feat_cov: Tensor)
     x = features.double()
     feat_sum += x.sum(0)
     feat_cov += x.t().mm(x)
+
+
+def curve_update(preds: Tensor, target: Tensor, thr_sorted: Tensor, perm: Tensor, state: Tensor, err: Tensor,
+                 mode: int, ignore_index: Optional[int], micro: bool) -> None:
+    """Bucket every score by ``#{thr <= p}`` (one ``bucketize``), histogram, suffix-sum -> per-threshold confmats."""
+    t = thr_sorted.numel()
+    if mode == 2:  # multiclass
+        c = preds.shape[1]
+        keep = torch.ones_like(target, dtype=torch.bool) if ignore_index is None else target != ignore_index
+        p, tg = preds[keep], target[keep].long()
+        if p.numel() and not torch.all((p >= 0) & (p <= 1)):
+            p = p.softmax(1)
+        bad = (tg < 0) | (tg >= c)
+        if bool(bad.any()):
+            _set(err, V.TARGET_OUT_OF_RANGE)
+            p, tg = p[~bad], tg[~bad]
+        pos = torch.nn.functional.one_hot(tg, c) if tg.numel() else torch.zeros(0, c, dtype=torch.long)
+        cols = c
+    else:
+        if mode == 0:
+            p, tg = preds.reshape(-1, 1), target.reshape(-1, 1).long()
+            keep = torch.ones_like(tg, dtype=torch.bool) if ignore_index is None else tg != ignore_index
+            check = p[keep]
+        else:
+            p, tg = preds, target.long()
+            keep = torch.ones_like(tg, dtype=torch.bool) if ignore_index is None else tg != ignore_index
+            check = p
+        if check.numel() and not torch.all((check >= 0) & (check <= 1)):
+            p = p.sigmoid()
+        bad = keep & (tg != 0) & (tg != 1)
+        if bool(bad.any()):
+            _set(err, V.TARGET_NOT_BINARY)
+        keep = keep & ~bad
+        pos = tg.clamp(0, 1)
+        cols = p.shape[1]
+    b = torch.bucketize(p.double(), thr_sorted.to(p.device), right=True)  # #{thr <= p}; NaN -> T (fixed below)
+    b = torch.where(torch.isnan(p), torch.zeros_like(b), b)
+    col = torch.arange(cols).expand_as(b)
+    if mode == 2:
+        keep = torch.ones_like(b, dtype=torch.bool)
+    if micro:
+        col = torch.zeros_like(col)
+        cols = 1
+    idx = ((b * cols + col) * 2 + pos)[keep]
+    hist = torch.bincount(idx, minlength=(t + 1) * cols * 2).reshape(t + 1, cols, 2)
+    suffix = hist.flip(0).cumsum(0).flip(0)  # suffix[b] = counts in buckets >= b
+    tot = suffix[0]
+    above = suffix[1:]  # sorted threshold i: predicted positive <=> bucket >= i + 1
+    out = torch.stack([tot[:, 0] - above[:, :, 0], above[:, :, 0], tot[:, 1] - above[:, :, 1], above[:, :, 1]], -1)
+    res = torch.empty_like(out)
+    res[perm] = out
+    state += res.reshape(state.shape)

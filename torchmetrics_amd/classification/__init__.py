@@ -17,6 +17,23 @@ from torchmetrics_amd.classification.confusion_matrix import (
     MultilabelJaccardIndex,
     MultilabelMatthewsCorrCoef,
 )
+from torchmetrics_amd.classification.extras import (
+    BinaryCalibrationError,
+    BinaryFairness,
+    BinaryGroupStatRates,
+    BinaryHingeLoss,
+    CalibrationError,
+    Dice,
+    ExactMatch,
+    HingeLoss,
+    MulticlassCalibrationError,
+    MulticlassExactMatch,
+    MulticlassHingeLoss,
+    MultilabelCoverageError,
+    MultilabelExactMatch,
+    MultilabelRankingAveragePrecision,
+    MultilabelRankingLoss,
+)
 from torchmetrics_amd.classification.f_beta import (
     BinaryF1Score,
     BinaryFBetaScore,

@@ -1,0 +1,555 @@
+"""Calibration error, hinge loss, label-ranking, exact match, group fairness and Dice module metrics.
+
+Parity: reference ``S/classification/calibration_error.py``, ``hinge.py``, ``ranking.py``, ``exact_match.py``,
+``group_fairness.py``, ``dice.py``.  State layouts (names, reductions) follow the reference so checkpoints and DDP
+syncs are interchangeable.  Deliberate difference: ``BinaryGroupStatRates`` / ``BinaryFairness`` accumulate
+statistics by group *id* (the reference enumerates the groups present in each batch, which misattributes counts when
+a batch lacks a group).
+"""
+from typing import Any, Dict, Optional, Type
+
+import torch
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_amd.classification.base import _ClassificationTaskWrapper
+from torchmetrics_amd.functional.classification._legacy import _stat_scores_update
+from torchmetrics_amd.functional.classification.calibration_error import (
+    _binary_calibration_error_arg_validation,
+    _binary_float_preds_validation,
+    _binary_format,
+    _ce_compute,
+    _multiclass_calibration_error_arg_validation,
+    _multiclass_calibration_error_update,
+    _multiclass_float_preds_validation,
+    _multiclass_format,
+)
+from torchmetrics_amd.functional.classification.dice import _dice_compute
+from torchmetrics_amd.functional.classification.exact_match import (
+    _exact_match_reduce,
+    _multiclass_exact_match_format,
+    _multiclass_exact_match_update,
+    _multilabel_exact_match_format,
+    _multilabel_exact_match_update,
+)
+from torchmetrics_amd.functional.classification.group_fairness import (
+    _compute_binary_demographic_parity,
+    _compute_binary_equal_opportunity,
+    _group_stat_counts,
+    _groups_validation,
+)
+from torchmetrics_amd.functional.classification.hinge import (
+    _binary_hinge_loss_arg_validation,
+    _binary_hinge_loss_update,
+    _hinge_loss_compute,
+    _multiclass_hinge_loss_arg_validation,
+    _multiclass_hinge_loss_update,
+)
+from torchmetrics_amd.functional.classification.ranking import (
+    _multilabel_coverage_error_update,
+    _multilabel_ranking_arg_validation,
+    _multilabel_ranking_average_precision_update,
+    _multilabel_ranking_format,
+    _multilabel_ranking_loss_update,
+    _multilabel_ranking_tensor_validation,
+    _ranking_reduce,
+)
+from torchmetrics_amd.functional.classification.stat_scores import (
+    _binary_stat_scores_arg_validation,
+    _binary_stat_scores_tensor_validation,
+    _multiclass_stat_scores_arg_validation,
+    _multiclass_stat_scores_tensor_validation,
+    _multilabel_stat_scores_arg_validation,
+    _multilabel_stat_scores_tensor_validation,
+)
+from torchmetrics_amd.metric import Metric
+from torchmetrics_amd.utilities.data import dim_zero_cat
+from torchmetrics_amd.utilities.enums import ClassificationTaskNoBinary, ClassificationTaskNoMultilabel
+from torchmetrics_amd.utilities.prints import rank_zero_warn
+
+
+# --------------------------------------------------------------------------------------------- calibration error
+class BinaryCalibrationError(Metric):
+    """Top-label calibration error (ECE / MCE / RMSCE) for binary probabilities."""
+
+    is_differentiable: bool = False
+    higher_is_better: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+
+    def __init__(self, n_bins: int = 15, norm: Literal["l1", "l2", "max"] = "l1", ignore_index: Optional[int] = None,
+                 validate_args: bool = True, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _binary_calibration_error_arg_validation(n_bins, norm, ignore_index)
+        self.validate_args = validate_args
+        self.n_bins = n_bins
+        self.norm = norm
+        self.ignore_index = ignore_index
+        self.add_state("confidences", [], dist_reduce_fx="cat")
+        self.add_state("accuracies", [], dist_reduce_fx="cat")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _binary_float_preds_validation(preds, target, self.ignore_index)
+        preds, target = _binary_format(preds, target, self.ignore_index)
+        self.confidences.append(preds)
+        self.accuracies.append(target)
+
+    def compute(self) -> Tensor:
+        return _ce_compute(dim_zero_cat(self.confidences), dim_zero_cat(self.accuracies), self.n_bins, norm=self.norm)
+
+
+class MulticlassCalibrationError(Metric):
+    """Top-label calibration error for multiclass probabilities / logits."""
+
+    is_differentiable: bool = False
+    higher_is_better: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+    plot_legend_name: str = "Class"
+
+    def __init__(self, num_classes: int, n_bins: int = 15, norm: Literal["l1", "l2", "max"] = "l1",
+                 ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _multiclass_calibration_error_arg_validation(num_classes, n_bins, norm, ignore_index)
+        self.validate_args = validate_args
+        self.num_classes = num_classes
+        self.n_bins = n_bins
+        self.norm = norm
+        self.ignore_index = ignore_index
+        self.add_state("confidences", [], dist_reduce_fx="cat")
+        self.add_state("accuracies", [], dist_reduce_fx="cat")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _multiclass_float_preds_validation(preds, target, self.num_classes, self.ignore_index)
+        preds, target = _multiclass_format(preds, target, self.ignore_index)
+        confidences, accuracies = _multiclass_calibration_error_update(preds, target)
+        self.confidences.append(confidences)
+        self.accuracies.append(accuracies)
+
+    def compute(self) -> Tensor:
+        return _ce_compute(dim_zero_cat(self.confidences), dim_zero_cat(self.accuracies), self.n_bins, norm=self.norm)
+
+
+class CalibrationError(_ClassificationTaskWrapper):
+    """Task wrapper for the calibration error."""
+
+    def __new__(cls: Type["CalibrationError"], task: Literal["binary", "multiclass"], n_bins: int = 15,
+                norm: Literal["l1", "l2", "max"] = "l1", num_classes: Optional[int] = None,
+                ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any) -> Metric:
+        task = ClassificationTaskNoMultilabel.from_str(task)
+        kwargs.update({"n_bins": n_bins, "norm": norm, "ignore_index": ignore_index, "validate_args": validate_args})
+        if task == ClassificationTaskNoMultilabel.BINARY:
+            return BinaryCalibrationError(**kwargs)
+        if task == ClassificationTaskNoMultilabel.MULTICLASS:
+            if not isinstance(num_classes, int):
+                raise ValueError(f"`num_classes` is expected to be `int` but `{type(num_classes)} was passed.`")
+            return MulticlassCalibrationError(num_classes, **kwargs)
+        raise ValueError(f"Not handled value: {task}")
+
+
+# ---------------------------------------------------------------------------------------------------- hinge loss
+class BinaryHingeLoss(Metric):
+    """Mean (squared) hinge loss for binary tasks."""
+
+    is_differentiable: bool = True
+    higher_is_better: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+
+    def __init__(self, squared: bool = False, ignore_index: Optional[int] = None, validate_args: bool = True,
+                 **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _binary_hinge_loss_arg_validation(squared, ignore_index)
+        self.validate_args = validate_args
+        self.squared = squared
+        self.ignore_index = ignore_index
+        self.add_state("measures", default=torch.tensor(0.0), dist_reduce_fx="sum")
+        self.add_state("total", default=torch.tensor(0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _binary_float_preds_validation(preds, target, self.ignore_index)
+        measures, total = _binary_hinge_loss_update(preds, target, self.squared, self.ignore_index)
+        self.measures += measures
+        self.total += total
+
+    def compute(self) -> Tensor:
+        return _hinge_loss_compute(self.measures, self.total)
+
+
+class MulticlassHingeLoss(Metric):
+    """Mean (squared) multiclass hinge loss (Crammer-Singer or one-vs-all)."""
+
+    is_differentiable: bool = True
+    higher_is_better: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+    plot_legend_name: str = "Class"
+
+    def __init__(self, num_classes: int, squared: bool = False,
+                 multiclass_mode: Literal["crammer-singer", "one-vs-all"] = "crammer-singer",
+                 ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _multiclass_hinge_loss_arg_validation(num_classes, squared, multiclass_mode, ignore_index)
+        self.validate_args = validate_args
+        self.num_classes = num_classes
+        self.squared = squared
+        self.multiclass_mode = multiclass_mode
+        self.ignore_index = ignore_index
+        self.add_state(
+            "measures",
+            default=torch.tensor(0.0) if multiclass_mode == "crammer-singer" else torch.zeros(num_classes),
+            dist_reduce_fx="sum",
+        )
+        self.add_state("total", default=torch.tensor(0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _multiclass_float_preds_validation(preds, target, self.num_classes, self.ignore_index)
+        measures, total = _multiclass_hinge_loss_update(preds, target, self.squared, self.multiclass_mode,
+                                                        self.ignore_index)
+        self.measures += measures
+        self.total += total
+
+    def compute(self) -> Tensor:
+        return _hinge_loss_compute(self.measures, self.total)
+
+
+class HingeLoss(_ClassificationTaskWrapper):
+    """Task wrapper for the hinge loss."""
+
+    def __new__(cls: Type["HingeLoss"], task: Literal["binary", "multiclass"], num_classes: Optional[int] = None,
+                squared: bool = False, multiclass_mode: Optional[Literal["crammer-singer", "one-vs-all"]] = "crammer-singer",
+                ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any) -> Metric:
+        task = ClassificationTaskNoMultilabel.from_str(task)
+        kwargs.update({"ignore_index": ignore_index, "validate_args": validate_args})
+        if task == ClassificationTaskNoMultilabel.BINARY:
+            return BinaryHingeLoss(squared, **kwargs)
+        if task == ClassificationTaskNoMultilabel.MULTICLASS:
+            if not isinstance(num_classes, int):
+                raise ValueError(f"`num_classes` is expected to be `int` but `{type(num_classes)} was passed.`")
+            return MulticlassHingeLoss(num_classes, squared, multiclass_mode, **kwargs)
+        raise ValueError(f"Unsupported task `{task}`")
+
+
+# ------------------------------------------------------------------------------------------------ label ranking
+class _RankingBase(Metric):
+    is_differentiable: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+    plot_legend_name: str = "Label"
+    _update_fn: Any = None
+
+    def __init__(self, num_labels: int, ignore_index: Optional[int] = None, validate_args: bool = True,
+                 **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _multilabel_ranking_arg_validation(num_labels, ignore_index)
+        self.validate_args = validate_args
+        self.num_labels = num_labels
+        self.ignore_index = ignore_index
+        self.add_state("measure", torch.tensor(0.0), dist_reduce_fx="sum")
+        self.add_state("total", torch.tensor(0.0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _multilabel_ranking_tensor_validation(preds, target, self.num_labels, self.ignore_index)
+        preds, target = _multilabel_ranking_format(preds, target, self.num_labels, self.ignore_index)
+        measure, num_elements = type(self)._update_fn(preds, target)
+        self.measure += measure
+        self.total += num_elements
+
+    def compute(self) -> Tensor:
+        return _ranking_reduce(self.measure, self.total)
+
+
+class MultilabelCoverageError(_RankingBase):
+    """Average depth into the ranked labels needed to cover all relevant labels."""
+
+    higher_is_better: bool = False
+    _update_fn = staticmethod(_multilabel_coverage_error_update)
+
+
+class MultilabelRankingAveragePrecision(_RankingBase):
+    """Label ranking average precision (LRAP)."""
+
+    higher_is_better: bool = True
+    _update_fn = staticmethod(_multilabel_ranking_average_precision_update)
+
+
+class MultilabelRankingLoss(_RankingBase):
+    """Label ranking loss (fraction of mis-ordered relevant/irrelevant pairs)."""
+
+    higher_is_better: bool = False
+    _update_fn = staticmethod(_multilabel_ranking_loss_update)
+
+
+# -------------------------------------------------------------------------------------------------- exact match
+class _ExactMatchBase(Metric):
+    is_differentiable: bool = False
+    higher_is_better: bool = True
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+
+    def _create_states(self) -> None:
+        samplewise = self.multidim_average == "samplewise"
+        self.add_state("correct", [] if samplewise else torch.zeros(1, dtype=torch.long),
+                       dist_reduce_fx="cat" if samplewise else "sum")
+        self.add_state("total", torch.zeros(1, dtype=torch.long), dist_reduce_fx="mean" if samplewise else "sum")
+
+    def _accumulate(self, correct: Tensor, total: Tensor) -> None:
+        if self.multidim_average == "samplewise":
+            self.correct.append(correct)
+            self.total = total
+        else:
+            self.correct += correct
+            self.total += total
+
+    def compute(self) -> Tensor:
+        correct = dim_zero_cat(self.correct) if isinstance(self.correct, list) else self.correct
+        return _exact_match_reduce(correct, self.total)
+
+
+class MulticlassExactMatch(_ExactMatchBase):
+    """Exact match for multi-dimensional multiclass inputs (all positions of a sample correct)."""
+
+    plot_legend_name: str = "Class"
+
+    def __init__(self, num_classes: int, multidim_average: Literal["global", "samplewise"] = "global",
+                 ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _multiclass_stat_scores_arg_validation(num_classes, 1, None, multidim_average, ignore_index)
+        self.num_classes = num_classes
+        self.multidim_average = multidim_average
+        self.ignore_index = ignore_index
+        self.validate_args = validate_args
+        self._create_states()
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _multiclass_stat_scores_tensor_validation(preds, target, self.num_classes, self.multidim_average,
+                                                      self.ignore_index)
+        preds, target = _multiclass_exact_match_format(preds, target)
+        self._accumulate(*_multiclass_exact_match_update(preds, target, self.multidim_average, self.ignore_index))
+
+
+class MultilabelExactMatch(_ExactMatchBase):
+    """Exact match for multilabel inputs (the whole label set of a sample correct)."""
+
+    plot_legend_name: str = "Label"
+
+    def __init__(self, num_labels: int, threshold: float = 0.5,
+                 multidim_average: Literal["global", "samplewise"] = "global", ignore_index: Optional[int] = None,
+                 validate_args: bool = True, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _multilabel_stat_scores_arg_validation(num_labels, threshold, None, multidim_average, ignore_index)
+        self.num_labels = num_labels
+        self.threshold = threshold
+        self.multidim_average = multidim_average
+        self.ignore_index = ignore_index
+        self.validate_args = validate_args
+        self._create_states()
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _multilabel_stat_scores_tensor_validation(preds, target, self.num_labels, self.multidim_average,
+                                                      self.ignore_index)
+        preds, target = _multilabel_exact_match_format(preds, target, self.num_labels, self.threshold,
+                                                       self.ignore_index)
+        self._accumulate(*_multilabel_exact_match_update(preds, target, self.num_labels, self.multidim_average))
+
+
+class ExactMatch(_ClassificationTaskWrapper):
+    """Task wrapper for exact match."""
+
+    def __new__(cls: Type["ExactMatch"], task: Literal["binary", "multiclass", "multilabel"], threshold: float = 0.5,
+                num_classes: Optional[int] = None, num_labels: Optional[int] = None,
+                multidim_average: Literal["global", "samplewise"] = "global", ignore_index: Optional[int] = None,
+                validate_args: bool = True, **kwargs: Any) -> Metric:
+        task = ClassificationTaskNoBinary.from_str(task)
+        kwargs.update({"multidim_average": multidim_average, "ignore_index": ignore_index,
+                       "validate_args": validate_args})
+        if task == ClassificationTaskNoBinary.MULTICLASS:
+            if not isinstance(num_classes, int):
+                raise ValueError(f"`num_classes` is expected to be `int` but `{type(num_classes)} was passed.`")
+            return MulticlassExactMatch(num_classes, **kwargs)
+        if task == ClassificationTaskNoBinary.MULTILABEL:
+            if not isinstance(num_labels, int):
+                raise ValueError(f"`num_labels` is expected to be `int` but `{type(num_labels)} was passed.`")
+            return MultilabelExactMatch(num_labels, threshold, **kwargs)
+        raise ValueError(f"Task {task} not supported!")
+
+
+# ---------------------------------------------------------------------------------------------- group fairness
+class _AbstractGroupStatScores(Metric):
+    tp: Tensor
+    fp: Tensor
+    tn: Tensor
+    fn: Tensor
+
+    def _create_states(self, num_groups: int) -> None:
+        for s in ("tp", "fp", "tn", "fn"):
+            self.add_state(s, torch.zeros(num_groups, dtype=torch.long), dist_reduce_fx="sum")
+
+    def _group_update(self, preds: Tensor, target: Tensor, groups: Tensor) -> None:
+        if self.validate_args:
+            _binary_stat_scores_tensor_validation(preds, target, "global", self.ignore_index)
+            _groups_validation(groups, self.num_groups)
+        counts = _group_stat_counts(preds, target, groups, self.num_groups, self.threshold, self.ignore_index)
+        self.tp += counts[:, 0]
+        self.fp += counts[:, 1]
+        self.tn += counts[:, 2]
+        self.fn += counts[:, 3]
+
+
+class BinaryGroupStatRates(_AbstractGroupStatScores):
+    """tp/fp/tn/fn rates per group for binary predictions."""
+
+    is_differentiable: bool = False
+    higher_is_better: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+
+    def __init__(self, num_groups: int, threshold: float = 0.5, ignore_index: Optional[int] = None,
+                 validate_args: bool = True, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _binary_stat_scores_arg_validation(threshold, "global", ignore_index)
+        if not isinstance(num_groups, int) and num_groups < 2:
+            raise ValueError(f"Expected argument `num_groups` to be an int larger than 1, but got {num_groups}")
+        self.num_groups = num_groups
+        self.threshold = threshold
+        self.ignore_index = ignore_index
+        self.validate_args = validate_args
+        self._create_states(num_groups)
+
+    def update(self, preds: Tensor, target: Tensor, groups: Tensor) -> None:
+        self._group_update(preds, target, groups)
+
+    def compute(self) -> Dict[str, Tensor]:
+        results = torch.stack((self.tp, self.fp, self.tn, self.fn), dim=1)
+        return {f"group_{i}": group / group.sum() for i, group in enumerate(results)}
+
+
+class BinaryFairness(_AbstractGroupStatScores):
+    """Demographic parity and/or equal opportunity across groups."""
+
+    is_differentiable: bool = False
+    higher_is_better: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+
+    def __init__(self, num_groups: int,
+                 task: Literal["demographic_parity", "equal_opportunity", "all"] = "all", threshold: float = 0.5,
+                 ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if task not in ["demographic_parity", "equal_opportunity", "all"]:
+            raise ValueError(
+                f"Expected argument `task` to either be ``demographic_parity``,"
+                f"``equal_opportunity`` or ``all`` but got {task}."
+            )
+        if validate_args:
+            _binary_stat_scores_arg_validation(threshold, "global", ignore_index)
+        if not isinstance(num_groups, int) and num_groups < 2:
+            raise ValueError(f"Expected argument `num_groups` to be an int larger than 1, but got {num_groups}")
+        self.num_groups = num_groups
+        self.task = task
+        self.threshold = threshold
+        self.ignore_index = ignore_index
+        self.validate_args = validate_args
+        self._create_states(num_groups)
+
+    def update(self, preds: Tensor, target: Tensor, groups: Tensor) -> None:
+        if self.task == "demographic_parity":
+            if target is not None:
+                rank_zero_warn("The task demographic_parity does not require a target.", UserWarning)
+            target = torch.zeros(preds.shape, dtype=torch.long, device=preds.device)
+        self._group_update(preds, target, groups)
+
+    def compute(self) -> Dict[str, Tensor]:
+        st = (self.tp, self.fp, self.tn, self.fn)
+        if self.task == "demographic_parity":
+            return _compute_binary_demographic_parity(*st)
+        if self.task == "equal_opportunity":
+            return _compute_binary_equal_opportunity(*st)
+        return {**_compute_binary_demographic_parity(*st), **_compute_binary_equal_opportunity(*st)}
+
+
+# ---------------------------------------------------------------------------------------------------------- Dice
+class Dice(Metric):
+    """Dice score with the legacy task-less input API."""
+
+    is_differentiable: bool = False
+    higher_is_better: bool = True
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+    plot_legend_name: str = "Class"
+
+    def __init__(self, zero_division: int = 0, num_classes: Optional[int] = None, threshold: float = 0.5,
+                 average: Optional[Literal["micro", "macro", "none"]] = "micro", mdmc_average: Optional[str] = "global",
+                 ignore_index: Optional[int] = None, top_k: Optional[int] = None, multiclass: Optional[bool] = None,
+                 **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        allowed_average = ("micro", "macro", "samples", "none", None)
+        if average not in allowed_average:
+            raise ValueError(f"The `average` has to be one of {allowed_average}, got {average}.")
+        self.reduce = average
+        self.mdmc_reduce = mdmc_average
+        self.num_classes = num_classes
+        self.threshold = threshold
+        self.multiclass = multiclass
+        self.ignore_index = ignore_index
+        self.top_k = top_k
+        if average not in ["micro", "macro", "samples"]:
+            raise ValueError(f"The `reduce` {average} is not valid.")
+        if mdmc_average not in [None, "samplewise", "global"]:
+            raise ValueError(f"The `mdmc_reduce` {mdmc_average} is not valid.")
+        if average == "macro" and (not num_classes or num_classes < 1):
+            raise ValueError("When you set `average` as 'macro', you have to provide the number of classes.")
+        if num_classes and ignore_index is not None and (not ignore_index < num_classes or num_classes == 1):
+            raise ValueError(f"The `ignore_index` {ignore_index} is not valid for inputs with {num_classes} classes")
+        listed = mdmc_average == "samplewise" or average == "samples"
+        for s in ("tp", "fp", "tn", "fn"):
+            default = [] if listed else torch.zeros([] if average == "micro" else [num_classes], dtype=torch.long)
+            self.add_state(s, default=default, dist_reduce_fx="cat" if listed else "sum")
+        self.average = average
+        self.zero_division = zero_division
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        tp, fp, tn, fn = _stat_scores_update(
+            preds, target, reduce=self.reduce, mdmc_reduce=self.mdmc_reduce, threshold=self.threshold,
+            num_classes=self.num_classes, top_k=self.top_k, multiclass=self.multiclass,
+            ignore_index=self.ignore_index,
+        )
+        if isinstance(self.tp, list):
+            self.tp.append(tp)
+            self.fp.append(fp)
+            self.tn.append(tn)
+            self.fn.append(fn)
+        else:
+            self.tp += tp
+            self.fp += fp
+            self.tn += tn
+            self.fn += fn
+
+    def compute(self) -> Tensor:
+        cat = lambda x: torch.cat(x) if isinstance(x, list) else x  # noqa: E731
+        return _dice_compute(cat(self.tp), cat(self.fp), cat(self.fn), self.average, self.mdmc_reduce,
+                             self.zero_division)

@@ -38,6 +38,29 @@ from torchmetrics_amd.functional.classification.recall_fixed_precision import (
     specificity_at_sensitivity,
 )
 from torchmetrics_amd.functional.classification.roc import binary_roc, multiclass_roc, multilabel_roc, roc
+from torchmetrics_amd.functional.classification.calibration_error import (
+    binary_calibration_error,
+    calibration_error,
+    multiclass_calibration_error,
+)
+from torchmetrics_amd.functional.classification.dice import dice
+from torchmetrics_amd.functional.classification.exact_match import (
+    exact_match,
+    multiclass_exact_match,
+    multilabel_exact_match,
+)
+from torchmetrics_amd.functional.classification.group_fairness import (
+    binary_fairness,
+    binary_groups_stat_rates,
+    demographic_parity,
+    equal_opportunity,
+)
+from torchmetrics_amd.functional.classification.hinge import binary_hinge_loss, hinge_loss, multiclass_hinge_loss
+from torchmetrics_amd.functional.classification.ranking import (
+    multilabel_coverage_error,
+    multilabel_ranking_average_precision,
+    multilabel_ranking_loss,
+)
 from torchmetrics_amd.functional.classification.cohen_kappa import (
     binary_cohen_kappa,
     cohen_kappa,

@@ -1,0 +1,130 @@
+"""Wrapper metrics: BootStrapper, ClasswiseWrapper, MinMaxMetric, MultioutputWrapper, MultitaskWrapper,
+MetricTracker, FeatureShare (reference test model: ``T/wrappers``)."""
+import numpy as np
+import pytest
+import torch
+
+import torchmetrics_amd as tm
+from torchmetrics_amd.image import FrechetInceptionDistance, KernelInceptionDistance
+from torchmetrics_amd.wrappers import FeatureShare
+from torchmetrics_amd.wrappers.bootstrapping import _bootstrap_sampler
+from tests.helpers import assert_close
+
+DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("strategy", ["poisson", "multinomial"])
+def test_bootstrapper_matches_manual_resampling(device, strategy):
+    p, t = torch.randn(200), torch.randn(200)
+    torch.manual_seed(42)
+    bs = tm.BootStrapper(tm.MeanSquaredError(), num_bootstraps=5, sampling_strategy=strategy, raw=True,
+                         quantile=torch.tensor([0.05, 0.95], device=device)).to(device)
+    bs.update(p.to(device), t.to(device))
+    out = bs.compute()
+    torch.manual_seed(42)
+    vals = []
+    for _ in range(5):
+        idx = _bootstrap_sampler(200, strategy)
+        vals.append(((p[idx] - t[idx]) ** 2).mean())
+    vals = torch.stack(vals)
+    assert_close(out["raw"], vals, atol=1e-5)
+    assert_close(out["mean"], vals.mean(), atol=1e-5)
+    assert_close(out["std"], vals.std(), atol=1e-5)
+    assert out["quantile"].shape == (2,)
+
+
+def test_classwise_wrapper():
+    m = tm.ClasswiseWrapper(tm.MulticlassAccuracy(num_classes=3, average=None), labels=["a", "b", "c"])
+    p, t = torch.randn(20, 3), torch.randint(0, 3, (20,))
+    out = m(p, t)
+    assert set(out) == {"multiclassaccuracy_a", "multiclassaccuracy_b", "multiclassaccuracy_c"}
+    ref = tm.functional.multiclass_accuracy(p, t, 3, average=None)
+    assert_close(torch.stack([out[k] for k in sorted(out)]), ref)
+    m2 = tm.ClasswiseWrapper(tm.MulticlassAccuracy(num_classes=3, average=None), prefix="acc-")
+    assert set(m2(p, t)) == {"acc-0", "acc-1", "acc-2"}
+
+
+def test_minmax():
+    m = tm.MinMaxMetric(tm.MeanSquaredError())
+    vals = []
+    for i in range(4):
+        p, t = torch.randn(10), torch.randn(10)
+        m.update(p, t)
+        out = m.compute()
+        vals.append(out["raw"].item())
+        assert out["max"].item() == pytest.approx(max(vals))
+        assert out["min"].item() == pytest.approx(min(vals))
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_multioutput(device):
+    p, t = torch.randn(50, 3), torch.randn(50, 3)
+    t[3, 1] = float("nan")
+    m = tm.MultioutputWrapper(tm.MeanAbsoluteError(), num_outputs=3).to(device)
+    m.update(p.to(device), t.to(device))
+    res = m.compute()
+    ref = []
+    for j in range(3):
+        keep = ~torch.isnan(t[:, j])
+        ref.append((p[keep, j] - t[keep, j]).abs().mean())
+    assert_close(res, torch.stack(ref), atol=1e-6)
+
+
+def test_multitask():
+    mt = tm.MultitaskWrapper({
+        "cls": tm.BinaryAccuracy(),
+        "reg": tm.MetricCollection([tm.MeanSquaredError(), tm.MeanAbsoluteError()]),
+    })
+    pc, tc = torch.rand(10), torch.randint(0, 2, (10,))
+    pr, tr = torch.randn(10), torch.randn(10)
+    mt.update({"cls": pc, "reg": pr}, {"cls": tc, "reg": tr})
+    out = mt.compute()
+    assert_close(out["cls"], tm.functional.binary_accuracy(pc, tc))
+    assert_close(out["reg"]["MeanSquaredError"], ((pr - tr) ** 2).mean(), atol=1e-6)
+    assert list(mt.keys()) == ["cls", "reg_MeanSquaredError", "reg_MeanAbsoluteError"]
+    c = mt.clone(prefix="val_")
+    assert list(c.keys(flatten=False)) == ["val_cls", "val_reg"]
+    with pytest.raises(ValueError):
+        mt.update({"cls": pc}, {"cls": tc})
+
+
+def test_tracker():
+    tr = tm.MetricTracker(tm.MeanSquaredError(), maximize=False)
+    with pytest.raises(ValueError):
+        tr.update(torch.randn(3), torch.randn(3))
+    vals = []
+    for _ in range(3):
+        tr.increment()
+        p, t = torch.randn(10), torch.randn(10)
+        tr.update(p, t)
+        vals.append(((p - t) ** 2).mean().item())
+    all_ = tr.compute_all()
+    np.testing.assert_allclose(all_.numpy(), vals, rtol=1e-5)
+    best, step = tr.best_metric(return_step=True)
+    assert step == int(np.argmin(vals)) and best == pytest.approx(min(vals), rel=1e-5)
+    trc = tm.MetricTracker(tm.MetricCollection([tm.MeanSquaredError(), tm.MeanAbsoluteError()]), maximize=[False, False])
+    trc.increment()
+    trc.update(torch.randn(5), torch.randn(5))
+    b = trc.best_metric()
+    assert set(b) == {"MeanSquaredError", "MeanAbsoluteError"}
+
+
+class _CountingNet(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.calls = 0
+        self.num_features = 8
+        self.lin = torch.nn.Linear(8, 8)
+
+    def forward(self, x):
+        self.calls += 1
+        return self.lin(x.float())
+
+
+def test_feature_share_runs_network_once():
+    net = _CountingNet()
+    fs = FeatureShare([FrechetInceptionDistance(feature=net), KernelInceptionDistance(feature=net, subset_size=4)])
+    x = torch.randn(10, 8)
+    fs.update(x, real=True)
+    assert net.calls == 1

@@ -24,3 +24,11 @@ from torchmetrics_amd.classification import *  # noqa: E402,F401,F403
 from torchmetrics_amd.collections import MetricCollection  # noqa: E402
 from torchmetrics_amd.metric import CompositionalMetric, Metric  # noqa: E402
 from torchmetrics_amd.regression import *  # noqa: E402,F401,F403
+from torchmetrics_amd.wrappers import (  # noqa: E402
+    BootStrapper,
+    ClasswiseWrapper,
+    MetricTracker,
+    MinMaxMetric,
+    MultioutputWrapper,
+    MultitaskWrapper,
+)

@@ -1,0 +1,53 @@
+"""Per-class dict output for metrics with ``average=None`` (reference ``S/wrappers/classwise.py:26-200``)."""
+from typing import Any, Dict, List, Optional
+
+from torch import Tensor
+
+from torchmetrics_amd.metric import Metric
+from torchmetrics_amd.wrappers.abstract import WrapperMetric
+
+
+class ClasswiseWrapper(WrapperMetric):
+    """Turn a per-class tensor result into ``{prefix + label + postfix: value}``."""
+
+    def __init__(
+        self,
+        metric: Metric,
+        labels: Optional[List[str]] = None,
+        prefix: Optional[str] = None,
+        postfix: Optional[str] = None,
+    ) -> None:
+        super().__init__()
+        if not isinstance(metric, Metric):
+            raise ValueError(f"Expected argument `metric` to be an instance of `torchmetrics.Metric` but got {metric}")
+        self.metric = metric
+        if labels is not None and not (isinstance(labels, list) and all(isinstance(lab, str) for lab in labels)):
+            raise ValueError(f"Expected argument `labels` to either be `None` or a list of strings but got {labels}")
+        self.labels = labels
+        if prefix is not None and not isinstance(prefix, str):
+            raise ValueError(f"Expected argument `prefix` to either be `None` or a string but got {prefix}")
+        self._prefix = prefix
+        if postfix is not None and not isinstance(postfix, str):
+            raise ValueError(f"Expected argument `postfix` to either be `None` or a string but got {postfix}")
+        self._postfix = postfix
+        self._update_count = 1
+
+    def _convert(self, x: Tensor) -> Dict[str, Any]:
+        if not self._prefix and not self._postfix:
+            prefix, postfix = f"{self.metric.__class__.__name__.lower()}_", ""
+        else:
+            prefix, postfix = self._prefix or "", self._postfix or ""
+        names = range(len(x)) if self.labels is None else self.labels
+        return {f"{prefix}{name}{postfix}": val for name, val in zip(names, x)}
+
+    def forward(self, *args: Any, **kwargs: Any) -> Any:
+        return self._convert(self.metric(*args, **kwargs))
+
+    def update(self, *args: Any, **kwargs: Any) -> None:
+        self.metric.update(*args, **kwargs)
+
+    def compute(self) -> Dict[str, Tensor]:
+        return self._convert(self.metric.compute())
+
+    def reset(self) -> None:
+        self.metric.reset()

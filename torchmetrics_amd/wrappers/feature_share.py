@@ -1,0 +1,66 @@
+"""Share one (expensive) feature network between several metrics (reference ``S/wrappers/feature_share.py``).
+
+The first metric's ``feature_network`` module is wrapped in an LRU cache keyed by the input tensors and installed on
+every member, so FID + KID + IS on the same images run the Inception forward pass once per batch.
+"""
+from functools import lru_cache
+from typing import Any, Dict, Optional, Sequence, Union
+
+from torch.nn import Module
+
+from torchmetrics_amd.collections import MetricCollection
+from torchmetrics_amd.metric import Metric
+from torchmetrics_amd.utilities.prints import rank_zero_warn
+
+
+class NetworkCache(Module):
+    """``network`` with its ``forward`` memoised for the last ``max_size`` distinct argument tuples."""
+
+    def __init__(self, network: Module, max_size: int = 100) -> None:
+        super().__init__()
+        self.max_size = max_size
+        self.network = network
+        self.network.forward = lru_cache(maxsize=self.max_size)(network.forward)
+
+    def forward(self, *args: Any, **kwargs: Any) -> Any:
+        return self.network(*args, **kwargs)
+
+
+class FeatureShare(MetricCollection):
+    """A ``MetricCollection`` whose members share one cached feature extractor."""
+
+    def __init__(
+        self,
+        metrics: Union[Metric, Sequence[Metric], Dict[str, Metric]],
+        max_cache_size: Optional[int] = None,
+    ) -> None:
+        super().__init__(metrics=metrics, compute_groups=False)
+        if max_cache_size is None:
+            max_cache_size = len(self)
+        if not isinstance(max_cache_size, int):
+            raise TypeError(f"max_cache_size should be an integer, but got {max_cache_size}")
+        try:
+            first = next(iter(self.values()))
+            shared = getattr(first, first.feature_network)
+        except AttributeError as err:
+            raise AttributeError(
+                "Tried to extract the network to share from the first metric, but it did not have a `feature_network`"
+                " attribute. Please make sure that the metric has an attribute with that name,"
+                " else it cannot be shared."
+            ) from err
+        cached = NetworkCache(shared, max_size=max_cache_size)
+        for name, metric in self.items():
+            if not hasattr(metric, "feature_network"):
+                raise AttributeError(
+                    "Tried to set the cached network to all metrics, but one of the metrics did not have a"
+                    " `feature_network` attribute. Please make sure that all metrics have a attribute with that name,"
+                    f" else it cannot be shared. Failed on metric {name}."
+                )
+            if str(getattr(metric, metric.feature_network)) != str(shared):
+                rank_zero_warn(
+                    f"The network to share between the metrics is not the same for all metrics."
+                    f" Metric {name} has a different network than the first metric."
+                    " This may lead to unexpected behavior.",
+                    UserWarning,
+                )
+            setattr(metric, metric.feature_network, cached)

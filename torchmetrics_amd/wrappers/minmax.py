@@ -1,0 +1,55 @@
+"""Track the min / max of a scalar metric across ``compute`` calls (reference ``S/wrappers/minmax.py:25-140``)."""
+from typing import Any, Dict, Optional, Union
+
+import torch
+from torch import Tensor
+
+from torchmetrics_amd.metric import Metric
+from torchmetrics_amd.wrappers.abstract import WrapperMetric
+
+
+class MinMaxMetric(WrapperMetric):
+    """``compute`` returns ``{"raw", "max", "min"}`` of the wrapped scalar metric."""
+
+    full_state_update: Optional[bool] = True
+    min_val: Tensor
+    max_val: Tensor
+
+    def __init__(self, base_metric: Metric, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if not isinstance(base_metric, Metric):
+            raise ValueError(
+                f"Expected base metric to be an instance of `torchmetrics.Metric` but received {base_metric}"
+            )
+        self._base_metric = base_metric
+        self.min_val = torch.tensor(float("inf"))
+        self.max_val = torch.tensor(float("-inf"))
+
+    def update(self, *args: Any, **kwargs: Any) -> None:
+        self._base_metric.update(*args, **kwargs)
+
+    def compute(self) -> Dict[str, Tensor]:
+        val = self._base_metric.compute()
+        if not self._is_suitable_val(val):
+            raise RuntimeError(f"Returned value from base metric should be a float or scalar tensor, but got {val}.")
+        val = torch.as_tensor(val)
+        cur_max, cur_min = self.max_val.to(val.device), self.min_val.to(val.device)
+        # device-side select: no host round trip for the comparison
+        self.max_val = torch.where(cur_max < val, val, cur_max)
+        self.min_val = torch.where(cur_min > val, val, cur_min)
+        return {"raw": val, "max": self.max_val, "min": self.min_val}
+
+    def forward(self, *args: Any, **kwargs: Any) -> Any:
+        return super(WrapperMetric, self).forward(*args, **kwargs)
+
+    def reset(self) -> None:
+        super().reset()
+        self._base_metric.reset()
+
+    @staticmethod
+    def _is_suitable_val(val: Union[float, Tensor]) -> bool:
+        if isinstance(val, (int, float)):
+            return True
+        if isinstance(val, Tensor):
+            return val.numel() == 1
+        return False

@@ -1,3 +1,4 @@
 """Functional (stateless) metrics (parity: reference ``F/__init__.py``)."""
 from torchmetrics_amd.functional.classification import *  # noqa: F401,F403
 from torchmetrics_amd.functional.regression import *  # noqa: F401,F403
+from torchmetrics_amd.functional.retrieval import *  # noqa: F401,F403

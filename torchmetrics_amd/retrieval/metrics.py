@@ -1,0 +1,289 @@
+"""Retrieval module metrics (parity: reference ``S/retrieval/*.py``), evaluated for all queries in one pass."""
+from typing import Any, Callable, List, Optional, Tuple, Union
+
+import torch
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_amd.functional.retrieval._segments import Segments
+from torchmetrics_amd.functional.retrieval.metrics import (
+    _seg_auroc,
+    _seg_average_precision,
+    _seg_fall_out,
+    _seg_hit_rate,
+    _seg_ndcg,
+    _seg_pr_curve,
+    _seg_precision,
+    _seg_r_precision,
+    _seg_recall,
+    _seg_reciprocal_rank,
+    retrieval_auroc,
+)
+from torchmetrics_amd.metric import Metric
+from torchmetrics_amd.retrieval.base import RetrievalMetric, _retrieval_aggregate
+from torchmetrics_amd.utilities.checks import _check_retrieval_inputs
+from torchmetrics_amd.utilities.data import dim_zero_cat
+from torchmetrics_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_curve
+
+_Agg = Union[Literal["mean", "median", "min", "max"], Callable]
+
+
+def _check_top_k(top_k: Optional[int]) -> None:
+    if top_k is not None and not (isinstance(top_k, int) and top_k > 0):
+        raise ValueError("`top_k` has to be a positive integer or None")
+
+
+class RetrievalMAP(RetrievalMetric):
+    """Mean average precision over queries."""
+
+    def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None,
+                 top_k: Optional[int] = None, aggregation: _Agg = "mean", **kwargs: Any) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index,
+                         aggregation=aggregation, **kwargs)
+        if top_k is not None and not isinstance(top_k, int) and top_k <= 0:
+            raise ValueError(f"Argument ``top_k`` has to be a positive integer or None, but got {top_k}")
+        self.top_k = top_k
+
+    def _segment_metric(self, seg: Segments) -> Tensor:
+        return _seg_average_precision(seg, self.top_k)
+
+
+class RetrievalMRR(RetrievalMetric):
+    """Mean reciprocal rank of the first relevant document."""
+
+    def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None,
+                 top_k: Optional[int] = None, aggregation: _Agg = "mean", **kwargs: Any) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index,
+                         aggregation=aggregation, **kwargs)
+        if top_k is not None and not isinstance(top_k, int) and top_k <= 0:
+            raise ValueError(f"Argument ``top_k`` has to be a positive integer or None, but got {top_k}")
+        self.top_k = top_k
+
+    def _segment_metric(self, seg: Segments) -> Tensor:
+        return _seg_reciprocal_rank(seg, self.top_k)
+
+
+class RetrievalPrecision(RetrievalMetric):
+    """Precision at k averaged over queries."""
+
+    def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None,
+                 top_k: Optional[int] = None, adaptive_k: bool = False, aggregation: _Agg = "mean",
+                 **kwargs: Any) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index,
+                         aggregation=aggregation, **kwargs)
+        _check_top_k(top_k)
+        if not isinstance(adaptive_k, bool):
+            raise ValueError("`adaptive_k` has to be a boolean")
+        self.top_k = top_k
+        self.adaptive_k = adaptive_k
+
+    def _segment_metric(self, seg: Segments) -> Tensor:
+        return _seg_precision(seg, self.top_k, self.adaptive_k)
+
+
+class RetrievalRecall(RetrievalMetric):
+    """Recall at k averaged over queries."""
+
+    def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None,
+                 top_k: Optional[int] = None, aggregation: _Agg = "mean", **kwargs: Any) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index,
+                         aggregation=aggregation, **kwargs)
+        _check_top_k(top_k)
+        self.top_k = top_k
+
+    def _segment_metric(self, seg: Segments) -> Tensor:
+        return _seg_recall(seg, self.top_k)
+
+
+class RetrievalFallOut(RetrievalMetric):
+    """Fall-out at k (fraction of non-relevant documents retrieved); lower is better."""
+
+    higher_is_better: bool = False
+
+    def __init__(self, empty_target_action: str = "pos", ignore_index: Optional[int] = None,
+                 top_k: Optional[int] = None, aggregation: _Agg = "mean", **kwargs: Any) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index,
+                         aggregation=aggregation, **kwargs)
+        _check_top_k(top_k)
+        self.top_k = top_k
+
+    def _empty_queries(self, seg: Segments) -> Tensor:
+        return seg.seg_sum(1 - seg.target) == 0
+
+    def _empty_error(self) -> str:
+        return "`compute` method was provided with a query with no negative target."
+
+    def _segment_metric(self, seg: Segments) -> Tensor:
+        return _seg_fall_out(seg, self.top_k)
+
+
+class RetrievalHitRate(RetrievalMetric):
+    """Hit rate at k (any relevant document in the top k)."""
+
+    def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None,
+                 top_k: Optional[int] = None, aggregation: _Agg = "mean", **kwargs: Any) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index,
+                         aggregation=aggregation, **kwargs)
+        _check_top_k(top_k)
+        self.top_k = top_k
+
+    def _segment_metric(self, seg: Segments) -> Tensor:
+        return _seg_hit_rate(seg, self.top_k)
+
+
+class RetrievalNormalizedDCG(RetrievalMetric):
+    """Normalised discounted cumulative gain (graded relevance allowed)."""
+
+    def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None,
+                 top_k: Optional[int] = None, aggregation: _Agg = "mean", **kwargs: Any) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index,
+                         aggregation=aggregation, **kwargs)
+        _check_top_k(top_k)
+        self.top_k = top_k
+        self.allow_non_binary_target = True
+
+    def _segment_metric(self, seg: Segments) -> Tensor:
+        return _seg_ndcg(seg, self.top_k)
+
+
+class RetrievalRPrecision(RetrievalMetric):
+    """Precision at R, R = number of relevant documents of the query."""
+
+    def _segment_metric(self, seg: Segments) -> Tensor:
+        return _seg_r_precision(seg)
+
+
+class RetrievalAUROC(RetrievalMetric):
+    """ROC AUC of the top-k documents, averaged over queries."""
+
+    def __init__(self, empty_target_action: Literal["error", "skip", "neg", "pos"] = "neg",
+                 ignore_index: Optional[int] = None, top_k: Optional[int] = None, max_fpr: Optional[float] = None,
+                 aggregation: _Agg = "mean", **kwargs: Any) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index,
+                         aggregation=aggregation, **kwargs)
+        _check_top_k(top_k)
+        self.top_k = top_k
+        if max_fpr is not None and not isinstance(max_fpr, float) and 0 < max_fpr <= 1:
+            raise ValueError(f"Arguments `max_fpr` should be a float in range (0, 1], but got: {max_fpr}")
+        self.max_fpr = max_fpr
+
+    def _segment_metric(self, seg: Segments) -> Optional[Tensor]:
+        return _seg_auroc(seg, self.top_k) if self.max_fpr is None else None
+
+    def _metric(self, preds: Tensor, target: Tensor) -> Tensor:
+        return retrieval_auroc(preds, target, top_k=self.top_k, max_fpr=self.max_fpr)
+
+
+def _retrieval_recall_at_fixed_precision(
+    precision: Tensor, recall: Tensor, top_k: Tensor, min_precision: float
+) -> Tuple[Tensor, Tensor]:
+    ok = precision >= min_precision
+    if bool(ok.any()):
+        # lexicographic max over (recall, k) among qualifying points, as the reference's max over tuples
+        r = torch.where(ok, recall, torch.full_like(recall, -1.0))
+        best_r = r.max()
+        cand = torch.where(ok & (recall == best_r), top_k, torch.zeros_like(top_k))
+        max_recall, best_k = best_r, cand.max()
+    else:
+        max_recall = torch.tensor(0.0, device=recall.device, dtype=recall.dtype)
+        best_k = torch.tensor(len(top_k))
+    if max_recall == 0.0:
+        best_k = torch.tensor(len(top_k), device=top_k.device, dtype=top_k.dtype)
+    return max_recall, best_k
+
+
+class RetrievalPrecisionRecallCurve(Metric):
+    """Precision@k / recall@k curves for k = 1..max_k, aggregated over queries."""
+
+    is_differentiable: bool = False
+    higher_is_better: bool = True
+    full_state_update: bool = False
+    indexes: List[Tensor]
+    preds: List[Tensor]
+    target: List[Tensor]
+
+    def __init__(self, max_k: Optional[int] = None, adaptive_k: bool = False, empty_target_action: str = "neg",
+                 ignore_index: Optional[int] = None, aggregation: _Agg = "mean", **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        self.allow_non_binary_target = False
+        if empty_target_action not in ("error", "skip", "neg", "pos"):
+            raise ValueError(f"Argument `empty_target_action` received a wrong value `{empty_target_action}`.")
+        self.empty_target_action = empty_target_action
+        if ignore_index is not None and not isinstance(ignore_index, int):
+            raise ValueError("Argument `ignore_index` must be an integer or None.")
+        self.ignore_index = ignore_index
+        if (max_k is not None) and not (isinstance(max_k, int) and max_k > 0):
+            raise ValueError("`max_k` has to be a positive integer or None")
+        self.max_k = max_k
+        if not isinstance(adaptive_k, bool):
+            raise ValueError("`adaptive_k` has to be a boolean")
+        self.adaptive_k = adaptive_k
+        if not (aggregation in ("mean", "median", "min", "max") or callable(aggregation)):
+            raise ValueError(
+                "Argument `aggregation` must be one of `mean`, `median`, `min`, `max` or a custom callable function"
+                f"which takes tensor of values, but got {aggregation}."
+            )
+        self.aggregation = aggregation
+        self.add_state("indexes", default=[], dist_reduce_fx=None)
+        self.add_state("preds", default=[], dist_reduce_fx=None)
+        self.add_state("target", default=[], dist_reduce_fx=None)
+
+    def update(self, preds: Tensor, target: Tensor, indexes: Tensor) -> None:
+        if indexes is None:
+            raise ValueError("Argument `indexes` cannot be None")
+        indexes, preds, target = _check_retrieval_inputs(
+            indexes, preds, target, allow_non_binary_target=self.allow_non_binary_target, ignore_index=self.ignore_index
+        )
+        self.indexes.append(indexes)
+        self.preds.append(preds)
+        self.target.append(target)
+
+    def compute(self) -> Tuple[Tensor, Tensor, Tensor]:
+        preds = dim_zero_cat(self.preds)
+        seg = Segments(preds, dim_zero_cat(self.target), dim_zero_cat(self.indexes))
+        max_k = self.max_k if self.max_k is not None else int(seg.size.max().item())
+        precision, recall, _ = _seg_pr_curve(seg, max_k, self.adaptive_k)
+        empty = seg.seg_sum(seg.target) == 0
+        if self.empty_target_action == "error" and bool(empty.any()):
+            raise ValueError("`compute` method was provided with a query with no positive target.")
+        if self.empty_target_action == "skip":
+            precision, recall = precision[~empty], recall[~empty]
+        else:
+            fill = 1.0 if self.empty_target_action == "pos" else 0.0
+            e = empty.unsqueeze(1)
+            precision = torch.where(e, torch.full_like(precision, fill), precision)
+            recall = torch.where(e, torch.full_like(recall, fill), recall)
+        if precision.shape[0] == 0:
+            z = torch.zeros(max_k).to(preds)
+            return z, z.clone(), torch.arange(1, max_k + 1, device=preds.device)
+        precision = _retrieval_aggregate(precision.to(preds), self.aggregation, dim=0)
+        recall = _retrieval_aggregate(recall.to(preds), self.aggregation, dim=0)
+        return precision, recall, torch.arange(1, max_k + 1, device=preds.device)
+
+    def plot(self, curve: Optional[Tuple[Tensor, Tensor, Tensor]] = None,
+             ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        curve = curve or self.compute()
+        return plot_curve(curve, ax=ax, label_names=("False positive rate", "True positive rate"),
+                          name=self.__class__.__name__)
+
+
+class RetrievalRecallAtFixedPrecision(RetrievalPrecisionRecallCurve):
+    """Highest recall@k whose precision@k is at least ``min_precision``, and that k."""
+
+    higher_is_better = True
+
+    def __init__(self, min_precision: float = 0.0, max_k: Optional[int] = None, adaptive_k: bool = False,
+                 empty_target_action: str = "neg", ignore_index: Optional[int] = None, **kwargs: Any) -> None:
+        super().__init__(max_k=max_k, adaptive_k=adaptive_k, empty_target_action=empty_target_action,
+                         ignore_index=ignore_index, **kwargs)
+        if not (isinstance(min_precision, float) and 0.0 <= min_precision <= 1.0):
+            raise ValueError("`min_precision` has to be a positive float between 0 and 1")
+        self.min_precision = min_precision
+
+    def compute(self) -> Tuple[Tensor, Tensor]:
+        precisions, recalls, top_k = super().compute()
+        return _retrieval_recall_at_fixed_precision(precisions, recalls, top_k, self.min_precision)
+
+    def plot(self, val: Any = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        val = val or self.compute()[0]
+        return self._plot(val, ax)

@@ -5,5 +5,22 @@ from torchmetrics_amd.image.generative import (
     KernelInceptionDistance,
     MemorizationInformedFrechetInceptionDistance,
 )
+from torchmetrics_amd.image.quality import (
+    ErrorRelativeGlobalDimensionlessSynthesis,
+    MultiScaleStructuralSimilarityIndexMeasure,
+    PeakSignalNoiseRatio,
+    PeakSignalNoiseRatioWithBlockedEffect,
+    QualityWithNoReference,
+    RelativeAverageSpectralError,
+    RootMeanSquaredErrorUsingSlidingWindow,
+    SpatialCorrelationCoefficient,
+    SpatialDistortionIndex,
+    SpectralAngleMapper,
+    SpectralDistortionIndex,
+    StructuralSimilarityIndexMeasure,
+    TotalVariation,
+    UniversalImageQualityIndex,
+    VisualInformationFidelity,
+)
 
 __all__ = [k for k in dir() if k[0].isupper()]

@@ -215,3 +215,23 @@ def curve_update(preds: Tensor, target: Tensor, thr_sorted: Tensor, perm: Tensor
                             mode, -1 if ignore_index is None else int(ignore_index), ignore_index is not None, micro)
     else:
         _cpu.curve_update(preds, target, thr_sorted, perm, state, err, mode, ignore_index, micro)
+
+
+# ----------------------------------------------------------------------------------------------- image windows
+SSIM_MODE = 0
+UQI_MODE = 1
+
+
+def ssim2d_partials(x: Tensor, y: Tensor, wh: Tensor, ww: Tensor, c12: Tensor, mode: int = SSIM_MODE) -> Tensor:
+    """Per-plane sums of SSIM (or UQI) and contrast sensitivity over all windows fully inside the image.
+
+    ``x``/``y``: ``[P, H, W]``; ``wh``/``ww``: separable window weights; ``c12``: ``(c1, c2, eps)`` as a tensor (may
+    live on the device).  Returns ``[P, T, 2]`` partial sums (``T`` tiles on ROCm, 1 on the CPU); callers sum dim 1.
+    """
+    if x.is_cuda:
+        acc = torch.float64 if x.dtype == torch.float64 else torch.float32
+        if x.dtype not in (torch.float32, torch.float16, torch.bfloat16, torch.float64):
+            x, y = x.float(), y.float()
+        return _ops().ssim2d_partials(x.contiguous(), y.contiguous(), wh.to(acc).contiguous(),
+                                      ww.to(acc).contiguous(), c12.to(device=x.device, dtype=acc).contiguous(), mode)
+    return _cpu.ssim2d_partials(x, y, wh, ww, c12, mode)

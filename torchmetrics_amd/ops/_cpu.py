@@ -260,3 +260,25 @@ def curve_update(preds: Tensor, target: Tensor, thr_sorted: Tensor, perm: Tensor
     res = torch.empty_like(out)
     res[perm] = out
     state += res.reshape(state.shape)
+
+
+def ssim2d_partials(x: Tensor, y: Tensor, wh: Tensor, ww: Tensor, c12: Tensor, mode: int) -> Tensor:
+    """Valid-window SSIM / UQI sums per plane via one separable depthwise convolution of the 5 moment maps."""
+    acc = torch.float64 if x.dtype == torch.float64 else torch.float32
+    x, y = x.to(acc).unsqueeze(1), y.to(acc).unsqueeze(1)
+    k = (wh.to(acc)[:, None] * ww.to(acc)[None, :])[None, None]
+    maps = torch.cat([x, y, x * x, y * y, x * y], 1)  # [P, 5, H, W]
+    m = torch.nn.functional.conv2d(maps, k.expand(5, 1, -1, -1), groups=5)
+    mx, my, exx, eyy, exy = m.unbind(1)
+    mxx, myy, mxy = mx * mx, my * my, mx * my
+    sxx, syy, sxy = (exx - mxx).clamp(min=0), (eyy - myy).clamp(min=0), exy - mxy
+    c1, c2, eps = (float(v) for v in c12.to(acc).cpu()[:3])
+    if mode == 0:
+        upper, lower = 2 * sxy + c2, sxx + syy + c2
+        val = ((2 * mxy + c1) * upper) / ((mxx + myy + c1) * lower)
+        cs = upper / lower
+    else:
+        upper, lower = 2 * sxy, sxx + syy
+        val = ((2 * mxy) * upper) / ((mxx + myy) * lower + eps)
+        cs = torch.zeros_like(val)
+    return torch.stack([val.flatten(1).sum(1), cs.flatten(1).sum(1)], -1).unsqueeze(1)

@@ -1,0 +1,222 @@
+"""Detection: IoU family kernels, MeanAveragePrecision vs a plain-Python COCO oracle and published fixture values."""
+import numpy as np
+import pytest
+import torch
+
+from torchmetrics_amd import ops
+from torchmetrics_amd.detection import MeanAveragePrecision
+from tests._coco_oracle import coco_eval, summarize
+from tests.helpers import assert_close, run_ddp
+
+DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+IOU_THRS = torch.linspace(0.5, 0.95, 10).tolist()
+REC_THRS = torch.linspace(0.0, 1.0, 101).tolist()
+
+
+def _random_coco(seed, n_img=12, n_cls=4, max_gt=8, max_det=15, crowd=True):
+    g = torch.Generator().manual_seed(seed)
+    preds, target = [], []
+    for _ in range(n_img):
+        ng = int(torch.randint(0, max_gt + 1, (1,), generator=g))
+        nd = int(torch.randint(0, max_det + 1, (1,), generator=g))
+        gxy = torch.rand(ng, 2, generator=g) * 200
+        gwh = torch.rand(ng, 2, generator=g) * 120 + 4
+        gb = torch.cat([gxy, gxy + gwh], 1)
+        gl = torch.randint(0, n_cls, (ng,), generator=g)
+        # detections: jittered copies of ground truths plus clutter
+        src = torch.randint(0, max(ng, 1), (nd,), generator=g)
+        jitter = torch.randn(nd, 4, generator=g) * 6
+        db = gb[src] + jitter if ng else torch.rand(nd, 4, generator=g) * 200
+        db = torch.cat([torch.minimum(db[:, :2], db[:, 2:]), torch.maximum(db[:, :2], db[:, 2:]) + 1], 1)
+        dl = gl[src] if ng else torch.randint(0, n_cls, (nd,), generator=g)
+        flip = torch.rand(nd, generator=g) < 0.2
+        dl = torch.where(flip, torch.randint(0, n_cls, (nd,), generator=g), dl)
+        scores = (torch.rand(nd, generator=g) * 10).round() / 10  # ties
+        t = {"boxes": gb, "labels": gl}
+        if crowd:
+            t["iscrowd"] = (torch.rand(ng, generator=g) < 0.15).long()
+        preds.append({"boxes": db, "scores": scores, "labels": dl})
+        target.append(t)
+    return preds, target
+
+
+def _oracle(preds, target, max_dets=(1, 10, 100)):
+    def xywh(b):
+        return [[x1, y1, x2 - x1, y2 - y1] for x1, y1, x2, y2 in b.tolist()]
+
+    cats = sorted(set(torch.cat([p["labels"] for p in preds] + [t["labels"] for t in target]).tolist()))
+    dets = [[(bb, s, c) for bb, s, c in zip(xywh(p["boxes"]), p["scores"].tolist(), p["labels"].tolist())]
+            for p in preds]
+    gts = []
+    for t in target:
+        bb = xywh(t["boxes"])
+        crowd = t.get("iscrowd", torch.zeros_like(t["labels"])).tolist()
+        gts.append([(b, c, cr, b[2] * b[3]) for b, c, cr in zip(bb, t["labels"].tolist(), crowd)])
+    prec, rec = coco_eval(dets, gts, cats, IOU_THRS, REC_THRS, list(max_dets))
+    return summarize(prec, rec, IOU_THRS, list(max_dets)), prec, rec
+
+
+def _to(items, device):
+    return [{k: v.to(device) for k, v in it.items()} for it in items]
+
+
+# ---------------------------------------------------------------------------------------------------- box ops
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("op", [ops.BOX_IOU, ops.BOX_GIOU, ops.BOX_DIOU, ops.BOX_CIOU])
+def test_box_pairwise_matches_formula(device, op):
+    g = torch.Generator().manual_seed(op)
+    a = torch.rand(37, 2, generator=g) * 50
+    a = torch.cat([a, a + torch.rand(37, 2, generator=g) * 30 + 1], 1)
+    b = torch.rand(23, 2, generator=g) * 50
+    b = torch.cat([b, b + torch.rand(23, 2, generator=g) * 30 + 1], 1)
+    ref = ops._cpu.box_pairwise(a.double(), b.double(), op, False)
+    out = ops.box_pairwise(a.to(device), b.to(device), op)
+    assert_close(out, ref, atol=1e-5)
+    aligned = ops.box_pairwise(a[:23].to(device), b.to(device), op, aligned=True)
+    assert_close(aligned, ref[:23].diagonal(), atol=1e-5)
+    # torchvision-style reference for plain IoU
+    if op == ops.BOX_IOU:
+        area = lambda x: (x[:, 2] - x[:, 0]) * (x[:, 3] - x[:, 1])  # noqa: E731
+        lt = torch.max(a[:, None, :2], b[None, :, :2])
+        rb = torch.min(a[:, None, 2:], b[None, :, 2:])
+        inter = (rb - lt).clamp(min=0).prod(2)
+        assert_close(out, inter / (area(a)[:, None] + area(b)[None] - inter), atol=1e-5)
+
+
+# ------------------------------------------------------------------------------------------------------- mAP
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_map_vs_python_coco_oracle(device, seed):
+    preds, target = _random_coco(seed)
+    m = MeanAveragePrecision(class_metrics=True, extended_summary=True).to(device)
+    m.update(_to(preds[:6], device), _to(target[:6], device))
+    m.update(_to(preds[6:], device), _to(target[6:], device))
+    res = m.compute()
+    stats, prec, rec = _oracle(preds, target)
+    names = ["map", "map_50", "map_75", "map_small", "map_medium", "map_large", "mar_1", "mar_10", "mar_100",
+             "mar_small", "mar_medium", "mar_large"]
+    for name, v in zip(names, stats):
+        assert_close(res[name], v, atol=1e-6)
+    assert_close(res["precision"], prec, atol=1e-6)
+    assert_close(res["recall"], rec, atol=1e-6)
+    # per-class: mean over (iou, recall) of the class slice at area=all, maxdet=100
+    for k in range(prec.shape[2]):
+        s = prec[:, :, k, 0, -1]
+        exp = s[s > -1].mean() if (s > -1).any() else -1
+        assert_close(res["map_per_class"][k], exp, atol=1e-6)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_map_max_dets_and_micro(device):
+    preds, target = _random_coco(5, n_img=6, max_det=30)
+    m = MeanAveragePrecision(max_detection_thresholds=[2, 5, 20]).to(device)
+    m.update(_to(preds, device), _to(target, device))
+    res = m.compute()
+    stats, _, _ = _oracle(preds, target, max_dets=(2, 5, 20))
+    for name, v in zip(["map", "mar_2", "mar_5", "mar_20"], [stats[0], stats[6], stats[7], stats[8]]):
+        assert_close(res[name], v, atol=1e-6)
+    mm = MeanAveragePrecision(average="micro").to(device)
+    mm.update(_to(preds, device), _to(target, device))
+    zero = [{**p, "labels": torch.zeros_like(p["labels"])} for p in preds]
+    zt = [{**t, "labels": torch.zeros_like(t["labels"])} for t in target]
+    stats_micro, _, _ = _oracle(zero, zt)
+    assert_close(mm.compute()["map"], stats_micro[0], atol=1e-6)
+
+
+# reference test fixture (``T/detection/test_map.py`` ``_inputs``: COCO val2014 image ids 42, 73, 74, 987).  The
+# reference pins it against pycocotools at test time; pycocotools is not installable here, so the expected values
+# come from the plain-Python COCO oracle (``tests/_coco_oracle.py``) -- parity with pycocotools itself is unpinned.
+_FIXTURE_PREDS = [
+    {"boxes": [[258.15, 41.29, 606.41, 285.07]], "scores": [0.236], "labels": [4]},
+    {"boxes": [[61.00, 22.75, 565.00, 632.42], [12.66, 3.32, 281.26, 275.23]], "scores": [0.318, 0.726],
+     "labels": [3, 2]},
+    {"boxes": [[87.87, 276.25, 384.29, 379.43], [0.00, 3.66, 142.15, 316.06], [296.55, 93.96, 314.97, 152.79],
+               [328.94, 97.05, 342.49, 122.98], [356.62, 95.47, 372.33, 147.55], [464.08, 105.09, 495.74, 146.99],
+               [276.11, 103.84, 291.44, 150.72]],
+     "scores": [0.546, 0.3, 0.407, 0.611, 0.335, 0.805, 0.953], "labels": [4, 1, 0, 0, 0, 0, 0]},
+    {"boxes": [[72.92, 45.96, 91.23, 80.57], [45.17, 45.34, 66.28, 79.83], [82.28, 47.04, 99.66, 78.50],
+               [59.96, 46.17, 80.35, 80.48], [75.29, 23.01, 91.85, 50.85], [71.14, 1.10, 96.96, 28.33],
+               [61.34, 55.23, 77.14, 79.57], [41.17, 45.78, 60.99, 78.48], [56.18, 44.80, 64.42, 56.25]],
+     "scores": [0.532, 0.204, 0.782, 0.202, 0.883, 0.271, 0.561, 0.204, 0.349], "labels": [49] * 9},
+]
+_FIXTURE_TARGET = [
+    {"boxes": [[214.1500, 41.2900, 562.4100, 285.0700]], "labels": [4]},
+    {"boxes": [[13.00, 22.75, 548.98, 632.42], [1.66, 3.32, 270.26, 275.23]], "labels": [2, 2]},
+    {"boxes": [[61.87, 276.25, 358.29, 379.43], [2.75, 3.66, 162.15, 316.06], [295.55, 93.96, 313.97, 152.79],
+               [326.94, 97.05, 340.49, 122.98], [356.62, 95.47, 372.33, 147.55], [462.08, 105.09, 493.74, 146.99],
+               [277.11, 103.84, 292.44, 150.72]], "labels": [4, 1, 0, 0, 0, 0, 0]},
+    {"boxes": [[72.92, 45.96, 91.23, 80.57], [50.17, 45.34, 71.28, 79.83], [81.28, 47.04, 98.66, 78.50],
+               [63.96, 46.17, 84.35, 80.48], [75.29, 23.01, 91.85, 50.85], [56.39, 21.65, 75.66, 45.54],
+               [73.14, 1.10, 98.96, 28.33], [62.34, 55.23, 78.14, 79.57], [44.17, 45.78, 63.99, 78.48],
+               [58.18, 44.80, 66.42, 56.25]], "labels": [49] * 10},
+]
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_map_published_fixture(device):
+    def conv(items, with_scores):
+        out = []
+        for it in items:
+            d = {"boxes": torch.tensor(it["boxes"]), "labels": torch.tensor(it["labels"], dtype=torch.int32)}
+            if with_scores:
+                d["scores"] = torch.tensor(it["scores"])
+            out.append(d)
+        return out
+
+    preds, target = conv(_FIXTURE_PREDS, True), conv(_FIXTURE_TARGET, False)
+    m = MeanAveragePrecision(class_metrics=True).to(device)
+    m.update(_to(preds, device), _to(target, device))
+    res = m.compute()
+    stats, _, _ = _oracle(preds, target)
+    names = ["map", "map_50", "map_75", "map_small", "map_medium", "map_large", "mar_1", "mar_10", "mar_100",
+             "mar_small", "mar_medium", "mar_large"]
+    for name, v in zip(names, stats):
+        assert_close(res[name], v, atol=1e-6)
+
+
+def test_map_segm_matches_box_equivalent_masks():
+    # masks that are exactly the (integer) boxes give the same IoU as COCO's box IoU
+    g = torch.Generator().manual_seed(7)
+    preds, target = [], []
+    for _ in range(4):
+        gt = torch.randint(0, 40, (5, 2), generator=g)
+        gt = torch.cat([gt, gt + torch.randint(4, 20, (5, 2), generator=g)], 1)
+        dt = (gt + torch.randint(-3, 4, (5, 4), generator=g)).clamp(0, 63)
+        dt[:, 2:] = torch.maximum(dt[:, 2:], dt[:, :2] + 1)
+
+        def masks(bx):
+            m = torch.zeros(len(bx), 64, 64, dtype=torch.bool)
+            for i, (x1, y1, x2, y2) in enumerate(bx.tolist()):
+                m[i, y1:y2, x1:x2] = True
+            return m
+
+        lab = torch.randint(0, 2, (5,), generator=g)
+        preds.append({"masks": masks(dt), "boxes": dt.float(), "scores": torch.rand(5, generator=g), "labels": lab})
+        target.append({"masks": masks(gt), "boxes": gt.float(), "labels": lab})
+    seg = MeanAveragePrecision(iou_type="segm")
+    seg.update(preds, target)
+    box = MeanAveragePrecision(iou_type="bbox")
+    box.update(preds, target)
+    rs, rb = seg.compute(), box.compute()
+    for k in ("map", "map_50", "map_75", "mar_100"):
+        assert_close(rs[k], rb[k], atol=1e-6)
+    both = MeanAveragePrecision(iou_type=("bbox", "segm"))
+    both.update(preds, target)
+    rboth = both.compute()
+    assert_close(rboth["segm_map"], rs["map"], atol=1e-6)
+
+
+def _ddp_map(rank, world, preds, target):
+    m = MeanAveragePrecision()
+    m.update(preds[rank::world], target[rank::world])
+    res = m.compute()
+    # the gathered order interleaves ranks; COCO results do not depend on image order
+    stats, _, _ = _oracle(preds, target)
+    assert_close(res["map"], stats[0], atol=1e-6)
+    assert_close(res["mar_100"], stats[8], atol=1e-6)
+
+
+@pytest.mark.ddp
+def test_map_ddp():
+    preds, target = _random_coco(11, n_img=8)
+    run_ddp(_ddp_map, preds, target)

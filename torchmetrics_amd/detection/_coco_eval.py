@@ -1,0 +1,290 @@
+"""GPU COCO evaluation (evaluate + accumulate + summarize) for ``MeanAveragePrecision``.
+
+Behavioural reference: pycocotools ``COCOeval`` as driven by ``S/detection/mean_ap.py:513-588`` (parameters
+``iouThrs``, ``recThrs``, ``maxDets``, the 4 default area ranges, per (image, category) greedy matching, per
+(category, area, max-dets) precision / recall accumulation, the 12-number summary).
+
+MI355X design: every step is a batched device computation over *all* images and categories at once --
+(1) two stable sorts group detections by (image, category) in score order and truncate to the largest max-dets;
+(2) the ``coco_match`` HIP kernel runs every (group, area range, IoU threshold) greedy matching problem in its own
+thread; (3) accumulation is a segmented cumulative sum over detections sorted by (category, score) for all
+thresholds / areas at once, a segmented reverse running-max builds the precision envelope, and recall thresholds are
+assigned with one ``searchsorted`` + scatter; (4) the summary is masked means.  The host only sees the final numbers.
+"""
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+from torch import Tensor
+
+from torchmetrics_amd import ops
+
+AREA_RANGES = ((0.0, 1e5**2), (0.0, 32.0**2), (32.0**2, 96.0**2), (96.0**2, 1e5**2))
+AREA_LABELS = ("all", "small", "medium", "large")
+
+
+def _segment_starts(sorted_keys: Tensor) -> Tensor:
+    """Index of the first element of each element's run of equal keys."""
+    n = sorted_keys.numel()
+    idx = torch.arange(n, device=sorted_keys.device)
+    start = torch.ones(n, dtype=torch.bool, device=sorted_keys.device)
+    if n > 1:
+        start[1:] = sorted_keys[1:] != sorted_keys[:-1]
+    return torch.where(start, idx, torch.zeros_like(idx)).cummax(0).values
+
+
+def coco_evaluate(
+    det_boxes: Sequence[Tensor],
+    det_scores: Sequence[Tensor],
+    det_labels: Sequence[Tensor],
+    gt_boxes: Sequence[Tensor],
+    gt_labels: Sequence[Tensor],
+    gt_crowds: Sequence[Tensor],
+    gt_areas: Sequence[Tensor],
+    iou_thresholds: Sequence[float],
+    rec_thresholds: Sequence[float],
+    max_dets: Sequence[int],
+    classes: Tensor,
+    det_masks: Optional[Sequence[Tensor]] = None,
+    gt_masks: Optional[Sequence[Tensor]] = None,
+) -> Dict[str, Tensor]:
+    """COCO precision ``[T, R, K, A, M]``, recall ``[T, K, A, M]`` and scores.
+
+    Boxes are xywh.  With ``det_masks`` / ``gt_masks`` (``[n, H, W]`` per image) IoUs are mask IoUs and areas are
+    mask areas (``segm``).  ``classes`` are the sorted category ids of the K axis; annotations whose label is not
+    among them are dropped (pycocotools ``catIds`` filtering).
+    """
+    dev = classes.device
+    n_img = len(det_labels)
+    t_thr = torch.tensor(list(iou_thresholds), dtype=torch.float64, device=dev)
+    r_thr = torch.tensor(list(rec_thresholds), dtype=torch.float64, device=dev)
+    areas = torch.tensor(AREA_RANGES, dtype=torch.float64, device=dev)
+    T, R, A, M, K = t_thr.numel(), r_thr.numel(), areas.shape[0], len(max_dets), classes.numel()
+    precision = torch.full((T, R, K, A, M), -1.0, dtype=torch.float64, device=dev)
+    recall = torch.full((T, K, A, M), -1.0, dtype=torch.float64, device=dev)
+    scores_out = torch.full((T, R, K, A, M), -1.0, dtype=torch.float64, device=dev)
+    if K == 0:
+        return {"precision": precision, "recall": recall, "scores": scores_out}
+
+    def flat(seq, dtype, shape_tail=()):
+        parts = [x.to(device=dev).reshape(-1, *shape_tail) for x in seq]
+        return torch.cat(parts).to(dtype) if parts else torch.zeros((0, *shape_tail), dtype=dtype, device=dev)
+
+    dsz = torch.tensor([x.numel() for x in det_labels], device=dev, dtype=torch.long)
+    gsz = torch.tensor([x.numel() for x in gt_labels], device=dev, dtype=torch.long)
+    img_ids = torch.arange(n_img, device=dev)
+    d_img, g_img = torch.repeat_interleave(img_ids, dsz), torch.repeat_interleave(img_ids, gsz)
+    d_lab, g_lab = flat(det_labels, torch.long), flat(gt_labels, torch.long)
+    d_cls = torch.searchsorted(classes, d_lab).clamp(max=K - 1)
+    g_cls = torch.searchsorted(classes, g_lab).clamp(max=K - 1)
+    keep_d, keep_g = classes[d_cls] == d_lab, classes[g_cls] == g_lab
+    segm = det_masks is not None
+    if segm:
+        d_box = torch.zeros(d_lab.numel(), 4, dtype=torch.float64, device=dev)
+        g_box = torch.zeros(g_lab.numel(), 4, dtype=torch.float64, device=dev)
+        d_area = flat([m.flatten(1).sum(1) for m in det_masks], torch.float64)
+        g_mask_area = flat([m.flatten(1).sum(1) for m in gt_masks], torch.float64)
+    else:
+        d_box, g_box = flat(det_boxes, torch.float64, (4,)), flat(gt_boxes, torch.float64, (4,))
+        d_area = d_box[:, 2] * d_box[:, 3]
+        g_mask_area = g_box[:, 2] * g_box[:, 3]
+    d_score = flat(det_scores, torch.float64)
+    g_crowd = flat(gt_crowds, torch.long).clamp(0, 1).to(torch.uint8)
+    g_area_in = flat(gt_areas, torch.float64)
+    g_area = torch.where(g_area_in > 0, g_area_in, g_mask_area)
+    # drop annotations outside the category axis (micro averaging relabels everything to 0)
+    d_img, d_cls, d_box, d_area, d_score = (x[keep_d] for x in (d_img, d_cls, d_box, d_area, d_score))
+    g_img, g_cls, g_box, g_area, g_crowd = (x[keep_g] for x in (g_img, g_cls, g_box, g_area, g_crowd))
+
+    # (1) detections grouped by (image, category), score-descending (stable), truncated to max_dets[-1]
+    d_group = d_img * K + d_cls
+    order = torch.argsort(-d_score, stable=True)
+    order = order[torch.argsort(d_group[order], stable=True)]
+    grp_s = d_group[order]
+    rank = torch.arange(order.numel(), device=dev) - _segment_starts(grp_s)
+    keep = rank < max_dets[-1]
+    order, rank = order[keep], rank[keep]
+    grp_s = d_group[order]
+    g_group = g_img * K + g_cls
+    g_order = torch.argsort(g_group, stable=True)
+    n_groups = n_img * K
+    det_cnt = torch.bincount(grp_s, minlength=n_groups)
+    gt_cnt = torch.bincount(g_group[g_order], minlength=n_groups)
+    det_start = torch.cumsum(det_cnt, 0) - det_cnt
+    gt_start = torch.cumsum(gt_cnt, 0) - gt_cnt
+
+    # (2) greedy matching for every (group, area range, IoU threshold)
+    pre, off = None, None
+    if det_masks is not None:
+        pre, off = _mask_iou_blocks(det_masks, gt_masks, dsz, gsz, order, g_order, grp_s, det_start, gt_start,
+                                    gt_cnt, g_crowd, keep_d, keep_g)
+    dt_match, dt_ig = ops.coco_match(
+        d_box[order].contiguous(), d_area[order].contiguous(), g_box[g_order].contiguous(),
+        g_area[g_order].contiguous(), g_crowd[g_order].contiguous(), det_start.int(), det_cnt.int(),
+        gt_start.int(), gt_cnt.int(), areas.reshape(-1).contiguous(), t_thr, pre, off)
+
+    # (3) accumulate: detections of each category in score order (ties: image, then rank -- pycocotools mergesort)
+    cls_k = d_cls[order]
+    score_k = d_score[order]
+    o = torch.argsort(-score_k, stable=True)
+    o = o[torch.argsort(cls_k[o], stable=True)]
+    cls_s, rank_s, score_s = cls_k[o], rank[o], score_k[o]
+    match = dt_match[..., o].bool()
+    ig = dt_ig[..., o].bool()
+    tp_all, fp_all = match & ~ig, ~match & ~ig  # [T, A, D]
+    g_ig = (g_crowd.bool()[None, :] | (g_area[None, :] < areas[:, :1]) | (g_area[None, :] > areas[:, 1:]))  # [A, G]
+    npig = torch.zeros(A, K, dtype=torch.float64, device=dev)
+    npig.index_add_(1, g_cls, (~g_ig).to(torch.float64))  # [A, K]
+    has_gt = npig > 0
+    n = cls_s.numel()
+    if n:
+        seg_first = _segment_starts(cls_s)
+        is_last = torch.ones(n, dtype=torch.bool, device=dev)
+        is_last[:-1] = cls_s[1:] != cls_s[:-1]
+        seg_id = torch.cumsum((torch.arange(n, device=dev) == seg_first).long(), 0) - 1
+        n_seg = int(seg_id[-1].item()) + 1
+        npig_d = npig[:, cls_s].clamp(min=1)[None]  # [1, A, D]
+        eps = torch.finfo(torch.float64).eps
+        for mi, md in enumerate(max_dets):
+            incl = (rank_s < md)[None, None]
+            tp_c = torch.cumsum((tp_all & incl).to(torch.float64), -1)
+            fp_c = torch.cumsum((fp_all & incl).to(torch.float64), -1)
+            base_tp = torch.where(seg_first > 0, tp_c[..., (seg_first - 1).clamp(min=0)], torch.zeros_like(tp_c))
+            base_fp = torch.where(seg_first > 0, fp_c[..., (seg_first - 1).clamp(min=0)], torch.zeros_like(fp_c))
+            tp_c, fp_c = tp_c - base_tp, fp_c - base_fp
+            rc = tp_c / npig_d
+            pr = tp_c / (tp_c + fp_c + eps)
+            # precision envelope: running max from the end of each category segment
+            off = 2.0 * (n_seg - 1 - seg_id).to(torch.float64)
+            env = (pr.flip(-1) + off.flip(-1)).cummax(-1).values.flip(-1) - off
+            # recall thresholds in (rc of the previous included detection, rc] belong to this detection
+            inc = (rank_s < md).long()
+            inc_cs = torch.cumsum(inc, 0)
+            inc_before = inc_cs - inc - torch.where(seg_first > 0, inc_cs[(seg_first - 1).clamp(min=0)],
+                                                    torch.zeros_like(inc_cs))
+            prev_rc = torch.cat([torch.full_like(rc[..., :1], -1.0), rc[..., :-1]], -1)
+            prev_rc = torch.where(inc_before > 0, prev_rc, torch.full_like(rc, -1.0))
+            lo = torch.searchsorted(r_thr, prev_rc.reshape(-1, n).contiguous(), right=True).reshape(rc.shape)
+            hi = torch.searchsorted(r_thr, rc.reshape(-1, n).contiguous(), right=True).reshape(rc.shape)
+            nonempty = (hi > lo) & (inc > 0)
+            # first recall threshold index of every non-empty range -> detection index, filled forward along R
+            mark = torch.full((T, A, K, R + 1), -1, dtype=torch.long, device=dev)
+            ti, ai, di = torch.nonzero(nonempty, as_tuple=True)
+            mark.index_put_((ti, ai, cls_s[di], lo[ti, ai, di]), di, accumulate=False)
+            mark = mark[..., :R].cummax(-1).values
+            # thresholds beyond the last recall of the category get no detection
+            last_idx = torch.nonzero(is_last).flatten()
+            hi_last = torch.zeros(T, A, K, dtype=torch.long, device=dev)
+            hi_last[..., cls_s[last_idx]] = hi[..., last_idx]
+            valid = (mark >= 0) & (torch.arange(R, device=dev) < hi_last[..., None])
+            safe = mark.clamp(min=0)
+            q = torch.where(valid, torch.gather(env, -1, safe.reshape(T, A, -1)).reshape(T, A, K, R),
+                            torch.zeros((), dtype=torch.float64, device=dev))
+            ss = torch.where(valid, score_s[safe], torch.zeros((), dtype=torch.float64, device=dev))
+            rec = torch.zeros(T, A, K, dtype=torch.float64, device=dev)
+            rec[..., cls_s[last_idx]] = rc[..., last_idx]
+            precision[..., mi] = q.permute(0, 3, 2, 1)
+            scores_out[..., mi] = ss.permute(0, 3, 2, 1)
+            recall[..., mi] = rec.permute(0, 2, 1)
+    else:
+        precision.zero_()
+        scores_out.zero_()
+        recall.zero_()
+    # categories without any non-ignored ground truth stay at -1 (pycocotools skips them)
+    missing = ~has_gt.T  # [K, A]
+    precision.masked_fill_(missing[None, None, :, :, None], -1.0)
+    scores_out.masked_fill_(missing[None, None, :, :, None], -1.0)
+    recall.masked_fill_(missing[None, :, :, None], -1.0)
+    return {"precision": precision, "recall": recall, "scores": scores_out}
+
+
+def _masked_mean(s: Tensor) -> Tensor:
+    valid = s > -1
+    cnt = valid.sum()
+    return torch.where(cnt > 0, (s * valid).sum() / cnt.clamp(min=1), torch.tensor(-1.0, dtype=s.dtype,
+                                                                                 device=s.device))
+
+
+def coco_summarize(ev: Dict[str, Tensor], iou_thresholds: Sequence[float], max_dets: Sequence[int]) -> Tensor:
+    """The 12 COCO summary numbers (``COCOeval.summarize``) as a float64 device tensor."""
+    prec, rec = ev["precision"], ev["recall"]
+    thr = list(iou_thresholds)
+
+    def ap(iou=None, area=0, m=len(max_dets) - 1):
+        s = prec[..., area, m]
+        if iou is not None:
+            idx = [i for i, t in enumerate(thr) if t == iou]
+            s = s[idx]
+        return _masked_mean(s)
+
+    def ar(area=0, m=len(max_dets) - 1):
+        return _masked_mean(rec[..., area, m])
+
+    stats = [ap(), ap(0.5), ap(0.75), ap(area=1), ap(area=2), ap(area=3), ar(m=0), ar(m=1), ar(m=2),
+             ar(area=1), ar(area=2), ar(area=3)]
+    return torch.stack(stats)
+
+
+def per_class_stats(ev: Dict[str, Tensor]) -> Tuple[Tensor, Tensor]:
+    """Per-category mAP (all areas, last max-dets) and mAR at the last max-dets, -1 where undefined."""
+    prec = ev["precision"][..., 0, -1]  # [T, R, K]
+    rec = ev["recall"][..., 0, -1]  # [T, K]
+    pv, rv = prec > -1, rec > -1
+    p_cnt, r_cnt = pv.sum((0, 1)), rv.sum(0)
+    mp = torch.where(p_cnt > 0, (prec * pv).sum((0, 1)) / p_cnt.clamp(min=1), torch.full_like(p_cnt, -1.0,
+                                                                                                dtype=prec.dtype))
+    mr = torch.where(r_cnt > 0, (rec * rv).sum(0) / r_cnt.clamp(min=1), torch.full_like(r_cnt, -1.0,
+                                                                                        dtype=rec.dtype))
+    return mp, mr
+
+
+def _mask_iou_blocks(det_masks, gt_masks, dsz, gsz, order, g_order, grp_s, det_start, gt_start, gt_cnt, g_crowd,
+                     keep_d, keep_g) -> Tuple[Tensor, Tensor]:
+    """Per-group ``[det, gt]`` mask-IoU blocks laid out for ``coco_match`` (crowd gt: intersection / det area).
+
+    Each image's full IoU matrix is one GEMM of the flattened binary masks (exact fp32 pixel counts).
+    """
+    dev = grp_s.device
+    mats, offs = [], [0]
+    for dm, gm in zip(det_masks, gt_masks):
+        nd, ng = dm.shape[0], gm.shape[0]
+        if nd and ng:
+            a = dm.reshape(nd, -1).to(device=dev, dtype=torch.float32)
+            b = gm.reshape(ng, -1).to(device=dev, dtype=torch.float32)
+            inter = (a @ b.T).double()
+            da, ga = a.sum(1).double(), b.sum(1).double()
+            mats.append((inter, da, ga))
+        else:
+            mats.append(None)
+        offs.append(offs[-1] + nd * ng)
+    # crowd flags in original (unfiltered) gt order
+    crowd_full = torch.zeros(int(gsz.sum().item()), dtype=torch.bool, device=dev)
+    crowd_full[torch.nonzero(keep_g).flatten()] = g_crowd.bool()
+    g_base = torch.cumsum(gsz, 0) - gsz
+    flat_iou = torch.zeros(max(offs[-1], 1), dtype=torch.float64, device=dev)
+    for i, m in enumerate(mats):
+        if m is None:
+            continue
+        inter, da, ga = m
+        crowd = crowd_full[g_base[i]: g_base[i] + ga.numel()]
+        union = torch.where(crowd[None, :], da[:, None], da[:, None] + ga[None, :] - inter)
+        iou = torch.where(union > 0, inter / union.clamp(min=1e-12), torch.zeros_like(inter))
+        flat_iou[offs[i]: offs[i + 1]] = iou.flatten()
+    img_off = torch.tensor(offs[:-1], dtype=torch.long, device=dev)
+    d_orig = torch.nonzero(keep_d).flatten()[order]  # flat (unfiltered) index of each sorted detection
+    g_orig = torch.nonzero(keep_g).flatten()[g_order]
+    d_img = torch.repeat_interleave(torch.arange(gsz.numel(), device=dev), dsz)[d_orig]
+    d_base = torch.cumsum(dsz, 0) - dsz
+    d_loc = d_orig - d_base[d_img]
+    g_img_all = torch.repeat_interleave(torch.arange(gsz.numel(), device=dev), gsz)
+    g_loc_sorted = g_orig - g_base[g_img_all[g_orig]]
+    # block of group g starts at iou_off[g]; row k (k-th det of the group) holds gt_cnt[g] values
+    reps = gt_cnt[grp_s]
+    block_rows = torch.repeat_interleave(torch.arange(grp_s.numel(), device=dev), reps)
+    col = torch.arange(block_rows.numel(), device=dev) - torch.repeat_interleave(torch.cumsum(reps, 0) - reps, reps)
+    gsorted_idx = gt_start[grp_s[block_rows]] + col
+    ng_img = gsz[d_img[block_rows]]
+    vals = flat_iou[img_off[d_img[block_rows]] + d_loc[block_rows] * ng_img + g_loc_sorted[gsorted_idx]]
+    det_cnt = torch.bincount(grp_s, minlength=gt_cnt.numel())
+    sizes = det_cnt * gt_cnt
+    iou_off = torch.cumsum(sizes, 0) - sizes
+    return vals.contiguous(), iou_off.contiguous()

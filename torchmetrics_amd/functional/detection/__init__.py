@@ -1,0 +1,9 @@
+"""Functional detection metrics (parity: reference ``F/detection/__init__.py``)."""
+from torchmetrics_amd.functional.detection.iou import (
+    complete_intersection_over_union,
+    distance_intersection_over_union,
+    generalized_intersection_over_union,
+    intersection_over_union,
+)
+
+__all__ = [k for k in dir() if not k.startswith("_")]

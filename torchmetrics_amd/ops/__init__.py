@@ -235,3 +235,30 @@ def ssim2d_partials(x: Tensor, y: Tensor, wh: Tensor, ww: Tensor, c12: Tensor, m
         return _ops().ssim2d_partials(x.contiguous(), y.contiguous(), wh.to(acc).contiguous(),
                                       ww.to(acc).contiguous(), c12.to(device=x.device, dtype=acc).contiguous(), mode)
     return _cpu.ssim2d_partials(x, y, wh, ww, c12, mode)
+
+
+# ------------------------------------------------------------------------------------------------------- detection
+BOX_IOU, BOX_GIOU, BOX_DIOU, BOX_CIOU = range(4)
+
+
+def box_pairwise(a: Tensor, b: Tensor, op: int = BOX_IOU, aligned: bool = False) -> Tensor:
+    """IoU-family matrix ``[N, M]`` (or ``[N]`` for aligned pairs) of xyxy boxes (``csrc/detection/box_ops.hip``)."""
+    if a.is_cuda:
+        dt = a.dtype if a.dtype in (torch.float32, torch.float16, torch.bfloat16, torch.float64) else torch.float32
+        return _ops().box_pairwise(a.to(dt).contiguous(), b.to(dt).contiguous(), op, aligned)
+    return _cpu.box_pairwise(a, b, op, aligned)
+
+
+def coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, gt_cnt, area_rng, iou_thr,
+               iou_pre=None, iou_off=None):
+    """COCO greedy matching of every (image x class group, area range, IoU threshold); returns ``(dt_match, dt_ig)``
+    uint8 ``[T, A, D]``.  Detections must be grouped and score-sorted, ground truths grouped in annotation order.
+
+    ``iou_pre`` / ``iou_off`` optionally give precomputed per-group IoU blocks (``[det_cnt, gt_cnt]`` row-major at
+    ``iou_off[group]``), e.g. mask IoUs for ``iou_type="segm"``; otherwise COCO box IoU is computed from ``dbox``.
+    """
+    if dbox.is_cuda:
+        return _ops().coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, gt_cnt, area_rng,
+                                 iou_thr, iou_pre, iou_off)
+    return _cpu.coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, gt_cnt, area_rng, iou_thr,
+                           iou_pre, iou_off)

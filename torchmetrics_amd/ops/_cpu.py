@@ -282,3 +282,95 @@ def ssim2d_partials(x: Tensor, y: Tensor, wh: Tensor, ww: Tensor, c12: Tensor, m
         val = ((2 * mxy) * upper) / ((mxx + myy) * lower + eps)
         cs = torch.zeros_like(val)
     return torch.stack([val.flatten(1).sum(1), cs.flatten(1).sum(1)], -1).unsqueeze(1)
+
+
+def box_pairwise(a: Tensor, b: Tensor, op: int, aligned: bool) -> Tensor:
+    acc = torch.float64 if a.dtype == torch.float64 else torch.float32
+    out_dtype = a.dtype if a.is_floating_point() else torch.float32
+    a, b = a.to(acc), b.to(acc)
+    if aligned:
+        pa, pb = a, b
+    else:
+        pa, pb = a[:, None, :], b[None, :, :]
+    area_a = (pa[..., 2] - pa[..., 0]) * (pa[..., 3] - pa[..., 1])
+    area_b = (pb[..., 2] - pb[..., 0]) * (pb[..., 3] - pb[..., 1])
+    iw = (torch.minimum(pa[..., 2], pb[..., 2]) - torch.maximum(pa[..., 0], pb[..., 0])).clamp(min=0)
+    ih = (torch.minimum(pa[..., 3], pb[..., 3]) - torch.maximum(pa[..., 1], pb[..., 1])).clamp(min=0)
+    inter = iw * ih
+    union = area_a + area_b - inter
+    iou = inter / union
+    if op == 0:
+        return iou.to(out_dtype)
+    cw = torch.maximum(pa[..., 2], pb[..., 2]) - torch.minimum(pa[..., 0], pb[..., 0])
+    ch = torch.maximum(pa[..., 3], pb[..., 3]) - torch.minimum(pa[..., 1], pb[..., 1])
+    if op == 1:
+        area_c = cw * ch
+        return (iou - (area_c - union) / area_c).to(out_dtype)
+    eps = 1e-7
+    diag = cw**2 + ch**2 + eps
+    dx = (pa[..., 0] + pa[..., 2]) / 2 - (pb[..., 0] + pb[..., 2]) / 2
+    dy = (pa[..., 1] + pa[..., 3]) / 2 - (pb[..., 1] + pb[..., 3]) / 2
+    diou = iou - (dx**2 + dy**2) / diag
+    if op == 2:
+        return diou.to(out_dtype)
+    wa, ha = pa[..., 2] - pa[..., 0], pa[..., 3] - pa[..., 1]
+    wb, hb = pb[..., 2] - pb[..., 0], pb[..., 3] - pb[..., 1]
+    v = (4 / (torch.pi**2)) * (torch.atan(wb / hb) - torch.atan(wa / ha)) ** 2
+    alpha = v / (1 - iou + v + eps)
+    return (diou - alpha * v).to(out_dtype)
+
+
+def _coco_iou(d, g, crowd):
+    w = min(d[0] + d[2], g[0] + g[2]) - max(d[0], g[0])
+    if w <= 0:
+        return 0.0
+    h = min(d[1] + d[3], g[1] + g[3]) - max(d[1], g[1])
+    if h <= 0:
+        return 0.0
+    inter = w * h
+    da = d[2] * d[3]
+    return inter / (da if crowd else da + g[2] * g[3] - inter)
+
+
+def coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, gt_cnt, area_rng, iou_thr,
+               iou_pre=None, iou_off=None):
+    """Host reference of ``coco_match_kernel`` (same greedy COCO semantics, plain loops)."""
+    t_n, a_n, d_n = iou_thr.numel(), area_rng.numel() // 2, dbox.shape[0]
+    dt_match = torch.zeros(t_n, a_n, d_n, dtype=torch.uint8)
+    dt_ig = torch.zeros(t_n, a_n, d_n, dtype=torch.uint8)
+    db, da, gb, ga, gc = dbox.tolist(), darea.tolist(), gbox.tolist(), garea.tolist(), gcrowd.tolist()
+    rng = area_rng.reshape(-1, 2).tolist()
+    thrs = iou_thr.tolist()
+    pre = iou_pre.tolist() if iou_pre is not None else None
+    offs = iou_off.tolist() if iou_off is not None else None
+    for grp, (d0, dn, g0, gn) in enumerate(zip(det_start.tolist(), det_cnt.tolist(), gt_start.tolist(),
+                                              gt_cnt.tolist())):
+        if dn == 0:
+            continue
+        if pre is not None:
+            ious = [[pre[offs[grp] + k * gn + j] for j in range(gn)] for k in range(dn)]
+        else:
+            ious = [[_coco_iou(db[d0 + k], gb[g0 + j], gc[g0 + j] != 0) for j in range(gn)] for k in range(dn)]
+        for a, (lo, hi) in enumerate(rng):
+            ig = [gc[g0 + j] != 0 or ga[g0 + j] < lo or ga[g0 + j] > hi for j in range(gn)]
+            order = [j for j in range(gn) if not ig[j]] + [j for j in range(gn) if ig[j]]
+            for t, thr in enumerate(thrs):
+                used = [False] * gn
+                for k in range(dn):
+                    best, m = min(thr, 1 - 1e-10), -1
+                    for j in order:
+                        if used[j] and not gc[g0 + j]:
+                            continue
+                        if m > -1 and not ig[m] and ig[j]:
+                            break
+                        if ious[k][j] < best:
+                            continue
+                        best, m = ious[k][j], j
+                    di = d0 + k
+                    if m >= 0:
+                        used[m] = True
+                        dt_match[t, a, di] = 1
+                        dt_ig[t, a, di] = int(ig[m])
+                    else:
+                        dt_ig[t, a, di] = int(da[di] < lo or da[di] > hi)
+    return dt_match, dt_ig

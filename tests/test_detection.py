@@ -220,3 +220,86 @@ def _ddp_map(rank, world, preds, target):
 def test_map_ddp():
     preds, target = _random_coco(11, n_img=8)
     run_ddp(_ddp_map, preds, target)
+
+
+# ------------------------------------------------------------------------------------------------ panoptic quality
+def _pq_oracle(preds, target, things, stuffs, modified=False):
+    """Dict-based per-sample segment matching, straight from the panoptic-quality definition."""
+    things, stuffs = set(things), set(stuffs)
+    void = (1 + max([0, *things, *stuffs]), 0)
+    cats = {c: i for i, c in enumerate(things)}
+    cats.update({c: i + len(things) for i, c in enumerate(stuffs)})
+    k = len(cats)
+    iou_sum, tp, fp, fn = np.zeros(k), np.zeros(k), np.zeros(k), np.zeros(k)
+
+    def prep(x):
+        out = []
+        for c, i in x.reshape(x.shape[0], -1, 2).tolist()[0] if False else []:
+            pass
+        return out
+
+    for pb, tb in zip(preds, target):
+        def colors(x):
+            cols = []
+            for c, i in x.reshape(-1, 2).tolist():
+                if c in stuffs:
+                    cols.append((c, 0))
+                elif c in things:
+                    cols.append((c, i))
+                else:
+                    cols.append(void)
+            return cols
+
+        pc, tc = colors(pb), colors(tb)
+        from collections import Counter
+
+        pa, ta, inter = Counter(pc), Counter(tc), Counter(zip(pc, tc))
+        pm, tm = set(), set()
+        for (p, t), a in inter.items():
+            if t == void or p[0] != t[0]:
+                continue
+            union = pa[p] - inter.get((p, void), 0) + ta[t] - inter.get((void, t), 0) - a
+            iou = a / union
+            ci = cats[t[0]]
+            if (t[0] not in stuffs or not modified) and iou > 0.5:
+                pm.add(p)
+                tm.add(t)
+                iou_sum[ci] += iou
+                tp[ci] += 1
+            elif modified and t[0] in stuffs and iou > 0:
+                iou_sum[ci] += iou
+        for t in set(ta) - tm - {void}:
+            if inter.get((void, t), 0) / ta[t] <= 0.5 and not (modified and t[0] in stuffs):
+                fn[cats[t[0]]] += 1
+        for p in set(pa) - pm - {void}:
+            if inter.get((p, void), 0) / pa[p] <= 0.5 and not (modified and p[0] in stuffs):
+                fp[cats[p[0]]] += 1
+        if modified:
+            for t in ta:
+                if t[0] in stuffs:
+                    tp[cats[t[0]]] += 1
+    den = tp + 0.5 * fp + 0.5 * fn
+    return np.mean(iou_sum[den > 0] / den[den > 0])
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("modified", [False, True])
+def test_panoptic_quality(device, modified):
+    from torchmetrics_amd.detection import ModifiedPanopticQuality, PanopticQuality
+
+    g = torch.Generator().manual_seed(3 + modified)
+    things, stuffs = [0, 1, 3], [6, 7]
+    # blocky segmentations so segments overlap substantially
+    cat = torch.tensor([0, 1, 3, 6, 7, 9])[torch.randint(0, 6, (3, 8, 8), generator=g)]
+    cat = cat.repeat_interleave(4, 1).repeat_interleave(4, 2)
+    inst = torch.randint(0, 3, (3, 32, 32), generator=g)
+    target = torch.stack([cat, inst], -1)
+    preds = target.clone()
+    noise = torch.rand(3, 32, 32, generator=g) < 0.25
+    preds[..., 0] = torch.where(noise, torch.tensor([0, 1, 3, 6, 7])[torch.randint(0, 5, (3, 32, 32), generator=g)],
+                                preds[..., 0])
+    cls = ModifiedPanopticQuality if modified else PanopticQuality
+    m = cls(things=things, stuffs=stuffs, allow_unknown_preds_category=True).to(device)
+    m.update(preds[:2].to(device), target[:2].to(device))
+    m.update(preds[2:].to(device), target[2:].to(device))
+    assert_close(m.compute(), _pq_oracle(preds, target, things, stuffs, modified), atol=1e-9)

@@ -5,3 +5,4 @@ from torchmetrics_amd.functional.retrieval import *  # noqa: F401,F403
 from torchmetrics_amd.functional.image import *  # noqa: F401,F403
 from torchmetrics_amd.functional.detection import *  # noqa: F401,F403
 from torchmetrics_amd.functional.clustering import *  # noqa: F401,F403
+from torchmetrics_amd.functional.nominal import *  # noqa: F401,F403

@@ -137,6 +137,10 @@ def histogram(x: Tensor, minlength: int) -> Tensor:
         x = x if x.dtype in (torch.int64, torch.int32, torch.uint8) else x.long()
         _ops().histogram(x.contiguous(), out, flag)
         return out
+    x = x.long()
+    ok = (x >= 0) & (x < minlength)
+    if not bool(ok.all()):  # out-of-range keys are skipped, as in the kernel
+        x = x[ok]
     return torch.bincount(x, minlength=minlength)
 
 

@@ -47,7 +47,7 @@ class _NominalMetric(Metric):
         self.add_state("confmat", torch.zeros(num_classes, num_classes), dist_reduce_fx="sum")
 
     def update(self, preds: Tensor, target: Tensor) -> None:
-        flag = self._device_error_buffer(preds.device) if preds.is_cuda and self.validate_args else None
+        flag = self._device_error_buffer(preds.device) if preds.is_cuda else None
         cm = _nominal_confmat(preds, target, self.num_classes, self.nan_strategy, self.nan_replace_value, flag)
         self.confmat += cm.to(self.confmat.dtype)
 

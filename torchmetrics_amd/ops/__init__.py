@@ -266,3 +266,32 @@ def coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, g
                                  iou_thr, iou_pre, iou_off)
     return _cpu.coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, gt_cnt, area_rng, iou_thr,
                            iou_pre, iou_off)
+
+
+# -------------------------------------------------------------------------------------------------------- pairwise
+# metric ids of csrc/pairwise/pairwise.hip
+PW_L1, PW_L2, PW_LP, PW_LP_INT = range(4)
+_PW_TILE = 64
+
+
+def pairwise_distance(x: Tensor, y: Tensor, metric: int, p: float = 2.0, zero_diagonal: bool = False,
+                      reduction: Optional[str] = None) -> Tensor:
+    """``[N, M]`` L1 / L2 / Lp distance matrix (or its row ``sum`` / ``mean`` ``[N]``) in the input's dtype; the
+    HIP kernel fuses root, ``zero_diagonal`` and the row reduction (``csrc/pairwise/pairwise.hip``)."""
+    if not x.is_cuda:
+        return _cpu.pairwise_distance(x, y, metric, p, zero_diagonal, reduction)
+    if x.dtype not in (torch.float32, torch.float16, torch.bfloat16, torch.float64):
+        x, y = x.float(), y.float()
+    x, y = x.contiguous(), y.to(x.dtype).contiguous()
+    acc = torch.float64 if x.dtype == torch.float64 else torch.float32
+    if metric == PW_LP and float(p).is_integer() and 3 <= p <= 15:
+        metric = PW_LP_INT
+    n, m = x.shape[0], y.shape[0]
+    reduce = reduction in ("sum", "mean")
+    out = torch.empty(n, -(-m // _PW_TILE) if reduce else m, dtype=acc, device=x.device)
+    _ops().pairwise_distance(x, y, out, int(metric), float(p), bool(zero_diagonal), reduce)
+    if reduce:
+        out = out.sum(1)
+        if reduction == "mean":
+            out = out / m
+    return out.to(x.dtype)

@@ -374,3 +374,19 @@ def coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, g
                     else:
                         dt_ig[t, a, di] = int(da[di] < lo or da[di] > hi)
     return dt_match, dt_ig
+
+
+def pairwise_distance(x: Tensor, y: Tensor, metric: int, p: float, zero_diagonal: bool,
+                      reduction: Optional[str]) -> Tensor:
+    """Difference-form distances in fp64 (no norm-expansion cancellation), cast back to the input dtype."""
+    dt = x.dtype if x.is_floating_point() else torch.float32
+    pp = 1.0 if metric == 0 else (2.0 if metric == 1 else float(p))  # 2 = Lp, 3 = integer Lp
+    dist = torch.cdist(x.double(), y.double(), p=pp, compute_mode="donot_use_mm_for_euclid_dist")
+    if zero_diagonal:
+        k = min(dist.shape)
+        dist[torch.arange(k), torch.arange(k)] = 0
+    if reduction == "sum":
+        dist = dist.sum(-1)
+    elif reduction == "mean":
+        dist = dist.mean(-1)
+    return dist.to(dt)

@@ -7,3 +7,4 @@ from torchmetrics_amd.functional.detection import *  # noqa: F401,F403
 from torchmetrics_amd.functional.clustering import *  # noqa: F401,F403
 from torchmetrics_amd.functional.nominal import *  # noqa: F401,F403
 from torchmetrics_amd.functional.pairwise import *  # noqa: F401,F403
+from torchmetrics_amd.functional.text import *  # noqa: F401,F403

@@ -295,3 +295,72 @@ def pairwise_distance(x: Tensor, y: Tensor, metric: int, p: float = 2.0, zero_di
         if reduction == "mean":
             out = out / m
     return out.to(x.dtype)
+
+
+# ------------------------------------------------------------------------------------------------------------ text
+def levenshtein(pred: Tensor, poff: Tensor, ref: Tensor, roff: Tensor, ins: int = 1, dele: int = 1, sub: int = 1,
+                use_beam: bool = False, max_ref_len: Optional[int] = None) -> Tensor:
+    """Batched edit distances ``[B]`` (int64) of int32 token-id sequences packed with int64 offsets
+    (``csrc/text/levenshtein.hip``).  ROCm tensors run the wave-per-pair LDS kernel; CPU tensors run the native
+    multithreaded host DP when the library is loaded, else the Python DP of :mod:`ops._cpu`."""
+    out = torch.empty(poff.numel() - 1, dtype=torch.int64, device=pred.device)
+    if max_ref_len is None:
+        max_ref_len = int((roff[1:] - roff[:-1]).max().item()) if roff.numel() > 1 else 0
+    args = (pred.int().contiguous(), poff.long().contiguous(), ref.int().contiguous(), roff.long().contiguous(), out,
+            int(ins), int(dele), int(sub), bool(use_beam), int(max_ref_len))
+    if pred.is_cuda or native_available():
+        _ops().levenshtein(*args)
+        return out
+    _cpu.levenshtein(*args)
+    return out
+
+
+def eed_scores(hyps, refs, alpha: float, rho: float, deletion: float, insertion: float):
+    """Extended edit distance of each (hypothesis, reference) string pair (native host DP, ``csrc/text/eed_host.cpp``)."""
+    import numpy as np
+
+    def pack(strs):
+        arrs = [np.frombuffer(s.encode("utf-32-le"), dtype=np.uint32).astype(np.int32) for s in strs]
+        off = np.zeros(len(arrs) + 1, dtype=np.int64)
+        np.cumsum([len(a) for a in arrs], out=off[1:])
+        ids = np.concatenate(arrs) if off[-1] else np.zeros(0, dtype=np.int32)
+        return torch.from_numpy(ids), torch.from_numpy(off)
+
+    h, ho = pack(hyps)
+    r, ro = pack(refs)
+    return _ops().eed_scores(h, ho, r, ro, float(alpha), float(rho), float(deletion), float(insertion)).tolist()
+
+
+class _TokenNLL(torch.autograd.Function):
+    """Autograd wrapper: forward = fused kernel (nll + per-row logsumexp), backward = (softmax - onehot) * g."""
+
+    @staticmethod
+    def forward(ctx, logits, target, ignore_index, flag):  # noqa: D102
+        acc = torch.float64 if logits.dtype == torch.float64 else torch.float32
+        nll = torch.empty(logits.shape[0], dtype=torch.float32, device=logits.device)
+        lse = torch.empty(logits.shape[0], dtype=acc, device=logits.device)
+        _ops().token_nll(logits, target, nll, lse, flag, 0 if ignore_index is None else int(ignore_index),
+                         ignore_index is not None)
+        ctx.save_for_backward(logits, target, lse)
+        ctx.ignore_index = ignore_index
+        return nll
+
+    @staticmethod
+    def backward(ctx, g):  # noqa: D102
+        logits, target, lse = ctx.saved_tensors
+        keep = torch.ones_like(target, dtype=torch.bool) if ctx.ignore_index is None else target != ctx.ignore_index
+        gs = (g.to(lse.dtype) * keep)[:, None]
+        grad = torch.exp(logits.to(lse.dtype) - lse[:, None]) * gs
+        grad.scatter_add_(1, torch.where(keep, target, torch.zeros_like(target))[:, None], -gs)
+        return grad.to(logits.dtype), None, None, None
+
+
+def token_nll(logits: Tensor, target: Tensor, ignore_index: Optional[int], flag: Optional[Tensor] = None) -> Tensor:
+    """Per-row ``-log softmax(logits)[target]`` (``[rows]`` fp32, 0 for ignored rows) -- fused single-pass HIP
+    kernel on ROCm (``csrc/text/perplexity.hip``, differentiable via :class:`_TokenNLL`), fp32 ``log_softmax`` +
+    gather on the host."""
+    if logits.is_cuda:
+        if flag is None:
+            flag = torch.zeros(1, dtype=torch.int32, device=logits.device)
+        return _TokenNLL.apply(logits.contiguous(), target.long().contiguous(), ignore_index, flag)
+    return _cpu.token_nll(logits, target, ignore_index)

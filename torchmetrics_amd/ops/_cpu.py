@@ -390,3 +390,47 @@ def pairwise_distance(x: Tensor, y: Tensor, metric: int, p: float, zero_diagonal
     elif reduction == "mean":
         dist = dist.mean(-1)
     return dist.to(dt)
+
+
+def levenshtein(pred, poff, ref, roff, out, ins, dele, sub, use_beam, max_ref_len) -> None:
+    """Python DP with the same (optional tercom-beam) semantics as ``csrc/text/levenshtein.hip``."""
+    import math
+
+    inf = 1 << 28
+    p_all, r_all = pred.tolist(), ref.tolist()
+    po, ro = poff.tolist(), roff.tolist()
+    for b in range(len(po) - 1):
+        p, r = p_all[po[b]:po[b + 1]], r_all[ro[b]:ro[b + 1]]
+        plen, rlen = len(p), len(r)
+        ratio = rlen / plen if plen else 1.0
+        width = math.ceil(ratio / 2 + 25) if ratio / 2 > 25 else 25
+        prev = [j * ins for j in range(rlen + 1)]
+        for i in range(1, plen + 1):
+            lo, hi = 0, rlen + 1
+            if use_beam:
+                diag = math.floor(i * ratio)
+                lo = max(0, diag - width)
+                hi = rlen + 1 if i == plen else min(rlen + 1, diag + width)
+            cur = [inf] * (rlen + 1)
+            tok = p[i - 1]
+            for j in range(lo, hi):
+                v = prev[j] + dele if prev[j] < inf else inf
+                if j > 0:
+                    if prev[j - 1] < inf:
+                        v = min(v, prev[j - 1] + (0 if r[j - 1] == tok else sub))
+                    if cur[j - 1] < inf:
+                        v = min(v, cur[j - 1] + ins)
+                cur[j] = v
+            prev = cur
+        out[b] = prev[rlen]
+
+
+def token_nll(logits: Tensor, target: Tensor, ignore_index: Optional[int]) -> Tensor:
+    acc = torch.float64 if logits.dtype == torch.float64 else torch.float32
+    t = target.long()
+    mask = torch.ones_like(t, dtype=torch.bool) if ignore_index is None else t != ignore_index
+    safe = torch.where(mask, t, torch.zeros_like(t))
+    if bool(((safe < 0) | (safe >= logits.shape[1])).any()):
+        raise IndexError("Perplexity: target index out of range of the vocabulary")
+    lp = torch.log_softmax(logits.to(acc), dim=1).gather(1, safe[:, None])[:, 0]
+    return torch.where(mask, -lp, torch.zeros_like(lp)).float()

@@ -31,3 +31,11 @@ __all__ = [
     "word_information_lost",
     "word_information_preserved",
 ]
+
+from torchmetrics_amd.utilities.imports import _TRANSFORMERS_AVAILABLE  # noqa: E402
+
+if _TRANSFORMERS_AVAILABLE:
+    from torchmetrics_amd.functional.text.bert import bert_score  # noqa: F401
+    from torchmetrics_amd.functional.text.infolm import infolm  # noqa: F401
+
+    __all__ += ["bert_score", "infolm"]

@@ -1,0 +1,184 @@
+"""Audio metrics (reference ``tests/unittests/audio``).  mir_eval / fast_bss_eval / pesq / pystoi are not installed:
+SNR-family values are pinned to the reference docstrings, SDR to a direct numpy least-squares oracle of the
+distortion-filter projection and to the reference docstring values."""
+import numpy as np
+import pytest
+import torch
+
+from torchmetrics_amd import ops
+from torchmetrics_amd.audio import (
+    ComplexScaleInvariantSignalNoiseRatio,
+    PerceptualEvaluationSpeechQuality,
+    PermutationInvariantTraining,
+    ScaleInvariantSignalDistortionRatio,
+    ScaleInvariantSignalNoiseRatio,
+    ShortTimeObjectiveIntelligibility,
+    SignalDistortionRatio,
+    SignalNoiseRatio,
+    SourceAggregatedSignalDistortionRatio,
+)
+from torchmetrics_amd.functional.audio import (
+    complex_scale_invariant_signal_noise_ratio,
+    permutation_invariant_training,
+    pit_permutate,
+    scale_invariant_signal_distortion_ratio,
+    scale_invariant_signal_noise_ratio,
+    signal_distortion_ratio,
+    signal_noise_ratio,
+    source_aggregated_signal_distortion_ratio,
+)
+
+T = torch.tensor([3.0, -0.5, 2.0, 7.0])
+P = torch.tensor([2.5, 0.0, 2.0, 8.0])
+
+
+def test_docstring_values():
+    assert torch.isclose(signal_noise_ratio(P, T), torch.tensor(16.1805), atol=1e-4)
+    assert torch.isclose(scale_invariant_signal_noise_ratio(P, T), torch.tensor(15.0918), atol=1e-4)
+    assert torch.isclose(scale_invariant_signal_distortion_ratio(P, T), torch.tensor(18.4030), atol=1e-4)
+    torch.manual_seed(1)
+    p, t = torch.randn((1, 257, 100, 2)), torch.randn((1, 257, 100, 2))
+    assert torch.isclose(complex_scale_invariant_signal_noise_ratio(p, t), torch.tensor([-63.4849]), atol=1e-3)
+    torch.manual_seed(1)
+    p, t = torch.randn(8000), torch.randn(8000)
+    assert torch.isclose(signal_distortion_ratio(p, t), torch.tensor(-12.0589), atol=1e-3)
+    p, t = torch.randn(4, 2, 8000), torch.randn(4, 2, 8000)
+    best, perm = permutation_invariant_training(p, t, signal_distortion_ratio)
+    assert torch.allclose(best, torch.tensor([-11.6375, -11.4358, -11.7148, -11.6325]), atol=1e-3)
+    assert perm.tolist() == [[1, 0], [0, 1], [1, 0], [0, 1]]
+    torch.manual_seed(1)
+    p, t = torch.randn(2, 8000), torch.randn(2, 8000)
+    assert torch.isclose(source_aggregated_signal_distortion_ratio(p, t), torch.tensor(-41.6579), atol=1e-3)
+    p, t = torch.randn(4, 2, 8000), torch.randn(4, 2, 8000)
+    best, perm = permutation_invariant_training(p, t, source_aggregated_signal_distortion_ratio,
+                                                mode="permutation-wise")
+    assert torch.allclose(best, torch.tensor([-37.9511, -41.9124, -42.7369, -42.5155]), atol=1e-3)
+    assert perm.tolist() == [[1, 0], [1, 0], [0, 1], [1, 0]]
+    p = torch.tensor([[[-0.0579, 0.3560, -0.9604], [-0.1719, 0.3205, 0.2951]]])
+    t = torch.tensor([[[1.0958, -0.1648, 0.5228], [-0.4100, 1.1942, -0.5103]]])
+    best, perm = permutation_invariant_training(p, t, scale_invariant_signal_distortion_ratio,
+                                                mode="speaker-wise", eval_func="max")
+    assert torch.allclose(best, torch.tensor([-5.1091]), atol=1e-4) and perm.tolist() == [[0, 1]]
+    assert torch.equal(pit_permutate(p, perm), p)
+
+
+def _sdr_oracle(p, t, L=512):
+    """Project normalised preds onto the span of L shifts of the normalised target (dense least squares)."""
+    p = np.asarray(p, dtype=np.float64)
+    t = np.asarray(t, dtype=np.float64)
+    t = t / max(np.linalg.norm(t), 1e-6)
+    p = p / max(np.linalg.norm(p), 1e-6)
+    n = len(t)
+    A = np.zeros((n + L - 1, L))
+    for k in range(L):
+        A[k:k + n, k] = t
+    pp = np.concatenate([p, np.zeros(L - 1)])
+    h, *_ = np.linalg.lstsq(A, pp, rcond=None)
+    proj = A @ h
+    coh = proj @ pp
+    return 10 * np.log10(coh / (1 - coh))
+
+
+def test_sdr_oracle_and_toeplitz():
+    g = torch.Generator().manual_seed(3)
+    t = torch.randn(3, 1000, generator=g)
+    p = t + 0.5 * torch.randn(3, 1000, generator=g)
+    got = signal_distortion_ratio(p, t, filter_length=64)
+    ref = [_sdr_oracle(p[i], t[i], 64) for i in range(3)]
+    assert np.allclose(got.numpy(), ref, atol=1e-3)
+    r = torch.tensor([4.0, 1.0, 0.5, 0.25], dtype=torch.float64)
+    b = torch.tensor([1.0, 2.0, 3.0, 4.0], dtype=torch.float64)
+    x = ops.toeplitz_solve(r, b)
+    from torchmetrics_amd.ops._cpu import symmetric_toeplitz
+
+    assert torch.allclose(symmetric_toeplitz(r) @ x, b)
+
+
+@pytest.mark.parametrize(
+    ("cls", "fn", "kw"),
+    [
+        (SignalNoiseRatio, signal_noise_ratio, {"zero_mean": True}),
+        (ScaleInvariantSignalNoiseRatio, scale_invariant_signal_noise_ratio, {}),
+        (ScaleInvariantSignalDistortionRatio, scale_invariant_signal_distortion_ratio, {}),
+        (SignalDistortionRatio, signal_distortion_ratio, {"filter_length": 32}),
+        (SourceAggregatedSignalDistortionRatio, source_aggregated_signal_distortion_ratio, {}),
+    ],
+)
+def test_modules_mean_of_batches(cls, fn, kw, device="cpu"):
+    g = torch.Generator().manual_seed(0)
+    batches = [(torch.randn(4, 2, 500, generator=g), torch.randn(4, 2, 500, generator=g)) for _ in range(3)]
+    m = cls(**kw).to(device)
+    vals = []
+    for p, t in batches:
+        m.update(p.to(device), t.to(device))
+        vals.append(fn(p, t, **kw).reshape(-1))
+    assert torch.allclose(m.compute().cpu().float(), torch.cat(vals).mean().float(), atol=1e-4)
+
+
+def test_complex_and_pit_modules():
+    g = torch.Generator().manual_seed(1)
+    p, t = torch.randn(2, 17, 9, 2, generator=g), torch.randn(2, 17, 9, 2, generator=g)
+    m = ComplexScaleInvariantSignalNoiseRatio()
+    m.update(p, t)
+    assert torch.isclose(m.compute(), complex_scale_invariant_signal_noise_ratio(p, t).mean())
+    assert "num" in m._defaults and "ci_snr_sum" in m._defaults
+    pit = PermutationInvariantTraining(scale_invariant_signal_distortion_ratio, eval_func="max")
+    p, t = torch.randn(3, 3, 200, generator=g), torch.randn(3, 3, 200, generator=g)
+    pit.update(p, t)
+    best, _ = permutation_invariant_training(p, t, scale_invariant_signal_distortion_ratio)
+    assert torch.isclose(pit.compute(), best.mean())
+
+
+def test_pit_exhaustive_matches_assignment():
+    """Device exhaustive search and scipy's Hungarian agree (4 speakers, random metric matrices)."""
+    from torchmetrics_amd.functional.audio.pit import (
+        _find_best_perm_by_exhaustive_method,
+        _find_best_perm_by_linear_sum_assignment,
+    )
+
+    mm = torch.randn(16, 4, 4, generator=torch.Generator().manual_seed(2))
+    for op in (torch.max, torch.min):
+        a, pa = _find_best_perm_by_exhaustive_method(mm, op)
+        b, pb = _find_best_perm_by_linear_sum_assignment(mm, op)
+        assert torch.allclose(a, b) and torch.equal(pa, pb)
+
+
+def test_external_wrappers_gated():
+    with pytest.raises(ModuleNotFoundError):
+        PerceptualEvaluationSpeechQuality(16000, "wb")
+    with pytest.raises(ModuleNotFoundError):
+        ShortTimeObjectiveIntelligibility(16000)
+
+
+@pytest.mark.gpu
+def test_levinson_kernel_gpu():
+    g = torch.Generator().manual_seed(5)
+    for n_sys, L in ((1, 4), (37, 512), (5, 1500)):
+        sig = torch.randn(n_sys, 4 * L, generator=g, dtype=torch.float64)
+        r = torch.stack([torch.tensor(np.correlate(s.numpy(), s.numpy(), "full")[4 * L - 1:4 * L - 1 + L]) for s in sig])
+        r[:, 0] += 1e-3
+        b = torch.randn(n_sys, L, generator=g, dtype=torch.float64)
+        x = ops.toeplitz_solve(r.cuda(), b.cuda()).cpu()
+        ref = ops.toeplitz_solve(r, b)
+        assert torch.allclose(x, ref, rtol=1e-6, atol=1e-8), (n_sys, L)
+    # autograd through the kernel vs dense solve
+    r = r[:2, :64].clone()
+    b = b[:2, :64].clone()
+    rc, bc = r.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+    (ops.toeplitz_solve(rc, bc) ** 2).sum().backward()
+    rr, bb = r.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    (ops.toeplitz_solve(rr, bb) ** 2).sum().backward()
+    assert torch.allclose(rc.grad.cpu(), rr.grad, rtol=1e-6, atol=1e-8)
+    assert torch.allclose(bc.grad.cpu(), bb.grad, rtol=1e-6, atol=1e-8)
+
+
+@pytest.mark.gpu
+def test_audio_modules_gpu():
+    torch.manual_seed(1)
+    p, t = torch.randn(8000), torch.randn(8000)
+    assert torch.isclose(signal_distortion_ratio(p.cuda(), t.cuda()).cpu(), torch.tensor(-12.0589), atol=1e-3)
+    for cls, fn, kw in (
+        (SignalDistortionRatio, signal_distortion_ratio, {"filter_length": 32}),
+        (ScaleInvariantSignalDistortionRatio, scale_invariant_signal_distortion_ratio, {}),
+    ):
+        test_modules_mean_of_batches(cls, fn, kw, device="cuda")

@@ -1,0 +1,24 @@
+"""Audio metrics (reference ``S/audio/__init__.py``)."""
+from torchmetrics_amd.audio.metrics import (
+    ComplexScaleInvariantSignalNoiseRatio,
+    PerceptualEvaluationSpeechQuality,
+    PermutationInvariantTraining,
+    ScaleInvariantSignalDistortionRatio,
+    ScaleInvariantSignalNoiseRatio,
+    ShortTimeObjectiveIntelligibility,
+    SignalDistortionRatio,
+    SignalNoiseRatio,
+    SourceAggregatedSignalDistortionRatio,
+)
+
+__all__ = [
+    "ComplexScaleInvariantSignalNoiseRatio",
+    "PerceptualEvaluationSpeechQuality",
+    "PermutationInvariantTraining",
+    "ScaleInvariantSignalDistortionRatio",
+    "ScaleInvariantSignalNoiseRatio",
+    "ShortTimeObjectiveIntelligibility",
+    "SignalDistortionRatio",
+    "SignalNoiseRatio",
+    "SourceAggregatedSignalDistortionRatio",
+]

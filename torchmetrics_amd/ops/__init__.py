@@ -364,3 +364,45 @@ def token_nll(logits: Tensor, target: Tensor, ignore_index: Optional[int], flag:
             flag = torch.zeros(1, dtype=torch.int32, device=logits.device)
         return _TokenNLL.apply(logits.contiguous(), target.long().contiguous(), ignore_index, flag)
     return _cpu.token_nll(logits, target, ignore_index)
+
+
+# ----------------------------------------------------------------------------------------------------------- audio
+def _toeplitz_solve_kernel(r: Tensor, b: Tensor) -> Tensor:
+    shape = r.shape
+    rr = r.reshape(-1, shape[-1]).double().contiguous()
+    bb = b.reshape(-1, shape[-1]).double().contiguous()
+    x = torch.empty_like(rr)
+    _ops().toeplitz_solve(rr, bb, x)
+    return x.reshape(shape)
+
+
+class _ToeplitzSolve(torch.autograd.Function):
+    """x = T(r)^-1 b.  Backward: y = T^-1 g (T is symmetric), grad_b = y, grad_r[k] = -sum_{|i-j|=k} y_i x_j."""
+
+    @staticmethod
+    def forward(ctx, r, b):  # noqa: D102
+        x = _toeplitz_solve_kernel(r, b)
+        ctx.save_for_backward(r, x)
+        return x
+
+    @staticmethod
+    def backward(ctx, g):  # noqa: D102
+        r, x = ctx.saved_tensors
+        y = _toeplitz_solve_kernel(r, g.contiguous())
+        n = x.shape[-1]
+        nfft = 1 << (2 * n - 1).bit_length()
+        xf, yf = torch.fft.rfft(x, n=nfft), torch.fft.rfft(y, n=nfft)
+        c_xy = torch.fft.irfft(xf * yf.conj(), n=nfft)[..., :n]  # sum_i y_i x_{i+k}
+        c_yx = torch.fft.irfft(yf * xf.conj(), n=nfft)[..., :n]  # sum_i x_i y_{i+k}
+        grad_r = -(c_xy + c_yx)
+        grad_r[..., 0] = grad_r[..., 0] / 2
+        return grad_r.to(r.dtype), y.to(r.dtype)
+
+
+def toeplitz_solve(r: Tensor, b: Tensor) -> Tensor:
+    """Solve ``T(r) x = b`` for batches of symmetric Toeplitz systems ``r, b: [..., L]`` (fp64): Levinson recursion,
+    one wave per system on ROCm (``csrc/audio/levinson.hip``, differentiable); dense LU of the explicit matrix on the
+    host."""
+    if r.is_cuda:
+        return _ToeplitzSolve.apply(r, b)
+    return _cpu.toeplitz_solve(r, b)

@@ -434,3 +434,14 @@ def token_nll(logits: Tensor, target: Tensor, ignore_index: Optional[int]) -> Te
         raise IndexError("Perplexity: target index out of range of the vocabulary")
     lp = torch.log_softmax(logits.to(acc), dim=1).gather(1, safe[:, None])[:, 0]
     return torch.where(mask, -lp, torch.zeros_like(lp)).float()
+
+
+def symmetric_toeplitz(vector: Tensor) -> Tensor:
+    """``[..., L] -> [..., L, L]`` with ``T[i, j] = v[|i - j|]``."""
+    n = vector.shape[-1]
+    idx = torch.arange(n, device=vector.device)
+    return vector[..., (idx[:, None] - idx[None, :]).abs()]
+
+
+def toeplitz_solve(r: Tensor, b: Tensor) -> Tensor:
+    return torch.linalg.solve(symmetric_toeplitz(r), b.unsqueeze(-1)).squeeze(-1)

@@ -1,0 +1,84 @@
+"""Segmentation utilities vs scipy.ndimage (reference ``tests/unittests/segmentation``)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+from scipy import ndimage
+
+from torchmetrics_amd.functional.segmentation.utils import (
+    binary_erosion,
+    distance_transform,
+    generate_binary_structure,
+    mask_edges,
+    surface_distance,
+    table_contour_length,
+    table_surface_area,
+)
+
+
+def test_binary_structure():
+    for rank in (1, 2, 3):
+        for conn in (1, 2, 3):
+            assert np.array_equal(generate_binary_structure(rank, conn).numpy(),
+                                  ndimage.generate_binary_structure(rank, conn))
+
+
+@pytest.mark.parametrize("rank", [2, 3])
+@pytest.mark.parametrize("conn", [1, 2])
+def test_binary_erosion_vs_scipy(rank, conn):
+    g = torch.Generator().manual_seed(rank * 10 + conn)
+    img = (torch.rand((2, 1) + (12,) * rank, generator=g) > 0.3).int()
+    st = generate_binary_structure(rank, conn).int()
+    out = binary_erosion(img, st)
+    for b in range(2):
+        ref = ndimage.binary_erosion(img[b, 0].numpy(), st.numpy(), border_value=0)
+        assert np.array_equal(out[b, 0].numpy().astype(bool), ref)
+    doc = torch.tensor([[[[0, 0, 0, 0, 0], [0, 1, 1, 1, 0], [0, 1, 1, 1, 0], [0, 1, 1, 1, 0], [0, 0, 0, 0, 0]]]])
+    exp = torch.zeros_like(doc)
+    exp[0, 0, 2, 2] = 1
+    assert torch.equal(binary_erosion(doc).long(), exp)
+
+
+@pytest.mark.parametrize("metric", ["euclidean", "chessboard", "taxicab"])
+@pytest.mark.parametrize("shape", [(9, 9), (13, 7)])
+def test_distance_transform_vs_scipy(metric, shape):
+    g = torch.Generator().manual_seed(sum(shape))
+    x = (torch.rand(shape, generator=g) > 0.25).int()
+    x[0, 0] = 0
+    out = distance_transform(x, metric=metric)
+    if metric == "euclidean":
+        ref = ndimage.distance_transform_edt(x.numpy())
+        assert np.allclose(out.numpy(), ref, atol=1e-5)
+        out2 = distance_transform(x, sampling=[2.0, 0.5], metric=metric)
+        assert np.allclose(out2.numpy(), ndimage.distance_transform_edt(x.numpy(), [2.0, 0.5]), atol=1e-5)
+    else:
+        ref = ndimage.distance_transform_cdt(x.numpy(), metric=metric)
+        assert np.array_equal(out.numpy(), ref)
+
+
+def test_mask_edges_and_surface_distance():
+    preds = torch.zeros(8, 8, dtype=torch.bool)
+    target = torch.zeros(8, 8, dtype=torch.bool)
+    preds[2:6, 2:6] = True
+    target[3:7, 2:6] = True
+    ep, et = mask_edges(preds, target)
+    assert ep.sum() == 12 and et.sum() == 12
+    ep, et, ap, at = mask_edges(preds, target, spacing=(1, 1))
+    assert ep.shape == (9, 9) and torch.isclose(ap.sum(), torch.tensor(12 + 2 * math.sqrt(2)), atol=1e-4)
+    d = surface_distance(ep, et)
+    assert d.numel() == int(ep.sum()) and torch.isfinite(d).all()
+    assert torch.isinf(surface_distance(preds, torch.zeros_like(target))).all()
+
+
+def test_neighbour_tables():
+    t2, k2 = table_contour_length((1, 1))
+    assert torch.allclose(t2[[0, 1, 3, 5, 6, 15]], torch.tensor([0, math.sqrt(2) / 2, 1, 1, math.sqrt(2), 0]))
+    assert k2.tolist() == [[[[8, 4], [2, 1]]]]
+    t3, k3 = table_surface_area((2, 2, 2))
+    # single corner cut (sqrt(3)/2 at spacing 2), two adjacent corners (2 sqrt 2), a full face (4), empty / full
+    assert torch.allclose(t3[[0, 1, 3, 15, 255]], torch.tensor([0.0, 0.8660, 2.8284, 4.0, 0.0]), atol=1e-4)
+    assert torch.allclose(t3[6], 2 * t3[1]) and torch.allclose(t3, t3.flip(0) * 0 + t3)
+    assert k3.shape == (1, 1, 2, 2, 2)
+    t3b, _ = table_surface_area((1, 1, 1))
+    assert torch.allclose(t3b * 4, t3, atol=1e-4)

@@ -1,0 +1,84 @@
+"""CLIPScore / CLIP-IQA with a tiny random-init CLIP saved to a temp dir (no network).  The oracle uses
+``CLIPModel.forward``'s ``logits_per_image`` (an independent code path) divided by the logit scale."""
+import json
+
+import pytest
+import torch
+
+transformers = pytest.importorskip("transformers")
+
+from torchmetrics_amd.functional.multimodal import clip_image_quality_assessment, clip_score  # noqa: E402
+from torchmetrics_amd.multimodal import CLIPImageQualityAssessment, CLIPScore  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def tiny_clip(tmp_path_factory):
+    d = tmp_path_factory.mktemp("tinyclip")
+    keep = list(range(ord("!"), ord("~") + 1)) + list(range(0xA1, 0xAD)) + list(range(0xAE, 0x100))
+    extra = [b for b in range(256) if b not in keep]
+    chars = [chr(b) for b in keep] + [chr(256 + i) for i in range(len(extra))]  # GPT-2 byte -> unicode alphabet
+    vocab = {c: i for i, c in enumerate(chars)}
+    for c in chars:
+        vocab[c + "</w>"] = len(vocab)
+    vocab["<|startoftext|>"] = len(vocab)
+    vocab["<|endoftext|>"] = len(vocab)
+    (d / "vocab.json").write_text(json.dumps(vocab))
+    (d / "merges.txt").write_text("#version: 0.2\n")
+    tok = transformers.CLIPTokenizer(str(d / "vocab.json"), str(d / "merges.txt"))
+    improc = transformers.CLIPImageProcessor(size={"shortest_edge": 32}, crop_size={"height": 32, "width": 32})
+    proc = transformers.CLIPProcessor(image_processor=improc, tokenizer=tok)
+    torch.manual_seed(0)
+    cfg = transformers.CLIPConfig(
+        text_config={"vocab_size": len(vocab), "hidden_size": 32, "intermediate_size": 64, "num_hidden_layers": 2,
+                     "num_attention_heads": 2, "max_position_embeddings": 77},
+        vision_config={"image_size": 32, "patch_size": 8, "hidden_size": 32, "intermediate_size": 64,
+                       "num_hidden_layers": 2, "num_attention_heads": 2},
+        projection_dim=16)
+    model = transformers.CLIPModel(cfg).eval()
+    model.save_pretrained(str(d))
+    proc.save_pretrained(str(d))
+    return str(d), model, proc
+
+
+def _cos_oracle(model, proc, images, texts):
+    inp = proc(text=texts, images=[i for i in images], return_tensors="pt", padding=True)
+    with torch.no_grad():
+        out = model(**inp)
+    return out.logits_per_image / model.logit_scale.exp()
+
+
+def test_clip_score(tiny_clip):
+    path, model, proc = tiny_clip
+    g = torch.Generator().manual_seed(1)
+    images = torch.randint(0, 255, (3, 3, 40, 40), generator=g).float()
+    texts = ["a cat on a mat", "a red car", "the quick brown fox"]
+    cos = _cos_oracle(model, proc, images, texts)
+    expected = torch.clamp(100 * cos.diag().mean(), min=0)
+    assert torch.allclose(clip_score(images, texts, model_name_or_path=path), expected, atol=1e-4)
+    m = CLIPScore(model_name_or_path=path)
+    m.update(images[:2], texts[:2])
+    m.update(images[2], texts[2])
+    assert torch.allclose(m.compute(), expected, atol=1e-4)
+    with pytest.raises(ValueError):
+        m.update(images[:2], texts)
+
+
+def test_clip_iqa(tiny_clip):
+    path, model, proc = tiny_clip
+    images = torch.rand(4, 3, 32, 32, generator=torch.Generator().manual_seed(2))
+    prompts = ("quality", ("Super good photo.", "Super bad photo."))
+    out = clip_image_quality_assessment(images, model_name_or_path=path, prompts=prompts)
+    assert set(out) == {"quality", "user_defined_0"}
+    flat = ["Good photo.", "Bad photo.", "Super good photo.", "Super bad photo."]
+    cos = _cos_oracle(model, proc, images, flat)
+    probs = (100 * cos).reshape(4, 2, 2).softmax(-1)[:, :, 0]
+    assert torch.allclose(out["quality"], probs[:, 0], atol=1e-4)
+    assert torch.allclose(out["user_defined_0"], probs[:, 1], atol=1e-4)
+    m = CLIPImageQualityAssessment(model_name_or_path=path, prompts=("quality",))
+    m.update(images[:2])
+    m.update(images[2:])
+    assert torch.allclose(m.compute(), probs[:, 0], atol=1e-4)
+    with pytest.raises(ValueError):
+        CLIPImageQualityAssessment(model_name_or_path=path, prompts=("nope",))
+    with pytest.raises(ModuleNotFoundError):
+        CLIPImageQualityAssessment()  # default "clip_iqa" network needs piq

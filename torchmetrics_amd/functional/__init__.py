@@ -9,3 +9,4 @@ from torchmetrics_amd.functional.nominal import *  # noqa: F401,F403
 from torchmetrics_amd.functional.pairwise import *  # noqa: F401,F403
 from torchmetrics_amd.functional.text import *  # noqa: F401,F403
 from torchmetrics_amd.functional.audio import *  # noqa: F401,F403
+from torchmetrics_amd.functional.multimodal import *  # noqa: F401,F403

@@ -9,6 +9,8 @@ from torchmetrics_amd.functional.image.basic import (
     spectral_angle_mapper,
     total_variation,
 )
+from torchmetrics_amd.functional.image.lpips import learned_perceptual_image_patch_similarity
+from torchmetrics_amd.functional.image.perceptual_path_length import perceptual_path_length
 from torchmetrics_amd.functional.image.spatial import (
     quality_with_no_reference,
     spatial_correlation_coefficient,

@@ -406,3 +406,17 @@ def toeplitz_solve(r: Tensor, b: Tensor) -> Tensor:
     if r.is_cuda:
         return _ToeplitzSolve.apply(r, b)
     return _cpu.toeplitz_solve(r, b)
+
+
+def lpips_layer(f0: Tensor, f1: Tensor, w: Tensor, eps: float = 1e-8) -> Tensor:
+    """``[N]`` spatial mean of ``sum_c w_c (f0/|f0| - f1/|f1|)^2`` for one LPIPS layer ``[N, C, H, W]`` -- fused
+    single-pass HIP kernel on ROCm (``csrc/image/lpips.hip``), composite ATen ops on the host."""
+    n, c = f0.shape[:2]
+    pixels = f0[0, 0].numel()
+    if f0.is_cuda:
+        a = f0.reshape(n, c, pixels).contiguous()
+        b = f1.to(a.dtype).reshape(n, c, pixels).contiguous()
+        part = torch.empty(n, -(-pixels // 256), dtype=torch.float64, device=f0.device)
+        _ops().lpips_layer(a, b, w.reshape(-1).float().contiguous(), part, float(eps))
+        return (part.sum(1) / pixels).to(f0.dtype if f0.is_floating_point() else torch.float32)
+    return _cpu.lpips_layer(f0, f1, w, eps)

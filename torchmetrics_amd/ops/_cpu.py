@@ -445,3 +445,10 @@ def symmetric_toeplitz(vector: Tensor) -> Tensor:
 
 def toeplitz_solve(r: Tensor, b: Tensor) -> Tensor:
     return torch.linalg.solve(symmetric_toeplitz(r), b.unsqueeze(-1)).squeeze(-1)
+
+
+def lpips_layer(f0: Tensor, f1: Tensor, w: Tensor, eps: float) -> Tensor:
+    n0 = f0 / (torch.sqrt((f0**2).sum(1, keepdim=True)) + eps)
+    n1 = f1 / (torch.sqrt((f1**2).sum(1, keepdim=True)) + eps)
+    d = ((n0 - n1) ** 2 * w.reshape(1, -1, 1, 1)).sum(1)
+    return d.mean(dim=(-2, -1))

@@ -32,3 +32,17 @@ from torchmetrics_amd.wrappers import (  # noqa: E402
     MultioutputWrapper,
     MultitaskWrapper,
 )
+from torchmetrics_amd.nominal import (  # noqa: E402
+    CramersV,
+    FleissKappa,
+    PearsonsContingencyCoefficient,
+    TheilsU,
+    TschuprowsT,
+)
+from torchmetrics_amd._deprecated import ROOT_CLASSES as __ROOT_CLASSES  # noqa: E402
+from torchmetrics_amd._deprecated import deprecated_class as __deprecated_class  # noqa: E402
+
+# deprecated root aliases (audio / detection / image / retrieval / text), reference ``S/__init__.py:33-151``
+for __name, __domain in __ROOT_CLASSES.items():
+    globals()[__name] = __deprecated_class(__name, __domain)
+del __name, __domain

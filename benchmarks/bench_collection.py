@@ -1,0 +1,115 @@
+"""BASELINE config #5: ``MetricCollection`` of 20 classification + regression metrics with ``compute_groups=True``.
+
+Per step (weak scaling, one rank per GPU): the 15-metric multiclass collection (num_classes=10) is updated with an
+8192 x 10 bf16 logit batch and the 5-metric regression collection with 8192 float pairs; ``--sync-every-step``
+additionally runs ``compute()`` (RCCL all-reduce of every state bucket) after every step, matching "per-step
+all-reduce".  Reported: metric-updates/sec over the node (20 metric updates per step).  Synthetic data.
+Prints one JSON line.  Usage: ``python benchmarks/bench_collection.py [--steps K] [--warmup W] [--sync-every-step]``
+(multi-GPU via ``torch.distributed.run``).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from torchmetrics_amd import MetricCollection  # noqa: E402
+from torchmetrics_amd import classification as C  # noqa: E402
+from torchmetrics_amd import regression as R  # noqa: E402
+
+NC, BATCH, NBUF = 10, 8192, 4
+
+
+def build(device):
+    cls = MetricCollection({
+        "acc": C.MulticlassAccuracy(NC, average="macro"),
+        "prec": C.MulticlassPrecision(NC, average="macro"),
+        "rec": C.MulticlassRecall(NC, average="macro"),
+        "f1": C.MulticlassF1Score(NC, average="macro"),
+        "fbeta": C.MulticlassFBetaScore(2.0, NC, average="macro"),
+        "spec": C.MulticlassSpecificity(NC, average="macro"),
+        "hamming": C.MulticlassHammingDistance(NC, average="macro"),
+        "stat": C.MulticlassStatScores(NC, average="macro"),
+        "jacc": C.MulticlassJaccardIndex(NC),
+        "mcc": C.MulticlassMatthewsCorrCoef(NC),
+        "kappa": C.MulticlassCohenKappa(NC),
+        "cm": C.MulticlassConfusionMatrix(NC),
+        "auroc": C.MulticlassAUROC(NC, thresholds=100),
+        "ap": C.MulticlassAveragePrecision(NC, thresholds=100),
+        "ece": C.MulticlassCalibrationError(NC, n_bins=15),
+    }, compute_groups=True).to(device)
+    reg = MetricCollection({
+        "mse": R.MeanSquaredError(), "mae": R.MeanAbsoluteError(), "r2": R.R2Score(),
+        "pearson": R.PearsonCorrCoef(), "ev": R.ExplainedVariance(),
+    }, compute_groups=True).to(device)
+    return cls, reg
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--sync-every-step", action="store_true")
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl" if device.type == "cuda" else "gloo", rank=rank, world_size=world)
+    g = torch.Generator().manual_seed(7 + rank)
+    logits = [torch.randn(BATCH, NC, generator=g).to(device, torch.bfloat16) for _ in range(NBUF)]
+    labels = [torch.randint(0, NC, (BATCH,), generator=g).to(device) for _ in range(NBUF)]
+    xs = [torch.randn(BATCH, generator=g).to(device) for _ in range(NBUF)]
+    ys = [(x + 0.3 * torch.randn(BATCH, generator=g).to(device)) for x in xs]
+    cls, reg = build(device)
+
+    def step(i):
+        cls.update(logits[i % NBUF], labels[i % NBUF])
+        reg.update(xs[i % NBUF], ys[i % NBUF])
+        if args.sync_every_step:
+            cls.compute()
+            reg.compute()
+
+    def sync():
+        if world > 1:
+            dist.barrier()
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    cls.compute(), reg.compute()
+    cls.reset(), reg.reset()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    out = {**cls.compute(), **reg.compute()}
+    sync()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({
+            "bench": "metric_collection_20", "metric": "metric-updates/sec (whole node)",
+            "value": round(world * args.steps * 20 / elapsed, 1), "unit": "metric-updates/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "sync_every_step": args.sync_every_step, "compute_groups": True, "dtype": "bf16", "data": "synthetic",
+            "groups": len(cls.compute_groups), "acc": float(out["acc"]), "r2": float(out["r2"]),
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -271,6 +271,89 @@ __global__ void __launch_bounds__(kBlock) mc_items_kernel(const scalar_t* __rest
   if (use_lds) lds_flush(lds, nbins, out);
 }
 
+// Few-bin multiclass path (nbins <= 256, e.g. C <= 85 stats / C <= 16 confusion matrix): every bin is a popcount of
+// a wave ballot, accumulated in the registers of the lane owning the bin (lane = bin % 64, slot = bin / 64).  With few
+// bins the LDS/global atomic histogram serialises on a handful of hot addresses (8192 x 10 classes: 75 us); here a
+// wave spends one ballot per bin per 64 items and the block flushes <= 256 int64 atomics.
+template <typename scalar_t, typename target_t, bool kArgmax>
+__global__ void __launch_bounds__(kBlock) mc_fewbins_kernel(const scalar_t* __restrict__ preds,
+                                                            const target_t* __restrict__ target, long long N,
+                                                            long long X, int C, long long ignore, bool has_ignore,
+                                                            int mode, int64_t* __restrict__ out,
+                                                            int* __restrict__ flag) {
+  __shared__ int lds[256];
+  const int nbins = mode == kMcConfmat ? C * C : 3 * C + 1;
+  const int lane = threadIdx.x & (kWave - 1);
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) lds[b] = 0;
+  __syncthreads();
+  int acc[4] = {0, 0, 0, 0};
+  const long long items = N * X;
+  const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
+  // loop bounds are wave-uniform so every ballot sees the whole wave
+  const long long wave_base = static_cast<long long>(blockIdx.x) * blockDim.x + (threadIdx.x & ~(kWave - 1));
+  for (long long base = wave_base; base < items; base += stride) {
+    const long long it = base + lane;
+    int t = -1, p = -1;
+    if (it < items && mc_target(target, it, C, ignore, has_ignore, flag, t)) {
+      const long long n = it / X, x = it - n * X;
+      if constexpr (kArgmax) {
+        const scalar_t* pr = preds + n * C * X + x;
+        float best = to_f32(pr[0]);
+        int bidx = 0;
+        for (int c = 1; c < C; ++c) {
+          const float v = to_f32(pr[static_cast<long long>(c) * X]);
+          if (argmax_better(v, c, best, bidx)) {
+            best = v;
+            bidx = c;
+          }
+        }
+        p = bidx;
+      } else {
+        const long long v = static_cast<long long>(preds[it]);
+        if (v < 0 || v >= C) {
+          raise_flag(flag, kErrPredsOutOfRange);
+          t = -1;
+        } else {
+          p = static_cast<int>(v);
+        }
+      }
+    }
+    const bool valid = t >= 0;
+    if (mode == kMcConfmat) {
+      const int key = valid ? t * C + p : -1;
+#pragma unroll
+      for (int slot = 0; slot < 4; ++slot) {
+        const int b0 = slot * kWave;
+        if (b0 >= nbins) break;
+        const int nb = min(kWave, nbins - b0);
+        for (int l = 0; l < nb; ++l) {
+          const int cnt = __popcll(__ballot(key == b0 + l));
+          if (lane == l) acc[slot] += cnt;
+        }
+      }
+    } else {
+      for (int c = 0; c < C; ++c) {
+        const int tp = __popcll(__ballot(valid && p == c && t == c));
+        const int fp = __popcll(__ballot(valid && p == c && t != c));
+        const int fn = __popcll(__ballot(valid && t == c && p != c));
+        const int bt = c, bf = C + c, bn = 2 * C + c;
+        if ((bt & (kWave - 1)) == lane) acc[bt >> 6] += tp;
+        if ((bf & (kWave - 1)) == lane) acc[bf >> 6] += fp;
+        if ((bn & (kWave - 1)) == lane) acc[bn >> 6] += fn;
+      }
+      const int cnt = __popcll(__ballot(valid));
+      const int bc = 3 * C;
+      if ((bc & (kWave - 1)) == lane) acc[bc >> 6] += cnt;
+    }
+  }
+#pragma unroll
+  for (int slot = 0; slot < 4; ++slot) {
+    const int b = slot * kWave + lane;
+    if (b < nbins && acc[slot]) atomicAdd(&lds[b], acc[slot]);
+  }
+  lds_flush(lds, nbins, out);
+}
+
 // fold a multiclass stats workspace [G, 3C+1] into the states; optionally micro-reduce over classes.
 // accumulate=true: states += batch ; false: states = batch (samplewise outputs). Re-zeros the workspace.
 __global__ void __launch_bounds__(kBlock) mc_finalize_kernel(int64_t* __restrict__ ws, int C, bool micro,
@@ -627,11 +710,19 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
           const int grid = pick_grid(N, waves_per_block);
           hipLaunchKernelGGL((mc_argmax_rows_kernel<scalar_t, target_t>), dim3(grid), dim3(kBlock), lds_bytes, s, pp,
                              tp, N, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, vec, samplewise);
+        } else if (!samplewise && nbins <= 256) {
+          const int grid = pick_grid(N * X, kBlock * 4);
+          hipLaunchKernelGGL((mc_fewbins_kernel<scalar_t, target_t, true>), dim3(grid), dim3(kBlock), 0, s, pp, tp, N,
+                             X, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp);
         } else {
           const int grid = pick_grid(N * X, kBlock);
           hipLaunchKernelGGL((mc_items_kernel<scalar_t, target_t, true>), dim3(grid), dim3(kBlock), lds_bytes, s, pp,
                              tp, N, X, C, 1, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, samplewise);
         }
+      } else if (!samplewise && nbins <= 256 && K == 1) {
+        const int grid = pick_grid(N * X, kBlock * 4);
+        hipLaunchKernelGGL((mc_fewbins_kernel<scalar_t, target_t, false>), dim3(grid), dim3(kBlock), 0, s, pp, tp, N,
+                           X, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp);
       } else {
         const int grid = pick_grid(N * X, kBlock);
         hipLaunchKernelGGL((mc_items_kernel<scalar_t, target_t, false>), dim3(grid), dim3(kBlock), lds_bytes, s, pp,

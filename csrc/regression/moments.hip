@@ -84,6 +84,27 @@ __global__ void __launch_bounds__(kBlock) moments_partial_kernel(const scalar_t*
     if (mask & (1 << kMINK)) acc[kMINK] += pow(static_cast<double>(ad), pw);
     acc[kCOUNT] += 1.0;
   }
+  if ((kWave % k) == 0) {
+    // k divides the wave: lanes l and l ^ off (off >= k) share a column -> xor-shuffle tree inside the wave, then a
+    // 4-wave fold in LDS (the generic path below walks the block serially per column: ~25 us for k = 1)
+    __shared__ double wred[kBlock / kWave][kWave][kMaxSums];
+    const int wid = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+#pragma unroll
+    for (int s = 0; s < kMaxSums; ++s) {
+      double v = acc[s];
+      for (int off = kWave / 2; off >= k; off >>= 1) v += __shfl_xor(v, off, kWave);
+      if (lane < k) wred[wid][lane][s] = v;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < k * kMaxSums; i += blockDim.x) {
+      const int c = i / kMaxSums, s = i % kMaxSums;
+      double v = 0.0;
+      for (int w = 0; w < kBlock / kWave; ++w) v += wred[w][c][s];
+      // lane l of every wave holds column (block_base + l) % k; block_base is a multiple of k here
+      partial[(static_cast<long long>(blockIdx.x) * k + c) * kMaxSums + s] = v;
+    }
+    return;
+  }
   // block reduction per (column, sum): threads with equal tid % k hold the same column
   __shared__ double red[kBlock][kMaxSums + 1];
 #pragma unroll

@@ -126,7 +126,8 @@ class MulticlassCalibrationError(Metric):
 
     def update(self, preds: Tensor, target: Tensor) -> None:
         if self.validate_args:
-            _multiclass_float_preds_validation(preds, target, self.num_classes, self.ignore_index)
+            flag = self._device_error_buffer(preds.device) if preds.is_cuda else None
+            _multiclass_float_preds_validation(preds, target, self.num_classes, self.ignore_index, flag)
         preds, target = _multiclass_format(preds, target, self.ignore_index)
         confidences, accuracies = _multiclass_calibration_error_update(preds, target)
         self.confidences.append(confidences)

@@ -9,7 +9,11 @@ from typing import Callable, Dict, Optional
 import torch
 from torch import Tensor
 
+from torchmetrics_amd import ops
 from torchmetrics_amd.utilities.compute import _adjust_weights_safe_divide, _safe_divide
+
+_KIND_IDS = {"accuracy": 0, "hamming": 1, "precision": 2, "recall": 3, "specificity": 4, "fbeta": 5}
+_AVG_IDS = {"micro": 0, "macro": 1, "weighted": 2, "none": 3}
 
 
 def _sum_stats(x: Tensor, multidim_average: str) -> Tensor:
@@ -52,7 +56,16 @@ def _stat_reduce(
     multilabel: bool = False,
     beta: float = 1.0,
 ) -> Tensor:
-    """Reduce tp/fp/tn/fn to a score according to ``average`` (``binary``/``micro``/``macro``/``weighted``/``none``)."""
+    """Reduce tp/fp/tn/fn to a score according to ``average`` (``binary``/``micro``/``macro``/``weighted``/``none``).
+
+    ROCm int64 states take the single-launch fused reduction (``csrc/classification/stat_reduce.hip``)."""
+    if (tp.is_cuda and average != "binary" and tp.dtype == torch.int64 and tp.ndim in (1, 2)
+            and all(t.shape == tp.shape and t.dtype == torch.int64 for t in (fp, tn, fn))):
+        rows = (lambda t: t.reshape(1, -1)) if tp.ndim == 1 else (lambda t: t)
+        if tp.ndim == 1 or multidim_average != "global":
+            avg = _AVG_IDS[average if average is not None else "none"]
+            out = ops.stat_reduce(rows(tp), rows(fp), rows(tn), rows(fn), _KIND_IDS[kind], avg, multilabel, beta)
+            return out.reshape(tp.shape) if avg == _AVG_IDS["none"] else (out[0] if tp.ndim == 1 else out)
     if average == "binary":
         return _binary_score(kind, tp, fp, tn, fn, beta)
     if average == "micro":

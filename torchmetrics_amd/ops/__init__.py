@@ -420,3 +420,13 @@ def lpips_layer(f0: Tensor, f1: Tensor, w: Tensor, eps: float = 1e-8) -> Tensor:
         _ops().lpips_layer(a, b, w.reshape(-1).float().contiguous(), part, float(eps))
         return (part.sum(1) / pixels).to(f0.dtype if f0.is_floating_point() else torch.float32)
     return _cpu.lpips_layer(f0, f1, w, eps)
+
+
+def stat_reduce(tp: Tensor, fp: Tensor, tn: Tensor, fn: Tensor, kind: int, average: int, multilabel: bool,
+                beta: float = 1.0) -> Tensor:
+    """Fused stat-score compute on ``[R, C]`` int64 states (``csrc/classification/stat_reduce.hip``): ``[R]`` for
+    micro / macro / weighted (ids 0 / 1 / 2), ``[R, C]`` for none (3)."""
+    out = torch.empty(tp.shape[0] * (tp.shape[1] if average == 3 else 1), dtype=torch.float32, device=tp.device)
+    _ops().stat_reduce(tp.contiguous(), fp.contiguous(), tn.contiguous(), fn.contiguous(), out, int(kind),
+                       int(average), bool(multilabel), float(beta))
+    return out.reshape(tp.shape[0], -1) if average == 3 else out

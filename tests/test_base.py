@@ -328,3 +328,22 @@ def test_aggregation_gpu_deferred_nan_error():
     m2 = tm.SumMetric(nan_strategy="ignore").cuda()
     m2.update(tensor([1.0, float("nan"), 2.0], device="cuda"))
     assert m2.compute().item() == 3.0
+
+
+def test_collection_repeated_compute_keeps_member_results():
+    """A second ``compute()`` without an update must not hand the group leader's cached value to the other members."""
+    import torch
+
+    from torchmetrics_amd import MetricCollection
+    from torchmetrics_amd.classification import MulticlassAccuracy, MulticlassPrecision, MulticlassSpecificity
+
+    g = torch.Generator().manual_seed(3)
+    preds, target = torch.randn(64, 5, generator=g), torch.randint(0, 5, (64,), generator=g)
+    mc = MetricCollection([MulticlassAccuracy(5), MulticlassPrecision(5), MulticlassSpecificity(5)],
+                          compute_groups=True)
+    mc.update(preds, target)
+    first, second = mc.compute(), mc.compute()
+    assert len(mc.compute_groups) == 1
+    for k in first:
+        assert torch.equal(first[k], second[k]), k
+    assert not torch.equal(second["MulticlassAccuracy"], second["MulticlassSpecificity"])

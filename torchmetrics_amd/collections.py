@@ -120,9 +120,18 @@ class MetricCollection(ModuleDict):
                     mi = getattr(self, name)
                     for state in m0._defaults:
                         val = getattr(m0, state)
-                        setattr(mi, state, deepcopy(val) if copy else val)
+                        if copy:
+                            setattr(mi, state, deepcopy(val))
+                        elif mi.__dict__.get(state, None) is not val and getattr(mi, state) is not val:
+                            setattr(mi, state, val)  # Module.__setattr__ is costly: only re-point stale refs
                     mi._update_count = deepcopy(m0._update_count) if copy else m0._update_count
-                    mi._computed = deepcopy(m0._computed) if copy else m0._computed
+                    # members share the leader's *states*, not its result: only propagate cache invalidation (the
+                    # reference copies the leader's cached value, so a second compute() without an update returned
+                    # the leader's result for every member, S/collections.py:307)
+                    if copy:
+                        mi._computed = deepcopy(mi._computed)
+                    elif m0._computed is None:
+                        mi._computed = None
         self._state_is_copy = copy
 
     def compute(self) -> Dict[str, Any]:

@@ -137,6 +137,79 @@ __global__ void __launch_bounds__(kBlock) mc_argmax_rows_kernel(const scalar_t* 
 // 16-byte loads before consuming any (memory-level parallelism instead of one dependent load chain per wave), the
 // row's target is fetched in the same batch, and the argmax is reduced inside the LPR-lane group (log2(LPR)
 // shuffles).  For C = 1000 bf16 (2000 B rows) LPR = 16 gives 8 loads in flight per lane, 4 rows per wave.
+// Wave-per-row argmax with a software pipeline across rows: a persistent grid (a few blocks per CU) walks rows
+// with a wave-uniform stride, and the 16-byte chunks of the *next* row are issued before the current row is reduced,
+// so every wave keeps two rows of loads in flight instead of paying one full memory latency per row.
+// kPer = 16-byte chunks per lane per row (ceil(C * sizeof(T) / 16 / 64)).
+template <typename scalar_t, typename target_t, int kPer>
+__global__ void __launch_bounds__(kBlock) mc_argmax_pipe_kernel(const scalar_t* __restrict__ preds,
+                                                                const target_t* __restrict__ target, long long N,
+                                                                int C, long long ignore, bool has_ignore, int mode,
+                                                                int64_t* __restrict__ out, int* __restrict__ flag) {
+  constexpr int kVec = 16 / sizeof(scalar_t);
+  const int lane = threadIdx.x & (kWave - 1);
+  const long long nwaves = static_cast<long long>(gridDim.x) * (blockDim.x / kWave);
+  const long long wave = (static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
+  const int nchunks = C / kVec;
+  u32x4 cur[kPer], nxt[kPer];
+  long long tcur = 0, tnxt = 0;
+  auto issue = [&](long long row, u32x4* buf, long long& t) {
+    const u32x4* rp = reinterpret_cast<const u32x4*>(preds + row * C);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int ci = lane + j * kWave;
+      if (ci < nchunks) buf[j] = __builtin_nontemporal_load(rp + ci);
+    }
+    if (lane == 0) t = static_cast<long long>(target[row]);
+  };
+  long long row = wave;
+  if (row < N) issue(row, cur, tcur);
+  for (; row < N; row += nwaves) {  // wave-uniform
+    const long long next = row + nwaves;
+    if (next < N) issue(next, nxt, tnxt);
+    float best = -INFINITY;
+    int bidx = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int ci = lane + j * kWave;
+      if (ci < nchunks) {
+        const scalar_t* e = reinterpret_cast<const scalar_t*>(&cur[j]);
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+          const float v = to_f32(e[k]);
+          const int idx = ci * kVec + k;
+          if (argmax_better(v, idx, best, bidx)) {
+            best = v;
+            bidx = idx;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+      const float ov = __shfl_xor(best, off, kWave);
+      const int oi = __shfl_xor(bidx, off, kWave);
+      if (argmax_better(ov, oi, best, bidx)) {
+        best = ov;
+        bidx = oi;
+      }
+    }
+    if (lane == 0) {
+      const long long t = tcur;
+      bool ok = true;
+      if (has_ignore && t == ignore) ok = false;
+      else if (t < 0 || t >= C) {
+        raise_flag(flag, kErrTargetOutOfRange);
+        ok = false;
+      }
+      if (ok) mc_accumulate(mode, static_cast<int>(t), &bidx, 1, C, out, nullptr, false, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) cur[j] = nxt[j];
+    tcur = tnxt;
+  }
+}
+
 template <typename scalar_t, typename target_t, int LPR>
 __global__ void __launch_bounds__(kBlock) mc_argmax_subwave_kernel(const scalar_t* __restrict__ preds,
                                                                    const target_t* __restrict__ target, long long N,
@@ -678,9 +751,31 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
             const char* e = std::getenv("TM_AMD_MC_LPR");  // tuning knob: 16 / 32 / 64
             return e ? std::atoi(e) : 0;
           }();
-          // measured on MI355X (8192x1000 bf16, inputs cycling through MALL): LPR 64: 12.1 us, 32: 12.4, 16: 14.3, 8: 21.0
+          // measured on MI355X (8192x1000 bf16, inputs cycling through MALL): LPR 64: 12.1 us, 32: 12.4, 16: 14.3, 8: 21.0;
+          // the confusion-matrix LPR-64 case goes to mc_argmax_pipe_kernel (8.7 us), TM_AMD_MC_PIPE=0 disables it
           const int lpr = lpr_override ? lpr_override : (row_bytes >= 1024 ? 64 : (row_bytes >= 512 ? 32 : 16));
-          if (lpr == 32) {
+          static const int pipe_override = [] {
+            const char* e = std::getenv("TM_AMD_MC_PIPE");  // tuning knob: blocks per CU of the pipelined kernel
+            return e ? std::atoi(e) : 8;  // measured (8192 x 1000 bf16): 1/CU 23.1 us, 2: 13.9, 4: 10.3, 8: 8.75
+          }();
+          const int per = static_cast<int>((row_bytes / 16 + kWave - 1) / kWave);
+          const bool pipe = pipe_override > 0 && !samplewise && mode == kMcConfmat && per >= 1 && per <= 4 && lpr == 64;
+          if (pipe) {
+            int dev = 0, cus = 256;
+            hipGetDevice(&dev);
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            const long long want = (N + kBlock / kWave - 1) / (kBlock / kWave);
+            const int grid = static_cast<int>(std::min<long long>(want, static_cast<long long>(cus) * pipe_override));
+auto launch_pipe = [&](auto per_tag) {
+              constexpr int P = decltype(per_tag)::value;
+              hipLaunchKernelGGL((mc_argmax_pipe_kernel<scalar_t, target_t, P>), dim3(grid), dim3(kBlock), 0, s, pp,
+                                 tp, N, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp);
+            };
+            if (per == 1) launch_pipe(std::integral_constant<int, 1>{});
+            else if (per == 2) launch_pipe(std::integral_constant<int, 2>{});
+            else if (per == 3) launch_pipe(std::integral_constant<int, 3>{});
+            else launch_pipe(std::integral_constant<int, 4>{});
+          } else if (lpr == 32) {
             constexpr int LPR = 32;
             const int grid = pick_grid(N, (kBlock / kWave) * (kWave / LPR));
             hipLaunchKernelGGL((mc_argmax_subwave_kernel<scalar_t, target_t, LPR>), dim3(grid), dim3(kBlock),

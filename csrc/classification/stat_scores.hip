@@ -806,7 +806,7 @@ auto launch_pipe = [&](auto per_tag) {
           hipLaunchKernelGGL((mc_argmax_rows_kernel<scalar_t, target_t>), dim3(grid), dim3(kBlock), lds_bytes, s, pp,
                              tp, N, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, vec, samplewise);
         } else if (!samplewise && nbins <= 256) {
-          const int grid = pick_grid(N * X, kBlock * 4);
+          const int grid = pick_grid(N * X, kBlock);  // one item per lane: latency-bound, spread wide
           hipLaunchKernelGGL((mc_fewbins_kernel<scalar_t, target_t, true>), dim3(grid), dim3(kBlock), 0, s, pp, tp, N,
                              X, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp);
         } else {
@@ -815,7 +815,7 @@ auto launch_pipe = [&](auto per_tag) {
                              tp, N, X, C, 1, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, samplewise);
         }
       } else if (!samplewise && nbins <= 256 && K == 1) {
-        const int grid = pick_grid(N * X, kBlock * 4);
+        const int grid = pick_grid(N * X, kBlock);
         hipLaunchKernelGGL((mc_fewbins_kernel<scalar_t, target_t, false>), dim3(grid), dim3(kBlock), 0, s, pp, tp, N,
                            X, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp);
       } else {

@@ -182,3 +182,55 @@ def test_audio_modules_gpu():
         (ScaleInvariantSignalDistortionRatio, scale_invariant_signal_distortion_ratio, {}),
     ):
         test_modules_mean_of_batches(cls, fn, kw, device="cuda")
+
+
+def test_srmr_docstring_and_module():
+    from torchmetrics_amd.audio import SpeechReverberationModulationEnergyRatio
+    from torchmetrics_amd.functional.audio import speech_reverberation_modulation_energy_ratio as srmr
+
+    torch.manual_seed(1)
+    preds = torch.randn(8000)
+    out = srmr(preds, 8000)
+    assert out.shape == (1,) and torch.isclose(out, torch.tensor([0.3354], dtype=torch.float64), atol=1e-4).all()
+    m = SpeechReverberationModulationEnergyRatio(8000)
+    m.update(preds)
+    m.update(preds[None].repeat(2, 1))
+    assert torch.isclose(m.compute(), torch.tensor(0.3354), atol=1e-4)
+    assert srmr(torch.randn(2, 3, 4000), 8000, norm=True).shape == (2, 3)
+    with pytest.raises(ModuleNotFoundError):
+        srmr(preds, 8000, fast=True)  # FFT gammatonegram needs the `gammatone` package
+
+
+def test_gammatone_design_unit_gain_at_centre():
+    import numpy as np
+
+    from torchmetrics_amd.functional.audio.srmr import _centre_freqs, _gammatone_sections, _make_erb_filters
+
+    fs = 16000
+    fc = _make_erb_filters(fs, 23, 125.0)
+    imp = torch.zeros(1, 16384, dtype=torch.float64)
+    imp[0, 0] = 1
+    y = ops.biquad_cascade(imp, torch.from_numpy(_gammatone_sections(fc)), rep=23, clamp=False)
+    y = y / torch.from_numpy(fc[:, 9]).reshape(-1, 1)
+    spec = np.abs(np.fft.rfft(y.numpy(), axis=1))
+    freqs = np.fft.rfftfreq(16384, 1 / fs)
+    for i, c in enumerate(_centre_freqs(fs, 23, 125.0)):
+        assert abs(spec[i, np.argmin(np.abs(freqs - c))] - 1.0) < 2e-2
+
+
+@pytest.mark.gpu
+def test_biquad_cascade_kernel_gpu():
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(3, 2000, generator=g, dtype=torch.float64) * 0.1
+    from torchmetrics_amd.functional.audio.srmr import _gammatone_sections, _make_erb_filters
+
+    sec = torch.from_numpy(_gammatone_sections(_make_erb_filters(8000, 23, 125.0))) * 50
+    for clamp in (False, True):
+        got = ops.biquad_cascade(x.cuda(), sec, rep=23, clamp=clamp).cpu()
+        ref = ops.biquad_cascade(x, sec, rep=23, clamp=clamp)
+        assert torch.allclose(got, ref, rtol=1e-9, atol=1e-12)
+    torch.manual_seed(1)
+    preds = torch.randn(8000)
+    from torchmetrics_amd.functional.audio import speech_reverberation_modulation_energy_ratio as srmr
+
+    assert torch.isclose(srmr(preds.cuda(), 8000).cpu(), torch.tensor([0.3354], dtype=torch.float64), atol=1e-4).all()

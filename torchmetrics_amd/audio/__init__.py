@@ -9,6 +9,7 @@ from torchmetrics_amd.audio.metrics import (
     SignalDistortionRatio,
     SignalNoiseRatio,
     SourceAggregatedSignalDistortionRatio,
+    SpeechReverberationModulationEnergyRatio,
 )
 
 __all__ = [
@@ -21,4 +22,5 @@ __all__ = [
     "SignalDistortionRatio",
     "SignalNoiseRatio",
     "SourceAggregatedSignalDistortionRatio",
+    "SpeechReverberationModulationEnergyRatio",
 ]

@@ -10,6 +10,7 @@ from torchmetrics_amd.functional.audio.external import (
     short_time_objective_intelligibility,
 )
 from torchmetrics_amd.functional.audio.pit import permutation_invariant_training
+from torchmetrics_amd.functional.audio.srmr import _srmr_arg_validate, speech_reverberation_modulation_energy_ratio
 from torchmetrics_amd.functional.audio.snr_sdr import (
     complex_scale_invariant_signal_noise_ratio,
     scale_invariant_signal_distortion_ratio,
@@ -199,3 +200,23 @@ class ShortTimeObjectiveIntelligibility(_MeanOfBatch):
 
     def _batch(self, preds: Tensor, target: Tensor) -> Tensor:
         return short_time_objective_intelligibility(preds, target, self.fs, self.extended, False)
+
+
+class SpeechReverberationModulationEnergyRatio(_MeanOfBatch):
+    """SRMR (``S/audio/srmr.py:37``); native gammatone / modulation filterbanks (no ``gammatone`` / ``torchaudio``)."""
+
+    higher_is_better: bool = True
+    _sum_name = "msum"
+
+    def __init__(self, fs: int, n_cochlear_filters: int = 23, low_freq: float = 125, min_cf: float = 4,
+                 max_cf: Optional[float] = None, norm: bool = False, fast: bool = False, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        _srmr_arg_validate(fs, n_cochlear_filters, low_freq, min_cf, max_cf, norm, fast)
+        self.fs, self.n_cochlear_filters, self.low_freq = fs, n_cochlear_filters, low_freq
+        self.min_cf, self.max_cf, self.norm, self.fast = min_cf, max_cf, norm, fast
+
+    def update(self, preds: Tensor) -> None:  # type: ignore[override]
+        v = speech_reverberation_modulation_energy_ratio(preds, self.fs, self.n_cochlear_filters, self.low_freq,
+                                                         self.min_cf, self.max_cf, self.norm, self.fast)
+        self.msum += v.sum().to(self.msum)
+        self.total += v.numel()

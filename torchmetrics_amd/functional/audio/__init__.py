@@ -4,6 +4,7 @@ from torchmetrics_amd.functional.audio.external import (
     short_time_objective_intelligibility,
 )
 from torchmetrics_amd.functional.audio.pit import permutation_invariant_training, pit_permutate
+from torchmetrics_amd.functional.audio.srmr import speech_reverberation_modulation_energy_ratio
 from torchmetrics_amd.functional.audio.snr_sdr import (
     complex_scale_invariant_signal_noise_ratio,
     scale_invariant_signal_distortion_ratio,
@@ -24,4 +25,5 @@ __all__ = [
     "signal_distortion_ratio",
     "signal_noise_ratio",
     "source_aggregated_signal_distortion_ratio",
+    "speech_reverberation_modulation_energy_ratio",
 ]

@@ -430,3 +430,17 @@ def stat_reduce(tp: Tensor, fp: Tensor, tn: Tensor, fn: Tensor, kind: int, avera
     _ops().stat_reduce(tp.contiguous(), fp.contiguous(), tn.contiguous(), fn.contiguous(), out, int(kind),
                        int(average), bool(multilabel), float(beta))
     return out.reshape(tp.shape[0], -1) if average == 3 else out
+
+
+def biquad_cascade(x: Tensor, coefs: Tensor, rep: int, clamp: bool) -> Tensor:
+    """Filter signals ``x [S, T]`` through per-filter cascades of biquads ``coefs [F, sections, 6]``
+    ((b0, b1, b2, a0, a1, a2) per section); output row ``r`` = signal ``r // rep`` through filter ``r % F``
+    (``csrc/audio/iir.hip``, fp64).  ``clamp`` clamps every section's output to [-1, 1] like
+    ``torchaudio.functional.lfilter(clamp=True)``."""
+    xs = x.double().contiguous()
+    cf = coefs.double().contiguous()
+    if xs.is_cuda:
+        y = torch.empty(xs.shape[0] * rep, xs.shape[1], dtype=torch.float64, device=xs.device)
+        _ops().biquad_cascade(xs, cf.to(xs.device), y, int(rep), bool(clamp))
+        return y
+    return _cpu.biquad_cascade(xs, cf, rep, clamp)

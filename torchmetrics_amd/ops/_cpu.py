@@ -452,3 +452,21 @@ def lpips_layer(f0: Tensor, f1: Tensor, w: Tensor, eps: float) -> Tensor:
     n1 = f1 / (torch.sqrt((f1**2).sum(1, keepdim=True)) + eps)
     d = ((n0 - n1) ** 2 * w.reshape(1, -1, 1, 1)).sum(1)
     return d.mean(dim=(-2, -1))
+
+
+def biquad_cascade(x: Tensor, coefs: Tensor, rep: int, clamp: bool) -> Tensor:
+    from scipy.signal import lfilter
+
+    xs = x.numpy()
+    n_f = coefs.shape[0]
+    rows = []
+    for r in range(xs.shape[0] * rep):
+        v = xs[r // rep]
+        for sec in coefs[r % n_f].numpy():
+            v = lfilter(sec[:3], sec[3:], v)
+            if clamp:
+                v = v.clip(-1.0, 1.0)
+        rows.append(v)
+    import numpy as np
+
+    return torch.from_numpy(np.stack(rows)) if rows else torch.zeros(0, x.shape[1], dtype=torch.float64)

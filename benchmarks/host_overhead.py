@@ -33,10 +33,30 @@ def main():
     cm = torch.zeros(C * C, dtype=torch.int64, device=dev)
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
     m = tm.MulticlassConfusionMatrix(C).to(dev)
+    from torchmetrics_amd.functional.classification.confusion_matrix import (
+        _multiclass_confusion_matrix_tensor_validation as _val,
+    )
+
+    class _Noop(tm.Metric):
+        full_state_update = False
+
+        def update(self, p, t):
+            pass
+
+        def compute(self):
+            return 0
+
+    noop = _Noop().to(dev)
     m2 = tm.MulticlassConfusionMatrix(C, validate_args=False).to(dev)
     acc = tm.MulticlassAccuracy(C).to(dev)
     res = {
         "raw_torch_ops_call_us": rate(lambda: torch.ops.tm_amd.mc_update(preds, target, cm, flag, C, 0, False, 0, False)),
+        "raw_fastcall_us": rate(lambda: ops._fast_mod.mc_update(preds, target, cm, flag, C, 0, False, 0, False)),
+        "fastcall_args_only_us": rate(lambda: ops._fast_mod.arg_probe(preds, target, cm, flag, C, 0, False, 0, False)),
+        "fastcall_empty_launch_us": rate(lambda: ops._fast_mod.launch_probe(flag)),
+        "validation_only_us": rate(lambda: _val(preds, target, C, None)),
+        "preds.device_us": rate(lambda: preds.device),
+        "wrapper_noop_update_us": rate(lambda: noop.update(preds, target)),
         "ops.mc_update_us": rate(lambda: ops.mc_update(preds, target, cm, flag, C, None, 0, False)),
         "MulticlassConfusionMatrix.update_us": rate(lambda: m.update(preds, target)),
         "MulticlassConfusionMatrix(validate_args=False).update_us": rate(lambda: m2.update(preds, target)),

@@ -210,6 +210,134 @@ __global__ void __launch_bounds__(kBlock) mc_argmax_pipe_kernel(const scalar_t* 
   }
 }
 
+// 16-bit float rows (bf16 / fp16): argmax on packed 16-bit ordinals.  A sign-magnitude half h maps to the
+// order-preserving ordinal  h ^ ((h >>a 15) | 0x8000)  -- two halves per 32-bit word with v_pk_ashrrev_i16 + or + xor,
+// folded into a lane max / min with v_pk_max_u16 / v_pk_min_u16.  A reverse scan then finds the lane's first column
+// holding its max and ONE wave max over (ordinal << 16 | 0xffff - column) yields torch.argmax's first-max column.
+// Rows where that shortcut is not exact fall back, wave-uniformly, to the float compare on the same registers:
+// any NaN (positive NaN ordinals sit above +inf, negative ones below -inf) and a max of +-0 (-0 == +0 ties by index).
+// Measured on MI355X (8192 x 1000 bf16, 8 blocks/CU): 5.2 us vs 8.1 us for the float-compare wave argmax, against a
+// 3.3 us back-to-back empty-launch floor -- the float compare made the kernel VALU-bound (tools/mb/confmat_mb.hip).
+template <typename scalar_t>
+struct Ord16;
+template <>
+struct Ord16<c10::BFloat16> {
+  static constexpr uint32_t kPosInf = 0xff80u, kNegInf = 0x007fu;
+};
+template <>
+struct Ord16<c10::Half> {
+  static constexpr uint32_t kPosInf = 0xfc00u, kNegInf = 0x03ffu;
+};
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  return static_cast<uint32_t>(__reduce_max_sync(~0ull, static_cast<int>(v ^ 0x80000000u))) ^ 0x80000000u;
+}
+
+template <typename scalar_t, typename target_t, int kPer>
+__global__ void __launch_bounds__(kBlock) mc_argmax_ord16_kernel(const scalar_t* __restrict__ preds,
+                                                                 const target_t* __restrict__ target, long long N,
+                                                                 int C, long long ignore, bool has_ignore,
+                                                                 int64_t* __restrict__ out, int* __restrict__ flag) {
+  static_assert(sizeof(scalar_t) == 2, "16-bit floats only");
+  const int lane = threadIdx.x & (kWave - 1);
+  const long long nwaves = static_cast<long long>(gridDim.x) * (blockDim.x / kWave);
+  const long long wave = (static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
+  const int nchunks = C / 8;
+  u32x4 cur[kPer], nxt[kPer];
+  long long tcur = 0, tnxt = 0;
+  auto issue = [&](long long row, u32x4* buf, long long& t) {
+    const u32x4* rp = reinterpret_cast<const u32x4*>(preds + row * C);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int ci = lane + j * kWave;
+      if (ci < nchunks) buf[j] = __builtin_nontemporal_load(rp + ci);
+    }
+    if (lane == 0) t = static_cast<long long>(target[row]);
+  };
+  long long row = wave;
+  if (row < N) issue(row, cur, tcur);
+  for (; row < N; row += nwaves) {  // wave-uniform
+    const long long next = row + nwaves;
+    if (next < N) issue(next, nxt, tnxt);
+    u16x2 mx = {0, 0}, mn = {0xffff, 0xffff};
+    uint32_t ordw[kPer][4];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int ci = lane + j * kWave;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t w = cur[j][k];
+        const s16x2 sw = __builtin_bit_cast(s16x2, w);
+        const uint32_t sgn = __builtin_bit_cast(uint32_t, static_cast<s16x2>(sw >> (s16x2){15, 15}));
+        const uint32_t o = w ^ (sgn | 0x80008000u);
+        ordw[j][k] = o;
+        if (ci < nchunks) {
+          const u16x2 ov = __builtin_bit_cast(u16x2, o);
+          mx = __builtin_elementwise_max(mx, ov);
+          mn = __builtin_elementwise_min(mn, ov);
+        }
+      }
+    }
+    const uint32_t lmax = mx.x > mx.y ? mx.x : mx.y;
+    const uint32_t lmin = mn.x < mn.y ? mn.x : mn.y;
+    uint32_t first = 0xffffu;  // lane's first column holding lmax (reverse scan: the last hit is the first column)
+#pragma unroll
+    for (int j = kPer - 1; j >= 0; --j) {
+      const int ci = lane + j * kWave;
+      if (ci < nchunks) {
+#pragma unroll
+        for (int k = 3; k >= 0; --k) {
+          const uint32_t o = ordw[j][k];
+          if ((o >> 16) == lmax) first = ci * 8 + 2 * k + 1;
+          if ((o & 0xffffu) == lmax) first = ci * 8 + 2 * k;
+        }
+      }
+    }
+    const uint32_t key = wave_max_u32((lmax << 16) | (0xffffu - first));
+    const uint32_t kmax = key >> 16;
+    const bool exact = kmax <= Ord16<scalar_t>::kPosInf && kmax != 0x8000u && kmax != 0x7fffu &&
+                       !__any(lmin < Ord16<scalar_t>::kNegInf);
+    int bidx = 0xffff - static_cast<int>(key & 0xffffu);
+    if (!exact) {  // wave-uniform, rare
+      float best = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int ci = lane + j * kWave;
+        if (ci < nchunks) {
+          const scalar_t* e = reinterpret_cast<const scalar_t*>(&cur[j]);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float v = to_f32(e[k]);
+            if (argmax_better(v, ci * 8 + k, best, bi)) {
+              best = v;
+              bi = ci * 8 + k;
+            }
+          }
+        }
+      }
+      wave_argmax(best, bi);
+      bidx = bi;
+    }
+    if (lane == 0) {
+      const long long t = tcur;
+      bool ok = true;
+      if (has_ignore && t == ignore) ok = false;
+      else if (t < 0 || t >= C) {
+        raise_flag(flag, kErrTargetOutOfRange);
+        ok = false;
+      }
+      if (ok) atomic_add_i64(out + static_cast<long long>(t) * C + bidx, 1);
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) cur[j] = nxt[j];
+    tcur = tnxt;
+  }
+}
+
 template <typename scalar_t, typename target_t, int LPR>
 __global__ void __launch_bounds__(kBlock) mc_argmax_subwave_kernel(const scalar_t* __restrict__ preds,
                                                                    const target_t* __restrict__ target, long long N,
@@ -761,13 +889,19 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
           const int per = static_cast<int>((row_bytes / 16 + kWave - 1) / kWave);
           const bool pipe = pipe_override > 0 && !samplewise && mode == kMcConfmat && per >= 1 && per <= 4 && lpr == 64;
           if (pipe) {
-            int dev = 0, cus = 256;
-            hipGetDevice(&dev);
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            const int cus = cu_count(preds.get_device());
             const long long want = (N + kBlock / kWave - 1) / (kBlock / kWave);
             const int grid = static_cast<int>(std::min<long long>(want, static_cast<long long>(cus) * pipe_override));
-auto launch_pipe = [&](auto per_tag) {
+            static const bool ord16_off = std::getenv("TM_AMD_MC_ORD16") && std::atoi(std::getenv("TM_AMD_MC_ORD16")) == 0;
+            auto launch_pipe = [&](auto per_tag) {
               constexpr int P = decltype(per_tag)::value;
+              if constexpr (sizeof(scalar_t) == 2) {
+                if (!ord16_off) {
+                  hipLaunchKernelGGL((mc_argmax_ord16_kernel<scalar_t, target_t, P>), dim3(grid), dim3(kBlock), 0, s,
+                                     pp, tp, N, C, ignore_index, has_ignore, outp, flagp);
+                  return;
+                }
+              }
               hipLaunchKernelGGL((mc_argmax_pipe_kernel<scalar_t, target_t, P>), dim3(grid), dim3(kBlock), 0, s, pp,
                                  tp, N, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp);
             };
@@ -913,6 +1047,15 @@ void bin_confmat_finalize(at::Tensor ws, at::Tensor not_prob, at::Tensor confmat
                      ws.data_ptr<int64_t>(), G, not_prob.data_ptr<int>(), confmat.data_ptr<int64_t>());
   hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
   C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+__global__ void launch_probe_kernel(int* __restrict__ flag) {
+  if (threadIdx.x == 1000) flag[0] = 0;  // never taken: an empty dispatch with one real argument
+}
+
+// Host-cost probe: one empty kernel launch on the current stream (benchmarks/host_overhead.py).
+void launch_probe(at::Tensor flag) {
+  hipLaunchKernelGGL(launch_probe_kernel, dim3(1), dim3(64), 0, stream(), flag.data_ptr<int>());
 }
 
 }  // namespace tm_amd

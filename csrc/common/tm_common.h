@@ -138,6 +138,18 @@ inline int grid_cap(long long blocks, int cap = 256 * 16) {
 
 inline hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
 
+// CU count of a device, queried once per device (hipDeviceGetAttribute costs host time on every call).
+inline int cu_count(int device) {
+  static int cache[64] = {0};
+  if (device < 0 || device >= 64) device = 0;
+  int v = cache[device];
+  if (v == 0) {
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || v <= 0) v = 256;
+    cache[device] = v;
+  }
+  return v;
+}
+
 #define TM_CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a ROCm (cuda) tensor")
 #define TM_CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
 

@@ -64,6 +64,40 @@ def test_multiclass_argmax_ties_and_nan():
     assert torch.equal(g, c)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("C", [512, 1000, 1024, 1536, 2048])
+def test_multiclass_argmax_ord16_edge_rows(dtype, C):
+    """The packed-ordinal argmax kernel (16-bit rows of >= 1 KiB) on the rows its shortcut must hand to the float
+    compare: +NaN / -NaN (several, different payloads), -0 vs +0 maxima, +-inf, all-equal rows, all-negative rows."""
+    N = 20000  # > one row per wave of the persistent grid: exercises the cross-row prefetch
+    g = torch.Generator().manual_seed(C)
+    preds = torch.randn(N, C, generator=g).to(dtype)
+    bits = preds.view(torch.int16)
+    nan_pos, nan_neg = (0x7FC1, -0x3F) if dtype == torch.bfloat16 else (0x7E01, -0x1FF)  # -0x3F == 0xFFC1
+    for r in range(0, 64):
+        bits[r, (r * 37) % C] = nan_pos if r & 1 else nan_neg
+        bits[r, (r * 11) % C] = nan_neg if r & 2 else nan_pos + 2
+    preds[64:96] = -torch.rand(32, C, generator=g).to(dtype) - 1  # all negative, ties unlikely
+    preds[96:128] = 0.0
+    preds[96:112, 5] = -0.0
+    preds[112:128] = -torch.rand(16, C, generator=g).to(dtype)
+    preds[112:128, C - 1] = 0.0
+    preds[112:128, 7] = -0.0
+    preds[128:160] = float("inf")
+    preds[160:192] = float("-inf")
+    preds[192:224] = 1.0
+    preds[224:256, C // 2] = float("inf")
+    preds[224:256, C // 3] = float("inf")
+    target = torch.randint(0, C, (N,), generator=g)
+    target[::13] = -100
+    gpu, fg = _mc(preds, target, C, -100, ops.MC_CONFMAT, False, DEV)
+    ref = torch.zeros(C * C, dtype=torch.int64)
+    keep = target != -100
+    ref += torch.bincount(target[keep] * C + preds.float().argmax(1)[keep], minlength=C * C)
+    assert torch.equal(gpu, ref)
+    assert fg == 0
+
+
 def test_multiclass_flags_out_of_range():
     preds = torch.randn(100, 5)
     target = torch.randint(0, 5, (100,))

@@ -3,6 +3,8 @@
 
 Every ``csrc/**/*.hip`` / ``*.cpp`` is compiled to an object under ``build/`` (in parallel, incremental on mtime),
 then linked into ``torchmetrics_amd/_C/libtm_amd.so``, which registers the ``torch.ops.tm_amd.*`` operators.
+``csrc/bindings/fastcall.cpp`` becomes the CPython extension ``torchmetrics_amd/_C/_fastcall.so`` (dispatcher-free
+entry points of the per-batch hot ops), linked against ``libtm_amd.so``.
 
 Usage: ``python tools/build_ext.py [-j N] [--force] [--arch gfx950]``
 """
@@ -18,6 +20,8 @@ ROOT = Path(__file__).resolve().parents[1]
 CSRC = ROOT / "csrc"
 BUILD = ROOT / "build" / "obj"
 OUT = ROOT / "torchmetrics_amd" / "_C" / "libtm_amd.so"
+FAST_SRC = CSRC / "bindings" / "fastcall.cpp"
+FAST_OUT = ROOT / "torchmetrics_amd" / "_C" / "_fastcall.so"
 
 
 def _torch_paths():
@@ -31,7 +35,7 @@ def _torch_paths():
 
 
 def _sources():
-    return sorted(p for p in CSRC.rglob("*") if p.suffix in (".hip", ".cpp"))
+    return sorted(p for p in CSRC.rglob("*") if p.suffix in (".hip", ".cpp") and p.parent.name != "bindings")
 
 
 def _headers_mtime():
@@ -98,6 +102,32 @@ def link(objs, out: Path) -> None:
         raise RuntimeError("link failed")
 
 
+def build_fastcall(force: bool = False, verbose: bool = True) -> Path:
+    """Host-only C++ (no device code): Python + torch_python headers, linked to libtm_amd.so via $ORIGIN."""
+    import sysconfig
+
+    if not force and FAST_OUT.exists() and FAST_OUT.stat().st_mtime >= max(FAST_SRC.stat().st_mtime, OUT.stat().st_mtime):
+        if verbose:
+            print(f"[build_ext] {FAST_OUT.relative_to(ROOT)} up to date")
+        return FAST_OUT
+    inc, lib, abi = _torch_paths()
+    cmd = [
+        "g++", "-O2", "-fPIC", "-shared", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
+        "-D__HIP_PLATFORM_AMD__=1", "-Wno-deprecated-declarations",
+        f"-I{sysconfig.get_paths()['include']}", *[f"-I{p}" for p in inc], "-I/opt/rocm/include",
+        str(FAST_SRC), "-o", str(FAST_OUT),
+        f"-L{OUT.parent}", "-ltm_amd", f"-L{lib}", "-ltorch_python", "-ltorch", "-ltorch_cpu", "-lc10",
+        "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{lib}",
+    ]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        sys.stderr.write(res.stdout + res.stderr)
+        raise RuntimeError("fastcall build failed")
+    if verbose:
+        print(f"[build_ext] built {FAST_OUT.relative_to(ROOT)}")
+    return FAST_OUT
+
+
 def build(arch: str = "gfx950", jobs: int = 8, force: bool = False, verbose: bool = True) -> Path:
     srcs = _sources()
     hdr = _headers_mtime()
@@ -110,6 +140,7 @@ def build(arch: str = "gfx950", jobs: int = 8, force: bool = False, verbose: boo
             print(f"[build_ext] linked {OUT.relative_to(ROOT)} from {len(objs)} objects ({arch})")
     elif verbose:
         print(f"[build_ext] {OUT.relative_to(ROOT)} up to date")
+    build_fastcall(force=force, verbose=verbose)
     return OUT
 
 

@@ -48,8 +48,18 @@ class _ConfmatBase(Metric):
         return None
 
     def _accumulate(self, fn: Any, preds: Tensor, *args: Any) -> None:
-        flag = self._device_error_buffer(preds.device) if self.validate_args else None
-        target_cm = self._confmat_target(preds.device)
+        # device checks by index (Tensor.get_device is ~3x cheaper than building and comparing torch.device objects)
+        dev = preds.get_device()
+        flag = None
+        if self.validate_args:
+            flag = self._device_errors
+            if flag is None or flag.get_device() != dev:
+                flag = self._device_error_buffer(preds.device)
+        cm = self.confmat
+        if isinstance(cm, Tensor) and cm.get_device() == dev and cm.dtype is torch.long and cm.is_contiguous():
+            target_cm = cm
+        else:
+            target_cm = self._confmat_target(preds.device)
         if target_cm is None:
             tmp = torch.zeros_like(self.confmat, dtype=torch.long, device=preds.device)
             fn(preds, *args[:1], tmp, *args[1:], flag)

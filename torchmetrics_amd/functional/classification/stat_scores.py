@@ -96,7 +96,8 @@ def _multiclass_stat_scores_tensor_validation(
     multidim_average: str = "global",
     ignore_index: Optional[int] = None,
 ) -> None:
-    if preds.ndim == target.ndim + 1:
+    pnd = preds.ndim
+    if pnd == target.ndim + 1:
         if not preds.is_floating_point():
             raise ValueError("If `preds` have one dimension more than `target`, `preds` should be a float tensor.")
         if preds.shape[1] != num_classes:
@@ -104,7 +105,7 @@ def _multiclass_stat_scores_tensor_validation(
                 "If `preds` have one dimension more than `target`, `preds.shape[1]` should be"
                 " equal to number of classes."
             )
-        if preds.shape[2:] != target.shape[1:]:
+        if pnd > 2 and preds.shape[2:] != target.shape[1:]:
             raise ValueError(
                 "If `preds` have one dimension more than `target`, the shape of `preds` should be"
                 " (N, C, ...), and the shape of `target` should be (N, ...)."
@@ -114,7 +115,7 @@ def _multiclass_stat_scores_tensor_validation(
                 "If `preds` have one dimension more than `target`, the shape of `preds` should "
                 " at least 3D when multidim_average is set to `samplewise`"
             )
-    elif preds.ndim == target.ndim:
+    elif pnd == target.ndim:
         if preds.shape != target.shape:
             raise ValueError(
                 "The `preds` and `target` should have the same shape,",

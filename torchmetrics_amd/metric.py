@@ -314,27 +314,36 @@ class Metric(Module, ABC):
             setattr(self, attr, fn(val) if fn is not None else val)
 
     def _wrap_update(self, update: Callable) -> Callable:
+        # Host cost matters here: an MI355X update kernel runs in a few us, so this wrapper writes its bookkeeping
+        # straight into __dict__ (nn.Module.__setattr__ costs ~1 us per call) and flips grad mode with the raw C
+        # toggle instead of a context-manager object.
+        state = self.__dict__
+        set_grad = torch._C._set_grad_enabled
+
         @functools.wraps(update)
         def wrapped_func(*args: Any, **kwargs: Any) -> None:
-            self._computed = None
-            self._update_count += 1
-            grad_ctx = (
-                _NULL_CTX if torch.is_grad_enabled() == self._enable_grad else torch.set_grad_enabled(self._enable_grad)
-            )
-            with grad_ctx:
-                try:
-                    update(*args, **kwargs)
-                except RuntimeError as err:
-                    if "Expected all tensors to be on" in str(err):
-                        raise RuntimeError(
-                            "Encountered different devices in metric calculation (see stacktrace for details)."
-                            " This could be due to the metric class not being on the same device as input."
-                            f" Instead of `metric={self.__class__.__name__}(...)` try to do"
-                            f" `metric={self.__class__.__name__}(...).to(device)` where"
-                            " device corresponds to the device of the input."
-                        ) from err
-                    raise err
-            if _validation.STRICT and self._device_errors is not None:
+            state["_computed"] = None
+            state["_update_count"] += 1
+            prev = torch.is_grad_enabled()
+            want = state["_enable_grad"]
+            if prev != want:
+                set_grad(want)
+            try:
+                update(*args, **kwargs)
+            except RuntimeError as err:
+                if "Expected all tensors to be on" in str(err):
+                    raise RuntimeError(
+                        "Encountered different devices in metric calculation (see stacktrace for details)."
+                        " This could be due to the metric class not being on the same device as input."
+                        f" Instead of `metric={self.__class__.__name__}(...)` try to do"
+                        f" `metric={self.__class__.__name__}(...).to(device)` where"
+                        " device corresponds to the device of the input."
+                    ) from err
+                raise err
+            finally:
+                if prev != want:
+                    set_grad(prev)
+            if _validation.STRICT and state["_device_errors"] is not None:
                 self._raise_device_errors()
             if self.compute_on_cpu:
                 self._move_list_states_to_cpu()

@@ -4,6 +4,9 @@ Every op has exactly two implementations, selected by the *device of its inputs*
 
 * ROCm tensors (``tensor.is_cuda``) -> ``torch.ops.tm_amd.*`` HIP kernels for gfx950.  If the library is missing
   on a GPU host the call raises: there is no silent eager fallback on the GPU.
+  The per-batch hot ops (``mc_update``, ``bin_update``, ``moments_update``, the stat-score finalizers and
+  ``stat_reduce``) enter the same C++ launchers through ``_C/_fastcall.so`` (``csrc/bindings/fastcall.cpp``), a
+  METH_FASTCALL CPython module that skips the boxed dispatcher call (~5.5 us -> ~1.5 us of host time per update).
 * CPU tensors -> the host implementation in :mod:`torchmetrics_amd.ops._cpu` (ATen ops), which is the CPU
   device implementation of the same contract (used by CPU/gloo runs and as the numerics oracle in tests).
 """
@@ -18,8 +21,45 @@ from torch import Tensor
 from torchmetrics_amd.ops import _cpu
 
 _LIB_PATH = Path(__file__).resolve().parent.parent / "_C" / "libtm_amd.so"
+_FAST_PATH = _LIB_PATH.parent / "_fastcall.so"
 _lock = threading.Lock()
-_state = {"loaded": False, "error": None}
+_state = {"loaded": False, "error": None, "fast_error": None}
+_fast_mod = None  # the _fastcall extension module once loaded (or a torch.ops shim if it could not be)
+
+
+class _DispatcherShim:
+    """``_fastcall`` stand-in routing through ``torch.ops.tm_amd`` (used only if ``_fastcall.so`` failed to load)."""
+
+    def __getattr__(self, name):
+        op = getattr(torch.ops.tm_amd, name)
+        if name in ("mc_update", "bin_update", "moments_update", "stat_reduce"):
+            ncontig = 4 if name == "stat_reduce" else 2
+
+            def call(*args, _op=op, _n=ncontig):
+                return _op(*[a.contiguous() for a in args[:_n]], *args[_n:])
+
+            return call
+        return op
+
+
+def _load_fastcall() -> None:
+    global _fast_mod
+    import importlib.util
+
+    try:
+        spec = importlib.util.spec_from_file_location("_fastcall", _FAST_PATH)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _fast_mod = mod
+    except Exception as err:  # noqa: BLE001 - the dispatcher path is the same native code, just slower to enter
+        _state["fast_error"] = err
+        _fast_mod = _DispatcherShim()
+
+
+def _fast():
+    if _fast_mod is None:
+        load_native(strict=True)
+    return _fast_mod
 
 
 def native_library_path() -> Path:
@@ -40,6 +80,7 @@ def load_native(strict: bool = True) -> bool:
                     "(or `python -c 'import __graft_entry__ as g; g.build()'`)"
                 )
             torch.ops.load_library(str(_LIB_PATH))
+            _load_fastcall()
             _state["loaded"] = True
         except Exception as err:  # noqa: BLE001
             _state["error"] = err
@@ -79,9 +120,9 @@ def mc_update(
     ``mode=MC_CONFMAT`` accumulates ``out[C, C]``; ``mode=MC_STATS`` accumulates the ``[G, 3C+1]`` workspace.
     """
     if preds.is_cuda:
-        _ops().mc_update(
-            preds.contiguous(), target.contiguous(), out, flag, int(num_classes),
-            int(ignore_index) if ignore_index is not None else 0, ignore_index is not None, int(mode), bool(samplewise),
+        (_fast_mod or _fast()).mc_update(
+            preds, target, out, flag, num_classes, 0 if ignore_index is None else ignore_index,
+            ignore_index is not None, mode, samplewise,
         )
     else:
         _cpu.mc_update(preds, target, out, flag, num_classes, ignore_index, mode, samplewise)
@@ -90,7 +131,7 @@ def mc_update(
 def mc_stats_finalize(ws: Tensor, num_classes: int, micro: bool, accumulate: bool, tp: Tensor, fp: Tensor,
                       tn: Tensor, fn: Tensor) -> None:
     if ws.is_cuda:
-        _ops().mc_stats_finalize(ws, int(num_classes), bool(micro), bool(accumulate), tp, fp, tn, fn)
+        (_fast_mod or _fast()).mc_stats_finalize(ws, num_classes, micro, accumulate, tp, fp, tn, fn)
     else:
         _cpu.mc_stats_finalize(ws, num_classes, micro, accumulate, tp, fp, tn, fn)
 
@@ -103,10 +144,9 @@ def bin_update(preds: Tensor, target: Tensor, ws: Tensor, flag: Tensor, not_prob
     ``prob_check_all=False`` excludes ignored positions from the logits-vs-probabilities decision.
     """
     if preds.is_cuda:
-        _ops().bin_update(
-            preds.contiguous(), target.contiguous(), ws, flag, not_prob, int(num_labels), float(threshold),
-            int(ignore_index) if ignore_index is not None else 0, ignore_index is not None, bool(samplewise),
-            bool(prob_check_all),
+        (_fast_mod or _fast()).bin_update(
+            preds, target, ws, flag, not_prob, num_labels, float(threshold),
+            0 if ignore_index is None else ignore_index, ignore_index is not None, samplewise, prob_check_all,
         )
     else:
         _cpu.bin_update(preds, target, ws, flag, not_prob, num_labels, threshold, ignore_index, samplewise,
@@ -116,7 +156,7 @@ def bin_update(preds: Tensor, target: Tensor, ws: Tensor, flag: Tensor, not_prob
 def bin_confmat_finalize(ws: Tensor, not_prob: Tensor, confmat: Tensor) -> None:
     """Fold a ``[G, 7]`` workspace into ``[G, 2, 2]`` confusion matrices (in place) and re-zero it."""
     if ws.is_cuda:
-        _ops().bin_confmat_finalize(ws, not_prob, confmat)
+        (_fast_mod or _fast()).bin_confmat_finalize(ws, not_prob, confmat)
     else:
         _cpu.bin_confmat_finalize(ws, not_prob, confmat)
 
@@ -124,7 +164,7 @@ def bin_confmat_finalize(ws: Tensor, not_prob: Tensor, confmat: Tensor) -> None:
 def bin_stats_finalize(ws: Tensor, not_prob: Tensor, accumulate: bool, tp: Tensor, fp: Tensor, tn: Tensor,
                        fn: Tensor) -> None:
     if ws.is_cuda:
-        _ops().bin_stats_finalize(ws, not_prob, bool(accumulate), tp, fp, tn, fn)
+        (_fast_mod or _fast()).bin_stats_finalize(ws, not_prob, accumulate, tp, fp, tn, fn)
     else:
         _cpu.bin_stats_finalize(ws, not_prob, accumulate, tp, fp, tn, fn)
 
@@ -175,9 +215,10 @@ def moments_update(
             dt = torch.promote_types(preds.dtype, target.dtype)
             dt = dt if dt.is_floating_point else torch.float32
             preds, target = preds.to(dt), target.to(dt)
-        res = _ops().moments_update(
-            preds.contiguous(), target.contiguous(), int(num_outputs), mask, float(eps), float(power),
-            shift_p, shift_t, list(dests), [int(i) for i in dest_ids], bool(want_sums),
+        res = (_fast_mod or _fast()).moments_update(
+            preds, target, num_outputs, mask, float(eps), float(power), shift_p, shift_t,
+            dests if isinstance(dests, (list, tuple)) else list(dests),
+            dest_ids if isinstance(dest_ids, (list, tuple)) else list(dest_ids), want_sums,
         )
         return res if want_sums else None
     return _cpu.moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_t, dests, dest_ids,
@@ -427,8 +468,7 @@ def stat_reduce(tp: Tensor, fp: Tensor, tn: Tensor, fn: Tensor, kind: int, avera
     """Fused stat-score compute on ``[R, C]`` int64 states (``csrc/classification/stat_reduce.hip``): ``[R]`` for
     micro / macro / weighted (ids 0 / 1 / 2), ``[R, C]`` for none (3)."""
     out = torch.empty(tp.shape[0] * (tp.shape[1] if average == 3 else 1), dtype=torch.float32, device=tp.device)
-    _ops().stat_reduce(tp.contiguous(), fp.contiguous(), tn.contiguous(), fn.contiguous(), out, int(kind),
-                       int(average), bool(multilabel), float(beta))
+    (_fast_mod or _fast()).stat_reduce(tp, fp, tn, fn, out, kind, average, multilabel, float(beta))
     return out.reshape(tp.shape[0], -1) if average == 3 else out
 
 

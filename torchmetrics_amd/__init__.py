@@ -10,6 +10,10 @@ _logger = __logging.getLogger("torchmetrics_amd")
 _logger.addHandler(__logging.StreamHandler())
 _logger.setLevel(__logging.INFO)
 
+from torchmetrics_amd import _module_aliases  # noqa: E402
+
+_module_aliases.install()
+
 from torchmetrics_amd import functional  # noqa: E402,F401
 from torchmetrics_amd.aggregation import (  # noqa: E402
     CatMetric,

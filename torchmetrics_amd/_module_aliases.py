@@ -1,0 +1,140 @@
+"""Reference module paths as import aliases.
+
+The reference spreads every metric over its own file (``torchmetrics/text/wer.py``,
+``torchmetrics/functional/regression/mse.py``, ...).  This package groups each domain into a few modules, so the
+reference's per-file paths are provided as aliases: ``import torchmetrics_amd.text.wer`` (or
+``from torchmetrics_amd.functional.regression.mse import mean_squared_error``) yields a module carrying the public
+names of its domain package.  The aliases are resolved lazily by a ``sys.meta_path`` finder that only answers for
+the names listed here, after the regular finders have failed; it never shadows a real module.
+"""
+import importlib
+import importlib.abc
+import importlib.util
+import sys
+from typing import Dict, Optional, Tuple
+
+# domain package (relative to torchmetrics_amd) -> reference submodule names that alias it
+_TABLE: Dict[str, Tuple[str, ...]] = {
+    "audio": (
+        "_deprecated", "pesq", "pit", "sdr", "snr", "srmr", "stoi",
+    ),
+    "classification": (
+        "auroc", "average_precision", "calibration_error", "cohen_kappa", "dice", "exact_match",
+        "group_fairness", "hinge", "jaccard", "matthews_corrcoef", "precision_fixed_recall", "ranking",
+        "recall_fixed_precision", "roc", "sensitivity_specificity", "specificity_sensitivity",
+    ),
+    "clustering": (
+        "adjusted_mutual_info_score", "adjusted_rand_score", "calinski_harabasz_score",
+        "davies_bouldin_score", "dunn_index", "fowlkes_mallows_index",
+        "homogeneity_completeness_v_measure", "mutual_info_score", "normalized_mutual_info_score",
+        "rand_score",
+    ),
+    "detection": (
+        "_deprecated", "ciou", "diou", "giou",
+    ),
+    "functional.audio": (
+        "_deprecated", "pesq", "sdr", "snr", "stoi",
+    ),
+    "functional.classification": (
+        "precision_fixed_recall", "sensitivity_specificity", "specificity_sensitivity",
+    ),
+    "functional.clustering": (
+        "adjusted_mutual_info_score", "adjusted_rand_score", "calinski_harabasz_score",
+        "davies_bouldin_score", "dunn_index", "fowlkes_mallows_index",
+        "homogeneity_completeness_v_measure", "mutual_info_score", "normalized_mutual_info_score",
+        "rand_score", "utils",
+    ),
+    "functional.detection": (
+        "_deprecated", "_panoptic_quality_common", "ciou", "diou", "giou",
+    ),
+    "functional.image": (
+        "_deprecated", "d_lambda", "d_s", "ergas", "gradients", "psnr", "psnrb", "qnr", "rase", "rmse_sw",
+        "sam", "scc", "tv", "uqi", "vif",
+    ),
+    "functional.multimodal": (
+        "clip_iqa", "clip_score",
+    ),
+    "functional.nominal": (
+        "cramers", "fleiss_kappa", "pearson", "theils_u", "tschuprows", "utils",
+    ),
+    "functional.pairwise": (
+        "cosine", "euclidean", "helpers", "linear", "manhattan", "minkowski",
+    ),
+    "functional.regression": (
+        "concordance", "cosine_similarity", "csi", "explained_variance", "kendall", "kl_divergence",
+        "log_cosh", "log_mse", "mae", "mape", "minkowski", "mse", "pearson", "r2", "rse", "spearman",
+        "symmetric_mape", "tweedie_deviance", "utils", "wmape",
+    ),
+    "functional.retrieval": (
+        "_deprecated", "auroc", "average_precision", "fall_out", "hit_rate", "ndcg", "precision",
+        "precision_recall_curve", "r_precision", "recall", "reciprocal_rank",
+    ),
+    "functional.text": (
+        "_deprecated", "cer", "edit", "helper_embedding_metric", "mer", "sacre_bleu", "wer", "wil", "wip",
+    ),
+    "image": (
+        "_deprecated", "d_lambda", "d_s", "ergas", "fid", "inception", "kid", "lpip", "mifid",
+        "perceptual_path_length", "psnr", "psnrb", "qnr", "rase", "rmse_sw", "sam", "scc", "ssim", "tv",
+        "uqi", "vif",
+    ),
+    "multimodal": (
+        "clip_iqa", "clip_score",
+    ),
+    "nominal": (
+        "cramers", "fleiss_kappa", "pearson", "theils_u", "tschuprows",
+    ),
+    "regression": (
+        "concordance", "cosine_similarity", "csi", "explained_variance", "kendall", "kl_divergence",
+        "log_cosh", "log_mse", "mae", "mape", "minkowski", "mse", "pearson", "r2", "rse", "spearman",
+        "symmetric_mape", "tweedie_deviance", "wmape",
+    ),
+    "retrieval": (
+        "_deprecated", "auroc", "average_precision", "fall_out", "hit_rate", "ndcg", "precision",
+        "precision_recall_curve", "r_precision", "recall", "reciprocal_rank",
+    ),
+    "text": (
+        "_deprecated", "bert", "bleu", "cer", "chrf", "edit", "eed", "infolm", "mer", "perplexity",
+        "rouge", "sacre_bleu", "squad", "ter", "wer", "wil", "wip",
+    ),
+}
+
+# reference modules whose helpers live in a specific module of this package rather than in the domain package
+_SOURCES: Dict[str, str] = {
+    "torchmetrics_amd.image.kid": "torchmetrics_amd.image.generative",
+    "torchmetrics_amd.image.fid": "torchmetrics_amd.image.generative",
+    "torchmetrics_amd.image.mifid": "torchmetrics_amd.image.generative",
+    "torchmetrics_amd.image.inception": "torchmetrics_amd.image.generative",
+}
+
+_ALIASES: Dict[str, str] = {
+    f"torchmetrics_amd.{pkg}.{mod}": f"torchmetrics_amd.{pkg}" for pkg, mods in _TABLE.items() for mod in mods
+}
+
+
+class _AliasFinder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
+    def find_spec(self, fullname: str, path: Optional[object] = None, target: Optional[object] = None):  # noqa: ANN201
+        if fullname not in _ALIASES:
+            return None
+        return importlib.util.spec_from_loader(fullname, self)
+
+    def create_module(self, spec):  # noqa: ANN001, ANN201
+        return None
+
+    def exec_module(self, module) -> None:  # noqa: ANN001
+        target = importlib.import_module(_ALIASES[module.__name__])
+        extra = _SOURCES.get(module.__name__)
+        if extra is not None:
+            module.__dict__.update({k: v for k, v in vars(importlib.import_module(extra)).items()
+                                    if not k.startswith("__")})
+        module.__dict__.update({k: v for k, v in vars(target).items() if not (k.startswith("__") and k.endswith("__"))})
+        module.__doc__ = f"Reference module path; alias of :mod:`{target.__name__}`."
+        module.__all__ = [k for k in vars(target) if not k.startswith("_")]
+
+
+def install() -> None:
+    if not any(isinstance(f, _AliasFinder) for f in sys.meta_path):
+        sys.meta_path.append(_AliasFinder())
+
+
+def aliases() -> Dict[str, str]:
+    return dict(_ALIASES)

@@ -11,7 +11,7 @@ Weights are never downloaded.  ``pretrained=True`` loads the LPIPS linear heads 
 ``backbone_weights_path`` or the torch hub cache (torchvision file names); all with ``torch.load(weights_only=True)``.
 """
 import os
-from typing import List, Literal, Optional, Tuple, Union
+from typing import Any, List, Literal, NamedTuple, Optional, Tuple, Union
 
 import torch
 from torch import Tensor, nn
@@ -106,6 +106,102 @@ class _NetLinLayer(nn.Module):
         super().__init__()
         layers: List[nn.Module] = [nn.Dropout()] if use_dropout else []
         layers.append(nn.Conv2d(chn_in, 1, 1, stride=1, padding=0, bias=False))
+        self.model = nn.Sequential(*layers)
+
+    def forward(self, x: Tensor) -> Tensor:
+        return self.model(x)
+
+
+# ------------------------------------------------------------------------------------ public building blocks
+# Same names / constructor signatures / NamedTuple outputs as the reference's torchvision-backed classes
+# (F/image/lpips.py:65-255); here they are views of our own sliced backbones, with ImageNet weights read from the
+# local torch-hub cache when ``pretrained=True`` (nothing is downloaded).
+class _SqueezeOutput(NamedTuple):
+    relu1: Tensor
+    relu2: Tensor
+    relu3: Tensor
+    relu4: Tensor
+    relu5: Tensor
+    relu6: Tensor
+    relu7: Tensor
+
+
+class _AlexnetOutputs(NamedTuple):
+    relu1: Tensor
+    relu2: Tensor
+    relu3: Tensor
+    relu4: Tensor
+    relu5: Tensor
+
+
+class _VGGOutputs(NamedTuple):
+    relu1_2: Tensor
+    relu2_2: Tensor
+    relu3_3: Tensor
+    relu4_3: Tensor
+    relu5_3: Tensor
+
+
+class _PublicBackbone(_Backbone):
+    _net = "alex"
+    _out: Any = _AlexnetOutputs
+
+    def __init__(self, requires_grad: bool = False, pretrained: bool = True) -> None:
+        super().__init__(self._net)
+        if pretrained:
+            hub = os.path.join(torch.hub.get_dir(), "checkpoints", _HUB_FILES[self._net])
+            if not os.path.isfile(hub):
+                raise FileNotFoundError(f"ImageNet weights for `{self._net}` not found at {hub}; nothing is downloaded."
+                                        " Use `pretrained=False` for random weights.")
+            self.load_torchvision(torch.load(hub, map_location="cpu", weights_only=True))
+        if not requires_grad:
+            for p in self.parameters():
+                p.requires_grad = False
+
+    def forward(self, x: Tensor) -> NamedTuple:  # type: ignore[override]
+        return self._out(*super().forward(x))
+
+
+class SqueezeNet(_PublicBackbone):
+    """SqueezeNet 1.1 feature taps (7 ReLU outputs)."""
+
+    _net = "squeeze"
+    _out = _SqueezeOutput
+
+
+class Alexnet(_PublicBackbone):
+    """AlexNet feature taps (5 ReLU outputs)."""
+
+    _net = "alex"
+    _out = _AlexnetOutputs
+
+
+class Vgg16(_PublicBackbone):
+    """VGG16 feature taps (relu1_2 ... relu5_3)."""
+
+    _net = "vgg"
+    _out = _VGGOutputs
+
+
+class ScalingLayer(nn.Module):
+    """LPIPS input normalisation ``(x - shift) / scale``."""
+
+    def __init__(self) -> None:
+        super().__init__()
+        self.register_buffer("shift", torch.tensor([-0.030, -0.088, -0.188])[None, :, None, None], persistent=False)
+        self.register_buffer("scale", torch.tensor([0.458, 0.448, 0.450])[None, :, None, None], persistent=False)
+
+    def forward(self, inp: Tensor) -> Tensor:
+        return (inp - self.shift) / self.scale
+
+
+class NetLinLayer(nn.Module):
+    """A single 1x1 convolution (optionally after dropout): the LPIPS per-tap channel weighting."""
+
+    def __init__(self, chn_in: int, chn_out: int = 1, use_dropout: bool = False) -> None:
+        super().__init__()
+        layers: List[nn.Module] = [nn.Dropout()] if use_dropout else []
+        layers.append(nn.Conv2d(chn_in, chn_out, 1, stride=1, padding=0, bias=False))
         self.model = nn.Sequential(*layers)
 
     def forward(self, x: Tensor) -> Tensor:

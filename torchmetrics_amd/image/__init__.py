@@ -5,6 +5,7 @@ from torchmetrics_amd.image.generative import (
     KernelInceptionDistance,
     MemorizationInformedFrechetInceptionDistance,
 )
+from torchmetrics_amd.models.inception import NoTrainInceptionV3  # noqa: F401
 from torchmetrics_amd.image.perceptual import LearnedPerceptualImagePatchSimilarity, PerceptualPathLength
 from torchmetrics_amd.image.quality import (
     ErrorRelativeGlobalDimensionlessSynthesis,

@@ -233,7 +233,13 @@ class InceptionV3Features(nn.Module):
         return res[0] if len(res) == 1 else res
 
 
-def NoTrainInceptionV3(name: str = "inception-v3-compat", features_list: Optional[List[str]] = None,  # noqa: N802
-                       feature_extractor_weights_path: Optional[str] = None) -> InceptionV3Features:
-    """Factory with the reference's constructor signature (``S/image/fid.py:44``)."""
-    return InceptionV3Features(features_list or ["2048"], weights=feature_extractor_weights_path)
+class NoTrainInceptionV3(InceptionV3Features):
+    """Reference-compatible constructor (``S/image/fid.py:44-69``): ``NoTrainInceptionV3(name, features_list,
+    feature_extractor_weights_path)``; never leaves eval mode.  ``name`` is kept for API parity (the topology is
+    always the FID InceptionV3); weights come from ``feature_extractor_weights_path`` or
+    ``$TORCHMETRICS_AMD_INCEPTION_WEIGHTS`` (torch-fidelity's ``pt_inception-2015-12-05`` state dict layout)."""
+
+    def __init__(self, name: str = "inception-v3-compat", features_list: Optional[Sequence[str]] = None,
+                 feature_extractor_weights_path: Optional[str] = None) -> None:
+        super().__init__(features_list or ["2048"], weights=feature_extractor_weights_path)
+        self.name = name

@@ -32,10 +32,12 @@ void bin_confmat_finalize(at::Tensor ws, at::Tensor not_prob, at::Tensor confmat
 at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int64_t num_outputs, int64_t mask,
                           double eps, double power, const c10::optional<at::Tensor>& shift_p,
                           const c10::optional<at::Tensor>& shift_t, at::TensorList dests, at::IntArrayRef sum_ids,
-                          bool want_sums);
+                          bool want_sums, int64_t fold);
 void stat_reduce(const at::Tensor& tp, const at::Tensor& fp, const at::Tensor& tn, const at::Tensor& fn,
                  at::Tensor out, int64_t kind, int64_t average, bool multilabel, double beta);
 void launch_probe(at::Tensor flag);
+void mc_calibration_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor cand, at::Tensor conf,
+                           at::Tensor acc, at::Tensor notprob, int64_t slot, at::Tensor flag);
 }  // namespace tm_amd
 
 namespace {
@@ -59,9 +61,9 @@ void bin_update_fc(const at::Tensor& preds, const at::Tensor& target, at::Tensor
 at::Tensor moments_update_fc(const at::Tensor& preds, const at::Tensor& target, int64_t num_outputs, int64_t mask,
                              double eps, double power, const c10::optional<at::Tensor>& shift_p,
                              const c10::optional<at::Tensor>& shift_t, at::TensorList dests, at::IntArrayRef sum_ids,
-                             bool want_sums) {
+                             bool want_sums, int64_t fold) {
   return tm_amd::moments_update(preds.contiguous(), target.contiguous(), num_outputs, mask, eps, power, shift_p,
-                                shift_t, dests, sum_ids, want_sums);
+                                shift_t, dests, sum_ids, want_sums, fold);
 }
 
 void stat_reduce_fc(const at::Tensor& tp, const at::Tensor& fp, const at::Tensor& tn, const at::Tensor& fn,
@@ -217,6 +219,7 @@ PyMethodDef kMethods[] = {
     TM_FAST("moments_update", moments_update_fc),
     TM_FAST("stat_reduce", stat_reduce_fc),
     TM_FAST("launch_probe", tm_amd::launch_probe),
+    TM_FAST("mc_calibration_update", tm_amd::mc_calibration_update),
     TM_FAST("arg_probe", arg_probe),
     {nullptr, nullptr, 0, nullptr},
 };

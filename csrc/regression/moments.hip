@@ -129,11 +129,35 @@ __global__ void __launch_bounds__(kBlock) moments_partial_kernel(const scalar_t*
 
 struct DestSpec {
   void* ptr[kMaxSums];
-  int sum_id[kMaxSums];
-  int dtype[kMaxSums];  // 0 = f32, 1 = f64, 2 = i64
+  int sum_id[kMaxSums];   // dest += sum[sum_id]
+  int sub_id[kMaxSums];   // ... - sum[sub_id] when >= 0 (e.g. Σ(t - p) = Σt - Σp for explained variance)
+  int dtype[kMaxSums];    // 0 = f32, 1 = f64, 2 = i64
   int per_col[kMaxSums];  // 1: dest has k elements, 0: dest is a scalar (sum over columns)
   int n;
+  int fold;               // kFoldPearson: dests = running (mean_x, mean_y, m2_x, m2_y, c_xy, n) folded in place
 };
+
+// Pearson / concordance running-moment fold (Chan et al. merge of a centred batch into the running state, the
+// update of reference F/regression/pearson.py:25-78 without its host-side branching):
+//   tot = n0 + n;  dx = Σx~ / tot;  mean_x += dx;  m2_x += Σx~² - dx Σx~;  c_xy += Σx~y~ - dx Σy~;  n0 = tot
+// where x~ = x - mean_x(old) are the shifted sums of the partial kernel.  Each state is updated in its own dtype
+// with the increment rounded to that dtype first, exactly like the host formulation.
+constexpr int kFoldNone = 0;
+constexpr int kFoldPearson = 1;
+
+__device__ __forceinline__ double ld_state(const DestSpec& spec, int j, int c) {
+  return spec.dtype[j] == 0 ? static_cast<double>(reinterpret_cast<const float*>(spec.ptr[j])[c])
+                            : reinterpret_cast<const double*>(spec.ptr[j])[c];
+}
+
+__device__ __forceinline__ void add_state(const DestSpec& spec, int j, int c, double inc) {
+  if (spec.dtype[j] == 0) {
+    float* q = reinterpret_cast<float*>(spec.ptr[j]) + c;
+    *q = *q + static_cast<float>(inc);
+  } else {
+    reinterpret_cast<double*>(spec.ptr[j])[c] += inc;
+  }
+}
 
 // one block per column: fixed-order reduction over blocks, then add into the destination states
 __global__ void __launch_bounds__(kBlock) moments_finalize_kernel(const double* __restrict__ partial, int nblocks,
@@ -162,9 +186,24 @@ __global__ void __launch_bounds__(kBlock) moments_finalize_kernel(const double* 
     red[threadIdx.x][0] = v;
   }
   __syncthreads();
+  if (spec.fold == kFoldPearson) {
+    if (threadIdx.x == 0) {
+      const double sd = red[kSP][0], se = red[kST][0], sdd = red[kSPP][0], see = red[kSTT][0], sde = red[kSPT][0];
+      const double n = red[kCOUNT][0];
+      const double tot = ld_state(spec, 5, c) + n;
+      const double dx = sd / tot, dy = se / tot;
+      add_state(spec, 0, c, dx);
+      add_state(spec, 1, c, dy);
+      add_state(spec, 2, c, sdd - dx * sd);
+      add_state(spec, 3, c, see - dy * se);
+      add_state(spec, 4, c, sde - dx * se);
+      add_state(spec, 5, c, n);
+    }
+    return;
+  }
   if (threadIdx.x < spec.n) {
     const int j = threadIdx.x;
-    const double v = red[spec.sum_id[j]][0];
+    const double v = red[spec.sum_id[j]][0] - (spec.sub_id[j] >= 0 ? red[spec.sub_id[j]][0] : 0.0);
     const int idx = spec.per_col[j] ? c : 0;
     // per-column destination, or a scalar destination fed from column 0 (counts are equal in every column)
     if (spec.per_col[j] || c == 0) {
@@ -182,13 +221,14 @@ __global__ void __launch_bounds__(kBlock) moments_finalize_kernel(const double* 
 at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int64_t num_outputs, int64_t mask,
                           double eps, double power, const c10::optional<at::Tensor>& shift_p,
                           const c10::optional<at::Tensor>& shift_t, at::TensorList dests,
-                          at::IntArrayRef sum_ids, bool want_sums) {
+                          at::IntArrayRef sum_ids, bool want_sums, int64_t fold) {
   TM_CHECK_CUDA(preds);
   TM_CHECK_CONTIG(preds);
   TM_CHECK_CONTIG(target);
   TORCH_CHECK(preds.scalar_type() == target.scalar_type(), "moments_update: preds/target dtype mismatch");
   TORCH_CHECK(preds.numel() == target.numel(), "moments_update: preds/target numel mismatch");
-  TORCH_CHECK(dests.size() == sum_ids.size() && dests.size() <= kMaxSums, "moments_update: bad destination list");
+  TORCH_CHECK((fold != 0 || dests.size() == sum_ids.size()) && dests.size() <= kMaxSums,
+              "moments_update: bad destination list");
   const int k = static_cast<int>(num_outputs);
   TORCH_CHECK(k >= 1 && preds.numel() % k == 0, "moments_update: numel not divisible by num_outputs");
   const long long n_rows = preds.numel() / k;
@@ -227,13 +267,27 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
   });
   DestSpec spec{};
   spec.n = static_cast<int>(dests.size());
+  spec.fold = static_cast<int>(fold);
+  TORCH_CHECK(fold == kFoldNone || fold == kFoldPearson, "moments_update: bad fold mode");
+  if (fold == kFoldPearson) {
+    TORCH_CHECK(spec.n == 6 && (mask >> kCOUNT & 1) && (mask >> kSPT & 1) && (mask >> kSPP & 1) && (mask >> kSTT & 1),
+                "moments_update: the Pearson fold needs 6 states and the SP/ST/SPP/STT/SPT/COUNT sums");
+  }
   for (int j = 0; j < spec.n; ++j) {
     const at::Tensor& d = dests[j];
     TORCH_CHECK(d.is_cuda() && d.is_contiguous(), "moments_update: destination states must be contiguous GPU tensors");
-    TORCH_CHECK(d.numel() == k || d.numel() == 1, "moments_update: destination must have k or 1 elements");
+    TORCH_CHECK(d.get_device() == preds.get_device(), "moments_update: destination on another device");
+    TORCH_CHECK(d.numel() == k || (d.numel() == 1 && fold == kFoldNone),
+                "moments_update: destination must have k (or, without a fold, 1) elements");
     spec.ptr[j] = d.data_ptr();
-    spec.sum_id[j] = static_cast<int>(sum_ids[j]);
-    TORCH_CHECK(spec.sum_id[j] >= 0 && spec.sum_id[j] < kMaxSums, "moments_update: bad sum id");
+    // id < 16: sum[id];  id >= 16: sum[a] - sum[b] with id = 16 + 16 a + b
+    const int64_t id = fold == kFoldNone ? sum_ids[j] : kSP;
+    spec.sum_id[j] = static_cast<int>(id < 16 ? id : (id - 16) / 16);
+    spec.sub_id[j] = static_cast<int>(id < 16 ? -1 : (id - 16) % 16);
+    TORCH_CHECK(spec.sum_id[j] >= 0 && spec.sum_id[j] < kMaxSums && spec.sub_id[j] < kMaxSums,
+                "moments_update: bad sum id");
+    TORCH_CHECK(fold == kFoldNone || d.scalar_type() == at::kFloat || d.scalar_type() == at::kDouble,
+                "moments_update: folded states must be f32/f64");
     spec.per_col[j] = d.numel() == k && k > 1 ? 1 : (k == 1 ? 1 : 0);
     switch (d.scalar_type()) {
       case at::kFloat: spec.dtype[j] = 0; break;
@@ -253,7 +307,7 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
   m.def(
       "moments_update(Tensor preds, Tensor target, int num_outputs, int mask, float eps, float power, "
-      "Tensor? shift_p, Tensor? shift_t, Tensor(a!)[] dests, int[] sum_ids, bool want_sums) -> Tensor");
+      "Tensor? shift_p, Tensor? shift_t, Tensor(a!)[] dests, int[] sum_ids, bool want_sums, int fold=0) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) { m.impl("moments_update", &tm_amd::moments_update); }

@@ -161,3 +161,42 @@ def test_binary_confmat_prob_check_excludes_ignored():
 def test_histogram(n, bins):
     x = torch.randint(0, bins, (n,))
     assert torch.equal(ops.histogram(x.to(DEV), bins).cpu(), torch.bincount(x, minlength=bins))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("C", [3, 10, 64, 100, 1000])
+@pytest.mark.parametrize("kind", ["logits", "probs"])
+def test_calibration_fused_update_matches_cpu(dtype, C, kind):
+    """Fused top-label update (csrc/classification/calibration.hip) vs the CPU path of the same metric, over
+    several updates (exercises the double-buffered softmax decision word)."""
+    import torchmetrics_amd as tm
+
+    g = torch.Generator().manual_seed(C)
+    gpu = tm.MulticlassCalibrationError(num_classes=C, n_bins=15).to(DEV)
+    cpu = tm.MulticlassCalibrationError(num_classes=C, n_bins=15)
+    for step in range(4):
+        x = torch.randn(777, C, generator=g)
+        if kind == "probs" or step == 2:  # mixed batches: decision is per update
+            x = x.softmax(1)
+        x = x.to(dtype)
+        y = torch.randint(0, C, (777,), generator=g)
+        gpu.update(x.to(DEV), y.to(DEV))
+        cpu.update(x, y)
+    for a, b in zip(gpu.confidences, cpu.confidences):
+        # one unit in the last place of the input dtype (CPU and GPU expf may round a softmax value differently)
+        atol = {torch.float32: 1e-6, torch.bfloat16: 4e-3, torch.float16: 1e-3}[dtype]
+        torch.testing.assert_close(a.cpu(), b, rtol=0, atol=atol)
+    for a, b in zip(gpu.accuracies, cpu.accuracies):
+        assert torch.equal(a.cpu(), b)
+    torch.testing.assert_close(gpu.compute().cpu(), cpu.compute(), rtol=1e-5, atol=1e-6)
+
+
+def test_calibration_fused_flags_target_range():
+    import torchmetrics_amd as tm
+
+    m = tm.MulticlassCalibrationError(num_classes=5).to(DEV)
+    y = torch.randint(0, 5, (64,))
+    y[7] = 9
+    m.update(torch.randn(64, 5, device=DEV), y.to(DEV))
+    with pytest.raises(RuntimeError):
+        m.compute()

@@ -90,7 +90,8 @@ def _binary_float_preds_validation(preds: Tensor, target: Tensor, ignore_index: 
 
 
 def _multiclass_float_preds_validation(preds: Tensor, target: Tensor, num_classes: int,
-                                       ignore_index: Optional[int], flag: Optional[Tensor] = None) -> None:
+                                       ignore_index: Optional[int], flag: Optional[Tensor] = None,
+                                       check_values: bool = True) -> None:
     """Shape / dtype checks on the host; the target range check is a device-side flag (raised at ``compute``)
     when a metric error word ``flag`` is given, else an immediate host check."""
     if preds.ndim != target.ndim + 1:
@@ -108,6 +109,8 @@ def _multiclass_float_preds_validation(preds: Tensor, target: Tensor, num_classe
     if preds.shape[2:] != target.shape[1:]:
         raise ValueError("If `preds` have one dimension more than `target`, the shape of `preds` should be"
                          " (N, C, ...), and the shape of `target` should be (N, ...).")
+    if not check_values:  # the caller's kernel raises the target range bit itself
+        return
     bad = (target < 0) | (target >= num_classes)
     if ignore_index is not None:
         bad &= target != ignore_index

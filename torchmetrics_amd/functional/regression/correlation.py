@@ -43,6 +43,16 @@ def _pearson_corrcoef_update(
     n = preds.shape[0]
     shift_x = mean_x.reshape(k).float().contiguous()
     shift_y = mean_y.reshape(k).float().contiguous()
+    states = (mean_x, mean_y, var_x, var_y, corr_xy, num_prior)
+    if preds.is_cuda and all(
+        t.is_cuda and t.dtype in (torch.float32, torch.float64) and t.numel() == k and t.is_contiguous() for t in states
+    ) and not (torch.is_grad_enabled() and (preds.requires_grad or target.requires_grad)) and len(
+        {t.data_ptr() for t in states}
+    ) == 6:
+        # the whole fold runs on the device inside the update's two launches (states updated in place)
+        ops.moments_update(preds.reshape(n, k), target.reshape(n, k), k, [], list(states), [], shift_p=shift_x,
+                           shift_t=shift_y, fold=ops.FOLD_PEARSON)
+        return states
     s = ops.moments_update(preds.reshape(n, k), target.reshape(n, k), k, [ops.SP, ops.ST, ops.SPP, ops.STT, ops.SPT],
                            [], [], shift_p=shift_x, shift_t=shift_y, want_sums=True)
     sd, se = s[:, ops.SP], s[:, ops.ST]
@@ -100,7 +110,7 @@ def _final_aggregation(
 def pearson_corrcoef(preds: Tensor, target: Tensor) -> Tensor:
     d = preds.shape[1] if preds.ndim == 2 else 1
     z = torch.zeros(d, dtype=preds.dtype if preds.is_floating_point() else torch.float32, device=preds.device)
-    _, _, vx, vy, cxy, n = _pearson_corrcoef_update(preds, target, z, z, z, z, z, z.clone(), num_outputs=d)
+    _, _, vx, vy, cxy, n = _pearson_corrcoef_update(preds, target, *(z.clone() for _ in range(6)), num_outputs=d)
     return _pearson_corrcoef_compute(vx, vy, cxy, n)
 
 
@@ -115,7 +125,7 @@ def _concordance_corrcoef_compute(
 def concordance_corrcoef(preds: Tensor, target: Tensor) -> Tensor:
     d = preds.shape[1] if preds.ndim == 2 else 1
     z = torch.zeros(d, dtype=preds.dtype if preds.is_floating_point() else torch.float32, device=preds.device)
-    mx, my, vx, vy, cxy, n = _pearson_corrcoef_update(preds, target, z, z, z, z, z, z.clone(), num_outputs=d)
+    mx, my, vx, vy, cxy, n = _pearson_corrcoef_update(preds, target, *(z.clone() for _ in range(6)), num_outputs=d)
     return _concordance_corrcoef_compute(mx, my, vx, vy, cxy, n).squeeze()
 
 

@@ -184,9 +184,56 @@ def histogram(x: Tensor, minlength: int) -> Tensor:
     return torch.bincount(x, minlength=minlength)
 
 
+class CalibrationWorkspace:
+    """Per-metric device scratch of :func:`mc_calibration_update` (candidate rows + double-buffered decision word)."""
+
+    __slots__ = ("cand", "notprob", "slot")
+
+    def __init__(self) -> None:
+        self.cand: Optional[Tensor] = None
+        self.notprob: Optional[Tensor] = None
+        self.slot = 0
+
+
+_EMPTY_FLAG: dict = {}
+
+
+def mc_calibration_update(preds: Tensor, target: Tensor, ws: CalibrationWorkspace,
+                          flag: Optional[Tensor] = None) -> "tuple[Tensor, Tensor]":
+    """Top-label ``(confidences, accuracies)`` of ``[M, C]`` ROCm scores (softmax applied iff any score of the batch
+    is outside [0, 1]) in two launches (``csrc/classification/calibration.hip``); target range errors go to
+    ``flag``."""
+    m = preds.shape[0]
+    dev = preds.device
+    if ws.cand is None or ws.cand.device != dev or ws.cand.numel() < 4 * m:
+        ws.cand = torch.empty(max(4 * m, 1024), dtype=torch.float32, device=dev)
+        ws.notprob = torch.zeros(2, dtype=torch.int32, device=dev)
+        ws.slot = 0
+    conf = torch.empty(m, dtype=torch.float32, device=dev)
+    acc = torch.empty(m, dtype=torch.float32, device=dev)
+    if flag is None:
+        key = (dev.type, dev.index)
+        flag = _EMPTY_FLAG.get(key)
+        if flag is None:
+            flag = _EMPTY_FLAG[key] = torch.empty(0, dtype=torch.int32, device=dev)
+    (_fast_mod or _fast()).mc_calibration_update(preds, target, ws.cand, conf, acc, ws.notprob, ws.slot, flag)
+    ws.slot ^= 1
+    return conf, acc
+
+
 # ------------------------------------------------------------------------------------------------------ regression
 # sum ids of csrc/regression/moments.hip
 SSE, SAE, SP, ST, SPP, STT, SPT, MAPE, SMAPE, SABST, MSLE, LOGCOSH, MINK, COUNT = range(14)
+FOLD_NONE, FOLD_PEARSON = 0, 1
+
+
+def sum_diff(a: int, b: int) -> int:
+    """Destination id meaning ``sum[a] - sum[b]`` (e.g. ``sum_diff(ST, SP)`` = Σ(t - p))."""
+    return 16 + 16 * int(a) + int(b)
+
+
+def _sum_ids(i: int) -> "tuple[int, ...]":
+    return (i,) if i < 16 else ((i - 16) // 16, (i - 16) % 16)
 
 
 def moments_update(
@@ -201,14 +248,20 @@ def moments_update(
     shift_p: Optional[Tensor] = None,
     shift_t: Optional[Tensor] = None,
     want_sums: bool = False,
+    fold: int = FOLD_NONE,
 ) -> Optional[Tensor]:
     """One pass computing the requested per-output sums and adding ``sum[dest_ids[j]]`` into ``dests[j]``.
 
     ``preds``/``target`` are ``[N, num_outputs]`` (or 1-D). Returns the ``[num_outputs, 14]`` fp64 sums if asked.
+    ``dest_ids`` entries may be :func:`sum_diff` pairs.  ``fold=FOLD_PEARSON`` instead folds the batch into the six
+    running Pearson states ``dests = [mean_x, mean_y, m2_x, m2_y, c_xy, n]`` in place (``shift_p``/``shift_t`` must
+    be the current means), all inside the update's two launches.
     """
     mask = 0
-    for s in list(sums) + list(dest_ids):
+    for s in list(sums) + [j for i in dest_ids for j in _sum_ids(int(i))]:
         mask |= 1 << int(s)
+    if fold == FOLD_PEARSON:
+        mask |= (1 << SP) | (1 << ST) | (1 << SPP) | (1 << STT) | (1 << SPT) | (1 << COUNT)
     needs_grad = torch.is_grad_enabled() and (preds.requires_grad or target.requires_grad)
     if preds.is_cuda and not needs_grad:
         if preds.dtype != target.dtype or not preds.is_floating_point():
@@ -218,11 +271,11 @@ def moments_update(
         res = (_fast_mod or _fast()).moments_update(
             preds, target, num_outputs, mask, float(eps), float(power), shift_p, shift_t,
             dests if isinstance(dests, (list, tuple)) else list(dests),
-            dest_ids if isinstance(dest_ids, (list, tuple)) else list(dest_ids), want_sums,
+            dest_ids if isinstance(dest_ids, (list, tuple)) else list(dest_ids), want_sums, fold,
         )
         return res if want_sums else None
     return _cpu.moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_t, dests, dest_ids,
-                               want_sums)
+                               want_sums, fold)
 
 
 # ----------------------------------------------------------------------------------------------------------- image

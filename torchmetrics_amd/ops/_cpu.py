@@ -168,7 +168,8 @@ def bin_confmat_finalize(ws: Tensor, not_prob: Tensor, confmat: Tensor) -> None:
     not_prob.zero_()
 
 
-def moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_t, dests, dest_ids, want_sums):
+def moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_t, dests, dest_ids, want_sums,
+                   fold=0):
     k = int(num_outputs)
     p = preds.reshape(-1, k).double()
     t = target.reshape(-1, k).double()
@@ -196,8 +197,19 @@ def moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_
     for sid, fn in cols.items():
         if mask & (1 << sid) or sid == 13:
             sums[:, sid] = fn()
+    if fold == 1:  # Pearson running-moment fold, same formulation as csrc/regression/moments.hip
+        mean_x, mean_y, m2_x, m2_y, c_xy, n0 = dests
+        sd, se, sdd, see, sde = (sums[:, i] for i in (2, 3, 4, 5, 6))
+        tot = n0.reshape(k).double() + p.shape[0]
+        dx, dy = sd / tot, se / tot
+        for dst, inc in ((mean_x, dx), (mean_y, dy), (m2_x, sdd - dx * sd), (m2_y, see - dy * se),
+                         (c_xy, sde - dx * se)):
+            dst += inc.reshape(dst.shape).to(dst.dtype)
+        n0 += p.shape[0]
+        return sums if want_sums else None
     for dst, sid in zip(dests, dest_ids):
-        val = sums[:, sid] if dst.numel() == k else sums[0, sid]
+        col = sums[:, sid] if sid < 16 else sums[:, (sid - 16) // 16] - sums[:, (sid - 16) % 16]
+        val = col if dst.numel() == k else col[0]
         if dst.dtype == torch.int64:
             val = torch.round(val).long()
         dst += val.reshape(dst.shape).to(dst.dtype)

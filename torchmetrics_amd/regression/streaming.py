@@ -314,6 +314,13 @@ class ExplainedVariance(_MomentsMetric):
             for name in ("sum_error", "sum_squared_error", "sum_target", "sum_squared_target"):
                 setattr(self, name, getattr(self, name) + torch.zeros(k, dtype=getattr(self, name).dtype,
                                                                        device=preds.device))
+        dests = [self.sum_error, self.sum_squared_error, self.sum_target, self.sum_squared_target, self.num_obs]
+        if preds.is_cuda and all(d.is_cuda and d.is_contiguous() and d.dtype in (torch.float32, torch.float64)
+                                 for d in dests):
+            # Σ(t - p), Σ(p - t)², Σt, Σt², count: all added into the states by the moments finalize launch
+            ops.moments_update(preds.reshape(n, k), target.reshape(n, k), k, [],
+                               dests, [ops.sum_diff(ops.ST, ops.SP), ops.SSE, ops.ST, ops.STT, ops.COUNT])
+            return
         s = ops.moments_update(preds.reshape(n, k), target.reshape(n, k), k, [ops.SP, ops.ST, ops.SSE, ops.STT], [],
                                [], want_sums=True)
         sq = (lambda x: x[0]) if preds.ndim == 1 else (lambda x: x)

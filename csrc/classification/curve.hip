@@ -130,11 +130,14 @@ __global__ void __launch_bounds__(kBinThreads) curve_bin_kernel(
 
   const long long r0 = static_cast<long long>(blockIdx.y) * rows_per_split;
   const long long r1 = min(rows, r0 + rows_per_split);
-  const long long elems = (r1 - r0) * cw_eff;
+  // 32-bit element index inside the block's slab (the host caps an update at 2^31 elements): the per-element
+  // row / column split is one 32-bit division instead of a ~40-instruction 64-bit one
+  const int elems = static_cast<int>((r1 - r0) * cw_eff);
   int bad = 0;
-  for (long long e = threadIdx.x; e < elems; e += blockDim.x) {
-    const long long r = r0 + e / cw_eff;
-    const int cl = static_cast<int>(e % cw_eff);
+  for (int e = threadIdx.x; e < elems; e += blockDim.x) {
+    const int rr = e / cw_eff;
+    const long long r = r0 + rr;
+    const int cl = e - rr * cw_eff;
     const int col = c0 + cl;
     const long long idx = r * cols + col;
     double p;
@@ -323,7 +326,7 @@ void curve_update(const at::Tensor& preds, const at::Tensor& target, const at::T
         const int tiles = (cols + cw - 1) / cw;
         const long long elems_per_tile = rows * std::min(cw, cols);
         long long splits = std::max<long long>(1, std::min<long long>((2048 + tiles - 1) / tiles,
-                                                                      (elems_per_tile + 4095) / 4096));
+                                                                      (elems_per_tile + 1023) / 1024));
         splits = std::min<long long>(splits, rows);
         const long long rows_per_split = (rows + splits - 1) / splits;
         splits = (rows + rows_per_split - 1) / rows_per_split;

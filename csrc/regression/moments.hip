@@ -36,13 +36,54 @@ enum SumId : int {
   kCOUNT = 13,  // number of observations per column
 };
 
+// Destinations of one update: up to kMaxDests plain "state += sum" targets (a whole MetricCollection's worth of
+// streaming regression metrics on the same inputs) plus, optionally, one Pearson fold block.
+constexpr int kMaxDests = 32;
+struct DestSpec {
+  void* ptr[kMaxDests];
+  int sum_id[kMaxDests];   // dest += sum[sum_id]
+  int sub_id[kMaxDests];   // ... - sum[sub_id] when >= 0 (e.g. Σ(t - p) = Σt - Σp for explained variance)
+  int dtype[kMaxDests];    // 0 = f32, 1 = f64, 2 = i64
+  int per_col[kMaxDests];  // 1: dest has k elements, 0: dest is a scalar (sum over columns)
+  int n;
+  int fold;                // kFoldPearson: fptr = running (mean_x, mean_y, m2_x, m2_y, c_xy, n) folded in place
+  void* fptr[6];
+  int fdtype[6];
+};
+
+// Pearson / concordance running-moment fold (Chan et al. merge of a centred batch into the running state, the
+// update of reference F/regression/pearson.py:25-78 without its host-side branching):
+//   tot = n0 + n;  dx = Σx~ / tot;  mean_x += dx;  m2_x += Σx~² - dx Σx~;  c_xy += Σx~y~ - dx Σy~;  n0 = tot
+// where x~ = x - mean_x(old) are the shifted sums of the partial kernel.  Each state is updated in its own dtype
+// with the increment rounded to that dtype first, exactly like the host formulation.
+constexpr int kFoldNone = 0;
+constexpr int kFoldPearson = 1;
+
+__device__ __forceinline__ double ld_state(const DestSpec& spec, int j, int c) {
+  return spec.fdtype[j] == 0 ? static_cast<double>(reinterpret_cast<const float*>(spec.fptr[j])[c])
+                             : reinterpret_cast<const double*>(spec.fptr[j])[c];
+}
+
+__device__ __forceinline__ void add_state(const DestSpec& spec, int j, int c, double inc) {
+  if (spec.fdtype[j] == 0) {
+    float* q = reinterpret_cast<float*>(spec.fptr[j]) + c;
+    *q = *q + static_cast<float>(inc);
+  } else {
+    reinterpret_cast<double*>(spec.fptr[j])[c] += inc;
+  }
+}
+
+__device__ void finalize_column(const double* __restrict__ partial, int nblocks, int k, int c,
+                                const DestSpec& spec, double* __restrict__ out_sums, int mask);
+
 template <typename scalar_t>
 __global__ void __launch_bounds__(kBlock) moments_partial_kernel(const scalar_t* __restrict__ preds,
                                                                  const scalar_t* __restrict__ target, long long n_rows,
                                                                  int k, int mask, double eps, double pw,
                                                                  const float* __restrict__ shift_p,
                                                                  const float* __restrict__ shift_t,
-                                                                 double* __restrict__ partial) {
+                                                                 double* __restrict__ partial, int fuse,
+                                                                 DestSpec spec, double* __restrict__ out_sums) {
   // every thread keeps one column: total threads is a multiple of k (host guarantees blockDim % k == 0 or k > block)
   const long long tid = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
   const long long nthreads = static_cast<long long>(gridDim.x) * blockDim.x;
@@ -91,6 +132,7 @@ __global__ void __launch_bounds__(kBlock) moments_partial_kernel(const scalar_t*
     const int wid = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
 #pragma unroll
     for (int s = 0; s < kMaxSums; ++s) {
+      if (!((mask >> s) & 1) && s != kCOUNT) continue;  // uniform: only the requested sums cross the wave
       double v = acc[s];
       for (int off = kWave / 2; off >= k; off >>= 1) v += __shfl_xor(v, off, kWave);
       if (lane < k) wred[wid][lane][s] = v;
@@ -99,12 +141,12 @@ __global__ void __launch_bounds__(kBlock) moments_partial_kernel(const scalar_t*
     for (int i = threadIdx.x; i < k * kMaxSums; i += blockDim.x) {
       const int c = i / kMaxSums, s = i % kMaxSums;
       double v = 0.0;
-      for (int w = 0; w < kBlock / kWave; ++w) v += wred[w][c][s];
+      if (((mask >> s) & 1) || s == kCOUNT)
+        for (int w = 0; w < kBlock / kWave; ++w) v += wred[w][c][s];
       // lane l of every wave holds column (block_base + l) % k; block_base is a multiple of k here
       partial[(static_cast<long long>(blockIdx.x) * k + c) * kMaxSums + s] = v;
     }
-    return;
-  }
+  } else {
   // block reduction per (column, sum): threads with equal tid % k hold the same column
   __shared__ double red[kBlock][kMaxSums + 1];
 #pragma unroll
@@ -125,44 +167,18 @@ __global__ void __launch_bounds__(kBlock) moments_partial_kernel(const scalar_t*
 #pragma unroll
     for (int s = 0; s < kMaxSums; ++s) dst[s] = out[s];
   }
-}
-
-struct DestSpec {
-  void* ptr[kMaxSums];
-  int sum_id[kMaxSums];   // dest += sum[sum_id]
-  int sub_id[kMaxSums];   // ... - sum[sub_id] when >= 0 (e.g. Σ(t - p) = Σt - Σp for explained variance)
-  int dtype[kMaxSums];    // 0 = f32, 1 = f64, 2 = i64
-  int per_col[kMaxSums];  // 1: dest has k elements, 0: dest is a scalar (sum over columns)
-  int n;
-  int fold;               // kFoldPearson: dests = running (mean_x, mean_y, m2_x, m2_y, c_xy, n) folded in place
-};
-
-// Pearson / concordance running-moment fold (Chan et al. merge of a centred batch into the running state, the
-// update of reference F/regression/pearson.py:25-78 without its host-side branching):
-//   tot = n0 + n;  dx = Σx~ / tot;  mean_x += dx;  m2_x += Σx~² - dx Σx~;  c_xy += Σx~y~ - dx Σy~;  n0 = tot
-// where x~ = x - mean_x(old) are the shifted sums of the partial kernel.  Each state is updated in its own dtype
-// with the increment rounded to that dtype first, exactly like the host formulation.
-constexpr int kFoldNone = 0;
-constexpr int kFoldPearson = 1;
-
-__device__ __forceinline__ double ld_state(const DestSpec& spec, int j, int c) {
-  return spec.dtype[j] == 0 ? static_cast<double>(reinterpret_cast<const float*>(spec.ptr[j])[c])
-                            : reinterpret_cast<const double*>(spec.ptr[j])[c];
-}
-
-__device__ __forceinline__ void add_state(const DestSpec& spec, int j, int c, double inc) {
-  if (spec.dtype[j] == 0) {
-    float* q = reinterpret_cast<float*>(spec.ptr[j]) + c;
-    *q = *q + static_cast<float>(inc);
-  } else {
-    reinterpret_cast<double*>(spec.ptr[j])[c] += inc;
+  }
+  if (fuse) {  // single-block launch: this block also folds its sums into the states (one launch per update)
+    __threadfence_block();
+    __syncthreads();
+    for (int c = 0; c < k; ++c) finalize_column(partial, 1, k, c, spec, out_sums, mask);
   }
 }
 
-// one block per column: fixed-order reduction over blocks, then add into the destination states
-__global__ void __launch_bounds__(kBlock) moments_finalize_kernel(const double* __restrict__ partial, int nblocks,
-                                                                  int k, DestSpec spec, double* __restrict__ out_sums) {
-  const int c = blockIdx.x;
+// fixed-order reduction of one column's partials over blocks, then add / fold into the destination states;
+// called by every thread of a block
+__device__ void finalize_column(const double* __restrict__ partial, int nblocks, int k, int c, const DestSpec& spec,
+                                double* __restrict__ out_sums, int mask) {
   __shared__ double red[kMaxSums][kBlock / kWave];
   double acc[kMaxSums];
 #pragma unroll
@@ -175,6 +191,10 @@ __global__ void __launch_bounds__(kBlock) moments_finalize_kernel(const double* 
   const int wid = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
 #pragma unroll
   for (int s = 0; s < kMaxSums; ++s) {
+    if (!((mask >> s) & 1) && s != kCOUNT) {
+      if (lane == 0) red[s][wid] = 0.0;
+      continue;
+    }
     const double v = wave_sum(acc[s]);
     if (lane == 0) red[s][wid] = v;
   }
@@ -187,7 +207,7 @@ __global__ void __launch_bounds__(kBlock) moments_finalize_kernel(const double* 
   }
   __syncthreads();
   if (spec.fold == kFoldPearson) {
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == kWave) {  // a lane of the second wave: the first wave's lanes own the plain dests below
       const double sd = red[kSP][0], se = red[kST][0], sdd = red[kSPP][0], see = red[kSTT][0], sde = red[kSPT][0];
       const double n = red[kCOUNT][0];
       const double tot = ld_state(spec, 5, c) + n;
@@ -199,7 +219,6 @@ __global__ void __launch_bounds__(kBlock) moments_finalize_kernel(const double* 
       add_state(spec, 4, c, sde - dx * se);
       add_state(spec, 5, c, n);
     }
-    return;
   }
   if (threadIdx.x < spec.n) {
     const int j = threadIdx.x;
@@ -212,6 +231,14 @@ __global__ void __launch_bounds__(kBlock) moments_finalize_kernel(const double* 
       else reinterpret_cast<int64_t*>(spec.ptr[j])[idx] += static_cast<int64_t>(llrint(v));
     }
   }
+  __syncthreads();  // red[] is reused by the next column of a fused single-block launch
+}
+
+// one block per column
+__global__ void __launch_bounds__(kBlock) moments_finalize_kernel(const double* __restrict__ partial, int nblocks,
+                                                                  int k, DestSpec spec, double* __restrict__ out_sums,
+                                                                  int mask) {
+  finalize_column(partial, nblocks, k, blockIdx.x, spec, out_sums, mask);
 }
 
 }  // namespace
@@ -227,8 +254,10 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
   TM_CHECK_CONTIG(target);
   TORCH_CHECK(preds.scalar_type() == target.scalar_type(), "moments_update: preds/target dtype mismatch");
   TORCH_CHECK(preds.numel() == target.numel(), "moments_update: preds/target numel mismatch");
-  TORCH_CHECK((fold != 0 || dests.size() == sum_ids.size()) && dests.size() <= kMaxSums,
-              "moments_update: bad destination list");
+  const int nfold = fold != 0 ? 6 : 0;
+  TORCH_CHECK(static_cast<int64_t>(dests.size()) == nfold + static_cast<int64_t>(sum_ids.size()) &&
+                  sum_ids.size() <= static_cast<size_t>(kMaxDests),
+              "moments_update: bad destination list (fold states first, then one sum id per plain destination)");
   const int k = static_cast<int>(num_outputs);
   TORCH_CHECK(k >= 1 && preds.numel() % k == 0, "moments_update: numel not divisible by num_outputs");
   const long long n_rows = preds.numel() / k;
@@ -247,6 +276,46 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
     const long long step = k / g;
     blocks = ((blocks + step - 1) / step) * step;
   }
+  DestSpec spec{};
+  spec.n = static_cast<int>(sum_ids.size());
+  spec.fold = static_cast<int>(fold);
+  TORCH_CHECK(fold == kFoldNone || fold == kFoldPearson, "moments_update: bad fold mode");
+  if (fold == kFoldPearson) {
+    TORCH_CHECK((mask >> kCOUNT & 1) && (mask >> kSPT & 1) && (mask >> kSPP & 1) && (mask >> kSTT & 1),
+                "moments_update: the Pearson fold needs the SP/ST/SPP/STT/SPT/COUNT sums");
+    for (int j = 0; j < 6; ++j) {
+      const at::Tensor& d = dests[j];
+      TORCH_CHECK(d.is_cuda() && d.is_contiguous() && d.get_device() == preds.get_device() && d.numel() == k,
+                  "moments_update: folded states must be contiguous [k] tensors on the input's device");
+      TORCH_CHECK(d.scalar_type() == at::kFloat || d.scalar_type() == at::kDouble,
+                  "moments_update: folded states must be f32/f64");
+      spec.fptr[j] = d.data_ptr();
+      spec.fdtype[j] = d.scalar_type() == at::kFloat ? 0 : 1;
+    }
+  }
+  for (int j = 0; j < spec.n; ++j) {
+    const at::Tensor& d = dests[nfold + j];
+    TORCH_CHECK(d.is_cuda() && d.is_contiguous(), "moments_update: destination states must be contiguous GPU tensors");
+    TORCH_CHECK(d.get_device() == preds.get_device(), "moments_update: destination on another device");
+    TORCH_CHECK(d.numel() == k || d.numel() == 1, "moments_update: destination must have k or 1 elements");
+    spec.ptr[j] = d.data_ptr();
+    // id < 16: sum[id];  id >= 16: sum[a] - sum[b] with id = 16 + 16 a + b
+    const int64_t id = sum_ids[j];
+    spec.sum_id[j] = static_cast<int>(id < 16 ? id : (id - 16) / 16);
+    spec.sub_id[j] = static_cast<int>(id < 16 ? -1 : (id - 16) % 16);
+    TORCH_CHECK(spec.sum_id[j] >= 0 && spec.sum_id[j] < kMaxSums && spec.sub_id[j] < kMaxSums,
+                "moments_update: bad sum id");
+    spec.per_col[j] = d.numel() == k && k > 1 ? 1 : (k == 1 ? 1 : 0);
+    switch (d.scalar_type()) {
+      case at::kFloat: spec.dtype[j] = 0; break;
+      case at::kDouble: spec.dtype[j] = 1; break;
+      case at::kLong: spec.dtype[j] = 2; break;
+      default: TORCH_CHECK(false, "moments_update: destination dtype must be f32/f64/i64");
+    }
+  }
+  // small updates (the common per-batch case): one block does the pass AND the fold -> a single launch
+  const bool fuse = n_rows * k <= 4096 && kBlock % k == 0;
+  if (fuse) blocks = 1;
   at::Tensor partial = at::empty({blocks, k, kMaxSums}, dopt);
   const float* sp = nullptr;
   const float* st = nullptr;
@@ -263,41 +332,14 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
     hipLaunchKernelGGL((moments_partial_kernel<scalar_t>), dim3(blocks), dim3(block), 0, s,
                        reinterpret_cast<const scalar_t*>(preds.data_ptr()),
                        reinterpret_cast<const scalar_t*>(target.data_ptr()), n_rows, k, static_cast<int>(mask), eps,
-                       power, sp, st, partial.data_ptr<double>());
+                       power, sp, st, partial.data_ptr<double>(), fuse ? 1 : 0, spec,
+                       want_sums ? sums.data_ptr<double>() : nullptr);
   });
-  DestSpec spec{};
-  spec.n = static_cast<int>(dests.size());
-  spec.fold = static_cast<int>(fold);
-  TORCH_CHECK(fold == kFoldNone || fold == kFoldPearson, "moments_update: bad fold mode");
-  if (fold == kFoldPearson) {
-    TORCH_CHECK(spec.n == 6 && (mask >> kCOUNT & 1) && (mask >> kSPT & 1) && (mask >> kSPP & 1) && (mask >> kSTT & 1),
-                "moments_update: the Pearson fold needs 6 states and the SP/ST/SPP/STT/SPT/COUNT sums");
+  if (!fuse) {
+    hipLaunchKernelGGL(moments_finalize_kernel, dim3(k), dim3(kBlock), 0, s, partial.data_ptr<double>(),
+                       static_cast<int>(blocks), k, spec, want_sums ? sums.data_ptr<double>() : nullptr,
+                       static_cast<int>(mask));
   }
-  for (int j = 0; j < spec.n; ++j) {
-    const at::Tensor& d = dests[j];
-    TORCH_CHECK(d.is_cuda() && d.is_contiguous(), "moments_update: destination states must be contiguous GPU tensors");
-    TORCH_CHECK(d.get_device() == preds.get_device(), "moments_update: destination on another device");
-    TORCH_CHECK(d.numel() == k || (d.numel() == 1 && fold == kFoldNone),
-                "moments_update: destination must have k (or, without a fold, 1) elements");
-    spec.ptr[j] = d.data_ptr();
-    // id < 16: sum[id];  id >= 16: sum[a] - sum[b] with id = 16 + 16 a + b
-    const int64_t id = fold == kFoldNone ? sum_ids[j] : kSP;
-    spec.sum_id[j] = static_cast<int>(id < 16 ? id : (id - 16) / 16);
-    spec.sub_id[j] = static_cast<int>(id < 16 ? -1 : (id - 16) % 16);
-    TORCH_CHECK(spec.sum_id[j] >= 0 && spec.sum_id[j] < kMaxSums && spec.sub_id[j] < kMaxSums,
-                "moments_update: bad sum id");
-    TORCH_CHECK(fold == kFoldNone || d.scalar_type() == at::kFloat || d.scalar_type() == at::kDouble,
-                "moments_update: folded states must be f32/f64");
-    spec.per_col[j] = d.numel() == k && k > 1 ? 1 : (k == 1 ? 1 : 0);
-    switch (d.scalar_type()) {
-      case at::kFloat: spec.dtype[j] = 0; break;
-      case at::kDouble: spec.dtype[j] = 1; break;
-      case at::kLong: spec.dtype[j] = 2; break;
-      default: TORCH_CHECK(false, "moments_update: destination dtype must be f32/f64/i64");
-    }
-  }
-  hipLaunchKernelGGL(moments_finalize_kernel, dim3(k), dim3(kBlock), 0, s, partial.data_ptr<double>(),
-                     static_cast<int>(blocks), k, spec, want_sums ? sums.data_ptr<double>() : nullptr);
   C10_HIP_KERNEL_LAUNCH_CHECK();
   return sums;
 }

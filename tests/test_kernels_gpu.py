@@ -200,3 +200,37 @@ def test_calibration_fused_flags_target_range():
     m.update(torch.randn(64, 5, device=DEV), y.to(DEV))
     with pytest.raises(RuntimeError):
         m.compute()
+
+
+@pytest.mark.parametrize("k", [1, 3])
+@pytest.mark.parametrize("n", [1000, 20000])
+def test_collection_merged_moments_matches_individual(k, n):
+    """A MetricCollection merges its streaming regression members' kernel requests into one pass
+    (ops.run_moments_plans); results must equal each metric updated alone on the CPU."""
+    import torchmetrics_amd as tm
+    from torchmetrics_amd import regression as R
+
+    def members():
+        common = {
+            "mse": R.MeanSquaredError(num_outputs=k), "r2": R.R2Score(num_outputs=k),
+            "pearson": R.PearsonCorrCoef(num_outputs=k), "concordance": R.ConcordanceCorrCoef(num_outputs=k),
+            "ev": R.ExplainedVariance(),
+        }
+        if k == 1:
+            common.update({"mae": R.MeanAbsoluteError(), "mape": R.MeanAbsolutePercentageError(),
+                           "mink": R.MinkowskiDistance(p=3.0), "logcosh": R.LogCoshError(), "smape":
+                           R.SymmetricMeanAbsolutePercentageError()})
+        return common
+
+    gpu = tm.MetricCollection(members(), compute_groups=True).to(DEV)
+    cpu = members()
+    g = torch.Generator().manual_seed(n + k)
+    for step in range(3):
+        x = torch.randn(n, k, generator=g).squeeze(-1) + 2
+        y = x + 0.5 * torch.randn(n, k, generator=g).squeeze(-1)
+        gpu.update(x.to(DEV), y.to(DEV))
+        for m in cpu.values():
+            m.update(x, y)
+    out = gpu.compute()
+    for name, m in cpu.items():
+        torch.testing.assert_close(out[name].cpu().float(), m.compute().float(), rtol=2e-4, atol=1e-5)

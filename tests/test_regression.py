@@ -159,3 +159,38 @@ def test_regression_grad_flows():
 def test_regression_ddp(name, cls):
     p, t = _inputs()
     run_ddp_class_test(p, t, cls, partial(_ref, name), atol=1e-4)
+
+
+def test_moments_plan_merging_on_cpu(monkeypatch):
+    """The collection-level merge of streaming regression requests (ops.run_moments_plans) gives the same values as
+    separate updates; forced on CPU tensors so the merge logic (incl. the Pearson-fold / unshifted-sum conflict)
+    is covered without a GPU."""
+    import torchmetrics_amd as tm
+    from torchmetrics_amd import ops
+    from torchmetrics_amd import regression as R
+
+    monkeypatch.setattr(ops.MomentsPlan, "deferrable", lambda self: True)
+    calls = []
+    orig = ops.run_moments_plans
+    monkeypatch.setattr(ops, "run_moments_plans", lambda plans: calls.append(orig(plans)))
+
+    def members():
+        return {"mse": R.MeanSquaredError(), "r2": R.R2Score(), "pearson": R.PearsonCorrCoef(),
+                "concordance": R.ConcordanceCorrCoef(), "ev": R.ExplainedVariance(), "mae": R.MeanAbsoluteError(),
+                "mape": R.MeanAbsolutePercentageError(), "mink": R.MinkowskiDistance(p=3.0)}
+
+    coll = tm.MetricCollection(members(), compute_groups=True)
+    ref = members()
+    g = torch.Generator().manual_seed(3)
+    for _ in range(3):
+        x = torch.randn(500, generator=g) + 2
+        y = x + 0.5 * torch.randn(500, generator=g)
+        coll.update(x, y)
+        for m in ref.values():
+            m.update(x, y)
+    out = coll.compute()
+    for name, m in ref.items():
+        torch.testing.assert_close(out[name], m.compute())
+    # first update runs every member (group detection); later ones are merged: pearson fold / centred sums /
+    # Minkowski power -> 3 kernel calls for 8 metrics
+    assert calls and all(c == 3 for c in calls)

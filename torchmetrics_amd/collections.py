@@ -19,6 +19,7 @@ import torch
 from torch import Tensor
 from torch.nn import ModuleDict
 
+from torchmetrics_amd import ops
 from torchmetrics_amd.metric import CompositionalMetric, Metric
 from torchmetrics_amd.parallel.sync import sync_state_dicts
 from torchmetrics_amd.utilities.data import _flatten_dict, allclose
@@ -64,9 +65,19 @@ class MetricCollection(ModuleDict):
     def update(self, *args: Any, **kwargs: Any) -> None:
         """Update every metric (only the first member of each compute group once groups are known)."""
         if self._groups_checked:
+            # streaming regression leaders hand their moments requests to `sink`; requests on the same inputs are
+            # then merged into one kernel pass for the whole collection (ops.run_moments_plans)
+            sink: list = []
             for cg in self._groups.values():
                 m0 = getattr(self, cg[0])
-                m0.update(*args, **m0._filter_kwargs(**kwargs))
+                d = m0.__dict__
+                d["_moments_sink"] = sink
+                try:
+                    m0.update(*args, **m0._filter_kwargs(**kwargs))
+                finally:
+                    del d["_moments_sink"]
+            if sink:
+                ops.run_moments_plans(sink)
             if self._state_is_copy:
                 self._compute_groups_create_state_ref()
                 self._state_is_copy = False

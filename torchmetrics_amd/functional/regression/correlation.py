@@ -35,6 +35,7 @@ def _pearson_corrcoef_update(
     corr_xy: Tensor,
     num_prior: Tensor,
     num_outputs: int,
+    sink: Optional[list] = None,
 ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
     """Fold one batch into the running (mean, sum of squared deviations, co-moment, count) states."""
     _check_same_shape(preds, target)
@@ -49,9 +50,14 @@ def _pearson_corrcoef_update(
     ) and not (torch.is_grad_enabled() and (preds.requires_grad or target.requires_grad)) and len(
         {t.data_ptr() for t in states}
     ) == 6:
-        # the whole fold runs on the device inside the update's two launches (states updated in place)
-        ops.moments_update(preds.reshape(n, k), target.reshape(n, k), k, [], list(states), [], shift_p=shift_x,
-                           shift_t=shift_y, fold=ops.FOLD_PEARSON)
+        # the whole fold runs on the device inside the update's launch(es), states updated in place; a
+        # ``MetricCollection`` may defer it (``sink``) to merge it with its other streaming regression members
+        plan = ops.MomentsPlan(preds.reshape(n, k), target.reshape(n, k), k, [], [], fold_states=list(states),
+                               shift_p=shift_x, shift_t=shift_y)
+        if sink is not None and plan.deferrable():
+            sink.append(plan)
+        else:
+            plan.run()
         return states
     s = ops.moments_update(preds.reshape(n, k), target.reshape(n, k), k, [ops.SP, ops.ST, ops.SPP, ops.STT, ops.SPT],
                            [], [], shift_p=shift_x, shift_t=shift_y, want_sums=True)

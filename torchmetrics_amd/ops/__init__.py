@@ -253,9 +253,9 @@ def moments_update(
     """One pass computing the requested per-output sums and adding ``sum[dest_ids[j]]`` into ``dests[j]``.
 
     ``preds``/``target`` are ``[N, num_outputs]`` (or 1-D). Returns the ``[num_outputs, 14]`` fp64 sums if asked.
-    ``dest_ids`` entries may be :func:`sum_diff` pairs.  ``fold=FOLD_PEARSON`` instead folds the batch into the six
-    running Pearson states ``dests = [mean_x, mean_y, m2_x, m2_y, c_xy, n]`` in place (``shift_p``/``shift_t`` must
-    be the current means), all inside the update's two launches.
+    ``dest_ids`` entries may be :func:`sum_diff` pairs.  ``fold=FOLD_PEARSON`` additionally folds the batch into the
+    six running Pearson states given FIRST in ``dests`` (``[mean_x, mean_y, m2_x, m2_y, c_xy, n]``, in place;
+    ``shift_p``/``shift_t`` must be the current means); ``dest_ids`` then names the remaining destinations.
     """
     mask = 0
     for s in list(sums) + [j for i in dest_ids for j in _sum_ids(int(i))]:
@@ -276,6 +276,113 @@ def moments_update(
         return res if want_sums else None
     return _cpu.moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_t, dests, dest_ids,
                                want_sums, fold)
+
+
+class MomentsPlan:
+    """One metric's request to the moments kernel, deferrable so a ``MetricCollection`` can merge the requests of
+    all its streaming regression members on the same inputs into ONE :func:`moments_update` (one pass over the data,
+    one or two launches for the whole collection)."""
+
+    __slots__ = ("preds", "target", "k", "dests", "ids", "eps", "power", "fold_states", "shift_p", "shift_t", "src",
+                 "checked")
+
+    def __init__(self, preds: Tensor, target: Tensor, k: int, dests: "list[Tensor]", ids: "list[int]",
+                 eps: float = 1.17e-06, power: float = 2.0, fold_states: Optional["list[Tensor]"] = None,
+                 shift_p: Optional[Tensor] = None, shift_t: Optional[Tensor] = None,
+                 src: Optional[tuple] = None, checked: bool = False) -> None:
+        self.preds, self.target, self.k = preds, target, k
+        self.dests, self.ids = dests, ids
+        self.eps, self.power = eps, power
+        self.fold_states, self.shift_p, self.shift_t = fold_states, shift_p, shift_t
+        self.src = src if src is not None else (preds, target)  # the caller's input objects (merge key)
+        self.checked = checked  # destinations already validated (see states_ready)
+
+    def deferrable(self) -> bool:
+        p, t = self.preds, self.target
+        if not (p.is_cuda and t.is_cuda) or (torch.is_grad_enabled() and (p.requires_grad or t.requires_grad)):
+            return False
+        if self.checked:
+            return True
+        dev = p.get_device()
+        return all(d.get_device() == dev and d.is_contiguous() for d in self.dests + (self.fold_states or []))
+
+    def _uses(self) -> int:
+        m = 0
+        for i in self.ids:
+            for j in _sum_ids(int(i)):
+                m |= 1 << j
+        return m
+
+    def key(self) -> tuple:
+        """Plans merge when they read the same input objects with the same column count (and the same eps /
+        power where those enter the sums).  Object identity is exact here: every plan of one collection update
+        keeps its inputs alive until the merged call has run."""
+        m = self._uses()
+        eps = self.eps if m & ((1 << MAPE) | (1 << SMAPE)) else None
+        power = self.power if m & (1 << MINK) else None
+        return (id(self.src[0]), id(self.src[1]), self.k, eps, power)
+
+    def run(self) -> None:
+        fold = self.fold_states is not None
+        moments_update(self.preds, self.target, self.k, [], (self.fold_states or []) + self.dests, self.ids,
+                       eps=self.eps, power=self.power, shift_p=self.shift_p, shift_t=self.shift_t,
+                       fold=FOLD_PEARSON if fold else FOLD_NONE)
+
+
+def states_ready(owner: dict, states: tuple, dev: int, dtypes: tuple = (torch.float32, torch.float64, torch.int64)) -> bool:
+    """True if ``states`` are contiguous tensors on CUDA device ``dev`` with an accepted dtype.  The verdict is cached
+    in ``owner`` against the state OBJECTS (held, compared with ``is``): a metric's states stay the same objects
+    across in-place kernel updates, so the per-update check is a few identity tests instead of ~4 tensor queries per
+    state (host time is what bounds these updates)."""
+    c = owner.get("_states_ready")
+    if c is not None and c[0] == dev and len(c[1]) == len(states):
+        for a, b in zip(c[1], states):
+            if a is not b:
+                break
+        else:
+            return True
+    ok = all(t.is_cuda and t.get_device() == dev and t.is_contiguous() and t.dtype in dtypes for t in states)
+    owner["_states_ready"] = (dev, states) if ok else None
+    return ok
+
+
+_CENTRED = (1 << SP) | (1 << ST) | (1 << SPP) | (1 << STT) | (1 << SPT)
+
+
+def run_moments_plans(plans: "list[MomentsPlan]") -> int:
+    """Execute deferred plans, merging those on identical inputs (at most one Pearson fold and 32 plain
+    destinations per launch).  Returns the number of kernel calls issued."""
+    groups: "dict[tuple, list[MomentsPlan]]" = {}
+    for pl in plans:
+        groups.setdefault(pl.key(), []).append(pl)
+    calls = 0
+    for members in groups.values():
+        while members:
+            merged = MomentsPlan(members[0].preds, members[0].target, members[0].k, [], [], members[0].eps,
+                                 members[0].power, src=members[0].src, checked=True)
+            rest = []
+            for pl in members:
+                # the Pearson fold shifts the centred sums by the running means: it cannot share a pass with
+                # plain destinations that need the unshifted Σp / Σt / Σp² / Σt² / Σpt
+                pl_plain_centred = bool(pl._uses() & _CENTRED)
+                m_plain_centred = bool(merged._uses() & _CENTRED)
+                if (pl.fold_states is not None and (merged.fold_states is not None or m_plain_centred)) or \
+                        (merged.fold_states is not None and pl_plain_centred) or \
+                        len(merged.dests) + len(pl.dests) > 32:
+                    rest.append(pl)
+                    continue
+                merged.dests += pl.dests
+                merged.ids += pl.ids
+                if pl.fold_states is not None:
+                    merged.fold_states, merged.shift_p, merged.shift_t = pl.fold_states, pl.shift_p, pl.shift_t
+                if pl._uses() & ((1 << MAPE) | (1 << SMAPE)):
+                    merged.eps = pl.eps
+                if pl._uses() & (1 << MINK):
+                    merged.power = pl.power
+            merged.run()
+            calls += 1
+            members = rest
+    return calls
 
 
 # ----------------------------------------------------------------------------------------------------------- image

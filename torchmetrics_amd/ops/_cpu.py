@@ -197,8 +197,9 @@ def moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_
     for sid, fn in cols.items():
         if mask & (1 << sid) or sid == 13:
             sums[:, sid] = fn()
-    if fold == 1:  # Pearson running-moment fold, same formulation as csrc/regression/moments.hip
-        mean_x, mean_y, m2_x, m2_y, c_xy, n0 = dests
+    if fold == 1:  # Pearson running-moment fold (first 6 dests), same formulation as csrc/regression/moments.hip
+        mean_x, mean_y, m2_x, m2_y, c_xy, n0 = dests[:6]
+        dests = dests[6:]
         sd, se, sdd, see, sde = (sums[:, i] for i in (2, 3, 4, 5, 6))
         tot = n0.reshape(k).double() + p.shape[0]
         dx, dy = sd / tot, se / tot
@@ -206,7 +207,6 @@ def moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_
                          (c_xy, sde - dx * se)):
             dst += inc.reshape(dst.shape).to(dst.dtype)
         n0 += p.shape[0]
-        return sums if want_sums else None
     for dst, sid in zip(dests, dest_ids):
         col = sums[:, sid] if sid < 16 else sums[:, (sid - 16) // 16] - sums[:, (sid - 16) % 16]
         val = col if dst.numel() == k else col[0]

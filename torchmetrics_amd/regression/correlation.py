@@ -8,6 +8,7 @@ from typing import Any, List, Optional, Sequence, Tuple, Union
 import torch
 from torch import Tensor
 
+from torchmetrics_amd import ops
 from torchmetrics_amd.functional.regression.correlation import (
     _concordance_corrcoef_compute,
     _cosine_similarity_compute,
@@ -47,9 +48,32 @@ class PearsonCorrCoef(Metric):
             self.add_state(name, default=torch.zeros(self.num_outputs), dist_reduce_fx=None)
 
     def update(self, preds: Tensor, target: Tensor) -> None:
+        d = self.__dict__
+        states = (self.mean_x, self.mean_y, self.var_x, self.var_y, self.corr_xy, self.n_total)
+        k = self.num_outputs
+        if (preds.is_cuda and states[0].numel() == k and ops.states_ready(d, states, preds.get_device(),
+                                                                         (torch.float32, torch.float64))
+                and not (torch.is_grad_enabled() and (preds.requires_grad or target.requires_grad))):
+            # device fold in place (the states stay the same objects: no re-assignment through nn.Module)
+            _check_same_shape(preds, target)
+            _check_data_shape_to_num_outputs(preds, target, k)
+            shifts = d.get("_fold_shifts")
+            if shifts is None or shifts[0] is not states[0] or shifts[1] is not states[1]:
+                shifts = d["_fold_shifts"] = (states[0], states[1], states[0].view(k).float(), states[1].view(k).float())
+            if states[0].dtype != torch.float32:  # f64 means: the f32 shift copies must be refreshed every update
+                shifts = (shifts[0], shifts[1], states[0].view(k).float(), states[1].view(k).float())
+            n = preds.shape[0]
+            plan = ops.MomentsPlan(preds.reshape(n, k), target.reshape(n, k), k, [], [], fold_states=list(states),
+                                   shift_p=shifts[2], shift_t=shifts[3], src=(preds, target), checked=True)
+            sink = d.get("_moments_sink")
+            if sink is not None and plan.deferrable():
+                sink.append(plan)
+            else:
+                plan.run()
+            return
         (self.mean_x, self.mean_y, self.var_x, self.var_y, self.corr_xy, self.n_total) = _pearson_corrcoef_update(
             preds, target, self.mean_x, self.mean_y, self.var_x, self.var_y, self.corr_xy, self.n_total,
-            self.num_outputs,
+            self.num_outputs, sink=d.get("_moments_sink"),
         )
 
     def _merged(self) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:

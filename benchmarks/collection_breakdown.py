@@ -59,6 +59,20 @@ def main():
     for nm, f in (("collection_cls", fc), ("collection_reg", fr)):
         host, total = timed(f)
         print(json.dumps({"metric": nm, "host_us": round(host, 1), "total_us": round(total, 1)}), flush=True)
+    # compute() per member (cache cleared each call) and per collection
+    for name, m in list(cls.items(keep_base=True)) + list(reg.items(keep_base=True)):
+        def fcomp(m=m):
+            m._computed = None
+            m.compute()
+        host, total = timed(fcomp, n=50)
+        print(json.dumps({"compute": name, "host_us": round(host, 1), "total_us": round(total, 1)}), flush=True)
+    for nm, coll in (("collection_cls", cls), ("collection_reg", reg)):
+        def fcc(coll=coll):
+            for m in coll.values(copy_state=False):
+                m._computed = None
+            coll.compute()
+        host, total = timed(fcc, n=50)
+        print(json.dumps({"compute": nm, "host_us": round(host, 1), "total_us": round(total, 1)}), flush=True)
     print(json.dumps({"groups_cls": [list(v) for v in cls.compute_groups.values()],
                       "groups_reg": [list(v) for v in reg.compute_groups.values()]}))
 

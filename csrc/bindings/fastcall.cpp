@@ -36,6 +36,11 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
 void stat_reduce(const at::Tensor& tp, const at::Tensor& fp, const at::Tensor& tn, const at::Tensor& fn,
                  at::Tensor out, int64_t kind, int64_t average, bool multilabel, double beta);
 void launch_probe(at::Tensor flag);
+void confmat_reduce(const at::Tensor& confmat, int64_t kind, int64_t average, int64_t ignore, int64_t kw,
+                    at::Tensor out);
+void calibration_bins(const at::Tensor& conf, const at::Tensor& acc, const at::Tensor& bounds, at::Tensor sums,
+                      at::Tensor bad);
+void curve_score(const at::Tensor& state, int64_t kind, int64_t average, at::Tensor out, at::Tensor nan_flag);
 void mc_calibration_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor cand, at::Tensor conf,
                            at::Tensor acc, at::Tensor notprob, int64_t slot, at::Tensor flag);
 }  // namespace tm_amd
@@ -219,6 +224,9 @@ PyMethodDef kMethods[] = {
     TM_FAST("moments_update", moments_update_fc),
     TM_FAST("stat_reduce", stat_reduce_fc),
     TM_FAST("launch_probe", tm_amd::launch_probe),
+    TM_FAST("confmat_reduce", tm_amd::confmat_reduce),
+    TM_FAST("calibration_bins", tm_amd::calibration_bins),
+    TM_FAST("curve_score", tm_amd::curve_score),
     TM_FAST("mc_calibration_update", tm_amd::mc_calibration_update),
     TM_FAST("arg_probe", arg_probe),
     {nullptr, nullptr, 0, nullptr},

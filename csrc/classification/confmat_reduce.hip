@@ -1,0 +1,227 @@
+// Fused compute() of the confusion-matrix family on a multiclass [C, C] int64 state: Jaccard index, Cohen's kappa
+// and Matthews' correlation coefficient, plus the calibration-error bin statistics.
+//
+// Reference reductions (F/classification/{jaccard,cohen_kappa,matthews_corrcoef}.py `_*_reduce`) are ~10-25 ATen
+// launches each, and MCC branches on `denom == 0` / degenerate 2x2 cases with host syncs: ~0.12-0.17 ms of host time
+// per compute() at C = 10.  Here one block reads the matrix once (row sums, column sums, diagonal in LDS, fp64),
+// evaluates the reduction including the data-dependent branches on the device, and writes [C] per-class values
+// (Jaccard) plus the scalar result: one launch, no sync.
+//
+// Calibration (F/classification/calibration_error.py `_binning_bucketize`): bucketize + stack + index_add over
+// every accumulated confidence is replaced by one pass with an LDS-privatised (count, Σconf, Σacc) histogram
+// (SURVEY K7); the per-bin divisions stay a handful of [n_bins]-sized ops.
+#include "../common/tm_common.h"
+
+namespace tm_amd {
+namespace {
+
+constexpr int kThreads = 256;
+enum Kind : int { kJaccard = 0, kKappa = 1, kMcc = 2 };
+enum Avg : int { kMicro = 0, kMacro = 1, kWeighted = 2, kNone = 3 };
+enum KappaW : int { kWNone = 0, kWLinear = 1, kWQuadratic = 2 };
+
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  v = wave_sum(v);
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int w = 0; w < kThreads / kWave; ++w) s += red[w];
+  return s;
+}
+
+__global__ void __launch_bounds__(kThreads) confmat_reduce_kernel(const int64_t* __restrict__ cm, int C, int kind,
+                                                                  int average, int ignore, int kw,
+                                                                  float* __restrict__ out) {
+  extern __shared__ double sm[];  // rows [C], cols [C], diag [C]
+  __shared__ double red[kThreads / kWave];
+  double* rows = sm;
+  double* cols = sm + C;
+  double* diag = sm + 2 * C;
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    double r = 0.0, c = 0.0;
+    for (int j = 0; j < C; ++j) {
+      r += static_cast<double>(cm[static_cast<long long>(i) * C + j]);
+      c += static_cast<double>(cm[static_cast<long long>(j) * C + i]);
+    }
+    rows[i] = r;
+    cols[i] = c;
+    diag[i] = static_cast<double>(cm[static_cast<long long>(i) * C + i]);
+  }
+  __syncthreads();
+
+  if (kind == kJaccard) {
+    const bool drop = ignore >= 0 && ignore < C;
+    double tp_sum = 0.0, un_sum = 0.0, wsum = 0.0, wiou = 0.0;
+    for (int i = threadIdx.x; i < C; i += blockDim.x) {
+      const double tp = diag[i], un = rows[i] + cols[i] - tp;
+      const double iou = tp / (un == 0.0 ? 1.0 : un);
+      out[i] = static_cast<float>(iou);
+      tp_sum += tp;
+      un_sum += (drop && i == ignore) ? 0.0 : un;
+      double w = average == kWeighted ? rows[i] : 1.0;
+      if (average == kMacro && ((drop && i == ignore) || rows[i] + cols[i] == 0.0)) w = 0.0;
+      wsum += w;
+      wiou += w * iou;
+    }
+    tp_sum = block_sum(tp_sum, red);
+    un_sum = block_sum(un_sum, red);
+    wsum = block_sum(wsum, red);
+    wiou = block_sum(wiou, red);
+    if (threadIdx.x == 0) {
+      out[C] = average == kMicro ? static_cast<float>(tp_sum / (un_sum == 0.0 ? 1.0 : un_sum))
+                                 : static_cast<float>(wiou / wsum);  // 0/0 -> nan, as ((w * iou) / w.sum()).sum()
+    }
+    return;
+  }
+
+  double n = 0.0;
+  for (int i = threadIdx.x; i < C; i += blockDim.x) n += rows[i];
+  n = block_sum(n, red);
+
+  if (kind == kKappa) {
+    // 1 - sum(W * O) / sum(W * E),  E_ij = rows_i cols_j / n
+    double wo = 0.0, we = 0.0;
+    for (long long e = threadIdx.x; e < static_cast<long long>(C) * C; e += blockDim.x) {
+      const int i = static_cast<int>(e / C), j = static_cast<int>(e - static_cast<long long>(i) * C);
+      const double d = static_cast<double>(i - j);
+      const double w = kw == kWNone ? (i == j ? 0.0 : 1.0) : (kw == kWLinear ? fabs(d) : d * d);
+      wo += w * static_cast<double>(cm[e]);
+      we += w * rows[i] * cols[j] / n;
+    }
+    wo = block_sum(wo, red);
+    we = block_sum(we, red);
+    if (threadIdx.x == 0) out[0] = static_cast<float>(1.0 - wo / we);
+    return;
+  }
+
+  // MCC (Gorodkin R_K), with the reference's binary special cases
+  double tk_pk = 0.0, pk2 = 0.0, tk2 = 0.0, correct = 0.0;
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    tk_pk += rows[i] * cols[i];
+    pk2 += cols[i] * cols[i];
+    tk2 += rows[i] * rows[i];
+    correct += diag[i];
+  }
+  tk_pk = block_sum(tk_pk, red);
+  pk2 = block_sum(pk2, red);
+  tk2 = block_sum(tk2, red);
+  correct = block_sum(correct, red);
+  if (threadIdx.x != 0) return;
+  const bool binary = C == 2;
+  if (binary) {
+    const double tn = static_cast<double>(cm[0]), fp = static_cast<double>(cm[1]);
+    const double fn = static_cast<double>(cm[2]), tp = static_cast<double>(cm[3]);
+    if (tp + tn != 0.0 && fp + fn == 0.0) {
+      out[0] = 1.f;
+      return;
+    }
+    if (tp + tn == 0.0 && fp + fn != 0.0) {
+      out[0] = -1.f;
+      return;
+    }
+  }
+  double numer = correct * n - tk_pk;
+  double denom = (n * n - pk2) * (n * n - tk2);
+  if (denom == 0.0) {
+    if (!binary) {
+      out[0] = 0.f;
+      return;
+    }
+    const double tn = static_cast<double>(cm[0]), fp = static_cast<double>(cm[1]);
+    const double fn = static_cast<double>(cm[2]), tp = static_cast<double>(cm[3]);
+    const double eps = 1.1920928955078125e-07;  // torch.finfo(float32).eps
+    const double a = (tp == 0.0 || tn == 0.0) ? tp + tn : 0.0;
+    const double b = (fp == 0.0 || fn == 0.0) ? fp + fn : 0.0;
+    numer = sqrt(eps) * (a - b);
+    denom = (tp + fp + eps) * (tp + fn + eps) * (tn + fp + eps) * (tn + fn + eps);
+  }
+  out[0] = static_cast<float>(numer / sqrt(denom));
+}
+
+// (count, Σconf, Σacc) per bin; bin = #{boundaries <= conf} - 1 (torch.bucketize(right=True) - 1); nb <= 4096
+__global__ void __launch_bounds__(kThreads) calib_bins_kernel(const float* __restrict__ conf,
+                                                              const float* __restrict__ acc, long long n,
+                                                              const float* __restrict__ bounds, int nb,
+                                                              float* __restrict__ sums, int* __restrict__ bad) {
+  extern __shared__ float hs[];  // [nb][3] histogram, then [nb] boundaries
+  float* bs = hs + 3 * nb;
+  for (int i = threadIdx.x; i < 3 * nb; i += blockDim.x) hs[i] = 0.f;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) bs[i] = bounds[i];
+  __syncthreads();
+  bool oob = false;
+  for (long long e = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; e < n;
+       e += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const float x = conf[e];
+    int lo = 0, hi = nb;  // first index with bounds[idx] > x
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (bs[mid] <= x) lo = mid + 1;
+      else hi = mid;
+    }
+    const int b = lo - 1;
+    if (b < 0) {  // below the first boundary: index -1, which index_add rejects in the reference
+      oob = true;
+      continue;
+    }
+    atomicAdd(&hs[3 * b], 1.f);
+    atomicAdd(&hs[3 * b + 1], x);
+    atomicAdd(&hs[3 * b + 2], acc[e]);
+  }
+  if (oob) atomicOr(bad, 1);
+  __syncthreads();
+  for (int i = threadIdx.x; i < 3 * nb; i += blockDim.x)
+    if (hs[i] != 0.f) atomicAdd(&sums[i], hs[i]);
+}
+
+}  // namespace
+
+// confmat: int64 [C, C]; kind 0 Jaccard (average 0 micro / 1 macro / 2 weighted / 3 none, ignore: class to drop or -1),
+// 1 Cohen kappa (kw 0 none / 1 linear / 2 quadratic), 2 MCC.  out: f32 [C + 1] (Jaccard: per class + scalar) or [1].
+void confmat_reduce(const at::Tensor& confmat, int64_t kind, int64_t average, int64_t ignore, int64_t kw,
+                    at::Tensor out) {
+  TM_CHECK_CUDA(confmat);
+  TORCH_CHECK(confmat.scalar_type() == at::kLong && confmat.is_contiguous() && confmat.dim() == 2 &&
+                  confmat.size(0) == confmat.size(1), "confmat_reduce: int64 [C, C] contiguous");
+  const int C = static_cast<int>(confmat.size(0));
+  TORCH_CHECK(C >= 2 && C <= 4096, "confmat_reduce: 2 <= C <= 4096");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() >= (kind == kJaccard ? C + 1 : 1),
+              "confmat_reduce: out");
+  hipLaunchKernelGGL(confmat_reduce_kernel, dim3(1), dim3(kThreads), 3 * C * sizeof(double), stream(),
+                     confmat.data_ptr<int64_t>(), C, static_cast<int>(kind), static_cast<int>(average),
+                     static_cast<int>(ignore), static_cast<int>(kw), out.data_ptr<float>());
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+// conf/acc: f32 [N]; bounds: f32 [nb] ascending; sums: f32 [nb, 3] zeroed (accumulated); bad: i32 [1] (conf below
+// bounds[0]).
+void calibration_bins(const at::Tensor& conf, const at::Tensor& acc, const at::Tensor& bounds, at::Tensor sums,
+                      at::Tensor bad) {
+  TM_CHECK_CUDA(conf);
+  TORCH_CHECK(conf.scalar_type() == at::kFloat && acc.scalar_type() == at::kFloat && conf.is_contiguous() &&
+                  acc.is_contiguous() && conf.numel() == acc.numel(), "calibration_bins: f32 conf / acc");
+  TORCH_CHECK(bounds.scalar_type() == at::kFloat && bounds.is_contiguous(), "calibration_bins: f32 bounds");
+  const int nb = static_cast<int>(bounds.numel());
+  TORCH_CHECK(nb >= 1 && nb <= 4096, "calibration_bins: 1 <= bins <= 4096");
+  TORCH_CHECK(sums.scalar_type() == at::kFloat && sums.numel() == 3 * nb && sums.is_contiguous(),
+              "calibration_bins: sums f32 [nb, 3]");
+  const long long n = conf.numel();
+  if (n == 0) return;
+  const int grid = grid_cap((n + kThreads - 1) / kThreads, 256 * 4);
+  hipLaunchKernelGGL(calib_bins_kernel, dim3(grid), dim3(kThreads), 4 * nb * sizeof(float), stream(),
+                     conf.data_ptr<float>(), acc.data_ptr<float>(), n, bounds.data_ptr<float>(), nb,
+                     sums.data_ptr<float>(), bad.data_ptr<int>());
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+}  // namespace tm_amd
+
+TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def("confmat_reduce(Tensor confmat, int kind, int average, int ignore, int kw, Tensor(a!) out) -> ()");
+  m.def("calibration_bins(Tensor conf, Tensor acc, Tensor bounds, Tensor(a!) sums, Tensor(b!) bad) -> ()");
+}
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
+  m.impl("confmat_reduce", &tm_amd::confmat_reduce);
+  m.impl("calibration_bins", &tm_amd::calibration_bins);
+}

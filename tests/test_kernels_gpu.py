@@ -2,6 +2,8 @@
 
 Every case runs the GPU op and the CPU op on identical inputs and requires identical integer results.
 """
+import warnings
+
 import pytest
 import torch
 
@@ -234,3 +236,91 @@ def test_collection_merged_moments_matches_individual(k, n):
     out = gpu.compute()
     for name, m in cpu.items():
         torch.testing.assert_close(out[name].cpu().float(), m.compute().float(), rtol=2e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("task", ["multiclass", "multilabel"])
+@pytest.mark.parametrize("metric", ["auroc", "ap"])
+@pytest.mark.parametrize("average", ["macro", "weighted", "none"])
+@pytest.mark.parametrize("C", [3, 10, 130])
+def test_curve_score_fused_matches_cpu(task, metric, average, C):
+    """Binned AUROC / AP compute through the fused curve_score kernel vs the CPU op-by-op formulation, including
+    classes with no positives (NaN AUROC, nan-aware averages)."""
+    import torchmetrics_amd as tm
+
+    g = torch.Generator().manual_seed(C)
+    n = 600
+    if task == "multiclass":
+        preds = torch.randn(n, C, generator=g).softmax(1)
+        target = torch.randint(0, max(C - 1, 2), (n,), generator=g)  # last class never appears
+        cls = {"auroc": tm.MulticlassAUROC, "ap": tm.MulticlassAveragePrecision}[metric]
+        kw = {"num_classes": C}
+    else:
+        preds = torch.rand(n, C, generator=g)
+        target = (torch.rand(n, C, generator=g) > 0.6).long()
+        target[:, -1] = 0
+        cls = {"auroc": tm.MultilabelAUROC, "ap": tm.MultilabelAveragePrecision}[metric]
+        kw = {"num_labels": C}
+    gpu = cls(thresholds=50, average=average, **kw).to(DEV)
+    cpu = cls(thresholds=50, average=average, **kw)
+    gpu.update(preds.to(DEV), target.to(DEV))
+    cpu.update(preds, target)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        a, b = gpu.compute().cpu(), cpu.compute()
+    torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6, equal_nan=True)
+
+
+def _confmats(C, g):
+    cms = [torch.randint(0, 50, (C, C), generator=g)]
+    z = torch.zeros(C, C, dtype=torch.int64)
+    z[0, 0] = 7  # a single class seen
+    cms.append(z)
+    d = torch.diag(torch.randint(1, 9, (C,), generator=g))  # perfect predictions
+    cms.append(d)
+    e = torch.randint(0, 5, (C, C), generator=g)
+    e[C - 1, :] = 0
+    e[:, C - 1] = 0  # a class never seen
+    cms.append(e)
+    return cms
+
+
+@pytest.mark.parametrize("C", [2, 3, 10, 257])
+def test_confmat_reduce_matches_cpu(C):
+    """Fused Jaccard / Cohen kappa / MCC (csrc/classification/confmat_reduce.hip) vs the CPU formulations, on
+    random, single-class, perfect and missing-class matrices (incl. the degenerate 2x2 MCC cases)."""
+    from torchmetrics_amd.functional.classification.cohen_kappa import _cohen_kappa_reduce
+    from torchmetrics_amd.functional.classification.jaccard import _jaccard_index_reduce
+    from torchmetrics_amd.functional.classification.matthews_corrcoef import _matthews_corrcoef_reduce
+
+    g = torch.Generator().manual_seed(C)
+    cms = _confmats(C, g)
+    if C == 2:
+        cms += [torch.tensor([[5, 0], [0, 0]]), torch.tensor([[0, 0], [0, 5]]), torch.tensor([[0, 3], [0, 0]]),
+                torch.tensor([[0, 0], [4, 0]]), torch.tensor([[3, 2], [0, 0]]), torch.tensor([[0, 0], [2, 3]])]
+    for cm in cms:
+        for avg in ("micro", "macro", "weighted", "none"):
+            for ii in (None, 0, C + 3):
+                a = _jaccard_index_reduce(cm.to(DEV), avg, ii).cpu()
+                b = _jaccard_index_reduce(cm, avg, ii)
+                torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6, equal_nan=True)
+        for w in (None, "linear", "quadratic"):
+            torch.testing.assert_close(_cohen_kappa_reduce(cm.to(DEV), w).cpu(), _cohen_kappa_reduce(cm, w),
+                                       rtol=1e-5, atol=1e-6, equal_nan=True)
+        torch.testing.assert_close(_matthews_corrcoef_reduce(cm.to(DEV)).cpu().float(),
+                                   _matthews_corrcoef_reduce(cm).float(), rtol=1e-5, atol=1e-6, equal_nan=True)
+
+
+@pytest.mark.parametrize("n_bins", [1, 15, 100])
+def test_calibration_bins_matches_cpu(n_bins):
+    from torchmetrics_amd.functional.classification.calibration_error import _binning_bucketize
+
+    g = torch.Generator().manual_seed(n_bins)
+    conf = torch.rand(100000, generator=g)
+    conf[:7] = 1.0  # the last boundary: its own slot, as torch.bucketize(right=True) - 1
+    conf[7:9] = 0.0
+    acc = (torch.rand(100000, generator=g) > 0.4).float()
+    bounds = torch.linspace(0, 1, n_bins + 1)
+    ref = _binning_bucketize(conf, acc, bounds)
+    got = _binning_bucketize(conf.to(DEV), acc.to(DEV), bounds.to(DEV))
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a.cpu(), b, rtol=1e-4, atol=1e-6)

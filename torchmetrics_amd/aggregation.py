@@ -154,6 +154,8 @@ class SumMetric(BaseAggregator):
 class CatMetric(BaseAggregator):
     """Concatenate every value seen."""
 
+    _fold_cat_lists = True  # compute() only concatenates the list states
+
     value: Tensor
 
     def __init__(self, nan_strategy: Union[str, float] = "warn", **kwargs: Any) -> None:

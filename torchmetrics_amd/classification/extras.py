@@ -73,6 +73,8 @@ from torchmetrics_amd.utilities.prints import rank_zero_warn
 class BinaryCalibrationError(Metric):
     """Top-label calibration error (ECE / MCE / RMSCE) for binary probabilities."""
 
+    _fold_cat_lists = True  # compute() only concatenates the list states
+
     is_differentiable: bool = False
     higher_is_better: bool = False
     full_state_update: bool = False
@@ -104,6 +106,8 @@ class BinaryCalibrationError(Metric):
 
 class MulticlassCalibrationError(Metric):
     """Top-label calibration error for multiclass probabilities / logits."""
+
+    _fold_cat_lists = True  # compute() only concatenates the list states
 
     is_differentiable: bool = False
     higher_is_better: bool = False

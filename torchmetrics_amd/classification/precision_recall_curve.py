@@ -65,6 +65,8 @@ from torchmetrics_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_curve
 class _CurveBase(Metric):
     """Shared state handling: ``confmat`` (binned, summed) or ``preds``/``target`` lists (unbinned, cat)."""
 
+    _fold_cat_lists = True  # unbinned compute() only concatenates the preds / target lists
+
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = None
     full_state_update: bool = False

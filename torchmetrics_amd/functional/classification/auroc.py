@@ -11,6 +11,7 @@ import torch
 from torch import Tensor
 from typing_extensions import Literal
 
+from torchmetrics_amd import ops
 from torchmetrics_amd.functional.classification.precision_recall_curve import (
     Thresholds,
     _binary_curve_state,
@@ -104,6 +105,22 @@ def _reduce_scores(
     raise ValueError("Received an incompatible combinations of inputs to make reduction.")
 
 
+def _fused_curve_score(state: Tensor, kind: int, average: Optional[str], name: str) -> Tensor:
+    """Binned AUROC / AP on ROCm: one fused launch (``ops.curve_score``) instead of ~20 ops and two host syncs; the
+    reference's nan warning costs one 4-byte read."""
+    per_class, reduced, nan_flag = ops.curve_score(state, kind, average)
+    if average is None or average == "none":
+        return per_class
+    if average not in ("macro", "weighted"):
+        raise ValueError("Received an incompatible combinations of inputs to make reduction.")
+    if bool(nan_flag.item()):
+        rank_zero_warn(
+            f"{name} score for one or more classes was `nan`. Ignoring these classes in {average}-average",
+            UserWarning,
+        )
+    return reduced
+
+
 def _reduce_auroc(
     fpr: Union[Tensor, List[Tensor]],
     tpr: Union[Tensor, List[Tensor]],
@@ -182,6 +199,8 @@ def _multiclass_auroc_compute(
     thresholds: Optional[Tensor] = None,
 ) -> Tensor:
     if isinstance(state, Tensor) and thresholds is not None:
+        if state.is_cuda:
+            return _fused_curve_score(state, ops.SCORE_AUROC, average, "AUROC")
         fpr, tpr, _ = _multiclass_roc_compute(state, num_classes, thresholds)
         return _reduce_auroc(fpr, tpr, average, weights=state[0][:, 1, :].sum(-1))
     preds, target = state
@@ -234,6 +253,8 @@ def _multilabel_auroc_compute(
     if isinstance(state, Tensor) and thresholds is not None:
         if average == "micro":
             return _binary_auroc_compute(state.sum(1), thresholds, max_fpr=None)
+        if state.is_cuda:
+            return _fused_curve_score(state, ops.SCORE_AUROC, average, "AUROC")
         fpr, tpr, _ = _multilabel_roc_compute(state, num_labels, thresholds, ignore_index)
         return _reduce_auroc(fpr, tpr, average, weights=state[0][:, 1, :].sum(-1))
     preds, target = state

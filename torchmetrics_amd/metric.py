@@ -98,6 +98,8 @@ class Metric(Module, ABC):
     plot_lower_bound: Optional[float] = None
     plot_upper_bound: Optional[float] = None
     plot_legend_name: Optional[str] = None
+    # fold `cat` list states into one tensor before compute() (see _consolidate_cat_lists)
+    _fold_cat_lists: bool = False
 
     def __init__(self, **kwargs: Any) -> None:
         super().__init__()
@@ -438,6 +440,7 @@ class Metric(Module, ABC):
                 return self._computed
             if self._device_errors is not None:
                 self._raise_device_errors()
+            self._consolidate_cat_lists()
             with self.sync_context(
                 dist_sync_fn=self.dist_sync_fn,
                 should_sync=self._to_sync,
@@ -449,6 +452,24 @@ class Metric(Module, ABC):
             return value
 
         return wrapped_func
+
+    def _consolidate_cat_lists(self) -> None:
+        """Replace the elements of every ``cat`` list state by their concatenation, in place (same list object).
+
+        A list state grows by one tensor per update; ``compute()`` concatenates it.  Without this, a loop that calls
+        ``compute()`` every step (per-step logging) re-concatenates every batch seen so far each time: O(steps)
+        launches-worth of host work per call, O(steps^2) overall.  Folding the list into one tensor keeps each
+        ``compute()`` at one ``cat`` of [accumulated, new batches].  The concatenated contents -- the only thing a
+        ``cat`` reduction defines -- are unchanged (the reference folds cat lists the same way when it syncs them,
+        ``S/metric.py:431-433``).  Opt-in per class (``_fold_cat_lists``): a few reference computes look at the
+        list's element structure (e.g. EED averages per-element scores)."""
+        if not self._fold_cat_lists:
+            return
+        for attr, fn in self._reductions.items():
+            if fn is dim_zero_cat:
+                val = getattr(self, attr)
+                if isinstance(val, list) and len(val) > 1:
+                    val[:] = [dim_zero_cat(val)]
 
     @abstractmethod
     def update(self, *_: Any, **__: Any) -> None:

@@ -396,6 +396,58 @@ def feature_moments_update(features: Tensor, feat_sum: Tensor, feat_cov: Tensor)
         _cpu.feature_moments_update(features, feat_sum, feat_cov)
 
 
+# --------------------------------------------------------------------------------------- confmat reductions
+CM_JACCARD, CM_KAPPA, CM_MCC = 0, 1, 2
+_CM_AVG = {"micro": 0, "macro": 1, "weighted": 2, "none": 3, None: 3}
+_KAPPA_W = {None: 0, "none": 0, "linear": 1, "quadratic": 2}
+
+
+def confmat_reducible(confmat: Tensor) -> bool:
+    return confmat.is_cuda and confmat.dim() == 2 and confmat.dtype == torch.int64 and 2 <= confmat.shape[0] <= 4096 \
+        and confmat.shape[0] == confmat.shape[1]
+
+
+def confmat_reduce(confmat: Tensor, kind: int, average: Optional[str] = "macro", ignore_index: Optional[int] = None,
+                   weights: Optional[str] = None) -> Tensor:
+    """Jaccard / Cohen kappa / MCC of a ROCm ``[C, C]`` int64 confusion matrix in one launch
+    (``csrc/classification/confmat_reduce.hip``).  Jaccard returns the per-class ``[C]`` vector for average none."""
+    c = confmat.shape[0]
+    out = torch.empty(c + 1, dtype=torch.float32, device=confmat.device)
+    (_fast_mod or _fast()).confmat_reduce(confmat.contiguous(), kind, _CM_AVG[average],
+                                          -1 if ignore_index is None else int(ignore_index), _KAPPA_W[weights], out)
+    if kind == CM_JACCARD:
+        return out[:c] if average in (None, "none") else out[c]
+    return out[0]
+
+
+def calibration_bins(conf: Tensor, acc: Tensor, bounds: Tensor) -> Tensor:
+    """``[len(bounds), 3]`` (count, Σconf, Σacc) per ``bucketize(conf, bounds, right=True) - 1`` bin, one pass."""
+    nb = bounds.numel()
+    sums = torch.zeros(nb, 3, dtype=torch.float32, device=conf.device)
+    bad = torch.zeros(1, dtype=torch.int32, device=conf.device)
+    (_fast_mod or _fast()).calibration_bins(conf.contiguous(), acc.contiguous(), bounds.float().contiguous(), sums,
+                                            bad)
+    return sums
+
+
+# -------------------------------------------------------------------------------------------- curve scores
+SCORE_AUROC, SCORE_AP = 0, 1
+_AVG_IDS = {None: 0, "none": 0, "macro": 1, "weighted": 2}
+
+
+def curve_score(state: Tensor, kind: int, average: Optional[str]) -> "tuple[Tensor, Tensor, Tensor]":
+    """AUROC / AP of a binned ``[T, C, 2, 2]`` ROCm state in one launch (``csrc/classification/curve.hip``).
+
+    Returns ``(per_class [C], reduced [] , nan_flag i32 [1])``; ``reduced`` is the nan-aware macro / weighted
+    average (undefined for ``average`` none)."""
+    c = state.shape[1]
+    out = torch.empty(c + 1, dtype=torch.float32, device=state.device)
+    flag = torch.empty(1, dtype=torch.int32, device=state.device)
+    (_fast_mod or _fast()).curve_score(state if state.is_contiguous() else state.contiguous(), kind,
+                                       _AVG_IDS[average], out, flag)
+    return out[:c], out[c], flag
+
+
 # ------------------------------------------------------------------------------------------- classification curves
 CURVE_BINARY = 0
 CURVE_MULTILABEL = 1

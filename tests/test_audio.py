@@ -1,6 +1,8 @@
 """Audio metrics (reference ``tests/unittests/audio``).  mir_eval / fast_bss_eval / pesq / pystoi are not installed:
 SNR-family values are pinned to the reference docstrings, SDR to a direct numpy least-squares oracle of the
 distortion-filter projection and to the reference docstring values."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -23,6 +25,7 @@ from torchmetrics_amd.functional.audio import (
     pit_permutate,
     scale_invariant_signal_distortion_ratio,
     scale_invariant_signal_noise_ratio,
+    short_time_objective_intelligibility,
     signal_distortion_ratio,
     signal_noise_ratio,
     source_aggregated_signal_distortion_ratio,
@@ -146,8 +149,126 @@ def test_pit_exhaustive_matches_assignment():
 def test_external_wrappers_gated():
     with pytest.raises(ModuleNotFoundError):
         PerceptualEvaluationSpeechQuality(16000, "wb")
-    with pytest.raises(ModuleNotFoundError):
-        ShortTimeObjectiveIntelligibility(16000)
+
+
+# ---------------------------------------------------------------------------------------------------------- STOI
+# A NumPy transcription of the published STOI / ESTOI algorithm as pystoi implements it (frame grid, silent-frame
+# removal, 1/3-octave bands, 30-frame segments, clipping at -15 dB SDR) -- pystoi itself is not installed, so this
+# is the oracle; the resampler is checked against scipy.signal.resample_poly separately.
+def _np_stoi(x, y, fs, extended):
+    import scipy.signal
+
+    from torchmetrics_amd.functional.audio import stoi as S
+
+    if fs != S.FS:
+        h, up, down = S._octave_resample_filter(S.FS, fs)
+        x = scipy.signal.resample_poly(x, up, down, window=h)
+        y = scipy.signal.resample_poly(y, up, down, window=h)
+    eps = np.finfo("float").eps
+    w = np.hanning(S.N_FRAME + 2)[1:-1]
+    hop = S.N_FRAME // 2
+    xf = np.array([w * x[i:i + S.N_FRAME] for i in range(0, len(x) - S.N_FRAME, hop)])
+    yf = np.array([w * y[i:i + S.N_FRAME] for i in range(0, len(x) - S.N_FRAME, hop)])
+    en = 20 * np.log10(np.linalg.norm(xf, axis=1) + eps)
+    mask = (np.max(en) - S.DYN_RANGE - en) < 0
+    xf, yf = xf[mask], yf[mask]
+
+    def ola(fr):
+        out = np.zeros((len(fr) - 1) * hop + S.N_FRAME)
+        for i, f in enumerate(fr):
+            out[i * hop:i * hop + S.N_FRAME] += f
+        return out
+
+    x, y = ola(xf), ola(yf)
+
+    def spec(sig):
+        return np.array([np.fft.rfft(w * sig[i:i + S.N_FRAME], n=S.NFFT)
+                         for i in range(0, len(sig) - S.N_FRAME, hop)]).T
+
+    xs, ys = spec(x), spec(y)
+    if xs.shape[-1] < S.N_SEG:
+        return 1e-5
+    obm = S._third_octave_matrix()
+    xt = np.sqrt(obm @ np.abs(xs) ** 2)
+    yt = np.sqrt(obm @ np.abs(ys) ** 2)
+    xseg = np.array([xt[:, m - S.N_SEG:m] for m in range(S.N_SEG, xt.shape[1] + 1)])
+    yseg = np.array([yt[:, m - S.N_SEG:m] for m in range(S.N_SEG, xt.shape[1] + 1)])
+    if extended:
+        def rc(a):
+            a = a - a.mean(-1, keepdims=True)
+            a = a / np.sqrt((a ** 2).sum(-1, keepdims=True))
+            a = a - a.mean(1, keepdims=True)
+            return a / np.sqrt((a ** 2).sum(1, keepdims=True))
+
+        xn, yn = rc(xseg), rc(yseg)
+        return np.sum(xn * yn / S.N_SEG) / xn.shape[0]
+    nc = np.linalg.norm(xseg, axis=2, keepdims=True) / (np.linalg.norm(yseg, axis=2, keepdims=True) + eps)
+    yp = np.minimum(yseg * nc, xseg * (1 + 10 ** (-S.BETA / 20)))
+    yp = yp - yp.mean(2, keepdims=True)
+    xc = xseg - xseg.mean(2, keepdims=True)
+    yp /= np.linalg.norm(yp, axis=2, keepdims=True) + eps
+    xc /= np.linalg.norm(xc, axis=2, keepdims=True) + eps
+    return np.sum(yp * xc) / (xc.shape[0] * xc.shape[1])
+
+
+def _speechlike(n, fs, g, silence=True):
+    t = torch.arange(n, dtype=torch.float64) / fs
+    env = (torch.sin(2 * math.pi * 3 * t) ** 2) if silence else 1.0
+    sig = env * (torch.sin(2 * math.pi * 220 * t) + 0.5 * torch.sin(2 * math.pi * 1330 * t)
+                 + 0.3 * torch.randn(n, generator=g, dtype=torch.float64))
+    if silence:
+        sig[: n // 5] *= 1e-4  # a silent lead-in the frame removal must drop
+    return sig
+
+
+@pytest.mark.parametrize("fs", [8000, 10000, 16000])
+def test_resample_matches_scipy(fs):
+    import scipy.signal
+
+    from torchmetrics_amd.functional.audio import stoi as S
+
+    g = torch.Generator().manual_seed(fs)
+    x = torch.randn(3, 4321, generator=g, dtype=torch.float64)
+    h, up, down = S._octave_resample_filter(S.FS, fs)
+    got = S._resample_poly(x, up, down, h)
+    ref = np.stack([scipy.signal.resample_poly(r.numpy(), up, down, window=h) for r in x])
+    np.testing.assert_allclose(got.numpy(), ref, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("fs", [8000, 16000])
+@pytest.mark.parametrize("extended", [False, True])
+def test_stoi_matches_numpy_transcription(fs, extended):
+    g = torch.Generator().manual_seed(fs + extended)
+    clean = torch.stack([_speechlike(fs * 2, fs, g), _speechlike(fs * 2, fs, g, silence=False)])
+    noisy = clean + 0.8 * torch.randn(clean.shape, generator=g, dtype=torch.float64)
+    got = short_time_objective_intelligibility(noisy, clean, fs, extended)
+    ref = torch.tensor([_np_stoi(c.numpy(), n.numpy(), fs, extended) for c, n in zip(clean, noisy)])
+    torch.testing.assert_close(got, ref, rtol=1e-9, atol=1e-9)
+    # sanity: a clean signal scores (near) 1 and noise lowers it
+    same = short_time_objective_intelligibility(clean, clean, fs, extended)
+    assert torch.all(same > 0.99) and torch.all(got < same)
+
+
+def test_stoi_module_and_short_input_warning():
+    g = torch.Generator().manual_seed(0)
+    clean = _speechlike(16000, 16000, g, silence=False).float()
+    m = ShortTimeObjectiveIntelligibility(16000)
+    m.update(clean[None] + 0.1 * torch.randn(1, 16000, generator=g), clean[None])
+    assert 0 < float(m.compute()) < 1
+    with pytest.warns(RuntimeWarning, match="Not enough STFT frames"):
+        v = short_time_objective_intelligibility(torch.rand(2, 800), torch.rand(2, 800), 8000)
+    assert torch.allclose(v, torch.full((2,), 1e-5, dtype=torch.float64))
+
+
+@pytest.mark.gpu
+def test_stoi_gpu_matches_cpu():
+    g = torch.Generator().manual_seed(1)
+    clean = torch.stack([_speechlike(32000, 16000, g) for _ in range(3)])
+    noisy = clean + 0.5 * torch.randn(clean.shape, generator=g, dtype=torch.float64)
+    for ext in (False, True):
+        a = short_time_objective_intelligibility(noisy.cuda(), clean.cuda(), 16000, ext)
+        b = short_time_objective_intelligibility(noisy, clean, 16000, ext)
+        torch.testing.assert_close(a, b, rtol=1e-9, atol=1e-9)
 
 
 @pytest.mark.gpu

@@ -5,10 +5,8 @@ from typing import Any, Callable, Dict, Literal, Optional
 import torch
 from torch import Tensor
 
-from torchmetrics_amd.functional.audio.external import (
-    perceptual_evaluation_speech_quality,
-    short_time_objective_intelligibility,
-)
+from torchmetrics_amd.functional.audio.external import perceptual_evaluation_speech_quality
+from torchmetrics_amd.functional.audio.stoi import short_time_objective_intelligibility
 from torchmetrics_amd.functional.audio.pit import permutation_invariant_training
 from torchmetrics_amd.functional.audio.srmr import _srmr_arg_validate, speech_reverberation_modulation_energy_ratio
 from torchmetrics_amd.functional.audio.snr_sdr import (
@@ -20,7 +18,7 @@ from torchmetrics_amd.functional.audio.snr_sdr import (
     source_aggregated_signal_distortion_ratio,
 )
 from torchmetrics_amd.metric import Metric
-from torchmetrics_amd.utilities.imports import _PESQ_AVAILABLE, _PYSTOI_AVAILABLE
+from torchmetrics_amd.utilities.imports import _PESQ_AVAILABLE
 
 
 class _MeanOfBatch(Metric):
@@ -183,7 +181,8 @@ class PerceptualEvaluationSpeechQuality(_MeanOfBatch):
 
 
 class ShortTimeObjectiveIntelligibility(_MeanOfBatch):
-    """STOI (``S/audio/stoi.py:29``; needs the ``pystoi`` package)."""
+    """STOI / extended STOI (``S/audio/stoi.py:29``); native batched implementation (no ``pystoi``), see
+    :mod:`torchmetrics_amd.functional.audio.stoi`."""
 
     is_differentiable: bool = False
     plot_lower_bound: float = 0.0
@@ -192,10 +191,6 @@ class ShortTimeObjectiveIntelligibility(_MeanOfBatch):
 
     def __init__(self, fs: int, extended: bool = False, **kwargs: Any) -> None:
         super().__init__(**kwargs)
-        if not _PYSTOI_AVAILABLE:
-            raise ModuleNotFoundError(
-                "STOI metric requires that `pystoi` is installed."
-                " Either install as `pip install torchmetrics[audio]` or `pip install pystoi`.")
         self.fs, self.extended = fs, extended
 
     def _batch(self, preds: Tensor, target: Tensor) -> Tensor:

@@ -1,8 +1,6 @@
 """Audio metrics, functional API (reference ``F/audio/__init__.py``)."""
-from torchmetrics_amd.functional.audio.external import (
-    perceptual_evaluation_speech_quality,
-    short_time_objective_intelligibility,
-)
+from torchmetrics_amd.functional.audio.external import perceptual_evaluation_speech_quality
+from torchmetrics_amd.functional.audio.stoi import short_time_objective_intelligibility
 from torchmetrics_amd.functional.audio.pit import permutation_invariant_training, pit_permutate
 from torchmetrics_amd.functional.audio.srmr import speech_reverberation_modulation_energy_ratio
 from torchmetrics_amd.functional.audio.snr_sdr import (

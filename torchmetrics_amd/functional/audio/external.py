@@ -1,6 +1,7 @@
-"""PESQ and STOI (reference ``F/audio/pesq.py``, ``F/audio/stoi.py``): thin wrappers over the ITU-T P.862 ``pesq``
-and ``pystoi`` reference implementations, exactly like the reference.  Neither package is installed in this image, so
-the metrics raise ``ModuleNotFoundError`` at construction / call time, as the reference does."""
+"""PESQ (reference ``F/audio/pesq.py``): a thin wrapper over the ITU-T P.862 ``pesq`` C implementation, exactly like
+the reference (a host-side, standard-defined DSP pipeline; not a GPU target).  The package is not installed in this
+image, so the metric raises ``ModuleNotFoundError`` at construction / call time, as the reference does.  STOI is
+native: :mod:`torchmetrics_amd.functional.audio.stoi`."""
 from typing import Any
 
 import numpy as np
@@ -8,7 +9,7 @@ import torch
 from torch import Tensor
 
 from torchmetrics_amd.utilities.checks import _check_same_shape
-from torchmetrics_amd.utilities.imports import _PESQ_AVAILABLE, _PYSTOI_AVAILABLE
+from torchmetrics_amd.utilities.imports import _PESQ_AVAILABLE
 
 
 def perceptual_evaluation_speech_quality(preds: Tensor, target: Tensor, fs: int, mode: str,
@@ -35,25 +36,5 @@ def perceptual_evaluation_speech_quality(preds: Tensor, target: Tensor, fs: int,
             vals = np.array(vals)
         else:
             vals = np.array([pesq_backend.pesq(fs, t[i], p[i], mode) for i in range(p.shape[0])])
-        val = torch.from_numpy(vals).reshape(preds.shape[:-1])
-    return val.to(preds.device) if keep_same_device else val
-
-
-def short_time_objective_intelligibility(preds: Tensor, target: Tensor, fs: int, extended: bool = False,
-                                         keep_same_device: bool = False) -> Tensor:
-    """STOI / ESTOI per sample (``F/audio/stoi.py:25``)."""
-    if not _PYSTOI_AVAILABLE:
-        raise ModuleNotFoundError(
-            "ShortTimeObjectiveIntelligibility metric requires that `pystoi` is installed."
-            " Either install as `pip install torchmetrics[audio]` or `pip install pystoi`.")
-    from pystoi import stoi as stoi_backend
-
-    _check_same_shape(preds, target)
-    if preds.ndim == 1:
-        val = torch.tensor(stoi_backend(target.detach().cpu().numpy(), preds.detach().cpu().numpy(), fs, extended))
-    else:
-        p = preds.reshape(-1, preds.shape[-1]).detach().cpu().numpy()
-        t = target.reshape(-1, preds.shape[-1]).detach().cpu().numpy()
-        vals = np.array([stoi_backend(t[i], p[i], fs, extended) for i in range(p.shape[0])])
         val = torch.from_numpy(vals).reshape(preds.shape[:-1])
     return val.to(preds.device) if keep_same_device else val

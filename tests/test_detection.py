@@ -303,3 +303,78 @@ def test_panoptic_quality(device, modified):
     m.update(preds[:2].to(device), target[:2].to(device))
     m.update(preds[2:].to(device), target[2:].to(device))
     assert_close(m.compute(), _pq_oracle(preds, target, things, stuffs, modified), atol=1e-9)
+
+
+def _greedy_nms(boxes, scores, thr, idxs=None):
+    """Plain Python greedy NMS (the torchvision rule) as the oracle."""
+    order = sorted(range(len(scores)), key=lambda i: (-float(scores[i]), i))
+    keep = []
+    for i in order:
+        ok = True
+        for j in keep:
+            if idxs is not None and int(idxs[i]) != int(idxs[j]):
+                continue
+            a, b = boxes[i].tolist(), boxes[j].tolist()
+            iw = max(min(a[2], b[2]) - max(a[0], b[0]), 0.0)
+            ih = max(min(a[3], b[3]) - max(a[1], b[1]), 0.0)
+            inter = iw * ih
+            union = (a[2] - a[0]) * (a[3] - a[1]) + (b[2] - b[0]) * (b[3] - b[1]) - inter
+            if inter / union > thr:
+                ok = False
+                break
+        if ok:
+            keep.append(i)
+    return keep
+
+
+def _rand_boxes(n, g, scale=100.0):
+    xy = torch.rand(n, 2, generator=g) * scale
+    wh = torch.rand(n, 2, generator=g) * scale / 4 + 1
+    return torch.cat([xy, xy + wh], 1)
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 130])
+@pytest.mark.parametrize("batched", [False, True])
+def test_nms_cpu_matches_greedy_oracle(n, batched):
+    from torchmetrics_amd.functional.detection import batched_nms, nms
+
+    g = torch.Generator().manual_seed(n)
+    boxes = _rand_boxes(n, g, 30.0)
+    scores = torch.rand(n, generator=g)
+    if n > 3:
+        scores[3] = scores[1]  # a tie: lower index first
+    idxs = torch.randint(0, 3, (n,), generator=g)
+    got = batched_nms(boxes, scores, idxs, 0.3) if batched else nms(boxes, scores, 0.3)
+    assert got.tolist() == _greedy_nms(boxes, scores, 0.3, idxs if batched else None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 5000, 70000])
+@pytest.mark.parametrize("batched", [False, True])
+def test_nms_gpu_matches_cpu(n, batched):
+    """HIP bitmask NMS (csrc/detection/nms.hip) vs the CPU greedy rule: chunk boundaries, ties, class-aware."""
+    from torchmetrics_amd.functional.detection import batched_nms, nms
+
+    g = torch.Generator().manual_seed(n + batched)
+    boxes = _rand_boxes(n, g, 100.0 if n < 20000 else 2000.0)
+    scores = torch.rand(n, generator=g)
+    scores[n // 2:n // 2 + 10] = 0.5  # equal scores across a chunk boundary
+    idxs = torch.randint(0, 5, (n,), generator=g)
+    for thr in (0.3, 0.7):
+        if batched:
+            a = batched_nms(boxes.cuda(), scores.cuda(), idxs.cuda(), thr).cpu()
+            b = batched_nms(boxes, scores, idxs, thr) if n <= 5000 else None
+        else:
+            a = nms(boxes.cuda(), scores.cuda(), thr).cpu()
+            b = nms(boxes, scores, thr) if n <= 5000 else None
+        if b is not None:
+            assert torch.equal(a, b)
+        else:  # large case: kept indices unique, score ordered, and no kept pair (same class) above the threshold
+            assert len(set(a.tolist())) == len(a)
+            assert torch.all(scores[a][1:] <= scores[a][:-1])
+            head = a[:2000]
+            kb = boxes[head].cuda()
+            iou = ops.box_pairwise(kb, kb, ops.BOX_IOU).triu(1)
+            if batched:
+                iou = iou * (idxs[head][:, None] == idxs[head][None, :]).cuda()
+            assert float(iou.max()) <= thr

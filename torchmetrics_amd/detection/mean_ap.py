@@ -109,23 +109,56 @@ class MeanAveragePrecision(Metric):
     # ------------------------------------------------------------------------------------------------ update
     def update(self, preds: List[Dict[str, Tensor]], target: List[Dict[str, Tensor]]) -> None:
         _input_validator(preds, target, iou_type=self.iou_type)
-        for item in preds:
-            box, mask = self._get_safe_item_values(item, warn=self.warn_on_many_detections)
-            if box is not None:
-                self.detection_box.append(box)
-            if mask is not None:
-                self.detection_mask.append(mask)
+        # per-image work is batched over the whole call: one box conversion for all images (the reference converts
+        # image by image, ~4 launches each) and one zero tensor for all missing `iscrowd` / `area` entries
+        det_boxes = self._convert_boxes([item["boxes"] for item in preds]) if "bbox" in self.iou_type else None
+        gt_boxes = self._convert_boxes([item["boxes"] for item in target]) if "bbox" in self.iou_type else None
+        limit = self.max_detection_thresholds[-1]
+        for i, item in enumerate(preds):
+            if det_boxes is not None:
+                self.detection_box.append(det_boxes[i])
+            if "segm" in self.iou_type:
+                self.detection_mask.append(item["masks"].bool())
+            if self.warn_on_many_detections and len(item["labels"]) > limit:
+                _warning_on_too_many_detections(limit)
             self.detection_labels.append(item["labels"])
             self.detection_scores.append(item["scores"])
-        for item in target:
-            box, mask = self._get_safe_item_values(item)
-            if box is not None:
-                self.groundtruth_box.append(box)
-            if mask is not None:
-                self.groundtruth_mask.append(mask)
+        crowds = self._defaults_for(target, "iscrowd")
+        areas = self._defaults_for(target, "area")
+        for i, item in enumerate(target):
+            if gt_boxes is not None:
+                self.groundtruth_box.append(gt_boxes[i])
+            if "segm" in self.iou_type:
+                self.groundtruth_mask.append(item["masks"].bool())
             self.groundtruth_labels.append(item["labels"])
-            self.groundtruth_crowds.append(item.get("iscrowd", torch.zeros_like(item["labels"])))
-            self.groundtruth_area.append(item.get("area", torch.zeros_like(item["labels"])))
+            self.groundtruth_crowds.append(item["iscrowd"] if "iscrowd" in item else crowds[i])
+            self.groundtruth_area.append(item["area"] if "area" in item else areas[i])
+
+    def _convert_boxes(self, boxes: List[Tensor]) -> List[Tensor]:
+        """``box_convert(..., out_fmt="xywh")`` of every non-empty ``[n, 4]`` tensor, as one batched conversion."""
+        fixed = [_fix_empty_tensors(b) for b in boxes]
+        if len(fixed) > 1 and all(b.ndim == 2 and b.shape[-1] == 4 for b in fixed) and \
+                len({(b.device, b.dtype) for b in fixed}) == 1:
+            sizes = [b.shape[0] for b in fixed]
+            return list(torch.split(box_convert(torch.cat(fixed), in_fmt=self.box_format, out_fmt="xywh"), sizes))
+        return [box_convert(b, in_fmt=self.box_format, out_fmt="xywh") if b.numel() > 0 else b for b in fixed]
+
+    @staticmethod
+    def _defaults_for(target: List[Dict[str, Tensor]], key: str) -> List[Optional[Tensor]]:
+        """Zero ``[n_i]`` tensors (``zeros_like(labels)``) for the images without ``key``, carved from one allocation."""
+        missing = [i for i, t in enumerate(target) if key not in t]
+        out: List[Optional[Tensor]] = [None] * len(target)
+        if not missing:
+            return out
+        labels = [target[i]["labels"] for i in missing]
+        if len({(t.device, t.dtype) for t in labels}) == 1 and all(t.ndim == 1 for t in labels):
+            parts = torch.split(torch.zeros(sum(t.numel() for t in labels), dtype=labels[0].dtype,
+                                            device=labels[0].device), [t.numel() for t in labels])
+        else:
+            parts = [torch.zeros_like(t) for t in labels]
+        for i, z in zip(missing, parts):
+            out[i] = z
+        return out
 
     def _get_safe_item_values(self, item: Dict[str, Any], warn: bool = False) -> Tuple[Optional[Tensor], Optional[Tensor]]:
         box, mask = None, None

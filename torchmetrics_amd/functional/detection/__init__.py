@@ -5,6 +5,7 @@ from torchmetrics_amd.functional.detection.iou import (
     generalized_intersection_over_union,
     intersection_over_union,
 )
+from torchmetrics_amd.functional.detection.nms import batched_nms, nms
 from torchmetrics_amd.functional.detection.panoptic_qualities import modified_panoptic_quality, panoptic_quality
 
 __all__ = [k for k in dir() if not k.startswith("_")]

@@ -506,6 +506,17 @@ def box_pairwise(a: Tensor, b: Tensor, op: int = BOX_IOU, aligned: bool = False)
     return _cpu.box_pairwise(a, b, op, aligned)
 
 
+def nms(boxes: Tensor, scores: Tensor, iou_threshold: float, idxs: Optional[Tensor] = None) -> Tensor:
+    """Greedy NMS: indices of the kept ``[N, 4]`` xyxy boxes in descending score order (equal scores: lower index
+    first).  With ``idxs`` only boxes of the same class suppress each other.  ROCm: bitmask-tile kernel + one-wave
+    scan (``csrc/detection/nms.hip``); CPU: the same greedy rule over the IoU matrix."""
+    if boxes.is_cuda:
+        empty = boxes.new_empty(0, dtype=torch.long)
+        return _ops().nms(boxes.contiguous(), scores.contiguous(), empty if idxs is None else idxs.contiguous(),
+                          float(iou_threshold))
+    return _cpu.nms(boxes, scores, iou_threshold, idxs)
+
+
 def coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, gt_cnt, area_rng, iou_thr,
                iou_pre=None, iou_off=None):
     """COCO greedy matching of every (image x class group, area range, IoU threshold); returns ``(dt_match, dt_ig)``

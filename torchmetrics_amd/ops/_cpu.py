@@ -482,3 +482,29 @@ def biquad_cascade(x: Tensor, coefs: Tensor, rep: int, clamp: bool) -> Tensor:
     import numpy as np
 
     return torch.from_numpy(np.stack(rows)) if rows else torch.zeros(0, x.shape[1], dtype=torch.float64)
+
+
+def nms(boxes: Tensor, scores: Tensor, iou_threshold: float, idxs: Optional[Tensor] = None) -> Tensor:
+    n = boxes.shape[0]
+    if n == 0:
+        return torch.empty(0, dtype=torch.long, device=boxes.device)
+    order = torch.sort(scores, descending=True, stable=True).indices
+    b = boxes[order].float()
+    area = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
+    lt = torch.maximum(b[:, None, :2], b[None, :, :2])
+    rb = torch.minimum(b[:, None, 2:], b[None, :, 2:])
+    wh = (rb - lt).clamp(min=0)
+    inter = wh[..., 0] * wh[..., 1]
+    sup = inter / (area[:, None] + area[None, :] - inter) > iou_threshold
+    if idxs is not None:
+        c = idxs[order]
+        sup &= c[:, None] == c[None, :]
+    sup = torch.triu(sup, diagonal=1).cpu()
+    removed = torch.zeros(n, dtype=torch.bool)
+    keep = []
+    for i in range(n):
+        if removed[i]:
+            continue
+        keep.append(i)
+        removed |= sup[i]
+    return order[torch.tensor(keep, dtype=torch.long, device=boxes.device)]

@@ -194,3 +194,19 @@ def test_moments_plan_merging_on_cpu(monkeypatch):
     # first update runs every member (group detection); later ones are merged: pearson fold / centred sums /
     # Minkowski power -> 3 kernel calls for 8 metrics
     assert calls and all(c == 3 for c in calls)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 64, 65, 1000])
+@pytest.mark.parametrize("ties", [False, True])
+def test_kendall_pair_counts_nlogn_matches_allpairs(n, ties):
+    from torchmetrics_amd.functional.regression.correlation import _pair_counts, _pair_counts_allpairs
+
+    g = torch.Generator().manual_seed(n + ties)
+    if ties:
+        x = torch.randint(0, 5, (n, 3), generator=g).float()
+        y = torch.randint(0, 4, (n, 3), generator=g).float()
+    else:
+        x, y = torch.randn(n, 3, generator=g), torch.randn(n, 3, generator=g)
+    c1, d1 = _pair_counts(x, y)
+    c2, d2 = _pair_counts_allpairs(x, y)
+    assert torch.equal(c1, c2) and torch.equal(d1, d2)

@@ -7,8 +7,8 @@ Parity: reference ``F/regression/{pearson,concordance,spearman,kendall,cosine_si
   ``F/regression/pearson.py:56``) and no separate mean/var passes.
 * Spearman: vectorised average-rank with ties (sort + segment means) instead of the reference's Python loop over
   repeated values (``F/regression/spearman.py:42-50``).
-* Kendall: pair counts via a chunked all-pairs comparison on the device (no Python loop per element,
-  reference ``F/regression/kendall.py:61-85``).
+* Kendall: concordant / discordant counts in O(n log^2 n) (lexicographic sort + merge-sort inversion count,
+  batched over columns) instead of the reference's O(n^2) Python loop over i (``F/regression/kendall.py:61-85``).
 """
 import math
 from typing import Optional, Tuple, Union
@@ -206,8 +206,58 @@ class _TestAlternative(EnumStr):
         return "alternative"
 
 
-def _pair_counts(x: Tensor, y: Tensor, chunk: int = 2048) -> Tuple[Tensor, Tensor]:
-    """Concordant / discordant pair counts per column of ``[n, k]`` inputs (strict in both coordinates)."""
+def _tied_pairs(sorted_vals: Tensor, *more: Tensor) -> Tensor:
+    """Per column of ``[n, k]`` columns sorted so equal keys are adjacent: the number of pairs with equal keys
+    (sum over runs of t (t - 1) / 2), from each element's position inside its run."""
+    n = sorted_vals.shape[0]
+    if n < 2:
+        return torch.zeros(sorted_vals.shape[1], dtype=torch.int64, device=sorted_vals.device)
+    eq = sorted_vals[1:] == sorted_vals[:-1]
+    for m in more:
+        eq &= m[1:] == m[:-1]
+    idx = torch.arange(n, device=sorted_vals.device).unsqueeze(1).expand(n, sorted_vals.shape[1])
+    new_run = torch.ones_like(idx, dtype=torch.bool)
+    new_run[1:] = ~eq
+    start = torch.cummax(torch.where(new_run, idx, torch.zeros_like(idx)), dim=0).values
+    return (idx - start).sum(0)
+
+
+def _pair_counts(x: Tensor, y: Tensor) -> Tuple[Tensor, Tensor]:
+    """Concordant / discordant pair counts per column of ``[n, k]`` inputs in O(n log^2 n) (Knight's method).
+
+    Sort lexicographically by (x, y); the discordant pairs are then exactly the strict inversions of the y sequence
+    (pairs tied in x are ordered by y, pairs tied in y are not inversions), counted by a bottom-up merge sort whose
+    every pass is one batched ``searchsorted`` (right-run elements vs the sorted left run) + one batched sort.  The
+    concordant count follows from n(n-1)/2 - ties(x) - ties(y) + joint ties - discordant.  The reference compares all
+    pairs with a Python loop over i (``F/regression/kendall.py:61-85``)."""
+    n, k = x.shape
+    if n < 2:
+        z = torch.zeros(k, dtype=torch.int64, device=x.device)
+        return z, z.clone()
+    o1 = torch.argsort(y, dim=0, stable=True)
+    ys1 = torch.gather(y, 0, o1)
+    o2 = torch.argsort(torch.gather(x, 0, o1), dim=0, stable=True)
+    order = torch.gather(o1, 0, o2)
+    xs, ys = torch.gather(x, 0, order), torch.gather(y, 0, order)
+    size = 1 << (n - 1).bit_length()
+    seq = ys.t().double()
+    if size > n:
+        seq = torch.cat([seq, seq.new_full((k, size - n), float("inf"))], 1)
+    disc = torch.zeros(k, dtype=torch.int64, device=x.device)
+    w = 1
+    while w < size:
+        blocks = seq.reshape(k, size // (2 * w), 2, w)
+        left, right = blocks[:, :, 0].contiguous(), blocks[:, :, 1].contiguous()
+        disc += (w - torch.searchsorted(left, right, right=True)).sum(dim=(1, 2))
+        seq = torch.sort(blocks.reshape(k, size // (2 * w), 2 * w), dim=-1).values.reshape(k, size)
+        w *= 2
+    pairs = n * (n - 1) // 2
+    conc = pairs - _tied_pairs(xs) - _tied_pairs(ys1) + _tied_pairs(xs, ys) - disc
+    return conc, disc
+
+
+def _pair_counts_allpairs(x: Tensor, y: Tensor, chunk: int = 2048) -> Tuple[Tensor, Tensor]:
+    """O(n^2) chunked all-pairs reference of :func:`_pair_counts` (kept for tests)."""
     n = x.shape[0]
     conc = torch.zeros(x.shape[1], dtype=torch.int64, device=x.device)
     disc = torch.zeros_like(conc)

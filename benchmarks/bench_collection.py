@@ -55,6 +55,9 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--sync-every-step", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the tensor-state members' updates from HIP graphs (utils.graphs.GraphedUpdate); the "
+                         "list-state member (calibration error) stays eager")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -70,10 +73,24 @@ def main() -> None:
     xs = [torch.randn(BATCH, generator=g).to(device) for _ in range(NBUF)]
     ys = [(x + 0.3 * torch.randn(BATCH, generator=g).to(device)) for x in xs]
     cls, reg = build(device)
+    upd_cls, upd_reg = cls.update, reg.update
+    if args.graph:
+        from torchmetrics_amd.utils.graphs import GraphedUpdate
+
+        ece = cls["ece"]
+        cls_graph = MetricCollection({k: m for k, m in cls.items(keep_base=True) if k != "ece"}, compute_groups=True)
+        g_cls = GraphedUpdate(cls_graph, logits[0], labels[0])
+        g_reg = GraphedUpdate(reg, xs[0], ys[0])
+
+        def upd_cls(p, t):  # noqa: F811
+            g_cls(p, t)
+            ece.update(p, t)
+
+        upd_reg = g_reg
 
     def step(i):
-        cls.update(logits[i % NBUF], labels[i % NBUF])
-        reg.update(xs[i % NBUF], ys[i % NBUF])
+        upd_cls(logits[i % NBUF], labels[i % NBUF])
+        upd_reg(xs[i % NBUF], ys[i % NBUF])
         if args.sync_every_step:
             cls.compute()
             reg.compute()
@@ -87,7 +104,11 @@ def main() -> None:
     for i in range(args.warmup):
         step(i)
     cls.compute(), reg.compute()
-    cls.reset(), reg.reset()
+    if args.graph:  # reset() re-creates the state tensors: reset through the graphed collection, then re-capture
+        cls_graph.reset(), ece.reset(), reg.reset()
+        g_cls.recapture(), g_reg.recapture()
+    else:
+        cls.reset(), reg.reset()
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -104,7 +125,7 @@ def main() -> None:
             "bench": "metric_collection_20", "metric": "metric-updates/sec (whole node)",
             "value": round(world * args.steps * 20 / elapsed, 1), "unit": "metric-updates/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "sync_every_step": args.sync_every_step, "compute_groups": True, "dtype": "bf16", "data": "synthetic",
+            "sync_every_step": args.sync_every_step, "compute_groups": True, "hip_graph": args.graph, "dtype": "bf16", "data": "synthetic",
             "groups": len(cls.compute_groups), "acc": float(out["acc"]), "r2": float(out["r2"]),
         }), flush=True)
     if world > 1:

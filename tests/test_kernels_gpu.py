@@ -324,3 +324,55 @@ def test_calibration_bins_matches_cpu(n_bins):
     got = _binning_bucketize(conf.to(DEV), acc.to(DEV), bounds.to(DEV))
     for a, b in zip(got, ref):
         torch.testing.assert_close(a.cpu(), b, rtol=1e-4, atol=1e-6)
+
+
+def test_graphed_update_matches_eager():
+    """HIP-graph replay of update (utils.graphs.GraphedUpdate) for a metric and two collections equals eager updates;
+    list-state metrics are refused; reset + recapture works."""
+    import torchmetrics_amd as tm
+    from torchmetrics_amd import classification as C
+    from torchmetrics_amd import regression as R
+    from torchmetrics_amd.utils.graphs import GraphedUpdate
+
+    def cls_coll():
+        return tm.MetricCollection({
+            "acc": C.MulticlassAccuracy(10), "f1": C.MulticlassF1Score(10), "cm": C.MulticlassConfusionMatrix(10),
+            "jacc": C.MulticlassJaccardIndex(10), "mcc": C.MulticlassMatthewsCorrCoef(10),
+            "auroc": C.MulticlassAUROC(10, thresholds=50), "ap": C.MulticlassAveragePrecision(10, thresholds=50),
+        }, compute_groups=True).to(DEV)
+
+    def reg_coll():
+        return tm.MetricCollection({"mse": R.MeanSquaredError(), "mae": R.MeanAbsoluteError(), "r2": R.R2Score(),
+                                    "pearson": R.PearsonCorrCoef(), "ev": R.ExplainedVariance()}).to(DEV)
+
+    g = torch.Generator().manual_seed(0)
+    batches = [(torch.randn(512, 10, generator=g).to(DEV, torch.bfloat16), torch.randint(0, 10, (512,), generator=g).to(DEV),
+                torch.randn(512, generator=g).to(DEV)) for _ in range(5)]
+    eager_c, eager_r, eager_m = cls_coll(), reg_coll(), C.MulticlassConfusionMatrix(10).to(DEV)
+    graph_c, graph_r, graph_m = cls_coll(), reg_coll(), C.MulticlassConfusionMatrix(10).to(DEV)
+    gc = GraphedUpdate(graph_c, batches[0][0], batches[0][1])
+    gr = GraphedUpdate(graph_r, batches[0][2], batches[0][2] * 0.5 + 0.1)
+    gm = GraphedUpdate(graph_m, batches[0][0], batches[0][1])
+    for p, t, x in batches:
+        y = x * 0.5 + 0.1 * torch.sin(x)
+        eager_c.update(p, t)
+        eager_r.update(x, y)
+        eager_m.update(p, t)
+        gc(p, t)
+        gr(x, y)
+        gm(p, t)
+    a, b = graph_c.compute(), eager_c.compute()
+    for k in b:
+        torch.testing.assert_close(a[k], b[k])
+    a, b = graph_r.compute(), eager_r.compute()
+    for k in b:
+        torch.testing.assert_close(a[k], b[k], rtol=1e-5, atol=1e-6)
+    assert torch.equal(graph_m.compute(), eager_m.compute()) and graph_m.update_count == eager_m.update_count == 5
+    graph_m.reset()
+    gm.recapture()
+    gm(batches[0][0], batches[0][1])
+    eager_m.reset()
+    eager_m.update(batches[0][0], batches[0][1])
+    assert torch.equal(graph_m.compute(), eager_m.compute())
+    with pytest.raises(ValueError, match="list state"):
+        GraphedUpdate(C.MulticlassCalibrationError(10).to(DEV), batches[0][0], batches[0][1])

@@ -1,0 +1,103 @@
+"""HIP-graph capture of ``update`` for fixed-shape evaluation loops.
+
+A metric ``update`` on MI355X is a handful of short kernels; with a whole ``MetricCollection`` the host-side Python
+and launch work per step (tens of µs) exceeds the GPU time.  :class:`GraphedUpdate` records ``target.update`` once
+into a HIP graph (``torch.cuda.CUDAGraph`` is hipGraph on ROCm) and replays it for each new batch: the replay is one
+graph launch plus one device copy per input, whatever the number of metrics and kernels.
+
+Constraints (checked at capture):
+
+* every state is a tensor updated in place -- list ("cat") states grow by appending new tensors and cannot be
+  replayed (``MulticlassCalibrationError``, unbinned curves, retrieval ...): keep those metrics eager;
+* the update must not rebind a state to a new tensor object, nor synchronise with the host;
+* inputs keep the example's shapes / dtypes (a new shape needs a new capture).
+
+The metric's Python bookkeeping (``update_count``, the ``compute`` cache) is advanced on every replay, so
+``compute()``, ``reset()``, sync and ``state_dict`` behave exactly as after eager updates.  ``reset()`` re-creates the
+state tensors, so a graph must be re-captured after a reset (``GraphedUpdate.recapture``).
+"""
+from typing import Any, Dict, List, Tuple, Union
+
+import torch
+from torch import Tensor
+
+from torchmetrics_amd.collections import MetricCollection
+from torchmetrics_amd.metric import Metric
+
+
+def _members(target: Union[Metric, MetricCollection]) -> List[Tuple[str, Metric]]:
+    if isinstance(target, MetricCollection):
+        return list(target.items(keep_base=True, copy_state=False))
+    return [(type(target).__name__, target)]
+
+
+def _states(metrics: List[Tuple[str, Metric]]) -> Dict[Tuple[str, str], Any]:
+    return {(name, attr): getattr(m, attr) for name, m in metrics for attr in m._defaults}
+
+
+class GraphedUpdate:
+    """``GraphedUpdate(metric_or_collection, *example_inputs)``; then call it with each batch instead of ``update``."""
+
+    def __init__(self, target: Union[Metric, MetricCollection], *example_inputs: Tensor, warmup: int = 2) -> None:
+        if not example_inputs or not all(isinstance(a, Tensor) and a.is_cuda for a in example_inputs):
+            raise ValueError("GraphedUpdate needs the example inputs as ROCm tensors")
+        self.target = target
+        self._members = _members(target)
+        for name, m in self._members:
+            for attr in m._defaults:
+                if not isinstance(getattr(m, attr), Tensor):
+                    raise ValueError(f"metric `{name}` has the list state `{attr}`: it cannot be replayed from a graph")
+        self._static = [a.detach().clone() for a in example_inputs]
+        self._warmup = warmup
+        self._capture()
+
+    def _capture(self) -> None:
+        members = self._members
+        counts = {name: m._update_count for name, m in members}
+        # warm up on a side stream (workspaces, compute groups, lazily-created buffers reach their steady state)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        snapshot = None
+        with torch.cuda.stream(side):
+            for _ in range(max(self._warmup, 1)):
+                before = _states(members)
+                if snapshot is None:
+                    snapshot = {k: v.clone() for k, v in before.items()}
+                self.target.update(*self._static)
+        torch.cuda.current_stream().wait_stream(side)
+        before = _states(members)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.target.update(*self._static)
+        after = _states(members)
+        rebound = [f"{n}.{a}" for (n, a), t in after.items() if t is not before[(n, a)]]
+        if rebound:
+            raise RuntimeError(f"update() rebinds states {rebound}: not capturable, keep these metrics eager")
+        # undo the warm-up updates: the captured graph has not executed yet
+        with torch.no_grad():
+            for key, val in _states(members).items():
+                val.copy_(snapshot[key] if key in snapshot else val)
+        for name, m in members:
+            m.__dict__["_update_count"] = counts[name]
+            m.__dict__["_computed"] = None
+
+    def recapture(self) -> None:
+        """Capture again (after ``reset()`` re-created the state tensors, or after moving the metric)."""
+        self._capture()
+
+    def __call__(self, *inputs: Tensor) -> None:
+        if len(inputs) != len(self._static):
+            raise ValueError(f"expected {len(self._static)} inputs, got {len(inputs)}")
+        for s, x in zip(self._static, inputs):
+            if x.shape != s.shape or x.dtype != s.dtype:
+                raise ValueError(f"input of shape {tuple(x.shape)} / {x.dtype} does not match the captured "
+                                 f"{tuple(s.shape)} / {s.dtype}; capture a new GraphedUpdate for it")
+            s.copy_(x, non_blocking=True)
+        self.graph.replay()
+        for _, m in self._members:
+            d = m.__dict__
+            d["_update_count"] += 1
+            d["_computed"] = None
+
+
+__all__ = ["GraphedUpdate"]

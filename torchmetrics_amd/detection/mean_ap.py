@@ -160,19 +160,6 @@ class MeanAveragePrecision(Metric):
             out[i] = z
         return out
 
-    def _get_safe_item_values(self, item: Dict[str, Any], warn: bool = False) -> Tuple[Optional[Tensor], Optional[Tensor]]:
-        box, mask = None, None
-        if "bbox" in self.iou_type:
-            box = _fix_empty_tensors(item["boxes"])
-            if box.numel() > 0:
-                box = box_convert(box, in_fmt=self.box_format, out_fmt="xywh")
-        if "segm" in self.iou_type:
-            mask = item["masks"].bool()
-        limit = self.max_detection_thresholds[-1]
-        if warn and ((box is not None and len(box) > limit) or (mask is not None and len(mask) > limit)):
-            _warning_on_too_many_detections(limit)
-        return box, mask
-
     # ----------------------------------------------------------------------------------------------- compute
     def _get_classes(self) -> List[int]:
         if len(self.detection_labels) > 0 or len(self.groundtruth_labels) > 0:

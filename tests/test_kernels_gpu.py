@@ -376,3 +376,80 @@ def test_graphed_update_matches_eager():
     assert torch.equal(graph_m.compute(), eager_m.compute())
     with pytest.raises(ValueError, match="list state"):
         GraphedUpdate(C.MulticlassCalibrationError(10).to(DEV), batches[0][0], batches[0][1])
+
+
+# ------------------------------------------------------------------ fused regression compute (regression_compute.hip)
+def _reg_cases():
+    g = torch.Generator().manual_seed(7)
+    t = torch.randn(500, 4, generator=g)
+    p = t + 0.3 * torch.randn(500, 4, generator=g)
+    p[:, 1] = t[:, 1]  # perfect column: zero numerator / rss
+    t2 = t.clone()
+    t2[:, 2] = 1.5  # constant target column: zero denominator / tss
+    p2 = p.clone()
+    p2[:, 3] = 2.0  # constant prediction column (Pearson low variance)
+    return [(p, t), (p, t2), (p2, t2), (p[:, 0], t[:, 0])]
+
+
+@pytest.mark.parametrize("case", range(4))
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("multioutput", ["raw_values", "uniform_average", "variance_weighted"])
+def test_fused_ev_r2_compute_matches_cpu(case, dtype, multioutput):
+    from torchmetrics_amd.functional.regression.streaming import (
+        _explained_variance_compute, _explained_variance_update, _r2_score_compute, _r2_score_update)
+
+    p, t = (x.to(dtype) for x in _reg_cases()[case])
+    ev_states = _explained_variance_update(p, t)
+    ref = _explained_variance_compute(*ev_states, multioutput)
+    got = _explained_variance_compute(*(s.to(DEV) if isinstance(s, torch.Tensor) else s for s in ev_states),
+                                      multioutput)
+    assert got.shape == ref.shape and got.is_cuda
+    torch.testing.assert_close(got.cpu(), ref, rtol=1e-5, atol=1e-6, equal_nan=True)
+    r2_states = _r2_score_update(p, t)
+    for n in (r2_states[3], torch.tensor(r2_states[3])):
+        ref = _r2_score_compute(*r2_states[:3], n, 0, multioutput)
+        got = _r2_score_compute(*(s.to(DEV) for s in r2_states[:3]), n.to(DEV) if isinstance(n, torch.Tensor) else n,
+                                0, multioutput)
+        assert got.shape == ref.shape and got.is_cuda
+        torch.testing.assert_close(got.cpu(), ref, rtol=1e-5, atol=1e-6, equal_nan=True)
+
+
+def test_fused_r2_module_paths():
+    from torchmetrics_amd.regression import R2Score
+
+    p, t = _reg_cases()[0]
+    for adjusted in (0, 2):
+        cpu, gpu = R2Score(num_outputs=4, adjusted=adjusted), R2Score(num_outputs=4, adjusted=adjusted).to(DEV)
+        cpu.update(p, t)
+        gpu.update(p.to(DEV), t.to(DEV))
+        torch.testing.assert_close(gpu.compute().cpu(), cpu.compute(), rtol=1e-5, atol=1e-6)
+    one = R2Score().to(DEV)
+    one.update(p[:1, 0].to(DEV), t[:1, 0].to(DEV))
+    with pytest.raises(ValueError, match="at least two samples"):
+        one.compute()
+
+
+@pytest.mark.parametrize("case", range(4))
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_fused_pearson_concordance_matches_cpu(case, dtype):
+    from torchmetrics_amd.regression import ConcordanceCorrCoef, PearsonCorrCoef
+
+    p, t = (x.to(dtype) for x in _reg_cases()[case])
+    k = p.shape[1] if p.ndim == 2 else 1
+    for cls in (PearsonCorrCoef, ConcordanceCorrCoef):
+        cpu, gpu = cls(num_outputs=k), cls(num_outputs=k).to(DEV)
+        if dtype == torch.float64:
+            cpu, gpu = cpu.double(), gpu.double()
+        for lo in range(0, 500, 128):
+            cpu.update(p[lo:lo + 128], t[lo:lo + 128])
+            gpu.update(p[lo:lo + 128].to(DEV), t[lo:lo + 128].to(DEV))
+        with warnings.catch_warnings(record=True) as wc:
+            warnings.simplefilter("always")
+            ref = cpu.compute()
+        with warnings.catch_warnings(record=True) as wg:
+            warnings.simplefilter("always")
+            got = gpu.compute()
+        assert got.shape == ref.shape
+        torch.testing.assert_close(got.cpu(), ref, rtol=1e-4, atol=1e-5, equal_nan=True)
+        low = lambda ws: any("variance of predictions or target" in str(w.message) for w in ws)  # noqa: E731
+        assert low(wg) == low(wc)

@@ -124,26 +124,32 @@ class MetricCollection(ModuleDict):
 
     def _compute_groups_create_state_ref(self, copy: bool = False) -> None:
         """Point every group member's states at the leader's (or deep-copy them when ``copy``)."""
-        if not self._state_is_copy:
+        # called by every items() / values() / [] access: plain attributes go straight to __dict__ (they live there;
+        # nn.Module.__setattr__ costs ~1 us per call), states through setattr only when a reference is stale
+        d = self.__dict__
+        if not d["_state_is_copy"]:
+            modules = self._modules
             for cg in self._groups.values():
-                m0 = getattr(self, cg[0])
+                m0 = modules[cg[0]]
+                d0 = m0.__dict__
                 for name in cg[1:]:
-                    mi = getattr(self, name)
+                    mi = modules[name]
+                    di = mi.__dict__
                     for state in m0._defaults:
                         val = getattr(m0, state)
                         if copy:
                             setattr(mi, state, deepcopy(val))
-                        elif mi.__dict__.get(state, None) is not val and getattr(mi, state) is not val:
-                            setattr(mi, state, val)  # Module.__setattr__ is costly: only re-point stale refs
-                    mi._update_count = deepcopy(m0._update_count) if copy else m0._update_count
+                        elif di.get(state, None) is not val and getattr(mi, state) is not val:
+                            setattr(mi, state, val)
+                    di["_update_count"] = d0["_update_count"]
                     # members share the leader's *states*, not its result: only propagate cache invalidation (the
                     # reference copies the leader's cached value, so a second compute() without an update returned
                     # the leader's result for every member, S/collections.py:307)
                     if copy:
-                        mi._computed = deepcopy(mi._computed)
-                    elif m0._computed is None:
-                        mi._computed = None
-        self._state_is_copy = copy
+                        di["_computed"] = deepcopy(di["_computed"])
+                    elif d0["_computed"] is None:
+                        di["_computed"] = None
+        d["_state_is_copy"] = copy
 
     def compute(self) -> Dict[str, Any]:
         return self._compute_and_reduce("compute")
@@ -192,10 +198,26 @@ class MetricCollection(ModuleDict):
                     m._to_sync = False
         return restore
 
+    def _check_device_errors(self) -> None:
+        """Read every member's deferred-validation flag word with ONE device sync (a stack + one ``.item()``) instead
+        of one per member; clean members then skip their own read in ``compute()`` (any raised flag is left for its
+        metric to raise with its own message)."""
+        pending = [m for m in self._modules.values()
+                   if m.__dict__["_device_errors"] is not None and m.__dict__["_computed"] is None]
+        if len(pending) < 2:
+            return
+        bufs = [m.__dict__["_device_errors"] for m in pending]
+        if any(b.device != bufs[0].device for b in bufs):
+            return
+        if not bool(torch.cat(bufs).any()):
+            for m in pending:
+                m.__dict__["_device_errors_clean"] = True
+
     def _compute_and_reduce(self, method_name: str, *args: Any, **kwargs: Any) -> Dict[str, Any]:
         result = {}
         restore: List[Tuple[Metric, bool]] = []
         if method_name == "compute":
+            self._check_device_errors()
             restore = self._collection_sync()
         try:
             for k, m in self.items(keep_base=True, copy_state=False):
@@ -207,6 +229,8 @@ class MetricCollection(ModuleDict):
                     raise ValueError(f"method_name should be either 'compute' or 'forward', but got {method_name}")
                 result[k] = res
         finally:
+            for m in self._modules.values():
+                m.__dict__.pop("_device_errors_clean", None)
             for m, to_sync in restore:
                 if m._is_synced:
                     m.unsync()

@@ -76,7 +76,32 @@ def _pearson_corrcoef_update(
     return new_mean_x, new_mean_y, new_var_x, new_var_y, new_corr, num_prior + n
 
 
+_LOW_VAR_WARNING = (
+    "The variance of predictions or target is close to zero. This can cause instability in Pearson correlation"
+    "coefficient, leading to wrong results. Consider re-scaling the input if possible or computing using a"
+    "larger dtype (currently using {}).")
+
+
+def _fused_corr(kind: int, mean_x: Optional[Tensor], mean_y: Optional[Tensor], var_x: Tensor, var_y: Tensor,
+                corr_xy: Tensor, nb: Tensor) -> Optional[Tensor]:
+    """Pearson / concordance of ROCm f32 / f64 states in one launch (None: not eligible)."""
+    if not var_x.is_cuda:
+        return None
+    states = (mean_x if mean_x is not None else var_x, mean_y if mean_y is not None else var_y, var_x, var_y, corr_xy)
+    if not ops.regression_computable(states, nb):
+        return None
+    bound = math.sqrt(torch.finfo(var_x.dtype).eps)
+    out = ops.regression_compute(kind, states, nb, 0, bound)
+    k = var_x.numel()
+    if bool(out[k + 1]):
+        rank_zero_warn(_LOW_VAR_WARNING.format(var_x.dtype), UserWarning)
+    return out[:k].view(var_x.shape)
+
+
 def _pearson_corrcoef_compute(var_x: Tensor, var_y: Tensor, corr_xy: Tensor, nb: Tensor) -> Tensor:
+    fused = _fused_corr(ops.REG_PEARSON, None, None, var_x, var_y, corr_xy, nb)
+    if fused is not None:
+        return fused.squeeze()
     var_x = var_x / (nb - 1)
     var_y = var_y / (nb - 1)
     corr_xy = corr_xy / (nb - 1)
@@ -84,12 +109,7 @@ def _pearson_corrcoef_compute(var_x: Tensor, var_y: Tensor, corr_xy: Tensor, nb:
         var_x, var_y = var_x.bfloat16(), var_y.bfloat16()
     bound = math.sqrt(torch.finfo(var_x.dtype).eps)
     if (var_x < bound).any() or (var_y < bound).any():
-        rank_zero_warn(
-            "The variance of predictions or target is close to zero. This can cause instability in Pearson correlation"
-            "coefficient, leading to wrong results. Consider re-scaling the input if possible or computing using a"
-            f"larger dtype (currently using {var_x.dtype}).",
-            UserWarning,
-        )
+        rank_zero_warn(_LOW_VAR_WARNING.format(var_x.dtype), UserWarning)
     corr = (corr_xy / (var_x * var_y).sqrt()).squeeze()
     return torch.clamp(corr, -1.0, 1.0)
 
@@ -123,6 +143,9 @@ def pearson_corrcoef(preds: Tensor, target: Tensor) -> Tensor:
 def _concordance_corrcoef_compute(
     mean_x: Tensor, mean_y: Tensor, var_x: Tensor, var_y: Tensor, corr_xy: Tensor, nb: Tensor
 ) -> Tensor:
+    fused = _fused_corr(ops.REG_CONCORDANCE, mean_x, mean_y, var_x, var_y, corr_xy, nb)
+    if fused is not None:
+        return fused
     pearson = _pearson_corrcoef_compute(var_x, var_y, corr_xy, nb)
     vx, vy = var_x / (nb - 1), var_y / (nb - 1)
     return 2.0 * pearson * vx.sqrt() * vy.sqrt() / (vx + vy + (mean_x - mean_y) ** 2)

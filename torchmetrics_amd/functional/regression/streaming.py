@@ -189,6 +189,15 @@ def _r2_score_compute(
     adjusted: int = 0,
     multioutput: str = "uniform_average",
 ) -> Tensor:
+    mo = ops.MULTIOUT_IDS.get(multioutput)
+    if mo is not None and sum_obs.is_cuda and ops.regression_computable((sum_squared_obs, sum_obs, rss), num_obs):
+        # one launch for the per-output scores and their average (csrc/regression/regression_compute.hip)
+        out = ops.regression_compute(ops.REG_R2, (sum_squared_obs, sum_obs, rss), num_obs, mo)
+        if num_obs < 2:
+            raise ValueError("Needs at least two samples to calculate r2 score.")
+        k = sum_obs.numel()
+        r2 = out[:k].view(sum_obs.shape) if mo == 0 else out[k]
+        return _r2_adjust(r2, num_obs, adjusted)
     if num_obs < 2:
         raise ValueError("Needs at least two samples to calculate r2 score.")
     mean_obs = sum_obs / num_obs
@@ -208,6 +217,10 @@ def _r2_score_compute(
             "Argument `multioutput` must be either `raw_values`,"
             f" `uniform_average` or `variance_weighted`. Received {multioutput}."
         )
+    return _r2_adjust(r2, num_obs, adjusted)
+
+
+def _r2_adjust(r2: Tensor, num_obs: Union[int, Tensor], adjusted: int) -> Tensor:
     if adjusted < 0 or not isinstance(adjusted, int):
         raise ValueError("`adjusted` parameter should be an integer larger or equal to 0.")
     if adjusted != 0:
@@ -264,6 +277,12 @@ def _explained_variance_compute(
     sum_squared_target: Tensor,
     multioutput: str = "uniform_average",
 ) -> Tensor:
+    states = (sum_error, sum_squared_error, sum_target, sum_squared_target)
+    mo = ops.MULTIOUT_IDS.get(multioutput)
+    if mo is not None and sum_error.is_cuda and ops.regression_computable(states, num_obs):
+        out = ops.regression_compute(ops.REG_EV, states, num_obs, mo)
+        k = sum_error.numel()
+        return out[:k].view(sum_error.shape) if mo == 0 else out[k]
     diff_avg = sum_error / num_obs
     numerator = sum_squared_error / num_obs - diff_avg * diff_avg
     target_avg = sum_target / num_obs

@@ -436,19 +436,25 @@ class Metric(Module, ABC):
                     " as metric states have not yet been updated.",
                     UserWarning,
                 )
-            if self._computed is not None:
-                return self._computed
-            if self._device_errors is not None:
+            state = self.__dict__
+            if state["_computed"] is not None:
+                return state["_computed"]
+            if state["_device_errors"] is not None and not state.pop("_device_errors_clean", False):
                 self._raise_device_errors()
             self._consolidate_cat_lists()
-            with self.sync_context(
-                dist_sync_fn=self.dist_sync_fn,
-                should_sync=self._to_sync,
-                should_unsync=self._should_unsync,
-            ):
+            avail = state["distributed_available_fn"]
+            if not state["_is_synced"] and not (state["_to_sync"] and callable(avail) and avail()):
+                # nothing to gather: skip the sync / unsync context (generator + attribute traffic per call)
                 value = _squeeze_if_scalar(compute(*args, **kwargs))
-            if self.compute_with_cache:
-                self._computed = value
+            else:
+                with self.sync_context(
+                    dist_sync_fn=self.dist_sync_fn,
+                    should_sync=self._to_sync,
+                    should_unsync=self._should_unsync,
+                ):
+                    value = _squeeze_if_scalar(compute(*args, **kwargs))
+            if state["compute_with_cache"]:
+                state["_computed"] = value
             return value
 
         return wrapped_func

@@ -13,7 +13,7 @@ Every op has exactly two implementations, selected by the *device of its inputs*
 import os
 import threading
 from pathlib import Path
-from typing import Optional
+from typing import Optional, Sequence, Union
 
 import torch
 from torch import Tensor
@@ -428,6 +428,44 @@ def calibration_bins(conf: Tensor, acc: Tensor, bounds: Tensor) -> Tensor:
     (_fast_mod or _fast()).calibration_bins(conf.contiguous(), acc.contiguous(), bounds.float().contiguous(), sums,
                                             bad)
     return sums
+
+
+# ------------------------------------------------------------------------------------- regression ratio scores
+REG_EV, REG_R2, REG_PEARSON, REG_CONCORDANCE = 0, 1, 2, 3
+MULTIOUT_IDS = {"raw_values": 0, "uniform_average": 1, "variance_weighted": 2}
+_REG_STATE_DTYPES = (torch.float32, torch.float64)
+_REG_N_DTYPES = (torch.float32, torch.float64, torch.int64)
+
+
+def regression_computable(states: Sequence[Tensor], n: Union[Tensor, int, float]) -> bool:
+    """True when :func:`regression_compute` takes these states: ROCm, contiguous, one f32/f64 dtype, equal sizes."""
+    s0 = states[0]
+    if not s0.is_cuda or s0.dtype not in _REG_STATE_DTYPES or not s0.is_contiguous():
+        return False
+    dev, k, dt = s0.get_device(), s0.numel(), s0.dtype
+    if k < 1 or k > (1 << 20):
+        return False
+    for s in states[1:]:
+        if not (s.is_cuda and s.get_device() == dev and s.dtype == dt and s.numel() == k and s.is_contiguous()):
+            return False
+    if isinstance(n, Tensor):
+        return (n.is_cuda and n.get_device() == dev and n.dtype in _REG_N_DTYPES and n.numel() in (1, k)
+                and n.is_contiguous())
+    return isinstance(n, (int, float))
+
+
+def regression_compute(kind: int, states: Sequence[Tensor], n: Union[Tensor, int, float], multioutput: int,
+                       bound: float = 0.0) -> Tensor:
+    """Explained variance / R^2 / Pearson / concordance from their running sums in one launch
+    (``csrc/regression/regression_compute.hip``).  Returns ``[k + 2]``: the per-output scores, the
+    ``multioutput`` average and the low-variance flag (Pearson / concordance)."""
+    s0 = states[0]
+    out = torch.empty(s0.numel() + 2, dtype=s0.dtype, device=s0.device)
+    if isinstance(n, Tensor):
+        (_fast_mod or _fast()).regression_compute(kind, states, n, 0.0, multioutput, bound, out)
+    else:
+        (_fast_mod or _fast()).regression_compute(kind, states, None, float(n), multioutput, bound, out)
+    return out
 
 
 # -------------------------------------------------------------------------------------------- curve scores

@@ -15,6 +15,8 @@
 // ≡ 32 mod 64 for b64 reads) so the 4 k-rows read by one wave land on disjoint banks.
 //
 // Numerics: products and sums are fp64 exactly as in the reference (inputs are exactly representable in fp64).
+#include <cstdlib>
+
 #include "../common/tm_common.h"
 
 namespace tm_amd {
@@ -244,10 +246,26 @@ void feature_moments_update(const at::Tensor& features, at::Tensor sum, at::Tens
   const int ntile = (d + kTile - 1) / kTile;
   const int tiles = ntile * (ntile + 1) / 2;
   const long long chunks = (n + kKC - 1) / kKC;
-  // ~2 blocks per CU, but keep >= 4 chunks of work per split
-  int splits = static_cast<int>((512 + tiles - 1) / tiles);
-  splits = static_cast<int>(std::max<long long>(1, std::min<long long>(splits, chunks / 4)));
-  splits = std::min(splits, 64);
+  // Split-K count: the kernel is MFMA-bound, so its time is the busiest CU's share of the work.  With `slots`
+  // co-resident blocks (2 per CU) a grid of tiles * s blocks runs in ceil(tiles * s / slots) rounds of 1/s of a tile
+  // each; pick the s (<= 64, >= 4 chunks per split) minimising that, e.g. D = 2048 (136 tiles) on 256 CUs: s = 15
+  // (2040 blocks ~ 8 full rounds) instead of s = 4 (544 blocks = 2 full rounds + a 32-block tail).
+  const int slots = 2 * cu_count(features.get_device());
+  const long long max_s = std::max<long long>(1, std::min<long long>(64, chunks / 4));
+  int splits = 1;
+  double best = 1e30;
+  for (int s_try = 1; s_try <= max_s; ++s_try) {
+    const double rounds = static_cast<double>((static_cast<long long>(tiles) * s_try + slots - 1) / slots);
+    const double cost = rounds / s_try * 1.0 + 1e-3 * s_try;  // small per-split cost: partial-tile write-back
+    if (cost < best) {
+      best = cost;
+      splits = s_try;
+    }
+  }
+  if (const char* env = std::getenv("TM_AMD_SYRK_SPLITS")) {
+    const int v = std::atoi(env);
+    if (v > 0) splits = static_cast<int>(std::min<long long>(v, std::max<long long>(1, chunks)));
+  }
   auto opts = features.options().dtype(at::kDouble);
   at::Tensor cov_part = at::empty({static_cast<long long>(splits) * tiles * kTile * kTile}, opts);
   at::Tensor sum_part = at::zeros({static_cast<long long>(splits) * d}, opts);

@@ -69,6 +69,76 @@ def test_syrk_kernel_vs_fp64_gemm(n, d, dtype):
     torch.testing.assert_close(c, c0 + xd.t() @ xd, rtol=1e-12, atol=1e-9)
 
 
+def _fid_states(m):
+    names = ("real_features_sum", "real_features_cov_sum", "real_features_num_samples", "fake_features_sum",
+             "fake_features_cov_sum", "fake_features_num_samples")
+    return {k: getattr(m, k).clone() for k in names}
+
+
+def _assert_states_close(a, b):
+    for k in a:
+        torch.testing.assert_close(a[k], b[k], rtol=1e-11, atol=1e-8, msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [None, 1000])
+def test_fid_staged_update_exact_state_semantics(cap):
+    """Staged (deferred) SYRK: every observer of the states sees the eager values."""
+    d = 96
+    g = torch.Generator().manual_seed(3)
+    batches = [(torch.randn(300, d, generator=g) * (1 + i % 3)).cuda() for i in range(9)]
+    eager = FrechetInceptionDistance(feature=_Id(d)).cuda()
+    eager._STAGE_MAX_ROWS = 0  # never stage
+    staged = FrechetInceptionDistance(feature=_Id(d)).cuda()
+    if cap is not None:
+        staged._STAGE_MAX_ROWS = cap  # forces flushes between updates
+    for i, b in enumerate(batches):
+        for m in (eager, staged):
+            m.update(b, real=i % 2 == 0)
+    assert "_fid_hidden" in staged.__dict__ and staged.__dict__["_fid_hidden"]
+    # attribute reads, state_dict and compute all see the eager values
+    _assert_states_close(_fid_states(staged), _fid_states(eager))
+    for m in (eager, staged):
+        m.update(batches[0] * 0.5, real=False)
+        m.persistent(True)
+    sd_e, sd_s = eager.state_dict(), staged.state_dict()
+    assert sd_e.keys() == sd_s.keys() and "real_features_cov_sum" in sd_e
+    for k in sd_e:
+        if k.endswith(("_sum", "_num_samples")):
+            torch.testing.assert_close(sd_s[k], sd_e[k], rtol=1e-11, atol=1e-8)
+    torch.testing.assert_close(staged.compute(), eager.compute(), rtol=1e-9, atol=1e-9)
+    # reset drops staged rows; load_state_dict replaces them
+    staged.update(batches[1], real=True)
+    staged.reset()
+    fresh = FrechetInceptionDistance(feature=_Id(d)).cuda()
+    _assert_states_close(_fid_states(staged), _fid_states(fresh))
+    staged.update(batches[2], real=True)
+    staged.load_state_dict(sd_e)
+    _assert_states_close(_fid_states(staged), {k: v for k, v in sd_e.items() if k in _fid_states(staged)})
+    # clone with staged rows is independent and exact
+    staged.update(batches[3], real=True)
+    twin = staged.clone()
+    eager.load_state_dict(sd_e)
+    eager.update(batches[3], real=True)
+    _assert_states_close(_fid_states(twin), _fid_states(eager))
+    _assert_states_close(_fid_states(staged), _fid_states(eager))
+
+
+@pytest.mark.gpu
+def test_fid_staged_keep_real_features():
+    d = 32
+    g = torch.Generator().manual_seed(5)
+    real, fake = torch.randn(200, d, generator=g).cuda(), torch.randn(200, d, generator=g).cuda()
+    m = FrechetInceptionDistance(feature=_Id(d), reset_real_features=False).cuda()
+    ref = FrechetInceptionDistance(feature=_Id(d)).cuda()
+    ref._STAGE_MAX_ROWS = 0
+    m.update(real, real=True)
+    m.update(fake, real=False)
+    m.reset()
+    ref.update(real, real=True)
+    _assert_states_close(_fid_states(m), _fid_states(ref))
+
+
 def test_kid_matches_loop_oracle():
     g = torch.Generator().manual_seed(1)
     real, fake = torch.randn(120, 8, generator=g), torch.randn(120, 8, generator=g) + 0.3

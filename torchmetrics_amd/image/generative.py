@@ -127,6 +127,88 @@ class FrechetInceptionDistance(_FeatureNetMetric):
         self.add_state("fake_features_cov_sum", torch.zeros(nf).double(), dist_reduce_fx="sum")
         self.add_state("fake_features_num_samples", torch.tensor(0).long(), dist_reduce_fx="sum")
 
+    # Staged accumulation.  The SYRK's fixed cost per call (split-K partial tiles + their reduction, ~60 us at D = 2048)
+    # dominates small batches: 1000 x 2048 runs at 32 fp64 TFLOP/s, 32k x 2048 at 55+.  On ROCm a batch is therefore
+    # copied into a per-distribution staging buffer (<= 256 MiB) and the SYRK runs once per full buffer.  While rows are
+    # staged, the two affected states are held out of ``__dict__``: ANY read of them (``getattr`` from compute, sync,
+    # state_dict, merge, device moves, user code) goes through ``__getattr__``, which runs the pending SYRK first, so
+    # every observer sees exactly the eager values; assigning the state (reset, load_state_dict) drops the staged rows
+    # that belonged to the replaced value.
+    _STAGE_BYTES = 256 << 20
+    _STAGE_MAX_ROWS = 1 << 16
+
+    def _staged_names(self, prefix: str) -> Tuple[str, str]:
+        return f"{prefix}_features_sum", f"{prefix}_features_cov_sum"
+
+    def __getattr__(self, name: str) -> Any:
+        d = self.__dict__
+        hidden = d.get("_fid_hidden")
+        if hidden and name in hidden:
+            self._flush_staged(name.split("_", 1)[0])
+            return d[name]
+        return super().__getattr__(name)
+
+    def __setattr__(self, name: str, value: Any) -> None:
+        hidden = self.__dict__.get("_fid_hidden")
+        if hidden and name in hidden:
+            prefix = name.split("_", 1)[0]
+            self._unhide(prefix)  # the staged rows belong to the value being replaced
+            self.__dict__["_fid_rows"][prefix] = 0
+        super().__setattr__(name, value)
+
+    def _unhide(self, prefix: str) -> None:
+        d = self.__dict__
+        for name in self._staged_names(prefix):
+            if name in d["_fid_hidden"]:
+                d[name] = d["_fid_hidden"].pop(name)
+
+    def _flush_staged(self, prefix: str) -> None:
+        d = self.__dict__
+        rows = d.get("_fid_rows", {}).get(prefix, 0)
+        self._unhide(prefix)
+        if rows:
+            d["_fid_rows"][prefix] = 0
+            s_name, c_name = self._staged_names(prefix)
+            ops.feature_moments_update(d["_fid_stage"][prefix][:rows], d[s_name], d[c_name])
+
+    def _stage(self, prefix: str, features: Tensor) -> bool:
+        """Copy ``features`` into the staging buffer (flushing it when full); False: not stageable."""
+        d = self.__dict__
+        n, dim = features.shape
+        cap = min(self._STAGE_MAX_ROWS, self._STAGE_BYTES // max(1, dim * features.element_size()))
+        if not features.is_cuda or n >= cap or not features.is_floating_point():
+            return False
+        s_name, c_name = self._staged_names(prefix)
+        s, c = getattr(self, s_name), getattr(self, c_name)  # flushes anything staged
+        if s.device != features.device or not s.is_contiguous() or not c.is_contiguous() or s.numel() != dim:
+            return False
+        stage = d.setdefault("_fid_stage", {})
+        rows = d.setdefault("_fid_rows", {})
+        buf = stage.get(prefix)
+        if buf is None or buf.shape != (cap, dim) or buf.dtype != features.dtype or buf.device != features.device:
+            buf = stage[prefix] = torch.empty(cap, dim, dtype=features.dtype, device=features.device)
+        buf[:n].copy_(features)
+        rows[prefix] = n
+        hidden = d.setdefault("_fid_hidden", {})
+        for name in (s_name, c_name):
+            hidden[name] = d.pop(name)
+        return True
+
+    def _append_staged(self, prefix: str, features: Tensor) -> bool:
+        d = self.__dict__
+        rows = d.get("_fid_rows", {}).get(prefix, 0)
+        if not rows:
+            return False
+        buf = d["_fid_stage"][prefix]
+        n = features.shape[0]
+        if features.dtype != buf.dtype or features.device != buf.device or features.shape[1] != buf.shape[1]:
+            return False
+        if rows + n > buf.shape[0]:
+            return False
+        buf[rows:rows + n].copy_(features)
+        d["_fid_rows"][prefix] = rows + n
+        return True
+
     def update(self, imgs: Tensor, real: bool) -> None:
         feats = self._features(imgs)
         self.update_features(feats, real, num_samples=imgs.shape[0])
@@ -136,13 +218,15 @@ class FrechetInceptionDistance(_FeatureNetMetric):
         if features.dim() == 1:
             features = features.unsqueeze(0)
         prefix = "real" if real else "fake"
-        s = getattr(self, f"{prefix}_features_sum")
-        c = getattr(self, f"{prefix}_features_cov_sum")
-        if s.device != features.device or not s.is_contiguous() or not c.is_contiguous():
-            s, c = s.to(features.device).contiguous(), c.to(features.device).contiguous()
-            setattr(self, f"{prefix}_features_sum", s)
-            setattr(self, f"{prefix}_features_cov_sum", c)
-        ops.feature_moments_update(features, s, c)
+        features = features.detach()
+        if not (self._append_staged(prefix, features) or self._stage(prefix, features)):
+            s = getattr(self, f"{prefix}_features_sum")  # (runs any staged rows first)
+            c = getattr(self, f"{prefix}_features_cov_sum")
+            if s.device != features.device or not s.is_contiguous() or not c.is_contiguous():
+                s, c = s.to(features.device).contiguous(), c.to(features.device).contiguous()
+                setattr(self, f"{prefix}_features_sum", s)
+                setattr(self, f"{prefix}_features_cov_sum", c)
+            ops.feature_moments_update(features, s, c)
         n = getattr(self, f"{prefix}_features_num_samples")
         setattr(self, f"{prefix}_features_num_samples", n + (features.shape[0] if num_samples is None else num_samples))
 

@@ -378,3 +378,60 @@ def test_nms_gpu_matches_cpu(n, batched):
             if batched:
                 iou = iou * (idxs[head][:, None] == idxs[head][None, :]).cuda()
             assert float(iou.max()) <= thr
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+@pytest.mark.parametrize("precomputed", [False, True])
+def test_coco_match_native_host_matches_python_oracle(seed, precomputed):
+    """Native CPU matcher (csrc/detection/coco_match_host.cpp) == the plain-loop oracle, bitwise."""
+    from torchmetrics_amd.ops import _cpu
+
+    if not ops.load_native(strict=False):
+        pytest.skip("native library not built")
+    g = torch.Generator().manual_seed(seed)
+    groups, dets, gts = 40, [], []
+    det_start, det_cnt, gt_start, gt_cnt = [], [], [], []
+    nd = ng = 0
+    for _ in range(groups):
+        dn, gn = int(torch.randint(0, 12, (1,), generator=g)), int(torch.randint(0, 8, (1,), generator=g))
+        det_start.append(nd), det_cnt.append(dn), gt_start.append(ng), gt_cnt.append(gn)
+        nd, ng = nd + dn, ng + gn
+    xy = torch.rand(ng, 2, generator=g, dtype=torch.float64) * 100
+    wh = torch.rand(ng, 2, generator=g, dtype=torch.float64) * 60 + 1
+    gbox = torch.cat([xy, wh], 1)
+    src = torch.randint(0, max(ng, 1), (nd,), generator=g)
+    dbox = (gbox[src] if ng else torch.rand(nd, 4, dtype=torch.float64) * 50) + torch.randn(nd, 4, generator=g,
+                                                                                            dtype=torch.float64) * 4
+    dbox[:, 2:] = dbox[:, 2:].abs() + 1
+    darea, garea = dbox[:, 2] * dbox[:, 3], gbox[:, 2] * gbox[:, 3]
+    gcrowd = (torch.rand(ng, generator=g) < 0.2).to(torch.uint8)
+    i32 = lambda v: torch.tensor(v, dtype=torch.int32)  # noqa: E731
+    area_rng = torch.tensor([0, 1e10, 0, 1024, 1024, 3000, 3000, 1e10], dtype=torch.float64)
+    thr = torch.linspace(0.5, 0.95, 10, dtype=torch.float64)
+    pre = off = None
+    if precomputed:
+        blocks, offs, o = [], [], 0
+        for d0, dn, g0, gn in zip(det_start, det_cnt, gt_start, gt_cnt):
+            blocks.append(torch.rand(dn * gn, generator=g, dtype=torch.float64))
+            offs.append(o)
+            o += dn * gn
+        pre, off = torch.cat(blocks), torch.tensor(offs, dtype=torch.int64)
+    args = (dbox, darea, gbox, garea, gcrowd, i32(det_start), i32(det_cnt), i32(gt_start), i32(gt_cnt), area_rng, thr)
+    native = torch.ops.tm_amd.coco_match(*args, pre, off)
+    oracle = _cpu.coco_match(*args, pre, off)
+    assert torch.equal(native[0], oracle[0]) and torch.equal(native[1], oracle[1])
+    assert int(native[0].sum()) > 0
+
+
+def test_coco_iou_matrix_matches_scalar_formula():
+    from torchmetrics_amd.detection.mean_ap import _coco_iou_matrix
+    from torchmetrics_amd.ops._cpu import _coco_iou
+
+    g = torch.Generator().manual_seed(0)
+    d = torch.cat([torch.rand(9, 2, generator=g) * 50, torch.rand(9, 2, generator=g) * 30 + 0.5], 1).double()
+    t = torch.cat([torch.rand(7, 2, generator=g) * 50, torch.rand(7, 2, generator=g) * 30 + 0.5], 1).double()
+    crowd = torch.rand(7, generator=g) < 0.3
+    got = _coco_iou_matrix(d, t, crowd)
+    exp = torch.tensor([[_coco_iou(a, b, bool(c)) for b, c in zip(t.tolist(), crowd.tolist())] for a in d.tolist()],
+                       dtype=torch.float64)
+    torch.testing.assert_close(got, exp, rtol=1e-12, atol=1e-12)

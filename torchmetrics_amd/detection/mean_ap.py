@@ -241,10 +241,7 @@ class MeanAveragePrecision(Metric):
                     d = self.detection_box[img].reshape(-1, 4)[dl][order]
                     g = self.groundtruth_box[img].reshape(-1, 4)[gl]
                     crowd = self.groundtruth_crowds[img][gl].bool()
-                    from torchmetrics_amd.ops._cpu import _coco_iou
-
-                    mat = torch.tensor([[_coco_iou(a, b, bool(c)) for b, c in zip(g.tolist(), crowd.tolist())]
-                                        for a in d.tolist()], dtype=torch.float32).reshape(len(d), len(g))
+                    mat = _coco_iou_matrix(d.double(), g.double(), crowd).float().cpu()
                 else:
                     dm = self.detection_mask[img][dl][order].flatten(1).float()
                     gm = self.groundtruth_mask[img][gl].flatten(1).float()
@@ -328,6 +325,20 @@ class MeanAveragePrecision(Metric):
                        "iscrowd": torch.tensor(t["iscrowd"], dtype=torch.int32),
                        "area": torch.tensor(t["area"], dtype=torch.float32)})
         return bp, bt
+
+
+def _coco_iou_matrix(d: Tensor, g: Tensor, crowd: Tensor) -> Tensor:
+    """COCO (pycocotools ``maskUtils.iou``) box IoU of xywh boxes ``[n, 4] x [m, 4]``; crowd columns divide by the
+    detection area."""
+    x1 = torch.maximum(d[:, None, 0], g[None, :, 0])
+    y1 = torch.maximum(d[:, None, 1], g[None, :, 1])
+    x2 = torch.minimum(d[:, None, 0] + d[:, None, 2], g[None, :, 0] + g[None, :, 2])
+    y2 = torch.minimum(d[:, None, 1] + d[:, None, 3], g[None, :, 1] + g[None, :, 3])
+    w, h = x2 - x1, y2 - y1
+    inter = torch.where((w > 0) & (h > 0), w * h, torch.zeros_like(w))
+    da = (d[:, 2] * d[:, 3])[:, None]
+    union = torch.where(crowd[None, :], da, da + (g[:, 2] * g[:, 3])[None, :] - inter)
+    return torch.where(inter > 0, inter / union, torch.zeros_like(inter))
 
 
 def _warning_on_too_many_detections(limit: int) -> None:

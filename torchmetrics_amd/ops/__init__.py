@@ -563,7 +563,8 @@ def coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, g
     ``iou_pre`` / ``iou_off`` optionally give precomputed per-group IoU blocks (``[det_cnt, gt_cnt]`` row-major at
     ``iou_off[group]``), e.g. mask IoUs for ``iou_type="segm"``; otherwise COCO box IoU is computed from ``dbox``.
     """
-    if dbox.is_cuda:
+    if dbox.is_cuda or load_native(strict=False):
+        # ROCm: one thread per (group, area, threshold); CPU: native host matcher (csrc/detection/coco_match_host.cpp)
         return _ops().coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, gt_cnt, area_rng,
                                  iou_thr, iou_pre, iou_off)
     return _cpu.coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, gt_cnt, area_rng, iou_thr,

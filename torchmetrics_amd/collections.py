@@ -202,8 +202,8 @@ class MetricCollection(ModuleDict):
         """Read every member's deferred-validation flag word with ONE device sync (a stack + one ``.item()``) instead
         of one per member; clean members then skip their own read in ``compute()`` (any raised flag is left for its
         metric to raise with its own message)."""
-        pending = [m for m in self._modules.values()
-                   if m.__dict__["_device_errors"] is not None and m.__dict__["_computed"] is None]
+        # (members with a cached result never read their flag; the mark is cleared after compute either way)
+        pending = [m for m in self._modules.values() if m.__dict__["_device_errors"] is not None]
         if len(pending) < 2:
             return
         bufs = [m.__dict__["_device_errors"] for m in pending]

@@ -571,6 +571,21 @@ def coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, g
                            iou_pre, iou_off)
 
 
+# ------------------------------------------------------------------------------------------ distance transforms
+_DT_METRICS = {"euclidean": 0, "taxicab": 1, "chessboard": 2}
+
+
+def line_distance_transform(cost: Tensor, spacing: float, metric: str) -> Optional[Tensor]:
+    """Exact 1-D transform along the last dim: ``out[..., j] = min_k combine(|j - k| * spacing, cost[..., k])``
+    (squared-euclidean lower envelope / taxicab scans / chessboard min-max; ``csrc/segmentation/
+    distance_transform.hip``, ROCm kernel or native host loop).  None when the native library is unavailable."""
+    if cost.dtype not in (torch.float32, torch.float64) or not (cost.is_cuda or native_available()):
+        return None
+    n = cost.shape[-1]
+    out = _ops().line_distance_transform(cost.reshape(-1, n).contiguous(), float(spacing), _DT_METRICS[metric])
+    return out.reshape(cost.shape)
+
+
 # -------------------------------------------------------------------------------------------------------- pairwise
 # metric ids of csrc/pairwise/pairwise.hip
 PW_L1, PW_L2, PW_LP, PW_LP_INT = range(4)

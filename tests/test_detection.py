@@ -435,3 +435,16 @@ def test_coco_iou_matrix_matches_scalar_formula():
     exp = torch.tensor([[_coco_iou(a, b, bool(c)) for b, c in zip(t.tolist(), crowd.tolist())] for a in d.tolist()],
                        dtype=torch.float64)
     torch.testing.assert_close(got, exp, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("batched", [False, True])
+def test_nms_native_host_matches_matrix_fallback(batched):
+    from torchmetrics_amd.ops import _cpu
+
+    if not ops.native_available():
+        pytest.skip("native library not built")
+    g = torch.Generator().manual_seed(9)
+    boxes = _rand_boxes(700, g, 40.0)
+    scores = torch.rand(700, generator=g)
+    idxs = torch.randint(0, 4, (700,), generator=g) if batched else None
+    assert torch.equal(ops.nms(boxes, scores, 0.45, idxs), _cpu.nms(boxes, scores, 0.45, idxs))

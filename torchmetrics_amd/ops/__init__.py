@@ -547,8 +547,9 @@ def box_pairwise(a: Tensor, b: Tensor, op: int = BOX_IOU, aligned: bool = False)
 def nms(boxes: Tensor, scores: Tensor, iou_threshold: float, idxs: Optional[Tensor] = None) -> Tensor:
     """Greedy NMS: indices of the kept ``[N, 4]`` xyxy boxes in descending score order (equal scores: lower index
     first).  With ``idxs`` only boxes of the same class suppress each other.  ROCm: bitmask-tile kernel + one-wave
-    scan (``csrc/detection/nms.hip``); CPU: the same greedy rule over the IoU matrix."""
-    if boxes.is_cuda:
+    scan (``csrc/detection/nms.hip``); CPU: the same greedy rule in a native host loop (Python fallback: over the IoU
+    matrix)."""
+    if boxes.is_cuda or native_available():  # CPU: native host greedy loop (csrc/detection/nms_host.cpp)
         empty = boxes.new_empty(0, dtype=torch.long)
         return _ops().nms(boxes.contiguous(), scores.contiguous(), empty if idxs is None else idxs.contiguous(),
                           float(iou_threshold))

@@ -56,7 +56,8 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--sync-every-step", action="store_true")
     ap.add_argument("--graph", action="store_true",
-                    help="replay the tensor-state members' updates from HIP graphs (utils.graphs.GraphedUpdate); the "
+                    help="replay the tensor-state members' updates from HIP graphs (utils.graphs.GraphedUpdate, one graph "
+                    "bound to each buffer of the input ring); the "
                          "list-state member (calibration error) stays eager")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -79,14 +80,19 @@ def main() -> None:
 
         ece = cls["ece"]
         cls_graph = MetricCollection({k: m for k, m in cls.items(keep_base=True) if k != "ece"}, compute_groups=True)
-        g_cls = GraphedUpdate(cls_graph, logits[0], labels[0])
-        g_reg = GraphedUpdate(reg, xs[0], ys[0])
+        # one graph per input buffer of the ring, bound to that buffer: replays read the batch in place (no copy)
+        g_cls = [GraphedUpdate(cls_graph, logits[i], labels[i], bind_inputs=True) for i in range(NBUF)]
+        g_reg = [GraphedUpdate(reg, xs[i], ys[i], bind_inputs=True) for i in range(NBUF)]
+        slot = {id(t): i for i, t in enumerate(logits)}
 
         def upd_cls(p, t):  # noqa: F811
-            g_cls(p, t)
+            g_cls[slot[id(p)]]()
             ece.update(p, t)
 
-        upd_reg = g_reg
+        def upd_reg(p, t):  # noqa: F811
+            g_reg[slot_reg[id(p)]]()
+
+        slot_reg = {id(t): i for i, t in enumerate(xs)}
 
     def step(i):
         upd_cls(logits[i % NBUF], labels[i % NBUF])
@@ -106,7 +112,8 @@ def main() -> None:
     cls.compute(), reg.compute()
     if args.graph:  # reset() re-creates the state tensors: reset through the graphed collection, then re-capture
         cls_graph.reset(), ece.reset(), reg.reset()
-        g_cls.recapture(), g_reg.recapture()
+        for gr in g_cls + g_reg:
+            gr.recapture()
     else:
         cls.reset(), reg.reset()
     sync()

@@ -453,3 +453,43 @@ def test_fused_pearson_concordance_matches_cpu(case, dtype):
         torch.testing.assert_close(got.cpu(), ref, rtol=1e-4, atol=1e-5, equal_nan=True)
         low = lambda ws: any("variance of predictions or target" in str(w.message) for w in ws)  # noqa: E731
         assert low(wg) == low(wc)
+
+
+def test_graphed_update_bound_input_ring():
+    """bind_inputs=True: one graph per buffer of an input ring reads the buffers in place; refilled buffers give the
+    same states as eager updates on the same batches."""
+    import torchmetrics_amd as tm
+    from torchmetrics_amd import classification as C
+    from torchmetrics_amd import regression as R
+    from torchmetrics_amd.utils.graphs import GraphedUpdate
+
+    def coll():
+        return tm.MetricCollection({"acc": C.MulticlassAccuracy(7), "cm": C.MulticlassConfusionMatrix(7),
+                                    "auroc": C.MulticlassAUROC(7, thresholds=20)}, compute_groups=True).to(DEV)
+
+    g = torch.Generator().manual_seed(1)
+    ring = [(torch.empty(300, 7, device=DEV), torch.empty(300, dtype=torch.long, device=DEV)) for _ in range(3)]
+    for p, t in ring:
+        p.copy_(torch.randn(300, 7, generator=g))
+        t.copy_(torch.randint(0, 7, (300,), generator=g))
+    eager, graphed = coll(), coll()
+    reg_e, reg_g = R.MeanSquaredError().to(DEV), R.MeanSquaredError().to(DEV)
+    graphs = [GraphedUpdate(graphed, p, t, bind_inputs=True) for p, t in ring]
+    rgraphs = [GraphedUpdate(reg_g, p[:, 0].contiguous(), p[:, 1].contiguous(), bind_inputs=True) for p, _ in ring]
+    for step in range(7):
+        i = step % 3
+        p, t = ring[i]
+        p.copy_(torch.randn(300, 7, generator=g))  # the producer refills the slot in place
+        t.copy_(torch.randint(0, 7, (300,), generator=g))
+        eager.update(p, t)
+        graphs[i]()  # no arguments: read the bound buffers
+        x, y = rgraphs[i]._static
+        x.copy_(p[:, 0])
+        y.copy_(p[:, 1])
+        reg_e.update(x, y)
+        rgraphs[i](x, y)  # the bound tensors themselves: no copy
+    a, b = graphed.compute(), eager.compute()
+    for k in b:
+        torch.testing.assert_close(a[k], b[k])
+    torch.testing.assert_close(reg_g.compute(), reg_e.compute())
+    assert graphed["acc"].update_count == eager["acc"].update_count == 7

@@ -12,6 +12,12 @@ Constraints (checked at capture):
 * the update must not rebind a state to a new tensor object, nor synchronise with the host;
 * inputs keep the example's shapes / dtypes (a new shape needs a new capture).
 
+By default the example inputs are cloned into private static buffers and every call copies the new batch in (one
+device copy per input).  With ``bind_inputs=True`` the graph reads the example tensors themselves: a producer that
+writes each batch into those tensors (a model writing ``out=``, a pinned-memory ring filled by the data loader) calls
+the graph with them -- or with no arguments -- and no copy is made.  A ring of N input buffers is served by N
+``GraphedUpdate(..., bind_inputs=True)`` objects over the same target, one per buffer.
+
 The metric's Python bookkeeping (``update_count``, the ``compute`` cache) is advanced on every replay, so
 ``compute()``, ``reset()``, sync and ``state_dict`` behave exactly as after eager updates.  ``reset()`` re-creates the
 state tensors, so a graph must be re-captured after a reset (``GraphedUpdate.recapture``).
@@ -38,7 +44,8 @@ def _states(metrics: List[Tuple[str, Metric]]) -> Dict[Tuple[str, str], Any]:
 class GraphedUpdate:
     """``GraphedUpdate(metric_or_collection, *example_inputs)``; then call it with each batch instead of ``update``."""
 
-    def __init__(self, target: Union[Metric, MetricCollection], *example_inputs: Tensor, warmup: int = 2) -> None:
+    def __init__(self, target: Union[Metric, MetricCollection], *example_inputs: Tensor, warmup: int = 2,
+                 bind_inputs: bool = False) -> None:
         if not example_inputs or not all(isinstance(a, Tensor) and a.is_cuda for a in example_inputs):
             raise ValueError("GraphedUpdate needs the example inputs as ROCm tensors")
         self.target = target
@@ -47,7 +54,8 @@ class GraphedUpdate:
             for attr in m._defaults:
                 if not isinstance(getattr(m, attr), Tensor):
                     raise ValueError(f"metric `{name}` has the list state `{attr}`: it cannot be replayed from a graph")
-        self._static = [a.detach().clone() for a in example_inputs]
+        self._static = [a.detach() if bind_inputs else a.detach().clone() for a in example_inputs]
+        self._bound = bind_inputs
         self._warmup = warmup
         self._capture()
 
@@ -86,9 +94,14 @@ class GraphedUpdate:
         self._capture()
 
     def __call__(self, *inputs: Tensor) -> None:
+        if not inputs and self._bound:
+            inputs = tuple(self._static)  # the producer already wrote the bound buffers
         if len(inputs) != len(self._static):
             raise ValueError(f"expected {len(self._static)} inputs, got {len(inputs)}")
         for s, x in zip(self._static, inputs):
+            if x is s or (x.data_ptr() == s.data_ptr() and x.shape == s.shape and x.stride() == s.stride()
+                          and x.dtype == s.dtype):
+                continue  # the captured buffer itself: nothing to copy
             if x.shape != s.shape or x.dtype != s.dtype:
                 raise ValueError(f"input of shape {tuple(x.shape)} / {x.dtype} does not match the captured "
                                  f"{tuple(s.shape)} / {s.dtype}; capture a new GraphedUpdate for it")

@@ -347,3 +347,32 @@ def test_collection_repeated_compute_keeps_member_results():
     for k in first:
         assert torch.equal(first[k], second[k]), k
     assert not torch.equal(second["MulticlassAccuracy"], second["MulticlassSpecificity"])
+
+
+def test_device_error_read_skipped_without_new_updates(monkeypatch):
+    """compute() re-reads the deferred-validation word only after new updates (or a reset)."""
+    from torchmetrics_amd.classification import MulticlassConfusionMatrix
+    from torchmetrics_amd.utils import validation
+
+    monkeypatch.setattr(validation, "STRICT", False)
+    m = MulticlassConfusionMatrix(num_classes=3)
+    reads = []
+    orig = m._raise_device_errors
+    m._raise_device_errors = lambda: (reads.append(1), orig())[1]
+    m._device_error_buffer(torch.device("cpu"))  # make sure a flag word exists
+
+    def reads_in_compute():
+        before = len(reads)
+        m._computed = None
+        m.compute()
+        return len(reads) - before
+
+    m.update(torch.tensor([0, 1, 2]), torch.tensor([0, 1, 1]))
+    assert reads_in_compute() == 1
+    assert reads_in_compute() == 0  # nothing new since the clean read
+    m.update(torch.tensor([0]), torch.tensor([0]))
+    assert reads_in_compute() == 1
+    m.reset()
+    m._device_error_buffer(torch.device("cpu"))
+    m.update(torch.tensor([0]), torch.tensor([0]))
+    assert reads_in_compute() == 1

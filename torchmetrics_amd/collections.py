@@ -203,7 +203,8 @@ class MetricCollection(ModuleDict):
         of one per member; clean members then skip their own read in ``compute()`` (any raised flag is left for its
         metric to raise with its own message)."""
         # (members with a cached result never read their flag; the mark is cleared after compute either way)
-        pending = [m for m in self._modules.values() if m.__dict__["_device_errors"] is not None]
+        pending = [m for m in self._modules.values() if m.__dict__["_device_errors"] is not None
+                   and m.__dict__.get("_errors_checked_at") != m.__dict__["_update_count"]]
         if len(pending) < 2:
             return
         bufs = [m.__dict__["_device_errors"] for m in pending]
@@ -211,7 +212,9 @@ class MetricCollection(ModuleDict):
             return
         if not bool(torch.cat(bufs).any()):
             for m in pending:
-                m.__dict__["_device_errors_clean"] = True
+                d = m.__dict__
+                d["_device_errors_clean"] = True
+                d["_errors_checked_at"] = d["_update_count"]
 
     def _compute_and_reduce(self, method_name: str, *args: Any, **kwargs: Any) -> Dict[str, Any]:
         result = {}

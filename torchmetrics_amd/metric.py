@@ -440,7 +440,11 @@ class Metric(Module, ABC):
             if state["_computed"] is not None:
                 return state["_computed"]
             if state["_device_errors"] is not None and not state.pop("_device_errors_clean", False):
-                self._raise_device_errors()
+                # the flag word only changes through update() / graph replays, which all bump _update_count: a word
+                # read clean at this count is still clean (saves the device sync on repeated compute() calls)
+                if state.get("_errors_checked_at") != state["_update_count"]:
+                    self._raise_device_errors()
+                    state["_errors_checked_at"] = state["_update_count"]
             self._consolidate_cat_lists()
             avail = state["distributed_available_fn"]
             if not state["_is_synced"] and not (state["_to_sync"] and callable(avail) and avail()):
@@ -503,6 +507,7 @@ class Metric(Module, ABC):
 
     def reset(self) -> None:
         """Reset all states to their defaults."""
+        self.__dict__.pop("_errors_checked_at", None)
         self._update_count = 0
         self._forward_cache = None
         self._computed = None

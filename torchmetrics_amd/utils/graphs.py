@@ -88,6 +88,7 @@ class GraphedUpdate:
         for name, m in members:
             m.__dict__["_update_count"] = counts[name]
             m.__dict__["_computed"] = None
+            m.__dict__.pop("_errors_checked_at", None)  # warm-up launches may have raised validation bits
 
     def recapture(self) -> None:
         """Capture again (after ``reset()`` re-created the state tensors, or after moving the metric)."""

@@ -215,13 +215,68 @@ void calibration_bins(const at::Tensor& conf, const at::Tensor& acc, const at::T
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
+// Calibration error from the [nb, 3] (count, Σconf, Σacc) bins in one block: per bin acc / conf means (0 for empty
+// bins, the reference's nan_to_num), proportion = count / Σcount, then l1 = Σ |acc - conf| * prop or
+// max = max |acc - conf| (reference F/classification/calibration_error.py `_ce_compute`, ~10 ATen launches).
+namespace {
+__global__ void __launch_bounds__(kThreads) calib_reduce_kernel(const float* __restrict__ sums, int nb, int norm,
+                                                                float* __restrict__ out) {
+  __shared__ float red[kThreads / kWave];
+  float tot = 0.f;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) tot += sums[3 * b];
+  tot = wave_sum(tot);
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  if (lane == 0) red[wave] = tot;
+  __syncthreads();
+  tot = 0.f;
+  for (int w = 0; w < kThreads / kWave; ++w) tot += red[w];
+  __syncthreads();
+  float v = 0.f;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    const float cnt = sums[3 * b];
+    float conf = sums[3 * b + 1] / cnt, acc = sums[3 * b + 2] / cnt;
+    conf = conf != conf ? 0.f : conf;
+    acc = acc != acc ? 0.f : acc;
+    const float gap = fabsf(acc - conf);
+    v = norm == 0 ? v + gap * (cnt / tot) : fmaxf(v, gap);
+  }
+  if (norm == 0) {
+    v = wave_sum(v);
+  } else {
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+  }
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = red[0];
+    for (int w = 1; w < kThreads / kWave; ++w) r = norm == 0 ? r + red[w] : fmaxf(r, red[w]);
+    out[0] = r;
+  }
+}
+}  // namespace
+
+// sums: f32 [nb, 3] from calibration_bins; norm 0 = l1, 1 = max; out: f32 [1]
+void calibration_reduce(const at::Tensor& sums, int64_t norm, at::Tensor out) {
+  TM_CHECK_CUDA(sums);
+  TORCH_CHECK(sums.scalar_type() == at::kFloat && sums.is_contiguous() && sums.dim() == 2 && sums.size(1) == 3,
+              "calibration_reduce: sums must be contiguous f32 [nb, 3]");
+  TORCH_CHECK(norm == 0 || norm == 1, "calibration_reduce: norm 0 (l1) or 1 (max)");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 1, "calibration_reduce: out f32 [1]");
+  hipLaunchKernelGGL(calib_reduce_kernel, dim3(1), dim3(kThreads), 0, stream(), sums.data_ptr<float>(),
+                     static_cast<int>(sums.size(0)), static_cast<int>(norm), out.data_ptr<float>());
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
 }  // namespace tm_amd
 
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def("calibration_reduce(Tensor sums, int norm, Tensor(a!) out) -> ()");
   m.def("confmat_reduce(Tensor confmat, int kind, int average, int ignore, int kw, Tensor(a!) out) -> ()");
   m.def("calibration_bins(Tensor conf, Tensor acc, Tensor bounds, Tensor(a!) sums, Tensor(b!) bad) -> ()");
 }
 TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
   m.impl("confmat_reduce", &tm_amd::confmat_reduce);
   m.impl("calibration_bins", &tm_amd::calibration_bins);
+  m.impl("calibration_reduce", &tm_amd::calibration_reduce);
 }

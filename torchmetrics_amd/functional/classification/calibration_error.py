@@ -46,6 +46,10 @@ def _ce_compute(
         bin_boundaries = torch.linspace(0, 1, bin_boundaries + 1, dtype=confidences.dtype, device=confidences.device)
     if norm not in {"l1", "l2", "max"}:
         raise ValueError(f"Argument `norm` is expected to be one of 'l1', 'l2', 'max' but got {norm}")
+    if (norm != "l2" and confidences.is_cuda and confidences.dtype == torch.float32
+            and len(bin_boundaries) <= 4096):
+        with torch.no_grad():
+            return ops.calibration_error_l1_max(confidences, accuracies.float(), bin_boundaries, norm)
     with torch.no_grad():
         acc_bin, conf_bin, prop_bin = _binning_bucketize(confidences, accuracies, bin_boundaries)
     if norm == "l1":

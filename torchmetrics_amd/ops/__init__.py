@@ -468,6 +468,14 @@ def regression_compute(kind: int, states: Sequence[Tensor], n: Union[Tensor, int
     return out
 
 
+def calibration_error_l1_max(conf: Tensor, acc: Tensor, bounds: Tensor, norm: str) -> Tensor:
+    """``l1`` / ``max`` calibration error of ROCm f32 confidences in two launches (bins + one-block reduce)."""
+    sums = calibration_bins(conf, acc, bounds)
+    out = torch.empty(1, dtype=torch.float32, device=conf.device)
+    (_fast_mod or _fast()).calibration_reduce(sums, 0 if norm == "l1" else 1, out)
+    return out[0]
+
+
 # -------------------------------------------------------------------------------------------- curve scores
 SCORE_AUROC, SCORE_AP = 0, 1
 _AVG_IDS = {None: 0, "none": 0, "macro": 1, "weighted": 2}

@@ -508,3 +508,23 @@ def test_calibration_error_compute_matches_cpu(norm, n_bins):
     got = _ce_compute(conf.to(DEV), acc.to(DEV), n_bins, norm)
     assert got.shape == ref.shape
     torch.testing.assert_close(got.cpu().float(), ref.float(), rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("C", [3, 10, 32, 33])
+@pytest.mark.parametrize("kind", ["logits", "probs"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_multiclass_binned_curve_state_matches_cpu(C, kind, dtype):
+    """Small-C multiclass binning (fused two-plane kernel for C <= 32) == the CPU state, incl. ignore_index."""
+    from torchmetrics_amd.classification import MulticlassPrecisionRecallCurve
+
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(3000, C, generator=g)
+    preds = (x.softmax(-1) if kind == "probs" else x * 3).to(dtype)
+    target = torch.randint(0, C, (3000,), generator=g)
+    target[::17] = -1
+    cpu = MulticlassPrecisionRecallCurve(C, thresholds=37, ignore_index=-1)
+    gpu = MulticlassPrecisionRecallCurve(C, thresholds=37, ignore_index=-1).to(DEV)
+    for lo in range(0, 3000, 1000):
+        cpu.update(preds[lo:lo + 1000], target[lo:lo + 1000])
+        gpu.update(preds[lo:lo + 1000].to(DEV), target[lo:lo + 1000].to(DEV))
+    assert torch.equal(gpu.confmat.cpu(), cpu.confmat)

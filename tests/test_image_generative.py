@@ -80,16 +80,17 @@ def _assert_states_close(a, b):
         torch.testing.assert_close(a[k], b[k], rtol=1e-11, atol=1e-8, msg=k)
 
 
-@pytest.mark.gpu
+@pytest.mark.parametrize("device", DEVICES)
 @pytest.mark.parametrize("cap", [None, 1000])
-def test_fid_staged_update_exact_state_semantics(cap):
+def test_fid_staged_update_exact_state_semantics(device, cap):
     """Staged (deferred) SYRK: every observer of the states sees the eager values."""
     d = 96
     g = torch.Generator().manual_seed(3)
-    batches = [(torch.randn(300, d, generator=g) * (1 + i % 3)).cuda() for i in range(9)]
-    eager = FrechetInceptionDistance(feature=_Id(d)).cuda()
+    batches = [(torch.randn(300, d, generator=g, dtype=torch.float64) * (1 + i % 3)).to(device) for i in range(9)]
+    eager = FrechetInceptionDistance(feature=_Id(d)).to(device)
     eager._STAGE_MAX_ROWS = 0  # never stage
-    staged = FrechetInceptionDistance(feature=_Id(d)).cuda()
+    staged = FrechetInceptionDistance(feature=_Id(d)).to(device)
+    staged._STAGE_ON_CPU = True
     if cap is not None:
         staged._STAGE_MAX_ROWS = cap  # forces flushes between updates
     for i, b in enumerate(batches):
@@ -110,7 +111,7 @@ def test_fid_staged_update_exact_state_semantics(cap):
     # reset drops staged rows; load_state_dict replaces them
     staged.update(batches[1], real=True)
     staged.reset()
-    fresh = FrechetInceptionDistance(feature=_Id(d)).cuda()
+    fresh = FrechetInceptionDistance(feature=_Id(d)).to(device)
     _assert_states_close(_fid_states(staged), _fid_states(fresh))
     staged.update(batches[2], real=True)
     staged.load_state_dict(sd_e)

@@ -136,6 +136,7 @@ class FrechetInceptionDistance(_FeatureNetMetric):
     # that belonged to the replaced value.
     _STAGE_BYTES = 256 << 20
     _STAGE_MAX_ROWS = 1 << 16
+    _STAGE_ON_CPU = False  # staging is a ROCm optimisation; tests switch it on to cover the state semantics on CPU
 
     def _staged_names(self, prefix: str) -> Tuple[str, str]:
         return f"{prefix}_features_sum", f"{prefix}_features_cov_sum"
@@ -176,7 +177,7 @@ class FrechetInceptionDistance(_FeatureNetMetric):
         d = self.__dict__
         n, dim = features.shape
         cap = min(self._STAGE_MAX_ROWS, self._STAGE_BYTES // max(1, dim * features.element_size()))
-        if not features.is_cuda or n >= cap or not features.is_floating_point():
+        if not (features.is_cuda or self._STAGE_ON_CPU) or n >= cap or not features.is_floating_point():
             return False
         s_name, c_name = self._staged_names(prefix)
         s, c = getattr(self, s_name), getattr(self, c_name)  # flushes anything staged

@@ -835,7 +835,9 @@ __global__ void zero_int_kernel(int* p) { *p = 0; }
 void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out, at::Tensor flag, int64_t num_classes,
                int64_t ignore_index, bool has_ignore, int64_t mode, bool samplewise) {
   TM_CHECK_CUDA(preds);
-  TM_CHECK_CUDA(target);
+  TM_SAME_DEVICE(preds, target);
+  TM_SAME_DEVICE(preds, out);
+  TM_SAME_DEVICE(preds, flag);
   TM_CHECK_CONTIG(preds);
   TM_CHECK_CONTIG(target);
   TM_CHECK_CONTIG(out);
@@ -965,9 +967,11 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
 
 void mc_stats_finalize(at::Tensor ws, int64_t num_classes, bool micro, bool accumulate, at::Tensor tp, at::Tensor fp,
                        at::Tensor tn, at::Tensor fn) {
+  TM_CHECK_CUDA(ws);
   const int C = static_cast<int>(num_classes);
   const long long G = ws.numel() / (3LL * C + 1);
   for (auto* t : {&tp, &fp, &tn, &fn}) {
+    TM_SAME_DEVICE(ws, (*t));
     TORCH_CHECK(t->scalar_type() == at::kLong && t->is_contiguous(), "mc_stats_finalize: states must be int64");
     TORCH_CHECK(t->numel() == (micro ? G : G * C), "mc_stats_finalize: state size mismatch");
   }
@@ -983,7 +987,10 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
                 int64_t num_labels, double threshold, int64_t ignore_index, bool has_ignore, bool samplewise,
                 bool prob_check_all) {
   TM_CHECK_CUDA(preds);
-  TM_CHECK_CUDA(target);
+  TM_SAME_DEVICE(preds, target);
+  TM_SAME_DEVICE(preds, ws);
+  TM_SAME_DEVICE(preds, flag);
+  TM_SAME_DEVICE(preds, not_prob);
   TM_CHECK_CONTIG(preds);
   TM_CHECK_CONTIG(target);
   TORCH_CHECK(preds.numel() == target.numel(), "bin_update: preds/target numel mismatch");
@@ -1026,9 +1033,11 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
 
 void bin_stats_finalize(at::Tensor ws, at::Tensor not_prob, bool accumulate, at::Tensor tp, at::Tensor fp,
                         at::Tensor tn, at::Tensor fn) {
+  TM_CHECK_CUDA(ws);
+  TM_SAME_DEVICE(ws, not_prob);
   const long long G = ws.numel() / kBinSlots;
   for (auto* t : {&tp, &fp, &tn, &fn})
-    TORCH_CHECK(t->scalar_type() == at::kLong && t->is_contiguous() && t->numel() == G,
+    TORCH_CHECK(t->device() == ws.device() && t->scalar_type() == at::kLong && t->is_contiguous() && t->numel() == G,
                 "bin_stats_finalize: states must be contiguous int64 with G elements");
   auto s = stream();
   hipLaunchKernelGGL(bin_finalize_kernel, dim3(grid_cap((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
@@ -1039,6 +1048,9 @@ void bin_stats_finalize(at::Tensor ws, at::Tensor not_prob, bool accumulate, at:
 }
 
 void bin_confmat_finalize(at::Tensor ws, at::Tensor not_prob, at::Tensor confmat) {
+  TM_CHECK_CUDA(ws);
+  TM_SAME_DEVICE(ws, not_prob);
+  TM_SAME_DEVICE(ws, confmat);
   const long long G = ws.numel() / kBinSlots;
   TORCH_CHECK(confmat.scalar_type() == at::kLong && confmat.is_contiguous() && confmat.numel() == 4 * G,
               "bin_confmat_finalize: confmat must be contiguous int64 [G, 2, 2]");
@@ -1055,6 +1067,7 @@ __global__ void launch_probe_kernel(int* __restrict__ flag) {
 
 // Host-cost probe: one empty kernel launch on the current stream (benchmarks/host_overhead.py).
 void launch_probe(at::Tensor flag) {
+  TM_CHECK_CUDA(flag);
   hipLaunchKernelGGL(launch_probe_kernel, dim3(1), dim3(64), 0, stream(), flag.data_ptr<int>());
 }
 

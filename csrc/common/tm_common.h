@@ -9,6 +9,7 @@
 
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <c10/util/BFloat16.h>
 #include <c10/util/Half.h>
 #include <hip/hip_runtime.h>
@@ -150,7 +151,16 @@ inline int cu_count(int device) {
   return v;
 }
 
-#define TM_CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a ROCm (cuda) tensor")
+// Every launcher starts with TM_CHECK_CUDA(<first tensor>): it checks the tensor is on a ROCm device and makes that
+// device current for the rest of the launcher (kernels, stream() and allocations then all target the tensor's device,
+// whatever device the calling thread had selected).  TM_SAME_DEVICE checks the remaining tensor arguments.
+#define TM_CONCAT_(a, b) a##b
+#define TM_CONCAT(a, b) TM_CONCAT_(a, b)
+#define TM_CHECK_CUDA(x)                                                  \
+  TORCH_CHECK((x).is_cuda(), #x " must be a ROCm (cuda) tensor");          \
+  const c10::hip::HIPGuardMasqueradingAsCUDA TM_CONCAT(tm_device_guard_, __LINE__)((x).device())
+#define TM_SAME_DEVICE(a, b) \
+  TORCH_CHECK((a).device() == (b).device(), #b " is on ", (b).device(), " but " #a " is on ", (a).device())
 #define TM_CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
 
 // Dispatch over the element types a metric input can have (floating: f32/f16/bf16/f64; integral: i64/i32/u8/bool)

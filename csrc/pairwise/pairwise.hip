@@ -181,7 +181,7 @@ void launch(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, int metri
 void pairwise_distance(const at::Tensor& x, const at::Tensor& y, at::Tensor out, int64_t metric, double p,
                        bool zero_diag, bool reduce) {
   TM_CHECK_CUDA(x);
-  TM_CHECK_CUDA(y);
+  TM_SAME_DEVICE(x, y);
   TM_CHECK_CONTIG(x);
   TM_CHECK_CONTIG(y);
   TM_CHECK_CONTIG(out);

@@ -1,0 +1,99 @@
+"""Engine semantics on ROCm: deferred validation vs reset / forward, HIP-graph replay robustness, device guards."""
+import pytest
+import torch
+
+from torchmetrics_amd.classification import MulticlassAccuracy, MulticlassConfusionMatrix
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(n=64, c=4, bad=False, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    preds = torch.randn(n, c, generator=g)
+    target = torch.randint(0, c, (n,), generator=g)
+    if bad:
+        target[3] = c + 5
+    return preds.cuda(), target.cuda()
+
+
+def test_public_reset_clears_deferred_validation_word():
+    m = MulticlassConfusionMatrix(num_classes=4).cuda()
+    m.update(*_batch(bad=True))  # deferred: no raise yet
+    m.reset()  # the bad batch is gone with the state
+    m.update(*_batch(seed=1))
+    ref = MulticlassConfusionMatrix(num_classes=4)
+    p, t = _batch(seed=1)
+    ref.update(p.cpu(), t.cpu())
+    assert torch.equal(m.compute().cpu(), ref.compute())
+
+
+def test_forward_raise_restores_global_state_and_flags():
+    m = MulticlassAccuracy(num_classes=4, average="micro").cuda()
+    m.update(*_batch(seed=2))
+    before = {k: getattr(m, k).clone() for k in m._defaults}
+    count = m._update_count
+    with pytest.raises(ValueError):
+        m(*_batch(bad=True, seed=3))
+    for k, v in before.items():
+        assert torch.equal(getattr(m, k), v), k
+    assert m._update_count == count
+    assert m._to_sync == m.sync_on_compute and not m._enable_grad
+    ref = MulticlassAccuracy(num_classes=4, average="micro")
+    p, t = _batch(seed=2)
+    ref.update(p.cpu(), t.cpu())
+    torch.testing.assert_close(m.compute().cpu(), ref.compute())
+
+
+def test_graph_capture_on_garbage_bound_buffers_then_valid_batches():
+    from torchmetrics_amd.utils.graphs import GraphedUpdate
+
+    preds = torch.empty(256, 6, device="cuda").fill_(float("nan"))
+    target = torch.full((256,), 10**6, dtype=torch.long, device="cuda")  # out of range at capture time
+    m = MulticlassConfusionMatrix(num_classes=6).cuda()
+    g = GraphedUpdate(m, preds, target, bind_inputs=True)
+    ref = MulticlassConfusionMatrix(num_classes=6)
+    for s in range(3):
+        p, t = _batch(256, 6, seed=10 + s)
+        preds.copy_(p)
+        target.copy_(t)
+        g()
+        ref.update(p.cpu(), t.cpu())
+    assert torch.equal(m.compute().cpu(), ref.compute())  # no spurious ValueError from the capture warm-up
+
+
+def test_graph_replay_after_reset_recaptures():
+    from torchmetrics_amd.utils.graphs import GraphedUpdate
+
+    m = MulticlassConfusionMatrix(num_classes=5).cuda()
+    p0, t0 = _batch(128, 5, seed=20)
+    g = GraphedUpdate(m, p0, t0)
+    g(p0, t0)
+    m.reset()
+    p1, t1 = _batch(128, 5, seed=21)
+    g(p1, t1)
+    g(p1, t1)
+    ref = MulticlassConfusionMatrix(num_classes=5)
+    ref.update(p1.cpu(), t1.cpu())
+    ref.update(p1.cpu(), t1.cpu())
+    assert torch.equal(m.compute().cpu(), ref.compute())
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two ROCm devices")
+def test_kernels_follow_tensor_device_not_current_device():
+    torch.cuda.set_device(0)
+    m = MulticlassConfusionMatrix(num_classes=5).to("cuda:1")
+    p, t = _batch(128, 5, seed=30)
+    m.update(p.to("cuda:1"), t.to("cuda:1"))
+    ref = MulticlassConfusionMatrix(num_classes=5)
+    ref.update(p.cpu(), t.cpu())
+    assert torch.equal(m.compute().cpu(), ref.compute())
+
+
+def test_mismatched_devices_fail_loudly():
+    from torchmetrics_amd import ops
+
+    p, t = _batch(64, 4)
+    out = torch.zeros(4, 4, dtype=torch.long)  # CPU state with ROCm inputs
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    with pytest.raises(RuntimeError):
+        ops.mc_update(p, t, out, flag, 4, None, ops.MC_CONFMAT)

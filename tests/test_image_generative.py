@@ -188,3 +188,22 @@ def test_inception_network_shapes():
     fid.update(imgs, real=True)
     fid.update(imgs, real=False)
     assert fid.real_features_cov_sum.shape == (64, 64)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_fid_assigning_one_staged_state_keeps_sibling_rows(device):
+    """Replacing one staged state (partial load) runs the staged rows into both first: the sibling keeps them."""
+    d = 48
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(200, d, generator=g, dtype=torch.float64).to(device)
+    eager = FrechetInceptionDistance(feature=_Id(d)).to(device)
+    eager._STAGE_MAX_ROWS = 0
+    staged = FrechetInceptionDistance(feature=_Id(d)).to(device)
+    staged._STAGE_ON_CPU = True
+    for m in (eager, staged):
+        m.update(x, real=True)
+    assert staged.__dict__.get("_fid_hidden")
+    new_sum = torch.zeros(d, dtype=torch.float64, device=device)
+    staged.real_features_sum = new_sum
+    eager.real_features_sum = new_sum.clone()
+    _assert_states_close(_fid_states(staged), _fid_states(eager))

@@ -132,8 +132,8 @@ class FrechetInceptionDistance(_FeatureNetMetric):
     # copied into a per-distribution staging buffer (<= 256 MiB) and the SYRK runs once per full buffer.  While rows are
     # staged, the two affected states are held out of ``__dict__``: ANY read of them (``getattr`` from compute, sync,
     # state_dict, merge, device moves, user code) goes through ``__getattr__``, which runs the pending SYRK first, so
-    # every observer sees exactly the eager values; assigning the state (reset, load_state_dict) drops the staged rows
-    # that belonged to the replaced value.
+    # every observer sees exactly the eager values; assigning either state first runs the staged rows into both
+    # (reset / load_state_dict / device moves read every state anyway, so this costs them nothing extra).
     _STAGE_BYTES = 256 << 20
     _STAGE_MAX_ROWS = 1 << 16
     _STAGE_ON_CPU = False  # staging is a ROCm optimisation; tests switch it on to cover the state semantics on CPU
@@ -152,9 +152,9 @@ class FrechetInceptionDistance(_FeatureNetMetric):
     def __setattr__(self, name: str, value: Any) -> None:
         hidden = self.__dict__.get("_fid_hidden")
         if hidden and name in hidden:
-            prefix = name.split("_", 1)[0]
-            self._unhide(prefix)  # the staged rows belong to the value being replaced
-            self.__dict__["_fid_rows"][prefix] = 0
+            # run the staged rows into BOTH states before one of them is replaced: the sibling state (and
+            # num_samples, which already counts those rows) must keep them
+            self._flush_staged(name.split("_", 1)[0])
         super().__setattr__(name, value)
 
     def _unhide(self, prefix: str) -> None:

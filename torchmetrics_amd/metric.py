@@ -233,29 +233,48 @@ class Metric(Module, ABC):
         if self.compute_on_cpu:
             self._move_list_states_to_cpu()
 
+    def _batch_reset(self) -> None:
+        """``reset()`` inside ``forward``: the deferred-validation word survives (it belongs to the global state)."""
+        self.__dict__["_keep_device_errors"] = True
+        try:
+            self.reset()
+        finally:
+            self.__dict__.pop("_keep_device_errors", None)
+
+    def _restore_global(self, cache: Dict[str, Any], count: int, saved: bool) -> None:
+        for attr, val in cache.items():
+            setattr(self, attr, val)
+        self._update_count = count
+        self._exit_batch_mode(saved)
+
     def _forward_full_state_update(self, *args: Any, **kwargs: Any) -> Any:
         """Two ``update`` calls: one on the global state, one on a fresh state for the batch value."""
         self.update(*args, **kwargs)
         count = self._update_count
         saved = self._enter_batch_mode()
         cache = {attr: getattr(self, attr) for attr in self._defaults}
-        self.reset()
-        self.update(*args, **kwargs)
-        batch_val = self.compute()
-        for attr, val in cache.items():
-            setattr(self, attr, val)
-        self._update_count = count
-        self._exit_batch_mode(saved)
+        try:
+            self._batch_reset()
+            self.update(*args, **kwargs)
+            batch_val = self.compute()
+        finally:
+            # also on a raise (e.g. a validation bit surfacing in the batch compute): the global state and the
+            # batch-mode flags come back exactly as they were
+            self._restore_global(cache, count, saved)
         return batch_val
 
     def _forward_reduce_state_update(self, *args: Any, **kwargs: Any) -> Any:
         """One ``update`` on a fresh state, then fold the batch state into the saved global state."""
         global_state = {attr: getattr(self, attr) for attr in self._defaults}
         count = self._update_count
-        self.reset()
         saved = self._enter_batch_mode()
-        self.update(*args, **kwargs)
-        batch_val = self.compute()
+        try:
+            self._batch_reset()
+            self.update(*args, **kwargs)
+            batch_val = self.compute()
+        except BaseException:
+            self._restore_global(global_state, count, saved)
+            raise
         self._update_count = count + 1
         with torch.no_grad():
             self._reduce_states(global_state)
@@ -506,8 +525,14 @@ class Metric(Module, ABC):
         )
 
     def reset(self) -> None:
-        """Reset all states to their defaults."""
+        """Reset all states to their defaults.
+
+        A public reset also clears the deferred-validation word (stream-ordered ``zero_``, no host sync): a bad batch
+        that was never computed must not raise for data that is no longer in the state.
+        """
         self.__dict__.pop("_errors_checked_at", None)
+        if not self.__dict__.get("_keep_device_errors") and self.__dict__.get("_device_errors") is not None:
+            self._device_errors.zero_()
         self._update_count = 0
         self._forward_cache = None
         self._computed = None

@@ -20,7 +20,7 @@ the graph with them -- or with no arguments -- and no copy is made.  A ring of N
 
 The metric's Python bookkeeping (``update_count``, the ``compute`` cache) is advanced on every replay, so
 ``compute()``, ``reset()``, sync and ``state_dict`` behave exactly as after eager updates.  ``reset()`` re-creates the
-state tensors, so a graph must be re-captured after a reset (``GraphedUpdate.recapture``).
+state tensors: the next call notices (one identity check per member) and re-captures before replaying.
 """
 from typing import Any, Dict, List, Tuple, Union
 
@@ -66,6 +66,9 @@ class GraphedUpdate:
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         snapshot = None
+        # the warm-up runs on the example buffers, which may hold garbage (bound producer buffers are often
+        # torch.empty at capture time): the validation words are restored with the states afterwards
+        errs = {name: (m._device_errors.clone() if m._device_errors is not None else None) for name, m in members}
         with torch.cuda.stream(side):
             for _ in range(max(self._warmup, 1)):
                 before = _states(members)
@@ -88,7 +91,16 @@ class GraphedUpdate:
         for name, m in members:
             m.__dict__["_update_count"] = counts[name]
             m.__dict__["_computed"] = None
-            m.__dict__.pop("_errors_checked_at", None)  # warm-up launches may have raised validation bits
+            m.__dict__.pop("_errors_checked_at", None)
+            buf = m._device_errors
+            if buf is not None:
+                if errs[name] is None:
+                    buf.zero_()
+                else:
+                    buf.copy_(errs[name])
+        # one state tensor per member: a replay checks these are still the metric's states (reset() rebinds them)
+        self._sentinels = [(m, attr, after[(name, attr)]) for name, m in members
+                           for attr in list(m._defaults)[:1]]
 
     def recapture(self) -> None:
         """Capture again (after ``reset()`` re-created the state tensors, or after moving the metric)."""
@@ -107,6 +119,11 @@ class GraphedUpdate:
                 raise ValueError(f"input of shape {tuple(x.shape)} / {x.dtype} does not match the captured "
                                  f"{tuple(s.shape)} / {s.dtype}; capture a new GraphedUpdate for it")
             s.copy_(x, non_blocking=True)
+        for m, attr, t in self._sentinels:
+            if m.__dict__.get(attr) is not t and getattr(m, attr) is not t:
+                # reset() / load_state_dict / .to() rebound the states: the graph would replay into orphaned tensors
+                self._capture()
+                break
         self.graph.replay()
         for _, m in self._members:
             d = m.__dict__

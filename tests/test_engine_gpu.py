@@ -32,7 +32,7 @@ def test_forward_raise_restores_global_state_and_flags():
     m.update(*_batch(seed=2))
     before = {k: getattr(m, k).clone() for k in m._defaults}
     count = m._update_count
-    with pytest.raises(ValueError):
+    with pytest.raises(RuntimeError, match="unique values in `target`"):
         m(*_batch(bad=True, seed=3))
     for k, v in before.items():
         assert torch.equal(getattr(m, k), v), k

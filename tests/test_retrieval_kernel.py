@@ -1,0 +1,94 @@
+"""Retrieval kernel (``csrc/sort/retrieval.hip``) vs independent per-query numpy / sklearn oracles, all kinds."""
+import numpy as np
+import pytest
+import torch
+from sklearn.metrics import ndcg_score, roc_auc_score
+
+from torchmetrics_amd import ops
+
+DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+def _oracle(kind, p, t, k, adaptive):
+    """One query, reference definitions (F/retrieval/*.py), stable order among ties."""
+    order = np.argsort(-p, kind="stable")
+    ts = t[order]
+    n = len(p)
+    kk = n if k is None else k
+    top = ts[:kk]
+    rel = (t > 0).sum()
+    if kind == "map":
+        hits = np.nonzero(top > 0)[0]
+        return 0.0 if len(hits) == 0 else np.mean([(i + 1) / (h + 1) for i, h in enumerate(hits)])
+    if kind == "mrr":
+        hits = np.nonzero(top > 0)[0]
+        return 0.0 if len(hits) == 0 else 1.0 / (hits[0] + 1)
+    if kind == "precision":
+        denom = min(kk, n) if (adaptive and k is not None) else kk
+        return (top > 0).sum() / denom
+    if kind == "recall":
+        return (top > 0).sum() / rel if rel else 0.0
+    if kind == "fall_out":
+        neg = (t <= 0).sum()
+        return (top <= 0).sum() / neg if neg else 0.0
+    if kind == "hit_rate":
+        return float((top > 0).any())
+    if kind == "r_precision":
+        return (ts[:rel] > 0).sum() / rel if rel else 0.0
+    if kind == "ndcg":
+        if n == 1:
+            return 1.0 if t[0] > 0 else 0.0
+        return ndcg_score(t[None].astype(float), p[None], k=kk)
+    if kind == "auroc":
+        sel = order[:kk]
+        y = t[sel] > 0
+        if y.all() or (~y).all():
+            return 0.0
+        return roc_auc_score(y, p[sel])
+    raise ValueError(kind)
+
+
+KINDS = ["map", "mrr", "precision", "recall", "fall_out", "hit_rate", "r_precision", "ndcg", "auroc"]
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("top_k,adaptive", [(None, False), (3, False), (5, True)])
+def test_retrieval_kernel_kinds(device, kind, top_k, adaptive):
+    g = np.random.default_rng(hash((kind, top_k)) % 2**32)
+    n = 700
+    idx = g.integers(0, 60, n) * 7 - 100  # sparse, negative ids too
+    p = np.round(g.random(n), 1).astype(np.float32)  # ties
+    t = g.integers(0, 3 if kind == "ndcg" else 2, n)
+    vals, empty, nq = ops.retrieval_metric(torch.from_numpy(p).to(device), torch.from_numpy(t).to(device),
+                                           torch.from_numpy(idx).to(device), kind, top_k, adaptive)
+    q = int(nq[0])
+    uq = np.unique(idx)
+    assert q == len(uq)
+    vals, empty = vals.cpu().numpy()[:q], empty.cpu().numpy()[:q]
+    for j, qq in enumerate(uq):
+        m = idx == qq
+        exp_empty = (t[m] <= 0).all() if kind != "fall_out" else (t[m] > 0).all()
+        assert bool(empty[j]) == bool(exp_empty)
+        if exp_empty:
+            continue
+        np.testing.assert_allclose(vals[j], _oracle(kind, p[m], t[m], top_k, adaptive), rtol=1e-6, atol=1e-9,
+                                   err_msg=f"query {qq}")
+
+
+@pytest.mark.gpu
+def test_retrieval_module_gpu_matches_cpu_large():
+    import torchmetrics_amd as tm
+
+    g = torch.Generator().manual_seed(0)
+    n = 200_000
+    idx = torch.randint(0, 5000, (n,), generator=g)
+    p = torch.rand(n, generator=g)
+    t = torch.randint(0, 2, (n,), generator=g)
+    for cls, kw in [(tm.retrieval.RetrievalMAP, {}), (tm.retrieval.RetrievalNormalizedDCG, {"top_k": 10}),
+                    (tm.retrieval.RetrievalMRR, {"empty_target_action": "skip"}),
+                    (tm.retrieval.RetrievalPrecision, {"top_k": 5, "aggregation": "median"})]:
+        a, b = cls(**kw), cls(**kw).cuda()
+        a.update(p, t, idx)
+        b.update(p.cuda(), t.cuda(), idx.cuda())
+        torch.testing.assert_close(b.compute().cpu(), a.compute(), rtol=1e-5, atol=1e-6)

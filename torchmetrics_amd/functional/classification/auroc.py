@@ -1,9 +1,9 @@
 """Area under the ROC curve (reference ``F/classification/auroc.py:45-470``).
 
-Unbinned multiclass / multilabel AUROC is computed for *all* columns at once from one segmented sort
-(:func:`_batched_sorted_stats`): with scores sorted descending per column, every negative sample contributes the mean
-of the true-positive counts just before and just after its tie group, which is exactly the trapezoid under the
-tie-collapsed ROC curve.  The reference loops over classes, sorting and building each curve separately.
+Unbinned AUROC is computed for *all* columns at once by the sorted-curve kernels (``csrc/sort/clf_curve.hip``,
+:mod:`._sorted`): with scores sorted descending per column, every tie run contributes ``neg_run * (tp_before +
+pos_run / 2)``, which is exactly the trapezoid under the tie-collapsed ROC curve, and no curve is materialised.  The
+reference loops over classes, sorting and building each curve separately.
 """
 from typing import List, Optional, Tuple, Union
 
@@ -12,6 +12,7 @@ from torch import Tensor
 from typing_extensions import Literal
 
 from torchmetrics_amd import ops
+from torchmetrics_amd.functional.classification import _sorted
 from torchmetrics_amd.functional.classification.precision_recall_curve import (
     Thresholds,
     _binary_curve_state,
@@ -33,76 +34,53 @@ from torchmetrics_amd.utilities.prints import rank_zero_warn
 
 
 # ------------------------------------------------------------------------------------------- batched (unbinned)
-def _batched_sorted_stats(scores: Tensor, pos: Tensor, valid: Optional[Tensor] = None):
-    """Sort ``[M, K]`` scores per column (descending) and return tie-group statistics (fp64).
-
-    Returns ``(pos_w, neg_w, tp_before, tp_after, fp_after, P, F)``: per sorted element its positive / negative weight,
-    the cumulative TP count before its tie group and at its end, the cumulative FP count at its end, and the column
-    totals.
-    """
-    if valid is not None:
-        scores = torch.where(valid, scores, torch.full_like(scores, float("-inf")))
-    s, order = torch.sort(scores, dim=0, descending=True)
-    pos_w = torch.gather(pos.to(torch.float64), 0, order)
-    neg_w = 1.0 - pos_w
-    if valid is not None:
-        v = torch.gather(valid.to(torch.float64), 0, order)
-        pos_w, neg_w = pos_w * v, neg_w * v
-    m = s.shape[0]
-    tps, fps = pos_w.cumsum(0), neg_w.cumsum(0)
-    idx = torch.arange(m, device=s.device).unsqueeze(1).expand_as(s)
-    is_end = torch.ones_like(s, dtype=torch.bool)
-    is_end[:-1] = s[1:] != s[:-1]
-    is_start = torch.ones_like(s, dtype=torch.bool)
-    is_start[1:] = is_end[:-1]
-    # index of the group end at or after i: reverse running minimum over end positions
-    end_idx = torch.where(is_end, idx, torch.full_like(idx, m)).flip(0).cummin(0).values.flip(0)
-    start_idx = torch.where(is_start, idx, torch.full_like(idx, -1)).cummax(0).values
-    tp_after = torch.gather(tps, 0, end_idx)
-    fp_after = torch.gather(fps, 0, end_idx)
-    before = (start_idx - 1).clamp(min=0)
-    tp_before = torch.where(start_idx > 0, torch.gather(tps, 0, before), torch.zeros_like(tps))
-    return pos_w, neg_w, tp_before, tp_after, fp_after, tps[-1], fps[-1]
+def _column_auroc(preds: Tensor, target: Tensor, tmode: int, pos_label: int = 1,
+                  ignore_index: Optional[int] = None) -> Tuple[Tensor, Tensor]:
+    """Per-column ROC AUC (0 for columns without positives or negatives, as the reference) and the per-column
+    positive counts, from one sorted-curve launch for all columns."""
+    if preds.shape[0] == 0:
+        k = 1 if preds.ndim == 1 else preds.shape[1]
+        z = torch.zeros(k, dtype=torch.float32, device=preds.device)
+        return z, z.clone()
+    st = _sorted.column_stats(preds, target, tmode, pos_label, ignore_index)[0]
+    return _sorted.auroc_from_stats(st), st[:, _sorted.P].to(torch.float32)
 
 
-def _batched_auroc(scores: Tensor, pos: Tensor, valid: Optional[Tensor] = None) -> Tensor:
-    """Per-column ROC AUC of ``[M, K]`` scores; 0 for columns without positives or negatives (reference behaviour)."""
-    if scores.shape[0] == 0:
-        return torch.zeros(scores.shape[1], dtype=torch.float32, device=scores.device)
-    pos_w, neg_w, tp_b, tp_a, _, p, f = _batched_sorted_stats(scores, pos, valid)
-    area = (neg_w * (tp_a + tp_b)).sum(0) * 0.5
-    denom = p * f
-    res = torch.where(denom > 0, area / denom.clamp(min=1), torch.zeros_like(area))
-    return res.to(torch.float32)
-
-
-def _batched_average_precision(scores: Tensor, pos: Tensor, valid: Optional[Tensor] = None) -> Tensor:
-    """Per-column step-wise AP; NaN for columns without positives (reference behaviour)."""
-    if scores.shape[0] == 0:
-        return torch.full((scores.shape[1],), float("nan"), dtype=torch.float32, device=scores.device)
-    pos_w, _, _, tp_a, fp_a, p, _ = _batched_sorted_stats(scores, pos, valid)
-    prec = tp_a / (tp_a + fp_a).clamp(min=1)
-    num = torch.where(pos_w > 0, pos_w * prec, torch.zeros_like(prec)).sum(0)
-    return (num / p).to(torch.float32)  # p == 0 -> nan
+def _column_average_precision(preds: Tensor, target: Tensor, tmode: int, pos_label: int = 1,
+                              ignore_index: Optional[int] = None) -> Tuple[Tensor, Tensor]:
+    """Per-column step-wise AP (NaN without positives, as the reference) and the per-column positive counts."""
+    if preds.shape[0] == 0:
+        k = 1 if preds.ndim == 1 else preds.shape[1]
+        return (torch.full((k,), float("nan"), dtype=torch.float32, device=preds.device),
+                torch.zeros(k, dtype=torch.float32, device=preds.device))
+    st = _sorted.column_stats(preds, target, tmode, pos_label, ignore_index)[0]
+    return _sorted.ap_from_stats(st), st[:, _sorted.P].to(torch.float32)
 
 
 def _reduce_scores(
-    res: Tensor, average: Optional[str], weights: Optional[Tensor], name: str = "Average precision"
+    res: Tensor, average: Optional[str], weights: Optional[Tensor], name: str = "Average precision",
+    may_be_nan: bool = True,
 ) -> Tensor:
+    """macro / weighted reduction ignoring NaN classes, on the device (masked sums instead of boolean indexing).
+
+    The reference's nan warning costs one 1-byte read; ``may_be_nan=False`` (AUROC: never NaN) skips it.
+    """
     if average is None or average == "none":
         return res
-    if torch.isnan(res).any():
+    if average not in ("macro", "weighted") or (average == "weighted" and weights is None):
+        raise ValueError("Received an incompatible combinations of inputs to make reduction.")
+    nan = torch.isnan(res)
+    if may_be_nan and bool(nan.any()):
         rank_zero_warn(
             f"{name} score for one or more classes was `nan`. Ignoring these classes in {average}-average",
             UserWarning,
         )
-    idx = ~torch.isnan(res)
+    vals = torch.where(nan, torch.zeros_like(res), res)
+    keep = (~nan).to(res.dtype)
     if average == "macro":
-        return res[idx].mean()
-    if average == "weighted" and weights is not None:
-        w = _safe_divide(weights[idx], weights[idx].sum())
-        return (res[idx] * w).sum()
-    raise ValueError("Received an incompatible combinations of inputs to make reduction.")
+        return vals.sum() / keep.sum()
+    w = torch.where(nan, torch.zeros_like(res), weights.to(res.dtype))
+    return (vals * _safe_divide(w, w.sum())).sum()
 
 
 def _fused_curve_score(state: Tensor, kind: int, average: Optional[str], name: str) -> Tensor:
@@ -149,6 +127,22 @@ def _binary_auroc_compute(
     max_fpr: Optional[float] = None,
     pos_label: int = 1,
 ) -> Tensor:
+    if thresholds is None and (max_fpr is None or max_fpr == 1):
+        # whole-curve AUC straight from the sorted-run stats: no curve materialisation; the reference's
+        # degenerate-curve warnings need the two totals (one 16-byte read)
+        preds, target = state
+        if preds.ndim > target.ndim:
+            preds = preds[:, 0]
+        if preds.numel():
+            st = _sorted.column_stats(preds.reshape(-1), target.reshape(-1), ops.CLF_T_BINARY, pos_label)[0]
+            n_pos, n_neg = st[0, :2].tolist()
+            if n_neg <= 0:
+                rank_zero_warn("No negative samples in targets, false positive value should be meaningless."
+                               " Returning zero tensor in false positive score", UserWarning)
+            if n_pos <= 0:
+                rank_zero_warn("No positive samples in targets, true positive value should be meaningless."
+                               " Returning zero tensor in true positive score", UserWarning)
+            return _sorted.auroc_from_stats(st)[0]
     fpr, tpr, _ = _binary_roc_compute(state, thresholds, pos_label)
     if max_fpr is None or max_fpr == 1 or fpr.sum() == 0 or tpr.sum() == 0:
         return _auc_compute_without_check(fpr, tpr, 1.0)
@@ -204,9 +198,8 @@ def _multiclass_auroc_compute(
         fpr, tpr, _ = _multiclass_roc_compute(state, num_classes, thresholds)
         return _reduce_auroc(fpr, tpr, average, weights=state[0][:, 1, :].sum(-1))
     preds, target = state
-    pos = target.unsqueeze(1) == torch.arange(num_classes, device=target.device)
-    res = _batched_auroc(preds, pos)
-    return _reduce_scores(res, average, _bincount(target, minlength=num_classes).float())
+    res, n_pos = _column_auroc(preds, target, ops.CLF_T_OVR)
+    return _reduce_scores(res, average, n_pos, "AUROC", may_be_nan=False)
 
 
 def multiclass_auroc(
@@ -258,13 +251,10 @@ def _multilabel_auroc_compute(
         fpr, tpr, _ = _multilabel_roc_compute(state, num_labels, thresholds, ignore_index)
         return _reduce_auroc(fpr, tpr, average, weights=state[0][:, 1, :].sum(-1))
     preds, target = state
-    valid = _multilabel_valid(target, ignore_index)
     if average == "micro":
-        res = _batched_auroc(preds.reshape(-1, 1), (target == 1).reshape(-1, 1),
-                             None if valid is None else valid.reshape(-1, 1))
-        return res[0]
-    res = _batched_auroc(preds, target == 1, valid)
-    return _reduce_scores(res, average, (target == 1).sum(dim=0).float())
+        return _column_auroc(preds.reshape(-1), target.reshape(-1), ops.CLF_T_ELEM, 1, ignore_index)[0][0]
+    res, n_pos = _column_auroc(preds, target, ops.CLF_T_ELEM, 1, ignore_index)
+    return _reduce_scores(res, average, n_pos, "AUROC", may_be_nan=False)
 
 
 def multilabel_auroc(

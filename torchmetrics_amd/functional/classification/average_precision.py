@@ -1,7 +1,8 @@
 """Average precision (reference ``F/classification/average_precision.py:43-420``).
 
 Binned: from the HIP multi-threshold confusion matrices.  Unbinned multiclass / multilabel: all columns in one
-segmented sort (:func:`~torchmetrics_amd.functional.classification.auroc._batched_average_precision`).
+sorted-curve launch (``csrc/sort/clf_curve.hip`` via
+:func:`~torchmetrics_amd.functional.classification.auroc._column_average_precision`).
 """
 from typing import List, Optional, Tuple, Union
 
@@ -11,7 +12,7 @@ from typing_extensions import Literal
 
 from torchmetrics_amd import ops
 from torchmetrics_amd.functional.classification.auroc import (
-    _batched_average_precision,
+    _column_average_precision,
     _fused_curve_score,
     _multilabel_valid,
     _reduce_scores,
@@ -47,7 +48,9 @@ def _reduce_average_precision(
 def _binary_average_precision_compute(state: Union[Tensor, Tuple[Tensor, Tensor]], thresholds: Optional[Tensor]) -> Tensor:
     if not isinstance(state, Tensor) or thresholds is None:
         preds, target = state
-        return _batched_average_precision(preds.reshape(-1, 1), (target == 1).reshape(-1, 1))[0]
+        if preds.ndim > target.ndim:
+            preds = preds[:, 0]
+        return _column_average_precision(preds.reshape(-1), target.reshape(-1), ops.CLF_T_BINARY)[0][0]
     precision, recall, _ = _binary_precision_recall_curve_compute(state, thresholds)
     return -torch.sum((recall[1:] - recall[:-1]) * precision[:-1])
 
@@ -88,9 +91,8 @@ def _multiclass_average_precision_compute(
         precision, recall, _ = _multiclass_precision_recall_curve_compute(state, num_classes, thresholds)
         return _reduce_average_precision(precision, recall, average, weights=state[0][:, 1, :].sum(-1))
     preds, target = state
-    pos = target.unsqueeze(1) == torch.arange(num_classes, device=target.device)
-    res = _batched_average_precision(preds, pos)
-    return _reduce_scores(res, average, _bincount(target, minlength=num_classes).float())
+    res, n_pos = _column_average_precision(preds, target, ops.CLF_T_OVR)
+    return _reduce_scores(res, average, n_pos)
 
 
 def multiclass_average_precision(
@@ -138,13 +140,10 @@ def _multilabel_average_precision_compute(
         precision, recall, _ = _multilabel_precision_recall_curve_compute(state, num_labels, thresholds, ignore_index)
         return _reduce_average_precision(precision, recall, average, weights=state[0][:, 1, :].sum(-1))
     preds, target = state
-    valid = _multilabel_valid(target, ignore_index)
     if average == "micro":
-        return _batched_average_precision(
-            preds.reshape(-1, 1), (target == 1).reshape(-1, 1), None if valid is None else valid.reshape(-1, 1)
-        )[0]
-    res = _batched_average_precision(preds, target == 1, valid)
-    return _reduce_scores(res, average, (target == 1).sum(dim=0).float())
+        return _column_average_precision(preds.reshape(-1), target.reshape(-1), ops.CLF_T_ELEM, 1, ignore_index)[0][0]
+    res, n_pos = _column_average_precision(preds, target, ops.CLF_T_ELEM, 1, ignore_index)
+    return _reduce_scores(res, average, n_pos)
 
 
 def multilabel_average_precision(

@@ -12,12 +12,14 @@ from typing_extensions import Literal
 from torchmetrics_amd.functional.classification.precision_recall_curve import (
     Thresholds,
     _binary_clf_curve,
+    _clf_curves,
     _binary_curve_state,
     _multiclass_curve_state,
     _multilabel_curve_state,
     _multilabel_masked_column,
     _task_dispatch,
 )
+from torchmetrics_amd import ops
 from torchmetrics_amd.utilities.compute import _safe_divide, interp
 from torchmetrics_amd.utilities.prints import rank_zero_warn
 
@@ -35,11 +37,22 @@ def _binary_roc_compute(
     if isinstance(state, Tensor) and thresholds is not None:
         fpr, tpr = _rates_from_confmat(state)
         return fpr.flip(0), tpr.flip(0), thresholds.flip(0)
-    fps, tps, thres = _binary_clf_curve(preds=state[0], target=state[1], pos_label=pos_label)
+    preds, target = state[0], state[1]
+    if preds.ndim > target.ndim:
+        preds = preds[:, 0]
+    if preds.numel() == 0:
+        fps, tps, thres = _binary_clf_curve(preds=preds, target=target, pos_label=pos_label)
+        return _roc_from_clf(fps, tps, thres, 0.0, 0.0)
+    fps, tps, thres, host = _clf_curves(preds.reshape(-1), target.reshape(-1), ops.CLF_T_BINARY, pos_label)
+    return _roc_from_clf(fps[0], tps[0], thres[0], host[0][1], host[0][0])
+
+
+def _roc_from_clf(fps: Tensor, tps: Tensor, thres: Tensor, n_neg: float, n_pos: float) -> Tuple[Tensor, Tensor, Tensor]:
+    """ROC points from one ``_binary_clf_curve``; ``n_neg`` / ``n_pos`` are host totals (no device read here)."""
     tps = torch.cat([torch.zeros(1, dtype=tps.dtype, device=tps.device), tps])
     fps = torch.cat([torch.zeros(1, dtype=fps.dtype, device=fps.device), fps])
     thres = torch.cat([torch.ones(1, dtype=thres.dtype, device=thres.device), thres])
-    if fps[-1] <= 0:
+    if n_neg <= 0:
         rank_zero_warn(
             "No negative samples in targets, false positive value should be meaningless."
             " Returning zero tensor in false positive score",
@@ -48,7 +61,7 @@ def _binary_roc_compute(
         fpr = torch.zeros_like(thres)
     else:
         fpr = fps / fps[-1]
-    if tps[-1] <= 0:
+    if n_pos <= 0:
         rank_zero_warn(
             "No positive samples in targets, true positive value should be meaningless."
             " Returning zero tensor in true positive score",
@@ -86,8 +99,9 @@ def _multiclass_roc_compute(
         tensor_state = True
     else:
         fpr_list, tpr_list, thres_list = [], [], []
-        for i in range(num_classes):
-            res = _binary_roc_compute((state[0][:, i], state[1]), thresholds=None, pos_label=i)
+        fl, tl, hl, host = _clf_curves(state[0], state[1], ops.CLF_T_OVR)
+        for f, t, th, h in zip(fl, tl, hl, host):
+            res = _roc_from_clf(f, t, th, h[1], h[0])
             fpr_list.append(res[0])
             tpr_list.append(res[1])
             thres_list.append(res[2])
@@ -133,8 +147,9 @@ def _multilabel_roc_compute(
         fpr, tpr = _rates_from_confmat(state)
         return fpr.flip(0).T, tpr.flip(0).T, thresholds.flip(0)
     fpr_l, tpr_l, thr_l = [], [], []
-    for i in range(num_labels):
-        res = _binary_roc_compute(_multilabel_masked_column(state, i, ignore_index), thresholds=None, pos_label=1)
+    fl, tl, hl, host = _clf_curves(state[0], state[1], ops.CLF_T_ELEM, 1, ignore_index)
+    for f, t, th, h in zip(fl, tl, hl, host):
+        res = _roc_from_clf(f, t, th, h[1], h[0])
         fpr_l.append(res[0])
         tpr_l.append(res[1])
         thr_l.append(res[2])

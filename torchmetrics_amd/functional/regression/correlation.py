@@ -160,8 +160,20 @@ def concordance_corrcoef(preds: Tensor, target: Tensor) -> Tensor:
 
 # ---------------------------------------------------------------------------------------------------------- Spearman
 def _rank_data(data: Tensor) -> Tensor:
-    """1-based ranks along dim 0 with ties given their average rank (vectorised)."""
+    """1-based ranks along dim 0 with ties given their average rank (vectorised).
+
+    On ROCm: one sorted-run launch chain for all columns (``csrc/sort/clf_curve.hip`` average-rank emission: radix
+    sort with the flat id as payload, tie-run scan, scatter of the run's mean position).
+    """
     n = data.shape[0]
+    if data.is_cuda and n > 0 and data.is_floating_point():
+        from torchmetrics_amd.functional.classification import _sorted
+
+        x = data if data.ndim == 2 else data.reshape(n, -1)
+        k = x.shape[1]
+        dummy = torch.zeros(n, dtype=torch.uint8, device=data.device)
+        desc = _sorted.column_stats(x, dummy, ops.CLF_T_BINARY, emit=ops.EMIT_RANKS)[4].view(k, n).t()
+        return ((n + 1) - desc).reshape(data.shape).to(data.dtype)
     sorted_vals, order = torch.sort(data, dim=0, stable=True)
     pos = torch.arange(1, n + 1, dtype=torch.float64, device=data.device)
     pos = pos.view(-1, *([1] * (data.ndim - 1))).expand_as(sorted_vals)
@@ -325,23 +337,19 @@ def _kendall_corrcoef_compute(
     if preds.ndim == 1:
         preds, target = preds.unsqueeze(1), target.unsqueeze(1)
     n = preds.shape[0]
-    conc, disc = _pair_counts(preds, target)
-    conc, disc = conc.double(), disc.double()
-    cmd = conc - disc
+    # one stats launch chain (ROCm: csrc/sort/kendall.hip) -> discordant pairs, tie terms, distinct counts
+    st = ops.kendall_stats(preds, target)
+    disc, pt, pt1, pt2, tt, tt1, tt2, txy, pu, tu = st.to(preds.device).unbind(1)
     nt = torch.tensor(float(n), dtype=torch.float64, device=preds.device)
-    pt = tt = pt1 = pt2 = tt1 = tt2 = None
-    if variant != _MetricVariant.A:
-        pt, pt1, pt2 = _tie_stats(preds)
-        tt, tt1, tt2 = _tie_stats(target)
+    conc = nt * (nt - 1) / 2 - pt - tt + txy - disc
+    cmd = conc - disc
     if variant == _MetricVariant.A:
         tau = cmd / (conc + disc)
     elif variant == _MetricVariant.B:
         tot = nt * (nt - 1) / 2
         tau = cmd / torch.sqrt((tot - pt) * (tot - tt))
     else:
-        pu = torch.tensor([float(len(torch.unique(preds[:, c]))) for c in range(preds.shape[1])], device=preds.device)
-        tu = torch.tensor([float(len(torch.unique(target[:, c]))) for c in range(target.shape[1])], device=preds.device)
-        m = torch.minimum(pu, tu).double()
+        m = torch.minimum(pu, tu)
         tau = 2 * cmd / ((m - 1) / m * nt**2)
     p_value = None
     if alternative is not None:

@@ -11,6 +11,7 @@ import torch
 from torch import Tensor
 from torch.nn.functional import pad
 
+from torchmetrics_amd import ops
 from torchmetrics_amd.functional.retrieval._segments import Segments
 from torchmetrics_amd.utilities.checks import _check_retrieval_functional_inputs
 
@@ -131,11 +132,24 @@ def _one(preds: Tensor, target: Tensor, non_binary: bool = False) -> Segments:
     return Segments(preds, target)
 
 
+def _kernel_one(preds: Tensor, target: Tensor, kind: str, top_k: Optional[int] = None, adaptive_k: bool = False,
+                non_binary: bool = False) -> Optional[Tensor]:
+    """Single-query value from the retrieval kernel on ROCm (no host read); ``None`` on CPU tensors."""
+    if not preds.is_cuda:
+        return None
+    preds, target = _check_retrieval_functional_inputs(preds, target, allow_non_binary_target=non_binary)
+    idx = torch.zeros(preds.numel(), dtype=torch.long, device=preds.device)
+    return _f32(ops.retrieval_metric(preds, target, idx, kind, top_k, adaptive_k)[0][0])
+
+
 def retrieval_precision(preds: Tensor, target: Tensor, top_k: Optional[int] = None, adaptive_k: bool = False) -> Tensor:
     """Fraction of the top-k documents that are relevant (``F/retrieval/precision.py``)."""
     if not isinstance(adaptive_k, bool):
         raise ValueError("`adaptive_k` has to be a boolean")
     _check_top_k(top_k)
+    res = _kernel_one(preds, target, "precision", top_k, adaptive_k)
+    if res is not None:
+        return res
     seg = _one(preds, target)
     if not seg.target.sum():
         return torch.tensor(0.0, device=seg.preds.device)
@@ -145,6 +159,9 @@ def retrieval_precision(preds: Tensor, target: Tensor, top_k: Optional[int] = No
 def retrieval_recall(preds: Tensor, target: Tensor, top_k: Optional[int] = None) -> Tensor:
     """Fraction of the relevant documents retrieved in the top k (``F/retrieval/recall.py``)."""
     _check_top_k(top_k)
+    res = _kernel_one(preds, target, "recall", top_k)
+    if res is not None:
+        return res
     seg = _one(preds, target)
     if not seg.target.sum():
         return torch.tensor(0.0, device=seg.preds.device)
@@ -154,6 +171,9 @@ def retrieval_recall(preds: Tensor, target: Tensor, top_k: Optional[int] = None)
 def retrieval_fall_out(preds: Tensor, target: Tensor, top_k: Optional[int] = None) -> Tensor:
     """Fraction of the non-relevant documents retrieved in the top k (``F/retrieval/fall_out.py``)."""
     _check_top_k(top_k)
+    res = _kernel_one(preds, target, "fall_out", top_k)
+    if res is not None:
+        return res
     seg = _one(preds, target)
     if not (1 - seg.target).sum():
         return torch.tensor(0.0, device=seg.preds.device)
@@ -163,38 +183,47 @@ def retrieval_fall_out(preds: Tensor, target: Tensor, top_k: Optional[int] = Non
 def retrieval_hit_rate(preds: Tensor, target: Tensor, top_k: Optional[int] = None) -> Tensor:
     """1 if any relevant document is in the top k (``F/retrieval/hit_rate.py``)."""
     _check_top_k(top_k)
-    return _seg_hit_rate(_one(preds, target), top_k)[0]
+    res = _kernel_one(preds, target, "hit_rate", top_k)
+    return res if res is not None else _seg_hit_rate(_one(preds, target), top_k)[0]
 
 
 def retrieval_r_precision(preds: Tensor, target: Tensor) -> Tensor:
     """Precision at R = number of relevant documents (``F/retrieval/r_precision.py``)."""
-    return _seg_r_precision(_one(preds, target))[0]
+    res = _kernel_one(preds, target, "r_precision")
+    return res if res is not None else _seg_r_precision(_one(preds, target))[0]
 
 
 def retrieval_reciprocal_rank(preds: Tensor, target: Tensor, top_k: Optional[int] = None) -> Tensor:
     """1 / rank of the first relevant document within the top k (``F/retrieval/reciprocal_rank.py``)."""
     if top_k is not None and not isinstance(top_k, int) and top_k <= 0:
         raise ValueError(f"Argument ``top_k`` has to be a positive integer or None, but got {top_k}.")
-    return _seg_reciprocal_rank(_one(preds, target), top_k)[0]
+    res = _kernel_one(preds, target, "mrr", top_k)
+    return res if res is not None else _seg_reciprocal_rank(_one(preds, target), top_k)[0]
 
 
 def retrieval_average_precision(preds: Tensor, target: Tensor, top_k: Optional[int] = None) -> Tensor:
     """Mean precision at every relevant document within the top k (``F/retrieval/average_precision.py``)."""
     if top_k is not None and not isinstance(top_k, int) and top_k <= 0:
         raise ValueError(f"Argument ``top_k`` has to be a positive integer or None, but got {top_k}.")
-    return _seg_average_precision(_one(preds, target), top_k)[0]
+    res = _kernel_one(preds, target, "map", top_k)
+    return res if res is not None else _seg_average_precision(_one(preds, target), top_k)[0]
 
 
 def retrieval_normalized_dcg(preds: Tensor, target: Tensor, top_k: Optional[int] = None) -> Tensor:
     """Tie-averaged normalised discounted cumulative gain (``F/retrieval/ndcg.py``)."""
     _check_top_k(top_k)
-    return _seg_ndcg(_one(preds, target, non_binary=True), top_k)[0]
+    res = _kernel_one(preds, target, "ndcg", top_k, non_binary=True)
+    return res if res is not None else _seg_ndcg(_one(preds, target, non_binary=True), top_k)[0]
 
 
 def retrieval_auroc(preds: Tensor, target: Tensor, top_k: Optional[int] = None,
                     max_fpr: Optional[float] = None) -> Tensor:
     """ROC AUC of the top-k documents (``F/retrieval/auroc.py``)."""
     _check_top_k(top_k)
+    if max_fpr is None:
+        res = _kernel_one(preds, target, "auroc", top_k)
+        if res is not None:
+            return res
     seg = _one(preds, target)
     if max_fpr is None:
         return _seg_auroc(seg, top_k)[0]

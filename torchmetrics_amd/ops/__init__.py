@@ -184,6 +184,65 @@ def histogram(x: Tensor, minlength: int) -> Tensor:
     return torch.bincount(x, minlength=minlength)
 
 
+# ------------------------------------------------------------------------------------- sorted curves / ranks
+CLF_T_BINARY = 0  # target[e] == pos_label, one segment
+CLF_T_OVR = 1  # target[e] == segment index (multiclass one-vs-rest columns)
+CLF_T_ELEM = 2  # target stored like the scores (multilabel columns, label-ranking rows)
+EMIT_CURVE = 1
+EMIT_RANKS = 2
+
+
+def clf_curve(scores: Tensor, target: Tensor, S: int, M: int, seg_stride: int, elem_stride: int, tmode: int,
+              pos_label: int = 1, ignore_index: Optional[int] = None, weights: Optional[Tensor] = None,
+              emit: int = 0) -> list:
+    """Segmented descending sort + tie-run scan over ``S`` segments of ``M`` scores (``csrc/sort/clf_curve.hip``).
+
+    Element ``e`` of segment ``s`` is ``scores[s * seg_stride + e * elem_stride]`` (element strides of ``scores``
+    itself).  Returns ``[stats [S, 8] fp64 = (P, N, auroc_area, ap_sum, coverage, 0, n_runs, 0), fps, tps, thr, ranks]``
+    (curve tensors ``[S, M]`` compacted per segment, present with ``emit & EMIT_CURVE``; ``ranks`` average 1-based
+    ranks by flat id ``s * M + e`` with ``emit & EMIT_RANKS``).
+    """
+    if scores.is_cuda:
+        w = None if weights is None else weights.to(torch.float64).contiguous()
+        return list(_ops().clf_curve(scores, target, w, S, M, seg_stride, elem_stride, tmode, pos_label,
+                                     0 if ignore_index is None else ignore_index, ignore_index is not None, emit))
+    return _cpu.clf_curve(scores, target, weights, S, M, seg_stride, elem_stride, tmode, pos_label, ignore_index,
+                          emit)
+
+
+RETRIEVAL_KIND = {name: i for i, name in enumerate(_cpu.RETRIEVAL_KINDS)}
+
+
+def retrieval_metric(preds: Tensor, target: Tensor, indexes: Tensor, kind: str, top_k: Optional[int] = None,
+                     adaptive_k: bool = False) -> list:
+    """Per-query retrieval metric for all queries at once (``csrc/sort/retrieval.hip``).
+
+    Returns ``[values fp64 [n], empty uint8 [n], n_queries int32 [1]]``; the first ``n_queries`` entries are the
+    queries in ascending id order.  ``empty`` marks queries without relevant documents (fall-out: without
+    non-relevant ones).  Nothing is read back to the host.
+    """
+    k = RETRIEVAL_KIND[kind]
+    tk = -1 if top_k is None else int(top_k)
+    if preds.is_cuda:
+        t = target if target.dtype != torch.bool else target.to(torch.uint8)
+        return list(_ops().retrieval_metric(preds.reshape(-1).contiguous(), t.reshape(-1).contiguous(),
+                                            indexes.reshape(-1).contiguous(), k, tk, adaptive_k))
+    return _cpu.retrieval_metric(preds.reshape(-1), target.reshape(-1), indexes.reshape(-1), k, tk, adaptive_k)
+
+
+def kendall_stats(x: Tensor, y: Tensor) -> Tensor:
+    """Per column of ``[n, k]`` inputs: ``[disc, tx, tx1, tx2, ty, ty1, ty2, txy, ux, uy]`` (fp64) -- discordant
+    pairs, tie terms of x / y (sum of t(t-1)/2, t(t-1)(t-2), t(t-1)(2t+5)), joint ties and distinct counts
+    (``csrc/sort/kendall.hip``: radix sorts + merge-path inversion count, O(n log n))."""
+    if x.is_cuda:
+        if y.dtype != x.dtype:
+            y = y.to(x.dtype)
+        if not x.is_floating_point():
+            x, y = x.double(), y.double()
+        return _ops().kendall_stats(x, y)
+    return _cpu.kendall_stats(x, y)
+
+
 class CalibrationWorkspace:
     """Per-metric device scratch of :func:`mc_calibration_update` (candidate rows + double-buffered decision word)."""
 

@@ -508,3 +508,128 @@ def nms(boxes: Tensor, scores: Tensor, iou_threshold: float, idxs: Optional[Tens
         keep.append(i)
         removed |= sup[i]
     return order[torch.tensor(keep, dtype=torch.long, device=boxes.device)]
+
+
+# ------------------------------------------------------------------------------------- sorted curves (clf_curve)
+def clf_curve(scores: Tensor, target: Tensor, weights: Optional[Tensor], S: int, M: int, seg_stride: int,
+              elem_stride: int, tmode: int, pos_label: int, ignore_index: Optional[int], emit: int):
+    """Host implementation of ``csrc/sort/clf_curve.hip`` (same outputs, same layout).
+
+    Returns ``[stats [S, 8] (P, N, area, ap, coverage, 0, nruns, 0), fps, tps, thr ([S, M], compacted per segment at
+    the run index; ``None`` unless ``emit & 1``), ranks ([S * M] average 1-based ranks by flat id; ``emit & 2``)]``.
+    """
+    f64 = torch.float64
+    sc = scores.as_strided((S, M), (seg_stride, elem_stride), scores.storage_offset()).to(f64)
+    if tmode == 2:
+        tg = target.as_strided((S, M), (seg_stride, elem_stride), target.storage_offset())
+    else:
+        tg = target.reshape(1, M).expand(S, M)
+    tg = tg.long()
+    valid = tg != ignore_index if ignore_index is not None else torch.ones_like(tg, dtype=torch.bool)
+    if tmode == 1:
+        pos = tg == torch.arange(S).unsqueeze(1)
+    else:
+        pos = tg == pos_label
+    pos = pos & valid
+    w = weights.to(f64).reshape(1, M).expand(S, M) if weights is not None else torch.ones(S, M, dtype=f64)
+    pw = torch.where(pos, w, torch.zeros_like(w))
+    nw = torch.where(valid & ~pos, w, torch.zeros_like(w))
+    # order: valid first, then descending score (NaN first), stable
+    canon = torch.where(torch.isnan(sc), torch.full_like(sc, float("inf")), sc)
+    _, o1 = torch.sort(canon, dim=1, descending=True, stable=True)
+    _, o2 = torch.sort((~valid).gather(1, o1).to(torch.int8), dim=1, stable=True)
+    order = o1.gather(1, o2)
+    s_sc, s_val = sc.gather(1, order), valid.gather(1, order)
+    s_pw, s_nw = pw.gather(1, order), nw.gather(1, order)
+    key = torch.where(torch.isnan(s_sc), torch.full_like(s_sc, float("inf")), s_sc)
+    nan = torch.isnan(s_sc)
+    same_prev = torch.zeros_like(s_val)
+    same_prev[:, 1:] = (key[:, 1:] == key[:, :-1]) & (nan[:, 1:] == nan[:, :-1])
+    start = s_val & ~same_prev
+    nxt_same = torch.zeros_like(s_val)
+    nxt_same[:, :-1] = same_prev[:, 1:] & s_val[:, 1:]
+    end = s_val & ~nxt_same
+    tps, fps = s_pw.cumsum(1), s_nw.cumsum(1)
+    idx = torch.arange(M).unsqueeze(0).expand(S, M)
+    sidx = torch.where(start, idx, torch.full_like(idx, -1)).cummax(1).values.clamp(min=0)
+    tp_b = tps.gather(1, sidx) - s_pw.gather(1, sidx)
+    fp_b = fps.gather(1, sidx) - s_nw.gather(1, sidx)
+    pos_r, neg_r = tps - tp_b, fps - fp_b
+    zero = torch.zeros_like(tps)
+    area = torch.where(end, neg_r * (tp_b + 0.5 * pos_r), zero).sum(1)
+    tot = tps + fps
+    ap = torch.where(end & (tot > 0), pos_r * tps / torch.where(tot > 0, tot, torch.ones_like(tot)), zero).sum(1)
+    cov = torch.where(end & (pos_r > 0), tot, zero).amax(1) if M else zero.sum(1)
+    stats = torch.zeros(S, 8, dtype=f64)
+    stats[:, 0], stats[:, 1], stats[:, 2], stats[:, 3], stats[:, 4] = pw.sum(1), nw.sum(1), area, ap, cov
+    stats[:, 6] = start.sum(1).to(f64)
+    out = [stats, None, None, None, None]
+    rid = start.long().cumsum(1) - 1
+    if emit & 1:
+        c_fps, c_tps, c_thr = (torch.zeros(S, M, dtype=f64) for _ in range(3))
+        seg = torch.arange(S).unsqueeze(1).expand(S, M)
+        c_fps[seg[end], rid[end]] = fps[end]
+        c_tps[seg[end], rid[end]] = tps[end]
+        c_thr[seg[end], rid[end]] = s_sc[end]
+        out[1:4] = [c_fps, c_tps, c_thr]
+    if emit & 2:
+        eidx = torch.where(end, idx, torch.full_like(idx, M)).flip(1).cummin(1).values.flip(1)
+        rank = 0.5 * (sidx.to(f64) + eidx.to(f64)) + 1.0
+        flat = torch.arange(S).unsqueeze(1) * M + order
+        ranks = torch.empty(S * M, dtype=f64)
+        ranks[flat.reshape(-1)] = rank.reshape(-1)
+        out[4] = ranks
+    return out
+
+
+RETRIEVAL_KINDS = ("map", "mrr", "precision", "recall", "fall_out", "hit_rate", "r_precision", "ndcg", "auroc")
+
+
+def retrieval_metric(preds: Tensor, target: Tensor, indexes: Tensor, kind: int, top_k: int, adaptive_k: bool):
+    """Host implementation of ``csrc/sort/retrieval.hip``: per-query values, empty flags, query count."""
+    from torchmetrics_amd.functional.retrieval import metrics as R
+    from torchmetrics_amd.functional.retrieval._segments import Segments
+
+    seg = Segments(preds, target, indexes)
+    k = None if top_k <= 0 else int(top_k)
+    name = RETRIEVAL_KINDS[kind]
+    fn = {
+        "map": lambda: R._seg_average_precision(seg, k),
+        "mrr": lambda: R._seg_reciprocal_rank(seg, k),
+        "precision": lambda: R._seg_precision(seg, k, adaptive_k),
+        "recall": lambda: R._seg_recall(seg, k),
+        "fall_out": lambda: R._seg_fall_out(seg, k),
+        "hit_rate": lambda: R._seg_hit_rate(seg, k),
+        "r_precision": lambda: R._seg_r_precision(seg),
+        "ndcg": lambda: R._seg_ndcg(seg, k),
+        "auroc": lambda: R._seg_auroc(seg, k),
+    }[name]
+    n = preds.numel()
+    vals = torch.zeros(n, dtype=torch.float64)
+    empty = torch.zeros(n, dtype=torch.uint8)
+    g = seg.num_groups
+    vals[:g] = torch.nan_to_num(fn().to(torch.float64), nan=0.0)
+    pos = (seg.target > 0).to(torch.long)
+    tot = seg.seg_sum(1 - pos) if name == "fall_out" else seg.seg_sum(pos)
+    empty[:g] = (tot == 0).to(torch.uint8)
+    return [vals, empty, torch.tensor([g], dtype=torch.int32)]
+
+
+def kendall_stats(x: Tensor, y: Tensor) -> Tensor:
+    """Host implementation of ``csrc/sort/kendall.hip`` (Knight's method in batched torch ops)."""
+    from torchmetrics_amd.functional.regression import correlation as C
+
+    _, disc = C._pair_counts(x, y)
+    tx, tx1, tx2 = C._tie_stats(x)
+    ty, ty1, ty2 = C._tie_stats(y)
+    n, k = x.shape
+    txy = torch.zeros(k, dtype=torch.float64)
+    ux = torch.zeros(k, dtype=torch.float64)
+    uy = torch.zeros(k, dtype=torch.float64)
+    for c in range(k):
+        _, cnt = torch.unique(torch.stack([x[:, c], y[:, c]], 1), dim=0, return_counts=True)
+        cnt = cnt.double()
+        txy[c] = (cnt * (cnt - 1) / 2).sum()
+        ux[c] = float(torch.unique(x[:, c]).numel())
+        uy[c] = float(torch.unique(y[:, c]).numel())
+    return torch.stack([disc.double(), tx, tx1, tx2, ty, ty1, ty2, txy, ux, uy], 1)

@@ -6,12 +6,13 @@ DDP sync gathers them).  ``compute`` evaluates every query in one segmented pass
 ``_metric`` hook still work through the per-query fallback loop.
 """
 from abc import ABC
-from typing import Any, Callable, List, Optional, Union
+from typing import Any, Callable, List, Optional, Tuple, Union
 
 import torch
 from torch import Tensor
 from typing_extensions import Literal
 
+from torchmetrics_amd import ops
 from torchmetrics_amd.functional.retrieval._segments import Segments
 from torchmetrics_amd.metric import Metric
 from torchmetrics_amd.utilities.checks import _check_retrieval_inputs
@@ -32,6 +33,29 @@ def _retrieval_aggregate(
     if aggregation == "max":
         return values.max() if dim is None else values.max(dim=dim).values
     return aggregation(values, dim=dim)
+
+
+def _aggregate_queries(vals: Tensor, empty: Tensor, nq: Tensor, action: str, aggregation, like: Tensor,
+                       error_msg: str) -> Tensor:
+    """Empty-query policy + aggregation of per-query values on the device (``mean``: no host read at all)."""
+    valid = torch.arange(vals.numel(), device=vals.device) < nq.to(vals.device)
+    empty = empty.bool() & valid
+    if action == "error" and bool(empty.any()):
+        raise ValueError(error_msg)
+    if action == "pos":
+        vals = torch.where(empty, torch.ones_like(vals), vals)
+    elif action == "neg":
+        vals = torch.where(empty, torch.zeros_like(vals), vals)
+    else:
+        valid = valid & ~empty
+    if aggregation == "mean":
+        cnt = valid.sum()
+        mean = torch.where(valid, vals, torch.zeros_like(vals)).sum() / cnt.clamp(min=1)
+        return torch.where(cnt > 0, mean, torch.zeros_like(mean)).to(like)
+    sel = vals[valid]
+    if sel.numel() == 0:
+        return torch.tensor(0.0).to(like)
+    return _retrieval_aggregate(sel.to(like), aggregation)
 
 
 class RetrievalMetric(Metric, ABC):
@@ -80,6 +104,10 @@ class RetrievalMetric(Metric, ABC):
         self.target.append(target)
 
     # -- hooks -------------------------------------------------------------------------------------------------
+    def _kernel_kind(self) -> Optional[Tuple[str, Optional[int], bool]]:
+        """``(kind, top_k, adaptive_k)`` of :func:`torchmetrics_amd.ops.retrieval_metric`, or ``None``."""
+        return None
+
     def _segment_metric(self, seg: Segments) -> Optional[Tensor]:
         """Per-query scores for all queries at once; ``None`` -> per-query ``_metric`` fallback."""
         return None
@@ -98,6 +126,11 @@ class RetrievalMetric(Metric, ABC):
     def compute(self) -> Tensor:
         preds = dim_zero_cat(self.preds)
         target = dim_zero_cat(self.target)
+        spec = self._kernel_kind()
+        if spec is not None and preds.is_cuda:
+            vals, empty, nq = ops.retrieval_metric(preds, target, dim_zero_cat(self.indexes), *spec)
+            return _aggregate_queries(vals, empty, nq, self.empty_target_action, self.aggregation, preds,
+                                      self._empty_error())
         seg = Segments(preds, target, dim_zero_cat(self.indexes))
         if seg.num_groups == 0:
             return torch.tensor(0.0).to(preds)

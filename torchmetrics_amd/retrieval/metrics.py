@@ -44,6 +44,9 @@ class RetrievalMAP(RetrievalMetric):
             raise ValueError(f"Argument ``top_k`` has to be a positive integer or None, but got {top_k}")
         self.top_k = top_k
 
+    def _kernel_kind(self):
+        return "map", self.top_k, False
+
     def _segment_metric(self, seg: Segments) -> Tensor:
         return _seg_average_precision(seg, self.top_k)
 
@@ -58,6 +61,9 @@ class RetrievalMRR(RetrievalMetric):
         if top_k is not None and not isinstance(top_k, int) and top_k <= 0:
             raise ValueError(f"Argument ``top_k`` has to be a positive integer or None, but got {top_k}")
         self.top_k = top_k
+
+    def _kernel_kind(self):
+        return "mrr", self.top_k, False
 
     def _segment_metric(self, seg: Segments) -> Tensor:
         return _seg_reciprocal_rank(seg, self.top_k)
@@ -77,6 +83,9 @@ class RetrievalPrecision(RetrievalMetric):
         self.top_k = top_k
         self.adaptive_k = adaptive_k
 
+    def _kernel_kind(self):
+        return "precision", self.top_k, self.adaptive_k
+
     def _segment_metric(self, seg: Segments) -> Tensor:
         return _seg_precision(seg, self.top_k, self.adaptive_k)
 
@@ -90,6 +99,9 @@ class RetrievalRecall(RetrievalMetric):
                          aggregation=aggregation, **kwargs)
         _check_top_k(top_k)
         self.top_k = top_k
+
+    def _kernel_kind(self):
+        return "recall", self.top_k, False
 
     def _segment_metric(self, seg: Segments) -> Tensor:
         return _seg_recall(seg, self.top_k)
@@ -113,6 +125,9 @@ class RetrievalFallOut(RetrievalMetric):
     def _empty_error(self) -> str:
         return "`compute` method was provided with a query with no negative target."
 
+    def _kernel_kind(self):
+        return "fall_out", self.top_k, False
+
     def _segment_metric(self, seg: Segments) -> Tensor:
         return _seg_fall_out(seg, self.top_k)
 
@@ -126,6 +141,9 @@ class RetrievalHitRate(RetrievalMetric):
                          aggregation=aggregation, **kwargs)
         _check_top_k(top_k)
         self.top_k = top_k
+
+    def _kernel_kind(self):
+        return "hit_rate", self.top_k, False
 
     def _segment_metric(self, seg: Segments) -> Tensor:
         return _seg_hit_rate(seg, self.top_k)
@@ -142,12 +160,18 @@ class RetrievalNormalizedDCG(RetrievalMetric):
         self.top_k = top_k
         self.allow_non_binary_target = True
 
+    def _kernel_kind(self):
+        return "ndcg", self.top_k, False
+
     def _segment_metric(self, seg: Segments) -> Tensor:
         return _seg_ndcg(seg, self.top_k)
 
 
 class RetrievalRPrecision(RetrievalMetric):
     """Precision at R, R = number of relevant documents of the query."""
+
+    def _kernel_kind(self):
+        return "r_precision", None, False
 
     def _segment_metric(self, seg: Segments) -> Tensor:
         return _seg_r_precision(seg)
@@ -166,6 +190,9 @@ class RetrievalAUROC(RetrievalMetric):
         if max_fpr is not None and not isinstance(max_fpr, float) and 0 < max_fpr <= 1:
             raise ValueError(f"Arguments `max_fpr` should be a float in range (0, 1], but got: {max_fpr}")
         self.max_fpr = max_fpr
+
+    def _kernel_kind(self):
+        return ("auroc", self.top_k, False) if self.max_fpr is None else None
 
     def _segment_metric(self, seg: Segments) -> Optional[Tensor]:
         return _seg_auroc(seg, self.top_k) if self.max_fpr is None else None

@@ -1,0 +1,426 @@
+// fp32 "NT" GEMM on the gfx950 matrix cores with fused metric epilogues: C[i, j] = sum_k X[i, k] * Y[j, k].
+//
+// Used by pairwise euclidean / cosine / linear (F/pairwise/{euclidean,cosine,linear}.py: fp64 GEMM + norm trick /
+// normalise + mm), KID's polynomial-kernel MMD sums (S/image/kid.py:33-66: three Gram matrices per subset, then
+// masked sums) and MiFID's memorisation distance (S/image/mifid.py:36-63: normalise, mm, row min).  Instead of a
+// library GEMM followed by elementwise/reduction passes over the [N, M] result, the epilogue consumes the
+// accumulator tile in registers:
+//
+//   * v_mfma_f32_32x32x2_f32 (exact fp32 products, k-ordered fma chain -- 64 FLOP/clk/SIMD, the fp32 peak);
+//     block 256 threads = 4 waves, block tile 128 x 128, wave tile 64 x 64 (2 x 2 MFMA tiles), k-step 32;
+//   * K is permuted per lane half (half h owns k in [16h, 16h+16) of each 32-chunk) so every operand fragment of a
+//     k-chunk is 16 contiguous floats: 4 x ds_read_b128 from LDS rows padded to 144 B (conflict-free);
+//   * global -> LDS staging is double buffered with the next chunk prefetched into registers during the MFMAs;
+//   * block ids are remapped so each XCD works through a contiguous band of row tiles (L2 reuse of the X band);
+//   * epilogues: STORE (scale), EUCLID (sqrt(|x|^2 + |y|^2 - 2 x.y) with an exact difference-form recompute when
+//     cancellation could cost more than ~1e-6 relative, zero_diagonal), COSINE (scaled by inverse norms),
+//     POLY_SUM (KID: (gamma x.y + c)^degree summed, diagonal optionally excluded, one fp64 partial per block),
+//     ROW_MIN (MiFID: min over j of 1 - |cos|, one partial per (row, column tile)), ROW_SUM (reduction='sum'/'mean').
+// Batched over blockIdx.z, with per-batch strides or per-batch row-index gathers (KID subsets are read straight from
+// the feature matrix through their index draws: the [subsets, m, D] gathered copies are never materialised).
+#include <cstdlib>
+
+#include "common/tm_common.h"
+
+namespace tm_amd {
+namespace {
+
+constexpr int kBM = 128, kBN = 128, kBK = 32, kNT = 256;
+constexpr int kRowF = 36;  // LDS row: 32 floats + 4 pad (144 B)
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+enum Epi : int { kStore = 0, kEuclid = 1, kCosine = 2, kPolySum = 3, kRowMin = 4, kRowSum = 5 };
+
+struct EpiParams {
+  const float* nx;  // |x_i|^2 (EUCLID) or 1/|x_i| (COSINE, ROW_MIN)
+  const float* ny;
+  float scale;      // STORE / COSINE scale, POLY gamma
+  float coef;       // POLY c
+  int degree;       // POLY degree
+  bool zero_diag;   // EUCLID: zero the diagonal; POLY_SUM: skip it
+  bool sqrt_out;    // EUCLID: sqrt (else squared distance)
+  float* out;       // [N, M] (STORE / EUCLID / COSINE) or partials
+  double* dpart;    // POLY_SUM partials [batch * blocks]
+  const int32_t* ix;  // optional row gather: X row i of batch b is X[ix[b * N + i]] (KID subsets); else batch-strided
+  const int32_t* iy;
+  int ldo;          // leading dim of out
+  int part_cols;    // ROW_MIN / ROW_SUM partial columns (= column tiles)
+};
+
+__device__ __forceinline__ float ipow(float b, int d) {
+  float r = 1.0f;
+  while (d) {
+    if (d & 1) r *= b;
+    b *= b;
+    d >>= 1;
+  }
+  return r;
+}
+
+template <int EPI, int STAGES>
+__global__ __launch_bounds__(kNT) void gemm_nt_kernel(const float* __restrict__ X, const float* __restrict__ Y, int N,
+                                                       int M, int D, long long bx, long long by, int tiles_m,
+                                                       EpiParams ep) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sa = smem;                          // [STAGES][kBM][kRowF]
+  float* sb = smem + STAGES * kBM * kRowF;   // [STAGES][kBN][kRowF]
+  const int batch = blockIdx.z;
+  const int32_t* gix = ep.ix ? ep.ix + (long long)batch * N : nullptr;
+  const int32_t* giy = ep.iy ? ep.iy + (long long)batch * M : nullptr;
+  if (!gix) X += batch * bx;
+  if (!giy) Y += batch * by;
+  auto xrow = [&](int i) -> const float* { return X + (long long)(gix ? gix[i] : i) * D; };
+  auto yrow = [&](int j) -> const float* { return Y + (long long)(giy ? giy[j] : j) * D; };
+  // XCD-aware tile order: hardware deals consecutive block ids round-robin over 8 XCDs; give each XCD a contiguous
+  // band of (row-major) tiles
+  const int tiles_n = (N + kBM - 1) / kBM;
+  const int total = tiles_n * tiles_m;
+  const int bid = blockIdx.x;
+  const int per = (total + 7) / 8;
+  const int tile = (bid % 8) * per + bid / 8;
+  if (tile >= total) return;
+  const int ti = tile / tiles_m, tj = tile - ti * tiles_m;
+  const int row0 = ti * kBM, col0 = tj * kBN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;  // wave tile origin inside the block tile
+  const int h = lane >> 5, r = lane & 31;
+
+  // staging: 128 rows x 8 float4 per operand = 1024 float4 = 4 per thread.  Row pointers (gathered or strided) and
+  // row validity are resolved ONCE per tile, so the k-loop's prefetch is 8 independent float4 loads with no index
+  // loads or waits in between.  D % 4 == 0 (host check): a float4 is either wholly inside K or wholly past it.
+  float4 ra[4], rb[4];
+  const float* pa_row[4];
+  const float* pb_row[4];
+  bool va_row[4], vb_row[4];
+  int c4_of[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = tid + q * kNT;
+    const int rr = idx >> 3;
+    c4_of[q] = (idx & 7) * 4;
+    const int gi = row0 + rr, gj = col0 + rr;
+    va_row[q] = gi < N;
+    vb_row[q] = gj < M;
+    pa_row[q] = va_row[q] ? xrow(gi) : X;
+    pb_row[q] = vb_row[q] ? yrow(gj) : Y;
+  }
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int gk = k0 + c4_of[q];
+      const bool kin = gk < D;
+      float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+      if (kin && va_row[q]) va = *reinterpret_cast<const float4*>(pa_row[q] + gk);
+      if (kin && vb_row[q]) vb = *reinterpret_cast<const float4*>(pb_row[q] + gk);
+      ra[q] = va;
+      rb[q] = vb;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = tid + q * kNT;
+      const int rr = idx >> 3, c4 = (idx & 7) * 4;
+      *reinterpret_cast<float4*>(sa + (buf * kBM + rr) * kRowF + c4) = ra[q];
+      *reinterpret_cast<float4*>(sb + (buf * kBN + rr) * kRowF + c4) = rb[q];
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  const int nk = (D + kBK - 1) / kBK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    const int buf = STAGES == 2 ? (kc & 1) : 0;
+    if (kc + 1 < nk) gload((kc + 1) * kBK);
+    // fragments: lane (r, h) -> rows wr + 32a + r, k in [16h, 16h + 16), read one float4 (4 k-steps) at a time and
+    // software-pipelined: the ds_reads of quarter q + 1 are in flight while the 16 MFMAs of quarter q issue
+    const float* pa0 = sa + (buf * kBM + wr + r) * kRowF + 16 * h;
+    const float* pb0 = sb + (buf * kBN + wc + r) * kRowF + 16 * h;
+    f32x4 ca[2], cb[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      ca[a] = *reinterpret_cast<const f32x4*>(pa0 + 32 * a * kRowF);
+      cb[a] = *reinterpret_cast<const f32x4*>(pb0 + 32 * a * kRowF);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 na[2], nb[2];
+      if (q < 3) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          na[a] = *reinterpret_cast<const f32x4*>(pa0 + 32 * a * kRowF + 4 * (q + 1));
+          nb[a] = *reinterpret_cast<const f32x4*>(pb0 + 32 * a * kRowF + 4 * (q + 1));
+        }
+      }
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[a][s4], cb[b][s4], acc[a][b], 0, 0, 0);
+      }
+      if (q < 3) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          ca[a] = na[a];
+          cb[a] = nb[a];
+        }
+      }
+    }
+    if (kc + 1 < nk) {
+      if constexpr (STAGES == 1) __syncthreads();  // every wave is done reading the single buffer
+      sstore(STAGES == 2 ? (buf ^ 1) : 0);
+      __syncthreads();
+    }
+  }
+
+  // ----------------------------------------------------------------------------------------------- epilogue
+  // acc[a][b][e]: row = wr + 32a + (e & 3) + 8 (e >> 2) + 4h, col = wc + 32b + r.  Reduction scratch reuses the
+  // (dynamic, 16-byte aligned) staging LDS after every wave is done with it.
+  __syncthreads();
+  if constexpr (EPI == kStore || EPI == kEuclid || EPI == kCosine) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int j = col0 + wc + 32 * b + r;
+        if (j >= M) continue;
+        float nyj = 0.f;
+        if constexpr (EPI != kStore) nyj = ep.ny[batch * (long long)M + j];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (i >= N) continue;
+          float v = acc[a][b][e];
+          if constexpr (EPI == kStore) {
+            v = (ep.zero_diag && i == j) ? 0.f : v * ep.scale;
+          } else if constexpr (EPI == kCosine) {
+            v = (ep.zero_diag && i == j) ? 0.f : v * ep.nx[batch * (long long)N + i] * nyj * ep.scale;
+          } else {
+            const float s2 = ep.nx[batch * (long long)N + i] + nyj;
+            float d2 = s2 - 2.0f * v;
+            if (d2 < s2 * (1.0f / 128.0f)) {
+              // cancellation guard: recompute this entry in the exact difference form
+              const float* xr = xrow(i);
+              const float* yr = yrow(j);
+              float t = 0.f;
+              for (int k = 0; k < D; ++k) {
+                const float d = xr[k] - yr[k];
+                t = fmaf(d, d, t);
+              }
+              d2 = t;
+            }
+            d2 = fmaxf(d2, 0.f);
+            if (ep.zero_diag && i == j) d2 = 0.f;
+            v = ep.sqrt_out ? sqrtf(d2) : d2;
+          }
+          ep.out[batch * (long long)N * ep.ldo + (long long)i * ep.ldo + j] = v;
+        }
+      }
+  } else if constexpr (EPI == kPolySum) {
+    double part = 0.0;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int j = col0 + wc + 32 * b + r;
+        if (j >= M) continue;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (i >= N || (ep.zero_diag && i == j)) continue;
+          part += static_cast<double>(ipow(fmaf(acc[a][b][e], ep.scale, ep.coef), ep.degree));
+        }
+      }
+    part = wave_sum(part);
+    double* red = reinterpret_cast<double*>(smem);
+    if (lane == 0) red[wave] = part;
+    __syncthreads();
+    if (tid == 0) ep.dpart[(long long)batch * gridDim.x + tile] = red[0] + red[1] + red[2] + red[3];
+  } else {
+    // ROW_MIN of (1 - cos) or ROW_SUM of the (scaled) dot: per row over this block's 128 columns
+    float* red = smem;  // [2][kBM]
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int il = wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int i = row0 + il;
+        float v = EPI == kRowMin ? 3.0e38f : 0.f;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int j = col0 + wc + 32 * b + r;
+          if (j >= M || i >= N) continue;
+          float x = acc[a][b][e];
+          if constexpr (EPI == kRowMin) {
+            x = 1.0f - fabsf(x * ep.nx[batch * (long long)N + i] * ep.ny[batch * (long long)M + j]);
+            v = fminf(v, x);
+          } else {
+            v += x * ep.scale;
+          }
+        }
+        // reduce over the 32 columns held by this lane half (lanes r = 0..31)
+#pragma unroll
+        for (int off = 16; off > 0; off >>= 1) {
+          const float o = __shfl_xor(v, off, 64);
+          v = EPI == kRowMin ? fminf(v, o) : v + o;
+        }
+        if (r == 0) red[(wave & 1) * kBM + il] = v;
+      }
+    }
+    __syncthreads();
+    if (tid < kBM) {
+      const int i = row0 + tid;
+      if (i < N) {
+        const float v = EPI == kRowMin ? fminf(red[tid], red[kBM + tid]) : red[tid] + red[kBM + tid];
+        ep.out[(long long)batch * N * ep.part_cols + (long long)i * ep.part_cols + tj] = v;
+      }
+    }
+  }
+}
+
+// LDS stages: double buffering (74 KB, 2 blocks/CU) pays for long K loops; for short ones the single buffer's higher
+// occupancy (37 KB, 3 blocks/CU: the next tile's loads overlap this tile's epilogue) wins (benchmarks/bench_gemm.py).
+// TM_AMD_GEMM_STAGES=1|2 overrides.
+int stages_choice(int D) {
+  static int forced = [] {
+    const char* e = std::getenv("TM_AMD_GEMM_STAGES");
+    return e ? (e[0] == '1' ? 1 : 2) : 0;
+  }();
+  return forced ? forced : (D >= 1024 ? 2 : 1);
+}
+
+template <int EPI>
+void launch(const at::Tensor& x, const at::Tensor& y, int batches, long long bx, long long by, int N, int M, int D,
+            const EpiParams& ep) {
+  const int tiles_n = (N + kBM - 1) / kBM, tiles_m = (M + kBN - 1) / kBN;
+  const int total = tiles_n * tiles_m;
+  const int per = (total + 7) / 8;
+  const dim3 grid(per * 8, 1, batches);
+  if (stages_choice(D) == 1) {
+    const size_t lds = (kBM + kBN) * kRowF * sizeof(float);
+    hipLaunchKernelGGL((gemm_nt_kernel<EPI, 1>), grid, dim3(kNT), lds, stream(), x.data_ptr<float>(),
+                       y.data_ptr<float>(), N, M, D, bx, by, tiles_m, ep);
+  } else {
+    const size_t lds = 2 * (kBM + kBN) * kRowF * sizeof(float);
+    hipLaunchKernelGGL((gemm_nt_kernel<EPI, 2>), grid, dim3(kNT), lds, stream(), x.data_ptr<float>(),
+                       y.data_ptr<float>(), N, M, D, bx, by, tiles_m, ep);
+  }
+}
+
+}  // namespace
+
+// x: [B, N, D] or [N, D]; y: [B, M, D] or [M, D] (fp32, contiguous).  kind: 0 store, 1 euclid, 2 cosine,
+// 3 poly-sum, 4 row-min(1 - cos), 5 row-sum.  aux_x / aux_y: per-row squared norms (euclid) or inverse norms.
+// Returns the output tensor ([B] dims only for batched operands): [B, N, M] fp32 (0-2), fp64 partials [B, blocks]
+// (3), fp32 partials [B, N, tiles_m] (4-5).
+at::Tensor gemm_nt(const at::Tensor& x, const at::Tensor& y, int64_t kind, const c10::optional<at::Tensor>& aux_x,
+                   const c10::optional<at::Tensor>& aux_y, double scale, double coef, int64_t degree, bool zero_diag,
+                   bool sqrt_out, const c10::optional<at::Tensor>& idx_x, const c10::optional<at::Tensor>& idx_y) {
+  TM_CHECK_CUDA(x);
+  TM_SAME_DEVICE(x, y);
+  TORCH_CHECK(x.scalar_type() == at::kFloat && y.scalar_type() == at::kFloat, "gemm_nt: fp32 operands");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous(), "gemm_nt: contiguous operands");
+  TORCH_CHECK(x.dim() == y.dim() && (x.dim() == 2 || x.dim() == 3), "gemm_nt: [N, D] / [B, N, D] operands");
+  const bool gathered = idx_x.has_value();
+  TORCH_CHECK(gathered == idx_y.has_value(), "gemm_nt: give both index sets or neither");
+  const bool batched = x.dim() == 3 || gathered;
+  TORCH_CHECK(!(gathered && x.dim() == 3), "gemm_nt: gathered rows come from 2-D operands");
+  const int B = gathered ? static_cast<int>(idx_x->size(0)) : (batched ? static_cast<int>(x.size(0)) : 1);
+  TORCH_CHECK(gathered || !batched || y.size(0) == B, "gemm_nt: batch mismatch");
+  int N = static_cast<int>(x.size(-2)), M = static_cast<int>(y.size(-2));
+  const int D = static_cast<int>(x.size(-1));
+  EpiParams ep{};
+  if (gathered) {
+    for (const auto* t : {&(*idx_x), &(*idx_y)}) {
+      TM_SAME_DEVICE(x, (*t));
+      TORCH_CHECK(t->scalar_type() == at::kInt && t->is_contiguous() && t->dim() == 2 && t->size(0) == B,
+                  "gemm_nt: index sets must be contiguous int32 [B, rows]");
+    }
+    // host-side bound check of the draws is the caller's contract (indices < rows of x / y); N, M = subset sizes
+    N = static_cast<int>(idx_x->size(1));
+    M = static_cast<int>(idx_y->size(1));
+    ep.ix = idx_x->data_ptr<int32_t>();
+    ep.iy = idx_y->data_ptr<int32_t>();
+  }
+  TORCH_CHECK(y.size(-1) == D, "gemm_nt: inner dimension mismatch");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
+              "gemm_nt: 16-byte aligned operands");
+  TORCH_CHECK(D % 4 == 0, "gemm_nt: D must be a multiple of 4 (float4 rows)");
+  TORCH_CHECK(static_cast<long long>(N) * M * B < (1LL << 40), "gemm_nt: output too large");
+  const int tiles_n = (N + kBM - 1) / kBM, tiles_m = (M + kBN - 1) / kBN;
+  const int blocks = ((tiles_n * tiles_m + 7) / 8) * 8;
+  auto f32 = x.options();
+  ep.scale = static_cast<float>(scale);
+  ep.coef = static_cast<float>(coef);
+  ep.degree = static_cast<int>(degree);
+  ep.zero_diag = zero_diag;
+  ep.sqrt_out = sqrt_out;
+  if (aux_x.has_value()) {
+    TM_SAME_DEVICE(x, (*aux_x));
+    TORCH_CHECK(aux_x->scalar_type() == at::kFloat && aux_x->numel() == static_cast<int64_t>(B) * N, "gemm_nt: aux_x");
+    ep.nx = aux_x->data_ptr<float>();
+  }
+  if (aux_y.has_value()) {
+    TM_SAME_DEVICE(x, (*aux_y));
+    TORCH_CHECK(aux_y->scalar_type() == at::kFloat && aux_y->numel() == static_cast<int64_t>(B) * M, "gemm_nt: aux_y");
+    ep.ny = aux_y->data_ptr<float>();
+  }
+  if ((kind == kEuclid || kind == kCosine || kind == kRowMin) && (!ep.nx || !ep.ny))
+    TORCH_CHECK(false, "gemm_nt: this epilogue needs aux_x and aux_y");
+  const long long bx = (batched && !gathered) ? static_cast<long long>(N) * D : 0;
+  const long long by = (batched && !gathered) ? static_cast<long long>(M) * D : 0;
+  at::Tensor out;
+  switch (kind) {
+    case kStore:
+    case kEuclid:
+    case kCosine:
+      out = batched ? at::empty({B, N, M}, f32) : at::empty({N, M}, f32);
+      ep.out = out.data_ptr<float>();
+      ep.ldo = M;
+      if (kind == kStore) launch<kStore>(x, y, B, bx, by, N, M, D, ep);
+      else if (kind == kEuclid) launch<kEuclid>(x, y, B, bx, by, N, M, D, ep);
+      else launch<kCosine>(x, y, B, bx, by, N, M, D, ep);
+      break;
+    case kPolySum:
+      out = batched ? at::zeros({B, blocks}, x.options().dtype(at::kDouble))
+                    : at::zeros({blocks}, x.options().dtype(at::kDouble));
+      ep.dpart = out.data_ptr<double>();
+      launch<kPolySum>(x, y, B, bx, by, N, M, D, ep);
+      break;
+    case kRowMin:
+    case kRowSum:
+      out = batched ? at::empty({B, N, tiles_m}, f32) : at::empty({N, tiles_m}, f32);
+      ep.out = out.data_ptr<float>();
+      ep.part_cols = tiles_m;
+      if (kind == kRowMin) launch<kRowMin>(x, y, B, bx, by, N, M, D, ep);
+      else launch<kRowSum>(x, y, B, bx, by, N, M, D, ep);
+      break;
+    default:
+      TORCH_CHECK(false, "gemm_nt: unknown epilogue ", kind);
+  }
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return out;
+}
+
+}  // namespace tm_amd
+
+TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def(
+      "gemm_nt(Tensor x, Tensor y, int kind, Tensor? aux_x, Tensor? aux_y, float scale, float coef, int degree, "
+      "bool zero_diag, bool sqrt_out, Tensor? idx_x=None, Tensor? idx_y=None) -> Tensor");
+}
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) { m.impl("gemm_nt", &tm_amd::gemm_nt); }

@@ -5,10 +5,10 @@
 // one argsort + curve + trapezoid per class).  Here every column of a [M, S] score matrix is one *segment* and all
 // segments are processed by the same few launches:
 //
-//   1. key build: one 64-bit radix key per element, [ segment | invalid | desc-score(32) | positive ] (packed path)
+//   1. key build: one radix key per element, [ segment | desc-score(32) ] (invalid -> sentinel) + a positive-flag byte
 //      -- the sort carries everything the scan needs, no payload and no gathers.  fp64 scores / sample weights use the
 //      payload path instead: (desc-score64 -> flat index) sort, then a stable (segment, invalid) sort.
-//   2. rocPRIM radix sort over exactly the key bits in use (34 + ceil(log2 S)).
+//   2. rocPRIM radix sort over exactly the key bits in use (32 + ceil(log2 S)).
 //   3. run_tile_aggregate / run_tile_scan / run_tile_epilogue: a tile-decomposed segmented scan whose element is the
 //      associative "tie-run" record {cum pos, cum neg, #run starts, cum (pos, neg) before the latest run start}.
 //      At every run end (last element of a group of equal scores) the epilogue knows the run's TP/FP before and after
@@ -35,16 +35,19 @@ constexpr int kTgtBinary = 0;      // target[e] == pos_label                    
 constexpr int kTgtOneVsRest = 1;   // target[e] == segment                            (multiclass columns)
 constexpr int kTgtElementwise = 2; // target at the score's own address == pos_label  (multilabel / rows)
 
+// C = int32_t for unit weights (exact counts, half the scan traffic of fp64), double for sample weights
+template <typename C>
 struct RunRec {
-  double p, n;    // inclusive positive / negative weight
-  double sp, sn;  // cumulative (p, n) just before the latest run start in range
-  int starts;     // number of run starts in range
-  int has;        // range contains a run start
+  C p, n;    // inclusive positive / negative weight
+  C sp, sn;  // cumulative (p, n) just before the latest run start in range
+  int starts;  // number of run starts in range
+  int has;     // range contains a run start
 };
 
 struct RunOp {
-  __device__ __forceinline__ RunRec operator()(const RunRec& a, const RunRec& b) const {
-    RunRec r;
+  template <typename C>
+  __device__ __forceinline__ RunRec<C> operator()(const RunRec<C>& a, const RunRec<C>& b) const {
+    RunRec<C> r;
     r.p = a.p + b.p;
     r.n = a.n + b.n;
     r.starts = a.starts + b.starts;
@@ -61,29 +64,42 @@ struct RunOp {
   }
 };
 
-__device__ __forceinline__ RunRec run_identity() { return RunRec{0.0, 0.0, 0.0, 0.0, 0, 0}; }
+template <typename C>
+__device__ __forceinline__ RunRec<C> run_identity() {
+  return RunRec<C>{C(0), C(0), C(0), C(0), 0, 0};
+}
 
+template <typename C>
 struct Elem {
   uint64_t rk;  // run key: equal rk <=> same score (compared inside one segment only)
-  double pw, nw;
+  C pw, nw;
   bool valid;
 };
 
-// Packed path: everything is in the sorted key.
-struct PackedLoader {
-  const uint64_t* keys;
-  __device__ __forceinline__ Elem load(int64_t gi) const {
-    const uint64_t k = keys[gi];
-    Elem e;
-    e.valid = ((k >> 33) & 1ULL) == 0ULL;
-    const bool pos = (k & 1ULL) != 0ULL;
-    e.rk = (k >> 1) & 0xffffffffULL;
-    e.pw = (e.valid && pos) ? 1.0 : 0.0;
-    e.nw = (e.valid && !pos) ? 1.0 : 0.0;
+// Packed path: the sorted key is [segment | desc-score32] (32-bit key when S == 1) with an invalid element's score
+// replaced by the 0xffffffff sentinel (sorts last in its segment; no real score maps to it: the only float whose
+// key it would be is a non-canonical NaN), and the sort's 1-byte value carries the positive flag.  Tiles are staged
+// through LDS with coalesced loads.
+template <typename K>
+struct KV8Loader {
+  static constexpr bool kStaged = true;
+  using key_type = K;
+  using count_t = int32_t;
+  const K* keys;
+  const uint8_t* flags;
+  __device__ __forceinline__ Elem<count_t> make(K k, uint8_t f) const {
+    Elem<count_t> e;
+    const uint32_t lo = static_cast<uint32_t>(k & 0xffffffffULL);
+    e.valid = lo != 0xffffffffu && !(f & 0x80);
+    e.rk = lo;
+    const bool pos = (f & 1) != 0;
+    e.pw = (e.valid && pos) ? 1 : 0;
+    e.nw = (e.valid && !pos) ? 1 : 0;
     return e;
   }
+  __device__ __forceinline__ Elem<count_t> load(int64_t gi) const { return make(keys[gi], flags[gi]); }
   __device__ __forceinline__ double threshold(int64_t gi) const {
-    return static_cast<double>(desc_key32_decode(static_cast<uint32_t>((keys[gi] >> 1) & 0xffffffffULL)));
+    return static_cast<double>(desc_key32_decode(static_cast<uint32_t>(keys[gi] & 0xffffffffULL)));
   }
   __device__ __forceinline__ int64_t origin(int64_t) const { return -1; }
 };
@@ -92,9 +108,12 @@ struct PackedLoader {
 //   kKeyed: non-fp64 scores -- the sorted 64-bit key [segment | invalid | desc-score32] gives run key and validity;
 //           otherwise (fp64) both come from gathers of the original score / target.
 //   kNeedPN: positive / negative weights are needed (curves, AUROC); ranks-only callers skip the target gathers.
-template <typename scalar_t, typename target_t, bool kKeyed, bool kNeedPN>
+template <typename scalar_t, typename target_t, bool kKeyed, bool kNeedPN, typename KT = uint64_t>
 struct PayloadLoader {
-  const uint64_t* keys;  // kKeyed only
+  static constexpr bool kStaged = false;
+  using key_type = KT;
+  using count_t = double;
+  const KT* keys;  // kKeyed only: [segment | invalid | desc32] (64-bit) or desc32 alone (one segment, no ignore)
   const int32_t* vals;
   const scalar_t* scores;
   const target_t* target;
@@ -109,11 +128,11 @@ struct PayloadLoader {
     s = divM.div(static_cast<uint32_t>(v));
     e = v - s * M;
   }
-  __device__ __forceinline__ Elem load(int64_t gi) const {
+  __device__ __forceinline__ Elem<double> load(int64_t gi) const {
     const int64_t v = vals[gi];
     int64_t s, e;
     se(v, s, e);
-    Elem r;
+    Elem<double> r;
     bool valid = true;
     int64_t t = 0;
     if (kNeedPN || !kKeyed)
@@ -121,7 +140,7 @@ struct PayloadLoader {
     if constexpr (kKeyed) {
       const uint64_t k = keys[gi];
       r.rk = k & 0xffffffffULL;
-      valid = ((k >> 32) & 1ULL) == 0ULL;
+      if constexpr (sizeof(KT) == 8) valid = ((k >> 32) & 1ULL) == 0ULL;
     } else {
       r.rk = desc_key64(static_cast<double>(scores[s * seg_stride + e * elem_stride]));
       valid = !(has_ignore && t == ignore_index);
@@ -176,8 +195,8 @@ struct Layout {
 template <typename scalar_t, typename target_t>
 __global__ void build_packed_keys_kernel(const scalar_t* __restrict__ scores, const target_t* __restrict__ target,
                                          int64_t total, Layout lay, int tmode, int64_t pos_label, int64_t ignore_index,
-                                         bool has_ignore, bool with_pos, uint64_t* __restrict__ keys,
-                                         int32_t* __restrict__ vals, int64_t M) {
+                                         bool has_ignore, uint64_t* __restrict__ keys, int32_t* __restrict__ vals,
+                                         int64_t M) {
   for (int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; a < total; a += (int64_t)gridDim.x * blockDim.x) {
     int64_t s, e;
     lay.se(static_cast<uint32_t>(a), s, e);
@@ -185,14 +204,36 @@ __global__ void build_packed_keys_kernel(const scalar_t* __restrict__ scores, co
     const int64_t t = static_cast<int64_t>(tmode == kTgtElementwise ? target[a] : target[e]);
     const bool invalid = has_ignore && t == ignore_index;
     const uint64_t sk = static_cast<uint64_t>(desc_key32(x));
-    if (with_pos) {
-      const bool pos = !invalid && (tmode == kTgtOneVsRest ? (t == s) : (t == pos_label));
-      keys[a] = (static_cast<uint64_t>(s) << 34) | (static_cast<uint64_t>(invalid) << 33) | (sk << 1) |
-                static_cast<uint64_t>(pos);
-    } else {
-      keys[a] = (static_cast<uint64_t>(s) << 33) | (static_cast<uint64_t>(invalid) << 32) | sk;
-      vals[a] = static_cast<int32_t>(s * M + e);
-    }
+    keys[a] = (static_cast<uint64_t>(s) << 33) | (static_cast<uint64_t>(invalid) << 32) | sk;
+    vals[a] = static_cast<int32_t>(s * M + e);
+  }
+}
+
+// packed path keys: [segment | desc-score32 or sentinel] + positive flag byte
+template <typename scalar_t, typename target_t, typename K>
+__global__ void build_kv8_kernel(const scalar_t* __restrict__ scores, const target_t* __restrict__ target,
+                                 int64_t total, Layout lay, int tmode, int64_t pos_label, int64_t ignore_index,
+                                 bool has_ignore, K* __restrict__ keys, uint8_t* __restrict__ flags) {
+  for (int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; a < total; a += (int64_t)gridDim.x * blockDim.x) {
+    int64_t s, e;
+    lay.se(static_cast<uint32_t>(a), s, e);
+    const int64_t t = static_cast<int64_t>(tmode == kTgtElementwise ? target[a] : target[e]);
+    const bool invalid = has_ignore && t == ignore_index;
+    const bool pos = !invalid && (tmode == kTgtOneVsRest ? (t == s) : (t == pos_label));
+    const uint32_t sk = invalid ? 0xffffffffu : desc_key32(to_f32(scores[a]));
+    if constexpr (sizeof(K) == 8) keys[a] = (static_cast<uint64_t>(s) << 32) | sk;
+    else keys[a] = sk;
+    flags[a] = pos ? 1 : 0;
+  }
+}
+
+// one segment, 32-bit scores: desc-score32 keys, element id values
+template <typename scalar_t>
+__global__ void build_score_keys32_kernel(const scalar_t* __restrict__ scores, int64_t total, uint32_t* __restrict__ keys,
+                                          int32_t* __restrict__ vals) {
+  for (int64_t a = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; a < total; a += (int64_t)gridDim.x * blockDim.x) {
+    keys[a] = desc_key32(to_f32(scores[a]));
+    vals[a] = static_cast<int32_t>(a);
   }
 }
 
@@ -226,67 +267,108 @@ __global__ void build_segment_keys_kernel(const int32_t* __restrict__ vals, cons
 // ----------------------------------------------------------------------------------------------- tile engine
 // One thread owns IT consecutive elements of a tile of NT * IT; grid = (tiles per segment, S).
 template <int NT, int IT, class L>
-__device__ __forceinline__ void load_tile(const L& ld, int64_t seg_base, int64_t M, int64_t e0, Elem (&el)[IT + 2]) {
+__device__ __forceinline__ void load_tile(const L& ld, int64_t seg_base, int64_t M, int64_t tile_e0,
+                                          Elem<typename L::count_t> (&el)[IT + 2]) {
+  const int64_t e0 = tile_e0 + static_cast<int64_t>(threadIdx.x) * IT;
+  if constexpr (L::kStaged) {
+    // coalesced cooperative load of the tile (+1 halo element each side) into LDS, padded 1 per 16 so the
+    // thread-contiguous reads below do not all fall into one bank
+    using K = typename L::key_type;
+    constexpr int T = NT * IT;
+    constexpr int P = T + 2 + (T + 2) / 16 + 1;
+    __shared__ K sk[P];
+    __shared__ uint8_t sf[P];
+    for (int j = threadIdx.x; j < T + 2; j += NT) {
+      const int64_t e = tile_e0 - 1 + j;
+      K k = 0;
+      uint8_t f = 0x80;
+      if (e >= 0 && e < M) {
+        k = ld.keys[seg_base + e];
+        f = ld.flags[seg_base + e];
+      }
+      sk[j + (j >> 4)] = k;
+      sf[j + (j >> 4)] = f;
+    }
+    __syncthreads();
 #pragma unroll
-  for (int j = 0; j < IT + 2; ++j) {
-    const int64_t e = e0 - 1 + j;
-    if (e >= 0 && e < M) {
-      el[j] = ld.load(seg_base + e);
-    } else {
-      el[j].valid = false;
-      el[j].rk = 0;
-      el[j].pw = el[j].nw = 0.0;
+    for (int j = 0; j < IT + 2; ++j) {
+      const int l = threadIdx.x * IT + j;
+      el[j] = ld.make(sk[l + (l >> 4)], sf[l + (l >> 4)]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < IT + 2; ++j) {
+      const int64_t e = e0 - 1 + j;
+      if (e >= 0 && e < M) {
+        el[j] = ld.load(seg_base + e);
+      } else {
+        el[j].valid = false;
+        el[j].rk = 0;
+        el[j].pw = el[j].nw = 0;
+      }
     }
   }
 }
 
-template <int IT>
-__device__ __forceinline__ RunRec item_rec(const Elem (&el)[IT + 2], int j, int64_t e) {
-  const Elem& x = el[j + 1];
+template <int IT, typename C>
+__device__ __forceinline__ RunRec<C> item_rec(const Elem<C> (&el)[IT + 2], int j, int64_t e) {
+  const Elem<C>& x = el[j + 1];
   const bool start = x.valid && (e == 0 || !el[j].valid || el[j].rk != x.rk);
-  RunRec r;
+  RunRec<C> r;
   r.p = x.pw;
   r.n = x.nw;
-  r.sp = 0.0;
-  r.sn = 0.0;
+  r.sp = C(0);
+  r.sn = C(0);
   r.starts = start ? 1 : 0;
   r.has = start ? 1 : 0;
   return r;
 }
 
 template <int NT, int IT, class L>
-__global__ __launch_bounds__(NT) void run_tile_aggregate_kernel(L ld, int64_t M, int tiles, RunRec* __restrict__ agg) {
-  __shared__ RunRec lds[NT / kWave];
+__global__ __launch_bounds__(NT) void run_tile_aggregate_kernel(L ld, int64_t M, int tiles,
+                                                                RunRec<typename L::count_t>* __restrict__ agg) {
+  using C = typename L::count_t;
+  __shared__ RunRec<C> lds[NT / kWave];
   const int64_t s = blockIdx.x / tiles;
   const int t = static_cast<int>(blockIdx.x - s * tiles);
   const int64_t e0 = static_cast<int64_t>(t) * NT * IT + static_cast<int64_t>(threadIdx.x) * IT;
-  Elem el[IT + 2];
-  load_tile<NT, IT>(ld, s * M, M, e0, el);
+  Elem<C> el[IT + 2];
+  load_tile<NT, IT>(ld, s * M, M, static_cast<int64_t>(t) * NT * IT, el);
   RunOp op;
-  RunRec acc = run_identity();
+  RunRec<C> acc = run_identity<C>();
 #pragma unroll
   for (int j = 0; j < IT; ++j) {
     const int64_t e = e0 + j;
     if (e < M) acc = op(acc, item_rec<IT>(el, j, e));
   }
-  RunRec excl, total;
-  sortscan::block_inclusive_scan<NT / kWave>(acc, op, run_identity(), lds, excl, total);
+  RunRec<C> excl, total;
+  sortscan::block_inclusive_scan<NT / kWave>(acc, op, run_identity<C>(), lds, excl, total);
   if (threadIdx.x == 0) agg[s * tiles + t] = total;
 }
 
-// Per segment: exclusive prefix of the tile aggregates (written over agg) and the segment total.
-template <int NT>
-__global__ __launch_bounds__(NT) void run_tile_scan_kernel(RunRec* __restrict__ agg, int tiles, RunRec* __restrict__ seg_total) {
-  __shared__ RunRec lds[NT / kWave];
+// Per segment: exclusive prefix of the tile aggregates (written over agg) and the segment total.  Each thread scans
+// TPT consecutive tiles sequentially, so one block scan covers NT * TPT tiles (4096 at 256 x 16).
+template <int NT, int TPT, typename C>
+__global__ __launch_bounds__(NT) void run_tile_scan_kernel(RunRec<C>* __restrict__ agg, int tiles,
+                                                           RunRec<C>* __restrict__ seg_total) {
+  __shared__ RunRec<C> lds[NT / kWave];
   const int64_t s = blockIdx.x;
   RunOp op;
-  RunRec carry = run_identity();
-  for (int base = 0; base < tiles; base += NT) {
-    const int t = base + threadIdx.x;
-    const RunRec v = t < tiles ? agg[s * tiles + t] : run_identity();
-    RunRec excl, total;
-    sortscan::block_inclusive_scan<NT / kWave>(v, op, run_identity(), lds, excl, total);
-    if (t < tiles) agg[s * tiles + t] = op(carry, excl);
+  RunRec<C> carry = run_identity<C>();
+  for (int base = 0; base < tiles; base += NT * TPT) {
+    const int t0 = base + threadIdx.x * TPT;
+    RunRec<C> acc = run_identity<C>();
+    for (int j = 0; j < TPT; ++j)
+      if (t0 + j < tiles) acc = op(acc, agg[s * tiles + t0 + j]);
+    RunRec<C> excl, total;
+    sortscan::block_inclusive_scan<NT / kWave>(acc, op, run_identity<C>(), lds, excl, total);
+    RunRec<C> run = op(carry, excl);
+    for (int j = 0; j < TPT; ++j) {
+      if (t0 + j >= tiles) break;
+      const RunRec<C> v = agg[s * tiles + t0 + j];
+      agg[s * tiles + t0 + j] = run;
+      run = op(run, v);
+    }
     carry = op(carry, total);
   }
   if (threadIdx.x == 0) seg_total[s] = carry;
@@ -296,46 +378,46 @@ constexpr int kEmitCurve = 1;
 constexpr int kEmitRanks = 2;
 
 template <int NT, int IT, class L>
-__global__ __launch_bounds__(NT) void run_tile_epilogue_kernel(L ld, int64_t M, int tiles, const RunRec* __restrict__ prefix,
+__global__ __launch_bounds__(NT) void run_tile_epilogue_kernel(L ld, int64_t M, int tiles,
+                                                               const RunRec<typename L::count_t>* __restrict__ prefix,
                                                                Partial* __restrict__ part, int emit,
                                                                double* __restrict__ c_fps, double* __restrict__ c_tps,
                                                                double* __restrict__ c_thr, int32_t* __restrict__ run_of,
                                                                int32_t* __restrict__ run_end) {
-  __shared__ RunRec lds[NT / kWave];
+  using C = typename L::count_t;
+  __shared__ RunRec<C> lds[NT / kWave];
   __shared__ double red[4][NT / kWave];
   const int64_t s = blockIdx.x / tiles;
   const int t = static_cast<int>(blockIdx.x - s * tiles);
   const int64_t e0 = static_cast<int64_t>(t) * NT * IT + static_cast<int64_t>(threadIdx.x) * IT;
-  Elem el[IT + 2];
-  load_tile<NT, IT>(ld, s * M, M, e0, el);
+  Elem<C> el[IT + 2];
+  load_tile<NT, IT>(ld, s * M, M, static_cast<int64_t>(t) * NT * IT, el);
   RunOp op;
-  RunRec recs[IT];
-  RunRec acc = run_identity();
+  RunRec<C> acc = run_identity<C>();
 #pragma unroll
   for (int j = 0; j < IT; ++j) {
     const int64_t e = e0 + j;
-    recs[j] = e < M ? item_rec<IT>(el, j, e) : run_identity();
-    acc = op(acc, recs[j]);
+    if (e < M) acc = op(acc, item_rec<IT>(el, j, e));
   }
-  RunRec excl, total;
-  sortscan::block_inclusive_scan<NT / kWave>(acc, op, run_identity(), lds, excl, total);
-  RunRec run = op(prefix[s * tiles + t], excl);
+  RunRec<C> excl, total;
+  sortscan::block_inclusive_scan<NT / kWave>(acc, op, run_identity<C>(), lds, excl, total);
+  RunRec<C> run = op(prefix[s * tiles + t], excl);
   double area = 0.0, ap = 0.0, cov = 0.0;
 #pragma unroll
   for (int j = 0; j < IT; ++j) {
     const int64_t e = e0 + j;
     if (e >= M) break;
-    run = op(run, recs[j]);
-    const Elem& x = el[j + 1];
-    const Elem& nx = el[j + 2];
+    run = op(run, item_rec<IT>(el, j, e));
+    const Elem<C>& x = el[j + 1];
+    const Elem<C>& nx = el[j + 2];
     if (!x.valid) continue;
     const int rid = run.starts - 1;
     if (emit & kEmitRanks) run_of[s * M + e] = rid;
     const bool end = (e == M - 1) || !nx.valid || nx.rk != x.rk;
     if (!end) continue;
-    const double P = run.p, N = run.n;
-    const double pos_r = P - run.sp, neg_r = N - run.sn;
-    area += neg_r * (run.sp + 0.5 * pos_r);
+    const double P = static_cast<double>(run.p), N = static_cast<double>(run.n);
+    const double pos_r = static_cast<double>(run.p - run.sp), neg_r = static_cast<double>(run.n - run.sn);
+    area += neg_r * (static_cast<double>(run.sp) + 0.5 * pos_r);
     if (P + N > 0.0) ap += pos_r * (P / (P + N));
     if (pos_r > 0.0) cov = fmax(cov, P + N);
     if (emit & kEmitCurve) {
@@ -368,7 +450,9 @@ __global__ __launch_bounds__(NT) void run_tile_epilogue_kernel(L ld, int64_t M, 
 }
 
 // stats[s] = {P, N, area, ap, coverage, 0, nruns, 0}
-__global__ __launch_bounds__(256) void run_finalize_kernel(const Partial* __restrict__ part, const RunRec* __restrict__ seg_total,
+template <typename C>
+__global__ __launch_bounds__(256) void run_finalize_kernel(const Partial* __restrict__ part,
+                                                           const RunRec<C>* __restrict__ seg_total,
                                                            int tiles, double* __restrict__ stats) {
   __shared__ double red[3][256 / kWave];
   const int64_t s = blockIdx.x;
@@ -397,10 +481,10 @@ __global__ __launch_bounds__(256) void run_finalize_kernel(const Partial* __rest
       B += red[1][w];
       Cv = fmax(Cv, red[2][w]);
     }
-    const RunRec tot = seg_total[s];
+    const RunRec<C> tot = seg_total[s];
     double* o = stats + s * kStatCols;
-    o[0] = tot.p;
-    o[1] = tot.n;
+    o[0] = static_cast<double>(tot.p);
+    o[1] = static_cast<double>(tot.n);
     o[2] = A;
     o[3] = B;
     o[4] = Cv;
@@ -430,19 +514,24 @@ void run_engine(const L& ld, int64_t S, int64_t M, int emit, const at::Tensor& s
   constexpr int64_t kTile = static_cast<int64_t>(NT) * IT;
   const int tiles = static_cast<int>((M + kTile - 1) / kTile);
   auto opts = at::TensorOptions().dtype(at::kByte).device(dev);
-  auto agg_t = at::empty({S * tiles * static_cast<int64_t>(sizeof(RunRec))}, opts);
-  auto tot_t = at::empty({S * static_cast<int64_t>(sizeof(RunRec))}, opts);
+  using C = typename L::count_t;
+  using RR = RunRec<C>;
+  auto agg_t = at::empty({S * tiles * static_cast<int64_t>(sizeof(RR))}, opts);
+  auto tot_t = at::empty({S * static_cast<int64_t>(sizeof(RR))}, opts);
   auto part_t = at::empty({S * tiles * static_cast<int64_t>(sizeof(Partial))}, opts);
-  auto* agg = reinterpret_cast<RunRec*>(agg_t.data_ptr());
-  auto* tot = reinterpret_cast<RunRec*>(tot_t.data_ptr());
+  auto* agg = reinterpret_cast<RR*>(agg_t.data_ptr());
+  auto* tot = reinterpret_cast<RR*>(tot_t.data_ptr());
   auto* part = reinterpret_cast<Partial*>(part_t.data_ptr());
   TORCH_CHECK(S * tiles < (1LL << 31), "clf_curve: too many segments / tiles");
   const dim3 grid(static_cast<unsigned>(S * tiles));  // block b -> (segment b / tiles, tile b % tiles)
   hipLaunchKernelGGL((run_tile_aggregate_kernel<NT, IT, L>), grid, dim3(NT), 0, st, ld, M, tiles, agg);
-  hipLaunchKernelGGL((run_tile_scan_kernel<256>), dim3(S), dim3(256), 0, st, agg, tiles, tot);
+  if (tiles > 256)
+    hipLaunchKernelGGL((run_tile_scan_kernel<256, 16, C>), dim3(S), dim3(256), 0, st, agg, tiles, tot);
+  else
+    hipLaunchKernelGGL((run_tile_scan_kernel<64, 4, C>), dim3(S), dim3(64), 0, st, agg, tiles, tot);
   hipLaunchKernelGGL((run_tile_epilogue_kernel<NT, IT, L>), grid, dim3(NT), 0, st, ld, M, tiles, agg, part, emit, fps,
                      tps, thr, run_of, run_end);
-  hipLaunchKernelGGL(run_finalize_kernel, dim3(S), dim3(256), 0, st, part, tot, tiles, stats.data_ptr<double>());
+  hipLaunchKernelGGL(run_finalize_kernel<C>, dim3(S), dim3(256), 0, st, part, tot, tiles, stats.data_ptr<double>());
 }
 
 template <class L>
@@ -516,12 +605,26 @@ std::vector<at::Tensor> clf_curve(const at::Tensor& scores, const at::Tensor& ta
       auto* a = reinterpret_cast<uint64_t*>(k1.data_ptr());
       auto* b = reinterpret_cast<uint64_t*>(k2.data_ptr());
       if (!payload) {
-        TORCH_CHECK(S < (1LL << 29), "clf_curve: too many segments for packed keys");
-        hipLaunchKernelGGL((build_packed_keys_kernel<scalar_t, target_t>), dim3(grid), dim3(256), 0, st, sc, tg, n,
-                           lay, static_cast<int>(tmode), pos_label, ignore_index, has_ignore, true, a,
-                           static_cast<int32_t*>(nullptr), M);
-        sortscan::sort_keys<uint64_t>(a, b, n, 0, 34 + sortscan::ceil_log2(S), dev, st);
-        run_engine_auto(PackedLoader{b}, S, M, static_cast<int>(emit), stats, fp, tp, th, ro, re, dev, st);
+        TORCH_CHECK(S < (1LL << 31), "clf_curve: too many segments for packed keys");
+        auto f1 = at::empty({n}, at::TensorOptions().dtype(at::kByte).device(dev));
+        auto f2 = at::empty({n}, at::TensorOptions().dtype(at::kByte).device(dev));
+        auto* fa = f1.data_ptr<uint8_t>();
+        auto* fb = f2.data_ptr<uint8_t>();
+        if (S == 1) {
+          auto* a32 = reinterpret_cast<uint32_t*>(a);
+          auto* b32 = reinterpret_cast<uint32_t*>(b);
+          hipLaunchKernelGGL((build_kv8_kernel<scalar_t, target_t, uint32_t>), dim3(grid), dim3(256), 0, st, sc, tg,
+                             n, lay, static_cast<int>(tmode), pos_label, ignore_index, has_ignore, a32, fa);
+          sortscan::sort_pairs<uint32_t, uint8_t>(a32, b32, fa, fb, n, 0, 32, dev, st);
+          run_engine_auto(KV8Loader<uint32_t>{b32, fb}, S, M, static_cast<int>(emit), stats, fp, tp, th, ro, re, dev,
+                          st);
+        } else {
+          hipLaunchKernelGGL((build_kv8_kernel<scalar_t, target_t, uint64_t>), dim3(grid), dim3(256), 0, st, sc, tg,
+                             n, lay, static_cast<int>(tmode), pos_label, ignore_index, has_ignore, a, fa);
+          sortscan::sort_pairs<uint64_t, uint8_t>(a, b, fa, fb, n, 0, 32 + sortscan::ceil_log2(S), dev, st);
+          run_engine_auto(KV8Loader<uint64_t>{b, fb}, S, M, static_cast<int>(emit), stats, fp, tp, th, ro, re, dev,
+                          st);
+        }
         return;
       }
       auto v1 = at::empty({n}, i32), v2 = at::empty({n}, i32);
@@ -535,10 +638,26 @@ std::vector<at::Tensor> clf_curve(const at::Tensor& scores, const at::Tensor& ta
                              ro, re, ranks.data_ptr<double>());
       };
       if constexpr (!std::is_same<scalar_t, double>::value) {
+        if (S == 1 && !has_ignore && !want_curve && !wp) {
+          // ranks of one column: 32-bit desc-score keys carrying the element id (4 radix passes)
+          auto* a32 = reinterpret_cast<uint32_t*>(a);
+          auto* b32 = reinterpret_cast<uint32_t*>(b);
+          hipLaunchKernelGGL((build_score_keys32_kernel<scalar_t>), dim3(grid), dim3(256), 0, st, sc, n, a32, va);
+          sortscan::sort_pairs<uint32_t, int32_t>(a32, b32, va, vb, n, 0, 32, dev, st);
+          if (want_ranks)
+            finish(PayloadLoader<scalar_t, target_t, true, false, uint32_t>{b32, vb, sc, tg, wp, divM, M, seg_stride,
+                                                                            elem_stride, static_cast<int>(tmode),
+                                                                            pos_label, ignore_index, has_ignore});
+          else
+            finish(PayloadLoader<scalar_t, target_t, true, true, uint32_t>{b32, vb, sc, tg, wp, divM, M, seg_stride,
+                                                                           elem_stride, static_cast<int>(tmode),
+                                                                           pos_label, ignore_index, has_ignore});
+          return;
+        }
         // one sort: [segment | invalid | desc-score32] keys carrying the flat id
         TORCH_CHECK(S < (1LL << 30), "clf_curve: too many segments");
         hipLaunchKernelGGL((build_packed_keys_kernel<scalar_t, target_t>), dim3(grid), dim3(256), 0, st, sc, tg, n,
-                           lay, static_cast<int>(tmode), pos_label, ignore_index, has_ignore, false, a, va, M);
+                           lay, static_cast<int>(tmode), pos_label, ignore_index, has_ignore, a, va, M);
         sortscan::sort_pairs<uint64_t, int32_t>(a, b, va, vb, n, 0, 33 + sortscan::ceil_log2(S), dev, st);
         if (want_curve || !want_ranks || wp) {
           finish(PayloadLoader<scalar_t, target_t, true, true>{b, vb, sc, tg, wp, divM, M, seg_stride, elem_stride,

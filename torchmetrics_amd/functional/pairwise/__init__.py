@@ -63,17 +63,33 @@ def _zero_diag(d: Tensor, zero_diagonal: bool) -> Tensor:
     return d
 
 
+def _mfma_ok(x: Tensor) -> bool:
+    """ROCm, non-fp64 operands with 4-aligned rows: the matrix-core GEMM path (``ops.gemm_nt``)."""
+    return x.is_cuda and x.dtype != torch.float64 and x.shape[-1] % 4 == 0 and x.shape[-1] > 0
+
+
+def _euclid_mfma(x: Tensor, y: Tensor, zd: bool) -> Tensor:
+    xf, yf = x.float(), y.float()
+    nx = (xf * xf).sum(1)
+    ny = nx if y is x else (yf * yf).sum(1)
+    return ops.gemm_nt(xf, yf, ops.GEMM_EUCLID, nx, ny, zero_diagonal=zd).to(x.dtype)
+
+
 def _distance(x: Tensor, y: Optional[Tensor], metric: int, p: float, reduction: _Reduction,
               zero_diagonal: Optional[bool]) -> Tensor:
     _check_reduction(reduction)
     x, y, zd = _check_input(x, y, zero_diagonal)
     red = reduction if reduction in ("sum", "mean") else None
+    if metric == ops.PW_L2 and red is None and _mfma_ok(x):
+        return _euclid_mfma(x, y, zd)
     return ops.pairwise_distance(x, y, metric, p, zd, red)
 
 
 def _pairwise_euclidean_distance_update(x: Tensor, y: Optional[Tensor] = None,
                                         zero_diagonal: Optional[bool] = None) -> Tensor:
     x, y, zd = _check_input(x, y, zero_diagonal)
+    if _mfma_ok(x):
+        return _euclid_mfma(x, y, zd)
     return ops.pairwise_distance(x, y, ops.PW_L2, 2.0, zd, None)
 
 
@@ -116,6 +132,8 @@ def pairwise_minkowski_distance(x: Tensor, y: Optional[Tensor] = None, exponent:
 def _pairwise_linear_similarity_update(x: Tensor, y: Optional[Tensor] = None,
                                        zero_diagonal: Optional[bool] = None) -> Tensor:
     x, y, zd = _check_input(x, y, zero_diagonal)
+    if _mfma_ok(x):
+        return ops.gemm_nt(x, y, ops.GEMM_STORE, zero_diagonal=zd).to(x.dtype)
     return _zero_diag(_safe_matmul(x, y), zd)
 
 
@@ -129,6 +147,10 @@ def pairwise_linear_similarity(x: Tensor, y: Optional[Tensor] = None, reduction:
 def _pairwise_cosine_similarity_update(x: Tensor, y: Optional[Tensor] = None,
                                        zero_diagonal: Optional[bool] = None) -> Tensor:
     x, y, zd = _check_input(x, y, zero_diagonal)
+    if _mfma_ok(x):
+        ix = 1.0 / torch.linalg.vector_norm(x.float(), 2, dim=1)
+        iy = ix if y is x else 1.0 / torch.linalg.vector_norm(y.float(), 2, dim=1)
+        return ops.gemm_nt(x, y, ops.GEMM_COSINE, ix, iy, zero_diagonal=zd).to(x.dtype)
     xn = x / torch.linalg.vector_norm(x, 2, dim=1, keepdim=True)
     yn = xn if y is x else y / torch.linalg.vector_norm(y, 2, dim=1, keepdim=True)
     return _zero_diag(_safe_matmul(xn, yn), zd)

@@ -9,9 +9,11 @@ MI355X-first changes:
   the fp64 states -- upper triangle only, inputs converted to fp64 while staged in LDS (no fp64 copy of the batch).
 * FID ``compute``: ``tr sqrt(Σ1 Σ2)`` via the symmetric form ``Σ sqrt(λ(A Σ2 A))`` with ``A = Σ1^{1/2}`` -- two
   symmetric eigensolves (rocSOLVER) instead of the reference's non-symmetric ``eigvals`` (``fid.py:177``).
-* KID: all ``subsets`` draws are evaluated as one batched GEMM with the polynomial kernel and masked diagonal sums
-  fused in the epilogue, instead of a Python loop of 3 GEMMs per subset (``kid.py:267``).  The RNG is consumed in the
-  reference's order, so the sampled subsets are identical for the same seed.
+* KID: on ROCm the subset draws are made on the device and all subsets run as three gathered-row MFMA GEMM launches
+  (``csrc/pairwise/gemm_nt.hip``) whose epilogue raises ``(gamma x.y + c)^d`` and sums it per subset (diagonal masked
+  for the self terms) -- instead of a Python loop of 3 GEMMs + elementwise pow + sums per subset (``kid.py:267``).
+  On CPU tensors the RNG is consumed in the reference's order (identical subsets for the same seed).
+* MiFID: the memorisation distance ``mean_i min_j (1 - |cos|)`` is one MFMA GEMM with a row-min epilogue.
 """
 from copy import deepcopy
 from typing import Any, List, Optional, Sequence, Tuple, Union
@@ -348,15 +350,30 @@ class KernelInceptionDistance(_FeatureNetMetric):
             raise ValueError("Argument `subset_size` should be smaller than the number of samples")
         if n_fake < self.subset_size:
             raise ValueError("Argument `subset_size` should be smaller than the number of samples")
-        # draw the permutations in the reference order (real, fake, real, fake, ...) on the host generator
+        m = self.subset_size
+        if real.is_cuda and real.shape[-1] % 4 == 0:
+            # ROCm: subset draws on the device (one batched rand + argsort), then three gathered-row MFMA GEMM
+            # launches whose epilogue raises (gamma x.y + c)^d and sums it per subset -- the [subsets, m, D]
+            # gathers and [subsets, m, m] kernel matrices never exist.  Same distribution of draws as the reference,
+            # from the device generator instead of the host one.
+            ir = torch.rand(self.subsets, n_real, device=real.device).argsort(dim=1)[:, :m].to(torch.int32)
+            jf = torch.rand(self.subsets, n_fake, device=fake.device).argsort(dim=1)[:, :m].to(torch.int32)
+            gamma = 1.0 / real.shape[-1] if self.gamma is None else self.gamma
+            kw = {"scale": gamma, "coef": self.coef, "degree": self.degree}
+            kxx = ops.gemm_nt(real, real, ops.GEMM_POLY_SUM, idx_x=ir, idx_y=ir, zero_diagonal=True, **kw).sum(-1)
+            kyy = ops.gemm_nt(fake, fake, ops.GEMM_POLY_SUM, idx_x=jf, idx_y=jf, zero_diagonal=True, **kw).sum(-1)
+            kxy = ops.gemm_nt(real, fake, ops.GEMM_POLY_SUM, idx_x=ir, idx_y=jf, **kw).sum(-1)
+            kid = ((kxx + kyy) / (m * (m - 1)) - 2 * kxy / (m**2)).to(real.dtype)
+            return kid.mean(), kid.std(unbiased=False)
+        # host: draw the permutations in the reference order (real, fake, real, fake, ...) on the host generator
         idx_r, idx_f = [], []
         for _ in range(self.subsets):
-            idx_r.append(torch.randperm(n_real)[: self.subset_size])
-            idx_f.append(torch.randperm(n_fake)[: self.subset_size])
+            idx_r.append(torch.randperm(n_real)[:m])
+            idx_f.append(torch.randperm(n_fake)[:m])
         ir = torch.stack(idx_r).to(real.device)
         if_ = torch.stack(idx_f).to(fake.device)
         scores = []
-        chunk = max(1, int(2**28 // max(1, self.subset_size * self.subset_size * 3)))
+        chunk = max(1, int(2**28 // max(1, m * m * 3)))
         for s in range(0, self.subsets, chunk):
             fr = real[ir[s : s + chunk]]  # [b, m, D]
             ff = fake[if_[s : s + chunk]]
@@ -427,6 +444,13 @@ class InceptionScore(_FeatureNetMetric):
 def _compute_cosine_distance(features1: Tensor, features2: Tensor, cosine_distance_eps: float = 0.1) -> Tensor:
     f1 = features1[torch.sum(features1, dim=1) != 0]
     f2 = features2[torch.sum(features2, dim=1) != 0]
+    if f1.is_cuda and f1.shape[-1] % 4 == 0 and f1.shape[0] and f2.shape[0]:
+        # one MFMA GEMM whose epilogue takes min_j (1 - |cos|) per row: no [n1, n2] similarity matrix
+        i1 = 1.0 / torch.norm(f1.float(), dim=1)
+        i2 = 1.0 / torch.norm(f2.float(), dim=1)
+        d_min = ops.gemm_nt(f1, f2, ops.GEMM_ROW_MIN, i1, i2).amin(-1).to(f1.dtype)
+        mean_min_d = torch.mean(d_min)
+        return mean_min_d if mean_min_d < cosine_distance_eps else torch.ones_like(mean_min_d)
     n1 = f1 / torch.norm(f1, dim=1, keepdim=True)
     n2 = f2 / torch.norm(f2, dim=1, keepdim=True)
     d = 1.0 - torch.abs(n1 @ n2.t())

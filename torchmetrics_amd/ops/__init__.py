@@ -683,6 +683,37 @@ def pairwise_distance(x: Tensor, y: Tensor, metric: int, p: float = 2.0, zero_di
     return out.to(x.dtype)
 
 
+# ------------------------------------------------------------------------------------------- MFMA GEMM epilogues
+GEMM_STORE, GEMM_EUCLID, GEMM_COSINE, GEMM_POLY_SUM, GEMM_ROW_MIN, GEMM_ROW_SUM = range(6)
+
+
+def gemm_nt(x: Tensor, y: Tensor, kind: int, aux_x: Optional[Tensor] = None, aux_y: Optional[Tensor] = None,
+            scale: float = 1.0, coef: float = 0.0, degree: int = 1, zero_diagonal: bool = False,
+            sqrt_out: bool = True, idx_x: Optional[Tensor] = None, idx_y: Optional[Tensor] = None) -> Tensor:
+    """``X @ Y^T`` (fp32, ``[N, D] x [M, D]`` or batched ``[B, N, D] x [B, M, D]``) with a fused epilogue
+    (``csrc/pairwise/gemm_nt.hip``: v_mfma_f32_32x32x2f32, 128 x 128 block tiles).
+
+    ``kind``: ``GEMM_STORE`` (scale * dot), ``GEMM_EUCLID`` (aux = squared row norms; sqrt(|x|^2 + |y|^2 - 2 x.y),
+    exact recompute under cancellation), ``GEMM_COSINE`` (aux = inverse norms), ``GEMM_POLY_SUM`` (fp64 partial sums of
+    ``(scale * dot + coef) ** degree`` per block, diagonal skipped with ``zero_diagonal``), ``GEMM_ROW_MIN``
+    (``min_j 1 - |cos|`` partials ``[.., N, ceil(M / 128)]``), ``GEMM_ROW_SUM`` (row-sum partials of ``scale * dot``).
+    ``idx_x`` / ``idx_y`` (int32 ``[B, rows]``): batch ``b`` multiplies the gathered rows ``x[idx_x[b]]`` and
+    ``y[idx_y[b]]`` without materialising them (the caller guarantees the indices are in range).
+    """
+    if x.is_cuda:
+        x = x.float().contiguous()
+        y = y.float().contiguous()
+        ax = None if aux_x is None else aux_x.float().contiguous()
+        ay = None if aux_y is None else aux_y.float().contiguous()
+        ix = None if idx_x is None else idx_x.to(torch.int32).contiguous()
+        iy = None if idx_y is None else idx_y.to(torch.int32).contiguous()
+        return _ops().gemm_nt(x, y, int(kind), ax, ay, float(scale), float(coef), int(degree), bool(zero_diagonal),
+                              bool(sqrt_out), ix, iy)
+    if idx_x is not None:
+        x, y = x[idx_x.long()], y[idx_y.long()]
+    return _cpu.gemm_nt(x, y, kind, aux_x, aux_y, scale, coef, degree, zero_diagonal, sqrt_out)
+
+
 # ------------------------------------------------------------------------------------------------------------ text
 def levenshtein(pred: Tensor, poff: Tensor, ref: Tensor, roff: Tensor, ins: int = 1, dele: int = 1, sub: int = 1,
                 use_beam: bool = False, max_ref_len: Optional[int] = None) -> Tensor:

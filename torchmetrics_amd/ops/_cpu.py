@@ -633,3 +633,50 @@ def kendall_stats(x: Tensor, y: Tensor) -> Tensor:
         ux[c] = float(torch.unique(x[:, c]).numel())
         uy[c] = float(torch.unique(y[:, c]).numel())
     return torch.stack([disc.double(), tx, tx1, tx2, ty, ty1, ty2, txy, ux, uy], 1)
+
+
+_GEMM_TILE = 128
+
+
+def gemm_nt(x: Tensor, y: Tensor, kind: int, aux_x, aux_y, scale: float, coef: float, degree: int,
+            zero_diagonal: bool, sqrt_out: bool) -> Tensor:
+    """Host implementation of ``csrc/pairwise/gemm_nt.hip`` (same outputs / partial layouts)."""
+    xf, yf = x.float(), y.float()
+    batched = xf.dim() == 3
+    if not batched:
+        xf, yf = xf.unsqueeze(0), yf.unsqueeze(0)
+        aux_x = None if aux_x is None else aux_x.reshape(1, -1)
+        aux_y = None if aux_y is None else aux_y.reshape(1, -1)
+    b, n, m = xf.shape[0], xf.shape[1], yf.shape[1]
+    dot = torch.bmm(xf, yf.transpose(1, 2))
+    eye = torch.eye(n, m, dtype=torch.bool).unsqueeze(0)
+    if kind in (0, 1, 2):
+        if kind == 0:
+            out = dot * scale
+        elif kind == 2:
+            out = dot * aux_x.reshape(b, n, 1).float() * aux_y.reshape(b, 1, m).float() * scale
+        else:
+            d2 = aux_x.reshape(b, n, 1).float() + aux_y.reshape(b, 1, m).float() - 2 * dot
+            exact = torch.cdist(xf.double(), yf.double()).pow(2).float()
+            d2 = torch.where(d2 < (aux_x.reshape(b, n, 1) + aux_y.reshape(b, 1, m)).float() / 128, exact, d2)
+            d2 = d2.clamp(min=0)
+            out = d2.sqrt() if sqrt_out else d2
+        if zero_diagonal:
+            out = out.masked_fill(eye, 0.0)
+        return out if batched else out[0]
+    if kind == 3:
+        v = (dot.double() * scale + coef) ** degree
+        if zero_diagonal:
+            v = v.masked_fill(eye, 0.0)
+        v = v.sum((1, 2)).reshape(b, 1)  # one "partial" per batch
+        return v if batched else v[0]
+    tiles = -(-m // _GEMM_TILE)
+    pad = tiles * _GEMM_TILE - m
+    if kind == 4:
+        v = 1.0 - (dot * aux_x.reshape(b, n, 1).float() * aux_y.reshape(b, 1, m).float()).abs()
+        v = torch.nn.functional.pad(v, (0, pad), value=3.0e38)
+        v = v.reshape(b, n, tiles, _GEMM_TILE).amin(-1)
+        return v if batched else v[0]
+    v = torch.nn.functional.pad(dot * scale, (0, pad))
+    v = v.reshape(b, n, tiles, _GEMM_TILE).sum(-1)
+    return v if batched else v[0]

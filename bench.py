@@ -25,7 +25,9 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 NUM_CLASSES = 1000
 BATCH = 8192
-N_BUFFERS = 4
+# input ring: 400 MB by default, larger than MI355X's 256 MB MALL (Infinity Cache), so every update streams its
+# logits from HBM as it would straight after a model forward on another batch (--ring-mb 64 = cache-resident ring)
+DEFAULT_RING_MB = 400
 
 
 def _setup(gpus: int):
@@ -58,22 +60,26 @@ def _max_over_ranks(x: float, device: torch.device, world: int) -> float:
     return float(t.item())
 
 
-def _data(device: torch.device, rank: int):
-    g = torch.Generator(device="cpu").manual_seed(1234 + rank)
-    preds = [torch.randn(BATCH, NUM_CLASSES, generator=g).to(device=device, dtype=torch.bfloat16) for _ in range(N_BUFFERS)]
-    target = [torch.randint(0, NUM_CLASSES, (BATCH,), generator=g).to(device) for _ in range(N_BUFFERS)]
+def _data(device: torch.device, rank: int, ring_mb: int):
+    per = BATCH * NUM_CLASSES * 2
+    k = max(2, (ring_mb * 2**20 + per - 1) // per)
+    gdev = device if device.type == "cuda" else torch.device("cpu")
+    g = torch.Generator(device=gdev).manual_seed(1234 + rank)
+    preds = [torch.randn(BATCH, NUM_CLASSES, generator=g, device=gdev).to(torch.bfloat16) for _ in range(k)]
+    target = [torch.randint(0, NUM_CLASSES, (BATCH,), generator=g, device=gdev) for _ in range(k)]
     return preds, target
 
 
 def _run(metric, preds, target, steps: int, warmup: int, device, world):
+    nbuf = len(preds)
     for i in range(warmup):
-        metric.update(preds[i % N_BUFFERS], target[i % N_BUFFERS])
+        metric.update(preds[i % nbuf], target[i % nbuf])
     metric.compute() if hasattr(metric, "_computed") else metric.compute()
     _reset(metric)
     _barrier_sync(device, world)
     t0 = time.perf_counter()
     for i in range(steps):
-        metric.update(preds[i % N_BUFFERS], target[i % N_BUFFERS])
+        metric.update(preds[(warmup + i) % nbuf], target[(warmup + i) % nbuf])
     result = metric.compute()
     _barrier_sync(device, world)
     elapsed = time.perf_counter() - t0
@@ -103,15 +109,20 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-baseline", action="store_true", help="skip the in-run reference-emulation baseline")
+    ap.add_argument("--ring-mb", type=int, default=DEFAULT_RING_MB, help="size of the input ring (MB)")
     args = ap.parse_args()
 
     world, rank, device = _setup(args.gpus)
     from torchmetrics_amd.classification import MulticlassConfusionMatrix
 
-    preds, target = _data(device, rank)
+    preds, target = _data(device, rank, args.ring_mb)
+    from torchmetrics_amd.parallel.sync import comm_stats
+
+    comm_stats(reset=True)
 
     ours = MulticlassConfusionMatrix(num_classes=NUM_CLASSES).to(device)
     t_ours, cms_ours, res_ours = _run(ours, preds, target, args.steps, args.warmup, device, world)
+    comms = comm_stats()
     t_ours = _max_over_ranks(t_ours, device, world)
     cms_ours = _max_over_ranks(cms_ours, device, world)
 
@@ -142,7 +153,7 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": round(value / base_val, 3) if base_val else None,
             "dtype": "bf16",
-            "data": "synthetic (randn bf16 logits, uniform int64 targets; fixed seeds)",
+            "data": "synthetic (randn bf16 logits, uniform int64 targets; fixed seeds; HBM-streamed input ring)",
             "config": {
                 "model": "MulticlassConfusionMatrix(num_classes=1000)",
                 "global_batch": BATCH * world,
@@ -150,9 +161,15 @@ def main() -> None:
                 "parallelism": f"dp{world}",
             },
             "compute_ms": round(cms_ours, 4),
+            "input_ring_mb": round(len(preds) * BATCH * NUM_CLASSES * 2 / 2**20, 1),
+            "dist": {
+                "world_size_seen": dist.get_world_size() if world > 1 else 1,
+                "backend": dist.get_backend() if world > 1 else None,
+                "engine_collectives": comms,
+            },
             "samples_per_s": round(value * BATCH, 1),
             "baseline": {
-                "impl": "reference torchmetrics 1.4.0dev op sequence (benchmarks/reference_path.py)",
+                "impl": "emulated reference op chain: torchmetrics 1.4.0dev op sequence re-run in this process (benchmarks/reference_path.py; the reference package is not importable on the box)",
                 "value": round(base_val, 2) if base_val else None,
                 "ms_per_step": round(t_ref / args.steps * 1e3, 4) if t_ref else None,
                 "compute_ms": round(cms_ref, 4) if cms_ref else None,

@@ -80,26 +80,38 @@ def main() -> None:
 
         ece = cls["ece"]
         cls_graph = MetricCollection({k: m for k, m in cls.items(keep_base=True) if k != "ece"}, compute_groups=True)
-        # one graph per input buffer of the ring, bound to that buffer: replays read the batch in place (no copy)
-        g_cls = [GraphedUpdate(cls_graph, logits[i], labels[i], bind_inputs=True) for i in range(NBUF)]
-        g_reg = [GraphedUpdate(reg, xs[i], ys[i], bind_inputs=True) for i in range(NBUF)]
+        # one graph per input buffer of the ring, bound to that buffer: replays read the batch in place (no copy);
+        # both collections' updates replay from that ONE graph (UpdateGroup)
+        from torchmetrics_amd.utils.graphs import UpdateGroup
+
+        group = UpdateGroup((cls_graph, 2), (reg, 2))
+        g_all = [GraphedUpdate(group, logits[i], labels[i], xs[i], ys[i], bind_inputs=True) for i in range(NBUF)]
+        g_cls, g_reg = g_all, []
         slot = {id(t): i for i, t in enumerate(logits)}
 
         def upd_cls(p, t):  # noqa: F811
-            g_cls[slot[id(p)]]()
+            g_all[slot[id(p)]]()
             ece.update(p, t)
 
         def upd_reg(p, t):  # noqa: F811
-            g_reg[slot_reg[id(p)]]()
+            pass  # replayed with the classification collection
 
-        slot_reg = {id(t): i for i, t in enumerate(xs)}
+    comp_cls, comp_reg = cls.compute, reg.compute
+    if args.graph and args.sync_every_step:
+        from torchmetrics_amd.utils.graphs import GraphedCompute
+
+        for i in range(2):  # states exist and compute groups are known before capture
+            upd_cls(logits[i], labels[i])
+            upd_reg(xs[i], ys[i])
+        both = GraphedCompute(cls, reg)  # one graph, one replay and one status read for both collections
+        comp_cls, comp_reg = both, (lambda: {})
 
     def step(i):
         upd_cls(logits[i % NBUF], labels[i % NBUF])
         upd_reg(xs[i % NBUF], ys[i % NBUF])
         if args.sync_every_step:
-            cls.compute()
-            reg.compute()
+            comp_cls()
+            comp_reg()
 
     def sync():
         if world > 1:
@@ -120,7 +132,8 @@ def main() -> None:
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
-    out = {**cls.compute(), **reg.compute()}
+    res = comp_cls()
+    out = {**res[0], **res[1]} if isinstance(res, tuple) else {**res, **comp_reg()}
     sync()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)

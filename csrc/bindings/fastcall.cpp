@@ -42,6 +42,7 @@ void calibration_bins(const at::Tensor& conf, const at::Tensor& acc, const at::T
                       at::Tensor bad);
 void curve_score(const at::Tensor& state, int64_t kind, int64_t average, at::Tensor out, at::Tensor nan_flag);
 void calibration_reduce(const at::Tensor& sums, int64_t norm, at::Tensor out);
+void calibration_reduce_clear(at::Tensor sums, int64_t norm, at::Tensor out);
 void regression_compute(int64_t kind, at::TensorList states, const c10::optional<at::Tensor>& n, double n_value,
                         int64_t multioutput, double bound, at::Tensor out);
 void mc_calibration_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor cand, at::Tensor conf,
@@ -230,6 +231,7 @@ PyMethodDef kMethods[] = {
     TM_FAST("confmat_reduce", tm_amd::confmat_reduce),
     TM_FAST("calibration_bins", tm_amd::calibration_bins),
     TM_FAST("calibration_reduce", tm_amd::calibration_reduce),
+    TM_FAST("calibration_reduce_clear", tm_amd::calibration_reduce_clear),
     TM_FAST("curve_score", tm_amd::curve_score),
     TM_FAST("regression_compute", tm_amd::regression_compute),
     TM_FAST("mc_calibration_update", tm_amd::mc_calibration_update),

@@ -10,134 +10,20 @@
 // Calibration (F/classification/calibration_error.py `_binning_bucketize`): bucketize + stack + index_add over
 // every accumulated confidence is replaced by one pass with an LDS-privatised (count, Σconf, Σacc) histogram
 // (SURVEY K7); the per-bin divisions stay a handful of [n_bins]-sized ops.
-#include "../common/tm_common.h"
+#include "common/compute_bodies.h"
 
 namespace tm_amd {
 namespace {
 
-constexpr int kThreads = 256;
-enum Kind : int { kJaccard = 0, kKappa = 1, kMcc = 2 };
-enum Avg : int { kMicro = 0, kMacro = 1, kWeighted = 2, kNone = 3 };
-enum KappaW : int { kWNone = 0, kWLinear = 1, kWQuadratic = 2 };
-
-__device__ __forceinline__ double block_sum(double v, double* red) {
-  v = wave_sum(v);
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-  __syncthreads();
-  if (lane == 0) red[wave] = v;
-  __syncthreads();
-  double s = 0.0;
-  for (int w = 0; w < kThreads / kWave; ++w) s += red[w];
-  return s;
-}
+constexpr int kThreads = cbody::kThreads;
+using cbody::kJaccard;
 
 __global__ void __launch_bounds__(kThreads) confmat_reduce_kernel(const int64_t* __restrict__ cm, int C, int kind,
                                                                   int average, int ignore, int kw,
                                                                   float* __restrict__ out) {
   extern __shared__ double sm[];  // rows [C], cols [C], diag [C]
   __shared__ double red[kThreads / kWave];
-  double* rows = sm;
-  double* cols = sm + C;
-  double* diag = sm + 2 * C;
-  for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    double r = 0.0, c = 0.0;
-    for (int j = 0; j < C; ++j) {
-      r += static_cast<double>(cm[static_cast<long long>(i) * C + j]);
-      c += static_cast<double>(cm[static_cast<long long>(j) * C + i]);
-    }
-    rows[i] = r;
-    cols[i] = c;
-    diag[i] = static_cast<double>(cm[static_cast<long long>(i) * C + i]);
-  }
-  __syncthreads();
-
-  if (kind == kJaccard) {
-    const bool drop = ignore >= 0 && ignore < C;
-    double tp_sum = 0.0, un_sum = 0.0, wsum = 0.0, wiou = 0.0;
-    for (int i = threadIdx.x; i < C; i += blockDim.x) {
-      const double tp = diag[i], un = rows[i] + cols[i] - tp;
-      const double iou = tp / (un == 0.0 ? 1.0 : un);
-      out[i] = static_cast<float>(iou);
-      tp_sum += tp;
-      un_sum += (drop && i == ignore) ? 0.0 : un;
-      double w = average == kWeighted ? rows[i] : 1.0;
-      if (average == kMacro && ((drop && i == ignore) || rows[i] + cols[i] == 0.0)) w = 0.0;
-      wsum += w;
-      wiou += w * iou;
-    }
-    tp_sum = block_sum(tp_sum, red);
-    un_sum = block_sum(un_sum, red);
-    wsum = block_sum(wsum, red);
-    wiou = block_sum(wiou, red);
-    if (threadIdx.x == 0) {
-      out[C] = average == kMicro ? static_cast<float>(tp_sum / (un_sum == 0.0 ? 1.0 : un_sum))
-                                 : static_cast<float>(wiou / wsum);  // 0/0 -> nan, as ((w * iou) / w.sum()).sum()
-    }
-    return;
-  }
-
-  double n = 0.0;
-  for (int i = threadIdx.x; i < C; i += blockDim.x) n += rows[i];
-  n = block_sum(n, red);
-
-  if (kind == kKappa) {
-    // 1 - sum(W * O) / sum(W * E),  E_ij = rows_i cols_j / n
-    double wo = 0.0, we = 0.0;
-    for (long long e = threadIdx.x; e < static_cast<long long>(C) * C; e += blockDim.x) {
-      const int i = static_cast<int>(e / C), j = static_cast<int>(e - static_cast<long long>(i) * C);
-      const double d = static_cast<double>(i - j);
-      const double w = kw == kWNone ? (i == j ? 0.0 : 1.0) : (kw == kWLinear ? fabs(d) : d * d);
-      wo += w * static_cast<double>(cm[e]);
-      we += w * rows[i] * cols[j] / n;
-    }
-    wo = block_sum(wo, red);
-    we = block_sum(we, red);
-    if (threadIdx.x == 0) out[0] = static_cast<float>(1.0 - wo / we);
-    return;
-  }
-
-  // MCC (Gorodkin R_K), with the reference's binary special cases
-  double tk_pk = 0.0, pk2 = 0.0, tk2 = 0.0, correct = 0.0;
-  for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    tk_pk += rows[i] * cols[i];
-    pk2 += cols[i] * cols[i];
-    tk2 += rows[i] * rows[i];
-    correct += diag[i];
-  }
-  tk_pk = block_sum(tk_pk, red);
-  pk2 = block_sum(pk2, red);
-  tk2 = block_sum(tk2, red);
-  correct = block_sum(correct, red);
-  if (threadIdx.x != 0) return;
-  const bool binary = C == 2;
-  if (binary) {
-    const double tn = static_cast<double>(cm[0]), fp = static_cast<double>(cm[1]);
-    const double fn = static_cast<double>(cm[2]), tp = static_cast<double>(cm[3]);
-    if (tp + tn != 0.0 && fp + fn == 0.0) {
-      out[0] = 1.f;
-      return;
-    }
-    if (tp + tn == 0.0 && fp + fn != 0.0) {
-      out[0] = -1.f;
-      return;
-    }
-  }
-  double numer = correct * n - tk_pk;
-  double denom = (n * n - pk2) * (n * n - tk2);
-  if (denom == 0.0) {
-    if (!binary) {
-      out[0] = 0.f;
-      return;
-    }
-    const double tn = static_cast<double>(cm[0]), fp = static_cast<double>(cm[1]);
-    const double fn = static_cast<double>(cm[2]), tp = static_cast<double>(cm[3]);
-    const double eps = 1.1920928955078125e-07;  // torch.finfo(float32).eps
-    const double a = (tp == 0.0 || tn == 0.0) ? tp + tn : 0.0;
-    const double b = (fp == 0.0 || fn == 0.0) ? fp + fn : 0.0;
-    numer = sqrt(eps) * (a - b);
-    denom = (tp + fp + eps) * (tp + fn + eps) * (tn + fp + eps) * (tn + fn + eps);
-  }
-  out[0] = static_cast<float>(numer / sqrt(denom));
+  cbody::confmat_reduce_block(cm, C, kind, average, ignore, kw, out, sm, red);
 }
 
 // (count, Σconf, Σacc) per bin; bin = #{boundaries <= conf} - 1 (torch.bucketize(right=True) - 1); nb <= 4096
@@ -175,6 +61,48 @@ __global__ void __launch_bounds__(kThreads) calib_bins_kernel(const float* __res
     if (hs[i] != 0.f) atomicAdd(&sums[i], hs[i]);
 }
 
+// Few-bin variant (nb <= 16, the default 15 bins): every thread owns a private (count, Σconf, Σacc) column in LDS
+// (layout [3 * nb][256]: a lane's updates never collide with another lane's, no atomics), so the per-element cost is
+// three plain LDS read-modify-writes instead of three same-address LDS atomics contended by the whole wave.  At the
+// end each wave reduces whole rows (256 values -> 1) and adds them to the global sums with one atomic per row.
+constexpr int kPrivBins = 16;
+
+__global__ void __launch_bounds__(kThreads) calib_bins_private_kernel(const float* __restrict__ conf,
+                                                                      const float* __restrict__ acc, long long n,
+                                                                      const float* __restrict__ bounds, int nb,
+                                                                      float* __restrict__ sums,
+                                                                      int* __restrict__ bad) {
+  __shared__ float hist[3 * kPrivBins * kThreads];
+  __shared__ float bs[kPrivBins];
+  for (int i = threadIdx.x; i < 3 * nb * kThreads; i += kThreads) hist[i] = 0.f;
+  if (threadIdx.x < nb) bs[threadIdx.x] = bounds[threadIdx.x];
+  __syncthreads();
+  bool oob = false;
+  const int t = threadIdx.x;
+  for (long long e = static_cast<long long>(blockIdx.x) * kThreads + t; e < n;
+       e += static_cast<long long>(gridDim.x) * kThreads) {
+    const float x = conf[e];
+    int b = -1;
+    for (int k = 0; k < nb; ++k) b += (bs[k] <= x) ? 1 : 0;  // #{bounds <= x} - 1 (ascending bounds)
+    if (b < 0) {
+      oob = true;
+      continue;
+    }
+    hist[(3 * b) * kThreads + t] += 1.f;
+    hist[(3 * b + 1) * kThreads + t] += x;
+    hist[(3 * b + 2) * kThreads + t] += acc[e];
+  }
+  if (oob) atomicOr(bad, 1);
+  __syncthreads();
+  const int lane = t & (kWave - 1), wave = t / kWave;
+  for (int row = wave; row < 3 * nb; row += kThreads / kWave) {
+    const float* r = hist + row * kThreads;
+    float v = r[lane] + r[lane + 64] + r[lane + 128] + r[lane + 192];
+    v = wave_sum(v);
+    if (lane == 0 && v != 0.f) atomicAdd(&sums[row], v);
+  }
+}
+
 }  // namespace
 
 // confmat: int64 [C, C]; kind 0 Jaccard (average 0 micro / 1 macro / 2 weighted / 3 none, ignore: class to drop or -1),
@@ -208,6 +136,15 @@ void calibration_bins(const at::Tensor& conf, const at::Tensor& acc, const at::T
               "calibration_bins: sums f32 [nb, 3]");
   const long long n = conf.numel();
   if (n == 0) return;
+  if (nb <= kPrivBins) {
+    // ~32 elements per thread: enough work to amortise the 3*nb*256-float LDS clear and row reduction per block
+    const int grid = grid_cap((n + kThreads * 32 - 1) / (kThreads * 32), 1024);
+    hipLaunchKernelGGL(calib_bins_private_kernel, dim3(grid), dim3(kThreads), 0, stream(), conf.data_ptr<float>(),
+                       acc.data_ptr<float>(), n, bounds.data_ptr<float>(), nb, sums.data_ptr<float>(),
+                       bad.data_ptr<int>());
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+    return;
+  }
   const int grid = grid_cap((n + kThreads - 1) / kThreads, 256 * 4);
   hipLaunchKernelGGL(calib_bins_kernel, dim3(grid), dim3(kThreads), 4 * nb * sizeof(float), stream(),
                      conf.data_ptr<float>(), acc.data_ptr<float>(), n, bounds.data_ptr<float>(), nb,
@@ -219,8 +156,8 @@ void calibration_bins(const at::Tensor& conf, const at::Tensor& acc, const at::T
 // bins, the reference's nan_to_num), proportion = count / Σcount, then l1 = Σ |acc - conf| * prop or
 // max = max |acc - conf| (reference F/classification/calibration_error.py `_ce_compute`, ~10 ATen launches).
 namespace {
-__global__ void __launch_bounds__(kThreads) calib_reduce_kernel(const float* __restrict__ sums, int nb, int norm,
-                                                                float* __restrict__ out) {
+__global__ void __launch_bounds__(kThreads) calib_reduce_kernel(float* __restrict__ sums, int nb, int norm,
+                                                                float* __restrict__ out, int clear) {
   __shared__ float red[kThreads / kWave];
   float tot = 0.f;
   for (int b = threadIdx.x; b < nb; b += blockDim.x) tot += sums[3 * b];
@@ -253,6 +190,10 @@ __global__ void __launch_bounds__(kThreads) calib_reduce_kernel(const float* __r
     for (int w = 1; w < kThreads / kWave; ++w) r = norm == 0 ? r + red[w] : fmaxf(r, red[w]);
     out[0] = r;
   }
+  if (clear) {  // self-cleaning workspace: the next calibration_bins accumulates into zeros
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * nb; i += blockDim.x) sums[i] = 0.f;
+  }
 }
 }  // namespace
 
@@ -264,7 +205,19 @@ void calibration_reduce(const at::Tensor& sums, int64_t norm, at::Tensor out) {
   TORCH_CHECK(norm == 0 || norm == 1, "calibration_reduce: norm 0 (l1) or 1 (max)");
   TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 1, "calibration_reduce: out f32 [1]");
   hipLaunchKernelGGL(calib_reduce_kernel, dim3(1), dim3(kThreads), 0, stream(), sums.data_ptr<float>(),
-                     static_cast<int>(sums.size(0)), static_cast<int>(norm), out.data_ptr<float>());
+                     static_cast<int>(sums.size(0)), static_cast<int>(norm), out.data_ptr<float>(), 0);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+// as calibration_reduce, then zeroes `sums` (a persistent workspace reused by the next compute())
+void calibration_reduce_clear(at::Tensor sums, int64_t norm, at::Tensor out) {
+  TM_CHECK_CUDA(sums);
+  TORCH_CHECK(sums.scalar_type() == at::kFloat && sums.is_contiguous() && sums.dim() == 2 && sums.size(1) == 3,
+              "calibration_reduce_clear: sums must be contiguous f32 [nb, 3]");
+  TORCH_CHECK(norm == 0 || norm == 1, "calibration_reduce_clear: norm 0 (l1) or 1 (max)");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 1, "calibration_reduce_clear: out f32 [1]");
+  hipLaunchKernelGGL(calib_reduce_kernel, dim3(1), dim3(kThreads), 0, stream(), sums.data_ptr<float>(),
+                     static_cast<int>(sums.size(0)), static_cast<int>(norm), out.data_ptr<float>(), 1);
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
@@ -272,6 +225,7 @@ void calibration_reduce(const at::Tensor& sums, int64_t norm, at::Tensor out) {
 
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
   m.def("calibration_reduce(Tensor sums, int norm, Tensor(a!) out) -> ()");
+  m.def("calibration_reduce_clear(Tensor(a!) sums, int norm, Tensor(b!) out) -> ()");
   m.def("confmat_reduce(Tensor confmat, int kind, int average, int ignore, int kw, Tensor(a!) out) -> ()");
   m.def("calibration_bins(Tensor conf, Tensor acc, Tensor bounds, Tensor(a!) sums, Tensor(b!) bad) -> ()");
 }
@@ -279,4 +233,5 @@ TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
   m.impl("confmat_reduce", &tm_amd::confmat_reduce);
   m.impl("calibration_bins", &tm_amd::calibration_bins);
   m.impl("calibration_reduce", &tm_amd::calibration_reduce);
+  m.impl("calibration_reduce_clear", &tm_amd::calibration_reduce_clear);
 }

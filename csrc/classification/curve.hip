@@ -15,7 +15,7 @@
 //
 // Launches per update: range/rowstat pass, binning pass, finalize (suffix scan + add into the int64 state + re-zero
 // of the scratch histogram and control word so the workspace is ready for the next update without a memset).
-#include "../common/tm_common.h"
+#include "common/compute_bodies.h"
 
 namespace tm_amd {
 namespace {
@@ -252,86 +252,15 @@ __global__ void __launch_bounds__(256) curve_finalize_kernel(unsigned* __restric
 // Reference chain (F/classification/{roc,auroc,precision_recall_curve,average_precision}.py binned branches):
 // rates / precision-recall from the [T, C, 2, 2] confmat (_safe_divide: 0/0 -> 0), flip, trapz or the AP step sum,
 // then a nan-aware macro / weighted reduction with two host syncs (`isnan().any()`, boolean-mask indexing).
-// One block: wave w scores classes w, w + 4, ...; lane-strided over thresholds + wave sum; then one wave reduces
-// over classes.  out[0..C) = per-class score, out[C] = the reduced score; *nan_flag = 1 if any class is NaN.
-constexpr int kScoreAuroc = 0;
-constexpr int kScoreAp = 1;
-
-__device__ __forceinline__ float safe_div(long long a, long long b) {
-  return static_cast<float>(a) / (b == 0 ? 1.f : static_cast<float>(b));
-}
+// AUROC / AP of a binned state: one block (body in common/compute_bodies.h, shared with compute_tasks.hip)
+using cbody::kScoreAp;
+using cbody::kScoreAuroc;
 
 __global__ void __launch_bounds__(256) curve_score_kernel(const int64_t* __restrict__ st, int T, int C, int kind,
                                                           int average, float* __restrict__ out,
                                                           int* __restrict__ nan_flag) {
   extern __shared__ float sm[];  // [C] scores, [C] weights
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave, nw = blockDim.x / kWave;
-  auto at = [&](int t, int c, int a, int b) -> long long { return st[((static_cast<long long>(t) * C + c) * 2 + a) * 2 + b]; };
-  for (int c = wave; c < C; c += nw) {
-    float acc = 0.f;
-    if (kind == kScoreAuroc) {
-      // points i = 0..T-1 of the flipped curve: x_i = fpr(T-1-i), y_i = tpr(T-1-i); trapz over consecutive pairs
-      for (int i = lane; i < T - 1; i += kWave) {
-        const int t0 = T - 1 - i, t1 = T - 2 - i;
-        const float x0 = safe_div(at(t0, c, 0, 1), at(t0, c, 0, 1) + at(t0, c, 0, 0));
-        const float x1 = safe_div(at(t1, c, 0, 1), at(t1, c, 0, 1) + at(t1, c, 0, 0));
-        const float y0 = safe_div(at(t0, c, 1, 1), at(t0, c, 1, 1) + at(t0, c, 1, 0));
-        const float y1 = safe_div(at(t1, c, 1, 1), at(t1, c, 1, 1) + at(t1, c, 1, 0));
-        acc += (x1 - x0) * (y1 + y0) / 2.f;
-      }
-    } else {
-      // AP = -sum_k (recall[k+1] - recall[k]) * precision[k], with the appended point (precision 1, recall 0)
-      for (int k = lane; k < T; k += kWave) {
-        const long long tp = at(k, c, 1, 1), fp = at(k, c, 0, 1), fn = at(k, c, 1, 0);
-        const float prec = safe_div(tp, tp + fp), rec = safe_div(tp, tp + fn);
-        float rec_next = 0.f;
-        if (k + 1 < T) {
-          const long long tp1 = at(k + 1, c, 1, 1), fn1 = at(k + 1, c, 1, 0);
-          rec_next = safe_div(tp1, tp1 + fn1);
-        }
-        acc += (rec_next - rec) * prec;
-      }
-      acc = -acc;
-    }
-    acc = wave_sum(acc);
-    if (lane == 0) {
-      sm[c] = acc;
-      sm[C + c] = static_cast<float>(at(0, c, 1, 0) + at(0, c, 1, 1));  // positives per class (weights)
-      out[c] = acc;
-    }
-  }
-  __syncthreads();
-  if (wave == 0) {
-    float sum = 0.f, wsum = 0.f, cnt = 0.f;
-    int nan = 0;
-    for (int c = lane; c < C; c += kWave) {
-      const float r = sm[c];
-      if (r != r) {
-        nan = 1;
-        continue;
-      }
-      sum += r;
-      cnt += 1.f;
-      wsum += sm[C + c];
-    }
-    sum = wave_sum(sum);
-    cnt = wave_sum(cnt);
-    wsum = wave_sum(wsum);
-    nan = __any(nan);
-    float wred = 0.f;
-    if (average == 2) {
-      const float denom = wsum == 0.f ? 1.f : wsum;
-      for (int c = lane; c < C; c += kWave) {
-        const float r = sm[c];
-        if (r == r) wred += r * (sm[C + c] / denom);
-      }
-      wred = wave_sum(wred);
-    }
-    if (lane == 0) {
-      out[C] = average == 2 ? wred : sum / cnt;
-      *nan_flag = nan;
-    }
-  }
+  cbody::curve_score_block(st, T, C, kind, average, out, nan_flag, sm);
 }
 }  // namespace
 

@@ -5,40 +5,12 @@
 // safe divides, where, weighted sum): host-launch bound at ~0.17 ms per metric.  One block per row (global: 1 row,
 // samplewise: N rows) loads the C-class tp/fp/tn/fn, evaluates the per-class score, and reduces micro / macro /
 // weighted in one pass -- a single launch.  Scores are computed in fp32 from the int64 counts, as ATen does.
-#include "common/tm_common.h"
+#include "common/compute_bodies.h"
 
 namespace tm_amd {
 namespace {
 
-constexpr int kThreads = 256;
-enum Kind : int { kAccuracy = 0, kHamming = 1, kPrecision = 2, kRecall = 3, kSpecificity = 4, kFBeta = 5 };
-enum Avg : int { kMicro = 0, kMacro = 1, kWeighted = 2, kNone = 3 };
-
-__device__ __forceinline__ float sdiv(float n, float d) { return n / (d == 0.f ? 1.f : d); }
-
-// per-class score (`_score` in functional/classification/_reductions.py)
-__device__ __forceinline__ float class_score(int kind, float tp, float fp, float tn, float fn, bool multilabel,
-                                             float beta2) {
-  switch (kind) {
-    case kAccuracy: return multilabel ? sdiv(tp + tn, tp + tn + fp + fn) : sdiv(tp, tp + fn);
-    case kHamming: return 1.f - (multilabel ? sdiv(tp + tn, tp + tn + fp + fn) : sdiv(tp, tp + fn));
-    case kPrecision: return sdiv(tp, tp + fp);
-    case kRecall: return sdiv(tp, tp + fn);
-    case kSpecificity: return sdiv(tn, tn + fp);
-    default: return sdiv((1.f + beta2) * tp, (1.f + beta2) * tp + beta2 * fn + fp);
-  }
-}
-
-__device__ __forceinline__ double block_sum(double v, double* red) {
-  v = wave_sum(v);
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-  __syncthreads();
-  if (lane == 0) red[wave] = v;
-  __syncthreads();
-  double s = 0.0;
-  for (int w = 0; w < kThreads / kWave; ++w) s += red[w];
-  return s;
-}
+constexpr int kThreads = cbody::kThreads;
 
 __global__ void __launch_bounds__(kThreads) stat_reduce_kernel(const int64_t* __restrict__ tp,
                                                                const int64_t* __restrict__ fp,
@@ -47,50 +19,7 @@ __global__ void __launch_bounds__(kThreads) stat_reduce_kernel(const int64_t* __
                                                                int avg, bool multilabel, float beta2,
                                                                float* __restrict__ out) {
   __shared__ double red[kThreads / kWave];
-  const long long row = blockIdx.x;
-  const int64_t* a = tp + row * C;
-  const int64_t* b = fp + row * C;
-  const int64_t* c = tn + row * C;
-  const int64_t* d = fn + row * C;
-  if (avg == kNone) {
-    for (int k = threadIdx.x; k < C; k += kThreads)
-      out[row * C + k] = class_score(kind, static_cast<float>(a[k]), static_cast<float>(b[k]), static_cast<float>(c[k]),
-                                     static_cast<float>(d[k]), multilabel, beta2);
-    return;
-  }
-  if (avg == kMicro) {
-    double s[4] = {0, 0, 0, 0};
-    for (int k = threadIdx.x; k < C; k += kThreads) {
-      s[0] += static_cast<double>(a[k]);
-      s[1] += static_cast<double>(b[k]);
-      s[2] += static_cast<double>(c[k]);
-      s[3] += static_cast<double>(d[k]);
-    }
-    for (int i = 0; i < 4; ++i) s[i] = block_sum(s[i], red);
-    if (threadIdx.x == 0) {
-      // micro accuracy / hamming of a multilabel problem use the binary formula, everything else the class formula
-      const bool binary_form = multilabel && (kind == kAccuracy || kind == kHamming);
-      out[row] = class_score(kind, static_cast<float>(s[0]), static_cast<float>(s[1]), static_cast<float>(s[2]),
-                             static_cast<float>(s[3]), binary_form, beta2);
-    }
-    return;
-  }
-  double num = 0.0, den = 0.0;
-  for (int k = threadIdx.x; k < C; k += kThreads) {
-    const float ftp = static_cast<float>(a[k]), ffp = static_cast<float>(b[k]), ftn = static_cast<float>(c[k]),
-                ffn = static_cast<float>(d[k]);
-    const float sc = class_score(kind, ftp, ffp, ftn, ffn, multilabel, beta2);
-    float w;
-    if (avg == kWeighted)
-      w = ftp + ffn;
-    else
-      w = (!multilabel && a[k] + b[k] + d[k] == 0) ? 0.f : 1.f;
-    num += static_cast<double>(w * sc);
-    den += static_cast<double>(w);
-  }
-  num = block_sum(num, red);
-  den = block_sum(den, red);
-  if (threadIdx.x == 0) out[row] = static_cast<float>(num / (den == 0.0 ? 1.0 : den));
+  cbody::stat_reduce_row(tp, fp, tn, fn, C, kind, avg, multilabel, beta2, out, blockIdx.x, red);
 }
 
 }  // namespace

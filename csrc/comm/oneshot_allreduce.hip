@@ -1,0 +1,220 @@
+// One-shot intra-node all-reduce over xGMI peer reads, for the tiny metric-state buckets.
+//
+// Why: a classification / regression collection syncs a few hundred bytes to a few KiB per compute() (tp/fp/tn/fn of
+// 20 metrics, regression moments).  A ring all-reduce over W ranks is 2(W-1) latency-bound steps; on MI355X every
+// GPU has a direct xGMI link to every other GPU of the node, so one step suffices: each rank publishes its bucket in
+// a buffer the peers have mapped (hipIpcGetMemHandle / hipIpcOpenMemHandle), raises a flag in every peer's flag
+// array, waits for all W flags, and reads the W buckets straight out of the peers' HBM.  Reference behaviour being
+// replaced: S/utilities/distributed.py:97-147 (per-state barrier + all_gather + local reduce).
+//
+// Buffer layout (one hipMalloc per rank, identical on every rank):
+//   [ data parity 0 : slot bytes ][ data parity 1 : slot bytes ][ flags: 2 x kMaxBlocks x kMaxRanks uint32 ]
+// Call number `epoch` (1, 2, ...) uses parity epoch & 1.  Double buffering is enough: a rank can only start call e+2
+// after its call e+1 finished, and call e+1 needs every peer's e+1 flag, which a peer raises only after its call e
+// (the last reader of the e-parity buffer) has completed on its stream.
+//
+// Block b owns elements [b*chunk, (b+1)*chunk) on every rank, so the flags are per (parity, block, source rank): the
+// block only waits for the peers' copies of its own chunk.  Waits are bounded (kSpinNs of wall clock); a timed-out
+// wait sets bit 1 of `status` and the block leaves without reducing, so a dead peer can never hang the GPU.
+#include "common/tm_common.h"
+
+namespace tm_amd {
+namespace {
+
+constexpr int kMaxRanks = 16;
+constexpr int kMaxBlocks = 64;
+constexpr int kThreads = 256;
+constexpr long long kSpinTicks = 100LL * 1000 * 1000 * 2;  // wall_clock64 runs at 100 MHz -> 2 s
+
+struct PeerPtrs {
+  char* p[kMaxRanks];
+};
+
+enum : int { kOpSum = 0, kOpMax = 1, kOpMin = 2 };
+
+template <typename T>
+__device__ __forceinline__ T combine(T a, T b, int op) {
+  if (op == kOpSum) return a + b;
+  if (op == kOpMax) return a > b ? a : b;
+  return a < b ? a : b;
+}
+
+__device__ __forceinline__ uint32_t* flag_slot(char* base, long long slot_bytes, int parity, int block, int src) {
+  uint32_t* flags = reinterpret_cast<uint32_t*>(base + 2 * slot_bytes);
+  return flags + (static_cast<long long>(parity) * kMaxBlocks + block) * kMaxRanks + src;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads) oneshot_allreduce_kernel(const T* __restrict__ inp, T* __restrict__ out,
+                                                                     long long n, long long chunk, PeerPtrs peers,
+                                                                     int rank, int world, long long slot_bytes,
+                                                                     uint32_t epoch, int op, int publish,
+                                                                     int* __restrict__ status) {
+  const int b = blockIdx.x;
+  const int parity = static_cast<int>(epoch & 1u);
+  const long long lo = static_cast<long long>(b) * chunk;
+  const long long hi = lo + chunk < n ? lo + chunk : n;
+  // 1. publish this rank's chunk in its own (peer-visible) buffer
+  T* mine = reinterpret_cast<T*>(peers.p[rank] + parity * slot_bytes);
+  if (publish) {
+    for (long long i = lo + threadIdx.x; i < hi; i += kThreads) mine[i] = inp[i];
+  }
+  __threadfence_system();
+  __syncthreads();
+  // 2. tell every peer that chunk b of this rank is ready (remote store over xGMI), 3. wait for theirs
+  if (threadIdx.x < world) {
+    const int p = threadIdx.x;
+    __hip_atomic_store(flag_slot(peers.p[p], slot_bytes, parity, b, rank), epoch, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __shared__ int timed_out;
+  if (threadIdx.x == 0) timed_out = 0;
+  __syncthreads();
+  if (threadIdx.x < world) {
+    const int p = threadIdx.x;
+    uint32_t* f = flag_slot(peers.p[rank], slot_bytes, parity, b, p);
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+      if (wall_clock64() - t0 > kSpinTicks) {
+        atomicOr(&timed_out, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  if (timed_out) {
+    if (threadIdx.x == 0) atomicOr(status, 1);
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // peers' data is visible to every lane of the block
+  // 4. reduce the W copies of chunk b, always in rank order (identical rounding on every rank)
+  for (long long i = lo + threadIdx.x; i < hi; i += kThreads) {
+    T acc = reinterpret_cast<const T*>(peers.p[0] + parity * slot_bytes)[i];
+    for (int r = 1; r < world; ++r) acc = combine(acc, reinterpret_cast<const T*>(peers.p[r] + parity * slot_bytes)[i], op);
+    out[i] = acc;
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------------- host side
+int64_t ipc_buffer_alloc(int64_t nbytes, int64_t device) {
+  TORCH_CHECK(nbytes > 0, "ipc_buffer_alloc: nbytes must be positive");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, static_cast<int>(device)));
+  void* p = nullptr;
+  TORCH_CHECK(hipMalloc(&p, nbytes) == hipSuccess, "ipc_buffer_alloc: hipMalloc failed");
+  TORCH_CHECK(hipMemset(p, 0, nbytes) == hipSuccess, "ipc_buffer_alloc: hipMemset failed");
+  TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "ipc_buffer_alloc: sync failed");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void ipc_buffer_free(int64_t ptr, int64_t device) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, static_cast<int>(device)));
+  (void)hipFree(reinterpret_cast<void*>(ptr));
+}
+
+at::Tensor ipc_get_handle(int64_t ptr, int64_t device) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, static_cast<int>(device)));
+  hipIpcMemHandle_t h;
+  TORCH_CHECK(hipIpcGetMemHandle(&h, reinterpret_cast<void*>(ptr)) == hipSuccess, "ipc_get_handle failed");
+  at::Tensor out = at::empty({static_cast<int64_t>(sizeof(h))}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(out.data_ptr<uint8_t>(), &h, sizeof(h));
+  return out;
+}
+
+int64_t ipc_open_handle(const at::Tensor& handle, int64_t device) {
+  TORCH_CHECK(!handle.is_cuda() && handle.scalar_type() == at::kByte && handle.numel() == sizeof(hipIpcMemHandle_t),
+              "ipc_open_handle: expected a CPU uint8 tensor of ", sizeof(hipIpcMemHandle_t), " bytes");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, static_cast<int>(device)));
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle.contiguous().data_ptr<uint8_t>(), sizeof(h));
+  void* p = nullptr;
+  const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+  TORCH_CHECK(e == hipSuccess, "ipc_open_handle: hipIpcOpenMemHandle failed: ", hipGetErrorString(e));
+  return reinterpret_cast<int64_t>(p);
+}
+
+void ipc_close_handle(int64_t ptr, int64_t device) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, static_cast<int>(device)));
+  (void)hipIpcCloseMemHandle(reinterpret_cast<void*>(ptr));
+}
+
+// uint8 view of `nbytes` at a raw device pointer (no ownership): lets tests and tools fill / inspect the buffers
+at::Tensor ipc_view(int64_t ptr, int64_t nbytes, int64_t device) {
+  return at::from_blob(reinterpret_cast<void*>(ptr), {nbytes},
+                       at::TensorOptions().dtype(at::kByte).device(c10::Device(c10::DeviceType::CUDA,
+                                                                               static_cast<int>(device))));
+}
+
+// out = reduce_op over ranks of inp (1-D, <= slot_bytes).  peers: CPU int64 [world] of device pointers (this rank's
+// own buffer at index `rank`).  publish=false skips step 1 (tests that pre-fill the buffers).
+void oneshot_allreduce(const at::Tensor& inp, at::Tensor out, const at::Tensor& peers, int64_t rank, int64_t slot_bytes,
+                       int64_t epoch, int64_t op, bool publish, at::Tensor status) {
+  TM_CHECK_CUDA(inp);
+  TM_SAME_DEVICE(inp, out);
+  TM_SAME_DEVICE(inp, status);
+  TM_CHECK_CONTIG(inp);
+  TM_CHECK_CONTIG(out);
+  TORCH_CHECK(out.scalar_type() == inp.scalar_type() && out.numel() == inp.numel(), "oneshot_allreduce: bad out");
+  TORCH_CHECK(status.scalar_type() == at::kInt && status.numel() >= 1, "oneshot_allreduce: bad status");
+  TORCH_CHECK(!peers.is_cuda() && peers.scalar_type() == at::kLong && peers.dim() == 1, "oneshot_allreduce: peers");
+  const int world = static_cast<int>(peers.numel());
+  TORCH_CHECK(world >= 1 && world <= kMaxRanks, "oneshot_allreduce: world size must be in [1, ", kMaxRanks, "]");
+  TORCH_CHECK(rank >= 0 && rank < world, "oneshot_allreduce: bad rank");
+  TORCH_CHECK(op >= 0 && op <= 2, "oneshot_allreduce: op must be sum/max/min");
+  TORCH_CHECK(epoch > 0 && epoch < (1LL << 32), "oneshot_allreduce: epoch out of range");
+  const long long n = inp.numel();
+  TORCH_CHECK(static_cast<long long>(n * inp.element_size()) <= slot_bytes, "oneshot_allreduce: bucket exceeds slot");
+  if (n == 0) return;
+  PeerPtrs pp{};
+  const int64_t* pv = peers.data_ptr<int64_t>();
+  for (int r = 0; r < world; ++r) {
+    TORCH_CHECK(pv[r] != 0, "oneshot_allreduce: null peer pointer");
+    pp.p[r] = reinterpret_cast<char*>(pv[r]);
+  }
+  // >= 4 KiB per block, at most kMaxBlocks blocks, chunk a multiple of 64 elements
+  const long long bytes = n * inp.element_size();
+  long long blocks = (bytes + 4095) / 4096;
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  long long chunk = (n + blocks - 1) / blocks;
+  chunk = (chunk + 63) / 64 * 64;
+  blocks = (n + chunk - 1) / chunk;
+  switch (inp.scalar_type()) {
+#define TM_ONESHOT_CASE(ATYPE, CTYPE)                                                                              \
+  case ATYPE:                                                                                                      \
+    hipLaunchKernelGGL((oneshot_allreduce_kernel<CTYPE>), dim3(blocks), dim3(kThreads), 0, stream(),               \
+                       inp.data_ptr<CTYPE>(), out.data_ptr<CTYPE>(), n, chunk, pp, static_cast<int>(rank), world,    \
+                       slot_bytes, static_cast<uint32_t>(epoch), static_cast<int>(op), publish ? 1 : 0,            \
+                       status.data_ptr<int>());                                                                    \
+    break;
+    TM_ONESHOT_CASE(at::kFloat, float)
+    TM_ONESHOT_CASE(at::kDouble, double)
+    TM_ONESHOT_CASE(at::kLong, int64_t)
+    TM_ONESHOT_CASE(at::kInt, int32_t)
+#undef TM_ONESHOT_CASE
+    default:
+      TORCH_CHECK(false, "oneshot_allreduce: unsupported dtype ", inp.scalar_type());
+  }
+}
+
+int64_t oneshot_buffer_bytes(int64_t slot_bytes) {
+  return 2 * slot_bytes + 2LL * kMaxBlocks * kMaxRanks * static_cast<int64_t>(sizeof(uint32_t));
+}
+
+TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  // pointer / handle management takes no device tensor: catch-all kernels
+  m.def("ipc_buffer_alloc(int nbytes, int device) -> int", &ipc_buffer_alloc);
+  m.def("ipc_buffer_free(int ptr, int device) -> ()", &ipc_buffer_free);
+  m.def("ipc_get_handle(int ptr, int device) -> Tensor", &ipc_get_handle);
+  m.def("ipc_open_handle(Tensor handle, int device) -> int", &ipc_open_handle);
+  m.def("ipc_close_handle(int ptr, int device) -> ()", &ipc_close_handle);
+  m.def("oneshot_buffer_bytes(int slot_bytes) -> int", &oneshot_buffer_bytes);
+  m.def("ipc_view(int ptr, int nbytes, int device) -> Tensor", &ipc_view);
+  m.def(
+      "oneshot_allreduce(Tensor inp, Tensor(a!) out, Tensor peers, int rank, int slot_bytes, int epoch, int op, "
+      "bool publish, Tensor(b!) status) -> ()");
+}
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) { m.impl("oneshot_allreduce", &oneshot_allreduce); }
+
+}  // namespace tm_amd

@@ -6,37 +6,20 @@
 // here one block evaluates the per-output formulas, their zero-variance rules and the raw / uniform /
 // variance-weighted averaging in one launch.  Arithmetic stays in the states' dtype (as the reference's eager ops),
 // so the exact-zero tests (`numerator != 0`, `isclose(x, 0, atol=1e-4)`) see the same values.
-#include "../common/tm_common.h"
+#include "common/compute_bodies.h"
 
 namespace tm_amd {
 namespace {
 
-constexpr int kThreads = 256;
-enum Kind : int { kExplainedVariance = 0, kR2 = 1, kPearson = 2, kConcordance = 3 };
-enum MultiOut : int { kRaw = 0, kUniform = 1, kVarianceWeighted = 2 };
-enum NKind : int { kNScalar = 0, kNFloat = 1, kNDouble = 2, kNLong = 3 };
-
-template <typename T>
-__device__ __forceinline__ T load_n(const void* p, int kind, int idx, double scalar) {
-  switch (kind) {
-    case kNFloat: return static_cast<T>(static_cast<const float*>(p)[idx]);
-    case kNDouble: return static_cast<T>(static_cast<const double*>(p)[idx]);
-    case kNLong: return static_cast<T>(static_cast<const int64_t*>(p)[idx]);
-    default: return static_cast<T>(scalar);
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ T block_sum(T v, T* red) {
-  v = wave_sum(v);
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-  __syncthreads();
-  if (lane == 0) red[wave] = v;
-  __syncthreads();
-  T s = 0;
-  for (int w = 0; w < kThreads / kWave; ++w) s += red[w];
-  return s;
-}
+constexpr int kThreads = cbody::kThreads;
+using cbody::kExplainedVariance;
+using cbody::kNDouble;
+using cbody::kNFloat;
+using cbody::kNLong;
+using cbody::kNScalar;
+using cbody::kR2;
+using cbody::kRaw;
+using cbody::kVarianceWeighted;
 
 // s0..s4: per-kind state pointers (see the host function)
 template <typename T>
@@ -46,56 +29,8 @@ __global__ void __launch_bounds__(kThreads)
                               const void* __restrict__ n_ptr, int n_kind, int n_per_col, double n_scalar,
                               int multioutput, T bound, T* __restrict__ out) {
   __shared__ T red[kThreads / kWave];
-  T num_sum = 0, w_sum = 0, wscore = 0;
-  int low_var = 0;
-  for (int c = threadIdx.x; c < k; c += kThreads) {
-    const T n = load_n<T>(n_ptr, n_kind, n_per_col ? c : 0, n_scalar);
-    T score = 0, weight = 0;
-    if (kind == kExplainedVariance) {
-      // s0 = sum_error, s1 = sum_squared_error, s2 = sum_target, s3 = sum_squared_target
-      const T diff_avg = s0[c] / n;
-      const T numer = s1[c] / n - diff_avg * diff_avg;
-      const T tavg = s2[c] / n;
-      const T denom = s3[c] / n - tavg * tavg;
-      score = (numer != T(0) && denom != T(0)) ? T(1) - numer / denom : (numer != T(0) ? T(0) : T(1));
-      weight = denom;
-    } else if (kind == kR2) {
-      // s0 = sum_squared_obs, s1 = sum_obs, s2 = rss; nonzero = !isclose(x, 0, atol=1e-4) (NaN counts as nonzero)
-      const T mean = s1[c] / n;
-      const T tss = s0[c] - s1[c] * mean;
-      const T rss = s2[c];
-      const bool nz_rss = !(fabs(rss) <= T(1e-4)), nz_tss = !(fabs(tss) <= T(1e-4));
-      score = (nz_rss && nz_tss) ? T(1) - rss / tss : (nz_rss ? T(0) : T(1));
-      weight = tss;
-    } else {
-      // s0 = mean_x, s1 = mean_y, s2 = m2_x, s3 = m2_y, s4 = c_xy (sums of squared deviations)
-      const T vx = s2[c] / (n - T(1)), vy = s3[c] / (n - T(1)), cxy = s4[c] / (n - T(1));
-      low_var |= (vx < bound || vy < bound) ? 1 : 0;
-      T corr = cxy / sqrt(vx * vy);
-      corr = corr != corr ? corr : fmin(fmax(corr, T(-1)), T(1));
-      if (kind == kPearson) {
-        score = corr;
-      } else {
-        const T dm = s0[c] - s1[c];
-        score = T(2) * corr * sqrt(vx) * sqrt(vy) / (vx + vy + dm * dm);
-      }
-    }
-    out[c] = score;
-    num_sum += score;
-    w_sum += weight;
-    wscore += weight * score;
-  }
-  if (multioutput != kRaw) {
-    num_sum = block_sum(num_sum, red);
-    w_sum = block_sum(w_sum, red);
-    wscore = block_sum(wscore, red);
-  }
-  low_var = __syncthreads_or(low_var);
-  if (threadIdx.x == 0) {
-    out[k + 1] = low_var ? T(1) : T(0);
-    if (multioutput == kUniform) out[k] = num_sum / static_cast<T>(k);
-    else if (multioutput == kVarianceWeighted) out[k] = wscore / w_sum;
-  }
+  cbody::regression_compute_block<T>(kind, k, s0, s1, s2, s3, s4, n_ptr, n_kind, n_per_col, n_scalar, multioutput,
+                                     bound, out, red);
 }
 
 }  // namespace

@@ -310,7 +310,7 @@ def test_confmat_reduce_matches_cpu(C):
                                    _matthews_corrcoef_reduce(cm).float(), rtol=1e-5, atol=1e-6, equal_nan=True)
 
 
-@pytest.mark.parametrize("n_bins", [1, 15, 100])
+@pytest.mark.parametrize("n_bins", [1, 15, 16, 17, 100])
 def test_calibration_bins_matches_cpu(n_bins):
     from torchmetrics_amd.functional.classification.calibration_error import _binning_bucketize
 
@@ -496,18 +496,20 @@ def test_graphed_update_bound_input_ring():
 
 
 @pytest.mark.parametrize("norm", ["l1", "max", "l2"])
-@pytest.mark.parametrize("n_bins", [1, 15, 100])
-def test_calibration_error_compute_matches_cpu(norm, n_bins):
+@pytest.mark.parametrize("n_bins", [1, 15, 16, 17, 100])
+@pytest.mark.parametrize("n", [50000, 2000003])
+def test_calibration_error_compute_matches_cpu(norm, n_bins, n):
     from torchmetrics_amd.functional.classification.calibration_error import _ce_compute
 
     g = torch.Generator().manual_seed(n_bins + len(norm))
-    conf = torch.rand(50000, generator=g)
+    conf = torch.rand(n, generator=g)
     conf[:5] = 1.0
-    acc = (torch.rand(50000, generator=g) > 0.3).float()
-    ref = _ce_compute(conf, acc, n_bins, norm)
-    got = _ce_compute(conf.to(DEV), acc.to(DEV), n_bins, norm)
-    assert got.shape == ref.shape
-    torch.testing.assert_close(got.cpu().float(), ref.float(), rtol=1e-4, atol=1e-6)
+    acc = (torch.rand(n, generator=g) > 0.3).float()
+    ref = _ce_compute(conf.double(), acc.double(), n_bins, norm).float()
+    for _ in range(2):  # the second call reuses the (self-clearing) bin workspace
+        got = _ce_compute(conf.to(DEV), acc.to(DEV), n_bins, norm)
+        assert got.shape == ref.shape
+        torch.testing.assert_close(got.cpu().float(), ref, rtol=1e-4, atol=1e-6)
 
 
 @pytest.mark.parametrize("C", [3, 10, 32, 33])

@@ -1,0 +1,156 @@
+"""One-shot xGMI all-reduce kernel (``csrc/comm/oneshot_allreduce.hip``).
+
+* simulated peers on one device: W buffers on cuda:0, the other ranks' data and flags pre-written, our rank's kernel
+  publishes, signals and reduces -> compared with a plain torch reduction of the W inputs (fp32/fp64 in rank order);
+* a missing peer ends in the timeout status instead of a hang;
+* two real processes on one device exchange IPC handles over gloo and reduce through each other's buffers; the
+  engine's reduce bucket routed through the same communicator gives the gloo all_reduce's result.
+"""
+import pytest
+import torch
+
+from tests.helpers import run_ddp
+
+pytestmark = pytest.mark.gpu
+
+SLOT = 256 * 1024
+MAXB, MAXR = 64, 16
+
+
+def _ops():
+    from torchmetrics_amd import ops
+
+    return ops._ops()
+
+
+def _plan_blocks(n, esize):
+    bytes_ = n * esize
+    blocks = min(MAXB, (bytes_ + 4095) // 4096)
+    chunk = (n + blocks - 1) // blocks
+    chunk = (chunk + 63) // 64 * 64
+    return (n + chunk - 1) // chunk
+
+
+class _SimPeers:
+    def __init__(self, world):
+        o = _ops()
+        self.world = world
+        self.total = int(o.oneshot_buffer_bytes(SLOT))
+        self.ptrs = [int(o.ipc_buffer_alloc(self.total, 0)) for _ in range(world)]
+        self.views = [o.ipc_view(p, self.total, 0) for p in self.ptrs]
+
+    def data(self, r, parity, dtype, n):
+        v = self.views[r][parity * SLOT : parity * SLOT + n * torch.empty(0, dtype=dtype).element_size()]
+        return v.view(dtype)
+
+    def flags(self, r):
+        return self.views[r][2 * SLOT :].view(torch.int32).view(2, MAXB, MAXR)
+
+    def close(self):
+        o = _ops()
+        torch.cuda.synchronize()
+        for p in self.ptrs:
+            o.ipc_buffer_free(p, 0)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.int64, torch.int32])
+@pytest.mark.parametrize("n", [1, 63, 1000, 20000])
+def test_simulated_peers(world, dtype, n):
+    o = _ops()
+    sim = _SimPeers(world)
+    try:
+        me = world - 1
+        g = torch.Generator().manual_seed(n + world)
+        if dtype.is_floating_point:
+            inputs = [torch.randn(n, generator=g, dtype=torch.float64).to(dtype) for _ in range(world)]
+        else:
+            inputs = [torch.randint(-1000, 1000, (n,), generator=g).to(dtype) for _ in range(world)]
+        for epoch in (1, 2, 3):
+            parity = epoch & 1
+            nb = _plan_blocks(n, inputs[0].element_size())
+            for r in range(world):
+                if r != me:
+                    sim.data(r, parity, dtype, n).copy_(inputs[r].cuda())
+                    sim.flags(me)[parity, :nb, r] = epoch
+            status = torch.zeros(1, dtype=torch.int32, device="cuda")
+            for op_name, op in (("sum", 0), ("max", 1), ("min", 2)):
+                out = torch.empty(n, dtype=dtype, device="cuda")
+                peers = torch.tensor(sim.ptrs, dtype=torch.int64)
+                o.oneshot_allreduce(inputs[me].cuda(), out, peers, me, SLOT, epoch, op, True, status)
+                torch.cuda.synchronize()
+                assert int(status.item()) == 0
+                stack = torch.stack(inputs)
+                if op_name == "sum":
+                    ref = stack[0].clone()
+                    for r in range(1, world):
+                        ref = ref + stack[r]  # rank order, same rounding as the kernel
+                elif op_name == "max":
+                    ref = stack.max(0).values
+                else:
+                    ref = stack.min(0).values
+                assert torch.equal(out.cpu(), ref), (op_name, epoch)
+                # our rank published its data and raised its flag in every peer's array
+                assert torch.equal(sim.data(me, parity, dtype, n).cpu(), inputs[me])
+                for p in range(world):
+                    assert bool((sim.flags(p)[parity, :nb, me] == epoch).all().item())
+    finally:
+        sim.close()
+
+
+def test_missing_peer_times_out_without_hanging():
+    o = _ops()
+    sim = _SimPeers(2)
+    try:
+        status = torch.zeros(1, dtype=torch.int32, device="cuda")
+        out = torch.empty(16, dtype=torch.float32, device="cuda")
+        peers = torch.tensor(sim.ptrs, dtype=torch.int64)
+        o.oneshot_allreduce(torch.ones(16, device="cuda"), out, peers, 0, SLOT, 1, 0, True, status)  # rank 1 absent
+        torch.cuda.synchronize()
+        assert int(status.item()) == 1
+    finally:
+        sim.close()
+
+
+# ------------------------------------------------------------------------------ two processes sharing one device
+def _body_two_procs(rank, world):
+    import torch.distributed as dist
+
+    from torchmetrics_amd.parallel import sync
+    from torchmetrics_amd.parallel.oneshot import OneShotAllReduce
+
+    torch.cuda.set_device(0)
+    comm = OneShotAllReduce(None, allow_shared_device=True)
+    assert comm.usable, "IPC handles could not be opened"
+    try:
+        for step in range(5):
+            g = torch.Generator().manual_seed(100 * step + rank)
+            x = torch.randn(3000 + step, generator=g, dtype=torch.float64)
+            ref = x.clone()
+            dist.all_reduce(ref)  # gloo on the host
+            buf = x.cuda()
+            comm.all_reduce(buf, "sum")
+            torch.cuda.synchronize()
+            torch.testing.assert_close(buf.cpu(), ref, rtol=1e-12, atol=1e-12)
+        comm.check()
+        # the engine's reduce bucket through the same communicator (sum / max states, int64 + float32)
+        sync._is_nccl = lambda group: True
+        sync.get_oneshot = lambda group: comm
+        from torchmetrics_amd.utilities.data import dim_zero_max, dim_zero_sum
+
+        tp = torch.arange(10, dtype=torch.int64, device="cuda") * (rank + 1)
+        mx = torch.full((4,), float(rank), device="cuda")
+        sync.comm_stats(reset=True)
+        out = sync.sync_state_dicts([({"tp": tp, "mx": mx}, {"tp": dim_zero_sum, "mx": dim_zero_max})])[0]
+        assert torch.equal(out["tp"].cpu(), torch.arange(10) * 3)
+        assert torch.equal(out["mx"].cpu(), torch.full((4,), 1.0))
+        assert sync.comm_stats()["oneshot_all_reduce"] == 2
+        comm.check()
+    finally:
+        torch.cuda.synchronize()
+        dist.barrier()
+        comm.close()
+
+
+def test_two_processes_one_device():
+    run_ddp(_body_two_procs)

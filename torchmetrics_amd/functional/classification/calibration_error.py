@@ -35,6 +35,9 @@ def _binning_bucketize(confidences: Tensor, accuracies: Tensor, bin_boundaries: 
     return acc_bin, conf_bin, prop_bin
 
 
+_BOUNDARIES: dict = {}  # (n_bins, dtype, device) -> linspace(0, 1, n_bins + 1): one launch saved per compute()
+
+
 def _ce_compute(
     confidences: Tensor,
     accuracies: Tensor,
@@ -43,7 +46,12 @@ def _ce_compute(
     debias: bool = False,
 ) -> Tensor:
     if isinstance(bin_boundaries, int):
-        bin_boundaries = torch.linspace(0, 1, bin_boundaries + 1, dtype=confidences.dtype, device=confidences.device)
+        key = (bin_boundaries, confidences.dtype, confidences.device)
+        cached = _BOUNDARIES.get(key)
+        if cached is None:
+            cached = _BOUNDARIES[key] = torch.linspace(0, 1, bin_boundaries + 1, dtype=confidences.dtype,
+                                                       device=confidences.device)
+        bin_boundaries = cached
     if norm not in {"l1", "l2", "max"}:
         raise ValueError(f"Argument `norm` is expected to be one of 'l1', 'l2', 'max' but got {norm}")
     if (norm != "l2" and confidences.is_cuda and confidences.dtype == torch.float32

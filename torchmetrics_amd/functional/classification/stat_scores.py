@@ -341,6 +341,10 @@ def _multiclass_stat_scores_update(
 def _multiclass_stat_scores_compute(
     tp: Tensor, fp: Tensor, tn: Tensor, fn: Tensor, average: Optional[str] = "macro", multidim_average: str = "global"
 ) -> Tensor:
+    if multidim_average == "global" and ops._RECORDER is not None:  # one task of the fused compute launch
+        fused = ops.stat_scores_output(tp, fp, tn, fn, average)
+        if fused is not None:
+            return fused
     res = torch.stack([tp, fp, tn, fn, tp + fn], dim=-1)
     sum_dim = 0 if multidim_average == "global" else 1
     if average == "micro":
@@ -379,6 +383,10 @@ def _multilabel_stat_scores_update(
 def _multilabel_stat_scores_compute(
     tp: Tensor, fp: Tensor, tn: Tensor, fn: Tensor, average: Optional[str] = "macro", multidim_average: str = "global"
 ) -> Tensor:
+    if multidim_average == "global" and ops._RECORDER is not None:  # one task of the fused compute launch
+        fused = ops.stat_scores_output(tp, fp, tn, fn, average)
+        if fused is not None:
+            return fused
     res = torch.stack([tp, fp, tn, fn, tp + fn], dim=-1)
     sum_dim = 0 if multidim_average == "global" else 1
     if average == "micro":

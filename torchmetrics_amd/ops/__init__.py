@@ -11,6 +11,7 @@ Every op has exactly two implementations, selected by the *device of its inputs*
   device implementation of the same contract (used by CPU/gloo runs and as the numerics oracle in tests).
 """
 import os
+import struct
 import threading
 from pathlib import Path
 from typing import Optional, Sequence, Union
@@ -455,6 +456,107 @@ def feature_moments_update(features: Tensor, feat_sum: Tensor, feat_cov: Tensor)
         _cpu.feature_moments_update(features, feat_sum, feat_cov)
 
 
+# ------------------------------------------------------------------------------ fused compute() of a collection
+class _TaskRecorder:
+    """Records the one-block reductions of ``stat_reduce`` / ``confmat_reduce`` / ``curve_score`` /
+    ``regression_compute`` as task descriptors; :meth:`flush` runs all of them in ONE launch
+    (``csrc/common/compute_tasks.hip``).  Output tensors are allocated at record time, so the callers get their
+    results as views of tensors the flush fills."""
+
+    def __init__(self, poison: bool = False) -> None:
+        self.rows: list = []
+        self.keep: list = []
+        self.lds = 0
+        self.anchor: Optional[Tensor] = None
+        self.poison = poison
+
+    def add(self, kind: int, blocks: int, ints: Sequence[int], floats: Sequence[float], tensors: Sequence[Optional[Tensor]],
+            outs: Sequence[Tensor], lds: int) -> None:
+        row = [kind, blocks] + [int(v) for v in ints] + [0] * (6 - len(ints))
+        fl = list(floats) + [0.0] * (2 - len(floats))
+        row += [struct.unpack("<q", struct.pack("<d", float(v)))[0] for v in fl]
+        ptrs = [t.data_ptr() if t is not None else 0 for t in tensors]
+        row += ptrs + [0] * (8 - len(ptrs))
+        self.rows.append(row)
+        self.keep.extend(t for t in tensors if t is not None)
+        self.lds = max(self.lds, lds)
+        if self.anchor is None:
+            self.anchor = outs[0]
+        if self.poison:
+            for o in outs:
+                o.fill_(float("nan") if o.is_floating_point() else -(2**30))
+
+    def flush(self) -> int:
+        """Launch the recorded tasks (``ceil(n / 32)`` launches); returns the number of tasks."""
+        n = len(self.rows)
+        for i in range(0, n, 32):
+            desc = torch.tensor(self.rows[i : i + 32], dtype=torch.int64)
+            _ops().compute_tasks(desc, self.anchor, self.lds)
+        self.rows, self.keep = [], []
+        return n
+
+
+_RECORDER: Optional[_TaskRecorder] = None
+
+
+class fused_compute:  # noqa: N801 - context manager
+    """``with ops.fused_compute() as rec: ...; rec.flush()`` -- record instead of launching the fused reductions."""
+
+    def __init__(self, poison: bool = False) -> None:
+        self.rec = _TaskRecorder(poison)
+
+    def __enter__(self) -> _TaskRecorder:
+        global _RECORDER
+        self._prev = _RECORDER
+        _RECORDER = self.rec
+        return self.rec
+
+    def __exit__(self, *exc) -> None:
+        global _RECORDER
+        _RECORDER = self._prev
+
+
+_TASK_STAT, _TASK_CONFMAT, _TASK_CURVE, _TASK_REG_F32, _TASK_REG_F64 = 0, 1, 2, 3, 4
+_TASK_RATIO_F32, _TASK_RATIO_F64, _TASK_STAT_SCORES = 5, 6, 7
+_N_KIND = {torch.float32: 1, torch.float64: 2, torch.int64: 3}
+
+
+def ratio(a: Tensor, b: Union[Tensor, int, float], take_sqrt: bool = False) -> Tensor:
+    """``a / b`` (then ``sqrt``): the compute() of MSE / RMSE / MAE and similar running-sum metrics.  Eager ATen
+    ops normally; inside :class:`fused_compute` a task of the one-launch compute kernel."""
+    rec = _RECORDER
+    if (rec is not None and isinstance(b, Tensor) and a.is_cuda and b.is_cuda and a.dtype in (torch.float32, torch.float64)
+            and (b.dtype == torch.int64 or b.dtype == a.dtype) and a.is_contiguous() and b.is_contiguous()
+            and 1 <= a.numel() <= (1 << 20) and (b.dim() == 0 or b.shape == a.shape)):
+        out = torch.empty_like(a, memory_format=torch.contiguous_format)
+        rec.add(_TASK_RATIO_F32 if a.dtype == torch.float32 else _TASK_RATIO_F64, 1,
+                [a.numel(), _N_KIND[b.dtype], 1 if (b.dim() > 0 and b.numel() > 1) else 0, int(bool(take_sqrt))], [],
+                [a, b, out], [out], 0)
+        return out
+    r = a / b
+    return torch.sqrt(r) if take_sqrt else r
+
+
+def stat_scores_output(tp: Tensor, fp: Tensor, tn: Tensor, fn: Tensor, average: Optional[str]) -> Optional[Tensor]:
+    """Recorded StatScores compute (global multidim, micro / macro / none) inside :class:`fused_compute`; None when
+    not recording or not applicable (the caller then runs its ATen ops)."""
+    rec = _RECORDER
+    if rec is None or not tp.is_cuda or tp.dim() != 1 or average not in ("micro", "macro", "none", None):
+        return None
+    if not all(t.dtype == torch.int64 and t.is_contiguous() and t.shape == tp.shape for t in (tp, fp, tn, fn)):
+        return None
+    c = tp.numel()
+    if c < 1:
+        return None
+    avg = {"micro": 0, "macro": 1}.get(average, 3)
+    if avg == 3:
+        out = torch.empty(c, 5, dtype=torch.int64, device=tp.device)
+    else:
+        out = torch.empty(5, dtype=torch.float32 if avg == 1 else torch.int64, device=tp.device)
+    rec.add(_TASK_STAT_SCORES, 1, [c, avg], [], [tp, fp, tn, fn, out], [out], 0)
+    return out
+
+
 # --------------------------------------------------------------------------------------- confmat reductions
 CM_JACCARD, CM_KAPPA, CM_MCC = 0, 1, 2
 _CM_AVG = {"micro": 0, "macro": 1, "weighted": 2, "none": 3, None: 3}
@@ -472,8 +574,14 @@ def confmat_reduce(confmat: Tensor, kind: int, average: Optional[str] = "macro",
     (``csrc/classification/confmat_reduce.hip``).  Jaccard returns the per-class ``[C]`` vector for average none."""
     c = confmat.shape[0]
     out = torch.empty(c + 1, dtype=torch.float32, device=confmat.device)
-    (_fast_mod or _fast()).confmat_reduce(confmat.contiguous(), kind, _CM_AVG[average],
-                                          -1 if ignore_index is None else int(ignore_index), _KAPPA_W[weights], out)
+    rec = _RECORDER
+    if rec is not None and confmat.is_cuda and confmat_reducible(confmat):
+        cm = confmat.contiguous()
+        rec.add(_TASK_CONFMAT, 1, [c, kind, _CM_AVG[average], -1 if ignore_index is None else int(ignore_index),
+                                   _KAPPA_W[weights]], [], [cm, out], [out], 3 * c * 8)
+    else:
+        (_fast_mod or _fast()).confmat_reduce(confmat.contiguous(), kind, _CM_AVG[average],
+                                              -1 if ignore_index is None else int(ignore_index), _KAPPA_W[weights], out)
     if kind == CM_JACCARD:
         return out[:c] if average in (None, "none") else out[c]
     return out[0]
@@ -520,18 +628,46 @@ def regression_compute(kind: int, states: Sequence[Tensor], n: Union[Tensor, int
     ``multioutput`` average and the low-variance flag (Pearson / concordance)."""
     s0 = states[0]
     out = torch.empty(s0.numel() + 2, dtype=s0.dtype, device=s0.device)
-    if isinstance(n, Tensor):
+    rec = _RECORDER
+    if rec is not None and s0.is_cuda and regression_computable(states, n):
+        k = s0.numel()
+        need = {REG_EV: 4, REG_R2: 3}.get(kind, 5)
+        st = list(states[:need]) + [states[0]] * (5 - need)
+        if isinstance(n, Tensor):
+            n_kind = {torch.float32: 1, torch.float64: 2, torch.int64: 3}[n.dtype]
+            n_per_col = 1 if (n.numel() == k and k > 1) else 0
+            n_t, n_val = n, 0.0
+        else:
+            n_kind, n_per_col, n_t, n_val = 0, 0, None, float(n)
+        rec.add(_TASK_REG_F32 if s0.dtype == torch.float32 else _TASK_REG_F64, 1,
+                [kind, k, n_kind, n_per_col, int(multioutput)], [n_val, bound], st + [n_t, out], [out], 0)
+    elif isinstance(n, Tensor):
         (_fast_mod or _fast()).regression_compute(kind, states, n, 0.0, multioutput, bound, out)
     else:
         (_fast_mod or _fast()).regression_compute(kind, states, None, float(n), multioutput, bound, out)
     return out
 
 
+_CALIB_WS: dict = {}
+
+
 def calibration_error_l1_max(conf: Tensor, acc: Tensor, bounds: Tensor, norm: str) -> Tensor:
-    """``l1`` / ``max`` calibration error of ROCm f32 confidences in two launches (bins + one-block reduce)."""
-    sums = calibration_bins(conf, acc, bounds)
+    """``l1`` / ``max`` calibration error of ROCm f32 confidences in two launches (bins + one-block reduce).
+
+    The (count, Σconf, Σacc) bins live in a per-(n_bins, device, stream) workspace that the reduce kernel zeroes
+    after reading it: no allocation or fill launch per compute()."""
+    nb = bounds.numel()
+    key = (nb, conf.device, torch.cuda.current_stream(conf.device).cuda_stream)
+    ws = _CALIB_WS.get(key)
+    if ws is None:
+        ws = _CALIB_WS[key] = (torch.zeros(nb, 3, dtype=torch.float32, device=conf.device),
+                               torch.zeros(1, dtype=torch.int32, device=conf.device))
+    sums, bad = ws
+    b = bounds if (bounds.dtype == torch.float32 and bounds.is_contiguous()) else bounds.float().contiguous()
+    f = _fast_mod or _fast()
+    f.calibration_bins(conf.contiguous(), acc.contiguous(), b, sums, bad)
     out = torch.empty(1, dtype=torch.float32, device=conf.device)
-    (_fast_mod or _fast()).calibration_reduce(sums, 0 if norm == "l1" else 1, out)
+    f.calibration_reduce_clear(sums, 0 if norm == "l1" else 1, out)
     return out[0]
 
 
@@ -548,8 +684,13 @@ def curve_score(state: Tensor, kind: int, average: Optional[str]) -> "tuple[Tens
     c = state.shape[1]
     out = torch.empty(c + 1, dtype=torch.float32, device=state.device)
     flag = torch.empty(1, dtype=torch.int32, device=state.device)
-    (_fast_mod or _fast()).curve_score(state if state.is_contiguous() else state.contiguous(), kind,
-                                       _AVG_IDS[average], out, flag)
+    st = state if state.is_contiguous() else state.contiguous()
+    rec = _RECORDER
+    if (rec is not None and st.is_cuda and st.dtype == torch.int64 and st.dim() == 4 and st.shape[2:] == (2, 2)
+            and st.shape[0] >= 1 and 1 <= c <= 16384):
+        rec.add(_TASK_CURVE, 1, [st.shape[0], c, kind, _AVG_IDS[average]], [], [st, out, flag], [out, flag], 8 * c)
+    else:
+        (_fast_mod or _fast()).curve_score(st, kind, _AVG_IDS[average], out, flag)
     return out[:c], out[c], flag
 
 
@@ -844,7 +985,14 @@ def stat_reduce(tp: Tensor, fp: Tensor, tn: Tensor, fn: Tensor, kind: int, avera
     """Fused stat-score compute on ``[R, C]`` int64 states (``csrc/classification/stat_reduce.hip``): ``[R]`` for
     micro / macro / weighted (ids 0 / 1 / 2), ``[R, C]`` for none (3)."""
     out = torch.empty(tp.shape[0] * (tp.shape[1] if average == 3 else 1), dtype=torch.float32, device=tp.device)
-    (_fast_mod or _fast()).stat_reduce(tp, fp, tn, fn, out, kind, average, multilabel, float(beta))
+    rec = _RECORDER
+    if (rec is not None and tp.is_cuda and tp.dim() == 2 and tp.shape[0] >= 1
+            and all(t.dtype == torch.int64 and t.is_contiguous() and t.shape == tp.shape for t in (tp, fp, tn, fn))
+            and 0 <= kind <= 5 and 0 <= average <= 3):
+        rec.add(_TASK_STAT, tp.shape[0], [tp.shape[1], kind, average, int(bool(multilabel))], [float(beta) ** 2],
+                [tp, fp, tn, fn, out], [out], 0)
+    else:
+        (_fast_mod or _fast()).stat_reduce(tp, fp, tn, fn, out, kind, average, multilabel, float(beta))
     return out.reshape(tp.shape[0], -1) if average == 3 else out
 
 

@@ -1,0 +1,157 @@
+"""One-shot intra-node all-reduce over xGMI peer reads (``csrc/comm/oneshot_allreduce.hip``).
+
+Used by the sync engine (:mod:`torchmetrics_amd.parallel.sync`) for reduce buckets of at most ``slot_bytes``
+(256 KiB by default) when the process group runs on RCCL and every rank of it lives on this node.  Per call: one
+kernel per rank, no host round trip.  Every rank publishes its bucket in a buffer the peers have mapped, raises a
+flag in each peer's flag array and reduces the W copies straight out of the peers' HBM (rank order, so every rank
+gets bit-identical sums).  Larger buckets (FID's 32 MiB covariances) stay on RCCL's ring, which is per-link
+bandwidth-bound; the one-shot path is latency-bound and wins below a few hundred KiB.
+
+The reference has no counterpart (it gathers each state with ``barrier`` + 2 ``all_gather``,
+``S/utilities/distributed.py:97-147``); SURVEY.md §2.2 / §7.1.5 asks for this path.
+
+Setup (once per process group): every rank ``hipMalloc``s one buffer, exports it with ``hipIpcGetMemHandle`` and the
+handles are exchanged with ``all_gather_object``; peers open them with ``hipIpcOpenMemHandle``.  Setup also checks
+that all ranks are on one host and on distinct devices; otherwise the path is disabled for that group.
+"""
+import os
+import socket
+import threading
+from typing import Any, Dict, Optional
+
+import torch
+import torch.distributed as dist
+from torch import Tensor
+
+_OPS = {"sum": 0, "mean": 0, "max": 1, "min": 2}
+_DTYPES = (torch.float32, torch.float64, torch.int64, torch.int32)
+DEFAULT_SLOT_BYTES = 256 * 1024
+
+
+def _enabled_by_env() -> bool:
+    return os.environ.get("TORCHMETRICS_AMD_ONESHOT", "1") not in ("0", "false", "False")
+
+
+class OneShotAllReduce:
+    """Peer-mapped buffers of one process group plus the call counter (``epoch``) that pairs the ranks' flags.
+
+    Args:
+        group: the process group (``None`` = WORLD).
+        slot_bytes: the largest bucket this communicator reduces.
+        allow_shared_device: permit several ranks on one device (test harness only; RCCL itself refuses it).
+    """
+
+    def __init__(self, group: Optional[Any] = None, slot_bytes: int = DEFAULT_SLOT_BYTES,
+                 allow_shared_device: bool = False) -> None:
+        from torchmetrics_amd import ops
+
+        self._ops = ops._ops()
+        self.group = group
+        self.slot_bytes = int(slot_bytes)
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = torch.device("cuda", torch.cuda.current_device())
+        dev = self.device.index
+        self._own = int(self._ops.ipc_buffer_alloc(int(self._ops.oneshot_buffer_bytes(self.slot_bytes)), dev))
+        handle = self._ops.ipc_get_handle(self._own, dev)
+        info = (socket.gethostname(), dev, os.getpid(), handle.tolist())
+        infos: list = [None] * self.world
+        dist.all_gather_object(infos, info, group=group)
+        same_host = all(i[0] == infos[0][0] for i in infos)
+        distinct = len({i[1] for i in infos}) == self.world
+        self.usable = bool(same_host and (distinct or allow_shared_device) and self.world <= 16)
+        self._opened = []
+        ptrs = []
+        ok = self.usable
+        if ok:
+            try:
+                for r, i in enumerate(infos):
+                    if r == self.rank:
+                        ptrs.append(self._own)
+                    else:
+                        p = int(self._ops.ipc_open_handle(torch.tensor(i[3], dtype=torch.uint8), dev))
+                        self._opened.append(p)
+                        ptrs.append(p)
+            except RuntimeError:
+                ok = False
+        # every rank must take the same path: agree on the outcome (MIN over ranks)
+        flag_dev = self.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        agree = torch.tensor([1 if ok else 0], dtype=torch.int32, device=flag_dev)
+        dist.all_reduce(agree, op=dist.ReduceOp.MIN, group=group)
+        self.usable = bool(int(agree.item()))
+        self._peers = torch.tensor(ptrs or [self._own], dtype=torch.int64)
+        self._status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.epoch = 0
+        self.calls = 0
+
+    def supports(self, buf: Tensor) -> bool:
+        return (
+            self.usable
+            and buf.device == self.device
+            and buf.dtype in _DTYPES
+            and buf.numel() * buf.element_size() <= self.slot_bytes
+            and not torch.cuda.is_current_stream_capturing()  # the epoch is a launch argument
+        )
+
+    def all_reduce(self, buf: Tensor, op: str = "sum") -> Tensor:
+        """In-place reduction of a contiguous 1-D ``buf`` across the group (``mean`` is left as a sum)."""
+        self.epoch += 1
+        if self.epoch >= 2**32 - 1:
+            raise RuntimeError("one-shot all-reduce: epoch counter exhausted")
+        inp = buf.contiguous()
+        self._ops.oneshot_allreduce(inp, buf, self._peers, self.rank, self.slot_bytes, self.epoch, _OPS[op], True,
+                                    self._status)
+        self.calls += 1
+        return buf
+
+    def check(self) -> None:
+        """Raise if a wait for a peer ever timed out (reads the status word: one device sync)."""
+        if int(self._status.item()) != 0:
+            raise RuntimeError("one-shot all-reduce: a peer did not arrive within 2 s; results are invalid")
+
+    def close(self) -> None:
+        dev = self.device.index
+        for p in self._opened:
+            self._ops.ipc_close_handle(p, dev)
+        self._opened = []
+        if self._own:
+            self._ops.ipc_buffer_free(self._own, dev)
+            self._own = 0
+        self.usable = False
+
+
+_registry: Dict[Any, Optional[OneShotAllReduce]] = {}
+_lock = threading.Lock()
+
+
+def get_oneshot(group: Optional[Any] = None) -> Optional[OneShotAllReduce]:
+    """The group's communicator (created collectively on first use), or ``None`` where the path does not apply.
+
+    Every rank reaches this call at the same point of the engine's collective sequence (the decision depends only on
+    the backend, the env switch and the bucket size, which agree across ranks), so the setup collective is safe.
+    """
+    key = id(group) if group is not None else None
+    with _lock:
+        if key in _registry:
+            comm = _registry[key]
+            return comm if comm is not None and comm.usable else None
+    comm = None
+    if _enabled_by_env() and torch.cuda.is_available():
+        from torchmetrics_amd import ops
+
+        if ops.load_native(strict=False):
+            comm = OneShotAllReduce(group)  # collective; ranks agree on `usable` inside
+    with _lock:
+        _registry[key] = comm
+    return comm if comm is not None and comm.usable else None
+
+
+def reset_registry() -> None:
+    with _lock:
+        for c in _registry.values():
+            if c is not None:
+                c.close()
+        _registry.clear()
+
+
+__all__ = ["OneShotAllReduce", "get_oneshot", "reset_registry", "DEFAULT_SLOT_BYTES"]

@@ -10,9 +10,11 @@ This engine keeps the exact *result* semantics but changes the communication pla
   ``(op, dtype, device)`` into one flat buffer and reduced with ONE ``all_reduce`` per bucket (mean = sum / W).
   No metadata, no host sync, no barrier.  A whole ``MetricCollection`` (all compute groups) is synced in one call,
   so a 20-metric collection costs ~2 collectives instead of ~3x(#states).
-* **gather bucket** -- ``cat``, ``None`` and custom-callable states. One small metadata ``all_gather`` (element
-  counts + shapes; one device->host copy), then ONE ``all_gather`` of the packed payload per dtype, padded only to the
-  largest rank's payload (not per-dimension to the max shape).  Partially-empty list states do not hang (the
+* **one-shot path** -- on RCCL, reduce buckets of <= 256 KiB (every classification / regression state) skip the
+  ring: one peer-read kernel over xGMI (:mod:`torchmetrics_amd.parallel.oneshot`).
+* **gather bucket** -- ``cat``, ``None`` and custom-callable states. One fixed-size metadata header per rank (element
+  counts, dtype codes and shapes: one ``all_gather``, one device->host copy), then ONE ``all_gather`` of the packed
+  payload per dtype, padded only to the largest rank's payload (not per-dimension to the max shape).  Partially-empty list states do not hang (the
   reference's collective sequence diverges in that case, ``T/bases/test_ddp.py:269-279``).
 
 Ordering guarantees (identical to the reference):
@@ -29,6 +31,7 @@ import torch
 import torch.distributed as dist
 from torch import Tensor
 
+from torchmetrics_amd.parallel.oneshot import get_oneshot
 from torchmetrics_amd.utilities.data import (
     _flatten,
     dim_zero_cat,
@@ -55,7 +58,7 @@ _DTYPE_CODES = [
     torch.uint8, torch.bool, torch.complex64, torch.complex128,
 ]
 
-_stats = {"all_reduce": 0, "all_gather": 0, "meta_all_gather": 0, "bytes": 0}
+_stats = {"all_reduce": 0, "oneshot_all_reduce": 0, "all_gather": 0, "meta_all_gather": 0, "bytes": 0}
 
 
 def comm_stats(reset: bool = False) -> Dict[str, int]:
@@ -164,7 +167,13 @@ def sync_state_dicts(
         else:
             flat = torch.cat([t.reshape(-1).to(wire) for _, t in members])
         if world > 1:
-            _all_reduce(flat, kind, group)
+            comm = get_oneshot(group) if (flat.is_cuda and _is_nccl(group)) else None
+            if comm is not None and comm.supports(flat):
+                comm.all_reduce(flat, kind)  # one peer-read kernel over xGMI
+                _stats["oneshot_all_reduce"] += 1
+                _stats["bytes"] += flat.numel() * flat.element_size()
+            else:
+                _all_reduce(flat, kind, group)
         off = 0
         for (mi, name), t in members:
             n = t.numel()
@@ -191,7 +200,10 @@ def _gather_items(items: List[_GatherItem], world: int, group: Optional[Any]) ->
     if world == 1:
         return [[it.elems] for it in items]
     dev = _comm_device(items, group)
-    # metadata: [n_elems per item] ++ [ndim, *shape per element] ; lengths differ across ranks -> two phases
+    # metadata in ONE fixed-size header per rank (one all_gather, one device->host copy):
+    #   [n_elems per item] ++ [dtype code per item] ++ [meta_len] ++ [ndim, *shape per element] (zero padded)
+    # Every rank derives the same header length from the item count; a rank whose shapes do not fit writes
+    # meta_len = -(needed) and the shapes travel in a second, exactly sized all_gather (rare: many-element lists).
     counts = [len(it.elems) for it in items]
     shape_meta: List[int] = []
     dtypes: List[torch.dtype] = []
@@ -200,26 +212,34 @@ def _gather_items(items: List[_GatherItem], world: int, group: Optional[Any]) ->
             shape_meta.append(e.ndim)
             shape_meta.extend(e.shape)
     codes = [_DTYPE_CODES.index(it.elems[0].dtype) if it.elems else -1 for it in items]
-    header = torch.tensor(counts + codes + [len(shape_meta)], dtype=torch.int64, device=dev)
-    all_headers = _all_gather_flat(header, world, group).cpu()
+    n_it = len(items)
+    cap = max(256, 8 * n_it)
+    fits = len(shape_meta) <= cap
+    header = torch.zeros(2 * n_it + 1 + cap, dtype=torch.int64)
+    header[: 2 * n_it] = torch.tensor(counts + codes, dtype=torch.int64)
+    header[2 * n_it] = len(shape_meta) if fits else -len(shape_meta)
+    if fits and shape_meta:
+        header[2 * n_it + 1 : 2 * n_it + 1 + len(shape_meta)] = torch.tensor(shape_meta, dtype=torch.int64)
+    hdr = _all_gather_flat(header.to(dev), world, group).cpu().tolist()
     _stats["meta_all_gather"] += 1
-    max_meta = int(all_headers[:, -1].max())
-    meta = torch.zeros(max_meta, dtype=torch.int64)
-    if shape_meta:
+    if any(h[2 * n_it] < 0 for h in hdr):
+        max_meta = max(abs(h[2 * n_it]) for h in hdr)
+        meta = torch.zeros(max_meta, dtype=torch.int64)
         meta[: len(shape_meta)] = torch.tensor(shape_meta, dtype=torch.int64)
-    all_meta = _all_gather_flat(meta.to(dev), world, group).cpu() if max_meta else torch.zeros(world, 0, dtype=torch.int64)
-    _stats["meta_all_gather"] += 1
+        all_meta = _all_gather_flat(meta.to(dev), world, group).cpu().tolist()
+        _stats["meta_all_gather"] += 1
+    else:
+        all_meta = [h[2 * n_it + 1 :] for h in hdr]
 
     # decode every rank's shapes
     shapes: List[List[List[Tuple[int, ...]]]] = []  # [rank][item][elem] -> shape
     for r in range(world):
-        row = all_meta[r].tolist()
+        row = all_meta[r]
         pos = 0
         per_item = []
-        for i, _ in enumerate(items):
-            n_el = int(all_headers[r, i])
+        for i in range(n_it):
             el_shapes = []
-            for _ in range(n_el):
+            for _ in range(hdr[r][i]):
                 nd = row[pos]
                 el_shapes.append(tuple(row[pos + 1 : pos + 1 + nd]))
                 pos += 1 + nd
@@ -228,9 +248,8 @@ def _gather_items(items: List[_GatherItem], world: int, group: Optional[Any]) ->
 
     # element dtype per item: the first rank that holds an element decides (a locally-empty list has no dtype),
     # so every rank builds the same dtype buckets and issues the same collective sequence
-    n_it = len(items)
     for i in range(n_it):
-        code = next((int(all_headers[r, n_it + i]) for r in range(world) if int(all_headers[r, n_it + i]) >= 0), -1)
+        code = next((hdr[r][n_it + i] for r in range(world) if hdr[r][n_it + i] >= 0), -1)
         dtypes.append(_DTYPE_CODES[code] if code >= 0 else torch.float32)
 
     out: List[List[List[Tensor]]] = [[[] for _ in range(world)] for _ in items]

@@ -34,6 +34,65 @@ def test_bootstrapper_matches_manual_resampling(device, strategy):
     assert out["quantile"].shape == (2,)
 
 
+def test_bootstrapper_reference_docstring_values():
+    """Golden value of reference ``S/wrappers/bootstrapping.py:76-86`` (same seed -> same replicates)."""
+    torch.manual_seed(123)
+    bootstrap = tm.BootStrapper(tm.MulticlassAccuracy(num_classes=5, average="micro"), num_bootstraps=20)
+    bootstrap.update(torch.randint(5, (20,)), torch.randint(5, (20,)))
+    out = bootstrap.compute()
+    assert set(out) == {"mean", "std"}
+    assert torch.allclose(out["mean"], torch.tensor(0.2205), atol=5e-5)
+    assert torch.allclose(out["std"], torch.tensor(0.0859), atol=5e-5)
+
+
+STAT_FAMILY = [tm.MulticlassAccuracy, tm.MulticlassPrecision, tm.MulticlassRecall, tm.MulticlassF1Score,
+               tm.MulticlassSpecificity, tm.MulticlassHammingDistance, tm.MulticlassStatScores]
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("cls", STAT_FAMILY)
+@pytest.mark.parametrize("average", ["micro", "macro", "weighted", "none"])
+@pytest.mark.parametrize("strategy", ["poisson", "multinomial"])
+def test_bootstrapper_batched_stat_family_matches_copies(device, cls, average, strategy):
+    """The stacked one-kernel update / one-reduction compute equals computing every replicate copy on its own, and
+    both equal replaying the same replicates through a fresh metric (ignore_index and label preds included)."""
+    torch.manual_seed(3)
+    base = cls(num_classes=4, average=average, ignore_index=2)
+    bs = tm.BootStrapper(base, num_bootstraps=6, mean=False, std=False, raw=True, sampling_strategy=strategy)
+    bs = bs.to(device)
+    assert bs._stacked is not None
+    batches = [(torch.randn(40, 4), torch.randint(4, (40,))), (torch.randint(4, (33,)), torch.randint(4, (33,)))]
+    torch.manual_seed(11)
+    for p, t in batches:
+        bs.update(p.to(device), t.to(device))
+    raw = bs.compute()["raw"].cpu()
+    per_copy = torch.stack([m.compute() for m in bs.metrics]).cpu()
+    torch.testing.assert_close(raw.float(), per_copy.float(), equal_nan=True)
+    # replay the same replicates through fresh metrics
+    torch.manual_seed(11)
+    refs = [cls(num_classes=4, average=average, ignore_index=2) for _ in range(6)]
+    for p, t in batches:
+        for r in refs:
+            idx = _bootstrap_sampler(len(t), strategy)
+            if idx.numel():
+                r.update(p[idx], t[idx])
+    expect = torch.stack([r.compute() for r in refs])
+    torch.testing.assert_close(raw.float(), expect.float(), equal_nan=True)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_bootstrapper_batched_flags_out_of_range_target(device):
+    bs = tm.BootStrapper(tm.MulticlassAccuracy(num_classes=3), num_bootstraps=4).to(device)
+    t = torch.tensor([0, 1, 2, 7])
+    if device == "cpu":
+        with pytest.raises(RuntimeError):
+            bs.update(torch.randn(4, 3), t)
+    else:
+        bs.update(torch.randn(4, 3, device=device), t.to(device))
+        with pytest.raises(RuntimeError):
+            bs.compute()
+
+
 def test_classwise_wrapper():
     m = tm.ClasswiseWrapper(tm.MulticlassAccuracy(num_classes=3, average=None), labels=["a", "b", "c"])
     p, t = torch.randn(20, 3), torch.randint(0, 3, (20,))

@@ -129,6 +129,18 @@ def mc_update(
         _cpu.mc_update(preds, target, out, flag, num_classes, ignore_index, mode, samplewise)
 
 
+def mc_bootstrap_update(preds: Tensor, target: Tensor, weights: Tensor, ws: Tensor, flag: Tensor, num_classes: int,
+                        ignore_index: Optional[int]) -> None:
+    """Weighted multiclass stat workspace for B bootstraps at once (``csrc/classification/bootstrap.hip``):
+    ``weights`` int32 ``[N, B]`` sample multiplicities; ``ws`` int64 ``[B, 3C + 1]`` (fold with
+    :func:`mc_stats_finalize`)."""
+    if preds.is_cuda:
+        _ops().mc_bootstrap_update(preds, target, weights, ws, flag, int(num_classes),
+                                   0 if ignore_index is None else int(ignore_index), ignore_index is not None)
+    else:
+        _cpu.mc_bootstrap_update(preds, target, weights, ws, flag, num_classes, ignore_index)
+
+
 def mc_stats_finalize(ws: Tensor, num_classes: int, micro: bool, accumulate: bool, tp: Tensor, fp: Tensor,
                       tn: Tensor, fn: Tensor) -> None:
     if ws.is_cuda:

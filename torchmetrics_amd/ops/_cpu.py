@@ -680,3 +680,30 @@ def gemm_nt(x: Tensor, y: Tensor, kind: int, aux_x, aux_y, scale: float, coef: f
     v = torch.nn.functional.pad(dot * scale, (0, pad))
     v = v.reshape(b, n, tiles, _GEMM_TILE).sum(-1)
     return v if batched else v[0]
+
+
+def mc_bootstrap_update(preds: Tensor, target: Tensor, weights: Tensor, ws: Tensor, flag: Tensor, num_classes: int,
+                        ignore_index: Optional[int]) -> None:
+    """Host contract of ``csrc/classification/bootstrap.hip``: weighted [B, 3C+1] stat workspace per bootstrap."""
+    C = int(num_classes)
+    t = target.reshape(-1).long()
+    p = preds.reshape(t.numel(), C).argmax(1) if preds.is_floating_point() else preds.reshape(-1).long()
+    keep = torch.ones_like(t, dtype=torch.bool) if ignore_index is None else t != ignore_index
+    bad_t = keep & ((t < 0) | (t >= C))
+    bad_p = keep & ~bad_t & ((p < 0) | (p >= C))
+    if bool(bad_t.any()):
+        flag.view(-1)[0] |= 1
+    if bool(bad_p.any()):
+        flag.view(-1)[0] |= 2
+    keep = keep & ~bad_t & ~bad_p
+    w = weights.long().t() * keep  # [B, n]
+    B = w.shape[0]
+    stride = 3 * C + 1
+    flat = ws.view(-1)
+    base = (torch.arange(B) * stride).unsqueeze(1)
+    tt, pp = t.clamp(0, C - 1), p.clamp(0, C - 1)
+    hit = (pp == tt).unsqueeze(0)
+    flat.index_add_(0, (base + tt).reshape(-1), (w * hit).reshape(-1))
+    flat.index_add_(0, (base + C + pp).reshape(-1), (w * ~hit).reshape(-1))
+    flat.index_add_(0, (base + 2 * C + tt).reshape(-1), (w * ~hit).reshape(-1))
+    flat.index_add_(0, (base[:, 0] + 3 * C), w.sum(1))

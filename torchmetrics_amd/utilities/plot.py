@@ -1,10 +1,12 @@
-"""matplotlib rendering for ``Metric.plot`` (parity: reference ``S/utilities/plot.py:53-330``).
+"""matplotlib rendering behind ``Metric.plot`` (same call signatures as reference ``S/utilities/plot.py``).
 
-Host-only: values are moved to CPU once per call.
+Structure: every public function first turns its metric values into plain *series* / *panels* (host numpy arrays,
+one device->host copy per value; :func:`_series_of`, :func:`_confmat_panels`, :func:`_curve_series`) and only then
+draws them, so the value handling is testable without matplotlib (which is optional, as in the reference).
 """
 from itertools import product
 from math import ceil, floor, sqrt
-from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
+from typing import Any, Dict, List, NamedTuple, Optional, Sequence, Tuple, Union
 
 import numpy as np
 import torch
@@ -14,6 +16,7 @@ from torchmetrics_amd.utilities.imports import _MATPLOTLIB_AVAILABLE
 
 _PLOT_OUT_TYPE = Tuple[Any, Any]
 _AX_TYPE = Any
+_MARKER = {"marker": "o", "markersize": 10}
 
 
 def _error_on_missing_matplotlib() -> None:
@@ -23,7 +26,7 @@ def _error_on_missing_matplotlib() -> None:
         )
 
 
-def _plt() -> Any:
+def _pyplot() -> Any:
     _error_on_missing_matplotlib()
     import matplotlib
 
@@ -33,8 +36,56 @@ def _plt() -> Any:
     return plt
 
 
-def _cpu(v: Tensor) -> np.ndarray:
-    return v.detach().float().cpu().numpy()
+def _host(v: Any) -> np.ndarray:
+    return v.detach().float().cpu().numpy() if isinstance(v, Tensor) else np.asarray(v, dtype=np.float32)
+
+
+class _Series(NamedTuple):
+    label: Optional[str]
+    x: np.ndarray
+    y: np.ndarray
+    line: bool  # connect the points (time series) or scatter them
+
+
+def _series_of(val: Any, legend_name: Optional[str] = None) -> Tuple[List[_Series], int]:
+    """Metric value(s) -> drawable series, plus the number of steps when ``val`` is a history (0 otherwise).
+
+    One value: a point.  A per-class vector: one point per class.  A dict: one point (or one series for non-scalar
+    entries) per key.  A sequence of any of those: one series per class / key over the steps.
+    """
+    tag = (lambda i: f"{legend_name} {i}") if legend_name else str
+    if isinstance(val, Tensor):
+        if val.numel() == 1:
+            return [_Series(None, np.zeros(1), _host(val).reshape(1), False)], 0
+        return [_Series(tag(i), np.full(1, i), _host(v).reshape(-1), False) for i, v in enumerate(val)], 0
+    if isinstance(val, dict):
+        out, steps = [], 0
+        for i, (k, v) in enumerate(val.items()):
+            if v.numel() == 1:
+                out.append(_Series(k, np.full(1, i), _host(v).reshape(1), False))
+            else:
+                y = _host(v).reshape(-1)
+                out.append(_Series(k, np.arange(len(y)), y, True))
+                steps = max(steps, len(y))
+        return out, steps
+    if isinstance(val, Sequence) and len(val) > 0:
+        steps = len(val)
+        xs = np.arange(steps)
+        if isinstance(val[0], dict):
+            return [_Series(k, xs, _host(torch.stack([step[k] for step in val])).reshape(steps), True)
+                    for k in val[0]], steps
+        stacked = _host(torch.stack(list(val), 0))
+        if stacked.ndim == 1:
+            return [_Series(None, xs, stacked, True)], steps
+        return [_Series(tag(i), xs, col, True) for i, col in enumerate(stacked.reshape(steps, -1).T)], steps
+    raise ValueError("Got unknown format for argument `val`.")
+
+
+def _padded_limits(lo: float, hi: float, lower: Optional[float], upper: Optional[float]) -> Tuple[float, float]:
+    """y-limits: the metric's bounds (or the data range) widened by 10 % of the bounded span."""
+    span = (upper - lower) if (lower is not None and upper is not None) else (hi - lo)
+    pad = 0.1 * span
+    return (lower if lower is not None else lo) - pad, (upper if upper is not None else hi) + pad
 
 
 def plot_single_or_multi_val(
@@ -46,95 +97,70 @@ def plot_single_or_multi_val(
     legend_name: Optional[str] = None,
     name: Optional[str] = None,
 ) -> _PLOT_OUT_TYPE:
-    """Plot one value, a per-class vector, a dict of values, or a time series (sequence) of any of those."""
-    plt = _plt()
+    """Plot one value, a per-class vector, a dict of values, or a history of any of those."""
+    plt = _pyplot()
+    series, steps = _series_of(val, legend_name)
     fig, ax = plt.subplots() if ax is None else (None, ax)
-    ax.get_xaxis().set_visible(False)
-    if isinstance(val, Tensor):
-        if val.numel() == 1:
-            ax.plot([_cpu(val).item()], marker="o", markersize=10)
-        else:
-            for i, v in enumerate(val):
-                ax.plot(i, _cpu(v), marker="o", markersize=10, linestyle="None",
-                        label=f"{legend_name} {i}" if legend_name else f"{i}")
-    elif isinstance(val, dict):
-        for i, (k, v) in enumerate(val.items()):
-            if v.numel() != 1:
-                ax.plot(_cpu(v), marker="o", markersize=10, linestyle="-", label=k)
-                ax.get_xaxis().set_visible(True)
-                ax.set_xlabel("Step")
-                ax.set_xticks(np.arange(len(v)))
-            else:
-                ax.plot(i, _cpu(v), marker="o", markersize=10, label=k)
-    elif isinstance(val, Sequence):
-        steps = len(val)
-        if isinstance(val[0], dict):
-            series = {k: torch.stack([val[i][k] for i in range(steps)]) for k in val[0]}
-            for k, v in series.items():
-                ax.plot(_cpu(v), marker="o", markersize=10, linestyle="-", label=k)
-        else:
-            stacked = torch.stack(list(val), 0)
-            if stacked.ndim != 1:
-                for i, v in enumerate(stacked.T):
-                    ax.plot(_cpu(v), marker="o", markersize=10, linestyle="-",
-                            label=f"{legend_name} {i}" if legend_name else f"{i}")
-            else:
-                ax.plot(_cpu(stacked), marker="o", markersize=10, linestyle="-")
-        ax.get_xaxis().set_visible(True)
+    for s in series:
+        ax.plot(s.x, s.y, linestyle="-" if s.line else "None", label=s.label, **_MARKER)
+    ax.get_xaxis().set_visible(steps > 0)
+    if steps:
         ax.set_xlabel("Step")
         ax.set_xticks(np.arange(steps))
-    else:
-        raise ValueError("Got unknown format for argument `val`.")
     handles, labels = ax.get_legend_handles_labels()
     if handles and labels:
         ax.legend(handles, labels, loc="upper center", bbox_to_anchor=(0.5, 1.15), ncol=3, fancybox=True, shadow=True)
-    ylim = ax.get_ylim()
-    if lower_bound is not None and upper_bound is not None:
-        factor = 0.1 * (upper_bound - lower_bound)
-    else:
-        factor = 0.1 * (ylim[1] - ylim[0])
-    ax.set_ylim(
-        bottom=lower_bound - factor if lower_bound is not None else ylim[0] - factor,
-        top=upper_bound + factor if upper_bound is not None else ylim[1] + factor,
-    )
+    bottom, top = _padded_limits(*ax.get_ylim(), lower_bound, upper_bound)
+    ax.set_ylim(bottom=bottom, top=top)
     ax.grid(True)
-    ax.set_ylabel(name if name is not None else None)
-    xlim = ax.get_xlim()
-    factor = 0.1 * (xlim[1] - xlim[0])
-    y_lines = []
-    if lower_bound is not None:
-        y_lines.append(lower_bound)
-    if upper_bound is not None:
-        y_lines.append(upper_bound)
-    ax.hlines(y_lines, xlim[0], xlim[1], linestyles="dashed", colors="k")
-    if higher_is_better is not None:
-        if lower_bound is not None and not higher_is_better:
-            ax.set_xlim(xlim[0] - factor, xlim[1])
-            ax.text(xlim[0], lower_bound, s="Optimal \n value", horizontalalignment="center", verticalalignment="center")
-        if upper_bound is not None and higher_is_better:
-            ax.set_xlim(xlim[0] - factor, xlim[1])
-            ax.text(xlim[0], upper_bound, s="Optimal \n value", horizontalalignment="center", verticalalignment="center")
+    ax.set_ylabel(name)
+    left, right = ax.get_xlim()
+    bounds = [b for b in (lower_bound, upper_bound) if b is not None]
+    ax.hlines(bounds, left, right, linestyles="dashed", colors="k")
+    optimum = {True: upper_bound, False: lower_bound}.get(higher_is_better) if higher_is_better is not None else None
+    if optimum is not None:  # make room left of the data and label the optimal bound
+        ax.set_xlim(left - 0.1 * (right - left), right)
+        ax.text(left, optimum, s="Optimal \n value", horizontalalignment="center", verticalalignment="center")
     return fig, ax
 
 
 def _get_col_row_split(n: int) -> Tuple[int, int]:
-    """Near-square grid for ``n`` subplots."""
-    nsq = sqrt(n)
-    if int(nsq) ** 2 == n:
-        return int(nsq), int(nsq)
-    if floor(nsq) * ceil(nsq) >= n:
-        return floor(nsq), ceil(nsq)
-    return ceil(nsq), ceil(nsq)
+    """(rows, cols) of the most square grid with at least ``n`` cells."""
+    side = sqrt(n)
+    if int(side) ** 2 == n:
+        return int(side), int(side)
+    if floor(side) * ceil(side) >= n:
+        return floor(side), ceil(side)
+    return ceil(side), ceil(side)
 
 
 def trim_axs(axs: Any, nb: int) -> Any:
-    """Hide the surplus axes of a subplot grid."""
-    if isinstance(axs, np.ndarray) is False:
+    """Remove the unused axes of a subplot grid and return the first ``nb``."""
+    if not isinstance(axs, np.ndarray):
         return axs
-    flat = axs.flat
-    for ax in flat[nb:]:
-        ax.remove()
+    for extra in axs.flat[nb:]:
+        extra.remove()
     return axs.flat[:nb]
+
+
+class _Panel(NamedTuple):
+    title: Optional[str]
+    matrix: np.ndarray
+    ticks: List[Any]
+
+
+def _confmat_panels(confmat: Tensor, labels: Optional[List[Union[int, str]]]) -> List[_Panel]:
+    """One panel per label for a multilabel ``[L, 2, 2]`` stack, one panel for a ``[C, C]`` matrix."""
+    if confmat.ndim == 3:
+        names = labels if labels is not None else list(range(confmat.shape[0]))
+        return [_Panel(f"Label {names[i]}", _host(confmat[i]), ["0", "1"]) for i in range(confmat.shape[0])]
+    n = confmat.shape[0]
+    if labels is not None and len(labels) != n:
+        raise ValueError(
+            "Expected number of elements in arg `labels` to match number of labels in confmat but "
+            f"got {len(labels)} and {n}"
+        )
+    return [_Panel(None, _host(confmat), list(labels) if labels is not None else list(range(n)))]
 
 
 def plot_confusion_matrix(
@@ -144,42 +170,52 @@ def plot_confusion_matrix(
     labels: Optional[List[Union[int, str]]] = None,
     cmap: Optional[Any] = None,
 ) -> _PLOT_OUT_TYPE:
-    """Heat-map of a ``[C, C]`` (or ``[L, 2, 2]`` multilabel) confusion matrix."""
-    plt = _plt()
-    if confmat.ndim == 3:
-        nb, n_classes = confmat.shape[0], 2
-        rows, cols = _get_col_row_split(nb)
-    else:
-        nb, n_classes, rows, cols = 1, confmat.shape[0], 1, 1
-    if labels is not None and confmat.ndim != 3 and len(labels) != n_classes:
-        raise ValueError(
-            "Expected number of elements in arg `labels` to match number of labels in confmat but "
-            f"got {len(labels)} and {n_classes}"
-        )
-    if confmat.ndim == 3:
-        fig_label = labels or np.arange(nb)
-        labels = list(map(str, range(n_classes)))
-    else:
-        fig_label = None
-        labels = labels or np.arange(n_classes).tolist()
+    """Heat map of a ``[C, C]`` confusion matrix (or a grid of ``[2, 2]`` ones for a multilabel ``[L, 2, 2]``)."""
+    plt = _pyplot()
+    panels = _confmat_panels(confmat, labels)
+    rows, cols = _get_col_row_split(len(panels)) if confmat.ndim == 3 else (1, 1)
     fig, axs = plt.subplots(nrows=rows, ncols=cols) if ax is None else (ax.get_figure(), ax)
-    axs = trim_axs(axs, nb)
-    for i in range(nb):
-        a = axs[i] if rows != 1 and cols != 1 else axs
-        if fig_label is not None:
-            a.set_title(f"Label {fig_label[i]}", fontsize=15)
-        m = _cpu(confmat[i] if confmat.ndim == 3 else confmat)
-        a.imshow(m, cmap=cmap)
+    axs = trim_axs(axs, len(panels))
+    for i, panel in enumerate(panels):
+        a = axs[i] if (rows != 1 and cols != 1) else axs
+        if panel.title is not None:
+            a.set_title(panel.title, fontsize=15)
+        a.imshow(panel.matrix, cmap=cmap)
         a.set_xlabel("Predicted class", fontsize=15)
         a.set_ylabel("True class", fontsize=15)
-        a.set_xticks(list(range(n_classes)))
-        a.set_yticks(list(range(n_classes)))
-        a.set_xticklabels(labels, rotation=45, fontsize=10)
-        a.set_yticklabels(labels, rotation=25, fontsize=10)
+        k = len(panel.ticks)
+        a.set_xticks(list(range(k)))
+        a.set_yticks(list(range(k)))
+        a.set_xticklabels(panel.ticks, rotation=45, fontsize=10)
+        a.set_yticklabels(panel.ticks, rotation=25, fontsize=10)
         if add_text:
-            for ii, jj in product(range(n_classes), range(n_classes)):
-                a.text(jj, ii, str(round(float(m[ii, jj]), 2)), ha="center", va="center", fontsize=15)
+            for r, c in product(range(k), range(k)):
+                a.text(c, r, str(round(float(panel.matrix[r, c]), 2)), ha="center", va="center", fontsize=15)
     return fig, axs
+
+
+def _curve_series(curve: Sequence[Any], score: Optional[Tensor], legend_name: Optional[str]) -> List[_Series]:
+    """(x, y[, thresholds]) of one curve or of per-class curves -> series labelled with their AUC when given."""
+    if len(curve) < 2:
+        raise ValueError(f"Expected 2 or 3 elements in curve but got {len(curve)}")
+    if score is not None and not isinstance(score, Tensor):
+        raise ValueError(f"Expected score to be a tensor but got {type(score)}")
+    x, y = curve[0], curve[1]
+    if isinstance(x, Tensor) and isinstance(y, Tensor) and x.ndim == 1 and y.ndim == 1:
+        return [_Series(f"AUC={score.item():0.3f}" if score is not None else None, _host(x), _host(y), True)]
+    per_class = (isinstance(x, list) and isinstance(y, list)) or (
+        isinstance(x, Tensor) and isinstance(y, Tensor) and x.ndim == 2 and y.ndim == 2)
+    if not per_class:
+        raise ValueError(
+            f"Unknown format for argument `x` and `y`. Expected either list or tensors but got {type(x)} and {type(y)}."
+        )
+    out = []
+    for i, (xi, yi) in enumerate(zip(x, y)):
+        label = f"{legend_name}_{i}" if legend_name is not None else str(i)
+        if score is not None:
+            label += f" AUC={score[i].item():0.3f}"
+        out.append(_Series(label, _host(xi), _host(yi), True))
+    return out
 
 
 def plot_curve(
@@ -190,34 +226,18 @@ def plot_curve(
     legend_name: Optional[str] = None,
     name: Optional[str] = None,
 ) -> _PLOT_OUT_TYPE:
-    """Plot a ROC / PR style curve (one or per-class)."""
-    plt = _plt()
-    if len(curve) < 2:
-        raise ValueError("Expected 2 or 3 elements in curve but got {len(curve)}")
-    x, y = curve[:2]
-    if score is not None and not isinstance(score, Tensor):
-        raise ValueError(f"Expected score to be a tensor but got {type(score)}")
+    """ROC / PR style curve(s), each labelled with its score when one is given."""
+    plt = _pyplot()
+    series = _curve_series(curve, score, legend_name)
     fig, ax = plt.subplots() if ax is None else (None, ax)
-    if isinstance(x, Tensor) and isinstance(y, Tensor) and x.ndim == 1 and y.ndim == 1:
-        label = f"AUC={score.item():0.3f}" if score is not None else None
-        ax.plot(_cpu(x), _cpu(y), linestyle="-", linewidth=2, label=label)
-        if label_names is not None:
-            ax.set_xlabel(label_names[0])
-            ax.set_ylabel(label_names[1])
-        if label is not None:
-            ax.legend()
-    elif (isinstance(x, list) and isinstance(y, list)) or (
-        isinstance(x, Tensor) and isinstance(y, Tensor) and x.ndim == 2 and y.ndim == 2
-    ):
-        for i, (x_, y_) in enumerate(zip(x, y)):
-            label = f"{legend_name}_{i}" if legend_name is not None else str(i)
-            label += f" AUC={score[i].item():0.3f}" if score is not None else ""
-            ax.plot(_cpu(x_), _cpu(y_), linestyle="-", linewidth=2, label=label)
-            ax.legend()
-    else:
-        raise ValueError(
-            f"Unknown format for argument `x` and `y`. Expected either list or tensors but got {type(x)} and {type(y)}."
-        )
+    for s in series:
+        ax.plot(s.x, s.y, linestyle="-", linewidth=2, label=s.label)
+    single = len(series) == 1 and isinstance(curve[0], Tensor) and curve[0].ndim == 1
+    if single and label_names is not None:
+        ax.set_xlabel(label_names[0])
+        ax.set_ylabel(label_names[1])
+    if any(s.label is not None for s in series):
+        ax.legend()
     ax.grid(True)
     ax.set_title(name)
     return fig, ax

@@ -2,8 +2,9 @@
 
 Speaker-wise mode evaluates the ``spk x spk`` metric matrix with ONE batched ``metric_func`` call on
 ``[B * spk * spk, ...]`` views instead of ``spk^2`` calls, and solves the assignment on the device by scoring every
-permutation with a gather (no host sync) up to ``_MAX_EXHAUSTIVE_SPK`` speakers; beyond that it falls back to
-scipy's Hungarian solver on the host like the reference.
+permutation with a gather (no host sync) up to ``_MAX_EXHAUSTIVE_SPK`` speakers; beyond that a batched Hungarian
+solve runs on the device (one wave per batch item, ``ops.linear_sum_assignment``) -- scipy on the host only for CPU
+tensors, like the reference.
 """
 from itertools import permutations
 from typing import Any, Callable, Dict, Literal, Tuple
@@ -12,6 +13,7 @@ import numpy as np
 import torch
 from torch import Tensor
 
+from torchmetrics_amd import ops
 from torchmetrics_amd.utilities.imports import _SCIPY_AVAILABLE
 
 _MAX_EXHAUSTIVE_SPK = 5
@@ -35,11 +37,15 @@ def _find_best_perm_by_exhaustive_method(metric_mtx: Tensor, eval_func: Callable
 
 
 def _find_best_perm_by_linear_sum_assignment(metric_mtx: Tensor, eval_func: Callable) -> Tuple[Tensor, Tensor]:
-    from scipy.optimize import linear_sum_assignment
+    if metric_mtx.is_cuda:
+        # batched Hungarian solve on the device (csrc/audio/lsa.hip): no host round trip
+        perm = ops.linear_sum_assignment(metric_mtx, maximize=eval_func == torch.max)
+    else:
+        from scipy.optimize import linear_sum_assignment
 
-    mm = metric_mtx.detach().cpu()
-    perm = torch.tensor(np.array([linear_sum_assignment(m, eval_func == torch.max)[1] for m in mm]))
-    perm = perm.to(metric_mtx.device)
+        mm = metric_mtx.detach().cpu()
+        perm = torch.tensor(np.array([linear_sum_assignment(m, eval_func == torch.max)[1] for m in mm]))
+        perm = perm.to(metric_mtx.device)
     return torch.gather(metric_mtx, 2, perm[:, :, None]).mean([-1, -2]), perm
 
 
@@ -72,7 +78,7 @@ def permutation_invariant_training(preds: Tensor, target: Tensor, metric_func: C
     pp = preds[:, None].expand(b, spk, spk, *tail).reshape(b * spk * spk, *tail)
     tt = target[:, :, None].expand(b, spk, spk, *tail).reshape(b * spk * spk, *tail)
     metric_mtx = metric_func(pp, tt, **kwargs).reshape(b, spk, spk)
-    if spk <= _MAX_EXHAUSTIVE_SPK or not _SCIPY_AVAILABLE:
+    if spk <= _MAX_EXHAUSTIVE_SPK or not (_SCIPY_AVAILABLE or metric_mtx.is_cuda):
         return _find_best_perm_by_exhaustive_method(metric_mtx, eval_op)
     return _find_best_perm_by_linear_sum_assignment(metric_mtx, eval_op)
 

@@ -424,7 +424,10 @@ class InceptionScore(_FeatureNetMetric):
 
     def compute(self) -> Tuple[Tensor, Tensor]:
         features = dim_zero_cat(self.features)
-        idx = torch.randperm(features.shape[0])
+        idx = torch.randperm(features.shape[0])  # host draw, as the reference (same seed -> same splits)
+        if features.is_cuda and features.dtype in (torch.float32, torch.float16, torch.bfloat16) and features.ndim == 2:
+            out = ops.inception_score(features, idx, self.splits)  # 3 launches, no permuted / softmax copies
+            return out[0], out[1]
         features = features[idx.to(features.device)]
         prob = features.softmax(dim=1)
         log_prob = features.log_softmax(dim=1)

@@ -1020,3 +1020,49 @@ def biquad_cascade(x: Tensor, coefs: Tensor, rep: int, clamp: bool) -> Tensor:
         _ops().biquad_cascade(xs, cf.to(xs.device), y, int(rep), bool(clamp))
         return y
     return _cpu.biquad_cascade(xs, cf, rep, clamp)
+
+
+# ------------------------------------------------------------------------------------------------ audio / image
+def snr_rows(preds: Tensor, target: Tensor, seg: int, scale_invariant: bool, zero_mean: bool, eps: float) -> Tensor:
+    """SNR (``scale_invariant=False``) or SI-SDR-style ratio in dB per row of contiguous ``[rows, L]`` ROCm signals,
+    one block per row (``csrc/audio/snr.hip``); ``seg``: zero-mean segment length (SA-SDR: per speaker)."""
+    out = torch.empty(preds.shape[0], dtype=preds.dtype, device=preds.device)
+    _ops().snr_rows(preds.contiguous(), target.contiguous(), out, int(seg), bool(scale_invariant), bool(zero_mean),
+                    float(eps))
+    return out
+
+
+def inception_score(logits: Tensor, perm: Tensor, splits: int) -> Tensor:
+    """(mean, std) Inception Score of ROCm ``[N, C]`` logits taken in ``perm`` order, ``torch.chunk`` splits
+    (``csrc/image/inception_score.hip``, three launches)."""
+    out = torch.empty(2, dtype=torch.float32, device=logits.device)
+    _ops().inception_score(logits.contiguous(), perm.to(logits.device, torch.int64).contiguous(), int(splits), out)
+    return out
+
+
+HINGE_BINARY, HINGE_CRAMMER_SINGER, HINGE_ONE_VS_ALL = 0, 1, 2
+
+
+def hinge_update(preds: Tensor, target: Tensor, mode: int, squared: bool, ignore_index: Optional[int], owner: dict,
+                 measures: Tensor, total: Tensor, flag: Tensor) -> None:
+    """Fused hinge-loss update of ROCm scores into the ``measures`` / ``total`` states (``csrc/classification/
+    hinge.hip``): both readings of the scores (as given / sigmoid-or-softmax) accumulated in one pass, the fold keeps
+    the one the batch calls for.  ``owner``: the metric's ``__dict__`` (holds the reusable workspace)."""
+    k = measures.numel()
+    ws = owner.get("_hinge_ws")
+    if ws is None or ws[0].numel() != 2 * k + 1 or ws[0].device != preds.device:
+        ws = owner["_hinge_ws"] = (torch.zeros(2 * k + 1, dtype=torch.float64, device=preds.device),
+                                   torch.zeros(1, dtype=torch.int32, device=preds.device))
+    _ops().hinge_update(preds, target, mode, bool(squared), 0 if ignore_index is None else int(ignore_index),
+                        ignore_index is not None, ws[0], ws[1], measures, total, flag)
+
+
+def linear_sum_assignment(cost: Tensor, maximize: bool = False) -> Tensor:
+    """Optimal assignment of every ``[n, n]`` problem in a ROCm ``[B, n, n]`` cost batch (one wave per problem,
+    Hungarian method; ``csrc/audio/lsa.hip``).  Returns int64 ``[B, n]``: the column of each row."""
+    c = cost.detach()
+    if c.dtype not in (torch.float32, torch.float64):
+        c = c.float()
+    out = torch.zeros(c.shape[0], c.shape[1], dtype=torch.int64, device=c.device)
+    _ops().linear_sum_assignment(c.contiguous(), bool(maximize), out)
+    return out

@@ -10,7 +10,9 @@ the names listed here, after the regular finders have failed; it never shadows a
 import importlib
 import importlib.abc
 import importlib.util
+import pkgutil
 import sys
+import types
 from typing import Dict, Optional, Tuple
 
 # domain package (relative to torchmetrics_amd) -> reference submodule names that alias it
@@ -111,6 +113,17 @@ _ALIASES: Dict[str, str] = {
 }
 
 
+class _GuardedPackage(types.ModuleType):
+    """A domain package whose public (non-module) attributes are not overwritten by its alias submodules."""
+
+    def __setattr__(self, name: str, value: object) -> None:
+        cur = self.__dict__.get(name)
+        if (isinstance(value, types.ModuleType) and value.__name__ in _ALIASES and cur is not None
+                and not isinstance(cur, types.ModuleType)):
+            return
+        super().__setattr__(name, value)
+
+
 class _AliasFinder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
     def find_spec(self, fullname: str, path: Optional[object] = None, target: Optional[object] = None):  # noqa: ANN201
         if fullname not in _ALIASES:
@@ -122,6 +135,29 @@ class _AliasFinder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
 
     def exec_module(self, module) -> None:  # noqa: ANN001
         target = importlib.import_module(_ALIASES[module.__name__])
+        # the import system will bind this alias module on the package under its short name; the package's own
+        # attribute of that name (e.g. the function `explained_variance`) must survive it
+        if type(target) is types.ModuleType:
+            target.__class__ = _GuardedPackage
+        # private helpers of the domain's real modules (the reference's per-file helpers, e.g. `_r2_score_update`)
+        for info in pkgutil.iter_modules(getattr(target, "__path__", [])):
+            try:
+                sub = importlib.import_module(f"{target.__name__}.{info.name}")
+            except ImportError:
+                continue
+            module.__dict__.update({k: v for k, v in vars(sub).items()
+                                    if k.startswith("_") and not k.startswith("__") and callable(v)})
+        if module.__name__.endswith("._deprecated"):
+            # the reference's `_deprecated.py` modules hold the warning aliases under underscore names
+            from torchmetrics_amd import _deprecated as dep
+
+            domain = module.__name__.split(".")[-2]
+            if ".functional." in module.__name__:
+                module.__dict__.update({f"_{n}": dep.deprecated_function(n, d)
+                                        for n, d in dep.FUNCTIONAL_ROOT.items() if d == domain})
+            else:
+                module.__dict__.update({f"_{n}": dep.deprecated_class(n, d)
+                                        for n, d in dep.ROOT_CLASSES.items() if d == domain})
         extra = _SOURCES.get(module.__name__)
         if extra is not None:
             module.__dict__.update({k: v for k, v in vars(importlib.import_module(extra)).items()

@@ -66,8 +66,8 @@ class MulticlassFBetaScore(MulticlassStatScores):
         self,
         beta: float,
         num_classes: int,
-        average: Optional[str] = "macro",
         top_k: int = 1,
+        average: Optional[str] = "macro",
         multidim_average: str = "global",
         ignore_index: Optional[int] = None,
         validate_args: bool = True,
@@ -163,14 +163,15 @@ class MulticlassF1Score(MulticlassFBetaScore):
     def __init__(
         self,
         num_classes: int,
-        average: Optional[str] = "macro",
         top_k: int = 1,
+        average: Optional[str] = "macro",
         multidim_average: str = "global",
         ignore_index: Optional[int] = None,
         validate_args: bool = True,
         **kwargs: Any,
     ) -> None:
-        super().__init__(1.0, num_classes, average, top_k, multidim_average, ignore_index, validate_args, **kwargs)
+        super().__init__(1.0, num_classes, top_k=top_k, average=average, multidim_average=multidim_average,
+                         ignore_index=ignore_index, validate_args=validate_args, **kwargs)
 
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()

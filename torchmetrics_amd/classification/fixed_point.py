@@ -4,6 +4,7 @@ Parity: reference ``S/classification/recall_fixed_precision.py``, ``precision_fi
 ``sensitivity_specificity.py``, ``specificity_sensitivity.py``.  Each class shares the binned / unbinned curve state
 of :mod:`~torchmetrics_amd.classification.precision_recall_curve` and returns ``(value, threshold)``.
 """
+import inspect
 from typing import Any, Optional, Tuple, Type
 
 from torch import Tensor
@@ -121,6 +122,16 @@ def _named_init(cls, min_name: str, positional_num: Optional[str]):
             if min_name in kwargs:
                 kwargs["min_value"] = kwargs.pop(min_name)
             base_init(self, *args, **kwargs)
+    # introspection shows the reference signature (``min_precision`` ... in its reference position)
+    params = [inspect.Parameter("self", inspect.Parameter.POSITIONAL_OR_KEYWORD)]
+    if positional_num is not None:
+        params.append(inspect.Parameter(positional_num, inspect.Parameter.POSITIONAL_OR_KEYWORD))
+    params += [inspect.Parameter(min_name, inspect.Parameter.POSITIONAL_OR_KEYWORD),
+               inspect.Parameter("thresholds", inspect.Parameter.POSITIONAL_OR_KEYWORD, default=None),
+               inspect.Parameter("ignore_index", inspect.Parameter.POSITIONAL_OR_KEYWORD, default=None),
+               inspect.Parameter("validate_args", inspect.Parameter.POSITIONAL_OR_KEYWORD, default=True),
+               inspect.Parameter("kwargs", inspect.Parameter.VAR_KEYWORD)]
+    __init__.__signature__ = inspect.Signature(params)
     cls.__init__ = __init__
     return cls
 
@@ -142,15 +153,34 @@ BinarySpecificityAtSensitivity, MulticlassSpecificityAtSensitivity, MultilabelSp
 
 
 def _wrapper(name: str, min_name: str, classes):
-    def __new__(cls: Type, task: Literal["binary", "multiclass", "multilabel"], *args: Any,
-                thresholds: Thresholds = None, num_classes: Optional[int] = None, num_labels: Optional[int] = None,
-                ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any) -> Metric:
-        min_value = kwargs.pop(min_name) if min_name in kwargs else args[0]
-        kwargs.update({"thresholds": thresholds, "ignore_index": ignore_index, "validate_args": validate_args})
-        return _curve_task(*classes, task, num_classes, num_labels, kwargs,
+    # reference order: (task, <min_name>, thresholds, num_classes, num_labels, ignore_index, validate_args)
+    order = (min_name, "thresholds", "num_classes", "num_labels", "ignore_index", "validate_args")
+    defaults = {"thresholds": None, "num_classes": None, "num_labels": None, "ignore_index": None,
+                "validate_args": True}
+
+    def __new__(cls: Type, task: Literal["binary", "multiclass", "multilabel"], *args: Any, **kwargs: Any) -> Metric:
+        if len(args) > len(order):
+            raise TypeError(f"{name}() takes at most {len(order) + 1} positional arguments")
+        for key, val in zip(order, args):
+            if key in kwargs:
+                raise TypeError(f"{name}() got multiple values for argument '{key}'")
+            kwargs[key] = val
+        if min_name not in kwargs:
+            raise TypeError(f"{name}() missing required argument: '{min_name}'")
+        min_value = kwargs.pop(min_name)
+        opts = {k: kwargs.pop(k, d) for k, d in defaults.items()}
+        kwargs.update({"thresholds": opts["thresholds"], "ignore_index": opts["ignore_index"],
+                       "validate_args": opts["validate_args"]})
+        return _curve_task(*classes, task, opts["num_classes"], opts["num_labels"], kwargs,
                            bin_extra={"min_value": min_value}, mc_extra={"min_value": min_value},
                            ml_extra={"min_value": min_value})
 
+    __new__.__signature__ = inspect.Signature(
+        [inspect.Parameter("cls", inspect.Parameter.POSITIONAL_OR_KEYWORD),
+         inspect.Parameter("task", inspect.Parameter.POSITIONAL_OR_KEYWORD),
+         inspect.Parameter(min_name, inspect.Parameter.POSITIONAL_OR_KEYWORD)]
+        + [inspect.Parameter(k, inspect.Parameter.POSITIONAL_OR_KEYWORD, default=defaults[k]) for k in order[1:]]
+        + [inspect.Parameter("kwargs", inspect.Parameter.VAR_KEYWORD)])
     return type(name, (_ClassificationTaskWrapper,), {"__new__": __new__, "__doc__": f"Task wrapper for {name}."})
 
 

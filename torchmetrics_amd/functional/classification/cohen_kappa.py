@@ -61,8 +61,8 @@ def binary_cohen_kappa(
     preds: Tensor,
     target: Tensor,
     threshold: float = 0.5,
-    ignore_index: Optional[int] = None,
     weights: Optional[str] = None,
+    ignore_index: Optional[int] = None,
     validate_args: bool = True,
 ) -> Tensor:
     """Cohen's kappa for binary tasks."""
@@ -76,8 +76,8 @@ def multiclass_cohen_kappa(
     preds: Tensor,
     target: Tensor,
     num_classes: int,
-    ignore_index: Optional[int] = None,
     weights: Optional[str] = None,
+    ignore_index: Optional[int] = None,
     validate_args: bool = True,
 ) -> Tensor:
     """Cohen's kappa for multiclass tasks."""
@@ -100,9 +100,9 @@ def cohen_kappa(
     """Task-dispatching Cohen's kappa (binary / multiclass)."""
     task = ClassificationTaskNoMultilabel.from_str(task)
     if task == ClassificationTaskNoMultilabel.BINARY:
-        return binary_cohen_kappa(preds, target, threshold, ignore_index, weights, validate_args)
+        return binary_cohen_kappa(preds, target, threshold, weights, ignore_index, validate_args)
     if task == ClassificationTaskNoMultilabel.MULTICLASS:
         if not isinstance(num_classes, int):
             raise ValueError(f"`num_classes` is expected to be `int` but `{type(num_classes)} was passed.`")
-        return multiclass_cohen_kappa(preds, target, num_classes, ignore_index, weights, validate_args)
+        return multiclass_cohen_kappa(preds, target, num_classes, weights, ignore_index, validate_args)
     raise ValueError(f"Not handled value: {task}")

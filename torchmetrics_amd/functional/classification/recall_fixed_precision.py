@@ -5,6 +5,7 @@ Recall @ fixed precision and precision @ fixed recall (reference ``F/classificat
 ``F/classification/sensitivity_specificity.py``, ``specificity_sensitivity.py`` incl. the deprecated misspelled
 ``specicity_at_sensitivity`` alias).  Curve states come from the shared binned HIP histogram / unbinned sort path.
 """
+import inspect
 import warnings
 from typing import Callable, List, Optional, Tuple, Union
 
@@ -371,3 +372,6 @@ def specicity_at_sensitivity(*args, **kwargs):
         stacklevel=1,
     )
     return specificity_at_sensitivity(*args, **kwargs)
+
+
+specicity_at_sensitivity.__signature__ = inspect.signature(specificity_at_sensitivity)  # type: ignore[attr-defined]

@@ -155,7 +155,7 @@ def concordance_corrcoef(preds: Tensor, target: Tensor) -> Tensor:
     d = preds.shape[1] if preds.ndim == 2 else 1
     z = torch.zeros(d, dtype=preds.dtype if preds.is_floating_point() else torch.float32, device=preds.device)
     mx, my, vx, vy, cxy, n = _pearson_corrcoef_update(preds, target, *(z.clone() for _ in range(6)), num_outputs=d)
-    return _concordance_corrcoef_compute(mx, my, vx, vy, cxy, n).squeeze()
+    return _concordance_corrcoef_compute(mx, my, vx, vy, cxy, n)  # [1] for 1-D inputs, as the reference
 
 
 # ---------------------------------------------------------------------------------------------------------- Spearman

@@ -68,6 +68,7 @@ class SignalNoiseRatio(_MeanOfBatch):
 class ScaleInvariantSignalNoiseRatio(_MeanOfBatch):
     """SI-SNR (``S/audio/snr.py:145``)."""
 
+    full_state_update: Optional[bool] = None
     _sum_name = "sum_si_snr"
 
     def _batch(self, preds: Tensor, target: Tensor) -> Tensor:
@@ -77,6 +78,7 @@ class ScaleInvariantSignalNoiseRatio(_MeanOfBatch):
 class ComplexScaleInvariantSignalNoiseRatio(_MeanOfBatch):
     """C-SI-SNR (``S/audio/snr.py:244``)."""
 
+    full_state_update: Optional[bool] = None
     _sum_name = "ci_snr_sum"
     _count_name = "num"
 
@@ -109,6 +111,7 @@ class SignalDistortionRatio(_MeanOfBatch):
 class ScaleInvariantSignalDistortionRatio(_MeanOfBatch):
     """SI-SDR (``S/audio/sdr.py:173``)."""
 
+    full_state_update: Optional[bool] = None
     _sum_name = "sum_si_sdr"
 
     def __init__(self, zero_mean: bool = False, **kwargs: Any) -> None:
@@ -140,6 +143,7 @@ class SourceAggregatedSignalDistortionRatio(_MeanOfBatch):
 class PermutationInvariantTraining(_MeanOfBatch):
     """PIT (``S/audio/pit.py:30``); extra keyword arguments are forwarded to ``metric_func``."""
 
+    higher_is_better: Optional[bool] = None
     _sum_name = "sum_pit_metric"
 
     def __init__(self, metric_func: Callable, mode: Literal["speaker-wise", "permutation-wise"] = "speaker-wise",

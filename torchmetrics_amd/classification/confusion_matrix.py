@@ -396,7 +396,7 @@ class BinaryMatthewsCorrCoef(BinaryConfusionMatrix):
     is_differentiable: bool = False
     higher_is_better: bool = True
     full_state_update: bool = False
-    plot_lower_bound: float = -1.0
+    plot_lower_bound: Optional[float] = 0.0
     plot_upper_bound: float = 1.0
 
     def __init__(self, threshold: float = 0.5, ignore_index: Optional[int] = None, validate_args: bool = True,
@@ -414,7 +414,7 @@ class MulticlassMatthewsCorrCoef(MulticlassConfusionMatrix):
     is_differentiable: bool = False
     higher_is_better: bool = True
     full_state_update: bool = False
-    plot_lower_bound: float = -1.0
+    plot_lower_bound: Optional[float] = 0.0
     plot_upper_bound: float = 1.0
     plot_legend_name: str = "Class"
 
@@ -433,7 +433,7 @@ class MultilabelMatthewsCorrCoef(MultilabelConfusionMatrix):
     is_differentiable: bool = False
     higher_is_better: bool = True
     full_state_update: bool = False
-    plot_lower_bound: float = -1.0
+    plot_lower_bound: Optional[float] = 0.0
     plot_upper_bound: float = 1.0
     plot_legend_name: str = "Label"
 

@@ -251,6 +251,8 @@ class MultilabelPrecisionRecallCurve(_CurveBase):
 class BinaryROC(BinaryPrecisionRecallCurve):
     """Receiver operating characteristic for binary tasks: ``(fpr, tpr, thresholds)``."""
 
+    plot_upper_bound: Optional[float] = 1.0
+    plot_lower_bound: Optional[float] = 0.0
     def compute(self) -> Tuple[Tensor, Tensor, Tensor]:
         return _binary_roc_compute(self._state(), self.thresholds)
 
@@ -263,6 +265,9 @@ class BinaryROC(BinaryPrecisionRecallCurve):
 class MulticlassROC(MulticlassPrecisionRecallCurve):
     """One-vs-rest ROC curves for multiclass tasks."""
 
+    plot_legend_name: Optional[str] = 'Class'
+    plot_upper_bound: Optional[float] = 1.0
+    plot_lower_bound: Optional[float] = 0.0
     def compute(self) -> Union[Tuple[Tensor, Tensor, Tensor], Tuple[List[Tensor], List[Tensor], List[Tensor]]]:
         return _multiclass_roc_compute(self._state(), self.num_classes, self.thresholds, self.average)
 
@@ -275,6 +280,9 @@ class MulticlassROC(MulticlassPrecisionRecallCurve):
 class MultilabelROC(MultilabelPrecisionRecallCurve):
     """Per-label ROC curves for multilabel tasks."""
 
+    plot_legend_name: Optional[str] = 'Label'
+    plot_upper_bound: Optional[float] = 1.0
+    plot_lower_bound: Optional[float] = 0.0
     def compute(self) -> Union[Tuple[Tensor, Tensor, Tensor], Tuple[List[Tensor], List[Tensor], List[Tensor]]]:
         return _multilabel_roc_compute(self._state(), self.num_labels, self.thresholds, self.ignore_index)
 

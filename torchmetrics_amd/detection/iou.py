@@ -16,8 +16,8 @@ class IntersectionOverUnion(Metric):
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = True
     full_state_update: bool = True
-    plot_lower_bound: float = 0.0
-    plot_upper_bound: float = 1.0
+    plot_lower_bound: Optional[float] = None
+    plot_upper_bound: Optional[float] = None
     groundtruth_labels: List[Tensor]
     iou_matrix: List[Tensor]
     _iou_type: str = "iou"
@@ -80,7 +80,7 @@ class IntersectionOverUnion(Metric):
 class GeneralizedIntersectionOverUnion(IntersectionOverUnion):
     """Mean generalised IoU (GIoU)."""
 
-    plot_lower_bound: float = -1.0
+    plot_lower_bound: Optional[float] = None
     _iou_type: str = "giou"
     _op: int = ops.BOX_GIOU
     _invalid_val: float = -1.0
@@ -89,7 +89,7 @@ class GeneralizedIntersectionOverUnion(IntersectionOverUnion):
 class DistanceIntersectionOverUnion(IntersectionOverUnion):
     """Mean distance IoU (DIoU)."""
 
-    plot_lower_bound: float = -1.0
+    plot_lower_bound: Optional[float] = None
     _iou_type: str = "diou"
     _op: int = ops.BOX_DIOU
     _invalid_val: float = -1.0
@@ -98,7 +98,7 @@ class DistanceIntersectionOverUnion(IntersectionOverUnion):
 class CompleteIntersectionOverUnion(IntersectionOverUnion):
     """Mean complete IoU (CIoU)."""
 
-    plot_lower_bound: float = -1.0
+    plot_lower_bound: Optional[float] = None
     _iou_type: str = "ciou"
     _op: int = ops.BOX_CIOU
     _invalid_val: float = -2.0

@@ -285,6 +285,7 @@ def poly_mmd(f_real: Tensor, f_fake: Tensor, degree: int = 3, gamma: Optional[fl
 
 
 class KernelInceptionDistance(_FeatureNetMetric):
+    plot_upper_bound: Optional[float] = 1.0
     higher_is_better: bool = False
     is_differentiable: bool = False
     full_state_update: bool = False
@@ -472,7 +473,7 @@ class MemorizationInformedFrechetInceptionDistance(_FeatureNetMetric):
     higher_is_better: bool = False
     is_differentiable: bool = False
     full_state_update: bool = False
-    plot_lower_bound: float = 0.0
+    plot_lower_bound: Optional[float] = None
 
     def __init__(self, feature: Union[int, Module] = 2048, reset_real_features: bool = True, normalize: bool = False,
                  cosine_distance_eps: float = 0.1, **kwargs: Any) -> None:

@@ -264,7 +264,7 @@ class PeakSignalNoiseRatioWithBlockedEffect(Metric):
     is_differentiable: bool = True
     higher_is_better: bool = True
     full_state_update: bool = False
-    plot_lower_bound: float = 0.0
+    plot_lower_bound: Optional[float] = None
 
     def __init__(self, block_size: int = 8, **kwargs: Any) -> None:
         super().__init__(**kwargs)
@@ -333,8 +333,8 @@ class SpatialCorrelationCoefficient(Metric):
     is_differentiable = True
     higher_is_better = True
     full_state_update = False
-    plot_lower_bound: float = -1.0
-    plot_upper_bound: float = 1.0
+    plot_lower_bound: Optional[float] = None
+    plot_upper_bound: Optional[float] = None
 
     def __init__(self, high_pass_filter: Optional[Tensor] = None, window_size: int = 8, **kwargs: Any) -> None:
         super().__init__(**kwargs)
@@ -360,7 +360,7 @@ class VisualInformationFidelity(Metric):
     is_differentiable = True
     higher_is_better = True
     full_state_update = False
-    plot_lower_bound: float = 0.0
+    plot_lower_bound: Optional[float] = None
 
     def __init__(self, sigma_n_sq: float = 2.0, **kwargs: Any) -> None:
         super().__init__(**kwargs)
@@ -444,6 +444,7 @@ class RelativeAverageSpectralError(Metric):
 class SpectralAngleMapper(Metric):
     """Spectral angle mapper (radians)."""
 
+    plot_upper_bound: Optional[float] = 1.0
     higher_is_better: bool = False
     is_differentiable: bool = True
     full_state_update: bool = False

@@ -90,6 +90,8 @@ class PearsonCorrCoef(Metric):
 
 
 class ConcordanceCorrCoef(PearsonCorrCoef):
+    higher_is_better: Optional[bool] = True
+
     def compute(self) -> Tensor:
         mean_x, mean_y, var_x, var_y, corr_xy, n_total = self._merged()
         return _concordance_corrcoef_compute(mean_x, mean_y, var_x, var_y, corr_xy, n_total)
@@ -130,7 +132,7 @@ class KendallRankCorrCoef(Metric):
     is_differentiable = False
     higher_is_better = None
     full_state_update = True
-    plot_lower_bound: float = -1.0
+    plot_lower_bound: Optional[float] = 0.0
     plot_upper_bound: float = 1.0
 
     def __init__(
@@ -170,6 +172,7 @@ class KendallRankCorrCoef(Metric):
 
 
 class CosineSimilarity(Metric):
+    plot_upper_bound: Optional[float] = 1.0
     is_differentiable: bool = True
     higher_is_better: bool = True
     full_state_update: bool = False

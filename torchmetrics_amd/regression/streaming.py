@@ -151,7 +151,7 @@ class SymmetricMeanAbsolutePercentageError(_MomentsMetric):
     higher_is_better = False
     full_state_update = False
     plot_lower_bound: float = 0.0
-    plot_upper_bound: float = 2.0
+    plot_upper_bound: Optional[float] = None
 
     def __init__(self, **kwargs: Any) -> None:
         super().__init__(**kwargs)
@@ -232,6 +232,7 @@ class LogCoshError(_MomentsMetric):
 
 
 class R2Score(_MomentsMetric):
+    plot_lower_bound: Optional[float] = 0.0
     is_differentiable = True
     higher_is_better = True
     full_state_update = False
@@ -303,6 +304,7 @@ class RelativeSquaredError(_MomentsMetric):
 
 
 class ExplainedVariance(_MomentsMetric):
+    plot_lower_bound: Optional[float] = 0.0
     is_differentiable = True
     higher_is_better = True
     full_state_update = False

@@ -201,6 +201,12 @@ class RetrievalAUROC(RetrievalMetric):
         return retrieval_auroc(preds, target, top_k=self.top_k, max_fpr=self.max_fpr)
 
 
+# the scores are fractions: plotted on [0, 1] (the reference sets the bounds per class, not on RetrievalMetric)
+for _cls in (RetrievalMAP, RetrievalMRR, RetrievalPrecision, RetrievalRecall, RetrievalFallOut, RetrievalHitRate,
+             RetrievalNormalizedDCG, RetrievalRPrecision, RetrievalAUROC):
+    _cls.plot_lower_bound, _cls.plot_upper_bound = 0.0, 1.0
+
+
 def _retrieval_recall_at_fixed_precision(
     precision: Tensor, recall: Tensor, top_k: Tensor, min_precision: float
 ) -> Tuple[Tensor, Tensor]:

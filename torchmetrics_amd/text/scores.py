@@ -282,6 +282,7 @@ class CHRFScore(Metric):
 class TranslationEditRate(Metric):
     """Translation edit rate (``S/text/ter.py:29``)."""
 
+    plot_upper_bound: Optional[float] = 1.0
     is_differentiable: bool = False
     higher_is_better: bool = False
     full_state_update: bool = False

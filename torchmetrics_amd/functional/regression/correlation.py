@@ -401,7 +401,9 @@ def _cosine_similarity_update(preds: Tensor, target: Tensor) -> Tuple[Tensor, Te
             "Expected input to cosine similarity to be 2D tensors of shape `[N,D]` where `N` is the number of samples"
             f" and `D` is the number of dimensions, but got tensor of shape {preds.shape}"
         )
-    return preds.float(), target.float()
+    # at least fp32 (the reference casts to fp32 unconditionally; fp64 inputs keep their precision here)
+    dt = torch.promote_types(torch.promote_types(preds.dtype, target.dtype), torch.float32)
+    return preds.to(dt), target.to(dt)
 
 
 def _cosine_similarity_compute(preds: Tensor, target: Tensor, reduction: Optional[str] = "sum") -> Tensor:

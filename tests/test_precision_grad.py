@@ -152,6 +152,9 @@ def test_low_precision_cpu(name, dtype):
         _assert_finite_tensor(_call(functional, p, t))
 
 
+_DTYPE_EPS = {"snr", "si_snr", "si_sdr", "sa_sdr"}
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.half, torch.bfloat16])
 @pytest.mark.parametrize("name", sorted(CASES))
@@ -166,7 +169,9 @@ def test_low_precision_gpu(name, dtype):
                 t.float() if torch.is_tensor(t) and t.is_floating_point() else t)
     lows = low if isinstance(low, (tuple, list)) else [low]
     refs = ref if isinstance(ref, (tuple, list)) else [ref]
+    # the audio family adds finfo(input dtype).eps (as the reference does): bf16's eps is 7.8e-3, so its values move
+    tol = 0.15 if name in _DTYPE_EPS else 0.05
     for a, b in zip(lows, refs):
-        torch.testing.assert_close(a.float(), b.float(), atol=0.05, rtol=0.05, equal_nan=True)
+        torch.testing.assert_close(a.float(), b.float(), atol=tol, rtol=tol, equal_nan=True)
     if functional is not None:
         _assert_finite_tensor(_call(functional, p, t))

@@ -1,0 +1,383 @@
+// Run-length encoded masks for `MeanAveragePrecision(iou_type="segm")` (K21 segm path).
+//
+// Reference: S/detection/mean_ap.py:825-829 encodes every mask on the host with pycocotools (`mask_utils.encode` of a
+// Fortran-ordered numpy copy), keeps (size, counts-bytes) tuples in state, gathers them with all_gather_object
+// (:1007-1038) and lets COCOeval compute mask IoUs with `rleIou` on the CPU.
+//
+// Here a mask is stored by its *change positions*: the column-major (COCO order, index x*H + y) pixel indices where
+// the value flips, starting from background.  That is COCO's RLE in cumulative form (counts = successive differences),
+// so areas, IoUs and the COCO counts string all follow from it, and it makes IoU a merge of two sorted interval lists.
+// One image's masks live in a single int32 "pack" tensor (device-resident state, gathered by the sync engine like any
+// list state):
+//     [n, H, W, area_0 .. area_{n-1}, off_0 .. off_n, positions...]      off: start of mask l's positions
+//
+// rle_encode   two kernels over all masks of an update call (one block per mask): (1) per-thread change counts and
+//              the mask area; one D2H copy of the per-mask totals sizes the packs; (2) a block scan of the per-thread
+//              counts and an ordered write of the positions.  Threads own contiguous column strips, so at a fixed row
+//              the lanes of a wave read bytes `c` apart (c = ceil(W / 256)) -- a few cache lines per wave load.
+// rle_iou      one thread per (detection, ground truth) pair: two-pointer merge of the foreground intervals; crowd
+//              ground truths divide by the detection area; size mismatch -> -1 (pycocotools rleIou semantics).
+// The CPU dispatch key runs the same algorithms on host threads.
+#include "common/tm_common.h"
+
+#include <ATen/Parallel.h>
+
+#include <vector>
+
+namespace tm_amd {
+namespace {
+
+constexpr int kThreads = 256;
+
+// foreground interval i of a mask with k change positions: [pos[2i], pos[2i+1]) (open end -> hw)
+__host__ __device__ inline long long rle_intersection(const int* a, int ka, const int* b, int kb, long long hw) {
+  const int na = (ka + 1) / 2, nb = (kb + 1) / 2;
+  int i = 0, j = 0;
+  long long inter = 0;
+  while (i < na && j < nb) {
+    const long long a0 = a[2 * i], a1 = (2 * i + 1 < ka) ? a[2 * i + 1] : hw;
+    const long long b0 = b[2 * j], b1 = (2 * j + 1 < kb) ? b[2 * j + 1] : hw;
+    const long long lo = a0 > b0 ? a0 : b0, hi = a1 < b1 ? a1 : b1;
+    if (hi > lo) inter += hi - lo;
+    if (a1 < b1) ++i;
+    else ++j;
+  }
+  return inter;
+}
+
+__host__ __device__ inline double rle_iou_value(const int* dbuf, const int64_t* dd, const int* gbuf, const int64_t* gd,
+                                                bool crowd) {
+  // desc row: pos_start, k, area, H, W
+  if (dd[3] != gd[3] || dd[4] != gd[4]) return -1.0;
+  const long long inter = rle_intersection(dbuf + dd[0], static_cast<int>(dd[1]), gbuf + gd[0],
+                                           static_cast<int>(gd[1]), dd[3] * dd[4]);
+  if (inter == 0) return 0.0;
+  const long long uni = crowd ? dd[2] : dd[2] + gd[2] - inter;
+  return static_cast<double>(inter) / static_cast<double>(uni);
+}
+
+__device__ inline int block_exclusive_scan(int v, int* lds_wave) {
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  int inc = v;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const int o = __shfl_up(inc, off, kWave);
+    if (lane >= off) inc += o;
+  }
+  if (lane == kWave - 1) lds_wave[wid] = inc;
+  __syncthreads();
+  int base = 0;
+  for (int w = 0; w < wid; ++w) base += lds_wave[w];
+  return base + inc - v;
+}
+
+// table row: ptr, H, W
+__global__ void __launch_bounds__(kThreads) rle_count_kernel(const int64_t* __restrict__ table, int* __restrict__ tcnt,
+                                                              int* __restrict__ stats) {
+  const int mid = blockIdx.x, tid = threadIdx.x;
+  const uint8_t* m = reinterpret_cast<const uint8_t*>(table[mid * 3]);
+  const int H = static_cast<int>(table[mid * 3 + 1]), W = static_cast<int>(table[mid * 3 + 2]);
+  const int c = (W + kThreads - 1) / kThreads;
+  const int x0 = tid * c, x1 = min(W, x0 + c);
+  int chg = 0, ones = 0;
+  if (x0 < x1 && H > 0) {
+    int prev = x0 == 0 ? 0 : (m[static_cast<long long>(H - 1) * W + x0 - 1] != 0);
+    for (int x = x0; x < x1; ++x) {
+      for (int y = 0; y < H; ++y) {
+        const int v = m[static_cast<long long>(y) * W + x] != 0;
+        chg += v != prev;
+        ones += v;
+        prev = v;
+      }
+    }
+  }
+  tcnt[static_cast<long long>(mid) * kThreads + tid] = chg;
+  __shared__ int red[2][kThreads / kWave];
+  const int wc = wave_sum(chg), wo = wave_sum(ones);
+  if ((tid & (kWave - 1)) == 0) {
+    red[0][tid / kWave] = wc;
+    red[1][tid / kWave] = wo;
+  }
+  __syncthreads();
+  if (tid < 2) {
+    int s = 0;
+    for (int w = 0; w < kThreads / kWave; ++w) s += red[tid][w];
+    stats[mid * 2 + tid] = s;
+  }
+}
+
+// table row: ptr, H, W, pack_base, l, n, off_rel, nchg, area
+__global__ void __launch_bounds__(kThreads) rle_write_kernel(const int64_t* __restrict__ table,
+                                                              const int* __restrict__ tcnt, int* __restrict__ out) {
+  const int mid = blockIdx.x, tid = threadIdx.x;
+  const int64_t* row = table + mid * 9;
+  const uint8_t* m = reinterpret_cast<const uint8_t*>(row[0]);
+  const int H = static_cast<int>(row[1]), W = static_cast<int>(row[2]);
+  const long long n = row[5], l = row[4], off_rel = row[6];
+  int* pack = out + row[3];
+  if (tid == 0) {
+    if (l == 0) {
+      pack[0] = static_cast<int>(n);
+      pack[1] = H;
+      pack[2] = W;
+    }
+    pack[3 + l] = static_cast<int>(row[8]);
+    pack[3 + n + l] = static_cast<int>(off_rel);
+    if (l == n - 1) pack[3 + 2 * n] = static_cast<int>(off_rel + row[7]);
+  }
+  __shared__ int wsum[kThreads / kWave];
+  int k = block_exclusive_scan(tcnt[static_cast<long long>(mid) * kThreads + tid], wsum);
+  int* pos = pack + 3 + 2 * n + 1 + off_rel;
+  const int c = (W + kThreads - 1) / kThreads;
+  const int x0 = tid * c, x1 = min(W, x0 + c);
+  if (x0 >= x1 || H <= 0) return;
+  int prev = x0 == 0 ? 0 : (m[static_cast<long long>(H - 1) * W + x0 - 1] != 0);
+  for (int x = x0; x < x1; ++x) {
+    for (int y = 0; y < H; ++y) {
+      const int v = m[static_cast<long long>(y) * W + x] != 0;
+      if (v != prev) pos[k++] = x * H + y;
+      prev = v;
+    }
+  }
+}
+
+__global__ void rle_iou_kernel(const int* __restrict__ dbuf, const int64_t* __restrict__ ddesc,
+                               const int* __restrict__ gbuf, const int64_t* __restrict__ gdesc,
+                               const int64_t* __restrict__ pd, const int64_t* __restrict__ pg,
+                               const uint8_t* __restrict__ gcrowd, long long P, double* __restrict__ out) {
+  for (long long p = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; p < P;
+       p += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int64_t d = pd[p], g = pg[p];
+    out[p] = rle_iou_value(dbuf, ddesc + d * 5, gbuf, gdesc + g * 5, gcrowd[g] != 0);
+  }
+}
+
+struct MaskRef {
+  const uint8_t* ptr;
+  int64_t h, w;
+  int64_t image, local, n;
+};
+
+std::vector<MaskRef> mask_refs(at::TensorList masks, std::vector<at::Tensor>& keep) {
+  std::vector<MaskRef> refs;
+  for (size_t i = 0; i < masks.size(); ++i) {
+    TORCH_CHECK(masks[i].dim() == 3, "rle_encode: masks must be [n, H, W]");
+    at::Tensor m = masks[i];
+    if (m.scalar_type() != at::kBool && m.scalar_type() != at::kByte) m = m.ne(0);
+    m = m.contiguous();
+    keep.push_back(m);
+    const int64_t n = m.size(0), h = m.size(1), w = m.size(2);
+    TORCH_CHECK(h * w < (1LL << 31), "rle_encode: H * W must be < 2^31");
+    for (int64_t l = 0; l < n; ++l)
+      refs.push_back({reinterpret_cast<const uint8_t*>(m.data_ptr()) + l * h * w, h, w, static_cast<int64_t>(i), l, n});
+  }
+  return refs;
+}
+
+// per-image pack sizes / bases from the per-mask change counts
+int64_t pack_layout(at::TensorList masks, const std::vector<MaskRef>& refs, const int* nchg,
+                    std::vector<int64_t>& base, std::vector<int64_t>& off_rel) {
+  base.assign(masks.size(), 0);
+  off_rel.assign(refs.size(), 0);
+  std::vector<int64_t> tot(masks.size(), 0);
+  for (size_t r = 0; r < refs.size(); ++r) {
+    off_rel[r] = tot[refs[r].image];
+    tot[refs[r].image] += nchg[r];
+  }
+  int64_t total = 0;
+  for (size_t i = 0; i < masks.size(); ++i) {
+    base[i] = total;
+    total += 3 + 2 * masks[i].size(0) + 1 + tot[i];
+  }
+  TORCH_CHECK(total < (1LL << 31), "rle_encode: packed masks of one call exceed 2^31 words");
+  return total;
+}
+
+std::vector<at::Tensor> split_packs(const at::Tensor& buf, at::TensorList masks, const std::vector<int64_t>& base) {
+  std::vector<at::Tensor> out;
+  for (size_t i = 0; i < masks.size(); ++i) {
+    const int64_t end = i + 1 < masks.size() ? base[i + 1] : buf.numel();
+    out.push_back(buf.narrow(0, base[i], end - base[i]));
+  }
+  return out;
+}
+
+}  // namespace
+
+std::vector<at::Tensor> rle_encode_cuda(at::TensorList masks) {
+  TORCH_CHECK(!masks.empty(), "rle_encode: empty list");
+  TM_CHECK_CUDA(masks[0]);
+  for (const auto& m : masks) TM_SAME_DEVICE(masks[0], m);
+  std::vector<at::Tensor> keep;
+  const std::vector<MaskRef> refs = mask_refs(masks, keep);
+  const int64_t N = static_cast<int64_t>(refs.size());
+  auto i64 = at::TensorOptions().dtype(at::kLong);
+  auto dev_i32 = masks[0].options().dtype(at::kInt);
+  std::vector<int64_t> base, off_rel;
+  at::Tensor buf;
+  if (N > 0) {
+    TORCH_CHECK(N < (1LL << 31), "rle_encode: too many masks");
+    at::Tensor t1 = at::empty({N, 3}, i64);
+    int64_t* t1p = t1.data_ptr<int64_t>();
+    for (int64_t r = 0; r < N; ++r) {
+      t1p[r * 3] = reinterpret_cast<int64_t>(refs[r].ptr);
+      t1p[r * 3 + 1] = refs[r].h;
+      t1p[r * 3 + 2] = refs[r].w;
+    }
+    at::Tensor t1d = t1.to(masks[0].device());
+    at::Tensor tcnt = at::empty({N, kThreads}, dev_i32);
+    at::Tensor stats = at::empty({N, 2}, dev_i32);
+    hipLaunchKernelGGL(rle_count_kernel, dim3(static_cast<unsigned>(N)), dim3(kThreads), 0, stream(),
+                       t1d.data_ptr<int64_t>(), tcnt.data_ptr<int>(), stats.data_ptr<int>());
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+    at::Tensor st = stats.cpu();  // the one host sync of an update: sizes the packs
+    const int* sp = st.data_ptr<int>();
+    std::vector<int> nchg(N);
+    for (int64_t r = 0; r < N; ++r) nchg[r] = sp[r * 2];
+    const int64_t total = pack_layout(masks, refs, nchg.data(), base, off_rel);
+    buf = at::empty({total}, dev_i32);
+    at::Tensor t2 = at::empty({N, 9}, i64);
+    int64_t* t2p = t2.data_ptr<int64_t>();
+    for (int64_t r = 0; r < N; ++r) {
+      const MaskRef& f = refs[r];
+      const int64_t row[9] = {reinterpret_cast<int64_t>(f.ptr), f.h, f.w, base[f.image], f.local, f.n,
+                              off_rel[r], nchg[r], sp[r * 2 + 1]};
+      for (int c = 0; c < 9; ++c) t2p[r * 9 + c] = row[c];
+    }
+    at::Tensor t2d = t2.to(masks[0].device());
+    hipLaunchKernelGGL(rle_write_kernel, dim3(static_cast<unsigned>(N)), dim3(kThreads), 0, stream(),
+                       t2d.data_ptr<int64_t>(), tcnt.data_ptr<int>(), buf.data_ptr<int>());
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  } else {
+    pack_layout(masks, refs, nullptr, base, off_rel);
+    buf = at::empty({static_cast<int64_t>(4 * masks.size())}, dev_i32);
+  }
+  // images without masks: [0, H, W, 0] headers written from the host (rare; one small copy each)
+  for (size_t i = 0; i < masks.size(); ++i) {
+    if (masks[i].size(0) != 0) continue;
+    at::Tensor h = at::tensor({0, static_cast<int>(masks[i].size(1)), static_cast<int>(masks[i].size(2)), 0},
+                              at::TensorOptions().dtype(at::kInt));
+    buf.narrow(0, base[i], 4).copy_(h, /*non_blocking=*/false);
+  }
+  return split_packs(buf, masks, base);
+}
+
+std::vector<at::Tensor> rle_encode_cpu(at::TensorList masks) {
+  TORCH_CHECK(!masks.empty(), "rle_encode: empty list");
+  std::vector<at::Tensor> keep;
+  const std::vector<MaskRef> refs = mask_refs(masks, keep);
+  const int64_t N = static_cast<int64_t>(refs.size());
+  std::vector<int> nchg(N), area(N);
+  at::parallel_for(0, N, 1, [&](int64_t b, int64_t e) {
+    for (int64_t r = b; r < e; ++r) {
+      const MaskRef& f = refs[r];
+      int prev = 0, c = 0, a = 0;
+      for (int64_t x = 0; x < f.w; ++x)
+        for (int64_t y = 0; y < f.h; ++y) {
+          const int v = f.ptr[y * f.w + x] != 0;
+          c += v != prev;
+          a += v;
+          prev = v;
+        }
+      nchg[r] = c;
+      area[r] = a;
+    }
+  });
+  std::vector<int64_t> base, off_rel;
+  const int64_t total = pack_layout(masks, refs, nchg.data(), base, off_rel);
+  at::Tensor buf = at::empty({total}, at::TensorOptions().dtype(at::kInt));
+  int* out = buf.data_ptr<int>();
+  for (size_t i = 0; i < masks.size(); ++i) {
+    int* pack = out + base[i];
+    const int64_t n = masks[i].size(0);
+    pack[0] = static_cast<int>(n);
+    pack[1] = static_cast<int>(masks[i].size(1));
+    pack[2] = static_cast<int>(masks[i].size(2));
+    pack[3 + 2 * n] = 0;
+  }
+  at::parallel_for(0, N, 1, [&](int64_t b, int64_t e) {
+    for (int64_t r = b; r < e; ++r) {
+      const MaskRef& f = refs[r];
+      int* pack = out + base[f.image];
+      pack[3 + f.local] = area[r];
+      pack[3 + f.n + f.local] = static_cast<int>(off_rel[r]);
+      if (f.local == f.n - 1) pack[3 + 2 * f.n] = static_cast<int>(off_rel[r] + nchg[r]);
+      int* pos = pack + 3 + 2 * f.n + 1 + off_rel[r];
+      int prev = 0, k = 0;
+      for (int64_t x = 0; x < f.w; ++x)
+        for (int64_t y = 0; y < f.h; ++y) {
+          const int v = f.ptr[y * f.w + x] != 0;
+          if (v != prev) pos[k++] = static_cast<int>(x * f.h + y);
+          prev = v;
+        }
+    }
+  });
+  return split_packs(buf, masks, base);
+}
+
+static void check_iou_args(const at::Tensor& dbuf, const at::Tensor& ddesc, const at::Tensor& gbuf,
+                           const at::Tensor& gdesc, const at::Tensor& pd, const at::Tensor& pg,
+                           const at::Tensor& gcrowd) {
+  TORCH_CHECK(dbuf.scalar_type() == at::kInt && gbuf.scalar_type() == at::kInt, "rle_iou: int32 buffers");
+  TORCH_CHECK(ddesc.scalar_type() == at::kLong && gdesc.scalar_type() == at::kLong && ddesc.dim() == 2 &&
+                  gdesc.dim() == 2 && ddesc.size(1) == 5 && gdesc.size(1) == 5,
+              "rle_iou: descriptors must be int64 [N, 5]");
+  TORCH_CHECK(pd.scalar_type() == at::kLong && pg.scalar_type() == at::kLong && pd.numel() == pg.numel(),
+              "rle_iou: int64 pair indices of equal length");
+  TORCH_CHECK(gcrowd.scalar_type() == at::kByte && gcrowd.numel() == gdesc.size(0), "rle_iou: uint8 crowd per gt");
+  for (const at::Tensor* t : {&dbuf, &ddesc, &gbuf, &gdesc, &pd, &pg, &gcrowd}) TM_CHECK_CONTIG(*t);
+}
+
+// pair indices are trusted to be in range: the caller builds them from the descriptor row counts
+at::Tensor rle_iou_cuda(const at::Tensor& dbuf, const at::Tensor& ddesc, const at::Tensor& gbuf,
+                        const at::Tensor& gdesc, const at::Tensor& pd, const at::Tensor& pg,
+                        const at::Tensor& gcrowd) {
+  TM_CHECK_CUDA(pd);
+  for (const at::Tensor* t : {&dbuf, &ddesc, &gbuf, &gdesc, &pg, &gcrowd}) TM_SAME_DEVICE(pd, *t);
+  check_iou_args(dbuf, ddesc, gbuf, gdesc, pd, pg, gcrowd);
+  const long long P = pd.numel();
+  at::Tensor out = at::empty({P}, pd.options().dtype(at::kDouble));
+  if (P == 0) return out;
+  hipLaunchKernelGGL(rle_iou_kernel, dim3(grid_cap((P + 255) / 256, 256 * 64)), dim3(256), 0, stream(),
+                     dbuf.data_ptr<int>(), ddesc.data_ptr<int64_t>(), gbuf.data_ptr<int>(), gdesc.data_ptr<int64_t>(),
+                     pd.data_ptr<int64_t>(), pg.data_ptr<int64_t>(), gcrowd.data_ptr<uint8_t>(), P,
+                     out.data_ptr<double>());
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return out;
+}
+
+at::Tensor rle_iou_cpu(const at::Tensor& dbuf, const at::Tensor& ddesc, const at::Tensor& gbuf,
+                       const at::Tensor& gdesc, const at::Tensor& pd, const at::Tensor& pg, const at::Tensor& gcrowd) {
+  check_iou_args(dbuf, ddesc, gbuf, gdesc, pd, pg, gcrowd);
+  const int64_t P = pd.numel();
+  at::Tensor out = at::empty({P}, at::TensorOptions().dtype(at::kDouble));
+  const int* db = dbuf.data_ptr<int>();
+  const int* gb = gbuf.data_ptr<int>();
+  const int64_t *dd = ddesc.data_ptr<int64_t>(), *gd = gdesc.data_ptr<int64_t>();
+  const int64_t *pdp = pd.data_ptr<int64_t>(), *pgp = pg.data_ptr<int64_t>();
+  const uint8_t* cr = gcrowd.data_ptr<uint8_t>();
+  double* o = out.data_ptr<double>();
+  const int64_t nd = ddesc.size(0), ng = gdesc.size(0);
+  at::parallel_for(0, P, 256, [&](int64_t b, int64_t e) {
+    for (int64_t p = b; p < e; ++p) {
+      TORCH_CHECK(pdp[p] >= 0 && pdp[p] < nd && pgp[p] >= 0 && pgp[p] < ng, "rle_iou: pair index out of range");
+      o[p] = rle_iou_value(db, dd + pdp[p] * 5, gb, gd + pgp[p] * 5, cr[pgp[p]] != 0);
+    }
+  });
+  return out;
+}
+
+TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def("rle_encode(Tensor[] masks) -> Tensor[]");
+  m.def("rle_iou(Tensor dbuf, Tensor ddesc, Tensor gbuf, Tensor gdesc, Tensor pd, Tensor pg, Tensor gcrowd) -> Tensor");
+}
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
+  m.impl("rle_encode", &rle_encode_cuda);
+  m.impl("rle_iou", &rle_iou_cuda);
+}
+TORCH_LIBRARY_IMPL(tm_amd, CPU, m) {
+  m.impl("rle_encode", &rle_encode_cpu);
+  m.impl("rle_iou", &rle_iou_cpu);
+}
+
+}  // namespace tm_amd

@@ -18,8 +18,13 @@ def _iou(d, g, crowd):
     return inter / u
 
 
-def coco_eval(dets, gts, cats, iou_thrs, rec_thrs, max_dets):
-    """dets: per image list of (box_xywh, score, cat); gts: per image list of (box_xywh, cat, crowd, area)."""
+def coco_eval(dets, gts, cats, iou_thrs, rec_thrs, max_dets, iou_fn=None, area_fn=None):
+    """dets: per image list of (box_xywh, score, cat); gts: per image list of (box_xywh, cat, crowd, area).
+
+    ``iou_fn(d_geom, g_geom, crowd)`` / ``area_fn(d_geom)`` replace the box IoU / area (e.g. dense-mask IoU for segm,
+    with the geometry slot holding a numpy mask)."""
+    iou_fn = iou_fn or _iou
+    area_fn = area_fn or (lambda b: b[2] * b[3])
     T, R, K, A, M = len(iou_thrs), len(rec_thrs), len(cats), len(AREAS), len(max_dets)
     evals = {}
     for img in range(len(dets)):
@@ -46,7 +51,7 @@ def coco_eval(dets, gts, cats, iou_thrs, rec_thrs, max_dets):
                                 continue
                             if m > -1 and gi[m] == 0 and gi[j] == 1:
                                 break
-                            v = _iou(d[0], g[0], g[2])
+                            v = iou_fn(d[0], g[0], g[2])
                             if v < best:
                                 continue
                             best, m = v, j
@@ -56,7 +61,7 @@ def coco_eval(dets, gts, cats, iou_thrs, rec_thrs, max_dets):
                         dtm[t, di] = 1
                         gtm[m] = 1
                 for di, d in enumerate(dt):
-                    area = d[0][2] * d[0][3]
+                    area = area_fn(d[0])
                     if area < lo or area > hi:
                         dtig[:, di] = np.where(dtm[:, di] == 0, 1, dtig[:, di])
                 evals[(img, k, a)] = (np.array([d[1] for d in dt]), dtm, dtig, np.array(gi))

@@ -109,12 +109,19 @@ def test_map_vs_python_coco_oracle(device, seed):
 @pytest.mark.parametrize("device", DEVICES)
 def test_map_max_dets_and_micro(device):
     preds, target = _random_coco(5, n_img=6, max_det=30)
-    m = MeanAveragePrecision(max_detection_thresholds=[2, 5, 20]).to(device)
+    m = MeanAveragePrecision(max_detection_thresholds=[2, 5, 20], backend="faster_coco_eval").to(device)
     m.update(_to(preds, device), _to(target, device))
     res = m.compute()
     stats, _, _ = _oracle(preds, target, max_dets=(2, 5, 20))
     for name, v in zip(["map", "mar_2", "mar_5", "mar_20"], [stats[0], stats[6], stats[7], stats[8]]):
         assert_close(res[name], v, atol=1e-6)
+    # pycocotools' summarize takes mAP at a hard-coded 100 detections: -1 without that threshold, the rest unchanged
+    legacy = MeanAveragePrecision(max_detection_thresholds=[2, 5, 20]).to(device)
+    legacy.update(_to(preds, device), _to(target, device))
+    rl = legacy.compute()
+    assert float(rl["map"]) == -1.0
+    for name in ("map_50", "map_75", "mar_2", "mar_5", "mar_20"):
+        assert_close(rl[name], res[name], atol=1e-7)
     mm = MeanAveragePrecision(average="micro").to(device)
     mm.update(_to(preds, device), _to(target, device))
     zero = [{**p, "labels": torch.zeros_like(p["labels"])} for p in preds]
@@ -448,3 +455,31 @@ def test_nms_native_host_matches_matrix_fallback(batched):
     scores = torch.rand(700, generator=g)
     idxs = torch.randint(0, 4, (700,), generator=g) if batched else None
     assert torch.equal(ops.nms(boxes, scores, 0.45, idxs), _cpu.nms(boxes, scores, 0.45, idxs))
+
+
+@pytest.mark.parametrize("backend", ["pycocotools", "faster_coco_eval"])
+def test_map_many_detection_thresholds_reference_case(backend):
+    """``T/unittests/detection/test_map.py:826-856``: 0.6 with faster-coco-eval, not with pycocotools."""
+    preds = [{"boxes": torch.tensor([[258.0, 41.0, 606.0, 285.0]]), "scores": torch.tensor([0.536]),
+              "labels": torch.tensor([0])}]
+    target = [{"boxes": torch.tensor([[214.0, 41.0, 562.0, 285.0]]), "labels": torch.tensor([0])}]
+    metric = MeanAveragePrecision(max_detection_thresholds=[1, 10, 1000], backend=backend)
+    res = metric(preds, target)
+    if backend == "pycocotools":
+        assert round(res["map"].item(), 5) != 0.6
+    else:
+        assert round(res["map"].item(), 5) == 0.6
+    assert "mar_1" in res and "mar_10" in res and "mar_1000" in res
+
+
+@pytest.mark.parametrize(("box_format", "iou_val_expected", "map_val_expected"),
+                         [("xyxy", 0.25, 1), ("xywh", 0.143, 0.0), ("cxcywh", 0.143, 0.0)])
+def test_map_box_format_reference_case(box_format, iou_val_expected, map_val_expected):
+    """``T/unittests/detection/test_map.py:686-712``: only the right box format scores 1."""
+    preds = [{"boxes": torch.tensor([[0.5, 0.5, 1, 1]]), "scores": torch.tensor([1.0]), "labels": torch.tensor([0])}]
+    targets = [{"boxes": torch.tensor([[0, 0, 1, 1]]), "labels": torch.tensor([0])}]
+    metric = MeanAveragePrecision(box_format=box_format, iou_thresholds=[0.2], extended_summary=True)
+    metric.update(preds, targets)
+    result = metric.compute()
+    assert result["map"].item() == map_val_expected
+    assert round(float(result["ious"][(0, 0)]), 3) == iou_val_expected

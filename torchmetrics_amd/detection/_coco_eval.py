@@ -44,13 +44,14 @@ def coco_evaluate(
     rec_thresholds: Sequence[float],
     max_dets: Sequence[int],
     classes: Tensor,
-    det_masks: Optional[Sequence[Tensor]] = None,
-    gt_masks: Optional[Sequence[Tensor]] = None,
+    det_rle: Optional[Tuple[Tensor, Tensor]] = None,
+    gt_rle: Optional[Tuple[Tensor, Tensor]] = None,
 ) -> Dict[str, Tensor]:
     """COCO precision ``[T, R, K, A, M]``, recall ``[T, K, A, M]`` and scores.
 
-    Boxes are xywh.  With ``det_masks`` / ``gt_masks`` (``[n, H, W]`` per image) IoUs are mask IoUs and areas are
-    mask areas (``segm``).  ``classes`` are the sorted category ids of the K axis; annotations whose label is not
+    Boxes are xywh.  With ``det_rle`` / ``gt_rle`` (``(buffer, descriptors)`` of the run-length encoded masks, one
+    descriptor row per annotation in flat image order, :func:`torchmetrics_amd.detection._rle.descriptors`) IoUs are
+    mask IoUs and areas are mask areas (``segm``).  ``classes`` are the sorted category ids of the K axis; annotations whose label is not
     among them are dropped (pycocotools ``catIds`` filtering).
     """
     dev = classes.device
@@ -77,23 +78,26 @@ def coco_evaluate(
     d_cls = torch.searchsorted(classes, d_lab).clamp(max=K - 1)
     g_cls = torch.searchsorted(classes, g_lab).clamp(max=K - 1)
     keep_d, keep_g = classes[d_cls] == d_lab, classes[g_cls] == g_lab
-    segm = det_masks is not None
+    segm = det_rle is not None
     if segm:
         d_box = torch.zeros(d_lab.numel(), 4, dtype=torch.float64, device=dev)
         g_box = torch.zeros(g_lab.numel(), 4, dtype=torch.float64, device=dev)
-        d_area = flat([m.flatten(1).sum(1) for m in det_masks], torch.float64)
-        g_mask_area = flat([m.flatten(1).sum(1) for m in gt_masks], torch.float64)
+        d_area = det_rle[1][:, 2].to(torch.float64)
+        g_mask_area = gt_rle[1][:, 2].to(torch.float64)
     else:
         d_box, g_box = flat(det_boxes, torch.float64, (4,)), flat(gt_boxes, torch.float64, (4,))
         d_area = d_box[:, 2] * d_box[:, 3]
         g_mask_area = g_box[:, 2] * g_box[:, 3]
     d_score = flat(det_scores, torch.float64)
-    g_crowd = flat(gt_crowds, torch.long).clamp(0, 1).to(torch.uint8)
+    g_crowd_all = flat(gt_crowds, torch.long).clamp(0, 1).to(torch.uint8)
     g_area_in = flat(gt_areas, torch.float64)
     g_area = torch.where(g_area_in > 0, g_area_in, g_mask_area)
+    d_idx = torch.arange(d_lab.numel(), device=dev)
+    g_idx = torch.arange(g_lab.numel(), device=dev)
     # drop annotations outside the category axis (micro averaging relabels everything to 0)
-    d_img, d_cls, d_box, d_area, d_score = (x[keep_d] for x in (d_img, d_cls, d_box, d_area, d_score))
-    g_img, g_cls, g_box, g_area, g_crowd = (x[keep_g] for x in (g_img, g_cls, g_box, g_area, g_crowd))
+    d_img, d_cls, d_box, d_area, d_score, d_idx = (x[keep_d] for x in (d_img, d_cls, d_box, d_area, d_score, d_idx))
+    g_img, g_cls, g_box, g_area, g_crowd, g_idx = (x[keep_g] for x in (g_img, g_cls, g_box, g_area, g_crowd_all,
+                                                                       g_idx))
 
     # (1) detections grouped by (image, category), score-descending (stable), truncated to max_dets[-1]
     d_group = d_img * K + d_cls
@@ -114,9 +118,9 @@ def coco_evaluate(
 
     # (2) greedy matching for every (group, area range, IoU threshold)
     pre, off = None, None
-    if det_masks is not None:
-        pre, off = _mask_iou_blocks(det_masks, gt_masks, dsz, gsz, order, g_order, grp_s, det_start, gt_start,
-                                    gt_cnt, g_crowd, keep_d, keep_g)
+    if segm:
+        pre, off = _rle_iou_blocks(det_rle, gt_rle, g_crowd_all, d_idx[order], g_idx[g_order], grp_s, det_cnt,
+                                   gt_start, gt_cnt)
     dt_match, dt_ig = ops.coco_match(
         d_box[order].contiguous(), d_area[order].contiguous(), g_box[g_order].contiguous(),
         g_area[g_order].contiguous(), g_crowd[g_order].contiguous(), det_start.int(), det_cnt.int(),
@@ -141,7 +145,6 @@ def coco_evaluate(
         is_last = torch.ones(n, dtype=torch.bool, device=dev)
         is_last[:-1] = cls_s[1:] != cls_s[:-1]
         seg_id = torch.cumsum((torch.arange(n, device=dev) == seg_first).long(), 0) - 1
-        n_seg = int(seg_id[-1].item()) + 1
         npig_d = npig[:, cls_s].clamp(min=1)[None]  # [1, A, D]
         eps = torch.finfo(torch.float64).eps
         for mi, md in enumerate(max_dets):
@@ -154,7 +157,7 @@ def coco_evaluate(
             rc = tp_c / npig_d
             pr = tp_c / (tp_c + fp_c + eps)
             # precision envelope: running max from the end of each category segment
-            off = 2.0 * (n_seg - 1 - seg_id).to(torch.float64)
+            off = 2.0 * (seg_id[-1] - seg_id).to(torch.float64)
             env = (pr.flip(-1) + off.flip(-1)).cummax(-1).values.flip(-1) - off
             # recall thresholds in (rc of the previous included detection, rc] belong to this detection
             inc = (rank_s < md).long()
@@ -204,10 +207,17 @@ def _masked_mean(s: Tensor) -> Tensor:
                                                                                  device=s.device))
 
 
-def coco_summarize(ev: Dict[str, Tensor], iou_thresholds: Sequence[float], max_dets: Sequence[int]) -> Tensor:
-    """The 12 COCO summary numbers (``COCOeval.summarize``) as a float64 device tensor."""
+def coco_summarize(ev: Dict[str, Tensor], iou_thresholds: Sequence[float], max_dets: Sequence[int],
+                   map_max_det: Optional[int] = None) -> Tensor:
+    """The 12 COCO summary numbers (``COCOeval.summarize``) as a float64 device tensor.
+
+    ``map_max_det=100`` reproduces pycocotools' ``summarize``, whose first number (mAP) is taken at a hard-coded 100
+    detections -- -1 when 100 is not among ``max_dets`` (the reference's ``backend="pycocotools"``,
+    ``T/unittests/detection/test_map.py:826-856``); ``None`` uses the largest threshold (faster-coco-eval).
+    """
     prec, rec = ev["precision"], ev["recall"]
     thr = list(iou_thresholds)
+    missing = torch.tensor(-1.0, dtype=prec.dtype, device=prec.device)
 
     def ap(iou=None, area=0, m=len(max_dets) - 1):
         s = prec[..., area, m]
@@ -219,72 +229,51 @@ def coco_summarize(ev: Dict[str, Tensor], iou_thresholds: Sequence[float], max_d
     def ar(area=0, m=len(max_dets) - 1):
         return _masked_mean(rec[..., area, m])
 
-    stats = [ap(), ap(0.5), ap(0.75), ap(area=1), ap(area=2), ap(area=3), ar(m=0), ar(m=1), ar(m=2),
+    first = ap() if map_max_det is None else (
+        ap(m=list(max_dets).index(map_max_det)) if map_max_det in max_dets else missing)
+    stats = [first, ap(0.5), ap(0.75), ap(area=1), ap(area=2), ap(area=3), ar(m=0), ar(m=1), ar(m=2),
              ar(area=1), ar(area=2), ar(area=3)]
     return torch.stack(stats)
 
 
-def per_class_stats(ev: Dict[str, Tensor]) -> Tuple[Tensor, Tensor]:
-    """Per-category mAP (all areas, last max-dets) and mAR at the last max-dets, -1 where undefined."""
-    prec = ev["precision"][..., 0, -1]  # [T, R, K]
+def per_class_stats(ev: Dict[str, Tensor], max_dets: Optional[Sequence[int]] = None,
+                    map_max_det: Optional[int] = None) -> Tuple[Tensor, Tensor]:
+    """Per-category mAP (all areas) and mAR at the last max-dets, -1 where undefined; mAP at ``map_max_det``
+    detections when given (pycocotools' per-class ``stats[0]``, -1 without such a threshold)."""
+    m_ap = -1
+    if map_max_det is not None and max_dets is not None:
+        m_ap = list(max_dets).index(map_max_det) if map_max_det in max_dets else None
     rec = ev["recall"][..., 0, -1]  # [T, K]
-    pv, rv = prec > -1, rec > -1
-    p_cnt, r_cnt = pv.sum((0, 1)), rv.sum(0)
-    mp = torch.where(p_cnt > 0, (prec * pv).sum((0, 1)) / p_cnt.clamp(min=1), torch.full_like(p_cnt, -1.0,
-                                                                                                dtype=prec.dtype))
+    rv = rec > -1
+    r_cnt = rv.sum(0)
     mr = torch.where(r_cnt > 0, (rec * rv).sum(0) / r_cnt.clamp(min=1), torch.full_like(r_cnt, -1.0,
                                                                                         dtype=rec.dtype))
+    if m_ap is None:
+        return torch.full_like(mr, -1.0), mr
+    prec = ev["precision"][..., 0, m_ap]  # [T, R, K]
+    pv = prec > -1
+    p_cnt = pv.sum((0, 1))
+    mp = torch.where(p_cnt > 0, (prec * pv).sum((0, 1)) / p_cnt.clamp(min=1), torch.full_like(p_cnt, -1.0,
+                                                                                                dtype=prec.dtype))
     return mp, mr
 
 
-def _mask_iou_blocks(det_masks, gt_masks, dsz, gsz, order, g_order, grp_s, det_start, gt_start, gt_cnt, g_crowd,
-                     keep_d, keep_g) -> Tuple[Tensor, Tensor]:
-    """Per-group ``[det, gt]`` mask-IoU blocks laid out for ``coco_match`` (crowd gt: intersection / det area).
+def _rle_iou_blocks(det_rle: Tuple[Tensor, Tensor], gt_rle: Tuple[Tensor, Tensor], crowd: Tensor, d_of: Tensor,
+                    g_of: Tensor, grp_s: Tensor, det_cnt: Tensor, gt_start: Tensor, gt_cnt: Tensor) -> Tuple[Tensor,
+                                                                                                          Tensor]:
+    """Per-group ``[det, gt]`` mask-IoU blocks laid out for ``coco_match``, from the run-length encoded masks.
 
-    Each image's full IoU matrix is one GEMM of the flattened binary masks (exact fp32 pixel counts).
+    Every (detection, ground truth) pair of a group is one entry of a flat pair list -- block of group ``g`` at
+    ``off[g]``, row ``k`` = ``k``-th score-ordered detection, ``gt_cnt[g]`` columns in ground-truth order -- and
+    ``ops.rle_iou`` evaluates them all in one launch (crowd ground truths: intersection over detection area).
+    ``d_of`` / ``g_of`` map sorted detections / ground truths to their descriptor rows; ``crowd`` is per descriptor row.
     """
     dev = grp_s.device
-    mats, offs = [], [0]
-    for dm, gm in zip(det_masks, gt_masks):
-        nd, ng = dm.shape[0], gm.shape[0]
-        if nd and ng:
-            a = dm.reshape(nd, -1).to(device=dev, dtype=torch.float32)
-            b = gm.reshape(ng, -1).to(device=dev, dtype=torch.float32)
-            inter = (a @ b.T).double()
-            da, ga = a.sum(1).double(), b.sum(1).double()
-            mats.append((inter, da, ga))
-        else:
-            mats.append(None)
-        offs.append(offs[-1] + nd * ng)
-    # crowd flags in original (unfiltered) gt order
-    crowd_full = torch.zeros(int(gsz.sum().item()), dtype=torch.bool, device=dev)
-    crowd_full[torch.nonzero(keep_g).flatten()] = g_crowd.bool()
-    g_base = torch.cumsum(gsz, 0) - gsz
-    flat_iou = torch.zeros(max(offs[-1], 1), dtype=torch.float64, device=dev)
-    for i, m in enumerate(mats):
-        if m is None:
-            continue
-        inter, da, ga = m
-        crowd = crowd_full[g_base[i]: g_base[i] + ga.numel()]
-        union = torch.where(crowd[None, :], da[:, None], da[:, None] + ga[None, :] - inter)
-        iou = torch.where(union > 0, inter / union.clamp(min=1e-12), torch.zeros_like(inter))
-        flat_iou[offs[i]: offs[i + 1]] = iou.flatten()
-    img_off = torch.tensor(offs[:-1], dtype=torch.long, device=dev)
-    d_orig = torch.nonzero(keep_d).flatten()[order]  # flat (unfiltered) index of each sorted detection
-    g_orig = torch.nonzero(keep_g).flatten()[g_order]
-    d_img = torch.repeat_interleave(torch.arange(gsz.numel(), device=dev), dsz)[d_orig]
-    d_base = torch.cumsum(dsz, 0) - dsz
-    d_loc = d_orig - d_base[d_img]
-    g_img_all = torch.repeat_interleave(torch.arange(gsz.numel(), device=dev), gsz)
-    g_loc_sorted = g_orig - g_base[g_img_all[g_orig]]
-    # block of group g starts at iou_off[g]; row k (k-th det of the group) holds gt_cnt[g] values
     reps = gt_cnt[grp_s]
     block_rows = torch.repeat_interleave(torch.arange(grp_s.numel(), device=dev), reps)
     col = torch.arange(block_rows.numel(), device=dev) - torch.repeat_interleave(torch.cumsum(reps, 0) - reps, reps)
-    gsorted_idx = gt_start[grp_s[block_rows]] + col
-    ng_img = gsz[d_img[block_rows]]
-    vals = flat_iou[img_off[d_img[block_rows]] + d_loc[block_rows] * ng_img + g_loc_sorted[gsorted_idx]]
-    det_cnt = torch.bincount(grp_s, minlength=gt_cnt.numel())
+    pd = d_of[block_rows].contiguous()
+    pg = g_of[gt_start[grp_s[block_rows]] + col].contiguous()
+    vals = ops.rle_iou(det_rle[0], det_rle[1], gt_rle[0], gt_rle[1], pd, pg, crowd.contiguous())
     sizes = det_cnt * gt_cnt
-    iou_off = torch.cumsum(sizes, 0) - sizes
-    return vals.contiguous(), iou_off.contiguous()
+    return vals.contiguous(), (torch.cumsum(sizes, 0) - sizes).contiguous()

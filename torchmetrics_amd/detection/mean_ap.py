@@ -5,17 +5,23 @@ Here the same COCO protocol (IoU thresholds, 101 recall thresholds, max-detectio
 areas, crowd handling, macro / micro averaging, per-class numbers, extended summary) is evaluated on the device by
 :mod:`torchmetrics_amd.detection._coco_eval` (HIP greedy matcher + batched accumulation); no pycocotools needed.
 
-Deliberate difference: ``iou_type="segm"`` states keep the binary masks as tensors (the reference keeps RLE tuples).
+``iou_type="segm"``: masks are run-length encoded on the device in ``update`` (``csrc/detection/rle.hip``; the
+reference encodes on the host with pycocotools, ``S/detection/mean_ap.py:825-829``) and kept as one int32 pack per
+image -- ordinary tensor list states, so the sync engine gathers them (the reference needs ``all_gather_object``,
+``:1007-1038``) -- and mask IoUs come from the runs (``ops.rle_iou``), never from dense ``[n, H, W]`` masks.
 """
 import contextlib
 import io
 import json
 from typing import Any, ClassVar, Dict, List, Optional, Sequence, Tuple, Union
 
+import numpy as np
 import torch
 from torch import Tensor
 from typing_extensions import Literal
 
+from torchmetrics_amd import ops
+from torchmetrics_amd.detection import _rle
 from torchmetrics_amd.detection._coco_eval import coco_evaluate, coco_summarize, per_class_stats
 from torchmetrics_amd.detection.helpers import _fix_empty_tensors, _input_validator, _validate_iou_type_arg, box_convert
 from torchmetrics_amd.metric import Metric
@@ -113,12 +119,15 @@ class MeanAveragePrecision(Metric):
         # image by image, ~4 launches each) and one zero tensor for all missing `iscrowd` / `area` entries
         det_boxes = self._convert_boxes([item["boxes"] for item in preds]) if "bbox" in self.iou_type else None
         gt_boxes = self._convert_boxes([item["boxes"] for item in target]) if "bbox" in self.iou_type else None
+        segm = "segm" in self.iou_type
+        det_rle = _rle.encode([item["masks"] for item in preds]) if segm else None
+        gt_rle = _rle.encode([item["masks"] for item in target]) if segm else None
         limit = self.max_detection_thresholds[-1]
         for i, item in enumerate(preds):
             if det_boxes is not None:
                 self.detection_box.append(det_boxes[i])
-            if "segm" in self.iou_type:
-                self.detection_mask.append(item["masks"].bool())
+            if det_rle is not None:
+                self.detection_mask.append(det_rle[i])
             if self.warn_on_many_detections and len(item["labels"]) > limit:
                 _warning_on_too_many_detections(limit)
             self.detection_labels.append(item["labels"])
@@ -128,8 +137,8 @@ class MeanAveragePrecision(Metric):
         for i, item in enumerate(target):
             if gt_boxes is not None:
                 self.groundtruth_box.append(gt_boxes[i])
-            if "segm" in self.iou_type:
-                self.groundtruth_mask.append(item["masks"].bool())
+            if gt_rle is not None:
+                self.groundtruth_mask.append(gt_rle[i])
             self.groundtruth_labels.append(item["labels"])
             self.groundtruth_crowds.append(item["iscrowd"] if "iscrowd" in item else crowds[i])
             self.groundtruth_area.append(item["area"] if "area" in item else areas[i])
@@ -172,6 +181,12 @@ class MeanAveragePrecision(Metric):
                 return lst[0].device
         return self.device
 
+    def _rle_states(self, dev: torch.device):
+        """``(buffer, descriptors)`` of the detection and ground-truth mask packs (one descriptor row per mask)."""
+        det = _rle.descriptors(self.detection_mask, [x.numel() for x in self.detection_labels], dev)
+        gt = _rle.descriptors(self.groundtruth_mask, [x.numel() for x in self.groundtruth_labels], dev)
+        return det, gt
+
     def _evaluate(self, i_type: str, micro: bool) -> Dict[str, Tensor]:
         dev = self._state_device()
         classes = torch.tensor(self._get_classes(), dtype=torch.long, device=dev)
@@ -179,6 +194,13 @@ class MeanAveragePrecision(Metric):
         n = len(self.detection_labels)
         boxes_ok = i_type == "bbox"
         empty_box = torch.zeros(0, 4, device=dev)
+        det_rle, gt_rle = self._rle_states(dev) if "segm" in self.iou_type else (None, None)
+        gt_areas = self.groundtruth_area
+        if len(self.iou_type) > 1:
+            # with both iou types the reference keeps the ground-truth area of the mask for the bbox evaluation too
+            mask_area = torch.split(gt_rle[1][:, 2], [x.numel() for x in self.groundtruth_labels])
+            gt_areas = [torch.where(a.to(dev) > 0, a.to(dev, torch.float64), m.to(torch.float64))
+                        for a, m in zip(self.groundtruth_area, mask_area)]
         return coco_evaluate(
             det_boxes=[b.reshape(-1, 4) for b in self.detection_box] if boxes_ok else [empty_box] * n,
             det_scores=self.detection_scores,
@@ -186,16 +208,13 @@ class MeanAveragePrecision(Metric):
             gt_boxes=[b.reshape(-1, 4) for b in self.groundtruth_box] if boxes_ok else [empty_box] * n,
             gt_labels=relabel(self.groundtruth_labels),
             gt_crowds=self.groundtruth_crowds,
-            # with both iou types the reference keeps the ground-truth area of the mask for the bbox evaluation too
-            gt_areas=self.groundtruth_area if len(self.iou_type) == 1 else [
-                torch.where(a > 0, a.double(), m.flatten(1).sum(1).double())
-                for a, m in zip(self.groundtruth_area, self.groundtruth_mask)],
+            gt_areas=gt_areas,
             iou_thresholds=self.iou_thresholds,
             rec_thresholds=self.rec_thresholds,
             max_dets=self.max_detection_thresholds,
             classes=classes,
-            det_masks=None if boxes_ok else self.detection_mask,
-            gt_masks=None if boxes_ok else self.groundtruth_mask,
+            det_rle=None if boxes_ok else det_rle,
+            gt_rle=None if boxes_ok else gt_rle,
         )
 
     def compute(self) -> dict:
@@ -204,7 +223,10 @@ class MeanAveragePrecision(Metric):
         for i_type in self.iou_type:
             prefix = "" if len(self.iou_type) == 1 else f"{i_type}_"
             ev = self._evaluate(i_type, micro=self.average == "micro")
-            stats = coco_summarize(ev, self.iou_thresholds, mdt).to(torch.float32).cpu()
+            # pycocotools takes mAP at a hard-coded 100 detections (-1 without that threshold); faster-coco-eval
+            # uses the largest threshold
+            legacy = 100 if self.backend == "pycocotools" else None
+            stats = coco_summarize(ev, self.iou_thresholds, mdt, map_max_det=legacy).to(torch.float32).cpu()
             names = ["map", "map_50", "map_75", "map_small", "map_medium", "map_large", f"mar_{mdt[0]}",
                      f"mar_{mdt[1]}", f"mar_{mdt[2]}", "mar_small", "mar_medium", "mar_large"]
             result.update({f"{prefix}{k}": stats[i] for i, k in enumerate(names)})
@@ -217,7 +239,7 @@ class MeanAveragePrecision(Metric):
                 })
             if self.class_metrics:
                 ev_cls = self._evaluate(i_type, micro=False) if self.average == "micro" else ev
-                mp, mr = per_class_stats(ev_cls)
+                mp, mr = per_class_stats(ev_cls, mdt, map_max_det=legacy)
                 map_pc, mar_pc = mp.to(torch.float32).cpu(), mr.to(torch.float32).cpu()
             else:
                 map_pc = torch.tensor([-1.0], dtype=torch.float32)
@@ -230,6 +252,17 @@ class MeanAveragePrecision(Metric):
         """Per (image, class) IoU matrices: detections in score order (max-dets truncated) x ground truths."""
         out: Dict[Tuple[int, int], Tensor] = {}
         classes = self._get_classes()
+        if i_type == "segm":
+            (dbuf, ddesc), (gbuf, gdesc) = self._rle_states(self._state_device())
+            d_base = [0]
+            for x in self.detection_labels:
+                d_base.append(d_base[-1] + x.numel())
+            g_base = [0]
+            for x in self.groundtruth_labels:
+                g_base.append(g_base[-1] + x.numel())
+            g_crowd = torch.cat([c.reshape(-1) for c in self.groundtruth_crowds]).to(gdesc.device).clamp(0, 1)
+            g_crowd = g_crowd.to(torch.uint8) if g_crowd.numel() else torch.zeros(0, dtype=torch.uint8,
+                                                                                device=gdesc.device)
         for img in range(len(self.detection_labels)):
             for cls in classes:
                 dl, gl = self.detection_labels[img] == cls, self.groundtruth_labels[img] == cls
@@ -243,30 +276,43 @@ class MeanAveragePrecision(Metric):
                     crowd = self.groundtruth_crowds[img][gl].bool()
                     mat = _coco_iou_matrix(d.double(), g.double(), crowd).float().cpu()
                 else:
-                    dm = self.detection_mask[img][dl][order].flatten(1).float()
-                    gm = self.groundtruth_mask[img][gl].flatten(1).float()
-                    inter = dm @ gm.T
-                    crowd = self.groundtruth_crowds[img][gl].bool()
-                    union = torch.where(crowd[None], dm.sum(1)[:, None], dm.sum(1)[:, None] + gm.sum(1)[None] - inter)
-                    mat = (inter / union.clamp(min=1e-12)).float().cpu()
+                    dev = ddesc.device
+                    di = torch.nonzero(dl.to(dev)).flatten()[order.to(dev)] + d_base[img]
+                    gi = torch.nonzero(gl.to(dev)).flatten() + g_base[img]
+                    pd = di.repeat_interleave(gi.numel())
+                    pg = gi.repeat(di.numel())
+                    vals = ops.rle_iou(dbuf, ddesc, gbuf, gdesc, pd.contiguous(), pg.contiguous(), g_crowd)
+                    mat = vals.reshape(di.numel(), gi.numel()).float().cpu()
                 out[(img, cls)] = mat
         return out
 
     # ---------------------------------------------------------------------------------------- COCO interop
     def tm_to_coco(self, name: str = "tm_map_input") -> None:
-        """Write the accumulated boxes as COCO json files ``{name}_preds.json`` / ``{name}_target.json``."""
-        def fmt(labels, boxes, scores=None, crowds=None, areas=None):
+        """Write the accumulated annotations as COCO json files ``{name}_preds.json`` / ``{name}_target.json``
+        (boxes as xywh ``bbox``; masks as compressed-RLE ``segmentation`` built from the stored runs)."""
+        bbox, segm = "bbox" in self.iou_type, "segm" in self.iou_type
+
+        def fmt(labels, boxes, masks, scores=None, crowds=None, areas=None):
             images, anns, aid = [], [], 1
             for img, lab in enumerate(labels):
+                rles = _rle.pack_to_coco(masks[img]) if segm else []
+                if segm and not rles and not bbox:
+                    continue
                 images.append({"id": img})
-                b = boxes[img].reshape(-1, 4).cpu().tolist() if boxes else []
+                if rles:
+                    images[-1]["height"], images[-1]["width"] = rles[0]["size"]
+                b = boxes[img].reshape(-1, 4).cpu().tolist() if bbox else []
                 for k, label in enumerate(lab.cpu().tolist()):
-                    area = float(areas[img][k]) if areas is not None and float(areas[img][k]) > 0 else (
-                        b[k][2] * b[k][3] if b else 0.0)
+                    if areas is not None and float(areas[img][k]) > 0:
+                        area = float(areas[img][k])
+                    else:
+                        area = float(self._rle_area(masks[img], k)) if segm else b[k][2] * b[k][3]
                     ann = {"id": aid, "image_id": img, "area": area, "category_id": int(label),
                            "iscrowd": int(crowds[img][k]) if crowds is not None else 0}
-                    if b:
+                    if bbox:
                         ann["bbox"] = b[k]
+                    if rles:
+                        ann["segmentation"] = rles[k]
                     if scores is not None:
                         ann["score"] = float(scores[img][k])
                     anns.append(ann)
@@ -274,13 +320,17 @@ class MeanAveragePrecision(Metric):
             cats = [{"id": i, "name": str(i)} for i in self._get_classes()]
             return {"images": images, "annotations": anns, "categories": cats}
 
-        target = fmt(self.groundtruth_labels, self.groundtruth_box, crowds=self.groundtruth_crowds,
-                     areas=self.groundtruth_area)
-        preds = fmt(self.detection_labels, self.detection_box, scores=self.detection_scores)
+        target = fmt(self.groundtruth_labels, self.groundtruth_box, self.groundtruth_mask,
+                     crowds=self.groundtruth_crowds, areas=self.groundtruth_area)
+        preds = fmt(self.detection_labels, self.detection_box, self.detection_mask, scores=self.detection_scores)
         with open(f"{name}_preds.json", "w") as f:
             f.write(json.dumps(preds["annotations"], indent=4))
         with open(f"{name}_target.json", "w") as f:
             f.write(json.dumps(target, indent=4))
+
+    @staticmethod
+    def _rle_area(pack: Tensor, k: int) -> int:
+        return int(pack[3 + k].item())
 
     @staticmethod
     def coco_to_tm(
@@ -289,41 +339,78 @@ class MeanAveragePrecision(Metric):
         iou_type: Union[Literal["bbox", "segm"], List[str]] = "bbox",
         backend: Literal["pycocotools", "faster_coco_eval"] = "pycocotools",
     ) -> Tuple[List[Dict[str, Tensor]], List[Dict[str, Tensor]]]:
-        """Read COCO json (target dataset + prediction list) into the ``update`` input format (bbox)."""
+        """Read COCO json (target dataset + prediction list) into the ``update`` input format.
+
+        ``segm`` annotations may be polygons, uncompressed RLE or compressed RLE; masks are rasterised at the image's
+        ``height`` x ``width`` (``images`` entries of the target file) as ``uint8 [n, H, W]``, like the reference's
+        ``annToMask`` (``S/detection/mean_ap.py:694-747``).
+        """
         iou_type = _validate_iou_type_arg(iou_type)
-        if "segm" in iou_type:
-            raise NotImplementedError("coco_to_tm: RLE / polygon decoding of `segm` annotations is not supported")
+        bbox, segm = "bbox" in iou_type, "segm" in iou_type
         with open(coco_target) as f:
             gt = json.load(f)
         with open(coco_preds) as f:
             dt = json.load(f)
-        order = [img["id"] for img in gt.get("images", [])]
-        for ann in gt["annotations"]:
-            if ann["image_id"] not in order:
-                order.append(ann["image_id"])
-        target = {i: {"boxes": [], "labels": [], "iscrowd": [], "area": []} for i in order}
+        # images in order of their first ground-truth annotation (images without ground truth are not evaluated)
+        order = list(dict.fromkeys(ann["image_id"] for ann in gt["annotations"]))
+        sizes = {img["id"]: (img.get("height"), img.get("width")) for img in gt.get("images", [])}
+
+        def mask_of(ann):
+            h, w = sizes.get(ann["image_id"], (None, None))
+            seg = ann["segmentation"]
+            if (h is None or w is None) and isinstance(seg, dict):
+                h, w = seg["size"]
+            if h is None or w is None:
+                raise ValueError(f"coco_to_tm: image {ann['image_id']} has no height / width for its segmentation")
+            return _rle.segmentation_to_mask(seg, int(h), int(w))
+
+        def new_entry(image_id, with_scores):
+            e = {"boxes": [], "labels": [], "masks": []}
+            e.update({"scores": []} if with_scores else {"iscrowd": [], "area": []})
+            return e
+
+        target = {i: new_entry(i, False) for i in order}
         for ann in gt["annotations"]:
             t = target[ann["image_id"]]
-            t["boxes"].append(ann["bbox"])
+            if bbox:
+                t["boxes"].append(ann["bbox"])
+            if segm:
+                t["masks"].append(mask_of(ann))
             t["labels"].append(ann["category_id"])
             t["iscrowd"].append(ann.get("iscrowd", 0))
             t["area"].append(ann.get("area", 0.0))
-        preds = {i: {"boxes": [], "labels": [], "scores": []} for i in order}
+        preds = {i: new_entry(i, True) for i in order}
         for ann in dt:
-            p = preds.setdefault(ann["image_id"], {"boxes": [], "labels": [], "scores": []})
-            p["boxes"].append(ann["bbox"])
+            p = preds.setdefault(ann["image_id"], new_entry(ann["image_id"], True))
+            if bbox:
+                p["boxes"].append(ann["bbox"])
+            if segm:
+                p["masks"].append(mask_of(ann))
             p["labels"].append(ann["category_id"])
             p["scores"].append(ann["score"])
+
+        def masks_tensor(lst, image_id):
+            if lst:
+                return torch.from_numpy(np.stack(lst)).to(torch.uint8)
+            h, w = sizes.get(image_id, (0, 0))
+            return torch.zeros(0, int(h or 0), int(w or 0), dtype=torch.uint8)
+
         bp, bt = [], []
         for key in order:
             p, t = preds[key], target[key]
-            bp.append({"boxes": torch.tensor(p["boxes"], dtype=torch.float32).reshape(-1, 4),
-                       "scores": torch.tensor(p["scores"], dtype=torch.float32),
-                       "labels": torch.tensor(p["labels"], dtype=torch.int32)})
-            bt.append({"boxes": torch.tensor(t["boxes"], dtype=torch.float32).reshape(-1, 4),
-                       "labels": torch.tensor(t["labels"], dtype=torch.int32),
-                       "iscrowd": torch.tensor(t["iscrowd"], dtype=torch.int32),
-                       "area": torch.tensor(t["area"], dtype=torch.float32)})
+            ep = {"scores": torch.tensor(p["scores"], dtype=torch.float32),
+                  "labels": torch.tensor(p["labels"], dtype=torch.int32)}
+            et = {"labels": torch.tensor(t["labels"], dtype=torch.int32),
+                  "iscrowd": torch.tensor(t["iscrowd"], dtype=torch.int32),
+                  "area": torch.tensor(t["area"], dtype=torch.float32)}
+            if bbox:
+                ep["boxes"] = torch.tensor(p["boxes"], dtype=torch.float32).reshape(-1, 4)
+                et["boxes"] = torch.tensor(t["boxes"], dtype=torch.float32).reshape(-1, 4)
+            if segm:
+                ep["masks"] = masks_tensor(p["masks"], key)
+                et["masks"] = masks_tensor(t["masks"], key)
+            bp.append(ep)
+            bt.append(et)
         return bp, bt
 
 

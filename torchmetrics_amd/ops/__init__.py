@@ -14,7 +14,7 @@ import os
 import struct
 import threading
 from pathlib import Path
-from typing import Optional, Sequence, Union
+from typing import List, Optional, Sequence, Union
 
 import torch
 from torch import Tensor
@@ -790,6 +790,26 @@ def coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, g
                                  iou_thr, iou_pre, iou_off)
     return _cpu.coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, gt_cnt, area_rng, iou_thr,
                            iou_pre, iou_off)
+
+
+def rle_encode(masks: List[Tensor]) -> List[Tensor]:
+    """Run-length encode every ``[n_i, H_i, W_i]`` mask tensor into one int32 pack per image
+    (``[n, H, W, areas(n), offsets(n+1), change positions...]``, ``csrc/detection/rle.hip``): ROCm kernels (one host
+    sync per call, to size the packs) or the native host loop; a torch fallback without the library."""
+    if not masks:
+        return []
+    if masks[0].is_cuda or load_native(strict=False):
+        return list(_ops().rle_encode(list(masks)))
+    return _cpu.rle_encode(masks)
+
+
+def rle_iou(dbuf: Tensor, ddesc: Tensor, gbuf: Tensor, gdesc: Tensor, pd: Tensor, pg: Tensor, gcrowd: Tensor) -> Tensor:
+    """fp64 mask IoU of every (detection ``pd[p]``, ground truth ``pg[p]``) pair from their RLE descriptors
+    (``[N, 5]``: position start, change count, area, H, W); crowd ground truths divide by the detection area,
+    mismatched sizes give -1 (pycocotools ``rleIou``)."""
+    if pd.is_cuda or load_native(strict=False):
+        return _ops().rle_iou(dbuf, ddesc, gbuf, gdesc, pd, pg, gcrowd)
+    return _cpu.rle_iou(dbuf, ddesc, gbuf, gdesc, pd, pg, gcrowd)
 
 
 # ------------------------------------------------------------------------------------------ distance transforms

@@ -707,3 +707,49 @@ def mc_bootstrap_update(preds: Tensor, target: Tensor, weights: Tensor, ws: Tens
     flat.index_add_(0, (base + C + pp).reshape(-1), (w * ~hit).reshape(-1))
     flat.index_add_(0, (base + 2 * C + tt).reshape(-1), (w * ~hit).reshape(-1))
     flat.index_add_(0, (base[:, 0] + 3 * C), w.sum(1))
+
+
+# ------------------------------------------------------------------------------------------------------ RLE masks
+def rle_encode(masks):
+    """Host contract of ``tm_amd::rle_encode``: per image ``[n, H, W, areas, offsets(n+1), change positions]``.
+    Change positions are the column-major indices where a mask flips value (starting from background)."""
+    packs = []
+    for m in masks:
+        n, h, w = m.shape
+        cm = m.detach().cpu().ne(0).transpose(1, 2).reshape(n, h * w).to(torch.int8)
+        prev = torch.cat([torch.zeros(n, 1, dtype=torch.int8), cm[:, :-1]], 1)
+        mi, pos = torch.nonzero(cm != prev, as_tuple=True)
+        counts = torch.bincount(mi, minlength=n)
+        off = torch.cat([torch.zeros(1, dtype=torch.long), torch.cumsum(counts, 0)])
+        head = torch.tensor([n, h, w], dtype=torch.long)
+        packs.append(torch.cat([head, cm.sum(1, dtype=torch.long), off, pos]).to(torch.int32).to(m.device))
+    return packs
+
+
+def rle_iou(dbuf, ddesc, gbuf, gdesc, pd, pg, gcrowd):
+    out = torch.empty(pd.numel(), dtype=torch.float64)
+    db, gb, dd, gd = dbuf.cpu().tolist(), gbuf.cpu().tolist(), ddesc.cpu().tolist(), gdesc.cpu().tolist()
+    crowd = gcrowd.cpu().tolist()
+
+    def intervals(buf, row):
+        s, k, hw = row[0], row[1], row[3] * row[4]
+        pts = buf[s:s + k] + ([hw] if k % 2 else [])
+        return list(zip(pts[0::2], pts[1::2]))
+
+    for p, (d, g) in enumerate(zip(pd.cpu().tolist(), pg.cpu().tolist())):
+        a, b = dd[d], gd[g]
+        if a[3] != b[3] or a[4] != b[4]:
+            out[p] = -1.0
+            continue
+        ia, ib = intervals(db, a), intervals(gb, b)
+        i = j = inter = 0
+        while i < len(ia) and j < len(ib):
+            lo, hi = max(ia[i][0], ib[j][0]), min(ia[i][1], ib[j][1])
+            inter += max(0, hi - lo)
+            if ia[i][1] < ib[j][1]:
+                i += 1
+            else:
+                j += 1
+        union = a[2] if crowd[g] else a[2] + b[2] - inter
+        out[p] = inter / union if inter else 0.0
+    return out.to(pd.device)

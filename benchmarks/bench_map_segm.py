@@ -60,15 +60,19 @@ def main():
             print(f"[segm] {start + nb} images", flush=True)
     state = sum(p.numel() * p.element_size() for p in m.detection_mask + m.groundtruth_mask)
     dense = args.images * (args.masks + args.gts) * args.h * args.w
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    res = m.compute()
-    torch.cuda.synchronize()
-    comp = time.perf_counter() - t0
+    times = []
+    for _ in range(3):  # first call includes lazy kernel loading; report cold and warm
+        m._computed = None
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = m.compute()
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    comp = min(times[1:])
     print(json.dumps({"bench": "map_segm", "images": args.images, "masks_per_image": args.masks,
                       "gts_per_image": args.gts, "hw": [args.h, args.w], "state_mb": state / 2**20,
                       "dense_mask_mb": dense / 2**20, "update_ms_per_image": 1e3 * upd / args.images,
-                      "compute_ms": 1e3 * comp, "map": float(res["map"]), "map_50": float(res["map_50"])}))
+                      "compute_ms": 1e3 * comp, "compute_cold_ms": 1e3 * times[0], "map": float(res["map"]), "map_50": float(res["map_50"])}))
 
 
 if __name__ == "__main__":

@@ -11,10 +11,11 @@
 // list state):
 //     [n, H, W, area_0 .. area_{n-1}, off_0 .. off_n, positions...]      off: start of mask l's positions
 //
-// rle_encode   two kernels over all masks of an update call (one block per mask): (1) per-thread change counts and
-//              the mask area; one D2H copy of the per-mask totals sizes the packs; (2) a block scan of the per-thread
-//              counts and an ordered write of the positions.  Threads own contiguous column strips, so at a fixed row
-//              the lanes of a wave read bytes `c` apart (c = ceil(W / 256)) -- a few cache lines per wave load.
+// rle_encode   two kernels over all masks of an update call (one block per mask): (1) per-column change counts and
+//              the mask area; one D2H copy of the per-mask totals sizes the packs; (2) a block scan of the column
+//              counts (tiles of 1024 columns with a carry) and an ordered write of the positions.  A thread owns 4
+//              adjacent columns and walks them row by row with one 4-byte load per row, so a wave reads 256
+//              contiguous bytes per row (byte loads when rows are not 4-byte aligned).
 // rle_iou      one thread per (detection, ground truth) pair: two-pointer merge of the foreground intervals; crowd
 //              ground truths divide by the detection area; size mismatch -> -1 (pycocotools rleIou semantics).
 // The CPU dispatch key runs the same algorithms on host threads.
@@ -28,6 +29,7 @@ namespace tm_amd {
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kRows = 8;  // rows loaded per batch in the encode kernels
 
 // foreground interval i of a mask with k change positions: [pos[2i], pos[2i+1]) (open end -> hw)
 __host__ __device__ inline long long rle_intersection(const int* a, int ka, const int* b, int kb, long long hw) {
@@ -71,29 +73,60 @@ __device__ inline int block_exclusive_scan(int v, int* lds_wave) {
   return base + inc - v;
 }
 
-// table row: ptr, H, W
-__global__ void __launch_bounds__(kThreads) rle_count_kernel(const int64_t* __restrict__ table, int* __restrict__ tcnt,
-                                                              int* __restrict__ stats) {
+// Column strips: a thread owns VW consecutive columns of a tile of kThreads * VW columns and walks them row by row,
+// one VW-byte load per row (VW = 4 when rows are 4-byte aligned: a wave reads 256 contiguous bytes per row; else 1).
+// Column x's value sequence in COCO order is rows 0..H-1 of column x, preceded by pixel (x-1, H-1).
+template <int VW>
+struct Strip {
+  static __device__ __forceinline__ uint32_t load(const uint8_t* p) {
+    if constexpr (VW == 4) return *reinterpret_cast<const uint32_t*>(p);
+    else return *p;
+  }
+  static __device__ __forceinline__ int bit(uint32_t word, int j) { return ((word >> (8 * j)) & 0xffu) != 0; }
+};
+
+// table row: ptr, H, W, colcnt offset.  colcnt [N, W]: changes per column; stats [N, 2]: total changes, area.
+template <int VW>
+__global__ void __launch_bounds__(kThreads) rle_count_kernel(const int64_t* __restrict__ table,
+                                                              int* __restrict__ colcnt, int* __restrict__ stats) {
   const int mid = blockIdx.x, tid = threadIdx.x;
-  const uint8_t* m = reinterpret_cast<const uint8_t*>(table[mid * 3]);
-  const int H = static_cast<int>(table[mid * 3 + 1]), W = static_cast<int>(table[mid * 3 + 2]);
-  const int c = (W + kThreads - 1) / kThreads;
-  const int x0 = tid * c, x1 = min(W, x0 + c);
-  int chg = 0, ones = 0;
-  if (x0 < x1 && H > 0) {
-    int prev = x0 == 0 ? 0 : (m[static_cast<long long>(H - 1) * W + x0 - 1] != 0);
-    for (int x = x0; x < x1; ++x) {
-      for (int y = 0; y < H; ++y) {
-        const int v = m[static_cast<long long>(y) * W + x] != 0;
-        chg += v != prev;
-        ones += v;
-        prev = v;
+  const uint8_t* m = reinterpret_cast<const uint8_t*>(table[mid * 4]);
+  const int H = static_cast<int>(table[mid * 4 + 1]), W = static_cast<int>(table[mid * 4 + 2]);
+  int* cc = colcnt + static_cast<long long>(table[mid * 4 + 3]);
+  int chg_all = 0, ones = 0;
+  for (int x0 = tid * VW; x0 < W && H > 0; x0 += kThreads * VW) {
+    int prev[VW], chg[VW];
+    const uint32_t last = Strip<VW>::load(m + static_cast<long long>(H - 1) * W + x0);
+    prev[0] = x0 == 0 ? 0 : (m[static_cast<long long>(H - 1) * W + x0 - 1] != 0);
+#pragma unroll
+    for (int j = 1; j < VW; ++j) prev[j] = Strip<VW>::bit(last, j - 1);
+#pragma unroll
+    for (int j = 0; j < VW; ++j) chg[j] = 0;
+    for (int y0 = 0; y0 < H; y0 += kRows) {  // kRows independent loads in flight per lane
+      uint32_t w[kRows];
+#pragma unroll
+      for (int r = 0; r < kRows; ++r)
+        w[r] = y0 + r < H ? Strip<VW>::load(m + static_cast<long long>(y0 + r) * W + x0) : 0u;
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) {
+        if (y0 + r >= H) break;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+          const int v = Strip<VW>::bit(w[r], j);
+          chg[j] += v != prev[j];
+          ones += v;
+          prev[j] = v;
+        }
       }
     }
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      cc[x0 + j] = chg[j];
+      chg_all += chg[j];
+    }
   }
-  tcnt[static_cast<long long>(mid) * kThreads + tid] = chg;
   __shared__ int red[2][kThreads / kWave];
-  const int wc = wave_sum(chg), wo = wave_sum(ones);
+  const int wc = wave_sum(chg_all), wo = wave_sum(ones);
   if ((tid & (kWave - 1)) == 0) {
     red[0][tid / kWave] = wc;
     red[1][tid / kWave] = wo;
@@ -106,38 +139,75 @@ __global__ void __launch_bounds__(kThreads) rle_count_kernel(const int64_t* __re
   }
 }
 
-// table row: ptr, H, W, pack_base, l, n, off_rel, nchg, area
+// table row: ptr, H, W, colcnt offset, pack_base, l, n, off_rel, nchg, area
+template <int VW>
 __global__ void __launch_bounds__(kThreads) rle_write_kernel(const int64_t* __restrict__ table,
-                                                              const int* __restrict__ tcnt, int* __restrict__ out) {
+                                                              const int* __restrict__ colcnt, int* __restrict__ out) {
   const int mid = blockIdx.x, tid = threadIdx.x;
-  const int64_t* row = table + mid * 9;
+  const int64_t* row = table + mid * 10;
   const uint8_t* m = reinterpret_cast<const uint8_t*>(row[0]);
   const int H = static_cast<int>(row[1]), W = static_cast<int>(row[2]);
-  const long long n = row[5], l = row[4], off_rel = row[6];
-  int* pack = out + row[3];
+  const int* cc = colcnt + row[3];
+  const long long n = row[6], l = row[5], off_rel = row[7];
+  int* pack = out + row[4];
   if (tid == 0) {
     if (l == 0) {
       pack[0] = static_cast<int>(n);
       pack[1] = H;
       pack[2] = W;
     }
-    pack[3 + l] = static_cast<int>(row[8]);
+    pack[3 + l] = static_cast<int>(row[9]);
     pack[3 + n + l] = static_cast<int>(off_rel);
-    if (l == n - 1) pack[3 + 2 * n] = static_cast<int>(off_rel + row[7]);
+    if (l == n - 1) pack[3 + 2 * n] = static_cast<int>(off_rel + row[8]);
   }
-  __shared__ int wsum[kThreads / kWave];
-  int k = block_exclusive_scan(tcnt[static_cast<long long>(mid) * kThreads + tid], wsum);
   int* pos = pack + 3 + 2 * n + 1 + off_rel;
-  const int c = (W + kThreads - 1) / kThreads;
-  const int x0 = tid * c, x1 = min(W, x0 + c);
-  if (x0 >= x1 || H <= 0) return;
-  int prev = x0 == 0 ? 0 : (m[static_cast<long long>(H - 1) * W + x0 - 1] != 0);
-  for (int x = x0; x < x1; ++x) {
-    for (int y = 0; y < H; ++y) {
-      const int v = m[static_cast<long long>(y) * W + x] != 0;
-      if (v != prev) pos[k++] = x * H + y;
-      prev = v;
+  __shared__ int wsum[kThreads / kWave];
+  __shared__ int carry_s;
+  int carry = 0;
+  for (int t0 = 0; t0 < W; t0 += kThreads * VW) {  // tiles of columns; uniform trip count across the block
+    const int x0 = t0 + tid * VW;
+    int cnt[VW];
+    int mine = 0;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      cnt[j] = x0 + j < W ? cc[x0 + j] : 0;
+      mine += cnt[j];
     }
+    const int excl = block_exclusive_scan(mine, wsum);
+    if (tid == kThreads - 1) carry_s = excl + mine;
+    __syncthreads();
+    const int tile_total = carry_s;
+    if (x0 < W && H > 0) {
+      int k[VW], prev[VW];
+      int acc = carry + excl;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        k[j] = acc;
+        acc += cnt[j];
+      }
+      const uint32_t last = Strip<VW>::load(m + static_cast<long long>(H - 1) * W + x0);
+      prev[0] = x0 == 0 ? 0 : (m[static_cast<long long>(H - 1) * W + x0 - 1] != 0);
+#pragma unroll
+      for (int j = 1; j < VW; ++j) prev[j] = Strip<VW>::bit(last, j - 1);
+      for (int y0 = 0; y0 < H; y0 += kRows) {
+        uint32_t w[kRows];
+#pragma unroll
+        for (int r = 0; r < kRows; ++r)
+          w[r] = y0 + r < H ? Strip<VW>::load(m + static_cast<long long>(y0 + r) * W + x0) : 0u;
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+          if (y0 + r >= H) break;
+#pragma unroll
+          for (int j = 0; j < VW; ++j) {
+            const int v = Strip<VW>::bit(w[r], j);
+            if (v != prev[j]) pos[k[j]++] = (x0 + j) * H + y0 + r;
+            prev[j] = v;
+          }
+        }
+      }
+    }
+    carry += tile_total;
+    __syncthreads();  // wsum / carry_s reuse by the next tile
   }
 }
 
@@ -217,18 +287,32 @@ std::vector<at::Tensor> rle_encode_cuda(at::TensorList masks) {
   at::Tensor buf;
   if (N > 0) {
     TORCH_CHECK(N < (1LL << 31), "rle_encode: too many masks");
-    at::Tensor t1 = at::empty({N, 3}, i64);
+    // 4-byte column groups when every mask row is 4-byte aligned (W % 4 == 0 and 4-aligned mask starts)
+    bool vec4 = true;
+    std::vector<int64_t> col_off(N);
+    int64_t cols = 0;
+    for (int64_t r = 0; r < N; ++r) {
+      vec4 = vec4 && refs[r].w % 4 == 0 && reinterpret_cast<uintptr_t>(refs[r].ptr) % 4 == 0;
+      col_off[r] = cols;
+      cols += refs[r].w + 4;  // + padding: a 4-wide group may straddle W only when W % 4 != 0 (byte path then)
+    }
+    at::Tensor t1 = at::empty({N, 4}, i64);
     int64_t* t1p = t1.data_ptr<int64_t>();
     for (int64_t r = 0; r < N; ++r) {
-      t1p[r * 3] = reinterpret_cast<int64_t>(refs[r].ptr);
-      t1p[r * 3 + 1] = refs[r].h;
-      t1p[r * 3 + 2] = refs[r].w;
+      t1p[r * 4] = reinterpret_cast<int64_t>(refs[r].ptr);
+      t1p[r * 4 + 1] = refs[r].h;
+      t1p[r * 4 + 2] = refs[r].w;
+      t1p[r * 4 + 3] = col_off[r];
     }
     at::Tensor t1d = t1.to(masks[0].device());
-    at::Tensor tcnt = at::empty({N, kThreads}, dev_i32);
+    at::Tensor colcnt = at::empty({cols}, dev_i32);
     at::Tensor stats = at::empty({N, 2}, dev_i32);
-    hipLaunchKernelGGL(rle_count_kernel, dim3(static_cast<unsigned>(N)), dim3(kThreads), 0, stream(),
-                       t1d.data_ptr<int64_t>(), tcnt.data_ptr<int>(), stats.data_ptr<int>());
+    if (vec4)
+      hipLaunchKernelGGL(rle_count_kernel<4>, dim3(static_cast<unsigned>(N)), dim3(kThreads), 0, stream(),
+                         t1d.data_ptr<int64_t>(), colcnt.data_ptr<int>(), stats.data_ptr<int>());
+    else
+      hipLaunchKernelGGL(rle_count_kernel<1>, dim3(static_cast<unsigned>(N)), dim3(kThreads), 0, stream(),
+                         t1d.data_ptr<int64_t>(), colcnt.data_ptr<int>(), stats.data_ptr<int>());
     C10_HIP_KERNEL_LAUNCH_CHECK();
     at::Tensor st = stats.cpu();  // the one host sync of an update: sizes the packs
     const int* sp = st.data_ptr<int>();
@@ -236,17 +320,21 @@ std::vector<at::Tensor> rle_encode_cuda(at::TensorList masks) {
     for (int64_t r = 0; r < N; ++r) nchg[r] = sp[r * 2];
     const int64_t total = pack_layout(masks, refs, nchg.data(), base, off_rel);
     buf = at::empty({total}, dev_i32);
-    at::Tensor t2 = at::empty({N, 9}, i64);
+    at::Tensor t2 = at::empty({N, 10}, i64);
     int64_t* t2p = t2.data_ptr<int64_t>();
     for (int64_t r = 0; r < N; ++r) {
       const MaskRef& f = refs[r];
-      const int64_t row[9] = {reinterpret_cast<int64_t>(f.ptr), f.h, f.w, base[f.image], f.local, f.n,
-                              off_rel[r], nchg[r], sp[r * 2 + 1]};
-      for (int c = 0; c < 9; ++c) t2p[r * 9 + c] = row[c];
+      const int64_t row[10] = {reinterpret_cast<int64_t>(f.ptr), f.h, f.w, col_off[r], base[f.image], f.local, f.n,
+                               off_rel[r], nchg[r], sp[r * 2 + 1]};
+      for (int c = 0; c < 10; ++c) t2p[r * 10 + c] = row[c];
     }
     at::Tensor t2d = t2.to(masks[0].device());
-    hipLaunchKernelGGL(rle_write_kernel, dim3(static_cast<unsigned>(N)), dim3(kThreads), 0, stream(),
-                       t2d.data_ptr<int64_t>(), tcnt.data_ptr<int>(), buf.data_ptr<int>());
+    if (vec4)
+      hipLaunchKernelGGL(rle_write_kernel<4>, dim3(static_cast<unsigned>(N)), dim3(kThreads), 0, stream(),
+                         t2d.data_ptr<int64_t>(), colcnt.data_ptr<int>(), buf.data_ptr<int>());
+    else
+      hipLaunchKernelGGL(rle_write_kernel<1>, dim3(static_cast<unsigned>(N)), dim3(kThreads), 0, stream(),
+                         t2d.data_ptr<int64_t>(), colcnt.data_ptr<int>(), buf.data_ptr<int>());
     C10_HIP_KERNEL_LAUNCH_CHECK();
   } else {
     pack_layout(masks, refs, nullptr, base, off_rel);

@@ -52,10 +52,15 @@ def _edge_masks(h, w):
 
 
 @pytest.mark.parametrize("device", DEVICES)
-def test_encode_matches_contract_and_decodes(device):
+@pytest.mark.parametrize("aligned", [False, True])
+def test_encode_matches_contract_and_decodes(device, aligned):
     g = torch.Generator().manual_seed(0)
-    masks = [_blobs(g, n, h, w, noise=0.02 if h > 1 else 0.3) for n, h, w in SHAPES]
-    masks += [_edge_masks(9, 300), torch.zeros(2, 5, 6, dtype=torch.uint8)]
+    if aligned:  # every row 4-byte aligned: the 4-column kernels; W > 1024 exercises the tile carry
+        masks = [_blobs(g, n, h, w, noise=0.02) for n, h, w in [(3, 40, 300), (2, 17, 516), (2, 9, 1028), (1, 1, 4)]]
+        masks += [_edge_masks(9, 300), (torch.rand(2, 6, 8, generator=g) < 0.5).to(torch.uint8) * 255]
+    else:
+        masks = [_blobs(g, n, h, w, noise=0.02 if h > 1 else 0.3) for n, h, w in SHAPES]
+        masks += [_edge_masks(9, 300), torch.zeros(2, 5, 6, dtype=torch.uint8)]
     dev_masks = [m.to(device) for m in masks]
     packs = ops.rle_encode(dev_masks)
     want = ops._cpu.rle_encode(masks)
@@ -65,7 +70,7 @@ def test_encode_matches_contract_and_decodes(device):
         assert torch.equal(p.cpu(), wnt), (m.shape, p[:12], wnt[:12])
         assert torch.equal(_rle.decode(p).cpu(), m.bool())
         n = m.shape[0]
-        assert torch.equal(p[3:3 + n].cpu().long(), m.flatten(1).sum(1))
+        assert torch.equal(p[3:3 + n].cpu().long(), m.flatten(1).ne(0).sum(1))
 
 
 def test_contract_matches_coco_counts_convention():

@@ -70,6 +70,11 @@ def reference(real, fake):
     v = a + b - 2 * c
     _sync()
     t2 = time.perf_counter()
+    # the previous compute path of this package (Cholesky + symmetric eigensolve) on the same covariances
+    lower = torch.linalg.cholesky(cr)
+    mm = lower.T @ cf @ lower
+    c_eigh = torch.linalg.eigvalsh(0.5 * (mm + mm.T)).clamp(min=0).sqrt().sum()
+    reference.eigh_fid = (a + b - 2 * c_eigh).item()
     return v.item(), t1 - t0, t2 - t1
 
 
@@ -91,6 +96,8 @@ def main():
         "end_to_end_speedup": round((up_r + cp_r) / (up_o + cp_o), 3),
         "compute_speedup": round(cp_r / cp_o, 3),
         "rel_diff": abs(v_o - v_r) / max(abs(v_r), 1e-12),
+        "eigh_path_fid": reference.eigh_fid,
+        "rel_diff_vs_eigh": abs(v_o - reference.eigh_fid) / max(abs(reference.eigh_fid), 1e-12),
     }
     print(json.dumps(out))
 

@@ -47,6 +47,30 @@ def test_fid_matches_scipy(device, d):
     assert_close(m.compute(), _np_fid(real, fake), atol=1e-3, rtol=1e-4)
 
 
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("case", ["random", "decay1e4", "decay1e10", "rank_deficient"])
+def test_trace_sqrt_newton_schulz_matches_eigensolve(device, case):
+    """The GEMM-only Newton-Schulz ``tr sqrt(Σ1 Σ2)`` (ROCm compute path) vs an fp64 eigensolve, including
+    ill-conditioned and singular covariances (the unscaled tail must keep iterating until the trace settles)."""
+    from torchmetrics_amd.image.generative import _trace_sqrt_newton_schulz, _trace_sqrt_product
+
+    g = torch.Generator().manual_seed(1)
+    d = 160
+    n = 100 if case == "rank_deficient" else 2000
+    decay = {"random": 0.0, "decay1e4": 4.0, "decay1e10": 10.0, "rank_deficient": 0.0}[case]
+    sc = torch.logspace(0, -decay / 2, d, dtype=torch.float64)
+    f1 = torch.randn(n, d, dtype=torch.float64, generator=g) * sc
+    f2 = (torch.randn(n, d, dtype=torch.float64, generator=g) * 1.1 + 0.05) * sc
+    s1, s2 = torch.cov(f1.T), torch.cov(f2.T)
+    exact = torch.linalg.eigvals(s1 @ s2).real.clamp(min=0).sqrt().sum()
+    got = _trace_sqrt_newton_schulz(s1.to(device), s2.to(device))
+    if got is None:  # eigenvalues below the 1e-6 floor: the iteration declines and FID takes the eigensolve
+        assert case in ("rank_deficient", "decay1e10")
+        got = _trace_sqrt_product(s1.to(device), s2.to(device))
+    # near-singular products limit the accuracy of the eigvals oracle itself to ~1e-8
+    assert abs(float((got.cpu() - exact) / exact)) < (1e-7 if case in ("rank_deficient", "decay1e10") else 1e-9)
+
+
 def test_fid_reset_real_features():
     m = FrechetInceptionDistance(feature=_Id(8), reset_real_features=False)
     m.update(torch.randn(10, 8), real=True)

@@ -58,6 +58,7 @@ struct DestSpec {
 // with the increment rounded to that dtype first, exactly like the host formulation.
 constexpr int kFoldNone = 0;
 constexpr int kFoldPearson = 1;
+constexpr int kColParMin = 256;  // above this many outputs: moments_colpar_kernel
 
 __device__ __forceinline__ double ld_state(const DestSpec& spec, int j, int c) {
   return spec.fdtype[j] == 0 ? static_cast<double>(reinterpret_cast<const float*>(spec.fptr[j])[c])
@@ -75,6 +76,39 @@ __device__ __forceinline__ void add_state(const DestSpec& spec, int j, int c, do
 
 __device__ void finalize_column(const double* __restrict__ partial, int nblocks, int k, int c,
                                 const DestSpec& spec, double* __restrict__ out_sums, int mask);
+
+template <typename scalar_t>
+__device__ __forceinline__ void accumulate_pair(double* acc, scalar_t pv, scalar_t tv, float sp, float st, int mask,
+                                                double eps, double pw) {
+  const float p = to_f32(pv);
+  const float t = to_f32(tv);
+  const float d = p - t;
+  const float ad = fabsf(d);
+  if (mask & (1 << kSSE)) acc[kSSE] += static_cast<double>(d) * d;
+  if (mask & (1 << kSAE)) acc[kSAE] += ad;
+  if (mask & ((1 << kSP) | (1 << kSPP) | (1 << kSPT) | (1 << kST) | (1 << kSTT))) {
+    const double pc = static_cast<double>(p) - sp, tc = static_cast<double>(t) - st;
+    acc[kSP] += pc;
+    acc[kST] += tc;
+    acc[kSPP] += pc * pc;
+    acc[kSTT] += tc * tc;
+    acc[kSPT] += pc * tc;
+  }
+  if (mask & (1 << kMAPE)) acc[kMAPE] += ad / fmax(static_cast<double>(fabsf(t)), eps);
+  if (mask & (1 << kSMAPE)) acc[kSMAPE] += 2.0 * ad / fmax(static_cast<double>(fabsf(p) + fabsf(t)), eps);
+  if (mask & (1 << kSABST)) acc[kSABST] += fabsf(t);
+  if (mask & (1 << kMSLE)) {
+    const double l = log1p(static_cast<double>(p)) - log1p(static_cast<double>(t));
+    acc[kMSLE] += l * l;
+  }
+  if (mask & (1 << kLOGCOSH)) {
+    // log(cosh(x)) = |x| + log1p(exp(-2|x|)) - log(2)  (overflow-free)
+    const double x = fabs(static_cast<double>(d));
+    acc[kLOGCOSH] += x + log1p(exp(-2.0 * x)) - 0.69314718055994530942;
+  }
+  if (mask & (1 << kMINK)) acc[kMINK] += pow(static_cast<double>(ad), pw);
+  acc[kCOUNT] += 1.0;
+}
 
 template <typename scalar_t>
 __global__ void __launch_bounds__(kBlock) moments_partial_kernel(const scalar_t* __restrict__ preds,
@@ -96,34 +130,7 @@ __global__ void __launch_bounds__(kBlock) moments_partial_kernel(const scalar_t*
   const float st = shift_t ? shift_t[col] : 0.f;
   // stride is a multiple of k -> the column of this thread never changes
   for (long long i = tid; i < total; i += nthreads) {
-    const float p = to_f32(preds[i]);
-    const float t = to_f32(target[i]);
-    const float d = p - t;
-    const float ad = fabsf(d);
-    if (mask & (1 << kSSE)) acc[kSSE] += static_cast<double>(d) * d;
-    if (mask & (1 << kSAE)) acc[kSAE] += ad;
-    if (mask & ((1 << kSP) | (1 << kSPP) | (1 << kSPT) | (1 << kST) | (1 << kSTT))) {
-      const double pc = static_cast<double>(p) - sp, tc = static_cast<double>(t) - st;
-      acc[kSP] += pc;
-      acc[kST] += tc;
-      acc[kSPP] += pc * pc;
-      acc[kSTT] += tc * tc;
-      acc[kSPT] += pc * tc;
-    }
-    if (mask & (1 << kMAPE)) acc[kMAPE] += ad / fmax(static_cast<double>(fabsf(t)), eps);
-    if (mask & (1 << kSMAPE)) acc[kSMAPE] += 2.0 * ad / fmax(static_cast<double>(fabsf(p) + fabsf(t)), eps);
-    if (mask & (1 << kSABST)) acc[kSABST] += fabsf(t);
-    if (mask & (1 << kMSLE)) {
-      const double l = log1p(static_cast<double>(p)) - log1p(static_cast<double>(t));
-      acc[kMSLE] += l * l;
-    }
-    if (mask & (1 << kLOGCOSH)) {
-      // log(cosh(x)) = |x| + log1p(exp(-2|x|)) - log(2)  (overflow-free)
-      const double x = fabs(static_cast<double>(d));
-      acc[kLOGCOSH] += x + log1p(exp(-2.0 * x)) - 0.69314718055994530942;
-    }
-    if (mask & (1 << kMINK)) acc[kMINK] += pow(static_cast<double>(ad), pw);
-    acc[kCOUNT] += 1.0;
+    accumulate_pair(acc, preds[i], target[i], sp, st, mask, eps, pw);
   }
   if ((kWave % k) == 0) {
     // k divides the wave: lanes l and l ^ off (off >= k) share a column -> xor-shuffle tree inside the wave, then a
@@ -235,6 +242,35 @@ __device__ void finalize_column(const double* __restrict__ partial, int nblocks,
 }
 
 // one block per column
+// Many outputs (k > kColParMin): one thread per column walks a chunk of rows (reads of a row are coalesced across
+// the block's consecutive columns); grid.y splits the rows so k * chunks threads fill the GPU.  Partials use the same
+// [chunk][column][sum] layout as moments_partial_kernel, so moments_finalize_kernel folds both.
+template <typename scalar_t>
+__global__ void __launch_bounds__(kBlock) moments_colpar_kernel(const scalar_t* __restrict__ preds,
+                                                                const scalar_t* __restrict__ target,
+                                                                long long n_rows, int k, long long rows_per_chunk,
+                                                                int mask, double eps, double pw,
+                                                                const float* __restrict__ shift_p,
+                                                                const float* __restrict__ shift_t,
+                                                                double* __restrict__ partial) {
+  const long long col = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (col >= k) return;
+  double acc[kMaxSums];
+#pragma unroll
+  for (int s = 0; s < kMaxSums; ++s) acc[s] = 0.0;
+  const float sp = shift_p ? shift_p[col] : 0.f;
+  const float st = shift_t ? shift_t[col] : 0.f;
+  const long long r0 = static_cast<long long>(blockIdx.y) * rows_per_chunk;
+  const long long r1 = r0 + rows_per_chunk < n_rows ? r0 + rows_per_chunk : n_rows;
+  for (long long r = r0; r < r1; ++r) {
+    const long long i = r * k + col;
+    accumulate_pair(acc, preds[i], target[i], sp, st, mask, eps, pw);
+  }
+  double* dst = partial + (static_cast<long long>(blockIdx.y) * k + col) * kMaxSums;
+#pragma unroll
+  for (int s = 0; s < kMaxSums; ++s) dst[s] = acc[s];
+}
+
 __global__ void __launch_bounds__(kBlock) moments_finalize_kernel(const double* __restrict__ partial, int nblocks,
                                                                   int k, DestSpec spec, double* __restrict__ out_sums,
                                                                   int mask) {
@@ -313,10 +349,7 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
       default: TORCH_CHECK(false, "moments_update: destination dtype must be f32/f64/i64");
     }
   }
-  // small updates (the common per-batch case): one block does the pass AND the fold -> a single launch
-  const bool fuse = n_rows * k <= 4096 && kBlock % k == 0;
-  if (fuse) blocks = 1;
-  at::Tensor partial = at::empty({blocks, k, kMaxSums}, dopt);
+  auto s = stream();
   const float* sp = nullptr;
   const float* st = nullptr;
   if (shift_p.has_value()) {
@@ -327,7 +360,35 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
     TORCH_CHECK(shift_t->scalar_type() == at::kFloat && shift_t->numel() == k, "shift_t must be f32[k]");
     st = shift_t->data_ptr<float>();
   }
-  auto s = stream();
+  if (k > kColParMin) {
+    // the one-column-per-thread-with-grid-stride scheme below needs a grid that is a multiple of k (partials of
+    // O(k^2)): many outputs take the column-parallel kernel, ~2^18 threads in total, partials <= ~30 MB
+    const long long col_blocks = (k + kBlock - 1) / kBlock;
+    long long chunks = (1LL << 18) / k;
+    chunks = chunks < 1 ? 1 : chunks;
+    const long long max_chunks = (n_rows + 15) / 16;  // >= 16 rows per thread
+    chunks = chunks > max_chunks ? max_chunks : chunks;
+    chunks = chunks < 1 ? 1 : (chunks > 65535 ? 65535 : chunks);
+    const long long rows_per_chunk = (n_rows + chunks - 1) / chunks;
+    chunks = (n_rows + rows_per_chunk - 1) / rows_per_chunk;
+    at::Tensor partial = at::empty({chunks, k, kMaxSums}, dopt);
+    TM_DISPATCH_FLOAT(preds.scalar_type(), "moments_update", [&] {
+      hipLaunchKernelGGL((moments_colpar_kernel<scalar_t>), dim3(static_cast<unsigned>(col_blocks),
+                         static_cast<unsigned>(chunks)), dim3(kBlock), 0, s,
+                         reinterpret_cast<const scalar_t*>(preds.data_ptr()),
+                         reinterpret_cast<const scalar_t*>(target.data_ptr()), n_rows, k, rows_per_chunk,
+                         static_cast<int>(mask), eps, power, sp, st, partial.data_ptr<double>());
+    });
+    hipLaunchKernelGGL(moments_finalize_kernel, dim3(k), dim3(kBlock), 0, s, partial.data_ptr<double>(),
+                       static_cast<int>(chunks), k, spec, want_sums ? sums.data_ptr<double>() : nullptr,
+                       static_cast<int>(mask));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+    return sums;
+  }
+  // small updates (the common per-batch case): one block does the pass AND the fold -> a single launch
+  const bool fuse = n_rows * k <= 4096 && kBlock % k == 0;
+  if (fuse) blocks = 1;
+  at::Tensor partial = at::empty({blocks, k, kMaxSums}, dopt);
   TM_DISPATCH_FLOAT(preds.scalar_type(), "moments_update", [&] {
     hipLaunchKernelGGL((moments_partial_kernel<scalar_t>), dim3(blocks), dim3(block), 0, s,
                        reinterpret_cast<const scalar_t*>(preds.data_ptr()),

@@ -55,3 +55,17 @@ def test_regression_compute_at_the_kernel_limit(cls, k):
     if states:
         assert ops.regression_computable(states, 6) == (k <= 1 << 20)
     assert_close(gpu.compute().cpu(), cpu.compute(), atol=1e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("k", [255, 256, 257, 1000, 4099])
+def test_moments_update_kernel_switch(k):
+    """Up to 256 outputs the grid-stride moments kernel, beyond it the column-parallel one (rows split in chunks)."""
+    g = torch.Generator().manual_seed(k)
+    preds = torch.randn(3000, k, generator=g)
+    target = preds + 0.5 * torch.randn(3000, k, generator=g)
+    for cls, kw in ((MeanSquaredError, {}), (PearsonCorrCoef, {}), (R2Score, {"multioutput": "raw_values"})):
+        gpu, cpu = cls(num_outputs=k, **kw).cuda(), cls(num_outputs=k, **kw)
+        for lo in range(0, 3000, 1000):
+            gpu.update(preds[lo:lo + 1000].cuda(), target[lo:lo + 1000].cuda())
+            cpu.update(preds[lo:lo + 1000], target[lo:lo + 1000])
+        assert_close(gpu.compute().cpu(), cpu.compute(), atol=1e-5, rtol=1e-4)

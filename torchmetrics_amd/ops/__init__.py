@@ -683,6 +683,23 @@ def calibration_error_l1_max(conf: Tensor, acc: Tensor, bounds: Tensor, norm: st
     return out[0]
 
 
+def calibration_error_from_bins(sums: Tensor, norm: str) -> Tensor:
+    """``l1`` / ``max`` calibration error of ROCm f32 ``[nb, 3]`` (count, Σconf, Σacc) bins in one launch (the bins
+    are left untouched: incremental caches keep accumulating into them)."""
+    out = torch.empty(1, dtype=torch.float32, device=sums.device)
+    (_fast_mod or _fast()).calibration_reduce(sums, 0 if norm == "l1" else 1, out)
+    return out[0]
+
+
+def calibration_bins_into(conf: Tensor, acc: Tensor, bounds: Tensor, sums: Tensor) -> None:
+    """Add the (count, Σconf, Σacc) bins of ROCm f32 ``conf`` / ``acc`` into ``sums`` ``[nb, 3]`` (one launch)."""
+    key = ("bad", conf.device)
+    bad = _CALIB_WS.get(key)
+    if bad is None:
+        bad = _CALIB_WS[key] = torch.zeros(1, dtype=torch.int32, device=conf.device)
+    (_fast_mod or _fast()).calibration_bins(conf, acc, bounds, sums, bad)
+
+
 # -------------------------------------------------------------------------------------------- curve scores
 SCORE_AUROC, SCORE_AP = 0, 1
 _AVG_IDS = {None: 0, "none": 0, "macro": 1, "weighted": 2}

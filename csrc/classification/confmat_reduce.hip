@@ -137,8 +137,11 @@ void calibration_bins(const at::Tensor& conf, const at::Tensor& acc, const at::T
   const long long n = conf.numel();
   if (n == 0) return;
   if (nb <= kPrivBins) {
-    // ~32 elements per thread: enough work to amortise the 3*nb*256-float LDS clear and row reduction per block
-    const int grid = grid_cap((n + kThreads * 32 - 1) / (kThreads * 32), 1024);
+    // ~32 elements per thread amortise the 3*nb*256-float LDS clear and row reduction per block on large inputs;
+    // small ones (a per-update batch) spread over more blocks instead: one block walking 8k elements is ~26 us of
+    // latency, eight blocks of 4 elements per thread finish in a few us
+    const long long per = n >= (1LL << 20) ? 32 : 4;
+    const int grid = grid_cap((n + kThreads * per - 1) / (kThreads * per), 1024);
     hipLaunchKernelGGL(calib_bins_private_kernel, dim3(grid), dim3(kThreads), 0, stream(), conf.data_ptr<float>(),
                        acc.data_ptr<float>(), n, bounds.data_ptr<float>(), nb, sums.data_ptr<float>(),
                        bad.data_ptr<int>());

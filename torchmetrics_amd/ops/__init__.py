@@ -700,6 +700,27 @@ def calibration_bins_into(conf: Tensor, acc: Tensor, bounds: Tensor, sums: Tenso
     (_fast_mod or _fast()).calibration_bins(conf, acc, bounds, sums, bad)
 
 
+RANK_COVERAGE, RANK_LRAP, RANK_LOSS = 0, 1, 2
+_RANK_MAX_LABELS = 2048
+
+
+def label_ranking_rows(preds: Tensor, target: Tensor, mode: int) -> Optional["tuple[Tensor, Tensor]"]:
+    """Per-row coverage / LRAP / ranking loss of ROCm ``[M, L]`` scores (``csrc/classification/ranking.hip``: one
+    wave per row, all-pairs counting in LDS).  Returns ``(values f64 [M], valid u8 [M])`` or None when the kernel does
+    not apply (CPU tensors, L > 2048, non-float scores)."""
+    if not (preds.is_cuda and preds.dim() == 2 and preds.dtype in (torch.float32, torch.float16, torch.bfloat16,
+                                                                     torch.float64)
+            and 1 <= preds.shape[1] <= _RANK_MAX_LABELS and not target.is_floating_point()):
+        return None
+    m = preds.shape[0]
+    out = torch.empty(m, dtype=torch.float64, device=preds.device)
+    valid = torch.empty(m, dtype=torch.uint8, device=preds.device)
+    p = preds.contiguous()
+    gmin = p.min().reshape(1) if (mode == RANK_COVERAGE and m) else p.new_zeros(1)
+    _ops().label_ranking(p, target.contiguous(), mode, gmin, out, valid)
+    return out, valid
+
+
 # -------------------------------------------------------------------------------------------- curve scores
 SCORE_AUROC, SCORE_AP = 0, 1
 _AVG_IDS = {None: 0, "none": 0, "macro": 1, "weighted": 2}

@@ -31,7 +31,7 @@ constexpr int kRowF = 36;  // LDS row: 32 floats + 4 pad (144 B)
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-enum Epi : int { kStore = 0, kEuclid = 1, kCosine = 2, kPolySum = 3, kRowMin = 4, kRowSum = 5 };
+enum Epi : int { kStore = 0, kEuclid = 1, kCosine = 2, kPolySum = 3, kRowMin = 4, kRowSum = 5, kRowColMax = 6 };
 
 struct EpiParams {
   const float* nx;  // |x_i|^2 (EUCLID) or 1/|x_i| (COSINE, ROW_MIN)
@@ -42,6 +42,7 @@ struct EpiParams {
   bool zero_diag;   // EUCLID: zero the diagonal; POLY_SUM: skip it
   bool sqrt_out;    // EUCLID: sqrt (else squared distance)
   float* out;       // [N, M] (STORE / EUCLID / COSINE) or partials
+  float* out2;      // ROW_COL_MAX column partials [batch][tiles_n][M]
   double* dpart;    // POLY_SUM partials [batch * blocks]
   const int32_t* ix;  // optional row gather: X row i of batch b is X[ix[b * N + i]] (KID subsets); else batch-strided
   const int32_t* iy;
@@ -250,6 +251,50 @@ __global__ __launch_bounds__(kNT) void gemm_nt_kernel(const float* __restrict__ 
     if (lane == 0) red[wave] = part;
     __syncthreads();
     if (tid == 0) ep.dpart[(long long)batch * gridDim.x + tile] = red[0] + red[1] + red[2] + red[3];
+  } else if constexpr (EPI == kRowColMax) {
+    // row maxima over this block's 128 columns and column maxima over its 128 rows (scaled dot)
+    float* redr = smem;            // [2][kBM]: per column half
+    float* redc = smem + 2 * kBM;  // [2][kBN]: per row half
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int il = wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int i = row0 + il;
+        float v = -3.0e38f;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int j = col0 + wc + 32 * b + r;
+          if (j < M && i < N) v = fmaxf(v, acc[a][b][e] * ep.scale);
+        }
+#pragma unroll
+        for (int off = 16; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+        if (r == 0) redr[(wave & 1) * kBM + il] = v;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int jl = wc + 32 * b + r;
+      float v = -3.0e38f;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (i < N && col0 + jl < M) v = fmaxf(v, acc[a][b][e] * ep.scale);
+        }
+      v = fmaxf(v, __shfl_xor(v, 32, 64));  // the two lane halves hold interleaved row groups
+      if (h == 0) redc[(wave >> 1) * kBN + jl] = v;
+    }
+    __syncthreads();
+    if (tid < kBM) {
+      const int i = row0 + tid;
+      if (i < N) ep.out[(long long)batch * N * ep.part_cols + (long long)i * ep.part_cols + tj] =
+          fmaxf(redr[tid], redr[kBM + tid]);
+    } else if (tid < kBM + kBN) {
+      const int jl = tid - kBM, j = col0 + jl;
+      if (j < M) ep.out2[((long long)batch * tiles_n + ti) * M + j] = fmaxf(redc[jl], redc[kBN + jl]);
+    }
   } else {
     // ROW_MIN of (1 - cos) or ROW_SUM of the (scaled) dot: per row over this block's 128 columns
     float* red = smem;  // [2][kBM]
@@ -324,9 +369,9 @@ void launch(const at::Tensor& x, const at::Tensor& y, int batches, long long bx,
 }  // namespace
 
 // x: [B, N, D] or [N, D]; y: [B, M, D] or [M, D] (fp32, contiguous).  kind: 0 store, 1 euclid, 2 cosine,
-// 3 poly-sum, 4 row-min(1 - cos), 5 row-sum.  aux_x / aux_y: per-row squared norms (euclid) or inverse norms.
+// 3 poly-sum, 4 row-min(1 - cos), 5 row-sum, 6 row-and-column max of the scaled dot.  aux_x / aux_y: per-row squared norms (euclid) or inverse norms.
 // Returns the output tensor ([B] dims only for batched operands): [B, N, M] fp32 (0-2), fp64 partials [B, blocks]
-// (3), fp32 partials [B, N, tiles_m] (4-5).
+// (3), fp32 partials [B, N, tiles_m] (4-5), flat fp32 [B*N*tiles_m row partials | B*tiles_n*M column partials] (6).
 at::Tensor gemm_nt(const at::Tensor& x, const at::Tensor& y, int64_t kind, const c10::optional<at::Tensor>& aux_x,
                    const c10::optional<at::Tensor>& aux_y, double scale, double coef, int64_t degree, bool zero_diag,
                    bool sqrt_out, const c10::optional<at::Tensor>& idx_x, const c10::optional<at::Tensor>& idx_y) {
@@ -401,6 +446,16 @@ at::Tensor gemm_nt(const at::Tensor& x, const at::Tensor& y, int64_t kind, const
       ep.dpart = out.data_ptr<double>();
       launch<kPolySum>(x, y, B, bx, by, N, M, D, ep);
       break;
+    case kRowColMax: {
+      // row partials [B, N, tiles_m] then column partials [B, tiles_n, M] in one allocation
+      const long long nrow = static_cast<long long>(B) * N * tiles_m, ncol = static_cast<long long>(B) * tiles_n * M;
+      out = at::empty({nrow + ncol}, f32);
+      ep.out = out.data_ptr<float>();
+      ep.out2 = ep.out + nrow;
+      ep.part_cols = tiles_m;
+      launch<kRowColMax>(x, y, B, bx, by, N, M, D, ep);
+      break;
+    }
     case kRowMin:
     case kRowSum:
       out = batched ? at::empty({B, N, tiles_m}, f32) : at::empty({N, tiles_m}, f32);

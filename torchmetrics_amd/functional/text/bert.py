@@ -15,6 +15,7 @@ import torch
 from torch import Tensor
 from torch.nn import Module
 
+from torchmetrics_amd import ops
 from torchmetrics_amd.functional.text._embedding import idf_table, idf_weights, run_sorted, tokenize
 from torchmetrics_amd.utilities.imports import _TQDM_AVAILABLE, _TRANSFORMERS_AVAILABLE
 from torchmetrics_amd.utilities.prints import rank_zero_warn
@@ -68,7 +69,20 @@ def _embed(model: Module, input_ids: Tensor, attention_mask: Tensor, weights: Te
 
 
 def _greedy_match(pe: Tensor, te: Tensor, pw: Tensor, tw: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
-    """Batched greedy matching: pe [N, L, P, D], te [N, L, R, D] -> precision / recall / f1 [N, L]."""
+    """Batched greedy matching: pe [N, L, P, D], te [N, L, R, D] -> precision / recall / f1 [N, L].
+
+    ROCm: one MFMA GEMM over all N * L pairs whose epilogue keeps only the row / column maxima of the token
+    similarities (``ops.gemm_row_col_max``); the reference materialises the [N, L, P, R] cosine tensor
+    (``F/text/bert.py:134-167``)."""
+    n, nl, p, d = pe.shape
+    r = te.shape[2]
+    if pe.is_cuda and d % 4 == 0 and not (pe.requires_grad or te.requires_grad):
+        rmax, cmax = ops.gemm_row_col_max(pe.reshape(n * nl, p, d).float().contiguous(),
+                                          te.reshape(n * nl, r, d).float().contiguous())
+        precision = (rmax.reshape(n, nl, p) * pw[:, None, :].float()).sum(-1)
+        recall = (cmax.reshape(n, nl, r) * tw[:, None, :].float()).sum(-1)
+        f1 = (2 * precision * recall / (precision + recall)).nan_to_num(0.0)
+        return precision, recall, f1
     cos = torch.matmul(pe, te.transpose(-1, -2))  # [N, L, P, R]
     precision = (cos.amax(dim=3) * pw[:, None, :].to(cos)).sum(-1)
     recall = (cos.amax(dim=2) * tw[:, None, :].to(cos)).sum(-1)

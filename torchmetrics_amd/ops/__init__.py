@@ -895,7 +895,7 @@ def pairwise_distance(x: Tensor, y: Tensor, metric: int, p: float = 2.0, zero_di
 
 
 # ------------------------------------------------------------------------------------------- MFMA GEMM epilogues
-GEMM_STORE, GEMM_EUCLID, GEMM_COSINE, GEMM_POLY_SUM, GEMM_ROW_MIN, GEMM_ROW_SUM = range(6)
+GEMM_STORE, GEMM_EUCLID, GEMM_COSINE, GEMM_POLY_SUM, GEMM_ROW_MIN, GEMM_ROW_SUM, GEMM_ROW_COL_MAX = range(7)
 
 
 def gemm_nt(x: Tensor, y: Tensor, kind: int, aux_x: Optional[Tensor] = None, aux_y: Optional[Tensor] = None,
@@ -923,6 +923,18 @@ def gemm_nt(x: Tensor, y: Tensor, kind: int, aux_x: Optional[Tensor] = None, aux
     if idx_x is not None:
         x, y = x[idx_x.long()], y[idx_y.long()]
     return _cpu.gemm_nt(x, y, kind, aux_x, aux_y, scale, coef, degree, zero_diagonal, sqrt_out)
+
+
+def gemm_row_col_max(x: Tensor, y: Tensor, scale: float = 1.0) -> "tuple[Tensor, Tensor]":
+    """``max_j scale * x_i.y_j`` per row and ``max_i`` per column of batched ``[B, N, D] x [B, M, D]`` fp32 operands
+    from one MFMA GEMM launch whose epilogue keeps only the per-tile maxima (the ``[B, N, M]`` score matrix is never
+    written), plus two tiny max reductions.  Returns ``(rows [B, N], cols [B, M])``."""
+    b, n, m = x.shape[0], x.shape[1], y.shape[1]
+    flat = gemm_nt(x, y, GEMM_ROW_COL_MAX, scale=scale)
+    tm, tn = -(-m // 128), -(-n // 128)
+    rows = flat[: b * n * tm].reshape(b, n, tm).amax(-1)
+    cols = flat[b * n * tm:].reshape(b, tn, m).amax(1)
+    return rows, cols
 
 
 # ------------------------------------------------------------------------------------------------------------ text

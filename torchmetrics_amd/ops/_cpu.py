@@ -672,6 +672,13 @@ def gemm_nt(x: Tensor, y: Tensor, kind: int, aux_x, aux_y, scale: float, coef: f
         return v if batched else v[0]
     tiles = -(-m // _GEMM_TILE)
     pad = tiles * _GEMM_TILE - m
+    if kind == 6:  # row partials [b, n, tiles_m] | column partials [b, tiles_n, m], flattened
+        tn = -(-n // _GEMM_TILE)
+        v = dot * scale
+        rows = torch.nn.functional.pad(v, (0, pad), value=-3.0e38).reshape(b, n, tiles, _GEMM_TILE).amax(-1)
+        cols = torch.nn.functional.pad(v, (0, 0, 0, tn * _GEMM_TILE - n), value=-3.0e38)
+        cols = cols.reshape(b, tn, _GEMM_TILE, m).amax(2)
+        return torch.cat([rows.reshape(-1), cols.reshape(-1)])
     if kind == 4:
         v = 1.0 - (dot * aux_x.reshape(b, n, 1).float() * aux_y.reshape(b, 1, m).float()).abs()
         v = torch.nn.functional.pad(v, (0, pad), value=3.0e38)

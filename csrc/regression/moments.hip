@@ -262,10 +262,18 @@ __global__ void __launch_bounds__(kBlock) moments_colpar_kernel(const scalar_t* 
   const float st = shift_t ? shift_t[col] : 0.f;
   const long long r0 = static_cast<long long>(blockIdx.y) * rows_per_chunk;
   const long long r1 = r0 + rows_per_chunk < n_rows ? r0 + rows_per_chunk : n_rows;
-  for (long long r = r0; r < r1; ++r) {
-    const long long i = r * k + col;
-    accumulate_pair(acc, preds[i], target[i], sp, st, mask, eps, pw);
+  long long r = r0;
+  for (; r + 4 <= r1; r += 4) {  // four rows' loads in flight before the dependent accumulation
+    scalar_t pv[4], tv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      pv[q] = preds[(r + q) * k + col];
+      tv[q] = target[(r + q) * k + col];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) accumulate_pair(acc, pv[q], tv[q], sp, st, mask, eps, pw);
   }
+  for (; r < r1; ++r) accumulate_pair(acc, preds[r * k + col], target[r * k + col], sp, st, mask, eps, pw);
   double* dst = partial + (static_cast<long long>(blockIdx.y) * k + col) * kMaxSums;
 #pragma unroll
   for (int s = 0; s < kMaxSums; ++s) dst[s] = acc[s];

@@ -76,7 +76,10 @@ def _greedy_match(pe: Tensor, te: Tensor, pw: Tensor, tw: Tensor) -> Tuple[Tenso
     (``F/text/bert.py:134-167``)."""
     n, nl, p, d = pe.shape
     r = te.shape[2]
-    if pe.is_cuda and d % 4 == 0 and not (pe.requires_grad or te.requires_grad):
+    # the epilogue path pays off once the [N, L, P, R] similarity tensor is large and the per-pair matrices fill the
+    # 128 x 128 GEMM tiles; short sentences stay on the batched library GEMM (benchmarks/bench_misc_kernels.py)
+    big = p >= 128 and r >= 128 and n * nl * p * r >= (1 << 26)
+    if big and pe.is_cuda and d % 4 == 0 and not (pe.requires_grad or te.requires_grad):
         rmax, cmax = ops.gemm_row_col_max(pe.reshape(n * nl, p, d).float().contiguous(),
                                           te.reshape(n * nl, r, d).float().contiguous())
         precision = (rmax.reshape(n, nl, p) * pw[:, None, :].float()).sum(-1)

@@ -289,6 +289,19 @@ def ssim2d_partials(x: Tensor, y: Tensor, wh: Tensor, ww: Tensor, c12: Tensor, m
         upper, lower = 2 * sxy + c2, sxx + syy + c2
         val = ((2 * mxy + c1) * upper) / ((mxx + myy + c1) * lower)
         cs = upper / lower
+    elif mode == 2:  # one VIF scale: x reference, y distorted, c1 = sigma_n^2
+        stt = sxx
+        g = sxy / (sxx + eps)
+        sv = syy - g * sxy
+        low_t = stt < eps
+        g, sv, stt = torch.where(low_t, 0.0, g), torch.where(low_t, syy, sv), torch.where(low_t, 0.0, stt)
+        low_p = syy < eps
+        g, sv = torch.where(low_p, 0.0, g), torch.where(low_p, 0.0, sv)
+        neg = g < 0
+        sv, g = torch.where(neg, syy, sv), torch.where(neg, 0.0, g)
+        sv = sv.clamp(min=eps)
+        val = torch.log10(1.0 + g * g * stt / (sv + c1))
+        cs = torch.log10(1.0 + stt / c1)
     else:
         upper, lower = 2 * sxy, sxx + syy
         val = ((2 * mxy) * upper) / ((mxx + myy) * lower + eps)

@@ -1,4 +1,4 @@
-// Fused SSIM / contrast-sensitivity kernel (2-D, Gaussian or uniform window); also UQI and one VIF scale.
+// Fused SSIM / contrast-sensitivity kernel (2-D, Gaussian or uniform window); also UQI, SCC and one VIF scale.
 //
 // Reference (F/image/ssim.py:45-186) reflect-pads both images, stacks 5 maps (x, y, x*x, y*y, x*y) into a 5B-batch,
 // runs a grouped 11x11 conv2d, then forms the SSIM map and crops the padded border before the per-image mean.  The
@@ -115,6 +115,9 @@ __global__ void __launch_bounds__(kThreads) ssim2d_kernel(const scalar_t* __rest
       const acc_t upper = 2 * sxy;
       const acc_t lower = sxx + syy;
       s_ssim += ((2 * mxy) * upper) / ((mxx + myy) * lower + eps);
+    } else if (mode == 3) {  // spatial correlation coefficient (F/image/scc.py): cov / (sd_x sd_y), 0 where undefined
+      const acc_t den = sqrt(sxx) * sqrt(syy);
+      s_ssim += den == acc_t(0) ? acc_t(0) : sxy / den;
     } else {  // VIF at one scale (F/image/vif.py): x = reference, y = distorted; c1 = sigma_n^2, eps = 1e-10
       acc_t stt = sxx, g = sxy / (sxx + eps), sv = syy - g * sxy;
       if (stt < eps) {
@@ -159,7 +162,8 @@ __global__ void __launch_bounds__(kThreads) ssim2d_kernel(const scalar_t* __rest
 
 // x, y: [P, H, W] planes (contiguous, same dtype); wh [kh], ww [kw] window weights; c12 [3] (c1, c2, eps) in the
 // accumulation dtype (f32, or f64 for f64 inputs); mode 0 = SSIM, 1 = UQI, 2 = VIF (x reference, y distorted;
-// c12 = (sigma_n^2, -, eps)).  Returns part [P, tiles, 2] of per-tile (sum SSIM|UQI|VIF numerator, sum CS|VIF
+// c12 = (sigma_n^2, -, eps)), 3 = SCC (x, y high-passed, uniform window;
+// c12 unused).  Returns part [P, tiles, 2] of per-tile (sum SSIM|UQI|VIF numerator, sum CS|VIF
 // denominator) over the valid windows.
 at::Tensor ssim2d_partials(const at::Tensor& x, const at::Tensor& y, const at::Tensor& wh, const at::Tensor& ww,
                            const at::Tensor& c12, int64_t mode) {

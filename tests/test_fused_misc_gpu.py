@@ -182,3 +182,22 @@ def test_vif_fused_scales_match_torch_path(shape, dtype):
     got = S.visual_information_fidelity(p.cuda(), t.cuda()).cpu()
     want = S.visual_information_fidelity(p, t)
     torch.testing.assert_close(got, want, atol=1e-5 if dtype == torch.float32 else 1e-10, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("window_size", [3, 8, 11])
+@pytest.mark.parametrize("reduction", ["mean", "none"])
+def test_scc_fused_matches_torch_path(window_size, reduction):
+    from torchmetrics_amd.functional.image import spatial_correlation_coefficient
+
+    g = torch.Generator().manual_seed(window_size)
+    p = torch.rand(3, 2, 50, 45, generator=g)
+    t = (p + 0.2 * torch.rand(3, 2, 50, 45, generator=g)).clamp(0, 1)
+    got = spatial_correlation_coefficient(p.cuda(), t.cuda(), window_size=window_size, reduction=reduction).cpu()
+    want = spatial_correlation_coefficient(p, t, window_size=window_size, reduction=reduction)
+    torch.testing.assert_close(got, want, atol=1e-5, rtol=1e-4)
+    m_gpu = tm.image.SpatialCorrelationCoefficient(window_size=window_size).cuda()
+    m_cpu = tm.image.SpatialCorrelationCoefficient(window_size=window_size)
+    m_gpu.update(p.cuda(), t.cuda())
+    m_cpu.update(p, t)
+    torch.testing.assert_close(m_gpu.compute().cpu(), m_cpu.compute(), atol=1e-5, rtol=1e-4)

@@ -44,6 +44,29 @@ def _scc_update(preds: Tensor, target: Tensor, hp_filter: Tensor, window_size: i
     return preds, target, hp_filter[None, None, :].to(dtype=preds.dtype, device=preds.device)
 
 
+def _scc_plane_means(preds: Tensor, target: Tensor, hp_filter: Tensor, window_size: int) -> Tensor:
+    """Per-image SCC averaged over channels and pixels, ``[B]``.
+
+    ROCm: after the (symmetric-padded) high-pass convolution, the zero-padded windowed moments and the per-window
+    correlation run in one launch of the SSIM window kernel (SCC mode, uniform separable window, per-tile sums); the
+    reference stacks 5 maps, runs a grouped conv and forms the map elementwise (``F/image/scc.py:41-90``)."""
+    b, c, h, w = preds.shape
+    if not (preds.is_cuda and window_size <= 33):
+        return _scc_map(preds, target, hp_filter, window_size).mean(dim=[1, 2, 3])
+    x = torch.cat([preds, target], 0).reshape(2 * b * c, 1, h, w)
+    kh, kw = hp_filter.shape[-2:]
+    x = _symmetric_pad(x, 3, (kw - 1) // 2, math.ceil((kw - 1) / 2))
+    x = _symmetric_pad(x, 2, (kh - 1) // 2, math.ceil((kh - 1) / 2))
+    hp = F.conv2d(x, hp_filter.flip([2, 3])) * 2.0
+    lo, hi = math.ceil((window_size - 1) / 2), (window_size - 1) // 2
+    hp = F.pad(hp, (lo, hi, lo, hi))[:, 0]
+    win = torch.full((window_size,), 1.0 / window_size, dtype=hp.dtype, device=hp.device)
+    consts = torch.zeros(3, dtype=hp.dtype, device=hp.device)
+    part = ops.ssim2d_partials(hp[: b * c].contiguous(), hp[b * c:].contiguous(), win, win, consts, ops.SCC_MODE)
+    per_plane = part.sum(1)[:, 0].to(preds.dtype)
+    return per_plane.reshape(b, c).sum(1) / (c * h * w)
+
+
 def _scc_map(preds: Tensor, target: Tensor, hp_filter: Tensor, window_size: int) -> Tensor:
     """Per-pixel spatial correlation of Laplacian-filtered images, all channels at once: ``[B, C, H, W]``."""
     b, c, h, w = preds.shape
@@ -81,10 +104,10 @@ def spatial_correlation_coefficient(
     if reduction not in ("mean", "none"):
         raise ValueError(f"Expected reduction to be 'mean' or 'none', but got {reduction}")
     preds, target, hp_filter = _scc_update(preds, target, hp_filter, window_size)
-    scc = _scc_map(preds, target, hp_filter, window_size)
+    per_image = _scc_plane_means(preds, target, hp_filter, window_size)
     if reduction == "none":
-        return scc.mean(dim=[1, 2, 3])
-    return scc.mean()
+        return per_image
+    return per_image.mean()
 
 
 # ------------------------------------------------------------------------------------------------------------ VIF

@@ -774,6 +774,7 @@ def curve_update(preds: Tensor, target: Tensor, thr_sorted: Tensor, perm: Tensor
 SSIM_MODE = 0
 UQI_MODE = 1
 VIF_MODE = 2
+SCC_MODE = 3
 
 
 def ssim2d_partials(x: Tensor, y: Tensor, wh: Tensor, ww: Tensor, c12: Tensor, mode: int = SSIM_MODE) -> Tensor:

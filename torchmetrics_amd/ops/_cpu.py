@@ -289,6 +289,10 @@ def ssim2d_partials(x: Tensor, y: Tensor, wh: Tensor, ww: Tensor, c12: Tensor, m
         upper, lower = 2 * sxy + c2, sxx + syy + c2
         val = ((2 * mxy + c1) * upper) / ((mxx + myy + c1) * lower)
         cs = upper / lower
+    elif mode == 3:  # spatial correlation coefficient of high-passed planes
+        den = sxx.sqrt() * syy.sqrt()
+        val = torch.where(den == 0, torch.zeros_like(sxy), sxy / torch.where(den == 0, 1.0, den))
+        cs = torch.zeros_like(val)
     elif mode == 2:  # one VIF scale: x reference, y distorted, c1 = sigma_n^2
         stt = sxx
         g = sxy / (sxx + eps)

@@ -832,6 +832,14 @@ def coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, g
                            iou_pre, iou_off)
 
 
+def panoptic_tables(pcode: Tensor, tcode: Tensor) -> List[Tensor]:
+    """Per-image pixel areas of predicted segments, target segments and segment pairs from int32 ``[B, P]`` segment
+    codes (``csrc/detection/panoptic.hip``: LDS hash tables, one block per image).  Returns pair keys (int64:
+    ``pred << 32 | target``) and counts ``[B, 4096]``, pred / target keys and counts ``[B, 1024]`` (empty slots: key
+    -1), and an overflow flag."""
+    return list(_ops().panoptic_tables(pcode, tcode))
+
+
 def rle_encode(masks: List[Tensor]) -> List[Tensor]:
     """Run-length encode every ``[n_i, H_i, W_i]`` mask tensor into one int32 pack per image
     (``[n, H, W, areas(n), offsets(n+1), change positions...]``, ``csrc/detection/rle.hip``): ROCm kernels (one host

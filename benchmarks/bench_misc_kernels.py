@@ -86,6 +86,30 @@ def main():
     print(json.dumps({"case": "moments sse 2e4 x 4096 outputs", "ours_ms": round(t_ours, 4), "torch_ms": round(t_ref, 4),
                       "speedup": round(t_ref / t_ours, 2),
                       "GBps": round(2 * x.numel() * 4 / t_ours / 1e6, 1)}), flush=True)
+    del x, y
+
+    from torchmetrics_amd.classification import MulticlassAccuracy
+
+    for dtype in (torch.bfloat16, torch.float32):
+        s = torch.randn(65536, 1000, device=dev, generator=g).to(dtype)
+        lab = torch.randint(0, 1000, (65536,), device=dev, generator=g)
+        t_ours, a = timed(lambda: ops.topk_labels(s, 5))
+        t_ref, b = timed(lambda: torch.topk(s, 5, dim=1).indices)
+        print(json.dumps({"case": f"topk_labels k=5 65536x1000 {str(dtype)[6:]}", "ours_ms": round(t_ours, 4),
+                          "torch_ms": round(t_ref, 4), "speedup": round(t_ref / t_ours, 2),
+                          "GBps": round(s.numel() * s.element_size() / t_ours / 1e6, 1),
+                          "mismatch_rows": int((a.long() != b).any(1).sum())}), flush=True)
+        m = MulticlassAccuracy(num_classes=1000, top_k=5).to(dev)
+        t_ours, _ = timed(lambda: m.update(s, lab))
+        saved = ops.mc_topk_update
+        ops.mc_topk_update = lambda *a, **k: False  # torch.topk labels + the label histogram kernel
+        try:
+            t_ref, _ = timed(lambda: m.update(s, lab))
+        finally:
+            ops.mc_topk_update = saved
+        print(json.dumps({"case": f"MulticlassAccuracy(top_k=5).update 65536x1000 {str(dtype)[6:]}",
+                          "ours_ms": round(t_ours, 4), "torch_topk_ms": round(t_ref, 4),
+                          "speedup": round(t_ref / t_ours, 2)}), flush=True)
 
 
 if __name__ == "__main__":

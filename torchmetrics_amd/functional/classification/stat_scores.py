@@ -254,9 +254,10 @@ def _multiclass_stats(
         t = t.reshape(1)
         preds = preds.reshape(1, *preds.shape) if preds.ndim <= 1 else preds
     N = t.shape[0]
+    fused_topk = top_k > 1 and preds.is_floating_point() and preds.ndim == 2 == t.ndim + 1
     if preds.is_floating_point() and preds.ndim == t.ndim + 1:
         p = preds
-        if top_k > 1:
+        if top_k > 1 and not fused_topk:
             p = preds.topk(top_k, dim=1).indices  # [N, K, ...] int64 labels
     else:
         p = _as_preds(preds)
@@ -269,7 +270,11 @@ def _multiclass_stats(
         ws, _ = workspace.get(G * (3 * C + 1), dev)
     else:
         ws = torch.zeros(G * (3 * C + 1), dtype=torch.int64, device=dev)
-    ops.mc_update(p.contiguous(), t.contiguous(), ws, flag, C, ignore_index, ops.MC_STATS, samplewise)
+    # top_k > 1 on [N, C] scores: selection + histogram in one launch (topk.hip), else topk labels + mc_update
+    if not (fused_topk and ops.mc_topk_update(preds, t, ws, flag, top_k, ignore_index, samplewise)):
+        if fused_topk:
+            p = preds.topk(top_k, dim=1).indices
+        ops.mc_update(p.contiguous(), t.contiguous(), ws, flag, C, ignore_index, ops.MC_STATS, samplewise)
     if out is not None and not samplewise:
         ops.mc_stats_finalize(ws, C, micro, True, *out)
         return out

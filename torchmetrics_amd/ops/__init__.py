@@ -721,6 +721,33 @@ def label_ranking_rows(preds: Tensor, target: Tensor, mode: int) -> Optional["tu
     return out, valid
 
 
+_TOPK_MAX = 16
+
+
+def topk_labels(preds: Tensor, k: int) -> Optional[Tensor]:
+    """Column indices of the ``k`` largest scores per row of ROCm ``[N, C]`` scores, descending, as int32 ``[N, k]``
+    (``csrc/classification/topk.hip``: one wave per row, register top-k per lane + k wave arg-max rounds; NaN ranks
+    highest, ties go to the smaller column).  None when the kernel does not apply (CPU, k > 16, f64 / int scores)."""
+    if not (preds.is_cuda and preds.dim() == 2 and preds.dtype in (torch.float32, torch.float16, torch.bfloat16)
+            and 1 <= k <= min(_TOPK_MAX, preds.shape[1])):
+        return None
+    return _ops().topk_labels(preds.contiguous(), int(k))
+
+
+def mc_topk_update(preds: Tensor, target: Tensor, ws: Tensor, flag: Tensor, k: int, ignore_index: Optional[int],
+                   samplewise: bool) -> bool:
+    """top_k > 1 multiclass stats fused with the top-k selection (``csrc/classification/topk.hip``): accumulates the
+    ``[G, 3C + 1]`` :func:`mc_update` stats workspace from ROCm ``[N, C]`` scores and ``[N]`` targets.  Returns False
+    (nothing done) when the kernel does not apply; the caller then takes topk + :func:`mc_update`."""
+    if not (preds.is_cuda and preds.dim() == 2 and target.dim() == 1
+            and preds.dtype in (torch.float32, torch.float16, torch.bfloat16)
+            and 2 <= k <= min(_TOPK_MAX, preds.shape[1]) and not target.is_floating_point()):
+        return False
+    _ops().mc_topk_update(preds.contiguous(), target.contiguous(), ws, flag, int(k),
+                          0 if ignore_index is None else int(ignore_index), ignore_index is not None, samplewise)
+    return True
+
+
 # -------------------------------------------------------------------------------------------- curve scores
 SCORE_AUROC, SCORE_AP = 0, 1
 _AVG_IDS = {None: 0, "none": 0, "macro": 1, "weighted": 2}

@@ -1,0 +1,255 @@
+// Exact match (subset accuracy) update in two launches (K10 in SURVEY.md §2.5).
+//
+// Reference (F/classification/exact_match.py:32-128): multiclass -- argmax over dim 1 (a [N, P] label copy), a
+// masked fill for ignore_index, `preds == target` ([N, P] bool), `.sum(1) == P`, `.sum()`; multilabel -- a host sync
+// to decide whether the scores are probabilities (`_prob_or`), a sigmoid copy, a threshold copy, two masked fills,
+// `movedim(1, -1).reshape(-1, L)` (a transposed copy for multi-dim inputs), `== target`, `.sum(1) == L`, `.sum()`.
+// Here one pass decides each unit directly from the scores:
+//   * multiclass, P == 1: one wave per sample, lanes over the C scores (wave argmax, torch.argmax tie / NaN rules);
+//   * multiclass, P > 1: one wave per sample, lanes over the P positions (coalesced over the [N, C, P] layout), each
+//     lane a sequential argmax over C; a wave vote ANDs the positions;
+//   * multilabel: one thread per (sample, position) unit looping over the L labels, judging BOTH readings of float
+//     scores (as given / sigmoid in the scores' dtype) and OR-ing a "not a probability" word; the fold keeps the
+//     reading the batch calls for (the reference's global `_prob_or` decision) without a host round trip.
+// Counts are int64 atomics (order independent, deterministic).  The fold adds the global count and total into the
+// metric states in place, or writes the per-sample counts (samplewise), and re-zeroes the workspace.
+#include "common/tm_common.h"
+
+namespace tm_amd {
+namespace {
+
+constexpr int kBlock = 256;
+
+// multiclass, P == 1: preds [N, C] (float scores) or [N] labels; ws: i64 [1] (global) or [N] (samplewise)
+template <typename scalar_t, typename target_t>
+__global__ void __launch_bounds__(kBlock) em_multiclass_row_kernel(const scalar_t* __restrict__ preds,
+                                                                   const target_t* __restrict__ target, long long N,
+                                                                   int C, long long ignore, bool has_ignore,
+                                                                   bool samplewise, int64_t* __restrict__ ws) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const long long nw = static_cast<long long>(gridDim.x) * (kBlock / kWave);
+  long long local = 0;
+  for (long long n = (static_cast<long long>(blockIdx.x) * kBlock + threadIdx.x) / kWave; n < N; n += nw) {
+    const long long t = static_cast<long long>(target[n]);
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    const scalar_t* r = preds + n * C;
+    for (int c = lane; c < C; c += kWave) {
+      const float v = to_f32(r[c]);
+      if (argmax_better(v, c, bv, bi)) {
+        bv = v;
+        bi = c;
+      }
+    }
+    wave_argmax(bv, bi);
+    const bool ok = (has_ignore && t == ignore) || static_cast<long long>(bi) == t;
+    if (lane == 0) {
+      if (samplewise)
+        ws[n] = ok ? 1 : 0;
+      else
+        local += ok ? 1 : 0;
+    }
+  }
+  if (!samplewise && lane == 0 && local) atomic_add_i64(ws, local);
+}
+
+// multiclass, P > 1: preds [N, C, P] scores; target [N, P]
+template <typename scalar_t, typename target_t>
+__global__ void __launch_bounds__(kBlock) em_multiclass_pos_kernel(const scalar_t* __restrict__ preds,
+                                                                   const target_t* __restrict__ target, long long N,
+                                                                   int C, long long P, long long ignore,
+                                                                   bool has_ignore, bool samplewise,
+                                                                   int64_t* __restrict__ ws) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const long long nw = static_cast<long long>(gridDim.x) * (kBlock / kWave);
+  long long local = 0;
+  for (long long n = (static_cast<long long>(blockIdx.x) * kBlock + threadIdx.x) / kWave; n < N; n += nw) {
+    int bad = 0;
+    for (long long p = lane; p < P; p += kWave) {
+      const long long t = static_cast<long long>(target[n * P + p]);
+      if (has_ignore && t == ignore) continue;
+      const scalar_t* r = preds + n * C * P + p;
+      float bv = to_f32(r[0]);
+      int bi = 0;
+      for (int c = 1; c < C; ++c) {
+        const float v = to_f32(r[static_cast<long long>(c) * P]);
+        if (argmax_better(v, c, bv, bi)) {
+          bv = v;
+          bi = c;
+        }
+      }
+      const long long label = bi;
+      bad |= label != t;
+    }
+    const bool ok = !__any(bad);
+    if (lane == 0) {
+      if (samplewise)
+        ws[n] = ok ? 1 : 0;
+      else
+        local += ok ? 1 : 0;
+    }
+  }
+  if (!samplewise && lane == 0 && local) atomic_add_i64(ws, local);
+}
+
+// multilabel: preds / target [N, L, P]; unit u = (n, p); ws: i64 [2] (global: reading A, B) or [2N] (samplewise:
+// per-sample counts of correct positions, A then B); notprob: i32 [1]
+template <typename scalar_t, typename target_t>
+__global__ void __launch_bounds__(kBlock) em_multilabel_kernel(const scalar_t* __restrict__ preds,
+                                                               const target_t* __restrict__ target, long long N,
+                                                               int L, long long P, float thr, long long ignore,
+                                                               bool has_ignore, bool samplewise,
+                                                               int64_t* __restrict__ ws, int* __restrict__ notprob) {
+  const long long U = N * P;
+  long long ca = 0, cb = 0;
+  int np = 0;
+  for (long long u = static_cast<long long>(blockIdx.x) * kBlock + threadIdx.x; u < U;
+       u += static_cast<long long>(gridDim.x) * kBlock) {
+    const long long n = u / P, p = u - n * P;
+    const scalar_t* pr = preds + n * L * P + p;
+    const target_t* tr = target + n * L * P + p;
+    bool oka = true, okb = true;
+    for (int l = 0; l < L; ++l) {
+      const long long t = static_cast<long long>(tr[static_cast<long long>(l) * P]);
+      const scalar_t v = pr[static_cast<long long>(l) * P];
+      if constexpr (IsFloating<scalar_t>::value) {
+        const float x = to_f32(v);
+        np |= !(x >= 0.f && x <= 1.f);  // the reference decides over every score, ignored positions included
+        if (has_ignore && t == ignore) continue;
+        const float s = round_to<scalar_t>(1.f / (1.f + expf(-x)));
+        oka &= static_cast<long long>(x > thr) == t;
+        okb &= static_cast<long long>(s > thr) == t;
+      } else {
+        if (has_ignore && t == ignore) continue;
+        const bool eq = static_cast<long long>(v) == t;
+        oka &= eq;
+        okb &= eq;
+      }
+    }
+    if (samplewise) {
+      if (oka) atomic_add_i64(ws + n, 1);
+      if (okb) atomic_add_i64(ws + N + n, 1);
+    } else {
+      ca += oka;
+      cb += okb;
+    }
+  }
+  if (__any(np) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(notprob, 1);
+  if (!samplewise) {
+    ca = wave_sum_ll(ca);
+    cb = wave_sum_ll(cb);
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+      if (ca) atomic_add_i64(ws, ca);
+      if (cb) atomic_add_i64(ws + 1, cb);
+    }
+  }
+}
+
+// global: correct += (notprob ? ws[1] : ws[0]); total += total_add.  samplewise: out[n] = ws[(notprob ? N : 0) + n].
+// Re-zeroes ws (two_readings: 2 slots / 2N) and notprob.
+__global__ void em_fold_kernel(int64_t* __restrict__ ws, long long N, bool samplewise, bool two_readings,
+                               int* __restrict__ notprob, int64_t* __restrict__ correct, int64_t* __restrict__ total,
+                               long long total_add, int64_t* __restrict__ out) {
+  const bool use_b = two_readings && *notprob != 0;
+  if (samplewise) {
+    for (long long n = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; n < N;
+         n += static_cast<long long>(gridDim.x) * blockDim.x) {
+      out[n] = use_b ? ws[N + n] : ws[n];
+      ws[n] = 0;
+      if (two_readings) ws[N + n] = 0;
+    }
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *correct += use_b ? ws[1] : ws[0];
+    *total += total_add;
+    ws[0] = 0;
+    ws[1] = 0;
+    *notprob = 0;
+  }
+}
+
+__global__ void em_reset_notprob_kernel(int* notprob) { *notprob = 0; }
+
+}  // namespace
+
+// kind 0 multiclass (preds [N, C, P] scores, has_c; target [N, P]); kind 1 multilabel (preds / target [N, L, P];
+// C = L; also multiclass integer labels as L = positions, P = 1).  ws: i64 zeroed, [max(2, 2N)]; notprob: i32 [1] zero.  Global: correct / total
+// i64 [1] states updated in place (total += N for multiclass, N * P for multilabel).  Samplewise: out i64 [N] receives
+// the per-sample counts (0/1 multiclass, correct positions multilabel).
+void exact_match_update(const at::Tensor& preds, const at::Tensor& target, int64_t kind, int64_t C, int64_t P,
+                        bool has_c, double threshold, int64_t ignore_index, bool has_ignore, bool samplewise,
+                        at::Tensor ws, at::Tensor notprob, at::Tensor correct, at::Tensor total, at::Tensor out) {
+  TM_CHECK_CUDA(preds);
+  for (const at::Tensor* t :
+       std::initializer_list<const at::Tensor*>{&target, &ws, &notprob, &correct, &total, &out})
+    TM_SAME_DEVICE(preds, (*t));
+  TM_CHECK_CONTIG(preds);
+  TM_CHECK_CONTIG(target);
+  TORCH_CHECK(kind == 0 || kind == 1, "exact_match_update: bad kind");
+  // multiclass labels are the multilabel integer case with L = P positions and one unit per sample
+  TORCH_CHECK(kind == 1 || has_c, "exact_match_update: multiclass labels go through kind 1 (L = P, P = 1)");
+  TORCH_CHECK(C >= 1 && P >= 1, "exact_match_update: C and P must be positive");
+  const long long N = P > 0 ? target.numel() / (kind == 0 ? P : C * P) : 0;
+  TORCH_CHECK(target.numel() == N * (kind == 0 ? P : C * P), "exact_match_update: target shape");
+  TORCH_CHECK(preds.numel() == N * C * P, "exact_match_update: preds shape");
+  TORCH_CHECK(ws.scalar_type() == at::kLong && ws.is_contiguous() && ws.numel() >= std::max<long long>(2, 2 * N),
+              "exact_match_update: ws");
+  TORCH_CHECK(notprob.scalar_type() == at::kInt && notprob.numel() == 1, "exact_match_update: notprob");
+  TORCH_CHECK(correct.scalar_type() == at::kLong && correct.numel() == 1 && total.scalar_type() == at::kLong &&
+                  total.numel() == 1, "exact_match_update: states");
+  TORCH_CHECK(!samplewise || (out.scalar_type() == at::kLong && out.numel() == N && out.is_contiguous()),
+              "exact_match_update: out");
+  auto s = stream();
+  int64_t* w = ws.data_ptr<int64_t>();
+  if (N > 0) {
+    TM_DISPATCH_TARGET(target.scalar_type(), "exact_match_update", [&] {
+      TM_DISPATCH_PREDS(preds.scalar_type(), "exact_match_update", [&] {
+        const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
+        const target_t* t = reinterpret_cast<const target_t*>(target.data_ptr());
+        const long long ig = static_cast<long long>(ignore_index);
+        float thr = static_cast<float>(threshold);  // the threshold as ATen compares it against 16-bit scores
+        if constexpr (std::is_same<scalar_t, c10::BFloat16>::value) thr = static_cast<float>(c10::BFloat16(thr));
+        if constexpr (std::is_same<scalar_t, c10::Half>::value) thr = static_cast<float>(c10::Half(thr));
+        if (kind == 0 && P == 1) {
+          hipLaunchKernelGGL((em_multiclass_row_kernel<scalar_t, target_t>),
+                             dim3(grid_cap((N + (kBlock / kWave) - 1) / (kBlock / kWave), 4096)), dim3(kBlock), 0,
+                             s, p, t, N, static_cast<int>(C), ig, has_ignore, samplewise, w);
+        } else if (kind == 0) {
+          hipLaunchKernelGGL((em_multiclass_pos_kernel<scalar_t, target_t>),
+                             dim3(grid_cap((N + (kBlock / kWave) - 1) / (kBlock / kWave), 4096)), dim3(kBlock), 0,
+                             s, p, t, N, static_cast<int>(C), static_cast<long long>(P), ig, has_ignore,
+                             samplewise, w);
+        } else {
+          hipLaunchKernelGGL((em_multilabel_kernel<scalar_t, target_t>),
+                             dim3(grid_cap((N * P + kBlock - 1) / kBlock, 4096)), dim3(kBlock), 0, s, p, t, N,
+                             static_cast<int>(C), static_cast<long long>(P), thr, ig,
+                             has_ignore, samplewise, w, notprob.data_ptr<int>());
+        }
+      });
+    });
+  }
+  const bool two = kind == 1;
+  const long long total_add = kind == 0 ? N : N * P;
+  if (samplewise) {
+    if (N > 0)
+      hipLaunchKernelGGL(em_fold_kernel, dim3(grid_cap((N + 255) / 256, 1024)), dim3(256), 0, s, w, N, true, two,
+                         notprob.data_ptr<int>(), correct.data_ptr<int64_t>(), total.data_ptr<int64_t>(), total_add,
+                         out.data_ptr<int64_t>());
+    if (two) hipLaunchKernelGGL(em_reset_notprob_kernel, dim3(1), dim3(1), 0, s, notprob.data_ptr<int>());
+  } else {
+    hipLaunchKernelGGL(em_fold_kernel, dim3(1), dim3(64), 0, s, w, N, false, two, notprob.data_ptr<int>(),
+                       correct.data_ptr<int64_t>(), total.data_ptr<int64_t>(), total_add, nullptr);
+  }
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def(
+      "exact_match_update(Tensor preds, Tensor target, int kind, int C, int P, bool has_c, float threshold, "
+      "int ignore_index, bool has_ignore, bool samplewise, Tensor(a!) ws, Tensor(b!) notprob, Tensor(c!) correct, "
+      "Tensor(d!) total, Tensor(e!) out) -> ()");
+}
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) { m.impl("exact_match_update", &exact_match_update); }
+
+}  // namespace tm_amd

@@ -1,0 +1,219 @@
+// Aggregator updates (Sum / Mean / Max / Min metrics) in ONE launch (K35 in SURVEY.md §2.5).
+//
+// Reference (S/aggregation.py:75-105 + the update bodies at :170-560): isnan(x), isnan(w), `nans.any()` (a host
+// sync on every update), a boolean-mask compaction `x[~nans]` / `w[~nans]` (a second sync for the output size),
+// ones_like(x) for the weights, then `(x * w).sum()` / `w.sum()` / `max()` / `min()` and the state add: ~8-10
+// launches and two host round trips per update, for what is usually a single loss scalar.
+// Here one grid-stride pass applies the nan strategy per element (error: validation bit; ignore / warn: the element
+// drops out; float: x and w imputed, as the reference does) and reduces sum(x*w), sum(w), max and min in fp64; the
+// last block to finish (ticket counter) folds the per-block partials in a fixed order -- deterministic whatever the
+// block completion order -- and adds the result into the metric's state tensors in place.  A python-number weight
+// is a kernel argument (no H2D copy of a ones tensor); a tensor weight may be one element (broadcast) or N.
+#include "common/tm_common.h"
+
+namespace tm_amd {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kMaxBlocks = 512;
+enum Kind : int { kSum = 0, kMean = 1, kMax = 2, kMin = 3 };
+enum NanMode : int { kNanError = 0, kNanIgnore = 1, kNanImpute = 2 };
+
+template <typename T>
+__device__ __forceinline__ double to_f64(T v) {
+  return static_cast<double>(to_f32(v));
+}
+template <>
+__device__ __forceinline__ double to_f64<double>(double v) {
+  return v;
+}
+
+__device__ __forceinline__ double nan_max(double a, double b) { return (a != a || a > b) ? a : b; }
+__device__ __forceinline__ double nan_min(double a, double b) { return (a != a || a < b) ? a : b; }
+
+// part: f64 [kMaxBlocks][5] (sum x*w, sum w, max, min, NaN count); ctl: i32 [2] = {ticket, NaN count of the last call}
+template <typename x_t, typename w_t, typename out_t>
+__global__ void __launch_bounds__(kBlock) agg_update_kernel(const x_t* __restrict__ x, const w_t* __restrict__ w,
+                                                            long long N, long long w_n, double wconst, int kind,
+                                                            int nan_mode, double impute, double* __restrict__ part,
+                                                            int* __restrict__ ctl, out_t* __restrict__ s0,
+                                                            out_t* __restrict__ s1, int* __restrict__ flag) {
+  __shared__ double red[4][kBlock / kWave];
+  __shared__ int red_nan[kBlock / kWave];
+  __shared__ bool last;
+  double s = 0.0, sw = 0.0, mx = -INFINITY, mn = INFINITY;
+  int nan = 0;
+  for (long long i = static_cast<long long>(blockIdx.x) * kBlock + threadIdx.x; i < N;
+       i += static_cast<long long>(gridDim.x) * kBlock) {
+    double xv = to_f64(x[i]);
+    double wv = w_n == 0 ? wconst : to_f64(w[w_n == 1 ? 0 : i]);
+    if (xv != xv || wv != wv) {
+      ++nan;
+      if (nan_mode == kNanImpute) {
+        xv = impute;
+        wv = impute;
+      } else {
+        continue;  // ignore / warn drop the element; error only raises the bit (the state is not used afterwards)
+      }
+    }
+    s += xv * wv;
+    sw += wv;
+    mx = nan_max(mx, xv);
+    mn = nan_min(mn, xv);
+  }
+  s = wave_sum(s);
+  sw = wave_sum(sw);
+  nan = static_cast<int>(wave_sum_ll(nan));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mx = nan_max(mx, __shfl_xor(mx, off, kWave));
+    mn = nan_min(mn, __shfl_xor(mn, off, kWave));
+  }
+  const int wv_id = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+    red[0][wv_id] = s;
+    red[1][wv_id] = sw;
+    red[2][wv_id] = mx;
+    red[3][wv_id] = mn;
+    red_nan[wv_id] = nan;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = 0.0, c = -INFINITY, d = INFINITY;
+    int n = 0;
+    for (int k = 0; k < kBlock / kWave; ++k) {
+      a += red[0][k];
+      b += red[1][k];
+      c = nan_max(c, red[2][k]);
+      d = nan_min(d, red[3][k]);
+      n += red_nan[k];
+    }
+    double* p = part + 5 * blockIdx.x;
+    p[0] = a;
+    p[1] = b;
+    p[2] = c;
+    p[3] = d;
+    p[4] = static_cast<double>(n);
+    __threadfence();
+    last = atomicAdd(ctl, 1) == static_cast<int>(gridDim.x) - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  // fixed-order fold of the block partials: thread t takes blocks t, t + 256, ... then one wave tree + LDS pass
+  double a = 0.0, b = 0.0, c = -INFINITY, d = INFINITY, e = 0.0;
+  for (int k = threadIdx.x; k < static_cast<int>(gridDim.x); k += kBlock) {
+    const double* p = part + 5 * k;
+    a += __builtin_nontemporal_load(p);
+    b += __builtin_nontemporal_load(p + 1);
+    c = nan_max(c, __builtin_nontemporal_load(p + 2));
+    d = nan_min(d, __builtin_nontemporal_load(p + 3));
+    e += __builtin_nontemporal_load(p + 4);
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  e = wave_sum(e);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    c = nan_max(c, __shfl_xor(c, off, kWave));
+    d = nan_min(d, __shfl_xor(d, off, kWave));
+  }
+  __syncthreads();
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+    red[0][wv_id] = a;
+    red[1][wv_id] = b;
+    red[2][wv_id] = c;
+    red[3][wv_id] = d;
+    red_nan[wv_id] = static_cast<int>(e);
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  int nan_total = red_nan[0];
+  for (int k = 1; k < kBlock / kWave; ++k) {
+    red[0][0] += red[0][k];
+    red[1][0] += red[1][k];
+    red[2][0] = nan_max(red[2][0], red[2][k]);
+    red[3][0] = nan_min(red[3][0], red[3][k]);
+    nan_total += red_nan[k];
+  }
+  if (nan_mode == kNanError && nan_total) raise_flag(flag, kErrValueNan);
+  switch (kind) {
+    case kSum:
+      *s0 = static_cast<out_t>(static_cast<double>(*s0) + red[0][0]);
+      break;
+    case kMean:
+      *s0 = static_cast<out_t>(static_cast<double>(*s0) + red[0][0]);
+      *s1 = static_cast<out_t>(static_cast<double>(*s1) + red[1][0]);
+      break;
+    case kMax:
+      if (N - (nan_mode == kNanImpute ? 0 : nan_total) > 0)
+        *s0 = static_cast<out_t>(nan_max(static_cast<double>(*s0), red[2][0]));
+      break;
+    default:
+      if (N - (nan_mode == kNanImpute ? 0 : nan_total) > 0)
+        *s0 = static_cast<out_t>(nan_min(static_cast<double>(*s0), red[3][0]));
+      break;
+  }
+  ctl[1] = nan_total;  // this call's NaN count, read by the host for 'warn'
+  ctl[0] = 0;
+}
+
+}  // namespace
+
+// x: ROCm float tensor [N] (contiguous); w: empty (use wconst), [1] or [N] float; kind 0 sum / 1 mean / 2 max /
+// 3 min; nan_mode 0 error / 1 ignore (and warn) / 2 impute; part: f64 [>= 5 * 512]; ctl: i32 [2] (ctl[0] == 0 on
+// entry); s0 (and s1 for mean): f32 / f64 0-d state tensors updated in place; flag: i32 validation word.
+void agg_update(const at::Tensor& x, const at::Tensor& w, double wconst, int64_t kind, int64_t nan_mode,
+                double impute, at::Tensor part, at::Tensor ctl, at::Tensor s0, at::Tensor s1, at::Tensor flag) {
+  TM_CHECK_CUDA(x);
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&part, &ctl, &s0, &s1, &flag})
+    TM_SAME_DEVICE(x, (*t));
+  TM_CHECK_CONTIG(x);
+  TORCH_CHECK(kind >= 0 && kind <= 3, "agg_update: bad kind");
+  TORCH_CHECK(nan_mode >= 0 && nan_mode <= 2, "agg_update: bad nan_mode");
+  const long long N = x.numel();
+  const long long w_n = w.numel();
+  TORCH_CHECK(w_n == 0 || w_n == 1 || w_n == N, "agg_update: weight must have 0, 1 or N elements");
+  if (w_n) {
+    TM_SAME_DEVICE(x, w);
+    TM_CHECK_CONTIG(w);
+  }
+  TORCH_CHECK(part.scalar_type() == at::kDouble && part.numel() >= 5 * kMaxBlocks && part.is_contiguous(),
+              "agg_update: part workspace");
+  TORCH_CHECK(ctl.scalar_type() == at::kInt && ctl.numel() >= 2, "agg_update: ctl workspace");
+  TORCH_CHECK(s0.scalar_type() == at::kFloat || s0.scalar_type() == at::kDouble, "agg_update: state dtype");
+  TORCH_CHECK(s0.numel() == 1 && s1.numel() == 1 && s1.scalar_type() == s0.scalar_type(), "agg_update: states");
+  TORCH_CHECK(flag.scalar_type() == at::kInt && flag.numel() >= 1, "agg_update: flag");
+  auto s = stream();
+  if (N == 0) return;
+  const int blocks = grid_cap((N + kBlock - 1) / kBlock, std::min(kMaxBlocks, 2 * cu_count(x.get_device())));
+  TM_DISPATCH_FLOAT(x.scalar_type(), "agg_update", [&] {
+    using x_t = scalar_t;
+    const at::ScalarType wt = w_n ? w.scalar_type() : x.scalar_type();
+    TM_DISPATCH_FLOAT(wt, "agg_update", [&] {
+      using w_t = scalar_t;
+      const w_t* wp = w_n ? reinterpret_cast<const w_t*>(w.data_ptr()) : nullptr;
+      const x_t* xp = reinterpret_cast<const x_t*>(x.data_ptr());
+      if (s0.scalar_type() == at::kFloat)
+        hipLaunchKernelGGL((agg_update_kernel<x_t, w_t, float>), dim3(blocks), dim3(kBlock), 0, s, xp, wp, N, w_n,
+                           wconst, static_cast<int>(kind), static_cast<int>(nan_mode), impute,
+                           part.data_ptr<double>(), ctl.data_ptr<int>(), s0.data_ptr<float>(), s1.data_ptr<float>(),
+                           flag.data_ptr<int>());
+      else
+        hipLaunchKernelGGL((agg_update_kernel<x_t, w_t, double>), dim3(blocks), dim3(kBlock), 0, s, xp, wp, N, w_n,
+                           wconst, static_cast<int>(kind), static_cast<int>(nan_mode), impute,
+                           part.data_ptr<double>(), ctl.data_ptr<int>(), s0.data_ptr<double>(),
+                           s1.data_ptr<double>(), flag.data_ptr<int>());
+    });
+  });
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def(
+      "agg_update(Tensor x, Tensor w, float wconst, int kind, int nan_mode, float impute, Tensor(a!) part, "
+      "Tensor(b!) ctl, Tensor(c!) s0, Tensor(d!) s1, Tensor(e!) flag) -> ()");
+}
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) { m.impl("agg_update", &agg_update); }
+
+}  // namespace tm_amd

@@ -6,12 +6,16 @@ NaN handling (``nan_strategy``) keeps the reference semantics, but on GPU tensor
 * ``'error'``  -> a device-side flag (raised at ``compute()``, or per update with ``TORCHMETRICS_AMD_STRICT=1``);
 * ``'ignore'`` / float -> NaNs are masked to the aggregator's neutral element / imputed in place, no sync;
 * ``'warn'``   -> needs the host to decide whether to warn, so it syncs (as the reference does).
+
+On ROCm, Sum / Mean / Max / Min updates are one launch of ``csrc/common/aggregate.hip`` (NaN strategy, fp64
+reduction and the in-place state fold together); ``'warn'`` then reads one int32 word.
 """
 from typing import Any, Callable, List, Optional, Sequence, Tuple, Union
 
 import torch
 from torch import Tensor
 
+from torchmetrics_amd import ops as _ops
 from torchmetrics_amd.metric import Metric
 from torchmetrics_amd.utilities.data import dim_zero_cat
 from torchmetrics_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
@@ -92,6 +96,40 @@ class BaseAggregator(Metric):
             x, weight = x[keep], weight[keep]
         return x.to(self.dtype), weight.to(self.dtype)
 
+    def _fused_update(self, kind: int, value: Union[float, Tensor], weight: Union[float, Tensor, None],
+                      s1: Optional[Tensor] = None) -> bool:
+        """ROCm path: the whole update as one ``agg_update`` launch.  False when it does not apply (CPU states,
+        autograd through the value, a state dtype other than f32 / f64): the caller runs the torch path."""
+        s0 = getattr(self, self.state_name)
+        if not (isinstance(s0, Tensor) and s0.is_cuda and s0.dtype in (torch.float32, torch.float64)):
+            return False
+        if isinstance(value, Tensor):
+            if value.device != s0.device or (value.requires_grad and torch.is_grad_enabled()):
+                return False
+        else:
+            value = torch.as_tensor(value, dtype=s0.dtype, device=s0.device)
+        if value.dtype not in (torch.float32, torch.float64, torch.float16, torch.bfloat16):
+            value = value.to(s0.dtype)
+        if isinstance(weight, Tensor):
+            if weight.device != s0.device or (weight.requires_grad and torch.is_grad_enabled()):
+                return False
+            if weight.numel() != 1:
+                weight = torch.broadcast_to(weight, value.shape)
+            if weight.dtype not in (torch.float32, torch.float64, torch.float16, torch.bfloat16):
+                weight = weight.to(s0.dtype)
+        if value.numel() == 0:
+            return True
+        strategy = self.nan_strategy
+        if isinstance(strategy, float):
+            mode, impute = _ops.AGG_NAN_IMPUTE, strategy
+        else:
+            mode, impute = (_ops.AGG_NAN_ERROR if strategy == "error" else _ops.AGG_NAN_IGNORE), 0.0
+        flag = self._device_error_buffer(s0.device)
+        ctl = _ops.agg_update(value, weight, kind, mode, impute, self.__dict__, s0, s1, flag)
+        if strategy == "warn" and int(ctl[1].item()):
+            rank_zero_warn("Encountered `nan` values in tensor. Will be removed.", UserWarning)
+        return True
+
     def update(self, value: Union[float, Tensor]) -> None:
         """Overridden by subclasses."""
 
@@ -114,6 +152,8 @@ class MaxMetric(BaseAggregator):
                          state_name="max_value", **kwargs)
 
     def update(self, value: Union[float, Tensor]) -> None:
+        if self._fused_update(_ops.AGG_MAX, value, None):
+            return
         value, _ = self._cast_and_nan_check_input(value, drop=False)
         if value.numel():
             self.max_value = torch.max(self.max_value, torch.max(value))
@@ -131,6 +171,8 @@ class MinMetric(BaseAggregator):
                          state_name="min_value", **kwargs)
 
     def update(self, value: Union[float, Tensor]) -> None:
+        if self._fused_update(_ops.AGG_MIN, value, None):
+            return
         value, _ = self._cast_and_nan_check_input(value, drop=False)
         if value.numel():
             self.min_value = torch.min(self.min_value, torch.min(value))
@@ -146,6 +188,8 @@ class SumMetric(BaseAggregator):
                          state_name="sum_value", **kwargs)
 
     def update(self, value: Union[float, Tensor]) -> None:
+        if self._fused_update(_ops.AGG_SUM, value, None):
+            return
         value, _ = self._cast_and_nan_check_input(value, drop=False)
         if value.numel():
             self.sum_value += value.sum()
@@ -183,6 +227,8 @@ class MeanMetric(BaseAggregator):
         self.add_state("weight", default=torch.tensor(0.0, dtype=torch.get_default_dtype()), dist_reduce_fx="sum")
 
     def update(self, value: Union[float, Tensor], weight: Union[float, Tensor] = 1.0) -> None:
+        if self._fused_update(_ops.AGG_MEAN, value, weight, self.weight):
+            return
         if not isinstance(value, Tensor):
             value = torch.as_tensor(value, dtype=self.dtype, device=self.device)
         if weight is not None and not isinstance(weight, Tensor):

@@ -8,6 +8,7 @@ import torch
 from torch import Tensor
 from typing_extensions import Literal
 
+from torchmetrics_amd import ops
 from torchmetrics_amd.functional.classification.precision_recall_curve import _prob_or
 from torchmetrics_amd.functional.classification.stat_scores import (
     _multiclass_stat_scores_arg_validation,
@@ -21,6 +22,57 @@ from torchmetrics_amd.utilities.enums import ClassificationTaskNoBinary
 
 def _exact_match_reduce(correct: Tensor, total: Tensor) -> Tensor:
     return _safe_divide(correct, total)
+
+
+_EM_FLOAT = (torch.float32, torch.float16, torch.bfloat16, torch.float64)
+
+
+def _exact_match_fused(
+    preds: Tensor,
+    target: Tensor,
+    multilabel: bool,
+    num: int,
+    threshold: float,
+    multidim_average: str,
+    ignore_index: Optional[int],
+    owner: dict,
+    correct: Optional[Tensor] = None,
+    total: Optional[Tensor] = None,
+) -> Optional[Tuple[Tensor, Tensor]]:
+    """ROCm path (``csrc/classification/exact_match.hip``) on the unformatted inputs: argmax / sigmoid-or-not /
+    threshold / ignore / all-positions vote in one pass.  Global with ``correct`` / ``total`` given: the states are
+    updated in place.  Returns ``(correct, total)`` as the torch update would, or None when it does not apply (CPU
+    tensors, float multiclass labels)."""
+    if not (preds.is_cuda and target.is_cuda and preds.device == target.device) or target.ndim < 1:
+        return None
+    n = target.shape[0]
+    samplewise = multidim_average == "samplewise"
+    if multilabel:
+        if preds.shape != target.shape or preds.ndim < 2:
+            return None
+        kind, c, p = ops.EM_MULTILABEL, preds.shape[1], target[0].numel() // max(preds.shape[1], 1)
+        total_val = (n * p) if not samplewise else p
+    elif preds.ndim == target.ndim + 1 and preds.dtype in _EM_FLOAT:
+        kind, c, p = ops.EM_MULTICLASS, preds.shape[1], target[0].numel()
+        total_val = n if not samplewise else 1
+    elif preds.ndim == target.ndim and preds.dtype not in _EM_FLOAT:
+        kind, c, p = ops.EM_MULTILABEL, target[0].numel(), 1  # integer labels: all positions of a sample equal
+        total_val = n if not samplewise else 1
+    else:
+        return None
+    if n == 0 or c == 0 or p == 0:
+        return None
+    preds, target = preds.contiguous(), target.contiguous()
+    if target.dtype not in (torch.int64, torch.int32, torch.uint8, torch.bool):
+        target = target.long()
+    if samplewise:
+        out = ops.exact_match_update(preds, target, kind, c, p, threshold, ignore_index, True, owner)
+        return out, torch.tensor(total_val, device=preds.device)
+    if correct is None:
+        correct = torch.zeros(1, dtype=torch.int64, device=preds.device)
+        total = torch.zeros(1, dtype=torch.int64, device=preds.device)
+    ops.exact_match_update(preds, target, kind, c, p, threshold, ignore_index, False, owner, correct, total)
+    return correct, total
 
 
 def _multiclass_exact_match_format(preds: Tensor, target: Tensor) -> Tuple[Tensor, Tensor]:
@@ -55,6 +107,10 @@ def multiclass_exact_match(
     if validate_args:
         _multiclass_stat_scores_arg_validation(num_classes, 1, None, multidim_average, ignore_index)
         _multiclass_stat_scores_tensor_validation(preds, target, num_classes, multidim_average, ignore_index)
+    fused = _exact_match_fused(preds, target, False, num_classes, 0.5, multidim_average, ignore_index, {})
+    if fused is not None:
+        correct, total = fused
+        return _exact_match_reduce(correct, total) if total.ndim == 0 else _exact_match_reduce(correct[0], total[0])
     preds, target = _multiclass_exact_match_format(preds, target)
     correct, total = _multiclass_exact_match_update(preds, target, multidim_average, ignore_index)
     return _exact_match_reduce(correct, total)
@@ -100,6 +156,10 @@ def multilabel_exact_match(
     if validate_args:
         _multilabel_stat_scores_arg_validation(num_labels, threshold, None, multidim_average, ignore_index)
         _multilabel_stat_scores_tensor_validation(preds, target, num_labels, multidim_average, ignore_index)
+    fused = _exact_match_fused(preds, target, True, num_labels, threshold, multidim_average, ignore_index, {})
+    if fused is not None:
+        correct, total = fused
+        return _exact_match_reduce(correct, total) if total.ndim == 0 else _exact_match_reduce(correct[0], total[0])
     preds, target = _multilabel_exact_match_format(preds, target, num_labels, threshold, ignore_index)
     correct, total = _multilabel_exact_match_update(preds, target, num_labels, multidim_average)
     return _exact_match_reduce(correct, total)

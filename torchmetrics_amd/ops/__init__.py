@@ -1147,6 +1147,64 @@ def inception_score(logits: Tensor, perm: Tensor, splits: int) -> Tensor:
     return out
 
 
+EM_MULTICLASS, EM_MULTILABEL = 0, 1
+
+
+def exact_match_update(preds: Tensor, target: Tensor, kind: int, C: int, P: int, threshold: float,
+                       ignore_index: Optional[int], samplewise: bool, owner: dict,
+                       correct: Optional[Tensor] = None, total: Optional[Tensor] = None) -> Optional[Tensor]:
+    """Exact-match update of contiguous ROCm inputs (``csrc/classification/exact_match.hip``).  ``kind``
+    EM_MULTICLASS: preds ``[N, C, P]`` scores, target ``[N, P]``; EM_MULTILABEL: preds / target ``[N, C, P]``
+    (integer multiclass labels: ``C`` = positions, ``P`` = 1).  Global: ``correct`` / ``total`` int64 ``[1]`` states
+    are updated in place, returns None.  Samplewise: returns the int64 ``[N]`` per-sample counts."""
+    n = target.numel() // (P if kind == EM_MULTICLASS else C * P) if P and C else 0
+    ws = owner.get("_em_ws")
+    need = max(2, 2 * n)
+    if ws is None or ws[0].numel() < need or ws[0].device != preds.device:
+        ws = owner["_em_ws"] = (torch.zeros(need, dtype=torch.int64, device=preds.device),
+                                torch.zeros(1, dtype=torch.int32, device=preds.device))
+    out = torch.empty(n if samplewise else 0, dtype=torch.int64, device=preds.device)
+    if correct is None:
+        correct = total = ws[0]  # unused by the samplewise fold
+    _ops().exact_match_update(preds, target, int(kind), int(C), int(P), kind == EM_MULTICLASS, float(threshold),
+                              0 if ignore_index is None else int(ignore_index), ignore_index is not None,
+                              bool(samplewise), ws[0], ws[1], correct, total, out)
+    return out if samplewise else None
+
+
+AGG_SUM, AGG_MEAN, AGG_MAX, AGG_MIN = 0, 1, 2, 3
+AGG_NAN_ERROR, AGG_NAN_IGNORE, AGG_NAN_IMPUTE = 0, 1, 2
+
+
+def agg_update(x: Tensor, weight: Union[Tensor, float, None], kind: int, nan_mode: int, impute: float, owner: dict,
+               s0: Tensor, s1: Optional[Tensor], flag: Tensor) -> Tensor:
+    """One-launch aggregator update (``csrc/common/aggregate.hip``): NaN strategy, sum(x*w) / sum(w) / max / min
+    in fp64 and the in-place state fold.  ``weight``: a python number (kernel argument), or a ROCm tensor of 1 or
+    ``x.numel()`` elements.  Returns the int32 ``[2]`` control word whose element 1 holds this call's NaN count."""
+    ws = owner.get("_agg_ws")
+    if ws is None or ws[0].device != x.device:
+        ws = owner["_agg_ws"] = (torch.empty(5 * 512, dtype=torch.float64, device=x.device),
+                                 torch.zeros(2, dtype=torch.int32, device=x.device))
+    if isinstance(weight, Tensor):
+        w, wconst = weight.reshape(-1).contiguous(), 1.0
+    else:
+        w = _EMPTY_F32.get(x.device)
+        if w is None:
+            w = _empty_f32(x.device)
+        wconst = 1.0 if weight is None else float(weight)
+    _ops().agg_update(x.reshape(-1).contiguous(), w, wconst, int(kind), int(nan_mode), float(impute), ws[0], ws[1],
+                      s0, s0 if s1 is None else s1, flag)
+    return ws[1]
+
+
+_EMPTY_F32: dict = {}
+
+
+def _empty_f32(device: torch.device) -> Tensor:
+    t = _EMPTY_F32[device] = torch.empty(0, dtype=torch.float32, device=device)
+    return t
+
+
 HINGE_BINARY, HINGE_CRAMMER_SINGER, HINGE_ONE_VS_ALL = 0, 1, 2
 
 

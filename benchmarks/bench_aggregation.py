@@ -1,6 +1,8 @@
-"""Aggregator updates: the one-launch ``agg_update`` kernel (``csrc/common/aggregate.hip``) vs the reference's op
+"""Aggregator and exact-match updates: the one-launch ``agg_update`` kernel (``csrc/common/aggregate.hip``) vs the reference's op
 chain (``S/aggregation.py:75-105`` + ``MeanMetric.update`` ``:550-575``: as_tensor weight, broadcast, isnan x2,
 ``nans.any()`` host check, cast, ``(x * w).sum()``, ``w.sum()``, in-place adds), same inputs, same process.
+Exact match (``csrc/classification/exact_match.hip``) vs the reference's chain (``F/classification/exact_match.py``:
+argmax / ``_prob_or`` host check + sigmoid + threshold, ``==``, ``.sum(1) == L``, ``.sum()``).
 One JSON line per case: ours_us / reference_us per update (wall clock over a loop of updates, then one sync)."""
 import json
 import os
@@ -65,6 +67,42 @@ def main():
         m = cls(nan_strategy="ignore").to(dev)
         t = loop_us(m.update, xs, 200)
         print(json.dumps({"case": f"{name}(nan_strategy='ignore').update 4096", "ours_us": round(t, 2)}), flush=True)
+    exact_match_cases(dev, g)
+
+
+def ref_multiclass_em(state, preds, target):
+    p = preds.argmax(1).reshape(preds.shape[0], -1)
+    t = target.reshape(target.shape[0], -1)
+    state[0] += ((p == t).sum(1) == p.shape[1]).sum()
+    state[1] += p.shape[0]
+
+
+def ref_multilabel_em(state, preds, target, threshold=0.5):
+    if not torch.all((preds >= 0) * (preds <= 1)):  # host sync, as the reference's _prob_or check
+        preds = preds.sigmoid()
+    p = (preds > threshold).long()
+    state[0] += ((p == target).sum(1) == p.shape[1]).sum()
+    state[1] += p.shape[0]
+
+
+def exact_match_cases(dev, g):
+    for label, c, dtype in (("65536x1000 bf16", 1000, torch.bfloat16), ("65536x10 f32", 10, torch.float32)):
+        xs = [(torch.randn(65536, c, device=dev, generator=g).to(dtype),
+               torch.randint(0, c, (65536,), device=dev, generator=g)) for _ in range(4)]
+        m = tm.MulticlassExactMatch(c).to(dev)
+        t_ours = loop_us(lambda a: m.update(*a), xs, 100)
+        st = [torch.zeros((), dtype=torch.long, device=dev), torch.zeros((), dtype=torch.long, device=dev)]
+        t_ref = loop_us(lambda a: ref_multiclass_em(st, *a), xs, 100)
+        print(json.dumps({"case": f"MulticlassExactMatch.update {label}", "ours_us": round(t_ours, 2),
+                          "reference_us": round(t_ref, 2), "speedup": round(t_ref / t_ours, 2)}), flush=True)
+    xs = [(torch.randn(65536, 64, device=dev, generator=g), torch.randint(0, 2, (65536, 64), device=dev, generator=g))
+          for _ in range(4)]
+    m = tm.MultilabelExactMatch(64).to(dev)
+    t_ours = loop_us(lambda a: m.update(*a), xs, 100)
+    st = [torch.zeros((), dtype=torch.long, device=dev), torch.zeros((), dtype=torch.long, device=dev)]
+    t_ref = loop_us(lambda a: ref_multilabel_em(st, *a), xs, 100)
+    print(json.dumps({"case": "MultilabelExactMatch.update 65536x64 logits", "ours_us": round(t_ours, 2),
+                      "reference_us": round(t_ref, 2), "speedup": round(t_ref / t_ours, 2)}), flush=True)
 
 
 if __name__ == "__main__":

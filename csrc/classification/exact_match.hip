@@ -5,13 +5,15 @@
 // to decide whether the scores are probabilities (`_prob_or`), a sigmoid copy, a threshold copy, two masked fills,
 // `movedim(1, -1).reshape(-1, L)` (a transposed copy for multi-dim inputs), `== target`, `.sum(1) == L`, `.sum()`.
 // Here one pass decides each unit directly from the scores:
-//   * multiclass, P == 1: one wave per sample, lanes over the C scores (wave argmax, torch.argmax tie / NaN rules);
+//   * multiclass, P == 1: G = 8..64 lanes per sample over the C scores (group argmax, torch.argmax tie / NaN rules;
+//     small C packs several samples into a wave);
 //   * multiclass, P > 1: one wave per sample, lanes over the P positions (coalesced over the [N, C, P] layout), each
 //     lane a sequential argmax over C; a wave vote ANDs the positions;
 //   * multilabel: one thread per (sample, position) unit looping over the L labels, judging BOTH readings of float
 //     scores (as given / sigmoid in the scores' dtype) and OR-ing a "not a probability" word; the fold keeps the
 //     reading the batch calls for (the reference's global `_prob_or` decision) without a host round trip.
-// Counts are int64 atomics (order independent, deterministic).  The fold adds the global count and total into the
+// Counts are reduced per block and added with one int64 atomic per block (order independent, deterministic; a
+// per-wave atomic on one address serialised the first version at ~70 us per 65536-row batch).  The fold adds the global count and total into the
 // metric states in place, or writes the per-sample counts (samplewise), and re-zeroes the workspace.
 #include "common/tm_common.h"
 
@@ -20,37 +22,75 @@ namespace {
 
 constexpr int kBlock = 256;
 
-// multiclass, P == 1: preds [N, C] (float scores) or [N] labels; ws: i64 [1] (global) or [N] (samplewise)
-template <typename scalar_t, typename target_t>
+// one int64 atomic per block for a per-thread count pair (every thread of the block must call it)
+__device__ __forceinline__ void block_add_counts(long long a, long long b, int64_t* __restrict__ dst_a,
+                                                 int64_t* __restrict__ dst_b) {
+  __shared__ long long red[2][kBlock / kWave];
+  a = wave_sum_ll(a);
+  b = wave_sum_ll(b);
+  const int w = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+    red[0][w] = a;
+    red[1][w] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long sa = 0, sb = 0;
+    for (int k = 0; k < kBlock / kWave; ++k) {
+      sa += red[0][k];
+      sb += red[1][k];
+    }
+    if (sa) atomic_add_i64(dst_a, sa);
+    if (sb && dst_b) atomic_add_i64(dst_b, sb);
+  }
+}
+
+// multiclass, P == 1: preds [N, C] scores, G lanes per row (G = 8 / 16 / 32 / 64 from C: small C packs several rows
+// into a wave), 4 loads in flight per lane; ws: i64 [1] (global) or [N] (samplewise)
+template <typename scalar_t, typename target_t, int G>
 __global__ void __launch_bounds__(kBlock) em_multiclass_row_kernel(const scalar_t* __restrict__ preds,
                                                                    const target_t* __restrict__ target, long long N,
                                                                    int C, long long ignore, bool has_ignore,
                                                                    bool samplewise, int64_t* __restrict__ ws) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const long long nw = static_cast<long long>(gridDim.x) * (kBlock / kWave);
+  constexpr int kRows = kBlock / G;
+  const int sub = threadIdx.x % G;
   long long local = 0;
-  for (long long n = (static_cast<long long>(blockIdx.x) * kBlock + threadIdx.x) / kWave; n < N; n += nw) {
-    const long long t = static_cast<long long>(target[n]);
+  for (long long base = static_cast<long long>(blockIdx.x) * kRows; base < N;
+       base += static_cast<long long>(gridDim.x) * kRows) {
+    const long long n = base + threadIdx.x / G;
     float bv = -INFINITY;
     int bi = 0x7fffffff;
-    const scalar_t* r = preds + n * C;
-    for (int c = lane; c < C; c += kWave) {
-      const float v = to_f32(r[c]);
-      if (argmax_better(v, c, bv, bi)) {
-        bv = v;
-        bi = c;
+    if (n < N) {
+      const scalar_t* r = preds + n * C;
+      int c = sub;
+      for (; c + 3 * G < C; c += 4 * G) {
+        const float v0 = to_f32(r[c]), v1 = to_f32(r[c + G]), v2 = to_f32(r[c + 2 * G]), v3 = to_f32(r[c + 3 * G]);
+        if (argmax_better(v0, c, bv, bi)) bv = v0, bi = c;
+        if (argmax_better(v1, c + G, bv, bi)) bv = v1, bi = c + G;
+        if (argmax_better(v2, c + 2 * G, bv, bi)) bv = v2, bi = c + 2 * G;
+        if (argmax_better(v3, c + 3 * G, bv, bi)) bv = v3, bi = c + 3 * G;
+      }
+      for (; c < C; c += G) {
+        const float v = to_f32(r[c]);
+        if (argmax_better(v, c, bv, bi)) bv = v, bi = c;
       }
     }
-    wave_argmax(bv, bi);
-    const bool ok = (has_ignore && t == ignore) || static_cast<long long>(bi) == t;
-    if (lane == 0) {
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) {
+      const float ov = __shfl_xor(bv, off, kWave);
+      const int oi = __shfl_xor(bi, off, kWave);
+      if (argmax_better(ov, oi, bv, bi)) bv = ov, bi = oi;
+    }
+    if (n < N && sub == 0) {
+      const long long t = static_cast<long long>(target[n]);
+      const bool ok = (has_ignore && t == ignore) || static_cast<long long>(bi) == t;
       if (samplewise)
         ws[n] = ok ? 1 : 0;
       else
         local += ok ? 1 : 0;
     }
   }
-  if (!samplewise && lane == 0 && local) atomic_add_i64(ws, local);
+  if (!samplewise) block_add_counts(local, 0, ws, nullptr);
 }
 
 // multiclass, P > 1: preds [N, C, P] scores; target [N, P]
@@ -89,7 +129,7 @@ __global__ void __launch_bounds__(kBlock) em_multiclass_pos_kernel(const scalar_
         local += ok ? 1 : 0;
     }
   }
-  if (!samplewise && lane == 0 && local) atomic_add_i64(ws, local);
+  if (!samplewise) block_add_counts(local, 0, ws, nullptr);
 }
 
 // multilabel: preds / target [N, L, P]; unit u = (n, p); ws: i64 [2] (global: reading A, B) or [2N] (samplewise:
@@ -135,14 +175,7 @@ __global__ void __launch_bounds__(kBlock) em_multilabel_kernel(const scalar_t* _
     }
   }
   if (__any(np) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(notprob, 1);
-  if (!samplewise) {
-    ca = wave_sum_ll(ca);
-    cb = wave_sum_ll(cb);
-    if ((threadIdx.x & (kWave - 1)) == 0) {
-      if (ca) atomic_add_i64(ws, ca);
-      if (cb) atomic_add_i64(ws + 1, cb);
-    }
-  }
+  if (!samplewise) block_add_counts(ca, cb, ws, ws + 1);
 }
 
 // global: correct += (notprob ? ws[1] : ws[0]); total += total_add.  samplewise: out[n] = ws[(notprob ? N : 0) + n].
@@ -212,17 +245,28 @@ void exact_match_update(const at::Tensor& preds, const at::Tensor& target, int64
         if constexpr (std::is_same<scalar_t, c10::BFloat16>::value) thr = static_cast<float>(c10::BFloat16(thr));
         if constexpr (std::is_same<scalar_t, c10::Half>::value) thr = static_cast<float>(c10::Half(thr));
         if (kind == 0 && P == 1) {
-          hipLaunchKernelGGL((em_multiclass_row_kernel<scalar_t, target_t>),
-                             dim3(grid_cap((N + (kBlock / kWave) - 1) / (kBlock / kWave), 4096)), dim3(kBlock), 0,
-                             s, p, t, N, static_cast<int>(C), ig, has_ignore, samplewise, w);
+          auto row = [&](auto g) {
+            constexpr int G = decltype(g)::value;
+            hipLaunchKernelGGL((em_multiclass_row_kernel<scalar_t, target_t, G>),
+                               dim3(grid_cap((N + kBlock / G - 1) / (kBlock / G), 1024)), dim3(kBlock), 0, s, p, t, N,
+                               static_cast<int>(C), ig, has_ignore, samplewise, w);
+          };
+          if (C <= 8)
+            row(std::integral_constant<int, 8>{});
+          else if (C <= 16)
+            row(std::integral_constant<int, 16>{});
+          else if (C <= 32)
+            row(std::integral_constant<int, 32>{});
+          else
+            row(std::integral_constant<int, 64>{});
         } else if (kind == 0) {
           hipLaunchKernelGGL((em_multiclass_pos_kernel<scalar_t, target_t>),
-                             dim3(grid_cap((N + (kBlock / kWave) - 1) / (kBlock / kWave), 4096)), dim3(kBlock), 0,
+                             dim3(grid_cap((N + (kBlock / kWave) - 1) / (kBlock / kWave), 2048)), dim3(kBlock), 0,
                              s, p, t, N, static_cast<int>(C), static_cast<long long>(P), ig, has_ignore,
                              samplewise, w);
         } else {
           hipLaunchKernelGGL((em_multilabel_kernel<scalar_t, target_t>),
-                             dim3(grid_cap((N * P + kBlock - 1) / kBlock, 4096)), dim3(kBlock), 0, s, p, t, N,
+                             dim3(grid_cap((N * P + kBlock - 1) / kBlock, 2048)), dim3(kBlock), 0, s, p, t, N,
                              static_cast<int>(C), static_cast<long long>(P), thr, ig,
                              has_ignore, samplewise, w, notprob.data_ptr<int>());
         }

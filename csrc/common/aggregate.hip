@@ -5,7 +5,8 @@
 // ones_like(x) for the weights, then `(x * w).sum()` / `w.sum()` / `max()` / `min()` and the state add: ~8-10
 // launches and two host round trips per update, for what is usually a single loss scalar.
 // Here one grid-stride pass applies the nan strategy per element (error: validation bit; ignore / warn: the element
-// drops out; float: x and w imputed, as the reference does) and reduces sum(x*w), sum(w), max and min in fp64; the
+// drops out, and 'warn' raises a warning bit that compute() turns into the reference's UserWarning -- no per-update
+// host sync; float: x and w imputed, as the reference does) and reduces sum(x*w), sum(w), max and min in fp64; the
 // last block to finish (ticket counter) folds the per-block partials in a fixed order -- deterministic whatever the
 // block completion order -- and adds the result into the metric's state tensors in place.  A python-number weight
 // is a kernel argument (no H2D copy of a ones tensor); a tensor weight may be one element (broadcast) or N.
@@ -15,9 +16,9 @@ namespace tm_amd {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kMaxBlocks = 512;
+constexpr int kMaxBlocks = 2048;
 enum Kind : int { kSum = 0, kMean = 1, kMax = 2, kMin = 3 };
-enum NanMode : int { kNanError = 0, kNanIgnore = 1, kNanImpute = 2 };
+enum NanMode : int { kNanError = 0, kNanIgnore = 1, kNanImpute = 2, kNanWarn = 3 };
 
 template <typename T>
 __device__ __forceinline__ double to_f64(T v) {
@@ -32,7 +33,9 @@ __device__ __forceinline__ double nan_max(double a, double b) { return (a != a |
 __device__ __forceinline__ double nan_min(double a, double b) { return (a != a || a < b) ? a : b; }
 
 // part: f64 [kMaxBlocks][5] (sum x*w, sum w, max, min, NaN count); ctl: i32 [2] = {ticket, NaN count of the last call}
-template <typename x_t, typename w_t, typename out_t>
+// WMODE: 0 python-number weight (wconst), 1 one-element weight tensor, 2 one weight per element -- a template
+// parameter so the unrolled loop below issues its loads back to back (a runtime select split them with waits)
+template <typename x_t, typename w_t, typename out_t, int WMODE>
 __global__ void __launch_bounds__(kBlock) agg_update_kernel(const x_t* __restrict__ x, const w_t* __restrict__ w,
                                                             long long N, long long w_n, double wconst, int kind,
                                                             int nan_mode, double impute, double* __restrict__ part,
@@ -43,24 +46,40 @@ __global__ void __launch_bounds__(kBlock) agg_update_kernel(const x_t* __restric
   __shared__ bool last;
   double s = 0.0, sw = 0.0, mx = -INFINITY, mn = INFINITY;
   int nan = 0;
-  for (long long i = static_cast<long long>(blockIdx.x) * kBlock + threadIdx.x; i < N;
-       i += static_cast<long long>(gridDim.x) * kBlock) {
-    double xv = to_f64(x[i]);
-    double wv = w_n == 0 ? wconst : to_f64(w[w_n == 1 ? 0 : i]);
-    if (xv != xv || wv != wv) {
-      ++nan;
-      if (nan_mode == kNanImpute) {
-        xv = impute;
-        wv = impute;
-      } else {
-        continue;  // ignore / warn drop the element; error only raises the bit (the state is not used afterwards)
-      }
+  const bool impute_nan = nan_mode == kNanImpute;
+  // branch-free element step: ignore / warn / error drop a NaN element (error only raises the bit), impute replaces
+  auto step = [&](double xv, double wv) {
+    const bool isn = xv != xv || wv != wv;
+    nan += isn;
+    if (impute_nan) {
+      xv = isn ? impute : xv;
+      wv = isn ? impute : wv;
     }
-    s += xv * wv;
-    sw += wv;
-    mx = nan_max(mx, xv);
-    mn = nan_min(mn, xv);
+    const bool keep = impute_nan || !isn;
+    s += keep ? xv * wv : 0.0;
+    sw += keep ? wv : 0.0;
+    mx = keep ? nan_max(mx, xv) : mx;
+    mn = keep ? nan_min(mn, xv) : mn;
+  };
+  const long long stride = static_cast<long long>(gridDim.x) * kBlock;
+  long long i = static_cast<long long>(blockIdx.x) * kBlock + threadIdx.x;
+  // 4 independent loads in flight per thread before any use (the loop is latency-bound, not ALU-bound)
+  const double wfix = WMODE == 0 ? wconst : (WMODE == 1 ? to_f64(w[0]) : 0.0);
+  for (; i + 3 * stride < N; i += 4 * stride) {
+    double xv[4], wv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xv[k] = to_f64(x[i + k * stride]);
+    if constexpr (WMODE == 2) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wv[k] = to_f64(w[i + k * stride]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wv[k] = wfix;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) step(xv[k], wv[k]);
   }
+  for (; i < N; i += stride) step(to_f64(x[i]), WMODE == 2 ? to_f64(w[i]) : wfix);
   s = wave_sum(s);
   sw = wave_sum(sw);
   nan = static_cast<int>(wave_sum_ll(nan));
@@ -137,6 +156,7 @@ __global__ void __launch_bounds__(kBlock) agg_update_kernel(const x_t* __restric
     nan_total += red_nan[k];
   }
   if (nan_mode == kNanError && nan_total) raise_flag(flag, kErrValueNan);
+  if (nan_mode == kNanWarn && nan_total) raise_flag(flag, kErrValueNanWarn);  // warned at compute(), no sync here
   switch (kind) {
     case kSum:
       *s0 = static_cast<out_t>(static_cast<double>(*s0) + red[0][0]);
@@ -161,7 +181,7 @@ __global__ void __launch_bounds__(kBlock) agg_update_kernel(const x_t* __restric
 }  // namespace
 
 // x: ROCm float tensor [N] (contiguous); w: empty (use wconst), [1] or [N] float; kind 0 sum / 1 mean / 2 max /
-// 3 min; nan_mode 0 error / 1 ignore (and warn) / 2 impute; part: f64 [>= 5 * 512]; ctl: i32 [2] (ctl[0] == 0 on
+// 3 min; nan_mode 0 error / 1 ignore / 2 impute / 3 warn (ignore + warning bit); part: f64 [>= 5 * 2048]; ctl: i32 [2] (ctl[0] == 0 on
 // entry); s0 (and s1 for mean): f32 / f64 0-d state tensors updated in place; flag: i32 validation word.
 void agg_update(const at::Tensor& x, const at::Tensor& w, double wconst, int64_t kind, int64_t nan_mode,
                 double impute, at::Tensor part, at::Tensor ctl, at::Tensor s0, at::Tensor s1, at::Tensor flag) {
@@ -170,7 +190,7 @@ void agg_update(const at::Tensor& x, const at::Tensor& w, double wconst, int64_t
     TM_SAME_DEVICE(x, (*t));
   TM_CHECK_CONTIG(x);
   TORCH_CHECK(kind >= 0 && kind <= 3, "agg_update: bad kind");
-  TORCH_CHECK(nan_mode >= 0 && nan_mode <= 2, "agg_update: bad nan_mode");
+  TORCH_CHECK(nan_mode >= 0 && nan_mode <= 3, "agg_update: bad nan_mode");
   const long long N = x.numel();
   const long long w_n = w.numel();
   TORCH_CHECK(w_n == 0 || w_n == 1 || w_n == N, "agg_update: weight must have 0, 1 or N elements");
@@ -186,7 +206,8 @@ void agg_update(const at::Tensor& x, const at::Tensor& w, double wconst, int64_t
   TORCH_CHECK(flag.scalar_type() == at::kInt && flag.numel() >= 1, "agg_update: flag");
   auto s = stream();
   if (N == 0) return;
-  const int blocks = grid_cap((N + kBlock - 1) / kBlock, std::min(kMaxBlocks, 2 * cu_count(x.get_device())));
+  // up to 4 blocks (16 waves) per CU, each thread >= 4 elements; few blocks also keep the ticket atomics cheap
+  const int blocks = grid_cap((N + 4 * kBlock - 1) / (4 * kBlock), std::min(kMaxBlocks, 4 * cu_count(x.get_device())));
   TM_DISPATCH_FLOAT(x.scalar_type(), "agg_update", [&] {
     using x_t = scalar_t;
     const at::ScalarType wt = w_n ? w.scalar_type() : x.scalar_type();
@@ -194,16 +215,25 @@ void agg_update(const at::Tensor& x, const at::Tensor& w, double wconst, int64_t
       using w_t = scalar_t;
       const w_t* wp = w_n ? reinterpret_cast<const w_t*>(w.data_ptr()) : nullptr;
       const x_t* xp = reinterpret_cast<const x_t*>(x.data_ptr());
+      auto launch = [&](auto out_tag, auto wmode) {
+        using out_t = decltype(out_tag);
+        hipLaunchKernelGGL((agg_update_kernel<x_t, w_t, out_t, decltype(wmode)::value>), dim3(blocks), dim3(kBlock), 0,
+                           s, xp, wp, N, w_n, wconst, static_cast<int>(kind), static_cast<int>(nan_mode), impute,
+                           part.data_ptr<double>(), ctl.data_ptr<int>(), reinterpret_cast<out_t*>(s0.data_ptr()),
+                           reinterpret_cast<out_t*>(s1.data_ptr()), flag.data_ptr<int>());
+      };
+      auto by_w = [&](auto out_tag) {
+        if (w_n == 0)
+          launch(out_tag, std::integral_constant<int, 0>{});
+        else if (w_n == 1)
+          launch(out_tag, std::integral_constant<int, 1>{});
+        else
+          launch(out_tag, std::integral_constant<int, 2>{});
+      };
       if (s0.scalar_type() == at::kFloat)
-        hipLaunchKernelGGL((agg_update_kernel<x_t, w_t, float>), dim3(blocks), dim3(kBlock), 0, s, xp, wp, N, w_n,
-                           wconst, static_cast<int>(kind), static_cast<int>(nan_mode), impute,
-                           part.data_ptr<double>(), ctl.data_ptr<int>(), s0.data_ptr<float>(), s1.data_ptr<float>(),
-                           flag.data_ptr<int>());
+        by_w(float{});
       else
-        hipLaunchKernelGGL((agg_update_kernel<x_t, w_t, double>), dim3(blocks), dim3(kBlock), 0, s, xp, wp, N, w_n,
-                           wconst, static_cast<int>(kind), static_cast<int>(nan_mode), impute,
-                           part.data_ptr<double>(), ctl.data_ptr<int>(), s0.data_ptr<double>(),
-                           s1.data_ptr<double>(), flag.data_ptr<int>());
+        by_w(double{});
     });
   });
   C10_HIP_KERNEL_LAUNCH_CHECK();

@@ -33,6 +33,7 @@ constexpr int kErrPredsNotBinary = 1 << 3;
 constexpr int kErrPredsNan = 1 << 4;
 constexpr int kErrValueNan = 1 << 5;
 constexpr int kErrNegValue = 1 << 6;
+constexpr int kErrValueNanWarn = 1 << 7;  // not an error: compute() emits the 'warn' nan_strategy UserWarning
 
 // ------------------------------------------------------------------------------------------------ type helpers
 template <typename T>

@@ -5,10 +5,12 @@ NaN handling (``nan_strategy``) keeps the reference semantics, but on GPU tensor
 
 * ``'error'``  -> a device-side flag (raised at ``compute()``, or per update with ``TORCHMETRICS_AMD_STRICT=1``);
 * ``'ignore'`` / float -> NaNs are masked to the aggregator's neutral element / imputed in place, no sync;
-* ``'warn'``   -> needs the host to decide whether to warn, so it syncs (as the reference does).
+* ``'warn'``   -> CPU: warns in ``update`` (a host check, as the reference).  ROCm: the NaNs are dropped on the device
+  and a warning bit is raised in the validation word; the reference's UserWarning is emitted by the next
+  ``compute()`` (``forward`` included), so the per-update host sync is gone.
 
 On ROCm, Sum / Mean / Max / Min updates are one launch of ``csrc/common/aggregate.hip`` (NaN strategy, fp64
-reduction and the in-place state fold together); ``'warn'`` then reads one int32 word.
+reduction and the in-place state fold together).
 """
 from typing import Any, Callable, List, Optional, Sequence, Tuple, Union
 
@@ -123,11 +125,9 @@ class BaseAggregator(Metric):
         if isinstance(strategy, float):
             mode, impute = _ops.AGG_NAN_IMPUTE, strategy
         else:
-            mode, impute = (_ops.AGG_NAN_ERROR if strategy == "error" else _ops.AGG_NAN_IGNORE), 0.0
-        flag = self._device_error_buffer(s0.device)
-        ctl = _ops.agg_update(value, weight, kind, mode, impute, self.__dict__, s0, s1, flag)
-        if strategy == "warn" and int(ctl[1].item()):
-            rank_zero_warn("Encountered `nan` values in tensor. Will be removed.", UserWarning)
+            modes = {"error": _ops.AGG_NAN_ERROR, "warn": _ops.AGG_NAN_WARN}
+            mode, impute = modes.get(strategy, _ops.AGG_NAN_IGNORE), 0.0
+        _ops.agg_update(value, weight, kind, mode, impute, self.__dict__, s0, s1, self._device_error_buffer(s0.device))
         return True
 
     def update(self, value: Union[float, Tensor]) -> None:

@@ -1165,7 +1165,7 @@ def exact_match_update(preds: Tensor, target: Tensor, kind: int, C: int, P: int,
                                 torch.zeros(1, dtype=torch.int32, device=preds.device))
     out = torch.empty(n if samplewise else 0, dtype=torch.int64, device=preds.device)
     if correct is None:
-        correct = total = ws[0]  # unused by the samplewise fold
+        correct = total = ws[0][:1]  # unused by the samplewise fold
     _ops().exact_match_update(preds, target, int(kind), int(C), int(P), kind == EM_MULTICLASS, float(threshold),
                               0 if ignore_index is None else int(ignore_index), ignore_index is not None,
                               bool(samplewise), ws[0], ws[1], correct, total, out)
@@ -1173,7 +1173,7 @@ def exact_match_update(preds: Tensor, target: Tensor, kind: int, C: int, P: int,
 
 
 AGG_SUM, AGG_MEAN, AGG_MAX, AGG_MIN = 0, 1, 2, 3
-AGG_NAN_ERROR, AGG_NAN_IGNORE, AGG_NAN_IMPUTE = 0, 1, 2
+AGG_NAN_ERROR, AGG_NAN_IGNORE, AGG_NAN_IMPUTE, AGG_NAN_WARN = 0, 1, 2, 3
 
 
 def agg_update(x: Tensor, weight: Union[Tensor, float, None], kind: int, nan_mode: int, impute: float, owner: dict,
@@ -1183,7 +1183,7 @@ def agg_update(x: Tensor, weight: Union[Tensor, float, None], kind: int, nan_mod
     ``x.numel()`` elements.  Returns the int32 ``[2]`` control word whose element 1 holds this call's NaN count."""
     ws = owner.get("_agg_ws")
     if ws is None or ws[0].device != x.device:
-        ws = owner["_agg_ws"] = (torch.empty(5 * 512, dtype=torch.float64, device=x.device),
+        ws = owner["_agg_ws"] = (torch.empty(5 * 2048, dtype=torch.float64, device=x.device),
                                  torch.zeros(2, dtype=torch.int32, device=x.device))
     if isinstance(weight, Tensor):
         w, wconst = weight.reshape(-1).contiguous(), 1.0

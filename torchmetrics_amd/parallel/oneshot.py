@@ -52,14 +52,22 @@ class OneShotAllReduce:
         self.rank = dist.get_rank(group)
         self.device = torch.device("cuda", torch.cuda.current_device())
         dev = self.device.index
-        self._own = int(self._ops.ipc_buffer_alloc(int(self._ops.oneshot_buffer_bytes(self.slot_bytes)), dev))
-        handle = self._ops.ipc_get_handle(self._own, dev)
-        info = (socket.gethostname(), dev, os.getpid(), handle.tolist())
+        # a local failure (allocation / export) must not skip the setup collectives: every rank reaches the
+        # all_gather_object and the agreement all_reduce below, and a failed rank turns the path off for all
+        self._own = 0
+        handle = None
+        try:
+            self._own = int(self._ops.ipc_buffer_alloc(int(self._ops.oneshot_buffer_bytes(self.slot_bytes)), dev))
+            handle = self._ops.ipc_get_handle(self._own, dev).tolist()
+        except RuntimeError:
+            handle = None
+        info = (socket.gethostname(), dev, os.getpid(), handle)
         infos: list = [None] * self.world
         dist.all_gather_object(infos, info, group=group)
         same_host = all(i[0] == infos[0][0] for i in infos)
         distinct = len({i[1] for i in infos}) == self.world
-        self.usable = bool(same_host and (distinct or allow_shared_device) and self.world <= 16)
+        exported = all(i[3] is not None for i in infos)
+        self.usable = bool(same_host and exported and (distinct or allow_shared_device) and self.world <= 16)
         self._opened = []
         ptrs = []
         ok = self.usable

@@ -31,7 +31,7 @@ import torch
 import torch.distributed as dist
 from torch import Tensor
 
-from torchmetrics_amd.parallel.oneshot import get_oneshot
+from torchmetrics_amd.parallel.oneshot import DEFAULT_SLOT_BYTES, get_oneshot
 from torchmetrics_amd.utilities.data import (
     _flatten,
     dim_zero_cat,
@@ -167,7 +167,9 @@ def sync_state_dicts(
         else:
             flat = torch.cat([t.reshape(-1).to(wire) for _, t in members])
         if world > 1:
-            comm = get_oneshot(group) if (flat.is_cuda and _is_nccl(group)) else None
+            small = flat.numel() * flat.element_size() <= DEFAULT_SLOT_BYTES
+            # the communicator (IPC setup collective) is only created once a bucket small enough for it shows up
+            comm = get_oneshot(group) if (small and flat.is_cuda and _is_nccl(group)) else None
             if comm is not None and comm.supports(flat):
                 comm.all_reduce(flat, kind)  # one peer-read kernel over xGMI
                 _stats["oneshot_all_reduce"] += 1

@@ -43,6 +43,10 @@ def loop_us(fn, xs, reps):
     return 1e6 * (time.perf_counter() - t0) / reps
 
 
+def hbm_tb_s(nbytes, us):
+    return round(nbytes / (us * 1e-6) / 1e12, 2)
+
+
 def main():
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
@@ -61,7 +65,7 @@ def main():
         diff = abs(float(chk_o.compute()) - float(chk_r[0] / chk_r[1]))
         print(json.dumps({"case": f"MeanMetric.update {label}", "ours_us": round(t_ours, 2),
                           "reference_us": round(t_ref, 2), "speedup": round(t_ref / t_ours, 2),
-                          "abs_diff_vs_fp64": diff}), flush=True)
+                          "ours_effective_TB_s": hbm_tb_s(4 * n, t_ours), "abs_diff_vs_fp64": diff}), flush=True)
     xs = [torch.randn(4096, device=dev, generator=g) for _ in range(8)]
     for name, cls in (("SumMetric", tm.SumMetric), ("MaxMetric", tm.MaxMetric)):
         m = cls(nan_strategy="ignore").to(dev)
@@ -94,7 +98,9 @@ def exact_match_cases(dev, g):
         st = [torch.zeros((), dtype=torch.long, device=dev), torch.zeros((), dtype=torch.long, device=dev)]
         t_ref = loop_us(lambda a: ref_multiclass_em(st, *a), xs, 100)
         print(json.dumps({"case": f"MulticlassExactMatch.update {label}", "ours_us": round(t_ours, 2),
-                          "reference_us": round(t_ref, 2), "speedup": round(t_ref / t_ours, 2)}), flush=True)
+                          "reference_us": round(t_ref, 2), "speedup": round(t_ref / t_ours, 2),
+                          "ours_effective_TB_s": hbm_tb_s(xs[0][0].numel() * xs[0][0].element_size(), t_ours)}),
+              flush=True)
     xs = [(torch.randn(65536, 64, device=dev, generator=g), torch.randint(0, 2, (65536, 64), device=dev, generator=g))
           for _ in range(4)]
     m = tm.MultilabelExactMatch(64).to(dev)
@@ -102,7 +108,8 @@ def exact_match_cases(dev, g):
     st = [torch.zeros((), dtype=torch.long, device=dev), torch.zeros((), dtype=torch.long, device=dev)]
     t_ref = loop_us(lambda a: ref_multilabel_em(st, *a), xs, 100)
     print(json.dumps({"case": "MultilabelExactMatch.update 65536x64 logits", "ours_us": round(t_ours, 2),
-                      "reference_us": round(t_ref, 2), "speedup": round(t_ref / t_ours, 2)}), flush=True)
+                      "reference_us": round(t_ref, 2), "speedup": round(t_ref / t_ours, 2),
+                      "ours_effective_TB_s": hbm_tb_s(65536 * 64 * 12, t_ours)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -574,6 +574,13 @@ class _AbstractGroupStatScores(Metric):
         if self.validate_args:
             _binary_stat_scores_tensor_validation(preds, target, "global", self.ignore_index)
             _groups_validation(groups, self.num_groups)
+        states = (self.tp, self.fp, self.tn, self.fn)
+        if (preds.is_cuda and all(isinstance(t, Tensor) and t.device == preds.device and t.dtype == torch.int64
+                                  for t in states) and target.device == preds.device
+                and groups.device == preds.device and preds.numel() == target.numel() == groups.numel()):
+            ops.group_stats_update(preds, target, groups, self.num_groups, self.threshold, self.ignore_index,
+                                   self.__dict__, *states)
+            return
         counts = _group_stat_counts(preds, target, groups, self.num_groups, self.threshold, self.ignore_index)
         self.tp += counts[:, 0]
         self.fp += counts[:, 1]

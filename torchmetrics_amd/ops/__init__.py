@@ -1147,6 +1147,21 @@ def inception_score(logits: Tensor, perm: Tensor, splits: int) -> Tensor:
     return out
 
 
+def group_stats_update(preds: Tensor, target: Tensor, groups: Tensor, num_groups: int, threshold: float,
+                       ignore_index: Optional[int], owner: dict, tp: Tensor, fp: Tensor, tn: Tensor,
+                       fn: Tensor) -> None:
+    """Per-group tp / fp / tn / fn of binary ROCm inputs added into the int64 ``[num_groups]`` states in place
+    (``csrc/classification/group_stats.hip``: both score readings in one pass, LDS histogram, fold)."""
+    ws = owner.get("_group_ws")
+    if ws is None or ws[0].numel() != 8 * num_groups or ws[0].device != preds.device:
+        ws = owner["_group_ws"] = (torch.zeros(8 * num_groups, dtype=torch.int64, device=preds.device),
+                                   torch.zeros(1, dtype=torch.int32, device=preds.device))
+    _ops().group_stats_update(preds.reshape(-1).contiguous(), target.reshape(-1).contiguous(),
+                              groups.reshape(-1).to(torch.int64).contiguous(), int(num_groups), float(threshold),
+                              0 if ignore_index is None else int(ignore_index), ignore_index is not None, ws[0], ws[1],
+                              tp, fp, tn, fn)
+
+
 EM_MULTICLASS, EM_MULTILABEL = 0, 1
 
 

@@ -1,0 +1,35 @@
+"""bench.py driver contract on the multi-rank path: 2 gloo ranks under torch.distributed.run on the CPU print ONE
+JSON line with the whole-job value, world size 2, the engine's collectives, and a parity-checked baseline."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.timeout(600)
+def test_bench_two_rank_gloo_contract(tmp_path):
+    env = dict(os.environ, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
+           "2", "--warmup", "1", "--ring-mb", "8"]
+    res = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=580)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["warmup"] == 1
+    assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 2 * 8192
+    assert out["dist"]["world_size_seen"] == 2 and out["dist"]["backend"] == "gloo"
+    assert out["dist"]["engine_collectives"]["all_reduce"] >= 1
+    assert out["value"] > 0 and out["vs_baseline"] is not None and out["higher_is_better"] is True

@@ -47,6 +47,14 @@ void regression_compute(int64_t kind, at::TensorList states, const c10::optional
                         int64_t multioutput, double bound, at::Tensor out);
 void mc_calibration_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor cand, at::Tensor conf,
                            at::Tensor acc, at::Tensor notprob, int64_t slot, at::Tensor flag);
+void agg_update(const at::Tensor& x, const at::Tensor& w, double wconst, int64_t kind, int64_t nan_mode,
+                double impute, at::Tensor part, at::Tensor ctl, at::Tensor s0, at::Tensor s1, at::Tensor flag);
+void exact_match_update(const at::Tensor& preds, const at::Tensor& target, int64_t kind, int64_t C, int64_t P,
+                        bool has_c, double threshold, int64_t ignore_index, bool has_ignore, bool samplewise,
+                        at::Tensor ws, at::Tensor notprob, at::Tensor correct, at::Tensor total, at::Tensor out);
+void group_stats_update(const at::Tensor& preds, const at::Tensor& target, const at::Tensor& groups, int64_t G,
+                        double threshold, int64_t ignore_index, bool has_ignore, at::Tensor ws, at::Tensor notprob,
+                        at::Tensor tp, at::Tensor fp, at::Tensor tn, at::Tensor fn);
 }  // namespace tm_amd
 
 namespace {
@@ -235,6 +243,9 @@ PyMethodDef kMethods[] = {
     TM_FAST("curve_score", tm_amd::curve_score),
     TM_FAST("regression_compute", tm_amd::regression_compute),
     TM_FAST("mc_calibration_update", tm_amd::mc_calibration_update),
+    TM_FAST("agg_update", tm_amd::agg_update),
+    TM_FAST("exact_match_update", tm_amd::exact_match_update),
+    TM_FAST("group_stats_update", tm_amd::group_stats_update),
     TM_FAST("arg_probe", arg_probe),
     {nullptr, nullptr, 0, nullptr},
 };

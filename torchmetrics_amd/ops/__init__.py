@@ -1156,10 +1156,10 @@ def group_stats_update(preds: Tensor, target: Tensor, groups: Tensor, num_groups
     if ws is None or ws[0].numel() != 8 * num_groups or ws[0].device != preds.device:
         ws = owner["_group_ws"] = (torch.zeros(8 * num_groups, dtype=torch.int64, device=preds.device),
                                    torch.zeros(1, dtype=torch.int32, device=preds.device))
-    _ops().group_stats_update(preds.reshape(-1).contiguous(), target.reshape(-1).contiguous(),
-                              groups.reshape(-1).to(torch.int64).contiguous(), int(num_groups), float(threshold),
-                              0 if ignore_index is None else int(ignore_index), ignore_index is not None, ws[0], ws[1],
-                              tp, fp, tn, fn)
+    (_fast_mod or _fast()).group_stats_update(
+        preds.reshape(-1).contiguous(), target.reshape(-1).contiguous(), groups.reshape(-1).to(torch.int64).contiguous(),
+        int(num_groups), float(threshold), 0 if ignore_index is None else int(ignore_index), ignore_index is not None,
+        ws[0], ws[1], tp, fp, tn, fn)
 
 
 EM_MULTICLASS, EM_MULTILABEL = 0, 1
@@ -1181,9 +1181,10 @@ def exact_match_update(preds: Tensor, target: Tensor, kind: int, C: int, P: int,
     out = torch.empty(n if samplewise else 0, dtype=torch.int64, device=preds.device)
     if correct is None:
         correct = total = ws[0][:1]  # unused by the samplewise fold
-    _ops().exact_match_update(preds, target, int(kind), int(C), int(P), kind == EM_MULTICLASS, float(threshold),
-                              0 if ignore_index is None else int(ignore_index), ignore_index is not None,
-                              bool(samplewise), ws[0], ws[1], correct, total, out)
+    (_fast_mod or _fast()).exact_match_update(
+        preds, target, int(kind), int(C), int(P), kind == EM_MULTICLASS, float(threshold),
+        0 if ignore_index is None else int(ignore_index), ignore_index is not None, bool(samplewise), ws[0], ws[1],
+        correct, total, out)
     return out if samplewise else None
 
 
@@ -1207,8 +1208,8 @@ def agg_update(x: Tensor, weight: Union[Tensor, float, None], kind: int, nan_mod
         if w is None:
             w = _empty_f32(x.device)
         wconst = 1.0 if weight is None else float(weight)
-    _ops().agg_update(x.reshape(-1).contiguous(), w, wconst, int(kind), int(nan_mode), float(impute), ws[0], ws[1],
-                      s0, s0 if s1 is None else s1, flag)
+    (_fast_mod or _fast()).agg_update(x.reshape(-1).contiguous(), w, wconst, int(kind), int(nan_mode), float(impute),
+                                      ws[0], ws[1], s0, s0 if s1 is None else s1, flag)
     return ws[1]
 
 

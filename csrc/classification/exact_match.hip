@@ -106,30 +106,7 @@ __global__ void __launch_bounds__(kBlock) em_multiclass_vec_kernel(const scalar_
   const int nvec = C / kVec;
   const long long nw = static_cast<long long>(gridDim.x) * (kBlock / kWave);
   long long local = 0;
-  for (long long n = (static_cast<long long>(blockIdx.x) * kBlock + threadIdx.x) / kWave; n < N; n += nw) {
-    const u32x4* r = reinterpret_cast<const u32x4*>(preds + n * C);
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int v0 = lane; v0 < nvec; v0 += 4 * kWave) {
-      u32x4 buf[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int v = v0 + k * kWave;
-        if (v < nvec) buf[k] = __builtin_nontemporal_load(r + v);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int v = v0 + k * kWave;
-        if (v >= nvec) break;
-        const scalar_t* e = reinterpret_cast<const scalar_t*>(&buf[k]);
-#pragma unroll
-        for (int j = 0; j < kVec; ++j) {
-          const float x = to_f32(e[j]);
-          const int c = v * kVec + j;
-          if (argmax_better(x, c, bv, bi)) bv = x, bi = c;
-        }
-      }
-    }
+  auto judge = [&](long long n, float bv, int bi) {
     wave_argmax(bv, bi);
     if (lane == 0) {
       const long long t = static_cast<long long>(target[n]);
@@ -138,6 +115,55 @@ __global__ void __launch_bounds__(kBlock) em_multiclass_vec_kernel(const scalar_
         ws[n] = ok ? 1 : 0;
       else
         local += ok ? 1 : 0;
+    }
+  };
+  auto scan = [&](const u32x4* buf, int v0, float& bv, int& bi) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int v = v0 + k * kWave;
+      if (v >= nvec) break;
+      const scalar_t* e = reinterpret_cast<const scalar_t*>(&buf[k]);
+#pragma unroll
+      for (int j = 0; j < kVec; ++j) {
+        const float x = to_f32(e[j]);
+        const int c = v * kVec + j;
+        if (argmax_better(x, c, bv, bi)) bv = x, bi = c;
+      }
+    }
+  };
+  auto load = [&](long long n, int v0, u32x4* buf) {
+    const u32x4* r = reinterpret_cast<const u32x4*>(preds + n * C);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int v = v0 + k * kWave;
+      if (v < nvec) buf[k] = __builtin_nontemporal_load(r + v);
+    }
+  };
+  long long n = (static_cast<long long>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  if (nvec <= 4 * kWave) {
+    // a whole row fits one 4-vector-per-lane chunk: software-pipelined, the next row's loads are in flight while
+    // this row is scanned
+    u32x4 cur[4], nxt[4];
+    if (n < N) load(n, lane, cur);
+    for (; n < N; n += nw) {
+      if (n + nw < N) load(n + nw, lane, nxt);
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+      scan(cur, lane, bv, bi);
+      judge(n, bv, bi);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+    }
+  } else {
+    for (; n < N; n += nw) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int v0 = lane; v0 < nvec; v0 += 4 * kWave) {
+        u32x4 buf[4];
+        load(n, v0, buf);
+        scan(buf, v0, bv, bi);
+      }
+      judge(n, bv, bi);
     }
   }
   if (!samplewise) block_add_counts(local, 0, ws, nullptr);

@@ -231,12 +231,20 @@ __global__ void __launch_bounds__(kBlock) em_multilabel_kernel(const scalar_t* _
       if constexpr (IsFloating<scalar_t>::value) {
         const float x = to_f32(v);
         np |= !(x >= 0.f && x <= 1.f);  // the reference decides over every score, ignored positions included
-        if (has_ignore && t == ignore) continue;
+        // reference semantics (_multilabel_stat_scores_format): an ignored target becomes -1 while the prediction
+        // stays 0/1, so an ignored position never matches and its sample is never an exact match
+        if (has_ignore && t == ignore) {
+          oka = okb = false;
+          continue;
+        }
         const float s = round_to<scalar_t>(1.f / (1.f + expf(-x)));
         oka &= static_cast<long long>(x > thr) == t;
         okb &= static_cast<long long>(s > thr) == t;
       } else {
-        if (has_ignore && t == ignore) continue;
+        if (has_ignore && t == ignore) {
+          oka = okb = false;
+          continue;
+        }
         const bool eq = static_cast<long long>(v) == t;
         oka &= eq;
         okb &= eq;

@@ -34,6 +34,7 @@ constexpr int kErrPredsNan = 1 << 4;
 constexpr int kErrValueNan = 1 << 5;
 constexpr int kErrNegValue = 1 << 6;
 constexpr int kErrValueNanWarn = 1 << 7;  // not an error: compute() emits the 'warn' nan_strategy UserWarning
+constexpr int kErrOneshot = 1 << 8;        // a one-shot all-reduce of this metric's states failed (comm/oneshot)
 
 // ------------------------------------------------------------------------------------------------ type helpers
 template <typename T>

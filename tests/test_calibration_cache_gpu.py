@@ -1,84 +1,48 @@
-"""Incremental calibration bins (``classification/extras.py`` ``_BinnedCalibration``) on the GPU.
-
-The cached bins must give the CPU list-state result after many updates, after ``forward()`` merges, resets,
-state-dict loads and under a 2-rank sync (bins all-reduced instead of lists gathered)."""
+"""The calibration-error bin cache (``classification/extras.py``) must never outlive the list states it summarises:
+a loaded state dict with the same sample count, ``.to()`` round trips and manual ``sync()``/``unsync()`` all give the
+value the lists themselves give."""
 import pytest
 import torch
 
-from torchmetrics_amd.classification import BinaryCalibrationError, MulticlassCalibrationError
-from tests.helpers import assert_close, run_ddp
+import torchmetrics_amd as tm
+from torchmetrics_amd.functional.classification import binary_calibration_error
 
 pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
 
 
-def _batches(seed, n=6, m=4000, c=7):
+def _batch(seed, n=4096):
     g = torch.Generator().manual_seed(seed)
-    return [(torch.randn(m, c, generator=g) * 2, torch.randint(0, c, (m,), generator=g)) for _ in range(n)]
+    return torch.rand(n, generator=g), torch.randint(0, 2, (n,), generator=g)
 
 
-@pytest.mark.parametrize("norm", ["l1", "max", "l2"])
-@pytest.mark.parametrize("n_bins", [1, 15, 100])
-def test_multiclass_cached_bins_match_cpu(norm, n_bins):
-    gpu = MulticlassCalibrationError(7, n_bins=n_bins, norm=norm).cuda()
-    cpu = MulticlassCalibrationError(7, n_bins=n_bins, norm=norm)
-    for k, (p, t) in enumerate(_batches(n_bins)):
-        gpu.update(p.cuda(), t.cuda())
-        cpu.update(p, t)
-        assert gpu.__dict__.get("_bin_cache") is not None
-        if k % 2:  # compute every other step (the per-step-compute pattern), the cache keeps accumulating
-            assert_close(gpu.compute().cpu(), cpu.compute(), atol=2e-6, rtol=1e-5)
-    assert_close(gpu.compute().cpu(), cpu.compute(), atol=2e-6, rtol=1e-5)
+def test_load_state_dict_same_numel_drops_cache():
+    p1, t1 = _batch(1)
+    p2, t2 = _batch(2)
+    a = tm.BinaryCalibrationError(n_bins=10).to(DEV)
+    a.update(p1.to(DEV), t1.to(DEV))
+    first = a.compute()
+    b = tm.BinaryCalibrationError(n_bins=10)
+    b.persistent(True)
+    b.update(p2, t2)
+    a.persistent(True)
+    a.load_state_dict({k: (v.to(DEV) if isinstance(v, torch.Tensor) else [x.to(DEV) for x in v])
+                       for k, v in b.state_dict().items()})
+    got = a.compute()
+    exp = binary_calibration_error(p2, t2, n_bins=10)
+    torch.testing.assert_close(got.cpu(), exp, rtol=1e-5, atol=1e-6)
+    assert not torch.allclose(first.cpu(), exp)
 
 
-@pytest.mark.parametrize("norm", ["l1", "max", "l2"])
-def test_binary_cached_bins_match_cpu(norm):
-    g = torch.Generator().manual_seed(3)
-    gpu = BinaryCalibrationError(n_bins=10, norm=norm).cuda()
-    cpu = BinaryCalibrationError(n_bins=10, norm=norm)
-    for _ in range(5):
-        p, t = torch.rand(3000, generator=g), torch.randint(0, 2, (3000,), generator=g)
-        gpu.update(p.cuda(), t.cuda())
-        cpu.update(p, t)
-    assert_close(gpu.compute().cpu(), cpu.compute(), atol=2e-6, rtol=1e-5)
-
-
-def test_cache_survives_forward_reset_and_state_loads():
-    batches = _batches(11)
-    gpu = MulticlassCalibrationError(7, n_bins=15).cuda()
-    cpu = MulticlassCalibrationError(7, n_bins=15)
-    for p, t in batches[:3]:
-        assert_close(gpu(p.cuda(), t.cuda()).cpu(), cpu(p, t), atol=2e-6, rtol=1e-5)  # forward: batch value
-    assert_close(gpu.compute().cpu(), cpu.compute(), atol=2e-6, rtol=1e-5)  # re-seeded from the merged lists
-    gpu.update(*(x.cuda() for x in batches[3]))
-    cpu.update(*batches[3])
-    assert_close(gpu.compute().cpu(), cpu.compute(), atol=2e-6, rtol=1e-5)
-    gpu.reset()
-    cpu.reset()
-    gpu.update(*(x.cuda() for x in batches[4]))
-    cpu.update(*batches[4])
-    assert_close(gpu.compute().cpu(), cpu.compute(), atol=2e-6, rtol=1e-5)
-    # states written from outside: the element count no longer matches the cache -> re-bin from the lists
-    gpu.confidences = [torch.rand(100, device="cuda")]
-    gpu.accuracies = [torch.ones(100, device="cuda")]
-    cpu.confidences = [gpu.confidences[0].cpu()]
-    cpu.accuracies = [torch.ones(100)]
-    gpu._computed = cpu._computed = None
-    assert_close(gpu.compute().cpu(), cpu.compute(), atol=2e-6, rtol=1e-5)
-
-
-def _ddp_body(rank, world):
-    torch.cuda.set_device(0)
-    batches = _batches(21, n=4)
-    m = MulticlassCalibrationError(7, n_bins=15).cuda()
-    for p, t in batches[rank::world]:
-        m.update(p.cuda(), t.cuda())
-    got = m.compute().cpu()
-    assert len(m.confidences) in (1, 2)  # local lists untouched by the bins all-reduce
-    ref = MulticlassCalibrationError(7, n_bins=15)
-    for p, t in batches:
-        ref.update(p, t)
-    assert_close(got, ref.compute(), atol=2e-6, rtol=1e-5)
-
-
-def test_cached_bins_two_ranks_one_device():
-    run_ddp(_ddp_body)
+def test_to_cpu_and_back_uses_lists():
+    p1, t1 = _batch(3)
+    m = tm.BinaryCalibrationError(n_bins=15).to(DEV)
+    m.update(p1.to(DEV), t1.to(DEV))
+    m.compute()
+    m = m.to("cpu")
+    torch.testing.assert_close(m.compute(), binary_calibration_error(p1, t1, n_bins=15), rtol=1e-5, atol=1e-6)
+    m = m.to(DEV)
+    p2, t2 = _batch(4)
+    m.update(p2.to(DEV), t2.to(DEV))
+    exp = binary_calibration_error(torch.cat([p1, p2]), torch.cat([t1, t2]), n_bins=15)
+    torch.testing.assert_close(m.compute().cpu(), exp, rtol=1e-5, atol=1e-6)

@@ -153,6 +153,31 @@ def test_exact_match(device):
                    lambda a, b: ((_np(a) > 0.5) == _np(b)).all(-1).mean(), {"num_labels": L}, device=device)
 
 
+@pytest.mark.parametrize("ignore_index", [0, -1])
+@pytest.mark.parametrize("samplewise", [False, True])
+def test_multilabel_exact_match_ignore_index(ignore_index, samplewise):
+    """Reference baseline ``_baseline_exact_match_multilabel`` (T/classification/test_exact_match.py:150-171): an
+    ignored target becomes -1 while the prediction stays 0/1, so a sample with an ignored position never matches."""
+    from torchmetrics_amd.functional.classification import multilabel_exact_match
+
+    g = torch.Generator().manual_seed(11)
+    preds = torch.rand(64, L, 3, generator=g)
+    target = (preds > 0.5).long()
+    target[::7, 1, 0] = 1 - target[::7, 1, 0]
+    if ignore_index == -1:
+        target[::3, 2, 1] = -1
+    p_np, t_np = (_np(preds) > 0.5).astype(np.int64), _np(target).astype(np.int64).copy()
+    t_np[t_np == ignore_index] = -1
+    if samplewise:
+        exp = ((p_np == t_np).sum(1) == L).sum(1) / p_np.shape[2]
+    else:
+        pp, tt = np.moveaxis(p_np, 1, -1).reshape(-1, L), np.moveaxis(t_np, 1, -1).reshape(-1, L)
+        exp = ((pp == tt).sum(1) == L).mean()
+    avg = "samplewise" if samplewise else "global"
+    got = multilabel_exact_match(preds, target, L, multidim_average=avg, ignore_index=ignore_index)
+    np.testing.assert_allclose(_np(got), exp, rtol=1e-6)
+
+
 # -------------------------------------------------------------------------------------------- group fairness
 @pytest.mark.parametrize("device", DEVICES)
 def test_group_fairness(device):

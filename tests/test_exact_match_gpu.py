@@ -29,8 +29,8 @@ def _ref_multilabel(preds, target, threshold, ignore_index, samplewise):
     n, l = preds.shape[:2]
     preds, target = preds.reshape(n, l, -1), target.reshape(n, l, -1)
     if ignore_index is not None:
-        m = target == ignore_index
-        preds, target = preds.masked_fill(m, -1), target.masked_fill(m, -1)
+        # reference test baseline (T/classification/test_exact_match.py:160-167): only the target is masked
+        target = target.masked_fill(target == ignore_index, -1)
     ok = ((preds == target).sum(1) == l).float()  # [N, P]
     return ok.mean(1) if samplewise else ok.mean()
 
@@ -79,7 +79,7 @@ def test_multiclass_labels(shape, samplewise):
 
 @pytest.mark.parametrize("shape", [(5000, 6), (400, 3, 50), (128, 16, 2, 3)])
 @pytest.mark.parametrize("reading", ["probs", "logits", "labels"])
-@pytest.mark.parametrize("ignore_index", [None, -1])
+@pytest.mark.parametrize("ignore_index", [None, -1, 0])
 @pytest.mark.parametrize("samplewise", [False, True])
 def test_multilabel(shape, reading, ignore_index, samplewise):
     if samplewise and len(shape) == 2:
@@ -93,7 +93,7 @@ def test_multilabel(shape, reading, ignore_index, samplewise):
         preds = (noisy * 2 - 1) * 3 + torch.randn(shape, generator=g)
     else:
         preds = noisy.long()
-    if ignore_index is not None:
+    if ignore_index == -1:
         target[torch.rand(shape, generator=g) < 0.05] = ignore_index
     avg = "samplewise" if samplewise else "global"
     exp = _ref_multilabel(preds, target, 0.5, ignore_index, samplewise)

@@ -100,11 +100,11 @@ class _BinnedCalibration(Metric):
             self.__dict__.pop("_bin_cache", None)
             return
         cache = self.__dict__.get("_bin_cache")
-        if cache is None or cache[0].device != conf.device:
+        if cache is None or cache[0].device != conf.device or cache[2] is not self.confidences:
             if self._list_numel() != conf.numel():  # samples before this batch are not in any cache
                 self.__dict__.pop("_bin_cache", None)
                 return
-            cache = [torch.zeros(self.n_bins + 1, 3, dtype=torch.float32, device=conf.device), 0]
+            cache = [torch.zeros(self.n_bins + 1, 3, dtype=torch.float32, device=conf.device), 0, self.confidences]
             self.__dict__["_bin_cache"] = cache
         ops.calibration_bins_into(conf.contiguous(), acc.float().contiguous(), self._bounds(conf.device), cache[0])
         cache[1] += conf.numel()
@@ -114,15 +114,33 @@ class _BinnedCalibration(Metric):
         return c.numel() if isinstance(c, Tensor) else sum(x.numel() for x in c)
 
     def _valid_cache(self) -> Optional[list]:
+        """The cache, if it covers exactly the samples in the list states: same list OBJECT (a loaded state dict,
+        ``.to()`` or a forward merge rebinds the list) and the same element count."""
         cache = self.__dict__.get("_bin_cache")
-        if cache is not None and cache[1] == self._list_numel() and cache[1] > 0:
+        if cache is not None and cache[2] is self.confidences and cache[1] == self._list_numel() and cache[1] > 0:
             return cache
+        if cache is not None:
+            self.__dict__.pop("_bin_cache", None)  # drop it (and its reference to the replaced list)
         return None
 
     def reset(self) -> None:
         super().reset()
         self.__dict__.pop("_bin_cache", None)
         self.__dict__.pop("_bin_synced", None)
+
+    def unsync(self, should_unsync: bool = True) -> None:
+        # the globally reduced bins belong to the synced view only
+        if should_unsync:
+            self.__dict__.pop("_bin_synced", None)
+        super().unsync(should_unsync)
+
+    def _load_from_state_dict(self, *args: Any, **kwargs: Any) -> None:
+        self.__dict__.pop("_bin_cache", None)
+        super()._load_from_state_dict(*args, **kwargs)
+
+    def _apply(self, fn: Any, exclude_state: Any = "") -> Any:
+        self.__dict__.pop("_bin_cache", None)
+        return super()._apply(fn, exclude_state)
 
     def _sync_dist(self, dist_sync_fn: Optional[Any] = None, process_group: Optional[Any] = None) -> None:
         import torch.distributed as dist
@@ -151,7 +169,8 @@ class _BinnedCalibration(Metric):
             conf, acc = dim_zero_cat(self.confidences), dim_zero_cat(self.accuracies)
             if conf.is_cuda and conf.dtype == torch.float32 and not self._is_synced and self.n_bins + 1 <= 4096:
                 # re-seed the cache from the lists (one binning pass, which this compute needs anyway)
-                cache = [torch.zeros(self.n_bins + 1, 3, dtype=torch.float32, device=conf.device), 0]
+                cache = [torch.zeros(self.n_bins + 1, 3, dtype=torch.float32, device=conf.device), 0,
+                         self.confidences]
                 ops.calibration_bins_into(conf.contiguous(), acc.float().contiguous(), self._bounds(conf.device),
                                           cache[0])
                 cache[1] = conf.numel()

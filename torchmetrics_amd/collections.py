@@ -187,7 +187,8 @@ class MetricCollection(ModuleDict):
         for _, grp_list in plans.items():
             leaders = [g[0] for g in grp_list]
             entries = [({a: getattr(m, a) for a in m._reductions}, m._reductions) for m in leaders]
-            synced = sync_state_dicts(entries, group=leaders[0].process_group)
+            word = self._sync_word(entries)
+            synced = sync_state_dicts(entries, group=leaders[0].process_group, err_word=word)
             for g, states in zip(grp_list, synced):
                 for m in g:
                     m._cache = {a: getattr(m, a) for a in m._defaults}
@@ -198,31 +199,64 @@ class MetricCollection(ModuleDict):
                     m._to_sync = False
         return restore
 
+    def _sync_word(self, entries: List[Tuple[Dict[str, Any], Dict[str, Any]]]) -> Optional[Tensor]:
+        """The collection's int32 status word for the one-shot buckets of its one engine call (``None`` off-GPU)."""
+        dev = next((v.device for st, _ in entries for v in st.values() if isinstance(v, Tensor) and v.is_cuda), None)
+        if dev is None:
+            return None
+        d = self.__dict__
+        word = d.get("_oneshot_word")
+        if word is None or word.device != dev:
+            word = torch.zeros(1, dtype=torch.int32, device=dev)
+            d["_oneshot_word"] = word
+        d["_oneshot_word_pending"] = True
+        return word
+
     def _check_device_errors(self) -> None:
-        """Read every member's deferred-validation flag word with ONE device sync (a stack + one ``.item()``) instead
-        of one per member; clean members then skip their own read in ``compute()`` (any raised flag is left for its
-        metric to raise with its own message)."""
+        """Read every member's deferred-validation flag word -- and the collection's one-shot status word after a
+        sync -- with ONE device sync (a cat + one ``.any()``) instead of one per member; clean members then skip their
+        own read in ``compute()`` (any raised flag is left for its metric to raise with its own message)."""
         # (members with a cached result never read their flag; the mark is cleared after compute either way)
+        d = self.__dict__
+        word = d.get("_oneshot_word") if d.pop("_oneshot_word_pending", False) else None
         pending = [m for m in self._modules.values() if m.__dict__["_device_errors"] is not None
                    and m.__dict__.get("_errors_checked_at") != m.__dict__["_update_count"]]
-        if len(pending) < 2:
-            return
         bufs = [m.__dict__["_device_errors"] for m in pending]
-        if any(b.device != bufs[0].device for b in bufs):
+        if word is not None:
+            bufs = [word] + bufs
+        if not bufs or (word is None and len(pending) < 2):
             return
-        if not bool(torch.cat(bufs).any()):
+        if any(b.device != bufs[0].device for b in bufs):
+            if word is not None and int(word.item()):
+                self._raise_oneshot(word)
+            return
+        flags = torch.cat(bufs)
+        if not bool(flags.any()):
             for m in pending:
-                d = m.__dict__
-                d["_device_errors_clean"] = True
-                d["_errors_checked_at"] = d["_update_count"]
+                md = m.__dict__
+                md["_device_errors_clean"] = True
+                md["_errors_checked_at"] = md["_update_count"]
+        elif word is not None and int(flags[0].item()):
+            self._raise_oneshot(word)
+
+    @staticmethod
+    def _raise_oneshot(word: Tensor) -> None:
+        from torchmetrics_amd.utils import validation as _validation
+
+        code = int(word.item())
+        word.zero_()
+        _validation.raise_for_code(code)
 
     def _compute_and_reduce(self, method_name: str, *args: Any, **kwargs: Any) -> Dict[str, Any]:
         result = {}
         restore: List[Tuple[Metric, bool]] = []
         if method_name == "compute":
-            self._check_device_errors()
+            # sync first, then ONE read of every validation word plus the sync's one-shot status (a rank raising
+            # before the collectives would leave its peers waiting in them)
             restore = self._collection_sync()
         try:
+            if method_name == "compute":
+                self._check_device_errors()
             for k, m in self.items(keep_base=True, copy_state=False):
                 if method_name == "compute":
                     res = m.compute()

@@ -126,9 +126,8 @@ def _multilabel_exact_match_format(
     preds = preds.reshape(*preds.shape[:2], -1)
     target = target.reshape(*target.shape[:2], -1)
     if ignore_index is not None:
-        idx = target == ignore_index
-        target = target.masked_fill(idx, -1)
-        preds = preds.masked_fill(idx, -1)
+        # only the target is masked (reference _multilabel_stat_scores_format): an ignored position never matches
+        target = target.masked_fill(target == ignore_index, -1)
     return preds, target
 
 

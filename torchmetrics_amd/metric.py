@@ -312,9 +312,15 @@ class Metric(Module, ABC):
         group = process_group or self.process_group
         states = {attr: getattr(self, attr) for attr in self._reductions}
         if dist_sync_fn is None:
-            synced = sync_state_dicts([(states, self._reductions)], group=group)[0]
+            # a one-shot xGMI bucket reports failure in this metric's validation word: compute() reads the word after
+            # the sync (sync() reads it right away when called on its own)
+            dev = next((v.device for v in states.values() if isinstance(v, Tensor) and v.is_cuda), None)
+            err = self._device_error_buffer(dev) if dev is not None else None
+            synced = sync_state_dicts([(states, self._reductions)], group=group, err_word=err)[0]
             for attr, val in synced.items():
                 setattr(self, attr, val)
+            if err is not None:
+                self.__dict__["_sync_word_pending"] = True
             return
         # user-supplied per-tensor gather: reference contract, one call per state tensor
         for attr, fn in self._reductions.items():
@@ -379,13 +385,21 @@ class Metric(Module, ABC):
             self._device_errors = buf
         return buf
 
-    def _raise_device_errors(self) -> None:
+    def _raise_device_errors(self, only: int = 0) -> None:
+        """Read the deferred-validation word (one device sync) and raise what it holds; ``only``: a bit mask -- raise
+        just those bits and leave the others for ``compute()``."""
         buf = self._device_errors
+        self.__dict__.pop("_sync_word_pending", None)
         if buf is None:
             return
         code = int(buf.item())
+        if only:
+            code &= only
         if code:
-            buf.zero_()
+            if only:
+                buf.bitwise_and_(~only)
+            else:
+                buf.zero_()
             _validation.raise_for_code(code, self)
 
     def _move_list_states_to_cpu(self) -> None:
@@ -412,6 +426,13 @@ class Metric(Module, ABC):
         self._cache = {attr: getattr(self, attr) for attr in self._defaults}
         self._sync_dist(dist_sync_fn, process_group=process_group)
         self._is_synced = True
+        if self.__dict__.get("_sync_word_pending") and not self.__dict__.get("_in_compute"):
+            # stand-alone sync(): a failed one-shot bucket must raise now, before anyone reads the states
+            try:
+                self._raise_device_errors(only=_validation.ONESHOT_FAILED)
+            except RuntimeError:
+                self.unsync()
+                raise
 
     def unsync(self, should_unsync: bool = True) -> None:
         """Restore the local (pre-sync) states."""
@@ -458,29 +479,45 @@ class Metric(Module, ABC):
             state = self.__dict__
             if state["_computed"] is not None:
                 return state["_computed"]
-            if state["_device_errors"] is not None and not state.pop("_device_errors_clean", False):
-                # the flag word only changes through update() / graph replays, which all bump _update_count: a word
-                # read clean at this count is still clean (saves the device sync on repeated compute() calls)
-                if state.get("_errors_checked_at") != state["_update_count"]:
-                    self._raise_device_errors()
-                    state["_errors_checked_at"] = state["_update_count"]
             self._consolidate_cat_lists()
             avail = state["distributed_available_fn"]
             if not state["_is_synced"] and not (state["_to_sync"] and callable(avail) and avail()):
-                # nothing to gather: skip the sync / unsync context (generator + attribute traffic per call)
+                # nothing to gather: skip the sync / unsync bookkeeping (attribute traffic per call)
+                self._check_errors_once(state)
                 value = _squeeze_if_scalar(compute(*args, **kwargs))
             else:
-                with self.sync_context(
-                    dist_sync_fn=self.dist_sync_fn,
-                    should_sync=self._to_sync,
-                    should_unsync=self._should_unsync,
-                ):
+                # sync FIRST, then read the validation word once: every rank has finished its collectives before any
+                # rank raises (a rank raising before the sync would leave its peers waiting), and the same read
+                # covers a failed one-shot bucket of this very sync
+                state["_in_compute"] = True
+                try:
+                    self.sync(dist_sync_fn=self.dist_sync_fn, should_sync=self._to_sync)
+                finally:
+                    state.pop("_in_compute", None)
+                try:
+                    self._check_errors_once(state)
                     value = _squeeze_if_scalar(compute(*args, **kwargs))
+                finally:
+                    # also on a raise: the local states come back, accumulation can go on
+                    self.unsync(should_unsync=self._is_synced and self._should_unsync)
             if state["compute_with_cache"]:
                 state["_computed"] = value
             return value
 
         return wrapped_func
+
+    def _check_errors_once(self, state: Dict[str, Any]) -> None:
+        """Raise what the deferred-validation word holds (one 4-byte device read).  The word only changes through
+        update() / graph replays (which bump ``_update_count``) and through a sync's one-shot buckets: a word read
+        clean at this count, with no sync since, is still clean (no device sync on repeated ``compute()`` calls)."""
+        if state["_device_errors"] is None:
+            return
+        pending = state.get("_sync_word_pending", False)
+        if state.pop("_device_errors_clean", False) and not pending:
+            return
+        if pending or state.get("_errors_checked_at") != state["_update_count"]:
+            self._raise_device_errors()
+            state["_errors_checked_at"] = state["_update_count"]
 
     def _consolidate_cat_lists(self) -> None:
         """Replace the elements of every ``cat`` list state by their concatenation, in place (same list object).

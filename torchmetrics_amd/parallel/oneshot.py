@@ -13,11 +13,24 @@ The reference has no counterpart (it gathers each state with ``barrier`` + 2 ``a
 Setup (once per process group): every rank ``hipMalloc``s one buffer, exports it with ``hipIpcGetMemHandle`` and the
 handles are exchanged with ``all_gather_object``; peers open them with ``hipIpcOpenMemHandle``.  Setup also checks
 that all ranks are on one host and on distinct devices; otherwise the path is disabled for that group.
+
+Failure semantics (never a silent partial result):
+
+* a peer wait blocks up to ``timeout_s``: ``TORCHMETRICS_AMD_ONESHOT_TIMEOUT_S`` if set, else the process group's own
+  timeout (the time RCCL itself would wait), so a rank that reaches ``compute()`` seconds after its peers (rank 0
+  checkpointing or logging) simply gets the right sums;
+* on a timeout the kernel reduces nothing, disowns the call on every rank (two-phase protocol in the ``.hip`` file)
+  and ORs ``ONESHOT_FAILED`` into the status word the caller passed -- the metric's deferred-validation word, which
+  ``compute()`` reads once anyway -- so EVERY rank raises ``RuntimeError`` before a value is returned;
+* raising that error disables every communicator of the process (:func:`disable_all`): all ranks raised, so all
+  ranks take the RCCL path from the next sync on and their collective sequences stay matched.
 """
 import os
 import socket
 import threading
-from typing import Any, Dict, Optional
+import weakref
+from datetime import timedelta
+from typing import Any, Dict, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -30,6 +43,31 @@ DEFAULT_SLOT_BYTES = 256 * 1024
 
 def _enabled_by_env() -> bool:
     return os.environ.get("TORCHMETRICS_AMD_ONESHOT", "1") not in ("0", "false", "False")
+
+
+def _resolve_group(group: Optional[Any]) -> Any:
+    return group if group is not None else dist.distributed_c10d._get_default_group()
+
+
+def group_timeout_s(group: Optional[Any] = None) -> float:
+    """How long a peer wait may block: ``TORCHMETRICS_AMD_ONESHOT_TIMEOUT_S``, else the group's own timeout (what RCCL
+    would wait before its watchdog fires), else torch's default for the backend."""
+    env = os.environ.get("TORCHMETRICS_AMD_ONESHOT_TIMEOUT_S")
+    if env:
+        return float(env)
+    g = _resolve_group(group)
+    backend = dist.get_backend(g)
+    dev = torch.device("cuda") if backend == "nccl" else torch.device("cpu")
+    try:
+        t = g._get_backend(dev).options._timeout
+        if isinstance(t, timedelta) and t.total_seconds() > 0:
+            return t.total_seconds()
+    except Exception:  # noqa: BLE001 - private API, fall back to the documented default
+        pass
+    try:
+        return dist.distributed_c10d._get_default_timeout(backend).total_seconds()
+    except Exception:  # noqa: BLE001
+        return 600.0
 
 
 class OneShotAllReduce:
@@ -89,8 +127,11 @@ class OneShotAllReduce:
         self.usable = bool(int(agree.item()))
         self._peers = torch.tensor(ptrs or [self._own], dtype=torch.int64)
         self._status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.timeout_s = group_timeout_s(group)
         self.epoch = 0
         self.calls = 0
+        self.failed = False
+        _instances.add(self)
 
     def supports(self, buf: Tensor) -> bool:
         return (
@@ -101,21 +142,37 @@ class OneShotAllReduce:
             and not torch.cuda.is_current_stream_capturing()  # the epoch is a launch argument
         )
 
-    def all_reduce(self, buf: Tensor, op: str = "sum") -> Tensor:
-        """In-place reduction of a contiguous 1-D ``buf`` across the group (``mean`` is left as a sum)."""
+    def all_reduce(self, buf: Tensor, op: str = "sum", err: Optional[Tensor] = None) -> Tensor:
+        """In-place reduction of a contiguous 1-D ``buf`` across the group (``mean`` is left as a sum).
+
+        ``err``: an int32 device word that receives ``ONESHOT_FAILED`` if the call fails; the caller MUST read it (or
+        call :meth:`check`) before using ``buf``.  Without ``err`` the status is checked here (one device sync)."""
+        if not self.usable:
+            raise RuntimeError("one-shot all-reduce: communicator is disabled")
         self.epoch += 1
-        if self.epoch >= 2**32 - 1:
+        if self.epoch >= 2**31 - 1:
             raise RuntimeError("one-shot all-reduce: epoch counter exhausted")
         inp = buf.contiguous()
         self._ops.oneshot_allreduce(inp, buf, self._peers, self.rank, self.slot_bytes, self.epoch, _OPS[op], True,
-                                    self._status)
+                                    float(self.timeout_s), self._status, err)
         self.calls += 1
+        if err is None:
+            self.check()
         return buf
 
     def check(self) -> None:
-        """Raise if a wait for a peer ever timed out (reads the status word: one device sync)."""
-        if int(self._status.item()) != 0:
-            raise RuntimeError("one-shot all-reduce: a peer did not arrive within 2 s; results are invalid")
+        """Raise (and disable every communicator) if a call ever timed out or was disowned by a peer (one device
+        sync)."""
+        code = int(self._status.item())
+        if code != 0:
+            disable_all()
+            raise RuntimeError(failure_message(code, self.timeout_s))
+
+    def disable(self) -> None:
+        """Stop using this communicator (after a failure every rank raised, so every rank disables it; buffers stay
+        mapped until :meth:`close`, a late peer's kernel may still be reading them)."""
+        self.usable = False
+        self.failed = True
 
     def close(self) -> None:
         dev = self.device.index
@@ -128,7 +185,26 @@ class OneShotAllReduce:
         self.usable = False
 
 
-_registry: Dict[Any, Optional[OneShotAllReduce]] = {}
+def failure_message(code: int = 1, timeout_s: Optional[float] = None) -> str:
+    what = "a peer did not arrive" if code & 1 else "a peer timed out and disowned the call"
+    limit = f" within {timeout_s:g} s" if timeout_s is not None and code & 1 else ""
+    return (f"one-shot all-reduce failed: {what}{limit}; the metric states were NOT synchronised and no value is "
+            "returned. The one-shot path is now disabled on every rank; the next sync uses RCCL "
+            "(raise the limit with TORCHMETRICS_AMD_ONESHOT_TIMEOUT_S or the process group's timeout).")
+
+
+_instances: "weakref.WeakSet[OneShotAllReduce]" = weakref.WeakSet()
+
+
+def disable_all() -> None:
+    """Disable every communicator of this process (called on every rank when a one-shot failure is raised)."""
+    for c in list(_instances):
+        c.disable()
+
+
+# registry: id(resolved group) -> (weakref to the group, communicator or None); the weakref guards against a new
+# group allocated at a destroyed group's address (a re-initialised WORLD included)
+_registry: Dict[int, Tuple[Any, Optional[OneShotAllReduce]]] = {}
 _lock = threading.Lock()
 
 
@@ -138,11 +214,17 @@ def get_oneshot(group: Optional[Any] = None) -> Optional[OneShotAllReduce]:
     Every rank reaches this call at the same point of the engine's collective sequence (the decision depends only on
     the backend, the env switch and the bucket size, which agree across ranks), so the setup collective is safe.
     """
-    key = id(group) if group is not None else None
+    g = _resolve_group(group)
+    key = id(g)
     with _lock:
-        if key in _registry:
-            comm = _registry[key]
-            return comm if comm is not None and comm.usable else None
+        hit = _registry.get(key)
+        if hit is not None:
+            if hit[0]() is g:
+                comm = hit[1]
+                return comm if comm is not None and comm.usable else None
+            stale = _registry.pop(key)[1]  # the group this entry belonged to is gone
+            if stale is not None:
+                stale.close()
     comm = None
     if _enabled_by_env() and torch.cuda.is_available():
         from torchmetrics_amd import ops
@@ -150,16 +232,16 @@ def get_oneshot(group: Optional[Any] = None) -> Optional[OneShotAllReduce]:
         if ops.load_native(strict=False):
             comm = OneShotAllReduce(group)  # collective; ranks agree on `usable` inside
     with _lock:
-        _registry[key] = comm
+        _registry[key] = (weakref.ref(g), comm)
     return comm if comm is not None and comm.usable else None
 
 
 def reset_registry() -> None:
     with _lock:
-        for c in _registry.values():
+        for _, c in _registry.values():
             if c is not None:
                 c.close()
         _registry.clear()
 
 
-__all__ = ["OneShotAllReduce", "get_oneshot", "reset_registry", "DEFAULT_SLOT_BYTES"]
+__all__ = ["OneShotAllReduce", "get_oneshot", "reset_registry", "disable_all", "group_timeout_s", "DEFAULT_SLOT_BYTES"]

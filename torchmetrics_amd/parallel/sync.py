@@ -127,6 +127,7 @@ class _GatherItem:
 def sync_state_dicts(
     entries: Sequence[Tuple[Dict[str, State], Dict[str, Any]]],
     group: Optional[Any] = None,
+    err_word: Optional[Tensor] = None,
 ) -> List[Dict[str, State]]:
     """Synchronise the states of several metrics at once.
 
@@ -134,6 +135,9 @@ def sync_state_dicts(
         entries: one ``(states, reductions)`` pair per metric; ``reductions[name]`` is the metric's
             ``dist_reduce_fx`` after string resolution (``dim_zero_sum`` ...), ``None`` or a callable.
         group: process group (``None`` = WORLD).
+        err_word: int32 device word (the metric's / collection's deferred-validation word).  One-shot buckets OR
+            ``ONESHOT_FAILED`` into it on failure and the CALLER must read it before using the results (``compute()``
+            reads it once anyway).  Without it a one-shot bucket is checked here with its own device sync.
 
     Returns:
         One dict of synced states per entry.
@@ -171,7 +175,8 @@ def sync_state_dicts(
             # the communicator (IPC setup collective) is only created once a bucket small enough for it shows up
             comm = get_oneshot(group) if (small and flat.is_cuda and _is_nccl(group)) else None
             if comm is not None and comm.supports(flat):
-                comm.all_reduce(flat, kind)  # one peer-read kernel over xGMI
+                word = err_word if err_word is not None and err_word.device == flat.device else None
+                comm.all_reduce(flat, kind, word)  # one peer-read kernel over xGMI (checked now if word is None)
                 _stats["oneshot_all_reduce"] += 1
                 _stats["bytes"] += flat.numel() * flat.element_size()
             else:

@@ -334,6 +334,7 @@ class GraphedCompute:
                     views[id(t)] = flat[off : off + t.numel()].view(t.shape)
                     off += t.numel()
                 arenas[key] = flat
+        oneshot_word: Optional[Tensor] = None
         words = [(m._device_errors, 0) for _, m in self._all_members
                  if m._device_errors is not None and m._device_errors.is_cuda]
         graph = torch.cuda.CUDAGraph()
@@ -388,6 +389,11 @@ class GraphedCompute:
                     if flat.numel() != 1 or flat.dtype not in _WORD_CODES:
                         flat = flat.to(torch.int32).amax().reshape(1)
                     words.append((flat, _WORD_CODES[flat.dtype]))
+                # the one-shot buckets' status word (replays all-reduce the arena before the graph runs): gathered
+                # last, so a failed bucket is seen by the same host read as the validation words
+                if use_arena and self._world_size > 1 and arenas:
+                    oneshot_word = torch.zeros(1, dtype=torch.int32, device=next(iter(arenas.values())).device)
+                    words.append((oneshot_word, 0))
                 if len(words) > host_words.numel():
                     raise RuntimeError("GraphedCompute: more than 128 status words")
                 if words:
@@ -415,6 +421,7 @@ class GraphedCompute:
                 self._leaf_views.append((i, dt, tuple(leaves[i].shape), off))
                 off += leaves[i].numel()
         self._host_words = host_words[: len(words)] if words else None
+        self._oneshot_word = oneshot_word
         self._word_keep = words  # the flag tensors the graph reads
         self._err_members = [m for _, m in self._all_members if m._device_errors is not None and m._device_errors.is_cuda]
         self._n_err = len(self._err_members)
@@ -451,7 +458,8 @@ class GraphedCompute:
                     continue
                 comm = _sync.get_oneshot(None) if _sync._is_nccl(None) else None
                 if comm is not None and comm.supports(flat):
-                    comm.all_reduce(flat, kind)
+                    word = self._oneshot_word
+                    comm.all_reduce(flat, kind, word if word is not None and word.device == flat.device else None)
                 else:
                     _sync._all_reduce(flat, kind, None)
                 if kind == "mean":
@@ -465,6 +473,11 @@ class GraphedCompute:
         if self._host_words is not None:
             torch.cuda.current_stream().synchronize()
             codes = self._host_words.tolist()
+            if self._oneshot_word is not None and codes[-1]:
+                self._oneshot_word.zero_()
+                from torchmetrics_amd.utils import validation as _validation
+
+                _validation.raise_for_code(codes[-1])  # never hand out values from a failed sync
             if any(codes):
                 ne = self._n_err
                 for m, code in zip(self._err_members, codes[:ne]):

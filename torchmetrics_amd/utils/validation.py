@@ -23,6 +23,7 @@ PREDS_NAN = 1 << 4  # NaN in float preds where not allowed
 VALUE_NAN = 1 << 5  # NaN in an aggregation input with nan_strategy='error'
 NEG_VALUE = 1 << 6  # negative value where a non-negative one is required
 VALUE_NAN_WARN = 1 << 7  # NaN dropped by an aggregator with nan_strategy='warn': a warning, not an error
+ONESHOT_FAILED = 1 << 8  # the one-shot all-reduce of this metric's states timed out / was disowned by a peer
 
 _MESSAGES: Dict[int, str] = {
     TARGET_OUT_OF_RANGE: "Detected more unique values in `target` than expected. Expected only {num_classes} values"
@@ -47,6 +48,11 @@ def raise_for_code(code: int, metric: Any = None) -> None:
         code &= ~VALUE_NAN_WARN
         if not code:
             return
+    if code & ONESHOT_FAILED:
+        from torchmetrics_amd.parallel import oneshot
+
+        oneshot.disable_all()  # every rank raises here, so every rank falls back to RCCL together
+        raise RuntimeError(oneshot.failure_message())
     ctx = {"num_classes": getattr(metric, "num_classes", getattr(metric, "num_labels", "?"))}
     for bit, msg in _MESSAGES.items():
         if code & bit:

@@ -250,8 +250,209 @@ PyMethodDef kMethods[] = {
     {nullptr, nullptr, 0, nullptr},
 };
 
+// ------------------------------------------------------------------------------------------ native metric update
+// ``MulticlassConfusionMatrix.update`` as ONE native callable (installed as the instance's ``update``): the shape /
+// dtype / device checks of the reference's tensor validation (F/classification/stat_scores.py:281-319), the metric's
+// bookkeeping through its ``__dict__`` (``_update_count``, ``_computed``: what Metric._wrap_update does,
+// S/metric.py:459-481) and the kernel launch, with no Python frame in between.  Anything off the fast path -- CPU or
+// non-contiguous inputs, other ranks of input, a state not on the input's device, kwargs, ``compute_on_cpu`` -- goes to
+// the regular Python ``update`` (``fallback``), which raises the reference's exceptions.
+PyObject* g_k_confmat = nullptr;
+PyObject* g_k_err = nullptr;
+PyObject* g_k_count = nullptr;
+PyObject* g_k_computed = nullptr;
+PyObject* g_k_cpu = nullptr;
+PyObject* g_k_classes = nullptr;
+PyObject* g_k_ignore = nullptr;
+PyObject* g_k_validate = nullptr;
+
+struct NativeUpdate {
+  PyObject_HEAD
+  vectorcallfunc vectorcall;
+  PyObject* state;     // the metric's __dict__
+  PyObject* fallback;  // the Python update (Metric._wrap_update wrapper)
+  at::Tensor* sink;    // flag word for validate_args=False (kernels always have somewhere to report)
+  int64_t calls;       // fast-path calls (tests / benchmarks read it)
+};
+
+inline const at::Tensor* tensor_item(PyObject* dict, PyObject* key) {
+  PyObject* o = PyDict_GetItem(dict, key);  // borrowed
+  if (o == nullptr || !THPVariable_Check(o)) return nullptr;
+  return &THPVariable_Unpack(o);
+}
+
+// 1 = done, 0 = not handled (take the Python path), -1 = Python error set
+int confmat_fast(NativeUpdate* self, PyObject* a, PyObject* b) {
+  if (!THPVariable_Check(a) || !THPVariable_Check(b)) return 0;
+  const at::Tensor& p = THPVariable_Unpack(a);
+  const at::Tensor& t = THPVariable_Unpack(b);
+  if (!p.is_cuda() || !t.is_cuda()) return 0;
+  const auto pd = p.scalar_type();
+  const auto td = t.scalar_type();
+  if (pd != at::kBFloat16 && pd != at::kHalf && pd != at::kFloat) return 0;
+  if (td != at::kLong && td != at::kInt) return 0;
+  PyObject* st = self->state;
+  PyObject* co = PyDict_GetItem(st, g_k_classes);
+  if (co == nullptr || !PyLong_CheckExact(co)) return 0;
+  const long long C = PyLong_AsLongLong(co);
+  if (p.dim() != 2 || t.dim() != 1 || p.size(1) != C || p.size(0) != t.size(0) || p.size(0) == 0) return 0;
+  if (!p.is_contiguous() || !t.is_contiguous()) return 0;
+  const int dev = p.get_device();
+  if (t.get_device() != dev) return 0;
+  if (PyDict_GetItem(st, g_k_cpu) != Py_False) return 0;
+  const at::Tensor* cm = tensor_item(st, g_k_confmat);
+  if (cm == nullptr || !cm->is_cuda() || cm->get_device() != dev || cm->scalar_type() != at::kLong ||
+      !cm->is_contiguous() || cm->numel() != C * C)
+    return 0;
+  PyObject* vo = PyDict_GetItem(st, g_k_validate);
+  if (vo == nullptr) return 0;
+  const bool validate = vo == Py_True;
+  const at::Tensor* flag;
+  if (validate) {
+    flag = tensor_item(st, g_k_err);  // created by the first (Python) update on this device
+    if (flag == nullptr || !flag->is_cuda() || flag->get_device() != dev || flag->scalar_type() != at::kInt) return 0;
+  } else {
+    if (self->sink == nullptr || self->sink->get_device() != dev) {
+      delete self->sink;
+      self->sink = new at::Tensor(at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev)));
+    }
+    flag = self->sink;
+  }
+  PyObject* io = PyDict_GetItem(st, g_k_ignore);
+  if (io == nullptr) return 0;
+  long long ignore = 0;
+  const bool has_ignore = io != Py_None;
+  if (has_ignore) {
+    if (!PyLong_CheckExact(io)) return 0;
+    ignore = PyLong_AsLongLong(io);
+  }
+  PyObject* cnt = PyDict_GetItem(st, g_k_count);
+  if (cnt == nullptr || !PyLong_CheckExact(cnt)) return 0;
+  const long long n = PyLong_AsLongLong(cnt);
+  try {
+    tm_amd::mc_update(p, t, *cm, *flag, C, ignore, has_ignore, 0, false);
+  } catch (const c10::Error& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what_without_backtrace());
+    return -1;
+  }
+  PyObject* n1 = PyLong_FromLongLong(n + 1);
+  if (n1 == nullptr) return -1;
+  const int rc = PyDict_SetItem(st, g_k_count, n1);
+  Py_DECREF(n1);
+  if (rc != 0 || PyDict_SetItem(st, g_k_computed, Py_None) != 0) return -1;
+  ++self->calls;
+  return 1;
+}
+
+PyObject* native_update_vectorcall(PyObject* o, PyObject* const* args, size_t nargsf, PyObject* kwnames) {
+  auto* self = reinterpret_cast<NativeUpdate*>(o);
+  const Py_ssize_t nargs = PyVectorcall_NARGS(nargsf);
+  if (nargs == 2 && (kwnames == nullptr || PyTuple_GET_SIZE(kwnames) == 0)) {
+    const int r = confmat_fast(self, args[0], args[1]);
+    if (r == 1) Py_RETURN_NONE;
+    if (r < 0) return nullptr;
+  }
+  return PyObject_Vectorcall(self->fallback, args, nargsf, kwnames);
+}
+
+int native_update_traverse(PyObject* o, visitproc visit, void* arg) {
+  auto* self = reinterpret_cast<NativeUpdate*>(o);
+  Py_VISIT(self->state);
+  Py_VISIT(self->fallback);
+  return 0;
+}
+
+int native_update_clear(PyObject* o) {
+  auto* self = reinterpret_cast<NativeUpdate*>(o);
+  Py_CLEAR(self->state);
+  Py_CLEAR(self->fallback);
+  return 0;
+}
+
+void native_update_dealloc(PyObject* o) {
+  auto* self = reinterpret_cast<NativeUpdate*>(o);
+  PyObject_GC_UnTrack(o);
+  native_update_clear(o);
+  delete self->sink;
+  self->sink = nullptr;
+  Py_TYPE(o)->tp_free(o);
+}
+
+PyObject* native_update_wrapped(PyObject* o, void*) {
+  // what the Python wrapper wraps (the bound ``update``): ``is_overridden`` and ``inspect.signature`` unwrap to it
+  return PyObject_GetAttrString(reinterpret_cast<NativeUpdate*>(o)->fallback, "__wrapped__");
+}
+
+PyObject* native_update_fallback(PyObject* o, void*) {
+  PyObject* f = reinterpret_cast<NativeUpdate*>(o)->fallback;
+  Py_INCREF(f);
+  return f;
+}
+
+PyObject* native_update_calls(PyObject* o, void*) {
+  return PyLong_FromLongLong(reinterpret_cast<NativeUpdate*>(o)->calls);
+}
+
+PyGetSetDef kNativeUpdateGetSet[] = {
+    {"__wrapped__", native_update_wrapped, nullptr, nullptr, nullptr},
+    {"fallback", native_update_fallback, nullptr, nullptr, nullptr},
+    {"native_calls", native_update_calls, nullptr, nullptr, nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr},
+};
+
+PyTypeObject NativeUpdateType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+// confmat_updater(state_dict, fallback) -> callable
+PyObject* make_confmat_updater(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 2 || !PyDict_Check(args[0]) || !PyCallable_Check(args[1])) {
+    PyErr_SetString(PyExc_TypeError, "confmat_updater(state: dict, fallback: callable)");
+    return nullptr;
+  }
+  auto* self = PyObject_GC_New(NativeUpdate, &NativeUpdateType);
+  if (self == nullptr) return nullptr;
+  self->vectorcall = native_update_vectorcall;
+  Py_INCREF(args[0]);
+  self->state = args[0];
+  Py_INCREF(args[1]);
+  self->fallback = args[1];
+  self->sink = nullptr;
+  self->calls = 0;
+  PyObject_GC_Track(reinterpret_cast<PyObject*>(self));
+  return reinterpret_cast<PyObject*>(self);
+}
+
+PyMethodDef kFactoryMethods[] = {
+    {"confmat_updater", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&make_confmat_updater)),
+     METH_FASTCALL, "native MulticlassConfusionMatrix.update bound to a metric's __dict__"},
+    {nullptr, nullptr, 0, nullptr},
+};
+
 PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_fastcall", "dispatcher-free entry points of libtm_amd", -1, kMethods};
 
 }  // namespace
 
-PyMODINIT_FUNC PyInit__fastcall() { return PyModule_Create(&kModule); }
+PyMODINIT_FUNC PyInit__fastcall() {
+  NativeUpdateType.tp_name = "torchmetrics_amd._C._fastcall.NativeUpdate";
+  NativeUpdateType.tp_basicsize = sizeof(NativeUpdate);
+  NativeUpdateType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC | Py_TPFLAGS_HAVE_VECTORCALL;
+  NativeUpdateType.tp_vectorcall_offset = offsetof(NativeUpdate, vectorcall);
+  NativeUpdateType.tp_call = PyVectorcall_Call;
+  NativeUpdateType.tp_traverse = native_update_traverse;
+  NativeUpdateType.tp_clear = native_update_clear;
+  NativeUpdateType.tp_dealloc = native_update_dealloc;
+  NativeUpdateType.tp_getset = kNativeUpdateGetSet;
+  NativeUpdateType.tp_doc = "native metric update (see csrc/bindings/fastcall.cpp)";
+  if (PyType_Ready(&NativeUpdateType) < 0) return nullptr;
+  g_k_confmat = PyUnicode_InternFromString("confmat");
+  g_k_err = PyUnicode_InternFromString("_device_errors");
+  g_k_count = PyUnicode_InternFromString("_update_count");
+  g_k_computed = PyUnicode_InternFromString("_computed");
+  g_k_cpu = PyUnicode_InternFromString("compute_on_cpu");
+  g_k_classes = PyUnicode_InternFromString("num_classes");
+  g_k_ignore = PyUnicode_InternFromString("ignore_index");
+  g_k_validate = PyUnicode_InternFromString("validate_args");
+  PyObject* m = PyModule_Create(&kModule);
+  if (m == nullptr) return nullptr;
+  if (PyModule_AddFunctions(m, kFactoryMethods) < 0) return nullptr;
+  return m;
+}

@@ -1,0 +1,369 @@
+// fp64 matrix-core GEMM and power-iteration GEMV for FID's compute() (tr sqrt(Σ1 Σ2) by Newton-Schulz).
+//
+// Reference site: S/image/fid.py:159-179 (`_compute_fid`: `eigvals(sigma1 @ sigma2)` on a non-symmetric D x D fp64
+// matrix).  Our compute runs the coupled Newton-Schulz iteration (torchmetrics_amd/image/generative.py) -- three
+// D x D fp64 GEMMs per step -- entirely on these kernels, so no vendor GEMM (Tensile / rocBLAS) runs in compute().
+//
+// dgemm_nn_kernel: C_p = alpha_p * A_p B_p + beta_p * Cin_p + diag_p * I for up to kMaxBatch problems of one shape in
+// ONE launch (the Newton-Schulz update Y' = a Y W + b Y and Z' = a W Z + b Z are two GEMMs sharing W: batching them
+// gives 2 tiles per CU instead of 1 at D = 2048).  Row-major operands, M x K times K x N.
+//   * 128 x 128 C tile per block, 4 waves as 2 x 2, each wave 64 x 64 = 4 x 4 v_mfma_f64_16x16x4_f64 accumulators.
+//   * K chunk of 16, two LDS stages; chunk c+1 staged while chunk c is consumed, chunk c+2 in flight in registers.
+//     A is stored m-major (row stride 17 doubles: the 16 rows a wave reads at one k land on distinct banks), B k-major
+//     (row stride 144 doubles: consecutive k rows start 32 banks apart).
+//   * XCD-aware tile order: block b runs on XCD b % 8 (observed dispatch), so the tile id is remapped to give each XCD
+//     a contiguous range of tile ids, and tile ids walk groups of 4 tile rows column by column: the 32 tiles one XCD
+//     holds at D = 2048 are a 4 x 8 patch (A panels read by 8 tiles, B panels by 4, out of that XCD's L2).
+//   * Epilogue in registers (f64 C/D layout: col = lane & 15, row = (lane >> 4) + 4 r), coalesced 128-byte rows.
+// Numerics: fp64 products and fp64 accumulation in a fixed order (bitwise reproducible run to run).
+//
+// dgemv4_resid_kernel: one power-iteration step on 4 vectors, W = V - A V with V = Wprev / ||Wprev|| (column norms from
+// the previous step's fixed-order per-block partials, so every block normalises identically), and this step's
+// per-block partial squared norms.  V lives in LDS; one wave per row, 16-byte loads of A.
+#include <cstdlib>
+
+#include "../common/tm_common.h"
+
+namespace tm_amd {
+namespace {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kT = 128;        // C tile edge
+constexpr int kKC = 16;        // K chunk
+constexpr int kAStride = kKC + 1;
+constexpr int kBStride = kT + 16;
+constexpr int kMaxBatch = 2;
+constexpr int kGroupRows = 4;  // tile-row group of the L2-friendly order
+
+struct GemmProblem {
+  const double* a;
+  const double* b;
+  const double* cin;  // may be null (beta ignored)
+  double* c;
+  double alpha, beta, diag;
+};
+
+struct GemmBatch {
+  GemmProblem p[kMaxBatch];
+};
+
+__device__ __forceinline__ void tile_of(int t, int nti, int ntj, int& ti, int& tj) {
+  const int per_group = kGroupRows * ntj;
+  const int g = t / per_group;
+  const int r = t - g * per_group;
+  const int rows_in_group = min(kGroupRows, nti - g * kGroupRows);
+  tj = r / rows_in_group;
+  ti = g * kGroupRows + r % rows_in_group;
+}
+
+// kWC waves across the tile's columns (2 or 4), 2 down its rows: 4 waves (64 x 64 per wave, 16 accumulators) or 8
+// waves (64 x 32 per wave, 8 accumulators: two waves per SIMD at one block per CU, so one wave's LDS waits and barrier
+// hide under the other's MFMAs).
+template <int kWC>
+__global__ void __launch_bounds__(128 * kWC, 2)
+    dgemm_nn_kernel(GemmBatch batch, int nprob, int M, int N, int K, bool vec_ok) {
+  constexpr int kThr = 128 * kWC;
+  constexpr int kQ = 4 / (kWC / 2);           // 16-col MFMA tiles per wave (4 or 2)
+  constexpr int kPerA = kT * kKC / kThr;      // A doubles staged per thread (8 or 4)
+  constexpr int kPerB = kKC * kT / kThr;      // B doubles staged per thread
+  __shared__ __attribute__((aligned(16))) double As[2][kT * kAStride];
+  __shared__ __attribute__((aligned(16))) double Bs[2][kKC * kBStride];
+  const int nti = (M + kT - 1) / kT, ntj = (N + kT - 1) / kT;
+  const int per = nti * ntj;
+  const int total = per * nprob;
+  // XCD-aware remap: contiguous tile ids per XCD (when the grid divides evenly over 8 XCDs)
+  int t = blockIdx.x;
+  if (total % 8 == 0) t = (blockIdx.x % 8) * (total / 8) + blockIdx.x / 8;
+  const int pi = t / per;
+  int ti, tj;
+  tile_of(t - pi * per, nti, ntj, ti, tj);
+  const GemmProblem& pr = batch.p[pi];
+  const double* __restrict__ A = pr.a;
+  const double* __restrict__ B = pr.b;
+  const int i0 = ti * kT, j0 = tj * kT;
+
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave, lane = tid & (kWave - 1);
+  const int wr = wave / kWC, wc = wave % kWC;
+  constexpr int kWaveCols = kT / kWC;
+  // staging: A chunk 128 rows x 16 k (thread: one row, kPerA consecutive k); B chunk 16 k x 128 cols (thread: one k
+  // row, kPerB consecutive cols)
+  constexpr int kAThrPerRow = kKC / kPerA;
+  constexpr int kBThrPerRow = kT / kPerB;
+  const int ar = tid / kAThrPerRow, ak = (tid % kAThrPerRow) * kPerA;
+  const int bk = tid / kBThrPerRow, bc = (tid % kBThrPerRow) * kPerB;
+  double ra[kPerA], rb[kPerB];
+  auto load = [&](int k0) {
+    const int row = i0 + ar;
+    if (vec_ok && row < M && k0 + ak + kPerA <= K) {
+      const double* p = A + static_cast<long long>(row) * K + k0 + ak;
+#pragma unroll
+      for (int v = 0; v < kPerA / 2; ++v) {
+        const double2 x = *reinterpret_cast<const double2*>(p + 2 * v);
+        ra[2 * v] = x.x;
+        ra[2 * v + 1] = x.y;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < kPerA; ++e) {
+        const int k = k0 + ak + e;
+        ra[e] = (row < M && k < K) ? A[static_cast<long long>(row) * K + k] : 0.0;
+      }
+    }
+    const int kr = k0 + bk;
+    if (vec_ok && kr < K && j0 + bc + kPerB <= N) {
+      const double* p = B + static_cast<long long>(kr) * N + j0 + bc;
+#pragma unroll
+      for (int v = 0; v < kPerB / 2; ++v) {
+        const double2 x = *reinterpret_cast<const double2*>(p + 2 * v);
+        rb[2 * v] = x.x;
+        rb[2 * v + 1] = x.y;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < kPerB; ++e) {
+        const int c = j0 + bc + e;
+        rb[e] = (kr < K && c < N) ? B[static_cast<long long>(kr) * N + c] : 0.0;
+      }
+    }
+  };
+  auto store = [&](int s) {
+    double* a = &As[s][ar * kAStride + ak];
+#pragma unroll
+    for (int e = 0; e < kPerA; ++e) a[e] = ra[e];
+    double* b = &Bs[s][bk * kBStride + bc];
+#pragma unroll
+    for (int e = 0; e < kPerB; ++e) b[e] = rb[e];
+  };
+
+  f64x4 acc[4][kQ];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) acc[m][q] = f64x4{0.0, 0.0, 0.0, 0.0};
+
+  const int chunks = (K + kKC - 1) / kKC;
+  load(0);
+  store(0);
+  if (chunks > 1) load(kKC);
+  __syncthreads();
+  int s = 0;
+  for (int c = 0; c < chunks; ++c) {
+    const double* as = As[s];
+    const double* bs = Bs[s];
+#pragma unroll
+    for (int ks = 0; ks < kKC / 4; ++ks) {
+      const int k = ks * 4 + (lane >> 4);
+      double av[4], bv[kQ];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) av[m] = as[(wr * 64 + m * 16 + (lane & 15)) * kAStride + k];
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) bv[q] = bs[k * kBStride + wc * kWaveCols + q * 16 + (lane & 15)];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], bv[q], acc[m][q], 0, 0, 0);
+    }
+    if (c + 1 < chunks) {
+      store(s ^ 1);  // the other stage was released by the previous iteration's barrier
+      if (c + 2 < chunks) load((c + 2) * kKC);
+    }
+    __syncthreads();
+    s ^= 1;
+  }
+
+  double* __restrict__ C = pr.c;
+  const double* __restrict__ Cin = pr.cin;
+  const double alpha = pr.alpha, beta = pr.beta, dg = pr.diag;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int q = 0; q < kQ; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i0 + wr * 64 + m * 16 + (lane >> 4) + 4 * r;
+        const int col = j0 + wc * kWaveCols + q * 16 + (lane & 15);
+        if (row < M && col < N) {
+          const long long e = static_cast<long long>(row) * N + col;
+          double v = alpha * acc[m][q][r];
+          if (Cin != nullptr) v += beta * Cin[e];
+          if (row == col) v += dg;
+          C[e] = v;
+        }
+      }
+}
+
+// ----------------------------------------------------------------------------------------------- power iteration
+constexpr int kGemvThreads = 256;
+constexpr int kGemvRowsPerWave = 2;
+
+// w_out[i][c] = v[i][c] - sum_k A[i][k] v[k][c],  v = w_in / ||w_in[:, c]||  (normalize=false: v = w_in)
+// part_in: [nb_in][4] per-block partial squared norms of w_in; part_out: [gridDim.x][4] of w_out.
+__global__ void __launch_bounds__(kGemvThreads)
+    dgemv4_resid_kernel(const double* __restrict__ A, const double* __restrict__ w_in,
+                        const double* __restrict__ part_in, int nb_in, bool normalize, int d,
+                        double* __restrict__ w_out, double* __restrict__ part_out) {
+  extern __shared__ __attribute__((aligned(16))) double vs[];  // [d][4]
+  __shared__ double scale[4];
+  __shared__ double wsum[kGemvThreads / kWave][4];
+  const int tid = threadIdx.x;
+  if (tid < 4) {
+    double s = 1.0;
+    if (normalize) {
+      double acc = 0.0;
+      for (int b = 0; b < nb_in; ++b) acc += part_in[b * 4 + tid];  // fixed order: identical in every block
+      const double n = sqrt(acc);
+      s = 1.0 / (n > 1e-300 ? n : 1e-300);
+    }
+    scale[tid] = s;
+  }
+  __syncthreads();
+  for (int e = tid; e < d * 4; e += kGemvThreads) vs[e] = w_in[e] * scale[e & 3];
+  __syncthreads();
+  const int wave = tid / kWave, lane = tid & (kWave - 1);
+  double sq[4] = {0.0, 0.0, 0.0, 0.0};
+  const int row0 = (blockIdx.x * (kGemvThreads / kWave) + wave) * kGemvRowsPerWave;
+  for (int rr = 0; rr < kGemvRowsPerWave; ++rr) {
+    const int row = row0 + rr;
+    if (row >= d) break;  // wave-uniform
+    const double* ar = A + static_cast<long long>(row) * d;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    for (int k = lane * 2; k < d; k += 2 * kWave) {
+      double a0, a1;
+      if (k + 1 < d && ((d & 1) == 0)) {
+        const double2 x = *reinterpret_cast<const double2*>(ar + k);
+        a0 = x.x;
+        a1 = x.y;
+      } else {
+        a0 = ar[k];
+        a1 = k + 1 < d ? ar[k + 1] : 0.0;
+      }
+      const double* v0 = vs + k * 4;
+      s0 += a0 * v0[0];
+      s1 += a0 * v0[1];
+      s2 += a0 * v0[2];
+      s3 += a0 * v0[3];
+      if (k + 1 < d) {
+        s0 += a1 * v0[4];
+        s1 += a1 * v0[5];
+        s2 += a1 * v0[6];
+        s3 += a1 * v0[7];
+      }
+    }
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+      s0 += __shfl_xor(s0, off, kWave);
+      s1 += __shfl_xor(s1, off, kWave);
+      s2 += __shfl_xor(s2, off, kWave);
+      s3 += __shfl_xor(s3, off, kWave);
+    }
+    if (lane < 4) {
+      const double s = lane == 0 ? s0 : lane == 1 ? s1 : lane == 2 ? s2 : s3;
+      const double w = vs[row * 4 + lane] - s;
+      w_out[row * 4 + lane] = w;
+      sq[lane] += w * w;
+    }
+  }
+  if (lane < 4) wsum[wave][lane] = sq[lane];
+  __syncthreads();
+  if (tid < 4) {
+    double acc = 0.0;
+    for (int w = 0; w < kGemvThreads / kWave; ++w) acc += wsum[w][tid];
+    part_out[blockIdx.x * 4 + tid] = acc;
+  }
+}
+
+}  // namespace
+
+// C_i = alpha_i * A_i @ B_i + beta_i * Cin_i + diag_i * I  (fp64, row-major, all problems [M,K] x [K,N]);
+// a cin entry with no elements means "no Cin" (beta ignored); an empty list means none for every problem.
+void dgemm_nn(at::TensorList a, at::TensorList b, at::TensorList c, at::TensorList cin, at::ArrayRef<double> alpha,
+              at::ArrayRef<double> beta, at::ArrayRef<double> diag) {
+  const int np = static_cast<int>(a.size());
+  TORCH_CHECK(np >= 1 && np <= kMaxBatch, "dgemm_nn: 1..", kMaxBatch, " problems per launch");
+  TORCH_CHECK(static_cast<int>(b.size()) == np && static_cast<int>(c.size()) == np &&
+                  static_cast<int>(alpha.size()) == np && static_cast<int>(beta.size()) == np &&
+                  static_cast<int>(diag.size()) == np && (cin.empty() || static_cast<int>(cin.size()) == np),
+              "dgemm_nn: argument lists must have one entry per problem");
+  TM_CHECK_CUDA(a[0]);
+  const int M = static_cast<int>(a[0].size(0)), K = static_cast<int>(a[0].size(1));
+  const int N = static_cast<int>(b[0].size(1));
+  bool vec_ok = (K % 2 == 0) && (N % 2 == 0);
+  GemmBatch gb{};
+  for (int i = 0; i < np; ++i) {
+    for (const at::Tensor* t : {&a[i], &b[i], &c[i]}) {
+      TM_SAME_DEVICE(a[0], *t);
+      TM_CHECK_CONTIG(*t);
+      TORCH_CHECK(t->scalar_type() == at::kDouble && t->dim() == 2, "dgemm_nn: operands must be 2-D fp64");
+    }
+    TORCH_CHECK(a[i].size(0) == M && a[i].size(1) == K && b[i].size(0) == K && b[i].size(1) == N &&
+                    c[i].size(0) == M && c[i].size(1) == N,
+                "dgemm_nn: shape mismatch in problem ", i);
+    const double* cinp = nullptr;
+    if (!cin.empty() && cin[i].defined() && cin[i].numel() > 0) {
+      TM_SAME_DEVICE(a[0], cin[i]);
+      TM_CHECK_CONTIG(cin[i]);
+      TORCH_CHECK(cin[i].scalar_type() == at::kDouble && cin[i].numel() == static_cast<long long>(M) * N,
+                  "dgemm_nn: cin must be fp64 [M, N]");
+      cinp = cin[i].data_ptr<double>();
+    }
+    gb.p[i] = GemmProblem{a[i].data_ptr<double>(), b[i].data_ptr<double>(), cinp, c[i].data_ptr<double>(),
+                          alpha[i], beta[i], diag[i]};
+    vec_ok = vec_ok && reinterpret_cast<uintptr_t>(gb.p[i].a) % 16 == 0 &&
+             reinterpret_cast<uintptr_t>(gb.p[i].b) % 16 == 0;
+  }
+  if (M == 0 || N == 0) return;
+  const int tiles = ((M + kT - 1) / kT) * ((N + kT - 1) / kT) * np;
+  static const int waves = [] {
+    const char* e = std::getenv("TM_AMD_DGEMM_WAVES");  // tuning knob: 4 or 8 waves per 128 x 128 tile
+    return e ? std::atoi(e) : 8;
+  }();
+  if (waves == 4) {
+    hipLaunchKernelGGL(dgemm_nn_kernel<2>, dim3(tiles), dim3(256), 0, stream(), gb, np, M, N, K, vec_ok);
+  } else {
+    hipLaunchKernelGGL(dgemm_nn_kernel<4>, dim3(tiles), dim3(512), 0, stream(), gb, np, M, N, K, vec_ok);
+  }
+}
+
+// One power-iteration step (see dgemv4_resid_kernel); returns nothing, writes w_out [d, 4] and part_out [blocks, 4].
+int64_t dgemv4_blocks(int64_t d) {
+  const int rows_per_block = (kGemvThreads / kWave) * kGemvRowsPerWave;
+  return (d + rows_per_block - 1) / rows_per_block;
+}
+
+void dgemv4_resid(const at::Tensor& a, const at::Tensor& w_in, const at::Tensor& part_in, bool normalize,
+                  at::Tensor w_out, at::Tensor part_out) {
+  TM_CHECK_CUDA(a);
+  for (const at::Tensor* t : {&w_in, &part_in, const_cast<const at::Tensor*>(&w_out),
+                              const_cast<const at::Tensor*>(&part_out)}) {
+    TM_SAME_DEVICE(a, *t);
+    TM_CHECK_CONTIG(*t);
+    TORCH_CHECK(t->scalar_type() == at::kDouble, "dgemv4_resid: fp64 operands");
+  }
+  TM_CHECK_CONTIG(a);
+  const int d = static_cast<int>(a.size(0));
+  TORCH_CHECK(a.dim() == 2 && a.size(1) == d && a.scalar_type() == at::kDouble, "dgemv4_resid: A must be fp64 [d, d]");
+  TORCH_CHECK(w_in.numel() == 4LL * d && w_out.numel() == 4LL * d, "dgemv4_resid: vectors must be [d, 4]");
+  const int nb = static_cast<int>(dgemv4_blocks(d));
+  TORCH_CHECK(part_out.numel() == 4LL * nb, "dgemv4_resid: part_out must be [", nb, ", 4]");
+  TORCH_CHECK(!normalize || part_in.numel() % 4 == 0, "dgemv4_resid: part_in must be [blocks, 4]");
+  const size_t lds = static_cast<size_t>(d) * 4 * sizeof(double);
+  TORCH_CHECK(lds <= 128 * 1024, "dgemv4_resid: d too large for the LDS-resident vectors");
+  hipLaunchKernelGGL(dgemv4_resid_kernel, dim3(nb), dim3(kGemvThreads), lds, stream(), a.data_ptr<double>(),
+                     w_in.data_ptr<double>(), part_in.data_ptr<double>(), static_cast<int>(part_in.numel() / 4),
+                     normalize, d, w_out.data_ptr<double>(), part_out.data_ptr<double>());
+}
+
+TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def(
+      "dgemm_nn(Tensor[] a, Tensor[] b, Tensor(a!)[] c, Tensor[] cin, float[] alpha, float[] beta, float[] diag) -> ()");
+  m.def("dgemv4_blocks(int d) -> int", &dgemv4_blocks);
+  m.def("dgemv4_resid(Tensor a, Tensor w_in, Tensor part_in, bool normalize, Tensor(a!) w_out, Tensor(b!) part_out) -> ()");
+}
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
+  m.impl("dgemm_nn", &dgemm_nn);
+  m.impl("dgemv4_resid", &dgemv4_resid);
+}
+
+}  // namespace tm_amd

@@ -230,7 +230,7 @@ def _body_late_peer(rank, world, timeout_s, late_s):
         coll["mx"].update(torch.tensor([float(rank)], device=dev))
         coll["st"].update(p.to(dev), t.to(dev))
         # expected values over both ranks (stat scores from a gloo all_reduce of the local counts)
-        local_st = MulticlassStatScores(num_classes=4, average=None)
+        local_st = MulticlassStatScores(num_classes=4, average=None, sync_on_compute=False)
         local_st.update(p, t)
         exp_st = local_st.compute().clone()
         dist.all_reduce(exp_st)

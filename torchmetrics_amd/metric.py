@@ -594,6 +594,10 @@ class Metric(Module, ABC):
         self._update_signature = inspect.signature(self.update)
         self.update: Callable = self._wrap_update(self.update)  # type: ignore[method-assign]
         self.compute: Callable = self._wrap_compute(self.compute)  # type: ignore[method-assign]
+        self._install_native_update()
+
+    def _install_native_update(self) -> None:
+        """Hook: classes with a native ``update`` entry point install it over the Python wrapper here."""
 
     def __setattr__(self, name: str, value: Any) -> None:
         if name in _CONST_ATTRS:
@@ -700,6 +704,9 @@ class Metric(Module, ABC):
             name = prefix + key
             if name in state_dict:
                 setattr(self, key, state_dict.pop(name))
+                # loaded states invalidate a cached compute() result (the reference, S/metric.py:873-890, would keep
+                # returning the value of the states that were replaced)
+                self._computed = None
         super()._load_from_state_dict(state_dict, prefix, local_metadata, True, missing_keys, unexpected_keys, error_msgs)
 
     def _filter_kwargs(self, **kwargs: Any) -> Dict[str, Any]:

@@ -14,7 +14,7 @@ import os
 import struct
 import threading
 from pathlib import Path
-from typing import List, Optional, Sequence, Union
+from typing import Any, List, Optional, Sequence, Union
 
 import torch
 from torch import Tensor
@@ -61,6 +61,19 @@ def _fast():
     if _fast_mod is None:
         load_native(strict=True)
     return _fast_mod
+
+
+def native_updater(kind: str, state: dict, fallback: Any) -> Any:
+    """A native ``update`` callable bound to a metric's ``__dict__`` (``csrc/bindings/fastcall.cpp``), or ``None``
+    where it does not apply (no GPU, native library missing, ``TORCHMETRICS_AMD_STRICT=1``).  Inputs off its fast path
+    go to ``fallback`` (the metric's Python update)."""
+    from torchmetrics_amd.utils import validation
+
+    if validation.STRICT or not torch.cuda.is_available() or not load_native(strict=False):
+        return None
+    mod = _fast_mod
+    factory = getattr(mod, f"{kind}_updater", None) if not isinstance(mod, _DispatcherShim) else None
+    return factory(state, fallback) if factory is not None else None
 
 
 def native_library_path() -> Path:
@@ -466,6 +479,50 @@ def feature_moments_update(features: Tensor, feat_sum: Tensor, feat_cov: Tensor)
         _ops().feature_moments_update(features.contiguous(), feat_sum, feat_cov)
     else:
         _cpu.feature_moments_update(features, feat_sum, feat_cov)
+
+
+_EMPTY_F64: dict = {}
+
+
+def dgemm(a: Union[Tensor, Sequence[Tensor]], b: Union[Tensor, Sequence[Tensor]], out: Union[Tensor, Sequence[Tensor]],
+          alpha: Union[float, Sequence[float]] = 1.0, beta: Union[float, Sequence[float]] = 0.0,
+          cin: Optional[Union[Tensor, Sequence[Optional[Tensor]]]] = None,
+          diag: Union[float, Sequence[float]] = 0.0) -> None:
+    """``out_i = alpha_i a_i @ b_i + beta_i cin_i + diag_i I`` in fp64 on the matrix cores (``csrc/image/dgemm.hip``);
+    one or two problems of one shape per launch.  CPU: the same formula with torch ops."""
+    def seq(x, n):
+        return list(x) if isinstance(x, (list, tuple)) else [x] * n
+
+    single = isinstance(a, Tensor)
+    a_l = [a] if single else list(a)
+    n = len(a_l)
+    b_l, o_l = seq(b, n) if not single else [b], seq(out, n) if not single else [out]
+    al, be, dg, ci = seq(alpha, n), seq(beta, n), seq(diag, n), seq(cin, n)
+    if a_l[0].is_cuda:
+        dev = a_l[0].device
+        empty = _EMPTY_F64.get(dev)
+        if empty is None:
+            empty = _EMPTY_F64[dev] = torch.empty(0, dtype=torch.float64, device=dev)
+        _ops().dgemm_nn(a_l, b_l, o_l, [c if c is not None else empty for c in ci], [float(x) for x in al],
+                        [float(x) for x in be], [float(x) for x in dg])
+        return
+    for i in range(n):
+        r = al[i] * (a_l[i] @ b_l[i])
+        if ci[i] is not None:
+            r = r + be[i] * ci[i]
+        if dg[i]:
+            r = r + dg[i] * torch.eye(r.shape[0], r.shape[1], dtype=r.dtype)
+        o_l[i].copy_(r)
+
+
+def dgemv4_blocks(d: int) -> int:
+    return int(_ops().dgemv4_blocks(d))
+
+
+def dgemv4_resid(a: Tensor, w_in: Tensor, part_in: Tensor, normalize: bool, w_out: Tensor, part_out: Tensor) -> None:
+    """One power-iteration step on 4 vectors: ``w_out = v - a v`` with ``v = w_in / ||w_in||`` (column norms from the
+    previous step's per-block partials ``part_in``); writes this step's partial squared norms into ``part_out``."""
+    _ops().dgemv4_resid(a, w_in, part_in, normalize, w_out, part_out)
 
 
 # ------------------------------------------------------------------------------ fused compute() of a collection

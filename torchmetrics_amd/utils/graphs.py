@@ -334,7 +334,12 @@ class GraphedCompute:
                     views[id(t)] = flat[off : off + t.numel()].view(t.shape)
                     off += t.numel()
                 arenas[key] = flat
+        # the one-shot buckets' status word (replays all-reduce the arena BEFORE the graph runs; allocated here, outside
+        # the capture, so no captured memset clears it): the graph gathers it with the validation words, and one host
+        # read after the replay sees a failed bucket
         oneshot_word: Optional[Tensor] = None
+        if use_arena and self._world_size > 1 and arenas:
+            oneshot_word = torch.zeros(1, dtype=torch.int32, device=next(iter(arenas.values())).device)
         words = [(m._device_errors, 0) for _, m in self._all_members
                  if m._device_errors is not None and m._device_errors.is_cuda]
         graph = torch.cuda.CUDAGraph()
@@ -389,11 +394,8 @@ class GraphedCompute:
                     if flat.numel() != 1 or flat.dtype not in _WORD_CODES:
                         flat = flat.to(torch.int32).amax().reshape(1)
                     words.append((flat, _WORD_CODES[flat.dtype]))
-                # the one-shot buckets' status word (replays all-reduce the arena before the graph runs): gathered
-                # last, so a failed bucket is seen by the same host read as the validation words
-                if use_arena and self._world_size > 1 and arenas:
-                    oneshot_word = torch.zeros(1, dtype=torch.int32, device=next(iter(arenas.values())).device)
-                    words.append((oneshot_word, 0))
+                if oneshot_word is not None:
+                    words.append((oneshot_word, 0))  # gathered last (see its allocation above)
                 if len(words) > host_words.numel():
                     raise RuntimeError("GraphedCompute: more than 128 status words")
                 if words:

@@ -70,12 +70,19 @@ def _data(device: torch.device, rank: int, ring_mb: int):
     return preds, target
 
 
-def _run(metric, preds, target, steps: int, warmup: int, device, world):
+def _warm(metric, preds, target, warmup: int) -> None:
+    """W untimed warm-up updates, then compute() and reset() (the state the timed region starts from)."""
     nbuf = len(preds)
     for i in range(warmup):
         metric.update(preds[i % nbuf], target[i % nbuf])
-    metric.compute() if hasattr(metric, "_computed") else metric.compute()
+    metric.compute()
     _reset(metric)
+
+
+def _timed(metric, preds, target, steps: int, warmup: int, device, world):
+    """EXACTLY ``steps`` updates and one synced compute(), bracketed by barrier + synchronize; then the synced
+    compute() wall-clock on its own (5 reps)."""
+    nbuf = len(preds)
     _barrier_sync(device, world)
     t0 = time.perf_counter()
     for i in range(steps):
@@ -121,18 +128,25 @@ def main() -> None:
     comm_stats(reset=True)
 
     ours = MulticlassConfusionMatrix(num_classes=NUM_CLASSES).to(device)
-    t_ours, cms_ours, res_ours = _run(ours, preds, target, args.steps, args.warmup, device, world)
+    ref = None
+    if not args.no_baseline:
+        from benchmarks.reference_path import ReferenceEmulatedConfusionMatrix
+
+        ref = ReferenceEmulatedConfusionMatrix(NUM_CLASSES, device)
+    # both implementations get their W warm-up updates before either is timed (a region that directly follows a long
+    # idle period -- data generation -- runs on a cold host launch path; see profiles/r03_first_region.md)
+    _warm(ours, preds, target, args.warmup)
+    if ref is not None:
+        _warm(ref, preds, target, args.warmup)
+    t_ours, cms_ours, res_ours = _timed(ours, preds, target, args.steps, args.warmup, device, world)
     comms = comm_stats()
     t_ours = _max_over_ranks(t_ours, device, world)
     cms_ours = _max_over_ranks(cms_ours, device, world)
 
     base_val = None
     t_ref = cms_ref = None
-    if not args.no_baseline:
-        from benchmarks.reference_path import ReferenceEmulatedConfusionMatrix
-
-        ref = ReferenceEmulatedConfusionMatrix(NUM_CLASSES, device)
-        t_ref, cms_ref, res_ref = _run(ref, preds, target, args.steps, args.warmup, device, world)
+    if ref is not None:
+        t_ref, cms_ref, res_ref = _timed(ref, preds, target, args.steps, args.warmup, device, world)
         t_ref = _max_over_ranks(t_ref, device, world)
         cms_ref = _max_over_ranks(cms_ref, device, world)
         if not torch.equal(res_ref.to(res_ours.device), res_ours):

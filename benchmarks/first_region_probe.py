@@ -1,0 +1,89 @@
+"""Fresh-process first-region cost of the headline loop (bench.py's exact shape: 406 MB ring, W warm-up updates,
+compute, reset, sync, then ONE timed region of 20 updates + compute + sync).  Each case runs in its own process:
+
+  python benchmarks/first_region_probe.py <case>   (case: plain | inplace_reset | warm50 | sleep10ms)
+Environment variables (e.g. HSA_ENABLE_INTERRUPT) are inherited from the caller.  Prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from torchmetrics_amd.classification import MulticlassConfusionMatrix  # noqa: E402
+
+C, B, K = 1000, 8192, 26
+
+
+def main():
+    case = sys.argv[1] if len(sys.argv) > 1 else "plain"
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(1234)
+    preds = [torch.randn(B, C, generator=g, device=dev).to(torch.bfloat16) for _ in range(K)]
+    target = [torch.randint(0, C, (B,), generator=g, device=dev) for _ in range(K)]
+    m = MulticlassConfusionMatrix(num_classes=C).to(dev)
+    import gc
+
+    if case == "nogc":
+        gc.collect()
+        gc.disable()
+    warm = 50 if case == "warm50" else 5
+    for i in range(warm):
+        m.update(preds[i % K], target[i % K])
+    m.compute()
+    m.reset()  # (refills the state in place when unobserved)
+    torch.cuda.synchronize()
+    if case == "sleep10ms":
+        time.sleep(0.01)
+    if case == "launches200":
+        x = torch.zeros(1, device=dev)
+        for _ in range(200):
+            x.add_(1)
+        torch.cuda.synchronize()
+    if case == "cpuspin20":
+        t_s = time.perf_counter()
+        while time.perf_counter() - t_s < 0.02:
+            pass
+    if case == "heavyspin20":
+        a = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
+        t_s = time.perf_counter()
+        while time.perf_counter() - t_s < 0.02:
+            a = (a @ a).clamp_(-1, 1)
+            torch.cuda.synchronize()
+    if case == "readring":
+        acc = torch.zeros((), device=dev)
+        for p in preds:
+            acc += p.float().sum()
+        torch.cuda.synchronize()
+    if case == "gpuspin20":
+        x = torch.zeros(1, device=dev)
+        t_s = time.perf_counter()
+        while time.perf_counter() - t_s < 0.02:
+            x.add_(1)
+        torch.cuda.synchronize()
+    out = {"case": case, "env_interrupt": os.environ.get("HSA_ENABLE_INTERRUPT")}
+    for rep in range(3):
+        torch.cuda.synchronize()
+        gc0 = gc.get_count()
+        ts = []
+        t0 = time.perf_counter()
+        for i in range(20):
+            m.update(preds[(5 + 20 * rep + i) % K], target[(5 + 20 * rep + i) % K])
+            ts.append(time.perf_counter())
+        t1 = time.perf_counter()
+        out[f"per_update{rep}"] = [round(1e6 * (b - a), 1) for a, b in zip([t0] + ts[:-1], ts)]
+        out[f"gc{rep}"] = [gc0, gc.get_count()]
+        m.compute()
+        t2 = time.perf_counter()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        out[f"rep{rep}"] = [round(1e6 * (t3 - t0), 1), round(1e6 * (t1 - t0), 1), round(1e6 * (t2 - t1), 1),
+                            round(1e6 * (t3 - t2), 1)]
+        m.reset()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -102,3 +102,27 @@ def test_gpu_fast_path_semantics():
     m3 = m3.to("cpu")
     m3.update(p.cpu(), t.cpu())
     assert int(m3.compute().sum()) == 128
+
+
+def test_reset_refills_unobserved_state_in_place():
+    """``Metric.reset`` refills a state's own memory only when nothing can observe it (no other reference, no view);
+    otherwise it allocates a fresh default like the reference (S/metric.py:673-688)."""
+    g = torch.Generator().manual_seed(1)
+    m = tm.MulticlassConfusionMatrix(5)
+    m.update(torch.randn(10, 5, generator=g), torch.randint(0, 5, (10,), generator=g))
+    ident = id(m.confmat)
+    m.reset()
+    assert id(m.confmat) == ident and int(m.confmat.sum()) == 0
+    m.update(torch.randn(10, 5, generator=g), torch.randint(0, 5, (10,), generator=g))
+    held = m.compute()
+    m.reset()
+    assert int(held.sum()) == 10 and int(m.confmat.sum()) == 0  # a returned result is never clobbered
+    m.update(torch.randn(10, 5, generator=g), torch.randint(0, 5, (10,), generator=g))
+    view = m.confmat[0]
+    before = view.clone()
+    m.reset()
+    assert torch.equal(view, before)  # nor is a view of the old state
+    mx = tm.MaxMetric()
+    mx.update(torch.tensor(3.0))
+    mx.reset()
+    assert float(mx.max_value) == float("-inf")  # non-zero defaults are restored too

@@ -1,0 +1,195 @@
+// Device time per launch of the headline confusion-matrix update over a 406 MB input ring (26 x 8192 x 1000 bf16,
+// larger than the 256 MB MALL, as bench.py streams it), back-to-back launches timed with HIP events.
+// Variants isolate the costs: empty launch, pure streaming read, argmax without / with the int64 atomics, and launch
+// shapes (one row per wave vs two).  Build: hipcc -O3 --offload-arch=gfx950 confmat_ring_mb.hip -o confmat_ring_mb
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                               \
+  do {                                                                      \
+    hipError_t e = (x);                                                     \
+    if (e != hipSuccess) {                                                  \
+      std::printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); \
+      std::exit(1);                                                         \
+    }                                                                       \
+  } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__global__ void empty_kernel(int* p) {
+  if (p == nullptr && threadIdx.x == 1234) *p = 0;
+}
+
+// pure read floor: each wave reads rows (kPer x 16 B per lane), xor-folds them, writes nothing
+template <int kPer, int kRowsPerWave>
+__global__ void __launch_bounds__(256) vread(const uint16_t* __restrict__ preds, int N, int C, int* __restrict__ sink) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
+  const int nchunks = C / 8;
+  uint32_t x = 0;
+#pragma unroll
+  for (int r = 0; r < kRowsPerWave; ++r) {
+    const int row = wave * kRowsPerWave + r;
+    if (row >= N) break;
+    const u32x4* rp = reinterpret_cast<const u32x4*>(preds + (long long)row * C);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int ci = lane + j * 64;
+      if (ci < nchunks) {
+        const u32x4 v = __builtin_nontemporal_load(rp + ci);
+        x ^= v[0] ^ v[1] ^ v[2] ^ v[3];
+      }
+    }
+  }
+  if (x == 0x12345678u) sink[0] = x;
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  return static_cast<uint32_t>(__reduce_max_sync(~0ull, static_cast<int>(v ^ 0x80000000u))) ^ 0x80000000u;
+}
+
+// production-style ordinal argmax (see csrc/classification/stat_scores.hip mc_argmax_ord16_kernel), all rows of a
+// wave's share loaded up front; kMode 0: int64 atomic into confmat, 1: label store only, 2: int32 atomic
+template <int kPer, int kRowsPerWave, int kMode>
+__global__ void __launch_bounds__(256) vord(const uint16_t* __restrict__ preds, const int64_t* __restrict__ target,
+                                            int N, int C, unsigned long long* __restrict__ out,
+                                            int* __restrict__ lab) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
+  const int nchunks = C / 8;
+  u32x4 buf[kRowsPerWave][kPer];
+  long long t[kRowsPerWave];
+#pragma unroll
+  for (int r = 0; r < kRowsPerWave; ++r) {
+    const int row = wave * kRowsPerWave + r;
+    const u32x4* rp = reinterpret_cast<const u32x4*>(preds + (long long)(row < N ? row : 0) * C);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int ci = lane + j * 64;
+      if (ci < nchunks) buf[r][j] = __builtin_nontemporal_load(rp + ci);
+    }
+    t[r] = lane == 0 && row < N ? target[row] : 0;
+  }
+#pragma unroll
+  for (int r = 0; r < kRowsPerWave; ++r) {
+    const int row = wave * kRowsPerWave + r;
+    if (row >= N) break;
+    u16x2 mx = {0, 0};
+    uint32_t ordw[kPer][4];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int ci = lane + j * 64;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t w = buf[r][j][k];
+        const s16x2 sw = __builtin_bit_cast(s16x2, w);
+        const uint32_t sgn = __builtin_bit_cast(uint32_t, static_cast<s16x2>(sw >> (s16x2){15, 15}));
+        const uint32_t o = w ^ (sgn | 0x80008000u);
+        ordw[j][k] = o;
+        if (ci < nchunks) mx = __builtin_elementwise_max(mx, __builtin_bit_cast(u16x2, o));
+      }
+    }
+    const uint32_t lmax = mx.x > mx.y ? mx.x : mx.y;
+    uint32_t first = 0xffffu;
+#pragma unroll
+    for (int j = kPer - 1; j >= 0; --j) {
+      const int ci = lane + j * 64;
+      if (ci < nchunks) {
+#pragma unroll
+        for (int k = 3; k >= 0; --k) {
+          const uint32_t o = ordw[j][k];
+          if ((o >> 16) == lmax) first = ci * 8 + 2 * k + 1;
+          if ((o & 0xffffu) == lmax) first = ci * 8 + 2 * k;
+        }
+      }
+    }
+    const uint32_t key = wave_max_u32((lmax << 16) | (0xffffu - first));
+    const int bidx = 0xffff - static_cast<int>(key & 0xffffu);
+    if (lane == 0) {
+      if (kMode == 0) atomicAdd(out + t[r] * C + bidx, 1ull);
+      else if (kMode == 1) lab[row] = bidx;
+      else atomicAdd(reinterpret_cast<unsigned int*>(out) + t[r] * C + bidx, 1u);
+    }
+  }
+}
+
+int main() {
+  const int N = 8192, C = 1000, NB = 26;
+  int cus = 256;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  std::vector<uint16_t> h(static_cast<size_t>(N) * C);
+  std::vector<int64_t> ht(N);
+  uint32_t s = 12345;
+  auto rnd = [&] {
+    s = s * 1664525u + 1013904223u;
+    return s;
+  };
+  uint16_t* dp[NB];
+  int64_t* dt[NB];
+  for (int b = 0; b < NB; ++b) {
+    for (auto& x : h) {
+      float f = ((rnd() >> 8) / 16777216.0f - 0.5f) * 6.f;
+      uint32_t u;
+      std::memcpy(&u, &f, 4);
+      x = (uint16_t)(u >> 16);
+    }
+    for (auto& t : ht) t = rnd() % C;
+    CK(hipMalloc(&dp[b], h.size() * 2));
+    CK(hipMalloc(&dt[b], N * 8));
+    CK(hipMemcpy(dp[b], h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dt[b], ht.data(), N * 8, hipMemcpyHostToDevice));
+  }
+  unsigned long long* out;
+  int* lab;
+  CK(hipMalloc(&out, (size_t)C * C * 8));
+  CK(hipMalloc(&lab, N * 4));
+  CK(hipMemset(out, 0, (size_t)C * C * 8));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int reps = 520;
+  auto timeit = [&](const char* name, auto launch) {
+    for (int i = 0; i < 52; ++i) launch(i % NB);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i) launch(i % NB);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::printf("{\"variant\": \"%s\", \"us\": %.3f, \"TBps\": %.2f}\n", name, ms * 1e3 / reps,
+                (double)N * C * 2 / (ms * 1e-3 / reps) / 1e12);
+    std::fflush(stdout);
+  };
+  timeit("empty_2048x256", [&](int) { hipLaunchKernelGGL(empty_kernel, dim3(2048), dim3(256), 0, 0, lab); });
+  timeit("empty_1x64", [&](int) { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, 0, lab); });
+  timeit("read_1row", [&](int b) { hipLaunchKernelGGL((vread<2, 1>), dim3(N / 4), dim3(256), 0, 0, dp[b], N, C, lab); });
+  timeit("read_2row", [&](int b) { hipLaunchKernelGGL((vread<2, 2>), dim3(N / 8), dim3(256), 0, 0, dp[b], N, C, lab); });
+  timeit("read_4row", [&](int b) { hipLaunchKernelGGL((vread<2, 4>), dim3(N / 16), dim3(256), 0, 0, dp[b], N, C, lab); });
+  timeit("ord_1row_i64atomic", [&](int b) {
+    hipLaunchKernelGGL((vord<2, 1, 0>), dim3(N / 4), dim3(256), 0, 0, dp[b], dt[b], N, C, out, lab);
+  });
+  timeit("ord_1row_label", [&](int b) {
+    hipLaunchKernelGGL((vord<2, 1, 1>), dim3(N / 4), dim3(256), 0, 0, dp[b], dt[b], N, C, out, lab);
+  });
+  timeit("ord_1row_i32atomic", [&](int b) {
+    hipLaunchKernelGGL((vord<2, 1, 2>), dim3(N / 4), dim3(256), 0, 0, dp[b], dt[b], N, C, out, lab);
+  });
+  timeit("ord_2row_i64atomic", [&](int b) {
+    hipLaunchKernelGGL((vord<2, 2, 0>), dim3(N / 8), dim3(256), 0, 0, dp[b], dt[b], N, C, out, lab);
+  });
+  timeit("ord_4row_i64atomic", [&](int b) {
+    hipLaunchKernelGGL((vord<2, 4, 0>), dim3(N / 16), dim3(256), 0, 0, dp[b], dt[b], N, C, out, lab);
+  });
+  timeit("ord_2row_label", [&](int b) {
+    hipLaunchKernelGGL((vord<2, 2, 1>), dim3(N / 8), dim3(256), 0, 0, dp[b], dt[b], N, C, out, lab);
+  });
+  return 0;
+}

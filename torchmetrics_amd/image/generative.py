@@ -51,19 +51,24 @@ def _ns_schedule(low: float, tol: float = 1e-10) -> List[float]:
     return alphas
 
 
-def _ns_floor(apply, v: Tensor, iters: int = 8) -> Tuple[float, float]:
-    """Estimates of the smallest eigenvalue ``p`` of an operator with real spectrum in [0, 1] (``apply(v) = B v``)
-    after ``iters`` and ``2 iters`` steps of power iteration on ``I - B`` (dominant eigenvalue ``1 - p_min``), 4
-    vectors at once.  Power iteration approaches from below, so both over-estimate p_min; their agreement says whether
-    the estimate can be trusted."""
-    out = []
-    for _ in range(2):
-        for _ in range(iters):
-            w = v - apply(v)
-            v = w / w.norm(dim=0, keepdim=True).clamp(min=1e-300)
-        out.append(1.0 - (v - apply(v)).norm(dim=0).max().clamp(max=1.0))
-    first, second = torch.stack(out).tolist()
-    return first, second
+def _ns_floor(a0: Tensor, v: Tensor, iters: int = 8) -> Tensor:
+    """Estimates of the smallest eigenvalue ``p`` of ``a0`` (real spectrum in [0, 1]) after ``iters`` and ``2 iters``
+    steps of power iteration on ``I - a0`` (dominant eigenvalue ``1 - p_min``), 4 vectors at once, as a device
+    tensor ``[2]``.  Power iteration approaches from below, so both over-estimate p_min; their agreement says whether
+    the estimate can be trusted.  Each step is ONE ``dgemv4_resid`` launch (``w = v - a0 v`` with the previous step's
+    normalisation folded in); the estimate after ``k`` steps is the norm of step ``k + 1``, which is also the first
+    step of the next round, so 2 iters + 1 launches in all."""
+    d = a0.shape[0]
+    nb = ops.dgemv4_blocks(d, a0.device)
+    w = [torch.empty(d, 4, dtype=a0.dtype, device=a0.device) for _ in range(2)]
+    part = [torch.empty(nb, 4, dtype=a0.dtype, device=a0.device) for _ in range(2)]
+    ops.dgemv4_resid(a0, v.contiguous(), part[1], False, w[0], part[0])
+    ests = []
+    for k in range(1, 2 * iters + 1):
+        ops.dgemv4_resid(a0, w[(k - 1) % 2], part[(k - 1) % 2], True, w[k % 2], part[k % 2])
+        if k == iters or k == 2 * iters:
+            ests.append(1.0 - part[k % 2].sum(0).sqrt().max().clamp(max=1.0))
+    return torch.stack(ests)
 
 
 def _trace_sqrt_newton_schulz(sigma1: Tensor, sigma2: Tensor, rtol: float = 1e-8,
@@ -71,35 +76,50 @@ def _trace_sqrt_newton_schulz(sigma1: Tensor, sigma2: Tensor, rtol: float = 1e-8
     """``tr sqrt(Σ1 Σ2)`` by the coupled Newton-Schulz iteration ``T = a (3I - a² Z Y) / 2, Y <- Y T, Z <- T Z`` on
     ``Y0 = P / c`` (``P = Σ1 Σ2``, ``c`` >= its spectral radius: min of trace and the max row / column abs sums, all
     valid because P's eigenvalues are real and >= 0), ``Z0 = I``: ``Y -> (P / c)^{1/2}``, ``Z -> (P / c)^{-1/2}``.
-    The iterates are polynomials in P, so the non-symmetric product needs no Cholesky factor; each step is three fp64
-    GEMMs with the scaling folded into ``addmm``'s alpha / beta.  None when it does not converge.
+    The iterates are polynomials in P, so the non-symmetric product needs no Cholesky factor.
+
+    Every matrix product is our fp64 matrix-core GEMM (``ops.dgemm``, ``csrc/image/dgemm.hip``) with the update fused
+    into its epilogue: with ``W = Z Y``, ``Y' = a Y W + b Y`` and ``Z' = a W Z + b Z`` (``T = b I + a W``) run as ONE
+    batched launch sharing ``W``; the first step (``Z0 = I``) is one GEMM ``Y0²`` plus an elementwise ``Z1``.  No vendor
+    GEMM runs in compute().
 
     The Chen-Chow schedule needs a floor for the smallest ``sqrt(λ / c)``: first from a short power iteration when
     that settles (well-conditioned covariances: 7 steps on the 50k x 2048 bench), else -- or when one unscaled probe
     step still moves ``tr Y`` by more than ``rtol`` (convergence is quadratic: a probe step of 1e-8 leaves ~1e-16) --
-    a fresh run with floor 1e-6 (a schedule cannot be resumed: its first scale factors
-    collapse the converged eigenvalues).  Covariance products with eigenvalues below that (rank-deficient or
-    extremely ill-conditioned: |Z| ~ P^{-1/2} explodes and its rounding feeds back through ``Z Y``) return None and
-    the caller takes the eigensolve."""
-    p = sigma1 @ sigma2
-    d = p.shape[0]
+    a fresh run with floor 1e-6 (a schedule cannot be resumed: its first scale factors collapse the converged
+    eigenvalues).  Covariance products with eigenvalues below that (rank-deficient or extremely ill-conditioned: |Z| ~
+    P^{-1/2} explodes and its rounding feeds back through ``Z Y``) return None and the caller takes the eigensolve.
+    Host reads: one for the two floor estimates, one per schedule for (tr before, tr after, max |Z|)."""
+    d = sigma1.shape[0]
+    p = torch.empty_like(sigma1)
+    ops.dgemm(sigma1.contiguous(), sigma2.contiguous(), p)
     tr_p = p.diagonal().sum()
     c = torch.minimum(torch.minimum(tr_p, p.abs().sum(1).max()), p.abs().sum(0).max())
     c = torch.where(c > 0, c, torch.ones_like(c))
-    eye = torch.eye(d, dtype=p.dtype, device=p.device)
     a0 = p / c
     gen = torch.Generator(device=p.device).manual_seed(0)
     v0 = torch.rand(d, 4, dtype=p.dtype, device=p.device, generator=gen)
-    p_short, p_long = _ns_floor(lambda v: a0 @ v, v0)
+    p_short, p_long = _ns_floor(a0, v0).tolist()
     floors = ([0.5 * math.sqrt(p_long)] if p_long > 0 and abs(p_short - p_long) <= 0.25 * p_long else []) + [1e-6]
+    bufs = [torch.empty_like(p) for _ in range(5)]
     for low in floors:
-        y, z = a0, eye
-        for a in _ns_schedule(low):
-            t = torch.addmm(eye, z, y, beta=1.5 * a, alpha=-0.5 * a ** 3)
-            y, z = y @ t, t @ z
-        before = y.diagonal().sum()
-        t = torch.addmm(eye, z, y, beta=1.5, alpha=-0.5)  # probe: one unscaled step
-        y, z = y @ t, t @ z
+        sched = (_ns_schedule(low) or [1.0]) + [1.0]  # the last, unscaled step is the convergence probe
+        y, z = bufs[0], bufs[1]  # current iterates
+        yn, zn, w = bufs[2], bufs[3], bufs[4]  # next iterates, W = Z Y
+        before = None
+        for i, a in enumerate(sched):
+            beta, alpha = 1.5 * a, -0.5 * a ** 3
+            if i == 0:
+                ops.dgemm(a0, a0, y, alpha=alpha, beta=beta, cin=a0)  # Y1 = Y0 T = b Y0 + a Y0²  (Z0 = I)
+                torch.mul(a0, alpha, out=z)  # Z1 = T = b I + a Y0
+                z.diagonal().add_(beta)
+                continue
+            if i == len(sched) - 1:
+                before = y.diagonal().sum()
+            ops.dgemm(z, y, w)  # W = Z Y
+            ops.dgemm([y, w], [w, z], [yn, zn], alpha=[alpha, alpha], beta=[beta, beta], cin=[y, z])
+            y, yn = yn, y
+            z, zn = zn, z
         before, after, zmax = torch.stack([before, y.diagonal().sum(), z.abs().max()]).tolist()
         if math.isfinite(after) and abs(after - before) <= rtol * abs(after) and zmax <= zcap:
             return c.sqrt() * y.diagonal().sum()
@@ -317,10 +337,12 @@ class FrechetInceptionDistance(_FeatureNetMetric):
             raise RuntimeError("More than one sample is required for both the real and fake distributed to compute FID")
         mean_real = (self.real_features_sum / self.real_features_num_samples).unsqueeze(0)
         mean_fake = (self.fake_features_sum / self.fake_features_num_samples).unsqueeze(0)
-        cov_real = (self.real_features_cov_sum - self.real_features_num_samples * mean_real.t().mm(mean_real)) / (
+        # the reference's K = 1 ``mean.t().mm(mean)`` is an outer product: one fp64 multiply per element, so the
+        # broadcast product gives the same bits without a (vendor) GEMM launch
+        cov_real = (self.real_features_cov_sum - self.real_features_num_samples * (mean_real.t() * mean_real)) / (
             self.real_features_num_samples - 1
         )
-        cov_fake = (self.fake_features_cov_sum - self.fake_features_num_samples * mean_fake.t().mm(mean_fake)) / (
+        cov_fake = (self.fake_features_cov_sum - self.fake_features_num_samples * (mean_fake.t() * mean_fake)) / (
             self.fake_features_num_samples - 1
         )
         return _compute_fid(mean_real.squeeze(0), cov_real, mean_fake.squeeze(0), cov_fake).to(self.orig_dtype)

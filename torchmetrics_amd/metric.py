@@ -16,6 +16,7 @@ MI355X-first differences:
 import builtins
 import functools
 import inspect
+import sys
 from abc import ABC, abstractmethod
 from contextlib import contextmanager, nullcontext
 from copy import deepcopy
@@ -567,20 +568,40 @@ class Metric(Module, ABC):
         A public reset also clears the deferred-validation word (stream-ordered ``zero_``, no host sync): a bad batch
         that was never computed must not raise for data that is no longer in the state.
         """
-        self.__dict__.pop("_errors_checked_at", None)
-        if not self.__dict__.get("_keep_device_errors") and self.__dict__.get("_device_errors") is not None:
+        d = self.__dict__
+        d.pop("_errors_checked_at", None)
+        if not d.get("_keep_device_errors") and d.get("_device_errors") is not None:
             self._device_errors.zero_()
         self._update_count = 0
         self._forward_cache = None
         self._computed = None
         for attr, default in self._defaults.items():
-            cur = getattr(self, attr)
+            cur = d[attr] if attr in d else getattr(self, attr)
             if isinstance(default, Tensor):
-                setattr(self, attr, default.detach().clone().to(cur.device))
+                # references: the state dict's entry, this local, getrefcount's argument -- nothing else
+                if not (sys.getrefcount(cur) <= 3 and self._refill_in_place(cur, default)):
+                    setattr(self, attr, default.detach().clone().to(cur.device))
             else:
                 setattr(self, attr, [])
+            del cur
         self._cache = None
         self._is_synced = False
+
+    @staticmethod
+    def _refill_in_place(cur: Any, default: Tensor) -> bool:
+        """Reset a tensor state by refilling its own memory when nothing else can observe it (the caller checked that
+        no other Python reference to the tensor exists (a returned ``compute()`` result, a forward()'s saved global state, a compute-group
+        sibling, a user handle); here: no other tensor on its storage (views).  Then the refill is invisible, and the
+        state keeps its warm memory (allocator block, TLB and cache residency) -- the reference's reset always
+        allocates a fresh clone of the default (S/metric.py:673-688), which is what happens here otherwise."""
+        if not isinstance(cur, Tensor) or cur.requires_grad or cur.layout != torch.strided:
+            return False
+        if cur.shape != default.shape or cur.dtype != default.dtype or cur.device != default.device:
+            return False
+        if not cur.is_contiguous() or torch._C._storage_Use_Count(cur.untyped_storage()._cdata) > 2:
+            return False
+        cur.copy_(default)
+        return True
 
     def clone(self) -> "Metric":
         return deepcopy(self)

@@ -515,14 +515,22 @@ def dgemm(a: Union[Tensor, Sequence[Tensor]], b: Union[Tensor, Sequence[Tensor]]
         o_l[i].copy_(r)
 
 
-def dgemv4_blocks(d: int) -> int:
+def dgemv4_blocks(d: int, device: Optional[torch.device] = None) -> int:
+    """Rows of per-block partial norms ``dgemv4_resid`` writes (1 on CPU)."""
+    if device is not None and device.type != "cuda":
+        return 1
     return int(_ops().dgemv4_blocks(d))
 
 
 def dgemv4_resid(a: Tensor, w_in: Tensor, part_in: Tensor, normalize: bool, w_out: Tensor, part_out: Tensor) -> None:
     """One power-iteration step on 4 vectors: ``w_out = v - a v`` with ``v = w_in / ||w_in||`` (column norms from the
     previous step's per-block partials ``part_in``); writes this step's partial squared norms into ``part_out``."""
-    _ops().dgemv4_resid(a, w_in, part_in, normalize, w_out, part_out)
+    if a.is_cuda:
+        _ops().dgemv4_resid(a, w_in, part_in, normalize, w_out, part_out)
+        return
+    v = w_in / part_in.sum(0).sqrt().clamp(min=1e-300) if normalize else w_in
+    w_out.copy_(v - a @ v)
+    part_out.copy_((w_out * w_out).sum(0, keepdim=True))
 
 
 # ------------------------------------------------------------------------------ fused compute() of a collection

@@ -55,6 +55,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--sync-every-step", action="store_true")
+    ap.add_argument("--no-baseline", action="store_true", help="skip the emulated-reference collection")
     ap.add_argument("--graph", action="store_true",
                     help="replay the tensor-state members' updates from HIP graphs (utils.graphs.GraphedUpdate, one graph "
                     "bound to each buffer of the input ring); the "
@@ -140,10 +141,45 @@ def main() -> None:
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+
+    # ---- emulated reference collection on the same data (benchmarks/reference_path.py ReferenceEmulatedCollection)
+    base = None
+    if not args.no_baseline:
+        from benchmarks.reference_path import ReferenceEmulatedCollection
+
+        ref = ReferenceEmulatedCollection(NC, device)
+
+        def ref_step(i):
+            ref.update_cls(logits[i % NBUF], labels[i % NBUF])
+            ref.update_reg(xs[i % NBUF], ys[i % NBUF])
+            if args.sync_every_step:
+                ref.compute()
+
+        for i in range(args.warmup):
+            ref_step(i)
+        ref.compute()
+        ref.reset()
+        sync()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            ref_step(i)
+        ref_out = ref.compute()
+        sync()
+        rt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(rt, op=dist.ReduceOp.MAX)
+        base = world * args.steps * 20 / float(rt.item())
+        for k in ("acc", "r2"):
+            if abs(float(ref_out[k]) - float(out[k])) > 1e-4:
+                raise RuntimeError(f"benchmark parity failure on {k}: {float(out[k])} vs {float(ref_out[k])}")
     if rank == 0:
+        value = world * args.steps * 20 / elapsed
         print(json.dumps({
             "bench": "metric_collection_20", "metric": "metric-updates/sec (whole node)",
-            "value": round(world * args.steps * 20 / elapsed, 1), "unit": "metric-updates/s", "n_gpus": world,
+            "value": round(value, 1), "unit": "metric-updates/s", "n_gpus": world,
+            "vs_baseline": round(value / base, 3) if base else None,
+            "baseline": {"impl": "emulated reference MetricCollection op chain (benchmarks/reference_path.py)",
+                         "value": round(base, 1) if base else None},
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "sync_every_step": args.sync_every_step, "compute_groups": True, "hip_graph": args.graph, "dtype": "bf16", "data": "synthetic",
             "groups": len(cls.compute_groups), "acc": float(out["acc"]), "r2": float(out["r2"]),

@@ -33,3 +33,41 @@ def test_bench_two_rank_gloo_contract(tmp_path):
     assert out["dist"]["world_size_seen"] == 2 and out["dist"]["backend"] == "gloo"
     assert out["dist"]["engine_collectives"]["all_reduce"] >= 1
     assert out["value"] > 0 and out["vs_baseline"] is not None and out["higher_is_better"] is True
+
+
+def _torchrun_json(tmp_path, script, *args):
+    env = dict(os.environ, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "benchmarks", script), *args]
+    res = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=580)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(600)
+def test_bench_fid_two_rank_gloo(tmp_path):
+    """BASELINE config #4 at N ranks: sharded updates, one engine all-reduce per state bucket, FID parity."""
+    out = _torchrun_json(tmp_path, "bench_fid.py", "--samples", "2000", "--dim", "64", "--batch", "250")
+    assert out["n_gpus"] == 2 and out["dist"]["world_size_seen"] == 2 and out["dist"]["backend"] == "gloo"
+    assert out["dist"]["engine_collectives"]["all_reduce"] >= 2
+    assert out["reference_emulated"]["rel_diff_vs_ours"] < 1e-6
+    assert out["rel_diff_fp64_vs_eigh"] < 1e-9
+
+
+@pytest.mark.timeout(600)
+def test_bench_map_two_rank_gloo(tmp_path):
+    """BASELINE config #3 at N ranks: list states gathered by the engine, reference per-element sync timed."""
+    out = _torchrun_json(tmp_path, "bench_map.py", "--images", "128")
+    assert out["n_gpus"] == 2 and out["dist"]["world_size_seen"] == 2
+    assert out["dist"]["engine_collectives"]["all_gather"] >= 1
+    assert out["reference_sync_s"] is not None and 0 < out["map"] < 1
+
+
+@pytest.mark.timeout(600)
+def test_bench_collection_two_rank_gloo(tmp_path):
+    """BASELINE config #5 at N ranks: per-step synced compute of the 20-metric collection against the emulated
+    reference collection (parity-checked inside the bench)."""
+    out = _torchrun_json(tmp_path, "bench_collection.py", "--steps", "3", "--warmup", "1", "--sync-every-step")
+    assert out["n_gpus"] == 2 and out["vs_baseline"] is not None and out["baseline"]["value"] > 0

@@ -34,52 +34,88 @@ def _validate_generator_model(generator: GeneratorType, conditional: bool = Fals
         raise ValueError("The generator's `num_classes` attribute must be an integer when `conditional=True`.")
 
 
+_INTERPOLATIONS = ("lerp", "slerp_any", "slerp_unit")
+_SIM_NETS = ("alex", "vgg", "squeeze")
+
+
 def _perceptual_path_length_validate_arguments(num_samples: int = 10_000, conditional: bool = False,
                                                batch_size: int = 128, interpolation_method: str = "lerp",
                                                epsilon: float = 1e-4, resize: Optional[int] = 64,
                                                lower_discard: Optional[float] = 0.01,
                                                upper_discard: Optional[float] = 0.99) -> None:
-    if not (isinstance(num_samples, int) and num_samples > 0):
-        raise ValueError(f"Argument `num_samples` must be a positive integer, but got {num_samples}.")
-    if not isinstance(conditional, bool):
-        raise ValueError(f"Argument `conditional` must be a boolean, but got {conditional}.")
-    if not (isinstance(batch_size, int) and batch_size > 0):
-        raise ValueError(f"Argument `batch_size` must be a positive integer, but got {batch_size}.")
-    if interpolation_method not in ["lerp", "slerp_any", "slerp_unit"]:
-        raise ValueError(
-            f"Argument `interpolation_method` must be one of 'lerp', 'slerp_any', 'slerp_unit',got {interpolation_method}.")
-    if not (isinstance(epsilon, float) and epsilon > 0):
-        raise ValueError(f"Argument `epsilon` must be a positive float, but got {epsilon}.")
-    if resize is not None and not (isinstance(resize, int) and resize > 0):
-        raise ValueError(f"Argument `resize` must be a positive integer or `None`, but got {resize}.")
+    """Argument checks with the reference's messages (``F/image/perceptual_path_length.py:65-104``), table-driven."""
+    rules = [
+        (isinstance(num_samples, int) and num_samples > 0,
+         f"Argument `num_samples` must be a positive integer, but got {num_samples}."),
+        (isinstance(conditional, bool), f"Argument `conditional` must be a boolean, but got {conditional}."),
+        (isinstance(batch_size, int) and batch_size > 0,
+         f"Argument `batch_size` must be a positive integer, but got {batch_size}."),
+        (interpolation_method in _INTERPOLATIONS,
+         f"Argument `interpolation_method` must be one of 'lerp', 'slerp_any', 'slerp_unit',got {interpolation_method}."),
+        (isinstance(epsilon, float) and epsilon > 0, f"Argument `epsilon` must be a positive float, but got {epsilon}."),
+        (resize is None or (isinstance(resize, int) and resize > 0),
+         f"Argument `resize` must be a positive integer or `None`, but got {resize}."),
+    ]
     for name, v in (("lower_discard", lower_discard), ("upper_discard", upper_discard)):
-        if v is not None and not (isinstance(v, float) and 0 <= v <= 1):
-            raise ValueError(f"Argument `{name}` must be a float between 0 and 1 or `None`, but got {v}.")
+        rules.append((v is None or (isinstance(v, float) and 0 <= v <= 1),
+                      f"Argument `{name}` must be a float between 0 and 1 or `None`, but got {v}."))
+    for ok, msg in rules:
+        if not ok:
+            raise ValueError(msg)
+
+
+def _unit(x: Tensor, eps: float) -> Tensor:
+    return x / (x * x).sum(dim=-1, keepdim=True).sqrt().clamp_min(eps)
 
 
 def _interpolate(latents1: Tensor, latents2: Tensor, epsilon: float = 1e-4,
                  interpolation_method: Literal["lerp", "slerp_any", "slerp_unit"] = "lerp") -> Tensor:
-    """Point at fraction ``epsilon`` from ``latents1`` towards ``latents2`` (linear or spherical)."""
-    eps = 1e-7
+    """Point at fraction ``epsilon`` from ``latents1`` towards ``latents2``.
+
+    ``lerp``: straight line.  ``slerp_any``: along the great circle through the two directions, with the endpoints'
+    own norms as weights (falls back to ``lerp`` for (anti)parallel or zero latents).  ``slerp_unit``: the slerp point
+    projected back onto the unit sphere."""
     if latents1.shape != latents2.shape:
         raise ValueError("Latents must have the same shape.")
+    if interpolation_method not in _INTERPOLATIONS:
+        raise ValueError(
+            f"Interpolation method {interpolation_method} not supported. Choose from 'lerp', 'slerp_any', 'slerp_unit'.")
+    line = torch.lerp(latents1, latents2, epsilon)
     if interpolation_method == "lerp":
-        return latents1 + (latents2 - latents1) * epsilon
-    if interpolation_method == "slerp_any":
-        u1 = latents1 / (latents1**2).sum(dim=-1, keepdim=True).sqrt().clamp_min(eps)
-        u2 = latents2 / (latents2**2).sum(dim=-1, keepdim=True).sqrt().clamp_min(eps)
-        d = (u1 * u2).sum(dim=-1, keepdim=True)
-        degenerate = (u1.norm(dim=-1, keepdim=True) < eps) | (u2.norm(dim=-1, keepdim=True) < eps)
-        degenerate = degenerate | (d > 1 - eps) | (d < -1 + eps)
-        omega = d.acos()
-        denom = omega.sin().clamp_min(eps)
-        out = ((1 - epsilon) * omega).sin() / denom * latents1 + (epsilon * omega).sin() / denom * latents2
-        return torch.where(degenerate.expand_as(out), latents1 + (latents2 - latents1) * epsilon, out)
-    if interpolation_method == "slerp_unit":
-        out = _interpolate(latents1, latents2, epsilon, "slerp_any")
-        return out / (out**2).sum(dim=-1, keepdim=True).sqrt().clamp_min(eps)
-    raise ValueError(
-        f"Interpolation method {interpolation_method} not supported. Choose from 'lerp', 'slerp_any', 'slerp_unit'.")
+        return line
+    tiny = 1e-7
+    u1, u2 = _unit(latents1, tiny), _unit(latents2, tiny)
+    cos = (u1 * u2).sum(dim=-1, keepdim=True)
+    omega = cos.acos()
+    inv_sin = 1.0 / omega.sin().clamp_min(tiny)
+    arc = torch.sin((1 - epsilon) * omega) * inv_sin * latents1 + torch.sin(epsilon * omega) * inv_sin * latents2
+    # a zero latent or (anti)parallel directions make the arc undefined: those rows take the straight line
+    degenerate = (u1.norm(dim=-1, keepdim=True) < tiny) | (u2.norm(dim=-1, keepdim=True) < tiny) | \
+        (cos.abs() > 1 - tiny)
+    out = torch.where(degenerate, line, arc)
+    return _unit(out, tiny) if interpolation_method == "slerp_unit" else out
+
+
+def _resolve_sim_net(sim_net: Union[nn.Module, str], resize: Optional[int], device: torch.device) -> nn.Module:
+    if isinstance(sim_net, nn.Module):
+        return sim_net.to(device)
+    if sim_net in _SIM_NETS:
+        return _LPIPS(pretrained=True, net=sim_net, resize=resize).to(device)
+    raise ValueError(f"sim_net must be a nn.Module or one of 'alex', 'vgg', 'squeeze', got {sim_net}")
+
+
+def _quantile_trim(d: Tensor, lower_discard: Optional[float], upper_discard: Optional[float]) -> Tensor:
+    """Keep the values between the two "lower"-interpolated quantiles, on the device: one sort gives both order
+    statistics (``torch.quantile(..., interpolation="lower")`` is the element at ``floor(q (n - 1))``).  Without a
+    lower quantile the floor is 0 (negative distances dropped) and without an upper one nothing is cut above, as in
+    the reference."""
+    n = d.numel()
+    srt = d.sort().values
+    lo = srt[int(math.floor(lower_discard * (n - 1)))] if lower_discard is not None else 0.0
+    keep = d >= lo
+    if upper_discard is not None:
+        keep &= d <= srt[int(math.floor(upper_discard * (n - 1)))]
+    return d[keep]
 
 
 def perceptual_path_length(generator: GeneratorType, num_samples: int = 10_000, conditional: bool = False,
@@ -88,30 +124,30 @@ def perceptual_path_length(generator: GeneratorType, num_samples: int = 10_000, 
                            upper_discard: Optional[float] = 0.99,
                            sim_net: Union[nn.Module, Literal["alex", "vgg", "squeeze"]] = "vgg",
                            device: Union[str, torch.device] = "cpu") -> Tuple[Tensor, Tensor, Tensor]:
-    """(mean, std, all kept distances) of the perceptual path length (``F/image/perceptual_path_length.py:150``)."""
+    """(mean, std, kept distances) of the perceptual path length (API of ``F/image/perceptual_path_length.py:150``).
+
+    Every latent pair ``(z, I(z, z', eps))`` is drawn up front; each batch sends both halves through the generator
+    as ONE call and writes its LPIPS distances (scaled by ``1 / eps²``) into a preallocated device buffer, and the
+    quantile trim runs on the device -- no per-batch host work beyond the generator / network calls."""
     _perceptual_path_length_validate_arguments(num_samples, conditional, batch_size, interpolation_method, epsilon,
                                                resize, lower_discard, upper_discard)
     _validate_generator_model(generator, conditional)
+    device = torch.device(device)
     generator = generator.to(device)
-    z1 = generator.sample(num_samples).to(device)
-    z2 = _interpolate(z1, generator.sample(num_samples).to(device), epsilon, interpolation_method)
+    start = generator.sample(num_samples).to(device)
+    end = _interpolate(start, generator.sample(num_samples).to(device), epsilon, interpolation_method)
     labels = torch.randint(0, generator.num_classes, (num_samples,)).to(device) if conditional else None
-    if isinstance(sim_net, nn.Module):
-        net = sim_net.to(device)
-    elif sim_net in ["alex", "vgg", "squeeze"]:
-        net = _LPIPS(pretrained=True, net=sim_net, resize=resize).to(device)
-    else:
-        raise ValueError(f"sim_net must be a nn.Module or one of 'alex', 'vgg', 'squeeze', got {sim_net}")
+    net = _resolve_sim_net(sim_net, resize, device)
+    scale = 1.0 / (epsilon * epsilon)
     with torch.inference_mode():
-        dists = []
-        for b in range(math.ceil(num_samples / batch_size)):
-            sl = slice(b * batch_size, (b + 1) * batch_size)
-            z = torch.cat((z1[sl], z2[sl]), dim=0)
-            out = generator(z, torch.cat((labels[sl], labels[sl]))) if conditional else generator(z)
-            o1, o2 = out.chunk(2, dim=0)
-            dists.append((net(2 * (o1 / 255) - 1, 2 * (o2 / 255) - 1) / epsilon**2).detach().reshape(-1))
-        d = torch.cat(dists)
-        lower = torch.quantile(d, lower_discard, interpolation="lower") if lower_discard is not None else 0.0
-        upper = torch.quantile(d, upper_discard, interpolation="lower") if upper_discard is not None else d.max()
-        d = d[(d >= lower) & (d <= upper)]
-        return d.mean(), d.std(), d
+        dist = torch.empty(num_samples, device=device)
+        for lo in range(0, num_samples, batch_size):
+            hi = min(lo + batch_size, num_samples)
+            pair = torch.cat((start[lo:hi], end[lo:hi]))
+            imgs = generator(pair, labels[lo:hi].repeat(2)) if conditional else generator(pair)
+            # generator outputs are in [0, 255]; LPIPS takes [-1, 1]
+            imgs = imgs * (2.0 / 255.0) - 1.0
+            a, b = imgs[: hi - lo], imgs[hi - lo:]
+            dist[lo:hi] = net(a, b).reshape(-1).to(dist.dtype) * scale
+        kept = _quantile_trim(dist, lower_discard, upper_discard)
+        return kept.mean(), kept.std(), kept

@@ -19,6 +19,12 @@ C, B, K = 1000, 8192, 26
 
 def main():
     case = sys.argv[1] if len(sys.argv) > 1 else "plain"
+    if case.startswith("sched_"):
+        import ctypes
+
+        flag = {"sched_spin": 1, "sched_yield": 2, "sched_blocking": 4}[case]
+        rc = ctypes.CDLL("libamdhip64.so").hipSetDeviceFlags(flag)  # before the HIP context exists
+        assert rc == 0, rc
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(1234)
     preds = [torch.randn(B, C, generator=g, device=dev).to(torch.bfloat16) for _ in range(K)]

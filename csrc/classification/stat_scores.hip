@@ -236,8 +236,11 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return static_cast<uint32_t>(__reduce_max_sync(~0ull, static_cast<int>(v ^ 0x80000000u))) ^ 0x80000000u;
 }
 
+constexpr int kOrdBlock = 512;  // 8 waves: half the workgroups of 256-thread blocks for the same waves (measured on
+                                // the 406 MB ring, tools/mb/confmat_ring_mb.hip: 5.06 us vs 5.38 us per 8192 x 1000)
+
 template <typename scalar_t, typename target_t, int kPer>
-__global__ void __launch_bounds__(kBlock) mc_argmax_ord16_kernel(const scalar_t* __restrict__ preds,
+__global__ void __launch_bounds__(kOrdBlock) mc_argmax_ord16_kernel(const scalar_t* __restrict__ preds,
                                                                  const target_t* __restrict__ target, long long N,
                                                                  int C, long long ignore, bool has_ignore,
                                                                  int64_t* __restrict__ out, int* __restrict__ flag) {
@@ -899,8 +902,10 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
               constexpr int P = decltype(per_tag)::value;
               if constexpr (sizeof(scalar_t) == 2) {
                 if (!ord16_off) {
-                  hipLaunchKernelGGL((mc_argmax_ord16_kernel<scalar_t, target_t, P>), dim3(grid), dim3(kBlock), 0, s,
-                                     pp, tp, N, C, ignore_index, has_ignore, outp, flagp);
+                  const long long want16 = (N + kOrdBlock / kWave - 1) / (kOrdBlock / kWave);  // one row per wave
+                  const int grid16 = static_cast<int>(std::min<long long>(want16, static_cast<long long>(cus) * 4));
+                  hipLaunchKernelGGL((mc_argmax_ord16_kernel<scalar_t, target_t, P>), dim3(grid16), dim3(kOrdBlock),
+                                     0, s, pp, tp, N, C, ignore_index, has_ignore, outp, flagp);
                   return;
                 }
               }

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <chrono>
 
 #define CK(x)                                                               \
   do {                                                                      \
@@ -29,7 +30,7 @@ __global__ void empty_kernel(int* p) {
 
 // pure read floor: each wave reads rows (kPer x 16 B per lane), xor-folds them, writes nothing
 template <int kPer, int kRowsPerWave>
-__global__ void __launch_bounds__(256) vread(const uint16_t* __restrict__ preds, int N, int C, int* __restrict__ sink) {
+__global__ void __launch_bounds__(1024) vread(const uint16_t* __restrict__ preds, int N, int C, int* __restrict__ sink) {
   const int lane = threadIdx.x & 63;
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64;
   const int nchunks = C / 8;
@@ -58,7 +59,7 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // production-style ordinal argmax (see csrc/classification/stat_scores.hip mc_argmax_ord16_kernel), all rows of a
 // wave's share loaded up front; kMode 0: int64 atomic into confmat, 1: label store only, 2: int32 atomic
 template <int kPer, int kRowsPerWave, int kMode>
-__global__ void __launch_bounds__(256) vord(const uint16_t* __restrict__ preds, const int64_t* __restrict__ target,
+__global__ void __launch_bounds__(1024) vord(const uint16_t* __restrict__ preds, const int64_t* __restrict__ target,
                                             int N, int C, unsigned long long* __restrict__ out,
                                             int* __restrict__ lab) {
   const int lane = threadIdx.x & 63;
@@ -170,26 +171,33 @@ int main() {
   };
   timeit("empty_2048x256", [&](int) { hipLaunchKernelGGL(empty_kernel, dim3(2048), dim3(256), 0, 0, lab); });
   timeit("empty_1x64", [&](int) { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, 0, lab); });
-  timeit("read_1row", [&](int b) { hipLaunchKernelGGL((vread<2, 1>), dim3(N / 4), dim3(256), 0, 0, dp[b], N, C, lab); });
-  timeit("read_2row", [&](int b) { hipLaunchKernelGGL((vread<2, 2>), dim3(N / 8), dim3(256), 0, 0, dp[b], N, C, lab); });
-  timeit("read_4row", [&](int b) { hipLaunchKernelGGL((vread<2, 4>), dim3(N / 16), dim3(256), 0, 0, dp[b], N, C, lab); });
-  timeit("ord_1row_i64atomic", [&](int b) {
-    hipLaunchKernelGGL((vord<2, 1, 0>), dim3(N / 4), dim3(256), 0, 0, dp[b], dt[b], N, C, out, lab);
-  });
-  timeit("ord_1row_label", [&](int b) {
-    hipLaunchKernelGGL((vord<2, 1, 1>), dim3(N / 4), dim3(256), 0, 0, dp[b], dt[b], N, C, out, lab);
-  });
-  timeit("ord_1row_i32atomic", [&](int b) {
-    hipLaunchKernelGGL((vord<2, 1, 2>), dim3(N / 4), dim3(256), 0, 0, dp[b], dt[b], N, C, out, lab);
-  });
-  timeit("ord_2row_i64atomic", [&](int b) {
-    hipLaunchKernelGGL((vord<2, 2, 0>), dim3(N / 8), dim3(256), 0, 0, dp[b], dt[b], N, C, out, lab);
-  });
-  timeit("ord_4row_i64atomic", [&](int b) {
-    hipLaunchKernelGGL((vord<2, 4, 0>), dim3(N / 16), dim3(256), 0, 0, dp[b], dt[b], N, C, out, lab);
-  });
-  timeit("ord_2row_label", [&](int b) {
-    hipLaunchKernelGGL((vord<2, 2, 1>), dim3(N / 8), dim3(256), 0, 0, dp[b], dt[b], N, C, out, lab);
-  });
+  timeit("empty_512x1024", [&](int) { hipLaunchKernelGGL(empty_kernel, dim3(512), dim3(1024), 0, 0, lab); });
+  for (int bs : {256, 512, 1024}) {
+    char name[64];
+    std::snprintf(name, sizeof(name), "read_1row_b%d", bs);
+    timeit(name, [&](int b) { hipLaunchKernelGGL((vread<2, 1>), dim3(N / (bs / 64)), dim3(bs), 0, 0, dp[b], N, C, lab); });
+    std::snprintf(name, sizeof(name), "read_2row_b%d", bs);
+    timeit(name, [&](int b) { hipLaunchKernelGGL((vread<2, 2>), dim3(N / (bs / 32)), dim3(bs), 0, 0, dp[b], N, C, lab); });
+    std::snprintf(name, sizeof(name), "ord_1row_i64atomic_b%d", bs);
+    timeit(name, [&](int b) {
+      hipLaunchKernelGGL((vord<2, 1, 0>), dim3(N / (bs / 64)), dim3(bs), 0, 0, dp[b], dt[b], N, C, out, lab);
+    });
+    std::snprintf(name, sizeof(name), "ord_2row_i64atomic_b%d", bs);
+    timeit(name, [&](int b) {
+      hipLaunchKernelGGL((vord<2, 2, 0>), dim3(N / (bs / 32)), dim3(bs), 0, 0, dp[b], dt[b], N, C, out, lab);
+    });
+  }
+  // host-side launch cost alone: launches into a stream blocked behind a long kernel are queued, not run
+  {
+    const int L = 400;
+    hipEvent_t h0;
+    CK(hipEventCreate(&h0));
+    auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < L; ++i) hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, 0, lab);
+    auto t1 = std::chrono::steady_clock::now();
+    CK(hipDeviceSynchronize());
+    std::printf("{\"variant\": \"host_launch_cost\", \"us\": %.3f}\n",
+                std::chrono::duration<double, std::micro>(t1 - t0).count() / L);
+  }
   return 0;
 }

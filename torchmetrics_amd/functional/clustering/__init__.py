@@ -1,9 +1,11 @@
 """Clustering metrics (reference ``F/clustering/*.py``).
 
-Extrinsic scores share one contingency table built as a 2-D histogram of relabelled (target, pred) ids (no sparse
-COO round trip); the expected mutual information of AMI enumerates all (row, column, n_ij) hypergeometric terms in
-one vectorised pass instead of three nested Python loops; intrinsic scores compute all centroids / dispersions with
-``index_add`` instead of a per-cluster loop.
+Extrinsic scores share one contingency table: on ROCm a min/max pass per label tensor and ONE 2-D histogram kernel
+over the dense label ranges (``ops.contingency``, ``csrc/clustering/cluster.hip``) -- no ``unique`` sorts, no sparse
+COO round trip; the expected mutual information of AMI enumerates all (row, column, n_ij) hypergeometric terms in one
+vectorised pass instead of three nested Python loops; intrinsic scores get all centroids from one segmented-sum kernel
+and all per-cluster distance sums / maxima and the within-dispersion from one more pass, instead of a per-cluster
+loop.
 """
 from typing import Literal, Optional, Tuple, Union
 
@@ -64,10 +66,7 @@ def calculate_contingency_matrix(preds: Tensor, target: Tensor, eps: Optional[fl
         raise ValueError("Cannot specify `eps` and return sparse tensor.")
     if preds.ndim != 1 or target.ndim != 1:
         raise ValueError(f"Expected 1d `preds` and `target` but got {preds.ndim} and {target.dim}.")
-    p_cls, p_idx = torch.unique(preds, return_inverse=True)
-    t_cls, t_idx = torch.unique(target, return_inverse=True)
-    kp, kt = p_cls.numel(), t_cls.numel()
-    cont = ops.histogram(t_idx * kp + p_idx, kt * kp).reshape(kt, kp)
+    cont = ops.contingency(preds, target)
     if sparse:
         return cont.to_sparse()
     if eps:
@@ -284,12 +283,12 @@ def v_measure_score(preds: Tensor, target: Tensor, beta: float = 1.0) -> Tensor:
 
 # ---------------------------------------------------------------------------------------------- intrinsic
 def _cluster_stats(data: Tensor, labels: Tensor) -> Tuple[Tensor, Tensor, Tensor, int]:
-    """(relabelled ids, centroids [K, D], cluster sizes [K], K) with one index_add pass."""
-    uniq, inv = torch.unique(labels, return_inverse=True)
-    k = uniq.numel()
-    sums = torch.zeros(k, data.shape[1], dtype=data.dtype, device=data.device).index_add_(0, inv, data)
-    sizes = ops.histogram(inv, k)
-    return inv, sums / sizes[:, None].to(data.dtype), sizes, k
+    """(dense ids, centroids [K, D] in the data dtype, cluster sizes [K], K): one relabelling pass and one segmented
+    sum (``ops.dense_labels`` / ``ops.cluster_sums``, fp64 accumulation) instead of the reference's per-cluster
+    ``data[labels == k].mean(0)`` loop (``F/clustering/davies_bouldin_score.py:46-57``)."""
+    inv, k = ops.dense_labels(labels)
+    sums, sizes = ops.cluster_sums(data, inv, k)
+    return inv, (sums / sizes[:, None].to(torch.float64)).to(data.dtype), sizes, k
 
 
 def calinski_harabasz_score(data: Tensor, labels: Tensor) -> Tensor:
@@ -300,7 +299,8 @@ def calinski_harabasz_score(data: Tensor, labels: Tensor) -> Tensor:
     _validate_intrinsic_labels_to_samples(k, n)
     mean = data.mean(dim=0)
     between = (((cent - mean) ** 2).sum(1) * sizes.to(data.dtype)).sum()
-    within = ((data - cent[inv]) ** 2).sum()
+    _, _, within = ops.cluster_dispersion(data, inv, cent, 2.0)
+    within = within.to(data.dtype)
     if within == 0:
         return torch.tensor(1.0, device=data.device, dtype=torch.float32)
     return between * (n - k) / (within * (k - 1.0))
@@ -311,9 +311,9 @@ def davies_bouldin_score(data: Tensor, labels: Tensor) -> Tensor:
     _validate_intrinsic_cluster_data(data, labels)
     inv, cent, sizes, k = _cluster_stats(data, labels)
     _validate_intrinsic_labels_to_samples(k, data.shape[0])
-    dist = (data - cent[inv]).pow(2).sum(1).sqrt()
-    intra = torch.zeros(k, dtype=data.dtype, device=data.device).index_add_(0, inv, dist) / sizes.to(data.dtype)
-    cd = torch.cdist(cent, cent)
+    dsum, _, _ = ops.cluster_dispersion(data, inv, cent, 2.0)
+    intra = (dsum / sizes.to(torch.float64)).to(data.dtype)
+    cd = torch.cdist(cent, cent, compute_mode="donot_use_mm_for_euclid_dist")
     if torch.allclose(intra, torch.zeros_like(intra)) or torch.allclose(cd, torch.zeros_like(cd)):
         return torch.tensor(0.0, device=data.device, dtype=torch.float32)
     cd = torch.where(cd == 0, torch.full_like(cd, float("inf")), cd)
@@ -324,10 +324,8 @@ def _dunn_index_update(data: Tensor, labels: Tensor, p: float) -> Tuple[Tensor, 
     inv, cent, _, k = _cluster_stats(data, labels)
     iu = torch.triu_indices(k, k, offset=1, device=data.device)
     inter = torch.linalg.norm(cent[iu[0]] - cent[iu[1]], ord=p, dim=1)
-    dist = torch.linalg.norm(data - cent[inv], ord=p, dim=1)
-    intra = torch.full((k,), float("-inf"), dtype=data.dtype, device=data.device)
-    intra = intra.scatter_reduce(0, inv, dist, reduce="amax", include_self=True)
-    return inter, intra
+    _, intra, _ = ops.cluster_dispersion(data, inv, cent, p)
+    return inter, intra.to(data.dtype)
 
 
 def _dunn_index_compute(intercluster_distance: Tensor, max_intracluster_distance: Tensor) -> Tensor:

@@ -14,7 +14,7 @@ import os
 import struct
 import threading
 from pathlib import Path
-from typing import Any, List, Optional, Sequence, Union
+from typing import Any, List, Optional, Sequence, Tuple, Union
 
 import torch
 from torch import Tensor
@@ -208,6 +208,84 @@ def histogram(x: Tensor, minlength: int) -> Tensor:
     if not bool(ok.all()):  # out-of-range keys are skipped, as in the kernel
         x = x[ok]
     return torch.bincount(x, minlength=minlength)
+
+
+# ----------------------------------------------------------------------------------- clustering / nominal
+_DENSE_CONTINGENCY_MAX = 1 << 26  # dense-range bins before falling back to unique() relabelling
+
+
+def _label_ranges(*xs: Tensor) -> List[Tuple[int, int]]:
+    """``[(min, max)]`` of integer label tensors: one ``label_minmax`` launch pair each, ONE host read for all."""
+    mm = torch.cat([_ops().label_minmax(x.contiguous()) for x in xs]).tolist()
+    return [(mm[2 * i], mm[2 * i + 1]) for i in range(len(xs))]
+
+
+def contingency(preds: Tensor, target: Tensor) -> Tensor:
+    """``[n_target_values, n_pred_values]`` co-occurrence counts over the sorted distinct values of each.
+
+    ROCm, integer labels: one min/max pass per tensor (one host read), then the 2-D histogram over the dense label
+    ranges with the key built in registers (``csrc/clustering/cluster.hip``); value ranges that never occur are
+    dropped by their zero marginals, which leaves exactly the sorted-unique rows / columns.  Otherwise (CPU, float
+    labels, huge ranges): ``unique(return_inverse)`` relabelling + the histogram kernel."""
+    if preds.is_cuda and not preds.is_floating_point() and not target.is_floating_point() and preds.numel():
+        (tmin, tmax), (pmin, pmax) = _label_ranges(target, preds)
+        rt, rp = tmax - tmin + 1, pmax - pmin + 1
+        if rt * rp <= _DENSE_CONTINGENCY_MAX:
+            p = preds if preds.dtype in (torch.int64, torch.int32, torch.uint8) else preds.long()
+            t = target if target.dtype in (torch.int64, torch.int32, torch.uint8) else target.long()
+            cont = torch.zeros(rt, rp, dtype=torch.int64, device=preds.device)
+            _ops().contingency_dense(t.contiguous(), p.contiguous(), tmin, pmin, cont)
+            rows, cols = cont.sum(1) > 0, cont.sum(0) > 0
+            if bool(rows.all()) and bool(cols.all()):
+                return cont
+            return cont[rows][:, cols]
+    p_cls, p_idx = torch.unique(preds, return_inverse=True)
+    t_cls, t_idx = torch.unique(target, return_inverse=True)
+    kp, kt = p_cls.numel(), t_cls.numel()
+    return histogram(t_idx * kp + p_idx, kt * kp).reshape(kt, kp)
+
+
+def dense_labels(labels: Tensor) -> Tuple[Tensor, int]:
+    """``(ids, K)``: ``labels`` relabelled to ``0..K-1`` in sorted-value order (``unique(return_inverse)``).  ROCm
+    integer labels with a modest range: a presence histogram over the range and a prefix sum, no sort."""
+    if labels.is_cuda and not labels.is_floating_point() and labels.numel():
+        ((lo, hi),) = _label_ranges(labels)
+        r = hi - lo + 1
+        if r <= _DENSE_CONTINGENCY_MAX:
+            shifted = labels.long() - lo
+            present = histogram(shifted, r) > 0
+            remap = torch.cumsum(present, 0) - 1
+            return remap[shifted], int(present.sum())
+    uniq, inv = torch.unique(labels, return_inverse=True)
+    return inv, uniq.numel()
+
+
+def cluster_sums(data: Tensor, ids: Tensor, k: int) -> Tuple[Tensor, Tensor]:
+    """Per-cluster feature sums (fp64 ``[K, D]``) and sizes (int64 ``[K]``) for dense ids."""
+    if data.is_cuda:
+        sums = torch.zeros(k, data.shape[1], dtype=torch.float64, device=data.device)
+        sizes = torch.zeros(k, dtype=torch.int64, device=data.device)
+        _ops().cluster_sums(data.contiguous(), ids.contiguous(), k, sums, sizes)
+        return sums, sizes
+    sums = torch.zeros(k, data.shape[1], dtype=torch.float64).index_add_(0, ids, data.double())
+    return sums, torch.bincount(ids, minlength=k)
+
+
+def cluster_dispersion(data: Tensor, ids: Tensor, centroids: Tensor, p: float = 2.0) -> Tuple[Tensor, Tensor, Tensor]:
+    """Per cluster Σ ||x - c||_p and max ||x - c||_p (fp64 ``[K]``), and the total Σ ||x - c||² (fp64 scalar)."""
+    k = centroids.shape[0]
+    cent = centroids.to(torch.float64).contiguous()
+    if data.is_cuda and (k * data.shape[1] + 2 * k) * 8 <= 64 * 1024:
+        dsum = torch.zeros(k, dtype=torch.float64, device=data.device)
+        dmax = torch.zeros(k, dtype=torch.float64, device=data.device)
+        sq = torch.zeros(1, dtype=torch.float64, device=data.device)
+        _ops().cluster_dispersion(data.contiguous(), ids.contiguous(), cent, float(p), dsum, dmax, sq)
+        return dsum, dmax, sq[0]
+    diff = data.double() - cent[ids]
+    dist = torch.linalg.vector_norm(diff, ord=p, dim=1)
+    dsum = torch.zeros(k, dtype=torch.float64, device=data.device).index_add_(0, ids, dist)
+    dmax = torch.zeros(k, dtype=torch.float64, device=data.device).scatter_reduce(0, ids, dist, reduce="amax")
+    return dsum, dmax, (diff * diff).sum()
 
 
 # ------------------------------------------------------------------------------------- sorted curves / ranks

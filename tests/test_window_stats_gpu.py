@@ -1,0 +1,52 @@
+"""Box-window / neighbour-difference kernels (``csrc/image/window_stats.hip``) for RMSE-SW, RASE, PSNR-B and total
+variation, against the same functionals' CPU formulation (grouped conv / strided views of the reference math)."""
+import pytest
+import torch
+
+from torchmetrics_amd.functional.image import (
+    peak_signal_noise_ratio_with_blocked_effect,
+    relative_average_spectral_error,
+    root_mean_squared_error_using_sliding_window,
+    total_variation,
+)
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("shape", [(3, 3, 40, 70), (2, 1, 17, 130), (1, 4, 64, 64)])
+@pytest.mark.parametrize("window", [1, 4, 7, 8, 15])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_rmse_sw_and_rase(shape, window, dtype):
+    g = torch.Generator().manual_seed(sum(shape) + window)
+    p = torch.rand(shape, generator=g, dtype=dtype)
+    t = torch.rand(shape, generator=g, dtype=dtype)
+    if round(window / 2) >= min(shape[2], shape[3]):
+        pytest.skip("window too large for the image")
+    tol = dict(rtol=1e-4, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-10, atol=1e-12)
+    v_gpu, m_gpu = root_mean_squared_error_using_sliding_window(p.to(DEV), t.to(DEV), window, return_rmse_map=True)
+    v_cpu, m_cpu = root_mean_squared_error_using_sliding_window(p, t, window, return_rmse_map=True)
+    torch.testing.assert_close(m_gpu.cpu(), m_cpu, **tol)
+    torch.testing.assert_close(v_gpu.cpu(), v_cpu, **tol)
+    torch.testing.assert_close(relative_average_spectral_error(p.to(DEV), t.to(DEV), window).cpu(),
+                               relative_average_spectral_error(p, t, window), **tol)
+
+
+@pytest.mark.parametrize("shape", [(4, 1, 64, 64), (2, 1, 37, 90)])
+@pytest.mark.parametrize("block", [8, 4])
+def test_psnrb(shape, block):
+    g = torch.Generator().manual_seed(block)
+    t = torch.rand(shape, generator=g) * 255
+    p = (t + torch.randn(shape, generator=g) * 8).clamp(0, 255)
+    got = peak_signal_noise_ratio_with_blocked_effect(p.to(DEV), t.to(DEV), block)
+    exp = peak_signal_noise_ratio_with_blocked_effect(p.double(), t.double(), block)
+    torch.testing.assert_close(got.cpu().double(), exp, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("reduction", ["sum", "mean", "none"])
+def test_total_variation(reduction):
+    g = torch.Generator().manual_seed(3)
+    img = torch.rand(5, 3, 50, 61, generator=g)
+    got = total_variation(img.to(DEV), reduction)
+    exp = total_variation(img.double(), reduction)
+    torch.testing.assert_close(got.cpu().double(), exp, rtol=1e-5, atol=1e-4)

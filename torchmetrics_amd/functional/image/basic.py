@@ -1,8 +1,10 @@
 """Pixel / band statistics: PSNR, PSNR-B, SAM, ERGAS, total variation, image gradients, RMSE-SW, RASE.
 
 Behavioural references: ``F/image/psnr.py``, ``psnrb.py``, ``sam.py``, ``ergas.py``, ``tv.py``, ``gradients.py``,
-``rmse_sw.py``, ``rase.py``.  All channels are filtered by one grouped convolution (the reference loops over
-channels in Python) and the blocking-effect factor of PSNR-B is built from strided views instead of index lists.
+``rmse_sw.py``, ``rase.py``.  On ROCm, RMSE-SW / RASE maps come from one box-window kernel launch over all channels
+and images, and PSNR-B's SSE + blocking-effect sums and total variation from one neighbour-difference pass
+(``csrc/image/window_stats.hip``); on CPU all channels are filtered by one grouped convolution (the reference loops over
+channels in Python) and the blocking-effect factor is built from strided views instead of index lists.
 """
 import math
 from typing import Optional, Tuple, Union
@@ -11,6 +13,7 @@ import torch
 from torch import Tensor
 from typing_extensions import Literal
 
+from torchmetrics_amd import ops
 from torchmetrics_amd.functional.image.helper import _uniform_filter
 from torchmetrics_amd.utilities.checks import _check_same_shape
 from torchmetrics_amd.utilities.distributed import reduce
@@ -77,6 +80,16 @@ def _compute_bef(x: Tensor, block_size: int = 8) -> Tensor:
     vb[block_size - 1::block_size] = True
     d_b = dh[..., hb].sum() + dv[..., vb, :].sum()
     d_bc = dh[..., ~hb].sum() + dv[..., ~vb, :].sum()
+    return _bef_from_sums(d_b, d_bc, height, width, block_size)
+
+
+def _psnrb_compute(sum_squared_error: Tensor, bef: Tensor, num_obs: Tensor, data_range: Tensor) -> Tensor:
+    mse = sum_squared_error / num_obs + bef
+    peak = torch.where(data_range > 2, data_range**2, torch.ones_like(data_range))
+    return 10 * torch.log10(peak / mse)
+
+
+def _bef_from_sums(d_b: Tensor, d_bc: Tensor, height: int, width: int, block_size: int) -> Tensor:
     n_hb = height * (width / block_size) - 1
     n_hbc = (height * (width - 1)) - n_hb
     n_vb = width * (height / block_size) - 1
@@ -87,13 +100,13 @@ def _compute_bef(x: Tensor, block_size: int = 8) -> Tensor:
     return torch.where(d_b > d_bc, t * (d_b - d_bc), torch.zeros_like(d_b))
 
 
-def _psnrb_compute(sum_squared_error: Tensor, bef: Tensor, num_obs: Tensor, data_range: Tensor) -> Tensor:
-    mse = sum_squared_error / num_obs + bef
-    peak = torch.where(data_range > 2, data_range**2, torch.ones_like(data_range))
-    return 10 * torch.log10(peak / mse)
-
-
 def _psnrb_update(preds: Tensor, target: Tensor, block_size: int = 8) -> Tuple[Tensor, Tensor, Tensor]:
+    stats = ops.neighbour_diff_stats(preds, target, block_size, True) if preds.shape[1] == 1 else None
+    if stats is not None:
+        # ROCm: SSE and the four blocking-effect sums in one pass (csrc/image/window_stats.hip)
+        s = stats.sum(0)
+        bef = _bef_from_sums(s[1] + s[3], s[2] + s[4], preds.shape[2], preds.shape[3], block_size)
+        return s[0].to(preds.dtype), bef.to(preds.dtype), torch.tensor(target.numel(), device=target.device)
     sse = torch.sum((preds - target) ** 2)
     return sse, _compute_bef(preds, block_size=block_size), torch.tensor(target.numel(), device=target.device)
 
@@ -170,6 +183,9 @@ def error_relative_global_dimensionless_synthesis(
 def _total_variation_update(img: Tensor) -> Tuple[Tensor, int]:
     if img.ndim != 4:
         raise RuntimeError(f"Expected input `img` to be an 4D tensor, but got {img.shape}")
+    stats = ops.neighbour_diff_stats(img, None, 1, False) if img.is_floating_point() else None
+    if stats is not None:  # ROCm: both shifted-difference sums in one pass
+        return stats[:, 1:].sum(1).to(img.dtype), img.shape[0]
     score = (img[..., 1:, :] - img[..., :-1, :]).abs().sum([1, 2, 3]) + \
         (img[..., :, 1:] - img[..., :, :-1]).abs().sum([1, 2, 3])
     return score, img.shape[0]
@@ -237,10 +253,14 @@ def _rmse_sw_update(
         )
     total_images = (total_images + target.shape[0]) if total_images is not None else torch.tensor(
         target.shape[0], device=target.device)
-    local = torch.sqrt(_uniform_filter((target - preds) ** 2, window_size))
-    val = local[:, :, crop:-crop, crop:-crop].sum(0).mean()
+    maps = ops.box_rmse_maps(preds, target, window_size, False)
+    if maps is not None:  # ROCm: the batch-summed map straight from the box-window kernel
+        local_sum = maps[0]
+    else:
+        local_sum = torch.sqrt(_uniform_filter((target - preds) ** 2, window_size)).sum(0)
+    val = local_sum[:, crop:-crop, crop:-crop].mean()
     rmse_val_sum = val if rmse_val_sum is None else rmse_val_sum + val
-    rmse_map = local.sum(0) if rmse_map is None else rmse_map + local.sum(0)
+    rmse_map = local_sum if rmse_map is None else rmse_map + local_sum
     return rmse_val_sum, rmse_map, total_images
 
 
@@ -265,6 +285,12 @@ def root_mean_squared_error_using_sliding_window(
 
 def _rase_update(preds: Tensor, target: Tensor, window_size: int, rmse_map: Tensor, target_sum: Tensor,
                  total_images: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
+    maps = ops.box_rmse_maps(preds, target, window_size, True) if preds.shape == target.shape and \
+        preds.ndim == 4 and preds.dtype == target.dtype else None
+    if maps is not None and round(window_size / 2) < min(target.shape[2], target.shape[3]):
+        # ROCm: both filtered maps from ONE pass of the box-window kernel
+        total_images = total_images + target.shape[0]
+        return rmse_map + maps[0], target_sum + maps[1], total_images
     _, rmse_map, total_images = _rmse_sw_update(preds, target, window_size, None, rmse_map, total_images)
     target_sum = target_sum + torch.sum(_uniform_filter(target, window_size) / (window_size**2), dim=0)
     return rmse_map, target_sum, total_images

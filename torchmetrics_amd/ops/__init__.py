@@ -210,6 +210,35 @@ def histogram(x: Tensor, minlength: int) -> Tensor:
     return torch.bincount(x, minlength=minlength)
 
 
+# ------------------------------------------------------------------------------- windowed image statistics
+_BOX_MAX_WINDOW = 32
+
+
+def box_rmse_maps(preds: Tensor, target: Tensor, window: int, want_target: bool) -> Optional[Tuple[Tensor, Tensor]]:
+    """Batch-summed ``sqrt(box_mean((t - p)^2))`` map ``[C, H, W]`` and (``want_target``) ``box_mean(t) / w^2`` map,
+    with the reference's symmetric padding (``csrc/image/window_stats.hip``); ``None`` where the kernel does not
+    apply (CPU, window > 32 or larger than the image)."""
+    if not preds.is_cuda or window > _BOX_MAX_WINDOW or window > preds.shape[2] or window > preds.shape[3]:
+        return None
+    c, h, w = preds.shape[1:]
+    rmse_map = torch.empty(c, h, w, dtype=preds.dtype, device=preds.device)
+    t_map = torch.empty(c, h, w, dtype=preds.dtype, device=preds.device) if want_target else \
+        torch.empty(0, dtype=preds.dtype, device=preds.device)
+    _ops().box_rmse_maps(preds.contiguous(), target.contiguous(), int(window), rmse_map, t_map)
+    return rmse_map, t_map
+
+
+def neighbour_diff_stats(x: Tensor, y: Optional[Tensor], block_size: int, squared: bool) -> Optional[Tensor]:
+    """Per image f64 ``[B, 5]``: ``Σ(x - y)^2``, neighbour differences across / off ``block_size`` boundaries
+    (horizontal, then vertical); ``None`` off-GPU."""
+    if not x.is_cuda:
+        return None
+    out = torch.empty(x.shape[0], 5, dtype=torch.float64, device=x.device)
+    yy = y.contiguous() if y is not None else torch.empty(0, dtype=x.dtype, device=x.device)
+    _ops().neighbour_diff_stats(x.contiguous(), yy, int(block_size), bool(squared), out)
+    return out
+
+
 # ----------------------------------------------------------------------------------- clustering / nominal
 _DENSE_CONTINGENCY_MAX = 1 << 26  # dense-range bins before falling back to unique() relabelling
 

@@ -31,10 +31,12 @@ __device__ __forceinline__ float to_acc(T v) {
 __device__ __forceinline__ double to_acc(double v) { return v; }
 
 __device__ __forceinline__ int mirror(int i, int n) {
-  // edge-inclusive mirror: -1 -> 0, -2 -> 1, n -> n-1, n+1 -> n-2 (windows are shorter than the image)
+  // edge-inclusive mirror: -1 -> 0, -2 -> 1, n -> n-1, n+1 -> n-2 (the reference's padding; its windows are shorter
+  // than the image).  Halo rows / cols staged for output positions past the image edge (the last tile) can lie
+  // further out: those feed no output, and the clamp keeps every load in bounds.
   if (i < 0) i = -i - 1;
   if (i >= n) i = 2 * n - i - 1;
-  return i;
+  return i < 0 ? 0 : (i >= n ? n - 1 : i);
 }
 
 template <typename T>

@@ -76,12 +76,20 @@ def _greedy_match(pe: Tensor, te: Tensor, pw: Tensor, tw: Tensor) -> Tuple[Tenso
     (``F/text/bert.py:134-167``)."""
     n, nl, p, d = pe.shape
     r = te.shape[2]
-    # the epilogue path pays off once the [N, L, P, R] similarity tensor is large and the per-pair matrices fill the
-    # 128 x 128 GEMM tiles; short sentences stay on the batched library GEMM (benchmarks/bench_misc_kernels.py)
-    big = p >= 128 and r >= 128 and n * nl * p * r >= (1 << 26)
-    if big and pe.is_cuda and d % 4 == 0 and not (pe.requires_grad or te.requires_grad):
-        rmax, cmax = ops.gemm_row_col_max(pe.reshape(n * nl, p, d).float().contiguous(),
-                                          te.reshape(n * nl, r, d).float().contiguous())
+    if pe.is_cuda and not (pe.requires_grad or te.requires_grad) and n * nl * p * r > 0:
+        # ROCm: no [N, L, P, R] tensor -- sentence-length pairs (<= 128 tokens a side) on the per-pair 64 x 64
+        # super-tile kernel, longer ones on the 128 x 128 MFMA GEMM with the row / column max epilogue
+        x = pe.reshape(n * nl, p, d).float().contiguous()
+        y = te.reshape(n * nl, r, d).float().contiguous()
+        if p <= 128 and r <= 128:
+            rmax, cmax = ops.bert_rowcol_max(x, y)
+        elif d % 4 == 0:
+            rmax, cmax = ops.gemm_row_col_max(x, y)
+        else:
+            rmax = cmax = None
+    else:
+        rmax = cmax = None
+    if rmax is not None:
         precision = (rmax.reshape(n, nl, p) * pw[:, None, :].float()).sum(-1)
         recall = (cmax.reshape(n, nl, r) * tw[:, None, :].float()).sum(-1)
         f1 = (2 * precision * recall / (precision + recall)).nan_to_num(0.0)

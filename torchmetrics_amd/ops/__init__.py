@@ -1134,6 +1134,17 @@ def gemm_nt(x: Tensor, y: Tensor, kind: int, aux_x: Optional[Tensor] = None, aux
     return _cpu.gemm_nt(x, y, kind, aux_x, aux_y, scale, coef, degree, zero_diagonal, sqrt_out)
 
 
+def bert_rowcol_max(x: Tensor, y: Tensor) -> "tuple[Tensor, Tensor]":
+    """Row / column maxima of ``x[b] @ y[b]^T`` for token sets of at most 128 per side (``csrc/text/bert_match.hip``,
+    one block per pair, 64 x 64 MFMA super-tiles).  x ``[B, P, D]``, y ``[B, R, D]`` fp32."""
+    b, p, _ = x.shape
+    r = y.shape[1]
+    rmax = torch.empty(b, p, dtype=torch.float32, device=x.device)
+    cmax = torch.empty(b, r, dtype=torch.float32, device=x.device)
+    _ops().bert_rowcol_max(x.contiguous(), y.contiguous(), rmax, cmax)
+    return rmax, cmax
+
+
 def gemm_row_col_max(x: Tensor, y: Tensor, scale: float = 1.0) -> "tuple[Tensor, Tensor]":
     """``max_j scale * x_i.y_j`` per row and ``max_i`` per column of batched ``[B, N, D] x [B, M, D]`` fp32 operands
     from one MFMA GEMM launch whose epilogue keeps only the per-tile maxima (the ``[B, N, M]`` score matrix is never

@@ -61,13 +61,18 @@ def _max_over_ranks(x: float, device: torch.device, world: int) -> float:
 
 
 def _data(device: torch.device, rank: int, ring_mb: int):
+    """The input ring as ONE [k, 8192, 1000] bf16 allocation (plus one [k, 8192] int64 target block), filled in
+    place: a single large segment instead of k separate ones (measured: the first timed region after k separate
+    allocations ran ~25 % slower, profiles/r03_first_region.md)."""
     per = BATCH * NUM_CLASSES * 2
     k = max(2, (ring_mb * 2**20 + per - 1) // per)
     gdev = device if device.type == "cuda" else torch.device("cpu")
     g = torch.Generator(device=gdev).manual_seed(1234 + rank)
-    preds = [torch.randn(BATCH, NUM_CLASSES, generator=g, device=gdev).to(torch.bfloat16) for _ in range(k)]
-    target = [torch.randint(0, NUM_CLASSES, (BATCH,), generator=g, device=gdev) for _ in range(k)]
-    return preds, target
+    ring = torch.empty(k, BATCH, NUM_CLASSES, dtype=torch.bfloat16, device=gdev)
+    for i in range(k):
+        ring[i].copy_(torch.randn(BATCH, NUM_CLASSES, generator=g, device=gdev))
+    target = torch.randint(0, NUM_CLASSES, (k, BATCH), generator=g, device=gdev)
+    return list(ring.unbind(0)), list(target.unbind(0))
 
 
 def _warm(metric, preds, target, warmup: int) -> None:
@@ -133,11 +138,7 @@ def main() -> None:
         from benchmarks.reference_path import ReferenceEmulatedConfusionMatrix
 
         ref = ReferenceEmulatedConfusionMatrix(NUM_CLASSES, device)
-    # both implementations get their W warm-up updates before either is timed (a region that directly follows a long
-    # idle period -- data generation -- runs on a cold host launch path; see profiles/r03_first_region.md)
     _warm(ours, preds, target, args.warmup)
-    if ref is not None:
-        _warm(ref, preds, target, args.warmup)
     t_ours, cms_ours, res_ours = _timed(ours, preds, target, args.steps, args.warmup, device, world)
     comms = comm_stats()
     t_ours = _max_over_ranks(t_ours, device, world)
@@ -146,6 +147,7 @@ def main() -> None:
     base_val = None
     t_ref = cms_ref = None
     if ref is not None:
+        _warm(ref, preds, target, args.warmup)
         t_ref, cms_ref, res_ref = _timed(ref, preds, target, args.steps, args.warmup, device, world)
         t_ref = _max_over_ranks(t_ref, device, world)
         cms_ref = _max_over_ranks(cms_ref, device, world)

@@ -27,8 +27,15 @@ def main():
         assert rc == 0, rc
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(1234)
-    preds = [torch.randn(B, C, generator=g, device=dev).to(torch.bfloat16) for _ in range(K)]
-    target = [torch.randint(0, C, (B,), generator=g, device=dev) for _ in range(K)]
+    if case.startswith("onering"):
+        ring = torch.empty(K, B, C, dtype=torch.bfloat16, device=dev)
+        for i in range(K):
+            ring[i].copy_(torch.randn(B, C, generator=g, device=dev))
+        preds = list(ring.unbind(0))
+        target = list(torch.randint(0, C, (K, B), generator=g, device=dev).unbind(0))
+    else:
+        preds = [torch.randn(B, C, generator=g, device=dev).to(torch.bfloat16) for _ in range(K)]
+        target = [torch.randint(0, C, (B,), generator=g, device=dev) for _ in range(K)]
     m = MulticlassConfusionMatrix(num_classes=C).to(dev)
     import gc
 
@@ -52,13 +59,13 @@ def main():
         t_s = time.perf_counter()
         while time.perf_counter() - t_s < 0.02:
             pass
-    if case == "heavyspin20":
+    if case in ("heavyspin20", "onering_heavy"):
         a = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
         t_s = time.perf_counter()
         while time.perf_counter() - t_s < 0.02:
             a = (a @ a).clamp_(-1, 1)
             torch.cuda.synchronize()
-    if case == "readring":
+    if case in ("readring", "onering_read"):
         acc = torch.zeros((), device=dev)
         for p in preds:
             acc += p.float().sum()

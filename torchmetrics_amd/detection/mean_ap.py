@@ -13,6 +13,7 @@ image -- ordinary tensor list states, so the sync engine gathers them (the refer
 import contextlib
 import io
 import json
+from collections.abc import Mapping
 from typing import Any, ClassVar, Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
@@ -248,43 +249,87 @@ class MeanAveragePrecision(Metric):
         result.update({"classes": torch.tensor(self._get_classes(), dtype=torch.int32)})
         return result
 
-    def _ious(self, i_type: str) -> Dict[Tuple[int, int], Tensor]:
-        """Per (image, class) IoU matrices: detections in score order (max-dets truncated) x ground truths."""
-        out: Dict[Tuple[int, int], Tensor] = {}
+    def _ious(self, i_type: str) -> "IoUTable":
+        """Per (image, class) IoU matrices -- detections in score order (max-dets truncated) x ground truths -- for every
+        pair where the class occurs in the image.
+
+        Batched: all images' detections and ground truths are keyed ``image * K + class``, ordered by (key, score)
+        with one stable sort each, every (detection, ground truth) pair of a key is enumerated with prefix sums and all
+        IoUs are evaluated in one pass (boxes elementwise, masks by one ``rle_iou`` launch), then copied to the host
+        ONCE.  The reference gets the same dictionary from pycocotools' per-(image, class) Python loop; the previous
+        version here synchronised twice per (image, class)."""
         classes = self._get_classes()
-        if i_type == "segm":
-            (dbuf, ddesc), (gbuf, gdesc) = self._rle_states(self._state_device())
-            d_base = [0]
-            for x in self.detection_labels:
-                d_base.append(d_base[-1] + x.numel())
-            g_base = [0]
-            for x in self.groundtruth_labels:
-                g_base.append(g_base[-1] + x.numel())
+        n_img = len(self.detection_labels)
+        if n_img == 0 or not classes:
+            return IoUTable([], torch.zeros(0), [], [])
+        dev = self._state_device()
+        cls_t = torch.tensor(classes, dtype=torch.long, device=dev)
+        k = len(classes)
+        max_det = self.max_detection_thresholds[-1]
+
+        def flat(lst, img_count=None):
+            parts = [x.reshape(-1).to(dev) for x in lst]
+            sizes = torch.tensor([x.numel() for x in lst], device=dev)
+            cat = torch.cat(parts) if parts else torch.zeros(0, device=dev)
+            return cat, torch.repeat_interleave(torch.arange(len(lst), device=dev), sizes)
+
+        d_lab, d_img = flat(self.detection_labels)
+        g_lab, g_img = flat(self.groundtruth_labels)
+        d_key = d_img * k + torch.searchsorted(cls_t, d_lab.long())
+        g_key = g_img * k + torch.searchsorted(cls_t, g_lab.long())
+        d_score = torch.cat([x.reshape(-1).to(dev) for x in self.detection_scores])
+        # detections: by key, then descending score (stable: ties keep their input order, as argsort(-s, stable))
+        by_score = torch.argsort(-d_score, stable=True)
+        d_order = by_score[torch.argsort(d_key[by_score], stable=True)]
+        ks = d_key[d_order]
+        nk = n_img * k
+        d_cnt = torch.bincount(ks, minlength=nk)
+        d_start = torch.cumsum(d_cnt, 0) - d_cnt
+        rank = torch.arange(ks.numel(), device=dev) - d_start[ks]
+        keep = rank < max_det
+        d_order, ks = d_order[keep], ks[keep]
+        d_cnt = torch.bincount(ks, minlength=nk)
+        g_order = torch.argsort(g_key, stable=True)
+        g_cnt = torch.bincount(g_key, minlength=nk)
+        g_start = torch.cumsum(g_cnt, 0) - g_cnt
+        present = torch.nonzero((d_cnt > 0) | (g_cnt > 0)).flatten()
+        # pairs: detection i (sorted) x every ground truth of its key
+        per_det = g_cnt[ks]
+        pair_det = torch.repeat_interleave(torch.arange(ks.numel(), device=dev), per_det)
+        pair_start = torch.cumsum(per_det, 0) - per_det
+        within = torch.arange(pair_det.numel(), device=dev) - pair_start[pair_det]
+        pd = d_order[pair_det]
+        pg = g_order[g_start[ks[pair_det]] + within]
+        if i_type == "bbox":
+            db = torch.cat([b.reshape(-1, 4).to(dev) for b in self.detection_box]).double()
+            gb = torch.cat([b.reshape(-1, 4).to(dev) for b in self.groundtruth_box]).double()
+            crowd = torch.cat([c.reshape(-1).to(dev) for c in self.groundtruth_crowds]).bool()
+            d, g = db[pd], gb[pg]
+            x1, y1 = torch.maximum(d[:, 0], g[:, 0]), torch.maximum(d[:, 1], g[:, 1])
+            x2 = torch.minimum(d[:, 0] + d[:, 2], g[:, 0] + g[:, 2])
+            y2 = torch.minimum(d[:, 1] + d[:, 3], g[:, 1] + g[:, 3])
+            w, h = x2 - x1, y2 - y1
+            inter = torch.where((w > 0) & (h > 0), w * h, torch.zeros_like(w))
+            da = d[:, 2] * d[:, 3]
+            union = torch.where(crowd[pg], da, da + g[:, 2] * g[:, 3] - inter)
+            vals = torch.where(inter > 0, inter / union, torch.zeros_like(inter)).float()
+        else:
+            (dbuf, ddesc), (gbuf, gdesc) = self._rle_states(dev)
             g_crowd = torch.cat([c.reshape(-1) for c in self.groundtruth_crowds]).to(gdesc.device).clamp(0, 1)
             g_crowd = g_crowd.to(torch.uint8) if g_crowd.numel() else torch.zeros(0, dtype=torch.uint8,
                                                                                 device=gdesc.device)
-        for img in range(len(self.detection_labels)):
-            for cls in classes:
-                dl, gl = self.detection_labels[img] == cls, self.groundtruth_labels[img] == cls
-                if not bool(dl.any()) and not bool(gl.any()):
-                    continue
-                scores = self.detection_scores[img][dl]
-                order = torch.argsort(-scores, stable=True)[: self.max_detection_thresholds[-1]]
-                if i_type == "bbox":
-                    d = self.detection_box[img].reshape(-1, 4)[dl][order]
-                    g = self.groundtruth_box[img].reshape(-1, 4)[gl]
-                    crowd = self.groundtruth_crowds[img][gl].bool()
-                    mat = _coco_iou_matrix(d.double(), g.double(), crowd).float().cpu()
-                else:
-                    dev = ddesc.device
-                    di = torch.nonzero(dl.to(dev)).flatten()[order.to(dev)] + d_base[img]
-                    gi = torch.nonzero(gl.to(dev)).flatten() + g_base[img]
-                    pd = di.repeat_interleave(gi.numel())
-                    pg = gi.repeat(di.numel())
-                    vals = ops.rle_iou(dbuf, ddesc, gbuf, gdesc, pd.contiguous(), pg.contiguous(), g_crowd)
-                    mat = vals.reshape(di.numel(), gi.numel()).float().cpu()
-                out[(img, cls)] = mat
-        return out
+            vals = ops.rle_iou(dbuf, ddesc, gbuf, gdesc, pd.to(ddesc.device).contiguous(),
+                               pg.to(ddesc.device).contiguous(), g_crowd).float()
+        # ONE host transfer: the values and the per-key shapes (pairs of a key are contiguous, row-major)
+        shapes = torch.stack([d_cnt[present], g_cnt[present]], 1)
+        pair_cnt = d_cnt * g_cnt
+        offs = (torch.cumsum(pair_cnt, 0) - pair_cnt)[present]
+        host = torch.cat([present.double(), shapes.reshape(-1).double(), offs.double(), vals.double()]).cpu()
+        npres = present.numel()
+        keys = [(int(x) // k, classes[int(x) % k]) for x in host[:npres].tolist()]
+        shp = host[npres: 3 * npres].long().reshape(-1, 2).tolist()
+        off = host[3 * npres: 4 * npres].long().tolist()
+        return IoUTable(keys, host[4 * npres:].float(), shp, off)
 
     # ---------------------------------------------------------------------------------------- COCO interop
     def tm_to_coco(self, name: str = "tm_map_input") -> None:
@@ -412,6 +457,45 @@ class MeanAveragePrecision(Metric):
             bp.append(ep)
             bt.append(et)
         return bp, bt
+
+
+class IoUTable(Mapping):
+    """``{(image, class): IoU matrix}`` backed by ONE flat host tensor; each matrix is a view made on access (the
+    extended-summary ``ious`` of tens of thousands of (image, class) pairs costs no per-entry tensor up front)."""
+
+    def __init__(self, keys: List[Tuple[int, int]], values: Tensor, shapes: List[List[int]], offsets: List[int]) -> None:
+        self._index = {key: i for i, key in enumerate(keys)}
+        self._keys = keys
+        self._values = values
+        self._shapes = shapes
+        self._offsets = offsets
+
+    def __getitem__(self, key: Tuple[int, int]) -> Tensor:
+        i = self._index[key]
+        n, m = self._shapes[i]
+        o = self._offsets[i]
+        if n * m == 1:  # compute() results go through _squeeze_if_scalar: a 1 x 1 matrix comes out 0-d, as there
+            return self._values[o]
+        return self._values[o: o + n * m].view(n, m)
+
+    def __iter__(self):
+        return iter(self._keys)
+
+    def __len__(self) -> int:
+        return len(self._keys)
+
+    def __repr__(self) -> str:
+        return f"IoUTable({len(self)} (image, class) pairs)"
+
+    _tm_flat_mapping = True
+
+    def apply_flat(self, fn: Any) -> Any:
+        """``fn`` applied to every matrix, evaluated once on the flat storage when that is equivalent (a device /
+        dtype move keeps the element count); otherwise per matrix into a plain dict."""
+        out = fn(self._values)
+        if isinstance(out, Tensor) and out.numel() == self._values.numel() and out.dim() == 1:
+            return IoUTable(self._keys, out, self._shapes, self._offsets)
+        return {k: fn(self[k]) for k in self._keys}
 
 
 def _coco_iou_matrix(d: Tensor, g: Tensor, crowd: Tensor) -> Tensor:

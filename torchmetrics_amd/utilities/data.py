@@ -26,6 +26,10 @@ def apply_to_collection(
     """Recursively apply ``function`` to every element of ``data`` that is an instance of ``dtype``."""
     if isinstance(data, dtype) and (wrong_dtype is None or not isinstance(data, wrong_dtype)):
         return function(data, *args, **kwargs)
+    if getattr(data, "_tm_flat_mapping", False):
+        # a mapping backed by one flat tensor (e.g. mAP's extended-summary IoU table): apply to the storage once
+        return data.apply_flat(lambda t: apply_to_collection(t, dtype, function, *args, wrong_dtype=wrong_dtype,
+                                                             **kwargs))
     if isinstance(data, Mapping):
         return type(data)(
             {k: apply_to_collection(v, dtype, function, *args, wrong_dtype=wrong_dtype, **kwargs) for k, v in data.items()}

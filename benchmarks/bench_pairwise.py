@@ -15,6 +15,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from torchmetrics_amd import functional as F  # noqa: E402
+from torchmetrics_amd import ops  # noqa: E402
 
 
 def ref_euclid(x, y):
@@ -50,7 +51,9 @@ def main():
         x = torch.randn(n, d, device=dev, generator=g)
         y = torch.randn(m, d, device=dev, generator=g)
         iters = 5 if n >= 8192 else 20
+        nx, ny = (x * x).sum(1), (y * y).sum(1)
         cases = [
+            ("euclidean_fp32_mfma_r2", lambda: ops.gemm_nt(x, y, ops.GEMM_EUCLID, nx, ny), None, None),
             ("euclidean", lambda: F.pairwise_euclidean_distance(x, y), lambda: ref_euclid(x, y),
              lambda: torch.cdist(x, y)),
             ("manhattan", lambda: F.pairwise_manhattan_distance(x, y),

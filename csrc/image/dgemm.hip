@@ -42,6 +42,12 @@ struct GemmProblem {
   const double* cin;  // may be null (beta ignored)
   double* c;
   double alpha, beta, diag;
+  // euclidean epilogue (out32 != null): out32[i, j] = f32(rowv[i] + colv[j] + alpha * acc), clamped at 0, sqrt'ed
+  // when sqrt_out, 0 on the diagonal when zero_diag -- the reference's fp64 formula (F/pairwise/euclidean.py:35-44)
+  const double* rowv;
+  const double* colv;
+  float* out32;
+  bool sqrt_out, zero_diag;
 };
 
 struct GemmBatch {
@@ -60,7 +66,8 @@ __device__ __forceinline__ void tile_of(int t, int nti, int ntj, int& ti, int& t
 // kWC waves across the tile's columns (2 or 4), 2 down its rows: 4 waves (64 x 64 per wave, 16 accumulators) or 8
 // waves (64 x 32 per wave, 8 accumulators: two waves per SIMD at one block per CU, so one wave's LDS waits and barrier
 // hide under the other's MFMAs).
-template <int kWC>
+// kBT: B given as [N, K] row-major (C = A B^T), staged like A and transposed into the k-major LDS slab.
+template <int kWC, bool kBT>
 __global__ void __launch_bounds__(128 * kWC, 2)
     dgemm_nn_kernel(GemmBatch batch, int nprob, int M, int N, int K, bool vec_ok) {
   constexpr int kThr = 128 * kWC;
@@ -93,6 +100,8 @@ __global__ void __launch_bounds__(128 * kWC, 2)
   constexpr int kBThrPerRow = kT / kPerB;
   const int ar = tid / kAThrPerRow, ak = (tid % kAThrPerRow) * kPerA;
   const int bk = tid / kBThrPerRow, bc = (tid % kBThrPerRow) * kPerB;
+  constexpr int kBTThrPerRow = kKC / kPerB;  // kBT: thread -> one B row (output column), kPerB consecutive k
+  const int btn = tid / kBTThrPerRow, btk = (tid % kBTThrPerRow) * kPerB;
   double ra[kPerA], rb[kPerB];
   auto load = [&](int k0) {
     const int row = i0 + ar;
@@ -110,6 +119,25 @@ __global__ void __launch_bounds__(128 * kWC, 2)
         const int k = k0 + ak + e;
         ra[e] = (row < M && k < K) ? A[static_cast<long long>(row) * K + k] : 0.0;
       }
+    }
+    if constexpr (kBT) {
+      const int n = j0 + btn;
+      if (vec_ok && n < N && k0 + btk + kPerB <= K) {
+        const double* p = B + static_cast<long long>(n) * K + k0 + btk;
+#pragma unroll
+        for (int v = 0; v < kPerB / 2; ++v) {
+          const double2 x = *reinterpret_cast<const double2*>(p + 2 * v);
+          rb[2 * v] = x.x;
+          rb[2 * v + 1] = x.y;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < kPerB; ++e) {
+          const int k = k0 + btk + e;
+          rb[e] = (n < N && k < K) ? B[static_cast<long long>(n) * K + k] : 0.0;
+        }
+      }
+      return;
     }
     const int kr = k0 + bk;
     if (vec_ok && kr < K && j0 + bc + kPerB <= N) {
@@ -132,9 +160,14 @@ __global__ void __launch_bounds__(128 * kWC, 2)
     double* a = &As[s][ar * kAStride + ak];
 #pragma unroll
     for (int e = 0; e < kPerA; ++e) a[e] = ra[e];
-    double* b = &Bs[s][bk * kBStride + bc];
+    if constexpr (kBT) {
 #pragma unroll
-    for (int e = 0; e < kPerB; ++e) b[e] = rb[e];
+      for (int e = 0; e < kPerB; ++e) Bs[s][(btk + e) * kBStride + btn] = rb[e];
+    } else {
+      double* b = &Bs[s][bk * kBStride + bc];
+#pragma unroll
+      for (int e = 0; e < kPerB; ++e) b[e] = rb[e];
+    }
   };
 
   f64x4 acc[4][kQ];
@@ -187,6 +220,13 @@ __global__ void __launch_bounds__(128 * kWC, 2)
         if (row < M && col < N) {
           const long long e = static_cast<long long>(row) * N + col;
           double v = alpha * acc[m][q][r];
+          if (pr.out32 != nullptr) {
+            float d2 = static_cast<float>(v + pr.rowv[row] + pr.colv[col]);
+            d2 = d2 > 0.f ? d2 : 0.f;
+            if (pr.zero_diag && row == col) d2 = 0.f;
+            pr.out32[e] = pr.sqrt_out ? sqrtf(d2) : d2;
+            continue;
+          }
           if (Cin != nullptr) v += beta * Cin[e];
           if (row == col) v += dg;
           C[e] = v;
@@ -309,7 +349,7 @@ void dgemm_nn(at::TensorList a, at::TensorList b, at::TensorList c, at::TensorLi
       cinp = cin[i].data_ptr<double>();
     }
     gb.p[i] = GemmProblem{a[i].data_ptr<double>(), b[i].data_ptr<double>(), cinp, c[i].data_ptr<double>(),
-                          alpha[i], beta[i], diag[i]};
+                          alpha[i], beta[i], diag[i], nullptr, nullptr, nullptr, false, false};
     vec_ok = vec_ok && reinterpret_cast<uintptr_t>(gb.p[i].a) % 16 == 0 &&
              reinterpret_cast<uintptr_t>(gb.p[i].b) % 16 == 0;
   }
@@ -320,10 +360,39 @@ void dgemm_nn(at::TensorList a, at::TensorList b, at::TensorList c, at::TensorLi
     return e ? std::atoi(e) : 8;
   }();
   if (waves == 4) {
-    hipLaunchKernelGGL(dgemm_nn_kernel<2>, dim3(tiles), dim3(256), 0, stream(), gb, np, M, N, K, vec_ok);
+    hipLaunchKernelGGL((dgemm_nn_kernel<2, false>), dim3(tiles), dim3(256), 0, stream(), gb, np, M, N, K, vec_ok);
   } else {
-    hipLaunchKernelGGL(dgemm_nn_kernel<4>, dim3(tiles), dim3(512), 0, stream(), gb, np, M, N, K, vec_ok);
+    hipLaunchKernelGGL((dgemm_nn_kernel<4, false>), dim3(tiles), dim3(512), 0, stream(), gb, np, M, N, K, vec_ok);
   }
+}
+
+// Pairwise euclidean distances with the reference's fp64 formula (F/pairwise/euclidean.py:35-44): x [N, K] and y [M, K]
+// fp64, nx [N] / ny [M] their squared row norms (fp64) -> out fp32 [N, M] = sqrt(max(f32(nx_i + ny_j - 2 x_i.y_j), 0)),
+// all in one fp64-MFMA launch (y read as rows: no transposed copy).
+void euclid_f64(const at::Tensor& x, const at::Tensor& y, const at::Tensor& nx, const at::Tensor& ny, bool zero_diag,
+                bool sqrt_out, at::Tensor out) {
+  TM_CHECK_CUDA(x);
+  for (const at::Tensor* t : {&y, &nx, &ny}) {
+    TM_SAME_DEVICE(x, *t);
+    TM_CHECK_CONTIG(*t);
+    TORCH_CHECK(t->scalar_type() == at::kDouble, "euclid_f64: fp64 operands");
+  }
+  TM_CHECK_CONTIG(x);
+  TM_SAME_DEVICE(x, out);
+  TORCH_CHECK(x.scalar_type() == at::kDouble && x.dim() == 2 && y.dim() == 2 && x.size(1) == y.size(1),
+              "euclid_f64: x [N, K], y [M, K]");
+  const int M = static_cast<int>(x.size(0)), N = static_cast<int>(y.size(0)), K = static_cast<int>(x.size(1));
+  TORCH_CHECK(nx.numel() == M && ny.numel() == N, "euclid_f64: norm sizes");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == static_cast<long long>(M) * N,
+              "euclid_f64: out must be contiguous fp32 [N, M]");
+  if (M == 0 || N == 0) return;
+  GemmBatch gb{};
+  gb.p[0] = GemmProblem{x.data_ptr<double>(), y.data_ptr<double>(), nullptr, nullptr, -2.0, 0.0, 0.0,
+                        nx.data_ptr<double>(), ny.data_ptr<double>(), out.data_ptr<float>(), sqrt_out, zero_diag};
+  const bool vec_ok = K % 2 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+                      reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0;
+  const int tiles = ((M + kT - 1) / kT) * ((N + kT - 1) / kT);
+  hipLaunchKernelGGL((dgemm_nn_kernel<4, true>), dim3(tiles), dim3(512), 0, stream(), gb, 1, M, N, K, vec_ok);
 }
 
 // One power-iteration step (see dgemv4_resid_kernel); returns nothing, writes w_out [d, 4] and part_out [blocks, 4].
@@ -359,11 +428,13 @@ TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
   m.def(
       "dgemm_nn(Tensor[] a, Tensor[] b, Tensor(a!)[] c, Tensor[] cin, float[] alpha, float[] beta, float[] diag) -> ()");
   m.def("dgemv4_blocks(int d) -> int", &dgemv4_blocks);
+  m.def("euclid_f64(Tensor x, Tensor y, Tensor nx, Tensor ny, bool zero_diag, bool sqrt_out, Tensor(a!) out) -> ()");
   m.def("dgemv4_resid(Tensor a, Tensor w_in, Tensor part_in, bool normalize, Tensor(a!) w_out, Tensor(b!) part_out) -> ()");
 }
 TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
   m.impl("dgemm_nn", &dgemm_nn);
   m.impl("dgemv4_resid", &dgemv4_resid);
+  m.impl("euclid_f64", &euclid_f64);
 }
 
 }  // namespace tm_amd

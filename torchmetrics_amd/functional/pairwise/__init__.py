@@ -64,15 +64,21 @@ def _zero_diag(d: Tensor, zero_diagonal: bool) -> Tensor:
 
 
 def _mfma_ok(x: Tensor) -> bool:
-    """ROCm, non-fp64 operands with 4-aligned rows: the matrix-core GEMM path (``ops.gemm_nt``)."""
+    """ROCm, non-fp64 operands with 4-aligned rows: the fp32 matrix-core GEMM path (``ops.gemm_nt``)."""
     return x.is_cuda and x.dtype != torch.float64 and x.shape[-1] % 4 == 0 and x.shape[-1] > 0
 
 
+def _euclid_ok(x: Tensor) -> bool:
+    """ROCm, non-empty rows, non-fp64 inputs: the fp64 matrix-core GEMM path (``ops.euclid_f64``, fp32 output).  fp64
+    inputs keep the fp64 difference kernel (``ops.pairwise_distance``), which returns fp64 distances."""
+    return x.is_cuda and x.dtype != torch.float64 and x.shape[-1] > 0
+
+
 def _euclid_mfma(x: Tensor, y: Tensor, zd: bool) -> Tensor:
-    xf, yf = x.float(), y.float()
-    nx = (xf * xf).sum(1)
-    ny = nx if y is x else (yf * yf).sum(1)
-    return ops.gemm_nt(xf, yf, ops.GEMM_EUCLID, nx, ny, zero_diagonal=zd).to(x.dtype)
+    """The reference's fp64 formula (``F/pairwise/euclidean.py:35-44``) in one fp64-MFMA launch with an fp32 epilogue:
+    near-duplicate rows keep the fp64 cancellation accuracy (an fp32 GEMM would lose ~1e-7 * |x|^2 of it)."""
+    d = ops.euclid_f64(x, y, zd)
+    return d if x.dtype == torch.float32 else d.to(x.dtype)
 
 
 def _distance(x: Tensor, y: Optional[Tensor], metric: int, p: float, reduction: _Reduction,
@@ -80,7 +86,7 @@ def _distance(x: Tensor, y: Optional[Tensor], metric: int, p: float, reduction: 
     _check_reduction(reduction)
     x, y, zd = _check_input(x, y, zero_diagonal)
     red = reduction if reduction in ("sum", "mean") else None
-    if metric == ops.PW_L2 and red is None and _mfma_ok(x):
+    if metric == ops.PW_L2 and red is None and _euclid_ok(x):
         return _euclid_mfma(x, y, zd)
     return ops.pairwise_distance(x, y, metric, p, zd, red)
 
@@ -88,7 +94,7 @@ def _distance(x: Tensor, y: Optional[Tensor], metric: int, p: float, reduction: 
 def _pairwise_euclidean_distance_update(x: Tensor, y: Optional[Tensor] = None,
                                         zero_diagonal: Optional[bool] = None) -> Tensor:
     x, y, zd = _check_input(x, y, zero_diagonal)
-    if _mfma_ok(x):
+    if _euclid_ok(x):
         return _euclid_mfma(x, y, zd)
     return ops.pairwise_distance(x, y, ops.PW_L2, 2.0, zd, None)
 

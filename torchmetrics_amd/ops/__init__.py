@@ -629,6 +629,25 @@ def dgemv4_blocks(d: int, device: Optional[torch.device] = None) -> int:
     return int(_ops().dgemv4_blocks(d))
 
 
+def euclid_f64(x: Tensor, y: Optional[Tensor], zero_diagonal: bool, sqrt: bool = True) -> Tensor:
+    """Pairwise euclidean distances with the reference's fp64 formula (``F/pairwise/euclidean.py:35-44``):
+    ``sqrt(f32(|x_i|^2 + |y_j|^2 - 2 x_i.y_j))`` with fp64 norms and an fp64-MFMA GEMM whose epilogue writes the fp32
+    distances directly (``csrc/image/dgemm.hip`` ``euclid_f64``; ``y`` read as rows, no transposed copy).  Squared
+    distances that round below zero are clamped to 0 (the reference returns NaN for them).  Returns fp32 ``[N, M]``."""
+    x64 = x.to(torch.float64).contiguous()
+    y64 = x64 if y is None or y is x else y.to(torch.float64).contiguous()
+    nx = (x64 * x64).sum(1)
+    ny = nx if y64 is x64 else (y64 * y64).sum(1)
+    if x.is_cuda:
+        out = torch.empty(x64.shape[0], y64.shape[0], dtype=torch.float32, device=x.device)
+        _ops().euclid_f64(x64, y64, nx, ny, bool(zero_diagonal), bool(sqrt), out)
+        return out
+    d2 = (nx[:, None] + ny[None, :] - 2 * (x64 @ y64.T)).float().clamp_(min=0)
+    if zero_diagonal:
+        d2.fill_diagonal_(0)
+    return d2.sqrt_() if sqrt else d2
+
+
 def dgemv4_resid(a: Tensor, w_in: Tensor, part_in: Tensor, normalize: bool, w_out: Tensor, part_out: Tensor) -> None:
     """One power-iteration step on 4 vectors: ``w_out = v - a v`` with ``v = w_in / ||w_in||`` (column norms from the
     previous step's per-block partials ``part_in``); writes this step's partial squared norms into ``part_out``."""

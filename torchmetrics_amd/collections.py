@@ -21,6 +21,7 @@ from torch.nn import ModuleDict
 
 from torchmetrics_amd import ops
 from torchmetrics_amd.metric import CompositionalMetric, Metric
+from torchmetrics_amd.parallel import arena as _arena
 from torchmetrics_amd.parallel.sync import sync_state_dicts
 from torchmetrics_amd.utilities.data import _flatten_dict, allclose
 from torchmetrics_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_single_or_multi_val
@@ -186,6 +187,14 @@ class MetricCollection(ModuleDict):
         restore: List[Tuple[Metric, bool]] = []
         for _, grp_list in plans.items():
             leaders = [g[0] for g in grp_list]
+            # every leader's reducible states in ONE arena per (reduction, dtype, device), in the engine's bucket order:
+            # each bucket of this sync is then one span (no-op once laid out); followers re-point to the views
+            if not _arena.is_packed(leaders):
+                _arena.pack(leaders)
+                for g in grp_list:
+                    for m in g[1:]:
+                        for a in g[0]._defaults:
+                            m.__dict__[a] = g[0].__dict__[a]
             entries = [({a: getattr(m, a) for a in m._reductions}, m._reductions) for m in leaders]
             word = self._sync_word(entries)
             synced = sync_state_dicts(entries, group=leaders[0].process_group, err_word=word)

@@ -26,6 +26,7 @@ import torch
 from torch import Tensor
 from torch.nn import Module
 
+from torchmetrics_amd.parallel import arena as _arena
 from torchmetrics_amd.parallel.sync import distributed_available as _engine_dist_available
 from torchmetrics_amd.parallel.sync import sync_state_dicts
 from torchmetrics_amd.utilities.data import (
@@ -200,6 +201,13 @@ class Metric(Module, ABC):
         self._defaults[name] = deepcopy(default)
         self._persistent[name] = persistent
         self._reductions[name] = dist_reduce_fx
+        self._pack_states()
+
+    def _pack_states(self) -> None:
+        """Lay the reducible tensor states out as views of one buffer per (reduction, dtype, device)
+        (:mod:`torchmetrics_amd.parallel.arena`); the sync engine then sends each bucket as one span."""
+        _arena.pack([self], force=True)
+        self.__dict__.pop("_arena_repacks", None)
 
     # ---------------------------------------------------------------------------------------------------- forward
     @torch.jit.unused
@@ -313,6 +321,7 @@ class Metric(Module, ABC):
         group = process_group or self.process_group
         states = {attr: getattr(self, attr) for attr in self._reductions}
         if dist_sync_fn is None:
+            # (sync() packed the reducible states into their arena before caching them: each bucket is one span)
             # a one-shot xGMI bucket reports failure in this metric's validation word: compute() reads the word after
             # the sync (sync() reads it right away when called on its own)
             dev = next((v.device for v in states.values() if isinstance(v, Tensor) and v.is_cuda), None)
@@ -424,6 +433,8 @@ class Metric(Module, ABC):
         is_distributed = distributed_available() if callable(distributed_available) else None
         if not should_sync or not is_distributed:
             return
+        if dist_sync_fn is None and self.dist_sync_fn is None:
+            _arena.pack([self])  # no-op when laid out already; BEFORE the cache, so unsync restores the packed views
         self._cache = {attr: getattr(self, attr) for attr in self._defaults}
         self._sync_dist(dist_sync_fn, process_group=process_group)
         self._is_synced = True
@@ -570,16 +581,28 @@ class Metric(Module, ABC):
         """
         d = self.__dict__
         d.pop("_errors_checked_at", None)
+        d.pop("_arena_repacks", None)  # a reset's fresh states are re-packed at the next sync without counting
         if not d.get("_keep_device_errors") and d.get("_device_errors") is not None:
             self._device_errors.zero_()
         self._update_count = 0
         self._forward_cache = None
         self._computed = None
+        # storage -> this metric's own tensors on it: its states and their view bases (a packed arena's buffer)
+        views: Dict[int, set] = {}
+        for attr in self._defaults:
+            t = d.get(attr)
+            if isinstance(t, Tensor) and t.layout == torch.strided:
+                own = views.setdefault(t.untyped_storage().data_ptr(), set())
+                own.add(id(t))
+                if t._base is not None:
+                    own.add(id(t._base))
+        t = own = None  # (the loop variables would count as references below)
         for attr, default in self._defaults.items():
             cur = d[attr] if attr in d else getattr(self, attr)
             if isinstance(default, Tensor):
                 # references: the state dict's entry, this local, getrefcount's argument -- nothing else
-                if not (sys.getrefcount(cur) <= 3 and self._refill_in_place(cur, default)):
+                allowed = 1 + len(views.get(cur.untyped_storage().data_ptr(), ())) if cur.layout == torch.strided else 2
+                if not (sys.getrefcount(cur) <= 3 and self._refill_in_place(cur, default, allowed)):
                     setattr(self, attr, default.detach().clone().to(cur.device))
             else:
                 setattr(self, attr, [])
@@ -588,17 +611,18 @@ class Metric(Module, ABC):
         self._is_synced = False
 
     @staticmethod
-    def _refill_in_place(cur: Any, default: Tensor) -> bool:
+    def _refill_in_place(cur: Any, default: Tensor, allowed: int = 2) -> bool:
         """Reset a tensor state by refilling its own memory when nothing else can observe it (the caller checked that
         no other Python reference to the tensor exists (a returned ``compute()`` result, a forward()'s saved global state, a compute-group
-        sibling, a user handle); here: no other tensor on its storage (views).  Then the refill is invisible, and the
+        sibling, a user handle); here: no other tensor on its storage (views) but this metric's own states of the same
+        packed arena (``allowed`` = 1 + their count).  Then the refill is invisible, and the
         state keeps its warm memory (allocator block, TLB and cache residency) -- the reference's reset always
         allocates a fresh clone of the default (S/metric.py:673-688), which is what happens here otherwise."""
         if not isinstance(cur, Tensor) or cur.requires_grad or cur.layout != torch.strided:
             return False
         if cur.shape != default.shape or cur.dtype != default.dtype or cur.device != default.device:
             return False
-        if not cur.is_contiguous() or torch._C._storage_Use_Count(cur.untyped_storage()._cdata) > 2:
+        if not cur.is_contiguous() or torch._C._storage_Use_Count(cur.untyped_storage()._cdata) > allowed:
             return False
         cur.copy_(default)
         return True
@@ -676,6 +700,7 @@ class Metric(Module, ABC):
                 raise TypeError(
                     f"Expected metric state to be either a Tensor or a list of Tensor, but encountered {cur}"
                 )
+        this._pack_states()  # the moved / cast states are separate tensors again: one buffer per bucket
         probe = fn(torch.zeros(1, device=self.device))
         self._device = probe.device
         self._dtype = probe.dtype
@@ -708,7 +733,13 @@ class Metric(Module, ABC):
                     cur = cur.detach()
                 elif isinstance(cur, list):
                     cur = [v.detach() if isinstance(v, Tensor) else v for v in cur]
-            destination[prefix + key] = deepcopy(cur)
+            if isinstance(cur, Tensor) and cur.layout == torch.strided and \
+                    cur.untyped_storage().nbytes() > cur.numel() * cur.element_size():
+                # a view of the packed arena: copy just its own elements (deepcopy would copy the whole buffer)
+                cur = cur.detach().clone().requires_grad_(cur.requires_grad)
+            else:
+                cur = deepcopy(cur)
+            destination[prefix + key] = cur
         return destination
 
     def _load_from_state_dict(

@@ -6,8 +6,10 @@ locally to the ``[W, ...]`` stack. For S states that is 3*S collectives, and eac
 
 This engine keeps the exact *result* semantics but changes the communication plan:
 
-* **reduce bucket** -- tensor states whose reduction is ``sum``/``mean``/``max``/``min`` are packed by
-  ``(op, dtype, device)`` into one flat buffer and reduced with ONE ``all_reduce`` per bucket (mean = sum / W).
+* **reduce bucket** -- tensor states whose reduction is ``sum``/``mean``/``max``/``min`` are bucketed by
+  ``(op, dtype, device)`` and reduced with ONE ``all_reduce`` per bucket (mean = sum / W).  The states already live as
+  views of one packed arena per bucket (:mod:`torchmetrics_amd.parallel.arena`), so a bucket is sent as one copy of
+  its span (``torch.cat`` only for states that fell out of their arena).
   No metadata, no host sync, no barrier.  A whole ``MetricCollection`` (all compute groups) is synced in one call,
   so a 20-metric collection costs ~2 collectives instead of ~3x(#states).
 * **one-shot path** -- on RCCL, reduce buckets of <= 256 KiB (every classification / regression state) skip the
@@ -31,6 +33,7 @@ import torch
 import torch.distributed as dist
 from torch import Tensor
 
+from torchmetrics_amd.parallel.arena import contiguous_span
 from torchmetrics_amd.parallel.oneshot import DEFAULT_SLOT_BYTES, get_oneshot
 from torchmetrics_amd.utilities.data import (
     _flatten,
@@ -166,8 +169,10 @@ def sync_state_dicts(
     # ---- reduce bucket: one all_reduce per (op, dtype, device) ------------------------------------------------
     for (kind, dtype, _device), members in reduce_buckets.items():
         wire = _WIRE_DTYPE.get(dtype, dtype)
-        if len(members) == 1:
-            flat = members[0][1].reshape(-1).to(wire, copy=True)
+        span = members[0][1].reshape(-1) if len(members) == 1 else contiguous_span([t for _, t in members])
+        if span is not None:
+            # one packed arena (parallel/arena.py) or a single state: one copy, the local states stay untouched
+            flat = span.to(wire, copy=True)
         else:
             flat = torch.cat([t.reshape(-1).to(wire) for _, t in members])
         if world > 1:

@@ -32,6 +32,7 @@ from torch import Tensor
 from torchmetrics_amd import ops
 from torchmetrics_amd.collections import MetricCollection
 from torchmetrics_amd.metric import CompositionalMetric, Metric
+from torchmetrics_amd.parallel import arena as _arena
 from torchmetrics_amd.parallel import sync as _sync
 from torchmetrics_amd.utilities.data import _squeeze_if_scalar
 from torchmetrics_amd.utilities.prints import rank_zero_warn
@@ -218,8 +219,9 @@ class GraphedCompute:
     batch still raises, with the member's own message.  Members with list states, custom sync functions or computes
     that cannot be captured (host syncs) run through their normal ``compute()``.
 
-    Under ``torch.distributed`` the graph reads a persistent arena instead of the live states: each call packs the
-    states into it (one ``torch.cat(out=)`` per (reduction, dtype) bucket) and all-reduces the buckets in place (the
+    Under ``torch.distributed`` the graph reads a persistent arena instead of the live states: each call copies the
+    states into it (one copy of the members' packed state arena per (reduction, dtype) bucket, ``parallel/arena.py``;
+    a ``torch.cat(out=)`` if a state fell out of it) and all-reduces the buckets in place (the
     engine's one-shot xGMI kernel for small buckets, RCCL otherwise -- the reduction ``sync()`` would apply).  On one
     process the graph reads the live states; ``reset()`` / ``load_state_dict`` rebinding them triggers a re-capture.
 
@@ -311,6 +313,10 @@ class GraphedCompute:
 
     def _try_capture(self, members: List[Tuple[str, Metric]]) -> Optional[torch.cuda.CUDAGraph]:
         use_arena = self._world_size > 1 or self._force_arena
+        if use_arena and self._world_size > 1:
+            # lay the live states out in this graph's bucket order (parallel/arena.py): each replay then copies every
+            # bucket with ONE copy of its span
+            self._pack_live(members)
         # distinct live state tensors, bucketed by (reduction, dtype) for the arena
         buckets: Dict[Tuple[str, torch.dtype], List[Tuple[Metric, str, Tensor]]] = {}
         seen: Dict[int, Tuple[str, torch.dtype]] = {}
@@ -431,6 +437,28 @@ class GraphedCompute:
         self._err_ids = {id(m._device_errors) for m in self._err_members}
         return graph
 
+    def _pack_live(self, members: List[Tuple[str, Metric]]) -> None:
+        seen: set = set()
+        buckets: Dict[Tuple[str, torch.dtype], List[Tuple[Metric, str, Tensor]]] = {}
+        for _, m in members:
+            for a in m._defaults:
+                t = getattr(m, a)
+                if id(t) in seen or not isinstance(t, Tensor):
+                    continue
+                seen.add(id(t))
+                kind = _sync._reduce_kind(m._reductions[a])
+                if kind is not None:
+                    buckets.setdefault((kind, t.dtype), []).append((m, a, t))
+        moved = False
+        for items in buckets.values():
+            if len(items) > 1 and _arena.contiguous_span([t for _, _, t in items]) is None:
+                _arena.pack_items(items)
+                moved = True
+        if moved:
+            for t in self.targets:
+                if isinstance(t, MetricCollection):
+                    t._compute_groups_create_state_ref()  # compute-group followers see the packed views
+
     def recapture(self) -> None:
         self._capture()
 
@@ -454,7 +482,12 @@ class GraphedCompute:
     def _replay(self) -> Dict[str, Any]:
         if self._use_arena:
             for _, pairs, flat in self._buckets:
-                torch.cat([getattr(m, a).reshape(-1) for m, a in pairs], out=flat)
+                live = [getattr(m, a) for m, a in pairs]
+                span = _arena.contiguous_span(live)
+                if span is not None:
+                    flat.copy_(span)  # the members' packed arena (parallel/arena.py): one copy
+                else:
+                    torch.cat([t.reshape(-1) for t in live], out=flat)
             for (kind, _dt), _, flat in self._buckets:
                 if kind == "none":
                     continue

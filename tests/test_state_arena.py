@@ -137,14 +137,36 @@ def _body_collection_arena(rank, world):
     members = {"acc": tm.MulticlassAccuracy(5), "prec": tm.MulticlassPrecision(5), "cm": tm.MulticlassConfusionMatrix(5)}
     refs = {k: m.clone() for k, m in members.items()}
     coll = MetricCollection(members, compute_groups=True)
-    for step in range(2):
-        coll.update(p, t)
-        out = coll.compute()
-        leaders = [getattr(coll, cg[0]) for cg in coll._groups.values()]
-        assert arena.is_packed(leaders)  # every leader's sum states in one arena per dtype
-        for k, m in refs.items():
-            m.update(p, t)
-            assert torch.allclose(out[k].float(), m.compute().float()), (step, k)
+    import torchmetrics_amd.collections as coll_mod
+
+    real_sync, real_cat, cats = coll_mod.sync_state_dicts, torch.cat, []
+
+    def counting_sync(*a, **k):  # torch.cat calls made by the engine itself during the collection's sync
+        def cat(*ca, **ck):
+            cats.append(1)
+            return real_cat(*ca, **ck)
+
+        torch.cat = cat
+        try:
+            return real_sync(*a, **k)
+        finally:
+            torch.cat = real_cat
+
+    coll_mod.sync_state_dicts = counting_sync
+    try:
+        for step in range(3):
+            coll.update(p, t)
+            cats.clear()
+            out = coll.compute()
+            if step:
+                assert not cats, "packed leaders: every bucket is one span"
+            leaders = [getattr(coll, cg[0]) for cg in coll._groups.values()]
+            assert arena.is_packed(leaders)  # every leader's sum states in one arena per dtype
+            for k, m in refs.items():
+                m.update(p, t)
+                assert torch.allclose(out[k].float(), m.compute().float()), (step, k)
+    finally:
+        coll_mod.sync_state_dicts = real_sync
 
 
 def test_collection_leaders_share_one_arena():

@@ -59,13 +59,18 @@ def _stat_reduce(
     """Reduce tp/fp/tn/fn to a score according to ``average`` (``binary``/``micro``/``macro``/``weighted``/``none``).
 
     ROCm int64 states take the single-launch fused reduction (``csrc/classification/stat_reduce.hip``)."""
-    if (tp.is_cuda and average != "binary" and tp.dtype == torch.int64 and tp.ndim in (1, 2)
-            and all(t.shape == tp.shape and t.dtype == torch.int64 for t in (fp, tn, fn))):
-        rows = (lambda t: t.reshape(1, -1)) if tp.ndim == 1 else (lambda t: t)
-        if tp.ndim == 1 or multidim_average != "global":
+    if tp.is_cuda and average != "binary" and tp.dtype == torch.int64:
+        nd = tp.ndim
+        shape = tp.shape
+        if ((nd == 1 or (nd == 2 and multidim_average != "global")) and fp.shape == shape and tn.shape == shape
+                and fn.shape == shape and fp.dtype == tn.dtype == fn.dtype == torch.int64):
             avg = _AVG_IDS[average if average is not None else "none"]
-            out = ops.stat_reduce(rows(tp), rows(fp), rows(tn), rows(fn), _KIND_IDS[kind], avg, multilabel, beta)
-            return out.reshape(tp.shape) if avg == _AVG_IDS["none"] else (out[0] if tp.ndim == 1 else out)
+            if nd == 1:
+                tp, fp, tn, fn = tp.reshape(1, -1), fp.reshape(1, -1), tn.reshape(1, -1), fn.reshape(1, -1)
+            out = ops.stat_reduce(tp, fp, tn, fn, _KIND_IDS[kind], avg, multilabel, beta)
+            if avg == 3:
+                return out.view(shape)
+            return out.view(()) if nd == 1 else out
     if average == "binary":
         return _binary_score(kind, tp, fp, tn, fn, beta)
     if average == "micro":

@@ -491,12 +491,15 @@ class Metric(Module, ABC):
             state = self.__dict__
             if state["_computed"] is not None:
                 return state["_computed"]
-            self._consolidate_cat_lists()
+            if self._fold_cat_lists:
+                self._consolidate_cat_lists()
             avail = state["distributed_available_fn"]
             if not state["_is_synced"] and not (state["_to_sync"] and callable(avail) and avail()):
                 # nothing to gather: skip the sync / unsync bookkeeping (attribute traffic per call)
                 self._check_errors_once(state)
-                value = _squeeze_if_scalar(compute(*args, **kwargs))
+                value = compute(*args, **kwargs)
+                value = (value.squeeze() if value.numel() == 1 else value) if isinstance(value, Tensor) \
+                    else _squeeze_if_scalar(value)
             else:
                 # sync FIRST, then read the validation word once: every rank has finished its collectives before any
                 # rank raises (a rank raising before the sync would leave its peers waiting), and the same read

@@ -36,7 +36,7 @@ from torchmetrics_amd.parallel import arena as _arena
 from torchmetrics_amd.parallel import sync as _sync
 from torchmetrics_amd.utilities.data import _squeeze_if_scalar
 from torchmetrics_amd.utilities.prints import rank_zero_warn
-from torchmetrics_amd.utils.deferred import capture_sink
+from torchmetrics_amd.utils.deferred import WORD_CODES, capture_sink
 from torchmetrics_amd.utils.deferred import suppress as suppress_checks
 
 
@@ -204,7 +204,7 @@ def _contig_strides(shape: Tuple[int, ...]) -> Tuple[int, ...]:
     return tuple(reversed(st))
 
 
-_WORD_CODES = {torch.int32: 0, torch.float32: 1, torch.float64: 2, torch.int64: 3, torch.uint8: 4, torch.bool: 4}
+_WORD_CODES = WORD_CODES
 
 
 class GraphedCompute:

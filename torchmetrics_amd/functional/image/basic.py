@@ -145,6 +145,18 @@ def _sam_update(preds: Tensor, target: Tensor) -> Tuple[Tensor, Tensor]:
 
 def _sam_compute(preds: Tensor, target: Tensor,
                  reduction: Literal["elementwise_mean", "sum", "none", None] = "elementwise_mean") -> Tensor:
+    """ROCm (no autograd graph needed): one pass over the channels per pixel (``ops.sam_angles``); else the
+    reference's formulation (``F/image/sam.py:56-83``)."""
+    if reduction not in ("elementwise_mean", "sum", "none", None):
+        raise ValueError("Reduction parameter unknown.")
+    fused = ops.sam_angles(preds, target, want_map=reduction in ("none", None),
+                           want_sum=reduction in ("elementwise_mean", "sum"))
+    if fused is not None:
+        amap, total = fused
+        if amap is not None:
+            return amap
+        n = preds.shape[0] * preds.shape[2] * preds.shape[3]
+        return (total / n if reduction == "elementwise_mean" else total).to(preds.dtype)
     cos = (preds * target).sum(dim=1) / (preds.norm(dim=1) * target.norm(dim=1))
     return reduce(torch.clamp(cos, -1, 1).acos(), reduction)
 
@@ -164,6 +176,12 @@ def _ergas_update(preds: Tensor, target: Tensor) -> Tuple[Tensor, Tensor]:
 def _ergas_compute(preds: Tensor, target: Tensor, ratio: float = 4,
                    reduction: Literal["elementwise_mean", "sum", "none", None] = "elementwise_mean") -> Tensor:
     b, c, h, w = preds.shape
+    st = ops.band_stats(preds, target)  # ROCm: per (image, band) Σ(p - t)² and Σt in one pass, fp64
+    if st is not None:
+        hw = h * w
+        rmse_band = torch.sqrt(st[..., 0] / hw)
+        score = (100 * ratio * torch.sqrt(torch.sum((rmse_band / (st[..., 1] / hw)) ** 2, dim=1) / c)).to(preds.dtype)
+        return reduce(score, reduction)
     p, t = preds.reshape(b, c, h * w), target.reshape(b, c, h * w)
     rmse_band = torch.sqrt(((p - t) ** 2).sum(dim=2) / (h * w))
     score = 100 * ratio * torch.sqrt(torch.sum((rmse_band / t.mean(dim=2)) ** 2, dim=1) / c)

@@ -228,6 +228,40 @@ def box_rmse_maps(preds: Tensor, target: Tensor, window: int, want_target: bool)
     return rmse_map, t_map
 
 
+def _no_grad_path(*ts: Tensor) -> bool:
+    """ROCm tensors that autograd does not need to see through (the kernels are forward-only)."""
+    return ts[0].is_cuda and not (torch.is_grad_enabled() and any(t.requires_grad for t in ts))
+
+
+def sam_angles(preds: Tensor, target: Tensor, want_map: bool, want_sum: bool) -> Optional[Tuple[Optional[Tensor],
+                                                                                                Optional[Tensor]]]:
+    """Spectral angles of ``[B, C, H, W]`` images (``csrc/image/spectral.hip``): the ``[B, H, W]`` angle map and/or
+    their fp64 sum (0-d), one pass; ``None`` off-GPU or when autograd needs the graph."""
+    if not _no_grad_path(preds, target):
+        return None
+    p, t = preds.contiguous(), target.contiguous()
+    b, _, h, w = p.shape
+    amap = torch.empty(b, h, w, dtype=p.dtype, device=p.device) if want_map else p.new_empty(0)
+    blocks = max(1, min((b * h * w + 255) // 256, 2048))
+    part = torch.empty(blocks, dtype=torch.float64, device=p.device) if want_sum else \
+        torch.empty(0, dtype=torch.float64, device=p.device)
+    _ops().sam_angles(p, t, amap, part)
+    return (amap if want_map else None), (part.sum() if want_sum else None)
+
+
+def band_stats(preds: Tensor, target: Tensor) -> Optional[Tensor]:
+    """Per (image, band) of ``[B, C, H, W]`` images: fp64 ``[B, C, 2]`` = (Σ(p - t)², Σt) in one pass
+    (``csrc/image/spectral.hip``); ``None`` off-GPU or when autograd needs the graph."""
+    if not _no_grad_path(preds, target):
+        return None
+    b, c = preds.shape[:2]
+    p, t = preds.contiguous().reshape(b * c, -1), target.contiguous().reshape(b * c, -1)
+    bpr = max(1, min(64, p.shape[1] // (256 * 32)))
+    part = torch.empty(b * c, bpr, 2, dtype=torch.float64, device=p.device)
+    _ops().band_stats(p, t, part)
+    return part.sum(1).view(b, c, 2)
+
+
 def neighbour_diff_stats(x: Tensor, y: Optional[Tensor], block_size: int, squared: bool) -> Optional[Tensor]:
     """Per image f64 ``[B, 5]``: ``Σ(x - y)^2``, neighbour differences across / off ``block_size`` boundaries
     (horizontal, then vertical); ``None`` off-GPU."""

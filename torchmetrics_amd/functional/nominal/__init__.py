@@ -71,29 +71,43 @@ def _num_classes_of(preds: Tensor, target: Tensor) -> int:
 
 
 class _TableStats:
-    """Masked statistics of a batch of contingency tables ``cm[B, R, C]`` (fp64)."""
+    """Statistics of a batch of contingency tables ``cm[B, R, C]`` with empty rows / columns masked (equal to those
+    of the compacted tables the reference builds, ``F/nominal/utils.py:34-59``).  ROCm: one block per table
+    (``ops.nominal_table_stats``, fp64); else the same quantities with masked torch ops."""
 
     def __init__(self, cm: Tensor) -> None:
-        cm = cm.to(torch.float64)
-        self.cm = cm
-        self.rs, self.cs = cm.sum(2), cm.sum(1)
-        self.rowm, self.colm = self.rs > 0, self.cs > 0
-        self.r = self.rowm.sum(1).to(torch.float64)
-        self.c = self.colm.sum(1).to(torch.float64)
-        self.n = cm.sum((1, 2))
-        self.valid = self.rowm[:, :, None] & self.colm[:, None, :]
+        st = ops.nominal_table_stats(cm) if cm.shape[-1] == cm.shape[-2] else None
+        if st is None:
+            st = self._torch_stats(cm.to(torch.float64))
+        self.n, self.r, self.c = st[:, 0], st[:, 1], st[:, 2]
+        self._chi, self._chi_yates, self.s_xy, self.s_x = st[:, 3], st[:, 4], st[:, 5], st[:, 6]
+
+    @staticmethod
+    def _torch_stats(cm: Tensor) -> Tensor:
+        rs, cs = cm.sum(2), cm.sum(1)
+        rowm, colm = rs > 0, cs > 0
+        n = cm.sum((1, 2))
+        valid = rowm[:, :, None] & colm[:, None, :]
+        exp = rs[:, :, None] * cs[:, None, :] / n[:, None, None].clamp(min=1)
+        safe_exp = torch.where(valid, exp, torch.ones_like(exp))
+        zero = torch.zeros_like(exp)
+        chi = torch.where(valid, (cm - exp) ** 2 / safe_exp, zero).sum((1, 2))
+        yates = cm + 0.5 * torch.sign(exp - cm)
+        chi_y = torch.where(valid, (yates - exp) ** 2 / safe_exp, zero).sum((1, 2))
+        nz = cm > 0
+        ratio = rs[:, :, None] / torch.where(nz, cm, torch.ones_like(cm))
+        s_xy = torch.where(nz, cm / n[:, None, None].clamp(min=1) * torch.log(ratio), zero).sum((1, 2))
+        p_x = cs / n[:, None].clamp(min=1)
+        s_x = -torch.where(colm, p_x * torch.log(torch.where(colm, p_x, torch.ones_like(p_x))),
+                           torch.zeros_like(p_x)).sum(1)
+        r, c = rowm.sum(1).to(torch.float64), colm.sum(1).to(torch.float64)
+        return torch.stack([n, r, c, chi, chi_y, s_xy, s_x, torch.zeros_like(n)], 1)
 
     def chi_squared(self, bias_correction: bool) -> Tensor:
         """Pearson chi^2 with Yates continuity correction for 2x2 tables (scipy ``chi2_contingency`` semantics)."""
-        cm, valid = self.cm, self.valid
-        exp = self.rs[:, :, None] * self.cs[:, None, :] / self.n[:, None, None].clamp(min=1)
         df = (self.r - 1) * (self.c - 1)
-        if bias_correction:
-            yates = (df == 1)[:, None, None]
-            cm = cm + torch.where(yates, 0.5 * torch.sign(exp - cm), torch.zeros_like(cm))
-        terms = torch.where(valid, (cm - exp) ** 2 / torch.where(valid, exp, torch.ones_like(exp)),
-                            torch.zeros_like(exp))
-        return torch.where(df == 0, torch.zeros_like(df), terms.sum((1, 2)))
+        chi = torch.where(df == 1, self._chi_yates, self._chi) if bias_correction else self._chi
+        return torch.where(df == 0, torch.zeros_like(df), chi)
 
     def bias_corrected(self, phi2: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
         n1 = self.n - 1
@@ -139,15 +153,7 @@ def _pearsons_batched(cm: Tensor) -> Tensor:
 def _theils_u_batched(cm: Tensor) -> Tensor:
     """U(X|Y) with X = columns (preds), Y = rows (target): (H(X) - H(X|Y)) / H(X)."""
     st = _TableStats(cm)
-    n = st.n[:, None, None]
-    p_xy = st.cm / n
-    p_y = (st.rs / st.n[:, None])[:, :, None]
-    nz = st.cm > 0
-    s_xy = torch.where(nz, p_xy * torch.log(p_y / torch.where(nz, p_xy, torch.ones_like(p_xy))),
-                       torch.zeros_like(p_xy)).sum((1, 2))
-    p_x = st.cs / st.n[:, None]
-    s_x = -torch.where(st.colm, p_x * torch.log(torch.where(st.colm, p_x, torch.ones_like(p_x))),
-                       torch.zeros_like(p_x)).sum(1)
+    s_x, s_xy = st.s_x, st.s_xy
     u = torch.where(s_x == 0, torch.zeros_like(s_x), (s_x - s_xy) / torch.where(s_x == 0, torch.ones_like(s_x), s_x))
     return u.to(torch.float32)
 

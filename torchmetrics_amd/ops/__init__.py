@@ -228,6 +228,16 @@ def box_rmse_maps(preds: Tensor, target: Tensor, window: int, want_target: bool)
     return rmse_map, t_map
 
 
+def nominal_table_stats(cm: Tensor) -> Optional[Tensor]:
+    """fp64 ``[B, 8]`` statistics of int64 contingency tables ``[B, K, K]`` (``csrc/nominal/table_stats.hip``: n, r, c,
+    chi^2, Yates chi^2, sum p_xy log(p_y / p_xy), H(X)); ``None`` off-GPU or for K > 1024."""
+    if not cm.is_cuda or cm.dim() != 3 or cm.shape[1] != cm.shape[2] or cm.shape[1] > 1024 or cm.shape[1] < 1:
+        return None
+    out = torch.empty(cm.shape[0], 8, dtype=torch.float64, device=cm.device)
+    _ops().nominal_table_stats(cm.to(torch.int64).contiguous(), out)
+    return out
+
+
 def _no_grad_path(*ts: Tensor) -> bool:
     """ROCm tensors that autograd does not need to see through (the kernels are forward-only)."""
     return ts[0].is_cuda and not (torch.is_grad_enabled() and any(t.requires_grad for t in ts))

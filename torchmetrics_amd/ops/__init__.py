@@ -228,6 +228,37 @@ def box_rmse_maps(preds: Tensor, target: Tensor, window: int, want_target: bool)
     return rmse_map, t_map
 
 
+INFO_MEASURE_IDS = {"kl_divergence": 0, "alpha_divergence": 1, "beta_divergence": 2, "ab_divergence": 3,
+                    "renyi_divergence": 4, "l1_distance": 5, "l2_distance": 6, "l_infinity_distance": 7,
+                    "fisher_rao_distance": 8}
+
+
+def info_measure(p: Tensor, t: Tensor, measure: str, alpha: float, beta: float) -> Optional[Tensor]:
+    """InfoLM information measure per row of fp32 ``[N, V]`` distributions in one launch (``csrc/text/infolm.hip``),
+    including the reference's ``nan_to_num``; ``None`` off-GPU / non-fp32 / autograd."""
+    if not _no_grad_path(p, t) or p.dtype != torch.float32 or t.dtype != torch.float32 or p.dim() != 2 \
+            or p.shape != t.shape:
+        return None
+    out = torch.empty(p.shape[0], dtype=torch.float32, device=p.device)
+    mid = INFO_MEASURE_IDS[measure]
+    _ops().info_measure(p.contiguous(), t.contiguous(), mid, float(1.0 if mid == 2 else alpha), float(beta), out)
+    return out
+
+
+def infolm_accumulate(logits: Tensor, temperature: float, w: Tensor, rows: Tensor, acc: Tensor) -> None:
+    """``acc[rows[r]] += w[r] * softmax(logits[r] / temperature)`` for masked-LM logits ``[R, V]`` whose ``rows`` (CPU
+    int64, non-decreasing: one sentence's positions are consecutive) name the destination row of ``acc`` fp32 [N, V];
+    two launches, no [R, V] probabilities (``csrc/text/infolm.hip``)."""
+    if rows.numel() == 0:
+        return
+    sents, counts = torch.unique_consecutive(rows, return_counts=True)
+    seg = torch.zeros(counts.numel() + 1, dtype=torch.int64)
+    torch.cumsum(counts, 0, out=seg[1:])
+    dev = logits.device
+    _ops().infolm_accumulate(logits.contiguous(), float(temperature), w.to(dev, torch.float32).contiguous(),
+                             seg.to(dev), sents.to(dev, torch.int64), acc)
+
+
 def nominal_table_stats(cm: Tensor) -> Optional[Tensor]:
     """fp64 ``[B, 8]`` statistics of int64 contingency tables ``[B, K, K]`` (``csrc/nominal/table_stats.hip``: n, r, c,
     chi^2, Yates chi^2, sum p_xy log(p_y / p_xy), H(X)); ``None`` off-GPU or for K > 1024."""

@@ -1,0 +1,167 @@
+// COCO accumulation for every (category, IoU threshold, area range, max-dets) at once.
+//
+// Reference: pycocotools COCOeval.accumulate as driven by S/detection/mean_ap.py:513-588 -- per (k, a, m) a Python
+// loop that concatenates the per-image matches, a mergesort by score, float cumulative sums, the precision envelope
+// (a reverse running max) and a searchsorted of the 101 recall thresholds.  The round-2 device version ran that as
+// ~40 batched torch ops and a host sync per max-dets value (~10 ms at 512 images x 100 detections).
+//
+// Here ONE thread per (k, t, a, m) walks its category's detections (sorted by category, then score; `seg` offsets):
+//   forward:  detections ranked past the max-dets value are skipped (pycocotools truncates each image's list); the
+//             integer true / false positive counts give rc = tp / npig, and every recall threshold is assigned the
+//             first position with rc >= threshold (searchsorted 'left', one pointer: both sequences are sorted);
+//   backward: the counts are unwound from the end, pr = tp / (tp + fp + eps) is recomputed exactly (same integers, same
+//             fp64 formula), its running maximum is the envelope, and each threshold takes the envelope value and the
+//             detection score at its position.
+// The per-detection match flags of all (t, a) pairs are packed into two 64-bit words (true / false positive bits), so
+// an iteration loads three words shared by every thread of the category (broadcast from cache).  Outputs go straight
+// into precision / scores [T, R, K, A, M] and recall [T, K, A, M]; categories without non-ignored ground truth get -1.
+#include "../common/tm_common.h"
+
+namespace tm_amd {
+namespace {
+
+constexpr int kMaxM = 8, kMaxR = 1024;
+
+struct AccArgs {
+  int T, A, M, K, R;
+  int max_dets[kMaxM];
+};
+
+__global__ void __launch_bounds__(128) coco_accumulate_kernel(const int64_t* __restrict__ tpb,
+                                                              const int64_t* __restrict__ fpb,
+                                                              const int64_t* __restrict__ rank,
+                                                              const double* __restrict__ score,
+                                                              const int64_t* __restrict__ seg,
+                                                              const double* __restrict__ npig,
+                                                              const double* __restrict__ r_thr, AccArgs args,
+                                                              int* __restrict__ pos_scratch,
+                                                              double* __restrict__ precision,
+                                                              double* __restrict__ recall,
+                                                              double* __restrict__ scores) {
+  const int T = args.T, A = args.A, M = args.M, K = args.K, R = args.R;
+  const long long gid = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (gid >= static_cast<long long>(K) * T * A * M) return;
+  const int m = static_cast<int>(gid % M);
+  const int a = static_cast<int>((gid / M) % A);
+  const int t = static_cast<int>((gid / (static_cast<long long>(M) * A)) % T);
+  const int k = static_cast<int>(gid / (static_cast<long long>(M) * A * T));
+  const int md = args.max_dets[m];
+  const long long bit = 1LL << (t * A + a);
+  const double np = npig[static_cast<long long>(a) * K + k];
+  // output addressing: precision / scores [T, R, K, A, M], recall [T, K, A, M]
+  const long long pr_base = ((static_cast<long long>(t) * R) * K + k) * A * M + static_cast<long long>(a) * M + m;
+  const long long pr_stride_r = static_cast<long long>(K) * A * M;
+  const long long rc_idx = ((static_cast<long long>(t) * K + k) * A + a) * M + m;
+  if (np <= 0.0) {  // no non-ignored ground truth: pycocotools skips the category
+    for (int r = 0; r < R; ++r) {
+      precision[pr_base + r * pr_stride_r] = -1.0;
+      scores[pr_base + r * pr_stride_r] = -1.0;
+    }
+    recall[rc_idx] = -1.0;
+    return;
+  }
+  const long long s = seg[k], e = seg[k + 1];
+  int* pos = pos_scratch + gid * R;
+  // forward: counts, recall, threshold positions
+  long long tp = 0, fp = 0;
+  int nd = 0, r = 0;
+  for (long long i = s; i < e; ++i) {
+    if (rank[i] >= md) continue;
+    tp += (tpb[i] & bit) ? 1 : 0;
+    fp += (fpb[i] & bit) ? 1 : 0;
+    ++nd;
+    const double rc = static_cast<double>(tp) / np;
+    while (r < R && rc >= r_thr[r]) pos[r++] = static_cast<int>(i);
+  }
+  recall[rc_idx] = nd ? static_cast<double>(tp) / np : 0.0;
+  // thresholds above the last recall get 0 precision / score
+  for (int q = r; q < R; ++q) {
+    precision[pr_base + q * pr_stride_r] = 0.0;
+    scores[pr_base + q * pr_stride_r] = 0.0;
+  }
+  if (r == 0) return;
+  // backward: envelope (running max of precision from the end), thresholds in decreasing order
+  const double eps = 2.220446049250313e-16;  // np.spacing(1)
+  double env = 0.0;
+  int q = r - 1;
+  for (long long i = e - 1; i >= s && q >= 0; --i) {
+    if (rank[i] >= md) continue;
+    const double p = static_cast<double>(tp) / (static_cast<double>(tp) + static_cast<double>(fp) + eps);
+    env = p > env ? p : env;
+    while (q >= 0 && pos[q] == i) {
+      precision[pr_base + q * pr_stride_r] = env;
+      scores[pr_base + q * pr_stride_r] = score[i];
+      --q;
+    }
+    tp -= (tpb[i] & bit) ? 1 : 0;
+    fp -= (fpb[i] & bit) ? 1 : 0;
+  }
+}
+
+}  // namespace
+
+// tpb / fpb int64 [D]: per detection (sorted by category, then score) bit t * A + a set for a true / false positive of
+// (IoU threshold t, area range a); rank int64 [D] (rank within its image and category); score fp64 [D]; seg int64
+// [K + 1]; npig fp64 [A, K]; r_thr fp64 [R]; max_dets int64 [M] (CPU); outputs fp64 precision / scores [T, R, K, A, M],
+// recall [T, K, A, M].
+void coco_accumulate(const at::Tensor& tpb, const at::Tensor& fpb, const at::Tensor& rank, const at::Tensor& score,
+                     const at::Tensor& seg, const at::Tensor& npig, const at::Tensor& r_thr,
+                     const at::Tensor& max_dets, int64_t T, at::Tensor precision, at::Tensor recall,
+                     at::Tensor scores) {
+  TM_CHECK_CUDA(tpb);
+  for (const at::Tensor* x : {&fpb, &rank, &score, &seg, &npig, &r_thr}) {
+    TM_SAME_DEVICE(tpb, *x);
+    TM_CHECK_CONTIG(*x);
+  }
+  TM_SAME_DEVICE(tpb, precision);
+  TM_SAME_DEVICE(tpb, recall);
+  TM_SAME_DEVICE(tpb, scores);
+  TM_CHECK_CONTIG(tpb);
+  const long long D = tpb.numel();
+  TORCH_CHECK(tpb.scalar_type() == at::kLong && fpb.scalar_type() == at::kLong && rank.scalar_type() == at::kLong &&
+                  fpb.numel() == D && rank.numel() == D,
+              "coco_accumulate: tpb / fpb / rank must be int64 [D]");
+  TORCH_CHECK(score.scalar_type() == at::kDouble && score.numel() == D, "coco_accumulate: score fp64 [D]");
+  TORCH_CHECK(npig.scalar_type() == at::kDouble && npig.dim() == 2, "coco_accumulate: npig fp64 [A, K]");
+  const int A = static_cast<int>(npig.size(0)), K = static_cast<int>(npig.size(1));
+  TORCH_CHECK(seg.scalar_type() == at::kLong && seg.numel() == K + 1, "coco_accumulate: seg int64 [K + 1]");
+  TORCH_CHECK(r_thr.scalar_type() == at::kDouble, "coco_accumulate: r_thr fp64");
+  const int R = static_cast<int>(r_thr.numel());
+  TORCH_CHECK(!max_dets.is_cuda() && max_dets.scalar_type() == at::kLong, "coco_accumulate: max_dets CPU int64");
+  const int M = static_cast<int>(max_dets.numel());
+  TORCH_CHECK(M >= 1 && M <= kMaxM && R >= 1 && R <= kMaxR && T >= 1 && T * A <= 63,
+              "coco_accumulate: 1 <= M <= 8, 1 <= R <= 1024, T * A <= 63");
+  TORCH_CHECK(D < (1LL << 31), "coco_accumulate: too many detections");
+  const long long nthr = static_cast<long long>(K) * T * A * M;
+  TORCH_CHECK(precision.scalar_type() == at::kDouble && precision.is_contiguous() &&
+                  precision.numel() == static_cast<long long>(T) * R * K * A * M &&
+                  scores.scalar_type() == at::kDouble && scores.is_contiguous() && scores.numel() == precision.numel() &&
+                  recall.scalar_type() == at::kDouble && recall.is_contiguous() && recall.numel() == nthr,
+              "coco_accumulate: outputs must be fp64 [T, R, K, A, M] / [T, K, A, M]");
+  if (nthr == 0) return;
+  AccArgs args{};
+  args.T = static_cast<int>(T);
+  args.A = A;
+  args.M = M;
+  args.K = K;
+  args.R = R;
+  const int64_t* mdp = max_dets.data_ptr<int64_t>();
+  for (int i = 0; i < M; ++i) args.max_dets[i] = static_cast<int>(std::min<int64_t>(mdp[i], 1 << 30));
+  at::Tensor pos = at::empty({nthr * R}, tpb.options().dtype(at::kInt));
+  const unsigned blocks = static_cast<unsigned>((nthr + 127) / 128);
+  hipLaunchKernelGGL(coco_accumulate_kernel, dim3(blocks), dim3(128), 0, stream(), tpb.data_ptr<int64_t>(),
+                     fpb.data_ptr<int64_t>(), rank.data_ptr<int64_t>(), score.data_ptr<double>(),
+                     seg.data_ptr<int64_t>(), npig.data_ptr<double>(), r_thr.data_ptr<double>(), args,
+                     pos.data_ptr<int>(), precision.data_ptr<double>(), recall.data_ptr<double>(),
+                     scores.data_ptr<double>());
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def(
+      "coco_accumulate(Tensor tpb, Tensor fpb, Tensor rank, Tensor score, Tensor seg, Tensor npig, Tensor r_thr, "
+      "Tensor max_dets, int T, Tensor(a!) precision, Tensor(b!) recall, Tensor(c!) scores) -> ()");
+}
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) { m.impl("coco_accumulate", &coco_accumulate); }
+
+}  // namespace tm_amd

@@ -483,3 +483,27 @@ def test_map_box_format_reference_case(box_format, iou_val_expected, map_val_exp
     result = metric.compute()
     assert result["map"].item() == map_val_expected
     assert round(float(result["ious"][(0, 0)]), 3) == iou_val_expected
+
+
+@pytest.mark.gpu
+def test_coco_accumulate_kernel_matches_torch_path(monkeypatch):
+    """The fused accumulation kernel (csrc/detection/coco_accumulate.hip) equals the batched-torch accumulation bit
+    for bit (same integer counts, same fp64 formulas), for all IoU thresholds, areas and max-dets."""
+    from benchmarks.bench_map import make_data
+    from torchmetrics_amd import ops
+    from torchmetrics_amd.detection import MeanAveragePrecision
+
+    dev = torch.device("cuda", 0)
+    preds, target = make_data(96, dev, seed=3)
+
+    def run():
+        m = MeanAveragePrecision(class_metrics=True, extended_summary=True, max_detection_thresholds=[1, 7, 50]).to(dev)
+        for i in range(0, 96, 32):
+            m.update(preds[i:i + 32], target[i:i + 32])
+        return m.compute()
+
+    fused = run()
+    monkeypatch.setattr(ops, "coco_accumulate", lambda *a, **k: False)
+    ref = run()
+    for key in ("precision", "recall", "scores", "map", "map_per_class", "mar_50_per_class", "mar_small"):
+        assert torch.equal(fused[key], ref[key]), key

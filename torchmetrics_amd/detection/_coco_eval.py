@@ -7,9 +7,11 @@ Behavioural reference: pycocotools ``COCOeval`` as driven by ``S/detection/mean_
 MI355X design: every step is a batched device computation over *all* images and categories at once --
 (1) two stable sorts group detections by (image, category) in score order and truncate to the largest max-dets;
 (2) the ``coco_match`` HIP kernel runs every (group, area range, IoU threshold) greedy matching problem in its own
-thread; (3) accumulation is a segmented cumulative sum over detections sorted by (category, score) for all
-thresholds / areas at once, a segmented reverse running-max builds the precision envelope, and recall thresholds are
-assigned with one ``searchsorted`` + scatter; (4) the summary is masked means.  The host only sees the final numbers.
+thread; (3) accumulation: on ROCm one kernel thread per (category, IoU threshold, area, max-dets) walks the
+category's score-sorted detections forward (counts, recall, threshold positions) and backward (exact precision
+envelope), ``csrc/detection/coco_accumulate.hip``; elsewhere a segmented cumulative sum over detections sorted by
+(category, score) for all thresholds / areas at once, a segmented reverse running-max for the envelope and one
+``searchsorted`` + scatter per max-dets; (4) the summary is masked means.  The host only sees the final numbers.
 """
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -30,6 +32,21 @@ def _segment_starts(sorted_keys: Tensor) -> Tensor:
     if n > 1:
         start[1:] = sorted_keys[1:] != sorted_keys[:-1]
     return torch.where(start, idx, torch.zeros_like(idx)).cummax(0).values
+
+
+def cat_states(seq: Sequence[Tensor], dev: torch.device, shape_tail: Tuple[int, ...] = ()) -> Tensor:
+    """Concatenate per-image list states into one ``[N, *shape_tail]`` tensor on ``dev``: one ``cat`` when they already
+    have that layout on one device (no per-image Python work), else reshaped one by one."""
+    seq = seq if isinstance(seq, list) else list(seq)
+    if not seq:
+        return torch.zeros((0, *shape_tail), device=dev)
+    try:
+        out = torch.cat(seq)
+        if out.dim() == 1 + len(shape_tail) and tuple(out.shape[1:]) == tuple(shape_tail):
+            return out.to(dev)
+    except RuntimeError:
+        pass
+    return torch.cat([x.to(device=dev).reshape(-1, *shape_tail) for x in seq])
 
 
 def coco_evaluate(
@@ -67,8 +84,7 @@ def coco_evaluate(
         return {"precision": precision, "recall": recall, "scores": scores_out}
 
     def flat(seq, dtype, shape_tail=()):
-        parts = [x.to(device=dev).reshape(-1, *shape_tail) for x in seq]
-        return torch.cat(parts).to(dtype) if parts else torch.zeros((0, *shape_tail), dtype=dtype, device=dev)
+        return cat_states(seq, dev, shape_tail).to(dtype)
 
     dsz = torch.tensor([x.numel() for x in det_labels], device=dev, dtype=torch.long)
     gsz = torch.tensor([x.numel() for x in gt_labels], device=dev, dtype=torch.long)
@@ -140,7 +156,10 @@ def coco_evaluate(
     npig.index_add_(1, g_cls, (~g_ig).to(torch.float64))  # [A, K]
     has_gt = npig > 0
     n = cls_s.numel()
-    if n:
+    if n and ops.coco_accumulate(tp_all, fp_all, rank_s, score_s, cls_s, npig, r_thr, max_dets, precision, recall,
+                                 scores_out):
+        pass  # ROCm: one thread per (category, threshold, area, max-dets), csrc/detection/coco_accumulate.hip
+    elif n:
         seg_first = _segment_starts(cls_s)
         is_last = torch.ones(n, dtype=torch.bool, device=dev)
         is_last[:-1] = cls_s[1:] != cls_s[:-1]

@@ -23,7 +23,7 @@ from typing_extensions import Literal
 
 from torchmetrics_amd import ops
 from torchmetrics_amd.detection import _rle
-from torchmetrics_amd.detection._coco_eval import coco_evaluate, coco_summarize, per_class_stats
+from torchmetrics_amd.detection._coco_eval import cat_states, coco_evaluate, coco_summarize, per_class_stats
 from torchmetrics_amd.detection.helpers import _fix_empty_tensors, _input_validator, _validate_iou_type_arg, box_convert
 from torchmetrics_amd.metric import Metric
 from torchmetrics_amd.utilities.prints import rank_zero_warn
@@ -203,10 +203,10 @@ class MeanAveragePrecision(Metric):
             gt_areas = [torch.where(a.to(dev) > 0, a.to(dev, torch.float64), m.to(torch.float64))
                         for a, m in zip(self.groundtruth_area, mask_area)]
         return coco_evaluate(
-            det_boxes=[b.reshape(-1, 4) for b in self.detection_box] if boxes_ok else [empty_box] * n,
+            det_boxes=self.detection_box if boxes_ok else [empty_box] * n,  # (coco_evaluate flattens with one cat)
             det_scores=self.detection_scores,
             det_labels=relabel(self.detection_labels),
-            gt_boxes=[b.reshape(-1, 4) for b in self.groundtruth_box] if boxes_ok else [empty_box] * n,
+            gt_boxes=self.groundtruth_box if boxes_ok else [empty_box] * n,
             gt_labels=relabel(self.groundtruth_labels),
             gt_crowds=self.groundtruth_crowds,
             gt_areas=gt_areas,
@@ -261,23 +261,21 @@ class MeanAveragePrecision(Metric):
         classes = self._get_classes()
         n_img = len(self.detection_labels)
         if n_img == 0 or not classes:
-            return IoUTable([], torch.zeros(0), [], [])
+            return IoUTable([], torch.zeros(0), np.zeros((0, 2), dtype=np.int64), np.zeros(0, dtype=np.int64))
         dev = self._state_device()
         cls_t = torch.tensor(classes, dtype=torch.long, device=dev)
         k = len(classes)
         max_det = self.max_detection_thresholds[-1]
 
         def flat(lst, img_count=None):
-            parts = [x.reshape(-1).to(dev) for x in lst]
             sizes = torch.tensor([x.numel() for x in lst], device=dev)
-            cat = torch.cat(parts) if parts else torch.zeros(0, device=dev)
-            return cat, torch.repeat_interleave(torch.arange(len(lst), device=dev), sizes)
+            return cat_states(lst, dev), torch.repeat_interleave(torch.arange(len(lst), device=dev), sizes)
 
         d_lab, d_img = flat(self.detection_labels)
         g_lab, g_img = flat(self.groundtruth_labels)
         d_key = d_img * k + torch.searchsorted(cls_t, d_lab.long())
         g_key = g_img * k + torch.searchsorted(cls_t, g_lab.long())
-        d_score = torch.cat([x.reshape(-1).to(dev) for x in self.detection_scores])
+        d_score = cat_states(self.detection_scores, dev)
         # detections: by key, then descending score (stable: ties keep their input order, as argsort(-s, stable))
         by_score = torch.argsort(-d_score, stable=True)
         d_order = by_score[torch.argsort(d_key[by_score], stable=True)]
@@ -301,9 +299,9 @@ class MeanAveragePrecision(Metric):
         pd = d_order[pair_det]
         pg = g_order[g_start[ks[pair_det]] + within]
         if i_type == "bbox":
-            db = torch.cat([b.reshape(-1, 4).to(dev) for b in self.detection_box]).double()
-            gb = torch.cat([b.reshape(-1, 4).to(dev) for b in self.groundtruth_box]).double()
-            crowd = torch.cat([c.reshape(-1).to(dev) for c in self.groundtruth_crowds]).bool()
+            db = cat_states(self.detection_box, dev, (4,)).double()
+            gb = cat_states(self.groundtruth_box, dev, (4,)).double()
+            crowd = cat_states(self.groundtruth_crowds, dev).bool()
             d, g = db[pd], gb[pg]
             x1, y1 = torch.maximum(d[:, 0], g[:, 0]), torch.maximum(d[:, 1], g[:, 1])
             x2 = torch.minimum(d[:, 0] + d[:, 2], g[:, 0] + g[:, 2])
@@ -326,10 +324,11 @@ class MeanAveragePrecision(Metric):
         offs = (torch.cumsum(pair_cnt, 0) - pair_cnt)[present]
         host = torch.cat([present.double(), shapes.reshape(-1).double(), offs.double(), vals.double()]).cpu()
         npres = present.numel()
-        keys = [(int(x) // k, classes[int(x) % k]) for x in host[:npres].tolist()]
-        shp = host[npres: 3 * npres].long().reshape(-1, 2).tolist()
-        off = host[3 * npres: 4 * npres].long().tolist()
-        return IoUTable(keys, host[4 * npres:].float(), shp, off)
+        pres = host[:npres].long().numpy()
+        img, cls = pres // k, np.asarray(classes, dtype=np.int64)[pres % k]
+        shp = host[npres: 3 * npres].long().reshape(-1, 2).numpy()
+        off = host[3 * npres: 4 * npres].long().numpy()
+        return IoUTable((img, cls), host[4 * npres:].float(), shp, off)
 
     # ---------------------------------------------------------------------------------------- COCO interop
     def tm_to_coco(self, name: str = "tm_map_input") -> None:
@@ -461,28 +460,42 @@ class MeanAveragePrecision(Metric):
 
 class IoUTable(Mapping):
     """``{(image, class): IoU matrix}`` backed by ONE flat host tensor; each matrix is a view made on access (the
-    extended-summary ``ious`` of tens of thousands of (image, class) pairs costs no per-entry tensor up front)."""
+    extended-summary ``ious`` of tens of thousands of (image, class) pairs costs no per-entry tensor up front).  The keys
+    are two integer arrays; the tuple keys and the lookup index are only built when the mapping is first iterated /
+    indexed, so ``compute()`` itself does no per-pair Python work."""
 
-    def __init__(self, keys: List[Tuple[int, int]], values: Tensor, shapes: List[List[int]], offsets: List[int]) -> None:
-        self._index = {key: i for i, key in enumerate(keys)}
-        self._keys = keys
+    def __init__(self, keys: Any, values: Tensor, shapes: Any, offsets: Any) -> None:
+        if isinstance(keys, tuple) and len(keys) == 2 and isinstance(keys[0], np.ndarray):
+            self._img, self._cls = keys
+        else:  # a list of (image, class) tuples
+            arr = np.asarray(keys, dtype=np.int64).reshape(-1, 2)
+            self._img, self._cls = arr[:, 0], arr[:, 1]
         self._values = values
-        self._shapes = shapes
-        self._offsets = offsets
+        self._shapes = np.asarray(shapes, dtype=np.int64).reshape(-1, 2)
+        self._offsets = np.asarray(offsets, dtype=np.int64).reshape(-1)
+        self._index: Optional[Dict[Tuple[int, int], int]] = None
+        self._key_list: Optional[List[Tuple[int, int]]] = None
+
+    def _keys(self) -> List[Tuple[int, int]]:
+        if self._key_list is None:
+            self._key_list = list(zip(self._img.tolist(), self._cls.tolist()))
+        return self._key_list
 
     def __getitem__(self, key: Tuple[int, int]) -> Tensor:
+        if self._index is None:
+            self._index = {kk: i for i, kk in enumerate(self._keys())}
         i = self._index[key]
-        n, m = self._shapes[i]
-        o = self._offsets[i]
+        n, m = int(self._shapes[i, 0]), int(self._shapes[i, 1])
+        o = int(self._offsets[i])
         if n * m == 1:  # compute() results go through _squeeze_if_scalar: a 1 x 1 matrix comes out 0-d, as there
             return self._values[o]
         return self._values[o: o + n * m].view(n, m)
 
     def __iter__(self):
-        return iter(self._keys)
+        return iter(self._keys())
 
     def __len__(self) -> int:
-        return len(self._keys)
+        return int(self._img.shape[0])
 
     def __repr__(self) -> str:
         return f"IoUTable({len(self)} (image, class) pairs)"
@@ -494,8 +507,8 @@ class IoUTable(Mapping):
         dtype move keeps the element count); otherwise per matrix into a plain dict."""
         out = fn(self._values)
         if isinstance(out, Tensor) and out.numel() == self._values.numel() and out.dim() == 1:
-            return IoUTable(self._keys, out, self._shapes, self._offsets)
-        return {k: fn(self[k]) for k in self._keys}
+            return IoUTable((self._img, self._cls), out, self._shapes, self._offsets)
+        return {k: fn(self[k]) for k in self._keys()}
 
 
 def _coco_iou_matrix(d: Tensor, g: Tensor, crowd: Tensor) -> Tensor:

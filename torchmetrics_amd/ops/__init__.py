@@ -1125,6 +1125,27 @@ def coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, g
                            iou_pre, iou_off)
 
 
+def coco_accumulate(tp_all: Tensor, fp_all: Tensor, rank_s: Tensor, score_s: Tensor, cls_s: Tensor, npig: Tensor,
+                    r_thr: Tensor, max_dets: Sequence[int], precision: Tensor, recall: Tensor, scores: Tensor) -> bool:
+    """COCO accumulation of every (category, IoU threshold, area, max-dets) in one launch
+    (``csrc/detection/coco_accumulate.hip``).  ``tp_all`` / ``fp_all`` bool ``[T, A, D]`` over detections sorted by
+    (category, score); fills ``precision`` / ``scores`` ``[T, R, K, A, M]`` and ``recall`` ``[T, K, A, M]`` in place.
+    Returns False (nothing written) where the kernel does not apply: CPU, T * A > 63 or more than 8 max-dets values."""
+    T, A, n = tp_all.shape
+    K = npig.shape[1]
+    if not tp_all.is_cuda or T * A > 63 or len(max_dets) > 8 or n == 0:
+        return False
+    shifts = torch.arange(T * A, device=tp_all.device, dtype=torch.int64)[:, None]
+    tpb = (tp_all.reshape(T * A, n).to(torch.int64) << shifts).sum(0)
+    fpb = (fp_all.reshape(T * A, n).to(torch.int64) << shifts).sum(0)
+    seg = torch.zeros(K + 1, dtype=torch.int64, device=tp_all.device)
+    torch.cumsum(torch.bincount(cls_s, minlength=K), 0, out=seg[1:])
+    _ops().coco_accumulate(tpb, fpb, rank_s.to(torch.int64).contiguous(), score_s.to(torch.float64).contiguous(), seg,
+                           npig.contiguous(), r_thr.contiguous(), torch.tensor(list(max_dets), dtype=torch.int64),
+                           int(T), precision, recall, scores)
+    return True
+
+
 def panoptic_tables(pcode: Tensor, tcode: Tensor) -> List[Tensor]:
     """Per-image pixel areas of predicted segments, target segments and segment pairs from int32 ``[B, P]`` segment
     codes (``csrc/detection/panoptic.hip``: LDS hash tables, one block per image).  Returns pair keys (int64:

@@ -100,8 +100,8 @@ class Metric(Module, ABC):
     plot_lower_bound: Optional[float] = None
     plot_upper_bound: Optional[float] = None
     plot_legend_name: Optional[str] = None
-    # fold `cat` list states into one tensor before compute() (see _consolidate_cat_lists)
-    _fold_cat_lists: bool = False
+    # fold `cat` list states into one tensor before compute() (see _consolidate_cat_lists); opt-out per class
+    _fold_cat_lists: bool = True
 
     def __init__(self, **kwargs: Any) -> None:
         super().__init__()
@@ -542,8 +542,9 @@ class Metric(Module, ABC):
         launches-worth of host work per call, O(steps^2) overall.  Folding the list into one tensor keeps each
         ``compute()`` at one ``cat`` of [accumulated, new batches].  The concatenated contents -- the only thing a
         ``cat`` reduction defines -- are unchanged (the reference folds cat lists the same way when it syncs them,
-        ``S/metric.py:431-433``).  Opt-in per class (``_fold_cat_lists``): a few reference computes look at the
-        list's element structure (e.g. EED averages per-element scores)."""
+        ``S/metric.py:431-433``).  On by default; a class whose compute looks at the list's element structure opts out
+        with ``_fold_cat_lists = False`` (EED averages per-update scores; ``None``-reduction lists such as mAP's
+        per-image states are never folded)."""
         if not self._fold_cat_lists:
             return
         for attr, fn in self._reductions.items():

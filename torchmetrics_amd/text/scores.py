@@ -320,6 +320,8 @@ class TranslationEditRate(Metric):
 class ExtendedEditDistance(Metric):
     """Extended edit distance (``S/text/eed.py:28``)."""
 
+    # compute() averages the per-update sentence-score tensors element by element: keep the list structure
+    _fold_cat_lists = False
     higher_is_better: bool = False
     is_differentiable: bool = False
     full_state_update: bool = False

@@ -25,8 +25,7 @@
 namespace tm_amd {
 namespace {
 
-constexpr int kBM = 128, kBN = 128, kBK = 32, kNT = 256;
-constexpr int kRowF = 36;  // LDS row: 32 floats + 4 pad (144 B)
+constexpr int kBM = 128, kBN = 128, kNT = 256;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -60,10 +59,13 @@ __device__ __forceinline__ float ipow(float b, int d) {
   return r;
 }
 
-template <int EPI, int STAGES>
+template <int EPI, int STAGES, int kBK>
 __global__ __launch_bounds__(kNT) void gemm_nt_kernel(const float* __restrict__ X, const float* __restrict__ Y, int N,
                                                        int M, int D, long long bx, long long by, int tiles_m,
                                                        EpiParams ep) {
+  // LDS row: kBK floats + 4 pad (conflict-free ds_read_b128 of a lane half's slab); kQ f32x4 per lane-half slab;
+  // kLd float4 loads per thread per operand and k-chunk
+  constexpr int kRowF = kBK + 4, kQ = kBK / 8, kLd = kBM * (kBK / 4) / kNT, kC4 = kBK / 4;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sa = smem;                          // [STAGES][kBM][kRowF]
   float* sb = smem + STAGES * kBM * kRowF;   // [STAGES][kBN][kRowF]
@@ -92,16 +94,16 @@ __global__ __launch_bounds__(kNT) void gemm_nt_kernel(const float* __restrict__ 
   // staging: 128 rows x 8 float4 per operand = 1024 float4 = 4 per thread.  Row pointers (gathered or strided) and
   // row validity are resolved ONCE per tile, so the k-loop's prefetch is 8 independent float4 loads with no index
   // loads or waits in between.  D % 4 == 0 (host check): a float4 is either wholly inside K or wholly past it.
-  float4 ra[4], rb[4];
-  const float* pa_row[4];
-  const float* pb_row[4];
-  bool va_row[4], vb_row[4];
-  int c4_of[4];
+  float4 ra[kLd], rb[kLd];
+  const float* pa_row[kLd];
+  const float* pb_row[kLd];
+  bool va_row[kLd], vb_row[kLd];
+  int c4_of[kLd];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < kLd; ++q) {
     const int idx = tid + q * kNT;
-    const int rr = idx >> 3;
-    c4_of[q] = (idx & 7) * 4;
+    const int rr = idx / kC4;
+    c4_of[q] = (idx % kC4) * 4;
     const int gi = row0 + rr, gj = col0 + rr;
     va_row[q] = gi < N;
     vb_row[q] = gj < M;
@@ -110,7 +112,7 @@ __global__ __launch_bounds__(kNT) void gemm_nt_kernel(const float* __restrict__ 
   }
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < kLd; ++q) {
       const int gk = k0 + c4_of[q];
       const bool kin = gk < D;
       float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
@@ -122,9 +124,9 @@ __global__ __launch_bounds__(kNT) void gemm_nt_kernel(const float* __restrict__ 
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < kLd; ++q) {
       const int idx = tid + q * kNT;
-      const int rr = idx >> 3, c4 = (idx & 7) * 4;
+      const int rr = idx / kC4, c4 = (idx % kC4) * 4;
       *reinterpret_cast<float4*>(sa + (buf * kBM + rr) * kRowF + c4) = ra[q];
       *reinterpret_cast<float4*>(sb + (buf * kBN + rr) * kRowF + c4) = rb[q];
     }
@@ -145,10 +147,10 @@ __global__ __launch_bounds__(kNT) void gemm_nt_kernel(const float* __restrict__ 
   for (int kc = 0; kc < nk; ++kc) {
     const int buf = STAGES == 2 ? (kc & 1) : 0;
     if (kc + 1 < nk) gload((kc + 1) * kBK);
-    // fragments: lane (r, h) -> rows wr + 32a + r, k in [16h, 16h + 16), read one float4 (4 k-steps) at a time and
-    // software-pipelined: the ds_reads of quarter q + 1 are in flight while the 16 MFMAs of quarter q issue
-    const float* pa0 = sa + (buf * kBM + wr + r) * kRowF + 16 * h;
-    const float* pb0 = sb + (buf * kBN + wc + r) * kRowF + 16 * h;
+    // fragments: lane (r, h) -> rows wr + 32a + r, k in [h kBK/2, (h + 1) kBK/2), read one float4 (4 k-steps) at a
+    // time and software-pipelined: the ds_reads of quarter q + 1 are in flight while the 16 MFMAs of quarter q issue
+    const float* pa0 = sa + (buf * kBM + wr + r) * kRowF + (kBK / 2) * h;
+    const float* pb0 = sb + (buf * kBN + wc + r) * kRowF + (kBK / 2) * h;
     f32x4 ca[2], cb[2];
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
@@ -156,9 +158,9 @@ __global__ __launch_bounds__(kNT) void gemm_nt_kernel(const float* __restrict__ 
       cb[a] = *reinterpret_cast<const f32x4*>(pb0 + 32 * a * kRowF);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < kQ; ++q) {
       f32x4 na[2], nb[2];
-      if (q < 3) {
+      if (q < kQ - 1) {
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
           na[a] = *reinterpret_cast<const f32x4*>(pa0 + 32 * a * kRowF + 4 * (q + 1));
@@ -173,7 +175,7 @@ __global__ __launch_bounds__(kNT) void gemm_nt_kernel(const float* __restrict__ 
           for (int b = 0; b < 2; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[a][s4], cb[b][s4], acc[a][b], 0, 0, 0);
       }
-      if (q < 3) {
+      if (q < kQ - 1) {
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
           ca[a] = na[a];
@@ -348,6 +350,23 @@ int stages_choice(int D) {
   return forced ? forced : (D >= 1024 ? 2 : 1);
 }
 
+// K chunk per LDS stage: TM_AMD_GEMM_BK=32|64 overrides
+int bk_choice(int D) {
+  static int forced = [] {
+    const char* e = std::getenv("TM_AMD_GEMM_BK");
+    return e ? (e[0] == '6' ? 64 : 32) : 0;
+  }();
+  return forced ? forced : 32;
+}
+
+template <int EPI, int STAGES, int BK>
+void launch_one(const at::Tensor& x, const at::Tensor& y, dim3 grid, int N, int M, int D, long long bx, long long by,
+                int tiles_m, const EpiParams& ep) {
+  const size_t lds = static_cast<size_t>(STAGES) * (kBM + kBN) * (BK + 4) * sizeof(float);
+  hipLaunchKernelGGL((gemm_nt_kernel<EPI, STAGES, BK>), grid, dim3(kNT), lds, stream(), x.data_ptr<float>(),
+                     y.data_ptr<float>(), N, M, D, bx, by, tiles_m, ep);
+}
+
 template <int EPI>
 void launch(const at::Tensor& x, const at::Tensor& y, int batches, long long bx, long long by, int N, int M, int D,
             const EpiParams& ep) {
@@ -355,14 +374,13 @@ void launch(const at::Tensor& x, const at::Tensor& y, int batches, long long bx,
   const int total = tiles_n * tiles_m;
   const int per = (total + 7) / 8;
   const dim3 grid(per * 8, 1, batches);
-  if (stages_choice(D) == 1) {
-    const size_t lds = (kBM + kBN) * kRowF * sizeof(float);
-    hipLaunchKernelGGL((gemm_nt_kernel<EPI, 1>), grid, dim3(kNT), lds, stream(), x.data_ptr<float>(),
-                       y.data_ptr<float>(), N, M, D, bx, by, tiles_m, ep);
+  const int st = stages_choice(D), bk = bk_choice(D);
+  if (bk == 64) {
+    if (st == 1) launch_one<EPI, 1, 64>(x, y, grid, N, M, D, bx, by, tiles_m, ep);
+    else launch_one<EPI, 2, 64>(x, y, grid, N, M, D, bx, by, tiles_m, ep);
   } else {
-    const size_t lds = 2 * (kBM + kBN) * kRowF * sizeof(float);
-    hipLaunchKernelGGL((gemm_nt_kernel<EPI, 2>), grid, dim3(kNT), lds, stream(), x.data_ptr<float>(),
-                       y.data_ptr<float>(), N, M, D, bx, by, tiles_m, ep);
+    if (st == 1) launch_one<EPI, 1, 32>(x, y, grid, N, M, D, bx, by, tiles_m, ep);
+    else launch_one<EPI, 2, 32>(x, y, grid, N, M, D, bx, by, tiles_m, ep);
   }
 }
 

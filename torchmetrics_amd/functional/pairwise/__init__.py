@@ -3,8 +3,10 @@
 Distances (euclidean, manhattan, minkowski) run on the LDS-tiled HIP difference kernel
 (:func:`torchmetrics_amd.ops.pairwise_distance`), which never materialises the reference's ``[N, M, d]`` broadcast
 (``F/pairwise/manhattan.py:39``, ``minkowski.py:43``) and fuses root, ``zero_diagonal`` and the ``sum``/``mean`` row
-reduction into the epilogue.  Similarities (linear, cosine) are plain GEMMs and go to the vendor GEMM (hipBLASLt via
-``torch.mm``); cosine row-normalises first exactly like the reference (``F/pairwise/cosine.py:24-46``).
+reduction into the epilogue; euclidean (no reduction) is the reference's fp64 formula on the fp64 MFMA GEMM.
+Similarities (linear, cosine) are plain GEMMs: small ones run on the MFMA kernel (``ops.gemm_nt``, fused scaling),
+large ones on the vendor GEMM (hipBLASLt via ``torch.mm``, see ``_VENDOR_GEMM_MACS``); cosine row-normalises first
+exactly like the reference (``F/pairwise/cosine.py:24-46``).
 """
 from typing import Optional, Tuple
 
@@ -66,6 +68,17 @@ def _zero_diag(d: Tensor, zero_diagonal: bool) -> Tensor:
 def _mfma_ok(x: Tensor) -> bool:
     """ROCm, non-fp64 operands with 4-aligned rows: the fp32 matrix-core GEMM path (``ops.gemm_nt``)."""
     return x.is_cuda and x.dtype != torch.float64 and x.shape[-1] % 4 == 0 and x.shape[-1] > 0
+
+
+# plain (store-epilogue) GEMMs of at least this many multiply-adds go to the vendor GEMM (hipBLASLt via torch.mm):
+# past the launch-overhead regime its tuned kernels are faster than ours for a plain store (bench_pairwise.py: 8192^2 x
+# 512 0.52 vs 0.62 ms, 4096^2 x 128 0.048 vs 0.060 ms); below it our MFMA kernel wins (512^2 x 64: 0.011 vs 0.021 ms).
+# Fused REDUCTION epilogues (KID / MiFID / BERTScore / row sums) stay on ops.gemm_nt: no [N, M] round trip.
+_VENDOR_GEMM_MACS = 1 << 30
+
+
+def _vendor_gemm(x: Tensor, y: Tensor) -> bool:
+    return x.is_cuda and x.shape[0] * y.shape[0] * x.shape[1] >= _VENDOR_GEMM_MACS
 
 
 def _euclid_ok(x: Tensor) -> bool:
@@ -138,7 +151,7 @@ def pairwise_minkowski_distance(x: Tensor, y: Optional[Tensor] = None, exponent:
 def _pairwise_linear_similarity_update(x: Tensor, y: Optional[Tensor] = None,
                                        zero_diagonal: Optional[bool] = None) -> Tensor:
     x, y, zd = _check_input(x, y, zero_diagonal)
-    if _mfma_ok(x):
+    if _mfma_ok(x) and not _vendor_gemm(x, y):
         return ops.gemm_nt(x, y, ops.GEMM_STORE, zero_diagonal=zd).to(x.dtype)
     return _zero_diag(_safe_matmul(x, y), zd)
 
@@ -153,7 +166,7 @@ def pairwise_linear_similarity(x: Tensor, y: Optional[Tensor] = None, reduction:
 def _pairwise_cosine_similarity_update(x: Tensor, y: Optional[Tensor] = None,
                                        zero_diagonal: Optional[bool] = None) -> Tensor:
     x, y, zd = _check_input(x, y, zero_diagonal)
-    if _mfma_ok(x):
+    if _mfma_ok(x) and not _vendor_gemm(x, y):
         ix = 1.0 / torch.linalg.vector_norm(x.float(), 2, dim=1)
         iy = ix if y is x else 1.0 / torch.linalg.vector_norm(y.float(), 2, dim=1)
         return ops.gemm_nt(x, y, ops.GEMM_COSINE, ix, iy, zero_diagonal=zd).to(x.dtype)

@@ -19,7 +19,7 @@
 //
 // dgemv4_resid_kernel: one power-iteration step on 4 vectors, W = V - A V with V = Wprev / ||Wprev|| (column norms from
 // the previous step's fixed-order per-block partials, so every block normalises identically), and this step's
-// per-block partial squared norms.  V lives in LDS; one wave per row, 16-byte loads of A.
+// per-block partial squared norms.  One wave per row, four 16-byte loads of A in flight per lane, V read from L1/L2.
 #include <cstdlib>
 
 #include "../common/tm_common.h"
@@ -235,8 +235,8 @@ __global__ void __launch_bounds__(128 * kWC, 2)
 }
 
 // ----------------------------------------------------------------------------------------------- power iteration
-constexpr int kGemvThreads = 256;
-constexpr int kGemvRowsPerWave = 2;
+constexpr int kGemvThreads = 512;
+constexpr int kGemvRowsPerWave = 1;
 
 // w_out[i][c] = v[i][c] - sum_k A[i][k] v[k][c],  v = w_in / ||w_in[:, c]||  (normalize=false: v = w_in)
 // part_in: [nb_in][4] per-block partial squared norms of w_in; part_out: [gridDim.x][4] of w_out.
@@ -244,51 +244,83 @@ __global__ void __launch_bounds__(kGemvThreads)
     dgemv4_resid_kernel(const double* __restrict__ A, const double* __restrict__ w_in,
                         const double* __restrict__ part_in, int nb_in, bool normalize, int d,
                         double* __restrict__ w_out, double* __restrict__ part_out) {
-  extern __shared__ __attribute__((aligned(16))) double vs[];  // [d][4]
+  // (A (s * v))_j = s_j (A v)_j: the previous step's normalisation is applied after the dot products, so the raw
+  // vectors are read straight from global memory (64 KB at d = 2048: L1 / L2 resident, every wave of a block reads the
+  // same k at the same time) -- no LDS copy of V before the A stream starts
   __shared__ double scale[4];
   __shared__ double wsum[kGemvThreads / kWave][4];
   const int tid = threadIdx.x;
-  if (tid < 4) {
-    double s = 1.0;
-    if (normalize) {
-      double acc = 0.0;
-      for (int b = 0; b < nb_in; ++b) acc += part_in[b * 4 + tid];  // fixed order: identical in every block
-      const double n = sqrt(acc);
-      s = 1.0 / (n > 1e-300 ? n : 1e-300);
+  const int wave = tid / kWave, lane = tid & (kWave - 1);
+  if (normalize) {
+    // column norms from the previous step's per-block partials: the whole block sums them as a fixed-shape tree
+    // (thread t: partials t, t + 512, ...; then wave shuffles and the 8 wave sums in order), so every block gets
+    // bit-identical norms -- and no single thread walks all partials in a dependent chain
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    const f64x4* P = reinterpret_cast<const f64x4*>(part_in);
+    for (int b = tid; b < nb_in; b += kGemvThreads) {
+      const f64x4 v = P[b];
+      acc[0] += v[0];
+      acc[1] += v[1];
+      acc[2] += v[2];
+      acc[3] += v[3];
     }
-    scale[tid] = s;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = wave_sum(acc[j]);
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wsum[wave][j] = acc[j];
+    }
+    __syncthreads();
+    if (tid < 4) {
+      double tot = 0.0;
+      for (int w = 0; w < kGemvThreads / kWave; ++w) tot += wsum[w][tid];
+      const double n = sqrt(tot);
+      scale[tid] = 1.0 / (n > 1e-300 ? n : 1e-300);
+    }
+  } else if (tid < 4) {
+    scale[tid] = 1.0;
   }
   __syncthreads();
-  for (int e = tid; e < d * 4; e += kGemvThreads) vs[e] = w_in[e] * scale[e & 3];
-  __syncthreads();
-  const int wave = tid / kWave, lane = tid & (kWave - 1);
   double sq[4] = {0.0, 0.0, 0.0, 0.0};
   const int row0 = (blockIdx.x * (kGemvThreads / kWave) + wave) * kGemvRowsPerWave;
+  const f64x4* V = reinterpret_cast<const f64x4*>(w_in);  // [d][4]
   for (int rr = 0; rr < kGemvRowsPerWave; ++rr) {
     const int row = row0 + rr;
     if (row >= d) break;  // wave-uniform
     const double* ar = A + static_cast<long long>(row) * d;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    for (int k = lane * 2; k < d; k += 2 * kWave) {
-      double a0, a1;
-      if (k + 1 < d && ((d & 1) == 0)) {
-        const double2 x = *reinterpret_cast<const double2*>(ar + k);
-        a0 = x.x;
-        a1 = x.y;
-      } else {
-        a0 = ar[k];
-        a1 = k + 1 < d ? ar[k + 1] : 0.0;
+    if ((d & 1) == 0) {
+      // 4 independent 16-byte loads of A in flight per lane per iteration
+      int k = lane * 2;
+      for (; k + 3 * 2 * kWave < d; k += 4 * 2 * kWave) {
+        double2 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const double2*>(ar + k + u * 2 * kWave);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const f64x4 va = V[k + u * 2 * kWave], vb = V[k + u * 2 * kWave + 1];
+          s0 += x[u].x * va[0] + x[u].y * vb[0];
+          s1 += x[u].x * va[1] + x[u].y * vb[1];
+          s2 += x[u].x * va[2] + x[u].y * vb[2];
+          s3 += x[u].x * va[3] + x[u].y * vb[3];
+        }
       }
-      const double* v0 = vs + k * 4;
-      s0 += a0 * v0[0];
-      s1 += a0 * v0[1];
-      s2 += a0 * v0[2];
-      s3 += a0 * v0[3];
-      if (k + 1 < d) {
-        s0 += a1 * v0[4];
-        s1 += a1 * v0[5];
-        s2 += a1 * v0[6];
-        s3 += a1 * v0[7];
+      for (; k < d; k += 2 * kWave) {
+        const double2 x = *reinterpret_cast<const double2*>(ar + k);
+        const f64x4 va = V[k], vb = V[k + 1];
+        s0 += x.x * va[0] + x.y * vb[0];
+        s1 += x.x * va[1] + x.y * vb[1];
+        s2 += x.x * va[2] + x.y * vb[2];
+        s3 += x.x * va[3] + x.y * vb[3];
+      }
+    } else {
+      for (int k = lane; k < d; k += kWave) {
+        const double a0 = ar[k];
+        const f64x4 va = V[k];
+        s0 += a0 * va[0];
+        s1 += a0 * va[1];
+        s2 += a0 * va[2];
+        s3 += a0 * va[3];
       }
     }
 #pragma unroll
@@ -300,7 +332,7 @@ __global__ void __launch_bounds__(kGemvThreads)
     }
     if (lane < 4) {
       const double s = lane == 0 ? s0 : lane == 1 ? s1 : lane == 2 ? s2 : s3;
-      const double w = vs[row * 4 + lane] - s;
+      const double w = scale[lane] * (w_in[row * 4 + lane] - s);
       w_out[row * 4 + lane] = w;
       sq[lane] += w * w;
     }
@@ -417,9 +449,10 @@ void dgemv4_resid(const at::Tensor& a, const at::Tensor& w_in, const at::Tensor&
   const int nb = static_cast<int>(dgemv4_blocks(d));
   TORCH_CHECK(part_out.numel() == 4LL * nb, "dgemv4_resid: part_out must be [", nb, ", 4]");
   TORCH_CHECK(!normalize || part_in.numel() % 4 == 0, "dgemv4_resid: part_in must be [blocks, 4]");
-  const size_t lds = static_cast<size_t>(d) * 4 * sizeof(double);
-  TORCH_CHECK(lds <= 128 * 1024, "dgemv4_resid: d too large for the LDS-resident vectors");
-  hipLaunchKernelGGL(dgemv4_resid_kernel, dim3(nb), dim3(kGemvThreads), lds, stream(), a.data_ptr<double>(),
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(w_in.data_ptr()) % 32 == 0 && reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(part_in.data_ptr()) % 32 == 0,
+              "dgemv4_resid: 32-byte aligned vectors / partials, 16-byte aligned matrix");
+  hipLaunchKernelGGL(dgemv4_resid_kernel, dim3(nb), dim3(kGemvThreads), 0, stream(), a.data_ptr<double>(),
                      w_in.data_ptr<double>(), part_in.data_ptr<double>(), static_cast<int>(part_in.numel() / 4),
                      normalize, d, w_out.data_ptr<double>(), part_out.data_ptr<double>());
 }

@@ -89,6 +89,8 @@ def _trace_sqrt_newton_schulz(sigma1: Tensor, sigma2: Tensor, rtol: float = 1e-8
     a fresh run with floor 1e-6 (a schedule cannot be resumed: its first scale factors collapse the converged
     eigenvalues).  Covariance products with eigenvalues below that (rank-deficient or extremely ill-conditioned: |Z| ~
     P^{-1/2} explodes and its rounding feeds back through ``Z Y``) return None and the caller takes the eigensolve.
+    The final unscaled probe step is evaluated through its trace only (one GEMM for ``W``; ``tr(Y T)`` from
+    ``sum(Y * W^T)``) -- the result is that step's trace, as if the step had been taken.
     Host reads: one for the two floor estimates, one per schedule for (tr before, tr after, max |Z|)."""
     d = sigma1.shape[0]
     p = torch.empty_like(sigma1)
@@ -114,15 +116,21 @@ def _trace_sqrt_newton_schulz(sigma1: Tensor, sigma2: Tensor, rtol: float = 1e-8
                 torch.mul(a0, alpha, out=z)  # Z1 = T = b I + a Y0
                 z.diagonal().add_(beta)
                 continue
-            if i == len(sched) - 1:
-                before = y.diagonal().sum()
             ops.dgemm(z, y, w)  # W = Z Y
+            if i == len(sched) - 1:
+                # the unscaled probe step only needs its trace: tr(Y T) = tr(Y (3I - W)) / 2 = 1.5 tr Y - 0.5 tr(Y W),
+                # with tr(Y W) = sum(Y * W^T) -- one GEMM (W) instead of three
+                before = y.diagonal().sum()
+                after_t = 1.5 * before - 0.5 * (y * w.T).sum()
+                break
             ops.dgemm([y, w], [w, z], [yn, zn], alpha=[alpha, alpha], beta=[beta, beta], cin=[y, z])
             y, yn = yn, y
             z, zn = zn, z
-        before, after, zmax = torch.stack([before, y.diagonal().sum(), z.abs().max()]).tolist()
-        if math.isfinite(after) and abs(after - before) <= rtol * abs(after) and zmax <= zcap:
-            return c.sqrt() * y.diagonal().sum()
+        if before is None:  # (a one-step schedule cannot happen: every schedule ends with the probe)
+            continue
+        before_v, after, zmax = torch.stack([before, after_t, z.abs().max()]).tolist()
+        if math.isfinite(after) and abs(after - before_v) <= rtol * abs(after) and zmax <= zcap:
+            return c.sqrt() * after_t
     return None
 
 

@@ -275,36 +275,110 @@ __global__ __launch_bounds__(256) void retrieval_metric_kernel(const scalar_t* _
   }
 }
 
+// largest query size -> nq[1] (vector atomics; nq[1] zeroed by the caller)
+__global__ void query_max_size_kernel(const int32_t* __restrict__ begin, int32_t* __restrict__ nq) {
+  const int n_q = nq[0];
+  int m = 0;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n_q; q += gridDim.x * blockDim.x)
+    m = max(m, begin[q + 1] - begin[q]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off, kWave));
+  if ((threadIdx.x & (kWave - 1)) == 0 && m > 0) atomicMax(nq + 1, m);
+}
+
+// Precision@k / recall@k for k = 1..K of every query (reference F/retrieval/precision_recall_curve.py:87-99 per
+// query).  One wave per query walks k in 64-wide chunks: a wave inclusive scan of the relevance of the documents at
+// rank k gives the hit count of the top k; ranks past the query's size add nothing (the reference pads with zeros).
+// Denominators: k, or min(k, size) with adaptive_k; recall divides by the query's relevant count.  Queries without a
+// relevant document write zeros and set ``empty`` (the empty-target policy is applied by the caller).
+template <typename target_t>
+__global__ __launch_bounds__(256) void retrieval_pr_curve_kernel(const target_t* __restrict__ target,
+                                                                 const int32_t* __restrict__ order,
+                                                                 const int32_t* __restrict__ begin, int n_q,
+                                                                 int64_t K, bool adaptive_k, float* __restrict__ prec,
+                                                                 float* __restrict__ rec, uint8_t* __restrict__ empty) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kWave;
+  for (int64_t q = wave; q < n_q; q += nwaves) {
+    const int64_t b = begin[q], e = begin[q + 1];
+    const int64_t size = e - b;
+    double rel = 0.0;
+    for (int64_t i = b + lane; i < e; i += kWave) rel += tval(target, order[i]) > 0.0 ? 1.0 : 0.0;
+    rel = wave_sum(rel);
+    float* pq = prec + q * K;
+    float* rq = rec + q * K;
+    double cum = 0.0;
+    for (int64_t c = 0; c < K; c += kWave) {
+      const int64_t k = c + lane;  // rank k (0-based) -> top (k + 1)
+      double hv = (k < size && k < K && tval(target, order[b + k]) > 0.0) ? 1.0 : 0.0;
+#pragma unroll
+      for (int d = 1; d < kWave; d <<= 1) {
+        const double o = __shfl_up(hv, d, kWave);
+        if (lane >= d) hv += o;
+      }
+      const double hits = cum + hv;
+      if (k < K) {
+        const double denom = adaptive_k ? static_cast<double>(k + 1 < size ? k + 1 : size) : static_cast<double>(k + 1);
+        pq[k] = rel > 0.0 ? static_cast<float>(hits / denom) : 0.0f;
+        rq[k] = rel > 0.0 ? static_cast<float>(hits / rel) : 0.0f;
+      }
+      cum += __shfl(hv, kWave - 1, kWave);
+      if (c + kWave >= size) {
+        // every document of the query is counted: the rest of the row only changes through its denominator
+        for (int64_t k2 = c + kWave + lane; k2 < K; k2 += kWave) {
+          const double denom =
+              adaptive_k ? static_cast<double>(k2 + 1 < size ? k2 + 1 : size) : static_cast<double>(k2 + 1);
+          pq[k2] = rel > 0.0 ? static_cast<float>(cum / denom) : 0.0f;
+          rq[k2] = rel > 0.0 ? static_cast<float>(cum / rel) : 0.0f;
+        }
+        break;
+      }
+    }
+    if (lane == 0) empty[q] = rel == 0.0;
+  }
+}
+
 }  // namespace
 
-// preds [n] float, target [n] (int/bool/float), indexes [n] int64.
-// Returns (values fp64 [n] (first n_queries valid), empty uint8 [n], n_queries int32 [1]).
-std::vector<at::Tensor> retrieval_metric(const at::Tensor& preds, const at::Tensor& target, const at::Tensor& indexes,
-                                         int64_t kind, int64_t top_k, bool adaptive_k) {
+namespace {
+
+// Documents ordered by (query id, score descending) plus the device-side query table.
+struct QuerySegments {
+  at::Tensor order;   // int32 [n]: document ids in (query, score desc) order
+  at::Tensor begin;   // int32 [n + 1]: first sorted position of each query (first nq + 1 valid)
+  at::Tensor nq;      // int32 [2]: query count, largest query size (the latter filled by retrieval_pr_curve only)
+  at::Tensor incl;    // int32 [n]: 1-based query id of each sorted position
+  at::Tensor scratch; // int64 [n]: free 64-bit key buffer after segmentation
+};
+
+void check_flat_inputs(const at::Tensor& preds, const at::Tensor& target, const at::Tensor& indexes,
+                       const char* name) {
   TM_CHECK_CUDA(preds);
   TM_SAME_DEVICE(preds, target);
   TM_SAME_DEVICE(preds, indexes);
-  TORCH_CHECK(preds.dim() == 1 && target.numel() == preds.numel() && indexes.numel() == preds.numel(),
-              "retrieval_metric: flat inputs of equal size expected");
-  TORCH_CHECK(indexes.scalar_type() == at::kLong, "retrieval_metric: indexes must be int64");
-  TORCH_CHECK(preds.is_contiguous() && target.is_contiguous() && indexes.is_contiguous(),
-              "retrieval_metric: contiguous inputs expected");
+  TORCH_CHECK(preds.dim() == 1 && target.numel() == preds.numel() && indexes.numel() == preds.numel(), name,
+              ": flat inputs of equal size expected");
+  TORCH_CHECK(indexes.scalar_type() == at::kLong, name, ": indexes must be int64");
+  TORCH_CHECK(preds.is_contiguous() && target.is_contiguous() && indexes.is_contiguous(), name,
+              ": contiguous inputs expected");
+  TORCH_CHECK(preds.numel() > 0 && preds.numel() < (1LL << 31), name, ": 0 < n < 2^31 documents");
+}
+
+QuerySegments segment_queries(const at::Tensor& preds, const at::Tensor& indexes, hipStream_t st) {
   const int64_t n = preds.numel();
-  TORCH_CHECK(n > 0 && n < (1LL << 31), "retrieval_metric: 0 < n < 2^31 documents");
   const auto dev = preds.device();
-  auto st = stream();
   auto i64 = at::TensorOptions().dtype(at::kLong).device(dev);
   auto i32 = at::TensorOptions().dtype(at::kInt).device(dev);
-  auto values = at::empty({n}, at::TensorOptions().dtype(at::kDouble).device(dev));
-  auto empty = at::empty({n}, at::TensorOptions().dtype(at::kByte).device(dev));
-  auto nq = at::empty({1}, i32);
+  QuerySegments s;
+  s.nq = at::zeros({2}, i32);
   auto ka = at::empty({n}, i64), kb = at::empty({n}, i64);
   auto va = at::empty({n}, i32), vb = at::empty({n}, i32);
   auto* a = reinterpret_cast<uint64_t*>(ka.data_ptr());
   auto* bk = reinterpret_cast<uint64_t*>(kb.data_ptr());
   const int grid = grid_cap((n + 255) / 256);
   const bool f64 = preds.scalar_type() == at::kDouble;
-  TM_DISPATCH_FLOAT(preds.scalar_type(), "retrieval_metric", [&] {
+  TM_DISPATCH_FLOAT(preds.scalar_type(), "retrieval", [&] {
     hipLaunchKernelGGL((score_keys_kernel<scalar_t>), dim3(grid), dim3(256), 0, st, preds.data_ptr<scalar_t>(), n, a,
                        va.data_ptr<int32_t>());
   });
@@ -314,20 +388,47 @@ std::vector<at::Tensor> retrieval_metric(const at::Tensor& preds, const at::Tens
                      vb.data_ptr<int32_t>(), n, a);
   sortscan::sort_pairs<uint64_t, int32_t>(a, bk, vb.data_ptr<int32_t>(), va.data_ptr<int32_t>(), n, 0, 64, dev, st);
   // va: document ids in (query, score desc) order; bk: sorted query keys
-  auto flags = at::empty({n}, i32), incl = at::empty({n}, i32), begin = at::empty({n + 1}, i32);
+  auto flags = at::empty({n}, i32);
+  s.incl = at::empty({n}, i32);
+  s.begin = at::empty({n + 1}, i32);
   hipLaunchKernelGGL(query_flags_kernel, dim3(grid), dim3(256), 0, st, bk, n, flags.data_ptr<int32_t>());
   {
     size_t bytes = 0;
-    TORCH_CHECK(rocprim::inclusive_scan(nullptr, bytes, flags.data_ptr<int32_t>(), incl.data_ptr<int32_t>(),
+    TORCH_CHECK(rocprim::inclusive_scan(nullptr, bytes, flags.data_ptr<int32_t>(), s.incl.data_ptr<int32_t>(),
                                         static_cast<size_t>(n), rocprim::plus<int32_t>(), st) == hipSuccess,
-                "retrieval_metric: scan size query failed");
+                "retrieval: scan size query failed");
     auto tmp = at::empty({static_cast<int64_t>(bytes) + 16}, at::TensorOptions().dtype(at::kByte).device(dev));
-    TORCH_CHECK(rocprim::inclusive_scan(tmp.data_ptr(), bytes, flags.data_ptr<int32_t>(), incl.data_ptr<int32_t>(),
+    TORCH_CHECK(rocprim::inclusive_scan(tmp.data_ptr(), bytes, flags.data_ptr<int32_t>(), s.incl.data_ptr<int32_t>(),
                                         static_cast<size_t>(n), rocprim::plus<int32_t>(), st) == hipSuccess,
-                "retrieval_metric: scan failed");
+                "retrieval: scan failed");
   }
-  hipLaunchKernelGGL(query_offsets_kernel, dim3(grid), dim3(256), 0, st, incl.data_ptr<int32_t>(), n,
-                     begin.data_ptr<int32_t>(), nq.data_ptr<int32_t>());
+  hipLaunchKernelGGL(query_offsets_kernel, dim3(grid), dim3(256), 0, st, s.incl.data_ptr<int32_t>(), n,
+                     s.begin.data_ptr<int32_t>(), s.nq.data_ptr<int32_t>());
+  s.order = va;
+  s.scratch = ka;
+  return s;
+}
+
+}  // namespace
+
+// preds [n] float, target [n] (int/bool/float), indexes [n] int64.
+// Returns (values fp64 [n] (first n_queries valid), empty uint8 [n], n_queries int32 [1]).
+std::vector<at::Tensor> retrieval_metric(const at::Tensor& preds, const at::Tensor& target, const at::Tensor& indexes,
+                                         int64_t kind, int64_t top_k, bool adaptive_k) {
+  check_flat_inputs(preds, target, indexes, "retrieval_metric");
+  const int64_t n = preds.numel();
+  const auto dev = preds.device();
+  auto st = stream();
+  auto values = at::empty({n}, at::TensorOptions().dtype(at::kDouble).device(dev));
+  auto empty = at::empty({n}, at::TensorOptions().dtype(at::kByte).device(dev));
+  QuerySegments s = segment_queries(preds, indexes, st);
+  auto nq = s.nq.narrow(0, 0, 1);
+  auto va = s.order;
+  auto incl = s.incl;
+  auto begin = s.begin;
+  auto* a = reinterpret_cast<uint64_t*>(s.scratch.data_ptr());
+  auto i64 = at::TensorOptions().dtype(at::kLong).device(dev);
+  const int grid = grid_cap((n + 255) / 256);
   const uint64_t* ideal = nullptr;
   at::Tensor ik_sorted;
   if (kind == kNDCG) {
@@ -356,9 +457,46 @@ std::vector<at::Tensor> retrieval_metric(const at::Tensor& preds, const at::Tens
   return {values, empty, nq};
 }
 
+// Precision / recall curves of every query: (precision f32 [nq, K], recall f32 [nq, K], empty uint8 [nq]).
+// max_k <= 0 means K = the largest query size.  The query count (and largest size) is the one host read, as the
+// output shape depends on it (the reference reads all group sizes, S/retrieval/precision_recall_curve.py:198).
+std::vector<at::Tensor> retrieval_pr_curve(const at::Tensor& preds, const at::Tensor& target,
+                                           const at::Tensor& indexes, int64_t max_k, bool adaptive_k) {
+  check_flat_inputs(preds, target, indexes, "retrieval_pr_curve");
+  const auto dev = preds.device();
+  auto st = stream();
+  QuerySegments s = segment_queries(preds, indexes, st);
+  hipLaunchKernelGGL(query_max_size_kernel, dim3(grid_cap((preds.numel() + 255) / 256, 1024)), dim3(256), 0, st,
+                     s.begin.data_ptr<int32_t>(), s.nq.data_ptr<int32_t>());
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  const auto host = s.nq.to(at::kCPU);  // the one device->host read
+  const int n_q = host.data_ptr<int32_t>()[0];
+  const int64_t K = max_k > 0 ? max_k : static_cast<int64_t>(host.data_ptr<int32_t>()[1]);
+  TORCH_CHECK(static_cast<double>(n_q) * static_cast<double>(K) < 9.0e18, "retrieval_pr_curve: output too large");
+  auto f32 = at::TensorOptions().dtype(at::kFloat).device(dev);
+  auto prec = at::empty({n_q, K}, f32);
+  auto rec = at::empty({n_q, K}, f32);
+  auto empty = at::empty({n_q}, at::TensorOptions().dtype(at::kByte).device(dev));
+  if (n_q > 0 && K > 0) {
+    const int grid = grid_cap((static_cast<int64_t>(n_q) * kWave + 255) / 256, cu_count(dev.index()) * 8);
+    TM_DISPATCH_PREDS(target.scalar_type(), "retrieval_pr_curve", [&] {
+      hipLaunchKernelGGL((retrieval_pr_curve_kernel<scalar_t>), dim3(grid), dim3(256), 0, st,
+                         reinterpret_cast<const scalar_t*>(target.data_ptr()), s.order.data_ptr<int32_t>(),
+                         s.begin.data_ptr<int32_t>(), n_q, K, adaptive_k, prec.data_ptr<float>(),
+                         rec.data_ptr<float>(), empty.data_ptr<uint8_t>());
+    });
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+  return {prec, rec, empty};
+}
+
 }  // namespace tm_amd
 
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
   m.def("retrieval_metric(Tensor preds, Tensor target, Tensor indexes, int kind, int top_k, bool adaptive_k) -> Tensor[]");
+  m.def("retrieval_pr_curve(Tensor preds, Tensor target, Tensor indexes, int max_k, bool adaptive_k) -> Tensor[]");
 }
-TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) { m.impl("retrieval_metric", &tm_amd::retrieval_metric); }
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
+  m.impl("retrieval_metric", &tm_amd::retrieval_metric);
+  m.impl("retrieval_pr_curve", &tm_amd::retrieval_pr_curve);
+}

@@ -92,3 +92,64 @@ def test_retrieval_module_gpu_matches_cpu_large():
         a.update(p, t, idx)
         b.update(p.cuda(), t.cuda(), idx.cuda())
         torch.testing.assert_close(b.compute().cpu(), a.compute(), rtol=1e-5, atol=1e-6)
+
+
+def _pr_oracle(p, t, max_k, adaptive):
+    """One query, reference F/retrieval/precision_recall_curve.py:87-99 (stable order among ties)."""
+    order = np.argsort(-p, kind="stable")
+    n = len(p)
+    rel = (t[order] > 0).astype(np.float64)[:max_k]
+    rel = np.cumsum(np.pad(rel, (0, max(0, max_k - len(rel)))))
+    ks = np.arange(1, max_k + 1, dtype=np.float64)
+    if adaptive:
+        ks = np.minimum(ks, n)
+    tot = (t > 0).sum()
+    if tot == 0:
+        return np.zeros(max_k), np.zeros(max_k)
+    return (rel / ks).astype(np.float32), (rel / tot).astype(np.float32)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("max_k,adaptive", [(None, False), (None, True), (3, False), (40, True), (150, False)])
+def test_retrieval_pr_curve_kernel(device, max_k, adaptive):
+    g = np.random.default_rng(7 if max_k is None else max_k)
+    n = 1500
+    idx = g.integers(0, 25, n) * 3 - 20
+    p = np.round(g.random(n), 2).astype(np.float32)
+    t = (g.random(n) > 0.85).astype(np.int64)
+    t[idx == -20] = 0  # at least one empty query
+    prec, rec, empty = ops.retrieval_pr_curve(torch.from_numpy(p).to(device), torch.from_numpy(t).to(device),
+                                              torch.from_numpy(idx).to(device), max_k, adaptive)
+    uq = np.unique(idx)
+    k = max_k if max_k is not None else max(int((idx == q).sum()) for q in uq)
+    assert prec.shape == (len(uq), k) and rec.shape == (len(uq), k) and prec.dtype == torch.float32
+    prec, rec, empty = prec.cpu().numpy(), rec.cpu().numpy(), empty.cpu().numpy()
+    for j, qq in enumerate(uq):
+        m = idx == qq
+        assert bool(empty[j]) == bool((t[m] <= 0).all())
+        ep, er = _pr_oracle(p[m], t[m], k, adaptive)
+        np.testing.assert_array_equal(prec[j], ep, err_msg=f"query {qq}")
+        np.testing.assert_array_equal(rec[j], er, err_msg=f"query {qq}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cls_name,kw", [
+    ("RetrievalPrecisionRecallCurve", {}),
+    ("RetrievalPrecisionRecallCurve", {"max_k": 20, "adaptive_k": True, "empty_target_action": "pos"}),
+    ("RetrievalPrecisionRecallCurve", {"max_k": 7, "empty_target_action": "skip", "aggregation": "median"}),
+    ("RetrievalRecallAtFixedPrecision", {"min_precision": 0.3, "max_k": 30}),
+])
+def test_retrieval_pr_curve_module_gpu_matches_cpu(cls_name, kw):
+    import torchmetrics_amd as tm
+
+    g = torch.Generator().manual_seed(1)
+    n = 100_000
+    idx = torch.randint(0, 3000, (n,), generator=g)
+    p = torch.rand(n, generator=g)
+    t = torch.rand(n, generator=g) > 0.9
+    cls = getattr(tm.retrieval, cls_name)
+    a, b = cls(**kw), cls(**kw).cuda()
+    a.update(p, t, idx)
+    b.update(p.cuda(), t.cuda(), idx.cuda())
+    for x, y in zip(b.compute(), a.compute()):
+        torch.testing.assert_close(x.cpu(), y, rtol=1e-6, atol=1e-7)

@@ -240,19 +240,23 @@ def retrieval_precision_recall_curve(
     preds: Tensor, target: Tensor, max_k: Optional[int] = None, adaptive_k: bool = False
 ) -> Tuple[Tensor, Tensor, Tensor]:
     """Precision@k and recall@k for k = 1..max_k (``F/retrieval/precision_recall_curve.py``)."""
+    preds, target = _check_retrieval_functional_inputs(preds, target)
     if not isinstance(adaptive_k, bool):
         raise ValueError("`adaptive_k` has to be a boolean")
-    seg = _one(preds, target)
-    n = seg.preds.numel()
+    n = preds.numel()
     if max_k is None:
         max_k = n
     if not (isinstance(max_k, int) and max_k > 0):
         raise ValueError("`max_k` has to be a positive integer or None")
     if adaptive_k and max_k > n:
-        topk = pad(torch.arange(1, n + 1, device=seg.preds.device), (0, max_k - n), "constant", float(n))
+        topk = pad(torch.arange(1, n + 1, device=preds.device), (0, max_k - n), "constant", float(n))
     else:
-        topk = torch.arange(1, max_k + 1, device=seg.preds.device)
-    if not seg.target.sum():
-        return torch.zeros(max_k, device=seg.preds.device), torch.zeros(max_k, device=seg.preds.device), topk
-    precision, recall, _ = _seg_pr_curve(seg, max_k, adaptive_k)
+        topk = torch.arange(1, max_k + 1, device=preds.device)
+    if preds.is_cuda:  # one-query case of the batched curve kernel; an empty query comes back as zeros
+        idx = torch.zeros(n, dtype=torch.long, device=preds.device)
+        precision, recall, _ = ops.retrieval_pr_curve(preds, target, idx, max_k, adaptive_k)
+        return precision[0], recall[0], topk
+    if not target.sum():
+        return torch.zeros(max_k, device=preds.device), torch.zeros(max_k, device=preds.device), topk
+    precision, recall, _ = _seg_pr_curve(Segments(preds, target), max_k, adaptive_k)
     return precision[0], recall[0], topk

@@ -438,6 +438,22 @@ def retrieval_metric(preds: Tensor, target: Tensor, indexes: Tensor, kind: str, 
     return _cpu.retrieval_metric(preds.reshape(-1), target.reshape(-1), indexes.reshape(-1), k, tk, adaptive_k)
 
 
+def retrieval_pr_curve(preds: Tensor, target: Tensor, indexes: Tensor, max_k: Optional[int] = None,
+                       adaptive_k: bool = False) -> list:
+    """Precision@k / recall@k curves (k = 1..K) of every query (``csrc/sort/retrieval.hip``).
+
+    Returns ``[precision f32 [n_queries, K], recall f32 [n_queries, K], empty uint8 [n_queries]]``, queries in
+    ascending id order; ``K = max_k`` or the largest query size.  One host read (the query count and largest size,
+    which fix the output shape).
+    """
+    mk = -1 if max_k is None else int(max_k)
+    if preds.is_cuda:
+        t = target if target.dtype != torch.bool else target.to(torch.uint8)
+        return list(_ops().retrieval_pr_curve(preds.reshape(-1).contiguous(), t.reshape(-1).contiguous(),
+                                              indexes.reshape(-1).contiguous(), mk, adaptive_k))
+    return _cpu.retrieval_pr_curve(preds.reshape(-1), target.reshape(-1), indexes.reshape(-1), mk, adaptive_k)
+
+
 def kendall_stats(x: Tensor, y: Tensor) -> Tensor:
     """Per column of ``[n, k]`` inputs: ``[disc, tx, tx1, tx2, ty, ty1, ty2, txy, ux, uy]`` (fp64) -- discordant
     pairs, tie terms of x / y (sum of t(t-1)/2, t(t-1)(t-2), t(t-1)(2t+5)), joint ties and distinct counts

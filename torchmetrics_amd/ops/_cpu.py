@@ -632,6 +632,22 @@ def retrieval_metric(preds: Tensor, target: Tensor, indexes: Tensor, kind: int, 
     return [vals, empty, torch.tensor([g], dtype=torch.int32)]
 
 
+def retrieval_pr_curve(preds: Tensor, target: Tensor, indexes: Tensor, max_k: int, adaptive_k: bool):
+    """Host implementation of ``retrieval_pr_curve`` in ``csrc/sort/retrieval.hip``."""
+    from torchmetrics_amd.functional.retrieval import metrics as R
+    from torchmetrics_amd.functional.retrieval._segments import Segments
+
+    seg = Segments(preds, target, indexes)
+    k = int(max_k) if max_k > 0 else int(seg.size.max()) if seg.num_groups else 0
+    empty = (seg.seg_sum((seg.target > 0).to(torch.long)) == 0)
+    if seg.num_groups == 0 or k == 0:
+        z = torch.zeros(seg.num_groups, k, dtype=torch.float32)
+        return [z, z.clone(), empty.to(torch.uint8)]
+    p, r, _ = R._seg_pr_curve(seg, k, adaptive_k)
+    e = empty.unsqueeze(1)
+    return [torch.where(e, torch.zeros_like(p), p), torch.where(e, torch.zeros_like(r), r), empty.to(torch.uint8)]
+
+
 def kendall_stats(x: Tensor, y: Tensor) -> Tensor:
     """Host implementation of ``csrc/sort/kendall.hip`` (Knight's method in batched torch ops)."""
     from torchmetrics_amd.functional.regression import correlation as C

@@ -82,3 +82,45 @@ def test_clip_iqa(tiny_clip):
         CLIPImageQualityAssessment(model_name_or_path=path, prompts=("nope",))
     with pytest.raises(ModuleNotFoundError):
         CLIPImageQualityAssessment()  # default "clip_iqa" network needs piq
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
+@pytest.mark.parametrize("n,d", [(1, 16), (1000, 768), (333, 77)])
+def test_clip_math_kernels_gpu(dtype, n, d):
+    """``csrc/multimodal/clip.hip`` vs the fp64 normalise-then-dot formula of the reference."""
+    from torchmetrics_amd import ops
+
+    g = torch.Generator().manual_seed(n + d)
+    a, b = torch.randn(n, d, generator=g).to(dtype), torch.randn(n, d, generator=g).to(dtype)
+    a64, b64 = a.double(), b.double()
+    exp = 100 * ((a64 / a64.norm(dim=-1, keepdim=True)) * (b64 / b64.norm(dim=-1, keepdim=True))).sum(-1)
+    got = ops.paired_cosine(a.cuda(), b.cuda(), 100.0)
+    assert got.dtype == torch.float32
+    torch.testing.assert_close(got.cpu().double(), exp, rtol=1e-5, atol=1e-4)
+    anchors = torch.randn(6, d, generator=g)
+    anchors = (anchors / anchors.norm(dim=-1, keepdim=True)).to(dtype)
+    img = (a64 / a64.norm(dim=-1, keepdim=True)).to(dtype)
+    logits = 100 * img.double() @ anchors.double().t()
+    exp_p = logits.reshape(n, 3, 2).softmax(-1)[:, :, 0]
+    got_p = ops.prompt_pair_prob(img.cuda(), anchors.cuda(), 100.0)
+    assert got_p.shape == (n, 3)
+    torch.testing.assert_close(got_p.cpu().double(), exp_p, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_clip_score_and_iqa_gpu(tiny_clip):
+    path, model, proc = tiny_clip
+    g = torch.Generator().manual_seed(1)
+    images = torch.randint(0, 255, (3, 3, 40, 40), generator=g).float()
+    texts = ["a cat on a mat", "a red car", "the quick brown fox"]
+    cos = _cos_oracle(model, proc, images, texts)
+    expected = torch.clamp(100 * cos.diag().mean(), min=0)
+    got = clip_score(images.cuda(), texts, model_name_or_path=path)
+    assert got.is_cuda and torch.allclose(got.cpu(), expected, atol=1e-4)
+    imgs = torch.rand(4, 3, 32, 32, generator=torch.Generator().manual_seed(2))
+    flat = ["Good photo.", "Bad photo."]
+    probs = (100 * _cos_oracle(model, proc, imgs, flat)).reshape(4, 1, 2).softmax(-1)[:, 0, 0]
+    m = CLIPImageQualityAssessment(model_name_or_path=path, prompts=("quality",)).cuda()
+    m.update(imgs.cuda())
+    assert torch.allclose(m.compute().cpu(), probs, atol=1e-4)

@@ -1,15 +1,16 @@
 """Multimodal metrics (reference ``F/multimodal/{clip_score,clip_iqa}.py``).
 
 The CLIP encoders run through HuggingFace ``transformers`` on PyTorch-ROCm (their GEMMs are vendor MFMA GEMMs); the
-metric math -- L2-normalised embedding dot products, the prompt-pair softmax of CLIP-IQA -- is fused into one
-``[N, D] x [D, 2P]`` GEMM.  Weights are never downloaded: ``model_name_or_path`` must resolve offline (a local
-directory or the HF cache).  The original CLIP-IQA network (``"clip_iqa"``) comes from ``piq`` and is gated on it.
+metric math -- cosine of each (image, caption) embedding pair, the prompt-pair softmax of CLIP-IQA -- runs in one
+wave-per-row kernel each on ROCm (``csrc/multimodal/clip.hip``).  Weights are never downloaded:
+``model_name_or_path`` must resolve offline (a local directory or the HF cache).  The original CLIP-IQA network (``"clip_iqa"``) comes from ``piq`` and is gated on it.
 """
 from typing import Dict, List, Literal, Tuple, Union
 
 import torch
 from torch import Tensor
 
+from torchmetrics_amd import ops
 from torchmetrics_amd.utilities.imports import _TRANSFORMERS_AVAILABLE
 from torchmetrics_amd.utilities.prints import rank_zero_warn
 
@@ -65,7 +66,7 @@ def _clip_score_update(images: Union[Tensor, List[Tensor]], text: Union[str, Lis
             f"Expected the number of images and text examples to be the same but got {len(images)} and {len(text)}")
     device = images[0].device
     proc = processor(text=text, images=[i.cpu() for i in images], return_tensors="pt", padding=True)
-    img = _normalize(model.get_image_features(proc["pixel_values"].to(device)))
+    img = _features(model.get_image_features(proc["pixel_values"].to(device)))
     max_pos = model.config.text_config.max_position_embeddings
     ids, am = proc["input_ids"], proc["attention_mask"]
     if am.shape[-1] > max_pos:
@@ -74,8 +75,16 @@ def _clip_score_update(images: Union[Tensor, List[Tensor]], text: Union[str, Lis
             "If longer captions are needed, initialize argument `model_name_or_path` with a model that supports"
             "longer sequences")
         ids, am = ids[..., :max_pos], am[..., :max_pos]
-    txt = _normalize(model.get_text_features(ids.to(device), am.to(device)))
-    return 100 * (img * txt).sum(dim=-1), len(text)
+    txt = _features(model.get_text_features(ids.to(device), am.to(device)))
+    return _scaled_cosine(img, txt, 100.0), len(text)
+
+
+def _scaled_cosine(img: Tensor, txt: Tensor, scale: float) -> Tensor:
+    """``scale * cos`` per embedding pair: one wave per pair on ROCm (``ops.paired_cosine``); the normalise-then-dot
+    formulation of the reference when gradients are needed."""
+    if img.is_cuda and not (torch.is_grad_enabled() and (img.requires_grad or txt.requires_grad)):
+        return ops.paired_cosine(img, txt, scale).to(img.dtype)
+    return scale * (_normalize(img) * _normalize(txt)).sum(dim=-1)
 
 
 def clip_score(images: Union[Tensor, List[Tensor]], text: Union[str, List[str]],
@@ -162,8 +171,12 @@ def _clip_iqa_update(model_name_or_path: str, images: Tensor, model, processor, 
 def _clip_iqa_compute(img_features: Tensor, anchors: Tensor, prompts_names: List[str],
                       format_as_dict: bool = True) -> Union[Tensor, Dict[str, Tensor]]:
     """P(positive prompt) per image and prompt pair: softmax over each (positive, negative) logit pair."""
-    logits = 100 * img_features @ anchors.t()
-    probs = logits.reshape(logits.shape[0], -1, 2).softmax(-1)[:, :, 0]
+    if img_features.is_cuda and not (torch.is_grad_enabled() and img_features.requires_grad):
+        # both dot products and the pair softmax in one launch (no [N, 2P] logits tensor)
+        probs = ops.prompt_pair_prob(img_features, anchors, 100.0).to(img_features.dtype)
+    else:
+        logits = 100 * img_features @ anchors.t()
+        probs = logits.reshape(logits.shape[0], -1, 2).softmax(-1)[:, :, 0]
     if len(prompts_names) == 1:
         return probs.squeeze()
     if format_as_dict:

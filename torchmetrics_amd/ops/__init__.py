@@ -454,6 +454,26 @@ def retrieval_pr_curve(preds: Tensor, target: Tensor, indexes: Tensor, max_k: Op
     return _cpu.retrieval_pr_curve(preds.reshape(-1), target.reshape(-1), indexes.reshape(-1), mk, adaptive_k)
 
 
+def paired_cosine(a: Tensor, b: Tensor, scale: float = 1.0) -> Tensor:
+    """``scale * cos(a_i, b_i)`` of ``[N, D]`` embedding pairs as fp32 ``[N]`` (``csrc/multimodal/clip.hip``: one wave
+    per pair, no normalised copies)."""
+    if a.is_cuda:
+        if b.dtype != a.dtype:
+            b = b.to(a.dtype)
+        return _ops().paired_cosine(a.contiguous(), b.contiguous(), float(scale))
+    return _cpu.paired_cosine(a, b, scale)
+
+
+def prompt_pair_prob(img: Tensor, anchors: Tensor, scale: float = 100.0) -> Tensor:
+    """Softmax of ``scale * img @ anchors^T`` over each (positive, negative) anchor pair -> probability of the
+    positive prompt, fp32 ``[N, P]`` (``csrc/multimodal/clip.hip``)."""
+    if img.is_cuda:
+        if anchors.dtype != img.dtype:
+            anchors = anchors.to(img.dtype)
+        return _ops().prompt_pair_prob(img.contiguous(), anchors.contiguous(), float(scale))
+    return _cpu.prompt_pair_prob(img, anchors, scale)
+
+
 def kendall_stats(x: Tensor, y: Tensor) -> Tensor:
     """Per column of ``[n, k]`` inputs: ``[disc, tx, tx1, tx2, ty, ty1, ty2, txy, ux, uy]`` (fp64) -- discordant
     pairs, tie terms of x / y (sum of t(t-1)/2, t(t-1)(t-2), t(t-1)(2t+5)), joint ties and distinct counts

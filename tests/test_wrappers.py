@@ -187,3 +187,47 @@ def test_feature_share_runs_network_once():
     x = torch.randn(10, 8)
     fs.update(x, real=True)
     assert net.calls == 1
+
+
+class _Extremes(tm.Metric):
+    full_state_update = False
+
+    def __init__(self):
+        super().__init__()
+        self.add_state("hi", torch.tensor(float("-inf")), dist_reduce_fx="max")
+        self.add_state("lo", torch.tensor(float("inf")), dist_reduce_fx="min")
+
+    def update(self, x):
+        self.hi = torch.maximum(self.hi, x.max())
+        self.lo = torch.minimum(self.lo, x.min())
+
+    def compute(self):
+        return torch.stack([self.lo, self.hi])
+
+
+@pytest.mark.parametrize("make,arg_fn", [
+    (lambda: tm.MeanSquaredError(), lambda g: (torch.randn(7, generator=g), torch.randn(7, generator=g))),
+    (lambda: _Extremes(), lambda g: (torch.randn(7, generator=g),)),
+    (lambda: tm.MeanMetric(), lambda g: (torch.randn(7, generator=g),)),
+    (lambda: tm.CatMetric(), lambda g: (torch.randn(3, generator=g),)),
+    (lambda: tm.MulticlassStatScores(4, average=None), lambda g: (torch.randint(0, 4, (9,), generator=g),
+                                                                   torch.randint(0, 4, (9,), generator=g))),
+])
+@pytest.mark.parametrize("window", [1, 3])
+def test_running_window_equals_metric_on_last_batches(make, arg_fn, window):
+    """Running(window) == the wrapped metric fed only the last ``window`` batches (every reduction kind)."""
+    g = torch.Generator().manual_seed(window)
+    run = tm.wrappers.Running(make(), window=window)
+    batches = []
+    for _ in range(5):
+        args = arg_fn(g)
+        batches.append(args)
+        run.update(*args)
+        ref = make()
+        for a in batches[-window:]:
+            ref.update(*a)
+        got, exp = run.compute(), ref.compute()
+        if isinstance(ref, tm.CatMetric):  # the window is merged newest-first (as the reference's list merge)
+            got, exp = got.sort().values, exp.sort().values
+        torch.testing.assert_close(got, exp)
+        run._computed = None

@@ -69,6 +69,12 @@ def jit_distributed_available() -> bool:
     return _engine_dist_available()
 
 
+def _is_partial_view(t: Any) -> bool:
+    """A strided tensor that covers only part of its storage (a view of a packed or cat arena)."""
+    return (isinstance(t, Tensor) and t.layout == torch.strided
+            and t.untyped_storage().nbytes() > t.numel() * t.element_size())
+
+
 class Metric(Module, ABC):
     """Base class for all metrics.
 
@@ -290,9 +296,10 @@ class Metric(Module, ABC):
         self._exit_batch_mode(saved)
         return batch_val
 
-    def _reduce_states(self, incoming_state: Dict[str, Any]) -> None:
-        """Merge ``incoming_state`` (the pre-batch global state) with the current (batch) state."""
-        for attr in self._defaults:
+    def _reduce_states(self, incoming_state: Dict[str, Any], only: Optional[str] = None) -> None:
+        """Merge ``incoming_state`` (the pre-batch global state) with the current (batch) state (every state, or just
+        ``only``)."""
+        for attr in (self._defaults if only is None else (only,)):
             local = getattr(self, attr)
             glob = incoming_state[attr]
             fn = self._reductions[attr]
@@ -551,7 +558,47 @@ class Metric(Module, ABC):
             if fn is dim_zero_cat:
                 val = getattr(self, attr)
                 if isinstance(val, list) and len(val) > 1:
-                    val[:] = [dim_zero_cat(val)]
+                    val[:] = [self._fold_into_arena(attr, val)]
+
+    def _fold_into_arena(self, attr: str, parts: List[Any]) -> Any:
+        """Concatenate a ``cat`` list state into its growable HBM arena.
+
+        The fold's result is a view ``buf[:rows]`` of a per-state buffer.  When the list is that view plus new
+        batches, only the new batches are copied (one ``cat`` into ``buf[rows:]``); the buffer is re-allocated with
+        amortised doubling when they do not fit, so per-step ``compute()`` costs O(new rows) instead of re-copying the
+        whole history.  The first fold allocates exactly what it needs (a compute-once evaluation carries no slack).
+        Autograd, mixed dtypes / devices / trailing shapes and ``forward()``'s batch states take a plain ``cat``."""
+        d = self.__dict__
+        if d.get("_enable_grad"):
+            return dim_zero_cat(parts)  # forward()'s batch state: never touch the global state's arena
+        first = parts[0]
+        if not isinstance(first, Tensor) or first.ndim == 0:
+            return dim_zero_cat(parts)
+        tail, dtype, dev = first.shape[1:], first.dtype, first.device
+        grad = torch.is_grad_enabled()
+        for p in parts:
+            if (not isinstance(p, Tensor) or p.ndim == 0 or p.shape[1:] != tail or p.dtype != dtype or p.device != dev
+                    or p.layout != torch.strided or (grad and p.requires_grad)):
+                return dim_zero_cat(parts)
+        arenas = d.get("_cat_arenas")
+        if arenas is None:
+            arenas = d["_cat_arenas"] = {}
+        entry = arenas.get(attr)
+        if entry is not None and entry[1] is first and entry[0].dtype == dtype and entry[0].device == dev:
+            buf, used, new = entry[0], first.shape[0], parts[1:]
+        else:
+            buf, used, new = None, 0, parts
+        need = used + sum(p.shape[0] for p in new)
+        if buf is None or need > buf.shape[0]:
+            cap = need if buf is None else max(need, 2 * buf.shape[0])
+            grown = torch.empty((cap,) + tuple(tail), dtype=dtype, device=dev)
+            if used:
+                grown[:used].copy_(buf[:used])
+            buf = grown
+        torch.cat(new, dim=0, out=buf[used:need])
+        view = buf[:need]
+        arenas[attr] = (buf, view)
+        return view
 
     @abstractmethod
     def update(self, *_: Any, **__: Any) -> None:
@@ -586,6 +633,8 @@ class Metric(Module, ABC):
         d = self.__dict__
         d.pop("_errors_checked_at", None)
         d.pop("_arena_repacks", None)  # a reset's fresh states are re-packed at the next sync without counting
+        if not d.get("_keep_device_errors"):
+            d.pop("_cat_arenas", None)  # (forward()'s batch reset keeps the global state's arenas)
         if not d.get("_keep_device_errors") and d.get("_device_errors") is not None:
             self._device_errors.zero_()
         self._update_count = 0
@@ -636,7 +685,13 @@ class Metric(Module, ABC):
 
     # ------------------------------------------------------------------------------------------------- pickling
     def __getstate__(self) -> Dict[str, Any]:
-        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature")}
+        state = {k: v for k, v in self.__dict__.items()
+                 if k not in ("update", "compute", "_update_signature", "_cat_arenas")}
+        for key in self._defaults:  # a folded list state: its own rows only, not the arena's spare capacity
+            cur = state.get(key)
+            if isinstance(cur, list) and any(_is_partial_view(v) for v in cur):
+                state[key] = [v.clone() if _is_partial_view(v) else v for v in cur]
+        return state
 
     def __setstate__(self, state: Dict[str, Any]) -> None:
         self.__dict__.update(state)
@@ -704,6 +759,7 @@ class Metric(Module, ABC):
                 raise TypeError(
                     f"Expected metric state to be either a Tensor or a list of Tensor, but encountered {cur}"
                 )
+        this.__dict__.pop("_cat_arenas", None)  # folded list states were moved out of their arenas
         this._pack_states()  # the moved / cast states are separate tensors again: one buffer per bucket
         probe = fn(torch.zeros(1, device=self.device))
         self._device = probe.device
@@ -737,10 +793,11 @@ class Metric(Module, ABC):
                     cur = cur.detach()
                 elif isinstance(cur, list):
                     cur = [v.detach() if isinstance(v, Tensor) else v for v in cur]
-            if isinstance(cur, Tensor) and cur.layout == torch.strided and \
-                    cur.untyped_storage().nbytes() > cur.numel() * cur.element_size():
+            if _is_partial_view(cur):
                 # a view of the packed arena: copy just its own elements (deepcopy would copy the whole buffer)
                 cur = cur.detach().clone().requires_grad_(cur.requires_grad)
+            elif isinstance(cur, list) and any(_is_partial_view(v) for v in cur):
+                cur = [v.detach().clone() if _is_partial_view(v) else deepcopy(v) for v in cur]  # folded cat arena
             else:
                 cur = deepcopy(cur)
             destination[prefix + key] = cur

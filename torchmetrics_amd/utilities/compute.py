@@ -46,9 +46,8 @@ def _adjust_weights_safe_divide(
 
 
 def _auc_format_inputs(x: Tensor, y: Tensor) -> Tuple[Tensor, Tensor]:
-    x = x.squeeze() if x.ndim > 1 else x
-    y = y.squeeze() if y.ndim > 1 else y
-    if x.ndim > 1 or y.ndim > 1:
+    x, y = (t.squeeze() if t.ndim > 1 else t for t in (x, y))
+    if max(x.ndim, y.ndim) > 1:
         raise ValueError(
             f"Expected both `x` and `y` tensor to be 1d, but got tensors with dimension {x.ndim} and {y.ndim}"
         )
@@ -70,14 +69,17 @@ def _auc_compute(x: Tensor, y: Tensor, reorder: bool = False) -> Tensor:
         if reorder:
             x, order = torch.sort(x, stable=True)
             y = y[order]
-        dx = x[1:] - x[:-1]
         direction = 1.0
-        if (dx < 0).any():
-            if not (dx <= 0).all():
-                raise ValueError(
-                    "The `x` tensor is neither increasing or decreasing. Try setting the reorder argument to `True`."
-                )
-            direction = -1.0
+        if x.numel() > 1:
+            # both monotonicity tests in one host read
+            dx = x.diff()
+            falls, non_increasing = torch.stack([(dx < 0).any(), (dx <= 0).all()]).tolist()
+            if falls:
+                if not non_increasing:
+                    raise ValueError(
+                        "The `x` tensor is neither increasing or decreasing. Try setting the reorder argument to `True`."
+                    )
+                direction = -1.0
         return _auc_compute_without_check(x, y, direction)
 
 

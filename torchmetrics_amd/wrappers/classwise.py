@@ -1,10 +1,19 @@
-"""Per-class dict output for metrics with ``average=None`` (reference ``S/wrappers/classwise.py:26-200``)."""
-from typing import Any, Dict, List, Optional
+"""Per-class dict output for metrics with ``average=None`` (reference ``S/wrappers/classwise.py:26-200``).
+
+The output keys depend only on the configuration and the number of classes, so they are built once per class count
+and reused: ``compute()`` is one ``unbind`` of the wrapped result plus a ``dict(zip(...))``.
+"""
+from typing import Any, Dict, List, Optional, Tuple
 
 from torch import Tensor
 
 from torchmetrics_amd.metric import Metric
 from torchmetrics_amd.wrappers.abstract import WrapperMetric
+
+
+def _check_optional(value: Any, ok: bool, name: str, what: str) -> None:
+    if value is not None and not ok:
+        raise ValueError(f"Expected argument `{name}` to either be `None` or {what} but got {value}")
 
 
 class ClasswiseWrapper(WrapperMetric):
@@ -20,25 +29,31 @@ class ClasswiseWrapper(WrapperMetric):
         super().__init__()
         if not isinstance(metric, Metric):
             raise ValueError(f"Expected argument `metric` to be an instance of `torchmetrics.Metric` but got {metric}")
+        _check_optional(labels, isinstance(labels, list) and all(isinstance(s, str) for s in labels),
+                        "labels", "a list of strings")
+        _check_optional(prefix, isinstance(prefix, str), "prefix", "a string")
+        _check_optional(postfix, isinstance(postfix, str), "postfix", "a string")
         self.metric = metric
-        if labels is not None and not (isinstance(labels, list) and all(isinstance(lab, str) for lab in labels)):
-            raise ValueError(f"Expected argument `labels` to either be `None` or a list of strings but got {labels}")
         self.labels = labels
-        if prefix is not None and not isinstance(prefix, str):
-            raise ValueError(f"Expected argument `prefix` to either be `None` or a string but got {prefix}")
         self._prefix = prefix
-        if postfix is not None and not isinstance(postfix, str):
-            raise ValueError(f"Expected argument `postfix` to either be `None` or a string but got {postfix}")
         self._postfix = postfix
+        self._keys: Tuple[Any, List[str]] = (None, [])
         self._update_count = 1
 
+    def _names(self, n: int) -> List[str]:
+        key = (n, None if self.labels is None else tuple(self.labels), self._prefix, self._postfix)
+        if self._keys[0] != key:
+            # no prefix and no postfix: "<metric class name>_" in front (the reference's default naming)
+            if self._prefix or self._postfix:
+                head, tail = self._prefix or "", self._postfix or ""
+            else:
+                head, tail = type(self.metric).__name__.lower() + "_", ""
+            labels = list(range(n)) if self.labels is None else self.labels
+            self._keys = (key, [f"{head}{lab}{tail}" for lab in labels])
+        return self._keys[1]
+
     def _convert(self, x: Tensor) -> Dict[str, Any]:
-        if not self._prefix and not self._postfix:
-            prefix, postfix = f"{self.metric.__class__.__name__.lower()}_", ""
-        else:
-            prefix, postfix = self._prefix or "", self._postfix or ""
-        names = range(len(x)) if self.labels is None else self.labels
-        return {f"{prefix}{name}{postfix}": val for name, val in zip(names, x)}
+        return dict(zip(self._names(len(x)), x))
 
     def forward(self, *args: Any, **kwargs: Any) -> Any:
         return self._convert(self.metric(*args, **kwargs))

@@ -26,6 +26,23 @@ class NetworkCache(Module):
         return self.network(*args, **kwargs)
 
 
+_NO_ATTR_FIRST = (
+    "Tried to extract the network to share from the first metric, but it did not have a `feature_network`"
+    " attribute. Please make sure that the metric has an attribute with that name,"
+    " else it cannot be shared."
+)
+_NO_ATTR_MEMBER = (
+    "Tried to set the cached network to all metrics, but one of the metrics did not have a"
+    " `feature_network` attribute. Please make sure that all metrics have a attribute with that name,"
+    " else it cannot be shared. Failed on metric {}."
+)
+
+
+def _network_of(metric: Metric) -> Module:
+    """The module a metric names in its ``feature_network`` attribute."""
+    return getattr(metric, metric.feature_network)
+
+
 class FeatureShare(MetricCollection):
     """A ``MetricCollection`` whose members share one cached feature extractor."""
 
@@ -35,30 +52,22 @@ class FeatureShare(MetricCollection):
         max_cache_size: Optional[int] = None,
     ) -> None:
         super().__init__(metrics=metrics, compute_groups=False)
-        if max_cache_size is None:
-            max_cache_size = len(self)
-        if not isinstance(max_cache_size, int):
-            raise TypeError(f"max_cache_size should be an integer, but got {max_cache_size}")
+        size = len(self) if max_cache_size is None else max_cache_size
+        if not isinstance(size, int):
+            raise TypeError(f"max_cache_size should be an integer, but got {size}")
+        members = list(self.items())
         try:
-            first = next(iter(self.values()))
-            shared = getattr(first, first.feature_network)
+            shared = _network_of(members[0][1])
         except AttributeError as err:
-            raise AttributeError(
-                "Tried to extract the network to share from the first metric, but it did not have a `feature_network`"
-                " attribute. Please make sure that the metric has an attribute with that name,"
-                " else it cannot be shared."
-            ) from err
-        cached = NetworkCache(shared, max_size=max_cache_size)
-        for name, metric in self.items():
+            raise AttributeError(_NO_ATTR_FIRST) from err
+        signature = str(shared)
+        cached = NetworkCache(shared, max_size=size)
+        for name, metric in members:
             if not hasattr(metric, "feature_network"):
-                raise AttributeError(
-                    "Tried to set the cached network to all metrics, but one of the metrics did not have a"
-                    " `feature_network` attribute. Please make sure that all metrics have a attribute with that name,"
-                    f" else it cannot be shared. Failed on metric {name}."
-                )
-            if str(getattr(metric, metric.feature_network)) != str(shared):
+                raise AttributeError(_NO_ATTR_MEMBER.format(name))
+            if str(_network_of(metric)) != signature:
                 rank_zero_warn(
-                    f"The network to share between the metrics is not the same for all metrics."
+                    "The network to share between the metrics is not the same for all metrics."
                     f" Metric {name} has a different network than the first metric."
                     " This may lead to unexpected behavior.",
                     UserWarning,

@@ -4,8 +4,8 @@
 // temporaries) and reduces their product.  ``paired_cosine_kernel``: one 64-lane wave per pair streams both rows
 // once with 16-byte loads and keeps the three sums (a.b, a.a, b.b) in registers -- scale * a.b / (|a| |b|).
 // CLIP-IQA: logits = 100 * img @ anchors^T followed by a softmax over each (positive, negative) prompt pair.
-// ``prompt_pair_prob_kernel``: one wave per (image, prompt pair) computes both dot products and writes the pair's
-// softmax probability of the positive prompt, 1 / (1 + exp(l_neg - l_pos)), without the [N, 2P] logits tensor.
+// ``prompt_pair_prob_kernel``: an LDS-tiled [16 images x 32 anchors] dot-product block writes each pair's softmax
+// probability of the positive prompt, 1 / (1 + exp(l_neg - l_pos)), without the [N, 2P] logits tensor.
 // Sums are fp32 (fp64 for fp64 embeddings), reduced across the wave in a fixed order (deterministic).
 #include "common/tm_common.h"
 
@@ -76,25 +76,60 @@ __global__ void __launch_bounds__(kThreads) paired_cosine_kernel(const T* __rest
   }
 }
 
+// Block = 16 images x 32 anchors (16 prompt pairs); K (the embedding dim) in chunks of 64 staged through LDS, each
+// thread accumulating 2 of the 512 dot products; then the pair softmax from an LDS logits tile.  The anchors (2P x D,
+// a few hundred KB at most) are re-read per block from L2, the images once from HBM.
+constexpr int kImgTile = 16, kAncTile = 32, kKTile = 64;
+
 template <typename T>
 __global__ void __launch_bounds__(kThreads) prompt_pair_prob_kernel(const T* __restrict__ img,
                                                                     const T* __restrict__ anchors, long long n,
-                                                                    int pairs, int D, bool vec, float scale,
+                                                                    int n_anc, int D, float scale,
                                                                     float* __restrict__ out) {
   using A = acc_t<T>;
-  const long long wave = (blockIdx.x * (long long)kThreads + threadIdx.x) / kWave;
-  const long long nwaves = (long long)gridDim.x * kWavesPerBlock;
-  const long long total = n * pairs;
-  for (long long w = wave; w < total; w += nwaves) {
-    const long long i = w / pairs;
-    const int p = static_cast<int>(w - i * pairs);
-    A lp, ln, unused;
-    row_dots<T, false, false>(img + i * D, anchors + (2LL * p) * D, D, vec, lp, unused, unused);
-    row_dots<T, false, false>(img + i * D, anchors + (2LL * p + 1) * D, D, vec, ln, unused, unused);
-    if ((threadIdx.x & (kWave - 1)) == 0) {
-      const A s = static_cast<A>(scale);
-      out[w] = static_cast<float>(A(1) / (A(1) + exp(s * ln - s * lp)));
+  __shared__ A s_img[kImgTile][kKTile + 1];
+  __shared__ A s_anc[kAncTile][kKTile + 1];
+  __shared__ A s_log[kImgTile][kAncTile + 1];
+  const int t = threadIdx.x;
+  const int r = t / 16, c = t % 16;  // this thread's image row and its two anchor columns c, c + 16
+  const long long i0 = static_cast<long long>(blockIdx.x) * kImgTile;
+  const int pairs = n_anc / 2;
+  for (int a0 = 0; a0 < n_anc; a0 += kAncTile) {
+    A acc0 = A(0), acc1 = A(0);
+    for (int k0 = 0; k0 < D; k0 += kKTile) {
+#pragma unroll
+      for (int e = t; e < kImgTile * kKTile; e += kThreads) {
+        const int rr = e / kKTile, kk = e % kKTile;
+        const long long gi = i0 + rr;
+        s_img[rr][kk] = (gi < n && k0 + kk < D) ? ldx<T>(img + gi * D + k0 + kk) : A(0);
+      }
+#pragma unroll
+      for (int e = t; e < kAncTile * kKTile; e += kThreads) {
+        const int aa = e / kKTile, kk = e % kKTile;
+        const int ga = a0 + aa;
+        s_anc[aa][kk] = (ga < n_anc && k0 + kk < D) ? ldx<T>(anchors + static_cast<long long>(ga) * D + k0 + kk) : A(0);
+      }
+      __syncthreads();
+#pragma unroll 16
+      for (int kk = 0; kk < kKTile; ++kk) {
+        const A x = s_img[r][kk];
+        acc0 += x * s_anc[c][kk];
+        acc1 += x * s_anc[c + 16][kk];
+      }
+      __syncthreads();
     }
+    s_log[r][c] = static_cast<A>(scale) * acc0;
+    s_log[r][c + 16] = static_cast<A>(scale) * acc1;
+    __syncthreads();
+    // one (image, pair) per thread: 16 images x 16 pairs of this anchor tile
+    const int pr = t % 16;
+    const int p = a0 / 2 + pr;
+    const long long gi = i0 + r;
+    if (gi < n && p < pairs) {
+      const A lp = s_log[r][2 * pr], ln = s_log[r][2 * pr + 1];
+      out[gi * pairs + p] = static_cast<float>(A(1) / (A(1) + exp(ln - lp)));
+    }
+    __syncthreads();
   }
 }
 
@@ -142,13 +177,12 @@ at::Tensor prompt_pair_prob(const at::Tensor& img, const at::Tensor& anchors, do
   const int D = static_cast<int>(img.size(1));
   auto out = at::empty({n, pairs}, img.options().dtype(at::kFloat));
   if (n == 0 || pairs == 0) return out;
-  const long long waves = n * pairs;
-  const int grid = grid_cap((waves + kWavesPerBlock - 1) / kWavesPerBlock, cu_count(img.get_device()) * 8);
+  const long long blocks = (n + kImgTile - 1) / kImgTile;
+  TORCH_CHECK(blocks < (1LL << 31), "prompt_pair_prob: too many images");
   TM_DISPATCH_FLOAT(img.scalar_type(), "prompt_pair_prob", [&] {
-    const bool vec = aligned16(img, D, sizeof(scalar_t)) && aligned16(anchors, D, sizeof(scalar_t));
-    hipLaunchKernelGGL((prompt_pair_prob_kernel<scalar_t>), dim3(grid), dim3(kThreads), 0, stream(),
-                       img.data_ptr<scalar_t>(), anchors.data_ptr<scalar_t>(), n, pairs, D, vec,
-                       static_cast<float>(scale), out.data_ptr<float>());
+    hipLaunchKernelGGL((prompt_pair_prob_kernel<scalar_t>), dim3(static_cast<unsigned>(blocks)), dim3(kThreads), 0,
+                       stream(), img.data_ptr<scalar_t>(), anchors.data_ptr<scalar_t>(), n,
+                       static_cast<int>(anchors.size(0)), D, static_cast<float>(scale), out.data_ptr<float>());
   });
   C10_HIP_KERNEL_LAUNCH_CHECK();
   return out;

@@ -200,3 +200,75 @@ def _body_collection_sync_once(rank, world):
 
 def test_collection_sync_once():
     run_ddp(_body_collection_sync_once)
+
+
+def _narrow_wire_body(rank, world, num_classes, scale):
+    import torchmetrics_amd as tm
+    from torchmetrics_amd.parallel import sync
+
+    g = torch.Generator().manual_seed(7)
+    preds = torch.randint(0, num_classes, (world, 4000 * scale), generator=g)
+    target = torch.randint(0, num_classes, (world, 4000 * scale), generator=g)
+    m = tm.MulticlassConfusionMatrix(num_classes)
+    for _ in range(scale):
+        m.update(preds[rank], target[rank])
+    comm_stats(reset=True)
+    out = m.compute()
+    st = comm_stats()
+    ref = tm.MulticlassConfusionMatrix(num_classes, sync_on_compute=False)
+    for r in range(world):
+        for _ in range(scale):
+            ref.update(preds[r], target[r])
+    assert torch.equal(out, ref.compute()) and out.dtype == torch.int64
+    state_bytes = num_classes * num_classes * 8
+    # one range all-reduce (2 int64) + the bucket on the narrowed wire
+    assert st["all_reduce"] == 2, st
+    assert st["bytes"] < state_bytes // 2, st
+    # local state untouched by the sync
+    local = tm.MulticlassConfusionMatrix(num_classes, sync_on_compute=False)
+    for _ in range(scale):
+        local.update(preds[rank], target[rank])
+    assert torch.equal(m.confmat, local.confmat)
+
+
+@pytest.mark.parametrize("scale", [1, 40])  # max cell x world <= 255 (uint8) / larger counts (fp16 or int32)
+def test_narrow_wire_count_bucket_exact(scale):
+    run_ddp(_narrow_wire_body, 400, scale, world=2)
+
+
+def _narrow_negative_body(rank, world):
+    from torchmetrics_amd.parallel.sync import sync_state_dicts
+    from torchmetrics_amd.utilities.data import dim_zero_sum
+
+    x = torch.arange(200_000, dtype=torch.int64) * (1 if rank == 0 else -1) + rank
+    comm_stats(reset=True)
+    out = sync_state_dicts([({"x": x}, {"x": dim_zero_sum})])[0]["x"]
+    assert torch.equal(out, torch.ones(200_000, dtype=torch.int64))
+    assert comm_stats()["bytes"] >= 200_000 * 8  # negative values: the int64 wire
+
+
+def test_narrow_wire_keeps_int64_for_negative_values():
+    run_ddp(_narrow_negative_body, world=2)
+
+
+def _narrow_tier_body(rank, world, top, wire_bytes):
+    from torchmetrics_amd.parallel.sync import sync_state_dicts
+    from torchmetrics_amd.utilities.data import dim_zero_sum
+
+    n = 300_000
+    g = torch.Generator().manual_seed(rank)
+    x = torch.randint(0, top + 1, (n,), generator=g, dtype=torch.int64)
+    x[rank] = top  # the bound is reached on some rank
+    parts = [torch.randint(0, top + 1, (n,), generator=torch.Generator().manual_seed(r), dtype=torch.int64)
+             for r in range(world)]
+    for r in range(world):
+        parts[r][r] = top
+    comm_stats(reset=True)
+    out = sync_state_dicts([({"x": x}, {"x": dim_zero_sum})])[0]["x"]
+    assert out.dtype == torch.int64 and torch.equal(out, sum(parts))
+    assert comm_stats()["bytes"] == 16 + n * wire_bytes, comm_stats()
+
+
+@pytest.mark.parametrize("top,wire_bytes", [(100, 1), (1000, 2), (5000, 4), (2**40, 8)])
+def test_narrow_wire_tiers(top, wire_bytes):
+    run_ddp(_narrow_tier_body, top, wire_bytes, world=2)

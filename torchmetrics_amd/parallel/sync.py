@@ -12,6 +12,8 @@ This engine keeps the exact *result* semantics but changes the communication pla
   its span (``torch.cat`` only for states that fell out of their arena).
   No metadata, no host sync, no barrier.  A whole ``MetricCollection`` (all compute groups) is synced in one call,
   so a 20-metric collection costs ~2 collectives instead of ~3x(#states).
+* **narrow wire** -- integer SUM buckets of >= 1 MiB (count states) travel in the narrowest dtype that carries their
+  sums exactly (uint8 / fp16 / int32), agreed by one tiny MAX all-reduce of the range (:func:`_narrow_wire`).
 * **one-shot path** -- on RCCL, reduce buckets of <= 256 KiB (every classification / regression state) skip the
   ring: one peer-read kernel over xGMI (:mod:`torchmetrics_amd.parallel.oneshot`).
 * **gather bucket** -- ``cat``, ``None`` and custom-callable states. One fixed-size metadata header per rank (element
@@ -117,6 +119,45 @@ def _all_gather_flat(buf: Tensor, world: int, group: Optional[Any]) -> Tensor:
     return out
 
 
+# Integer SUM buckets of at least this many bytes are range-checked for a narrower wire dtype (count states such as a
+# 1000-class confusion matrix: 8 MB of int64 whose cells are small).
+NARROW_WIRE_MIN_BYTES = 1 << 20
+_NARROWABLE = (torch.int64, torch.int32)
+
+
+def _narrow_wire(src: Tensor, world: int, group: Optional[Any]) -> Optional[torch.dtype]:
+    """The narrowest dtype that carries this integer SUM bucket's all-reduce exactly, agreed by every rank.
+
+    One tiny MAX all-reduce of (local max, -local min) gives every rank the same global bound, so all ranks pick the
+    same wire dtype (the collective sequence stays matched).  Every partial sum of the all-reduce is at most
+    ``world * max``: <= 255 travels as uint8, <= 2048 as fp16 (integers are exact there), < 2^31 as int32.  The
+    ring all-reduce is per-link bandwidth-bound over xGMI, so an 8 MB int64 count bucket with small cells becomes a
+    1 MB uint8 one.  Negative values or small buckets keep their dtype.  ``TORCHMETRICS_AMD_NARROW_WIRE=0`` disables
+    it."""
+    if src.numel() * src.element_size() < NARROW_WIRE_MIN_BYTES or not _narrow_enabled():
+        return None
+    lo, hi = torch.aminmax(src)
+    bound = torch.stack([hi, -lo]).to(torch.int64)
+    _all_reduce(bound, "max", group)
+    gmax, neg_gmin = bound.tolist()
+    if neg_gmin > 0:
+        return None
+    total = world * gmax
+    if total <= 255:
+        return torch.uint8
+    if total <= 2048:
+        return torch.float16
+    if total < 2**31 and src.dtype == torch.int64:
+        return torch.int32
+    return None
+
+
+def _narrow_enabled() -> bool:
+    import os
+
+    return os.environ.get("TORCHMETRICS_AMD_NARROW_WIRE", "1") not in ("0", "false", "False")
+
+
 class _GatherItem:
     __slots__ = ("key", "is_list", "elems", "fn")
 
@@ -170,6 +211,10 @@ def sync_state_dicts(
     for (kind, dtype, _device), members in reduce_buckets.items():
         wire = _WIRE_DTYPE.get(dtype, dtype)
         span = members[0][1].reshape(-1) if len(members) == 1 else contiguous_span([t for _, t in members])
+        if world > 1 and kind == "sum" and dtype in _NARROWABLE:
+            src = span if span is not None else torch.cat([t.reshape(-1) for _, t in members])
+            wire = _narrow_wire(src, world, group) or wire
+            span = src
         if span is not None:
             # one packed arena (parallel/arena.py) or a single state: one copy, the local states stay untouched
             flat = span.to(wire, copy=True)

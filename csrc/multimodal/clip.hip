@@ -4,8 +4,9 @@
 // temporaries) and reduces their product.  ``paired_cosine_kernel``: one 64-lane wave per pair streams both rows
 // once with 16-byte loads and keeps the three sums (a.b, a.a, b.b) in registers -- scale * a.b / (|a| |b|).
 // CLIP-IQA: logits = 100 * img @ anchors^T followed by a softmax over each (positive, negative) prompt pair.
-// ``prompt_pair_prob_kernel``: an LDS-tiled [16 images x 32 anchors] dot-product block writes each pair's softmax
-// probability of the positive prompt, 1 / (1 + exp(l_neg - l_pos)), without the [N, 2P] logits tensor.
+// ``prompt_pair_prob_kernel``: anchors staged through LDS in groups of 32, each wave computing two images' 32 dot
+// products in registers, then each pair's softmax probability of the positive prompt,
+// 1 / (1 + exp(l_neg - l_pos)), without the [N, 2P] logits tensor.
 // Sums are fp32 (fp64 for fp64 embeddings), reduced across the wave in a fixed order (deterministic).
 #include "common/tm_common.h"
 
@@ -76,62 +77,86 @@ __global__ void __launch_bounds__(kThreads) paired_cosine_kernel(const T* __rest
   }
 }
 
-// Block = 16 images x 32 anchors (16 prompt pairs); K (the embedding dim) in chunks of 64 staged through LDS, each
-// thread accumulating 2 of the 512 dot products; then the pair softmax from an LDS logits tile.  The anchors (2P x D,
-// a few hundred KB at most) are re-read per block from L2, the images once from HBM.
-constexpr int kImgTile = 16, kAncTile = 32, kKTile = 64;
+// Block = 8 waves, 16 images (2 per wave).  The anchors are staged through LDS in groups of 32 (16 prompt pairs,
+// 32 x D values, <= 128 KB: every CLIP prompt set in one group); a wave holds its two image rows in registers
+// (16 values per lane per chunk, all loads in flight), keeps the 2 x 32 dot products in registers, reduces them
+// across the wave and writes the pair probabilities.  Images are read from HBM once, anchors from L2 once per block.
+constexpr int kPairThreads = 512, kAncGroup = 32, kImgPerWave = 2, kRegPerLane = 16;
+constexpr int kImgPerBlock = (kPairThreads / kWave) * kImgPerWave;
 
 template <typename T>
-__global__ void __launch_bounds__(kThreads) prompt_pair_prob_kernel(const T* __restrict__ img,
+__global__ void __launch_bounds__(kPairThreads) prompt_pair_prob_kernel(const T* __restrict__ img,
                                                                     const T* __restrict__ anchors, long long n,
                                                                     int n_anc, int D, float scale,
                                                                     float* __restrict__ out) {
   using A = acc_t<T>;
-  __shared__ A s_img[kImgTile][kKTile + 1];
-  __shared__ A s_anc[kAncTile][kKTile + 1];
-  __shared__ A s_log[kImgTile][kAncTile + 1];
-  const int t = threadIdx.x;
-  const int r = t / 16, c = t % 16;  // this thread's image row and its two anchor columns c, c + 16
-  const long long i0 = static_cast<long long>(blockIdx.x) * kImgTile;
+  extern __shared__ unsigned char smem_raw[];
+  A* s_anc = reinterpret_cast<A*>(smem_raw);  // [kAncGroup][D]
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
   const int pairs = n_anc / 2;
-  for (int a0 = 0; a0 < n_anc; a0 += kAncTile) {
-    A acc0 = A(0), acc1 = A(0);
-    for (int k0 = 0; k0 < D; k0 += kKTile) {
+  const long long img0 = static_cast<long long>(blockIdx.x) * kImgPerBlock + wave * kImgPerWave;
+  for (int g0 = 0; g0 < n_anc; g0 += kAncGroup) {
+    __syncthreads();  // the previous group's readers are done with s_anc
+    for (int d = threadIdx.x; d < D; d += kPairThreads) {
 #pragma unroll
-      for (int e = t; e < kImgTile * kKTile; e += kThreads) {
-        const int rr = e / kKTile, kk = e % kKTile;
-        const long long gi = i0 + rr;
-        s_img[rr][kk] = (gi < n && k0 + kk < D) ? ldx<T>(img + gi * D + k0 + kk) : A(0);
-      }
-#pragma unroll
-      for (int e = t; e < kAncTile * kKTile; e += kThreads) {
-        const int aa = e / kKTile, kk = e % kKTile;
-        const int ga = a0 + aa;
-        s_anc[aa][kk] = (ga < n_anc && k0 + kk < D) ? ldx<T>(anchors + static_cast<long long>(ga) * D + k0 + kk) : A(0);
-      }
-      __syncthreads();
-#pragma unroll 16
-      for (int kk = 0; kk < kKTile; ++kk) {
-        const A x = s_img[r][kk];
-        acc0 += x * s_anc[c][kk];
-        acc1 += x * s_anc[c + 16][kk];
-      }
-      __syncthreads();
-    }
-    s_log[r][c] = static_cast<A>(scale) * acc0;
-    s_log[r][c + 16] = static_cast<A>(scale) * acc1;
-    __syncthreads();
-    // one (image, pair) per thread: 16 images x 16 pairs of this anchor tile
-    const int pr = t % 16;
-    const int p = a0 / 2 + pr;
-    const long long gi = i0 + r;
-    if (gi < n && p < pairs) {
-      const A lp = s_log[r][2 * pr], ln = s_log[r][2 * pr + 1];
-      out[gi * pairs + p] = static_cast<float>(A(1) / (A(1) + exp(ln - lp)));
+      for (int a = 0; a < kAncGroup; ++a)  // 32 independent loads in flight per thread
+        s_anc[a * D + d] = (g0 + a < n_anc) ? ldx<T>(anchors + static_cast<long long>(g0 + a) * D + d) : A(0);
     }
     __syncthreads();
+    // both images' rows in registers, 16 values per lane per chunk: 32 independent loads in flight per lane
+    A acc[kImgPerWave][kAncGroup];
+#pragma unroll
+    for (int w = 0; w < kImgPerWave; ++w)
+#pragma unroll
+      for (int j = 0; j < kAncGroup; ++j) acc[w][j] = A(0);
+    for (int c0 = 0; c0 < D; c0 += kRegPerLane * kWave) {
+      A xr[kImgPerWave][kRegPerLane];
+#pragma unroll
+      for (int w = 0; w < kImgPerWave; ++w)
+#pragma unroll
+        for (int r = 0; r < kRegPerLane; ++r) {
+          const int d = c0 + r * kWave + lane;
+          const long long gi = img0 + w;
+          xr[w][r] = (gi < n && d < D) ? ldx<T>(img + gi * D + d) : A(0);
+        }
+#pragma unroll
+      for (int r = 0; r < kRegPerLane; ++r) {
+        const int d = c0 + r * kWave + lane;
+        if (d < D) {
+#pragma unroll
+          for (int j = 0; j < kAncGroup; ++j) {
+            const A a = s_anc[j * D + d];
+#pragma unroll
+            for (int w = 0; w < kImgPerWave; ++w) acc[w][j] += xr[w][r] * a;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < kImgPerWave; ++w) {
+      const long long gi = img0 + w;
+#pragma unroll
+      for (int j = 0; j < kAncGroup; ++j) acc[w][j] = wave_sum(acc[w][j]);
+      // lane p writes pair g0/2 + p of this group
+      A lp = A(0), ln = A(0);
+#pragma unroll
+      for (int p = 0; p < kAncGroup / 2; ++p) {
+        if (lane == p) {
+          lp = acc[w][2 * p];
+          ln = acc[w][2 * p + 1];
+        }
+      }
+      const int pp = g0 / 2 + lane;
+      if (gi < n && lane < kAncGroup / 2 && pp < pairs) {
+        const A s = static_cast<A>(scale);
+        out[gi * pairs + pp] = static_cast<float>(A(1) / (A(1) + exp(s * ln - s * lp)));
+      }
+    }
   }
 }
+
+constexpr size_t kMaxPromptLds = 128 * 1024;
 
 bool aligned16(const at::Tensor& t, int D, size_t elem) {
   return (reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0) && ((static_cast<size_t>(D) * elem) % 16 == 0);
@@ -177,10 +202,16 @@ at::Tensor prompt_pair_prob(const at::Tensor& img, const at::Tensor& anchors, do
   const int D = static_cast<int>(img.size(1));
   auto out = at::empty({n, pairs}, img.options().dtype(at::kFloat));
   if (n == 0 || pairs == 0) return out;
-  const long long blocks = (n + kImgTile - 1) / kImgTile;
+  const long long blocks = (n + kImgPerBlock - 1) / kImgPerBlock;
   TORCH_CHECK(blocks < (1LL << 31), "prompt_pair_prob: too many images");
   TM_DISPATCH_FLOAT(img.scalar_type(), "prompt_pair_prob", [&] {
-    hipLaunchKernelGGL((prompt_pair_prob_kernel<scalar_t>), dim3(static_cast<unsigned>(blocks)), dim3(kThreads), 0,
+    using A = acc_t<scalar_t>;
+    const size_t lds = static_cast<size_t>(kAncGroup) * D * sizeof(A);
+    TORCH_CHECK(lds <= kMaxPromptLds, "prompt_pair_prob: embedding dim too large for the LDS anchor group");
+    TORCH_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&prompt_pair_prob_kernel<scalar_t>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) == hipSuccess,
+                "prompt_pair_prob: LDS attribute");
+    hipLaunchKernelGGL((prompt_pair_prob_kernel<scalar_t>), dim3(static_cast<unsigned>(blocks)), dim3(kPairThreads), lds,
                        stream(), img.data_ptr<scalar_t>(), anchors.data_ptr<scalar_t>(), n,
                        static_cast<int>(anchors.size(0)), D, static_cast<float>(scale), out.data_ptr<float>());
   });

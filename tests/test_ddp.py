@@ -272,3 +272,31 @@ def _narrow_tier_body(rank, world, top, wire_bytes):
 @pytest.mark.parametrize("top,wire_bytes", [(100, 1), (1000, 2), (5000, 4), (2**40, 8)])
 def test_narrow_wire_tiers(top, wire_bytes):
     run_ddp(_narrow_tier_body, top, wire_bytes, world=2)
+
+
+def _narrow_gpu_body(rank, world):
+    import torchmetrics_amd as tm
+
+    torch.cuda.set_device(0)
+    g = torch.Generator().manual_seed(11)
+    preds = torch.randn(world, 3, 8192, 1000, generator=g).to(torch.bfloat16)
+    target = torch.randint(0, 1000, (world, 3, 8192), generator=g)
+    m = tm.MulticlassConfusionMatrix(1000).cuda()
+    for i in range(3):
+        m.update(preds[rank, i].cuda(), target[rank, i].cuda())
+    comm_stats(reset=True)
+    out = m.compute()
+    st = comm_stats()
+    ref = tm.MulticlassConfusionMatrix(1000, sync_on_compute=False)
+    for r in range(world):
+        for i in range(3):
+            ref.update(preds[r, i], target[r, i])
+    assert out.is_cuda and torch.equal(out.cpu(), ref.compute())
+    assert st["bytes"] == 16 + 1000 * 1000, st  # uint8 wire for the 8 MB int64 state
+
+
+@pytest.mark.gpu
+def test_narrow_wire_confmat_two_processes_one_device():
+    """The headline state synced through the engine's narrow wire with CUDA tensors (gloo between two processes on
+    one MI355X; RCCL itself refuses two ranks on one device)."""
+    run_ddp(_narrow_gpu_body, world=2)

@@ -86,7 +86,7 @@ def test_clip_iqa(tiny_clip):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
-@pytest.mark.parametrize("n,d", [(1, 16), (1000, 768), (333, 77)])
+@pytest.mark.parametrize("n,d", [(1, 16), (1000, 768), (333, 77), (9, 1024), (5, 3000)])
 def test_clip_math_kernels_gpu(dtype, n, d):
     """``csrc/multimodal/clip.hip`` vs the fp64 normalise-then-dot formula of the reference."""
     from torchmetrics_amd import ops

@@ -467,7 +467,8 @@ def paired_cosine(a: Tensor, b: Tensor, scale: float = 1.0) -> Tensor:
 def prompt_pair_prob(img: Tensor, anchors: Tensor, scale: float = 100.0) -> Tensor:
     """Softmax of ``scale * img @ anchors^T`` over each (positive, negative) anchor pair -> probability of the
     positive prompt, fp32 ``[N, P]`` (``csrc/multimodal/clip.hip``)."""
-    if img.is_cuda:
+    # the kernel stages 32 anchors x D in <= 128 KB of LDS (D <= 1024 in fp32; CLIP's projection dims are 512-1024)
+    if img.is_cuda and 32 * img.shape[-1] * (8 if img.dtype == torch.float64 else 4) <= 128 * 1024:
         if anchors.dtype != img.dtype:
             anchors = anchors.to(img.dtype)
         return _ops().prompt_pair_prob(img.contiguous(), anchors.contiguous(), float(scale))

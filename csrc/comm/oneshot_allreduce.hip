@@ -7,7 +7,7 @@
 // array, waits for all W flags, and reads the W buckets straight out of the peers' HBM.  Reference behaviour being
 // replaced: S/utilities/distributed.py:97-147 (per-state barrier + all_gather + local reduce).
 //
-// Buffer layout (one hipMalloc per rank, identical on every rank):
+// Buffer layout (one uncached fine-grained allocation per rank, identical on every rank):
 //   [ data parity 0 : slot ][ data parity 1 : slot ][ ready flags: 2 x kMaxBlocks x kMaxRanks u32 ]
 //   [ done flags: 2 x kMaxBlocks x kMaxRanks u32 ]
 // Call number `epoch` (1, 2, ...) uses parity epoch & 1.
@@ -147,7 +147,11 @@ int64_t ipc_buffer_alloc(int64_t nbytes, int64_t device) {
   TORCH_CHECK(nbytes > 0, "ipc_buffer_alloc: nbytes must be positive");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(c10::Device(c10::DeviceType::CUDA, static_cast<int>(device)));
   void* p = nullptr;
-  TORCH_CHECK(hipMalloc(&p, nbytes) == hipSuccess, "ipc_buffer_alloc: hipMalloc failed");
+  // uncached fine-grained memory: the peers poll flags and read data that another GPU writes while both kernels run;
+  // coarse-grained hipMalloc memory is only coherent at kernel boundaries (a peer's flag store could sit behind a
+  // stale line of this GPU's L2 for the whole wait)
+  TORCH_CHECK(hipExtMallocWithFlags(&p, nbytes, hipDeviceMallocUncached) == hipSuccess,
+              "ipc_buffer_alloc: hipExtMallocWithFlags(hipDeviceMallocUncached) failed");
   TORCH_CHECK(hipMemset(p, 0, nbytes) == hipSuccess, "ipc_buffer_alloc: hipMemset failed");
   TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "ipc_buffer_alloc: sync failed");
   return reinterpret_cast<int64_t>(p);

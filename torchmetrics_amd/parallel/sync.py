@@ -138,15 +138,7 @@ def _narrow_wire(src: Tensor, world: int, group: Optional[Any]) -> Optional[torc
         return None
     lo, hi = torch.aminmax(src)
     bound = torch.stack([hi, -lo]).to(torch.int64)
-    comm = get_oneshot(group) if (bound.is_cuda and _is_nccl(group)) else None
-    if comm is not None and comm.supports(bound):
-        # 16 bytes: the one-shot peer-read kernel, checked right here (a failure raises on every rank before any
-        # rank picks a wire dtype), instead of an RCCL launch
-        comm.all_reduce(bound, "max", None)
-        _stats["oneshot_all_reduce"] += 1
-        _stats["bytes"] += 16
-    else:
-        _all_reduce(bound, "max", group)
+    _all_reduce(bound, "max", group)  # RCCL / gloo: the same collective sequence on every rank, nothing to disown
     gmax, neg_gmin = bound.tolist()
     if neg_gmin > 0:
         return None

@@ -231,3 +231,22 @@ def test_running_window_equals_metric_on_last_batches(make, arg_fn, window):
             got, exp = got.sort().values, exp.sort().values
         torch.testing.assert_close(got, exp)
         run._computed = None
+
+
+@pytest.mark.parametrize("shape,output_dim", [((50, 3), -1), ((50, 3, 4), 1), ((50, 4, 3), -1)])
+@pytest.mark.parametrize("with_nans", [False, True])
+def test_multioutput_nan_rows_match_per_output_filter(shape, output_dim, with_nans):
+    g = torch.Generator().manual_seed(len(shape) + int(with_nans))
+    p, t = torch.randn(*shape, generator=g), torch.randn(*shape, generator=g)
+    if with_nans:
+        p.view(-1)[torch.randperm(p.numel(), generator=g)[:9]] = float("nan")
+        t.view(-1)[torch.randperm(t.numel(), generator=g)[:5]] = float("nan")
+    m = tm.MultioutputWrapper(tm.MeanSquaredError(), num_outputs=3, output_dim=output_dim)
+    m.update(p, t)
+    got = m.compute()
+    exp = []
+    for i in range(3):
+        pi, ti = p.narrow(output_dim, i, 1), t.narrow(output_dim, i, 1)
+        bad = torch.isnan(pi.flatten(1)).any(1) | torch.isnan(ti.flatten(1)).any(1)
+        exp.append(((pi[~bad] - ti[~bad]) ** 2).mean())
+    torch.testing.assert_close(got, torch.stack(exp))

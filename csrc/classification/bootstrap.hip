@@ -66,7 +66,6 @@ __global__ void __launch_bounds__(kBlock) mc_bootstrap_kernel(const scalar_t* __
         atomic_add_i64(g + C + p, m);
         atomic_add_i64(g + 2 * C + t, m);
       }
-      atomic_add_i64(g + 3 * C, m);
     }
   }
 }

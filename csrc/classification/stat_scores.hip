@@ -48,7 +48,9 @@ __device__ __forceinline__ void mc_accumulate(int mode, int t, const int* preds_
       atomic_add_i64(out + bin, 1);
     return;
   }
-  // stats workspace layout per group: [tp(C) | fp(C) | fn(C) | count]
+  // stats workspace layout per group: [tp(C) | fp(C) | fn(C) | (unused)]; every valid row adds exactly one to tp[t] or
+  // fn[t], so the finalize derives the row count from them -- no per-row atomic on one shared count address (with
+  // 8192 rows into one int64 that alone serialised the update at ~100 us)
   const long long base = group * (3LL * C + 1);
   bool hit = false;
   for (int k = 0; k < K; ++k) {
@@ -61,13 +63,8 @@ __device__ __forceinline__ void mc_accumulate(int mode, int t, const int* preds_
     }
   }
   const long long slot = hit ? t : 2LL * C + t;
-  if (use_lds) {
-    atomicAdd(&lds[slot], 1);
-    atomicAdd(&lds[3 * C], 1);
-  } else {
-    atomic_add_i64(out + base + slot, 1);
-    atomic_add_i64(out + base + 3LL * C, 1);
-  }
+  if (use_lds) atomicAdd(&lds[slot], 1);
+  else atomic_add_i64(out + base + slot, 1);
 }
 
 __device__ __forceinline__ void lds_flush(int* lds, int nbins, int64_t* out) {
@@ -239,7 +236,7 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 constexpr int kOrdBlock = 512;  // 8 waves: half the workgroups of 256-thread blocks for the same waves (measured on
                                 // the 406 MB ring, tools/mb/confmat_ring_mb.hip: 5.06 us vs 5.38 us per 8192 x 1000)
 
-template <typename scalar_t, typename target_t, int kPer>
+template <typename scalar_t, typename target_t, int kPer, int kMode>
 __global__ void __launch_bounds__(kOrdBlock) mc_argmax_ord16_kernel(const scalar_t* __restrict__ preds,
                                                                  const target_t* __restrict__ target, long long N,
                                                                  int C, long long ignore, bool has_ignore,
@@ -333,7 +330,18 @@ __global__ void __launch_bounds__(kOrdBlock) mc_argmax_ord16_kernel(const scalar
         raise_flag(flag, kErrTargetOutOfRange);
         ok = false;
       }
-      if (ok) atomic_add_i64(out + static_cast<long long>(t) * C + bidx, 1);
+      if (ok) {
+        if constexpr (kMode == kMcConfmat) {
+          atomic_add_i64(out + static_cast<long long>(t) * C + bidx, 1);
+        } else {  // stats workspace [tp | fp | fn | -]: a hit or a miss of the target class (+ the predicted class)
+          if (bidx == t) {
+            atomic_add_i64(out + t, 1);
+          } else {
+            atomic_add_i64(out + C + bidx, 1);
+            atomic_add_i64(out + 2LL * C + t, 1);
+          }
+        }
+      }
     }
 #pragma unroll
     for (int j = 0; j < kPer; ++j) cur[j] = nxt[j];
@@ -545,9 +553,6 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_kernel(const scalar_t* __re
         if ((bf & (kWave - 1)) == lane) acc[bf >> 6] += fp;
         if ((bn & (kWave - 1)) == lane) acc[bn >> 6] += fn;
       }
-      const int cnt = __popcll(__ballot(valid));
-      const int bc = 3 * C;
-      if ((bc & (kWave - 1)) == lane) acc[bc >> 6] += cnt;
     }
   }
 #pragma unroll
@@ -566,8 +571,16 @@ __global__ void __launch_bounds__(kBlock) mc_finalize_kernel(int64_t* __restrict
                                                              int64_t* __restrict__ fn) {
   const long long g = blockIdx.x;
   int64_t* w = ws + g * (3LL * C + 1);
-  const long long cnt = w[3 * C];
   __shared__ long long red[3][kBlock / kWave];
+  // rows counted in this group = sum over classes of tp + fn (each valid row is a hit or a miss of its target class)
+  long long rows = 0;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) rows += w[c] + w[2 * C + c];
+  rows = wave_sum_ll(rows);
+  if ((threadIdx.x & (kWave - 1)) == 0) red[0][threadIdx.x / kWave] = rows;
+  __syncthreads();
+  long long cnt = 0;
+  for (int i = 0; i < static_cast<int>(blockDim.x / kWave); ++i) cnt += red[0][i];
+  __syncthreads();  // red is reused by the micro reduction below
   long long st = 0, sf = 0, sn = 0;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const long long a = w[c], b = w[C + c], d = w[2 * C + c];
@@ -892,7 +905,11 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
             return e ? std::atoi(e) : 8;  // measured (8192 x 1000 bf16): 1/CU 23.1 us, 2: 13.9, 4: 10.3, 8: 8.75
           }();
           const int per = static_cast<int>((row_bytes / 16 + kWave - 1) / kWave);
-          const bool pipe = pipe_override > 0 && !samplewise && mode == kMcConfmat && per >= 1 && per <= 4 && lpr == 64;
+          // the order-key kernel (16-bit floats) serves both the confusion matrix and the stats workspace
+          const bool ord16_ok = sizeof(scalar_t) == 2 && !(std::getenv("TM_AMD_MC_ORD16") &&
+                                                           std::atoi(std::getenv("TM_AMD_MC_ORD16")) == 0);
+          const bool pipe = pipe_override > 0 && !samplewise && (mode == kMcConfmat || ord16_ok) && per >= 1 &&
+                            per <= 4 && lpr == 64;
           if (pipe) {
             const int cus = cu_count(preds.get_device());
             const long long want = (N + kBlock / kWave - 1) / (kBlock / kWave);
@@ -904,8 +921,12 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
                 if (!ord16_off) {
                   const long long want16 = (N + kOrdBlock / kWave - 1) / (kOrdBlock / kWave);  // one row per wave
                   const int grid16 = static_cast<int>(std::min<long long>(want16, static_cast<long long>(cus) * 4));
-                  hipLaunchKernelGGL((mc_argmax_ord16_kernel<scalar_t, target_t, P>), dim3(grid16), dim3(kOrdBlock),
-                                     0, s, pp, tp, N, C, ignore_index, has_ignore, outp, flagp);
+                  if (mode == kMcConfmat)
+                    hipLaunchKernelGGL((mc_argmax_ord16_kernel<scalar_t, target_t, P, kMcConfmat>), dim3(grid16),
+                                       dim3(kOrdBlock), 0, s, pp, tp, N, C, ignore_index, has_ignore, outp, flagp);
+                  else
+                    hipLaunchKernelGGL((mc_argmax_ord16_kernel<scalar_t, target_t, P, kMcStats>), dim3(grid16),
+                                       dim3(kOrdBlock), 0, s, pp, tp, N, C, ignore_index, has_ignore, outp, flagp);
                   return;
                 }
               }

@@ -181,7 +181,6 @@ __global__ void __launch_bounds__(kBlockT) topk_stats_kernel(const scalar_t* __r
   const int lane = threadIdx.x & (kWave - 1);
   const long long wave = (static_cast<long long>(blockIdx.x) * kBlockT + threadIdx.x) / kWave;
   const long long nwaves = static_cast<long long>(gridDim.x) * (kBlockT / kWave);
-  int counted = 0;  // valid rows seen by this wave (lane 0), one LDS add at the end
   for (long long row = wave; row < N; row += nwaves) {
     const long long tv = static_cast<long long>(target[row]);  // same address in every lane: one fetch
     LaneTopK<KP> tk;
@@ -199,18 +198,13 @@ __global__ void __launch_bounds__(kBlockT) topk_stats_kernel(const scalar_t* __r
     if (use_lds) {
       if (lane < K && lab != t) atomicAdd(&lds[C + lab], 1);
       if (lane == 0) atomicAdd(&lds[slot], 1);
-      ++counted;
     } else {
       int64_t* g = ws + (samplewise ? row : 0) * static_cast<long long>(nbins);
       if (lane < K && lab != t) atomic_add_i64(g + C + lab, 1);
-      if (lane == 0) {
-        atomic_add_i64(g + slot, 1);
-        atomic_add_i64(g + 3LL * C, 1);
-      }
+      if (lane == 0) atomic_add_i64(g + slot, 1);  // the row count is derived from tp + fn at finalize
     }
   }
   if (use_lds) {
-    if (lane == 0 && counted) atomicAdd(&lds[3 * C], counted);
     __syncthreads();
     for (int b = threadIdx.x; b < nbins; b += kBlockT) {
       const int v = lds[b];

@@ -63,7 +63,6 @@ def mc_update(
         ws[0, :C] += tp
         ws[0, C : 2 * C] += cm.sum(0) - tp
         ws[0, 2 * C : 3 * C] += cm.sum(1) - tp
-        ws[0, 3 * C] += t.numel()
         return
     onehot_t = torch.nn.functional.one_hot(target.clamp(0, C - 1), C) * valid.unsqueeze(-1)  # [N, X, C]
     pred_set = torch.zeros(N, X, C, dtype=torch.long)
@@ -72,13 +71,11 @@ def mc_update(
     tp = (onehot_t * pred_set).sum(1)  # [N, C]
     fn = (onehot_t * (1 - pred_set)).sum(1)
     fp = ((1 - onehot_t) * pred_set).sum(1)
-    cnt = valid.sum(1)
     if not samplewise:
-        tp, fp, fn, cnt = tp.sum(0, keepdim=True), fp.sum(0, keepdim=True), fn.sum(0, keepdim=True), cnt.sum(0, keepdim=True)
+        tp, fp, fn = tp.sum(0, keepdim=True), fp.sum(0, keepdim=True), fn.sum(0, keepdim=True)
     ws[:, :C] += tp
     ws[:, C : 2 * C] += fp
     ws[:, 2 * C : 3 * C] += fn
-    ws[:, 3 * C] += cnt
 
 
 def mc_stats_finalize(ws: Tensor, num_classes: int, micro: bool, accumulate: bool, tp: Tensor, fp: Tensor,
@@ -86,7 +83,10 @@ def mc_stats_finalize(ws: Tensor, num_classes: int, micro: bool, accumulate: boo
     C = int(num_classes)
     G = ws.numel() // (3 * C + 1)
     w = ws.view(G, 3 * C + 1)
-    a, b, d, cnt = w[:, :C], w[:, C : 2 * C], w[:, 2 * C : 3 * C], w[:, 3 * C : 3 * C + 1]
+    a, b, d = w[:, :C], w[:, C : 2 * C], w[:, 2 * C : 3 * C]
+    # every counted row added one to tp[t] or fn[t]: the row count of a group is sum(tp + fn) (the last slot of each
+    # group is unused, as in csrc/classification/stat_scores.hip)
+    cnt = (a + d).sum(1, keepdim=True)
     if micro:
         a, b, d = a.sum(1), b.sum(1), d.sum(1)
         e = C * cnt[:, 0] - a - b - d
@@ -760,7 +760,6 @@ def mc_bootstrap_update(preds: Tensor, target: Tensor, weights: Tensor, ws: Tens
     flat.index_add_(0, (base + tt).reshape(-1), (w * hit).reshape(-1))
     flat.index_add_(0, (base + C + pp).reshape(-1), (w * ~hit).reshape(-1))
     flat.index_add_(0, (base + 2 * C + tt).reshape(-1), (w * ~hit).reshape(-1))
-    flat.index_add_(0, (base[:, 0] + 3 * C), w.sum(1))
 
 
 # ------------------------------------------------------------------------------------------------------ RLE masks

@@ -269,12 +269,34 @@ class Metric(Module, ABC):
             self._move_list_states_to_cpu()
 
     def _batch_reset(self) -> None:
-        """``reset()`` inside ``forward``: the deferred-validation word survives (it belongs to the global state)."""
-        self.__dict__["_keep_device_errors"] = True
-        try:
-            self.reset()
-        finally:
-            self.__dict__.pop("_keep_device_errors", None)
+        """``reset()`` inside ``forward``: fresh default states for the batch (the saved global states are still
+        referenced, so nothing can be refilled in place: every tensor state bucket is ONE clone of its packed
+        defaults); the deferred-validation word and the global list arenas survive (they belong to the global
+        state)."""
+        d = self.__dict__
+        if type(self).reset is not Metric.reset:
+            # a subclass reset() may clear caches of its own: run it (keeping the global word and list arenas)
+            d["_keep_device_errors"] = True
+            try:
+                self.reset()
+            finally:
+                d.pop("_keep_device_errors", None)
+            return
+        d.pop("_errors_checked_at", None)
+        d["_update_count"] = 0
+        d["_forward_cache"] = None
+        d["_computed"] = None
+        fresh: Dict[Tuple[Any, torch.dtype, torch.device], List[str]] = {}
+        for attr, default in self._defaults.items():
+            if isinstance(default, Tensor):
+                cur = d.get(attr)
+                dev = cur.device if isinstance(cur, Tensor) else default.device
+                fresh.setdefault((_arena._reduce_kind(self._reductions[attr]), default.dtype, dev), []).append(attr)
+            else:
+                d[attr] = []
+        self._fill_fresh(fresh)
+        d["_cache"] = None
+        d["_is_synced"] = False
 
     def _restore_global(self, cache: Dict[str, Any], count: int, saved: bool) -> None:
         for attr, val in cache.items():
@@ -325,6 +347,7 @@ class Metric(Module, ABC):
         locals below reference it (a returned ``compute()`` result aliasing it, a compute-group sibling or a user handle
         keeps the out-of-place merge, which the reference always does: S/metric.py:329-352).  Merged entries are
         handed to :meth:`_reduce_states` as already reduced."""
+        pairs: List[Tuple[str, Tensor, Tensor]] = []
         for attr in list(global_state):
             if self._reductions[attr] is not dim_zero_sum:
                 continue
@@ -337,11 +360,21 @@ class Metric(Module, ABC):
             # references: global_state's entry, this local, getrefcount's argument
             if sys.getrefcount(glob) > 3:
                 continue
-            glob.add_(local)
-            setattr(self, attr, glob)
+            pairs.append((attr, glob, local))
+        glob = local = None
+        if not pairs:
+            return
+        gspan = _arena.contiguous_span([g for _, g, _ in pairs]) if len(pairs) > 1 else None
+        lspan = _arena.contiguous_span([t for _, _, t in pairs]) if gspan is not None else None
+        if gspan is not None and lspan is not None and lspan.dtype == gspan.dtype:
+            gspan.add_(lspan)  # the whole SUM bucket in one launch (both sides are packed spans in the same order)
+        else:
+            for _, g, t in pairs:
+                g.add_(t)
+        d = self.__dict__
+        for attr, g, _ in pairs:
+            d[attr] = g
             global_state[attr] = None  # consumed: _reduce_states skips it
-
-
 
     def _reduce_states(self, incoming_state: Dict[str, Any], only: Optional[str] = None) -> None:
         """Merge ``incoming_state`` (the pre-batch global state) with the current (batch) state (every state, or just
@@ -711,13 +744,18 @@ class Metric(Module, ABC):
             else:
                 setattr(self, attr, [])
             del cur
+        self._fill_fresh(fresh)
+        self._cache = None
+        self._is_synced = False
+
+    def _fill_fresh(self, fresh: Dict[Tuple[Any, torch.dtype, torch.device], List[str]]) -> None:
+        """Rebind ``fresh`` states (grouped by (reduction, dtype, device)) to copies of their defaults: several states of
+        one bucket are views of ONE clone of their packed defaults -- already laid out as the sync engine's arena span."""
         for (kind, _dt, dev), attrs in fresh.items():
             if kind is None or len(attrs) == 1:
                 for attr in attrs:
                     setattr(self, attr, self._defaults[attr].detach().clone().to(dev))
             else:
-                # several states of one (reduction, dtype, device) bucket: ONE clone of their packed defaults, the
-                # states are views of it -- already laid out as the sync engine's arena span
                 flat = self._packed_default(tuple(attrs), dev).clone()
                 off = 0
                 for attr in attrs:
@@ -725,8 +763,6 @@ class Metric(Module, ABC):
                     n = dflt.numel()
                     setattr(self, attr, flat[off : off + n].view(dflt.shape))
                     off += n
-        self._cache = None
-        self._is_synced = False
 
     def _packed_default(self, attrs: Tuple[str, ...], device: torch.device) -> Tensor:
         """The defaults of ``attrs`` back to back on ``device`` (cached until the defaults change)."""

@@ -1,0 +1,45 @@
+"""Binary / multilabel stat-score update throughput on ROCm (``csrc/classification/stat_scores.hip`` bin kernels):
+one JSON line per case with the update time and the effective input bandwidth."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torchmetrics_amd as tm  # noqa: E402
+
+
+def timed(m, p, t, reps=50):
+    for _ in range(5):
+        m.update(p, t)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        m.update(p, t)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e6
+
+
+def main():
+    g = torch.Generator(device="cuda").manual_seed(0)
+    cases = [
+        ("BinaryAccuracy", lambda: tm.BinaryAccuracy(), (1 << 24,), torch.float32, torch.int32),
+        ("BinaryAccuracy bf16/int64", lambda: tm.BinaryAccuracy(), (1 << 24,), torch.bfloat16, torch.int64),
+        ("MultilabelAccuracy(100)", lambda: tm.MultilabelAccuracy(100), (65536, 100), torch.float32, torch.int32),
+        ("MultilabelF1Score(1000)", lambda: tm.MultilabelF1Score(1000), (16384, 1000), torch.bfloat16, torch.int32),
+    ]
+    for name, make, shape, pdt, tdt in cases:
+        p = torch.rand(*shape, device="cuda", generator=g).to(pdt)
+        t = torch.randint(0, 2, shape, device="cuda", generator=g).to(tdt)
+        m = make().cuda()
+        us = timed(m, p, t)
+        nbytes = p.numel() * p.element_size() + t.numel() * t.element_size()
+        print(json.dumps({"case": name, "shape": list(shape), "update_us": round(us, 1),
+                          "TBps": round(nbytes / us / 1e6, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -123,7 +123,9 @@ def _bin(preds, target, L, thr, ignore, samplewise, dev, prob_check_all=True):
 
 
 @pytest.mark.parametrize("kind", ["prob", "logit", "int"])
-@pytest.mark.parametrize("shape,L", [((1000,), 1), ((64, 9), 9), ((16, 3, 2000), 3), ((8, 2, 5), 2)])
+@pytest.mark.parametrize("shape,L", [((1000,), 1), ((64, 9), 9), ((16, 3, 2000), 3), ((8, 2, 5), 2),
+                                     ((300000,), 1), ((3000, 100), 100), ((700, 1000), 1000), ((40, 7, 13), 7),
+                                     ((500, 1001), 1001)])
 @pytest.mark.parametrize("samplewise", [False, True])
 @pytest.mark.parametrize("ignore", [None, -1])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

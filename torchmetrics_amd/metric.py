@@ -636,11 +636,16 @@ class Metric(Module, ABC):
         per-image states are never folded)."""
         if not self._fold_cat_lists:
             return
-        for attr, fn in self._reductions.items():
-            if fn is dim_zero_cat:
-                val = getattr(self, attr)
-                if isinstance(val, list) and len(val) > 1:
-                    val[:] = [self._fold_into_arena(attr, val)]
+        d = self.__dict__
+        cats = d.get("_cat_attrs")
+        if cats is None or cats[0] is not self._reductions or cats[1] != len(self._reductions):
+            # the `cat` states, recomputed only when the reduction table changes (most metrics have none)
+            cats = d["_cat_attrs"] = (self._reductions, len(self._reductions),
+                                      tuple(a for a, fn in self._reductions.items() if fn is dim_zero_cat))
+        for attr in cats[2]:
+            val = d[attr] if attr in d else getattr(self, attr)
+            if isinstance(val, list) and len(val) > 1:
+                val[:] = [self._fold_into_arena(attr, val)]
 
     def _fold_into_arena(self, attr: str, parts: List[Any]) -> Any:
         """Concatenate a ``cat`` list state into its growable HBM arena.
@@ -799,7 +804,7 @@ class Metric(Module, ABC):
     # ------------------------------------------------------------------------------------------------- pickling
     def __getstate__(self) -> Dict[str, Any]:
         state = {k: v for k, v in self.__dict__.items()
-                 if k not in ("update", "compute", "_update_signature", "_cat_arenas", "_default_packs")}
+                 if k not in ("update", "compute", "_update_signature", "_cat_arenas", "_default_packs", "_cat_attrs")}
         for key in self._defaults:  # a folded list state: its own rows only, not the arena's spare capacity
             cur = state.get(key)
             if isinstance(cur, list) and any(_is_partial_view(v) for v in cur):

@@ -268,7 +268,7 @@ class Metric(Module, ABC):
         if self.compute_on_cpu:
             self._move_list_states_to_cpu()
 
-    def _batch_reset(self) -> None:
+    def _batch_reset(self, separate: bool = False) -> None:
         """``reset()`` inside ``forward``: fresh default states for the batch (the saved global states are still
         referenced, so nothing can be refilled in place: every tensor state bucket is ONE clone of its packed
         defaults); the deferred-validation word and the global list arenas survive (they belong to the global
@@ -294,7 +294,7 @@ class Metric(Module, ABC):
                 fresh.setdefault((_arena._reduce_kind(self._reductions[attr]), default.dtype, dev), []).append(attr)
             else:
                 d[attr] = []
-        self._fill_fresh(fresh)
+        self._fill_fresh(fresh, separate)
         d["_cache"] = None
         d["_is_synced"] = False
 
@@ -310,8 +310,10 @@ class Metric(Module, ABC):
         count = self._update_count
         saved = self._enter_batch_mode()
         cache = {attr: getattr(self, attr) for attr in self._defaults}
+        grad_in = torch.is_grad_enabled() and any(
+            isinstance(a, Tensor) and a.requires_grad for a in (*args, *kwargs.values()))
         try:
-            self._batch_reset()
+            self._batch_reset(separate=grad_in)
             self.update(*args, **kwargs)
             batch_val = self.compute()
         finally:
@@ -325,8 +327,12 @@ class Metric(Module, ABC):
         global_state = {attr: getattr(self, attr) for attr in self._defaults}
         count = self._update_count
         saved = self._enter_batch_mode()
+        # inputs carrying autograd history: the batch states must be separate leaves (in-place accumulation with
+        # grad into views of one packed clone is refused by autograd)
+        grad_in = torch.is_grad_enabled() and any(
+            isinstance(a, Tensor) and a.requires_grad for a in (*args, *kwargs.values()))
         try:
-            self._batch_reset()
+            self._batch_reset(separate=grad_in)
             self.update(*args, **kwargs)
             batch_val = self.compute()
         except BaseException:
@@ -753,11 +759,12 @@ class Metric(Module, ABC):
         self._cache = None
         self._is_synced = False
 
-    def _fill_fresh(self, fresh: Dict[Tuple[Any, torch.dtype, torch.device], List[str]]) -> None:
+    def _fill_fresh(self, fresh: Dict[Tuple[Any, torch.dtype, torch.device], List[str]],
+                    separate: bool = False) -> None:
         """Rebind ``fresh`` states (grouped by (reduction, dtype, device)) to copies of their defaults: several states of
         one bucket are views of ONE clone of their packed defaults -- already laid out as the sync engine's arena span."""
         for (kind, _dt, dev), attrs in fresh.items():
-            if kind is None or len(attrs) == 1:
+            if separate or kind is None or len(attrs) == 1:
                 for attr in attrs:
                     setattr(self, attr, self._defaults[attr].detach().clone().to(dev))
             else:

@@ -669,13 +669,15 @@ __device__ __forceinline__ void bin_slots(bool t, bool pa, bool pb, int& sa, int
 }
 
 // flat kernel: elements of preds [N, L, X] visited in memory order; group = samplewise ? n*L + l : l
+// partials != nullptr (LDS histogram, many labels): each block stores its [L * 7] int32 histogram to its own row of
+// `partials` and bin_partials_reduce_kernel folds the rows into ws -- instead of up to L * 7 global atomics per block.
 template <typename scalar_t, typename target_t>
 __global__ void __launch_bounds__(kBlock) bin_flat_kernel(const scalar_t* __restrict__ preds,
                                                           const target_t* __restrict__ target, long long total,
                                                           long long L, long long X, float thr_t, long long ignore,
                                                           bool has_ignore, bool samplewise, int64_t* __restrict__ ws,
                                                           int* __restrict__ flag, int* __restrict__ not_prob,
-                                                          bool prob_check_all) {
+                                                          bool prob_check_all, int* __restrict__ partials) {
   extern __shared__ __attribute__((aligned(16))) int lds[];
   const long long nbins = L * kBinSlots;
   const bool use_lds = !samplewise && nbins <= kLdsBins && static_cast<long long>(gridDim.x) * blockDim.x * 4 <= total;
@@ -684,11 +686,24 @@ __global__ void __launch_bounds__(kBlock) bin_flat_kernel(const scalar_t* __rest
     __syncthreads();
   }
   int local_not_prob = 0;
-  for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
-       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+  // (i / X, i % X, (i / X) % L) are advanced incrementally: no 64-bit division per element
+  const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
+  const long long i_start = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const long long s_q = stride / X, s_r = stride % X, s_l = s_q % L;
+  long long nl = i_start / X, rx = i_start % X, l = nl % L;
+  for (long long i = i_start; i < total; i += stride) {
+    if (i != i_start) {
+      rx += s_r;
+      long long carry = 0;
+      if (rx >= X) {
+        rx -= X;
+        carry = 1;
+      }
+      nl += s_q + carry;
+      l += s_l + carry;
+      if (l >= L) l -= L;
+    }
     const long long tv = static_cast<long long>(target[i]);
-    const long long nl = i / X;  // n*L + l
-    const long long l = nl % L;
     bool pa, pb, valid;
     // stat scores decide logits-vs-probabilities over ALL preds (ignored positions included); the binary
     // confusion matrix decides after dropping ignored positions (reference F/classification/confusion_matrix.py)
@@ -722,13 +737,34 @@ __global__ void __launch_bounds__(kBlock) bin_flat_kernel(const scalar_t* __rest
   if (IsFloating<scalar_t>::value) {
     if (__any(local_not_prob) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(not_prob, 1);
   }
+  if (partials != nullptr && !use_lds) {  // (the launcher only passes partials when LDS is used: keep the row valid)
+    int* row = partials + static_cast<long long>(blockIdx.x) * nbins;
+    for (long long b = threadIdx.x; b < nbins; b += blockDim.x) row[b] = 0;
+  }
   if (use_lds) {
     __syncthreads();
-    for (long long b = threadIdx.x; b < nbins; b += blockDim.x) {
-      const int v = lds[b];
-      if (v) atomic_add_i64(ws + b, v);
+    if (partials != nullptr) {
+      int* row = partials + static_cast<long long>(blockIdx.x) * nbins;
+      for (long long b = threadIdx.x; b < nbins; b += blockDim.x) row[b] = lds[b];
+    } else {
+      for (long long b = threadIdx.x; b < nbins; b += blockDim.x) {
+        const int v = lds[b];
+        if (v) atomic_add_i64(ws + b, v);
+      }
     }
   }
+}
+
+// ws[b] += sum over the blocks' partial histograms: grid (bin tiles, block groups); a thread sums its group's rows
+// of one bin (coalesced over bins) and adds once -- kPartialGroups atomics per bin in total.
+constexpr int kPartialGroups = 32;
+__global__ void __launch_bounds__(kBlock) bin_partials_reduce_kernel(const int* __restrict__ partials, int nrows,
+                                                                     int nbins, int64_t* __restrict__ ws) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nbins) return;
+  long long acc = 0;
+  for (int r = blockIdx.y; r < nrows; r += gridDim.y) acc += partials[static_cast<long long>(r) * nbins + b];
+  if (acc) atomic_add_i64(ws + b, acc);
 }
 
 // segment kernel for long contiguous segments (X large): block = one chunk of one (n, l) segment, register
@@ -1151,11 +1187,24 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
                            flag.data_ptr<int>(), not_prob.data_ptr<int>(), prob_check_all);
       } else {
         const long long nbins = L * kBinSlots;
-        const size_t lds_bytes = (!samplewise && nbins <= kLdsBins) ? nbins * sizeof(int) : 0;
+        const bool lds_hist = !samplewise && nbins <= kLdsBins;
+        const size_t lds_bytes = lds_hist ? nbins * sizeof(int) : 0;
         const int grid = pick_grid(total, kBlock * 4);
+        // many labels: per-block histograms go through a partials buffer instead of L * 7 atomics per block
+        // (the kernel itself only uses LDS when every thread sees >= 4 elements)
+        const bool use_partials = lds_hist && nbins > 64 && static_cast<long long>(grid) * kBlock * 4 <= total;
+        at::Tensor partials;
+        if (use_partials) partials = at::empty({static_cast<long long>(grid) * nbins}, ws.options().dtype(at::kInt));
         hipLaunchKernelGGL((bin_flat_kernel<scalar_t, target_t>), dim3(grid), dim3(kBlock), lds_bytes, s, pp, tp,
                            total, L, X, thr_t, ignore_index, has_ignore, samplewise, ws.data_ptr<int64_t>(),
-                           flag.data_ptr<int>(), not_prob.data_ptr<int>(), prob_check_all);
+                           flag.data_ptr<int>(), not_prob.data_ptr<int>(), prob_check_all,
+                           use_partials ? partials.data_ptr<int>() : nullptr);
+        if (use_partials) {
+          const dim3 rgrid(static_cast<unsigned>((nbins + kBlock - 1) / kBlock),
+                           static_cast<unsigned>(std::min(kPartialGroups, grid)));
+          hipLaunchKernelGGL(bin_partials_reduce_kernel, rgrid, dim3(kBlock), 0, s, partials.data_ptr<int>(), grid,
+                             static_cast<int>(nbins), ws.data_ptr<int64_t>());
+        }
       }
     });
   });

@@ -1,4 +1,4 @@
-"""Binary / multilabel stat-score update throughput on ROCm (``csrc/classification/stat_scores.hip`` bin kernels):
+"""Binary / multilabel / multiclass stat-score update throughput on ROCm (``csrc/classification/stat_scores.hip`` bin kernels):
 one JSON line per case with the update time and the effective input bandwidth."""
 import json
 import os
@@ -30,10 +30,18 @@ def main():
         ("BinaryAccuracy bf16/int64", lambda: tm.BinaryAccuracy(), (1 << 24,), torch.bfloat16, torch.int64),
         ("MultilabelAccuracy(100)", lambda: tm.MultilabelAccuracy(100), (65536, 100), torch.float32, torch.int32),
         ("MultilabelF1Score(1000)", lambda: tm.MultilabelF1Score(1000), (16384, 1000), torch.bfloat16, torch.int32),
+        ("MulticlassAccuracy(1000) bf16", lambda: tm.MulticlassAccuracy(1000), (8192, 1000), torch.bfloat16, None),
+        ("MulticlassAccuracy(1000) fp32", lambda: tm.MulticlassAccuracy(1000), (8192, 1000), torch.float32, None),
+        ("MulticlassConfusionMatrix(1000) fp32", lambda: tm.MulticlassConfusionMatrix(1000), (8192, 1000),
+         torch.float32, None),
+        ("MulticlassAccuracy(10) bf16", lambda: tm.MulticlassAccuracy(10), (1 << 20, 10), torch.bfloat16, None),
     ]
     for name, make, shape, pdt, tdt in cases:
         p = torch.rand(*shape, device="cuda", generator=g).to(pdt)
-        t = torch.randint(0, 2, shape, device="cuda", generator=g).to(tdt)
+        if tdt is None:  # multiclass: int64 class labels
+            t = torch.randint(0, shape[1], (shape[0],), device="cuda", generator=g)
+        else:
+            t = torch.randint(0, 2, shape, device="cuda", generator=g).to(tdt)
         m = make().cuda()
         us = timed(m, p, t)
         nbytes = p.numel() * p.element_size() + t.numel() * t.element_size()

@@ -1023,11 +1023,8 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
             return e ? std::atoi(e) : 8;  // measured (8192 x 1000 bf16): 1/CU 23.1 us, 2: 13.9, 4: 10.3, 8: 8.75
           }();
           const int per = static_cast<int>((row_bytes / 16 + kWave - 1) / kWave);
-          // the order-key kernel (16-bit floats) serves both the confusion matrix and the stats workspace
-          const bool ord16_ok = sizeof(scalar_t) == 2 && !(std::getenv("TM_AMD_MC_ORD16") &&
-                                                           std::atoi(std::getenv("TM_AMD_MC_ORD16")) == 0);
-          const bool pipe = pipe_override > 0 && !samplewise && (mode == kMcConfmat || ord16_ok) && per >= 1 &&
-                            per <= 4 && lpr == 64;
+          // the pipelined kernels (order-key for 16-bit floats) serve both the confusion matrix and the stats workspace
+          const bool pipe = pipe_override > 0 && !samplewise && per >= 1 && per <= 4 && lpr == 64;
           if (pipe) {
             const int cus = cu_count(preds.get_device());
             const long long want = (N + kBlock / kWave - 1) / (kBlock / kWave);

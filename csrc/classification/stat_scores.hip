@@ -18,6 +18,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kLdsBins = 12288;  // 48 KiB of int32 bins
+constexpr int kStageBytes = 16384;  // few-bin kernel: LDS copy of a block's 256 argmax rows
 
 // ----------------------------------------------------------------------------------------------------------------
 // multiclass: per-item predicted label
@@ -492,8 +493,13 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_kernel(const scalar_t* __re
                                                             const target_t* __restrict__ target, long long N,
                                                             long long X, int C, long long ignore, bool has_ignore,
                                                             int mode, int64_t* __restrict__ out,
-                                                            int* __restrict__ flag) {
+                                                            int* __restrict__ flag, bool stage) {
   __shared__ int lds[256];
+  // stage (argmax, X == 1, 256 * C * sizeof(scalar_t) <= kStageBytes): the block's 256 rows are one contiguous
+  // piece of preds, copied into LDS with 16-byte loads; each lane then reads its row from LDS (instead of C
+  // 2-4 byte loads per lane with a C-element stride across the wave)
+  __shared__ __attribute__((aligned(16))) unsigned char stage_raw[kStageBytes];
+  const scalar_t* srow = reinterpret_cast<const scalar_t*>(stage_raw);
   const int nbins = mode == kMcConfmat ? C * C : 3 * C + 1;
   const int lane = threadIdx.x & (kWave - 1);
   for (int b = threadIdx.x; b < nbins; b += blockDim.x) lds[b] = 0;
@@ -501,19 +507,30 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_kernel(const scalar_t* __re
   int acc[4] = {0, 0, 0, 0};
   const long long items = N * X;
   const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
-  // loop bounds are wave-uniform so every ballot sees the whole wave
-  const long long wave_base = static_cast<long long>(blockIdx.x) * blockDim.x + (threadIdx.x & ~(kWave - 1));
-  for (long long base = wave_base; base < items; base += stride) {
-    const long long it = base + lane;
+  // loop bounds are block-uniform so every ballot sees the whole wave (and the staging barriers the whole block)
+  for (long long bbase = static_cast<long long>(blockIdx.x) * blockDim.x; bbase < items; bbase += stride) {
+    if (kArgmax && stage) {
+      __syncthreads();  // the previous rows are read
+      const long long rows = items - bbase < blockDim.x ? items - bbase : blockDim.x;
+      const long long nbytes = rows * C * static_cast<long long>(sizeof(scalar_t));
+      const unsigned char* src = reinterpret_cast<const unsigned char*>(preds + bbase * C);
+      for (long long o = threadIdx.x * 16LL; o + 16 <= nbytes; o += blockDim.x * 16LL)
+        *reinterpret_cast<u32x4*>(stage_raw + o) = *reinterpret_cast<const u32x4*>(src + o);
+      for (long long o = (nbytes / 16) * 16 + threadIdx.x; o < nbytes; o += blockDim.x) stage_raw[o] = src[o];
+      __syncthreads();
+    }
+    const long long it = bbase + threadIdx.x;
     int t = -1, p = -1;
     if (it < items && mc_target(target, it, C, ignore, has_ignore, flag, t)) {
       const long long n = it / X, x = it - n * X;
       if constexpr (kArgmax) {
-        const scalar_t* pr = preds + n * C * X + x;
+        const bool staged = stage;
+        const scalar_t* pr = staged ? srow + static_cast<long long>(threadIdx.x) * C : preds + n * C * X + x;
+        const long long cs = staged ? 1 : X;
         float best = to_f32(pr[0]);
         int bidx = 0;
         for (int c = 1; c < C; ++c) {
-          const float v = to_f32(pr[static_cast<long long>(c) * X]);
+          const float v = to_f32(pr[static_cast<long long>(c) * cs]);
           if (argmax_better(v, c, best, bidx)) {
             best = v;
             bidx = c;
@@ -1083,18 +1100,22 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
           hipLaunchKernelGGL((mc_argmax_rows_kernel<scalar_t, target_t>), dim3(grid), dim3(kBlock), lds_bytes, s, pp,
                              tp, N, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, vec, samplewise);
         } else if (!samplewise && nbins <= 256) {
-          const int grid = pick_grid(N * X, kBlock);  // one item per lane: latency-bound, spread wide
+          // every block flushes its <= 256 bins with global atomics onto the SAME few addresses: keep the grid to
+          // ~2 blocks per CU (each thread walks several items) -- 2048 blocks serialised ~2048 atomics per bin
+          const int grid = static_cast<int>(std::min<long long>(pick_grid(N * X, kBlock), 2LL * cu_count(preds.get_device())));
+          const bool stage = X == 1 && static_cast<long long>(kBlock) * C * sizeof(scalar_t) <= kStageBytes &&
+                             reinterpret_cast<uintptr_t>(pp) % 16 == 0;
           hipLaunchKernelGGL((mc_fewbins_kernel<scalar_t, target_t, true>), dim3(grid), dim3(kBlock), 0, s, pp, tp, N,
-                             X, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp);
+                             X, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, stage);
         } else {
           const int grid = pick_grid(N * X, kBlock);
           hipLaunchKernelGGL((mc_items_kernel<scalar_t, target_t, true>), dim3(grid), dim3(kBlock), lds_bytes, s, pp,
                              tp, N, X, C, 1, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, samplewise);
         }
       } else if (!samplewise && nbins <= 256 && K == 1) {
-        const int grid = pick_grid(N * X, kBlock);
+        const int grid = static_cast<int>(std::min<long long>(pick_grid(N * X, kBlock), 2LL * cu_count(preds.get_device())));
         hipLaunchKernelGGL((mc_fewbins_kernel<scalar_t, target_t, false>), dim3(grid), dim3(kBlock), 0, s, pp, tp, N,
-                           X, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp);
+                           X, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, false);
       } else {
         const int grid = pick_grid(N * X, kBlock);
         hipLaunchKernelGGL((mc_items_kernel<scalar_t, target_t, false>), dim3(grid), dim3(kBlock), lds_bytes, s, pp,

@@ -29,7 +29,8 @@ def _mc(preds, target, C, ignore, mode, samplewise, dev):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("shape", [(257, 5), (1000, 64), (333, 1000), (64, 37), (8, 6, 7), (4, 130, 9)])
+@pytest.mark.parametrize("shape", [(257, 5), (1000, 64), (333, 1000), (64, 37), (8, 6, 7), (4, 130, 9), (70001, 10),
+                                   (5000, 16), (3000, 31)])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("ignore", [None, 0, -1])
 def test_multiclass_argmax(dtype, shape, mode, ignore):

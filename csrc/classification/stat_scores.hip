@@ -582,13 +582,14 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_kernel(const scalar_t* __re
 
 // fold a multiclass stats workspace [G, 3C+1] into the states; optionally micro-reduce over classes.
 // accumulate=true: states += batch ; false: states = batch (samplewise outputs). Re-zeros the workspace.
-__global__ void __launch_bounds__(kBlock) mc_finalize_kernel(int64_t* __restrict__ ws, int C, bool micro,
+template <int kT>
+__global__ void __launch_bounds__(kT) mc_finalize_kernel(int64_t* __restrict__ ws, int C, bool micro,
                                                              bool accumulate, int64_t* __restrict__ tp,
                                                              int64_t* __restrict__ fp, int64_t* __restrict__ tn,
                                                              int64_t* __restrict__ fn) {
   const long long g = blockIdx.x;
   int64_t* w = ws + g * (3LL * C + 1);
-  __shared__ long long red[3][kBlock / kWave];
+  __shared__ long long red[3][kT / kWave];
   // rows counted in this group = sum over classes of tp + fn (each valid row is a hit or a miss of its target class)
   long long rows = 0;
   for (int c = threadIdx.x; c < C; c += blockDim.x) rows += w[c] + w[2 * C + c];
@@ -1137,9 +1138,16 @@ void mc_stats_finalize(at::Tensor ws, int64_t num_classes, bool micro, bool accu
     TORCH_CHECK(t->scalar_type() == at::kLong && t->is_contiguous(), "mc_stats_finalize: states must be int64");
     TORCH_CHECK(t->numel() == (micro ? G : G * C), "mc_stats_finalize: state size mismatch");
   }
-  hipLaunchKernelGGL(mc_finalize_kernel, dim3(G), dim3(kBlock), 0, stream(), ws.data_ptr<int64_t>(), C, micro,
-                     accumulate, tp.data_ptr<int64_t>(), fp.data_ptr<int64_t>(), tn.data_ptr<int64_t>(),
-                     fn.data_ptr<int64_t>());
+  // one block per group; a single large group (the usual global stats, C in the hundreds or more) gets 1024 threads so
+  // both passes over the classes are one strided step per thread instead of a chain of dependent loads
+  if (G <= 8 && C >= 512)
+    hipLaunchKernelGGL(mc_finalize_kernel<1024>, dim3(G), dim3(1024), 0, stream(), ws.data_ptr<int64_t>(), C, micro,
+                       accumulate, tp.data_ptr<int64_t>(), fp.data_ptr<int64_t>(), tn.data_ptr<int64_t>(),
+                       fn.data_ptr<int64_t>());
+  else
+    hipLaunchKernelGGL(mc_finalize_kernel<kBlock>, dim3(G), dim3(kBlock), 0, stream(), ws.data_ptr<int64_t>(), C,
+                       micro, accumulate, tp.data_ptr<int64_t>(), fp.data_ptr<int64_t>(), tn.data_ptr<int64_t>(),
+                       fn.data_ptr<int64_t>());
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 

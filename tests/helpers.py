@@ -122,7 +122,11 @@ def _ddp_entry(rank: int, world: int, port: int, fn: Callable, args: tuple, errq
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
     try:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        except RuntimeError as err:  # a port / mesh race with another test process: run_ddp retries these
+            errq.put(f"{_RENDEZVOUS} rank {rank}: {err!r}")
+            raise
         fn(rank, world, *args)
     except BaseException as err:  # noqa: BLE001
         import traceback
@@ -134,23 +138,36 @@ def _ddp_entry(rank: int, world: int, port: int, fn: Callable, args: tuple, errq
             dist.destroy_process_group()
 
 
-def run_ddp(fn: Callable, *args: Any, world: int = NUM_PROCESSES) -> None:
-    """Run ``fn(rank, world, *args)`` on ``world`` gloo ranks (spawned processes); re-raise the first failure."""
+_RENDEZVOUS = "rendezvous failure"
+
+
+def run_ddp(fn: Callable, *args: Any, world: int = NUM_PROCESSES, attempts: int = 3) -> None:
+    """Run ``fn(rank, world, *args)`` on ``world`` gloo ranks (spawned processes); re-raise the first failure.
+    A failed rendezvous (a port taken by a concurrent test process between picking and binding it) is retried on a
+    fresh port."""
     ctx = mp.get_context("spawn")
-    errq = ctx.SimpleQueue()
-    port = _free_port()
-    procs = [ctx.Process(target=_ddp_entry, args=(r, world, port, fn, args, errq)) for r in range(world)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(timeout=300)
-    for p in procs:
-        if p.is_alive():
-            p.kill()
-    if not errq.empty():
-        raise AssertionError(errq.get())
-    for p in procs:
-        assert p.exitcode == 0, f"ddp worker exited with {p.exitcode}"
+    for attempt in range(attempts):
+        errq = ctx.SimpleQueue()
+        port = _free_port()
+        procs = [ctx.Process(target=_ddp_entry, args=(r, world, port, fn, args, errq)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=300)
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        errors = []
+        while not errq.empty():
+            errors.append(errq.get())
+        if errors and all(e.startswith(_RENDEZVOUS) for e in errors) and attempt + 1 < attempts:
+            continue
+        if errors:
+            real = [e for e in errors if not e.startswith(_RENDEZVOUS)]
+            raise AssertionError((real or errors)[0])
+        for p in procs:
+            assert p.exitcode == 0, f"ddp worker exited with {p.exitcode}"
+        return
 
 
 def run_ddp_class_test(

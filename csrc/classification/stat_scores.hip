@@ -1104,7 +1104,10 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
           // every block flushes its <= 256 bins with global atomics onto the SAME few addresses: keep the grid to
           // ~2 blocks per CU (each thread walks several items) -- 2048 blocks serialised ~2048 atomics per bin
           const int grid = static_cast<int>(std::min<long long>(pick_grid(N * X, kBlock), 2LL * cu_count(preds.get_device())));
-          const bool stage = X == 1 && static_cast<long long>(kBlock) * C * sizeof(scalar_t) <= kStageBytes &&
+          static const bool stage_off = std::getenv("TM_AMD_FEWBINS_STAGE") &&
+                                        std::atoi(std::getenv("TM_AMD_FEWBINS_STAGE")) == 0;  // A/B knob
+          const bool stage = !stage_off && X == 1 &&
+                             static_cast<long long>(kBlock) * C * sizeof(scalar_t) <= kStageBytes &&
                              reinterpret_cast<uintptr_t>(pp) % 16 == 0;
           hipLaunchKernelGGL((mc_fewbins_kernel<scalar_t, target_t, true>), dim3(grid), dim3(kBlock), 0, s, pp, tp, N,
                              X, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, stage);

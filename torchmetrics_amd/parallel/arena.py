@@ -24,10 +24,10 @@ _Key = Tuple[str, torch.dtype, torch.device]
 
 
 def _reduce_kind(fn) -> Optional[str]:
-    from torchmetrics_amd.utilities.data import dim_zero_max, dim_zero_mean, dim_zero_min, dim_zero_sum
-
     global _KINDS
-    if _KINDS is None:
+    if _KINDS is None:  # (imported lazily: utilities.data imports this package)
+        from torchmetrics_amd.utilities.data import dim_zero_max, dim_zero_mean, dim_zero_min, dim_zero_sum
+
         _KINDS = {dim_zero_sum: "sum", dim_zero_mean: "mean", dim_zero_max: "max", dim_zero_min: "min"}
     return _KINDS.get(fn) if fn is not None and not isinstance(fn, str) else None
 

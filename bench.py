@@ -10,7 +10,10 @@ the max over ranks is reported.  ``compute_ms`` (sync + compute wall-clock) is m
 The same loop is also run through an op-for-op emulation of the reference implementation (``benchmarks/reference_path.py``)
 on the same data in the same process; ``vs_baseline`` = ours / emulated reference.
 
-Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]`` (N>1: launch with torch.distributed.run).
+Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]``.  ``--gpus N`` always means N ranks: under a launcher
+(``torch.distributed.run``, ``WORLD_SIZE`` set) the world size must equal N or the run exits non-zero; without one,
+N > 1 spawns ``torch.distributed.run --nproc-per-node N`` itself as a child process before any GPU call
+(``benchmarks/_dist.py`` ``launch``).
 """
 import argparse
 import json
@@ -31,7 +34,11 @@ DEFAULT_RING_MB = 400
 
 
 def _setup(gpus: int):
+    from benchmarks._dist import launch
+
+    launch(gpus, __file__)  # returns only inside one of the ``gpus`` ranks
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    assert world == gpus, (world, gpus)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if torch.cuda.is_available():
@@ -117,14 +124,14 @@ def _reset(metric) -> None:
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE under a launcher, else 1)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-baseline", action="store_true", help="skip the in-run reference-emulation baseline")
     ap.add_argument("--ring-mb", type=int, default=DEFAULT_RING_MB, help="size of the input ring (MB)")
     args = ap.parse_args()
 
-    world, rank, device = _setup(args.gpus)
+    world, rank, device = _setup(args.gpus or int(os.environ.get("WORLD_SIZE", "1")))
     from torchmetrics_amd.classification import MulticlassConfusionMatrix
 
     preds, target = _data(device, rank, args.ring_mb)

@@ -18,6 +18,7 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+from benchmarks._dist import dist_info, launch  # noqa: E402
 from torchmetrics_amd import MetricCollection  # noqa: E402
 from torchmetrics_amd import classification as C  # noqa: E402
 from torchmetrics_amd import regression as R  # noqa: E402
@@ -52,6 +53,8 @@ def build(device):
 
 def main() -> None:
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None, help="ranks to run (default: WORLD_SIZE or 1); N > 1 without a "
+                    "launcher spawns N ranks itself")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--sync-every-step", action="store_true")
@@ -61,6 +64,7 @@ def main() -> None:
                     "bound to each buffer of the input ring); the "
                          "list-state member (calibration error) stays eager")
     args = ap.parse_args()
+    launch(args.gpus or int(os.environ.get("WORLD_SIZE", "1")), __file__)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -183,6 +187,7 @@ def main() -> None:
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "sync_every_step": args.sync_every_step, "compute_groups": True, "hip_graph": args.graph, "dtype": "bf16", "data": "synthetic",
             "groups": len(cls.compute_groups), "acc": float(out["acc"]), "r2": float(out["r2"]),
+            "dist": dist_info(world),
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -24,7 +24,7 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from benchmarks._dist import barrier_sync, dist_info, max_over_ranks, setup, sync, teardown  # noqa: E402
+from benchmarks._dist import barrier_sync, dist_info, launch, max_over_ranks, setup, sync, teardown  # noqa: E402
 from torchmetrics_amd.image import FrechetInceptionDistance  # noqa: E402
 from torchmetrics_amd.image.generative import _compute_fid  # noqa: E402
 from torchmetrics_amd.parallel.sync import comm_stats  # noqa: E402
@@ -117,11 +117,14 @@ def fp64_check(m):
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None, help="ranks to run (default: WORLD_SIZE or 1); N > 1 without a "
+                    "launcher spawns N ranks itself")
     ap.add_argument("--samples", type=int, default=50_000)
     ap.add_argument("--dim", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=1000)
     ap.add_argument("--no-baseline", action="store_true")
     args = ap.parse_args()
+    launch(args.gpus or int(os.environ.get("WORLD_SIZE", "1")), __file__)
     world, rank, device = setup()
     nb = args.samples // args.batch
     g = torch.Generator(device=device).manual_seed(0)

@@ -24,7 +24,7 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from benchmarks._dist import barrier_sync, dist_info, max_over_ranks, setup, teardown  # noqa: E402
+from benchmarks._dist import barrier_sync, dist_info, launch, max_over_ranks, setup, teardown  # noqa: E402
 from torchmetrics_amd.detection import MeanAveragePrecision  # noqa: E402
 from torchmetrics_amd.parallel.sync import comm_stats  # noqa: E402
 
@@ -120,8 +120,11 @@ def reference_sync(m, device, world):
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None, help="ranks to run (default: WORLD_SIZE or 1); N > 1 without a "
+                    "launcher spawns N ranks itself")
     ap.add_argument("--images", type=int, default=512)
     args = ap.parse_args()
+    launch(args.gpus or int(os.environ.get("WORLD_SIZE", "1")), __file__)
     world, rank, device = setup()
     preds, target = make_data(args.images, device)
     run(device, preds[:BATCH * world], target[:BATCH * world], BATCH * world, rank, world, reps=1)  # warm-up

@@ -8,6 +8,7 @@
 import os
 import pickle
 import socket
+import sys
 from functools import partial
 from typing import Any, Callable, Dict, Optional
 
@@ -125,9 +126,12 @@ def _ddp_entry(rank: int, world: int, port: int, fn: Callable, args: tuple, errq
         try:
             dist.init_process_group("gloo", rank=rank, world_size=world)
         except RuntimeError as err:  # a port / mesh race with another test process: run_ddp retries these
+            # queued once, as a rendezvous failure only (a second, traceback entry would defeat run_ddp's retry)
             errq.put(f"{_RENDEZVOUS} rank {rank}: {err!r}")
-            raise
+            sys.exit(3)
         fn(rank, world, *args)
+    except SystemExit:
+        raise  # the rendezvous failure above, already queued
     except BaseException as err:  # noqa: BLE001
         import traceback
 

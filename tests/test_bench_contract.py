@@ -35,11 +35,39 @@ def test_bench_two_rank_gloo_contract(tmp_path):
     assert out["value"] > 0 and out["vs_baseline"] is not None and out["higher_is_better"] is True
 
 
-def _torchrun_json(tmp_path, script, *args):
+def _self_launch(tmp_path, script, *args, extra_env=None):
+    """``python <script> --gpus 2 ...`` WITHOUT torchrun: the script itself must start the 2 ranks."""
     env = dict(os.environ, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "benchmarks", script), *args]
-    res = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=580)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(extra_env or {})
+    cmd = [sys.executable, os.path.join(ROOT, script), *args]
+    return subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=580)
+
+
+@pytest.mark.timeout(600)
+def test_bench_self_launches_n_ranks(tmp_path):
+    """The driver's single-process form ``python bench.py --gpus 2`` must run 2 ranks and report them."""
+    res = _self_launch(tmp_path, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--ring-mb", "8")
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["dist"]["world_size_seen"] == 2
+    assert out["config"]["parallelism"] == "dp2"
+    assert out["dist"]["engine_collectives"]["all_reduce"] >= 1
+
+
+def test_bench_world_size_mismatch_exits_nonzero(tmp_path):
+    res = _self_launch(tmp_path, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0", "--ring-mb", "8",
+                       extra_env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert res.returncode != 0
+    assert "disagrees with --gpus" in res.stderr
+    assert not [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+
+
+def _torchrun_json(tmp_path, script, *args):
+    res = _self_launch(tmp_path, os.path.join("benchmarks", script), "--gpus", "2", *args)
     assert res.returncode == 0, res.stderr[-3000:]
     lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, res.stdout
@@ -71,3 +99,4 @@ def test_bench_collection_two_rank_gloo(tmp_path):
     reference collection (parity-checked inside the bench)."""
     out = _torchrun_json(tmp_path, "bench_collection.py", "--steps", "3", "--warmup", "1", "--sync-every-step")
     assert out["n_gpus"] == 2 and out["vs_baseline"] is not None and out["baseline"]["value"] > 0
+    assert out["dist"]["world_size_seen"] == 2 and out["dist"]["engine_collectives"]["all_reduce"] >= 1

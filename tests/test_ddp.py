@@ -300,3 +300,34 @@ def test_narrow_wire_confmat_two_processes_one_device():
     """The headline state synced through the engine's narrow wire with CUDA tensors (gloo between two processes on
     one MI355X; RCCL itself refuses two ranks on one device)."""
     run_ddp(_narrow_gpu_body, world=2)
+
+
+def _noop_rank(rank, world):
+    import torch.distributed as dist
+
+    assert dist.is_initialized() and dist.get_world_size() == world
+
+
+def test_run_ddp_retries_a_failed_rendezvous(monkeypatch):
+    """A port taken between picking and binding it fails init_process_group; run_ddp must retry on a fresh port."""
+    import socket
+
+    from tests import helpers
+
+    busy = socket.socket()
+    busy.bind(("127.0.0.1", 0))
+    busy.listen(1)
+    ports = iter([busy.getsockname()[1]])
+    real = helpers._free_port
+    calls = []
+
+    def fake_port():
+        calls.append(1)
+        return next(ports, None) or real()
+
+    monkeypatch.setattr(helpers, "_free_port", fake_port)
+    try:
+        helpers.run_ddp(_noop_rank, world=1)
+    finally:
+        busy.close()
+    assert len(calls) == 2

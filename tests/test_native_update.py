@@ -126,3 +126,33 @@ def test_reset_refills_unobserved_state_in_place():
     mx.update(torch.tensor(3.0))
     mx.reset()
     assert float(mx.max_value) == float("-inf")  # non-zero defaults are restored too
+
+
+class _ShiftedConfmat(tm.MulticlassConfusionMatrix):
+    """A user subclass that preprocesses in its own update (the reference always runs it)."""
+
+    def update(self, preds, target):
+        super().update(preds, (target + 1) % self.num_classes)
+
+
+def test_subclass_update_is_not_bypassed_cpu():
+    m = _ShiftedConfmat(4)
+    assert "update" not in m.__dict__ or type(m.__dict__["update"]).__name__ != "NativeUpdate"
+    p, t = torch.randn(16, 4), torch.randint(0, 4, (16,))
+    m.update(p, t)
+    torch.testing.assert_close(m.compute(), tm.functional.multiclass_confusion_matrix(p, (t + 1) % 4, 4))
+    other = pickle.loads(pickle.dumps(m))
+    assert type(other.__dict__.get("update")).__name__ != "NativeUpdate"
+
+
+@pytest.mark.gpu
+def test_subclass_update_is_not_bypassed_gpu():
+    dev = torch.device("cuda", 0)
+    m = _ShiftedConfmat(6).to(dev)
+    assert type(m.update).__name__ != "NativeUpdate"
+    g = torch.Generator().manual_seed(3)
+    p, t = torch.randn(100, 6, generator=g), torch.randint(0, 6, (100,), generator=g)
+    m.update(p.to(dev), t.to(dev))
+    ref = tm.functional.multiclass_confusion_matrix(p, (t + 1) % 6, 6)
+    assert torch.equal(m.compute().cpu(), ref)
+    assert type(tm.MulticlassConfusionMatrix(6).to(dev).update).__name__ == "NativeUpdate"

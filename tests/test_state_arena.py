@@ -281,3 +281,72 @@ def test_cat_arena_per_step_compute_gpu():
         ref._computed = None
     buf, view = m.__dict__["_cat_arenas"]["preds"]
     assert buf.is_cuda and view is m.preds[0] and view.shape[0] == 12000 and buf.shape[0] >= 12000
+
+
+class _ViewCompute(Metric):
+    """compute() returns a VIEW of a SUM state (the case sys.getrefcount cannot see)."""
+
+    full_state_update = False
+
+    def __init__(self):
+        super().__init__()
+        self.add_state("a", torch.zeros(4), "sum")
+        self.add_state("b", torch.zeros(2), "sum")
+
+    def update(self, v):
+        self.a += v
+        self.b += v[:2]
+
+    def compute(self):
+        return self.a[:2]
+
+
+def test_forward_does_not_mutate_held_views():
+    """forward()'s in-place fold of the batch into the global SUM states must not change a previously returned
+    compute() value that aliases the state, nor a user-held view of it (the reference merges out of place)."""
+    m = _ViewCompute()
+    m.update(torch.ones(4))
+    v = m.compute()
+    assert v.tolist() == [1.0, 1.0]
+    m(torch.ones(4))
+    assert v.tolist() == [1.0, 1.0]
+    assert m.compute().tolist() == [2.0, 2.0]
+    held = m.a.view(2, 2)
+    m(torch.ones(4))
+    assert held.flatten().tolist() == [2.0, 2.0, 2.0, 2.0]
+    assert m.a.tolist() == [3.0] * 4
+    # nothing held any more: the fold goes back to in place (the global state keeps its packed storage)
+    del v, held
+    m._computed = None
+    ptr = m.a.untyped_storage().data_ptr()
+    m(torch.ones(4))
+    assert m.a.untyped_storage().data_ptr() == ptr and m.a.tolist() == [4.0] * 4
+
+
+@pytest.mark.parametrize("hand_out", ["attr", "compute_same_object", "state_dict", "metric_state", "view",
+                                      "collection_sibling"])
+def test_reset_never_zeroes_a_handed_out_state(hand_out):
+    """reset() refills a state in place only when nothing outside the metric can observe it; every path that hands a
+    state (or a view of it) out must keep its value across reset()."""
+    p, t = _data(3)
+    if hand_out == "collection_sibling":
+        coll = MetricCollection([tm.MulticlassPrecision(5, average=None), tm.MulticlassRecall(5, average=None)],
+                                compute_groups=True)
+        coll.update(p, t)
+        coll.compute()
+        m = coll["MulticlassPrecision"]
+        held = coll["MulticlassRecall"].tp
+    else:
+        m = _ViewCompute() if hand_out == "compute_same_object" else tm.MulticlassStatScores(5, average=None)
+        if hand_out == "compute_same_object":
+            m.compute = lambda: m.a  # returns the state object itself
+            m.update(torch.ones(4))
+            held = m.a
+        else:
+            m.persistent(True)
+            m.update(p, t)
+            held = {"attr": lambda: m.tp, "state_dict": lambda: m.state_dict(keep_vars=True)["tp"],
+                    "metric_state": lambda: m.metric_state["tp"], "view": lambda: m.tp[1:]}[hand_out]()
+    before = held.clone()
+    m.reset()
+    assert torch.equal(held, before)

@@ -148,7 +148,10 @@ class MulticlassConfusionMatrix(_ConfmatBase):
     def _install_native_update(self) -> None:
         """``update`` becomes ONE native call on ROCm (csrc/bindings/fastcall.cpp ``confmat_updater``): the shape /
         dtype checks, the ``_update_count`` / ``_computed`` bookkeeping and the kernel launch without a Python frame;
-        any other input goes through the Python ``update`` below."""
+        any other input goes through the Python ``update`` below.  A subclass that overrides ``update`` keeps its own
+        (the native call would bypass it)."""
+        if type(self).update is not MulticlassConfusionMatrix.update:
+            return
         fast = ops.native_updater("confmat", self.__dict__, self.__dict__["update"])
         if fast is not None:
             self.__dict__["update"] = fast

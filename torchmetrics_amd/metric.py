@@ -354,6 +354,16 @@ class Metric(Module, ABC):
         keeps the out-of-place merge, which the reference always does: S/metric.py:329-352).  Merged entries are
         handed to :meth:`_reduce_states` as already reduced."""
         pairs: List[Tuple[str, Tensor, Tensor]] = []
+        # storage -> the global state's own tensors on it (the states and their packed-arena base); any other tensor
+        # on that storage (a user view, a view returned by compute()) shows up in the storage's use count
+        views: Dict[int, set] = {}
+        for t in global_state.values():
+            if isinstance(t, Tensor) and t.layout == torch.strided:
+                own = views.setdefault(t.untyped_storage().data_ptr(), set())
+                own.add(id(t))
+                if t._base is not None:
+                    own.add(id(t._base))
+        t = own = None
         for attr in list(global_state):
             if self._reductions[attr] is not dim_zero_sum:
                 continue
@@ -363,11 +373,16 @@ class Metric(Module, ABC):
                     or local.requires_grad or glob.layout != torch.strided or glob.shape != local.shape
                     or glob.dtype != torch.promote_types(glob.dtype, local.dtype) or glob.device != local.device):
                 continue
-            # references: global_state's entry, this local, getrefcount's argument
+            # references: global_state's entry, this local, getrefcount's argument (catches the same tensor object
+            # held elsewhere); the storage use count catches views of it (+1: the temporary storage handle)
             if sys.getrefcount(glob) > 3:
                 continue
+            stor = glob.untyped_storage()
+            if torch._C._storage_Use_Count(stor._cdata) > 1 + len(views.get(stor.data_ptr(), ())):
+                continue
+            stor = None
             pairs.append((attr, glob, local))
-        glob = local = None
+        glob = local = stor = None
         if not pairs:
             return
         gspan = _arena.contiguous_span([g for _, g, _ in pairs]) if len(pairs) > 1 else None

@@ -42,7 +42,10 @@ DEFAULT_SLOT_BYTES = 256 * 1024
 
 
 def _enabled_by_env() -> bool:
-    return os.environ.get("TORCHMETRICS_AMD_ONESHOT", "1") not in ("0", "false", "False")
+    """Opt-in (``TORCHMETRICS_AMD_ONESHOT=1``): the path has run on one device with two processes, never across
+    distinct GPUs over xGMI, so the engine keeps RCCL for every bucket unless asked (a coherence or protocol issue on
+    a real xGMI mesh would otherwise show up as a long in-kernel wait on every multi-GPU sync)."""
+    return os.environ.get("TORCHMETRICS_AMD_ONESHOT", "0") not in ("0", "false", "False", "")
 
 
 def _resolve_group(group: Optional[Any]) -> Any:

@@ -55,6 +55,10 @@ void exact_match_update(const at::Tensor& preds, const at::Tensor& target, int64
 void group_stats_update(const at::Tensor& preds, const at::Tensor& target, const at::Tensor& groups, int64_t G,
                         double threshold, int64_t ignore_index, bool has_ignore, at::Tensor ws, at::Tensor notprob,
                         at::Tensor tp, at::Tensor fp, at::Tensor tn, at::Tensor fn);
+void mc_stats_forward(at::Tensor ws, int64_t num_classes, bool micro, at::Tensor tp, at::Tensor fp, at::Tensor tn,
+                      at::Tensor fn, int64_t kind, int64_t average, double beta, at::Tensor out);
+void bin_stats_forward(at::Tensor ws, at::Tensor not_prob, at::Tensor tp, at::Tensor fp, at::Tensor tn, at::Tensor fn,
+                       int64_t kind, int64_t average, double beta, at::Tensor out);
 }  // namespace tm_amd
 
 namespace {
@@ -246,6 +250,8 @@ PyMethodDef kMethods[] = {
     TM_FAST("agg_update", tm_amd::agg_update),
     TM_FAST("exact_match_update", tm_amd::exact_match_update),
     TM_FAST("group_stats_update", tm_amd::group_stats_update),
+    TM_FAST("mc_stats_forward", tm_amd::mc_stats_forward),
+    TM_FAST("bin_stats_forward", tm_amd::bin_stats_forward),
     TM_FAST("arg_probe", arg_probe),
     {nullptr, nullptr, 0, nullptr},
 };
@@ -266,13 +272,19 @@ PyObject* g_k_classes = nullptr;
 PyObject* g_k_ignore = nullptr;
 PyObject* g_k_validate = nullptr;
 
+struct NativeUpdate;
+// 1 = handled (*result: a new reference), 0 = not handled (take the Python path), -1 = Python error set
+using FastFn = int (*)(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** result);
+
 struct NativeUpdate {
   PyObject_HEAD
   vectorcallfunc vectorcall;
   PyObject* state;     // the metric's __dict__
-  PyObject* fallback;  // the Python update (Metric._wrap_update wrapper)
+  PyObject* fallback;  // the Python update (Metric._wrap_update wrapper) / forward (bound Metric.forward)
   at::Tensor* sink;    // flag word for validate_args=False (kernels always have somewhere to report)
   int64_t calls;       // fast-path calls (tests / benchmarks read it)
+  FastFn fast;         // the native body
+  int stat_kind;       // NativeForward of the stat-score family: the score (cbody::StatKind)
 };
 
 inline const at::Tensor* tensor_item(PyObject* dict, PyObject* key) {
@@ -282,7 +294,7 @@ inline const at::Tensor* tensor_item(PyObject* dict, PyObject* key) {
 }
 
 // 1 = done, 0 = not handled (take the Python path), -1 = Python error set
-int confmat_fast(NativeUpdate* self, PyObject* a, PyObject* b) {
+int confmat_fast(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** result) {
   if (!THPVariable_Check(a) || !THPVariable_Check(b)) return 0;
   const at::Tensor& p = THPVariable_Unpack(a);
   const at::Tensor& t = THPVariable_Unpack(b);
@@ -341,6 +353,8 @@ int confmat_fast(NativeUpdate* self, PyObject* a, PyObject* b) {
   Py_DECREF(n1);
   if (rc != 0 || PyDict_SetItem(st, g_k_computed, Py_None) != 0) return -1;
   ++self->calls;
+  Py_INCREF(Py_None);
+  *result = Py_None;
   return 1;
 }
 
@@ -348,8 +362,9 @@ PyObject* native_update_vectorcall(PyObject* o, PyObject* const* args, size_t na
   auto* self = reinterpret_cast<NativeUpdate*>(o);
   const Py_ssize_t nargs = PyVectorcall_NARGS(nargsf);
   if (nargs == 2 && (kwnames == nullptr || PyTuple_GET_SIZE(kwnames) == 0)) {
-    const int r = confmat_fast(self, args[0], args[1]);
-    if (r == 1) Py_RETURN_NONE;
+    PyObject* result = nullptr;
+    const int r = self->fast(self, args[0], args[1], &result);
+    if (r == 1) return result;
     if (r < 0) return nullptr;
   }
   return PyObject_Vectorcall(self->fallback, args, nargsf, kwnames);
@@ -417,11 +432,360 @@ PyObject* make_confmat_updater(PyObject*, PyObject* const* args, Py_ssize_t narg
   self->fallback = args[1];
   self->sink = nullptr;
   self->calls = 0;
+  self->fast = confmat_fast;
+  self->stat_kind = 0;
+  PyObject_GC_Track(reinterpret_cast<PyObject*>(self));
+  return reinterpret_cast<PyObject*>(self);
+}
+
+// ----------------------------------------------------------------------------------------- native metric forward
+// ``metric(preds, target)`` for the confusion-matrix and stat-score families as ONE native callable (installed as the
+// instance's ``forward``; nn.Module.__call__ dispatches to it).  The reference forward (S/metric.py:275-306,353-391)
+// saves the global state, resets, updates, computes the batch value and merges state by state; here it is
+//   confmat:     zeros(C, C) -> mc_update into it -> global += batch; the batch matrix is the value,
+//   stat scores: the update kernel into the per-metric workspace -> ONE fused launch (classification/forward.hip)
+//                that folds the batch counts into the global states and scores the batch with compute()'s own body,
+// plus the bookkeeping of Metric.forward (``_update_count``, ``_computed``, ``_forward_cache``).  Taken only when the
+// result is the reference's: no dist_sync_on_step, not synced, no compute_on_cpu, and global states that nothing
+// outside the metric can observe (the reference merges out of place, so a held state / view must not change: the
+// same Python-refcount + storage-use-count test as Metric._merge_sums_in_place).  Everything else -> Metric.forward.
+// Deviation (as for update on ROCm): value-range errors of the batch surface at the next compute(), not in forward.
+PyObject* g_k_tp = nullptr;
+PyObject* g_k_fp = nullptr;
+PyObject* g_k_tn = nullptr;
+PyObject* g_k_fn = nullptr;
+PyObject* g_k_wsobj = nullptr;
+PyObject* g_k_ws = nullptr;
+PyObject* g_k_notprob = nullptr;
+PyObject* g_k_topk = nullptr;
+PyObject* g_k_mdavg = nullptr;
+PyObject* g_k_average = nullptr;
+PyObject* g_k_micro = nullptr;
+PyObject* g_k_labels = nullptr;
+PyObject* g_k_threshold = nullptr;
+PyObject* g_k_beta = nullptr;
+PyObject* g_k_synced = nullptr;
+PyObject* g_k_dsos = nullptr;
+PyObject* g_k_fcache = nullptr;
+PyObject* g_k_defaults = nullptr;
+PyObject* g_k_normalize = nullptr;
+
+enum FwdKind : int { kFwdConfmat = 0, kFwdMulticlass = 1, kFwdBinary = 2, kFwdMultilabel = 3 };
+
+// the batch-mode preconditions of Metric.forward's reduce-state path
+bool forward_allowed(PyObject* st) {
+  return PyDict_GetItem(st, g_k_synced) == Py_False && PyDict_GetItem(st, g_k_dsos) == Py_False &&
+         PyDict_GetItem(st, g_k_cpu) == Py_False;
+}
+
+// No reference to the state tensors outside the metric: each state object is held by the metric's __dict__ only, and
+// its storage by nothing but the metric's own states on it and their view base (a packed arena's buffer).
+bool states_unobserved(PyObject* st, std::initializer_list<PyObject*> keys) {
+  PyObject* defaults = PyDict_GetItem(st, g_k_defaults);
+  if (defaults == nullptr || !PyDict_Check(defaults)) return false;
+  for (PyObject* key : keys) {
+    PyObject* o = PyDict_GetItem(st, key);
+    if (o == nullptr || !THPVariable_Check(o) || Py_REFCNT(o) != 1) return false;
+    const at::Tensor& t = THPVariable_Unpack(o);
+    if (!t.has_storage()) return false;
+    const c10::StorageImpl* si = t.storage().unsafeGetStorageImpl();
+    const c10::TensorImpl* impls[16];
+    size_t n = 0;
+    auto add = [&](const c10::TensorImpl* p) {
+      for (size_t i = 0; i < n; ++i)
+        if (impls[i] == p) return true;
+      if (n == 16) return false;
+      impls[n++] = p;
+      return true;
+    };
+    PyObject *k, *v;
+    Py_ssize_t pos = 0;
+    while (PyDict_Next(defaults, &pos, &k, &v)) {
+      PyObject* so = PyDict_GetItem(st, k);
+      if (so == nullptr || !THPVariable_Check(so)) continue;
+      const at::Tensor& s = THPVariable_Unpack(so);
+      if (!s.has_storage() || s.storage().unsafeGetStorageImpl() != si) continue;
+      if (!add(s.unsafeGetTensorImpl())) return false;
+      if (s.is_view() && !add(s._base().unsafeGetTensorImpl())) return false;
+    }
+    if (static_cast<size_t>(t.storage().use_count()) > n) return false;
+  }
+  return true;
+}
+
+// the int32 flag word the kernels report into: the metric's validation word (validate_args) or a private sink
+const at::Tensor* forward_flag(NativeUpdate* self, PyObject* st, int dev) {
+  PyObject* vo = PyDict_GetItem(st, g_k_validate);
+  if (vo == nullptr) return nullptr;
+  if (vo == Py_True) {
+    const at::Tensor* flag = tensor_item(st, g_k_err);  // created by the first (Python) update on this device
+    if (flag == nullptr || !flag->is_cuda() || flag->get_device() != dev || flag->scalar_type() != at::kInt)
+      return nullptr;
+    return flag;
+  }
+  if (self->sink == nullptr || self->sink->get_device() != dev) {
+    delete self->sink;
+    self->sink = new at::Tensor(at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev)));
+  }
+  return self->sink;
+}
+
+bool read_ignore(PyObject* st, long long& ignore, bool& has_ignore) {
+  PyObject* io = PyDict_GetItem(st, g_k_ignore);
+  if (io == nullptr) return false;
+  has_ignore = io != Py_None;
+  ignore = 0;
+  if (has_ignore) {
+    if (!PyLong_CheckExact(io)) return false;
+    ignore = PyLong_AsLongLong(io);
+  }
+  return true;
+}
+
+// average string -> cbody::StatAvg (micro 0, macro 1, weighted 2, none 3); -1 = not a fused average
+int read_average(PyObject* st) {
+  PyObject* a = PyDict_GetItem(st, g_k_average);
+  if (a == nullptr) return -1;
+  if (a == Py_None) return 3;
+  if (!PyUnicode_Check(a)) return -1;
+  if (PyUnicode_CompareWithASCIIString(a, "micro") == 0) return 0;
+  if (PyUnicode_CompareWithASCIIString(a, "macro") == 0) return 1;
+  if (PyUnicode_CompareWithASCIIString(a, "weighted") == 0) return 2;
+  if (PyUnicode_CompareWithASCIIString(a, "none") == 0) return 3;
+  return -1;
+}
+
+const at::Tensor* state_tensor(PyObject* st, PyObject* key, int dev, long long numel) {
+  const at::Tensor* t = tensor_item(st, key);
+  if (t == nullptr || !t->is_cuda() || t->get_device() != dev || t->scalar_type() != at::kLong ||
+      !t->is_contiguous() || t->numel() != numel)
+    return nullptr;
+  return t;
+}
+
+// the metric's _StatWorkspace buffers (created by its first Python update)
+bool workspace(PyObject* st, int dev, long long numel, at::Tensor& ws, at::Tensor* not_prob) {
+  PyObject* wo = PyDict_GetItem(st, g_k_wsobj);
+  if (wo == nullptr) return false;
+  PyObject* w = PyObject_GetAttr(wo, g_k_ws);
+  if (w == nullptr) {
+    PyErr_Clear();
+    return false;
+  }
+  bool ok = THPVariable_Check(w);
+  if (ok) {
+    ws = THPVariable_Unpack(w);
+    ok = ws.is_cuda() && ws.get_device() == dev && ws.scalar_type() == at::kLong && ws.is_contiguous() &&
+         ws.numel() == numel;
+  }
+  Py_DECREF(w);
+  if (ok && not_prob != nullptr) {
+    PyObject* np = PyObject_GetAttr(wo, g_k_notprob);
+    if (np == nullptr) {
+      PyErr_Clear();
+      return false;
+    }
+    ok = THPVariable_Check(np);
+    if (ok) {
+      *not_prob = THPVariable_Unpack(np);
+      ok = not_prob->is_cuda() && not_prob->get_device() == dev && not_prob->scalar_type() == at::kInt;
+    }
+    Py_DECREF(np);
+  }
+  return ok;
+}
+
+int forward_bookkeeping(NativeUpdate* self, PyObject* st, const at::Tensor& value, PyObject** result) {
+  PyObject* cnt = PyDict_GetItem(st, g_k_count);
+  if (cnt == nullptr || !PyLong_CheckExact(cnt)) return -1;
+  const long long n = PyLong_AsLongLong(cnt);
+  PyObject* out = THPVariable_Wrap(value);
+  if (out == nullptr) return -1;
+  PyObject* n1 = PyLong_FromLongLong(n + 1);
+  if (n1 == nullptr || PyDict_SetItem(st, g_k_count, n1) != 0 || PyDict_SetItem(st, g_k_fcache, out) != 0) {
+    Py_XDECREF(n1);
+    Py_DECREF(out);
+    return -1;
+  }
+  Py_DECREF(n1);
+  ++self->calls;
+  *result = out;
+  return 1;
+}
+
+bool float_preds(const at::Tensor& p) {
+  const auto d = p.scalar_type();
+  return d == at::kBFloat16 || d == at::kHalf || d == at::kFloat;
+}
+
+bool int_target(const at::Tensor& t) {
+  const auto d = t.scalar_type();
+  return d == at::kLong || d == at::kInt;
+}
+
+int confmat_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** result) {
+  if (!THPVariable_Check(a) || !THPVariable_Check(b)) return 0;
+  const at::Tensor& p = THPVariable_Unpack(a);
+  const at::Tensor& t = THPVariable_Unpack(b);
+  if (!p.is_cuda() || !t.is_cuda() || !float_preds(p) || !int_target(t)) return 0;
+  PyObject* st = self->state;
+  if (!forward_allowed(st) || PyDict_GetItem(st, g_k_normalize) != Py_None) return 0;
+  PyObject* co = PyDict_GetItem(st, g_k_classes);
+  if (co == nullptr || !PyLong_CheckExact(co)) return 0;
+  const long long C = PyLong_AsLongLong(co);
+  if (p.dim() != 2 || t.dim() != 1 || p.size(1) != C || p.size(0) != t.size(0) || p.size(0) == 0) return 0;
+  if (!p.is_contiguous() || !t.is_contiguous()) return 0;
+  const int dev = p.get_device();
+  if (t.get_device() != dev) return 0;
+  // forward() clears the cached compute() value first (a held compute() result of a confusion matrix IS the state)
+  if (PyDict_SetItem(st, g_k_computed, Py_None) != 0) return -1;
+  const at::Tensor* cm = state_tensor(st, g_k_confmat, dev, C * C);
+  if (cm == nullptr || !states_unobserved(st, {g_k_confmat})) return 0;
+  const at::Tensor* flag = forward_flag(self, st, dev);
+  long long ignore;
+  bool has_ignore;
+  if (flag == nullptr || !read_ignore(st, ignore, has_ignore)) return 0;
+  at::Tensor batch;
+  try {
+    batch = at::zeros({C, C}, cm->options());
+    tm_amd::mc_update(p, t, batch, *flag, C, ignore, has_ignore, 0, false);
+    cm->add_(batch);
+  } catch (const c10::Error& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what_without_backtrace());
+    return -1;
+  }
+  return forward_bookkeeping(self, st, batch, result);
+}
+
+int stats_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** result, int fkind) {
+  if (!THPVariable_Check(a) || !THPVariable_Check(b)) return 0;
+  const at::Tensor& p = THPVariable_Unpack(a);
+  const at::Tensor& t = THPVariable_Unpack(b);
+  if (!p.is_cuda() || !t.is_cuda() || !float_preds(p) || !int_target(t)) return 0;
+  if (!p.is_contiguous() || !t.is_contiguous() || p.numel() == 0) return 0;
+  const int dev = p.get_device();
+  if (t.get_device() != dev) return 0;
+  PyObject* st = self->state;
+  if (!forward_allowed(st)) return 0;
+  PyObject* md = PyDict_GetItem(st, g_k_mdavg);
+  if (md == nullptr || !PyUnicode_Check(md) || PyUnicode_CompareWithASCIIString(md, "global") != 0) return 0;
+  double beta = 1.0;
+  if (self->stat_kind == 5) {
+    PyObject* bo = PyDict_GetItem(st, g_k_beta);
+    if (bo == nullptr || !PyFloat_Check(bo) && !PyLong_Check(bo)) return 0;
+    beta = PyFloat_AsDouble(bo);
+  }
+  long long ignore;
+  bool has_ignore;
+  if (!read_ignore(st, ignore, has_ignore)) return 0;
+  long long size;  // classes / labels
+  int avg;
+  bool micro = false;
+  if (fkind == kFwdMulticlass) {
+    PyObject* co = PyDict_GetItem(st, g_k_classes);
+    PyObject* ko = PyDict_GetItem(st, g_k_topk);
+    if (co == nullptr || !PyLong_CheckExact(co) || ko == nullptr || !PyLong_CheckExact(ko)) return 0;
+    if (PyLong_AsLongLong(ko) != 1) return 0;
+    size = PyLong_AsLongLong(co);
+    if (p.dim() != 2 || t.dim() != 1 || p.size(1) != size || p.size(0) != t.size(0)) return 0;
+    micro = PyDict_GetItem(st, g_k_micro) == Py_True;
+    avg = micro ? 0 : read_average(st);
+  } else if (fkind == kFwdBinary) {
+    size = 1;
+    if (p.dim() != 1 || t.dim() != 1 || p.size(0) != t.size(0)) return 0;
+    avg = 0;  // the binary score = the micro body with the binary (multilabel) formula over one label
+  } else {
+    PyObject* lo = PyDict_GetItem(st, g_k_labels);
+    if (lo == nullptr || !PyLong_CheckExact(lo)) return 0;
+    size = PyLong_AsLongLong(lo);
+    if (p.dim() != 2 || t.dim() != 2 || p.size(1) != size || p.sizes() != t.sizes()) return 0;
+    avg = read_average(st);
+  }
+  if (avg < 0) return 0;
+  double threshold = 0.5;
+  if (fkind != kFwdMulticlass) {
+    PyObject* th = PyDict_GetItem(st, g_k_threshold);
+    if (th == nullptr || !(PyFloat_Check(th) || PyLong_Check(th))) return 0;
+    threshold = PyFloat_AsDouble(th);
+  }
+  if (PyDict_SetItem(st, g_k_computed, Py_None) != 0) return -1;
+  const long long ssize = micro ? 1 : size;
+  const at::Tensor* tp = state_tensor(st, g_k_tp, dev, ssize);
+  const at::Tensor* fp = state_tensor(st, g_k_fp, dev, ssize);
+  const at::Tensor* tn = state_tensor(st, g_k_tn, dev, ssize);
+  const at::Tensor* fn = state_tensor(st, g_k_fn, dev, ssize);
+  if (tp == nullptr || fp == nullptr || tn == nullptr || fn == nullptr) return 0;
+  if (!states_unobserved(st, {g_k_tp, g_k_fp, g_k_tn, g_k_fn})) return 0;
+  const at::Tensor* flag = forward_flag(self, st, dev);
+  if (flag == nullptr) return 0;
+  at::Tensor ws, not_prob;
+  const bool mc = fkind == kFwdMulticlass;
+  if (!workspace(st, dev, mc ? 3 * size + 1 : 7 * size, ws, mc ? nullptr : &not_prob)) return 0;
+  const bool per_class = avg == 3 && !micro;
+  at::Tensor out;
+  try {
+    out = at::empty({per_class ? size : 1}, p.options().dtype(at::kFloat));
+    if (mc) {
+      tm_amd::mc_update(p, t, ws, *flag, size, ignore, has_ignore, 1, false);
+      tm_amd::mc_stats_forward(ws, size, micro, *tp, *fp, *tn, *fn, self->stat_kind, avg, beta, out);
+    } else {
+      tm_amd::bin_update(p, t, ws, *flag, not_prob, size, threshold, ignore, has_ignore, false, true);
+      tm_amd::bin_stats_forward(ws, not_prob, *tp, *fp, *tn, *fn, self->stat_kind, avg, beta, out);
+    }
+  } catch (const c10::Error& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what_without_backtrace());
+    return -1;
+  }
+  // compute() squeezes one-element values
+  return forward_bookkeeping(self, st, out.numel() == 1 ? out.view({}) : out, result);
+}
+
+int mc_stats_forward_fast(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** r) {
+  return stats_forward(self, a, b, r, kFwdMulticlass);
+}
+int bin_stats_forward_fast(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** r) {
+  return stats_forward(self, a, b, r, kFwdBinary);
+}
+int ml_stats_forward_fast(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** r) {
+  return stats_forward(self, a, b, r, kFwdMultilabel);
+}
+
+PyTypeObject NativeForwardType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+// forward_native(kind, state_dict, fallback, stat_kind) -> callable;
+// kind: 0 confusion matrix, 1 multiclass / 2 binary / 3 multilabel stat scores; stat_kind: cbody::StatKind
+PyObject* make_forward(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 4 || !PyLong_Check(args[0]) || !PyDict_Check(args[1]) || !PyCallable_Check(args[2]) ||
+      !PyLong_Check(args[3])) {
+    PyErr_SetString(PyExc_TypeError, "forward_native(kind: int, state: dict, fallback: callable, stat_kind: int)");
+    return nullptr;
+  }
+  const long kind = PyLong_AsLong(args[0]);
+  const long sk = PyLong_AsLong(args[3]);
+  if (kind < 0 || kind > 3 || sk < 0 || sk > 5) {
+    PyErr_SetString(PyExc_ValueError, "forward_native: bad kind / stat_kind");
+    return nullptr;
+  }
+  auto* self = PyObject_GC_New(NativeUpdate, &NativeForwardType);
+  if (self == nullptr) return nullptr;
+  self->vectorcall = native_update_vectorcall;
+  Py_INCREF(args[1]);
+  self->state = args[1];
+  Py_INCREF(args[2]);
+  self->fallback = args[2];
+  self->sink = nullptr;
+  self->calls = 0;
+  static const FastFn kFns[] = {confmat_forward, mc_stats_forward_fast, bin_stats_forward_fast,
+                                ml_stats_forward_fast};
+  self->fast = kFns[kind];
+  self->stat_kind = static_cast<int>(sk);
   PyObject_GC_Track(reinterpret_cast<PyObject*>(self));
   return reinterpret_cast<PyObject*>(self);
 }
 
 PyMethodDef kFactoryMethods[] = {
+    {"forward_native", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&make_forward)), METH_FASTCALL,
+     "native Metric.forward of the confusion-matrix / stat-score families bound to a metric's __dict__"},
     {"confmat_updater", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&make_confmat_updater)),
      METH_FASTCALL, "native MulticlassConfusionMatrix.update bound to a metric's __dict__"},
     {nullptr, nullptr, 0, nullptr},
@@ -443,6 +807,17 @@ PyMODINIT_FUNC PyInit__fastcall() {
   NativeUpdateType.tp_getset = kNativeUpdateGetSet;
   NativeUpdateType.tp_doc = "native metric update (see csrc/bindings/fastcall.cpp)";
   if (PyType_Ready(&NativeUpdateType) < 0) return nullptr;
+  NativeForwardType.tp_name = "torchmetrics_amd._C._fastcall.NativeForward";
+  NativeForwardType.tp_basicsize = sizeof(NativeUpdate);
+  NativeForwardType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC | Py_TPFLAGS_HAVE_VECTORCALL;
+  NativeForwardType.tp_vectorcall_offset = offsetof(NativeUpdate, vectorcall);
+  NativeForwardType.tp_call = PyVectorcall_Call;
+  NativeForwardType.tp_traverse = native_update_traverse;
+  NativeForwardType.tp_clear = native_update_clear;
+  NativeForwardType.tp_dealloc = native_update_dealloc;
+  NativeForwardType.tp_getset = kNativeUpdateGetSet;
+  NativeForwardType.tp_doc = "native metric forward (see csrc/bindings/fastcall.cpp)";
+  if (PyType_Ready(&NativeForwardType) < 0) return nullptr;
   g_k_confmat = PyUnicode_InternFromString("confmat");
   g_k_err = PyUnicode_InternFromString("_device_errors");
   g_k_count = PyUnicode_InternFromString("_update_count");
@@ -451,6 +826,25 @@ PyMODINIT_FUNC PyInit__fastcall() {
   g_k_classes = PyUnicode_InternFromString("num_classes");
   g_k_ignore = PyUnicode_InternFromString("ignore_index");
   g_k_validate = PyUnicode_InternFromString("validate_args");
+  g_k_tp = PyUnicode_InternFromString("tp");
+  g_k_fp = PyUnicode_InternFromString("fp");
+  g_k_tn = PyUnicode_InternFromString("tn");
+  g_k_fn = PyUnicode_InternFromString("fn");
+  g_k_wsobj = PyUnicode_InternFromString("_ws");
+  g_k_ws = PyUnicode_InternFromString("ws");
+  g_k_notprob = PyUnicode_InternFromString("not_prob");
+  g_k_topk = PyUnicode_InternFromString("top_k");
+  g_k_mdavg = PyUnicode_InternFromString("multidim_average");
+  g_k_average = PyUnicode_InternFromString("average");
+  g_k_micro = PyUnicode_InternFromString("_micro");
+  g_k_labels = PyUnicode_InternFromString("num_labels");
+  g_k_threshold = PyUnicode_InternFromString("threshold");
+  g_k_beta = PyUnicode_InternFromString("beta");
+  g_k_synced = PyUnicode_InternFromString("_is_synced");
+  g_k_dsos = PyUnicode_InternFromString("dist_sync_on_step");
+  g_k_fcache = PyUnicode_InternFromString("_forward_cache");
+  g_k_defaults = PyUnicode_InternFromString("_defaults");
+  g_k_normalize = PyUnicode_InternFromString("normalize");
   PyObject* m = PyModule_Create(&kModule);
   if (m == nullptr) return nullptr;
   if (PyModule_AddFunctions(m, kFactoryMethods) < 0) return nullptr;

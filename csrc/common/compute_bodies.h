@@ -44,54 +44,74 @@ __device__ __forceinline__ float class_score(int kind, float tp, float fp, float
   }
 }
 
-// one row of the [R, C] states; red: >= 4 doubles of LDS
-__device__ __forceinline__ void stat_reduce_row(const int64_t* __restrict__ tp, const int64_t* __restrict__ fp,
-                                                const int64_t* __restrict__ tn, const int64_t* __restrict__ fn, int C,
-                                                int kind, int avg, bool multilabel, float beta2,
-                                                float* __restrict__ out, long long row, double* red) {
-  const int64_t* a = tp + row * C;
-  const int64_t* b = fp + row * C;
-  const int64_t* c = tn + row * C;
-  const int64_t* d = fn + row * C;
+// Reduction of C per-class counts to the score of ``avg``.  ``get(k, tp, fp, tn, fn)`` loads class k's counts (a state
+// row, or a forward()'s batch counts straight out of the update workspace); out: [C] (none) or out[0].
+// red: >= 4 doubles of LDS.  Every caller uses this one body, so every path gives bit-identical scores.
+template <typename Get>
+__device__ __forceinline__ void stat_reduce_body(Get get, int C, int kind, int avg, bool multilabel, float beta2,
+                                                 float* __restrict__ out, double* red) {
   if (avg == kNone) {
-    for (int k = threadIdx.x; k < C; k += kThreads)
-      out[row * C + k] = class_score(kind, static_cast<float>(a[k]), static_cast<float>(b[k]), static_cast<float>(c[k]),
-                                     static_cast<float>(d[k]), multilabel, beta2);
+    for (int k = threadIdx.x; k < C; k += kThreads) {
+      long long a, b, c, d;
+      get(k, a, b, c, d);
+      out[k] = class_score(kind, static_cast<float>(a), static_cast<float>(b), static_cast<float>(c),
+                           static_cast<float>(d), multilabel, beta2);
+    }
     return;
   }
   if (avg == kMicro) {
     double s[4] = {0, 0, 0, 0};
     for (int k = threadIdx.x; k < C; k += kThreads) {
-      s[0] += static_cast<double>(a[k]);
-      s[1] += static_cast<double>(b[k]);
-      s[2] += static_cast<double>(c[k]);
-      s[3] += static_cast<double>(d[k]);
+      long long a, b, c, d;
+      get(k, a, b, c, d);
+      s[0] += static_cast<double>(a);
+      s[1] += static_cast<double>(b);
+      s[2] += static_cast<double>(c);
+      s[3] += static_cast<double>(d);
     }
     for (int i = 0; i < 4; ++i) s[i] = block_sum(s[i], red);
     if (threadIdx.x == 0) {
       // micro accuracy / hamming of a multilabel problem use the binary formula, everything else the class formula
       const bool binary_form = multilabel && (kind == kAccuracy || kind == kHamming);
-      out[row] = class_score(kind, static_cast<float>(s[0]), static_cast<float>(s[1]), static_cast<float>(s[2]),
-                             static_cast<float>(s[3]), binary_form, beta2);
+      out[0] = class_score(kind, static_cast<float>(s[0]), static_cast<float>(s[1]), static_cast<float>(s[2]),
+                           static_cast<float>(s[3]), binary_form, beta2);
     }
     return;
   }
   double num = 0.0, den = 0.0;
   for (int k = threadIdx.x; k < C; k += kThreads) {
-    const float ftp = static_cast<float>(a[k]), ffp = static_cast<float>(b[k]), ftn = static_cast<float>(c[k]),
-                ffn = static_cast<float>(d[k]);
+    long long a, b, c, d;
+    get(k, a, b, c, d);
+    const float ftp = static_cast<float>(a), ffp = static_cast<float>(b), ftn = static_cast<float>(c),
+                ffn = static_cast<float>(d);
     const float sc = class_score(kind, ftp, ffp, ftn, ffn, multilabel, beta2);
     float w;
     if (avg == kWeighted)
       w = ftp + ffn;
     else
-      w = (!multilabel && a[k] + b[k] + d[k] == 0) ? 0.f : 1.f;
+      w = (!multilabel && a + b + d == 0) ? 0.f : 1.f;
     num += static_cast<double>(w * sc);
     den += static_cast<double>(w);
   }
   num = block_sum(num, red);
   den = block_sum(den, red);
-  if (threadIdx.x == 0) out[row] = static_cast<float>(num / (den == 0.0 ? 1.0 : den));
+  if (threadIdx.x == 0) out[0] = static_cast<float>(num / (den == 0.0 ? 1.0 : den));
+}
+
+// one row of the [R, C] states; red: >= 4 doubles of LDS
+__device__ __forceinline__ void stat_reduce_row(const int64_t* __restrict__ tp, const int64_t* __restrict__ fp,
+                                                const int64_t* __restrict__ tn, const int64_t* __restrict__ fn, int C,
+                                                int kind, int avg, bool multilabel, float beta2,
+                                                float* __restrict__ out, long long row, double* red) {
+  const long long o = row * C;
+  stat_reduce_body(
+      [&](int k, long long& a, long long& b, long long& c, long long& d) {
+        a = tp[o + k];
+        b = fp[o + k];
+        c = tn[o + k];
+        d = fn[o + k];
+      },
+      C, kind, avg, multilabel, beta2, avg == kNone ? out + o : out + row, red);
 }
 
 // ---------------------------------------------------------------------------------- confusion-matrix family

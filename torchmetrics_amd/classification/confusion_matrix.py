@@ -144,6 +144,18 @@ class MulticlassConfusionMatrix(_ConfmatBase):
         self.validate_args = validate_args
         self.add_state("confmat", torch.zeros(num_classes, num_classes, dtype=torch.long), dist_reduce_fx="sum")
         self._install_native_update()
+        self._install_native_forward()
+
+    def _install_native_forward(self) -> None:
+        """ROCm: ``forward`` = zeros(C, C) + the update kernel into it + one add into the global matrix, driven from C++
+        (csrc/bindings/fastcall.cpp NativeForward); only for this class's own update / compute / forward / reset."""
+        cls = type(self)
+        if (cls.update is not MulticlassConfusionMatrix.update or cls.compute is not MulticlassConfusionMatrix.compute
+                or cls.forward is not Metric.forward or cls.reset is not Metric.reset):
+            return
+        fast = ops.native_forward(ops.FWD_CONFMAT, self.__dict__, Metric.forward.__get__(self, cls))
+        if fast is not None:
+            self.__dict__["forward"] = fast
 
     def _install_native_update(self) -> None:
         """``update`` becomes ONE native call on ROCm (csrc/bindings/fastcall.cpp ``confmat_updater``): the shape /

@@ -44,6 +44,8 @@ class BinaryFBetaScore(BinaryStatScores):
         self.validate_args = validate_args
         self.beta = beta
 
+    _stat_kind = "fbeta"  # compute() is the fused `_stat_reduce` score: native forward applies
+
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()
         return _stat_reduce("fbeta", tp, fp, tn, fn, "binary", self.multidim_average, beta=self.beta)
@@ -78,6 +80,8 @@ class MulticlassFBetaScore(MulticlassStatScores):
         if validate_args:
             _check_beta(beta)
         self.beta = beta
+
+    _stat_kind = "fbeta"  # compute() is the fused `_stat_reduce` score: native forward applies
 
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()
@@ -115,6 +119,8 @@ class MultilabelFBetaScore(MultilabelStatScores):
             _check_beta(beta)
         self.beta = beta
 
+    _stat_kind = "fbeta"  # compute() is the fused `_stat_reduce` score: native forward applies
+
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()
         return _stat_reduce("fbeta", tp, fp, tn, fn, self.average, self.multidim_average, multilabel=True, beta=self.beta)
@@ -141,6 +147,8 @@ class BinaryF1Score(BinaryFBetaScore):
         **kwargs: Any,
     ) -> None:
         super().__init__(1.0, threshold, multidim_average, ignore_index, validate_args, **kwargs)
+
+    _stat_kind = "fbeta"  # compute() is the fused `_stat_reduce` score: native forward applies
 
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()
@@ -173,6 +181,8 @@ class MulticlassF1Score(MulticlassFBetaScore):
         super().__init__(1.0, num_classes, top_k=top_k, average=average, multidim_average=multidim_average,
                          ignore_index=ignore_index, validate_args=validate_args, **kwargs)
 
+    _stat_kind = "fbeta"  # compute() is the fused `_stat_reduce` score: native forward applies
+
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()
         return _stat_reduce("fbeta", tp, fp, tn, fn, self.average, self.multidim_average, beta=self.beta)
@@ -202,6 +212,8 @@ class MultilabelF1Score(MultilabelFBetaScore):
         **kwargs: Any,
     ) -> None:
         super().__init__(1.0, num_labels, threshold, average, multidim_average, ignore_index, validate_args, **kwargs)
+
+    _stat_kind = "fbeta"  # compute() is the fused `_stat_reduce` score: native forward applies
 
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()

@@ -25,6 +25,8 @@ class BinaryPrecision(BinaryStatScores):
     plot_lower_bound: float = 0.0
     plot_upper_bound: float = 1.0
 
+    _stat_kind = "precision"  # compute() is the fused `_stat_reduce` score: native forward applies
+
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()
         return _stat_reduce("precision", tp, fp, tn, fn, "binary", self.multidim_average)
@@ -43,6 +45,8 @@ class MulticlassPrecision(MulticlassStatScores):
     plot_upper_bound: float = 1.0
     plot_legend_name: str = "Class"
 
+    _stat_kind = "precision"  # compute() is the fused `_stat_reduce` score: native forward applies
+
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()
         return _stat_reduce("precision", tp, fp, tn, fn, self.average, self.multidim_average)
@@ -60,6 +64,8 @@ class MultilabelPrecision(MultilabelStatScores):
     plot_lower_bound: float = 0.0
     plot_upper_bound: float = 1.0
     plot_legend_name: str = "Label"
+
+    _stat_kind = "precision"  # compute() is the fused `_stat_reduce` score: native forward applies
 
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()
@@ -111,6 +117,8 @@ class BinaryRecall(BinaryStatScores):
     plot_lower_bound: float = 0.0
     plot_upper_bound: float = 1.0
 
+    _stat_kind = "recall"  # compute() is the fused `_stat_reduce` score: native forward applies
+
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()
         return _stat_reduce("recall", tp, fp, tn, fn, "binary", self.multidim_average)
@@ -129,6 +137,8 @@ class MulticlassRecall(MulticlassStatScores):
     plot_upper_bound: float = 1.0
     plot_legend_name: str = "Class"
 
+    _stat_kind = "recall"  # compute() is the fused `_stat_reduce` score: native forward applies
+
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()
         return _stat_reduce("recall", tp, fp, tn, fn, self.average, self.multidim_average)
@@ -146,6 +156,8 @@ class MultilabelRecall(MultilabelStatScores):
     plot_lower_bound: float = 0.0
     plot_upper_bound: float = 1.0
     plot_legend_name: str = "Label"
+
+    _stat_kind = "recall"  # compute() is the fused `_stat_reduce` score: native forward applies
 
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()

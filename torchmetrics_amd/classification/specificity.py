@@ -25,6 +25,8 @@ class BinarySpecificity(BinaryStatScores):
     plot_lower_bound: float = 0.0
     plot_upper_bound: float = 1.0
 
+    _stat_kind = "specificity"  # compute() is the fused `_stat_reduce` score: native forward applies
+
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()
         return _stat_reduce("specificity", tp, fp, tn, fn, "binary", self.multidim_average)
@@ -43,6 +45,8 @@ class MulticlassSpecificity(MulticlassStatScores):
     plot_upper_bound: float = 1.0
     plot_legend_name: str = "Class"
 
+    _stat_kind = "specificity"  # compute() is the fused `_stat_reduce` score: native forward applies
+
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()
         return _stat_reduce("specificity", tp, fp, tn, fn, self.average, self.multidim_average)
@@ -60,6 +64,8 @@ class MultilabelSpecificity(MultilabelStatScores):
     plot_lower_bound: float = 0.0
     plot_upper_bound: float = 1.0
     plot_legend_name: str = "Label"
+
+    _stat_kind = "specificity"  # compute() is the fused `_stat_reduce` score: native forward applies
 
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()

@@ -826,7 +826,8 @@ class Metric(Module, ABC):
     # ------------------------------------------------------------------------------------------------- pickling
     def __getstate__(self) -> Dict[str, Any]:
         state = {k: v for k, v in self.__dict__.items()
-                 if k not in ("update", "compute", "_update_signature", "_cat_arenas", "_default_packs", "_cat_attrs")}
+                 if k not in ("update", "compute", "forward", "_update_signature", "_cat_arenas", "_default_packs",
+                              "_cat_attrs")}
         for key in self._defaults:  # a folded list state: its own rows only, not the arena's spare capacity
             cur = state.get(key)
             if isinstance(cur, list) and any(_is_partial_view(v) for v in cur):
@@ -839,9 +840,14 @@ class Metric(Module, ABC):
         self.update: Callable = self._wrap_update(self.update)  # type: ignore[method-assign]
         self.compute: Callable = self._wrap_compute(self.compute)  # type: ignore[method-assign]
         self._install_native_update()
+        self._install_native_forward()
 
     def _install_native_update(self) -> None:
         """Hook: classes with a native ``update`` entry point install it over the Python wrapper here."""
+
+    def _install_native_forward(self) -> None:
+        """Hook: classes with a native ``forward`` (``csrc/bindings/fastcall.cpp`` ``NativeForward``) install it as the
+        instance's ``forward`` here (calls off its fast path run :meth:`Metric.forward`)."""
 
     def __setattr__(self, name: str, value: Any) -> None:
         if name in _CONST_ATTRS:

@@ -76,6 +76,24 @@ def native_updater(kind: str, state: dict, fallback: Any) -> Any:
     return factory(state, fallback) if factory is not None else None
 
 
+FWD_CONFMAT, FWD_MULTICLASS, FWD_BINARY, FWD_MULTILABEL = 0, 1, 2, 3
+STAT_KINDS = {"accuracy": 0, "hamming": 1, "precision": 2, "recall": 3, "specificity": 4, "fbeta": 5}
+
+
+def native_forward(kind: int, state: dict, fallback: Any, stat_kind: str = "accuracy") -> Any:
+    """A native ``forward`` callable bound to a metric's ``__dict__`` (``csrc/bindings/fastcall.cpp`` ``NativeForward``)
+    or ``None`` where it does not apply (no GPU, native library missing, ``TORCHMETRICS_AMD_STRICT=1``,
+    ``TORCHMETRICS_AMD_NATIVE_FORWARD=0``).  Calls off its fast path go to ``fallback`` (``Metric.forward``)."""
+    from torchmetrics_amd.utils import validation
+
+    if (validation.STRICT or os.environ.get("TORCHMETRICS_AMD_NATIVE_FORWARD", "1") == "0"
+            or not torch.cuda.is_available() or not load_native(strict=False)):
+        return None
+    mod = _fast_mod
+    factory = getattr(mod, "forward_native", None) if not isinstance(mod, _DispatcherShim) else None
+    return factory(kind, state, fallback, STAT_KINDS[stat_kind]) if factory is not None else None
+
+
 def native_library_path() -> Path:
     return _LIB_PATH
 

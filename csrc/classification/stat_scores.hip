@@ -580,6 +580,131 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_kernel(const scalar_t* __re
   lds_flush(lds, nbins, out);
 }
 
+// Few-bin multiclass argmax rows, tiled (X == 1, nbins <= 256, C * sizeof <= 128 B, 16-B aligned preds): the streaming
+// version of mc_fewbins_kernel's LDS staging.  A persistent block walks tiles of 256 * R rows (<= 32 KiB of logits,
+// one contiguous piece of preds): it issues ALL 16-byte loads of its NEXT tile (and that tile's targets) into
+// registers before it evaluates the current one from LDS, so every block keeps a whole tile of loads in flight
+// while it computes (the per-row staging of mc_fewbins_kernel issued ~1 load per thread and then waited on it:
+// 1 M x 10 bf16 rows ran at 0.59 TB/s).  Bins are ballot popcounts in the owning lane's registers, as there; each
+// block flushes its <= 256 bins once.
+constexpr int kTileChunks = 8;  // 16-byte loads per thread per tile (256 threads x 8 x 16 B = 32 KiB)
+constexpr int kTileRows = 8;    // rows per thread per tile (max R)
+
+template <typename scalar_t, typename target_t>
+__global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t* __restrict__ preds,
+                                                                 const target_t* __restrict__ target, long long N,
+                                                                 int C, int R, long long ignore, bool has_ignore,
+                                                                 int mode, int64_t* __restrict__ out,
+                                                                 int* __restrict__ flag) {
+  __shared__ int hist[256];
+  __shared__ __attribute__((aligned(16))) unsigned char tile_raw[kTileChunks * kBlock * 16];
+  const int nbins = mode == kMcConfmat ? C * C : 3 * C + 1;
+  const int lane = threadIdx.x & (kWave - 1);
+  for (int b = threadIdx.x; b < nbins; b += kBlock) hist[b] = 0;
+  const long long TR = static_cast<long long>(kBlock) * R;  // rows per tile
+  const long long ntiles = (N + TR - 1) / TR;
+  const long long row_bytes = static_cast<long long>(C) * sizeof(scalar_t);
+  u32x4 buf[kTileChunks];
+  long long tbuf[kTileRows];
+  long long nbytes_cur = 0;
+  auto issue = [&](long long tile, long long& nbytes) {
+    const long long r0 = tile * TR;
+    const long long rows = N - r0 < TR ? N - r0 : TR;
+    nbytes = rows * row_bytes;
+    const unsigned char* src = reinterpret_cast<const unsigned char*>(preds + r0 * C);
+#pragma unroll
+    for (int j = 0; j < kTileChunks; ++j) {
+      const long long o = (static_cast<long long>(j) * kBlock + threadIdx.x) * 16;
+      if (o + 16 <= nbytes) buf[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + o));
+    }
+#pragma unroll
+    for (int k = 0; k < kTileRows; ++k) {
+      const long long row = r0 + static_cast<long long>(k) * kBlock + threadIdx.x;
+      if (k < R && row < N) tbuf[k] = static_cast<long long>(__builtin_nontemporal_load(target + row));
+    }
+  };
+  int acc[4] = {0, 0, 0, 0};
+  long long tile = blockIdx.x;
+  if (tile < ntiles) issue(tile, nbytes_cur);
+  for (; tile < ntiles; tile += gridDim.x) {  // block-uniform
+    const long long nbytes = nbytes_cur;
+    long long tcur[kTileRows];
+#pragma unroll
+    for (int k = 0; k < kTileRows; ++k) tcur[k] = tbuf[k];
+    __syncthreads();  // the previous tile's rows are read
+#pragma unroll
+    for (int j = 0; j < kTileChunks; ++j) {
+      const long long o = (static_cast<long long>(j) * kBlock + threadIdx.x) * 16;
+      if (o + 16 <= nbytes) *reinterpret_cast<u32x4*>(tile_raw + o) = buf[j];
+    }
+    if (nbytes % 16) {  // the last tile's ragged end
+      const unsigned char* src = reinterpret_cast<const unsigned char*>(preds + tile * TR * C);
+      for (long long o = (nbytes / 16) * 16 + threadIdx.x; o < nbytes; o += kBlock) tile_raw[o] = src[o];
+    }
+    __syncthreads();
+    const long long next = tile + gridDim.x;
+    if (next < ntiles) issue(next, nbytes_cur);  // in flight while this tile is evaluated
+    const scalar_t* lrow = reinterpret_cast<const scalar_t*>(tile_raw);
+#pragma unroll
+    for (int k = 0; k < kTileRows; ++k) {
+      if (k >= R) break;  // uniform
+      const long long rt = static_cast<long long>(k) * kBlock + threadIdx.x;  // row within the tile
+      const long long row = tile * TR + rt;
+      int t = -1, p = -1;
+      if (row < N) {
+        const long long tv = tcur[k];
+        if (!(has_ignore && tv == ignore)) {
+          if (tv < 0 || tv >= C) {
+            raise_flag(flag, kErrTargetOutOfRange);
+          } else {
+            t = static_cast<int>(tv);
+            const scalar_t* pr = lrow + rt * C;
+            float best = to_f32(pr[0]);
+            int bidx = 0;
+            for (int c = 1; c < C; ++c) {
+              const float v = to_f32(pr[c]);
+              if (argmax_better(v, c, best, bidx)) {
+                best = v;
+                bidx = c;
+              }
+            }
+            p = bidx;
+          }
+        }
+      }
+      const bool valid = t >= 0;
+      if (mode == kMcConfmat) {
+        const int key = valid ? t * C + p : -1;
+#pragma unroll
+        for (int slot = 0; slot < 4; ++slot) {
+          const int b0 = slot * kWave;
+          if (b0 >= nbins) break;
+          const int nb = min(kWave, nbins - b0);
+          for (int l = 0; l < nb; ++l) {
+            const int cnt = __popcll(__ballot(key == b0 + l));
+            if (lane == l) acc[slot] += cnt;
+          }
+        }
+      } else {
+        for (int c = 0; c < C; ++c) {
+          const unsigned long long pm = __ballot(valid && p == c), tm = __ballot(valid && t == c);
+          const int tp = __popcll(pm & tm), fp = __popcll(pm & ~tm), fn = __popcll(tm & ~pm);
+          const int bt = c, bf = C + c, bn = 2 * C + c;
+          if ((bt & (kWave - 1)) == lane) acc[bt >> 6] += tp;
+          if ((bf & (kWave - 1)) == lane) acc[bf >> 6] += fp;
+          if ((bn & (kWave - 1)) == lane) acc[bn >> 6] += fn;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int slot = 0; slot < 4; ++slot) {
+    const int b = slot * kWave + lane;
+    if (b < nbins && acc[slot]) atomicAdd(&hist[b], acc[slot]);
+  }
+  lds_flush(hist, nbins, out);
+}
+
 // fold a multiclass stats workspace [G, 3C+1] into the states; optionally micro-reduce over classes.
 // accumulate=true: states += batch ; false: states = batch (samplewise outputs). Re-zeros the workspace.
 template <int kT>
@@ -783,6 +908,90 @@ __global__ void __launch_bounds__(kBlock) bin_partials_reduce_kernel(const int* 
   long long acc = 0;
   for (int r = blockIdx.y; r < nrows; r += gridDim.y) acc += partials[static_cast<long long>(r) * nbins + b];
   if (acc) atomic_add_i64(ws + b, acc);
+}
+
+// Multilabel rows [N, L] (X == 1, L % VEC == 0, VEC = 16 / sizeof(preds)): a thread reads one 16-byte vector of VEC
+// consecutive labels (and their targets) per step, and the grid stride S (in vectors) is a multiple of L / VEC, so a
+// thread's VEC labels never change -- its 7 x VEC counters stay in registers for the whole walk (kU vectors in flight
+// per thread).  No per-element atomics at all (bin_flat_kernel did 3 LDS atomics per element: MultilabelF1Score(1000)
+// on 16384 x 1000 bf16 ran at 1.3 TB/s); the block folds its counters into an LDS histogram once and stores it as its
+// row of `partials`, which bin_partials_reduce_kernel folds into the workspace.
+constexpr int kVecBlock = 512;
+
+template <typename scalar_t, typename target_t, int VEC>
+__global__ void __launch_bounds__(kVecBlock) bin_vec_kernel(const scalar_t* __restrict__ preds,
+                                                            const target_t* __restrict__ target, long long nvec,
+                                                            int L, float thr_t, long long ignore, bool has_ignore,
+                                                            int* __restrict__ flag, int* __restrict__ not_prob,
+                                                            bool prob_check_all, int* __restrict__ partials) {
+  static_assert(VEC * sizeof(scalar_t) == 16, "one 16-byte vector of preds per step");
+  constexpr int kTChunks = (VEC * sizeof(target_t) + 15) / 16;  // 16-byte chunks of the matching targets
+  extern __shared__ __attribute__((aligned(16))) int lds[];
+  const int nbins = L * kBinSlots;
+  for (int b = threadIdx.x; b < nbins; b += kVecBlock) lds[b] = 0;
+  __syncthreads();
+  const long long S = static_cast<long long>(gridDim.x) * kVecBlock;
+  const long long v0 = static_cast<long long>(blockIdx.x) * kVecBlock + threadIdx.x;
+  const int l0 = static_cast<int>((v0 * VEC) % L);
+  int c[VEC][kBinSlots];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e)
+#pragma unroll
+    for (int k = 0; k < kBinSlots; ++k) c[e][k] = 0;
+  int local_not_prob = 0;
+  const u32x4* pv = reinterpret_cast<const u32x4*>(preds);
+  const u32x4* tvp = reinterpret_cast<const u32x4*>(target);
+  constexpr int kU = 4;
+  for (long long base = v0; base < nvec; base += kU * S) {
+    u32x4 praw[kU];
+    u32x4 traw[kU][kTChunks];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const long long v = base + u * S;
+      if (v < nvec) {
+        praw[u] = __builtin_nontemporal_load(pv + v);
+#pragma unroll
+        for (int j = 0; j < kTChunks; ++j) traw[u][j] = __builtin_nontemporal_load(tvp + v * kTChunks + j);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (base + u * S >= nvec) break;
+      const scalar_t* pe = reinterpret_cast<const scalar_t*>(&praw[u]);
+      const target_t* te = reinterpret_cast<const target_t*>(&traw[u][0]);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const long long tv = static_cast<long long>(te[e]);
+        const bool ignored = has_ignore && tv == ignore;
+        const float x = to_f32(pe[e]);
+        if (!(x >= 0.f && x <= 1.f) && (prob_check_all || !ignored)) local_not_prob = 1;
+        if (ignored) continue;
+        if (tv != 0 && tv != 1) {
+          raise_flag(flag, kErrTargetNotBinary);
+          continue;
+        }
+        const bool pa = x > thr_t;
+        const bool pb = round_to<scalar_t>(1.f / (1.f + __expf(-x))) > thr_t;
+        const bool t = tv == 1;
+        c[e][0] += t & pa;
+        c[e][1] += !t & pa;
+        c[e][2] += t & !pa;
+        c[e][3] += t & pb;
+        c[e][4] += !t & pb;
+        c[e][5] += t & !pb;
+        c[e][6] += 1;
+      }
+    }
+  }
+  if (__any(local_not_prob) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(not_prob, 1);
+#pragma unroll
+  for (int e = 0; e < VEC; ++e)
+#pragma unroll
+    for (int k = 0; k < kBinSlots; ++k)
+      if (c[e][k]) atomicAdd(&lds[(l0 + e) * kBinSlots + k], c[e][k]);
+  __syncthreads();
+  int* row = partials + static_cast<long long>(blockIdx.x) * nbins;
+  for (int b = threadIdx.x; b < nbins; b += kVecBlock) row[b] = lds[b];
 }
 
 // segment kernel for long contiguous segments (X large): block = one chunk of one (n, l) segment, register
@@ -1109,8 +1318,21 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
           const bool stage = !stage_off && X == 1 &&
                              static_cast<long long>(kBlock) * C * sizeof(scalar_t) <= kStageBytes &&
                              reinterpret_cast<uintptr_t>(pp) % 16 == 0;
-          hipLaunchKernelGGL((mc_fewbins_kernel<scalar_t, target_t, true>), dim3(grid), dim3(kBlock), 0, s, pp, tp, N,
-                             X, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, stage);
+          static const int tile_grid = [] {
+            const char* e = std::getenv("TM_AMD_FEWBINS_TILE");  // blocks per CU of the tiled kernel; 0 = off
+            return e ? std::atoi(e) : 2;
+          }();
+          // rows per thread per tile: as many as fit 32 KiB of logits (at most kTileRows)
+          const long long R = std::min<long long>(kTileRows, (kTileChunks * 16LL) / (static_cast<long long>(C) * sizeof(scalar_t)));
+          if (tile_grid > 0 && stage && R >= 1) {
+            const long long ntiles = (N + kBlock * R - 1) / (kBlock * R);
+            const int tgrid = static_cast<int>(std::min<long long>(ntiles, static_cast<long long>(cu_count(preds.get_device())) * tile_grid));
+            hipLaunchKernelGGL((mc_fewbins_tile_kernel<scalar_t, target_t>), dim3(tgrid), dim3(kBlock), 0, s, pp, tp, N, C,
+                               static_cast<int>(R), ignore_index, has_ignore, static_cast<int>(mode), outp, flagp);
+          } else {
+            hipLaunchKernelGGL((mc_fewbins_kernel<scalar_t, target_t, true>), dim3(grid), dim3(kBlock), 0, s, pp, tp, N,
+                               X, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, stage);
+          }
         } else {
           const int grid = pick_grid(N * X, kBlock);
           hipLaunchKernelGGL((mc_items_kernel<scalar_t, target_t, true>), dim3(grid), dim3(kBlock), lds_bytes, s, pp,
@@ -1172,6 +1394,35 @@ long long reg_grid(long long P, long long total) {
   return (grid + q - 1) / q * q;
 }
 
+// Grid of bin_vec_kernel, or 0 where it does not apply: [N, L] floating rows (X == 1) of > 64 labels, L a multiple of
+// VEC, 16-byte aligned preds / targets, the per-block histogram in LDS; the grid (~1 block of 8 waves per CU) is a
+// multiple of q = (L / VEC) / gcd(kVecBlock, L / VEC), so the stride keeps every thread on its labels.
+template <typename scalar_t>
+long long vec_grid(const at::Tensor& preds, const at::Tensor& target, long long L, long long X, bool samplewise,
+                   long long total, int cus) {
+  if constexpr (!IsFloating<scalar_t>::value || sizeof(scalar_t) > 4) {
+    return 0;
+  } else {
+    constexpr long long VEC = 16 / sizeof(scalar_t);
+    static const bool off = std::getenv("TM_AMD_BIN_VEC") && std::atoi(std::getenv("TM_AMD_BIN_VEC")) == 0;
+    if (off || samplewise || X != 1 || L <= kWave || L % VEC != 0 || L * kBinSlots > kLdsBins) return 0;
+    const auto tsz = target.element_size();
+    if (tsz != 4 && tsz != 8) return 0;
+    if (reinterpret_cast<uintptr_t>(preds.data_ptr()) % 16 || reinterpret_cast<uintptr_t>(target.data_ptr()) % 16)
+      return 0;
+    long long m = L / VEC, a = kVecBlock, b = m;
+    while (b) {
+      const long long r = a % b;
+      a = b;
+      b = r;
+    }
+    const long long q = m / a;
+    const long long want = std::max<long long>(1, std::min<long long>(cus, (total / VEC + kVecBlock - 1) / kVecBlock));
+    const long long grid = std::max<long long>(1, (want + q / 2) / q) * q;
+    return grid > 4096 ? 0 : grid;
+  }
+}
+
 void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws, at::Tensor flag, at::Tensor not_prob,
                 int64_t num_labels, double threshold, int64_t ignore_index, bool has_ignore, bool samplewise,
                 bool prob_check_all) {
@@ -1207,6 +1458,22 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
         hipLaunchKernelGGL((bin_seg_kernel<scalar_t, target_t>), dim3(blocks), dim3(kBlock), 0, s, pp, tp, nseg, L, X,
                            chunk, thr_t, ignore_index, has_ignore, samplewise, ws.data_ptr<int64_t>(),
                            flag.data_ptr<int>(), not_prob.data_ptr<int>(), prob_check_all);
+      } else if (vec_grid<scalar_t>(preds, target, L, X, samplewise, total, cu_count(preds.get_device())) > 0) {
+        constexpr int VEC = 16 / sizeof(scalar_t);
+        const int grid = static_cast<int>(vec_grid<scalar_t>(preds, target, L, X, samplewise, total,
+                                                             cu_count(preds.get_device())));
+        const long long nbins = L * kBinSlots;
+        at::Tensor partials = at::empty({static_cast<long long>(grid) * nbins}, ws.options().dtype(at::kInt));
+        if constexpr (VEC * sizeof(scalar_t) == 16) {
+          hipLaunchKernelGGL((bin_vec_kernel<scalar_t, target_t, VEC>), dim3(grid), dim3(kVecBlock),
+                             nbins * sizeof(int), s, pp, tp, total / VEC, static_cast<int>(L), thr_t, ignore_index,
+                             has_ignore, flag.data_ptr<int>(), not_prob.data_ptr<int>(), prob_check_all,
+                             partials.data_ptr<int>());
+        }
+        const dim3 rgrid(static_cast<unsigned>((nbins + kBlock - 1) / kBlock),
+                         static_cast<unsigned>(std::min(kPartialGroups, grid)));
+        hipLaunchKernelGGL(bin_partials_reduce_kernel, rgrid, dim3(kBlock), 0, s, partials.data_ptr<int>(), grid,
+                           static_cast<int>(nbins), ws.data_ptr<int64_t>());
       } else if (!samplewise && reg_grid(L * X, total) > 0 && L * kBinSlots <= kLdsBins) {
         // grid stride a multiple of L * X: a fixed label per thread (register counters)
         const long long grid = reg_grid(L * X, total);

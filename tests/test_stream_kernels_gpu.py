@@ -1,0 +1,115 @@
+"""Streaming stat-score kernels (``csrc/classification/stat_scores.hip``): the tiled few-bin multiclass kernel
+(``mc_fewbins_tile_kernel``) and the vectorised multilabel kernel (``bin_vec_kernel``), each compared with the CPU
+(ATen) implementation of the same op contract -- identical integer workspaces and flags -- on shapes that put the
+tile / stride boundaries in every position (ragged last tile, rows < one tile, labels not a multiple of the vector
+width -> the other kernel), NaN rows, ignore_index, logits vs probabilities, invalid targets."""
+import pytest
+import torch
+
+from torchmetrics_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _mc(preds, target, C, ignore, mode, dev):
+    out = torch.zeros(C * C if mode == ops.MC_CONFMAT else 3 * C + 1, dtype=torch.int64, device=dev)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    ops.mc_update(preds.to(dev), target.to(dev), out, flag, C, ignore, mode, False)
+    return out.cpu(), int(flag.item())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("C", [2, 3, 10, 16, 31])
+@pytest.mark.parametrize("N", [1, 255, 2049, 100_003, 1 << 20])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_fewbins_tiled_matches_cpu(dtype, C, N, mode):
+    if mode == ops.MC_CONFMAT and C * C > 256:
+        pytest.skip("not a few-bin confusion matrix")
+    g = torch.Generator().manual_seed(C * 1000 + N % 997)
+    preds = torch.randn(N, C, generator=g).to(dtype)
+    target = torch.randint(0, C, (N,), generator=g)
+    gg, fg = _mc(preds, target, C, None, mode, DEV)
+    cc, fc = _mc(preds, target, C, None, mode, "cpu")
+    assert torch.equal(gg, cc)
+    assert fg == fc == 0
+
+
+@pytest.mark.parametrize("ignore", [0, -1])
+def test_fewbins_tiled_nan_ties_ignore_and_bad_target(ignore):
+    C, N = 10, 70_001
+    preds = torch.randn(N, C).to(torch.bfloat16)
+    preds[::5] = 0.0  # all-tie rows: first index
+    preds[1::13, 3] = float("nan")  # NaN wins
+    preds[2::17, 7] = float("inf")
+    target = torch.randint(0, C, (N,))
+    target[::9] = ignore
+    gg, fg = _mc(preds, target, C, ignore, 1, DEV)
+    cc, fc = _mc(preds, target, C, ignore, 1, "cpu")
+    assert torch.equal(gg, cc) and fg == fc == 0
+    bad = target.clone()
+    bad[N - 1] = C + 3
+    _, fg = _mc(preds, bad, C, ignore, 1, DEV)
+    assert fg & 1  # target out of range
+
+
+def test_fewbins_tiled_unaligned_input_takes_the_other_kernel():
+    C, N = 10, 10_000
+    base = torch.randn(N * C + 1).to(torch.bfloat16)
+    preds = base[1:].view(N, C)  # 2-byte offset: not 16-byte aligned
+    target = torch.randint(0, C, (N,))
+    gg, _ = _mc(preds, target, C, None, 1, DEV)
+    cc, _ = _mc(preds.contiguous(), target, C, None, 1, "cpu")
+    assert torch.equal(gg, cc)
+
+
+def _bin(preds, target, L, ignore, dev, threshold=0.5):
+    ws = torch.zeros(L * 7, dtype=torch.int64, device=dev)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    not_prob = torch.zeros(1, dtype=torch.int32, device=dev)
+    ops.bin_update(preds.to(dev), target.to(dev), ws, flag, not_prob, L, threshold, ignore, False)
+    return ws.cpu(), int(flag.item()), int(not_prob.item())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("tdtype", [torch.int32, torch.int64])
+@pytest.mark.parametrize("L", [65, 68, 100, 256, 1000, 1752])
+@pytest.mark.parametrize("logits", [False, True])
+def test_multilabel_vec_matches_cpu(dtype, tdtype, L, logits):
+    N = 3001
+    g = torch.Generator().manual_seed(L)
+    preds = (torch.randn(N, L, generator=g) * 3 if logits else torch.rand(N, L, generator=g)).to(dtype)
+    target = torch.randint(0, 2, (N, L), generator=g).to(tdtype)
+    gg = _bin(preds, target, L, None, DEV)
+    cc = _bin(preds, target, L, None, "cpu")
+    assert torch.equal(gg[0], cc[0]) and gg[1:] == cc[1:]
+    assert gg[2] == int(logits)
+
+
+@pytest.mark.parametrize("ignore", [-1, 1])
+def test_multilabel_vec_ignore_and_bad_target(ignore):
+    N, L = 4096, 128
+    preds = torch.rand(N, L).to(torch.bfloat16)
+    target = torch.randint(0, 2, (N, L))
+    target[::3, ::5] = ignore
+    preds[7, 9] = 1.5  # one non-probability: the logits reading for the whole call
+    gg = _bin(preds, target, L, ignore, DEV)
+    cc = _bin(preds, target, L, ignore, "cpu")
+    assert torch.equal(gg[0], cc[0]) and gg[1:] == cc[1:]
+    bad = target.clone()
+    bad[N - 1, L - 1] = 2
+    _, flag, _ = _bin(preds, bad, L, ignore, DEV)
+    assert flag & 4  # target not binary
+
+
+def test_multilabel_module_values_on_vec_path():
+    import torchmetrics_amd as tm
+
+    N, L = 16384, 1000
+    p = torch.rand(N, L).to(torch.bfloat16)
+    t = torch.randint(0, 2, (N, L), dtype=torch.int32)
+    m = tm.MultilabelF1Score(L).to(DEV)
+    m.update(p.to(DEV), t.to(DEV))
+    ref = tm.MultilabelF1Score(L)
+    ref.update(p, t)
+    torch.testing.assert_close(m.compute().cpu(), ref.compute())

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp PYTHONPATH="$GRAFT_REPO_ROOT"
-timeout -k 10 300 python -u -m pytest tests/test_native_forward_gpu.py tests/test_native_update.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4_pytest_fwd.log 2>&1 || { tail -60 gpurun_out/r4_pytest_fwd.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_native_forward_gpu.py tests/test_native_update.py tests/test_stream_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4_pytest_fwd.log 2>&1 || { tail -60 gpurun_out/r4_pytest_fwd.log; exit 1; }
 tail -2 gpurun_out/r4_pytest_fwd.log
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4_pytest_gpu.log 2>&1 || { tail -40 gpurun_out/r4_pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/r4_pytest_gpu.log
@@ -16,7 +16,7 @@ for i in 1 2; do
 done
 timeout -k 10 300 python benchmarks/bench_forward.py 2>/dev/null > gpurun_out/r4_bench_forward.jsonl || exit 1
 cat gpurun_out/r4_bench_forward.jsonl
-timeout -k 10 300 python benchmarks/bench_binary_stats.py 2>/dev/null > gpurun_out/r4_bench_stats_before.jsonl || exit 1
-cat gpurun_out/r4_bench_stats_before.jsonl
+timeout -k 10 300 python benchmarks/bench_binary_stats.py 2>/dev/null > gpurun_out/r4_bench_stats.jsonl || exit 1
+cat gpurun_out/r4_bench_stats.jsonl
 timeout -k 10 300 python benchmarks/bench_collection.py --steps 100 --warmup 10 --sync-every-step 2>/dev/null > gpurun_out/r4_collection_before.json || exit 1
 cat gpurun_out/r4_collection_before.json

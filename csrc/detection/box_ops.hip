@@ -80,6 +80,104 @@ __global__ void __launch_bounds__(256) box_pairwise_kernel<double, double>(const
   }
 }
 
+// Ragged batch of images (IntersectionOverUnion & co. update): block i computes image i's [n_i, m_i] matrix into its
+// slice of one flat output, with the reference's two in-place masks fused (F/detection/iou.py `_iou_update`:
+// values below iou_threshold -> invalid; S/detection/iou.py:191-193 respect_labels: label mismatch -> invalid).
+// One launch per update instead of one box_pairwise + 2 masked writes per image.
+template <typename scalar_t, typename acc_t>
+__global__ void __launch_bounds__(256) box_pairwise_ragged_kernel(
+    const scalar_t* __restrict__ a, const scalar_t* __restrict__ b, const int64_t* __restrict__ a_off,
+    const int64_t* __restrict__ b_off, const int64_t* __restrict__ o_off, const int64_t* __restrict__ a_lab,
+    const int64_t* __restrict__ b_lab, int op, bool has_thr, acc_t thr, acc_t invalid, scalar_t* __restrict__ out) {
+  const int img = blockIdx.x;
+  const long long a0 = a_off[img], b0 = b_off[img], o0 = o_off[img];
+  const long long m = b_off[img + 1] - b0;
+  const long long total = o_off[img + 1] - o0;
+  for (long long e = threadIdx.x; e < total; e += blockDim.x) {
+    const long long i = a0 + e / m, j = b0 + e % m;
+    acc_t pa[4], pb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pa[k] = static_cast<acc_t>(a[i * 4 + k]);
+      pb[k] = static_cast<acc_t>(b[j * 4 + k]);
+    }
+    acc_t v = pair_value<acc_t>(pa, pb, op);
+    if (has_thr && v < thr) v = invalid;
+    if (a_lab != nullptr && a_lab[i] != b_lab[j]) v = invalid;
+    out[o0 + e] = static_cast<scalar_t>(v);
+  }
+}
+
+// compute() of the IoU family over the flat values of every image: one block per image; column j of image i belongs
+// to class classes[k] == gt_lab[b_off[i] + j].  Sums (fp64) and counts of the valid (!= invalid) values, per class
+// (slot k < K, LDS-privatised per block) and over everything (slot K).  Replaces the reference's per-image boolean
+// indexing and per-class x per-image double loop (S/detection/iou.py:205-221).
+template <typename scalar_t>
+__global__ void __launch_bounds__(256) iou_class_reduce_kernel(
+    const scalar_t* __restrict__ vals, const int64_t* __restrict__ o_off, const int64_t* __restrict__ b_off,
+    const int64_t* __restrict__ gt_lab, const int64_t* __restrict__ classes, int K, double invalid,
+    double* __restrict__ sums, int64_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* lsum = reinterpret_cast<double*>(smem);
+  int* lcnt = reinterpret_cast<int*>(lsum + K);
+  const bool per_class = K > 0;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    lsum[k] = 0.0;
+    lcnt[k] = 0;
+  }
+  __syncthreads();
+  const int img = blockIdx.x;
+  const long long o0 = o_off[img], b0 = b_off[img];
+  const long long m = b_off[img + 1] - b0;
+  const long long total = o_off[img + 1] - o0;
+  double s = 0.0;
+  long long c = 0;
+  for (long long e = threadIdx.x; e < total; e += blockDim.x) {
+    const double v = static_cast<double>(vals[o0 + e]);
+    if (v == invalid) continue;
+    s += v;
+    ++c;
+    if (per_class) {
+      const long long lab = gt_lab[b0 + e % m];
+      int lo = 0, hi = K;  // lower_bound: classes is the sorted unique set of all ground-truth labels
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (classes[mid] < lab) lo = mid + 1;
+        else hi = mid;
+      }
+      atomicAdd(&lsum[lo], v);
+      atomicAdd(&lcnt[lo], 1);
+    }
+  }
+  __shared__ double rs[256 / kWave];
+  __shared__ long long rc[256 / kWave];
+  s = wave_sum(s);
+  c = wave_sum_ll(c);
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+    rs[threadIdx.x / kWave] = s;
+    rc[threadIdx.x / kWave] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double ts = 0.0;
+    long long tc = 0;
+    for (int w = 0; w < static_cast<int>(blockDim.x / kWave); ++w) {
+      ts += rs[w];
+      tc += rc[w];
+    }
+    if (tc) {
+      atomicAdd(&sums[K], ts);
+      atomic_add_i64(counts + K, tc);
+    }
+  }
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    if (lcnt[k]) {
+      atomicAdd(&sums[k], lsum[k]);
+      atomic_add_i64(counts + k, lcnt[k]);
+    }
+  }
+}
+
 // COCO bbox IoU (maskApi bbIou): boxes xywh, crowd ground truth => intersection over detection area.
 __device__ __forceinline__ double coco_iou(const double* d, const double* g, bool crowd) {
   const double w = min(d[0] + d[2], g[0] + g[2]) - max(d[0], g[0]);
@@ -181,6 +279,74 @@ at::Tensor box_pairwise(const at::Tensor& a, const at::Tensor& b, int64_t op, bo
   return out;
 }
 
+// Ragged batch: a [sum n_i, 4], b [sum m_i, 4] xyxy; a_off / b_off / o_off int64 [I + 1] (o_off: prefix sums of
+// n_i * m_i); labels int64 (empty tensors: respect_labels off).  Returns the flat [sum n_i m_i] values.
+at::Tensor box_pairwise_ragged(const at::Tensor& a, const at::Tensor& b, const at::Tensor& a_off,
+                               const at::Tensor& b_off, const at::Tensor& o_off, const at::Tensor& a_lab,
+                               const at::Tensor& b_lab, int64_t op, double threshold, bool has_thr, double invalid,
+                               int64_t total) {
+  TM_CHECK_CUDA(a);
+  for (const at::Tensor* t : {&b, &a_off, &b_off, &o_off, &a_lab, &b_lab}) TM_SAME_DEVICE(a, (*t));
+  for (const at::Tensor* t : {&a, &b, &a_off, &b_off, &o_off, &a_lab, &b_lab})
+    TORCH_CHECK(t->is_contiguous(), "box_pairwise_ragged: contiguous inputs expected");
+  TORCH_CHECK(a.dim() == 2 && a.size(1) == 4 && b.dim() == 2 && b.size(1) == 4, "box_pairwise_ragged: [*, 4] boxes");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() && (a.scalar_type() == at::kFloat || a.scalar_type() == at::kDouble),
+              "box_pairwise_ragged: float32 / float64 boxes of one dtype");
+  TORCH_CHECK(op >= 0 && op <= 3, "box_pairwise_ragged: unknown op");
+  for (const at::Tensor* t : {&a_off, &b_off, &o_off})
+    TORCH_CHECK(t->scalar_type() == at::kLong && t->numel() == a_off.numel() && t->numel() >= 1,
+                "box_pairwise_ragged: offsets int64 [I + 1]");
+  const bool labels = a_lab.numel() > 0 || b_lab.numel() > 0;
+  if (labels)
+    TORCH_CHECK(a_lab.scalar_type() == at::kLong && b_lab.scalar_type() == at::kLong && a_lab.numel() == a.size(0) &&
+                    b_lab.numel() == b.size(0),
+                "box_pairwise_ragged: int64 labels, one per box");
+  const long long I = a_off.numel() - 1;  // total = o_off[I], passed by the caller (no device read)
+  at::Tensor out = at::empty({total}, a.options());
+  if (total == 0 || I == 0) return out;
+  TM_DISPATCH_FLOAT(a.scalar_type(), "box_pairwise_ragged", [&] {
+    using acc_t = typename std::conditional<std::is_same<scalar_t, double>::value, double, float>::type;
+    hipLaunchKernelGGL((box_pairwise_ragged_kernel<scalar_t, acc_t>), dim3(static_cast<unsigned>(I)), dim3(256), 0,
+                       stream(), reinterpret_cast<const scalar_t*>(a.data_ptr()),
+                       reinterpret_cast<const scalar_t*>(b.data_ptr()), a_off.data_ptr<int64_t>(),
+                       b_off.data_ptr<int64_t>(), o_off.data_ptr<int64_t>(),
+                       labels ? a_lab.data_ptr<int64_t>() : nullptr, labels ? b_lab.data_ptr<int64_t>() : nullptr,
+                       static_cast<int>(op), has_thr, static_cast<acc_t>(threshold), static_cast<acc_t>(invalid),
+                       reinterpret_cast<scalar_t*>(out.data_ptr()));
+  });
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return out;
+}
+
+// (sums f64 [K + 1], counts int64 [K + 1]) of the valid values, per class (k < K) and overall (K); see the kernel.
+std::tuple<at::Tensor, at::Tensor> iou_class_reduce(const at::Tensor& vals, const at::Tensor& o_off,
+                                                    const at::Tensor& b_off, const at::Tensor& gt_lab,
+                                                    const at::Tensor& classes, double invalid) {
+  TM_CHECK_CUDA(vals);
+  for (const at::Tensor* t : {&o_off, &b_off, &gt_lab, &classes}) {
+    TM_SAME_DEVICE(vals, (*t));
+    TORCH_CHECK(t->scalar_type() == at::kLong && t->is_contiguous(), "iou_class_reduce: int64 contiguous tables");
+  }
+  TORCH_CHECK(vals.is_contiguous() && (vals.scalar_type() == at::kFloat || vals.scalar_type() == at::kDouble),
+              "iou_class_reduce: float32 / float64 values");
+  TORCH_CHECK(o_off.numel() == b_off.numel() && o_off.numel() >= 1, "iou_class_reduce: offsets [I + 1]");
+  const long long I = o_off.numel() - 1;
+  const int K = static_cast<int>(classes.numel());
+  const size_t lds = static_cast<size_t>(K) * (sizeof(double) + sizeof(int));
+  TORCH_CHECK(lds <= 60 * 1024, "iou_class_reduce: at most ~5000 classes");
+  at::Tensor sums = at::zeros({K + 1}, vals.options().dtype(at::kDouble));
+  at::Tensor counts = at::zeros({K + 1}, vals.options().dtype(at::kLong));
+  if (I == 0) return {sums, counts};
+  AT_DISPATCH_FLOATING_TYPES(vals.scalar_type(), "iou_class_reduce", [&] {
+    hipLaunchKernelGGL(iou_class_reduce_kernel<scalar_t>, dim3(static_cast<unsigned>(I)), dim3(256), lds, stream(),
+                       vals.data_ptr<scalar_t>(), o_off.data_ptr<int64_t>(), b_off.data_ptr<int64_t>(),
+                       gt_lab.data_ptr<int64_t>(), classes.data_ptr<int64_t>(), K, invalid, sums.data_ptr<double>(),
+                       counts.data_ptr<int64_t>());
+  });
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return {sums, counts};
+}
+
 // Greedy COCO matching for all groups / area ranges / thresholds.  Returns (dt_match, dt_ig), each uint8 [T, A, D].
 std::tuple<at::Tensor, at::Tensor> coco_match(const at::Tensor& dbox, const at::Tensor& darea, const at::Tensor& gbox,
                                               const at::Tensor& garea, const at::Tensor& gcrowd,
@@ -228,6 +394,12 @@ std::tuple<at::Tensor, at::Tensor> coco_match(const at::Tensor& dbox, const at::
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
   m.def("box_pairwise(Tensor a, Tensor b, int op, bool aligned) -> Tensor");
   m.def(
+      "box_pairwise_ragged(Tensor a, Tensor b, Tensor a_off, Tensor b_off, Tensor o_off, Tensor a_lab, Tensor b_lab, "
+      "int op, float threshold, bool has_thr, float invalid, int total) -> Tensor");
+  m.def(
+      "iou_class_reduce(Tensor vals, Tensor o_off, Tensor b_off, Tensor gt_lab, Tensor classes, float invalid) -> "
+      "(Tensor, Tensor)");
+  m.def(
       "coco_match(Tensor dbox, Tensor darea, Tensor gbox, Tensor garea, Tensor gcrowd, Tensor det_start, "
       "Tensor det_cnt, Tensor gt_start, Tensor gt_cnt, Tensor area_rng, Tensor iou_thr, Tensor? iou_pre=None, "
       "Tensor? iou_off=None) -> (Tensor, Tensor)");
@@ -235,5 +407,7 @@ TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
 
 TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
   m.impl("box_pairwise", &tm_amd::box_pairwise);
+  m.impl("box_pairwise_ragged", &tm_amd::box_pairwise_ragged);
+  m.impl("iou_class_reduce", &tm_amd::iou_class_reduce);
   m.impl("coco_match", &tm_amd::coco_match);
 }

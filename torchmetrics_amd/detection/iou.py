@@ -43,37 +43,72 @@ class IntersectionOverUnion(Metric):
 
     def _safe_boxes(self, boxes: Tensor) -> Tensor:
         boxes = _fix_empty_tensors(boxes)
-        if boxes.numel() > 0:
-            boxes = box_convert(boxes, in_fmt=self.box_format, out_fmt="xyxy")
         return boxes.reshape(-1, 4) if boxes.numel() else boxes.new_zeros(0, 4)
 
     def update(self, preds: List[Dict[str, Tensor]], target: List[Dict[str, Tensor]]) -> None:
+        """The whole batch in one launch: every image's boxes are concatenated (one box_convert for all), the
+        ``[n_i, m_i]`` matrices come out of one ragged kernel with the threshold / label masks fused, and the states
+        get per-image views of that flat result (reference S/detection/iou.py:180-193: one IoU call + two masked
+        writes per image)."""
         _input_validator(preds, target, ignore_score=True)
-        for p, t in zip(preds, target):
-            det, gt = self._safe_boxes(p["boxes"]), self._safe_boxes(t["boxes"])
+        if not preds:
+            return
+        dets = [self._safe_boxes(p["boxes"]) for p in preds]
+        gts = [self._safe_boxes(t["boxes"]) for t in target]
+        n = [d.shape[0] for d in dets]
+        m = [g.shape[0] for g in gts]
+        sizes = [a * b for a, b in zip(n, m)]
+        dev = dets[0].device
+        det, gt = torch.cat(dets), torch.cat(gts)
+        out_dtype = det.dtype if det.is_floating_point() else torch.float32
+        work = torch.float64 if det.dtype == torch.float64 else torch.float32
+        det, gt = det.to(work), gt.to(work)
+        if self.box_format != "xyxy" and det.numel():
+            det = box_convert(det, in_fmt=self.box_format, out_fmt="xyxy")
+        if self.box_format != "xyxy" and gt.numel():
+            gt = box_convert(gt, in_fmt=self.box_format, out_fmt="xyxy")
+        offs = torch.tensor([[0, 0, 0]] + list(zip(n, m, sizes)), dtype=torch.int64).cumsum(0).T.contiguous().to(dev)
+        if self.respect_labels:
+            dl = torch.cat([p["labels"].reshape(-1) for p in preds]).to(dev, torch.int64)
+            gl = torch.cat([t["labels"].reshape(-1) for t in target]).to(dev, torch.int64)
+        else:
+            dl = gl = torch.zeros(0, dtype=torch.int64, device=dev)
+        flat = ops.box_pairwise_ragged(det.contiguous(), gt.contiguous(), offs[0], offs[1], offs[2], dl, gl, self._op,
+                                       self.iou_threshold, self._invalid_val, sum(sizes)).to(out_dtype)
+        o = 0
+        for t, a, b, sz in zip(target, n, m, sizes):
             self.groundtruth_labels.append(t["labels"])
-            mat = ops.box_pairwise(det, gt, self._op)
-            if self.iou_threshold is not None:
-                mat = torch.where(mat < self.iou_threshold, torch.full_like(mat, self._invalid_val), mat)
-            if self.respect_labels:
-                same = p["labels"].unsqueeze(1) == t["labels"].unsqueeze(0)
-                mat = torch.where(same, mat, torch.full_like(mat, self._invalid_val))
-            self.iou_matrix.append(mat)
+            self.iou_matrix.append(flat[o : o + sz].view(a, b))
+            o += sz
 
     def compute(self) -> dict:
-        valid = [m[m != self._invalid_val] for m in self.iou_matrix]
-        score = torch.cat(valid, 0).mean() if valid else torch.tensor(float("nan"))
-        results: Dict[str, Tensor] = {f"{self._iou_type}": score}
+        """One masked segmented reduction over every image (``ops.iou_class_reduce``): the overall mean and, with
+        ``class_metrics``, the mean per ground-truth class -- no per-image or per-class host sync (the one host read
+        is the class list that names the output keys, as in the reference S/detection/iou.py:205-221)."""
+        mats = self.iou_matrix
+        if not mats:
+            return {f"{self._iou_type}": torch.tensor(float("nan"))}
+        dev = mats[0].device
+        sizes = [mt.numel() for mt in mats]
+        widths = [mt.shape[-1] if mt.ndim == 2 else 1 for mt in mats]
+        flat = torch.cat([mt.reshape(-1) for mt in mats])
+        work = torch.float64 if flat.dtype == torch.float64 else torch.float32
+        flat = flat.to(work)
+        o_off = torch.tensor([0] + sizes, dtype=torch.int64).cumsum(0).to(dev)
+        b_off = torch.tensor([0] + widths, dtype=torch.int64).cumsum(0).to(dev)
+        classes = torch.zeros(0, dtype=torch.int64, device=dev)
+        gt_lab = classes
+        if self.class_metrics and self.groundtruth_labels:
+            gt_lab = dim_zero_cat([g.reshape(-1) for g in self.groundtruth_labels]).to(dev, torch.int64)
+            if gt_lab.numel() != sum(widths):
+                raise RuntimeError("IoU states are inconsistent: one ground-truth label per matrix column expected")
+            classes = gt_lab.unique()
+        sums, counts = ops.iou_class_reduce(flat, o_off, b_off, gt_lab, classes, self._invalid_val)
+        means = (sums / counts).to(mats[0].dtype if mats[0].is_floating_point() else torch.float32)
+        results: Dict[str, Tensor] = {f"{self._iou_type}": means[-1]}
         if self.class_metrics:
-            gt_labels = dim_zero_cat(self.groundtruth_labels) if self.groundtruth_labels else torch.zeros(0)
-            for cl in (gt_labels.unique().tolist() if len(gt_labels) > 0 else []):
-                tot, cnt = torch.zeros_like(score), torch.zeros_like(score)
-                for mat, lab in zip(self.iou_matrix, self.groundtruth_labels):
-                    s = mat[:, lab == cl]
-                    keep = s != self._invalid_val
-                    tot = tot + s[keep].sum()
-                    cnt = cnt + keep.sum()
-                results[f"{self._iou_type}/cl_{cl}"] = tot / cnt
+            for k, cl in enumerate(classes.tolist()):
+                results[f"{self._iou_type}/cl_{cl}"] = means[k]
         return results
 
 

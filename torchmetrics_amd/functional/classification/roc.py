@@ -10,6 +10,7 @@ from torch import Tensor
 from typing_extensions import Literal
 
 from torchmetrics_amd.functional.classification.precision_recall_curve import (
+    _macro_average_curve,
     Thresholds,
     _binary_clf_curve,
     _clf_curves,
@@ -20,7 +21,7 @@ from torchmetrics_amd.functional.classification.precision_recall_curve import (
     _task_dispatch,
 )
 from torchmetrics_amd import ops
-from torchmetrics_amd.utilities.compute import _safe_divide, interp
+from torchmetrics_amd.utilities.compute import _safe_divide
 from torchmetrics_amd.utilities.prints import rank_zero_warn
 
 
@@ -107,17 +108,9 @@ def _multiclass_roc_compute(
             thres_list.append(res[2])
         tensor_state = False
     if average == "macro":
-        thres = thres.repeat(num_classes) if tensor_state else torch.cat(thres_list, dim=0)
-        thres = thres.sort(descending=True).values
-        mean_fpr = fpr.flatten() if tensor_state else torch.cat(fpr_list, dim=0)
-        mean_fpr = mean_fpr.sort().values
-        mean_tpr = torch.zeros_like(mean_fpr)
-        for i in range(num_classes):
-            mean_tpr += interp(
-                mean_fpr, fpr[i] if tensor_state else fpr_list[i], tpr[i] if tensor_state else tpr_list[i]
-            )
-        mean_tpr /= num_classes
-        return mean_fpr, mean_tpr, thres
+        if tensor_state:
+            return _macro_average_curve(fpr, tpr, thres.repeat(num_classes), descending=True)
+        return _macro_average_curve(fpr_list, tpr_list, torch.cat(thres_list), descending=True)
     if tensor_state:
         return fpr, tpr, thres
     return fpr_list, tpr_list, thres_list

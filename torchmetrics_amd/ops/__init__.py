@@ -1152,6 +1152,27 @@ def box_pairwise(a: Tensor, b: Tensor, op: int = BOX_IOU, aligned: bool = False)
     return _cpu.box_pairwise(a, b, op, aligned)
 
 
+def box_pairwise_ragged(a: Tensor, b: Tensor, a_off: Tensor, b_off: Tensor, o_off: Tensor, a_lab: Tensor,
+                        b_lab: Tensor, op: int, threshold: Optional[float], invalid: float, total: int) -> Tensor:
+    """IoU-family matrices of a ragged batch of images in one flat ``[sum n_i m_i]`` tensor (image i's ``[n_i, m_i]``
+    matrix at ``o_off[i]``), values ``< threshold`` and label mismatches (when labels are given, i.e. non-empty) set to
+    ``invalid`` (``csrc/detection/box_ops.hip``).  ``total`` = ``o_off[-1]`` (known on the host: no device read)."""
+    if a.is_cuda:
+        return _ops().box_pairwise_ragged(a.contiguous(), b.contiguous(), a_off, b_off, o_off, a_lab, b_lab, op,
+                                          0.0 if threshold is None else float(threshold), threshold is not None,
+                                          float(invalid), int(total))
+    return _cpu.box_pairwise_ragged(a, b, a_off, b_off, o_off, a_lab, b_lab, op, threshold, invalid)
+
+
+def iou_class_reduce(vals: Tensor, o_off: Tensor, b_off: Tensor, gt_lab: Tensor, classes: Tensor,
+                     invalid: float) -> Tuple[Tensor, Tensor]:
+    """fp64 sums and int64 counts of the valid (``!= invalid``) values of ragged IoU matrices: per class of the column's
+    ground-truth label (slots ``[0, K)``, ``classes`` sorted) and overall (slot ``K``)."""
+    if vals.is_cuda:
+        return _ops().iou_class_reduce(vals, o_off, b_off, gt_lab, classes, float(invalid))
+    return _cpu.iou_class_reduce(vals, o_off, b_off, gt_lab, classes, invalid)
+
+
 def nms(boxes: Tensor, scores: Tensor, iou_threshold: float, idxs: Optional[Tensor] = None) -> Tensor:
     """Greedy NMS: indices of the kept ``[N, 4]`` xyxy boxes in descending score order (equal scores: lower index
     first).  With ``idxs`` only boxes of the same class suppress each other.  ROCm: bitmask-tile kernel + one-wave
@@ -1450,6 +1471,13 @@ def lpips_layer(f0: Tensor, f1: Tensor, w: Tensor, eps: float = 1e-8) -> Tensor:
         _ops().lpips_layer(a, b, w.reshape(-1).float().contiguous(), part, float(eps))
         return (part.sum(1) / pixels).to(f0.dtype if f0.is_floating_point() else torch.float32)
     return _cpu.lpips_layer(f0, f1, w, eps)
+
+
+def interp_mean(x: Tensor, xp: Tensor, fp: Tensor, offsets: Tensor) -> Tensor:
+    """Mean over C ragged curves ``(xp, fp)[offsets[c]:offsets[c+1]]`` of their piecewise-linear interpolation at the
+    grid ``x`` (``csrc/classification/curve_interp.hip``: one launch on ROCm, the same walk on the host)."""
+    load_native(strict=True)
+    return torch.ops.tm_amd.interp_mean(x.contiguous(), xp.contiguous(), fp.contiguous(), offsets.contiguous())
 
 
 def stat_reduce(tp: Tensor, fp: Tensor, tn: Tensor, fn: Tensor, kind: int, average: int, multilabel: bool,

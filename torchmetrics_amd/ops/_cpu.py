@@ -806,3 +806,40 @@ def rle_iou(dbuf, ddesc, gbuf, gdesc, pd, pg, gcrowd):
         union = a[2] if crowd[g] else a[2] + b[2] - inter
         out[p] = inter / union if inter else 0.0
     return out.to(pd.device)
+
+
+def box_pairwise_ragged(a: Tensor, b: Tensor, a_off: Tensor, b_off: Tensor, o_off: Tensor, a_lab: Tensor, b_lab: Tensor,
+                        op: int, threshold, invalid: float) -> Tensor:
+    """Host twin of the ragged IoU-family kernel: image by image (CPU tensors)."""
+    ao, bo = a_off.tolist(), b_off.tolist()
+    parts = []
+    for i in range(len(ao) - 1):
+        mat = box_pairwise(a[ao[i]:ao[i + 1]], b[bo[i]:bo[i + 1]], op, False)
+        if threshold is not None:
+            mat = torch.where(mat < threshold, torch.full_like(mat, invalid), mat)
+        if a_lab.numel() or b_lab.numel():
+            same = a_lab[ao[i]:ao[i + 1]].unsqueeze(1) == b_lab[bo[i]:bo[i + 1]].unsqueeze(0)
+            mat = torch.where(same, mat, torch.full_like(mat, invalid))
+        parts.append(mat.reshape(-1))
+    dt = a.dtype if a.is_floating_point() else torch.float32
+    return torch.cat(parts) if parts else torch.zeros(0, dtype=dt)
+
+
+def iou_class_reduce(vals: Tensor, o_off: Tensor, b_off: Tensor, gt_lab: Tensor, classes: Tensor, invalid: float):
+    """Host twin of ``iou_class_reduce_kernel`` (vectorised over all images)."""
+    K = classes.numel()
+    sums = torch.zeros(K + 1, dtype=torch.float64)
+    counts = torch.zeros(K + 1, dtype=torch.int64)
+    sizes, m = o_off.diff(), b_off.diff()
+    img = torch.repeat_interleave(torch.arange(sizes.numel()), sizes)
+    valid = vals != invalid
+    v = vals[valid].double()
+    sums[K] = v.sum()
+    counts[K] = int(valid.sum())
+    if K:
+        local = torch.arange(vals.numel()) - o_off[img]
+        lab = gt_lab[b_off[img] + local % m[img].clamp(min=1)][valid]
+        k = torch.searchsorted(classes, lab)
+        sums[:K] = torch.zeros(K, dtype=torch.float64).index_add_(0, k, v)
+        counts[:K] = torch.bincount(k, minlength=K)
+    return sums, counts

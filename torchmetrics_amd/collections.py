@@ -284,6 +284,57 @@ class MetricCollection(ModuleDict):
             if code:
                 rank_zero_warn(msg, UserWarning)
 
+    def __getstate__(self) -> Dict[str, Any]:
+        # process-local handles: the mapped pinned status buffer (its device address) and the fused-compute plan
+        # (descriptor rows holding device pointers) are rebuilt on first use in the copy
+        state = self.__dict__.copy()
+        for k in ("_status_host", "_status_ptr", "_fused_plan", "_compute_calls", "_fused_rebuilds", "_fused_off"):
+            state.pop(k, None)
+        return state
+
+    def _fused_compute(self, members: List[Tuple[str, Metric]]) -> Tuple[Dict[str, Any], Dict[str, Any]]:
+        """The members whose compute() is only fused reductions, in ONE task-kernel launch (utils/fused_compute.py;
+        recorded at the second compute() of the collection, re-recorded when its members or their configuration
+        change)."""
+        from torchmetrics_amd.utils import fused_compute as _fc
+
+        d = self.__dict__
+        calls = d.get("_compute_calls", 0)
+        d["_compute_calls"] = calls + 1
+        if calls == 0 or d.get("_fused_off") or not _fc.enabled():
+            return {}, {}
+        ident = tuple(id(m) for _, m in members)
+        plan = d.get("_fused_plan")
+        if plan is None or plan[0] != ident or not plan[1].valid():
+            rebuilds = d.get("_fused_rebuilds", 0)
+            if rebuilds >= 8:  # members whose configuration keeps changing: stay eager
+                d["_fused_off"] = True
+                return {}, {}
+            d["_fused_rebuilds"] = rebuilds + 1
+            plan = (ident, _fc.CollectionPlan(members))
+            d["_fused_plan"] = plan
+        if not plan[1].ok:
+            return {}, {}
+        return plan[1].run()
+
+    @staticmethod
+    def _take_fused(m: Metric, value: Any) -> Any:
+        """What the member's compute() wrapper does around a value (Metric._wrap_compute): its cached value if it has
+        one, the compute-before-update warning, the cache."""
+        d = m.__dict__
+        if d["_computed"] is not None:
+            return d["_computed"]
+        if not d["_update_count"]:
+            rank_zero_warn(
+                f"The ``compute`` method of metric {m.__class__.__name__}"
+                " was called before the ``update`` method which may lead to errors,"
+                " as metric states have not yet been updated.",
+                UserWarning,
+            )
+        if d["compute_with_cache"]:
+            d["_computed"] = value
+        return value
+
     def _read_words(self, words: List[Tuple[Tensor, int]]) -> List[int]:
         """One kernel writes every word into pinned host memory, one stream sync reads them (no device->host copy)."""
         d = self.__dict__
@@ -320,9 +371,16 @@ class MetricCollection(ModuleDict):
             if method_name == "compute":
                 plan = self._defer_device_checks()
                 try:
+                    fused, fchecks = self._fused_compute(members)
+                    local = not fused or not _engine_dist_available()
                     with _deferred.defer() as dfr:
                         for k, m in members:
-                            result[k] = m.compute()
+                            val = fused.get(k) if fused else None
+                            if val is not None and (local or m.__dict__["_is_synced"]):
+                                result[k] = self._take_fused(m, val)
+                                dfr.items.extend(fchecks.get(k, ()))
+                            else:
+                                result[k] = m.compute()
                     self._finish_device_checks(plan, dfr.items)
                 except BaseException:
                     for m in self._modules.values():

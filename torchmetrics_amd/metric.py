@@ -254,7 +254,7 @@ class Metric(Module, ABC):
         self._to_sync = self.dist_sync_on_step
         self._should_unsync = False
         saved = self.compute_on_cpu
-        self.compute_on_cpu = False
+        self.__dict__["compute_on_cpu"] = False  # (lifecycle toggle: not a configuration change, see __setattr__)
         self._enable_grad = True
         return saved
 
@@ -264,7 +264,7 @@ class Metric(Module, ABC):
         self._to_sync = self.sync_on_compute
         self._computed = None
         self._enable_grad = False
-        self.compute_on_cpu = saved_compute_on_cpu
+        self.__dict__["compute_on_cpu"] = saved_compute_on_cpu
         if self.compute_on_cpu:
             self._move_list_states_to_cpu()
 
@@ -853,6 +853,10 @@ class Metric(Module, ABC):
         if name in _CONST_ATTRS:
             raise RuntimeError(f"Can't change const `{name}`.")
         d = self.__dict__
+        if name[0] != "_" and name not in d.get("_defaults", _NO_NAMES):
+            # a configuration attribute (average, num_classes, ...): plans recorded from this metric
+            # (utils/fused_compute.py) check the version before replaying
+            d["_cfg_version"] = d.get("_cfg_version", 0) + 1
         # fast path for the bookkeeping attributes and states the lifecycle rebinds on every update / compute /
         # forward (nn.Module.__setattr__ costs ~1.5-2.5 us per call): an attribute this instance already holds as a
         # plain value, that is no parameter, buffer, sub-module or class-level data descriptor, is rebound in place
@@ -914,6 +918,7 @@ class Metric(Module, ABC):
                 raise TypeError(
                     f"Expected metric state to be either a Tensor or a list of Tensor, but encountered {cur}"
                 )
+        this.__dict__["_cfg_version"] = this.__dict__.get("_cfg_version", 0) + 1  # device / dtype moved
         this.__dict__.pop("_cat_arenas", None)  # folded list states were moved out of their arenas
         this.__dict__.pop("_default_packs", None)  # the defaults were moved / cast
         this._pack_states()  # the moved / cast states are separate tensors again: one buffer per bucket

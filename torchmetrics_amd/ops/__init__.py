@@ -799,6 +799,7 @@ class _TaskRecorder:
     def __init__(self, poison: bool = False) -> None:
         self.rows: list = []
         self.keep: list = []
+        self.meta: list = []  # per row: (pointer-slot tensors, outputs) -- utils/fused_compute.py builds plans from it
         self.lds = 0
         self.anchor: Optional[Tensor] = None
         self.poison = poison
@@ -811,6 +812,7 @@ class _TaskRecorder:
         ptrs = [t.data_ptr() if t is not None else 0 for t in tensors]
         row += ptrs + [0] * (8 - len(ptrs))
         self.rows.append(row)
+        self.meta.append((list(tensors), list(outs)))
         self.keep.extend(t for t in tensors if t is not None)
         self.lds = max(self.lds, lds)
         if self.anchor is None:
@@ -825,7 +827,7 @@ class _TaskRecorder:
         for i in range(0, n, 32):
             desc = torch.tensor(self.rows[i : i + 32], dtype=torch.int64)
             _ops().compute_tasks(desc, self.anchor, self.lds)
-        self.rows, self.keep = [], []
+        self.rows, self.keep, self.meta = [], [], []
         return n
 
 

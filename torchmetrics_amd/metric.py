@@ -42,6 +42,7 @@ from torchmetrics_amd.utilities.data import (
 from torchmetrics_amd.utilities.exceptions import TorchMetricsUserError
 from torchmetrics_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_single_or_multi_val
 from torchmetrics_amd.utilities.prints import rank_zero_warn
+from torchmetrics_amd.utils import profiling as _prof
 from torchmetrics_amd.utils import validation as _validation
 
 _REDUCTION_BY_NAME = {
@@ -244,6 +245,12 @@ class Metric(Module, ABC):
                 "The Metric shouldn't be synced when performing ``forward``. "
                 "HINT: Did you forget to call ``unsync`` ?."
             )
+        if _prof.ENABLED:
+            with _prof.range(f"tm.forward/{type(self).__name__}"):
+                return self._forward_dispatch(*args, **kwargs)
+        return self._forward_dispatch(*args, **kwargs)
+
+    def _forward_dispatch(self, *args: Any, **kwargs: Any) -> Any:
         if self.full_state_update or self.full_state_update is None or self.dist_sync_on_step:
             self._forward_cache = self._forward_full_state_update(*args, **kwargs)
         else:
@@ -469,6 +476,15 @@ class Metric(Module, ABC):
 
         @functools.wraps(update)
         def wrapped_func(*args: Any, **kwargs: Any) -> None:
+            if _prof.ENABLED:
+                _prof.push(f"tm.update/{type(self).__name__}")
+                try:
+                    return _update_body(*args, **kwargs)
+                finally:
+                    _prof.pop()
+            return _update_body(*args, **kwargs)
+
+        def _update_body(*args: Any, **kwargs: Any) -> None:
             state["_computed"] = None
             state["_update_count"] += 1
             prev = torch.is_grad_enabled()
@@ -591,6 +607,15 @@ class Metric(Module, ABC):
     def _wrap_compute(self, compute: Callable) -> Callable:
         @functools.wraps(compute)
         def wrapped_func(*args: Any, **kwargs: Any) -> Any:
+            if _prof.ENABLED:
+                _prof.push(f"tm.compute/{type(self).__name__}")
+                try:
+                    return _compute_body(*args, **kwargs)
+                finally:
+                    _prof.pop()
+            return _compute_body(*args, **kwargs)
+
+        def _compute_body(*args: Any, **kwargs: Any) -> Any:
             if not self.update_called:
                 rank_zero_warn(
                     f"The ``compute`` method of metric {self.__class__.__name__}"

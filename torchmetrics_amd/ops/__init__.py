@@ -67,9 +67,9 @@ def native_updater(kind: str, state: dict, fallback: Any) -> Any:
     """A native ``update`` callable bound to a metric's ``__dict__`` (``csrc/bindings/fastcall.cpp``), or ``None``
     where it does not apply (no GPU, native library missing, ``TORCHMETRICS_AMD_STRICT=1``).  Inputs off its fast path
     go to ``fallback`` (the metric's Python update)."""
-    from torchmetrics_amd.utils import validation
+    from torchmetrics_amd.utils import profiling, validation
 
-    if validation.STRICT or not torch.cuda.is_available() or not load_native(strict=False):
+    if validation.STRICT or profiling.ENABLED or not torch.cuda.is_available() or not load_native(strict=False):
         return None
     mod = _fast_mod
     factory = getattr(mod, f"{kind}_updater", None) if not isinstance(mod, _DispatcherShim) else None
@@ -84,9 +84,9 @@ def native_forward(kind: int, state: dict, fallback: Any, stat_kind: str = "accu
     """A native ``forward`` callable bound to a metric's ``__dict__`` (``csrc/bindings/fastcall.cpp`` ``NativeForward``)
     or ``None`` where it does not apply (no GPU, native library missing, ``TORCHMETRICS_AMD_STRICT=1``,
     ``TORCHMETRICS_AMD_NATIVE_FORWARD=0``).  Calls off its fast path go to ``fallback`` (``Metric.forward``)."""
-    from torchmetrics_amd.utils import validation
+    from torchmetrics_amd.utils import profiling, validation
 
-    if (validation.STRICT or os.environ.get("TORCHMETRICS_AMD_NATIVE_FORWARD", "1") == "0"
+    if (validation.STRICT or profiling.ENABLED or os.environ.get("TORCHMETRICS_AMD_NATIVE_FORWARD", "1") == "0"
             or not torch.cuda.is_available() or not load_native(strict=False)):
         return None
     mod = _fast_mod

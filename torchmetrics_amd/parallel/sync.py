@@ -29,6 +29,7 @@ On ROCm, ``torch.distributed`` backend ``"nccl"`` *is* RCCL.  Bucket sizes are s
 (< 64 KiB: latency-bound, a single ring step over xGMI) and large only for FID (``f64[2048,2048]`` = 32 MiB, per-link
 bandwidth-bound): one collective per bucket is the right shape for both.
 """
+from contextlib import nullcontext
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple, Union
 
 import torch
@@ -36,6 +37,7 @@ import torch.distributed as dist
 from torch import Tensor
 
 from torchmetrics_amd.parallel.arena import contiguous_span
+from torchmetrics_amd.utils import profiling as _prof
 from torchmetrics_amd.parallel.oneshot import DEFAULT_SLOT_BYTES, get_oneshot
 from torchmetrics_amd.utilities.data import (
     _flatten,
@@ -168,6 +170,9 @@ class _GatherItem:
         self.fn = fn
 
 
+_NULL_CTX = nullcontext()
+
+
 def sync_state_dicts(
     entries: Sequence[Tuple[Dict[str, State], Dict[str, Any]]],
     group: Optional[Any] = None,
@@ -186,6 +191,17 @@ def sync_state_dicts(
     Returns:
         One dict of synced states per entry.
     """
+    if _prof.ENABLED:
+        with _prof.range(f"tm.sync/{sum(len(r) for _, r in entries)} states"):
+            return _sync_state_dicts(entries, group, err_word)
+    return _sync_state_dicts(entries, group, err_word)
+
+
+def _sync_state_dicts(
+    entries: Sequence[Tuple[Dict[str, State], Dict[str, Any]]],
+    group: Optional[Any],
+    err_word: Optional[Tensor],
+) -> List[Dict[str, State]]:
     world = _world_size(group)
     results: List[Dict[str, State]] = [dict() for _ in entries]
 
@@ -220,6 +236,8 @@ def sync_state_dicts(
             flat = span.to(wire, copy=True)
         else:
             flat = torch.cat([t.reshape(-1).to(wire) for _, t in members])
+        if world > 1 and _prof.ENABLED:
+            _prof.push(f"tm.sync.bucket/{kind}/{str(dtype).replace('torch.', '')}/{flat.numel() * flat.element_size()}B")
         if world > 1:
             small = flat.numel() * flat.element_size() <= DEFAULT_SLOT_BYTES
             # the communicator (IPC setup collective) is only created once a bucket small enough for it shows up
@@ -231,6 +249,8 @@ def sync_state_dicts(
                 _stats["bytes"] += flat.numel() * flat.element_size()
             else:
                 _all_reduce(flat, kind, group)
+            if _prof.ENABLED:
+                _prof.pop()
         off = 0
         for (mi, name), t in members:
             n = t.numel()
@@ -245,7 +265,8 @@ def sync_state_dicts(
             results[mi][name] = piece
 
     if gather_items:
-        gathered = _gather_items(gather_items, world, group)
+        with _prof.range(f"tm.sync.gather/{len(gather_items)} states") if _prof.ENABLED else _NULL_CTX:
+            gathered = _gather_items(gather_items, world, group)
         for item, per_rank in zip(gather_items, gathered):
             mi, name = item.key
             results[mi][name] = _finish_gather(item, per_rank)

@@ -867,6 +867,17 @@ class Metric(Module, ABC):
         self._install_native_update()
         self._install_native_forward()
 
+    def __prepare_scriptable__(self) -> "Metric":
+        """``torch.jit.script`` compiles the class's methods; the native C++ entry points installed as instance
+        attributes (``csrc/bindings/fastcall.cpp`` NativeUpdate / NativeForward) are not Python functions, so they are
+        taken off this instance first (its Python ``update`` / ``forward`` take over: same results)."""
+        d = self.__dict__
+        if type(d.get("forward")).__name__ == "NativeForward":
+            del d["forward"]
+        if type(d.get("update")).__name__ == "NativeUpdate":
+            d["update"] = d["update"].fallback
+        return self
+
     def _install_native_update(self) -> None:
         """Hook: classes with a native ``update`` entry point install it over the Python wrapper here."""
 

@@ -13,7 +13,7 @@ envelope), ``csrc/detection/coco_accumulate.hip``; elsewhere a segmented cumulat
 (category, score) for all thresholds / areas at once, a segmented reverse running-max for the envelope and one
 ``searchsorted`` + scatter per max-dets; (4) the summary is masked means.  The host only sees the final numbers.
 """
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import torch
 from torch import Tensor
@@ -34,9 +34,36 @@ def _segment_starts(sorted_keys: Tensor) -> Tensor:
     return torch.where(start, idx, torch.zeros_like(idx)).cummax(0).values
 
 
-def cat_states(seq: Sequence[Tensor], dev: torch.device, shape_tail: Tuple[int, ...] = ()) -> Tensor:
+class Packed:
+    """A per-image list state held flat: ``flat`` = the images' tensors back to back along dim 0, ``sizes`` = each
+    image's row count (``Metric._packed_state``).  ``len()`` is the number of images; :func:`cat_states` and
+    :func:`image_sizes` read it without per-image tensors."""
+
+    __slots__ = ("flat", "sizes")
+
+    def __init__(self, flat: Tensor, sizes: List[int]) -> None:
+        self.flat, self.sizes = flat, sizes
+
+    def __len__(self) -> int:
+        return len(self.sizes)
+
+    def zeros_like(self) -> "Packed":
+        return Packed(torch.zeros_like(self.flat), self.sizes)
+
+
+def image_sizes(seq: Union[Sequence[Tensor], Packed]) -> List[int]:
+    """Per-image element counts of a 1-D-per-image list state (labels, scores, ...)."""
+    if isinstance(seq, Packed):
+        return seq.sizes
+    return [x.numel() for x in seq]
+
+
+def cat_states(seq: Union[Sequence[Tensor], Packed], dev: torch.device, shape_tail: Tuple[int, ...] = ()) -> Tensor:
     """Concatenate per-image list states into one ``[N, *shape_tail]`` tensor on ``dev``: one ``cat`` when they already
     have that layout on one device (no per-image Python work), else reshaped one by one."""
+    if isinstance(seq, Packed):
+        out = seq.flat.to(dev)
+        return out if tuple(out.shape[1:]) == tuple(shape_tail) else out.reshape(-1, *shape_tail)
     seq = seq if isinstance(seq, list) else list(seq)
     if not seq:
         return torch.zeros((0, *shape_tail), device=dev)
@@ -86,8 +113,8 @@ def coco_evaluate(
     def flat(seq, dtype, shape_tail=()):
         return cat_states(seq, dev, shape_tail).to(dtype)
 
-    dsz = torch.tensor([x.numel() for x in det_labels], device=dev, dtype=torch.long)
-    gsz = torch.tensor([x.numel() for x in gt_labels], device=dev, dtype=torch.long)
+    dsz = torch.tensor(image_sizes(det_labels), device=dev, dtype=torch.long)
+    gsz = torch.tensor(image_sizes(gt_labels), device=dev, dtype=torch.long)
     img_ids = torch.arange(n_img, device=dev)
     d_img, g_img = torch.repeat_interleave(img_ids, dsz), torch.repeat_interleave(img_ids, gsz)
     d_lab, g_lab = flat(det_labels, torch.long), flat(gt_labels, torch.long)

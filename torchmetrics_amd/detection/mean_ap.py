@@ -23,7 +23,14 @@ from typing_extensions import Literal
 
 from torchmetrics_amd import ops
 from torchmetrics_amd.detection import _rle
-from torchmetrics_amd.detection._coco_eval import cat_states, coco_evaluate, coco_summarize, per_class_stats
+from torchmetrics_amd.detection._coco_eval import (
+    Packed,
+    cat_states,
+    coco_evaluate,
+    coco_summarize,
+    image_sizes,
+    per_class_stats,
+)
 from torchmetrics_amd.detection.helpers import _fix_empty_tensors, _input_validator, _validate_iou_type_arg, box_convert
 from torchmetrics_amd.metric import Metric
 from torchmetrics_amd.utilities.prints import rank_zero_warn
@@ -114,35 +121,77 @@ class MeanAveragePrecision(Metric):
             self.add_state(name, default=[], dist_reduce_fx=None)
 
     # ------------------------------------------------------------------------------------------------ update
+    _BOX_STATES = ("detection_box", "groundtruth_box")
+
     def update(self, preds: List[Dict[str, Tensor]], target: List[Dict[str, Tensor]]) -> None:
+        """Append the batch's images.  The whole batch is a handful of launches: per state ONE ``cat`` of all images
+        stored as one chunk (``Metric._append_chunk``: per-image views are only built if something reads the list),
+        one box conversion, one zero tensor for the missing ``iscrowd`` / ``area`` entries.  The reference appends
+        9 tensors per image and converts boxes image by image (``S/detection/mean_ap.py:470-511``)."""
         _input_validator(preds, target, iou_type=self.iou_type)
-        # per-image work is batched over the whole call: one box conversion for all images (the reference converts
-        # image by image, ~4 launches each) and one zero tensor for all missing `iscrowd` / `area` entries
-        det_boxes = self._convert_boxes([item["boxes"] for item in preds]) if "bbox" in self.iou_type else None
-        gt_boxes = self._convert_boxes([item["boxes"] for item in target]) if "bbox" in self.iou_type else None
-        segm = "segm" in self.iou_type
-        det_rle = _rle.encode([item["masks"] for item in preds]) if segm else None
-        gt_rle = _rle.encode([item["masks"] for item in target]) if segm else None
-        limit = self.max_detection_thresholds[-1]
-        for i, item in enumerate(preds):
-            if det_boxes is not None:
-                self.detection_box.append(det_boxes[i])
-            if det_rle is not None:
-                self.detection_mask.append(det_rle[i])
-            if self.warn_on_many_detections and len(item["labels"]) > limit:
+        if not preds:
+            return
+        if self.warn_on_many_detections:
+            limit = self.max_detection_thresholds[-1]
+            if max(len(item["labels"]) for item in preds) > limit:
                 _warning_on_too_many_detections(limit)
-            self.detection_labels.append(item["labels"])
-            self.detection_scores.append(item["scores"])
+        segm = "segm" in self.iou_type
+        if segm:
+            det_rle = _rle.encode([item["masks"] for item in preds])
+            gt_rle = _rle.encode([item["masks"] for item in target])
         crowds = self._defaults_for(target, "iscrowd")
         areas = self._defaults_for(target, "area")
-        for i, item in enumerate(target):
-            if gt_boxes is not None:
-                self.groundtruth_box.append(gt_boxes[i])
-            if gt_rle is not None:
-                self.groundtruth_mask.append(gt_rle[i])
-            self.groundtruth_labels.append(item["labels"])
-            self.groundtruth_crowds.append(item["iscrowd"] if "iscrowd" in item else crowds[i])
-            self.groundtruth_area.append(item["area"] if "area" in item else areas[i])
+        det_n = [item["labels"].shape[0] if item["labels"].ndim else 1 for item in preds]
+        gt_n = [item["labels"].shape[0] if item["labels"].ndim else 1 for item in target]
+        columns = {
+            "detection_labels": ([p["labels"] for p in preds], det_n),
+            "detection_scores": ([p["scores"] for p in preds], det_n),
+            "groundtruth_labels": ([t["labels"] for t in target], gt_n),
+            "groundtruth_crowds": ([t["iscrowd"] if "iscrowd" in t else c for t, c in zip(target, crowds)], gt_n),
+            "groundtruth_area": ([t["area"] if "area" in t else a for t, a in zip(target, areas)], gt_n),
+        }
+        if "bbox" in self.iou_type:
+            columns["detection_box"] = ([_fix_empty_tensors(p["boxes"]) for p in preds], det_n)
+            columns["groundtruth_box"] = ([_fix_empty_tensors(t["boxes"]) for t in target], gt_n)
+        for name, (parts, sizes) in columns.items():
+            flat = self._stack_images(parts, sizes, 4 if name in self._BOX_STATES else None)
+            if flat is None:  # irregular images (mixed devices / dtypes / shapes): one list entry per image
+                if name in self._BOX_STATES:
+                    parts = self._convert_boxes(parts)
+                getattr(self, name).extend(parts)
+                continue
+            if name in self._BOX_STATES and flat.numel():
+                flat = box_convert(flat, in_fmt=self.box_format, out_fmt="xywh")
+            self._append_chunk(name, flat, sizes)
+        if segm:
+            self.detection_mask.extend(det_rle)
+            self.groundtruth_mask.extend(gt_rle)
+
+    @staticmethod
+    def _stack_images(parts: List[Tensor], sizes: List[int], width: Optional[int]) -> Optional[Tensor]:
+        """The images' tensors as one ``cat`` along dim 0 when they stack exactly (one device / dtype, ``[n_i]`` or
+        ``[n_i, width]`` with ``n_i`` = the image's label count), else None."""
+        first = parts[0]
+        dev, dt = first.device, first.dtype
+        if width is None:
+            ok = all(p.ndim == 1 and p.device == dev and p.dtype == dt for p in parts)
+        else:
+            ok = all(p.ndim == 2 and p.shape[1] == width and p.device == dev and p.dtype == dt for p in parts)
+        if not ok or any(p.shape[0] != n for p, n in zip(parts, sizes)):
+            return None
+        return torch.cat(parts) if len(parts) > 1 else first
+
+    def _packed(self, name: str) -> Union[List[Tensor], "Packed"]:
+        """List state ``name`` for the evaluator: flat (:class:`Packed`) when it stacks, else the list itself
+        (memoised for the duration of one ``compute()``)."""
+        memo = self.__dict__.get("_packed_memo")
+        if memo is not None and name in memo:
+            return memo[name]
+        flat, sizes = self._packed_state(name)
+        out = getattr(self, name) if flat is None else Packed(flat, sizes)
+        if memo is not None:
+            memo[name] = out
+        return out
 
     def _convert_boxes(self, boxes: List[Tensor]) -> List[Tensor]:
         """``box_convert(..., out_fmt="xywh")`` of every non-empty ``[n, 4]`` tensor, as one batched conversion."""
@@ -172,43 +221,53 @@ class MeanAveragePrecision(Metric):
 
     # ----------------------------------------------------------------------------------------------- compute
     def _get_classes(self) -> List[int]:
-        if len(self.detection_labels) > 0 or len(self.groundtruth_labels) > 0:
-            return torch.cat(self.detection_labels + self.groundtruth_labels).unique().cpu().tolist()
-        return []
+        dev = self._state_device()
+        parts = [cat_states(self._packed(n), dev).reshape(-1).long() for n in ("detection_labels", "groundtruth_labels")]
+        labels = torch.cat(parts)
+        return labels.unique().cpu().tolist() if labels.numel() else []
 
     def _state_device(self) -> torch.device:
-        for lst in (self.detection_labels, self.groundtruth_labels):
-            if len(lst):
-                return lst[0].device
+        for name in ("detection_labels", "groundtruth_labels"):
+            st = self._packed(name)
+            if isinstance(st, Packed):
+                return st.flat.device
+            if len(st):
+                return st[0].device
         return self.device
 
     def _rle_states(self, dev: torch.device):
         """``(buffer, descriptors)`` of the detection and ground-truth mask packs (one descriptor row per mask)."""
-        det = _rle.descriptors(self.detection_mask, [x.numel() for x in self.detection_labels], dev)
-        gt = _rle.descriptors(self.groundtruth_mask, [x.numel() for x in self.groundtruth_labels], dev)
+        det = _rle.descriptors(self.detection_mask, image_sizes(self._packed("detection_labels")), dev)
+        gt = _rle.descriptors(self.groundtruth_mask, image_sizes(self._packed("groundtruth_labels")), dev)
         return det, gt
 
     def _evaluate(self, i_type: str, micro: bool) -> Dict[str, Tensor]:
         dev = self._state_device()
         classes = torch.tensor(self._get_classes(), dtype=torch.long, device=dev)
-        relabel = (lambda xs: [torch.zeros_like(x) for x in xs]) if micro else (lambda xs: list(xs))
-        n = len(self.detection_labels)
+
+        def relabel(xs):
+            if not micro:
+                return xs
+            return xs.zeros_like() if isinstance(xs, Packed) else [torch.zeros_like(x) for x in xs]
+
+        det_labels, gt_labels = self._packed("detection_labels"), self._packed("groundtruth_labels")
+        n = len(det_labels)
         boxes_ok = i_type == "bbox"
         empty_box = torch.zeros(0, 4, device=dev)
         det_rle, gt_rle = self._rle_states(dev) if "segm" in self.iou_type else (None, None)
-        gt_areas = self.groundtruth_area
+        gt_areas = self._packed("groundtruth_area")
         if len(self.iou_type) > 1:
             # with both iou types the reference keeps the ground-truth area of the mask for the bbox evaluation too
-            mask_area = torch.split(gt_rle[1][:, 2], [x.numel() for x in self.groundtruth_labels])
-            gt_areas = [torch.where(a.to(dev) > 0, a.to(dev, torch.float64), m.to(torch.float64))
-                        for a, m in zip(self.groundtruth_area, mask_area)]
+            a = cat_states(gt_areas, dev).reshape(-1)
+            m = gt_rle[1][:, 2].to(dev, torch.float64)
+            gt_areas = Packed(torch.where(a > 0, a.to(torch.float64), m), image_sizes(gt_labels))
         return coco_evaluate(
-            det_boxes=self.detection_box if boxes_ok else [empty_box] * n,  # (coco_evaluate flattens with one cat)
-            det_scores=self.detection_scores,
-            det_labels=relabel(self.detection_labels),
-            gt_boxes=self.groundtruth_box if boxes_ok else [empty_box] * n,
-            gt_labels=relabel(self.groundtruth_labels),
-            gt_crowds=self.groundtruth_crowds,
+            det_boxes=self._packed("detection_box") if boxes_ok else [empty_box] * n,
+            det_scores=self._packed("detection_scores"),
+            det_labels=relabel(det_labels),
+            gt_boxes=self._packed("groundtruth_box") if boxes_ok else [empty_box] * n,
+            gt_labels=relabel(gt_labels),
+            gt_crowds=self._packed("groundtruth_crowds"),
             gt_areas=gt_areas,
             iou_thresholds=self.iou_thresholds,
             rec_thresholds=self.rec_thresholds,
@@ -219,6 +278,13 @@ class MeanAveragePrecision(Metric):
         )
 
     def compute(self) -> dict:
+        self.__dict__["_packed_memo"] = {}
+        try:
+            return self._compute()
+        finally:
+            self.__dict__.pop("_packed_memo", None)
+
+    def _compute(self) -> dict:
         result: Dict[str, Tensor] = {}
         mdt = self.max_detection_thresholds
         for i_type in self.iou_type:
@@ -259,7 +325,7 @@ class MeanAveragePrecision(Metric):
         ONCE.  The reference gets the same dictionary from pycocotools' per-(image, class) Python loop; the previous
         version here synchronised twice per (image, class)."""
         classes = self._get_classes()
-        n_img = len(self.detection_labels)
+        n_img = len(self._packed("detection_labels"))
         if n_img == 0 or not classes:
             return IoUTable([], torch.zeros(0), np.zeros((0, 2), dtype=np.int64), np.zeros(0, dtype=np.int64))
         dev = self._state_device()
@@ -267,15 +333,15 @@ class MeanAveragePrecision(Metric):
         k = len(classes)
         max_det = self.max_detection_thresholds[-1]
 
-        def flat(lst, img_count=None):
-            sizes = torch.tensor([x.numel() for x in lst], device=dev)
+        def flat(lst):
+            sizes = torch.tensor(image_sizes(lst), device=dev)
             return cat_states(lst, dev), torch.repeat_interleave(torch.arange(len(lst), device=dev), sizes)
 
-        d_lab, d_img = flat(self.detection_labels)
-        g_lab, g_img = flat(self.groundtruth_labels)
+        d_lab, d_img = flat(self._packed("detection_labels"))
+        g_lab, g_img = flat(self._packed("groundtruth_labels"))
         d_key = d_img * k + torch.searchsorted(cls_t, d_lab.long())
         g_key = g_img * k + torch.searchsorted(cls_t, g_lab.long())
-        d_score = cat_states(self.detection_scores, dev)
+        d_score = cat_states(self._packed("detection_scores"), dev)
         # detections: by key, then descending score (stable: ties keep their input order, as argsort(-s, stable))
         by_score = torch.argsort(-d_score, stable=True)
         d_order = by_score[torch.argsort(d_key[by_score], stable=True)]
@@ -299,9 +365,9 @@ class MeanAveragePrecision(Metric):
         pd = d_order[pair_det]
         pg = g_order[g_start[ks[pair_det]] + within]
         if i_type == "bbox":
-            db = cat_states(self.detection_box, dev, (4,)).double()
-            gb = cat_states(self.groundtruth_box, dev, (4,)).double()
-            crowd = cat_states(self.groundtruth_crowds, dev).bool()
+            db = cat_states(self._packed("detection_box"), dev, (4,)).double()
+            gb = cat_states(self._packed("groundtruth_box"), dev, (4,)).double()
+            crowd = cat_states(self._packed("groundtruth_crowds"), dev).bool()
             d, g = db[pd], gb[pg]
             x1, y1 = torch.maximum(d[:, 0], g[:, 0]), torch.maximum(d[:, 1], g[:, 1])
             x2 = torch.minimum(d[:, 0] + d[:, 2], g[:, 0] + g[:, 2])
@@ -313,7 +379,7 @@ class MeanAveragePrecision(Metric):
             vals = torch.where(inter > 0, inter / union, torch.zeros_like(inter)).float()
         else:
             (dbuf, ddesc), (gbuf, gdesc) = self._rle_states(dev)
-            g_crowd = torch.cat([c.reshape(-1) for c in self.groundtruth_crowds]).to(gdesc.device).clamp(0, 1)
+            g_crowd = cat_states(self._packed("groundtruth_crowds"), gdesc.device).reshape(-1).clamp(0, 1)
             g_crowd = g_crowd.to(torch.uint8) if g_crowd.numel() else torch.zeros(0, dtype=torch.uint8,
                                                                                 device=gdesc.device)
             vals = ops.rle_iou(dbuf, ddesc, gbuf, gdesc, pd.to(ddesc.device).contiguous(),

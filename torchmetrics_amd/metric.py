@@ -764,6 +764,8 @@ class Metric(Module, ABC):
         that was never computed must not raise for data that is no longer in the state.
         """
         d = self.__dict__
+        for name in d.pop("_chunks", None) or ():
+            d[name] = []  # pending chunks of a list state: dropped with the state (rebuilt below)
         d.pop("_errors_checked_at", None)
         d.pop("_arena_repacks", None)  # a reset's fresh states are re-packed at the next sync without counting
         if not d.get("_keep_device_errors"):
@@ -850,6 +852,7 @@ class Metric(Module, ABC):
 
     # ------------------------------------------------------------------------------------------------- pickling
     def __getstate__(self) -> Dict[str, Any]:
+        self._materialize_all_chunks()
         state = {k: v for k, v in self.__dict__.items()
                  if k not in ("update", "compute", "forward", "_update_signature", "_cat_arenas", "_default_packs",
                               "_cat_attrs")}
@@ -866,6 +869,61 @@ class Metric(Module, ABC):
         self.compute: Callable = self._wrap_compute(self.compute)  # type: ignore[method-assign]
         self._install_native_update()
         self._install_native_forward()
+
+    # ------------------------------------------------------------------------------------- chunked list states
+    def _append_chunk(self, name: str, flat: Tensor, sizes: List[int]) -> None:
+        """Append ``len(sizes)`` per-sample tensors to list state ``name`` as ONE chunk: ``flat`` holds them back to
+        back along dim 0 (``sizes[i]`` rows each).  A list update of a whole batch is then one ``cat`` instead of one
+        Python append (and one tensor) per sample -- MeanAveragePrecision appends 9 per image.  The per-sample views
+        are only built when something reads the state as a list (first attribute access: ``__getattr__``; state_dict,
+        sync, pickling, ``metric_state``); computes that understand chunks read them flat (:meth:`_packed_state`)."""
+        d = self.__dict__
+        chunks = d.get("_chunks")
+        if chunks is None:
+            chunks = d["_chunks"] = {}
+        entry = chunks.get(name)
+        if entry is None:
+            entry = chunks[name] = (d.pop(name), [])  # (the samples already materialised, pending chunks)
+        entry[1].append((flat, list(sizes)))
+
+    def __getattr__(self, name: str) -> Any:
+        chunks = self.__dict__.get("_chunks")
+        if chunks and name in chunks:
+            return self._materialize_chunks(name)
+        return super().__getattr__(name)
+
+    def _materialize_chunks(self, name: str) -> List[Tensor]:
+        base, pending = self.__dict__["_chunks"].pop(name)
+        for flat, sizes in pending:
+            base.extend(torch.split(flat, sizes))
+        self.__dict__[name] = base
+        return base
+
+    def _materialize_all_chunks(self) -> None:
+        chunks = self.__dict__.get("_chunks")
+        for name in list(chunks or ()):
+            self._materialize_chunks(name)
+
+    def _packed_state(self, name: str) -> Tuple[Optional[Tensor], List[int]]:
+        """List state ``name`` as ``(flat, sizes)`` -- the samples back to back along dim 0 (one ``cat`` of the pending
+        chunks) and each sample's row count -- without building per-sample views.  ``(None, sizes)`` when the samples
+        do not stack that way (a ragged trailing shape, several devices / dtypes): read the list then."""
+        d = self.__dict__
+        chunks = d.get("_chunks")
+        if chunks and name in chunks:
+            base, pending = chunks[name]
+            parts = list(base) + [f for f, _ in pending]
+            sizes = [x.shape[0] if x.ndim else 1 for x in base] + [n for _, ns in pending for n in ns]
+        else:
+            parts = d[name] if name in d else getattr(self, name)
+            sizes = [x.shape[0] if x.ndim else 1 for x in parts]
+        if not parts:
+            return None, sizes
+        tail = parts[0].shape[1:]
+        if any(p.ndim == 0 or p.shape[1:] != tail or p.dtype != parts[0].dtype or p.device != parts[0].device
+               for p in parts):
+            return None, sizes
+        return (parts[0] if len(parts) == 1 else torch.cat(parts)), sizes
 
     def __prepare_scriptable__(self) -> "Metric":
         """``torch.jit.script`` compiles the class's methods; the native C++ entry points installed as instance
@@ -889,6 +947,9 @@ class Metric(Module, ABC):
         if name in _CONST_ATTRS:
             raise RuntimeError(f"Can't change const `{name}`.")
         d = self.__dict__
+        chunks = d.get("_chunks")
+        if chunks and name in chunks:
+            del chunks[name]  # the state is rebound (reset, sync, load): its pending chunks are no longer its value
         if name[0] != "_" and name not in d.get("_defaults", _NO_NAMES):
             # a configuration attribute (average, num_classes, ...): plans recorded from this metric
             # (utils/fused_compute.py) check the version before replaying

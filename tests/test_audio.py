@@ -355,3 +355,23 @@ def test_biquad_cascade_kernel_gpu():
     from torchmetrics_amd.functional.audio import speech_reverberation_modulation_energy_ratio as srmr
 
     assert torch.isclose(srmr(preds.cuda(), 8000).cpu(), torch.tensor([0.3354], dtype=torch.float64), atol=1e-4).all()
+
+
+@pytest.mark.gpu
+def test_stoi_segment_kernel_ragged_batch(monkeypatch):
+    """The segment kernel (csrc/audio/stoi.hip) on a batch whose signals keep different frame counts (silences), in
+    fp32 and fp64, against the host path; the kernel is the one that runs."""
+    calls = []
+    real = ops.stoi_segments
+    monkeypatch.setattr(ops, "stoi_segments", lambda *a: calls.append(1) or real(*a))
+    g = torch.Generator().manual_seed(7)
+    clean = torch.stack([_speechlike(48000, 16000, g), _speechlike(48000, 16000, g, silence=False),
+                         _speechlike(48000, 16000, g)])
+    clean[0, 20000:40000] = 0.0  # a long silence: fewer kept frames than the others
+    noisy = clean + 0.4 * torch.randn(clean.shape, generator=g, dtype=torch.float64)
+    for dt, tol in ((torch.float64, 1e-9), (torch.float32, 2e-5)):
+        for ext in (False, True):
+            a = short_time_objective_intelligibility(noisy.to(dt).cuda(), clean.to(dt).cuda(), 16000, ext)
+            b = short_time_objective_intelligibility(noisy.to(dt), clean.to(dt), 16000, ext)
+            torch.testing.assert_close(a.cpu(), b, rtol=tol, atol=tol)
+    assert len(calls) == 4

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp PYTHONPATH="$GRAFT_REPO_ROOT"
-timeout -k 10 300 python -u -m pytest tests/test_native_forward_gpu.py tests/test_native_update.py tests/test_stream_kernels_gpu.py tests/test_macro_curves.py tests/test_iou_module.py tests/test_fused_compute_gpu.py tests/test_functional_kernels_gpu.py tests/test_torchscript.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4_pytest_fwd.log 2>&1 || { tail -60 gpurun_out/r4_pytest_fwd.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_native_forward_gpu.py tests/test_native_update.py tests/test_stream_kernels_gpu.py tests/test_macro_curves.py tests/test_iou_module.py tests/test_fused_compute_gpu.py tests/test_functional_kernels_gpu.py tests/test_torchscript.py tests/test_audio.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4_pytest_fwd.log 2>&1 || { tail -60 gpurun_out/r4_pytest_fwd.log; exit 1; }
 tail -2 gpurun_out/r4_pytest_fwd.log
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4_pytest_gpu.log 2>&1 || { tail -40 gpurun_out/r4_pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/r4_pytest_gpu.log

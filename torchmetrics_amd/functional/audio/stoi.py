@@ -9,7 +9,9 @@ The reference calls the ``pystoi`` package per sample on the host (NumPy).  This
    dropped, the kept frames overlap-added back (per signal: the kept-frame count is data dependent);
 3. 512-point FFT of the frames (rocFFT on ROCm), one-third-octave band energies (15 bands from 150 Hz) by a
    ``[15, 257]`` band matrix product;
-4. 30-frame sliding segments (``unfold``), clipping + normalisation and correlation, averaged over bands/segments.
+4. 30-frame sliding segments, clipping + normalisation and correlation, averaged over bands/segments: on ROCm one
+   kernel over every segment of the batch (``csrc/audio/stoi.hip``, fp64, envelope windows staged in LDS), on the
+   host ``unfold`` + tensor ops.
 
 Steps 3-4 run for all signals at once, padded to the longest kept length and masked.  Signals with fewer than 30
 kept frames return 1e-5 with a ``RuntimeWarning``, as pystoi does.  The extended variant's row/column normalisation
@@ -163,9 +165,19 @@ def _stoi_batch(x: Tensor, y: Tensor, extended: bool) -> Tensor:
     if x_tob.shape[-1] < N_SEG:
         warnings.warn(_SHORT_MSG, RuntimeWarning)
         return short_val
+    m_valid = (n_frames - N_SEG + 1).clamp(min=0)  # segments entirely inside each signal's kept frames
+    short = m_valid < 1
+    if x_tob.is_cuda:
+        # every segment of every signal in one launch, fp64, windows staged in LDS (csrc/audio/stoi.hip)
+        from torchmetrics_amd import ops
+
+        sums = ops.stoi_segments(x_tob, y_tob, n_frames, extended)
+        vals = (sums / (m_valid.clamp(min=1) * (1 if extended else NUMBAND))).to(x.dtype)
+        if bool(short.any()):
+            warnings.warn(_SHORT_MSG, RuntimeWarning)
+        return torch.where(short, short_val, vals)
     xseg = x_tob.unfold(-1, N_SEG, 1).transpose(1, 2)  # [B, M, J, N]
     yseg = y_tob.unfold(-1, N_SEG, 1).transpose(1, 2)
-    m_valid = (n_frames - N_SEG + 1).clamp(min=0)  # segments entirely inside each signal's kept frames
     seg_mask = (torch.arange(xseg.shape[1], device=x.device)[None, :] < m_valid[:, None]).to(x.dtype)
     if extended:
         def _unit(s: Tensor, dim: int) -> Tensor:
@@ -190,7 +202,6 @@ def _stoi_batch(x: Tensor, y: Tensor, extended: bool) -> Tensor:
         xc = xc / (torch.linalg.norm(xc, dim=-1, keepdim=True) + EPS)
         corr = (y_primes * xc).sum(dim=(-1, -2))  # [B, M]
         vals = torch.where(seg_mask > 0, corr, torch.zeros_like(corr)).sum(-1) / (m_valid.clamp(min=1) * NUMBAND)
-    short = m_valid < 1
     if bool(short.any()):
         warnings.warn(_SHORT_MSG, RuntimeWarning)
     return torch.where(short, short_val, vals)

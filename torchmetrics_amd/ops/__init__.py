@@ -1621,6 +1621,13 @@ def hinge_update(preds: Tensor, target: Tensor, mode: int, squared: bool, ignore
                         ignore_index is not None, ws[0], ws[1], measures, total, flag)
 
 
+def stoi_segments(x_tob: Tensor, y_tob: Tensor, nframes: Tensor, extended: bool) -> Tensor:
+    """Sum over each signal's valid 30-frame segments of the (extended) STOI segment correlation of ``[B, 15, F]``
+    band envelopes (``csrc/audio/stoi.hip``); fp64 ``[B]``."""
+    return _ops().stoi_segments(x_tob.contiguous(), y_tob.contiguous(), nframes.to(torch.int64).contiguous(),
+                                bool(extended))
+
+
 def linear_sum_assignment(cost: Tensor, maximize: bool = False) -> Tensor:
     """Optimal assignment of every ``[n, n]`` problem in a ROCm ``[B, n, n]`` cost batch (one wave per problem,
     Hungarian method; ``csrc/audio/lsa.hip``).  Returns int64 ``[B, n]``: the column of each row."""

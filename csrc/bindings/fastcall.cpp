@@ -657,7 +657,9 @@ int confmat_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** res
   return forward_bookkeeping(self, st, batch, result);
 }
 
-int stats_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** result, int fkind) {
+// update_only: the family's ``update`` (accumulate the batch into the global states, the reference's in-place
+// ``_update_state``) -- the same checks and kernels as the forward below without the batch score.
+int stats_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** result, int fkind, bool update_only = false) {
   if (!THPVariable_Check(a) || !THPVariable_Check(b)) return 0;
   const at::Tensor& p = THPVariable_Unpack(a);
   const at::Tensor& t = THPVariable_Unpack(b);
@@ -666,11 +668,11 @@ int stats_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** resul
   const int dev = p.get_device();
   if (t.get_device() != dev) return 0;
   PyObject* st = self->state;
-  if (!forward_allowed(st)) return 0;
+  if (update_only ? PyDict_GetItem(st, g_k_cpu) != Py_False : !forward_allowed(st)) return 0;
   PyObject* md = PyDict_GetItem(st, g_k_mdavg);
   if (md == nullptr || !PyUnicode_Check(md) || PyUnicode_CompareWithASCIIString(md, "global") != 0) return 0;
   double beta = 1.0;
-  if (self->stat_kind == 5) {
+  if (self->stat_kind == 5 && !update_only) {
     PyObject* bo = PyDict_GetItem(st, g_k_beta);
     if (bo == nullptr || !PyFloat_Check(bo) && !PyLong_Check(bo)) return 0;
     beta = PyFloat_AsDouble(bo);
@@ -689,7 +691,7 @@ int stats_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** resul
     size = PyLong_AsLongLong(co);
     if (p.dim() != 2 || t.dim() != 1 || p.size(1) != size || p.size(0) != t.size(0)) return 0;
     micro = PyDict_GetItem(st, g_k_micro) == Py_True;
-    avg = micro ? 0 : read_average(st);
+    avg = micro ? 0 : (update_only ? 1 : read_average(st));
   } else if (fkind == kFwdBinary) {
     size = 1;
     if (p.dim() != 1 || t.dim() != 1 || p.size(0) != t.size(0)) return 0;
@@ -699,7 +701,7 @@ int stats_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** resul
     if (lo == nullptr || !PyLong_CheckExact(lo)) return 0;
     size = PyLong_AsLongLong(lo);
     if (p.dim() != 2 || t.dim() != 2 || p.size(1) != size || p.sizes() != t.sizes()) return 0;
-    avg = read_average(st);
+    avg = update_only ? 1 : read_average(st);
   }
   if (avg < 0) return 0;
   double threshold = 0.5;
@@ -715,12 +717,37 @@ int stats_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** resul
   const at::Tensor* tn = state_tensor(st, g_k_tn, dev, ssize);
   const at::Tensor* fn = state_tensor(st, g_k_fn, dev, ssize);
   if (tp == nullptr || fp == nullptr || tn == nullptr || fn == nullptr) return 0;
-  if (!states_unobserved(st, {g_k_tp, g_k_fp, g_k_tn, g_k_fn})) return 0;
+  if (!update_only && !states_unobserved(st, {g_k_tp, g_k_fp, g_k_tn, g_k_fn})) return 0;
   const at::Tensor* flag = forward_flag(self, st, dev);
   if (flag == nullptr) return 0;
   at::Tensor ws, not_prob;
   const bool mc = fkind == kFwdMulticlass;
   if (!workspace(st, dev, mc ? 3 * size + 1 : 7 * size, ws, mc ? nullptr : &not_prob)) return 0;
+  if (update_only) {
+    try {
+      if (mc) {
+        tm_amd::mc_update(p, t, ws, *flag, size, ignore, has_ignore, 1, false);
+        tm_amd::mc_stats_finalize(ws, size, micro, true, *tp, *fp, *tn, *fn);
+      } else {
+        tm_amd::bin_update(p, t, ws, *flag, not_prob, size, threshold, ignore, has_ignore, false, true);
+        tm_amd::bin_stats_finalize(ws, not_prob, true, *tp, *fp, *tn, *fn);
+      }
+    } catch (const c10::Error& e) {
+      PyErr_SetString(PyExc_RuntimeError, e.what_without_backtrace());
+      return -1;
+    }
+    PyObject* cnt = PyDict_GetItem(st, g_k_count);
+    if (cnt == nullptr || !PyLong_CheckExact(cnt)) return -1;
+    PyObject* n1 = PyLong_FromLongLong(PyLong_AsLongLong(cnt) + 1);
+    if (n1 == nullptr) return -1;
+    const int rc = PyDict_SetItem(st, g_k_count, n1);
+    Py_DECREF(n1);
+    if (rc != 0) return -1;
+    ++self->calls;
+    Py_INCREF(Py_None);
+    *result = Py_None;
+    return 1;
+  }
   const bool per_class = avg == 3 && !micro;
   at::Tensor out;
   try {
@@ -748,6 +775,43 @@ int bin_stats_forward_fast(NativeUpdate* self, PyObject* a, PyObject* b, PyObjec
 }
 int ml_stats_forward_fast(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** r) {
   return stats_forward(self, a, b, r, kFwdMultilabel);
+}
+int mc_stats_update_fast(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** r) {
+  return stats_forward(self, a, b, r, kFwdMulticlass, true);
+}
+int bin_stats_update_fast(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** r) {
+  return stats_forward(self, a, b, r, kFwdBinary, true);
+}
+int ml_stats_update_fast(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** r) {
+  return stats_forward(self, a, b, r, kFwdMultilabel, true);
+}
+
+// stats_updater(kind, state_dict, fallback) -> callable: the stat-score family's native update (kind 1 multiclass,
+// 2 binary, 3 multilabel; see stats_forward)
+PyObject* make_stats_updater(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 3 || !PyLong_Check(args[0]) || !PyDict_Check(args[1]) || !PyCallable_Check(args[2])) {
+    PyErr_SetString(PyExc_TypeError, "stats_updater(kind: int, state: dict, fallback: callable)");
+    return nullptr;
+  }
+  const long kind = PyLong_AsLong(args[0]);
+  if (kind < 1 || kind > 3) {
+    PyErr_SetString(PyExc_ValueError, "stats_updater: bad kind");
+    return nullptr;
+  }
+  auto* self = PyObject_GC_New(NativeUpdate, &NativeUpdateType);
+  if (self == nullptr) return nullptr;
+  self->vectorcall = native_update_vectorcall;
+  Py_INCREF(args[1]);
+  self->state = args[1];
+  Py_INCREF(args[2]);
+  self->fallback = args[2];
+  self->sink = nullptr;
+  self->calls = 0;
+  static const FastFn kFns[] = {nullptr, mc_stats_update_fast, bin_stats_update_fast, ml_stats_update_fast};
+  self->fast = kFns[kind];
+  self->stat_kind = 0;
+  PyObject_GC_Track(reinterpret_cast<PyObject*>(self));
+  return reinterpret_cast<PyObject*>(self);
 }
 
 PyTypeObject NativeForwardType = {PyVarObject_HEAD_INIT(nullptr, 0)};
@@ -784,6 +848,8 @@ PyObject* make_forward(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
 }
 
 PyMethodDef kFactoryMethods[] = {
+    {"stats_updater", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&make_stats_updater)),
+     METH_FASTCALL, "native update of the stat-score family bound to a metric's __dict__"},
     {"forward_native", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&make_forward)), METH_FASTCALL,
      "native Metric.forward of the confusion-matrix / stat-score families bound to a metric's __dict__"},
     {"confmat_updater", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&make_confmat_updater)),

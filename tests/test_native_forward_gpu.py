@@ -210,3 +210,38 @@ def test_collection_forward_uses_native_members():
     out, exp = coll.compute(), ref.compute()
     for k in exp:
         torch.testing.assert_close(out[k].cpu(), exp[k])
+
+
+@pytest.mark.parametrize("make", [
+    lambda: tm.classification.MulticlassAccuracy(10, average="micro"),
+    lambda: tm.classification.MulticlassF1Score(1000, ignore_index=3),
+    lambda: tm.classification.MulticlassStatScores(37, average=None),
+    lambda: tm.classification.BinaryPrecision(),
+    lambda: tm.classification.MultilabelRecall(19),
+])
+def test_native_stat_update(make):
+    m, ref = make().to(DEV), make()
+    assert type(m.update).__name__ == "NativeUpdate"
+    g = torch.Generator().manual_seed(11)
+    for i in range(4):
+        if isinstance(ref, tm.classification.MulticlassStatScores):
+            C = ref.num_classes
+            p, t = torch.randn(300 + i, C, generator=g).to(torch.bfloat16), torch.randint(0, C, (300 + i,), generator=g)
+        elif isinstance(ref, tm.classification.MultilabelStatScores):
+            p, t = torch.rand(300 + i, 19, generator=g), torch.randint(0, 2, (300 + i, 19), generator=g)
+        else:
+            p, t = torch.randn(300 + i, generator=g), torch.randint(0, 2, (300 + i,), generator=g)
+        m.update(p.to(DEV), t.to(DEV))
+        ref.update(p, t)
+    assert m.update.native_calls == 3 and m.update_count == 4
+    torch.testing.assert_close(m.compute().cpu(), ref.compute())
+
+
+def test_native_stat_update_fallbacks():
+    m = tm.classification.MulticlassAccuracy(10, top_k=2).to(DEV)
+    p, t = torch.randn(64, 10), torch.randint(0, 10, (64,))
+    m.update(p.to(DEV), t.to(DEV))
+    m.update(p.to(DEV), t.to(DEV))
+    assert m.update.native_calls == 0  # top_k > 1: the Python update (fused top-k kernel)
+    torch.testing.assert_close(m.compute().cpu(), tm.functional.multiclass_accuracy(p, t, 10, top_k=2))
+    assert type(_Shifted(5).to(DEV).update).__name__ != "NativeUpdate"

@@ -50,7 +50,29 @@ class _AbstractStatScores(Metric):
                 dist_reduce_fx="cat" if samplewise else "sum",
             )
         self._ws = _StatWorkspace()
+        self._install_native_update()
         self._install_native_forward()
+
+    def _native_family(self) -> Optional[type]:
+        cls = type(self)
+        family = next((c for c in (MulticlassStatScores, MultilabelStatScores, BinaryStatScores) if isinstance(self, c)),
+                      None)
+        if family is None or cls.update is not family.update or getattr(self, "multidim_average", None) != "global":
+            return None
+        return family
+
+    def _install_native_update(self) -> None:
+        """ROCm: ``update`` = the update kernel + the fold into the states, driven from C++ (csrc/bindings/
+        fastcall.cpp ``stats_updater``); inputs off its fast path (CPU, top_k > 1, other shapes / dtypes) run the
+        Python ``update``."""
+        family = self._native_family()
+        if family is None:
+            return
+        kind = {MulticlassStatScores: ops.FWD_MULTICLASS, MultilabelStatScores: ops.FWD_MULTILABEL,
+                BinaryStatScores: ops.FWD_BINARY}[family]
+        fast = ops.native_updater("stats", self.__dict__, self.__dict__["update"], kind)
+        if fast is not None:
+            self.__dict__["update"] = fast
 
     def _install_native_forward(self) -> None:
         """ROCm: ``forward`` = the update kernel + one fused fold-and-score launch, driven from C++ (the batch value is

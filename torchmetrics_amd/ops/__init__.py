@@ -63,7 +63,7 @@ def _fast():
     return _fast_mod
 
 
-def native_updater(kind: str, state: dict, fallback: Any) -> Any:
+def native_updater(kind: str, state: dict, fallback: Any, *extra: Any) -> Any:
     """A native ``update`` callable bound to a metric's ``__dict__`` (``csrc/bindings/fastcall.cpp``), or ``None``
     where it does not apply (no GPU, native library missing, ``TORCHMETRICS_AMD_STRICT=1``).  Inputs off its fast path
     go to ``fallback`` (the metric's Python update)."""
@@ -73,7 +73,9 @@ def native_updater(kind: str, state: dict, fallback: Any) -> Any:
         return None
     mod = _fast_mod
     factory = getattr(mod, f"{kind}_updater", None) if not isinstance(mod, _DispatcherShim) else None
-    return factory(state, fallback) if factory is not None else None
+    if factory is None:
+        return None
+    return factory(*extra, state, fallback) if extra else factory(state, fallback)
 
 
 FWD_CONFMAT, FWD_MULTICLASS, FWD_BINARY, FWD_MULTILABEL = 0, 1, 2, 3

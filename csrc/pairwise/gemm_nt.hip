@@ -339,6 +339,288 @@ __global__ __launch_bounds__(kNT) void gemm_nt_kernel(const float* __restrict__ 
   }
 }
 
+// ------------------------------------------------------------------------------------------------ 256 x 256 tiles
+// Large problems (D % 32 == 0, both sides >= 256): block tile 256 x 256, 8 waves as 2 (rows) x 4 (columns), wave tile
+// 128 x 64 = 4 x 2 MFMA 32x32 tiles (128 accumulators per lane), k-step 32.  Versus the 128 x 128 kernel above this
+// halves the LDS traffic and the barriers per MFMA, and stages global -> LDS with global_load_lds_dwordx4 (no VGPR
+// round trip, no write pass): two 64 KiB LDS stages, the next k-chunk's DMAs in flight while the current one is
+// multiplied, ONE barrier per k-chunk (the barrier that publishes chunk k also proves every wave finished chunk k-1,
+// so chunk k+1 may be staged into that buffer right after it).  The 128 x 128 kernel's waves spent 84 % of their
+// cycles in s_waitcnt at 4096^2 x 2048 (profiles/r03_gemm_vs_hipblaslt.md).
+//
+// LDS image: per operand 256 rows x 8 16-byte chunks (128 B rows, unpadded: a DMA instruction writes 1 KiB = 8 rows
+// lane-linearly), chunk c of row r stored at c ^ ((r >> 1) & 7) -- the swizzle is applied on the global SOURCE
+// address of each lane, and makes the fragment reads (32 rows x one chunk per lane half) bank-conflict free.
+constexpr int kGM = 256, kGN = 256, kGT = 512, kGK = 32;
+
+template <int EPI>
+__global__ __launch_bounds__(kGT) void gemm_nt_big_kernel(const float* __restrict__ X, const float* __restrict__ Y,
+                                                          int N, int M, int D, long long bx, long long by, int tiles_m,
+                                                          EpiParams ep) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // [2 stages][A 256 x 32 | B 256 x 32]
+  constexpr int kStage = (kGM + kGN) * kGK;                    // floats per stage
+  const int batch = blockIdx.z;
+  const int32_t* gix = ep.ix ? ep.ix + (long long)batch * N : nullptr;
+  const int32_t* giy = ep.iy ? ep.iy + (long long)batch * M : nullptr;
+  if (!gix) X += batch * bx;
+  if (!giy) Y += batch * by;
+  auto xrow = [&](int i) -> const float* { return X + (long long)(gix ? gix[i] : i) * D; };
+  auto yrow = [&](int j) -> const float* { return Y + (long long)(giy ? giy[j] : j) * D; };
+  const int tiles_n = (N + kGM - 1) / kGM;
+  const int total = tiles_n * tiles_m;
+  const int bid = blockIdx.x;
+  const int per = (total + 7) / 8;
+  const int tile = (bid % 8) * per + bid / 8;  // XCD-aware: each XCD takes a contiguous band of row-major tiles
+  if (tile >= total) return;
+  const int ti = tile / tiles_m, tj = tile - ti * tiles_m;
+  const int row0 = ti * kGM, col0 = tj * kGN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = (wave >> 2) * 128, wc = (wave & 3) * 64;
+  const int h = lane >> 5, r = lane & 31;
+
+  // DMA sources: wave w moves rows [32 w, 32 w + 32) of each operand tile, 8 rows (1 KiB) per instruction; lane l
+  // of instruction q covers row 32 w + 8 q + l / 8, LDS chunk l % 8 = logical chunk (l % 8) ^ ((row >> 1) & 7).
+  // Rows past N / M read a valid row (their products are never stored).
+  const float* srcA[4];
+  const float* srcB[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int rr = 32 * wave + 8 * q + (lane >> 3);
+    const int c = (lane & 7) ^ ((rr >> 1) & 7);
+    const int gi = min(row0 + rr, N - 1), gj = min(col0 + rr, M - 1);
+    srcA[q] = xrow(gi) + 4 * c;
+    srcB[q] = yrow(gj) + 4 * c;
+  }
+  typedef __attribute__((address_space(3))) void lds_t;
+  typedef __attribute__((address_space(1))) void glb_t;
+  auto stage = [&](int kc, int buf) {
+    float* sa = smem + buf * kStage;
+    float* sb = sa + kGM * kGK;
+    const int k0 = kc * kGK;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      __builtin_amdgcn_global_load_lds((glb_t*)(srcA[q] + k0), (lds_t*)(sa + (32 * wave + 8 * q) * kGK), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_t*)(srcB[q] + k0), (lds_t*)(sb + (32 * wave + 8 * q) * kGK), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  // fragment addresses: lane (r, h) reads row wr + 32 a + r (A) / wc + 32 b + r (B), logical chunk 4 h + q
+  const int swz_a = ((wr + r) >> 1) & 7;  // (32 a keeps (row >> 1) & 7: 32 rows shift it by 16)
+  const int swz_b = ((wc + r) >> 1) & 7;
+  const int nk = D / kGK;
+  stage(0, 0);
+  for (int kc = 0; kc < nk; ++kc) {
+    const int buf = kc & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk kc (the only ones in flight)
+    __builtin_amdgcn_s_barrier();                     // ... and every other wave's; all done with chunk kc - 1
+    if (kc + 1 < nk) stage(kc + 1, buf ^ 1);          // in flight during this chunk's MFMAs
+    const float* sa = smem + buf * kStage + (wr + r) * kGK;
+    const float* sb = smem + buf * kStage + kGM * kGK + (wc + r) * kGK;
+    f32x4 ca[4], cb[2];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) ca[a] = *reinterpret_cast<const f32x4*>(sa + 32 * a * kGK + 4 * ((4 * h) ^ swz_a));
+#pragma unroll
+    for (int b = 0; b < 2; ++b) cb[b] = *reinterpret_cast<const f32x4*>(sb + 32 * b * kGK + 4 * ((4 * h) ^ swz_b));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 na[4], nb[2];
+      if (q < 3) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+          na[a] = *reinterpret_cast<const f32x4*>(sa + 32 * a * kGK + 4 * ((4 * h + q + 1) ^ swz_a));
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          nb[b] = *reinterpret_cast<const f32x4*>(sb + 32 * b * kGK + 4 * ((4 * h + q + 1) ^ swz_b));
+      }
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[a][s4], cb[b][s4], acc[a][b], 0, 0, 0);
+      if (q < 3) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) ca[a] = na[a];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) cb[b] = nb[b];
+      }
+    }
+  }
+
+  // ----------------------------------------------------------------------------------------------- epilogue
+  // acc[a][b][e]: row = wr + 32a + (e & 3) + 8 (e >> 2) + 4h, col = wc + 32b + r.  Reduction scratch reuses the
+  // staging LDS after every wave is done with it (no DMA is in flight: the last chunk issued none).
+  __syncthreads();
+  if constexpr (EPI == kStore || EPI == kEuclid || EPI == kCosine) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int j = col0 + wc + 32 * b + r;
+        if (j >= M) continue;
+        float nyj = 0.f;
+        if constexpr (EPI != kStore) nyj = ep.ny[batch * (long long)M + j];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (i >= N) continue;
+          float v = acc[a][b][e];
+          if constexpr (EPI == kStore) {
+            v = (ep.zero_diag && i == j) ? 0.f : v * ep.scale;
+          } else if constexpr (EPI == kCosine) {
+            v = (ep.zero_diag && i == j) ? 0.f : v * ep.nx[batch * (long long)N + i] * nyj * ep.scale;
+          } else {
+            const float s2 = ep.nx[batch * (long long)N + i] + nyj;
+            float d2 = s2 - 2.0f * v;
+            if (d2 < s2 * (1.0f / 128.0f)) {
+              const float* xr = xrow(i);
+              const float* yr = yrow(j);
+              float t = 0.f;
+              for (int k = 0; k < D; ++k) {
+                const float d = xr[k] - yr[k];
+                t = fmaf(d, d, t);
+              }
+              d2 = t;
+            }
+            d2 = fmaxf(d2, 0.f);
+            if (ep.zero_diag && i == j) d2 = 0.f;
+            v = ep.sqrt_out ? sqrtf(d2) : d2;
+          }
+          ep.out[batch * (long long)N * ep.ldo + (long long)i * ep.ldo + j] = v;
+        }
+      }
+  } else if constexpr (EPI == kPolySum) {
+    double part = 0.0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int j = col0 + wc + 32 * b + r;
+        if (j >= M) continue;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (i >= N || (ep.zero_diag && i == j)) continue;
+          part += static_cast<double>(ipow(fmaf(acc[a][b][e], ep.scale, ep.coef), ep.degree));
+        }
+      }
+    part = wave_sum(part);
+    double* red = reinterpret_cast<double*>(smem);
+    if (lane == 0) red[wave] = part;
+    __syncthreads();
+    if (tid == 0) {
+      double t = 0.0;
+      for (int w = 0; w < kGT / 64; ++w) t += red[w];
+      ep.dpart[(long long)batch * gridDim.x + tile] = t;
+    }
+  } else if constexpr (EPI == kRowColMax) {
+    float* redr = smem;            // [4 wave columns][kGM]
+    float* redc = smem + 4 * kGM;  // [2 wave rows][kGN]
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int il = wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int i = row0 + il;
+        float v = -3.0e38f;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int j = col0 + wc + 32 * b + r;
+          if (j < M && i < N) v = fmaxf(v, acc[a][b][e] * ep.scale);
+        }
+#pragma unroll
+        for (int off = 16; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+        if (r == 0) redr[(wave & 3) * kGM + il] = v;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int jl = wc + 32 * b + r;
+      float v = -3.0e38f;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (i < N && col0 + jl < M) v = fmaxf(v, acc[a][b][e] * ep.scale);
+        }
+      v = fmaxf(v, __shfl_xor(v, 32, 64));
+      if (h == 0) redc[(wave >> 2) * kGN + jl] = v;
+    }
+    __syncthreads();
+    if (tid < kGM) {
+      const int i = row0 + tid;
+      if (i < N)
+        ep.out[(long long)batch * N * ep.part_cols + (long long)i * ep.part_cols + tj] =
+            fmaxf(fmaxf(redr[tid], redr[kGM + tid]), fmaxf(redr[2 * kGM + tid], redr[3 * kGM + tid]));
+    } else {
+      const int jl = tid - kGM, j = col0 + jl;
+      if (j < M) ep.out2[((long long)batch * tiles_n + ti) * M + j] = fmaxf(redc[jl], redc[kGN + jl]);
+    }
+  } else {
+    float* red = smem;  // [4 wave columns][kGM]
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int il = wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int i = row0 + il;
+        float v = EPI == kRowMin ? 3.0e38f : 0.f;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int j = col0 + wc + 32 * b + r;
+          if (j >= M || i >= N) continue;
+          float x = acc[a][b][e];
+          if constexpr (EPI == kRowMin) {
+            x = 1.0f - fabsf(x * ep.nx[batch * (long long)N + i] * ep.ny[batch * (long long)M + j]);
+            v = fminf(v, x);
+          } else {
+            v += x * ep.scale;
+          }
+        }
+#pragma unroll
+        for (int off = 16; off > 0; off >>= 1) {
+          const float o = __shfl_xor(v, off, 64);
+          v = EPI == kRowMin ? fminf(v, o) : v + o;
+        }
+        if (r == 0) red[(wave & 3) * kGM + il] = v;
+      }
+    }
+    __syncthreads();
+    if (tid < kGM) {
+      const int i = row0 + tid;
+      if (i < N) {
+        const float v = EPI == kRowMin
+                            ? fminf(fminf(red[tid], red[kGM + tid]), fminf(red[2 * kGM + tid], red[3 * kGM + tid]))
+                            : (red[tid] + red[kGM + tid]) + (red[2 * kGM + tid] + red[3 * kGM + tid]);
+        ep.out[(long long)batch * N * ep.part_cols + (long long)i * ep.part_cols + tj] = v;
+      }
+    }
+  }
+}
+
+// The 256 x 256 kernel for large problems: D a multiple of its k-step, both sides at least one tile, enough tiles to
+// fill the chip once; TM_AMD_GEMM_BIG=0|1 forces it off / on (where it applies).
+bool big_choice(int N, int M, int D, int batches) {
+  static const int forced = [] {
+    const char* e = std::getenv("TM_AMD_GEMM_BIG");
+    return e ? (e[0] == '0' ? 0 : 1) : -1;
+  }();
+  if (D % kGK != 0 || N < kGM || M < kGN || forced == 0) return false;
+  if (forced == 1) return true;
+  const long long tiles = static_cast<long long>((N + kGM - 1) / kGM) * ((M + kGN - 1) / kGN) * batches;
+  return tiles >= 128 && static_cast<long long>(N) * M * D * batches >= (1LL << 30);
+}
+
 // LDS stages: double buffering (74 KB, 2 blocks/CU) pays for long K loops; for short ones the single buffer's higher
 // occupancy (37 KB, 3 blocks/CU: the next tile's loads overlap this tile's epilogue) wins (benchmarks/bench_gemm.py).
 // TM_AMD_GEMM_STAGES=1|2 overrides.
@@ -370,6 +652,14 @@ void launch_one(const at::Tensor& x, const at::Tensor& y, dim3 grid, int N, int 
 template <int EPI>
 void launch(const at::Tensor& x, const at::Tensor& y, int batches, long long bx, long long by, int N, int M, int D,
             const EpiParams& ep) {
+  if (big_choice(N, M, D, batches)) {
+    const int tiles_n = (N + kGM - 1) / kGM, tiles_m = (M + kGN - 1) / kGN;
+    const int per = (tiles_n * tiles_m + 7) / 8;
+    const size_t lds = 2ull * (kGM + kGN) * kGK * sizeof(float);
+    hipLaunchKernelGGL((gemm_nt_big_kernel<EPI>), dim3(per * 8, 1, batches), dim3(kGT), lds, stream(),
+                       x.data_ptr<float>(), y.data_ptr<float>(), N, M, D, bx, by, tiles_m, ep);
+    return;
+  }
   const int tiles_n = (N + kBM - 1) / kBM, tiles_m = (M + kBN - 1) / kBN;
   const int total = tiles_n * tiles_m;
   const int per = (total + 7) / 8;
@@ -424,7 +714,9 @@ at::Tensor gemm_nt(const at::Tensor& x, const at::Tensor& y, int64_t kind, const
               "gemm_nt: 16-byte aligned operands");
   TORCH_CHECK(D % 4 == 0, "gemm_nt: D must be a multiple of 4 (float4 rows)");
   TORCH_CHECK(static_cast<long long>(N) * M * B < (1LL << 40), "gemm_nt: output too large");
-  const int tiles_n = (N + kBM - 1) / kBM, tiles_m = (M + kBN - 1) / kBN;
+  const bool big = big_choice(N, M, D, B);
+  const int tbm = big ? kGM : kBM, tbn = big ? kGN : kBN;
+  const int tiles_n = (N + tbm - 1) / tbm, tiles_m = (M + tbn - 1) / tbn;
   const int blocks = ((tiles_n * tiles_m + 7) / 8) * 8;
   auto f32 = x.options();
   ep.scale = static_cast<float>(scale);

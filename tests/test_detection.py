@@ -507,3 +507,40 @@ def test_coco_accumulate_kernel_matches_torch_path(monkeypatch):
     ref = run()
     for key in ("precision", "recall", "scores", "map", "map_per_class", "mar_50_per_class", "mar_small"):
         assert torch.equal(fused[key], ref[key]), key
+
+
+def _ddp_map_packed(rank, world, preds, target):
+    """The per-image states cross the engine flat (Metric._packed_sync_plan); rank 1 holds one image more than rank 0
+    and updates twice; after compute() the local (chunked, unbuilt) states are back; the synced order is element-major
+    as the reference's per-element gather (image 0 of every rank, then image 1, ...)."""
+    from torchmetrics_amd.parallel.sync import comm_stats
+
+    mine = list(range(rank, len(preds), world)) + ([len(preds) - 1] if rank == 1 else [])
+    m = MeanAveragePrecision()
+    m.update([preds[i] for i in mine[:2]], [target[i] for i in mine[:2]])
+    m.update([preds[i] for i in mine[2:]], [target[i] for i in mine[2:]])
+    assert "_chunks" in m.__dict__ and "detection_box" in m.__dict__["_chunks"]
+    comm_stats(reset=True)
+    res = m.compute()
+    stats = comm_stats()
+    assert stats["all_gather"] <= 4, stats  # one header + one payload per dtype bucket, not one per image
+    assert "detection_box" in m.__dict__["_chunks"]  # unsync restored the chunks unbuilt
+    allp = [preds[i] for i in range(len(preds))] + [preds[-1]]
+    allt = [target[i] for i in range(len(target))] + [target[-1]]
+    stats_ref, _, _ = _oracle(allp, allt)
+    assert_close(res["map"], stats_ref[0], atol=1e-6)
+    assert_close(res["mar_100"], stats_ref[8], atol=1e-6)
+    m.sync()
+    lab = m.detection_labels
+    per_rank = [list(range(r, len(preds), world)) + ([len(preds) - 1] if r == 1 else []) for r in range(world)]
+    order = [per_rank[r][e] for e in range(max(map(len, per_rank))) for r in range(world) if e < len(per_rank[r])]
+    assert len(lab) == len(order)
+    for got, i in zip(lab, order):
+        assert torch.equal(got, preds[i]["labels"])
+    m.unsync()
+
+
+@pytest.mark.ddp
+def test_map_ddp_packed_sync():
+    preds, target = _random_coco(13, n_img=9)
+    run_ddp(_ddp_map_packed, preds, target)

@@ -122,6 +122,9 @@ class MeanAveragePrecision(Metric):
 
     # ------------------------------------------------------------------------------------------------ update
     _BOX_STATES = ("detection_box", "groundtruth_box")
+    # the per-image tensor lists cross the sync engine as flat buffers (Metric._packed_sync_plan)
+    _packed_sync_states = ("detection_box", "detection_scores", "detection_labels", "groundtruth_box",
+                           "groundtruth_labels", "groundtruth_crowds", "groundtruth_area")
 
     def update(self, preds: List[Dict[str, Tensor]], target: List[Dict[str, Tensor]]) -> None:
         """Append the batch's images.  The whole batch is a handful of launches: per state ONE ``cat`` of all images

@@ -93,6 +93,39 @@ def _is_partial_view(t: Any) -> bool:
             and t.untyped_storage().nbytes() > t.numel() * t.element_size())
 
 
+class _ChunkSnapshot:
+    """A chunked list state's (materialised samples, pending chunks) entry held in the sync cache unbuilt."""
+
+    __slots__ = ("entry",)
+
+    def __init__(self, entry: Tuple[List[Tensor], List[Tuple[Tensor, List[int]]]]) -> None:
+        self.entry = entry
+
+
+def _interleave_gathered(flat: Tensor, sizes: Tensor, counts: Tensor) -> Tuple[Tensor, List[int]]:
+    """Every rank's flat buffer / sample sizes / sample count, concatenated rank after rank by the engine -> the
+    element-major sample order of the reference's per-element gather (sample 0 of every rank, then sample 1, ...;
+    ``S/metric.py:442-457`` ``_flatten``), as ONE row gather of the flat buffer."""
+    meta = torch.cat([counts.reshape(-1), sizes.reshape(-1)]).tolist()  # one host read of the metadata
+    world = counts.numel()
+    cnt, sz = meta[:world], meta[world:]
+    rank_first = [0] * world
+    for r in range(1, world):
+        rank_first[r] = rank_first[r - 1] + cnt[r - 1]
+    order = [rank_first[r] + e for e in range(max(cnt) if cnt else 0) for r in range(world) if e < cnt[r]]
+    if order == list(range(len(sz))):
+        return flat, sz
+    row_start = [0] * len(sz)
+    for i in range(1, len(sz)):
+        row_start[i] = row_start[i - 1] + sz[i - 1]
+    new_sizes = [sz[i] for i in order]
+    lens = torch.tensor(new_sizes, dtype=torch.int64)
+    starts = torch.tensor([row_start[i] for i in order], dtype=torch.int64)
+    out_start = torch.cumsum(lens, 0) - lens
+    idx = torch.repeat_interleave(starts - out_start, lens) + torch.arange(int(lens.sum()), dtype=torch.int64)
+    return flat.index_select(0, idx.to(flat.device)), new_sizes
+
+
 class Metric(Module, ABC):
     """Base class for all metrics.
 
@@ -436,14 +469,33 @@ class Metric(Module, ABC):
     # ------------------------------------------------------------------------------------------------------- sync
     def _sync_dist(self, dist_sync_fn: Optional[Callable] = None, process_group: Optional[Any] = None) -> None:
         group = process_group or self.process_group
-        states = {attr: getattr(self, attr) for attr in self._reductions}
+        packed = self._packed_sync_plan(group) if dist_sync_fn is None and self._packed_sync_states else {}
+        states = {attr: getattr(self, attr) for attr in self._reductions if attr not in packed}
         if dist_sync_fn is None:
+            reductions = self._reductions
+            if packed:
+                # a chunked list state crosses as its flat buffer + sample sizes (two cat items of the same engine
+                # call) instead of one list element per sample; re-interleaved element-major afterwards
+                reductions = {a: f for a, f in self._reductions.items() if a not in packed}
+                for attr, (flat, sizes) in packed.items():
+                    dev = flat.device if flat is not None else self.device
+                    states[attr + "\0flat"] = [flat] if flat is not None else []
+                    states[attr + "\0sizes"] = [torch.tensor(sizes, dtype=torch.int64, device=dev)] if sizes else []
+                    states[attr + "\0n"] = [torch.tensor([len(sizes)], dtype=torch.int64, device=dev)]
+                    for k in ("\0flat", "\0sizes", "\0n"):
+                        reductions[attr + k] = dim_zero_cat
             # (sync() packed the reducible states into their arena before caching them: each bucket is one span)
             # a one-shot xGMI bucket reports failure in this metric's validation word: compute() reads the word after
             # the sync (sync() reads it right away when called on its own)
             dev = next((v.device for v in states.values() if isinstance(v, Tensor) and v.is_cuda), None)
             err = self._device_error_buffer(dev) if dev is not None else None
-            synced = sync_state_dicts([(states, self._reductions)], group=group, err_word=err)[0]
+            synced = sync_state_dicts([(states, reductions)], group=group, err_word=err)[0]
+            for attr in packed:
+                flat, sizes, n = synced.pop(attr + "\0flat"), synced.pop(attr + "\0sizes"), synced.pop(attr + "\0n")
+                setattr(self, attr, [])
+                if isinstance(flat, Tensor) and isinstance(sizes, Tensor) and sizes.numel():
+                    flat, order = _interleave_gathered(flat, sizes, n)
+                    self._append_chunk(attr, flat, order)
             for attr, val in synced.items():
                 setattr(self, attr, val)
             if err is not None:
@@ -561,7 +613,9 @@ class Metric(Module, ABC):
             return
         if dist_sync_fn is None and self.dist_sync_fn is None:
             _arena.pack([self])  # no-op when laid out already; BEFORE the cache, so unsync restores the packed views
-        self._cache = {attr: getattr(self, attr) for attr in self._defaults}
+        chunks = self.__dict__.get("_chunks")
+        self._cache = {attr: (_ChunkSnapshot(chunks[attr]) if chunks and attr in chunks else getattr(self, attr))
+                       for attr in self._defaults}
         self._sync_dist(dist_sync_fn, process_group=process_group)
         self._is_synced = True
         if self.__dict__.get("_sync_word_pending") and not self.__dict__.get("_in_compute"):
@@ -581,7 +635,13 @@ class Metric(Module, ABC):
         if self._cache is None:
             raise TorchMetricsUserError("The internal cache should exist to unsync the Metric.")
         for attr, val in self._cache.items():
-            setattr(self, attr, val)
+            if isinstance(val, _ChunkSnapshot):  # a chunked list state goes back to its chunks, still unbuilt
+                setattr(self, attr, [])
+                d = self.__dict__
+                del d[attr]
+                d.setdefault("_chunks", {})[attr] = val.entry
+            else:
+                setattr(self, attr, val)
         self._is_synced = False
         self._cache = None
 
@@ -891,6 +951,26 @@ class Metric(Module, ABC):
         if chunks and name in chunks:
             return self._materialize_chunks(name)
         return super().__getattr__(name)
+
+    # list states this class lets the sync engine move as ONE flat buffer + sample sizes (``_packed_state``) instead
+    # of one list element per sample; the ranks agree on it per call (one flag all-reduce), since a rank whose samples
+    # do not stack (ragged trailing shapes, mixed dtypes) must keep the element-wise form on every rank
+    _packed_sync_states: Tuple[str, ...] = ()
+
+    def _packed_sync_plan(self, group: Optional[Any]) -> Dict[str, Tuple[Optional[Tensor], List[int]]]:
+        local: Dict[str, Tuple[Optional[Tensor], List[int]]] = {}
+        ok = []
+        for attr in self._packed_sync_states:
+            flat, sizes = self._packed_state(attr)
+            local[attr] = (flat, sizes)
+            ok.append(1 if (flat is not None and flat.ndim >= 1) or not sizes else 0)
+        dev = next((f.device for f, _ in local.values() if f is not None), self.device)
+        backend = torch.distributed.get_backend(group)
+        flag_dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+        flags = torch.tensor(ok, dtype=torch.int32, device=flag_dev)
+        torch.distributed.all_reduce(flags, op=torch.distributed.ReduceOp.MIN, group=group)
+        del dev
+        return {a: local[a] for a, f in zip(self._packed_sync_states, flags.tolist()) if f}
 
     def _materialize_chunks(self, name: str) -> List[Tensor]:
         base, pending = self.__dict__["_chunks"].pop(name)

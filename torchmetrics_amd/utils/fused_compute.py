@@ -34,7 +34,6 @@ from torchmetrics_amd import ops
 from torchmetrics_amd.utils import deferred as _deferred
 from torchmetrics_amd.utils.graphs import _leaves, _rebuild, _same_result
 
-_PTR0 = 10  # column of pointer slot 0 in a task descriptor row (kind, blocks, 6 ints, 2 floats, 8 pointers)
 
 
 def enabled() -> bool:

@@ -97,3 +97,37 @@ def test_mismatched_devices_fail_loudly():
     flag = torch.zeros(1, dtype=torch.int32, device="cuda")
     with pytest.raises(RuntimeError):
         ops.mc_update(p, t, out, flag, 4, None, ops.MC_CONFMAT)
+
+
+@pytest.mark.parametrize("src_dtype", [torch.int64, torch.int32])
+@pytest.mark.parametrize("code", [0, 1, 2])
+@pytest.mark.parametrize("world", [1, 2, 8])
+@pytest.mark.parametrize("n", [0, 1, 1023, 300_001])
+def test_narrow_wire_kernels_match_host_twin(src_dtype, code, world, n):
+    """csrc/comm/narrow_wire.hip against ops/_cpu.py: wire values, both check slots, the decode and the word bit."""
+    from torchmetrics_amd import ops
+    from torchmetrics_amd.ops import _cpu
+
+    if src_dtype == torch.int32 and code == 2:
+        pytest.skip("an int32 source is not narrowed to int32")
+    cap = (255, 2048, 2**31 - 1)[code] // world
+    g = torch.Generator().manual_seed(n + code)
+    for case in ("fits", "big", "neg"):
+        x = torch.randint(0, cap + 1, (n,), generator=g, dtype=torch.int64)
+        if n and case == "big":
+            x[n // 2] = cap + 1
+        if n and case == "neg":
+            x[n - 1] = -1
+        x = x.to(src_dtype)
+        wire = ops.narrow_encode(x.cuda(), code, world)
+        ref = _cpu.narrow_encode(x, code, world)
+        assert wire.dtype == ref.dtype and wire.shape == ref.shape
+        assert torch.equal(wire.cpu()[n:], ref[n:]), (case, wire.cpu()[n:], ref[n:])
+        if case == "fits":
+            assert torch.equal(wire.cpu(), ref)
+        word = torch.zeros(1, dtype=torch.int32, device="cuda")
+        out = ops.narrow_decode(wire, n, src_dtype, word, 1 << 9)
+        assert out.dtype == src_dtype and out.shape == (n,)
+        if case == "fits":
+            assert torch.equal(out.cpu(), x)
+        assert int(word.item()) == (0 if case == "fits" or n == 0 else 1 << 9)

@@ -182,7 +182,8 @@ def _body_two_procs(rank, world):
         assert torch.equal(out["mx"].cpu(), torch.full((4,), 1.0))
         assert sync.comm_stats()["oneshot_all_reduce"] == 2
         comm.check()
-        # a large integer SUM bucket: the range header and the counts (narrow wire) through the backend
+        # a large integer SUM bucket: the counts and their check slots (narrow wire) through the backend
+        sync._NARROW_LEVEL.clear()
         cm = torch.randint(0, 50, (1000, 1000), dtype=torch.int64, generator=torch.Generator().manual_seed(rank))
         both = sum(torch.randint(0, 50, (1000, 1000), dtype=torch.int64, generator=torch.Generator().manual_seed(r))
                    for r in range(world))
@@ -190,8 +191,8 @@ def _body_two_procs(rank, world):
         out = sync.sync_state_dicts([({"cm": cm.cuda()}, {"cm": dim_zero_sum})])[0]["cm"]
         st = sync.comm_stats()
         assert torch.equal(out.cpu(), both) and out.dtype == torch.int64
-        assert st["oneshot_all_reduce"] == 0 and st["all_reduce"] == 2, st
-        assert st["bytes"] == 16 + 1000 * 1000, st  # 2 x 49 <= 255: uint8 on the wire
+        assert st["oneshot_all_reduce"] == 0 and st["all_reduce"] == 1, st
+        assert st["bytes"] == 1000 * 1000 + 2, st  # 49 <= 255 // 2: uint8 on the wire
         comm.check()
     finally:
         torch.cuda.synchronize()

@@ -27,3 +27,5 @@ timeout -k 10 300 python benchmarks/bench_map.py 2>/dev/null > gpurun_out/r4_ben
 cat gpurun_out/r4_bench_map.json | cut -c1-400
 timeout -k 10 300 python benchmarks/bench_gemm.py 2>/dev/null > gpurun_out/r4_bench_gemm.jsonl || exit 1
 cat gpurun_out/r4_bench_gemm.jsonl | cut -c1-300
+timeout -k 10 120 python benchmarks/bench_word_read.py 2>/dev/null > gpurun_out/r4_word_read.jsonl || exit 1
+cat gpurun_out/r4_word_read.jsonl

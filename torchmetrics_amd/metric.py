@@ -489,7 +489,9 @@ class Metric(Module, ABC):
             # the sync (sync() reads it right away when called on its own)
             dev = next((v.device for v in states.values() if isinstance(v, Tensor) and v.is_cuda), None)
             err = self._device_error_buffer(dev) if dev is not None else None
-            synced = sync_state_dicts([(states, reductions)], group=group, err_word=err)[0]
+            # inside compute() a narrow-wire overflow is reported in the same word (no host read in the sync)
+            narrow = err if self.__dict__.get("_defer_narrow") else None
+            synced = sync_state_dicts([(states, reductions)], group=group, err_word=err, narrow_word=narrow)[0]
             for attr in packed:
                 flat, sizes, n = synced.pop(attr + "\0flat"), synced.pop(attr + "\0sizes"), synced.pop(attr + "\0n")
                 setattr(self, attr, [])
@@ -581,6 +583,8 @@ class Metric(Module, ABC):
         if buf is None:
             return
         code = int(buf.item())
+        if code & _validation.NARROW_RETRY and not only:
+            code = self._narrow_resync(buf, code)
         if only:
             code &= only
         if code:
@@ -589,6 +593,21 @@ class Metric(Module, ABC):
             else:
                 buf.zero_()
             _validation.raise_for_code(code, self)
+
+    def _narrow_resync(self, buf: Tensor, code: int) -> int:
+        """A narrow-wire bucket of compute()'s sync overflowed (``NARROW_RETRY``; every rank sees the same summed
+        check slots, so every rank is here): move those buckets one width up and sync again, checking the wire inline
+        this time.  Runs before any other bit of the word raises, so no rank leaves a peer inside the re-sync."""
+        from torchmetrics_amd.parallel.sync import narrow_resolve
+
+        while code & _validation.NARROW_RETRY:
+            buf.bitwise_and_(~_validation.NARROW_RETRY)
+            narrow_resolve(buf)
+            if self._is_synced:
+                self.unsync()
+                self.sync(dist_sync_fn=self.dist_sync_fn)
+            code = int(buf.item())
+        return code
 
     def _move_list_states_to_cpu(self) -> None:
         for key in self._defaults:
@@ -699,11 +718,12 @@ class Metric(Module, ABC):
                 # sync FIRST, then read the validation word once: every rank has finished its collectives before any
                 # rank raises (a rank raising before the sync would leave its peers waiting), and the same read
                 # covers a failed one-shot bucket of this very sync
-                state["_in_compute"] = True
+                state["_in_compute"] = state["_defer_narrow"] = True
                 try:
                     self.sync(dist_sync_fn=self.dist_sync_fn, should_sync=self._to_sync)
                 finally:
                     state.pop("_in_compute", None)
+                    state.pop("_defer_narrow", None)
                 try:
                     self._check_errors_once(state)
                     value = _squeeze_if_scalar(compute(*args, **kwargs))

@@ -1639,3 +1639,24 @@ def linear_sum_assignment(cost: Tensor, maximize: bool = False) -> Tensor:
     out = torch.zeros(c.shape[0], c.shape[1], dtype=torch.int64, device=c.device)
     _ops().linear_sum_assignment(c.contiguous(), bool(maximize), out)
     return out
+
+
+# ------------------------------------------------------------------------------------------------------- sync wire
+NARROW_WIRE_DTYPES = (torch.uint8, torch.float16, torch.int32)  # wire codes 0 / 1 / 2 of csrc/comm/narrow_wire.hip
+
+
+def narrow_encode(src: Tensor, code: int, world: int) -> Tensor:
+    """An integer SUM bucket in the narrow wire dtype ``NARROW_WIRE_DTYPES[code]`` plus two check slots (too big for
+    an exact ``world``-rank sum / negative), ``[n + 2]`` (``csrc/comm/narrow_wire.hip``)."""
+    src = src.reshape(-1)
+    if src.is_cuda:
+        return _ops().narrow_encode(src.contiguous(), int(code), int(world))
+    return _cpu.narrow_encode(src, int(code), int(world))
+
+
+def narrow_decode(wire: Tensor, n: int, out_dtype: torch.dtype, word: Optional[Tensor], bit: int) -> Tensor:
+    """The summed wire widened back to ``out_dtype`` ``[n]``; ``word |= bit`` on the device when a check slot of the
+    sum is set (the result is then not exact and the bucket must be re-sent wider)."""
+    if wire.is_cuda:
+        return _ops().narrow_decode(wire, int(n), out_dtype, word, int(bit))
+    return _cpu.narrow_decode(wire, int(n), out_dtype, word, int(bit))

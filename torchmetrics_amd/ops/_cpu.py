@@ -843,3 +843,26 @@ def iou_class_reduce(vals: Tensor, o_off: Tensor, b_off: Tensor, gt_lab: Tensor,
         sums[:K] = torch.zeros(K, dtype=torch.float64).index_add_(0, k, v)
         counts[:K] = torch.bincount(k, minlength=K)
     return sums, counts
+
+
+_NARROW_WIRES = ((torch.uint8, 255), (torch.float16, 2048), (torch.int32, 2**31 - 1))
+
+
+def narrow_encode(src: Tensor, code: int, world: int) -> Tensor:
+    """Host twin of ``narrow_encode_kernel``: values in the wire dtype + [too big, negative] check slots."""
+    dtype, wmax = _NARROW_WIRES[code]
+    if src.dtype == torch.int32 and code == 2:
+        raise RuntimeError("narrow_encode: an int32 source is not narrowed to int32")
+    wire = torch.zeros(src.numel() + 2, dtype=dtype)
+    flat = src.reshape(-1)
+    if flat.numel():
+        wire[:-2] = flat.to(dtype)
+        wire[-2] = int(bool((flat > wmax // world).any()))
+        wire[-1] = int(bool((flat < 0).any()))
+    return wire
+
+
+def narrow_decode(wire: Tensor, n: int, out_dtype: torch.dtype, word: Optional[Tensor], bit: int) -> Tensor:
+    if word is not None and bool((wire[n:] != 0).any()):
+        word.bitwise_or_(bit)
+    return wire[:n].to(out_dtype)

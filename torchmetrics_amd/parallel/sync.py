@@ -12,8 +12,10 @@ This engine keeps the exact *result* semantics but changes the communication pla
   its span (``torch.cat`` only for states that fell out of their arena).
   No metadata, no host sync, no barrier.  A whole ``MetricCollection`` (all compute groups) is synced in one call,
   so a 20-metric collection costs ~2 collectives instead of ~3x(#states).
-* **narrow wire** -- integer SUM buckets of >= 1 MiB (count states) travel in the narrowest dtype that carries their
-  sums exactly (uint8 / fp16 / int32), agreed by one tiny MAX all-reduce of the range (:func:`_narrow_wire`).
+* **narrow wire** -- integer SUM buckets of >= 1 MiB (count states) travel optimistically narrow (uint8, else fp16,
+  else int32) with two check slots summed by the same all-reduce; an overflow moves that bucket signature one width
+  up on every rank and re-sends it (:func:`_narrow_bucket`).  No extra collective and, inside ``compute()``, no extra
+  host read: the verdict lands in the metric's validation word.
 * **one-shot path** -- on RCCL, reduce buckets of <= 256 KiB (every classification / regression state) skip the
   ring: one peer-read kernel over xGMI (:mod:`torchmetrics_amd.parallel.oneshot`).
 * **gather bucket** -- ``cat``, ``None`` and custom-callable states. One fixed-size metadata header per rank (element
@@ -36,6 +38,7 @@ import torch
 import torch.distributed as dist
 from torch import Tensor
 
+from torchmetrics_amd import ops
 from torchmetrics_amd.parallel.arena import contiguous_span
 from torchmetrics_amd.utils import profiling as _prof
 from torchmetrics_amd.parallel.oneshot import DEFAULT_SLOT_BYTES, get_oneshot
@@ -65,7 +68,8 @@ _DTYPE_CODES = [
     torch.uint8, torch.bool, torch.complex64, torch.complex128,
 ]
 
-_stats = {"all_reduce": 0, "oneshot_all_reduce": 0, "all_gather": 0, "meta_all_gather": 0, "bytes": 0}
+_stats = {"all_reduce": 0, "oneshot_all_reduce": 0, "all_gather": 0, "meta_all_gather": 0, "bytes": 0,
+          "narrow_all_reduce": 0, "narrow_retry": 0}
 
 
 def comm_stats(reset: bool = False) -> Dict[str, int]:
@@ -121,43 +125,95 @@ def _all_gather_flat(buf: Tensor, world: int, group: Optional[Any]) -> Tensor:
     return out
 
 
-# Integer SUM buckets of at least this many bytes are range-checked for a narrower wire dtype (count states such as a
-# 1000-class confusion matrix: 8 MB of int64 whose cells are small).
+# Integer SUM buckets of at least this many bytes travel on the narrow wire (count states such as a 1000-class
+# confusion matrix: 8 MB of int64 whose cells are small).
 NARROW_WIRE_MIN_BYTES = 1 << 20
 _NARROWABLE = (torch.int64, torch.int32)
+_WIDE = len(ops.NARROW_WIRE_DTYPES)
+# bucket signature -> wire level (index into ops.NARROW_WIRE_DTYPES; _WIDE = the state's own dtype).  Every rank of a
+# group moves a signature up at the same sync, on the same all-reduced check slots, so the levels stay agreed without
+# a collective of their own.
+_NARROW_LEVEL: Dict[Tuple[Any, ...], int] = {}
+# id(validation word) -> [(signature, summed check slots)] of the deferred buckets of that word's last sync
+_NARROW_PENDING: Dict[int, List[Tuple[Tuple[Any, ...], Tensor]]] = {}
 
 
-def _narrow_wire(src: Tensor, world: int, group: Optional[Any]) -> Optional[torch.dtype]:
-    """The narrowest dtype that carries this integer SUM bucket's all-reduce exactly, agreed by every rank.
+def _narrow_key(group: Optional[Any], src: Tensor) -> Tuple[Any, ...]:
+    ranks = None if group is None or group is dist.group.WORLD else tuple(dist.get_process_group_ranks(group))
+    return (ranks, src.dtype, src.numel())
 
-    One tiny MAX all-reduce of (local max, -local min) gives every rank the same global bound, so all ranks pick the
-    same wire dtype (the collective sequence stays matched).  Every partial sum of the all-reduce is at most
-    ``world * max``: <= 255 travels as uint8, <= 2048 as fp16 (integers are exact there), < 2^31 as int32.  The
-    ring all-reduce is per-link bandwidth-bound over xGMI, so an 8 MB int64 count bucket with small cells becomes a
-    1 MB uint8 one.  Negative values or small buckets keep their dtype.  ``TORCHMETRICS_AMD_NARROW_WIRE=0`` disables
-    it."""
-    if src.numel() * src.element_size() < NARROW_WIRE_MIN_BYTES or not _narrow_enabled():
-        return None
-    lo, hi = torch.aminmax(src)
-    bound = torch.stack([hi, -lo]).to(torch.int64)
-    _all_reduce(bound, "max", group)  # RCCL / gloo: the same collective sequence on every rank, nothing to disown
-    gmax, neg_gmin = bound.tolist()
-    if neg_gmin > 0:
-        return None
-    total = world * gmax
-    if total <= 255:
-        return torch.uint8
-    if total <= 2048:
-        return torch.float16
-    if total < 2**31 and src.dtype == torch.int64:
-        return torch.int32
-    return None
+
+def _escalate(key: Tuple[Any, ...], big: int, neg: int) -> bool:
+    """Move ``key`` up after a failed check (negative values: straight to the wide dtype); True if it moved."""
+    if not (big or neg):
+        return False
+    _NARROW_LEVEL[key] = _WIDE if neg else _NARROW_LEVEL.get(key, 0) + 1
+    _stats["narrow_retry"] += 1
+    return True
+
+
+def _narrow_bucket(src: Tensor, world: int, group: Optional[Any], word: Optional[Tensor]) -> Optional[Tensor]:
+    """All-reduce an integer SUM bucket on the narrow wire; the summed bucket in ``src.dtype``, or None to send it wide.
+
+    The wire width is the level this bucket signature settled on (uint8 first).  Each rank checks that its own values
+    are at most ``wire max // world`` (then every partial sum of the ring, and the total, is exact in the wire dtype)
+    and non-negative; the two check slots ride in the same all-reduce, so every rank gets the same verdict.
+    ``word`` given (``compute()``'s sync): the decode ORs ``validation.NARROW_RETRY`` into it on a failed check and the
+    caller re-syncs after its one validation read (:func:`narrow_resolve`); without it the slots are read here and a
+    failed bucket is re-sent one width up at once.  ``TORCHMETRICS_AMD_NARROW_WIRE=0`` disables the narrow wire."""
+    from torchmetrics_amd.utils.validation import NARROW_RETRY
+
+    key = _narrow_key(group, src)
+    n = src.numel()
+    while True:
+        level = _NARROW_LEVEL.get(key, 0)
+        if level >= _WIDE or (level == 2 and src.dtype == torch.int32):
+            return None
+        wire = ops.narrow_encode(src, level, world)
+        if _prof.ENABLED:
+            _prof.push(f"tm.sync.narrow/{ops.NARROW_WIRE_DTYPES[level]}/{wire.numel() * wire.element_size()}B")
+        _all_reduce(wire, "sum", group)
+        _stats["narrow_all_reduce"] += 1
+        if _prof.ENABLED:
+            _prof.pop()
+        if word is not None and word.device == wire.device:
+            _NARROW_PENDING.setdefault(id(word), []).append((key, wire[n:]))
+            return ops.narrow_decode(wire, n, src.dtype, word, NARROW_RETRY)
+        big, neg = (int(v) for v in wire[n:].tolist())
+        if not _escalate(key, big, neg):
+            return ops.narrow_decode(wire, n, src.dtype, None, 0)
+
+
+def narrow_resolve(word: Tensor) -> None:
+    """After ``word`` showed ``NARROW_RETRY``: move every bucket of its last sync whose check failed one width up (the
+    caller then re-syncs; every rank sees the same summed slots, so every rank does the same)."""
+    for key, slots in _NARROW_PENDING.pop(id(word), []):
+        big, neg = (int(v) for v in slots.tolist())
+        _escalate(key, big, neg)
 
 
 def _narrow_enabled() -> bool:
     import os
 
     return os.environ.get("TORCHMETRICS_AMD_NARROW_WIRE", "1") not in ("0", "false", "False")
+
+
+def _reduce_flat(flat: Tensor, kind: str, group: Optional[Any], err_word: Optional[Tensor]) -> None:
+    """One reduce bucket in place: the one-shot xGMI kernel for small RCCL buckets (opt-in), else one all-reduce."""
+    if _prof.ENABLED:
+        _prof.push(f"tm.sync.bucket/{kind}/{str(flat.dtype).replace('torch.', '')}/{flat.numel() * flat.element_size()}B")
+    small = flat.numel() * flat.element_size() <= DEFAULT_SLOT_BYTES
+    # the communicator (IPC setup collective) is only created once a bucket small enough for it shows up
+    comm = get_oneshot(group) if (small and flat.is_cuda and _is_nccl(group)) else None
+    if comm is not None and comm.supports(flat):
+        word = err_word if err_word is not None and err_word.device == flat.device else None
+        comm.all_reduce(flat, kind, word)  # one peer-read kernel over xGMI (checked now if word is None)
+        _stats["oneshot_all_reduce"] += 1
+        _stats["bytes"] += flat.numel() * flat.element_size()
+    else:
+        _all_reduce(flat, kind, group)
+    if _prof.ENABLED:
+        _prof.pop()
 
 
 class _GatherItem:
@@ -177,6 +233,7 @@ def sync_state_dicts(
     entries: Sequence[Tuple[Dict[str, State], Dict[str, Any]]],
     group: Optional[Any] = None,
     err_word: Optional[Tensor] = None,
+    narrow_word: Optional[Tensor] = None,
 ) -> List[Dict[str, State]]:
     """Synchronise the states of several metrics at once.
 
@@ -187,20 +244,24 @@ def sync_state_dicts(
         err_word: int32 device word (the metric's / collection's deferred-validation word).  One-shot buckets OR
             ``ONESHOT_FAILED`` into it on failure and the CALLER must read it before using the results (``compute()``
             reads it once anyway).  Without it a one-shot bucket is checked here with its own device sync.
+        narrow_word: int32 word (same device) that receives ``NARROW_RETRY`` when a narrow-wire bucket overflowed; the
+            CALLER must read it before using the results and, if set, call :func:`narrow_resolve` and sync again.
+            Without it the narrow buckets' checks are read here (one host read per narrow bucket).
 
     Returns:
         One dict of synced states per entry.
     """
     if _prof.ENABLED:
         with _prof.range(f"tm.sync/{sum(len(r) for _, r in entries)} states"):
-            return _sync_state_dicts(entries, group, err_word)
-    return _sync_state_dicts(entries, group, err_word)
+            return _sync_state_dicts(entries, group, err_word, narrow_word)
+    return _sync_state_dicts(entries, group, err_word, narrow_word)
 
 
 def _sync_state_dicts(
     entries: Sequence[Tuple[Dict[str, State], Dict[str, Any]]],
     group: Optional[Any],
     err_word: Optional[Tensor],
+    narrow_word: Optional[Tensor] = None,
 ) -> List[Dict[str, State]]:
     world = _world_size(group)
     results: List[Dict[str, State]] = [dict() for _ in entries]
@@ -224,33 +285,27 @@ def _sync_state_dicts(
                 gather_items.append(_GatherItem((mi, name), True, [e.contiguous() for e in elems], fn))
 
     # ---- reduce bucket: one all_reduce per (op, dtype, device) ------------------------------------------------
+    if narrow_word is not None:
+        _NARROW_PENDING.pop(id(narrow_word), None)
     for (kind, dtype, _device), members in reduce_buckets.items():
         wire = _WIRE_DTYPE.get(dtype, dtype)
         span = members[0][1].reshape(-1) if len(members) == 1 else contiguous_span([t for _, t in members])
-        if world > 1 and kind == "sum" and dtype in _NARROWABLE:
+        summed = None
+        if (world > 1 and kind == "sum" and dtype in _NARROWABLE and _narrow_enabled()
+                and sum(t.numel() for _, t in members) * members[0][1].element_size() >= NARROW_WIRE_MIN_BYTES):
             src = span if span is not None else torch.cat([t.reshape(-1) for _, t in members])
-            wire = _narrow_wire(src, world, group) or wire
+            summed = _narrow_bucket(src, world, group, narrow_word)
             span = src
-        if span is not None:
-            # one packed arena (parallel/arena.py) or a single state: one copy, the local states stay untouched
-            flat = span.to(wire, copy=True)
+        if summed is not None:
+            flat = summed
         else:
-            flat = torch.cat([t.reshape(-1).to(wire) for _, t in members])
-        if world > 1 and _prof.ENABLED:
-            _prof.push(f"tm.sync.bucket/{kind}/{str(dtype).replace('torch.', '')}/{flat.numel() * flat.element_size()}B")
-        if world > 1:
-            small = flat.numel() * flat.element_size() <= DEFAULT_SLOT_BYTES
-            # the communicator (IPC setup collective) is only created once a bucket small enough for it shows up
-            comm = get_oneshot(group) if (small and flat.is_cuda and _is_nccl(group)) else None
-            if comm is not None and comm.supports(flat):
-                word = err_word if err_word is not None and err_word.device == flat.device else None
-                comm.all_reduce(flat, kind, word)  # one peer-read kernel over xGMI (checked now if word is None)
-                _stats["oneshot_all_reduce"] += 1
-                _stats["bytes"] += flat.numel() * flat.element_size()
+            if span is not None:
+                # one packed arena (parallel/arena.py) or a single state: one copy, the local states stay untouched
+                flat = span.to(wire, copy=True)
             else:
-                _all_reduce(flat, kind, group)
-            if _prof.ENABLED:
-                _prof.pop()
+                flat = torch.cat([t.reshape(-1).to(wire) for _, t in members])
+            if world > 1:
+                _reduce_flat(flat, kind, group, err_word)
         off = 0
         for (mi, name), t in members:
             n = t.numel()
@@ -402,4 +457,4 @@ def gather_tensor_uneven(t: Tensor, group: Optional[Any] = None) -> List[Tensor]
     return res if isinstance(res, list) else [res]
 
 
-__all__ = ["sync_state_dicts", "distributed_available", "comm_stats", "gather_tensor_uneven"]
+__all__ = ["sync_state_dicts", "distributed_available", "comm_stats", "gather_tensor_uneven", "narrow_resolve"]

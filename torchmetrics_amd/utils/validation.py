@@ -24,6 +24,7 @@ VALUE_NAN = 1 << 5  # NaN in an aggregation input with nan_strategy='error'
 NEG_VALUE = 1 << 6  # negative value where a non-negative one is required
 VALUE_NAN_WARN = 1 << 7  # NaN dropped by an aggregator with nan_strategy='warn': a warning, not an error
 ONESHOT_FAILED = 1 << 8  # the one-shot all-reduce of this metric's states timed out / was disowned by a peer
+NARROW_RETRY = 1 << 9  # not an error: a narrow-wire bucket of this metric's sync overflowed, re-sync it wider
 
 _MESSAGES: Dict[int, str] = {
     TARGET_OUT_OF_RANGE: "Detected more unique values in `target` than expected. Expected only {num_classes} values"
@@ -41,6 +42,7 @@ _MESSAGES: Dict[int, str] = {
 
 def raise_for_code(code: int, metric: Any = None) -> None:
     """Raise the first error encoded in ``code`` (warning bits are emitted as warnings; no raise if only those)."""
+    code &= ~NARROW_RETRY  # handled by the owner's re-sync (Metric._raise_device_errors)
     if code & VALUE_NAN_WARN:
         from torchmetrics_amd.utilities.prints import rank_zero_warn
 

@@ -285,7 +285,15 @@ struct NativeUpdate {
   int64_t calls;       // fast-path calls (tests / benchmarks read it)
   FastFn fast;         // the native body
   int stat_kind;       // NativeForward of the stat-score family: the score (cbody::StatKind)
+  int decline;         // source line of the last fast-path decline (0: none yet) -- ``decline_line`` for diagnostics
 };
+
+// leave the fast path, remembering where (NativeUpdate.decline_line names the check that sent a call to Python)
+#define TM_DECLINE        \
+  do {                    \
+    self->decline = __LINE__; \
+    return 0;             \
+  } while (0)
 
 inline const at::Tensor* tensor_item(PyObject* dict, PyObject* key) {
   PyObject* o = PyDict_GetItem(dict, key);  // borrowed
@@ -295,34 +303,34 @@ inline const at::Tensor* tensor_item(PyObject* dict, PyObject* key) {
 
 // 1 = done, 0 = not handled (take the Python path), -1 = Python error set
 int confmat_fast(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** result) {
-  if (!THPVariable_Check(a) || !THPVariable_Check(b)) return 0;
+  if (!THPVariable_Check(a) || !THPVariable_Check(b)) TM_DECLINE;
   const at::Tensor& p = THPVariable_Unpack(a);
   const at::Tensor& t = THPVariable_Unpack(b);
-  if (!p.is_cuda() || !t.is_cuda()) return 0;
+  if (!p.is_cuda() || !t.is_cuda()) TM_DECLINE;
   const auto pd = p.scalar_type();
   const auto td = t.scalar_type();
-  if (pd != at::kBFloat16 && pd != at::kHalf && pd != at::kFloat) return 0;
-  if (td != at::kLong && td != at::kInt) return 0;
+  if (pd != at::kBFloat16 && pd != at::kHalf && pd != at::kFloat) TM_DECLINE;
+  if (td != at::kLong && td != at::kInt) TM_DECLINE;
   PyObject* st = self->state;
   PyObject* co = PyDict_GetItem(st, g_k_classes);
-  if (co == nullptr || !PyLong_CheckExact(co)) return 0;
+  if (co == nullptr || !PyLong_CheckExact(co)) TM_DECLINE;
   const long long C = PyLong_AsLongLong(co);
-  if (p.dim() != 2 || t.dim() != 1 || p.size(1) != C || p.size(0) != t.size(0) || p.size(0) == 0) return 0;
-  if (!p.is_contiguous() || !t.is_contiguous()) return 0;
+  if (p.dim() != 2 || t.dim() != 1 || p.size(1) != C || p.size(0) != t.size(0) || p.size(0) == 0) TM_DECLINE;
+  if (!p.is_contiguous() || !t.is_contiguous()) TM_DECLINE;
   const int dev = p.get_device();
-  if (t.get_device() != dev) return 0;
-  if (PyDict_GetItem(st, g_k_cpu) != Py_False) return 0;
+  if (t.get_device() != dev) TM_DECLINE;
+  if (PyDict_GetItem(st, g_k_cpu) != Py_False) TM_DECLINE;
   const at::Tensor* cm = tensor_item(st, g_k_confmat);
   if (cm == nullptr || !cm->is_cuda() || cm->get_device() != dev || cm->scalar_type() != at::kLong ||
       !cm->is_contiguous() || cm->numel() != C * C)
-    return 0;
+    TM_DECLINE;
   PyObject* vo = PyDict_GetItem(st, g_k_validate);
-  if (vo == nullptr) return 0;
+  if (vo == nullptr) TM_DECLINE;
   const bool validate = vo == Py_True;
   const at::Tensor* flag;
   if (validate) {
     flag = tensor_item(st, g_k_err);  // created by the first (Python) update on this device
-    if (flag == nullptr || !flag->is_cuda() || flag->get_device() != dev || flag->scalar_type() != at::kInt) return 0;
+    if (flag == nullptr || !flag->is_cuda() || flag->get_device() != dev || flag->scalar_type() != at::kInt) TM_DECLINE;
   } else {
     if (self->sink == nullptr || self->sink->get_device() != dev) {
       delete self->sink;
@@ -331,15 +339,15 @@ int confmat_fast(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** result
     flag = self->sink;
   }
   PyObject* io = PyDict_GetItem(st, g_k_ignore);
-  if (io == nullptr) return 0;
+  if (io == nullptr) TM_DECLINE;
   long long ignore = 0;
   const bool has_ignore = io != Py_None;
   if (has_ignore) {
-    if (!PyLong_CheckExact(io)) return 0;
+    if (!PyLong_CheckExact(io)) TM_DECLINE;
     ignore = PyLong_AsLongLong(io);
   }
   PyObject* cnt = PyDict_GetItem(st, g_k_count);
-  if (cnt == nullptr || !PyLong_CheckExact(cnt)) return 0;
+  if (cnt == nullptr || !PyLong_CheckExact(cnt)) TM_DECLINE;
   const long long n = PyLong_AsLongLong(cnt);
   try {
     tm_amd::mc_update(p, t, *cm, *flag, C, ignore, has_ignore, 0, false);
@@ -404,6 +412,10 @@ PyObject* native_update_fallback(PyObject* o, void*) {
   return f;
 }
 
+PyObject* native_update_decline(PyObject* o, void*) {
+  return PyLong_FromLong(reinterpret_cast<NativeUpdate*>(o)->decline);
+}
+
 PyObject* native_update_calls(PyObject* o, void*) {
   return PyLong_FromLongLong(reinterpret_cast<NativeUpdate*>(o)->calls);
 }
@@ -412,6 +424,7 @@ PyGetSetDef kNativeUpdateGetSet[] = {
     {"__wrapped__", native_update_wrapped, nullptr, nullptr, nullptr},
     {"fallback", native_update_fallback, nullptr, nullptr, nullptr},
     {"native_calls", native_update_calls, nullptr, nullptr, nullptr},
+    {"decline_line", native_update_decline, nullptr, nullptr, nullptr},
     {nullptr, nullptr, nullptr, nullptr, nullptr},
 };
 
@@ -432,6 +445,7 @@ PyObject* make_confmat_updater(PyObject*, PyObject* const* args, Py_ssize_t narg
   self->fallback = args[1];
   self->sink = nullptr;
   self->calls = 0;
+  self->decline = 0;
   self->fast = confmat_fast;
   self->stat_kind = 0;
   PyObject_GC_Track(reinterpret_cast<PyObject*>(self));
@@ -480,14 +494,24 @@ bool forward_allowed(PyObject* st) {
 
 // No reference to the state tensors outside the metric: each state object is held by the metric's __dict__ only, and
 // its storage by nothing but the metric's own states on it and their view base (a packed arena's buffer).
-bool states_unobserved(PyObject* st, std::initializer_list<PyObject*> keys) {
+// why (optional): 1 no _defaults, 2 a state missing / not a tensor, 3 a Python reference besides the dict (detail: the
+// refcount), 4 no storage, 5 more than 16 tensors on the storage, 6 other tensors on the storage (detail: use count
+// * 100 + allowed), 7 the view base held from Python (detail: its refcount)
+template <typename Keys>
+bool states_unobserved_why(PyObject* st, const Keys& keys, int* why, long long* detail) {
+  auto fail = [&](int w, long long d) {
+    if (why != nullptr) *why = w;
+    if (detail != nullptr) *detail = d;
+    return false;
+  };
   PyObject* defaults = PyDict_GetItem(st, g_k_defaults);
-  if (defaults == nullptr || !PyDict_Check(defaults)) return false;
+  if (defaults == nullptr || !PyDict_Check(defaults)) return fail(1, 0);
   for (PyObject* key : keys) {
     PyObject* o = PyDict_GetItem(st, key);
-    if (o == nullptr || !THPVariable_Check(o) || Py_REFCNT(o) != 1) return false;
+    if (o == nullptr || !THPVariable_Check(o)) return fail(2, 0);
+    if (Py_REFCNT(o) != 1) return fail(3, Py_REFCNT(o));
     const at::Tensor& t = THPVariable_Unpack(o);
-    if (!t.has_storage()) return false;
+    if (!t.has_storage()) return fail(4, 0);
     const c10::StorageImpl* si = t.storage().unsafeGetStorageImpl();
     const c10::TensorImpl* impls[16];
     size_t n = 0;
@@ -505,12 +529,40 @@ bool states_unobserved(PyObject* st, std::initializer_list<PyObject*> keys) {
       if (so == nullptr || !THPVariable_Check(so)) continue;
       const at::Tensor& s = THPVariable_Unpack(so);
       if (!s.has_storage() || s.storage().unsafeGetStorageImpl() != si) continue;
-      if (!add(s.unsafeGetTensorImpl())) return false;
-      if (s.is_view() && !add(s._base().unsafeGetTensorImpl())) return false;
+      if (!add(s.unsafeGetTensorImpl())) return fail(5, 0);
+      if (s.is_view()) {
+        const c10::TensorImpl* bi = s._base().unsafeGetTensorImpl();
+        if (!add(bi)) return fail(5, 0);
+        // the view base (a packed arena's buffer) as a Python object: alive only through its views (one reference
+        // held for them), unless someone outside holds it
+        PyObject* bp = bi->pyobj_slot()->load_pyobj();
+        if (bp != nullptr && Py_REFCNT(bp) > 1) return fail(7, Py_REFCNT(bp));
+      }
     }
-    if (static_cast<size_t>(t.storage().use_count()) > n) return false;
+    // a Python UntypedStorage object of this storage, once created (untyped_storage(): the arena, the sync engine),
+    // is preserved by the StorageImpl for its lifetime and holds one reference of its own
+    if (si->pyobj_slot()->load_pyobj() != nullptr) ++n;
+    if (static_cast<size_t>(t.storage().use_count()) > n) return fail(6, t.storage().use_count() * 100 + n);
   }
   return true;
+}
+
+bool states_unobserved(PyObject* st, std::initializer_list<PyObject*> keys) {
+  return states_unobserved_why(st, keys, nullptr, nullptr);
+}
+
+// _states_unobserved(state_dict, keys) -> (ok, why, detail): the forward's aliasing test on its own (tests, diagnostics)
+PyObject* states_unobserved_probe(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 2 || !PyDict_Check(args[0]) || !PyTuple_Check(args[1])) {
+    PyErr_SetString(PyExc_TypeError, "_states_unobserved(state: dict, keys: tuple)");
+    return nullptr;
+  }
+  std::vector<PyObject*> keys;
+  for (Py_ssize_t i = 0; i < PyTuple_GET_SIZE(args[1]); ++i) keys.push_back(PyTuple_GET_ITEM(args[1], i));
+  int why = 0;
+  long long detail = 0;
+  const bool ok = states_unobserved_why(args[0], keys, &why, &detail);
+  return Py_BuildValue("(OiL)", ok ? Py_True : Py_False, why, detail);
 }
 
 // the int32 flag word the kernels report into: the metric's validation word (validate_args) or a private sink
@@ -624,27 +676,27 @@ bool int_target(const at::Tensor& t) {
 }
 
 int confmat_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** result) {
-  if (!THPVariable_Check(a) || !THPVariable_Check(b)) return 0;
+  if (!THPVariable_Check(a) || !THPVariable_Check(b)) TM_DECLINE;
   const at::Tensor& p = THPVariable_Unpack(a);
   const at::Tensor& t = THPVariable_Unpack(b);
-  if (!p.is_cuda() || !t.is_cuda() || !float_preds(p) || !int_target(t)) return 0;
+  if (!p.is_cuda() || !t.is_cuda() || !float_preds(p) || !int_target(t)) TM_DECLINE;
   PyObject* st = self->state;
-  if (!forward_allowed(st) || PyDict_GetItem(st, g_k_normalize) != Py_None) return 0;
+  if (!forward_allowed(st) || PyDict_GetItem(st, g_k_normalize) != Py_None) TM_DECLINE;
   PyObject* co = PyDict_GetItem(st, g_k_classes);
-  if (co == nullptr || !PyLong_CheckExact(co)) return 0;
+  if (co == nullptr || !PyLong_CheckExact(co)) TM_DECLINE;
   const long long C = PyLong_AsLongLong(co);
-  if (p.dim() != 2 || t.dim() != 1 || p.size(1) != C || p.size(0) != t.size(0) || p.size(0) == 0) return 0;
-  if (!p.is_contiguous() || !t.is_contiguous()) return 0;
+  if (p.dim() != 2 || t.dim() != 1 || p.size(1) != C || p.size(0) != t.size(0) || p.size(0) == 0) TM_DECLINE;
+  if (!p.is_contiguous() || !t.is_contiguous()) TM_DECLINE;
   const int dev = p.get_device();
-  if (t.get_device() != dev) return 0;
+  if (t.get_device() != dev) TM_DECLINE;
   // forward() clears the cached compute() value first (a held compute() result of a confusion matrix IS the state)
   if (PyDict_SetItem(st, g_k_computed, Py_None) != 0) return -1;
   const at::Tensor* cm = state_tensor(st, g_k_confmat, dev, C * C);
-  if (cm == nullptr || !states_unobserved(st, {g_k_confmat})) return 0;
+  if (cm == nullptr || !states_unobserved(st, {g_k_confmat})) TM_DECLINE;
   const at::Tensor* flag = forward_flag(self, st, dev);
   long long ignore;
   bool has_ignore;
-  if (flag == nullptr || !read_ignore(st, ignore, has_ignore)) return 0;
+  if (flag == nullptr || !read_ignore(st, ignore, has_ignore)) TM_DECLINE;
   at::Tensor batch;
   try {
     batch = at::zeros({C, C}, cm->options());
@@ -660,54 +712,54 @@ int confmat_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** res
 // update_only: the family's ``update`` (accumulate the batch into the global states, the reference's in-place
 // ``_update_state``) -- the same checks and kernels as the forward below without the batch score.
 int stats_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** result, int fkind, bool update_only = false) {
-  if (!THPVariable_Check(a) || !THPVariable_Check(b)) return 0;
+  if (!THPVariable_Check(a) || !THPVariable_Check(b)) TM_DECLINE;
   const at::Tensor& p = THPVariable_Unpack(a);
   const at::Tensor& t = THPVariable_Unpack(b);
-  if (!p.is_cuda() || !t.is_cuda() || !float_preds(p) || !int_target(t)) return 0;
-  if (!p.is_contiguous() || !t.is_contiguous() || p.numel() == 0) return 0;
+  if (!p.is_cuda() || !t.is_cuda() || !float_preds(p) || !int_target(t)) TM_DECLINE;
+  if (!p.is_contiguous() || !t.is_contiguous() || p.numel() == 0) TM_DECLINE;
   const int dev = p.get_device();
-  if (t.get_device() != dev) return 0;
+  if (t.get_device() != dev) TM_DECLINE;
   PyObject* st = self->state;
-  if (update_only ? PyDict_GetItem(st, g_k_cpu) != Py_False : !forward_allowed(st)) return 0;
+  if (update_only ? PyDict_GetItem(st, g_k_cpu) != Py_False : !forward_allowed(st)) TM_DECLINE;
   PyObject* md = PyDict_GetItem(st, g_k_mdavg);
-  if (md == nullptr || !PyUnicode_Check(md) || PyUnicode_CompareWithASCIIString(md, "global") != 0) return 0;
+  if (md == nullptr || !PyUnicode_Check(md) || PyUnicode_CompareWithASCIIString(md, "global") != 0) TM_DECLINE;
   double beta = 1.0;
   if (self->stat_kind == 5 && !update_only) {
     PyObject* bo = PyDict_GetItem(st, g_k_beta);
-    if (bo == nullptr || !PyFloat_Check(bo) && !PyLong_Check(bo)) return 0;
+    if (bo == nullptr || !PyFloat_Check(bo) && !PyLong_Check(bo)) TM_DECLINE;
     beta = PyFloat_AsDouble(bo);
   }
   long long ignore;
   bool has_ignore;
-  if (!read_ignore(st, ignore, has_ignore)) return 0;
+  if (!read_ignore(st, ignore, has_ignore)) TM_DECLINE;
   long long size;  // classes / labels
   int avg;
   bool micro = false;
   if (fkind == kFwdMulticlass) {
     PyObject* co = PyDict_GetItem(st, g_k_classes);
     PyObject* ko = PyDict_GetItem(st, g_k_topk);
-    if (co == nullptr || !PyLong_CheckExact(co) || ko == nullptr || !PyLong_CheckExact(ko)) return 0;
-    if (PyLong_AsLongLong(ko) != 1) return 0;
+    if (co == nullptr || !PyLong_CheckExact(co) || ko == nullptr || !PyLong_CheckExact(ko)) TM_DECLINE;
+    if (PyLong_AsLongLong(ko) != 1) TM_DECLINE;
     size = PyLong_AsLongLong(co);
-    if (p.dim() != 2 || t.dim() != 1 || p.size(1) != size || p.size(0) != t.size(0)) return 0;
+    if (p.dim() != 2 || t.dim() != 1 || p.size(1) != size || p.size(0) != t.size(0)) TM_DECLINE;
     micro = PyDict_GetItem(st, g_k_micro) == Py_True;
     avg = micro ? 0 : (update_only ? 1 : read_average(st));
   } else if (fkind == kFwdBinary) {
     size = 1;
-    if (p.dim() != 1 || t.dim() != 1 || p.size(0) != t.size(0)) return 0;
+    if (p.dim() != 1 || t.dim() != 1 || p.size(0) != t.size(0)) TM_DECLINE;
     avg = 0;  // the binary score = the micro body with the binary (multilabel) formula over one label
   } else {
     PyObject* lo = PyDict_GetItem(st, g_k_labels);
-    if (lo == nullptr || !PyLong_CheckExact(lo)) return 0;
+    if (lo == nullptr || !PyLong_CheckExact(lo)) TM_DECLINE;
     size = PyLong_AsLongLong(lo);
-    if (p.dim() != 2 || t.dim() != 2 || p.size(1) != size || p.sizes() != t.sizes()) return 0;
+    if (p.dim() != 2 || t.dim() != 2 || p.size(1) != size || p.sizes() != t.sizes()) TM_DECLINE;
     avg = update_only ? 1 : read_average(st);
   }
-  if (avg < 0) return 0;
+  if (avg < 0) TM_DECLINE;
   double threshold = 0.5;
   if (fkind != kFwdMulticlass) {
     PyObject* th = PyDict_GetItem(st, g_k_threshold);
-    if (th == nullptr || !(PyFloat_Check(th) || PyLong_Check(th))) return 0;
+    if (th == nullptr || !(PyFloat_Check(th) || PyLong_Check(th))) TM_DECLINE;
     threshold = PyFloat_AsDouble(th);
   }
   if (PyDict_SetItem(st, g_k_computed, Py_None) != 0) return -1;
@@ -716,13 +768,13 @@ int stats_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** resul
   const at::Tensor* fp = state_tensor(st, g_k_fp, dev, ssize);
   const at::Tensor* tn = state_tensor(st, g_k_tn, dev, ssize);
   const at::Tensor* fn = state_tensor(st, g_k_fn, dev, ssize);
-  if (tp == nullptr || fp == nullptr || tn == nullptr || fn == nullptr) return 0;
-  if (!update_only && !states_unobserved(st, {g_k_tp, g_k_fp, g_k_tn, g_k_fn})) return 0;
+  if (tp == nullptr || fp == nullptr || tn == nullptr || fn == nullptr) TM_DECLINE;
+  if (!update_only && !states_unobserved(st, {g_k_tp, g_k_fp, g_k_tn, g_k_fn})) TM_DECLINE;
   const at::Tensor* flag = forward_flag(self, st, dev);
-  if (flag == nullptr) return 0;
+  if (flag == nullptr) TM_DECLINE;
   at::Tensor ws, not_prob;
   const bool mc = fkind == kFwdMulticlass;
-  if (!workspace(st, dev, mc ? 3 * size + 1 : 7 * size, ws, mc ? nullptr : &not_prob)) return 0;
+  if (!workspace(st, dev, mc ? 3 * size + 1 : 7 * size, ws, mc ? nullptr : &not_prob)) TM_DECLINE;
   if (update_only) {
     try {
       if (mc) {
@@ -807,6 +859,7 @@ PyObject* make_stats_updater(PyObject*, PyObject* const* args, Py_ssize_t nargs)
   self->fallback = args[2];
   self->sink = nullptr;
   self->calls = 0;
+  self->decline = 0;
   static const FastFn kFns[] = {nullptr, mc_stats_update_fast, bin_stats_update_fast, ml_stats_update_fast};
   self->fast = kFns[kind];
   self->stat_kind = 0;
@@ -839,6 +892,7 @@ PyObject* make_forward(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   self->fallback = args[2];
   self->sink = nullptr;
   self->calls = 0;
+  self->decline = 0;
   static const FastFn kFns[] = {confmat_forward, mc_stats_forward_fast, bin_stats_forward_fast,
                                 ml_stats_forward_fast};
   self->fast = kFns[kind];
@@ -854,6 +908,8 @@ PyMethodDef kFactoryMethods[] = {
      "native Metric.forward of the confusion-matrix / stat-score families bound to a metric's __dict__"},
     {"confmat_updater", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&make_confmat_updater)),
      METH_FASTCALL, "native MulticlassConfusionMatrix.update bound to a metric's __dict__"},
+    {"_states_unobserved", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&states_unobserved_probe)),
+     METH_FASTCALL, "the native forward's test that nothing outside the metric holds the given states"},
     {nullptr, nullptr, 0, nullptr},
 };
 

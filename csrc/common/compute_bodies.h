@@ -354,6 +354,7 @@ __device__ __forceinline__ void regression_compute_block(int kind, int k, const 
       const bool nz_rss = !(fabs(rss) <= T(1e-4)), nz_tss = !(fabs(tss) <= T(1e-4));
       score = (nz_rss && nz_tss) ? T(1) - rss / tss : (nz_rss ? T(0) : T(1));
       weight = tss;
+      low_var |= n < T(2) ? 1 : 0;  // R^2's flag slot: fewer than two samples (the reference raises)
     } else {
       // s0 = mean_x, s1 = mean_y, s2 = m2_x, s3 = m2_y, s4 = c_xy (sums of squared deviations)
       const T vx = s2[c] / (n - T(1)), vy = s3[c] / (n - T(1)), cxy = s4[c] / (n - T(1));

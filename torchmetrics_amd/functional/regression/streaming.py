@@ -194,8 +194,9 @@ def _r2_score_compute(
     if mo is not None and sum_obs.is_cuda and ops.regression_computable((sum_squared_obs, sum_obs, rss), num_obs):
         # one launch for the per-output scores and their average (csrc/regression/regression_compute.hip)
         out = ops.regression_compute(ops.REG_R2, (sum_squared_obs, sum_obs, rss), num_obs, mo)
-        raise_if(num_obs < 2, ValueError, "Needs at least two samples to calculate r2 score.")
         k = sum_obs.numel()
+        # the kernel's flag slot holds n < 2 (a task output: a fused collection compute folds it into its status read)
+        raise_if(out[k + 1 : k + 2], ValueError, "Needs at least two samples to calculate r2 score.")
         r2 = out[:k].view(sum_obs.shape) if mo == 0 else out[k]
         return _r2_adjust(r2, num_obs, adjusted)
     if num_obs < 2:

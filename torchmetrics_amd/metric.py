@@ -1034,6 +1034,7 @@ class Metric(Module, ABC):
             del d["forward"]
         if type(d.get("update")).__name__ == "NativeUpdate":
             d["update"] = d["update"].fallback
+        d.pop("_default_packs", None)  # a cache keyed by (names, device) tuples, which TorchScript cannot type
         return self
 
     def _install_native_update(self) -> None:

@@ -962,7 +962,8 @@ def regression_compute(kind: int, states: Sequence[Tensor], n: Union[Tensor, int
                        bound: float = 0.0) -> Tensor:
     """Explained variance / R^2 / Pearson / concordance from their running sums in one launch
     (``csrc/regression/regression_compute.hip``).  Returns ``[k + 2]``: the per-output scores, the
-    ``multioutput`` average and the low-variance flag (Pearson / concordance)."""
+    ``multioutput`` average and the flag (Pearson / concordance: a variance below ``bound``; R^2: fewer than two
+    samples)."""
     s0 = states[0]
     out = torch.empty(s0.numel() + 2, dtype=s0.dtype, device=s0.device)
     rec = _RECORDER
@@ -1346,7 +1347,9 @@ def gemm_row_col_max(x: Tensor, y: Tensor, scale: float = 1.0) -> "tuple[Tensor,
     written), plus two tiny max reductions.  Returns ``(rows [B, N], cols [B, M])``."""
     b, n, m = x.shape[0], x.shape[1], y.shape[1]
     flat = gemm_nt(x, y, GEMM_ROW_COL_MAX, scale=scale)
-    tm, tn = -(-m // 128), -(-n // 128)
+    # partial counts follow the kernel's tile (128, or 256 for the large-problem kernel): the one that fits the output
+    tm, tn = next((-(-m // t), -(-n // t)) for t in (128, 256)
+                  if b * (n * -(-m // t) + -(-n // t) * m) == flat.numel())
     rows = flat[: b * n * tm].reshape(b, n, tm).amax(-1)
     cols = flat[b * n * tm:].reshape(b, tn, m).amax(1)
     return rows, cols

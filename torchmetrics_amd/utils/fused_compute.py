@@ -34,6 +34,8 @@ from torchmetrics_amd import ops
 from torchmetrics_amd.utils import deferred as _deferred
 from torchmetrics_amd.utils.graphs import _leaves, _rebuild, _same_result
 
+# descriptor row layout (ops._TaskRecorder.add): type, blocks, 6 ints, 2 float bit patterns, then the 8 pointer slots
+_PTR_COL = 10
 
 
 def enabled() -> bool:
@@ -116,9 +118,10 @@ class CollectionPlan:
             good = True
             for r, (tensors, row_outs) in enumerate(meta):
                 out_ids = {id(o) for o in row_outs}
-                for col, t in enumerate(tensors):
+                for j, t in enumerate(tensors):
                     if t is None:
                         continue
+                    col = _PTR_COL + j  # pointer slot j of the descriptor row
                     if id(t) in out_ids:
                         if id(t) not in outs:
                             outs[id(t)] = (t, len(local_outs))

@@ -36,6 +36,8 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
 void stat_reduce(const at::Tensor& tp, const at::Tensor& fp, const at::Tensor& tn, const at::Tensor& fn,
                  at::Tensor out, int64_t kind, int64_t average, bool multilabel, double beta);
 void launch_probe(at::Tensor flag);
+bool mc_confmat_dual(const at::Tensor& preds, const at::Tensor& target, at::Tensor batch, at::Tensor global,
+                     at::Tensor flag, int64_t num_classes, int64_t ignore_index, bool has_ignore);
 void confmat_reduce(const at::Tensor& confmat, int64_t kind, int64_t average, int64_t ignore, int64_t kw,
                     at::Tensor out);
 void calibration_bins(const at::Tensor& conf, const at::Tensor& acc, const at::Tensor& bounds, at::Tensor sums,
@@ -456,7 +458,8 @@ PyObject* make_confmat_updater(PyObject*, PyObject* const* args, Py_ssize_t narg
 // ``metric(preds, target)`` for the confusion-matrix and stat-score families as ONE native callable (installed as the
 // instance's ``forward``; nn.Module.__call__ dispatches to it).  The reference forward (S/metric.py:275-306,353-391)
 // saves the global state, resets, updates, computes the batch value and merges state by state; here it is
-//   confmat:     zeros(C, C) -> mc_update into it -> global += batch; the batch matrix is the value,
+//   confmat:     zeros(C, C) -> one kernel adding every row into it and into the global matrix (16-bit logits; else
+//                mc_update into it -> global += batch); the batch matrix is the value,
 //   stat scores: the update kernel into the per-metric workspace -> ONE fused launch (classification/forward.hip)
 //                that folds the batch counts into the global states and scores the batch with compute()'s own body,
 // plus the bookkeeping of Metric.forward (``_update_count``, ``_computed``, ``_forward_cache``).  Taken only when the
@@ -700,8 +703,11 @@ int confmat_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** res
   at::Tensor batch;
   try {
     batch = at::zeros({C, C}, cm->options());
-    tm_amd::mc_update(p, t, batch, *flag, C, ignore, has_ignore, 0, false);
-    cm->add_(batch);
+    // 16-bit logits: one kernel adds each row into the batch matrix and the global state; else update + add
+    if (!tm_amd::mc_confmat_dual(p, t, batch, *cm, *flag, C, ignore, has_ignore)) {
+      tm_amd::mc_update(p, t, batch, *flag, C, ignore, has_ignore, 0, false);
+      cm->add_(batch);
+    }
   } catch (const c10::Error& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what_without_backtrace());
     return -1;
@@ -816,7 +822,7 @@ int stats_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** resul
     return -1;
   }
   // compute() squeezes one-element values
-  return forward_bookkeeping(self, st, out.numel() == 1 ? out.view({}) : out, result);
+  return forward_bookkeeping(self, st, out.numel() == 1 ? out.view(at::IntArrayRef{}) : out, result);
 }
 
 int mc_stats_forward_fast(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** r) {

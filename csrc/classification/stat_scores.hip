@@ -23,7 +23,7 @@ constexpr int kStageBytes = 16384;  // few-bin kernel: LDS copy of a block's 256
 // ----------------------------------------------------------------------------------------------------------------
 // multiclass: per-item predicted label
 // ----------------------------------------------------------------------------------------------------------------
-enum McMode : int { kMcConfmat = 0, kMcStats = 1 };
+enum McMode : int { kMcConfmat = 0, kMcStats = 1, kMcConfmatDual = 2 };  // dual: the batch matrix and the global one
 
 template <typename target_t>
 __device__ __forceinline__ bool mc_target(const target_t* __restrict__ target, long long item, int C, long long ignore,
@@ -241,7 +241,8 @@ template <typename scalar_t, typename target_t, int kPer, int kMode>
 __global__ void __launch_bounds__(kOrdBlock) mc_argmax_ord16_kernel(const scalar_t* __restrict__ preds,
                                                                  const target_t* __restrict__ target, long long N,
                                                                  int C, long long ignore, bool has_ignore,
-                                                                 int64_t* __restrict__ out, int* __restrict__ flag) {
+                                                                 int64_t* __restrict__ out, int* __restrict__ flag,
+                                                                 int64_t* __restrict__ out2 = nullptr) {
   static_assert(sizeof(scalar_t) == 2, "16-bit floats only");
   const int lane = threadIdx.x & (kWave - 1);
   const long long nwaves = static_cast<long long>(gridDim.x) * (blockDim.x / kWave);
@@ -334,6 +335,9 @@ __global__ void __launch_bounds__(kOrdBlock) mc_argmax_ord16_kernel(const scalar
       if (ok) {
         if constexpr (kMode == kMcConfmat) {
           atomic_add_i64(out + static_cast<long long>(t) * C + bidx, 1);
+        } else if constexpr (kMode == kMcConfmatDual) {  // forward(): the batch value and the global state at once
+          atomic_add_i64(out + static_cast<long long>(t) * C + bidx, 1);
+          atomic_add_i64(out2 + static_cast<long long>(t) * C + bidx, 1);
         } else {  // stats workspace [tp | fp | fn | -]: a hit or a miss of the target class (+ the predicted class)
           if (bidx == t) {
             atomic_add_i64(out + t, 1);
@@ -580,15 +584,17 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_kernel(const scalar_t* __re
   lds_flush(lds, nbins, out);
 }
 
-// Few-bin multiclass argmax rows, tiled (X == 1, nbins <= 256, C * sizeof <= 128 B, 16-B aligned preds): the streaming
-// version of mc_fewbins_kernel's LDS staging.  A persistent block walks tiles of 256 * R rows (<= 32 KiB of logits,
-// one contiguous piece of preds): it issues ALL 16-byte loads of its NEXT tile (and that tile's targets) into
-// registers before it evaluates the current one from LDS, so every block keeps a whole tile of loads in flight
-// while it computes (the per-row staging of mc_fewbins_kernel issued ~1 load per thread and then waited on it:
-// 1 M x 10 bf16 rows ran at 0.59 TB/s).  Bins are ballot popcounts in the owning lane's registers, as there; each
-// block flushes its <= 256 bins once.
+// Few-class multiclass argmax rows, tiled (X == 1, C <= kTileMaxC, C * sizeof <= 128 B, 16-B aligned preds): the
+// streaming version of mc_fewbins_kernel's LDS staging.  A persistent block walks tiles of 256 * R rows (<= 32 KiB of
+// logits, one contiguous piece of preds): it issues ALL 16-byte loads of its NEXT tile (and that tile's targets) into
+// registers before it evaluates the current one from LDS, so every block keeps a whole tile of loads in flight while
+// it computes.  Each valid row is ONE LDS atomic into the block's C x C (target, prediction) histogram; the block
+// flushes the matrix (confusion-matrix mode) or the tp / fp / fn derived from it (stats mode: diagonal, column sum -
+// diagonal, row sum - diagonal) once.  (The ballot-per-bin counting this replaces cost O(bins) wave instructions per
+// row: 1 M x 10 bf16 rows ran at 0.56 TB/s, a 65536-row batch took 28 us.)
 constexpr int kTileChunks = 8;  // 16-byte loads per thread per tile (256 threads x 8 x 16 B = 32 KiB)
 constexpr int kTileRows = 8;    // rows per thread per tile (max R)
+constexpr int kTileMaxC = 64;   // the C x C LDS histogram: <= 16 KiB
 
 template <typename scalar_t, typename target_t>
 __global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t* __restrict__ preds,
@@ -596,11 +602,10 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t*
                                                                  int C, int R, long long ignore, bool has_ignore,
                                                                  int mode, int64_t* __restrict__ out,
                                                                  int* __restrict__ flag) {
-  __shared__ int hist[256];
+  __shared__ int hist[kTileMaxC * kTileMaxC];
   __shared__ __attribute__((aligned(16))) unsigned char tile_raw[kTileChunks * kBlock * 16];
-  const int nbins = mode == kMcConfmat ? C * C : 3 * C + 1;
-  const int lane = threadIdx.x & (kWave - 1);
-  for (int b = threadIdx.x; b < nbins; b += kBlock) hist[b] = 0;
+  const int ncm = C * C;
+  for (int b = threadIdx.x; b < ncm; b += kBlock) hist[b] = 0;
   const long long TR = static_cast<long long>(kBlock) * R;  // rows per tile
   const long long ntiles = (N + TR - 1) / TR;
   const long long row_bytes = static_cast<long long>(C) * sizeof(scalar_t);
@@ -623,7 +628,6 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t*
       if (k < R && row < N) tbuf[k] = static_cast<long long>(__builtin_nontemporal_load(target + row));
     }
   };
-  int acc[4] = {0, 0, 0, 0};
   long long tile = blockIdx.x;
   if (tile < ntiles) issue(tile, nbytes_cur);
   for (; tile < ntiles; tile += gridDim.x) {  // block-uniform
@@ -631,7 +635,7 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t*
     long long tcur[kTileRows];
 #pragma unroll
     for (int k = 0; k < kTileRows; ++k) tcur[k] = tbuf[k];
-    __syncthreads();  // the previous tile's rows are read
+    __syncthreads();  // the previous tile's rows are read (and, first time round, the histogram is zeroed)
 #pragma unroll
     for (int j = 0; j < kTileChunks; ++j) {
       const long long o = (static_cast<long long>(j) * kBlock + threadIdx.x) * 16;
@@ -650,59 +654,45 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t*
       if (k >= R) break;  // uniform
       const long long rt = static_cast<long long>(k) * kBlock + threadIdx.x;  // row within the tile
       const long long row = tile * TR + rt;
-      int t = -1, p = -1;
-      if (row < N) {
-        const long long tv = tcur[k];
-        if (!(has_ignore && tv == ignore)) {
-          if (tv < 0 || tv >= C) {
-            raise_flag(flag, kErrTargetOutOfRange);
-          } else {
-            t = static_cast<int>(tv);
-            const scalar_t* pr = lrow + rt * C;
-            float best = to_f32(pr[0]);
-            int bidx = 0;
-            for (int c = 1; c < C; ++c) {
-              const float v = to_f32(pr[c]);
-              if (argmax_better(v, c, best, bidx)) {
-                best = v;
-                bidx = c;
-              }
-            }
-            p = bidx;
-          }
+      if (row >= N) continue;
+      const long long tv = tcur[k];
+      if (has_ignore && tv == ignore) continue;
+      if (tv < 0 || tv >= C) {
+        raise_flag(flag, kErrTargetOutOfRange);
+        continue;
+      }
+      const scalar_t* pr = lrow + rt * C;
+      float best = to_f32(pr[0]);
+      int bidx = 0;
+      for (int c = 1; c < C; ++c) {
+        const float v = to_f32(pr[c]);
+        if (argmax_better(v, c, best, bidx)) {
+          best = v;
+          bidx = c;
         }
       }
-      const bool valid = t >= 0;
-      if (mode == kMcConfmat) {
-        const int key = valid ? t * C + p : -1;
-#pragma unroll
-        for (int slot = 0; slot < 4; ++slot) {
-          const int b0 = slot * kWave;
-          if (b0 >= nbins) break;
-          const int nb = min(kWave, nbins - b0);
-          for (int l = 0; l < nb; ++l) {
-            const int cnt = __popcll(__ballot(key == b0 + l));
-            if (lane == l) acc[slot] += cnt;
-          }
-        }
-      } else {
-        for (int c = 0; c < C; ++c) {
-          const unsigned long long pm = __ballot(valid && p == c), tm = __ballot(valid && t == c);
-          const int tp = __popcll(pm & tm), fp = __popcll(pm & ~tm), fn = __popcll(tm & ~pm);
-          const int bt = c, bf = C + c, bn = 2 * C + c;
-          if ((bt & (kWave - 1)) == lane) acc[bt >> 6] += tp;
-          if ((bf & (kWave - 1)) == lane) acc[bf >> 6] += fp;
-          if ((bn & (kWave - 1)) == lane) acc[bn >> 6] += fn;
-        }
-      }
+      atomicAdd(&hist[static_cast<int>(tv) * C + bidx], 1);
     }
   }
-#pragma unroll
-  for (int slot = 0; slot < 4; ++slot) {
-    const int b = slot * kWave + lane;
-    if (b < nbins && acc[slot]) atomicAdd(&hist[b], acc[slot]);
+  __syncthreads();
+  if (mode == kMcConfmat) {
+    for (int b = threadIdx.x; b < ncm; b += kBlock) {
+      const int v = hist[b];
+      if (v) atomic_add_i64(out + b, v);
+    }
+  } else {  // stats workspace [tp | fp | fn | -]
+    for (int c = threadIdx.x; c < C; c += kBlock) {
+      const int tp = hist[c * C + c];
+      int row = 0, col = 0;
+      for (int j = 0; j < C; ++j) {
+        row += hist[c * C + j];
+        col += hist[j * C + c];
+      }
+      if (tp) atomic_add_i64(out + c, tp);
+      if (col - tp) atomic_add_i64(out + C + c, col - tp);
+      if (row - tp) atomic_add_i64(out + 2LL * C + c, row - tp);
+    }
   }
-  lds_flush(hist, nbins, out);
 }
 
 // fold a multiclass stats workspace [G, 3C+1] into the states; optionally micro-reduce over classes.
@@ -1235,7 +1225,26 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
       const scalar_t* pp = reinterpret_cast<const scalar_t*>(preds.data_ptr());
       if constexpr (IsFloating<scalar_t>::value) {
         const bool vec = (C * sizeof(scalar_t)) % 16 == 0 && (reinterpret_cast<uintptr_t>(pp) % 16) == 0;
-        if (X == 1 && C >= 32 && vec) {
+        static const int tile_grid = [] {
+          const char* e = std::getenv("TM_AMD_FEWBINS_TILE");  // blocks per CU of the tiled kernel; 0 = off
+          return e ? std::atoi(e) : 2;
+        }();
+        // rows per thread per tile: as many as fit 32 KiB of logits (at most kTileRows; TM_AMD_FEWBINS_R caps it)
+        static const int r_cap = [] {
+          const char* e = std::getenv("TM_AMD_FEWBINS_R");
+          return e ? std::max(1, std::min(kTileRows, std::atoi(e))) : kTileRows;
+        }();
+        const long long R = std::min<long long>(r_cap, (kTileChunks * 16LL) / (static_cast<long long>(C) * sizeof(scalar_t)));
+        // short rows (<= 128 B, <= 64 classes): the tiled kernel with its C x C LDS histogram
+        const bool tile_rows = tile_grid > 0 && !samplewise && X == 1 && C <= kTileMaxC && R >= 1 &&
+                               reinterpret_cast<uintptr_t>(pp) % 16 == 0;
+        if (tile_rows) {
+          const long long ntiles = (N + kBlock * R - 1) / (kBlock * R);
+          const int tgrid = static_cast<int>(
+              std::min<long long>(ntiles, static_cast<long long>(cu_count(preds.get_device())) * tile_grid));
+          hipLaunchKernelGGL((mc_fewbins_tile_kernel<scalar_t, target_t>), dim3(tgrid), dim3(kBlock), 0, s, pp, tp, N,
+                             C, static_cast<int>(R), ignore_index, has_ignore, static_cast<int>(mode), outp, flagp);
+        } else if (X == 1 && C >= 32 && vec) {
           // rows of <= 16 lanes x 8 loads x 16 B go 16 lanes per row; longer rows use the whole wave per row
           const long long row_bytes = static_cast<long long>(C) * sizeof(scalar_t);
           static const int lpr_override = [] {
@@ -1318,21 +1327,8 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
           const bool stage = !stage_off && X == 1 &&
                              static_cast<long long>(kBlock) * C * sizeof(scalar_t) <= kStageBytes &&
                              reinterpret_cast<uintptr_t>(pp) % 16 == 0;
-          static const int tile_grid = [] {
-            const char* e = std::getenv("TM_AMD_FEWBINS_TILE");  // blocks per CU of the tiled kernel; 0 = off
-            return e ? std::atoi(e) : 2;
-          }();
-          // rows per thread per tile: as many as fit 32 KiB of logits (at most kTileRows)
-          const long long R = std::min<long long>(kTileRows, (kTileChunks * 16LL) / (static_cast<long long>(C) * sizeof(scalar_t)));
-          if (tile_grid > 0 && stage && R >= 1) {
-            const long long ntiles = (N + kBlock * R - 1) / (kBlock * R);
-            const int tgrid = static_cast<int>(std::min<long long>(ntiles, static_cast<long long>(cu_count(preds.get_device())) * tile_grid));
-            hipLaunchKernelGGL((mc_fewbins_tile_kernel<scalar_t, target_t>), dim3(tgrid), dim3(kBlock), 0, s, pp, tp, N, C,
-                               static_cast<int>(R), ignore_index, has_ignore, static_cast<int>(mode), outp, flagp);
-          } else {
-            hipLaunchKernelGGL((mc_fewbins_kernel<scalar_t, target_t, true>), dim3(grid), dim3(kBlock), 0, s, pp, tp, N,
-                               X, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, stage);
-          }
+          hipLaunchKernelGGL((mc_fewbins_kernel<scalar_t, target_t, true>), dim3(grid), dim3(kBlock), 0, s, pp, tp, N,
+                             X, C, ignore_index, has_ignore, static_cast<int>(mode), outp, flagp, stage);
         } else {
           const int grid = pick_grid(N * X, kBlock);
           hipLaunchKernelGGL((mc_items_kernel<scalar_t, target_t, true>), dim3(grid), dim3(kBlock), lds_bytes, s, pp,
@@ -1535,6 +1531,58 @@ void bin_confmat_finalize(at::Tensor ws, at::Tensor not_prob, at::Tensor confmat
                      ws.data_ptr<int64_t>(), G, not_prob.data_ptr<int>(), confmat.data_ptr<int64_t>());
   hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
   C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+// forward() of the confusion matrix on 16-bit logits: ONE pass of the order-key argmax kernel adds every row into the
+// zeroed batch matrix AND the global state (no separate update + add of two C x C matrices).  Returns false, doing
+// nothing, where the order-key kernel is not the one mc_update would pick (the caller takes update + add).
+bool mc_confmat_dual(const at::Tensor& preds, const at::Tensor& target, at::Tensor batch, at::Tensor global,
+                     at::Tensor flag, int64_t num_classes, int64_t ignore_index, bool has_ignore) {
+  const long long C = num_classes;
+  if (!preds.is_cuda() || preds.dim() != 2 || target.dim() != 1 || preds.size(1) != C || preds.size(0) != target.size(0))
+    return false;
+  if (preds.scalar_type() != at::kBFloat16 && preds.scalar_type() != at::kHalf) return false;
+  if (target.scalar_type() != at::kLong && target.scalar_type() != at::kInt) return false;
+  if (!preds.is_contiguous() || !target.is_contiguous() || reinterpret_cast<uintptr_t>(preds.data_ptr()) % 16 != 0)
+    return false;
+  const long long row_bytes = C * 2;
+  if (row_bytes % 16 != 0 || row_bytes < 1024) return false;  // the LPR-64 rows of the order-key kernel
+  const int per = static_cast<int>((row_bytes / 16 + kWave - 1) / kWave);
+  if (per < 1 || per > 4 || std::getenv("TM_AMD_MC_ORD16") || std::getenv("TM_AMD_MC_PIPE") || std::getenv("TM_AMD_MC_LPR"))
+    return false;
+  for (const at::Tensor* m : {&batch, &global})
+    TORCH_CHECK(m->is_cuda() && m->get_device() == preds.get_device() && m->scalar_type() == at::kLong &&
+                    m->is_contiguous() && m->numel() == C * C,
+                "mc_confmat_dual: matrices must be contiguous int64 [C, C] on the logits' device");
+  TORCH_CHECK(flag.is_cuda() && flag.scalar_type() == at::kInt && flag.get_device() == preds.get_device(),
+              "mc_confmat_dual: bad flag");
+  TM_SAME_DEVICE(preds, target);
+  const long long N = preds.size(0);
+  if (N == 0) return true;
+  const int cus = cu_count(preds.get_device());
+  const long long want16 = (N + kOrdBlock / kWave - 1) / (kOrdBlock / kWave);
+  const int grid16 = static_cast<int>(std::min<long long>(want16, static_cast<long long>(cus) * 4));
+  auto s = stream();
+  TM_DISPATCH_TARGET(target.scalar_type(), "mc_confmat_dual", [&] {
+    const target_t* tp = reinterpret_cast<const target_t*>(target.data_ptr());
+    auto go = [&](auto* pp, auto per_tag) {
+      using scalar_t = std::remove_const_t<std::remove_pointer_t<decltype(pp)>>;
+      constexpr int P = decltype(per_tag)::value;
+      hipLaunchKernelGGL((mc_argmax_ord16_kernel<scalar_t, target_t, P, kMcConfmatDual>), dim3(grid16),
+                         dim3(kOrdBlock), 0, s, pp, tp, N, static_cast<int>(C), ignore_index, has_ignore,
+                         batch.data_ptr<int64_t>(), flag.data_ptr<int>(), global.data_ptr<int64_t>());
+    };
+    auto by_per = [&](auto* pp) {
+      if (per == 1) go(pp, std::integral_constant<int, 1>{});
+      else if (per == 2) go(pp, std::integral_constant<int, 2>{});
+      else if (per == 3) go(pp, std::integral_constant<int, 3>{});
+      else go(pp, std::integral_constant<int, 4>{});
+    };
+    if (preds.scalar_type() == at::kBFloat16) by_per(reinterpret_cast<const c10::BFloat16*>(preds.data_ptr()));
+    else by_per(reinterpret_cast<const c10::Half*>(preds.data_ptr()));
+  });
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return true;
 }
 
 __global__ void launch_probe_kernel(int* __restrict__ flag) {

@@ -596,14 +596,57 @@ constexpr int kTileChunks = 8;  // 16-byte loads per thread per tile (256 thread
 constexpr int kTileRows = 8;    // rows per thread per tile (max R)
 constexpr int kTileMaxC = 64;   // the C x C LDS histogram: <= 16 KiB
 
-template <typename scalar_t, typename target_t>
+// argmax of one row held in LDS at byte offset `off` (16-bit or 32-bit scores): the row's dwords are read into
+// registers first (NW + 1 independent LDS reads, one wait), realigned for rows that start mid-dword (odd C with
+// 16-bit scores), then compared from registers with compile-time indices -- instead of a chain of dependent
+// element reads, each paying the LDS latency.  Same tie / NaN rule as argmax_better (first maximum; NaN wins).
+template <typename scalar_t, int NW>
+__device__ __forceinline__ int row_argmax_regs(const unsigned char* __restrict__ lds, int off, int C) {
+  const uint32_t* wp = reinterpret_cast<const uint32_t*>(lds + (off & ~3));
+  uint32_t w[NW + 1];
+#pragma unroll
+  for (int i = 0; i <= NW; ++i) w[i] = wp[i];
+  const uint32_t sh = static_cast<uint32_t>(off & 3) * 8;  // 0 or 16
+  uint32_t a[NW];
+#pragma unroll
+  for (int i = 0; i < NW; ++i) a[i] = __builtin_amdgcn_alignbit(w[i + 1], w[i], sh);
+  constexpr int kPerWord = 4 / sizeof(scalar_t);
+  float best = 0.0f;
+  int bidx = 0;
+#pragma unroll
+  for (int j = 0; j < NW * kPerWord; ++j) {
+    if (j < C) {
+      const uint32_t word = a[j / kPerWord];
+      float v;
+      if constexpr (sizeof(scalar_t) == 4) {
+        v = __builtin_bit_cast(float, word);
+      } else {
+        const uint16_t h = static_cast<uint16_t>((j % kPerWord) ? (word >> 16) : (word & 0xffffu));
+        v = to_f32(__builtin_bit_cast(scalar_t, h));
+      }
+      if (j == 0) {
+        best = v;
+      } else {
+        const bool take = (v != v) ? !(best != best) : (v > best);  // argmax_better against an earlier column
+        if (take) {
+          best = v;
+          bidx = j;
+        }
+      }
+    }
+  }
+  return bidx;
+}
+
+template <typename scalar_t, typename target_t, int NW>
 __global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t* __restrict__ preds,
                                                                  const target_t* __restrict__ target, long long N,
                                                                  int C, int R, long long ignore, bool has_ignore,
                                                                  int mode, int64_t* __restrict__ out,
                                                                  int* __restrict__ flag) {
   __shared__ int hist[kTileMaxC * kTileMaxC];
-  __shared__ __attribute__((aligned(16))) unsigned char tile_raw[kTileChunks * kBlock * 16];
+  // (+ 256 B: row_argmax_regs reads up to NW + 1 dwords from the last row's start)
+  __shared__ __attribute__((aligned(16))) unsigned char tile_raw[kTileChunks * kBlock * 16 + 256];
   const int ncm = C * C;
   for (int b = threadIdx.x; b < ncm; b += kBlock) hist[b] = 0;
   const long long TR = static_cast<long long>(kBlock) * R;  // rows per tile
@@ -661,14 +704,18 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t*
         raise_flag(flag, kErrTargetOutOfRange);
         continue;
       }
-      const scalar_t* pr = lrow + rt * C;
-      float best = to_f32(pr[0]);
       int bidx = 0;
-      for (int c = 1; c < C; ++c) {
-        const float v = to_f32(pr[c]);
-        if (argmax_better(v, c, best, bidx)) {
-          best = v;
-          bidx = c;
+      if constexpr (NW > 0 && (sizeof(scalar_t) == 2 || sizeof(scalar_t) == 4)) {
+        bidx = row_argmax_regs<scalar_t, NW>(tile_raw, static_cast<int>(rt * C * sizeof(scalar_t)), C);
+      } else {  // 8-byte scores: element reads from LDS
+        const scalar_t* pr = lrow + rt * C;
+        float best = to_f32(pr[0]);
+        for (int c = 1; c < C; ++c) {
+          const float v = to_f32(pr[c]);
+          if (argmax_better(v, c, best, bidx)) {
+            best = v;
+            bidx = c;
+          }
         }
       }
       atomicAdd(&hist[static_cast<int>(tv) * C + bidx], 1);
@@ -1242,8 +1289,20 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
           const long long ntiles = (N + kBlock * R - 1) / (kBlock * R);
           const int tgrid = static_cast<int>(
               std::min<long long>(ntiles, static_cast<long long>(cu_count(preds.get_device())) * tile_grid));
-          hipLaunchKernelGGL((mc_fewbins_tile_kernel<scalar_t, target_t>), dim3(tgrid), dim3(kBlock), 0, s, pp, tp, N,
-                             C, static_cast<int>(R), ignore_index, has_ignore, static_cast<int>(mode), outp, flagp);
+          // dwords per row for the register argmax: 8 (rows <= 32 B) or 32 (<= 128 B); 8-byte scores read LDS
+          const long long rbytes = static_cast<long long>(C) * sizeof(scalar_t);
+          auto launch_tile = [&](auto nw_tag) {
+            constexpr int NW = decltype(nw_tag)::value;
+            hipLaunchKernelGGL((mc_fewbins_tile_kernel<scalar_t, target_t, NW>), dim3(tgrid), dim3(kBlock), 0, s, pp,
+                               tp, N, C, static_cast<int>(R), ignore_index, has_ignore, static_cast<int>(mode), outp,
+                               flagp);
+          };
+          if constexpr (sizeof(scalar_t) == 2 || sizeof(scalar_t) == 4) {
+            if (rbytes <= 32) launch_tile(std::integral_constant<int, 8>{});
+            else launch_tile(std::integral_constant<int, 32>{});
+          } else {
+            launch_tile(std::integral_constant<int, 0>{});
+          }
         } else if (X == 1 && C >= 32 && vec) {
           // rows of <= 16 lanes x 8 loads x 16 B go 16 lanes per row; longer rows use the whole wave per row
           const long long row_bytes = static_cast<long long>(C) * sizeof(scalar_t);

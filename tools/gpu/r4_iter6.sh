@@ -25,3 +25,6 @@ for k, v in sorted(by.items()):
 PY
   rm -rf gpurun_out/prof_fb$r
 done
+timeout -k 10 200 python benchmarks/collection_phases.py --profile gpurun_out/r4i6_collection_profile.txt > gpurun_out/r4i6_collection_phases.json 2>gpurun_out/r4i6_phases.err || { tail -20 gpurun_out/r4i6_phases.err; exit 1; }
+cat gpurun_out/r4i6_collection_phases.json
+head -45 gpurun_out/r4i6_collection_profile.txt | tail -36 | cut -c1-160

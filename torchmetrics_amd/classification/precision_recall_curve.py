@@ -347,11 +347,13 @@ class MulticlassAUROC(MulticlassPrecisionRecallCurve):
         self.validate_args = validate_args
 
     def update(self, preds: Tensor, target: Tensor) -> None:
-        avg, self.average = self.average, None  # the curve state never uses micro averaging here
+        # the curve state never uses micro averaging here (a transient toggle through __dict__: no re-versioning)
+        d = self.__dict__
+        avg, d["average"] = d["average"], None
         try:
             super().update(preds, target)
         finally:
-            self.average = avg
+            d["average"] = avg
 
     def compute(self) -> Tensor:
         return _multiclass_auroc_compute(self._state(), self.num_classes, self.average, self.thresholds)
@@ -434,11 +436,14 @@ class MulticlassAveragePrecision(MulticlassPrecisionRecallCurve):
         self.validate_args = validate_args
 
     def update(self, preds: Tensor, target: Tensor) -> None:
-        avg, self.average = self.average, None
+        # the curve update must not see `average` (micro would flatten the states); a transient toggle through
+        # __dict__, so it is no configuration change (Metric.__setattr__ would re-version the metric every update)
+        d = self.__dict__
+        avg, d["average"] = d["average"], None
         try:
             super().update(preds, target)
         finally:
-            self.average = avg
+            d["average"] = avg
 
     def compute(self) -> Tensor:
         return _multiclass_average_precision_compute(self._state(), self.num_classes, self.average, self.thresholds)

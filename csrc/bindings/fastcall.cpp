@@ -11,6 +11,8 @@
 #include <torch/csrc/autograd/python_variable.h>
 
 #include <ATen/ATen.h>
+
+#include "../common/pack.h"
 #include <c10/util/Optional.h>
 
 #include <tuple>
@@ -907,6 +909,164 @@ PyObject* make_forward(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   return reinterpret_cast<PyObject*>(self);
 }
 
+// ------------------------------------------------------------------------------------- mAP update front end
+// map_pack(preds, target, box_mode) -> (det_box, det_scores, det_labels, gt_box, gt_labels, gt_crowds, gt_area,
+// det_sizes, gt_sizes) or None.  MeanAveragePrecision.update's whole per-image walk in C++: the same acceptance test
+// as detection/helpers.py _inputs_ok (dict keys, tensor types, per-image lengths) plus the conditions for one flat
+// buffer per state (one CUDA device, one dtype per state, contiguous [n] / [n, 4] tensors), then ONE pack kernel
+// launch per 128 (image, state) segments (csrc/detection/pack_images.hip).  box_mode 1 converts xyxy boxes to xywh in
+// the copy; 0 copies them.  None: anything else -- the Python path validates (raising the reference's errors) and
+// packs.
+namespace {
+
+struct ImgTensors {
+  const at::Tensor* t[7];  // det box, scores, labels, gt box, labels, crowds (or null), area (or null)
+  int64_t dn, gn;
+};
+
+const at::Tensor* dict_tensor(PyObject* d, const char* key) {
+  PyObject* o = PyDict_GetItemString(d, key);  // borrowed
+  if (o == nullptr || !THPVariable_Check(o)) return nullptr;
+  return &THPVariable_Unpack(o);
+}
+
+}  // namespace
+
+PyObject* map_pack(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 3 || !PyLong_Check(args[2])) {
+    PyErr_SetString(PyExc_TypeError, "map_pack(preds, target, box_mode)");
+    return nullptr;
+  }
+  const int box_mode = static_cast<int>(PyLong_AsLong(args[2]));
+  if (!(PyList_Check(args[0]) || PyTuple_Check(args[0])) || !(PyList_Check(args[1]) || PyTuple_Check(args[1])))
+    Py_RETURN_NONE;
+  PyObject* pf = PySequence_Fast(args[0], "preds");
+  PyObject* tf = PySequence_Fast(args[1], "target");
+  if (pf == nullptr || tf == nullptr) {
+    Py_XDECREF(pf);
+    Py_XDECREF(tf);
+    return nullptr;
+  }
+  auto done_none = [&]() {
+    Py_DECREF(pf);
+    Py_DECREF(tf);
+    Py_RETURN_NONE;
+  };
+  const Py_ssize_t N = PySequence_Fast_GET_SIZE(pf);
+  if (N == 0 || N != PySequence_Fast_GET_SIZE(tf)) return done_none();
+  std::vector<ImgTensors> imgs(static_cast<size_t>(N));
+  at::ScalarType dt[7];
+  bool have[7] = {false, false, false, false, false, false, false};
+  int dev = -1;
+  int64_t D = 0, G = 0;
+  for (Py_ssize_t i = 0; i < N; ++i) {
+    PyObject* p = PySequence_Fast_GET_ITEM(pf, i);
+    PyObject* t = PySequence_Fast_GET_ITEM(tf, i);
+    if (!PyDict_Check(p) || !PyDict_Check(t)) return done_none();
+    ImgTensors& im = imgs[static_cast<size_t>(i)];
+    im.t[0] = dict_tensor(p, "boxes");
+    im.t[1] = dict_tensor(p, "scores");
+    im.t[2] = dict_tensor(p, "labels");
+    im.t[3] = dict_tensor(t, "boxes");
+    im.t[4] = dict_tensor(t, "labels");
+    im.t[5] = PyDict_GetItemString(t, "iscrowd") ? dict_tensor(t, "iscrowd") : nullptr;
+    im.t[6] = PyDict_GetItemString(t, "area") ? dict_tensor(t, "area") : nullptr;
+    if (!im.t[0] || !im.t[1] || !im.t[2] || !im.t[3] || !im.t[4]) return done_none();
+    if ((PyDict_GetItemString(t, "iscrowd") && !im.t[5]) || (PyDict_GetItemString(t, "area") && !im.t[6]))
+      return done_none();
+    if (im.t[2]->dim() != 1 || im.t[4]->dim() != 1) return done_none();
+    im.dn = im.t[2]->size(0);
+    im.gn = im.t[4]->size(0);
+    for (int k = 0; k < 7; ++k) {
+      const at::Tensor* x = im.t[k];
+      if (x == nullptr) continue;
+      const int64_t n = k < 3 ? im.dn : im.gn;
+      if (!x->is_cuda() || !x->is_contiguous()) return done_none();
+      if (dev < 0) dev = x->get_device();
+      if (x->get_device() != dev) return done_none();
+      if (k == 0 || k == 3) {  // boxes [n, 4] (an empty image may hold any empty shape)
+        if (x->numel() == 0 ? n != 0 : (x->dim() != 2 || x->size(0) != n || x->size(1) != 4)) return done_none();
+      } else if (x->dim() != 1 || x->size(0) != n) {
+        return done_none();
+      }
+      if (!have[k]) {
+        dt[k] = x->scalar_type();
+        have[k] = true;
+      } else if (dt[k] != x->scalar_type()) {
+        return done_none();
+      }
+    }
+    D += im.dn;
+    G += im.gn;
+  }
+  // missing iscrowd / area are zeros of the labels' dtype (zeros_like(labels)): one dtype per state in any case
+  for (int k = 5; k < 7; ++k) {
+    bool missing = false;
+    for (const auto& im : imgs) missing |= im.t[k] == nullptr;
+    if (!have[k]) dt[k] = dt[4];
+    else if (missing && dt[k] != dt[4]) return done_none();
+  }
+  if (dt[0] != at::kFloat && dt[0] != at::kDouble) return done_none();
+  if (dt[3] != at::kFloat && dt[3] != at::kDouble) return done_none();
+  PyObject* result = nullptr;
+  try {
+    const auto opt = at::TensorOptions().device(at::kCUDA, dev);
+    at::Tensor out[7] = {
+        at::empty({D, 4}, opt.dtype(dt[0])), at::empty({D}, opt.dtype(dt[1])), at::empty({D}, opt.dtype(dt[2])),
+        at::empty({G, 4}, opt.dtype(dt[3])), at::empty({G}, opt.dtype(dt[4])), at::empty({G}, opt.dtype(dt[5])),
+        at::empty({G}, opt.dtype(dt[6]))};
+    std::vector<tm_amd::PackSeg> segs;
+    segs.reserve(static_cast<size_t>(N) * 7);
+    int64_t doff = 0, goff = 0;
+    for (const auto& im : imgs) {
+      for (int k = 0; k < 7; ++k) {
+        const int64_t n = k < 3 ? im.dn : im.gn;
+        if (n == 0) continue;
+        const int64_t off = k < 3 ? doff : goff;
+        const bool box = k == 0 || k == 3;
+        const int64_t es = static_cast<int64_t>(out[k].element_size());
+        tm_amd::PackSeg sg;
+        sg.dst = static_cast<char*>(out[k].data_ptr()) + off * es * (box ? 4 : 1);
+        sg.src = im.t[k] != nullptr ? im.t[k]->data_ptr() : nullptr;
+        sg.esize = static_cast<int16_t>(es);
+        if (box && box_mode == 1) {
+          sg.mode = tm_amd::kPackXyxyToXywh;
+          sg.n = static_cast<int32_t>(n);
+        } else {
+          sg.mode = sg.src == nullptr ? tm_amd::kPackZero : tm_amd::kPackCopy;
+          sg.n = static_cast<int32_t>(n * (box ? 4 : 1));
+        }
+        segs.push_back(sg);
+      }
+      doff += im.dn;
+      goff += im.gn;
+    }
+    tm_amd::pack_segments(segs.data(), static_cast<int>(segs.size()), dev);
+    PyObject* ds = PyList_New(N);
+    PyObject* gs = PyList_New(N);
+    if (ds == nullptr || gs == nullptr) {
+      Py_XDECREF(ds);
+      Py_XDECREF(gs);
+      Py_DECREF(pf);
+      Py_DECREF(tf);
+      return nullptr;
+    }
+    for (Py_ssize_t i = 0; i < N; ++i) {
+      PyList_SET_ITEM(ds, i, PyLong_FromLongLong(imgs[static_cast<size_t>(i)].dn));
+      PyList_SET_ITEM(gs, i, PyLong_FromLongLong(imgs[static_cast<size_t>(i)].gn));
+    }
+    result = PyTuple_New(9);
+    for (int k = 0; k < 7; ++k) PyTuple_SET_ITEM(result, k, THPVariable_Wrap(out[k]));
+    PyTuple_SET_ITEM(result, 7, ds);
+    PyTuple_SET_ITEM(result, 8, gs);
+  } catch (const c10::Error& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what_without_backtrace());
+  }
+  Py_DECREF(pf);
+  Py_DECREF(tf);
+  return result;
+}
+
 PyMethodDef kFactoryMethods[] = {
     {"stats_updater", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&make_stats_updater)),
      METH_FASTCALL, "native update of the stat-score family bound to a metric's __dict__"},
@@ -914,6 +1074,8 @@ PyMethodDef kFactoryMethods[] = {
      "native Metric.forward of the confusion-matrix / stat-score families bound to a metric's __dict__"},
     {"confmat_updater", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&make_confmat_updater)),
      METH_FASTCALL, "native MulticlassConfusionMatrix.update bound to a metric's __dict__"},
+    {"map_pack", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&map_pack)), METH_FASTCALL,
+     "MeanAveragePrecision.update's per-image validation and packing in one native call"},
     {"_states_unobserved", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&states_unobserved_probe)),
      METH_FASTCALL, "the native forward's test that nothing outside the metric holds the given states"},
     {nullptr, nullptr, 0, nullptr},

@@ -544,3 +544,74 @@ def _ddp_map_packed(rank, world, preds, target):
 def test_map_ddp_packed_sync():
     preds, target = _random_coco(13, n_img=9)
     run_ddp(_ddp_map_packed, preds, target)
+
+
+def _map_batch(n_img, seed, box_dtype=torch.float32, drop_keys=()):
+    g = torch.Generator().manual_seed(seed)
+    preds, target = [], []
+    for i in range(n_img):
+        nd, ng = int(torch.randint(0, 12, (1,), generator=g)), int(torch.randint(0, 6, (1,), generator=g))
+        xy = torch.rand(ng, 2, generator=g) * 100
+        gb = torch.cat([xy, xy + torch.rand(ng, 2, generator=g) * 50 + 1], 1).to(box_dtype)
+        dxy = torch.rand(nd, 2, generator=g) * 100
+        db = torch.cat([dxy, dxy + torch.rand(nd, 2, generator=g) * 50 + 1], 1).to(box_dtype)
+        p = {"boxes": db, "scores": torch.rand(nd, generator=g), "labels": torch.randint(0, 5, (nd,), generator=g)}
+        t = {"boxes": gb, "labels": torch.randint(0, 5, (ng,), generator=g)}
+        if "iscrowd" not in drop_keys or i % 2:
+            t["iscrowd"] = (torch.rand(ng, generator=g) < 0.2).long()
+        if "area" not in drop_keys or i % 3 == 0:
+            t["area"] = torch.rand(ng, generator=g) * 1000 if "area_float" in drop_keys else torch.randint(
+                1, 1000, (ng,), generator=g)
+        preds.append(p)
+        target.append(t)
+    return preds, target
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("box_format", ["xyxy", "xywh", "cxcywh"])
+@pytest.mark.parametrize("drop_keys", [(), ("iscrowd",), ("iscrowd", "area")])
+@pytest.mark.parametrize("box_dtype", [torch.float32, torch.float64])
+def test_map_native_pack_matches_python_path(monkeypatch, box_format, drop_keys, box_dtype):
+    """csrc/bindings/fastcall.cpp map_pack + csrc/detection/pack_images.hip: the flat states equal the Python
+    packing (cat + box_convert), including empty images and missing iscrowd / area; compute() is identical."""
+    dev = torch.device("cuda", 0)
+    batches = [_map_batch(17, s, box_dtype, drop_keys) for s in range(3)]
+    to = lambda b: [{k: v.to(dev) for k, v in d.items()} for d in b]  # noqa: E731
+    native = MeanAveragePrecision(box_format=box_format, class_metrics=True).to(dev)
+    python = MeanAveragePrecision(box_format=box_format, class_metrics=True).to(dev)
+    calls = []
+    real = ops.map_pack
+    monkeypatch.setattr(ops, "map_pack", lambda *a: calls.append(1) or real(*a))
+    for p, t in batches:
+        native.update(to(p), to(t))
+    assert len(calls) == 3
+    monkeypatch.setattr(MeanAveragePrecision, "_native_pack", lambda self, p, t: False)
+    for p, t in batches:
+        python.update(to(p), to(t))
+    for name in MeanAveragePrecision._NATIVE_ORDER:
+        a, sa = native._packed_state(name)
+        b, sb = python._packed_state(name)
+        assert sa == sb, name
+        assert a.dtype == b.dtype and torch.equal(a, b), name
+    ra, rb = native.compute(), python.compute()
+    for k in rb:
+        torch.testing.assert_close(ra[k], rb[k], equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_map_native_pack_declines_irregular_batches():
+    dev = torch.device("cuda", 0)
+    p, t = _map_batch(4, 9)
+    p = [{k: v.to(dev) for k, v in d.items()} for d in p]
+    t = [{k: v.to(dev) for k, v in d.items()} for d in t]
+    assert ops.map_pack(p, t, 1) is not None
+    mixed = [dict(d) for d in p]
+    mixed[1]["scores"] = mixed[1]["scores"].double()
+    assert ops.map_pack(mixed, t, 1) is None  # one dtype per state
+    short = [dict(d) for d in p]
+    short[2]["scores"] = short[2]["scores"][:-1] if short[2]["scores"].numel() else torch.rand(1, device=dev)
+    assert ops.map_pack(short, t, 1) is None  # per-image lengths disagree: the Python validator raises
+    with pytest.raises(ValueError):
+        MeanAveragePrecision().to(dev).update(short, t)
+    cpu = [{k: v.cpu() for k, v in d.items()} for d in p]
+    assert ops.map_pack(cpu, [{k: v.cpu() for k, v in d.items()} for d in t], 1) is None

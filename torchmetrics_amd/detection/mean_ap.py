@@ -131,6 +131,8 @@ class MeanAveragePrecision(Metric):
         stored as one chunk (``Metric._append_chunk``: per-image views are only built if something reads the list),
         one box conversion, one zero tensor for the missing ``iscrowd`` / ``area`` entries.  The reference appends
         9 tensors per image and converts boxes image by image (``S/detection/mean_ap.py:470-511``)."""
+        if self._native_pack(preds, target):
+            return
         _input_validator(preds, target, iou_type=self.iou_type)
         if not preds:
             return
@@ -169,6 +171,29 @@ class MeanAveragePrecision(Metric):
         if segm:
             self.detection_mask.extend(det_rle)
             self.groundtruth_mask.extend(gt_rle)
+
+    def _native_pack(self, preds: Any, target: Any) -> bool:
+        """ROCm bbox batches: validation and packing of every image into the 7 flat states in one native call
+        (``csrc/bindings/fastcall.cpp`` map_pack + ``csrc/detection/pack_images.hip``: one launch per 128 (image,
+        state) segments, xyxy -> xywh fused into the copy).  False (nothing done) for anything else: the Python path
+        below validates -- raising the reference's errors -- and packs."""
+        if self.iou_type != ("bbox",) or not preds or not ops.native_available():
+            return False
+        box_mode = 1 if self.box_format == "xyxy" else 0
+        got = ops.map_pack(preds, target, box_mode)
+        if got is None:
+            return False
+        *flats, det_n, gt_n = got
+        if self.warn_on_many_detections and max(det_n) > self.max_detection_thresholds[-1]:
+            _warning_on_too_many_detections(self.max_detection_thresholds[-1])
+        for name, flat in zip(self._NATIVE_ORDER, flats):
+            if name in self._BOX_STATES and box_mode == 0 and self.box_format != "xywh" and flat.numel():
+                flat = box_convert(flat, in_fmt=self.box_format, out_fmt="xywh")
+            self._append_chunk(name, flat, det_n if name.startswith("detection") else gt_n)
+        return True
+
+    _NATIVE_ORDER = ("detection_box", "detection_scores", "detection_labels", "groundtruth_box", "groundtruth_labels",
+                     "groundtruth_crowds", "groundtruth_area")
 
     @staticmethod
     def _stack_images(parts: List[Tensor], sizes: List[int], width: Optional[int]) -> Optional[Tensor]:

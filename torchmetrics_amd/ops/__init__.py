@@ -608,7 +608,7 @@ class MomentsPlan:
     one or two launches for the whole collection)."""
 
     __slots__ = ("preds", "target", "k", "dests", "ids", "eps", "power", "fold_states", "shift_p", "shift_t", "src",
-                 "checked")
+                 "checked", "_mask")
 
     def __init__(self, preds: Tensor, target: Tensor, k: int, dests: "list[Tensor]", ids: "list[int]",
                  eps: float = 1.17e-06, power: float = 2.0, fold_states: Optional["list[Tensor]"] = None,
@@ -620,6 +620,7 @@ class MomentsPlan:
         self.fold_states, self.shift_p, self.shift_t = fold_states, shift_p, shift_t
         self.src = src if src is not None else (preds, target)  # the caller's input objects (merge key)
         self.checked = checked  # destinations already validated (see states_ready)
+        self._mask = None
 
     def deferrable(self) -> bool:
         p, t = self.preds, self.target
@@ -631,11 +632,14 @@ class MomentsPlan:
         return all(d.get_device() == dev and d.is_contiguous() for d in self.dests + (self.fold_states or []))
 
     def _uses(self) -> int:
-        m = 0
-        for i in self.ids:
-            for j in _sum_ids(int(i)):
-                m |= 1 << j
-        return m
+        m = self._mask
+        if m is None or m[0] != len(self.ids):  # (ids only grow, by merging)
+            bits = 0
+            for i in self.ids:
+                for j in _sum_ids(int(i)):
+                    bits |= 1 << j
+            m = self._mask = (len(self.ids), bits)
+        return m[1]
 
     def key(self) -> tuple:
         """Plans merge when they read the same input objects with the same column count (and the same eps /
@@ -1155,6 +1159,15 @@ def box_pairwise(a: Tensor, b: Tensor, op: int = BOX_IOU, aligned: bool = False)
         dt = a.dtype if a.dtype in (torch.float32, torch.float16, torch.bfloat16, torch.float64) else torch.float32
         return _ops().box_pairwise(a.to(dt).contiguous(), b.to(dt).contiguous(), op, aligned)
     return _cpu.box_pairwise(a, b, op, aligned)
+
+
+def map_pack(preds: Any, target: Any, box_mode: int) -> Any:
+    """MeanAveragePrecision.update's per-image validation + packing into the 7 flat bbox states in one native call
+    (``csrc/bindings/fastcall.cpp`` map_pack): ``(7 flat tensors, det_sizes, gt_sizes)`` or None where the batch is
+    not a regular ROCm batch (the caller's Python path handles it)."""
+    mod = _fast_mod or _fast()
+    fn = getattr(mod, "map_pack", None)
+    return fn(preds, target, int(box_mode)) if fn is not None else None
 
 
 def box_pairwise_ragged(a: Tensor, b: Tensor, a_off: Tensor, b_off: Tensor, o_off: Tensor, a_lab: Tensor,

@@ -27,6 +27,7 @@ import os
 import warnings
 from typing import Any, Dict, List, Optional, Tuple
 
+import numpy as np
 import torch
 from torch import Tensor
 
@@ -61,6 +62,9 @@ class CollectionPlan:
         self.rows: Optional[Tensor] = None
         self.lds = 0
         self.ok = False
+        self.state_sig: List[Tuple[Any, str, Tuple[int, ...], torch.dtype]] = []
+        self._seen: Optional[Tuple[Any, ...]] = None  # the state objects valid() last checked in full
+        self._last_ptrs: Optional[Tuple[int, ...]] = None
         self._build(members)
 
     # ------------------------------------------------------------------------------------------------- record
@@ -188,13 +192,22 @@ class CollectionPlan:
         if not self.fused:
             return
         self.rows = torch.tensor(rows_all, dtype=torch.int64)
+        self.flat_np = self.rows.numpy().reshape(-1)  # the same memory: pointer patches go through numpy (~1 us each)
         self.ncol = self.rows.shape[1]
-        self.out_sizes = out_sizes
-        self.out_idx = {dt: torch.tensor([i for i, _ in sl], dtype=torch.int64) for dt, sl in out_slots.items()}
-        self.out_bytes = {dt: torch.tensor([o * torch.empty(0, dtype=dt).element_size() for _, o in sl],
-                                           dtype=torch.int64) for dt, sl in out_slots.items()}
-        self.in_idx = torch.tensor([i for i, _, _, _ in self.in_slots], dtype=torch.int64)
-        self.in_off = torch.tensor([o for _, _, _, o in self.in_slots], dtype=torch.int64)
+        # every output dtype's buffer is a 256-byte aligned piece of ONE byte allocation per run
+        self.out_layout: List[Tuple[torch.dtype, int, int]] = []  # (dtype, byte offset, bytes)
+        nbytes = 0
+        for dt, n in out_sizes.items():
+            nb = n * torch.empty(0, dtype=dt).element_size()
+            self.out_layout.append((dt, nbytes, nb))
+            nbytes += -(-nb // 256) * 256
+        self.out_bytes_total = max(nbytes, 256)
+        base = {dt: off for dt, off, _ in self.out_layout}
+        self.out_idx = np.array([i for sl in out_slots.values() for i, _ in sl], dtype=np.int64)
+        self.out_rel = np.array([base[dt] + o * torch.empty(0, dtype=dt).element_size()
+                                 for dt, sl in out_slots.items() for _, o in sl], dtype=np.int64)
+        self.in_idx = np.array([i for i, _, _, _ in self.in_slots], dtype=np.int64)
+        self.in_off = np.array([o for _, _, _, o in self.in_slots], dtype=np.int64)
         # distinct (metric, state) pairs, in slot order, and each slot's index into them
         pairs: Dict[Tuple[int, str], int] = {}
         self.in_pairs: List[Tuple[Any, str]] = []
@@ -205,7 +218,7 @@ class CollectionPlan:
                 pairs[k] = len(self.in_pairs)
                 self.in_pairs.append((m, a))
             slot_pair.append(pairs[k])
-        self.slot_pair = torch.tensor(slot_pair, dtype=torch.int64)
+        self.slot_pair = np.array(slot_pair, dtype=np.int64)
         self.keys = {f.key for f in self.fused}
         self.device = self.fused[0].metric.__dict__[self.in_pairs[0][1]].device if self.in_pairs else None
         self.ok = self.device is not None
@@ -215,32 +228,37 @@ class CollectionPlan:
         for f in self.fused:
             if f.metric.__dict__.get("_cfg_version", 0) != f.version:
                 return False
-        for m, a, shape, dtype in self.state_sig:
-            t = m.__dict__.get(a)
+        # the same state objects as at the last full check (the common case: states updated in place): valid
+        cur = tuple(m.__dict__.get(a) for m, a, _, _ in self.state_sig)
+        if self._seen is not None and len(cur) == len(self._seen) and all(x is y for x, y in zip(cur, self._seen)):
+            return True
+        for (m, a, shape, dtype), t in zip(self.state_sig, cur):
             if not isinstance(t, Tensor) or t.dtype != dtype or t.shape != shape or not t.is_cuda:
                 return False
+        self._seen = cur
         return True
 
     def run(self) -> Tuple[Dict[str, Any], Dict[str, List[Tuple[Tensor, str, Any]]]]:
         """One launch for every fused member: ``({key: result}, {key: deferred checks})``."""
-        d0 = self.device
-        ptrs = torch.tensor([m.__dict__[a].data_ptr() for m, a in self.in_pairs], dtype=torch.int64)
-        flat = self.rows.view(-1)
-        flat[self.in_idx] = ptrs[self.slot_pair] + self.in_off
-        bufs = {}
-        for dt, n in self.out_sizes.items():
-            buf = torch.empty(n, dtype=dt, device=d0)
-            bufs[dt] = buf
-            flat[self.out_idx[dt]] = self.out_bytes[dt] + buf.data_ptr()
-        anchor = next(iter(bufs.values()))
+        flat = self.flat_np
+        ptrs = tuple(m.__dict__[a].data_ptr() for m, a in self.in_pairs)
+        if ptrs != self._last_ptrs:  # states moved (reset, sync, .to()): re-point the input slots
+            flat[self.in_idx] = np.asarray(ptrs, dtype=np.int64)[self.slot_pair] + self.in_off
+            self._last_ptrs = ptrs
+        raw = torch.empty(self.out_bytes_total, dtype=torch.uint8, device=self.device)
+        flat[self.out_idx] = self.out_rel + raw.data_ptr()
+        bufs = {dt: raw[off : off + nb].view(dt) for dt, off, nb in self.out_layout}
         mx = 32
+        tasks = ops._ops().compute_tasks
         for i in range(0, self.rows.shape[0], mx):
-            ops._ops().compute_tasks(self.rows[i : i + mx], anchor, self.lds)
+            tasks(self.rows[i : i + mx], raw, self.lds)
         results: Dict[str, Any] = {}
         checks: Dict[str, List[Tuple[Tensor, str, Any]]] = {}
         strided = torch.as_strided
         for f in self.fused:
-            leaves = [strided(bufs[dt], shape, stride, off) for dt, off, shape, stride in f.leaves]
+            # (as_strided offsets count from the shared storage's start: add each dtype view's own offset)
+            leaves = [strided(bufs[dt], shape, stride, bufs[dt].storage_offset() + off)
+                      for dt, off, shape, stride in f.leaves]
             results[f.key] = _rebuild(f.spec, leaves)
             if f.checks:
                 checks[f.key] = [(bufs[dt][off : off + 1], msg, exc) for dt, off, msg, exc in f.checks]

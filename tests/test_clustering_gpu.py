@@ -82,3 +82,19 @@ def test_dense_labels_match_unique_inverse():
     ids, k = ops.dense_labels(lab.to(DEV))
     uniq, inv = torch.unique(lab, return_inverse=True)
     assert k == uniq.numel() and torch.equal(ids.cpu(), inv)
+
+
+@pytest.mark.parametrize("n,kp,kt", [(50, 3, 4), (5000, 7, 5), (200_000, 12, 9), (100, 1, 3)])
+def test_expected_mutual_info_kernel_matches_term_sum(n, kp, kt):
+    """csrc/clustering/emi.hip (log-gamma recurrence, one thread per run of terms) against the vectorised fp64 term
+    sum on the host (every (i, j, n_ij) term with nine lgamma calls, as the reference)."""
+    from torchmetrics_amd.functional import clustering as FC
+
+    g = torch.Generator().manual_seed(n + kp)
+    p = torch.randint(0, kp, (n,), generator=g)
+    t = torch.randint(0, kt, (n,), generator=g)
+    cont = FC._mutual_info_score_update(p, t)
+    ref = FC.expected_mutual_info_score(cont, n)
+    got = FC.expected_mutual_info_score(cont.cuda(), n)
+    assert got.is_cuda
+    torch.testing.assert_close(got.cpu(), ref, rtol=1e-6, atol=1e-9)

@@ -1161,6 +1161,12 @@ def box_pairwise(a: Tensor, b: Tensor, op: int = BOX_IOU, aligned: bool = False)
     return _cpu.box_pairwise(a, b, op, aligned)
 
 
+def expected_mutual_info(a: Tensor, b: Tensor, n: float) -> Tensor:
+    """Expected mutual information of clusterings with fp64 sizes ``a`` [R] / ``b`` [C] over ``n`` samples, one kernel
+    (``csrc/clustering/emi.hip``); fp64 0-d on the device."""
+    return _ops().expected_mutual_info(a, b, float(n))
+
+
 def map_pack(preds: Any, target: Any, box_mode: int) -> Any:
     """MeanAveragePrecision.update's per-image validation + packing into the 7 flat bbox states in one native call
     (``csrc/bindings/fastcall.cpp`` map_pack): ``(7 flat tensors, det_sizes, gt_sizes)`` or None where the batch is

@@ -43,6 +43,24 @@ def calculate_entropy(x: Tensor) -> Tensor:
     return -torch.sum((p / n) * (torch.log(p) - torch.log(n)))
 
 
+def _entropy_of_counts(counts: Tensor) -> Tensor:
+    """``calculate_entropy`` from a label histogram (a contingency table's row / column sums: the same counts
+    ``torch.unique`` would return, in the same order) -- no sort of the raw labels."""
+    p = counts[counts > 0].to(torch.float32)
+    if p.numel() == 1:
+        return torch.tensor(0.0, device=counts.device)
+    n = p.sum()
+    return -torch.sum((p / n) * (torch.log(p) - torch.log(n)))
+
+
+def _mi_and_entropies(preds: Tensor, target: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """(contingency [target x preds], MI, H(preds), H(target)) from ONE contingency table."""
+    cont = calculate_contingency_matrix(preds, target)
+    if preds.numel() == 0:
+        return cont, _mutual_info_score_compute(cont), calculate_entropy(preds), calculate_entropy(target)
+    return cont, _mutual_info_score_compute(cont), _entropy_of_counts(cont.sum(0)), _entropy_of_counts(cont.sum(1))
+
+
 def calculate_generalized_mean(x: Tensor, p: Union[int, Literal["min", "geometric", "arithmetic", "max"]]) -> Tensor:
     if torch.is_complex(x) or not is_nonnegative(x):
         raise ValueError("`x` must contain positive real numbers")
@@ -181,11 +199,10 @@ def adjusted_mutual_info_score(preds: Tensor, target: Tensor,
                                ) -> Tensor:
     """Mutual information adjusted for chance."""
     _validate_average_method_arg(average_method)
-    contingency = _mutual_info_score_update(preds, target)
-    mi = _mutual_info_score_compute(contingency)
+    check_cluster_labels(preds, target)
+    contingency, mi, h_p, h_t = _mi_and_entropies(preds, target)
     emi = expected_mutual_info_score(contingency, target.numel())
-    normalizer = calculate_generalized_mean(torch.stack([calculate_entropy(preds), calculate_entropy(target)]),
-                                            average_method)
+    normalizer = calculate_generalized_mean(torch.stack([h_p, h_t]), average_method)
     den = normalizer - emi
     eps = torch.finfo(den.dtype).eps
     den = torch.where(den < 0, torch.clamp(den, max=-eps), torch.clamp(den, min=eps))
@@ -198,11 +215,10 @@ def normalized_mutual_info_score(preds: Tensor, target: Tensor,
     """Mutual information normalised by a generalized mean of the two entropies."""
     check_cluster_labels(preds, target)
     _validate_average_method_arg(average_method)
-    mi = mutual_info_score(preds, target)
+    _, mi, h_p, h_t = _mi_and_entropies(preds, target)
     if torch.allclose(mi, torch.tensor(0.0, device=mi.device), atol=torch.finfo().eps):
         return mi
-    normalizer = calculate_generalized_mean(torch.stack([calculate_entropy(preds), calculate_entropy(target)]),
-                                            average_method)
+    normalizer = calculate_generalized_mean(torch.stack([h_p, h_t]), average_method)
     return mi / normalizer
 
 
@@ -254,8 +270,7 @@ def _homogeneity_score_compute(preds: Tensor, target: Tensor) -> Tuple[Tensor, T
     if len(target) == 0:
         zero = torch.tensor(0.0, dtype=torch.float32, device=preds.device)
         return zero.clone(), zero.clone(), zero.clone(), zero.clone()
-    h_t, h_p = calculate_entropy(target), calculate_entropy(preds)
-    mi = mutual_info_score(preds, target)
+    _, mi, h_p, h_t = _mi_and_entropies(preds, target)
     homogeneity = mi / h_t if h_t else torch.ones_like(h_t)
     return homogeneity, mi, h_p, h_t
 

@@ -28,7 +28,11 @@ def test_public_reset_clears_deferred_validation_word():
 
 
 def test_forward_raise_restores_global_state_and_flags():
+    """Metric.forward (the Python path: the native forward defers a batch's value-range error to the next compute(),
+    tests/test_native_forward_gpu.py::test_forward_errors_surface_at_compute) raises inside forward and restores the
+    global state and the batch-mode flags."""
     m = MulticlassAccuracy(num_classes=4, average="micro").cuda()
+    m.__dict__.pop("forward", None)
     m.update(*_batch(seed=2))
     before = {k: getattr(m, k).clone() for k in m._defaults}
     count = m._update_count

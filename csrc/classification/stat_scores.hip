@@ -1274,14 +1274,19 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
         const bool vec = (C * sizeof(scalar_t)) % 16 == 0 && (reinterpret_cast<uintptr_t>(pp) % 16) == 0;
         static const int tile_grid = [] {
           const char* e = std::getenv("TM_AMD_FEWBINS_TILE");  // blocks per CU of the tiled kernel; 0 = off
-          return e ? std::atoi(e) : 2;
+          return e ? std::atoi(e) : 3;                          // (3 x 49 KiB of LDS fit a CU: one round of tiles)
         }();
         // rows per thread per tile: as many as fit 32 KiB of logits (at most kTileRows; TM_AMD_FEWBINS_R caps it)
         static const int r_cap = [] {
           const char* e = std::getenv("TM_AMD_FEWBINS_R");
           return e ? std::max(1, std::min(kTileRows, std::atoi(e))) : kTileRows;
         }();
-        const long long R = std::min<long long>(r_cap, (kTileChunks * 16LL) / (static_cast<long long>(C) * sizeof(scalar_t)));
+        // ... and no more than it takes to give every co-resident block a tile: a small batch (8192 rows) is then
+        // 32 one-row-per-thread tiles in parallel instead of 6 six-row tiles
+        const long long r_fit = (kTileChunks * 16LL) / (static_cast<long long>(C) * sizeof(scalar_t));
+        const long long r_spread = (N + static_cast<long long>(kBlock) * cu_count(preds.get_device()) * std::max(tile_grid, 1) - 1) /
+                                   (static_cast<long long>(kBlock) * cu_count(preds.get_device()) * std::max(tile_grid, 1));
+        const long long R = std::min<long long>({static_cast<long long>(r_cap), r_fit, std::max<long long>(1, r_spread)});
         // short rows (<= 128 B, <= 64 classes): the tiled kernel with its C x C LDS histogram
         const bool tile_rows = tile_grid > 0 && !samplewise && X == 1 && C <= kTileMaxC && R >= 1 &&
                                reinterpret_cast<uintptr_t>(pp) % 16 == 0;

@@ -18,7 +18,8 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kLdsBins = 12288;  // 48 KiB of int32 bins
-constexpr int kStageBytes = 16384;  // few-bin kernel: LDS copy of a block's 256 argmax rows
+constexpr int kStageBytes = 16384;
+constexpr long long kFinalizeOneBlock = 8192;  // label groups a single finalize block folds (then no re-arm launch)  // few-bin kernel: LDS copy of a block's 256 argmax rows
 
 // ----------------------------------------------------------------------------------------------------------------
 // multiclass: per-item predicted label
@@ -1172,10 +1173,13 @@ __global__ void __launch_bounds__(kBlock) bin_seg_kernel(const scalar_t* __restr
 }
 
 // states (per group g): accumulate or write tp/fp/tn/fn; picks interpretation A/B from not_prob; zeros ws + flag.
+// zero_np (single-block launch): the block also re-arms not_prob after every thread has read it -- no separate
+// one-thread launch
 __global__ void __launch_bounds__(kBlock) bin_finalize_kernel(int64_t* __restrict__ ws, long long G,
                                                               int* __restrict__ not_prob, bool accumulate,
                                                               int64_t* __restrict__ tp, int64_t* __restrict__ fp,
-                                                              int64_t* __restrict__ tn, int64_t* __restrict__ fn) {
+                                                              int64_t* __restrict__ tn, int64_t* __restrict__ fn,
+                                                              bool zero_np) {
   const bool use_b = *not_prob != 0;
   for (long long g = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; g < G;
        g += static_cast<long long>(gridDim.x) * blockDim.x) {
@@ -1192,12 +1196,16 @@ __global__ void __launch_bounds__(kBlock) bin_finalize_kernel(int64_t* __restric
 #pragma unroll
     for (int s = 0; s < kBinSlots; ++s) w[s] = 0;
   }
+  if (zero_np) {
+    __syncthreads();
+    if (threadIdx.x == 0) *not_prob = 0;
+  }
 }
 
 // binary / multilabel confusion matrices [G, 2, 2] (rows = target, cols = pred) accumulated in place
 __global__ void __launch_bounds__(kBlock) bin_confmat_finalize_kernel(int64_t* __restrict__ ws, long long G,
-                                                                      const int* __restrict__ not_prob,
-                                                                      int64_t* __restrict__ confmat) {
+                                                                      int* __restrict__ not_prob,
+                                                                      int64_t* __restrict__ confmat, bool zero_np) {
   const bool use_b = *not_prob != 0;
   for (long long g = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; g < G;
        g += static_cast<long long>(gridDim.x) * blockDim.x) {
@@ -1213,6 +1221,10 @@ __global__ void __launch_bounds__(kBlock) bin_confmat_finalize_kernel(int64_t* _
     c[3] += tp;
 #pragma unroll
     for (int s = 0; s < kBinSlots; ++s) w[s] = 0;
+  }
+  if (zero_np) {
+    __syncthreads();
+    if (threadIdx.x == 0) *not_prob = 0;
   }
 }
 
@@ -1274,19 +1286,16 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
         const bool vec = (C * sizeof(scalar_t)) % 16 == 0 && (reinterpret_cast<uintptr_t>(pp) % 16) == 0;
         static const int tile_grid = [] {
           const char* e = std::getenv("TM_AMD_FEWBINS_TILE");  // blocks per CU of the tiled kernel; 0 = off
-          return e ? std::atoi(e) : 3;                          // (3 x 49 KiB of LDS fit a CU: one round of tiles)
+          return e ? std::atoi(e) : 2;  // measured (1 M x 10 bf16): 2 / CU beats 3 / CU (flush atomics per block)
         }();
         // rows per thread per tile: as many as fit 32 KiB of logits (at most kTileRows; TM_AMD_FEWBINS_R caps it)
         static const int r_cap = [] {
           const char* e = std::getenv("TM_AMD_FEWBINS_R");
           return e ? std::max(1, std::min(kTileRows, std::atoi(e))) : kTileRows;
         }();
-        // ... and no more than it takes to give every co-resident block a tile: a small batch (8192 rows) is then
-        // 32 one-row-per-thread tiles in parallel instead of 6 six-row tiles
-        const long long r_fit = (kTileChunks * 16LL) / (static_cast<long long>(C) * sizeof(scalar_t));
-        const long long r_spread = (N + static_cast<long long>(kBlock) * cu_count(preds.get_device()) * std::max(tile_grid, 1) - 1) /
-                                   (static_cast<long long>(kBlock) * cu_count(preds.get_device()) * std::max(tile_grid, 1));
-        const long long R = std::min<long long>({static_cast<long long>(r_cap), r_fit, std::max<long long>(1, r_spread)});
+        // (fewer rows per tile -- more blocks for a small batch -- measured slower: every block flushes its C x C
+        // histogram with global atomics)
+        const long long R = std::min<long long>(r_cap, (kTileChunks * 16LL) / (static_cast<long long>(C) * sizeof(scalar_t)));
         // short rows (<= 128 B, <= 64 classes): the tiled kernel with its C x C LDS histogram
         const bool tile_rows = tile_grid > 0 && !samplewise && X == 1 && C <= kTileMaxC && R >= 1 &&
                                reinterpret_cast<uintptr_t>(pp) % 16 == 0;
@@ -1576,10 +1585,11 @@ void bin_stats_finalize(at::Tensor ws, at::Tensor not_prob, bool accumulate, at:
     TORCH_CHECK(t->device() == ws.device() && t->scalar_type() == at::kLong && t->is_contiguous() && t->numel() == G,
                 "bin_stats_finalize: states must be contiguous int64 with G elements");
   auto s = stream();
-  hipLaunchKernelGGL(bin_finalize_kernel, dim3(grid_cap((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+  const bool one = G <= kFinalizeOneBlock;  // one block folds and re-arms not_prob itself
+  hipLaunchKernelGGL(bin_finalize_kernel, dim3(one ? 1 : grid_cap((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                      ws.data_ptr<int64_t>(), G, not_prob.data_ptr<int>(), accumulate, tp.data_ptr<int64_t>(),
-                     fp.data_ptr<int64_t>(), tn.data_ptr<int64_t>(), fn.data_ptr<int64_t>());
-  hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
+                     fp.data_ptr<int64_t>(), tn.data_ptr<int64_t>(), fn.data_ptr<int64_t>(), one);
+  if (!one) hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
@@ -1591,9 +1601,10 @@ void bin_confmat_finalize(at::Tensor ws, at::Tensor not_prob, at::Tensor confmat
   TORCH_CHECK(confmat.scalar_type() == at::kLong && confmat.is_contiguous() && confmat.numel() == 4 * G,
               "bin_confmat_finalize: confmat must be contiguous int64 [G, 2, 2]");
   auto s = stream();
-  hipLaunchKernelGGL(bin_confmat_finalize_kernel, dim3(grid_cap((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                     ws.data_ptr<int64_t>(), G, not_prob.data_ptr<int>(), confmat.data_ptr<int64_t>());
-  hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
+  const bool one = G <= kFinalizeOneBlock;
+  hipLaunchKernelGGL(bin_confmat_finalize_kernel, dim3(one ? 1 : grid_cap((G + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     s, ws.data_ptr<int64_t>(), G, not_prob.data_ptr<int>(), confmat.data_ptr<int64_t>(), one);
+  if (!one) hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 

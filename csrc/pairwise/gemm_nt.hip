@@ -356,7 +356,7 @@ constexpr int kGM = 256, kGN = 256, kGT = 512, kGK = 32;
 template <int EPI>
 __global__ __launch_bounds__(kGT) void gemm_nt_big_kernel(const float* __restrict__ X, const float* __restrict__ Y,
                                                           int N, int M, int D, long long bx, long long by, int tiles_m,
-                                                          EpiParams ep) {
+                                                          EpiParams ep, bool pipe) {
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [2 stages][A 256 x 32 | B 256 x 32]
   constexpr int kStage = (kGM + kGN) * kGK;                    // floats per stage
   const int batch = blockIdx.z;
@@ -416,42 +416,75 @@ __global__ __launch_bounds__(kGT) void gemm_nt_big_kernel(const float* __restric
   const int swz_a = ((wr + r) >> 1) & 7;  // (32 a keeps (row >> 1) & 7: 32 rows shift it by 16)
   const int swz_b = ((wc + r) >> 1) & 7;
   const int nk = D / kGK;
-  stage(0, 0);
-  for (int kc = 0; kc < nk; ++kc) {
-    const int buf = kc & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk kc (the only ones in flight)
-    __builtin_amdgcn_s_barrier();                     // ... and every other wave's; all done with chunk kc - 1
-    if (kc + 1 < nk) stage(kc + 1, buf ^ 1);          // in flight during this chunk's MFMAs
+  // fragment slice q (k columns 8q .. 8q + 7 of the chunk, as 4 x 2 f32x4) of LDS stage `buf`
+  auto frag = [&](int buf, int q, f32x4* fa, f32x4* fb) {
     const float* sa = smem + buf * kStage + (wr + r) * kGK;
     const float* sb = smem + buf * kStage + kGM * kGK + (wc + r) * kGK;
-    f32x4 ca[4], cb[2];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) ca[a] = *reinterpret_cast<const f32x4*>(sa + 32 * a * kGK + 4 * ((4 * h) ^ swz_a));
+    for (int a = 0; a < 4; ++a) fa[a] = *reinterpret_cast<const f32x4*>(sa + 32 * a * kGK + 4 * ((4 * h + q) ^ swz_a));
 #pragma unroll
-    for (int b = 0; b < 2; ++b) cb[b] = *reinterpret_cast<const f32x4*>(sb + 32 * b * kGK + 4 * ((4 * h) ^ swz_b));
+    for (int b = 0; b < 2; ++b) fb[b] = *reinterpret_cast<const f32x4*>(sb + 32 * b * kGK + 4 * ((4 * h + q) ^ swz_b));
+  };
+  auto mfma16 = [&](const f32x4* fa, const f32x4* fb) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      f32x4 na[4], nb[2];
-      if (q < 3) {
+    for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
-          na[a] = *reinterpret_cast<const f32x4*>(sa + 32 * a * kGK + 4 * ((4 * h + q + 1) ^ swz_a));
+      for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b)
-          nb[b] = *reinterpret_cast<const f32x4*>(sb + 32 * b * kGK + 4 * ((4 * h + q + 1) ^ swz_b));
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[a][s4], fb[b][s4], acc[a][b], 0, 0, 0);
+  };
+  f32x4 ca[4], cb[2], na[4], nb[2];
+  if (pipe) {
+    // The barrier of chunk kc+1 sits INSIDE chunk kc: after the last LDS read of chunk kc (slice 3, loaded during
+    // slice 2's MFMAs) and before slice 3's MFMAs, so the matrix pipe still holds slice 2's MFMAs while waves meet
+    // there, and chunk kc+1's first slice is read while slice 3 multiplies -- the pipe never drains at a chunk
+    // boundary.  The barrier also proves every wave is done reading stage kc & 1: chunk kc+2's DMAs go there next.
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (nk > 1) stage(1, 1);
+    frag(0, 0, ca, cb);
+    for (int kc = 0; kc < nk; ++kc) {
+      const int buf = kc & 1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool more = q < 3 || kc + 1 < nk;
+        if (q < 3) {
+          frag(buf, q + 1, na, nb);
+        } else if (kc + 1 < nk) {
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // chunk kc+1 DMAs; chunk kc reads landed
+          __builtin_amdgcn_s_barrier();
+          if (kc + 2 < nk) stage(kc + 2, buf);
+          frag(buf ^ 1, 0, na, nb);
+        }
+        mfma16(ca, cb);
+        if (more) {
+#pragma unroll
+          for (int a = 0; a < 4; ++a) ca[a] = na[a];
+#pragma unroll
+          for (int b = 0; b < 2; ++b) cb[b] = nb[b];
+        }
       }
+    }
+  } else {
+    stage(0, 0);
+    for (int kc = 0; kc < nk; ++kc) {
+      const int buf = kc & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of chunk kc (the only ones in flight)
+      __builtin_amdgcn_s_barrier();                     // ... and every other wave's; all done with chunk kc - 1
+      if (kc + 1 < nk) stage(kc + 1, buf ^ 1);          // in flight during this chunk's MFMAs
+      frag(buf, 0, ca, cb);
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
+      for (int q = 0; q < 4; ++q) {
+        if (q < 3) frag(buf, q + 1, na, nb);
+        mfma16(ca, cb);
+        if (q < 3) {
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+          for (int a = 0; a < 4; ++a) ca[a] = na[a];
 #pragma unroll
-          for (int b = 0; b < 2; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[a][s4], cb[b][s4], acc[a][b], 0, 0, 0);
-      if (q < 3) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a) ca[a] = na[a];
-#pragma unroll
-        for (int b = 0; b < 2; ++b) cb[b] = nb[b];
+          for (int b = 0; b < 2; ++b) cb[b] = nb[b];
+        }
       }
     }
   }
@@ -656,8 +689,12 @@ void launch(const at::Tensor& x, const at::Tensor& y, int batches, long long bx,
     const int tiles_n = (N + kGM - 1) / kGM, tiles_m = (M + kGN - 1) / kGN;
     const int per = (tiles_n * tiles_m + 7) / 8;
     const size_t lds = 2ull * (kGM + kGN) * kGK * sizeof(float);
+    static const bool pipe = [] {  // TM_AMD_GEMM_PIPE=0: the barrier at the chunk boundary (A/B knob)
+      const char* e = std::getenv("TM_AMD_GEMM_PIPE");
+      return !(e && e[0] == '0');
+    }();
     hipLaunchKernelGGL((gemm_nt_big_kernel<EPI>), dim3(per * 8, 1, batches), dim3(kGT), lds, stream(),
-                       x.data_ptr<float>(), y.data_ptr<float>(), N, M, D, bx, by, tiles_m, ep);
+                       x.data_ptr<float>(), y.data_ptr<float>(), N, M, D, bx, by, tiles_m, ep, pipe);
     return;
   }
   const int tiles_n = (N + kBM - 1) / kBM, tiles_m = (M + kBN - 1) / kBN;

@@ -9,6 +9,9 @@
 //
 // Pearson-style metrics pass per-column shifts (the running means) so the sums are of centred values, which keeps
 // the single-pass variance/covariance update stable (Σ(x-s)² instead of Σx² - n·mean²).
+#include <map>
+#include <mutex>
+
 #include "../common/tm_common.h"
 
 #include <vector>
@@ -117,7 +120,8 @@ __global__ void __launch_bounds__(kBlock) moments_partial_kernel(const scalar_t*
                                                                  const float* __restrict__ shift_p,
                                                                  const float* __restrict__ shift_t,
                                                                  double* __restrict__ partial, int fuse,
-                                                                 DestSpec spec, double* __restrict__ out_sums) {
+                                                                 DestSpec spec, double* __restrict__ out_sums,
+                                                                 unsigned int* __restrict__ ticket) {
   // every thread keeps one column: total threads is a multiple of k (host guarantees blockDim % k == 0 or k > block)
   const long long tid = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
   const long long nthreads = static_cast<long long>(gridDim.x) * blockDim.x;
@@ -179,6 +183,19 @@ __global__ void __launch_bounds__(kBlock) moments_partial_kernel(const scalar_t*
     __threadfence_block();
     __syncthreads();
     for (int c = 0; c < k; ++c) finalize_column(partial, 1, k, c, spec, out_sums, mask);
+  } else if (ticket != nullptr) {
+    // a few blocks (mid-size batches): the LAST block to finish folds every block's partials -- one launch instead
+    // of this pass + moments_finalize_kernel; it re-arms the ticket for the next launch on this stream
+    __shared__ bool last;
+    __threadfence();  // this block's partials are visible device-wide before its ticket
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (last) {
+      __threadfence();
+      for (int c = 0; c < k; ++c) finalize_column(partial, static_cast<int>(gridDim.x), k, c, spec, out_sums, mask);
+      if (threadIdx.x == 0) *ticket = 0u;
+    }
   }
 }
 
@@ -286,6 +303,21 @@ __global__ void __launch_bounds__(kBlock) moments_finalize_kernel(const double* 
 }
 
 }  // namespace
+
+// One zeroed uint32 per (device, stream), kept for the process: the last-block fold of moments_partial_kernel counts
+// finished blocks in it and resets it, so consecutive launches on a stream reuse it (launches on one stream never
+// overlap).
+unsigned int* stream_ticket(int device, hipStream_t s) {
+  static std::mutex mu;
+  // never destroyed: the tensors must not be freed after the runtime has shut down at process exit
+  static auto* tickets = new std::map<std::pair<int, hipStream_t>, at::Tensor>();
+  std::lock_guard<std::mutex> lock(mu);
+  auto key = std::make_pair(device, s);
+  auto it = tickets->find(key);
+  if (it == tickets->end())
+    it = tickets->emplace(key, at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, device))).first;
+  return reinterpret_cast<unsigned int*>(it->second.data_ptr<int>());
+}
 
 // preds/target: [N, k] (or [N] with k = 1), same floating dtype. dests[j] += sum[sum_ids[j]] (per column, or over
 // column 0 when dest has one element and k > 1, e.g. observation counts). Returns the [k, 14] fp64 sums when want_sums.
@@ -396,15 +428,18 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
   // small updates (the common per-batch case): one block does the pass AND the fold -> a single launch
   const bool fuse = n_rows * k <= 4096 && kBlock % k == 0;
   if (fuse) blocks = 1;
+  // mid-size (a few blocks of partials): the last block folds them (a per-stream ticket word, re-armed by that block)
+  unsigned int* ticket = nullptr;
+  if (!fuse && blocks * k <= 256) ticket = stream_ticket(preds.get_device(), s);
   at::Tensor partial = at::empty({blocks, k, kMaxSums}, dopt);
   TM_DISPATCH_FLOAT(preds.scalar_type(), "moments_update", [&] {
     hipLaunchKernelGGL((moments_partial_kernel<scalar_t>), dim3(blocks), dim3(block), 0, s,
                        reinterpret_cast<const scalar_t*>(preds.data_ptr()),
                        reinterpret_cast<const scalar_t*>(target.data_ptr()), n_rows, k, static_cast<int>(mask), eps,
                        power, sp, st, partial.data_ptr<double>(), fuse ? 1 : 0, spec,
-                       want_sums ? sums.data_ptr<double>() : nullptr);
+                       want_sums ? sums.data_ptr<double>() : nullptr, ticket);
   });
-  if (!fuse) {
+  if (!fuse && ticket == nullptr) {
     hipLaunchKernelGGL(moments_finalize_kernel, dim3(k), dim3(kBlock), 0, s, partial.data_ptr<double>(),
                        static_cast<int>(blocks), k, spec, want_sums ? sums.data_ptr<double>() : nullptr,
                        static_cast<int>(mask));

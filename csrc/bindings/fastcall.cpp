@@ -38,6 +38,7 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
 void stat_reduce(const at::Tensor& tp, const at::Tensor& fp, const at::Tensor& tn, const at::Tensor& fn,
                  at::Tensor out, int64_t kind, int64_t average, bool multilabel, double beta);
 void launch_probe(at::Tensor flag);
+void zero_async(at::Tensor t);
 bool mc_confmat_dual(const at::Tensor& preds, const at::Tensor& target, at::Tensor batch, at::Tensor global,
                      at::Tensor flag, int64_t num_classes, int64_t ignore_index, bool has_ignore);
 void confmat_reduce(const at::Tensor& confmat, int64_t kind, int64_t average, int64_t ignore, int64_t kw,
@@ -704,7 +705,8 @@ int confmat_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** res
   if (flag == nullptr || !read_ignore(st, ignore, has_ignore)) TM_DECLINE;
   at::Tensor batch;
   try {
-    batch = at::zeros({C, C}, cm->options());
+    batch = at::empty({C, C}, cm->options());
+    tm_amd::zero_async(batch);
     // 16-bit logits: one kernel adds each row into the batch matrix and the global state; else update + add
     if (!tm_amd::mc_confmat_dual(p, t, batch, *cm, *flag, C, ignore, has_ignore)) {
       tm_amd::mc_update(p, t, batch, *flag, C, ignore, has_ignore, 0, false);

@@ -157,6 +157,14 @@ void bin_stats_forward(at::Tensor ws, at::Tensor not_prob, at::Tensor tp, at::Te
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
+// A contiguous CUDA tensor zeroed with one hipMemsetAsync on the current stream (the native forward's batch matrix:
+// no TensorIterator fill setup on the host).
+void zero_async(at::Tensor t) {
+  TM_CHECK_CUDA(t);
+  TM_CHECK_CONTIG(t);
+  C10_HIP_CHECK(hipMemsetAsync(t.data_ptr(), 0, t.numel() * t.element_size(), stream()));
+}
+
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
   m.def(
       "mc_stats_forward(Tensor(a!) ws, int num_classes, bool micro, Tensor(b!) tp, Tensor(c!) fp, Tensor(d!) tn, "

@@ -210,3 +210,23 @@ def test_kendall_pair_counts_nlogn_matches_allpairs(n, ties):
     c1, d1 = _pair_counts(x, y)
     c2, d2 = _pair_counts_allpairs(x, y)
     assert torch.equal(c1, c2) and torch.equal(d1, d2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,k", [(8192, 1), (20000, 1), (8192, 2), (6000, 3), (16384, 4)])
+def test_moments_mid_size_last_block_fold(rows, k):
+    """csrc/regression/moments.hip: mid-size batches (a few blocks of partials) are folded by the last block to finish
+    (a per-stream ticket, re-armed by that block) -- repeated updates on one stream against the CPU path."""
+    g = torch.Generator().manual_seed(rows + k)
+    shape = (rows,) if k == 1 else (rows, k)
+    kw = {} if k == 1 else {"num_outputs": k}
+    makers = [lambda: tm.MeanSquaredError(**({"num_outputs": k} if k > 1 else {})), lambda: tm.MeanAbsoluteError(),
+              lambda: tm.R2Score(**({"multioutput": "raw_values"} if k > 1 else {})),
+              lambda: tm.PearsonCorrCoef(**kw), lambda: tm.ExplainedVariance()]
+    for make in makers:
+        gpu, cpu = make().cuda(), make()
+        for _ in range(5):
+            p, t = torch.randn(shape, generator=g), torch.randn(shape, generator=g)
+            gpu.update(p.cuda(), (p + t).cuda())
+            cpu.update(p, p + t)
+        torch.testing.assert_close(gpu.compute().cpu(), cpu.compute(), rtol=1e-5, atol=1e-6)

@@ -220,9 +220,9 @@ def test_moments_mid_size_last_block_fold(rows, k):
     g = torch.Generator().manual_seed(rows + k)
     shape = (rows,) if k == 1 else (rows, k)
     kw = {} if k == 1 else {"num_outputs": k}
-    makers = [lambda: tm.MeanSquaredError(**({"num_outputs": k} if k > 1 else {})), lambda: tm.MeanAbsoluteError(),
-              lambda: tm.R2Score(**({"multioutput": "raw_values"} if k > 1 else {})),
-              lambda: tm.PearsonCorrCoef(**kw), lambda: tm.ExplainedVariance()]
+    multi = {"multioutput": "raw_values"} if k > 1 else {}
+    makers = [lambda: tm.MeanSquaredError(**kw), lambda: tm.MeanAbsoluteError(),
+              lambda: tm.R2Score(**kw, **multi), lambda: tm.PearsonCorrCoef(**kw), lambda: tm.ExplainedVariance(**multi)]
     for make in makers:
         gpu, cpu = make().cuda(), make()
         for _ in range(5):

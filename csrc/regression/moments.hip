@@ -426,6 +426,8 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
     return sums;
   }
   // small updates (the common per-batch case): one block does the pass AND the fold -> a single launch
+  // (measured, 8192 rows, k = 1: one block 16.4 us, 32 blocks + last-block fold 12.5 us, 32 blocks + finalize
+  // launch 6.0 + 5.2 us: the single block stays for <= 4096 values)
   const bool fuse = n_rows * k <= 4096 && kBlock % k == 0;
   if (fuse) blocks = 1;
   // mid-size (a few blocks of partials): the last block folds them (a per-stream ticket word, re-armed by that block)

@@ -65,6 +65,7 @@ class CollectionPlan:
         self.state_sig: List[Tuple[Any, str, Tuple[int, ...], torch.dtype]] = []
         self._seen: Optional[Tuple[Any, ...]] = None  # the state objects valid() last checked in full
         self._last_ptrs: Optional[Tuple[int, ...]] = None
+        self._same = False
         self._build(members)
 
     # ------------------------------------------------------------------------------------------------- record
@@ -228,10 +229,13 @@ class CollectionPlan:
         for f in self.fused:
             if f.metric.__dict__.get("_cfg_version", 0) != f.version:
                 return False
-        # the same state objects as at the last full check (the common case: states updated in place): valid
+        # the same state objects as at the last full check (the common case: states updated in place): valid, and
+        # their memory has not moved (run() keeps the pointers it patched last time)
         cur = tuple(m.__dict__.get(a) for m, a, _, _ in self.state_sig)
         if self._seen is not None and len(cur) == len(self._seen) and all(x is y for x, y in zip(cur, self._seen)):
+            self._same = True
             return True
+        self._same = False
         for (m, a, shape, dtype), t in zip(self.state_sig, cur):
             if not isinstance(t, Tensor) or t.dtype != dtype or t.shape != shape or not t.is_cuda:
                 return False
@@ -241,10 +245,11 @@ class CollectionPlan:
     def run(self) -> Tuple[Dict[str, Any], Dict[str, List[Tuple[Tensor, str, Any]]]]:
         """One launch for every fused member: ``({key: result}, {key: deferred checks})``."""
         flat = self.flat_np
-        ptrs = tuple(m.__dict__[a].data_ptr() for m, a in self.in_pairs)
-        if ptrs != self._last_ptrs:  # states moved (reset, sync, .to()): re-point the input slots
-            flat[self.in_idx] = np.asarray(ptrs, dtype=np.int64)[self.slot_pair] + self.in_off
-            self._last_ptrs = ptrs
+        if not (self._same and self._last_ptrs is not None):
+            ptrs = tuple(m.__dict__[a].data_ptr() for m, a in self.in_pairs)
+            if ptrs != self._last_ptrs:  # states moved (reset, sync, .to()): re-point the input slots
+                flat[self.in_idx] = np.asarray(ptrs, dtype=np.int64)[self.slot_pair] + self.in_off
+                self._last_ptrs = ptrs
         raw = torch.empty(self.out_bytes_total, dtype=torch.uint8, device=self.device)
         flat[self.out_idx] = self.out_rel + raw.data_ptr()
         bufs = {dt: raw[off : off + nb].view(dt) for dt, off, nb in self.out_layout}

@@ -590,12 +590,16 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_kernel(const scalar_t* __re
 // logits, one contiguous piece of preds): it issues ALL 16-byte loads of its NEXT tile (and that tile's targets) into
 // registers before it evaluates the current one from LDS, so every block keeps a whole tile of loads in flight while
 // it computes.  Each valid row is ONE LDS atomic into the block's C x C (target, prediction) histogram; the block
-// flushes the matrix (confusion-matrix mode) or the tp / fp / fn derived from it (stats mode: diagonal, column sum -
-// diagonal, row sum - diagonal) once.  (The ballot-per-bin counting this replaces cost O(bins) wave instructions per
+// stores the histogram to its slot of a partials buffer and fewbins_fold_kernel sums the slots into the matrix
+// (confusion-matrix mode) or the tp / fp / fn derived from it (stats mode: diagonal, column sum - diagonal, row sum -
+// diagonal).  TM_AMD_FEWBINS_FOLD=0 restores the per-block global-atomic flush.  (The ballot-per-bin counting this replaces cost O(bins) wave instructions per
 // row: 1 M x 10 bf16 rows ran at 0.56 TB/s, a 65536-row batch took 28 us.)
 constexpr int kTileChunks = 8;  // 16-byte loads per thread per tile (256 threads x 8 x 16 B = 32 KiB)
 constexpr int kTileRows = 8;    // rows per thread per tile (max R)
 constexpr int kTileMaxC = 64;   // the C x C LDS histogram: <= 16 KiB
+// 16-bit rows of <= 32 B: ordinal argmax (row_argmax_ord16).  Measured (1 M rows, bf16): C = 10 10.4 -> 10.0 us,
+// C = 16 13.7 -> 12.5 us; the 32-dword variant (C = 32 / 64) ran slower (40.8 -> 46.8 us, 85 -> 101 us)
+constexpr int kOrdRowsMaxNW = 8;
 
 // argmax of one row held in LDS at byte offset `off` (16-bit or 32-bit scores): the row's dwords are read into
 // registers first (NW + 1 independent LDS reads, one wait), realigned for rows that start mid-dword (odd C with
@@ -639,16 +643,51 @@ __device__ __forceinline__ int row_argmax_regs(const unsigned char* __restrict__
   return bidx;
 }
 
+// The same argmax for 16-bit scores on order-preserving ordinals (the Ord16 mapping of mc_argmax_ord16_kernel): per
+// pair of columns one packed ordinal (v_pk_ashrrev_i16 + or + xor), then per column one 32-bit key
+// (ordinal << 16 | 0xffff - column) into a max -- the first maximum wins ties -- about 4 VALU per column instead of
+// the ~15 of the NaN-aware float compare (the tile kernel's row work was VALU-bound: 1 M x 10 bf16 spent 6 us of its
+// 11 us on it).  Rows where ordinals are not exact -- a NaN anywhere (positive NaN ordinals sit above +inf, negative
+// ones below -inf) or a maximum of +-0 (-0 == +0 ties by column) -- take the float compare instead.
+template <typename scalar_t, int NW>
+__device__ __forceinline__ int row_argmax_ord16(const unsigned char* __restrict__ lds, int off, int C) {
+  const uint32_t* wp = reinterpret_cast<const uint32_t*>(lds + (off & ~3));
+  uint32_t w[NW + 1];
+#pragma unroll
+  for (int i = 0; i <= NW; ++i) w[i] = wp[i];
+  const uint32_t sh = static_cast<uint32_t>(off & 3) * 8;  // 0 or 16
+  uint32_t best = 0u, mn = 0xffffffffu;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    if (2 * i < C) {  // uniform
+      const uint32_t a = __builtin_amdgcn_alignbit(w[i + 1], w[i], sh);
+      const s16x2 sg = __builtin_bit_cast(s16x2, a) >> static_cast<short>(15);
+      uint32_t o = a ^ (__builtin_bit_cast(uint32_t, sg) | 0x80008000u);
+      best = max(best, (o << 16) | (0xffffu - 2 * i));
+      if (2 * i + 1 < C) best = max(best, (o & 0xffff0000u) | (0xffffu - (2 * i + 1)));
+      else o |= 0xffff0000u;  // past the row's end: out of the min
+      mn = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, mn), __builtin_bit_cast(u16x2, o)));
+    }
+  }
+  const uint32_t mo = best >> 16;
+  const uint32_t lo = min(mn & 0xffffu, mn >> 16);
+  if (mo > Ord16<scalar_t>::kPosInf || lo < Ord16<scalar_t>::kNegInf || mo == 0x7fffu || mo == 0x8000u)
+    return row_argmax_regs<scalar_t, NW>(lds, off, C);
+  return static_cast<int>(0xffffu - (best & 0xffffu));
+}
+
 template <typename scalar_t, typename target_t, int NW>
 __global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t* __restrict__ preds,
                                                                  const target_t* __restrict__ target, long long N,
                                                                  int C, int R, long long ignore, bool has_ignore,
                                                                  int mode, int64_t* __restrict__ out,
-                                                                 int* __restrict__ flag) {
-  __shared__ int hist[kTileMaxC * kTileMaxC];
-  // (+ 256 B: row_argmax_regs reads up to NW + 1 dwords from the last row's start)
-  __shared__ __attribute__((aligned(16))) unsigned char tile_raw[kTileChunks * kBlock * 16 + 256];
+                                                                 int* __restrict__ part, int* __restrict__ flag) {
+  // dynamic LDS: the C x C histogram (padded to 16 B), then the logits tile (+ 256 B: row_argmax_regs reads up to
+  // NW + 1 dwords from the last row's start) -- a 10-class block takes 33 KiB, so 4 blocks fit a CU
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int ncm = C * C;
+  int* hist = reinterpret_cast<int*>(smem);
+  unsigned char* tile_raw = smem + ((ncm * 4 + 15) & ~15);
   for (int b = threadIdx.x; b < ncm; b += kBlock) hist[b] = 0;
   const long long TR = static_cast<long long>(kBlock) * R;  // rows per tile
   const long long ntiles = (N + TR - 1) / TR;
@@ -707,7 +746,10 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t*
       }
       int bidx = 0;
       if constexpr (NW > 0 && (sizeof(scalar_t) == 2 || sizeof(scalar_t) == 4)) {
-        bidx = row_argmax_regs<scalar_t, NW>(tile_raw, static_cast<int>(rt * C * sizeof(scalar_t)), C);
+        if constexpr (sizeof(scalar_t) == 2 && NW <= kOrdRowsMaxNW)
+          bidx = row_argmax_ord16<scalar_t, NW>(tile_raw, static_cast<int>(rt * C * sizeof(scalar_t)), C);
+        else
+          bidx = row_argmax_regs<scalar_t, NW>(tile_raw, static_cast<int>(rt * C * sizeof(scalar_t)), C);
       } else {  // 8-byte scores: element reads from LDS
         const scalar_t* pr = lrow + rt * C;
         float best = to_f32(pr[0]);
@@ -723,7 +765,10 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t*
     }
   }
   __syncthreads();
-  if (mode == kMcConfmat) {
+  if (part != nullptr) {  // this block's histogram, plain stores: fewbins_fold_kernel sums the blocks
+    int* dst = part + static_cast<long long>(blockIdx.x) * ncm;
+    for (int b = threadIdx.x; b < ncm; b += kBlock) dst[b] = hist[b];
+  } else if (mode == kMcConfmat) {
     for (int b = threadIdx.x; b < ncm; b += kBlock) {
       const int v = hist[b];
       if (v) atomic_add_i64(out + b, v);
@@ -739,6 +784,65 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t*
       if (tp) atomic_add_i64(out + c, tp);
       if (col - tp) atomic_add_i64(out + C + c, col - tp);
       if (row - tp) atomic_add_i64(out + 2LL * C + c, row - tp);
+    }
+  }
+}
+
+// Sum of the tile kernel's per-block C x C histograms [nblk, C * C] (int32).  Grid: x = groups of 64 bins (lanes walk
+// consecutive bins), y = splits of the blocks; each of the block's 16 waves sums at most kFoldRows rows, all its loads
+// in flight at once.  Confusion-matrix mode adds each bin into the matrix (plain add when there is one split, else one
+// atomic per split); stats mode gathers the block's tp (diagonal), fp (prediction column) and fn (target row) per
+// class in LDS and adds each non-zero one to the workspace with one atomic.  Measured on MI355X (1 M x 10 bf16, 512
+// tile blocks): the per-block global-atomic flush this replaces cost 6.4 us (confusion matrix, C^2 addresses) and
+// 12 us (stats, 3C addresses: every address takes one serialised atomic per block); the fold runs in ~4.6 us.
+constexpr int kFoldThreads = 1024;
+constexpr int kFoldRows = 8;
+__global__ void __launch_bounds__(kFoldThreads) fewbins_fold_kernel(const int* __restrict__ part, int nblk, int C,
+                                                                     int mode, int64_t* __restrict__ out) {
+  constexpr int kW = kFoldThreads / kWave;
+  __shared__ int red[kW][kWave];
+  __shared__ int cls[3][kTileMaxC];
+  const int ncm = C * C;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int bin = blockIdx.x * kWave + lane;
+  const int r0 = blockIdx.y * kW * kFoldRows + w;
+  int v[kFoldRows];
+#pragma unroll
+  for (int i = 0; i < kFoldRows; ++i) {
+    const int r = r0 + i * kW;
+    v[i] = (bin < ncm && r < nblk) ? part[static_cast<long long>(r) * ncm + bin] : 0;
+  }
+  int acc = 0;
+#pragma unroll
+  for (int i = 0; i < kFoldRows; ++i) acc += v[i];
+  red[w][lane] = acc;
+  if (mode != kMcConfmat)
+    for (int i = threadIdx.x; i < 3 * kTileMaxC; i += kFoldThreads) cls[i / kTileMaxC][i % kTileMaxC] = 0;
+  __syncthreads();
+  if (w == 0 && bin < ncm) {
+    int tot = 0;
+#pragma unroll
+    for (int i = 0; i < kW; ++i) tot += red[i][lane];
+    if (tot) {
+      if (mode == kMcConfmat) {
+        if (gridDim.y == 1) out[bin] += tot;
+        else atomic_add_i64(out + bin, tot);
+      } else {
+        const int t = bin / C, p = bin - t * C;
+        if (t == p) {
+          atomicAdd(&cls[0][t], tot);
+        } else {
+          atomicAdd(&cls[1][p], tot);
+          atomicAdd(&cls[2][t], tot);
+        }
+      }
+    }
+  }
+  if (mode != kMcConfmat) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * C; i += kFoldThreads) {
+      const int c = cls[i / C][i % C];
+      if (c) atomic_add_i64(out + i, c);  // [tp | fp | fn] are consecutive C-blocks of the workspace
     }
   }
 }
@@ -1286,15 +1390,14 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
         const bool vec = (C * sizeof(scalar_t)) % 16 == 0 && (reinterpret_cast<uintptr_t>(pp) % 16) == 0;
         static const int tile_grid = [] {
           const char* e = std::getenv("TM_AMD_FEWBINS_TILE");  // blocks per CU of the tiled kernel; 0 = off
-          return e ? std::atoi(e) : 2;  // measured (1 M x 10 bf16): 2 / CU beats 3 / CU (flush atomics per block)
+          return e ? std::atoi(e) : 3;  // measured (1 M x 10 bf16, fold path): 3 / CU 10.4 us, 2 / CU 12.0
         }();
         // rows per thread per tile: as many as fit 32 KiB of logits (at most kTileRows; TM_AMD_FEWBINS_R caps it)
         static const int r_cap = [] {
           const char* e = std::getenv("TM_AMD_FEWBINS_R");
           return e ? std::max(1, std::min(kTileRows, std::atoi(e))) : kTileRows;
         }();
-        // (fewer rows per tile -- more blocks for a small batch -- measured slower: every block flushes its C x C
-        // histogram with global atomics)
+        // (fewer rows per tile -- more blocks for a small batch -- measured slower: every block adds a histogram)
         const long long R = std::min<long long>(r_cap, (kTileChunks * 16LL) / (static_cast<long long>(C) * sizeof(scalar_t)));
         // short rows (<= 128 B, <= 64 classes): the tiled kernel with its C x C LDS histogram
         const bool tile_rows = tile_grid > 0 && !samplewise && X == 1 && C <= kTileMaxC && R >= 1 &&
@@ -1305,11 +1408,25 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
               std::min<long long>(ntiles, static_cast<long long>(cu_count(preds.get_device())) * tile_grid));
           // dwords per row for the register argmax: 8 (rows <= 32 B) or 32 (<= 128 B); 8-byte scores read LDS
           const long long rbytes = static_cast<long long>(C) * sizeof(scalar_t);
+          static const bool fold = [] {
+            const char* e = std::getenv("TM_AMD_FEWBINS_FOLD");  // 0: per-block global-atomic flush (A/B)
+            return !e || std::atoi(e) != 0;
+          }();
+          const int ncm = C * C;
+          at::Tensor part;
+          if (fold) part = at::empty({static_cast<long long>(tgrid) * ncm}, preds.options().dtype(at::kInt));
+          int* partp = fold ? part.data_ptr<int>() : nullptr;
+          const size_t smem = static_cast<size_t>((ncm * 4 + 15) & ~15) + kTileChunks * kBlock * 16 + 256;
           auto launch_tile = [&](auto nw_tag) {
             constexpr int NW = decltype(nw_tag)::value;
-            hipLaunchKernelGGL((mc_fewbins_tile_kernel<scalar_t, target_t, NW>), dim3(tgrid), dim3(kBlock), 0, s, pp,
-                               tp, N, C, static_cast<int>(R), ignore_index, has_ignore, static_cast<int>(mode), outp,
-                               flagp);
+            hipLaunchKernelGGL((mc_fewbins_tile_kernel<scalar_t, target_t, NW>), dim3(tgrid), dim3(kBlock), smem, s,
+                               pp, tp, N, C, static_cast<int>(R), ignore_index, has_ignore, static_cast<int>(mode),
+                               outp, partp, flagp);
+            if (fold)
+              hipLaunchKernelGGL(fewbins_fold_kernel,
+                                 dim3((ncm + kWave - 1) / kWave,
+                                      (tgrid + kFoldThreads / kWave * kFoldRows - 1) / (kFoldThreads / kWave * kFoldRows)),
+                                 dim3(kFoldThreads), 0, s, partp, tgrid, C, static_cast<int>(mode), outp);
           };
           if constexpr (sizeof(scalar_t) == 2 || sizeof(scalar_t) == 4) {
             if (rbytes <= 32) launch_tile(std::integral_constant<int, 8>{});

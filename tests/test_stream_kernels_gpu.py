@@ -53,6 +53,36 @@ def test_fewbins_tiled_nan_ties_ignore_and_bad_target(ignore):
     assert fg & 1  # target out of range
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("C", [7, 10, 16])
+def test_fewbins_ordinal_rows_signed_zero_nan_payloads_inf(dtype, C):
+    """The 16-bit rows go through order-preserving ordinals (row_argmax_ord16); every row where ordinals are not exact
+    (a max of +-0, negative NaN, NaN payloads, a NaN next to +inf) must still match torch.argmax."""
+    N = 50_003
+    g = torch.Generator().manual_seed(C)
+    preds = torch.randn(N, C, generator=g).to(dtype)
+    bits = preds.view(torch.int16)
+    preds[0::7] = -preds[0::7].abs()  # all-negative rows
+    preds[1::11] = 0.0
+    preds[1::11, C - 1] = -0.0  # +0 / -0 ties: first column
+    preds[2::11] = -0.0
+    preds[2::11, C // 2] = 0.0
+    preds[3::11] = -1.0
+    preds[3::11, 1] = -0.0  # max is -0 alone
+    bits[4::13, C // 3] = -1  # 0xffff: a negative NaN
+    bits[5::13, C - 2] = 0x7FC1 if dtype == torch.bfloat16 else 0x7E01  # positive NaN with a payload
+    preds[5::13, 0] = float("inf")
+    preds[6::17, 1] = float("-inf")
+    preds[7::19] = float("inf")  # all +inf: first column
+    target = torch.randint(0, C, (N,), generator=g)
+    for mode in (0, 1):
+        if mode == ops.MC_CONFMAT and C * C > 256:
+            continue
+        gg, fg = _mc(preds, target, C, None, mode, DEV)
+        cc, fc = _mc(preds, target, C, None, mode, "cpu")
+        assert torch.equal(gg, cc) and fg == fc == 0
+
+
 def test_fewbins_tiled_unaligned_input_takes_the_other_kernel():
     C, N = 10, 10_000
     base = torch.randn(N * C + 1).to(torch.bfloat16)

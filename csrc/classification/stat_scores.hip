@@ -955,7 +955,7 @@ __device__ __forceinline__ void bin_slots(bool t, bool pa, bool pb, int& sa, int
 
 // flat kernel: elements of preds [N, L, X] visited in memory order; group = samplewise ? n*L + l : l
 // partials != nullptr (LDS histogram, many labels): each block stores its [L * 7] int32 histogram to its own row of
-// `partials` and bin_partials_reduce_kernel folds the rows into ws -- instead of up to L * 7 global atomics per block.
+// `partials` and partials_fold_kernel folds the rows into ws -- instead of up to L * 7 global atomics per block.
 template <typename scalar_t, typename target_t>
 __global__ void __launch_bounds__(kBlock) bin_flat_kernel(const scalar_t* __restrict__ preds,
                                                           const target_t* __restrict__ target, long long total,
@@ -1040,16 +1040,44 @@ __global__ void __launch_bounds__(kBlock) bin_flat_kernel(const scalar_t* __rest
   }
 }
 
-// ws[b] += sum over the blocks' partial histograms: grid (bin tiles, block groups); a thread sums its group's rows
-// of one bin (coalesced over bins) and adds once -- kPartialGroups atomics per bin in total.
-constexpr int kPartialGroups = 32;
-__global__ void __launch_bounds__(kBlock) bin_partials_reduce_kernel(const int* __restrict__ partials, int nrows,
-                                                                     int nbins, int64_t* __restrict__ ws) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nbins) return;
-  long long acc = 0;
-  for (int r = blockIdx.y; r < nrows; r += gridDim.y) acc += partials[static_cast<long long>(r) * nbins + b];
-  if (acc) atomic_add_i64(ws + b, acc);
+// ws[b] += sum over the blocks' partial histograms [nrows, nbins] (int32).  Grid: x = groups of 64 bins (lanes walk
+// consecutive bins), y = splits of the rows; each of the block's 16 waves sums at most kFoldRows rows with all its
+// loads in flight, the block reduces in LDS and adds once per bin (a plain add when there is one split).  Partials +
+// this fold replace per-block global atomics onto a few shared addresses, which serialise at ~11 ns each (binary
+// inputs: 2048 blocks x 7 counters).
+__global__ void __launch_bounds__(kFoldThreads) partials_fold_kernel(const int* __restrict__ part, int nrows,
+                                                                      int nbins, int64_t* __restrict__ ws) {
+  constexpr int kW = kFoldThreads / kWave;
+  __shared__ int red[kW][kWave];
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int bin = blockIdx.x * kWave + lane;
+  const int r0 = blockIdx.y * kW * kFoldRows + w;
+  int v[kFoldRows];
+#pragma unroll
+  for (int i = 0; i < kFoldRows; ++i) {
+    const int r = r0 + i * kW;
+    v[i] = (bin < nbins && r < nrows) ? part[static_cast<long long>(r) * nbins + bin] : 0;
+  }
+  int acc = 0;
+#pragma unroll
+  for (int i = 0; i < kFoldRows; ++i) acc += v[i];
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && bin < nbins) {
+    int tot = 0;
+#pragma unroll
+    for (int i = 0; i < kW; ++i) tot += red[i][lane];
+    if (tot) {
+      if (gridDim.y == 1) ws[bin] += tot;
+      else atomic_add_i64(ws + bin, tot);
+    }
+  }
+}
+
+void launch_partials_fold(const int* part, int nrows, int nbins, int64_t* ws, hipStream_t s) {
+  constexpr int per = kFoldThreads / kWave * kFoldRows;
+  hipLaunchKernelGGL(partials_fold_kernel, dim3((nbins + kWave - 1) / kWave, (nrows + per - 1) / per),
+                     dim3(kFoldThreads), 0, s, part, nrows, nbins, ws);
 }
 
 // Multilabel rows [N, L] (X == 1, L % VEC == 0, VEC = 16 / sizeof(preds)): a thread reads one 16-byte vector of VEC
@@ -1057,7 +1085,7 @@ __global__ void __launch_bounds__(kBlock) bin_partials_reduce_kernel(const int* 
 // thread's VEC labels never change -- its 7 x VEC counters stay in registers for the whole walk (kU vectors in flight
 // per thread).  No per-element atomics at all (bin_flat_kernel did 3 LDS atomics per element: MultilabelF1Score(1000)
 // on 16384 x 1000 bf16 ran at 1.3 TB/s); the block folds its counters into an LDS histogram once and stores it as its
-// row of `partials`, which bin_partials_reduce_kernel folds into the workspace.
+// row of `partials`, which partials_fold_kernel folds into the workspace.
 constexpr int kVecBlock = 512;
 
 template <typename scalar_t, typename target_t, int VEC>
@@ -1141,14 +1169,14 @@ __global__ void __launch_bounds__(kVecBlock) bin_vec_kernel(const scalar_t* __re
 // Binary / small multilabel (L * X <= 64, not samplewise): the grid stride is a multiple of L * X, so every thread
 // always sees the SAME label -- its 7 counters (tp/fp/fn for both probability readings + count) stay in registers
 // for its whole grid-stride walk (4 independent loads in flight per iteration).  At the end one LDS add per counter
-// (after a wave reduction when the block has a single label) and one global add per (label, counter) and block.
+// (after a wave reduction when the block has a single label), then the block stores its row of partials.
 // The flat kernel instead did 2-3 LDS atomics per element onto the same 7 addresses (64-way serialised for binary
 // inputs): 16.8 M fp32 binary elements 115 us -> HBM-bound.
 template <typename scalar_t, typename target_t>
 __global__ void __launch_bounds__(kBlock) bin_reg_kernel(const scalar_t* __restrict__ preds,
                                                          const target_t* __restrict__ target, long long total,
                                                          long long L, long long X, float thr_t, long long ignore,
-                                                         bool has_ignore, int64_t* __restrict__ ws,
+                                                         bool has_ignore, int* __restrict__ partials,
                                                          int* __restrict__ flag, int* __restrict__ not_prob,
                                                          bool prob_check_all) {
   extern __shared__ __attribute__((aligned(16))) int lds[];
@@ -1214,10 +1242,8 @@ __global__ void __launch_bounds__(kBlock) bin_reg_kernel(const scalar_t* __restr
       if (c[k]) atomicAdd(&lds[label * kBinSlots + k], c[k]);
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
-    const int v = lds[b];
-    if (v) atomic_add_i64(ws + b, v);
-  }
+  int* row = partials + static_cast<long long>(blockIdx.x) * nbins;  // folded by partials_fold_kernel
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) row[b] = lds[b];
 }
 
 template <typename scalar_t, typename target_t>
@@ -1656,17 +1682,18 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
                              has_ignore, flag.data_ptr<int>(), not_prob.data_ptr<int>(), prob_check_all,
                              partials.data_ptr<int>());
         }
-        const dim3 rgrid(static_cast<unsigned>((nbins + kBlock - 1) / kBlock),
-                         static_cast<unsigned>(std::min(kPartialGroups, grid)));
-        hipLaunchKernelGGL(bin_partials_reduce_kernel, rgrid, dim3(kBlock), 0, s, partials.data_ptr<int>(), grid,
-                           static_cast<int>(nbins), ws.data_ptr<int64_t>());
+        launch_partials_fold(partials.data_ptr<int>(), grid, static_cast<int>(nbins), ws.data_ptr<int64_t>(), s);
       } else if (!samplewise && reg_grid(L * X, total) > 0 && L * kBinSlots <= kLdsBins) {
         // grid stride a multiple of L * X: a fixed label per thread (register counters)
         const long long grid = reg_grid(L * X, total);
-        const size_t lds = L * kBinSlots * sizeof(int);
+        const long long nbins = L * kBinSlots;
+        const size_t lds = nbins * sizeof(int);
+        at::Tensor partials = at::empty({grid * nbins}, ws.options().dtype(at::kInt));
         hipLaunchKernelGGL((bin_reg_kernel<scalar_t, target_t>), dim3(static_cast<unsigned>(grid)), dim3(kBlock), lds,
-                           s, pp, tp, total, L, X, thr_t, ignore_index, has_ignore, ws.data_ptr<int64_t>(),
+                           s, pp, tp, total, L, X, thr_t, ignore_index, has_ignore, partials.data_ptr<int>(),
                            flag.data_ptr<int>(), not_prob.data_ptr<int>(), prob_check_all);
+        launch_partials_fold(partials.data_ptr<int>(), static_cast<int>(grid), static_cast<int>(nbins),
+                             ws.data_ptr<int64_t>(), s);
       } else {
         const long long nbins = L * kBinSlots;
         const bool lds_hist = !samplewise && nbins <= kLdsBins;
@@ -1681,12 +1708,8 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
                            total, L, X, thr_t, ignore_index, has_ignore, samplewise, ws.data_ptr<int64_t>(),
                            flag.data_ptr<int>(), not_prob.data_ptr<int>(), prob_check_all,
                            use_partials ? partials.data_ptr<int>() : nullptr);
-        if (use_partials) {
-          const dim3 rgrid(static_cast<unsigned>((nbins + kBlock - 1) / kBlock),
-                           static_cast<unsigned>(std::min(kPartialGroups, grid)));
-          hipLaunchKernelGGL(bin_partials_reduce_kernel, rgrid, dim3(kBlock), 0, s, partials.data_ptr<int>(), grid,
-                             static_cast<int>(nbins), ws.data_ptr<int64_t>());
-        }
+        if (use_partials)
+          launch_partials_fold(partials.data_ptr<int>(), grid, static_cast<int>(nbins), ws.data_ptr<int64_t>(), s);
       }
     });
   });

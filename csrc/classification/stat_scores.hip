@@ -797,6 +797,7 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t*
 // 12 us (stats, 3C addresses: every address takes one serialised atomic per block); the fold runs in ~4.6 us.
 constexpr int kFoldThreads = 1024;
 constexpr int kFoldRows = 8;
+constexpr int kFoldMinBlocks = 64;  // grids up to this many blocks keep the per-block atomic flush
 __global__ void __launch_bounds__(kFoldThreads) fewbins_fold_kernel(const int* __restrict__ part, int nblk, int C,
                                                                      int mode, int64_t* __restrict__ out) {
   constexpr int kW = kFoldThreads / kWave;
@@ -1176,9 +1177,9 @@ template <typename scalar_t, typename target_t>
 __global__ void __launch_bounds__(kBlock) bin_reg_kernel(const scalar_t* __restrict__ preds,
                                                          const target_t* __restrict__ target, long long total,
                                                          long long L, long long X, float thr_t, long long ignore,
-                                                         bool has_ignore, int* __restrict__ partials,
-                                                         int* __restrict__ flag, int* __restrict__ not_prob,
-                                                         bool prob_check_all) {
+                                                         bool has_ignore, int64_t* __restrict__ ws,
+                                                         int* __restrict__ partials, int* __restrict__ flag,
+                                                         int* __restrict__ not_prob, bool prob_check_all) {
   extern __shared__ __attribute__((aligned(16))) int lds[];
   const int nbins = static_cast<int>(L) * kBinSlots;
   for (int b = threadIdx.x; b < nbins; b += blockDim.x) lds[b] = 0;
@@ -1242,8 +1243,15 @@ __global__ void __launch_bounds__(kBlock) bin_reg_kernel(const scalar_t* __restr
       if (c[k]) atomicAdd(&lds[label * kBinSlots + k], c[k]);
   }
   __syncthreads();
-  int* row = partials + static_cast<long long>(blockIdx.x) * nbins;  // folded by partials_fold_kernel
-  for (int b = threadIdx.x; b < nbins; b += blockDim.x) row[b] = lds[b];
+  if (partials != nullptr) {
+    int* row = partials + static_cast<long long>(blockIdx.x) * nbins;  // folded by partials_fold_kernel
+    for (int b = threadIdx.x; b < nbins; b += blockDim.x) row[b] = lds[b];
+  } else {  // a small grid: one global add per (label, counter) and block
+    for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
+      const int v = lds[b];
+      if (v) atomic_add_i64(ws + b, v);
+    }
+  }
 }
 
 template <typename scalar_t, typename target_t>
@@ -1434,11 +1442,13 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
               std::min<long long>(ntiles, static_cast<long long>(cu_count(preds.get_device())) * tile_grid));
           // dwords per row for the register argmax: 8 (rows <= 32 B) or 32 (<= 128 B); 8-byte scores read LDS
           const long long rbytes = static_cast<long long>(C) * sizeof(scalar_t);
-          static const bool fold = [] {
+          static const bool fold_on = [] {
             const char* e = std::getenv("TM_AMD_FEWBINS_FOLD");  // 0: per-block global-atomic flush (A/B)
             return !e || std::atoi(e) != 0;
           }();
           const int ncm = C * C;
+          // a few blocks (small batches) flush with atomics: the fold's extra launch would cost more than their chains
+          const bool fold = fold_on && tgrid > kFoldMinBlocks;
           at::Tensor part;
           if (fold) part = at::empty({static_cast<long long>(tgrid) * ncm}, preds.options().dtype(at::kInt));
           int* partp = fold ? part.data_ptr<int>() : nullptr;
@@ -1688,12 +1698,16 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
         const long long grid = reg_grid(L * X, total);
         const long long nbins = L * kBinSlots;
         const size_t lds = nbins * sizeof(int);
-        at::Tensor partials = at::empty({grid * nbins}, ws.options().dtype(at::kInt));
+        const bool fold = grid > kFoldMinBlocks;
+        at::Tensor partials;
+        if (fold) partials = at::empty({grid * nbins}, ws.options().dtype(at::kInt));
         hipLaunchKernelGGL((bin_reg_kernel<scalar_t, target_t>), dim3(static_cast<unsigned>(grid)), dim3(kBlock), lds,
-                           s, pp, tp, total, L, X, thr_t, ignore_index, has_ignore, partials.data_ptr<int>(),
-                           flag.data_ptr<int>(), not_prob.data_ptr<int>(), prob_check_all);
-        launch_partials_fold(partials.data_ptr<int>(), static_cast<int>(grid), static_cast<int>(nbins),
-                             ws.data_ptr<int64_t>(), s);
+                           s, pp, tp, total, L, X, thr_t, ignore_index, has_ignore, ws.data_ptr<int64_t>(),
+                           fold ? partials.data_ptr<int>() : nullptr, flag.data_ptr<int>(), not_prob.data_ptr<int>(),
+                           prob_check_all);
+        if (fold)
+          launch_partials_fold(partials.data_ptr<int>(), static_cast<int>(grid), static_cast<int>(nbins),
+                               ws.data_ptr<int64_t>(), s);
       } else {
         const long long nbins = L * kBinSlots;
         const bool lds_hist = !samplewise && nbins <= kLdsBins;

@@ -801,8 +801,8 @@ constexpr int kFoldMinBlocks = 64;  // grids up to this many blocks keep the per
 __global__ void __launch_bounds__(kFoldThreads) fewbins_fold_kernel(const int* __restrict__ part, int nblk, int C,
                                                                      int mode, int64_t* __restrict__ out) {
   constexpr int kW = kFoldThreads / kWave;
-  __shared__ int red[kW][kWave];
-  __shared__ int cls[3][kTileMaxC];
+  __shared__ long long red[kW][kWave];  // 64-bit sums: up to 128 blocks' int32 counts
+  __shared__ unsigned long long cls[3][kTileMaxC];
   const int ncm = C * C;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const int bin = blockIdx.x * kWave + lane;
@@ -813,7 +813,7 @@ __global__ void __launch_bounds__(kFoldThreads) fewbins_fold_kernel(const int* _
     const int r = r0 + i * kW;
     v[i] = (bin < ncm && r < nblk) ? part[static_cast<long long>(r) * ncm + bin] : 0;
   }
-  int acc = 0;
+  long long acc = 0;
 #pragma unroll
   for (int i = 0; i < kFoldRows; ++i) acc += v[i];
   red[w][lane] = acc;
@@ -821,7 +821,7 @@ __global__ void __launch_bounds__(kFoldThreads) fewbins_fold_kernel(const int* _
     for (int i = threadIdx.x; i < 3 * kTileMaxC; i += kFoldThreads) cls[i / kTileMaxC][i % kTileMaxC] = 0;
   __syncthreads();
   if (w == 0 && bin < ncm) {
-    int tot = 0;
+    long long tot = 0;
 #pragma unroll
     for (int i = 0; i < kW; ++i) tot += red[i][lane];
     if (tot) {
@@ -831,10 +831,10 @@ __global__ void __launch_bounds__(kFoldThreads) fewbins_fold_kernel(const int* _
       } else {
         const int t = bin / C, p = bin - t * C;
         if (t == p) {
-          atomicAdd(&cls[0][t], tot);
+          atomicAdd(&cls[0][t], static_cast<unsigned long long>(tot));
         } else {
-          atomicAdd(&cls[1][p], tot);
-          atomicAdd(&cls[2][t], tot);
+          atomicAdd(&cls[1][p], static_cast<unsigned long long>(tot));
+          atomicAdd(&cls[2][t], static_cast<unsigned long long>(tot));
         }
       }
     }
@@ -842,7 +842,7 @@ __global__ void __launch_bounds__(kFoldThreads) fewbins_fold_kernel(const int* _
   if (mode != kMcConfmat) {
     __syncthreads();
     for (int i = threadIdx.x; i < 3 * C; i += kFoldThreads) {
-      const int c = cls[i / C][i % C];
+      const long long c = static_cast<long long>(cls[i / C][i % C]);
       if (c) atomic_add_i64(out + i, c);  // [tp | fp | fn] are consecutive C-blocks of the workspace
     }
   }
@@ -1049,7 +1049,7 @@ __global__ void __launch_bounds__(kBlock) bin_flat_kernel(const scalar_t* __rest
 __global__ void __launch_bounds__(kFoldThreads) partials_fold_kernel(const int* __restrict__ part, int nrows,
                                                                       int nbins, int64_t* __restrict__ ws) {
   constexpr int kW = kFoldThreads / kWave;
-  __shared__ int red[kW][kWave];
+  __shared__ long long red[kW][kWave];  // 64-bit sums (no int32 wrap)
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   const int bin = blockIdx.x * kWave + lane;
   const int r0 = blockIdx.y * kW * kFoldRows + w;
@@ -1059,13 +1059,13 @@ __global__ void __launch_bounds__(kFoldThreads) partials_fold_kernel(const int* 
     const int r = r0 + i * kW;
     v[i] = (bin < nbins && r < nrows) ? part[static_cast<long long>(r) * nbins + bin] : 0;
   }
-  int acc = 0;
+  long long acc = 0;
 #pragma unroll
   for (int i = 0; i < kFoldRows; ++i) acc += v[i];
   red[w][lane] = acc;
   __syncthreads();
   if (w == 0 && bin < nbins) {
-    int tot = 0;
+    long long tot = 0;
 #pragma unroll
     for (int i = 0; i < kW; ++i) tot += red[i][lane];
     if (tot) {

@@ -33,6 +33,48 @@ __global__ void __launch_bounds__(kThreads)
                                      bound, out, red);
 }
 
+
+// Per-rank merge of the Pearson / concordance running states (reference S/regression/pearson.py:28-71, a Python loop
+// over the W ranks of ~25 elementwise ops each): one thread per output column folds the W stacked rows in rank order
+// with Chan et al.'s pairwise update, in fp64 (rounded once to the states' dtype at the end).
+// in: [6][W][k] = mean_x, mean_y, var_x, var_y, corr_xy, n (one dtype); out: [6][k].
+template <typename T>
+__host__ __device__ __forceinline__ void corr_merge_col(const T* __restrict__ in, int W, long long k, long long j,
+                                                        T* __restrict__ out) {
+  const long long plane = static_cast<long long>(W) * k;
+  double mx = in[j], my = in[plane + j], vx = in[2 * plane + j], vy = in[3 * plane + j], cxy = in[4 * plane + j],
+         n = in[5 * plane + j];
+  for (int w = 1; w < W; ++w) {
+    const long long o = static_cast<long long>(w) * k + j;
+    const double mx2 = in[o], my2 = in[plane + o], n2 = in[5 * plane + o];
+    const double tot = n + n2;
+    const double dx = mx2 - mx, dy = my2 - my;
+    const double wt = tot != 0.0 ? n * n2 / tot : 0.0;
+    vx += in[2 * plane + o] + dx * dx * wt;
+    vy += in[3 * plane + o] + dy * dy * wt;
+    cxy += in[4 * plane + o] + dx * dy * wt;
+    if (tot != 0.0) {
+      mx += dx * n2 / tot;
+      my += dy * n2 / tot;
+    }
+    n = tot;
+  }
+  out[j] = static_cast<T>(mx);
+  out[k + j] = static_cast<T>(my);
+  out[2 * k + j] = static_cast<T>(vx);
+  out[3 * k + j] = static_cast<T>(vy);
+  out[4 * k + j] = static_cast<T>(cxy);
+  out[5 * k + j] = static_cast<T>(n);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) corr_merge_kernel(const T* __restrict__ in, int W, long long k,
+                                                         T* __restrict__ out) {
+  for (long long j = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; j < k;
+       j += static_cast<long long>(gridDim.x) * blockDim.x)
+    corr_merge_col(in, W, k, j, out);
+}
+
 }  // namespace
 
 // kind 0 EV (s0..s3), 1 R2 (s0..s2), 2 Pearson / 3 concordance (s0..s4); every state is [k] in ONE dtype (f32/f64).
@@ -91,10 +133,38 @@ void regression_compute(int64_t kind, at::TensorList states, const c10::optional
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
+
+// stacked [6, W, k] per-rank Pearson states -> merged [6, k] (ROCm: one launch; CPU: the same fold on the host)
+at::Tensor corr_merge(const at::Tensor& stacked) {
+  TORCH_CHECK(stacked.dim() == 3 && stacked.size(0) == 6 && stacked.is_contiguous(), "corr_merge: contiguous [6, W, k]");
+  const auto dt = stacked.scalar_type();
+  TORCH_CHECK(dt == at::kFloat || dt == at::kDouble, "corr_merge: f32 / f64 states");
+  const int W = static_cast<int>(stacked.size(1));
+  const long long k = stacked.size(2);
+  TORCH_CHECK(W >= 1, "corr_merge: at least one rank");
+  auto out = at::empty({6, k}, stacked.options());
+  if (k == 0) return out;
+  AT_DISPATCH_FLOATING_TYPES(dt, "corr_merge", [&] {
+    if (stacked.is_cuda()) {
+      hipLaunchKernelGGL(corr_merge_kernel<scalar_t>, dim3(grid_cap((k + 255) / 256)), dim3(256), 0, stream(),
+                         stacked.data_ptr<scalar_t>(), W, k, out.data_ptr<scalar_t>());
+    } else {
+      for (long long j = 0; j < k; ++j) corr_merge_col(stacked.data_ptr<scalar_t>(), W, k, j, out.data_ptr<scalar_t>());
+    }
+  });
+  if (stacked.is_cuda()) C10_HIP_KERNEL_LAUNCH_CHECK();
+  return out;
+}
+
 }  // namespace tm_amd
 
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
   m.def("regression_compute(int kind, Tensor[] states, Tensor? n, float n_value, int multioutput, float bound, "
         "Tensor(a!) out) -> ()");
+  m.def("corr_merge(Tensor stacked) -> Tensor");
 }
-TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) { m.impl("regression_compute", &tm_amd::regression_compute); }
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
+  m.impl("regression_compute", &tm_amd::regression_compute);
+  m.impl("corr_merge", &tm_amd::corr_merge);
+}
+TORCH_LIBRARY_IMPL(tm_amd, CPU, m) { m.impl("corr_merge", &tm_amd::corr_merge); }

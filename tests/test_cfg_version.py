@@ -29,3 +29,17 @@ def test_update_and_compute_do_not_reversion_members():
         cls.compute(), reg.compute()
         cls(p, t), reg(x, y)
     assert (_versions(cls), _versions(reg)) == before
+
+
+def test_train_eval_do_not_reversion_members():
+    """train() / eval() rebind nn.Module's ``training`` on every member: not configuration."""
+    cls, reg = build(torch.device("cpu"))
+    before = (_versions(cls), _versions(reg))
+    for _ in range(3):
+        cls.train(), reg.train()
+        cls.eval(), reg.eval()
+    assert (_versions(cls), _versions(reg)) == before
+    m = next(iter(cls.values()))
+    v = m.__dict__.get("_cfg_version", 0)
+    m.average = "weighted" if getattr(m, "average", None) != "weighted" else "micro"
+    assert m.__dict__.get("_cfg_version", 0) == v + 1

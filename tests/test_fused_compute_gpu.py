@@ -123,3 +123,21 @@ def test_validation_error_and_device_warning_on_fused_path():
         warnings.simplefilter("always")
         gr.compute()
     assert any("variance of predictions or target is close to zero" in str(x.message) for x in w)
+
+
+def test_train_eval_toggle_keeps_fused_plan():
+    """nn.Module.train() / eval() set ``training`` on every member: not a configuration change, so the recorded plan
+    survives a train / validate loop (it used to be re-recorded at each switch and switched off after 8)."""
+    gc, cc = _cls().to(DEV), _cls()
+    plans = set()
+    for i in range(12):
+        p, t, _, _ = _batch(40 + i)
+        gc.train() if i % 2 else gc.eval()
+        gc.update(p.to(DEV), t.to(DEV))
+        cc.update(p, t)
+        _check(gc.compute(), cc.compute())
+        if "_fused_plan" in gc.__dict__:
+            plans.add(id(gc.__dict__["_fused_plan"][1]))
+    assert len(plans) == 1
+    assert not gc.__dict__.get("_fused_off")
+    assert gc.__dict__.get("_fused_rebuilds", 0) == 1

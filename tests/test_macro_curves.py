@@ -1,8 +1,8 @@
 """average="macro" ROC / precision-recall curves: one batched interpolation (``ops.interp_mean``,
 ``csrc/classification/curve_interp.hip``) against the reference's algorithm written out as a per-class loop
 (F/classification/roc.py:189-200, precision_recall_curve.py:566-580, utilities/compute.py:134-157) -- bit-identical,
-binned and unbinned, including per-class precision curves that are not monotone (the binary search's probe sequence
-decides the segment there, as in torch.searchsorted)."""
+binned and unbinned, including per-class precision curves that are not monotone (the segment is the reference's COUNT
+``sum(x >= xp) - 1``, not a search, so it differs from torch.searchsorted there)."""
 import pytest
 import torch
 
@@ -15,7 +15,7 @@ def _ref_interp(x, xp, fp):
     den[den == 0.0] = 1
     m = (fp[1:] - fp[:-1]) / den
     b = fp[:-1] - (m * xp[:-1])
-    idx = torch.searchsorted(xp.contiguous(), x.contiguous(), right=True) - 1
+    idx = torch.sum(torch.ge(x[:, None], xp[None, :]), 1) - 1  # S/utilities/compute.py:154, verbatim formula
     idx = torch.clamp(idx, 0, len(m) - 1)
     return m[idx] * x + b[idx]
 
@@ -75,3 +75,34 @@ def test_interp_mean_ragged(dtype, device):
     for x, y in zip(xs, ys):
         ref += _ref_interp(grid, x, y)
     assert torch.equal(out.cpu(), ref / 4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_interp_count_segment_non_monotone(dtype, device):
+    """xp = [0.5, 0.3, 0.8] at v = 0.4: the reference's count picks segment 0 (one xp <= v), a search would pick 1."""
+    xp = torch.tensor([0.5, 0.3, 0.8], dtype=dtype)
+    fp = torch.tensor([1.0, 2.0, 4.0], dtype=dtype)
+    grid = torch.tensor([-1.0, 0.3, 0.4, 0.5, 0.6, 0.8, 2.0], dtype=dtype)
+    ref = _ref_interp(grid, xp, fp)
+    out = ops.interp_mean(grid.to(device), xp.to(device), fp.to(device), torch.tensor([0, 3]).to(device))
+    assert torch.equal(out.cpu(), ref)
+    assert torch.equal(tm.utilities.compute.interp(grid, xp, fp), ref)
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_interp_nan_and_random_non_monotone(device):
+    g = torch.Generator().manual_seed(7)
+    xs = [torch.rand(n, generator=g, dtype=torch.float64) for n in (5, 40, 2, 17)]
+    xs[1][3] = float("nan")
+    ys = [torch.rand(x.numel(), generator=g, dtype=torch.float64) for x in xs]
+    grid = torch.cat([torch.rand(200, generator=g, dtype=torch.float64), torch.tensor([float("nan"), float("inf")],
+                                                                                     dtype=torch.float64)])
+    ref = torch.zeros_like(grid)
+    for x, y in zip(xs, ys):
+        ref += _ref_interp(grid, x, y)
+        assert torch.equal(tm.utilities.compute.interp(grid, x, y), _ref_interp(grid, x, y), ) or torch.allclose(
+            tm.utilities.compute.interp(grid, x, y), _ref_interp(grid, x, y), equal_nan=True)
+    off = torch.tensor([0, 5, 45, 47, 64])
+    out = ops.interp_mean(grid.to(device), torch.cat(xs).to(device), torch.cat(ys).to(device), off.to(device))
+    assert torch.allclose(out.cpu(), ref / 4, equal_nan=True, rtol=0, atol=0)

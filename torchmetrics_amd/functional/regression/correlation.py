@@ -117,7 +117,17 @@ def _pearson_corrcoef_compute(var_x: Tensor, var_y: Tensor, corr_xy: Tensor, nb:
 def _final_aggregation(
     means_x: Tensor, means_y: Tensor, vars_x: Tensor, vars_y: Tensor, corrs_xy: Tensor, nbs: Tensor
 ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
-    """Merge per-rank ``[W, k]`` running statistics (Chan et al. parallel update, equivalent to the reference)."""
+    """Merge per-rank ``[W, k]`` running statistics (Chan et al. parallel update, equivalent to the reference's
+    ``S/regression/pearson.py:28-71`` loop over ranks): ONE ``ops.corr_merge`` launch over the stacked states (fp64
+    arithmetic, one rounding to the states' dtype), a host fold of the same formula when the library is absent."""
+    states = (means_x, means_y, vars_x, vars_y, corrs_xy, nbs)
+    dt = means_x.dtype
+    if (dt in (torch.float32, torch.float64) and ops.native_available()
+            and all(t.dtype == dt and t.shape == means_x.shape and t.device == means_x.device for t in states)):
+        w = means_x.shape[0]
+        merged = ops.corr_merge(torch.stack(states).reshape(6, w, -1))
+        tail = means_x.shape[1:]
+        return tuple(merged[i].view(tail) for i in range(6))  # type: ignore[return-value]
     mx, my, vx, vy, cxy, n = means_x[0], means_y[0], vars_x[0], vars_y[0], corrs_xy[0], nbs[0]
     for i in range(1, len(means_x)):
         mx2, my2, vx2, vy2, cxy2, n2 = means_x[i], means_y[i], vars_x[i], vars_y[i], corrs_xy[i], nbs[i]

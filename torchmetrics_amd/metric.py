@@ -72,6 +72,8 @@ def jit_distributed_available() -> bool:
 
 _DESCRIPTORS: Dict[type, frozenset] = {}
 _NO_NAMES: frozenset = frozenset()
+# nn.Module lifecycle attributes that are not metric configuration (no fused-plan invalidation)
+_LIFECYCLE_ATTRS = frozenset({"training", "call_super_init", "dump_patches"})
 
 
 def _data_descriptors(cls: type) -> frozenset:
@@ -1051,9 +1053,12 @@ class Metric(Module, ABC):
         chunks = d.get("_chunks")
         if chunks and name in chunks:
             del chunks[name]  # the state is rebound (reset, sync, load): its pending chunks are no longer its value
-        if name[0] != "_" and name not in d.get("_defaults", _NO_NAMES):
-            # a configuration attribute (average, num_classes, ...): plans recorded from this metric
-            # (utils/fused_compute.py) check the version before replaying
+        if (name[0] != "_" and name not in _LIFECYCLE_ATTRS and name not in d.get("_defaults", _NO_NAMES)
+                and not (name in d and d[name] is value and isinstance(value, (str, int, float, bool, type(None))))):
+            # a configuration attribute (average, num_classes, ...) that changes: plans recorded from this metric
+            # (utils/fused_compute.py) check the version before replaying.  nn.Module's own mode flag (``training``,
+            # set on every member by train() / eval()) is not configuration: a train / validate loop must not
+            # invalidate the plan at each mode switch
             d["_cfg_version"] = d.get("_cfg_version", 0) + 1
         # fast path for the bookkeeping attributes and states the lifecycle rebinds on every update / compute /
         # forward (nn.Module.__setattr__ costs ~1.5-2.5 us per call): an attribute this instance already holds as a

@@ -1318,6 +1318,13 @@ def pairwise_distance(x: Tensor, y: Tensor, metric: int, p: float = 2.0, zero_di
     return out.to(x.dtype)
 
 
+def corr_merge(stacked: Tensor) -> Tensor:
+    """Merge ``[6, W, k]`` stacked per-rank Pearson states (mean_x, mean_y, var_x, var_y, corr_xy, n) into ``[6, k]``
+    in one launch (``csrc/regression/regression_compute.hip`` ``corr_merge``; CPU tensors: the same fold on the
+    host)."""
+    return _ops().corr_merge(stacked.contiguous())
+
+
 # ------------------------------------------------------------------------------------------- MFMA GEMM epilogues
 GEMM_STORE, GEMM_EUCLID, GEMM_COSINE, GEMM_POLY_SUM, GEMM_ROW_MIN, GEMM_ROW_SUM, GEMM_ROW_COL_MAX = range(7)
 

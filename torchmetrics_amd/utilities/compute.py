@@ -90,11 +90,20 @@ def auc(x: Tensor, y: Tensor, reorder: bool = False) -> Tensor:
 
 
 def interp(x: Tensor, xp: Tensor, fp: Tensor) -> Tensor:
-    """Piecewise-linear interpolation of ``(xp, fp)`` at ``x`` (``xp`` increasing), extrapolating at the ends."""
+    """Piecewise-linear interpolation of ``(xp, fp)`` at ``x``, extrapolating at the ends.
+
+    The segment of ``x[j]`` is ``#{i : x[j] >= xp[i]} - 1`` clamped to ``[0, len(xp) - 2]``, as in the reference
+    (``S/utilities/compute.py:154``: a count over the whole curve, so a non-monotone ``xp`` picks the same segment).  The
+    count is taken as a binary search over a sorted copy of ``xp`` (NaN sorts last and counts for nothing) instead of
+    the reference's ``[len(x), len(xp)]`` comparison matrix."""
     slope = _safe_divide(fp[1:] - fp[:-1], xp[1:] - xp[:-1])
     icpt = fp[:-1] - slope * xp[:-1]
-    idx = torch.searchsorted(xp.contiguous(), x.contiguous(), right=True) - 1
-    idx = idx.clamp(0, slope.numel() - 1)
+    xs = xp.contiguous().sort().values
+    xc = x.contiguous()
+    cnt = torch.searchsorted(xs.nan_to_num(nan=float("inf")), xc, right=True)
+    # a NaN xp is never counted (NaN -> +inf above would count it for x = +inf); a NaN x counts nothing
+    cnt = torch.minimum(cnt, (~torch.isnan(xs)).sum()).masked_fill(torch.isnan(xc), 0)
+    idx = (cnt - 1).clamp(0, slope.numel() - 1)
     return slope[idx] * x + icpt[idx]
 
 

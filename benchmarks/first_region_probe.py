@@ -1,7 +1,7 @@
 """Fresh-process first-region cost of the headline loop (bench.py's exact shape: 406 MB ring, W warm-up updates,
 compute, reset, sync, then ONE timed region of 20 updates + compute + sync).  Each case runs in its own process:
 
-  python benchmarks/first_region_probe.py <case>   (case: plain | inplace_reset | warm50 | sleep10ms)
+  python benchmarks/first_region_probe.py <case>   (case: plain | onering | onering_same5 | warm50 | sleep10ms ...)
 Environment variables (e.g. HSA_ENABLE_INTERRUPT) are inherited from the caller.  Prints one JSON line."""
 import json
 import os
@@ -45,8 +45,16 @@ def main():
     warm = 50 if case == "warm50" else 5
     for i in range(warm):
         m.update(preds[i % K], target[i % K])
-    m.compute()
-    m.reset()  # (refills the state in place when unobserved)
+    if not case.endswith(("_nocr", "_ronly")):
+        m.compute()
+    if case.endswith("_zero"):  # the state zeroed by hand instead of reset()
+        m.confmat.zero_()
+        m._update_count = 0
+        m._computed = None
+    elif not case.endswith(("_nocr", "_conly")):
+        tr = time.perf_counter()
+        m.reset()  # (refills the state in place when unobserved)
+        reset_us = (time.perf_counter() - tr) * 1e6
     torch.cuda.synchronize()
     if case == "sleep10ms":
         time.sleep(0.01)
@@ -76,14 +84,16 @@ def main():
         while time.perf_counter() - t_s < 0.02:
             x.add_(1)
         torch.cuda.synchronize()
-    out = {"case": case, "env_interrupt": os.environ.get("HSA_ENABLE_INTERRUPT")}
+    out = {"case": case, "env_interrupt": os.environ.get("HSA_ENABLE_INTERRUPT"),
+           "reset_us": round(reset_us, 1) if "reset_us" in locals() else None}
     for rep in range(3):
         torch.cuda.synchronize()
         gc0 = gc.get_count()
         ts = []
         t0 = time.perf_counter()
         for i in range(20):
-            m.update(preds[(5 + 20 * rep + i) % K], target[(5 + 20 * rep + i) % K])
+            j = i % 5 if case.endswith("same5") else (5 + 20 * rep + i) % K  # same5: only the warm-up's 5 slots
+            m.update(preds[j], target[j])
             ts.append(time.perf_counter())
         t1 = time.perf_counter()
         out[f"per_update{rep}"] = [round(1e6 * (b - a), 1) for a, b in zip([t0] + ts[:-1], ts)]

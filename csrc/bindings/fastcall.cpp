@@ -15,6 +15,10 @@
 #include "../common/pack.h"
 #include <c10/util/Optional.h>
 
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstring>
 #include <tuple>
 #include <type_traits>
 #include <utility>
@@ -291,7 +295,59 @@ struct NativeUpdate {
   FastFn fast;         // the native body
   int stat_kind;       // NativeForward of the stat-score family: the score (cbody::StatKind)
   int decline;         // source line of the last fast-path decline (0: none yet) -- ``decline_line`` for diagnostics
+  char range_name[120];  // roctx range of the native call ("tm.update/<Metric>"); "" = no range
 };
+
+// ---------------------------------------------------------------------------------------------- roctx ranges
+// Profiler ranges on the PRODUCTION path: with ranges on (``profiling.enable()`` /
+// TORCHMETRICS_AMD_ROCTX=1 -> set_ranges(True)), every native update / forward opens "tm.update/<Metric>" /
+// "tm.forward/<Metric>" around its checks and kernel launch, so rocprofv3 --marker-trace shows the launch inside the
+// range while the fast path stays the one that runs.  The roctx library is opened on first use (rocprofiler-sdk's,
+// which rocprofv3 intercepts, else the legacy libroctx64); no library -> no ranges.  Off: one branch on a global.
+using RoctxPush = int (*)(const char*);
+using RoctxPop = int (*)();
+RoctxPush g_roctx_push = nullptr;
+RoctxPop g_roctx_pop = nullptr;
+bool g_ranges_on = false;
+
+bool bind_roctx() {
+  if (g_roctx_push != nullptr) return true;
+  for (const char* lib : {"librocprofiler-sdk-roctx.so", "/opt/rocm/lib/librocprofiler-sdk-roctx.so", "libroctx64.so",
+                          "/opt/rocm/lib/libroctx64.so"}) {
+    void* h = dlopen(lib, RTLD_NOW | RTLD_GLOBAL);
+    if (h == nullptr) continue;
+    auto push = reinterpret_cast<RoctxPush>(dlsym(h, "roctxRangePushA"));
+    auto pop = reinterpret_cast<RoctxPop>(dlsym(h, "roctxRangePop"));
+    if (push != nullptr && pop != nullptr) {
+      g_roctx_push = push;
+      g_roctx_pop = pop;
+      return true;
+    }
+  }
+  return false;
+}
+
+struct RangeScope {  // one roctx range for the lifetime of the scope (nothing when ranges are off / unnamed)
+  bool on;
+  explicit RangeScope(const NativeUpdate* self) : on(g_ranges_on && self->range_name[0] != '\0') {
+    if (on) g_roctx_push(self->range_name);
+  }
+  ~RangeScope() {
+    if (on) g_roctx_pop();
+  }
+};
+
+// set_ranges(on: bool) -> bool: turn the native ranges on / off; returns whether they are on (False: no roctx library)
+PyObject* set_ranges(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 1) {
+    PyErr_SetString(PyExc_TypeError, "set_ranges(on: bool)");
+    return nullptr;
+  }
+  const int on = PyObject_IsTrue(args[0]);
+  if (on < 0) return nullptr;
+  g_ranges_on = on && bind_roctx();
+  return PyBool_FromLong(g_ranges_on);
+}
 
 // leave the fast path, remembering where (NativeUpdate.decline_line names the check that sent a call to Python)
 #define TM_DECLINE        \
@@ -376,7 +432,11 @@ PyObject* native_update_vectorcall(PyObject* o, PyObject* const* args, size_t na
   const Py_ssize_t nargs = PyVectorcall_NARGS(nargsf);
   if (nargs == 2 && (kwnames == nullptr || PyTuple_GET_SIZE(kwnames) == 0)) {
     PyObject* result = nullptr;
-    const int r = self->fast(self, args[0], args[1], &result);
+    int r;
+    {
+      RangeScope range(self);  // (a declined call's Python path opens its own range)
+      r = self->fast(self, args[0], args[1], &result);
+    }
     if (r == 1) return result;
     if (r < 0) return nullptr;
   }
@@ -421,6 +481,25 @@ PyObject* native_update_decline(PyObject* o, void*) {
   return PyLong_FromLong(reinterpret_cast<NativeUpdate*>(o)->decline);
 }
 
+PyObject* native_update_range_get(PyObject* o, void*) {
+  return PyUnicode_FromString(reinterpret_cast<NativeUpdate*>(o)->range_name);
+}
+
+int native_update_range_set(PyObject* o, PyObject* v, void*) {
+  if (v == nullptr || !PyUnicode_Check(v)) {
+    PyErr_SetString(PyExc_TypeError, "range_name must be a str");
+    return -1;
+  }
+  Py_ssize_t n = 0;
+  const char* c = PyUnicode_AsUTF8AndSize(v, &n);
+  if (c == nullptr) return -1;
+  auto* self = reinterpret_cast<NativeUpdate*>(o);
+  const size_t k = std::min<size_t>(static_cast<size_t>(n), sizeof(self->range_name) - 1);
+  std::memcpy(self->range_name, c, k);
+  self->range_name[k] = '\0';
+  return 0;
+}
+
 PyObject* native_update_calls(PyObject* o, void*) {
   return PyLong_FromLongLong(reinterpret_cast<NativeUpdate*>(o)->calls);
 }
@@ -430,6 +509,7 @@ PyGetSetDef kNativeUpdateGetSet[] = {
     {"fallback", native_update_fallback, nullptr, nullptr, nullptr},
     {"native_calls", native_update_calls, nullptr, nullptr, nullptr},
     {"decline_line", native_update_decline, nullptr, nullptr, nullptr},
+    {"range_name", native_update_range_get, native_update_range_set, nullptr, nullptr},
     {nullptr, nullptr, nullptr, nullptr, nullptr},
 };
 
@@ -451,6 +531,7 @@ PyObject* make_confmat_updater(PyObject*, PyObject* const* args, Py_ssize_t narg
   self->sink = nullptr;
   self->calls = 0;
   self->decline = 0;
+  self->range_name[0] = '\0';
   self->fast = confmat_fast;
   self->stat_kind = 0;
   PyObject_GC_Track(reinterpret_cast<PyObject*>(self));
@@ -870,6 +951,7 @@ PyObject* make_stats_updater(PyObject*, PyObject* const* args, Py_ssize_t nargs)
   self->sink = nullptr;
   self->calls = 0;
   self->decline = 0;
+  self->range_name[0] = '\0';
   static const FastFn kFns[] = {nullptr, mc_stats_update_fast, bin_stats_update_fast, ml_stats_update_fast};
   self->fast = kFns[kind];
   self->stat_kind = 0;
@@ -903,6 +985,7 @@ PyObject* make_forward(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   self->sink = nullptr;
   self->calls = 0;
   self->decline = 0;
+  self->range_name[0] = '\0';
   static const FastFn kFns[] = {confmat_forward, mc_stats_forward_fast, bin_stats_forward_fast,
                                 ml_stats_forward_fast};
   self->fast = kFns[kind];
@@ -1078,6 +1161,8 @@ PyMethodDef kFactoryMethods[] = {
      METH_FASTCALL, "native MulticlassConfusionMatrix.update bound to a metric's __dict__"},
     {"map_pack", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&map_pack)), METH_FASTCALL,
      "MeanAveragePrecision.update's per-image validation and packing in one native call"},
+    {"set_ranges", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&set_ranges)), METH_FASTCALL,
+     "turn the roctx ranges of the native update / forward entry points on or off"},
     {"_states_unobserved", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&states_unobserved_probe)),
      METH_FASTCALL, "the native forward's test that nothing outside the metric holds the given states"},
     {nullptr, nullptr, 0, nullptr},

@@ -47,6 +47,8 @@ struct EpiParams {
   const int32_t* iy;
   int ldo;          // leading dim of out
   int part_cols;    // ROW_MIN / ROW_SUM partial columns (= column tiles)
+  uint16_t* out16;  // STORE / COSINE with a 16-bit output: [N, M] in bf16 (out_kind 1) or fp16 (2), else nullptr
+  int out_kind;
 };
 
 __device__ __forceinline__ float ipow(float b, int d) {
@@ -57,6 +59,184 @@ __device__ __forceinline__ float ipow(float b, int d) {
     d >>= 1;
   }
   return r;
+}
+
+// 16-bit output: round to nearest even (the rounding of a library GEMM writing bf16 / fp16 from its fp32 accumulator)
+__device__ __forceinline__ void store_out(const EpiParams& ep, long long idx, float v) {
+  if (ep.out_kind == 0) {
+    ep.out[idx] = v;
+  } else if (ep.out_kind == 1) {
+    ep.out16[idx] = __builtin_bit_cast(uint16_t, static_cast<__bf16>(v));
+  } else {
+    ep.out16[idx] = __builtin_bit_cast(uint16_t, static_cast<_Float16>(v));
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ shared epilogue
+// One implementation for every kernel of this file.  The block tile is TM x TM, NT threads = NT / 64 waves laid out as
+// (NT / 64 / WC) wave rows x WC wave columns; a wave owns NA x 2 MFMA 32 x 32 tiles: acc[a][b][e] holds
+// row wr + 32 a + (e & 3) + 8 (e >> 2) + 4 h, column wc + 32 b + r (the C/D map of every 32x32 MFMA form used here:
+// f32 32x32x2, bf16 / f16 32x32x16).  Reduction scratch reuses the staging LDS (`smem`), after a barrier.
+// `dist2(i, j)`: the exact difference-form squared distance of rows i, j (EUCLID's cancellation recompute).
+template <int EPI, int NA, int WC, int TM, int NT, typename Dist2>
+__device__ __forceinline__ void tile_epilogue(f32x16 (&acc)[NA][2], float* smem, const EpiParams& ep, int batch, int N,
+                                              int M, int row0, int col0, int ti, int tj, int tiles_n, int tile,
+                                              Dist2 dist2) {
+  constexpr int NWR = NT / 64 / WC;  // wave rows
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = (wave / WC) * 32 * NA, wc = (wave % WC) * 64;
+  const int h = lane >> 5, r = lane & 31;
+  __syncthreads();
+  if constexpr (EPI == kStore || EPI == kEuclid || EPI == kCosine) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int j = col0 + wc + 32 * b + r;
+        if (j >= M) continue;
+        float nyj = 0.f;
+        if constexpr (EPI != kStore) nyj = ep.ny[batch * (long long)M + j];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (i >= N) continue;
+          float v = acc[a][b][e];
+          if constexpr (EPI == kStore) {
+            v = (ep.zero_diag && i == j) ? 0.f : v * ep.scale;
+          } else if constexpr (EPI == kCosine) {
+            v = (ep.zero_diag && i == j) ? 0.f : v * ep.nx[batch * (long long)N + i] * nyj * ep.scale;
+          } else {
+            const float s2 = ep.nx[batch * (long long)N + i] + nyj;
+            float d2 = s2 - 2.0f * v;
+            if (d2 < s2 * (1.0f / 128.0f)) d2 = dist2(i, j);  // cancellation guard: exact difference form
+            d2 = fmaxf(d2, 0.f);
+            if (ep.zero_diag && i == j) d2 = 0.f;
+            v = ep.sqrt_out ? sqrtf(d2) : d2;
+          }
+          store_out(ep, batch * (long long)N * ep.ldo + (long long)i * ep.ldo + j, v);
+        }
+      }
+  } else if constexpr (EPI == kPolySum) {
+    double part = 0.0;
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int j = col0 + wc + 32 * b + r;
+        if (j >= M) continue;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (i >= N || (ep.zero_diag && i == j)) continue;
+          part += static_cast<double>(ipow(fmaf(acc[a][b][e], ep.scale, ep.coef), ep.degree));
+        }
+      }
+    part = wave_sum(part);
+    double* red = reinterpret_cast<double*>(smem);
+    if (lane == 0) red[wave] = part;
+    __syncthreads();
+    if (tid == 0) {
+      double t = 0.0;
+      for (int w = 0; w < NT / 64; ++w) t += red[w];
+      ep.dpart[(long long)batch * gridDim.x + tile] = t;
+    }
+  } else if constexpr (EPI == kRowColMax) {
+    // row maxima over this block's TM columns and column maxima over its TM rows (scaled dot)
+    float* redr = smem;            // [WC wave columns][TM]
+    float* redc = smem + WC * TM;  // [NWR wave rows][TM]
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int il = wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int i = row0 + il;
+        float v = -3.0e38f;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int j = col0 + wc + 32 * b + r;
+          if (j < M && i < N) v = fmaxf(v, acc[a][b][e] * ep.scale);
+        }
+#pragma unroll
+        for (int off = 16; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+        if (r == 0) redr[(wave % WC) * TM + il] = v;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int jl = wc + 32 * b + r;
+      float v = -3.0e38f;
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (i < N && col0 + jl < M) v = fmaxf(v, acc[a][b][e] * ep.scale);
+        }
+      v = fmaxf(v, __shfl_xor(v, 32, 64));  // the two lane halves hold interleaved row groups
+      if (h == 0) redc[(wave / WC) * TM + jl] = v;
+    }
+    __syncthreads();
+    for (int t = tid; t < 2 * TM; t += NT) {
+      if (t < TM) {
+        const int i = row0 + t;
+        if (i < N) {
+          float v = redr[t];
+#pragma unroll
+          for (int w = 1; w < WC; ++w) v = fmaxf(v, redr[w * TM + t]);
+          ep.out[(long long)batch * N * ep.part_cols + (long long)i * ep.part_cols + tj] = v;
+        }
+      } else {
+        const int jl = t - TM, j = col0 + jl;
+        if (j < M) {
+          float v = redc[jl];
+#pragma unroll
+          for (int w = 1; w < NWR; ++w) v = fmaxf(v, redc[w * TM + jl]);
+          ep.out2[((long long)batch * tiles_n + ti) * M + j] = v;
+        }
+      }
+    }
+  } else {
+    // ROW_MIN of (1 - |cos|) or ROW_SUM of the (scaled) dot: per row over this block's TM columns
+    float* red = smem;  // [WC][TM]
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int il = wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int i = row0 + il;
+        float v = EPI == kRowMin ? 3.0e38f : 0.f;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int j = col0 + wc + 32 * b + r;
+          if (j >= M || i >= N) continue;
+          float x = acc[a][b][e];
+          if constexpr (EPI == kRowMin) {
+            x = 1.0f - fabsf(x * ep.nx[batch * (long long)N + i] * ep.ny[batch * (long long)M + j]);
+            v = fminf(v, x);
+          } else {
+            v += x * ep.scale;
+          }
+        }
+        // reduce over the 32 columns held by this lane half (lanes r = 0..31)
+#pragma unroll
+        for (int off = 16; off > 0; off >>= 1) {
+          const float o = __shfl_xor(v, off, 64);
+          v = EPI == kRowMin ? fminf(v, o) : v + o;
+        }
+        if (r == 0) red[(wave % WC) * TM + il] = v;
+      }
+    }
+    __syncthreads();
+    for (int t = tid; t < TM; t += NT) {
+      const int i = row0 + t;
+      if (i < N) {
+        float v = red[t];
+#pragma unroll
+        for (int w = 1; w < WC; ++w) v = EPI == kRowMin ? fminf(v, red[w * TM + t]) : v + red[w * TM + t];
+        ep.out[(long long)batch * N * ep.part_cols + (long long)i * ep.part_cols + tj] = v;
+      }
+    }
+  }
 }
 
 template <int EPI, int STAGES, int kBK>
@@ -191,152 +371,17 @@ __global__ __launch_bounds__(kNT) void gemm_nt_kernel(const float* __restrict__ 
   }
 
   // ----------------------------------------------------------------------------------------------- epilogue
-  // acc[a][b][e]: row = wr + 32a + (e & 3) + 8 (e >> 2) + 4h, col = wc + 32b + r.  Reduction scratch reuses the
-  // (dynamic, 16-byte aligned) staging LDS after every wave is done with it.
-  __syncthreads();
-  if constexpr (EPI == kStore || EPI == kEuclid || EPI == kCosine) {
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int j = col0 + wc + 32 * b + r;
-        if (j >= M) continue;
-        float nyj = 0.f;
-        if constexpr (EPI != kStore) nyj = ep.ny[batch * (long long)M + j];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (i >= N) continue;
-          float v = acc[a][b][e];
-          if constexpr (EPI == kStore) {
-            v = (ep.zero_diag && i == j) ? 0.f : v * ep.scale;
-          } else if constexpr (EPI == kCosine) {
-            v = (ep.zero_diag && i == j) ? 0.f : v * ep.nx[batch * (long long)N + i] * nyj * ep.scale;
-          } else {
-            const float s2 = ep.nx[batch * (long long)N + i] + nyj;
-            float d2 = s2 - 2.0f * v;
-            if (d2 < s2 * (1.0f / 128.0f)) {
-              // cancellation guard: recompute this entry in the exact difference form
-              const float* xr = xrow(i);
-              const float* yr = yrow(j);
-              float t = 0.f;
-              for (int k = 0; k < D; ++k) {
-                const float d = xr[k] - yr[k];
-                t = fmaf(d, d, t);
-              }
-              d2 = t;
-            }
-            d2 = fmaxf(d2, 0.f);
-            if (ep.zero_diag && i == j) d2 = 0.f;
-            v = ep.sqrt_out ? sqrtf(d2) : d2;
-          }
-          ep.out[batch * (long long)N * ep.ldo + (long long)i * ep.ldo + j] = v;
-        }
-      }
-  } else if constexpr (EPI == kPolySum) {
-    double part = 0.0;
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int j = col0 + wc + 32 * b + r;
-        if (j >= M) continue;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (i >= N || (ep.zero_diag && i == j)) continue;
-          part += static_cast<double>(ipow(fmaf(acc[a][b][e], ep.scale, ep.coef), ep.degree));
-        }
-      }
-    part = wave_sum(part);
-    double* red = reinterpret_cast<double*>(smem);
-    if (lane == 0) red[wave] = part;
-    __syncthreads();
-    if (tid == 0) ep.dpart[(long long)batch * gridDim.x + tile] = red[0] + red[1] + red[2] + red[3];
-  } else if constexpr (EPI == kRowColMax) {
-    // row maxima over this block's 128 columns and column maxima over its 128 rows (scaled dot)
-    float* redr = smem;            // [2][kBM]: per column half
-    float* redc = smem + 2 * kBM;  // [2][kBN]: per row half
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int il = wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const int i = row0 + il;
-        float v = -3.0e38f;
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int j = col0 + wc + 32 * b + r;
-          if (j < M && i < N) v = fmaxf(v, acc[a][b][e] * ep.scale);
-        }
-#pragma unroll
-        for (int off = 16; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-        if (r == 0) redr[(wave & 1) * kBM + il] = v;
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int jl = wc + 32 * b + r;
-      float v = -3.0e38f;
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (i < N && col0 + jl < M) v = fmaxf(v, acc[a][b][e] * ep.scale);
-        }
-      v = fmaxf(v, __shfl_xor(v, 32, 64));  // the two lane halves hold interleaved row groups
-      if (h == 0) redc[(wave >> 1) * kBN + jl] = v;
-    }
-    __syncthreads();
-    if (tid < kBM) {
-      const int i = row0 + tid;
-      if (i < N) ep.out[(long long)batch * N * ep.part_cols + (long long)i * ep.part_cols + tj] =
-          fmaxf(redr[tid], redr[kBM + tid]);
-    } else if (tid < kBM + kBN) {
-      const int jl = tid - kBM, j = col0 + jl;
-      if (j < M) ep.out2[((long long)batch * tiles_n + ti) * M + j] = fmaxf(redc[jl], redc[kBN + jl]);
-    }
-  } else {
-    // ROW_MIN of (1 - cos) or ROW_SUM of the (scaled) dot: per row over this block's 128 columns
-    float* red = smem;  // [2][kBM]
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int il = wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const int i = row0 + il;
-        float v = EPI == kRowMin ? 3.0e38f : 0.f;
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int j = col0 + wc + 32 * b + r;
-          if (j >= M || i >= N) continue;
-          float x = acc[a][b][e];
-          if constexpr (EPI == kRowMin) {
-            x = 1.0f - fabsf(x * ep.nx[batch * (long long)N + i] * ep.ny[batch * (long long)M + j]);
-            v = fminf(v, x);
-          } else {
-            v += x * ep.scale;
-          }
-        }
-        // reduce over the 32 columns held by this lane half (lanes r = 0..31)
-#pragma unroll
-        for (int off = 16; off > 0; off >>= 1) {
-          const float o = __shfl_xor(v, off, 64);
-          v = EPI == kRowMin ? fminf(v, o) : v + o;
-        }
-        if (r == 0) red[(wave & 1) * kBM + il] = v;
-      }
-    }
-    __syncthreads();
-    if (tid < kBM) {
-      const int i = row0 + tid;
-      if (i < N) {
-        const float v = EPI == kRowMin ? fminf(red[tid], red[kBM + tid]) : red[tid] + red[kBM + tid];
-        ep.out[(long long)batch * N * ep.part_cols + (long long)i * ep.part_cols + tj] = v;
-      }
-    }
-  }
+  tile_epilogue<EPI, 2, 2, kBM, kNT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile,
+                                     [&](int i, int j) {
+                                       const float* xr = xrow(i);
+                                       const float* yr = yrow(j);
+                                       float t = 0.f;
+                                       for (int k = 0; k < D; ++k) {
+                                         const float d = xr[k] - yr[k];
+                                         t = fmaf(d, d, t);
+                                       }
+                                       return t;
+                                     });
 }
 
 // ------------------------------------------------------------------------------------------------ 256 x 256 tiles
@@ -490,155 +535,179 @@ __global__ __launch_bounds__(kGT) void gemm_nt_big_kernel(const float* __restric
   }
 
   // ----------------------------------------------------------------------------------------------- epilogue
-  // acc[a][b][e]: row = wr + 32a + (e & 3) + 8 (e >> 2) + 4h, col = wc + 32b + r.  Reduction scratch reuses the
-  // staging LDS after every wave is done with it (no DMA is in flight: the last chunk issued none).
-  __syncthreads();
-  if constexpr (EPI == kStore || EPI == kEuclid || EPI == kCosine) {
+  // (no DMA is in flight: the last chunk issued none)
+  tile_epilogue<EPI, 4, 4, kGM, kGT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile,
+                                     [&](int i, int j) {
+                                       const float* xr = xrow(i);
+                                       const float* yr = yrow(j);
+                                       float t = 0.f;
+                                       for (int k = 0; k < D; ++k) {
+                                         const float d = xr[k] - yr[k];
+                                         t = fmaf(d, d, t);
+                                       }
+                                       return t;
+                                     });
+}
+
+// ------------------------------------------------------------------------------------------ 16-bit operands
+// bf16 / fp16 operands on the 16-bit matrix cores: v_mfma_f32_32x32x16_{bf16,f16} (fp32 accumulate; 16x the rate of the
+// fp32 MFMA above), read straight from the caller's 16-bit tensors -- no fp32 upcast copy.  The structure is the
+// 256 x 256 kernel's (the 128 x 128 form for small problems): a k-chunk of 64 elements is a 128-byte LDS row, exactly
+// the fp32 kernel's 32-float chunk, staged by global_load_lds_dwordx4 into two swizzled stages (chunk c of row r at
+// c ^ ((r >> 1) & 7)), one barrier per chunk placed inside its last k-step.  A chunk is 4 MFMA k-steps of 16: lane
+// (r, h) of step s reads logical chunk 2 s + h of its row = A[row][16 s + 8 h + j] / B[k][col] for j = 0..7 (the
+// operand map of the 32x32x16 forms), one ds_read_b128 per fragment.  K need not be a multiple of 64: a 16-byte
+// source chunk at or past D (D % 8 == 0) is redirected to a zero block, so the DMA itself writes the zero padding.
+template <typename T>
+struct Mfma16;
+template <>
+struct Mfma16<__bf16> {
+  typedef __bf16 v8 __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ f32x16 run(v8 a, v8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ float to_f32(uint16_t v) { return static_cast<float>(__builtin_bit_cast(__bf16, v)); }
+};
+template <>
+struct Mfma16<_Float16> {
+  typedef _Float16 v8 __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ f32x16 run(v8 a, v8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ float to_f32(uint16_t v) {
+    return static_cast<float>(__builtin_bit_cast(_Float16, v));
+  }
+};
+
+__device__ __attribute__((aligned(16))) uint32_t g_zero_chunk[4];  // the DMA source of K padding (never written)
+
+template <int EPI, typename T, int TM>
+__global__ __launch_bounds__(TM == 256 ? 512 : 256) void gemm_nt_h16_kernel(
+    const uint16_t* __restrict__ X, const uint16_t* __restrict__ Y, int N, int M, int D, long long bx, long long by,
+    int tiles_m, EpiParams ep) {
+  constexpr int NT = TM == 256 ? 512 : 256, WC = TM == 256 ? 4 : 2, NA = TM == 256 ? 4 : 2, KC = 64;
+  typedef typename Mfma16<T>::v8 v8;
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // [2 stages][A TM x 64 | B TM x 64] 16-bit elements
+  uint16_t* sh = reinterpret_cast<uint16_t*>(smem);
+  constexpr int kStage = 2 * TM * KC;  // elements per stage
+  const int batch = blockIdx.z;
+  const int32_t* gix = ep.ix ? ep.ix + (long long)batch * N : nullptr;
+  const int32_t* giy = ep.iy ? ep.iy + (long long)batch * M : nullptr;
+  if (!gix) X += batch * bx;
+  if (!giy) Y += batch * by;
+  auto xrow = [&](int i) -> const uint16_t* { return X + (long long)(gix ? gix[i] : i) * D; };
+  auto yrow = [&](int j) -> const uint16_t* { return Y + (long long)(giy ? giy[j] : j) * D; };
+  const int tiles_n = (N + TM - 1) / TM;
+  const int total = tiles_n * tiles_m;
+  const int bid = blockIdx.x;
+  const int per = (total + 7) / 8;
+  const int tile = (bid % 8) * per + bid / 8;  // XCD-aware: each XCD takes a contiguous band of row-major tiles
+  if (tile >= total) return;
+  const int ti = tile / tiles_m, tj = tile - ti * tiles_m;
+  const int row0 = ti * TM, col0 = tj * TM;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = (wave / WC) * 32 * NA, wc = (wave % WC) * 64;
+  const int h = lane >> 5, r = lane & 31;
+
+  // DMA: wave w moves rows [32 w, 32 w + 32) of each operand tile (TM / waves = 32 for both tile sizes), 8 rows
+  // (1 KiB) per instruction; lane l of instruction q covers row 32 w + 8 q + l / 8, LDS slot l % 8 = logical chunk
+  // (l % 8) ^ ((row >> 1) & 7).  Rows past N / M read a valid row (their products are never stored).
+  const uint16_t* srcA[4];
+  const uint16_t* srcB[4];
+  int kof[4];  // element offset of the lane's logical chunk inside a k-chunk
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+  for (int q = 0; q < 4; ++q) {
+    const int rr = 32 * wave + 8 * q + (lane >> 3);
+    const int c = (lane & 7) ^ ((rr >> 1) & 7);
+    kof[q] = 8 * c;
+    srcA[q] = xrow(min(row0 + rr, N - 1)) + 8 * c;
+    srcB[q] = yrow(min(col0 + rr, M - 1)) + 8 * c;
+  }
+  typedef __attribute__((address_space(3))) void lds_t;
+  typedef __attribute__((address_space(1))) void glb_t;
+  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
+  auto stage = [&](int kc, int buf) {
+    uint16_t* sa = sh + buf * kStage;
+    uint16_t* sb = sa + TM * KC;
+    const int k0 = kc * KC;
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int j = col0 + wc + 32 * b + r;
-        if (j >= M) continue;
-        float nyj = 0.f;
-        if constexpr (EPI != kStore) nyj = ep.ny[batch * (long long)M + j];
+    for (int q = 0; q < 4; ++q) {
+      const bool in = k0 + kof[q] < D;
+      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcA[q] + k0 : zero), (lds_t*)(sa + (32 * wave + 8 * q) * KC),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcB[q] + k0 : zero), (lds_t*)(sb + (32 * wave + 8 * q) * KC),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x16 acc[NA][2];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (i >= N) continue;
-          float v = acc[a][b][e];
-          if constexpr (EPI == kStore) {
-            v = (ep.zero_diag && i == j) ? 0.f : v * ep.scale;
-          } else if constexpr (EPI == kCosine) {
-            v = (ep.zero_diag && i == j) ? 0.f : v * ep.nx[batch * (long long)N + i] * nyj * ep.scale;
-          } else {
-            const float s2 = ep.nx[batch * (long long)N + i] + nyj;
-            float d2 = s2 - 2.0f * v;
-            if (d2 < s2 * (1.0f / 128.0f)) {
-              const float* xr = xrow(i);
-              const float* yr = yrow(j);
-              float t = 0.f;
-              for (int k = 0; k < D; ++k) {
-                const float d = xr[k] - yr[k];
-                t = fmaf(d, d, t);
-              }
-              d2 = t;
-            }
-            d2 = fmaxf(d2, 0.f);
-            if (ep.zero_diag && i == j) d2 = 0.f;
-            v = ep.sqrt_out ? sqrtf(d2) : d2;
-          }
-          ep.out[batch * (long long)N * ep.ldo + (long long)i * ep.ldo + j] = v;
-        }
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  const int swz_a = ((wr + r) >> 1) & 7;  // (32 a keeps (row >> 1) & 7)
+  const int swz_b = ((wc + r) >> 1) & 7;
+  const int nk = (D + KC - 1) / KC;
+  // fragments of k-step s of LDS stage `buf`: logical chunk 2 s + h of rows wr + 32 a + r / wc + 32 b + r
+  auto frag = [&](int buf, int s, v8* fa, v8* fb) {
+    const uint16_t* sa = sh + buf * kStage + (wr + r) * KC;
+    const uint16_t* sb = sh + buf * kStage + TM * KC + (wc + r) * KC;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) fa[a] = *reinterpret_cast<const v8*>(sa + 32 * a * KC + 8 * ((2 * s + h) ^ swz_a));
+#pragma unroll
+    for (int b = 0; b < 2; ++b) fb[b] = *reinterpret_cast<const v8*>(sb + 32 * b * KC + 8 * ((2 * s + h) ^ swz_b));
+  };
+  auto mma = [&](const v8* fa, const v8* fb) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] = Mfma16<T>::run(fa[a], fb[b], acc[a][b]);
+  };
+  v8 ca[NA], cb[2], na[NA], nb[2];
+  // chunk kc+1's barrier sits inside chunk kc, after its last LDS read (step 3's fragments, loaded during step 2's
+  // MFMAs) and before step 3's MFMAs: the matrix pipe still holds step 2's work while the waves meet there
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (nk > 1) stage(1, 1);
+  frag(0, 0, ca, cb);
+  for (int kc = 0; kc < nk; ++kc) {
+    const int buf = kc & 1;
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const bool more = s4 < 3 || kc + 1 < nk;
+      if (s4 < 3) {
+        frag(buf, s4 + 1, na, nb);
+      } else if (kc + 1 < nk) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // chunk kc+1 DMAs; chunk kc reads landed
+        __builtin_amdgcn_s_barrier();
+        if (kc + 2 < nk) stage(kc + 2, buf);
+        frag(buf ^ 1, 0, na, nb);
       }
-  } else if constexpr (EPI == kPolySum) {
-    double part = 0.0;
+      mma(ca, cb);
+      if (more) {
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < NA; ++a) ca[a] = na[a];
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int j = col0 + wc + 32 * b + r;
-        if (j >= M) continue;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (i >= N || (ep.zero_diag && i == j)) continue;
-          part += static_cast<double>(ipow(fmaf(acc[a][b][e], ep.scale, ep.coef), ep.degree));
-        }
-      }
-    part = wave_sum(part);
-    double* red = reinterpret_cast<double*>(smem);
-    if (lane == 0) red[wave] = part;
-    __syncthreads();
-    if (tid == 0) {
-      double t = 0.0;
-      for (int w = 0; w < kGT / 64; ++w) t += red[w];
-      ep.dpart[(long long)batch * gridDim.x + tile] = t;
-    }
-  } else if constexpr (EPI == kRowColMax) {
-    float* redr = smem;            // [4 wave columns][kGM]
-    float* redc = smem + 4 * kGM;  // [2 wave rows][kGN]
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int il = wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const int i = row0 + il;
-        float v = -3.0e38f;
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int j = col0 + wc + 32 * b + r;
-          if (j < M && i < N) v = fmaxf(v, acc[a][b][e] * ep.scale);
-        }
-#pragma unroll
-        for (int off = 16; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-        if (r == 0) redr[(wave & 3) * kGM + il] = v;
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int jl = wc + 32 * b + r;
-      float v = -3.0e38f;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int i = row0 + wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (i < N && col0 + jl < M) v = fmaxf(v, acc[a][b][e] * ep.scale);
-        }
-      v = fmaxf(v, __shfl_xor(v, 32, 64));
-      if (h == 0) redc[(wave >> 2) * kGN + jl] = v;
-    }
-    __syncthreads();
-    if (tid < kGM) {
-      const int i = row0 + tid;
-      if (i < N)
-        ep.out[(long long)batch * N * ep.part_cols + (long long)i * ep.part_cols + tj] =
-            fmaxf(fmaxf(redr[tid], redr[kGM + tid]), fmaxf(redr[2 * kGM + tid], redr[3 * kGM + tid]));
-    } else {
-      const int jl = tid - kGM, j = col0 + jl;
-      if (j < M) ep.out2[((long long)batch * tiles_n + ti) * M + j] = fmaxf(redc[jl], redc[kGN + jl]);
-    }
-  } else {
-    float* red = smem;  // [4 wave columns][kGM]
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int il = wr + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const int i = row0 + il;
-        float v = EPI == kRowMin ? 3.0e38f : 0.f;
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int j = col0 + wc + 32 * b + r;
-          if (j >= M || i >= N) continue;
-          float x = acc[a][b][e];
-          if constexpr (EPI == kRowMin) {
-            x = 1.0f - fabsf(x * ep.nx[batch * (long long)N + i] * ep.ny[batch * (long long)M + j]);
-            v = fminf(v, x);
-          } else {
-            v += x * ep.scale;
-          }
-        }
-#pragma unroll
-        for (int off = 16; off > 0; off >>= 1) {
-          const float o = __shfl_xor(v, off, 64);
-          v = EPI == kRowMin ? fminf(v, o) : v + o;
-        }
-        if (r == 0) red[(wave & 3) * kGM + il] = v;
-      }
-    }
-    __syncthreads();
-    if (tid < kGM) {
-      const int i = row0 + tid;
-      if (i < N) {
-        const float v = EPI == kRowMin
-                            ? fminf(fminf(red[tid], red[kGM + tid]), fminf(red[2 * kGM + tid], red[3 * kGM + tid]))
-                            : (red[tid] + red[kGM + tid]) + (red[2 * kGM + tid] + red[3 * kGM + tid]);
-        ep.out[(long long)batch * N * ep.part_cols + (long long)i * ep.part_cols + tj] = v;
+        for (int b = 0; b < 2; ++b) cb[b] = nb[b];
       }
     }
   }
+  // (no DMA is in flight: the last chunk issued none)
+  tile_epilogue<EPI, NA, WC, TM, NT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile,
+                                     [&](int i, int j) {
+                                       const uint16_t* xr = xrow(i);
+                                       const uint16_t* yr = yrow(j);
+                                       float t = 0.f;
+                                       for (int k = 0; k < D; ++k) {
+                                         const float d = Mfma16<T>::to_f32(xr[k]) - Mfma16<T>::to_f32(yr[k]);
+                                         t = fmaf(d, d, t);
+                                       }
+                                       return t;
+                                     });
 }
 
 // The 256 x 256 kernel for large problems: D a multiple of its k-step, both sides at least one tile, enough tiles to
@@ -711,6 +780,33 @@ void launch(const at::Tensor& x, const at::Tensor& y, int batches, long long bx,
   }
 }
 
+
+// 16-bit operands: the 256 x 256 tile where it fills the chip (the fp32 kernel's rule), else 128 x 128
+template <int EPI, typename T>
+void launch_h16(const at::Tensor& x, const at::Tensor& y, int batches, long long bx, long long by, int N, int M, int D,
+                const EpiParams& ep, bool big) {
+  const int tm = big ? 256 : 128;
+  const int tiles_n = (N + tm - 1) / tm, tiles_m = (M + tm - 1) / tm;
+  const int per = (tiles_n * tiles_m + 7) / 8;
+  const size_t lds = 2ull * 2 * tm * 64 * sizeof(uint16_t);
+  const auto* xp = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  const auto* yp = reinterpret_cast<const uint16_t*>(y.data_ptr());
+  if (big)
+    hipLaunchKernelGGL((gemm_nt_h16_kernel<EPI, T, 256>), dim3(per * 8, 1, batches), dim3(512), lds, stream(), xp, yp,
+                       N, M, D, bx, by, tiles_m, ep);
+  else
+    hipLaunchKernelGGL((gemm_nt_h16_kernel<EPI, T, 128>), dim3(per * 8, 1, batches), dim3(256), lds, stream(), xp, yp,
+                       N, M, D, bx, by, tiles_m, ep);
+}
+
+template <int EPI>
+void launch_any(const at::Tensor& x, const at::Tensor& y, int batches, long long bx, long long by, int N, int M, int D,
+                const EpiParams& ep, bool big16) {
+  if (x.scalar_type() == at::kBFloat16) launch_h16<EPI, __bf16>(x, y, batches, bx, by, N, M, D, ep, big16);
+  else if (x.scalar_type() == at::kHalf) launch_h16<EPI, _Float16>(x, y, batches, bx, by, N, M, D, ep, big16);
+  else launch<EPI>(x, y, batches, bx, by, N, M, D, ep);
+}
+
 }  // namespace
 
 // x: [B, N, D] or [N, D]; y: [B, M, D] or [M, D] (fp32, contiguous).  kind: 0 store, 1 euclid, 2 cosine,
@@ -719,10 +815,14 @@ void launch(const at::Tensor& x, const at::Tensor& y, int batches, long long bx,
 // (3), fp32 partials [B, N, tiles_m] (4-5), flat fp32 [B*N*tiles_m row partials | B*tiles_n*M column partials] (6).
 at::Tensor gemm_nt(const at::Tensor& x, const at::Tensor& y, int64_t kind, const c10::optional<at::Tensor>& aux_x,
                    const c10::optional<at::Tensor>& aux_y, double scale, double coef, int64_t degree, bool zero_diag,
-                   bool sqrt_out, const c10::optional<at::Tensor>& idx_x, const c10::optional<at::Tensor>& idx_y) {
+                   bool sqrt_out, const c10::optional<at::Tensor>& idx_x, const c10::optional<at::Tensor>& idx_y,
+                   int64_t out_kind) {
   TM_CHECK_CUDA(x);
   TM_SAME_DEVICE(x, y);
-  TORCH_CHECK(x.scalar_type() == at::kFloat && y.scalar_type() == at::kFloat, "gemm_nt: fp32 operands");
+  const auto dt = x.scalar_type();
+  const bool h16 = dt == at::kBFloat16 || dt == at::kHalf;
+  TORCH_CHECK((dt == at::kFloat || h16) && y.scalar_type() == dt, "gemm_nt: fp32 / bf16 / fp16 operands of one dtype");
+  TORCH_CHECK(out_kind == 0 || (out_kind == 1 && h16), "gemm_nt: out_kind 1 (16-bit output) needs 16-bit operands");
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous(), "gemm_nt: contiguous operands");
   TORCH_CHECK(x.dim() == y.dim() && (x.dim() == 2 || x.dim() == 3), "gemm_nt: [N, D] / [B, N, D] operands");
   const bool gathered = idx_x.has_value();
@@ -749,13 +849,15 @@ at::Tensor gemm_nt(const at::Tensor& x, const at::Tensor& y, int64_t kind, const
   TORCH_CHECK(y.size(-1) == D, "gemm_nt: inner dimension mismatch");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
               "gemm_nt: 16-byte aligned operands");
-  TORCH_CHECK(D % 4 == 0, "gemm_nt: D must be a multiple of 4 (float4 rows)");
+  TORCH_CHECK(D % (h16 ? 8 : 4) == 0, "gemm_nt: D must be a multiple of 16 bytes (4 fp32 / 8 16-bit elements)");
+  TORCH_CHECK(D > 0 && N > 0 && M > 0, "gemm_nt: empty operands");
   TORCH_CHECK(static_cast<long long>(N) * M * B < (1LL << 40), "gemm_nt: output too large");
-  const bool big = big_choice(N, M, D, B);
+  // 16-bit operands: the 256 x 256 tile once it alone fills the chip (256 tiles), else 128 x 128
+  const bool big = h16 ? static_cast<long long>((N + 255) / 256) * ((M + 255) / 256) * B >= 256 : big_choice(N, M, D, B);
   const int tbm = big ? kGM : kBM, tbn = big ? kGN : kBN;
   const int tiles_n = (N + tbm - 1) / tbm, tiles_m = (M + tbn - 1) / tbn;
   const int blocks = ((tiles_n * tiles_m + 7) / 8) * 8;
-  auto f32 = x.options();
+  auto f32 = x.options().dtype(at::kFloat);
   ep.scale = static_cast<float>(scale);
   ep.coef = static_cast<float>(coef);
   ep.degree = static_cast<int>(degree);
@@ -780,18 +882,23 @@ at::Tensor gemm_nt(const at::Tensor& x, const at::Tensor& y, int64_t kind, const
     case kStore:
     case kEuclid:
     case kCosine:
-      out = batched ? at::empty({B, N, M}, f32) : at::empty({N, M}, f32);
-      ep.out = out.data_ptr<float>();
+      out = batched ? at::empty({B, N, M}, out_kind ? x.options() : f32) : at::empty({N, M}, out_kind ? x.options() : f32);
+      if (out_kind) {
+        ep.out16 = reinterpret_cast<uint16_t*>(out.data_ptr());
+        ep.out_kind = dt == at::kBFloat16 ? 1 : 2;
+      } else {
+        ep.out = out.data_ptr<float>();
+      }
       ep.ldo = M;
-      if (kind == kStore) launch<kStore>(x, y, B, bx, by, N, M, D, ep);
-      else if (kind == kEuclid) launch<kEuclid>(x, y, B, bx, by, N, M, D, ep);
-      else launch<kCosine>(x, y, B, bx, by, N, M, D, ep);
+      if (kind == kStore) launch_any<kStore>(x, y, B, bx, by, N, M, D, ep, big);
+      else if (kind == kEuclid) launch_any<kEuclid>(x, y, B, bx, by, N, M, D, ep, big);
+      else launch_any<kCosine>(x, y, B, bx, by, N, M, D, ep, big);
       break;
     case kPolySum:
       out = batched ? at::zeros({B, blocks}, x.options().dtype(at::kDouble))
                     : at::zeros({blocks}, x.options().dtype(at::kDouble));
       ep.dpart = out.data_ptr<double>();
-      launch<kPolySum>(x, y, B, bx, by, N, M, D, ep);
+      launch_any<kPolySum>(x, y, B, bx, by, N, M, D, ep, big);
       break;
     case kRowColMax: {
       // row partials [B, N, tiles_m] then column partials [B, tiles_n, M] in one allocation
@@ -800,7 +907,7 @@ at::Tensor gemm_nt(const at::Tensor& x, const at::Tensor& y, int64_t kind, const
       ep.out = out.data_ptr<float>();
       ep.out2 = ep.out + nrow;
       ep.part_cols = tiles_m;
-      launch<kRowColMax>(x, y, B, bx, by, N, M, D, ep);
+      launch_any<kRowColMax>(x, y, B, bx, by, N, M, D, ep, big);
       break;
     }
     case kRowMin:
@@ -808,8 +915,8 @@ at::Tensor gemm_nt(const at::Tensor& x, const at::Tensor& y, int64_t kind, const
       out = batched ? at::empty({B, N, tiles_m}, f32) : at::empty({N, tiles_m}, f32);
       ep.out = out.data_ptr<float>();
       ep.part_cols = tiles_m;
-      if (kind == kRowMin) launch<kRowMin>(x, y, B, bx, by, N, M, D, ep);
-      else launch<kRowSum>(x, y, B, bx, by, N, M, D, ep);
+      if (kind == kRowMin) launch_any<kRowMin>(x, y, B, bx, by, N, M, D, ep, big);
+      else launch_any<kRowSum>(x, y, B, bx, by, N, M, D, ep, big);
       break;
     default:
       TORCH_CHECK(false, "gemm_nt: unknown epilogue ", kind);
@@ -823,6 +930,6 @@ at::Tensor gemm_nt(const at::Tensor& x, const at::Tensor& y, int64_t kind, const
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
   m.def(
       "gemm_nt(Tensor x, Tensor y, int kind, Tensor? aux_x, Tensor? aux_y, float scale, float coef, int degree, "
-      "bool zero_diag, bool sqrt_out, Tensor? idx_x=None, Tensor? idx_y=None) -> Tensor");
+      "bool zero_diag, bool sqrt_out, Tensor? idx_x=None, Tensor? idx_y=None, int out_kind=0) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) { m.impl("gemm_nt", &tm_amd::gemm_nt); }

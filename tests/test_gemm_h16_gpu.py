@@ -1,0 +1,116 @@
+"""16-bit MFMA NT-GEMM (``gemm_nt_h16_kernel``: v_mfma_f32_32x32x16_{bf16,f16}, fp32 accumulate) against a plain
+PyTorch fp32 GEMM of the same 16-bit values (the products are exact in fp32, only the summation order differs): every
+epilogue, both tile sizes (128 x 128 for small problems, 256 x 256 once the tiles fill the chip), K not a multiple of
+the 64-element k-chunk, partial tiles, batched and row-gathered operands, 16-bit outputs, and the pairwise functionals
+that route bf16 / fp16 here (reference F/pairwise/linear.py:23, cosine.py:24-46: GEMM in the input dtype)."""
+import pytest
+import torch
+
+import torchmetrics_amd as tm
+from torchmetrics_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+DT = [torch.bfloat16, torch.float16]
+
+
+def _xy(n, m, d, dtype, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return ((torch.randn(n, d, generator=g)).to(dtype), (torch.randn(m, d, generator=g) * 0.5 + 0.1).to(dtype))
+
+
+def _tol(d):
+    return dict(rtol=2e-5, atol=2e-5 * d ** 0.5)
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("n,m,d", [(300, 200, 72), (128, 128, 64), (1000, 777, 200), (4100, 4097, 96),
+                                   (4096, 4096, 8)])
+def test_h16_store(dtype, n, m, d):
+    x, y = _xy(n, m, d, dtype)
+    out = ops.gemm_nt(x.to(DEV), y.to(DEV), ops.GEMM_STORE, scale=0.5)
+    assert out.dtype == torch.float32
+    ref = 0.5 * (x.double() @ y.double().T)
+    torch.testing.assert_close(out.cpu().double(), ref, **_tol(d))
+    o16 = ops.gemm_nt(x.to(DEV), y.to(DEV), ops.GEMM_STORE, scale=0.5, out_dtype=dtype)
+    assert o16.dtype == dtype
+    assert torch.equal(o16.cpu(), out.cpu().to(dtype))  # the epilogue rounds exactly as a cast of the fp32 result
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("n,m,d", [(333, 257, 136), (4100, 4097, 96)])
+def test_h16_cosine_euclid(dtype, n, m, d):
+    x, y = _xy(n, m, d, dtype, 1)
+    xd, yd = x.double(), y.double()
+    ix, iy = 1 / xd.norm(dim=1), 1 / yd.norm(dim=1)
+    out = ops.gemm_nt(x.to(DEV), y.to(DEV), ops.GEMM_COSINE, ix.float().to(DEV), iy.float().to(DEV))
+    ref = (xd @ yd.T) * ix[:, None] * iy[None]
+    torch.testing.assert_close(out.cpu().double(), ref, rtol=1e-5, atol=1e-5)
+    nx, ny = (xd * xd).sum(1), (yd * yd).sum(1)
+    out = ops.gemm_nt(x.to(DEV), y.to(DEV), ops.GEMM_EUCLID, nx.float().to(DEV), ny.float().to(DEV))
+    torch.testing.assert_close(out.cpu().double(), torch.cdist(xd, yd), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("n,m,d", [(517, 300, 64), (4100, 4097, 96)])
+def test_h16_reductions(dtype, n, m, d):
+    x, y = _xy(n, m, d, dtype, 2)
+    xd, yd = x.to(DEV), y.to(DEV)
+    dot = x.double() @ y.double().T
+    part = ops.gemm_nt(xd, yd, ops.GEMM_POLY_SUM, scale=1 / d, coef=1.0, degree=3).cpu()
+    torch.testing.assert_close(part.sum(), ((dot / d + 1) ** 3).sum(), rtol=1e-5, atol=1e-2)
+    ix, iy = 1 / x.double().norm(dim=1), 1 / y.double().norm(dim=1)
+    rmin = ops.gemm_nt(xd, yd, ops.GEMM_ROW_MIN, ix.float().to(DEV), iy.float().to(DEV)).cpu().min(-1).values
+    cos = dot * ix[:, None] * iy[None]
+    torch.testing.assert_close(rmin.double(), (1 - cos.abs()).min(1).values, rtol=1e-5, atol=1e-5)
+    rsum = ops.gemm_nt(xd, yd, ops.GEMM_ROW_SUM, scale=0.25).cpu().sum(-1).double()
+    torch.testing.assert_close(rsum, 0.25 * dot.sum(1), rtol=1e-4, atol=1e-2)
+    rmax, cmax = ops.gemm_row_col_max(xd[None], yd[None], scale=0.5)
+    torch.testing.assert_close(rmax[0].cpu().double(), 0.5 * dot.max(1).values, **_tol(d))
+    torch.testing.assert_close(cmax[0].cpu().double(), 0.5 * dot.max(0).values, **_tol(d))
+
+
+@pytest.mark.parametrize("dtype", DT)
+def test_h16_batched_gathered_zero_diag(dtype):
+    g = torch.Generator().manual_seed(3)
+    xb, yb = torch.randn(3, 300, 136, generator=g).to(dtype), torch.randn(3, 260, 136, generator=g).to(dtype)
+    out = ops.gemm_nt(xb.to(DEV), yb.to(DEV), ops.GEMM_STORE, zero_diagonal=True).cpu().double()
+    ref = xb.double() @ yb.double().transpose(1, 2)
+    ref[:, torch.arange(260), torch.arange(260)] = 0
+    torch.testing.assert_close(out, ref, **_tol(136))
+    feats = torch.randn(2000, 128, generator=g).to(dtype)
+    ix = torch.randint(0, 2000, (4, 500), generator=g, dtype=torch.int32)
+    iy = torch.randint(0, 2000, (4, 400), generator=g, dtype=torch.int32)
+    part = ops.gemm_nt(feats.to(DEV), feats.to(DEV), ops.GEMM_POLY_SUM, scale=1 / 128, coef=1.0, degree=3,
+                       idx_x=ix.to(DEV), idx_y=iy.to(DEV)).cpu()
+    fx, fy = feats.double()[ix.long()], feats.double()[iy.long()]
+    torch.testing.assert_close(part.sum(-1), ((fx @ fy.transpose(1, 2) / 128 + 1) ** 3).sum((1, 2)), rtol=1e-5,
+                               atol=1e-2)
+
+
+@pytest.mark.parametrize("dtype", DT)
+def test_pairwise_functionals_16bit(dtype):
+    x, y = _xy(700, 500, 96, dtype, 4)
+    lin = tm.functional.pairwise_linear_similarity(x.to(DEV), y.to(DEV))
+    assert lin.dtype == dtype
+    torch.testing.assert_close(lin.cpu().float(), (x.float() @ y.float().T).to(dtype).float(), rtol=1e-2, atol=1e-2)
+    cos = tm.functional.pairwise_cosine_similarity(x.to(DEV), zero_diagonal=False)
+    assert cos.dtype == dtype
+    xn = x.double() / x.double().norm(dim=1, keepdim=True)
+    torch.testing.assert_close(cos.cpu().double(), xn @ xn.T, rtol=1e-2, atol=1e-2)
+    cz = tm.functional.pairwise_cosine_similarity(x.to(DEV))  # y defaults to x, zero diagonal
+    assert torch.count_nonzero(torch.diagonal(cz)) == 0
+
+
+def test_h16_no_upcast_kernel():
+    """bf16 operands reach the 16-bit kernel directly: no fp32 copy of the operands is made."""
+    x, y = _xy(4096, 4096, 512, torch.bfloat16)
+    xd, yd = x.to(DEV), y.to(DEV)
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats()
+    before = torch.cuda.memory_allocated()
+    out = ops.gemm_nt(xd, yd, ops.GEMM_STORE, out_dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    peak_extra = torch.cuda.max_memory_allocated() - before
+    assert out.dtype == torch.bfloat16
+    assert peak_extra <= out.numel() * 2 + (1 << 20)  # only the bf16 output (an fp32 copy of x would be 8 MB)

@@ -66,7 +66,8 @@ def _zero_diag(d: Tensor, zero_diagonal: bool) -> Tensor:
 
 
 def _mfma_ok(x: Tensor) -> bool:
-    """ROCm, non-fp64 operands with 4-aligned rows: the fp32 matrix-core GEMM path (``ops.gemm_nt``)."""
+    """ROCm, non-fp64 operands with 16-byte rows: the matrix-core GEMM path (``ops.gemm_nt``: fp32 MFMA, or the 16-bit
+    MFMA for bf16 / fp16 operands)."""
     return x.is_cuda and x.dtype != torch.float64 and x.shape[-1] % 4 == 0 and x.shape[-1] > 0
 
 
@@ -78,7 +79,9 @@ _VENDOR_GEMM_MACS = 1 << 30
 
 
 def _vendor_gemm(x: Tensor, y: Tensor) -> bool:
-    return x.is_cuda and x.shape[0] * y.shape[0] * x.shape[1] >= _VENDOR_GEMM_MACS
+    """fp32 store GEMMs past the launch-overhead regime.  bf16 / fp16 operands always run our 16-bit MFMA kernel."""
+    return (x.is_cuda and x.dtype == torch.float32 and y.dtype == torch.float32
+            and x.shape[0] * y.shape[0] * x.shape[1] >= _VENDOR_GEMM_MACS)
 
 
 def _euclid_ok(x: Tensor) -> bool:
@@ -152,7 +155,7 @@ def _pairwise_linear_similarity_update(x: Tensor, y: Optional[Tensor] = None,
                                        zero_diagonal: Optional[bool] = None) -> Tensor:
     x, y, zd = _check_input(x, y, zero_diagonal)
     if _mfma_ok(x) and not _vendor_gemm(x, y):
-        return ops.gemm_nt(x, y, ops.GEMM_STORE, zero_diagonal=zd).to(x.dtype)
+        return ops.gemm_nt(x, y, ops.GEMM_STORE, zero_diagonal=zd, out_dtype=x.dtype)
     return _zero_diag(_safe_matmul(x, y), zd)
 
 
@@ -167,9 +170,10 @@ def _pairwise_cosine_similarity_update(x: Tensor, y: Optional[Tensor] = None,
                                        zero_diagonal: Optional[bool] = None) -> Tensor:
     x, y, zd = _check_input(x, y, zero_diagonal)
     if _mfma_ok(x) and not _vendor_gemm(x, y):
-        ix = 1.0 / torch.linalg.vector_norm(x.float(), 2, dim=1)
-        iy = ix if y is x else 1.0 / torch.linalg.vector_norm(y.float(), 2, dim=1)
-        return ops.gemm_nt(x, y, ops.GEMM_COSINE, ix, iy, zero_diagonal=zd).to(x.dtype)
+        # fp32 norms read straight from the operand (dtype= accumulates in fp32: no upcast copy)
+        ix = 1.0 / torch.linalg.vector_norm(x, 2, dim=1, dtype=torch.float32)
+        iy = ix if y is x else 1.0 / torch.linalg.vector_norm(y, 2, dim=1, dtype=torch.float32)
+        return ops.gemm_nt(x, y, ops.GEMM_COSINE, ix, iy, zero_diagonal=zd, out_dtype=x.dtype)
     xn = x / torch.linalg.vector_norm(x, 2, dim=1, keepdim=True)
     yn = xn if y is x else y / torch.linalg.vector_norm(y, 2, dim=1, keepdim=True)
     return _zero_diag(_safe_matmul(xn, yn), zd)

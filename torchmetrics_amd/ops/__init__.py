@@ -52,6 +52,10 @@ def _load_fastcall() -> None:
         mod = importlib.util.module_from_spec(spec)
         spec.loader.exec_module(mod)
         _fast_mod = mod
+        from torchmetrics_amd.utils import profiling
+
+        if profiling.ENABLED:
+            mod.set_ranges(True)
     except Exception as err:  # noqa: BLE001 - the dispatcher path is the same native code, just slower to enter
         _state["fast_error"] = err
         _fast_mod = _DispatcherShim()
@@ -67,15 +71,23 @@ def native_updater(kind: str, state: dict, fallback: Any, *extra: Any) -> Any:
     """A native ``update`` callable bound to a metric's ``__dict__`` (``csrc/bindings/fastcall.cpp``), or ``None``
     where it does not apply (no GPU, native library missing, ``TORCHMETRICS_AMD_STRICT=1``).  Inputs off its fast path
     go to ``fallback`` (the metric's Python update)."""
-    from torchmetrics_amd.utils import profiling, validation
+    from torchmetrics_amd.utils import validation
 
-    if validation.STRICT or profiling.ENABLED or not torch.cuda.is_available() or not load_native(strict=False):
+    if validation.STRICT or not torch.cuda.is_available() or not load_native(strict=False):
         return None
     mod = _fast_mod
     factory = getattr(mod, f"{kind}_updater", None) if not isinstance(mod, _DispatcherShim) else None
     if factory is None:
         return None
-    return factory(*extra, state, fallback) if extra else factory(state, fallback)
+    fn = factory(*extra, state, fallback) if extra else factory(state, fallback)
+    fn.range_name = f"tm.update/{_owner_name(fallback)}"  # roctx range of the native call (utils/profiling.py)
+    return fn
+
+
+def _owner_name(fallback: Any) -> str:
+    """Class name of the metric a bound ``update`` / ``forward`` (or its ``functools.wraps`` wrapper) belongs to."""
+    owner = getattr(getattr(fallback, "__wrapped__", fallback), "__self__", None)
+    return type(owner).__name__ if owner is not None else "Metric"
 
 
 FWD_CONFMAT, FWD_MULTICLASS, FWD_BINARY, FWD_MULTILABEL = 0, 1, 2, 3
@@ -86,14 +98,18 @@ def native_forward(kind: int, state: dict, fallback: Any, stat_kind: str = "accu
     """A native ``forward`` callable bound to a metric's ``__dict__`` (``csrc/bindings/fastcall.cpp`` ``NativeForward``)
     or ``None`` where it does not apply (no GPU, native library missing, ``TORCHMETRICS_AMD_STRICT=1``,
     ``TORCHMETRICS_AMD_NATIVE_FORWARD=0``).  Calls off its fast path go to ``fallback`` (``Metric.forward``)."""
-    from torchmetrics_amd.utils import profiling, validation
+    from torchmetrics_amd.utils import validation
 
-    if (validation.STRICT or profiling.ENABLED or os.environ.get("TORCHMETRICS_AMD_NATIVE_FORWARD", "1") == "0"
+    if (validation.STRICT or os.environ.get("TORCHMETRICS_AMD_NATIVE_FORWARD", "1") == "0"
             or not torch.cuda.is_available() or not load_native(strict=False)):
         return None
     mod = _fast_mod
     factory = getattr(mod, "forward_native", None) if not isinstance(mod, _DispatcherShim) else None
-    return factory(kind, state, fallback, STAT_KINDS[stat_kind]) if factory is not None else None
+    if factory is None:
+        return None
+    fn = factory(kind, state, fallback, STAT_KINDS[stat_kind])
+    fn.range_name = f"tm.forward/{_owner_name(fallback)}"
+    return fn
 
 
 def native_library_path() -> Path:
@@ -1331,29 +1347,43 @@ GEMM_STORE, GEMM_EUCLID, GEMM_COSINE, GEMM_POLY_SUM, GEMM_ROW_MIN, GEMM_ROW_SUM,
 
 def gemm_nt(x: Tensor, y: Tensor, kind: int, aux_x: Optional[Tensor] = None, aux_y: Optional[Tensor] = None,
             scale: float = 1.0, coef: float = 0.0, degree: int = 1, zero_diagonal: bool = False,
-            sqrt_out: bool = True, idx_x: Optional[Tensor] = None, idx_y: Optional[Tensor] = None) -> Tensor:
-    """``X @ Y^T`` (fp32, ``[N, D] x [M, D]`` or batched ``[B, N, D] x [B, M, D]``) with a fused epilogue
-    (``csrc/pairwise/gemm_nt.hip``: v_mfma_f32_32x32x2f32, 128 x 128 block tiles).
+            sqrt_out: bool = True, idx_x: Optional[Tensor] = None, idx_y: Optional[Tensor] = None,
+            out_dtype: Optional[torch.dtype] = None) -> Tensor:
+    """``X @ Y^T`` (``[N, D] x [M, D]`` or batched ``[B, N, D] x [B, M, D]``) with a fused epilogue
+    (``csrc/pairwise/gemm_nt.hip``).  fp32 operands run v_mfma_f32_32x32x2f32; bf16 / fp16 operands run the 16-bit
+    matrix cores (v_mfma_f32_32x32x16_{bf16,f16}, fp32 accumulate) straight from the 16-bit tensors -- no upcast copy.
 
     ``kind``: ``GEMM_STORE`` (scale * dot), ``GEMM_EUCLID`` (aux = squared row norms; sqrt(|x|^2 + |y|^2 - 2 x.y),
     exact recompute under cancellation), ``GEMM_COSINE`` (aux = inverse norms), ``GEMM_POLY_SUM`` (fp64 partial sums of
     ``(scale * dot + coef) ** degree`` per block, diagonal skipped with ``zero_diagonal``), ``GEMM_ROW_MIN``
-    (``min_j 1 - |cos|`` partials ``[.., N, ceil(M / 128)]``), ``GEMM_ROW_SUM`` (row-sum partials of ``scale * dot``).
+    (``min_j 1 - |cos|`` partials ``[.., N, tiles]``), ``GEMM_ROW_SUM`` (row-sum partials of ``scale * dot``).
     ``idx_x`` / ``idx_y`` (int32 ``[B, rows]``): batch ``b`` multiplies the gathered rows ``x[idx_x[b]]`` and
     ``y[idx_y[b]]`` without materialising them (the caller guarantees the indices are in range).
+    ``out_dtype``: the STORE / EUCLID / COSINE matrix's dtype: fp32 (default) or the operands' 16-bit dtype, rounded
+    in the epilogue (no separate cast pass).
     """
     if x.is_cuda:
-        x = x.float().contiguous()
-        y = y.float().contiguous()
+        h16 = (x.dtype in (torch.bfloat16, torch.float16) and y.dtype == x.dtype and x.shape[-1] % 8 == 0
+               and x.shape[-1] > 0)
+        if h16:
+            x, y = x.contiguous(), y.contiguous()
+            if x.data_ptr() % 16 or y.data_ptr() % 16:
+                h16 = False
+        if not h16:
+            x = x.float().contiguous()
+            y = y.float().contiguous()
+        out16 = 1 if (h16 and out_dtype == x.dtype and kind in (GEMM_STORE, GEMM_EUCLID, GEMM_COSINE)) else 0
         ax = None if aux_x is None else aux_x.float().contiguous()
         ay = None if aux_y is None else aux_y.float().contiguous()
         ix = None if idx_x is None else idx_x.to(torch.int32).contiguous()
         iy = None if idx_y is None else idx_y.to(torch.int32).contiguous()
-        return _ops().gemm_nt(x, y, int(kind), ax, ay, float(scale), float(coef), int(degree), bool(zero_diagonal),
-                              bool(sqrt_out), ix, iy)
+        out = _ops().gemm_nt(x, y, int(kind), ax, ay, float(scale), float(coef), int(degree), bool(zero_diagonal),
+                             bool(sqrt_out), ix, iy, out16)
+        return out if out_dtype is None or out.dtype == out_dtype else out.to(out_dtype)
     if idx_x is not None:
         x, y = x[idx_x.long()], y[idx_y.long()]
-    return _cpu.gemm_nt(x, y, kind, aux_x, aux_y, scale, coef, degree, zero_diagonal, sqrt_out)
+    out = _cpu.gemm_nt(x, y, kind, aux_x, aux_y, scale, coef, degree, zero_diagonal, sqrt_out)
+    return out if out_dtype is None or kind not in (GEMM_STORE, GEMM_EUCLID, GEMM_COSINE) else out.to(out_dtype)
 
 
 def bert_rowcol_max(x: Tensor, y: Tensor) -> "tuple[Tensor, Tensor]":

@@ -8,8 +8,9 @@ or :func:`enable` at run time, turns on ranges named
 * ``tm.sync/<n> states`` around one engine sync and ``tm.sync.bucket/<reduction>/<dtype>/<bytes>B`` around each of its
   collectives (``parallel/sync.py``).
 
-While ranges are on, metrics use their Python ``update`` / ``forward`` (the native C++ entry points of
-``csrc/bindings/fastcall.cpp`` bypass the Python wrappers that open the ranges).
+The native C++ entry points (``csrc/bindings/fastcall.cpp`` ``NativeUpdate`` / ``NativeForward``) open the same
+``tm.update/<Metric>`` / ``tm.forward/<Metric>`` ranges themselves, so a traced run is the production run: the fast
+path stays on and its kernel launches show up inside the ranges.
 
 Ranges go to the rocprofiler-sdk roctx library that rocprofv3 intercepts (``librocprofiler-sdk-roctx.so``); if it is
 not present, to torch's roctx binding (``torch.cuda.nvtx`` is roctx on ROCm).  Every range is also a
@@ -59,6 +60,11 @@ def enable(on: bool = True) -> None:
     ENABLED = bool(on)
     if ENABLED:
         _bind()
+    from torchmetrics_amd import ops
+
+    mod = ops._fast_mod
+    if mod is not None and hasattr(mod, "set_ranges"):
+        mod.set_ranges(ENABLED)  # the native entry points' ranges
 
 
 def push(name: str) -> None:

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <string>
 #include <tuple>
 #include <type_traits>
 #include <utility>
@@ -42,6 +43,7 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
 void stat_reduce(const at::Tensor& tp, const at::Tensor& fp, const at::Tensor& tn, const at::Tensor& fn,
                  at::Tensor out, int64_t kind, int64_t average, bool multilabel, double beta);
 void launch_probe(at::Tensor flag);
+int64_t read_word_sync(const at::Tensor& word);
 void zero_async(at::Tensor t);
 bool mc_confmat_dual(const at::Tensor& preds, const at::Tensor& target, at::Tensor batch, at::Tensor global,
                      at::Tensor flag, int64_t num_classes, int64_t ignore_index, bool has_ignore);
@@ -1152,7 +1154,35 @@ PyObject* map_pack(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   return result;
 }
 
+// read_word(word: Tensor) -> int: an int32 device word through mapped host memory + a stream sync
+// (compute_tasks.hip read_word_sync), the GIL released while the stream drains
+PyObject* read_word(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 1 || !THPVariable_Check(args[0])) {
+    PyErr_SetString(PyExc_TypeError, "read_word(word: Tensor)");
+    return nullptr;
+  }
+  const at::Tensor w = THPVariable_Unpack(args[0]);
+  int64_t v = 0;
+  std::string err;
+  Py_BEGIN_ALLOW_THREADS
+  try {
+    v = tm_amd::read_word_sync(w);
+  } catch (const c10::Error& e) {
+    err = e.what_without_backtrace();
+  } catch (const std::exception& e) {
+    err = e.what();
+  }
+  Py_END_ALLOW_THREADS
+  if (!err.empty()) {
+    PyErr_SetString(PyExc_RuntimeError, err.c_str());
+    return nullptr;
+  }
+  return PyLong_FromLongLong(v);
+}
+
 PyMethodDef kFactoryMethods[] = {
+    {"read_word", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&read_word)), METH_FASTCALL,
+     "an int32 device word read through mapped host memory after a stream sync"},
     {"stats_updater", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&make_stats_updater)),
      METH_FASTCALL, "native update of the stat-score family bound to a metric's __dict__"},
     {"forward_native", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&make_forward)), METH_FASTCALL,

@@ -8,6 +8,8 @@
 // Descriptors travel by value in the kernel arguments (no device table to keep alive; capturable into a HIP graph).
 #include "common/compute_bodies.h"
 
+#include <mutex>
+
 namespace tm_amd {
 namespace {
 
@@ -119,7 +121,45 @@ __global__ void __launch_bounds__(kMaxWords) gather_words_kernel(WordTable tab, 
   __threadfence_system();
 }
 
+// one word of device memory copied into mapped host memory (vector store by lane 0) -- read_word_sync
+__global__ void __launch_bounds__(64) publish_word_kernel(const int* __restrict__ src, int* __restrict__ dst) {
+  if (threadIdx.x == 0) dst[0] = src[0];
+  __threadfence_system();
+}
+
 }  // namespace
+
+// The value of an int32 device word, read without a device->host copy: one 1-thread kernel stores it into mapped
+// (fine-grained, coherent) pinned host memory, the CURRENT STREAM is synchronised, the host reads the word.  Against
+// `.item()` (a blit + wait) this leaves the stream known-idle to the runtime, so a following
+// hipDeviceSynchronize / torch.cuda.synchronize() returns at once instead of issuing its own marker round trip
+// (profiles/r05_region_tail.jsonl: 0.2 us vs 14 us after the read).  The caller (metric.py _raise_device_errors)
+// releases nothing it holds; the GIL is released by the fastcall wrapper around this call.
+int64_t read_word_sync(const at::Tensor& word) {
+  TM_CHECK_CUDA(word);
+  TORCH_CHECK(word.scalar_type() == at::kInt && word.numel() >= 1, "read_word_sync: an int32 word");
+  const int dev = word.get_device();
+  TORCH_CHECK(dev >= 0 && dev < 64, "read_word_sync: device index");
+  static std::mutex mu;
+  static int* host[64] = {};
+  static int* mapped[64] = {};
+  std::lock_guard<std::mutex> lock(mu);  // one slot per device: serialise readers of one device
+  const c10::DeviceGuard guard(word.device());
+  if (host[dev] == nullptr) {
+    int* h = nullptr;
+    TORCH_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h), 64, hipHostMallocMapped | hipHostMallocCoherent) ==
+                    hipSuccess, "read_word_sync: pinned allocation failed");
+    void* d = nullptr;
+    TORCH_CHECK(hipHostGetDevicePointer(&d, h, 0) == hipSuccess, "read_word_sync: unmapped pinned memory");
+    host[dev] = h;
+    mapped[dev] = static_cast<int*>(d);
+  }
+  hipStream_t s = stream();
+  hipLaunchKernelGGL(publish_word_kernel, dim3(1), dim3(64), 0, s, word.data_ptr<int>(), mapped[dev]);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  TORCH_CHECK(hipStreamSynchronize(s) == hipSuccess, "read_word_sync: stream synchronisation failed");
+  return static_cast<int64_t>(*static_cast<volatile int*>(host[dev]));
+}
 
 // words: CPU int64 [n, 2] rows (device pointer, code: 0 i32 raw / 1 f32 / 2 f64 / 3 i64 / 4 u8|bool as 0-1);
 // dst: device-side address of a pinned int32 [>= n] buffer (mapped_device_ptr); anchor: a tensor on the device.
@@ -192,10 +232,12 @@ TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
   m.def("compute_tasks_max() -> int", &compute_tasks_max);
   m.def("gather_words(Tensor words, int dst, Tensor anchor) -> ()");
   m.def("mapped_device_ptr(Tensor pinned) -> int", &mapped_device_ptr);
+  m.def("read_word_sync(Tensor word) -> int");
 }
 TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
   m.impl("compute_tasks", &compute_tasks);
   m.impl("gather_words", &gather_words);
+  m.impl("read_word_sync", &read_word_sync);
 }
 
 }  // namespace tm_amd

@@ -180,3 +180,19 @@ def test_native_update_stays_on_with_roctx_ranges():
         assert f.forward.native_calls > 0
     finally:
         profiling.enable(False)
+
+
+@pytest.mark.gpu
+def test_read_word_matches_item_and_leaves_stream_idle():
+    """ops.read_word (mapped host memory + stream sync) returns the word's value and raises nothing on a clean word;
+    compute() still raises a deferred target-range error through it."""
+    w = torch.tensor([0x25], dtype=torch.int32, device="cuda")
+    assert ops.read_word(w) == 0x25
+    w.zero_()
+    assert ops.read_word(w) == 0
+    m = tm.MulticlassConfusionMatrix(num_classes=5).to("cuda")
+    p = torch.randn(16, 5, device="cuda")
+    m.update(p, torch.randint(0, 5, (16,), device="cuda"))
+    m.update(p, torch.full((16,), 7, device="cuda"))  # out of range: the kernel flags it
+    with pytest.raises(RuntimeError):
+        m.compute()

@@ -26,6 +26,7 @@ import torch
 from torch import Tensor
 from torch.nn import Module, Parameter
 
+from torchmetrics_amd import ops as _ops
 from torchmetrics_amd.parallel import arena as _arena
 from torchmetrics_amd.parallel.sync import distributed_available as _engine_dist_available
 from torchmetrics_amd.parallel.sync import sync_state_dicts
@@ -584,7 +585,7 @@ class Metric(Module, ABC):
         self.__dict__.pop("_sync_word_pending", None)
         if buf is None:
             return
-        code = int(buf.item())
+        code = _ops.read_word(buf)
         if code & _validation.NARROW_RETRY and not only:
             code = self._narrow_resync(buf, code)
         if only:

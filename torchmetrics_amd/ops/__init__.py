@@ -112,6 +112,17 @@ def native_forward(kind: int, state: dict, fallback: Any, stat_kind: str = "accu
     return fn
 
 
+def read_word(word: Tensor) -> int:
+    """The int32 word ``word[0]``: on ROCm through mapped host memory + a stream sync (``read_word_sync``: the stream is
+    then known idle, so the caller's next ``torch.cuda.synchronize()`` costs nothing), else ``.item()``."""
+    if word.is_cuda and word.dtype == torch.int32:
+        mod = _fast_mod if _fast_mod is not None else (_fast() if native_available() else None)
+        fn = getattr(mod, "read_word", None) if mod is not None else None
+        if fn is not None:
+            return fn(word)
+    return int(word.reshape(-1)[0].item())
+
+
 def native_library_path() -> Path:
     return _LIB_PATH
 

@@ -31,6 +31,7 @@ On ROCm, ``torch.distributed`` backend ``"nccl"`` *is* RCCL.  Bucket sizes are s
 (< 64 KiB: latency-bound, a single ring step over xGMI) and large only for FID (``f64[2048,2048]`` = 32 MiB, per-link
 bandwidth-bound): one collective per bucket is the right shape for both.
 """
+import math
 from contextlib import nullcontext
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple, Union
 
@@ -364,20 +365,25 @@ def _gather_items(items: List[_GatherItem], world: int, group: Optional[Any]) ->
     else:
         all_meta = [h[2 * n_it + 1 :] for h in hdr]
 
-    # decode every rank's shapes
+    # decode every rank's shapes (host ints only) and each element's size
     shapes: List[List[List[Tuple[int, ...]]]] = []  # [rank][item][elem] -> shape
+    sizes: List[List[List[int]]] = []  # [rank][item][elem] -> numel
     for r in range(world):
         row = all_meta[r]
         pos = 0
-        per_item = []
+        per_item, per_size = [], []
         for i in range(n_it):
-            el_shapes = []
+            el_shapes, el_sizes = [], []
             for _ in range(hdr[r][i]):
                 nd = row[pos]
-                el_shapes.append(tuple(row[pos + 1 : pos + 1 + nd]))
+                shp = tuple(row[pos + 1 : pos + 1 + nd])
+                el_shapes.append(shp)
+                el_sizes.append(math.prod(shp))
                 pos += 1 + nd
             per_item.append(el_shapes)
+            per_size.append(el_sizes)
         shapes.append(per_item)
+        sizes.append(per_size)
 
     # element dtype per item: the first rank that holds an element decides (a locally-empty list has no dtype),
     # so every rank builds the same dtype buckets and issues the same collective sequence
@@ -391,14 +397,9 @@ def _gather_items(items: List[_GatherItem], world: int, group: Optional[Any]) ->
         by_dtype.setdefault(dt, []).append(i)
     for dt, idxs in by_dtype.items():
         wire = _WIRE_DTYPE.get(dt, dt)
-        # per-rank payload length for this dtype bucket
-        lens = []
-        for r in range(world):
-            tot = 0
-            for i in idxs:
-                for shp in shapes[r][i]:
-                    tot += int(torch.Size(shp).numel())
-            lens.append(tot)
+        # per-rank element sizes of this dtype bucket, in payload order
+        flat_sizes = [[n for i in idxs for n in sizes[r][i]] for r in range(world)]
+        lens = [sum(fs) for fs in flat_sizes]
         max_len = max(lens)
         if max_len == 0:
             continue
@@ -409,14 +410,18 @@ def _gather_items(items: List[_GatherItem], world: int, group: Optional[Any]) ->
             local = torch.cat([local, local.new_zeros(max_len - local.numel())])
         allbuf = _all_gather_flat(local, world, group)
         target_dev = items[idxs[0]].elems[0].device if items[idxs[0]].elems else dev
+        # ONE dtype conversion / device move of the whole bucket, then ONE split per rank (views, no copies)
+        allbuf = allbuf.to(dtype=dt, device=target_dev)
         for r in range(world):
-            pos = 0
-            row = allbuf[r]
+            if not flat_sizes[r]:
+                continue
+            parts = torch.split(allbuf[r, : lens[r]], flat_sizes[r])
+            k = 0
             for i in idxs:
+                dst = out[i][r]
                 for shp in shapes[r][i]:
-                    n = int(torch.Size(shp).numel())
-                    out[i][r].append(row[pos : pos + n].view(shp).to(dtype=dt, device=target_dev))
-                    pos += n
+                    dst.append(parts[k].view(shp))
+                    k += 1
     return out
 
 

@@ -99,9 +99,15 @@ def _timed(metric, preds, target, steps: int, warmup: int, device, world):
     t0 = time.perf_counter()
     for i in range(steps):
         metric.update(preds[(warmup + i) % nbuf], target[(warmup + i) % nbuf])
+    t1 = time.perf_counter()
     result = metric.compute()
+    t2 = time.perf_counter()
     _barrier_sync(device, world)
-    elapsed = time.perf_counter() - t0
+    t3 = time.perf_counter()
+    elapsed = t3 - t0
+    # host-side phases of the timed region: issuing the K updates, compute() (sync + validation read: it waits for the
+    # device to drain), the closing barrier + synchronize
+    phases = {"update_issue_ms": (t1 - t0) * 1e3, "compute_ms": (t2 - t1) * 1e3, "closing_sync_ms": (t3 - t2) * 1e3}
     # separate measurement of the synced compute wall-clock
     _barrier_sync(device, world)
     c0 = time.perf_counter()
@@ -112,7 +118,7 @@ def _timed(metric, preds, target, steps: int, warmup: int, device, world):
         result = metric.compute()
     _barrier_sync(device, world)
     compute_ms = (time.perf_counter() - c0) / reps * 1e3
-    return elapsed, compute_ms, result
+    return elapsed, compute_ms, result, phases
 
 
 def _reset(metric) -> None:
@@ -146,16 +152,17 @@ def main() -> None:
 
         ref = ReferenceEmulatedConfusionMatrix(NUM_CLASSES, device)
     _warm(ours, preds, target, args.warmup)
-    t_ours, cms_ours, res_ours = _timed(ours, preds, target, args.steps, args.warmup, device, world)
+    t_ours, cms_ours, res_ours, phases = _timed(ours, preds, target, args.steps, args.warmup, device, world)
     comms = comm_stats()
     t_ours = _max_over_ranks(t_ours, device, world)
     cms_ours = _max_over_ranks(cms_ours, device, world)
+    phases = {k: round(_max_over_ranks(v, device, world), 4) for k, v in phases.items()}  # slowest rank per phase
 
     base_val = None
     t_ref = cms_ref = None
     if ref is not None:
         _warm(ref, preds, target, args.warmup)
-        t_ref, cms_ref, res_ref = _timed(ref, preds, target, args.steps, args.warmup, device, world)
+        t_ref, cms_ref, res_ref, _ = _timed(ref, preds, target, args.steps, args.warmup, device, world)
         t_ref = _max_over_ranks(t_ref, device, world)
         cms_ref = _max_over_ranks(cms_ref, device, world)
         if not torch.equal(res_ref.to(res_ours.device), res_ours):
@@ -184,6 +191,7 @@ def main() -> None:
                 "parallelism": f"dp{world}",
             },
             "compute_ms": round(cms_ours, 4),
+            "phases_ms_max_over_ranks": phases,
             "input_ring_mb": round(len(preds) * BATCH * NUM_CLASSES * 2 / 2**20, 1),
             "dist": {
                 "world_size_seen": dist.get_world_size() if world > 1 else 1,

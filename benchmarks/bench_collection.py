@@ -111,12 +111,23 @@ def main() -> None:
         both = GraphedCompute(cls, reg)  # one graph, one replay and one status read for both collections
         comp_cls, comp_reg = both, (lambda: {})
 
+    phase = [0.0, 0.0, 0.0, 0.0]  # host seconds in: update cls, update reg, compute cls (incl. sync), compute reg
+    clock = time.perf_counter
+
     def step(i):
+        t0 = clock()
         upd_cls(logits[i % NBUF], labels[i % NBUF])
+        t1 = clock()
         upd_reg(xs[i % NBUF], ys[i % NBUF])
+        t2 = clock()
+        phase[0] += t1 - t0
+        phase[1] += t2 - t1
         if args.sync_every_step:
             comp_cls()
+            t3 = clock()
             comp_reg()
+            phase[2] += t3 - t2
+            phase[3] += clock() - t3
 
     def sync():
         if world > 1:
@@ -134,6 +145,7 @@ def main() -> None:
     else:
         cls.reset(), reg.reset()
     sync()
+    phase[:] = [0.0, 0.0, 0.0, 0.0]
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
@@ -145,6 +157,11 @@ def main() -> None:
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    ph = torch.tensor(phase, dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(ph, op=dist.ReduceOp.MAX)
+    phases = {k: round(float(v) / args.steps * 1e3, 4) for k, v in
+              zip(("update_cls", "update_reg", "compute_cls_incl_sync", "compute_reg_incl_sync"), ph.tolist())}
 
     # ---- emulated reference collection on the same data (benchmarks/reference_path.py ReferenceEmulatedCollection)
     base = None
@@ -187,6 +204,7 @@ def main() -> None:
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "sync_every_step": args.sync_every_step, "compute_groups": True, "hip_graph": args.graph, "dtype": "bf16", "data": "synthetic",
             "groups": len(cls.compute_groups), "acc": float(out["acc"]), "r2": float(out["r2"]),
+            "phases_ms_per_step_max_over_ranks": phases,
             "dist": dist_info(world),
         }), flush=True)
     if world > 1:

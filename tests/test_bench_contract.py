@@ -100,3 +100,25 @@ def test_bench_collection_two_rank_gloo(tmp_path):
     out = _torchrun_json(tmp_path, "bench_collection.py", "--steps", "3", "--warmup", "1", "--sync-every-step")
     assert out["n_gpus"] == 2 and out["vs_baseline"] is not None and out["baseline"]["value"] > 0
     assert out["dist"]["world_size_seen"] == 2 and out["dist"]["engine_collectives"]["all_reduce"] >= 1
+
+
+@pytest.mark.timeout(900)
+def test_bench_eight_rank_gloo_rehearsal(tmp_path):
+    """8 gloo ranks on the CPU (the driver's N=8 shape, rehearsed without GPUs): bench.py and the config #5 collection
+    bench both see world size 8 and report their per-phase split (slowest rank)."""
+    res = _self_launch(tmp_path, "bench.py", "--gpus", "8", "--steps", "2", "--warmup", "1", "--ring-mb", "8",
+                       "--no-baseline")
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["dist"]["world_size_seen"] == 8 and out["config"]["parallelism"] == "dp8"
+    assert out["config"]["global_batch"] == 8 * 8192 and out["dist"]["engine_collectives"]["all_reduce"] >= 1
+    assert set(out["phases_ms_max_over_ranks"]) == {"update_issue_ms", "compute_ms", "closing_sync_ms"}
+    coll = _self_launch(tmp_path, os.path.join("benchmarks", "bench_collection.py"), "--gpus", "8", "--steps", "2",
+                        "--warmup", "1", "--sync-every-step", "--no-baseline")
+    assert coll.returncode == 0, coll.stderr[-3000:]
+    c = json.loads([ln for ln in coll.stdout.splitlines() if ln.startswith("{")][0])
+    assert c["n_gpus"] == 8 and c["dist"]["world_size_seen"] == 8
+    assert set(c["phases_ms_per_step_max_over_ranks"]) == {"update_cls", "update_reg", "compute_cls_incl_sync",
+                                                           "compute_reg_incl_sync"}

@@ -329,8 +329,9 @@ def _sync_state_dicts(
     return results
 
 
-def _gather_items(items: List[_GatherItem], world: int, group: Optional[Any]) -> List[List[List[Tensor]]]:
-    """Returns, per item, per rank, the list of element tensors that rank holds."""
+def _gather_items(items: List[_GatherItem], world: int, group: Optional[Any]) -> List[Any]:
+    """Returns, per item, per rank, the list of element tensors that rank holds -- or, for a single-tensor item whose
+    shape every rank shares, the ``[W, *shape]`` stack directly (a view of the gathered bucket)."""
     if world == 1:
         return [[it.elems] for it in items]
     dev = _comm_device(items, group)
@@ -392,14 +393,13 @@ def _gather_items(items: List[_GatherItem], world: int, group: Optional[Any]) ->
         dtypes.append(_DTYPE_CODES[code] if code >= 0 else torch.float32)
 
     out: List[List[List[Tensor]]] = [[[] for _ in range(world)] for _ in items]
+    stacked: List[Optional[Tensor]] = [None] * n_it  # [W, *shape] views of single-tensor items (uniform buckets)
     by_dtype: Dict[torch.dtype, List[int]] = {}
     for i, dt in enumerate(dtypes):
         by_dtype.setdefault(dt, []).append(i)
     for dt, idxs in by_dtype.items():
         wire = _WIRE_DTYPE.get(dt, dt)
-        # per-rank element sizes of this dtype bucket, in payload order
-        flat_sizes = [[n for i in idxs for n in sizes[r][i]] for r in range(world)]
-        lens = [sum(fs) for fs in flat_sizes]
+        lens = [sum(n for i in idxs for n in sizes[r][i]) for r in range(world)]
         max_len = max(lens)
         if max_len == 0:
             continue
@@ -410,19 +410,39 @@ def _gather_items(items: List[_GatherItem], world: int, group: Optional[Any]) ->
             local = torch.cat([local, local.new_zeros(max_len - local.numel())])
         allbuf = _all_gather_flat(local, world, group)
         target_dev = items[idxs[0]].elems[0].device if items[idxs[0]].elems else dev
-        # ONE dtype conversion / device move of the whole bucket, then ONE split per rank (views, no copies)
+        # ONE dtype conversion / device move of the whole bucket
         allbuf = allbuf.to(dtype=dt, device=target_dev)
+        # per rank, where each item's elements start in that rank's row
+        starts = []
         for r in range(world):
-            if not flat_sizes[r]:
-                continue
-            parts = torch.split(allbuf[r, : lens[r]], flat_sizes[r])
-            k = 0
+            pos, st = 0, {}
             for i in idxs:
-                dst = out[i][r]
-                for shp in shapes[r][i]:
-                    dst.append(parts[k].view(shp))
-                    k += 1
-    return out
+                st[i] = pos
+                pos += sum(sizes[r][i])
+            starts.append(st)
+        for i in idxs:
+            off = starts[0][i]
+            if all(shapes[r][i] == shapes[0][i] and starts[r][i] == off for r in range(1, world)):
+                # every rank holds this item's elements with the same shapes at the same columns: a single-tensor
+                # item is ONE [W, *shape] view of the bucket (no per-rank slicing, no stack), list elements are
+                # column slices
+                if not items[i].is_list and len(shapes[0][i]) == 1:
+                    stacked[i] = allbuf[:, off : off + sizes[0][i][0]].reshape((world,) + tuple(shapes[0][i][0]))
+                    continue
+                for shp, n in zip(shapes[0][i], sizes[0][i]):
+                    col = allbuf[:, off : off + n]
+                    for r in range(world):
+                        out[i][r].append(col[r].view(shp))
+                    off += n
+                continue
+            # ragged item: ONE split of each rank's span (views, no copies)
+            for r in range(world):
+                if not sizes[r][i]:
+                    continue
+                span = allbuf[r, starts[r][i] : starts[r][i] + sum(sizes[r][i])]
+                for part, shp in zip(torch.split(span, sizes[r][i]), shapes[r][i]):
+                    out[i][r].append(part.view(shp))
+    return [st if st is not None else per_rank for st, per_rank in zip(stacked, out)]
 
 
 def _comm_device(items: List[_GatherItem], group: Optional[Any]) -> torch.device:
@@ -431,10 +451,10 @@ def _comm_device(items: List[_GatherItem], group: Optional[Any]) -> torch.device
     return torch.device("cpu")
 
 
-def _finish_gather(item: _GatherItem, per_rank: List[List[Tensor]]) -> State:
+def _finish_gather(item: _GatherItem, per_rank: Any) -> State:
     fn = item.fn
     if not item.is_list:
-        stacked = torch.stack([r[0] for r in per_rank])
+        stacked = per_rank if isinstance(per_rank, Tensor) else torch.stack([r[0] for r in per_rank])
         if fn is None:
             return stacked
         if fn is dim_zero_cat:

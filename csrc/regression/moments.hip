@@ -1,4 +1,4 @@
-// Streaming regression moments: one pass over (preds, target) computing any subset of ~14 per-output sums
+// Streaming regression moments: one pass over (preds, target) computing any subset of 19 per-output sums
 // (SSE, SAE, Σp, Σt, Σp², Σt², Σpt, MAPE/SMAPE/WMAPE terms, MSLE, log-cosh, Minkowski, count), accumulated in fp64.
 //
 // This one kernel backs every streaming regression metric (reference F/regression/{mse,mae,mape,symmetric_mape,
@@ -20,7 +20,7 @@ namespace tm_amd {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kMaxSums = 14;
+constexpr int kMaxSums = 19;
 
 enum SumId : int {
   kSSE = 0,     // Σ (p - t)^2
@@ -37,7 +37,15 @@ enum SumId : int {
   kLOGCOSH = 11,// Σ log(cosh(p - t))
   kMINK = 12,   // Σ |p - t|^P
   kCOUNT = 13,  // number of observations per column
+  // the same five sums UNSHIFTED (p, t themselves): a Pearson fold (centred sums) and plain R^2 / explained-variance
+  // destinations (raw sums) on the same inputs then share ONE pass (ops.run_moments_plans)
+  kSP0 = 14,
+  kST0 = 15,
+  kSPP0 = 16,
+  kSTT0 = 17,
+  kSPT0 = 18,
 };
+constexpr int kUnshifted = (1 << kSP0) | (1 << kST0) | (1 << kSPP0) | (1 << kSTT0) | (1 << kSPT0);
 
 // Destinations of one update: up to kMaxDests plain "state += sum" targets (a whole MetricCollection's worth of
 // streaming regression metrics on the same inputs) plus, optionally, one Pearson fold block.
@@ -96,6 +104,14 @@ __device__ __forceinline__ void accumulate_pair(double* acc, scalar_t pv, scalar
     acc[kSPP] += pc * pc;
     acc[kSTT] += tc * tc;
     acc[kSPT] += pc * tc;
+  }
+  if (mask & kUnshifted) {
+    const double pd = p, td = t;
+    acc[kSP0] += pd;
+    acc[kST0] += td;
+    acc[kSPP0] += pd * pd;
+    acc[kSTT0] += td * td;
+    acc[kSPT0] += pd * td;
   }
   if (mask & (1 << kMAPE)) acc[kMAPE] += ad / fmax(static_cast<double>(fabsf(t)), eps);
   if (mask & (1 << kSMAPE)) acc[kSMAPE] += 2.0 * ad / fmax(static_cast<double>(fabsf(p) + fabsf(t)), eps);
@@ -302,6 +318,88 @@ __global__ void __launch_bounds__(kBlock) moments_finalize_kernel(const double* 
   finalize_column(partial, nblocks, k, blockIdx.x, spec, out_sums, mask);
 }
 
+
+// Small batches (n_rows * k <= kSmallMax, k dividing the wave): ONE 1024-thread block does the pass and the fold -- one
+// launch, no partials buffer, no grid-wide fence or ticket.  Every thread keeps one column (k | 64 | 1024, so the
+// stride never changes a thread's column) and issues up to kSmallUnroll pairs' loads before accumulating them; wave
+// xor-trees then a 16-wave LDS fold give the per-column sums, and (column, destination) threads apply them.
+constexpr int kSmallThreads = 1024;
+constexpr int kSmallUnroll = 8;
+constexpr long long kSmallMax = 65536;
+
+__device__ __forceinline__ void apply_sums(const double* __restrict__ v, int c, int j, const DestSpec& spec) {
+  // j < spec.n: plain destination j of column c; j == spec.n: the Pearson fold of column c
+  if (j < spec.n) {
+    const double x = v[spec.sum_id[j]] - (spec.sub_id[j] >= 0 ? v[spec.sub_id[j]] : 0.0);
+    const int idx = spec.per_col[j] ? c : 0;
+    if (spec.per_col[j] || c == 0) {
+      if (spec.dtype[j] == 0) reinterpret_cast<float*>(spec.ptr[j])[idx] += static_cast<float>(x);
+      else if (spec.dtype[j] == 1) reinterpret_cast<double*>(spec.ptr[j])[idx] += x;
+      else reinterpret_cast<int64_t*>(spec.ptr[j])[idx] += static_cast<int64_t>(llrint(x));
+    }
+  } else if (spec.fold == kFoldPearson) {
+    const double sd = v[kSP], se = v[kST], sdd = v[kSPP], see = v[kSTT], sde = v[kSPT], n = v[kCOUNT];
+    const double tot = ld_state(spec, 5, c) + n;
+    const double dx = sd / tot, dy = se / tot;
+    add_state(spec, 0, c, dx);
+    add_state(spec, 1, c, dy);
+    add_state(spec, 2, c, sdd - dx * sd);
+    add_state(spec, 3, c, see - dy * se);
+    add_state(spec, 4, c, sde - dx * se);
+    add_state(spec, 5, c, n);
+  }
+}
+
+template <typename scalar_t>
+__global__ void __launch_bounds__(kSmallThreads) moments_small_kernel(
+    const scalar_t* __restrict__ preds, const scalar_t* __restrict__ target, long long total, int k, int mask,
+    double eps, double pw, const float* __restrict__ shift_p, const float* __restrict__ shift_t, DestSpec spec,
+    double* __restrict__ out_sums) {
+  extern __shared__ double wsum[];  // [16 waves][k][kMaxSums], then [k][kMaxSums] block totals
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  constexpr int kWaves = kSmallThreads / kWave;
+  double acc[kMaxSums];
+#pragma unroll
+  for (int q = 0; q < kMaxSums; ++q) acc[q] = 0.0;
+  const int col = tid % k;
+  const float sp = shift_p ? shift_p[col] : 0.f;
+  const float st = shift_t ? shift_t[col] : 0.f;
+  for (long long base = tid; base < total; base += static_cast<long long>(kSmallThreads) * kSmallUnroll) {
+    scalar_t pv[kSmallUnroll], tv[kSmallUnroll];
+#pragma unroll
+    for (int u = 0; u < kSmallUnroll; ++u) {  // all loads in flight before the dependent fp64 accumulation
+      const long long i = base + static_cast<long long>(u) * kSmallThreads;
+      pv[u] = i < total ? preds[i] : scalar_t(0);
+      tv[u] = i < total ? target[i] : scalar_t(0);
+    }
+#pragma unroll
+    for (int u = 0; u < kSmallUnroll; ++u)
+      if (base + static_cast<long long>(u) * kSmallThreads < total) accumulate_pair(acc, pv[u], tv[u], sp, st, mask, eps, pw);
+  }
+#pragma unroll
+  for (int q = 0; q < kMaxSums; ++q) {
+    if (!((mask >> q) & 1) && q != kCOUNT) continue;  // uniform
+    double v = acc[q];
+    for (int off = kWave / 2; off >= k; off >>= 1) v += __shfl_xor(v, off, kWave);
+    if (lane < k) wsum[(wid * k + lane) * kMaxSums + q] = v;
+  }
+  __syncthreads();
+  double* tot = wsum + kWaves * k * kMaxSums;
+  for (int i = tid; i < k * kMaxSums; i += kSmallThreads) {
+    const int c = i / kMaxSums, q = i % kMaxSums;
+    double v = 0.0;
+    if (((mask >> q) & 1) || q == kCOUNT)
+      for (int w = 0; w < kWaves; ++w) v += wsum[(w * k + c) * kMaxSums + q];  // fixed order: reproducible
+    tot[i] = v;
+    if (out_sums) out_sums[i] = v;
+  }
+  __syncthreads();
+  for (int i = tid; i < k * (spec.n + 1); i += kSmallThreads) {
+    const int c = i / (spec.n + 1), j = i % (spec.n + 1);
+    apply_sums(tot + c * kMaxSums, c, j, spec);
+  }
+}
+
 }  // namespace
 
 // One zeroed uint32 per (device, stream), kept for the process: the last-block fold of moments_partial_kernel counts
@@ -320,7 +418,7 @@ unsigned int* stream_ticket(int device, hipStream_t s) {
 }
 
 // preds/target: [N, k] (or [N] with k = 1), same floating dtype. dests[j] += sum[sum_ids[j]] (per column, or over
-// column 0 when dest has one element and k > 1, e.g. observation counts). Returns the [k, 14] fp64 sums when want_sums.
+// column 0 when dest has one element and k > 1, e.g. observation counts). Returns the [k, 19] fp64 sums when want_sums.
 at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int64_t num_outputs, int64_t mask,
                           double eps, double power, const c10::optional<at::Tensor>& shift_p,
                           const c10::optional<at::Tensor>& shift_t, at::TensorList dests,
@@ -375,10 +473,10 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
     TORCH_CHECK(d.get_device() == preds.get_device(), "moments_update: destination on another device");
     TORCH_CHECK(d.numel() == k || d.numel() == 1, "moments_update: destination must have k or 1 elements");
     spec.ptr[j] = d.data_ptr();
-    // id < 16: sum[id];  id >= 16: sum[a] - sum[b] with id = 16 + 16 a + b
+    // id < 32: sum[id];  id >= 32: sum[a] - sum[b] with id = 32 + 32 a + b
     const int64_t id = sum_ids[j];
-    spec.sum_id[j] = static_cast<int>(id < 16 ? id : (id - 16) / 16);
-    spec.sub_id[j] = static_cast<int>(id < 16 ? -1 : (id - 16) % 16);
+    spec.sum_id[j] = static_cast<int>(id < 32 ? id : (id - 32) / 32);
+    spec.sub_id[j] = static_cast<int>(id < 32 ? -1 : (id - 32) % 32);
     TORCH_CHECK(spec.sum_id[j] >= 0 && spec.sum_id[j] < kMaxSums && spec.sub_id[j] < kMaxSums,
                 "moments_update: bad sum id");
     spec.per_col[j] = d.numel() == k && k > 1 ? 1 : (k == 1 ? 1 : 0);
@@ -422,6 +520,18 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
     hipLaunchKernelGGL(moments_finalize_kernel, dim3(k), dim3(kBlock), 0, s, partial.data_ptr<double>(),
                        static_cast<int>(chunks), k, spec, want_sums ? sums.data_ptr<double>() : nullptr,
                        static_cast<int>(mask));
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+    return sums;
+  }
+  if (kWave % k == 0 && n_rows * k <= kSmallMax) {
+    // per-batch sizes of the streaming metrics (config #5: 8192 pairs): ONE 1024-thread block, one launch
+    const size_t lds = static_cast<size_t>(kSmallThreads / kWave + 1) * k * kMaxSums * sizeof(double);
+    TM_DISPATCH_FLOAT(preds.scalar_type(), "moments_update", [&] {
+      hipLaunchKernelGGL((moments_small_kernel<scalar_t>), dim3(1), dim3(kSmallThreads), lds, s,
+                         reinterpret_cast<const scalar_t*>(preds.data_ptr()),
+                         reinterpret_cast<const scalar_t*>(target.data_ptr()), n_rows * k, k, static_cast<int>(mask),
+                         eps, power, sp, st, spec, want_sums ? sums.data_ptr<double>() : nullptr);
+    });
     C10_HIP_KERNEL_LAUNCH_CHECK();
     return sums;
   }

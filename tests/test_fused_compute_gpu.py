@@ -141,3 +141,28 @@ def test_train_eval_toggle_keeps_fused_plan():
     assert len(plans) == 1
     assert not gc.__dict__.get("_fused_off")
     assert gc.__dict__.get("_fused_rebuilds", 0) == 1
+
+
+def test_regression_collection_update_is_one_moments_pass(monkeypatch):
+    """MSE / MAE / R2 / Pearson / EV on the same inputs: the plain sums read the unshifted twins (SP0 ...) of the
+    centred sums the Pearson fold needs, so the whole collection update is ONE moments pass (one launch of the
+    single-block kernel for an 8192-pair batch), and every value still equals the CPU collection."""
+    from torchmetrics_amd import ops
+
+    calls = []
+    real = ops.moments_update
+
+    def counting(*a, **k):
+        calls.append(1)
+        return real(*a, **k)
+
+    monkeypatch.setattr(ops, "moments_update", counting)
+    gr, cr = _reg().to(DEV), _reg()
+    for i in range(4):
+        _, _, x, y = _batch(60 + i, n=8192)
+        calls.clear()
+        gr.update(x.to(DEV), y.to(DEV))
+        cr.update(x, y)
+        if i > 0:  # (the first update finds the compute groups member by member)
+            assert len(calls) == 1, len(calls)
+        _check(gr.compute(), cr.compute())

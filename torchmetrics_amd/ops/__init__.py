@@ -575,16 +575,27 @@ def mc_calibration_update(preds: Tensor, target: Tensor, ws: CalibrationWorkspac
 # ------------------------------------------------------------------------------------------------------ regression
 # sum ids of csrc/regression/moments.hip
 SSE, SAE, SP, ST, SPP, STT, SPT, MAPE, SMAPE, SABST, MSLE, LOGCOSH, MINK, COUNT = range(14)
+# the centred sums' unshifted twins (a Pearson fold and raw-sum destinations sharing one pass)
+SP0, ST0, SPP0, STT0, SPT0 = range(14, 19)
+_UNSHIFTED = {SP: SP0, ST: ST0, SPP: SPP0, STT: STT0, SPT: SPT0}
 FOLD_NONE, FOLD_PEARSON = 0, 1
 
 
 def sum_diff(a: int, b: int) -> int:
     """Destination id meaning ``sum[a] - sum[b]`` (e.g. ``sum_diff(ST, SP)`` = Σ(t - p))."""
-    return 16 + 16 * int(a) + int(b)
+    return 32 + 32 * int(a) + int(b)
 
 
 def _sum_ids(i: int) -> "tuple[int, ...]":
-    return (i,) if i < 16 else ((i - 16) // 16, (i - 16) % 16)
+    return (i,) if i < 32 else ((i - 32) // 32, (i - 32) % 32)
+
+
+def _unshifted_id(i: int) -> int:
+    """The same destination id reading the unshifted twins of the centred sums."""
+    if i < 32:
+        return _UNSHIFTED.get(i, i)
+    a, b = (i - 32) // 32, (i - 32) % 32
+    return sum_diff(_UNSHIFTED.get(a, a), _UNSHIFTED.get(b, b))
 
 
 def moments_update(
@@ -603,7 +614,7 @@ def moments_update(
 ) -> Optional[Tensor]:
     """One pass computing the requested per-output sums and adding ``sum[dest_ids[j]]`` into ``dests[j]``.
 
-    ``preds``/``target`` are ``[N, num_outputs]`` (or 1-D). Returns the ``[num_outputs, 14]`` fp64 sums if asked.
+    ``preds``/``target`` are ``[N, num_outputs]`` (or 1-D). Returns the ``[num_outputs, 19]`` fp64 sums if asked.
     ``dest_ids`` entries may be :func:`sum_diff` pairs.  ``fold=FOLD_PEARSON`` additionally folds the batch into the
     six running Pearson states given FIRST in ``dests`` (``[mean_x, mean_y, m2_x, m2_y, c_xy, n]``, in place;
     ``shift_p``/``shift_t`` must be the current means); ``dest_ids`` then names the remaining destinations.
@@ -701,9 +712,6 @@ def states_ready(owner: dict, states: tuple, dev: int, dtypes: tuple = (torch.fl
     return ok
 
 
-_CENTRED = (1 << SP) | (1 << ST) | (1 << SPP) | (1 << STT) | (1 << SPT)
-
-
 def run_moments_plans(plans: "list[MomentsPlan]") -> int:
     """Execute deferred plans, merging those on identical inputs (at most one Pearson fold and 32 plain
     destinations per launch).  Returns the number of kernel calls issued."""
@@ -716,24 +724,26 @@ def run_moments_plans(plans: "list[MomentsPlan]") -> int:
             merged = MomentsPlan(members[0].preds, members[0].target, members[0].k, [], [], members[0].eps,
                                  members[0].power, src=members[0].src, checked=True)
             rest = []
+            plain_ids: "list[bool]" = []  # per merged id: it came from a plan without a fold
             for pl in members:
-                # the Pearson fold shifts the centred sums by the running means: it cannot share a pass with
-                # plain destinations that need the unshifted Σp / Σt / Σp² / Σt² / Σpt
-                pl_plain_centred = bool(pl._uses() & _CENTRED)
-                m_plain_centred = bool(merged._uses() & _CENTRED)
-                if (pl.fold_states is not None and (merged.fold_states is not None or m_plain_centred)) or \
-                        (merged.fold_states is not None and pl_plain_centred) or \
+                # the Pearson fold shifts the centred sums by the running means; plain destinations on the same pass
+                # read the unshifted twins (SP0 ...) of those sums instead, so everything on these inputs is ONE pass
+                if (pl.fold_states is not None and merged.fold_states is not None) or \
                         len(merged.dests) + len(pl.dests) > 32:
                     rest.append(pl)
                     continue
                 merged.dests += pl.dests
                 merged.ids += pl.ids
+                plain_ids += [pl.fold_states is None] * len(pl.ids)
                 if pl.fold_states is not None:
                     merged.fold_states, merged.shift_p, merged.shift_t = pl.fold_states, pl.shift_p, pl.shift_t
                 if pl._uses() & ((1 << MAPE) | (1 << SMAPE)):
                     merged.eps = pl.eps
                 if pl._uses() & (1 << MINK):
                     merged.power = pl.power
+            if merged.fold_states is not None:
+                merged.ids = [_unshifted_id(int(i)) if plain else i for i, plain in zip(merged.ids, plain_ids)]
+                merged._mask = None
             merged.run()
             calls += 1
             members = rest

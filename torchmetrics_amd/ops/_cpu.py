@@ -175,7 +175,7 @@ def moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_
     t = target.reshape(-1, k).double()
     d = p - t
     ad = d.abs()
-    sums = torch.zeros(k, 14, dtype=torch.float64, device=p.device)
+    sums = torch.zeros(k, 19, dtype=torch.float64, device=p.device)
     pc = p - (shift_p.double() if shift_p is not None else 0.0)
     tc = t - (shift_t.double() if shift_t is not None else 0.0)
     cols = {
@@ -193,6 +193,11 @@ def moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_
         11: lambda: (ad + torch.log1p(torch.exp(-2 * ad)) - 0.69314718055994530942).sum(0),
         12: lambda: (ad**power).sum(0),
         13: lambda: torch.full((k,), float(p.shape[0]), dtype=torch.float64, device=p.device),
+        14: lambda: p.sum(0),
+        15: lambda: t.sum(0),
+        16: lambda: (p * p).sum(0),
+        17: lambda: (t * t).sum(0),
+        18: lambda: (p * t).sum(0),
     }
     for sid, fn in cols.items():
         if mask & (1 << sid) or sid == 13:
@@ -208,7 +213,7 @@ def moments_update(preds, target, num_outputs, mask, eps, power, shift_p, shift_
             dst += inc.reshape(dst.shape).to(dst.dtype)
         n0 += p.shape[0]
     for dst, sid in zip(dests, dest_ids):
-        col = sums[:, sid] if sid < 16 else sums[:, (sid - 16) // 16] - sums[:, (sid - 16) % 16]
+        col = sums[:, sid] if sid < 32 else sums[:, (sid - 32) // 32] - sums[:, (sid - 32) % 32]
         val = col if dst.numel() == k else col[0]
         if dst.dtype == torch.int64:
             val = torch.round(val).long()

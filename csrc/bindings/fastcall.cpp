@@ -44,6 +44,12 @@ void stat_reduce(const at::Tensor& tp, const at::Tensor& fp, const at::Tensor& t
                  at::Tensor out, int64_t kind, int64_t average, bool multilabel, double beta);
 void launch_probe(at::Tensor flag);
 int64_t read_word_sync(const at::Tensor& word);
+bool mc_stats_direct(const at::Tensor& preds, const at::Tensor& target, at::Tensor tp, at::Tensor fp, at::Tensor tn,
+                     at::Tensor fn, at::Tensor flag, int64_t num_classes);
+void mc_family_update(const at::Tensor& preds, const at::Tensor& target, at::TensorList cm, at::TensorList st,
+                      at::IntArrayRef st_micro, const at::Tensor& curve, const at::Tensor& thr_sorted,
+                      const at::Tensor& perm, const at::Tensor& conf, const at::Tensor& acc, const at::Tensor& bounds,
+                      const at::Tensor& bins, at::TensorList err, at::Tensor work, int64_t slot, at::Tensor cand);
 void zero_async(at::Tensor t);
 bool mc_confmat_dual(const at::Tensor& preds, const at::Tensor& target, at::Tensor batch, at::Tensor global,
                      at::Tensor flag, int64_t num_classes, int64_t ignore_index, bool has_ignore);
@@ -264,6 +270,7 @@ PyMethodDef kMethods[] = {
     TM_FAST("mc_stats_forward", tm_amd::mc_stats_forward),
     TM_FAST("bin_stats_forward", tm_amd::bin_stats_forward),
     TM_FAST("arg_probe", arg_probe),
+    TM_FAST("mc_family_update", tm_amd::mc_family_update),
     {nullptr, nullptr, 0, nullptr},
 };
 
@@ -870,7 +877,9 @@ int stats_forward(NativeUpdate* self, PyObject* a, PyObject* b, PyObject** resul
   if (!workspace(st, dev, mc ? 3 * size + 1 : 7 * size, ws, mc ? nullptr : &not_prob)) TM_DECLINE;
   if (update_only) {
     try {
-      if (mc) {
+      if (mc && !micro && !has_ignore && tm_amd::mc_stats_direct(p, t, *tp, *fp, *tn, *fn, *flag, size)) {
+        // one launch straight into the states (wide 16-bit rows)
+      } else if (mc) {
         tm_amd::mc_update(p, t, ws, *flag, size, ignore, has_ignore, 1, false);
         tm_amd::mc_stats_finalize(ws, size, micro, true, *tp, *fp, *tn, *fn);
       } else {

@@ -1,0 +1,447 @@
+// One fused update for a MetricCollection's few-class multiclass members on the same (logits, target) batch.
+//
+// Reference: S/collections.py:200-226 updates every compute group's leader separately, and each leader re-reads the
+// batch: the stat-score family (F/classification/stat_scores.py:405-419: argmax + bincount), the confusion-matrix
+// family (F/classification/confusion_matrix.py:333-337), the binned PR-curve family (F/classification/
+// precision_recall_curve.py:482-527: softmax-if-needed + per-threshold confmats) and the calibration error
+// (F/classification/calibration_error.py:29-59: softmax-if-needed, top-1 confidence / correctness).  On the
+// [8192, 10] bf16 batches of config #5 that was ~10 launches per step, every one latency-bound.
+//
+// Here the batch is read ONCE by `family_rows_kernel` (one row per thread; C <= 64): it computes the row's argmax,
+// its softmax (rounded to the input dtype, as torch.softmax stores it), the "score outside [0, 1]" bit, and feeds a
+// per-block LDS image of everything the members need:
+//   * the C x C (target, argmax) histogram          -> confusion matrices, and tp / fp / tn / fn of the stat scores;
+//   * per-class threshold-bucket histograms, for the raw scores AND for the softmax (the batch-wide softmax decision
+//     is only known when every block is done) -> the [T, C, 2, 2] binned-curve state;
+//   * top-1 (confidence, correct) candidates of both variants per row, and their (count, Σconf, Σacc) bins -> the
+//     calibration error's list states and its bin cache.
+// Each block adds its (non-zero) image words into one batch image in global memory (integer atomics: exact; the
+// calibration float bins in arrival order) and ORs its outside bit into the batch's decision word;
+// `family_fold_kernel` (one launch, blocks by role) reads the batch image once, adds it into every member's state,
+// selects the calibration outputs, publishes the target-range bit into every member's validation word, and re-zeroes
+// the image for the next update (the decision word is double-buffered by update parity).  Two launches per step for
+// the whole classification group, whatever the number of members.
+#include "common/tm_common.h"
+
+namespace tm_amd {
+namespace {
+
+constexpr int kFamThreads = 256;
+constexpr int kFamMaxC = 64;
+constexpr int kFamMaxCons = 4;   // confusion-matrix / stat-score consumers per launch
+constexpr int kFamMaxErr = 8;    // validation words
+constexpr int kFamMaxBlocks = 512;
+constexpr int kFoldCols = kFamThreads / kWave;  // curve columns per fold block (one wave each)
+
+struct FamilySpec {
+  int C;
+  int n_cm;
+  int64_t* cm[kFamMaxCons];                // [C, C] += batch
+  int n_st;
+  int64_t* st[kFamMaxCons][4];             // tp, fp, tn, fn: [C] (or [1] when micro) +=
+  int st_micro[kFamMaxCons];
+  int T;                                   // thresholds of the curve member (0: none)
+  const double* thr;                       // [T] ascending
+  const int64_t* perm;                     // caller index of each sorted threshold
+  int64_t* curve;                          // [T, C, 2, 2]
+  int nb;                                  // calibration bin bounds (0: no calibration member)
+  const float* bounds;                     // [nb] ascending
+  float* conf;                             // [N] outputs (list-state elements)
+  float* acc;
+  float* bins;                             // [nb, 3] cache or nullptr
+  int n_err;
+  int* err[kFamMaxErr];
+  // scratch (zero on entry, re-zeroed by the fold)
+  int* img;                                // batch image: [C*C cm][2][T+1][C][2] curve][2][nb][3] calib (f32)]
+  int* outside;                            // [2] decision words, by update parity
+  int slot;
+  float4* cand;                            // [N]
+  int* err_scratch;
+  int part_words, off_cv, off_cb;
+  int need_cm;
+};
+
+__device__ __forceinline__ int bucket_of(const double* __restrict__ thr, int t, double p) {
+  int lo = 0, hi = t;  // number of thresholds <= p (NaN -> 0)
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (thr[mid] <= p) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+template <typename scalar_t, typename target_t>
+__global__ void __launch_bounds__(kFamThreads) family_rows_kernel(const scalar_t* __restrict__ preds,
+                                                                  const target_t* __restrict__ target, long long N,
+                                                                  FamilySpec sp) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  int* h = smem;                                                 // this block's partial row
+  float* hf = reinterpret_cast<float*>(smem);                    // (the calibration bins are floats)
+  double* thr_s = reinterpret_cast<double*>(smem + ((sp.part_words + 1) & ~1));
+  float* bnd_s = reinterpret_cast<float*>(thr_s + sp.T);
+  __shared__ int blk_outside;
+  const int C = sp.C, T = sp.T, nb = sp.nb;
+  for (int i = threadIdx.x; i < sp.part_words; i += kFamThreads) h[i] = 0;
+  for (int i = threadIdx.x; i < T; i += kFamThreads) thr_s[i] = sp.thr[i];
+  for (int i = threadIdx.x; i < nb; i += kFamThreads) bnd_s[i] = sp.bounds[i];
+  if (threadIdx.x == 0) blk_outside = 0;
+  __syncthreads();
+  bool outside = false, bad = false;
+  for (long long row = static_cast<long long>(blockIdx.x) * kFamThreads + threadIdx.x; row < N;
+       row += static_cast<long long>(gridDim.x) * kFamThreads) {
+    const scalar_t* r = preds + row * C;
+    float mx = -INFINITY, mf = -INFINITY;  // argmax max (NaN wins) / NaN-ignoring max (the curve's softmax shift)
+    int mi = 0x7fffffff;
+    for (int c = 0; c < C; ++c) {
+      const float v = to_f32(r[c]);
+      outside |= !(v >= 0.f && v <= 1.f);
+      mf = fmaxf(mf, v);
+      if (argmax_better(v, c, mx, mi)) {
+        mx = v;
+        mi = c;
+      }
+    }
+    float s_cal = 0.f;
+    for (int c = 0; c < C; ++c) s_cal += expf(to_f32(r[c]) - mx);
+    float s_cur = s_cal;
+    if (!(mf == mx)) {  // a NaN in the row: the two shifts differ
+      s_cur = 0.f;
+      for (int c = 0; c < C; ++c) s_cur += expf(to_f32(r[c]) - mf);
+    }
+    const long long tv = static_cast<long long>(target[row]);
+    const bool valid = tv >= 0 && tv < C;
+    bad |= !valid;
+    const int t = static_cast<int>(valid ? tv : 0);
+    if (valid && sp.need_cm) atomicAdd(&h[t * C + mi], 1);
+    if (valid && T > 0) {
+      for (int c = 0; c < C; ++c) {
+        const float x = to_f32(r[c]);
+        const double praw = static_cast<double>(x);
+        const double psoft = static_cast<double>(round_to<scalar_t>(expf(x - mf) / s_cur));
+        const int pos = c == t;
+        const int braw = bucket_of(thr_s, T, praw), bsoft = bucket_of(thr_s, T, psoft);
+        atomicAdd(&h[sp.off_cv + ((0 * (T + 1) + braw) * C + c) * 2 + pos], 1);
+        atomicAdd(&h[sp.off_cv + ((1 * (T + 1) + bsoft) * C + c) * 2 + pos], 1);
+      }
+    }
+    if (nb > 0) {
+      float sv = -INFINITY;
+      int si = 0x7fffffff;
+      for (int c = 0; c < C; ++c) {
+        const float p = round_to<scalar_t>(expf(to_f32(r[c]) - mx) / s_cal);
+        if (argmax_better(p, c, sv, si)) {
+          sv = p;
+          si = c;
+        }
+      }
+      const float ar = mi == tv ? 1.f : 0.f, as = si == tv ? 1.f : 0.f;
+      sp.cand[row] = make_float4(mx, ar, sv, as);
+      // (count, Σconf, Σacc) bins of both variants: bin = #{bounds <= conf} - 1
+      const float cv[2] = {round_to<scalar_t>(mx), sv};
+      const float av[2] = {ar, as};
+#pragma unroll
+      for (int var = 0; var < 2; ++var) {
+        int b = -1;
+        for (int k = 0; k < nb; ++k) b += (bnd_s[k] <= cv[var]) ? 1 : 0;
+        if (b < 0) continue;
+        float* dst = hf + sp.off_cb + (var * nb + b) * 3;
+        atomicAdd(dst, 1.f);
+        atomicAdd(dst + 1, cv[var]);
+        atomicAdd(dst + 2, av[var]);
+      }
+    }
+  }
+  if (__any(outside) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(&blk_outside, 1);
+  if (__any(bad) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(sp.err_scratch, kErrTargetOutOfRange);
+  __syncthreads();
+  for (int i = threadIdx.x; i < sp.off_cb; i += kFamThreads)
+    if (h[i]) atomicAdd(&sp.img[i], h[i]);
+  for (int i = sp.off_cb + threadIdx.x; i < sp.part_words; i += kFamThreads)
+    if (hf[i] != 0.f) atomicAdd(reinterpret_cast<float*>(sp.img) + i, hf[i]);
+  if (threadIdx.x == 0 && blk_outside) atomicOr(&sp.outside[sp.slot], 1);
+}
+
+__device__ __forceinline__ long long wave_incl_scan_ll(long long v) {
+  const int lane = threadIdx.x & (kWave - 1);
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const long long u = __shfl_up(v, o, kWave);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// Fold roles by block: [0] confusion matrix + stat scores (+ validation words), then ceil(C / 4) curve blocks (a
+// wave per class column), then the calibration select blocks (rows), then one calibration-bins block.  Every image
+// word is read, and re-zeroed, by exactly one block.
+__global__ void __launch_bounds__(kFamThreads) family_fold_kernel(FamilySpec sp, long long N, int r_cv, int r_sel,
+                                                                  int n_sel, int r_bins) {
+  __shared__ long long cmb[kFamMaxC * kFamMaxC];
+  __shared__ long long red[4][kFamThreads / kWave];
+  const int C = sp.C, T = sp.T, nb = sp.nb;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  const int var = sp.outside[sp.slot] ? 1 : 0;  // the batch-wide `softmax unless every score is in [0, 1]`
+  const int bid = blockIdx.x;
+  if (bid == 0) {
+    if (tid == 0) {
+      const int e = *sp.err_scratch;
+      if (e) {
+        for (int k = 0; k < sp.n_err; ++k) atomicOr(sp.err[k], e);
+        *sp.err_scratch = 0;
+      }
+      sp.outside[sp.slot ^ 1] = 0;  // the next update's decision word
+    }
+    if (!sp.need_cm) return;
+    for (int i = tid; i < C * C; i += kFamThreads) {
+      const long long v = sp.img[i];
+      sp.img[i] = 0;
+      cmb[i] = v;
+      for (int k = 0; k < sp.n_cm; ++k)
+        if (v) sp.cm[k][i] += v;
+    }
+    __syncthreads();
+    if (sp.n_st == 0) return;
+    long long tp = 0, fp = 0, fn = 0, all = 0;
+    if (tid < C) {
+      long long rows = 0, cols = 0;
+      for (int j = 0; j < C; ++j) {
+        rows += cmb[tid * C + j];  // target == tid
+        cols += cmb[j * C + tid];  // argmax == tid
+      }
+      tp = cmb[tid * C + tid];
+      fp = cols - tp;
+      fn = rows - tp;
+      all = rows;
+    }
+    long long v4[4] = {tp, fp, fn, all};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const long long sum = wave_sum_ll(v4[q]);
+      if (lane == 0) red[q][wave] = sum;
+    }
+    __syncthreads();
+    long long tot[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      for (int w = 0; w < kFamThreads / kWave; ++w) tot[q] += red[q][w];
+    const long long n_valid = tot[3];
+    for (int k = 0; k < sp.n_st; ++k) {
+      if (sp.st_micro[k]) {
+        if (tid == 0) {
+          sp.st[k][0][0] += tot[0];
+          sp.st[k][1][0] += tot[1];
+          sp.st[k][2][0] += static_cast<long long>(C) * n_valid - tot[0] - tot[1] - tot[2];
+          sp.st[k][3][0] += tot[2];
+        }
+      } else if (tid < C) {
+        sp.st[k][0][tid] += tp;
+        sp.st[k][1][tid] += fp;
+        sp.st[k][2][tid] += n_valid - tp - fp - fn;
+        sp.st[k][3][tid] += fn;
+      }
+    }
+    return;
+  }
+  if (bid >= r_cv && bid < r_sel) {
+    const int col = (bid - r_cv) * kFoldCols + wave;
+    if (col >= C || T == 0) return;
+    // the chosen variant's bucket counts of this column; then curve_finalize_kernel's suffix scan: predicted positive
+    // at sorted threshold i <=> bucket > i.  Both variants' words of the column are re-zeroed.
+    int* base = sp.img + sp.off_cv + var * (T + 1) * C * 2;
+    int* other = sp.img + sp.off_cv + (var ^ 1) * (T + 1) * C * 2;
+    long long tot_neg = 0, tot_pos = 0;
+    for (int b = lane; b <= T; b += kWave) {
+      tot_neg += base[(b * C + col) * 2];
+      tot_pos += base[(b * C + col) * 2 + 1];
+    }
+    tot_neg = wave_sum_ll(tot_neg);
+    tot_pos = wave_sum_ll(tot_pos);
+    long long carry_neg = 0, carry_pos = 0;
+    for (int start = 0; start <= T; start += kWave) {
+      const int b = T - (start + lane);
+      long long neg = 0, pos = 0;
+      if (b >= 0) {
+        int* h = base + (b * C + col) * 2;
+        neg = h[0];
+        pos = h[1];
+        h[0] = 0;
+        h[1] = 0;
+        int* g = other + (b * C + col) * 2;
+        g[0] = 0;
+        g[1] = 0;
+      }
+      const long long sneg = wave_incl_scan_ll(neg) + carry_neg;
+      const long long spos = wave_incl_scan_ll(pos) + carry_pos;
+      if (b >= 1) {
+        const long long i = sp.perm[b - 1];
+        int64_t* out = sp.curve + (i * C + col) * 4;
+        out[0] += tot_neg - sneg;  // tn
+        out[1] += sneg;            // fp
+        out[2] += tot_pos - spos;  // fn
+        out[3] += spos;            // tp
+      }
+      carry_neg = __shfl(sneg, kWave - 1, kWave);
+      carry_pos = __shfl(spos, kWave - 1, kWave);
+    }
+    return;
+  }
+  if (bid >= r_sel && bid < r_sel + n_sel) {
+    for (long long i = static_cast<long long>(bid - r_sel) * kFamThreads + tid; i < N;
+         i += static_cast<long long>(n_sel) * kFamThreads) {
+      const float4 c = sp.cand[i];
+      sp.conf[i] = var ? c.z : c.x;
+      sp.acc[i] = var ? c.w : c.y;
+    }
+    return;
+  }
+  if (bid == r_bins) {
+    float* f = reinterpret_cast<float*>(sp.img) + sp.off_cb;
+    for (int i = tid; i < nb * 3; i += kFamThreads) {
+      const float v = f[var * nb * 3 + i];
+      if (sp.bins != nullptr && v != 0.f) sp.bins[i] += v;
+      f[i] = 0.f;
+      f[nb * 3 + i] = 0.f;
+    }
+  }
+}
+
+}  // namespace
+
+// preds [N, C] (bf16 / fp16 / fp32, C <= 64), target [N] (int32 / int64).  Consumers:
+//   cm: confusion matrices int64 [C, C]; st: stat-score states, 4 per consumer (tp, fp, tn, fn) int64 [C] or [1]
+//   (st_micro[k] = 1); curve: int64 [T, C, 2, 2] with thr_sorted f64 [T] / perm i64 [T] (empty curve: none);
+//   conf / acc: f32 [N] outputs with bounds f32 [nb] (empty conf: no calibration member), bins f32 [nb, 3] (may be
+//   empty); err: validation words (int32) that get the target-range bit.
+// work: int32 scratch of at least family_work_words(...) words, ZERO before its first use (every fold re-zeroes
+// what it read); slot: update parity (the decision word's double buffer); cand: f32 [4 N] scratch when a calibration
+// member is present.  Two launches.
+void mc_family_update(const at::Tensor& preds, const at::Tensor& target, at::TensorList cm, at::TensorList st,
+                      at::IntArrayRef st_micro, const at::Tensor& curve, const at::Tensor& thr_sorted,
+                      const at::Tensor& perm, const at::Tensor& conf, const at::Tensor& acc, const at::Tensor& bounds,
+                      const at::Tensor& bins, at::TensorList err, at::Tensor work, int64_t slot,
+                      at::Tensor cand) {
+  TM_CHECK_CUDA(preds);
+  TM_CHECK_CONTIG(preds);
+  TM_CHECK_CONTIG(target);
+  TORCH_CHECK(preds.dim() == 2 && target.dim() == 1 && target.size(0) == preds.size(0),
+              "mc_family_update: preds [N, C], target [N]");
+  const long long N = preds.size(0);
+  const int C = static_cast<int>(preds.size(1));
+  TORCH_CHECK(C >= 1 && C <= kFamMaxC, "mc_family_update: 1 <= C <= ", kFamMaxC);
+  TORCH_CHECK(cm.size() <= static_cast<size_t>(kFamMaxCons) && st.size() % 4 == 0 &&
+                  st.size() / 4 <= static_cast<size_t>(kFamMaxCons) && st_micro.size() == st.size() / 4 &&
+                  err.size() <= static_cast<size_t>(kFamMaxErr),
+              "mc_family_update: too many consumers");
+  FamilySpec sp{};
+  sp.C = C;
+  sp.n_cm = static_cast<int>(cm.size());
+  for (int k = 0; k < sp.n_cm; ++k) {
+    TORCH_CHECK(cm[k].scalar_type() == at::kLong && cm[k].is_contiguous() && cm[k].numel() == C * C &&
+                    cm[k].get_device() == preds.get_device(), "mc_family_update: confmat int64 [C, C]");
+    sp.cm[k] = cm[k].data_ptr<int64_t>();
+  }
+  sp.n_st = static_cast<int>(st.size() / 4);
+  for (int k = 0; k < sp.n_st; ++k) {
+    sp.st_micro[k] = static_cast<int>(st_micro[k]);
+    for (int q = 0; q < 4; ++q) {
+      const at::Tensor& s = st[4 * k + q];
+      TORCH_CHECK(s.scalar_type() == at::kLong && s.is_contiguous() && s.get_device() == preds.get_device() &&
+                      s.numel() == (sp.st_micro[k] ? 1 : C), "mc_family_update: stat states int64 [C] / [1]");
+      sp.st[k][q] = s.data_ptr<int64_t>();
+    }
+  }
+  sp.need_cm = sp.n_cm > 0 || sp.n_st > 0;
+  if (curve.numel() > 0) {
+    sp.T = static_cast<int>(thr_sorted.numel());
+    TORCH_CHECK(sp.T >= 1 && thr_sorted.scalar_type() == at::kDouble && perm.scalar_type() == at::kLong &&
+                    perm.numel() == sp.T && curve.scalar_type() == at::kLong && curve.is_contiguous() &&
+                    curve.numel() == static_cast<long long>(sp.T) * C * 4,
+                "mc_family_update: curve state int64 [T, C, 2, 2] with f64 thresholds and i64 perm");
+    sp.thr = thr_sorted.data_ptr<double>();
+    sp.perm = perm.data_ptr<int64_t>();
+    sp.curve = curve.data_ptr<int64_t>();
+  }
+  if (conf.numel() > 0 || N == 0) {
+    sp.nb = static_cast<int>(bounds.numel());
+    TORCH_CHECK(sp.nb >= 1 && bounds.scalar_type() == at::kFloat && conf.scalar_type() == at::kFloat &&
+                    acc.scalar_type() == at::kFloat && conf.numel() == N && acc.numel() == N,
+                "mc_family_update: calibration outputs f32 [N] with f32 bounds");
+    sp.bounds = bounds.data_ptr<float>();
+    sp.conf = conf.data_ptr<float>();
+    sp.acc = acc.data_ptr<float>();
+    if (bins.numel() > 0) {
+      TORCH_CHECK(bins.scalar_type() == at::kFloat && bins.is_contiguous() && bins.numel() == sp.nb * 3,
+                  "mc_family_update: bins f32 [nb, 3]");
+      sp.bins = bins.data_ptr<float>();
+    }
+  }
+  sp.n_err = static_cast<int>(err.size());
+  for (int k = 0; k < sp.n_err; ++k) {
+    TORCH_CHECK(err[k].scalar_type() == at::kInt && err[k].numel() >= 1, "mc_family_update: int32 error words");
+    sp.err[k] = err[k].data_ptr<int>();
+  }
+  if (N == 0) return;
+  sp.off_cv = sp.need_cm ? C * C : 0;
+  sp.off_cb = sp.off_cv + (sp.T > 0 ? 2 * (sp.T + 1) * C * 2 : 0);
+  sp.part_words = sp.off_cb + 2 * sp.nb * 3;
+  const size_t lds = static_cast<size_t>((sp.part_words + 1) & ~1) * 4 + static_cast<size_t>(sp.T) * 8 +
+                     static_cast<size_t>(sp.nb) * 4;
+  TORCH_CHECK(lds <= 64 * 1024, "mc_family_update: partial image exceeds 64 KiB of LDS");
+  const int nblk = static_cast<int>(std::min<long long>((N + kFamThreads - 1) / kFamThreads, kFamMaxBlocks));
+  TORCH_CHECK(work.scalar_type() == at::kInt && work.is_contiguous() && work.numel() >= sp.part_words + 3,
+              "mc_family_update: work scratch too small");
+  TORCH_CHECK(slot == 0 || slot == 1, "mc_family_update: slot 0 / 1");
+  sp.img = work.data_ptr<int>();
+  sp.outside = sp.img + sp.part_words;
+  sp.slot = static_cast<int>(slot);
+  sp.err_scratch = sp.outside + 2;
+  if (sp.nb > 0) {
+    TORCH_CHECK(cand.scalar_type() == at::kFloat && cand.numel() >= 4 * N, "mc_family_update: cand f32 [4 N]");
+    sp.cand = reinterpret_cast<float4*>(cand.data_ptr<float>());
+  }
+  auto s = stream();
+  TM_DISPATCH_TARGET(target.scalar_type(), "mc_family_update", [&] {
+    const target_t* tp = reinterpret_cast<const target_t*>(target.data_ptr());
+    switch (preds.scalar_type()) {
+      case at::kBFloat16:
+        hipLaunchKernelGGL((family_rows_kernel<c10::BFloat16, target_t>), dim3(nblk), dim3(kFamThreads), lds, s,
+                           reinterpret_cast<const c10::BFloat16*>(preds.data_ptr()), tp, N, sp);
+        break;
+      case at::kHalf:
+        hipLaunchKernelGGL((family_rows_kernel<c10::Half, target_t>), dim3(nblk), dim3(kFamThreads), lds, s,
+                           reinterpret_cast<const c10::Half*>(preds.data_ptr()), tp, N, sp);
+        break;
+      case at::kFloat:
+        hipLaunchKernelGGL((family_rows_kernel<float, target_t>), dim3(nblk), dim3(kFamThreads), lds, s,
+                           preds.data_ptr<float>(), tp, N, sp);
+        break;
+      default:
+        TORCH_CHECK(false, "mc_family_update: bf16 / fp16 / fp32 scores");
+    }
+  });
+  const int r_cv = 1;
+  const int n_cv = sp.T > 0 ? (C + kFoldCols - 1) / kFoldCols : 0;
+  const int r_sel = r_cv + n_cv;
+  const int n_sel = sp.nb > 0 ? static_cast<int>(std::min<long long>((N + kFamThreads - 1) / kFamThreads, 256)) : 0;
+  const int r_bins = r_sel + n_sel;
+  const int grid = r_bins + (sp.nb > 0 ? 1 : 0);
+  hipLaunchKernelGGL(family_fold_kernel, dim3(grid), dim3(kFamThreads), 0, s, sp, N, r_cv, r_sel, n_sel, r_bins);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+// int32 words the scratch `work` must hold
+int64_t mc_family_work_words(int64_t C, bool need_cm, int64_t T, int64_t nb) {
+  return (need_cm ? C * C : 0) + (T > 0 ? 2 * (T + 1) * C * 2 : 0) + 2 * nb * 3 + 3;
+}
+
+}  // namespace tm_amd
+
+TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def(
+      "mc_family_update(Tensor preds, Tensor target, Tensor(a!)[] cm, Tensor(b!)[] st, int[] st_micro, "
+      "Tensor(c!) curve, Tensor thr_sorted, Tensor perm, Tensor(d!) conf, Tensor(e!) acc, Tensor bounds, "
+      "Tensor(f!) bins, Tensor(g!)[] err, Tensor(h!) work, int slot, Tensor(i!) cand) -> ()");
+  m.def("mc_family_work_words(int C, bool need_cm, int T, int nb) -> int", &tm_amd::mc_family_work_words);
+}
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) { m.impl("mc_family_update", &tm_amd::mc_family_update); }

@@ -12,6 +12,7 @@
 #include "common/compute_bodies.h"
 
 namespace tm_amd {
+int notprob_current(const at::Tensor& np);  // stat_scores.hip
 namespace {
 
 constexpr int kThreads = cbody::kThreads;
@@ -81,9 +82,10 @@ __global__ void __launch_bounds__(kThreads) bin_stats_forward_kernel(int64_t* __
                                                                      int64_t* __restrict__ tp, int64_t* __restrict__ fp,
                                                                      int64_t* __restrict__ tn, int64_t* __restrict__ fn,
                                                                      int kind, int avg, float beta2,
-                                                                     float* __restrict__ out) {
+                                                                     float* __restrict__ out, int slot,
+                                                                     bool two_slots) {
   __shared__ double red[kThreads / kWave];
-  const bool use_b = *not_prob != 0;
+  const bool use_b = not_prob[slot] != 0;
   auto get = [&](int k, long long& a, long long& b, long long& c, long long& d) {
     const int64_t* w = ws + static_cast<long long>(k) * kBinSlots;
     a = use_b ? w[3] : w[0];
@@ -103,7 +105,7 @@ __global__ void __launch_bounds__(kThreads) bin_stats_forward_kernel(int64_t* __
   cbody::stat_reduce_body(get, L, kind, avg, true, beta2, out, red);
   __syncthreads();
   for (long long k = threadIdx.x; k < static_cast<long long>(L) * kBinSlots; k += kThreads) ws[k] = 0;
-  if (threadIdx.x == 0) *not_prob = 0;
+  if (threadIdx.x == 0) not_prob[two_slots ? (slot ^ 1) : 0] = 0;  // (two words: the next update's)
 }
 
 void check_states(const at::Tensor& ws, std::initializer_list<const at::Tensor*> states, long long n, const char* what) {
@@ -153,7 +155,8 @@ void bin_stats_forward(at::Tensor ws, at::Tensor not_prob, at::Tensor tp, at::Te
   hipLaunchKernelGGL(bin_stats_forward_kernel, dim3(1), dim3(kThreads), 0, stream(), ws.data_ptr<int64_t>(),
                      static_cast<int>(L), not_prob.data_ptr<int>(), tp.data_ptr<int64_t>(), fp.data_ptr<int64_t>(),
                      tn.data_ptr<int64_t>(), fn.data_ptr<int64_t>(), static_cast<int>(kind), static_cast<int>(average),
-                     static_cast<float>(beta * beta), out.data_ptr<float>());
+                     static_cast<float>(beta * beta), out.data_ptr<float>(), notprob_current(not_prob),
+                     not_prob.numel() >= 2);
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 

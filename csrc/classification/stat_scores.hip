@@ -11,6 +11,9 @@
 // Small histograms are privatised in LDS (one int32 sub-histogram per block) and flushed with 64-bit atomics.
 #include "../common/tm_common.h"
 
+#include <mutex>
+#include <unordered_map>
+
 #include <cstdlib>
 
 namespace tm_amd {
@@ -24,7 +27,9 @@ constexpr long long kFinalizeOneBlock = 8192;  // label groups a single finalize
 // ----------------------------------------------------------------------------------------------------------------
 // multiclass: per-item predicted label
 // ----------------------------------------------------------------------------------------------------------------
-enum McMode : int { kMcConfmat = 0, kMcStats = 1, kMcConfmatDual = 2 };  // dual: the batch matrix and the global one
+enum McMode : int { kMcConfmat = 0, kMcStats = 1, kMcConfmatDual = 2, kMcStatsDirect = 3 };
+// dual: the batch matrix and the global one; stats-direct: straight into the tp / fp / tn / fn states (see
+// mc_stats_direct)
 
 template <typename target_t>
 __device__ __forceinline__ bool mc_target(const target_t* __restrict__ target, long long item, int C, long long ignore,
@@ -243,8 +248,16 @@ __global__ void __launch_bounds__(kOrdBlock) mc_argmax_ord16_kernel(const scalar
                                                                  const target_t* __restrict__ target, long long N,
                                                                  int C, long long ignore, bool has_ignore,
                                                                  int64_t* __restrict__ out, int* __restrict__ flag,
-                                                                 int64_t* __restrict__ out2 = nullptr) {
+                                                                 int64_t* __restrict__ out2 = nullptr,
+                                                                 int64_t* __restrict__ tn_st = nullptr,
+                                                                 int64_t* __restrict__ fn_st = nullptr,
+                                                                 long long tn_all = 0) {
   static_assert(sizeof(scalar_t) == 2, "16-bit floats only");
+  if constexpr (kMode == kMcStatsDirect) {
+    // every class gains a true negative per row of the batch; the rows' own classes give theirs back below
+    if (blockIdx.x == 0)
+      for (int c = threadIdx.x; c < C; c += blockDim.x) atomic_add_i64(tn_st + c, tn_all);
+  }
   const int lane = threadIdx.x & (kWave - 1);
   const long long nwaves = static_cast<long long>(gridDim.x) * (blockDim.x / kWave);
   const long long wave = (static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
@@ -339,6 +352,15 @@ __global__ void __launch_bounds__(kOrdBlock) mc_argmax_ord16_kernel(const scalar
         } else if constexpr (kMode == kMcConfmatDual) {  // forward(): the batch value and the global state at once
           atomic_add_i64(out + static_cast<long long>(t) * C + bidx, 1);
           atomic_add_i64(out2 + static_cast<long long>(t) * C + bidx, 1);
+        } else if constexpr (kMode == kMcStatsDirect) {  // out = tp, out2 = fp
+          atomic_add_i64(tn_st + t, -1);
+          if (bidx == t) {
+            atomic_add_i64(out + t, 1);
+          } else {
+            atomic_add_i64(out2 + bidx, 1);
+            atomic_add_i64(fn_st + t, 1);
+            atomic_add_i64(tn_st + bidx, -1);
+          }
         } else {  // stats workspace [tp | fp | fn | -]: a hit or a miss of the target class (+ the predicted class)
           if (bidx == t) {
             atomic_add_i64(out + t, 1);
@@ -1317,8 +1339,9 @@ __global__ void __launch_bounds__(kBlock) bin_finalize_kernel(int64_t* __restric
                                                               int* __restrict__ not_prob, bool accumulate,
                                                               int64_t* __restrict__ tp, int64_t* __restrict__ fp,
                                                               int64_t* __restrict__ tn, int64_t* __restrict__ fn,
-                                                              bool zero_np) {
-  const bool use_b = *not_prob != 0;
+                                                              bool zero_np, int slot, bool two_slots) {
+  const bool use_b = not_prob[slot] != 0;
+  if (two_slots && blockIdx.x == 0 && threadIdx.x == 0) not_prob[slot ^ 1] = 0;  // the next update's word
   for (long long g = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; g < G;
        g += static_cast<long long>(gridDim.x) * blockDim.x) {
     int64_t* w = ws + g * kBinSlots;
@@ -1343,8 +1366,10 @@ __global__ void __launch_bounds__(kBlock) bin_finalize_kernel(int64_t* __restric
 // binary / multilabel confusion matrices [G, 2, 2] (rows = target, cols = pred) accumulated in place
 __global__ void __launch_bounds__(kBlock) bin_confmat_finalize_kernel(int64_t* __restrict__ ws, long long G,
                                                                       int* __restrict__ not_prob,
-                                                                      int64_t* __restrict__ confmat, bool zero_np) {
-  const bool use_b = *not_prob != 0;
+                                                                      int64_t* __restrict__ confmat, bool zero_np,
+                                                                      int slot, bool two_slots) {
+  const bool use_b = not_prob[slot] != 0;
+  if (two_slots && blockIdx.x == 0 && threadIdx.x == 0) not_prob[slot ^ 1] = 0;
   for (long long g = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; g < G;
        g += static_cast<long long>(gridDim.x) * blockDim.x) {
     int64_t* w = ws + g * kBinSlots;
@@ -1366,10 +1391,34 @@ __global__ void __launch_bounds__(kBlock) bin_confmat_finalize_kernel(int64_t* _
   }
 }
 
-// reset of the per-call logit flag is ordered after the finalize (same stream)
+// reset of the per-call logit flag is ordered after the finalize (same stream) -- only for one-word flags
 __global__ void zero_int_kernel(int* p) { *p = 0; }
 
 }  // namespace
+
+// The "scores are not probabilities" word of the binary / multilabel path, double-buffered by update parity when the
+// caller gives two words (the _StatWorkspace does): bin_update ORs into word `slot`, the finalize reads it and clears
+// word `slot ^ 1` for the next update -- a multi-block finalize needs no extra one-thread launch to re-arm the word.
+// The parity is kept here per word address; a one-word buffer keeps the old single-slot protocol.
+namespace {
+std::mutex g_np_mu;
+std::unordered_map<const void*, int> g_np_slot;
+}  // namespace
+
+int notprob_begin(const at::Tensor& np) {
+  if (np.numel() < 2) return 0;
+  std::lock_guard<std::mutex> lock(g_np_mu);
+  int& s = g_np_slot[np.data_ptr()];
+  s ^= 1;
+  return s;
+}
+
+int notprob_current(const at::Tensor& np) {
+  if (np.numel() < 2) return 0;
+  std::lock_guard<std::mutex> lock(g_np_mu);
+  auto it = g_np_slot.find(np.data_ptr());
+  return it == g_np_slot.end() ? 0 : it->second;
+}
 
 // ================================================================================================================
 // host launchers
@@ -1575,6 +1624,59 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
+// MulticlassStatScores-family update (top_k = 1, global, per-class states, no ignore_index) on 16-bit logits with
+// rows of >= 1 KiB (the order-key kernel's shape): ONE launch straight into the int64 states, instead of the
+// workspace pass + mc_finalize_kernel.  Per valid row: tp[t] or (fp[argmax], fn[t]); tn[c] += N for every class (block
+// 0) and -1 for the row's target and predicted classes -- tn = rows - tp - fp - fn per class without a count.  A
+// target out of range raises the flag (compute() raises) and its row is skipped.  Returns false, doing nothing,
+// anywhere else (the caller takes mc_update + mc_stats_finalize).
+bool mc_stats_direct(const at::Tensor& preds, const at::Tensor& target, at::Tensor tp, at::Tensor fp, at::Tensor tn,
+                     at::Tensor fn, at::Tensor flag, int64_t num_classes) {
+  const long long C = num_classes;
+  if (!preds.is_cuda() || preds.dim() != 2 || target.dim() != 1 || preds.size(1) != C || preds.size(0) != target.size(0))
+    return false;
+  if (preds.scalar_type() != at::kBFloat16 && preds.scalar_type() != at::kHalf) return false;
+  if (target.scalar_type() != at::kLong && target.scalar_type() != at::kInt) return false;
+  if (!preds.is_contiguous() || !target.is_contiguous() || reinterpret_cast<uintptr_t>(preds.data_ptr()) % 16 != 0)
+    return false;
+  const long long row_bytes = C * 2;
+  if (row_bytes % 16 != 0 || row_bytes < 1024 || row_bytes > 4 * 1024) return false;
+  for (const at::Tensor* t : {&tp, &fp, &tn, &fn})
+    if (!t->is_cuda() || t->get_device() != preds.get_device() || t->scalar_type() != at::kLong ||
+        !t->is_contiguous() || t->numel() != C)
+      return false;
+  static const bool off = std::getenv("TM_AMD_MC_STATS_DIRECT") && std::atoi(std::getenv("TM_AMD_MC_STATS_DIRECT")) == 0;
+  if (off) return false;
+  const long long N = preds.size(0);
+  if (N == 0) return true;
+  auto s = stream();
+  const int cus = cu_count(preds.get_device());
+  const long long want16 = (N + kOrdBlock / kWave - 1) / (kOrdBlock / kWave);
+  const int grid16 = static_cast<int>(std::min<long long>(want16, static_cast<long long>(cus) * 4));
+  const int per = static_cast<int>((row_bytes / 16 + kWave - 1) / kWave);
+  TM_DISPATCH_TARGET(target.scalar_type(), "mc_stats_direct", [&] {
+    const target_t* tg = reinterpret_cast<const target_t*>(target.data_ptr());
+    auto go = [&](auto scalar_tag, auto per_tag) {
+      using scalar_t = decltype(scalar_tag);
+      constexpr int P = decltype(per_tag)::value;
+      hipLaunchKernelGGL((mc_argmax_ord16_kernel<scalar_t, target_t, P, kMcStatsDirect>), dim3(grid16),
+                         dim3(kOrdBlock), 0, s, reinterpret_cast<const scalar_t*>(preds.data_ptr()), tg, N,
+                         static_cast<int>(C), 0LL, false, tp.data_ptr<int64_t>(), flag.data_ptr<int>(),
+                         fp.data_ptr<int64_t>(), tn.data_ptr<int64_t>(), fn.data_ptr<int64_t>(), N);
+    };
+    auto by_per = [&](auto scalar_tag) {
+      if (per == 1) go(scalar_tag, std::integral_constant<int, 1>{});
+      else if (per == 2) go(scalar_tag, std::integral_constant<int, 2>{});
+      else if (per == 3) go(scalar_tag, std::integral_constant<int, 3>{});
+      else go(scalar_tag, std::integral_constant<int, 4>{});
+    };
+    if (preds.scalar_type() == at::kBFloat16) by_per(c10::BFloat16{});
+    else by_per(c10::Half{});
+  });
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return true;
+}
+
 void mc_stats_finalize(at::Tensor ws, int64_t num_classes, bool micro, bool accumulate, at::Tensor tp, at::Tensor fp,
                        at::Tensor tn, at::Tensor fn) {
   TM_CHECK_CUDA(ws);
@@ -1665,6 +1767,7 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
   const long long G = samplewise ? N * L : L;
   TORCH_CHECK(ws.numel() == G * kBinSlots && ws.scalar_type() == at::kLong, "bin_update: bad workspace");
   auto s = stream();
+  int* const npw = not_prob.data_ptr<int>() + notprob_begin(not_prob);  // this update's "not probabilities" word
   TM_DISPATCH_TARGET(target.scalar_type(), "bin_update", [&] {
     const target_t* tp = reinterpret_cast<const target_t*>(target.data_ptr());
     TM_DISPATCH_PREDS(preds.scalar_type(), "bin_update", [&] {
@@ -1679,7 +1782,7 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
         TORCH_CHECK(blocks < (1LL << 31), "bin_update: too many segments");
         hipLaunchKernelGGL((bin_seg_kernel<scalar_t, target_t>), dim3(blocks), dim3(kBlock), 0, s, pp, tp, nseg, L, X,
                            chunk, thr_t, ignore_index, has_ignore, samplewise, ws.data_ptr<int64_t>(),
-                           flag.data_ptr<int>(), not_prob.data_ptr<int>(), prob_check_all);
+                           flag.data_ptr<int>(), npw, prob_check_all);
       } else if (vec_grid<scalar_t>(preds, target, L, X, samplewise, total, cu_count(preds.get_device())) > 0) {
         constexpr int VEC = 16 / sizeof(scalar_t);
         const int grid = static_cast<int>(vec_grid<scalar_t>(preds, target, L, X, samplewise, total,
@@ -1689,7 +1792,7 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
         if constexpr (VEC * sizeof(scalar_t) == 16) {
           hipLaunchKernelGGL((bin_vec_kernel<scalar_t, target_t, VEC>), dim3(grid), dim3(kVecBlock),
                              nbins * sizeof(int), s, pp, tp, total / VEC, static_cast<int>(L), thr_t, ignore_index,
-                             has_ignore, flag.data_ptr<int>(), not_prob.data_ptr<int>(), prob_check_all,
+                             has_ignore, flag.data_ptr<int>(), npw, prob_check_all,
                              partials.data_ptr<int>());
         }
         launch_partials_fold(partials.data_ptr<int>(), grid, static_cast<int>(nbins), ws.data_ptr<int64_t>(), s);
@@ -1703,7 +1806,7 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
         if (fold) partials = at::empty({grid * nbins}, ws.options().dtype(at::kInt));
         hipLaunchKernelGGL((bin_reg_kernel<scalar_t, target_t>), dim3(static_cast<unsigned>(grid)), dim3(kBlock), lds,
                            s, pp, tp, total, L, X, thr_t, ignore_index, has_ignore, ws.data_ptr<int64_t>(),
-                           fold ? partials.data_ptr<int>() : nullptr, flag.data_ptr<int>(), not_prob.data_ptr<int>(),
+                           fold ? partials.data_ptr<int>() : nullptr, flag.data_ptr<int>(), npw,
                            prob_check_all);
         if (fold)
           launch_partials_fold(partials.data_ptr<int>(), static_cast<int>(grid), static_cast<int>(nbins),
@@ -1720,7 +1823,7 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
         if (use_partials) partials = at::empty({static_cast<long long>(grid) * nbins}, ws.options().dtype(at::kInt));
         hipLaunchKernelGGL((bin_flat_kernel<scalar_t, target_t>), dim3(grid), dim3(kBlock), lds_bytes, s, pp, tp,
                            total, L, X, thr_t, ignore_index, has_ignore, samplewise, ws.data_ptr<int64_t>(),
-                           flag.data_ptr<int>(), not_prob.data_ptr<int>(), prob_check_all,
+                           flag.data_ptr<int>(), npw, prob_check_all,
                            use_partials ? partials.data_ptr<int>() : nullptr);
         if (use_partials)
           launch_partials_fold(partials.data_ptr<int>(), grid, static_cast<int>(nbins), ws.data_ptr<int64_t>(), s);
@@ -1739,11 +1842,13 @@ void bin_stats_finalize(at::Tensor ws, at::Tensor not_prob, bool accumulate, at:
     TORCH_CHECK(t->device() == ws.device() && t->scalar_type() == at::kLong && t->is_contiguous() && t->numel() == G,
                 "bin_stats_finalize: states must be contiguous int64 with G elements");
   auto s = stream();
+  const bool two = not_prob.numel() >= 2;  // double-buffered word: no re-arm launch
   const bool one = G <= kFinalizeOneBlock;  // one block folds and re-arms not_prob itself
   hipLaunchKernelGGL(bin_finalize_kernel, dim3(one ? 1 : grid_cap((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                      ws.data_ptr<int64_t>(), G, not_prob.data_ptr<int>(), accumulate, tp.data_ptr<int64_t>(),
-                     fp.data_ptr<int64_t>(), tn.data_ptr<int64_t>(), fn.data_ptr<int64_t>(), one);
-  if (!one) hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
+                     fp.data_ptr<int64_t>(), tn.data_ptr<int64_t>(), fn.data_ptr<int64_t>(), one && !two,
+                     notprob_current(not_prob), two);
+  if (!one && !two) hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
@@ -1756,9 +1861,11 @@ void bin_confmat_finalize(at::Tensor ws, at::Tensor not_prob, at::Tensor confmat
               "bin_confmat_finalize: confmat must be contiguous int64 [G, 2, 2]");
   auto s = stream();
   const bool one = G <= kFinalizeOneBlock;
+  const bool two = not_prob.numel() >= 2;
   hipLaunchKernelGGL(bin_confmat_finalize_kernel, dim3(one ? 1 : grid_cap((G + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                     s, ws.data_ptr<int64_t>(), G, not_prob.data_ptr<int>(), confmat.data_ptr<int64_t>(), one);
-  if (!one) hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
+                     s, ws.data_ptr<int64_t>(), G, not_prob.data_ptr<int>(), confmat.data_ptr<int64_t>(),
+                     one && !two, notprob_current(not_prob), two);
+  if (!one && !two) hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 

@@ -69,12 +69,18 @@ class MetricCollection(ModuleDict):
 
     def update(self, *args: Any, **kwargs: Any) -> None:
         """Update every metric (only the first member of each compute group once groups are known)."""
-        if self._groups_checked:
+        if self._groups_checked or not self._enable_compute_groups:
+            names = [cg[0] for cg in self._groups.values()] if self._groups_checked else list(self._modules.keys())
+            # few-class multiclass leaders on the same (preds, target): ONE fused pass for all of them
+            # (utils/fused_update.py, csrc/classification/family.hip)
+            done = self._fused_update(names, args, kwargs)
             # streaming regression leaders hand their moments requests to `sink`; requests on the same inputs are
             # then merged into one kernel pass for the whole collection (ops.run_moments_plans)
             sink: list = []
-            for cg in self._groups.values():
-                m0 = getattr(self, cg[0])
+            for name in names:
+                m0 = getattr(self, name)
+                if done and id(m0) in done:
+                    continue
                 d = m0.__dict__
                 d["_moments_sink"] = sink
                 try:
@@ -83,7 +89,7 @@ class MetricCollection(ModuleDict):
                     del d["_moments_sink"]
             if sink:
                 ops.run_moments_plans(sink)
-            if self._state_is_copy:
+            if self._state_is_copy and self._groups_checked:
                 self._compute_groups_create_state_ref()
                 self._state_is_copy = False
         else:
@@ -93,6 +99,28 @@ class MetricCollection(ModuleDict):
                 self._merge_compute_groups()
                 self._compute_groups_create_state_ref()
                 self._groups_checked = True
+
+    def _fused_update(self, names: List[str], args: tuple, kwargs: dict) -> Optional[set]:
+        """Run the fused few-class multiclass update (utils/fused_update.py) for the leaders it serves; returns the
+        ids of the metrics it updated (None: nothing fused)."""
+        if kwargs or len(args) != 2 or not isinstance(args[0], Tensor) or not args[0].is_cuda:
+            return None
+        from torchmetrics_amd.utils import fused_update as _fu
+        from torchmetrics_amd.utils import validation as _validation
+
+        if _validation.STRICT:  # the reference's per-update raises: every member validates on its own
+            return None
+
+        d = self.__dict__
+        ident = tuple(id(self._modules[n]) for n in names)
+        entry = d.get("_family_plan")
+        if entry is None or entry[0] != ident or not entry[1].valid(None):
+            entry = (ident, _fu.FamilyPlan([(n, self._modules[n]) for n in names]))
+            d["_family_plan"] = entry
+        plan = entry[1]
+        if not plan.ok or not plan.run(args[0], args[1]):
+            return None
+        return {id(m) for m in plan.metrics}
 
     def _merge_compute_groups(self) -> None:
         """Merge groups whose leaders hold identical states (O(M^2) pairwise, once)."""
@@ -292,7 +320,8 @@ class MetricCollection(ModuleDict):
         # process-local handles: the mapped pinned status buffer (its device address) and the fused-compute plan
         # (descriptor rows holding device pointers) are rebuilt on first use in the copy
         state = self.__dict__.copy()
-        for k in ("_status_host", "_status_ptr", "_fused_plan", "_compute_calls", "_fused_rebuilds", "_fused_off"):
+        for k in ("_status_host", "_status_ptr", "_fused_plan", "_compute_calls", "_fused_rebuilds", "_fused_off",
+                  "_family_plan"):
             state.pop(k, None)
         return state
 

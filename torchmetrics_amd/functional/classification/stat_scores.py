@@ -177,7 +177,8 @@ class _StatWorkspace:
     def get(self, numel: int, device: torch.device) -> Tuple[Tensor, Tensor]:
         if self.ws is None or self.ws.numel() != numel or self.ws.device != device:
             self.ws = torch.zeros(numel, dtype=torch.int64, device=device)
-            self.not_prob = torch.zeros(1, dtype=torch.int32, device=device)
+            # two words, double-buffered by update parity (csrc/classification/stat_scores.hip notprob_begin)
+            self.not_prob = torch.zeros(2, dtype=torch.int32, device=device)
         return self.ws, self.not_prob  # type: ignore[return-value]
 
 

@@ -145,7 +145,7 @@ def bin_update(preds: Tensor, target: Tensor, ws: Tensor, flag: Tensor, not_prob
 def bin_stats_finalize(ws: Tensor, not_prob: Tensor, accumulate: bool, tp: Tensor, fp: Tensor, tn: Tensor,
                        fn: Tensor) -> None:
     w = ws.view(-1, 7)
-    off = 3 if int(not_prob.item()) else 0
+    off = 3 if int(not_prob.reshape(-1)[0].item()) else 0
     a, b, d = w[:, off], w[:, off + 1], w[:, off + 2]
     e = w[:, 6] - a - b - d
     for dst, src in ((tp, a), (fp, b), (fn, d), (tn, e)):
@@ -160,7 +160,7 @@ def bin_stats_finalize(ws: Tensor, not_prob: Tensor, accumulate: bool, tp: Tenso
 
 def bin_confmat_finalize(ws: Tensor, not_prob: Tensor, confmat: Tensor) -> None:
     w = ws.view(-1, 7)
-    off = 3 if int(not_prob.item()) else 0
+    off = 3 if int(not_prob.reshape(-1)[0].item()) else 0
     tp, fp, fn = w[:, off], w[:, off + 1], w[:, off + 2]
     tn = w[:, 6] - tp - fp - fn
     confmat.view(-1, 4).add_(torch.stack([tn, fp, fn, tp], dim=1))

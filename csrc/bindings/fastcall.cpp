@@ -647,6 +647,24 @@ bool states_unobserved(PyObject* st, std::initializer_list<PyObject*> keys) {
   return states_unobserved_why(st, keys, nullptr, nullptr);
 }
 
+// _sole_ref(d: dict, key) -> bool: d[key] is a Tensor whose Python object nothing but `d` references.  Read from C with
+// the object fetched from the dict (borrowed), the count is exactly the strong references to the object -- no
+// argument / local-variable / interpreter-version convention enters it (sys.getrefcount counts its own argument and
+// the caller's locals, and CPython changes what the eval stack holds across versions).  The metric's reset() and
+// forward() ask this BEFORE binding the tensor to a local.
+PyObject* sole_ref(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 2 || !PyDict_Check(args[0])) {
+    PyErr_SetString(PyExc_TypeError, "_sole_ref(d: dict, key)");
+    return nullptr;
+  }
+  PyObject* o = PyDict_GetItemWithError(args[0], args[1]);  // borrowed
+  if (o == nullptr) {
+    if (PyErr_Occurred()) return nullptr;
+    Py_RETURN_FALSE;
+  }
+  return PyBool_FromLong(THPVariable_Check(o) && Py_REFCNT(o) == 1);
+}
+
 // _states_unobserved(state_dict, keys) -> (ok, why, detail): the forward's aliasing test on its own (tests, diagnostics)
 PyObject* states_unobserved_probe(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   if (nargs != 2 || !PyDict_Check(args[0]) || !PyTuple_Check(args[1])) {
@@ -1202,6 +1220,8 @@ PyMethodDef kFactoryMethods[] = {
      "MeanAveragePrecision.update's per-image validation and packing in one native call"},
     {"set_ranges", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&set_ranges)), METH_FASTCALL,
      "turn the roctx ranges of the native update / forward entry points on or off"},
+    {"_sole_ref", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&sole_ref)), METH_FASTCALL,
+     "whether a dict entry is a tensor referenced by nothing but that dict"},
     {"_states_unobserved", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&states_unobserved_probe)),
      METH_FASTCALL, "the native forward's test that nothing outside the metric holds the given states"},
     {nullptr, nullptr, 0, nullptr},

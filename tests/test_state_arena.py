@@ -350,3 +350,44 @@ def test_reset_never_zeroes_a_handed_out_state(hand_out):
     before = held.clone()
     m.reset()
     assert torch.equal(held, before)
+
+
+@pytest.mark.parametrize("hand_out", ["attr", "metric_state", "state_dict", "in_list", "in_dict", "compute_result"])
+def test_forward_never_mutates_a_handed_out_state_object(hand_out):
+    """forward()'s in-place fold must not change a state OBJECT (not a view) the user holds through any hand-out path,
+    including containers; the guard is the exact strong-reference count read from C (ops.sole_ref), not
+    sys.getrefcount's version-dependent conventions."""
+    p, t = _data(3)
+    m = tm.MulticlassConfusionMatrix(5) if hand_out == "compute_result" else tm.MulticlassStatScores(5, average=None)
+    m.persistent(True)
+    m.update(p, t)
+    key = "confmat" if hand_out == "compute_result" else "tp"
+    get = {"attr": lambda: getattr(m, key), "metric_state": lambda: m.metric_state[key],
+           "state_dict": lambda: m.state_dict(keep_vars=True)[key], "in_list": lambda: [getattr(m, key)],
+           "in_dict": lambda: {"x": getattr(m, key)}, "compute_result": lambda: m.compute()}[hand_out]
+    held = get()
+    obj = held[0] if hand_out == "in_list" else held["x"] if hand_out == "in_dict" else held
+    before = obj.clone()
+    del obj
+    m(p, t)
+    obj = held[0] if hand_out == "in_list" else held["x"] if hand_out == "in_dict" else held
+    assert torch.equal(obj, before)
+    m.reset()
+    assert torch.equal(obj, before)
+
+
+def test_sole_ref_probe_counts_every_holder():
+    from torchmetrics_amd import ops
+
+    if not ops.native_available():
+        pytest.skip("native library not built")
+    d = {"x": torch.zeros(3)}
+    assert ops.sole_ref(d, "x")
+    held = [d["x"]]
+    assert not ops.sole_ref(d, "x")
+    held.clear()
+    assert ops.sole_ref(d, "x")
+    y = d["x"]
+    assert not ops.sole_ref(d, "x")
+    del y
+    assert ops.sole_ref(d, "x") and not ops.sole_ref(d, "missing") and not ops.sole_ref({"a": 1}, "a")

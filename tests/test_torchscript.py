@@ -89,9 +89,23 @@ def test_scripting_with_native_entry_points(make):
     m = make().cuda()
     p, t = torch.randn(16, 5, device="cuda"), torch.randint(0, 5, (16,), device="cuda")
     m(p, t)
+    fwd, upd = type(m.forward).__name__, type(m.update).__name__
+    calls = m.update.native_calls if upd == "NativeUpdate" else None
     torch.jit.script(m)
-    m(p, t)  # the Python entry points took over: still correct
+    # scripting works on a copy: the eager metric keeps its native entry points and they keep running
+    assert type(m.forward).__name__ == fwd and type(m.update).__name__ == upd
+    m(p, t)
+    if calls is not None:
+        m.update(p, t)
+        assert m.update.native_calls > calls
+        m2 = make().cuda()
+        m2(p, t)
+        m2(p, t)
+        m2.update(p, t)
+        m = m2
     ref = make()
     ref(p.cpu(), t.cpu())
     ref(p.cpu(), t.cpu())
+    if calls is not None:
+        ref.update(p.cpu(), t.cpu())
     torch.testing.assert_close(m.compute().cpu(), ref.compute())

@@ -410,15 +410,17 @@ class Metric(Module, ABC):
         for attr in list(global_state):
             if self._reductions[attr] is not dim_zero_sum:
                 continue
+            # nothing but global_state may hold the global tensor object (a returned compute() result, a compute-group
+            # sibling or a user handle keeps the out-of-place merge); asked before `glob` binds it to a local
+            sole = _ops.sole_ref(global_state, attr)
             glob = global_state[attr]
             local = getattr(self, attr)
             if (not isinstance(glob, Tensor) or not isinstance(local, Tensor) or glob.requires_grad
                     or local.requires_grad or glob.layout != torch.strided or glob.shape != local.shape
                     or glob.dtype != torch.promote_types(glob.dtype, local.dtype) or glob.device != local.device):
                 continue
-            # references: global_state's entry, this local, getrefcount's argument (catches the same tensor object
-            # held elsewhere); the storage use count catches views of it (+1: the temporary storage handle)
-            if sys.getrefcount(glob) > 3:
+            # the storage use count catches views of it (+1: the temporary storage handle)
+            if not sole:
                 continue
             stor = glob.untyped_storage()
             if torch._C._storage_Use_Count(stor._cdata) > 1 + len(views.get(stor.data_ptr(), ())):
@@ -870,11 +872,12 @@ class Metric(Module, ABC):
         t = own = None  # (the loop variables would count as references below)
         fresh: Dict[Tuple[Any, torch.dtype, torch.device], List[str]] = {}
         for attr, default in self._defaults.items():
+            # nothing but the metric's __dict__ may hold the state object (asked before `cur` binds it)
+            sole = isinstance(default, Tensor) and _ops.sole_ref(d, attr)
             cur = d[attr] if attr in d else getattr(self, attr)
             if isinstance(default, Tensor):
-                # references: the state dict's entry, this local, getrefcount's argument -- nothing else
                 allowed = 1 + len(views.get(cur.untyped_storage().data_ptr(), ())) if cur.layout == torch.strided else 2
-                if not (sys.getrefcount(cur) <= 3 and self._refill_in_place(cur, default, allowed)):
+                if not (sole and self._refill_in_place(cur, default, allowed)):
                     key = (_arena._reduce_kind(self._reductions[attr]), default.dtype, cur.device)
                     fresh.setdefault(key, []).append(attr)
             else:
@@ -1030,15 +1033,21 @@ class Metric(Module, ABC):
 
     def __prepare_scriptable__(self) -> "Metric":
         """``torch.jit.script`` compiles the class's methods; the native C++ entry points installed as instance
-        attributes (``csrc/bindings/fastcall.cpp`` NativeUpdate / NativeForward) are not Python functions, so they are
-        taken off this instance first (its Python ``update`` / ``forward`` take over: same results)."""
-        d = self.__dict__
+        attributes (``csrc/bindings/fastcall.cpp`` NativeUpdate / NativeForward) are not Python functions, so the
+        module handed to the compiler is a shallow COPY without them (its Python ``update`` / ``forward`` take over:
+        same results, the same state tensors).  The eager metric itself keeps its native entry points: scripting it
+        once does not take the fast path away for the rest of the run.  The copy gets its own ``_modules`` dict, which
+        the compiler's recursion may rewrite."""
+        clone = object.__new__(type(self))
+        d = clone.__dict__
+        d.update(self.__dict__)
+        d["_modules"] = type(self._modules)(self._modules)
         if type(d.get("forward")).__name__ == "NativeForward":
             del d["forward"]
         if type(d.get("update")).__name__ == "NativeUpdate":
             d["update"] = d["update"].fallback
         d.pop("_default_packs", None)  # a cache keyed by (names, device) tuples, which TorchScript cannot type
-        return self
+        return clone
 
     def _install_native_update(self) -> None:
         """Hook: classes with a native ``update`` entry point install it over the Python wrapper here."""

@@ -123,6 +123,19 @@ def read_word(word: Tensor) -> int:
     return int(word.reshape(-1)[0].item())
 
 
+def sole_ref(d: dict, key: Any) -> bool:
+    """Whether ``d[key]`` is a tensor whose Python object is referenced by ``d`` alone (``_sole_ref`` in
+    ``csrc/bindings/fastcall.cpp``: the exact strong-reference count, read from C).  Without the native module:
+    False (callers then take their always-correct out-of-place path)."""
+    mod = _fast_mod
+    if mod is None:
+        if not native_available():
+            return False
+        mod = _fast()
+    fn = getattr(mod, "_sole_ref", None)
+    return bool(fn(d, key)) if fn is not None else False
+
+
 def native_library_path() -> Path:
     return _LIB_PATH
 

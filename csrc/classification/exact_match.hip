@@ -210,7 +210,11 @@ __global__ void __launch_bounds__(kBlock) em_multiclass_pos_kernel(const scalar_
 
 // multilabel: preds / target [N, L, P]; unit u = (n, p); ws: i64 [2] (global: reading A, B) or [2N] (samplewise:
 // per-sample counts of correct positions, A then B); notprob: i32 [1]
-template <typename scalar_t, typename target_t>
+//
+// kLabels (kind 2, multiclass labels [N, L] with P = 1): an ignored position counts as a match (the reference writes
+// ignore_index into preds there), float labels compare exactly in the scores' dtype (`preds == target` promotes the
+// integer target to it), and there is one reading.
+template <typename scalar_t, typename target_t, bool kLabels>
 __global__ void __launch_bounds__(kBlock) em_multilabel_kernel(const scalar_t* __restrict__ preds,
                                                                const target_t* __restrict__ target, long long N,
                                                                int L, long long P, float thr, long long ignore,
@@ -228,7 +232,18 @@ __global__ void __launch_bounds__(kBlock) em_multilabel_kernel(const scalar_t* _
     for (int l = 0; l < L; ++l) {
       const long long t = static_cast<long long>(tr[static_cast<long long>(l) * P]);
       const scalar_t v = pr[static_cast<long long>(l) * P];
-      if constexpr (IsFloating<scalar_t>::value) {
+      if constexpr (kLabels) {
+        if (has_ignore && t == ignore) continue;
+        bool eq;
+        if constexpr (std::is_same<scalar_t, double>::value)
+          eq = v == static_cast<double>(t);
+        else if constexpr (IsFloating<scalar_t>::value)
+          eq = to_f32(v) == to_f32(scalar_t(static_cast<float>(t)));
+        else
+          eq = static_cast<long long>(v) == t;
+        oka &= eq;
+        okb &= eq;
+      } else if constexpr (IsFloating<scalar_t>::value) {
         const float x = to_f32(v);
         np |= !(x >= 0.f && x <= 1.f);  // the reference decides over every score, ignored positions included
         // reference semantics (_multilabel_stat_scores_format): an ignored target becomes -1 while the prediction
@@ -252,13 +267,13 @@ __global__ void __launch_bounds__(kBlock) em_multilabel_kernel(const scalar_t* _
     }
     if (samplewise) {
       if (oka) atomic_add_i64(ws + n, 1);
-      if (okb) atomic_add_i64(ws + N + n, 1);
+      if (!kLabels && okb) atomic_add_i64(ws + N + n, 1);
     } else {
       ca += oka;
       cb += okb;
     }
   }
-  if (__any(np) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(notprob, 1);
+  if (!kLabels && __any(np) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(notprob, 1);
   if (!samplewise) block_add_counts(ca, cb, ws, ws + 1);
 }
 
@@ -291,7 +306,7 @@ __global__ void em_reset_notprob_kernel(int* notprob) { *notprob = 0; }
 }  // namespace
 
 // kind 0 multiclass (preds [N, C, P] scores, has_c; target [N, P]); kind 1 multilabel (preds / target [N, L, P];
-// C = L; also multiclass integer labels as L = positions, P = 1).  ws: i64 zeroed, [max(2, 2N)]; notprob: i32 [1] zero.  Global: correct / total
+// C = L); kind 2 multiclass labels of any dtype (preds / target [N, L], C = L positions, P = 1).  ws: i64 zeroed, [max(2, 2N)]; notprob: i32 [1] zero.  Global: correct / total
 // i64 [1] states updated in place (total += N for multiclass, N * P for multilabel).  Samplewise: out i64 [N] receives
 // the per-sample counts (0/1 multiclass, correct positions multilabel).
 void exact_match_update(const at::Tensor& preds, const at::Tensor& target, int64_t kind, int64_t C, int64_t P,
@@ -303,9 +318,9 @@ void exact_match_update(const at::Tensor& preds, const at::Tensor& target, int64
     TM_SAME_DEVICE(preds, (*t));
   TM_CHECK_CONTIG(preds);
   TM_CHECK_CONTIG(target);
-  TORCH_CHECK(kind == 0 || kind == 1, "exact_match_update: bad kind");
-  // multiclass labels are the multilabel integer case with L = P positions and one unit per sample
-  TORCH_CHECK(kind == 1 || has_c, "exact_match_update: multiclass labels go through kind 1 (L = P, P = 1)");
+  TORCH_CHECK(kind == 0 || kind == 1 || kind == 2, "exact_match_update: bad kind");
+  TORCH_CHECK((kind == 0) == has_c, "exact_match_update: only multiclass scores (kind 0) carry a class dimension");
+  TORCH_CHECK(kind != 2 || P == 1, "exact_match_update: multiclass labels are one unit per sample (P = 1)");
   TORCH_CHECK(C >= 1 && P >= 1, "exact_match_update: C and P must be positive");
   const long long N = P > 0 ? target.numel() / (kind == 0 ? P : C * P) : 0;
   TORCH_CHECK(target.numel() == N * (kind == 0 ? P : C * P), "exact_match_update: target shape");
@@ -355,17 +370,22 @@ void exact_match_update(const at::Tensor& preds, const at::Tensor& target, int64
                              dim3(grid_cap((N + (kBlock / kWave) - 1) / (kBlock / kWave), 2048)), dim3(kBlock), 0,
                              s, p, t, N, static_cast<int>(C), static_cast<long long>(P), ig, has_ignore,
                              samplewise, w);
-        } else {
-          hipLaunchKernelGGL((em_multilabel_kernel<scalar_t, target_t>),
+        } else if (kind == 1) {
+          hipLaunchKernelGGL((em_multilabel_kernel<scalar_t, target_t, false>),
                              dim3(grid_cap((N * P + kBlock - 1) / kBlock, 2048)), dim3(kBlock), 0, s, p, t, N,
                              static_cast<int>(C), static_cast<long long>(P), thr, ig,
                              has_ignore, samplewise, w, notprob.data_ptr<int>());
+        } else {
+          hipLaunchKernelGGL((em_multilabel_kernel<scalar_t, target_t, true>),
+                             dim3(grid_cap((N + kBlock - 1) / kBlock, 2048)), dim3(kBlock), 0, s, p, t, N,
+                             static_cast<int>(C), 1LL, thr, ig, has_ignore, samplewise, w,
+                             notprob.data_ptr<int>());
         }
       });
     });
   }
   const bool two = kind == 1;
-  const long long total_add = kind == 0 ? N : N * P;
+  const long long total_add = kind == 1 ? N * P : N;
   if (samplewise) {
     if (N > 0)
       hipLaunchKernelGGL(em_fold_kernel, dim3(grid_cap((N + 255) / 256, 1024)), dim3(256), 0, s, w, N, true, two,

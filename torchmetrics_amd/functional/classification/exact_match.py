@@ -2,6 +2,7 @@
 
 Reference: ``F/classification/exact_match.py:32-258``.
 """
+import math
 from typing import Optional, Tuple
 
 import torch
@@ -41,8 +42,10 @@ def _exact_match_fused(
 ) -> Optional[Tuple[Tensor, Tensor]]:
     """ROCm path (``csrc/classification/exact_match.hip``) on the unformatted inputs: argmax / sigmoid-or-not /
     threshold / ignore / all-positions vote in one pass.  Global with ``correct`` / ``total`` given: the states are
-    updated in place.  Returns ``(correct, total)`` as the torch update would, or None when it does not apply (CPU
-    tensors, float multiclass labels)."""
+    updated in place.  Returns ``(correct, total)`` as the torch update would, or None (the caller's torch body runs)
+    only for CPU tensors and shapes the reference's validation rejects (``validate_args=False`` with mismatched
+    shapes, an argmax over zero classes).  Every ROCm input the reference accepts runs here: scores, integer and
+    float labels, ``ignore_index``, empty batches and zero-size position dims (those two in closed form)."""
     if not (preds.is_cuda and target.is_cuda and preds.device == target.device) or target.ndim < 1:
         return None
     n = target.shape[0]
@@ -51,26 +54,51 @@ def _exact_match_fused(
         if preds.shape != target.shape or preds.ndim < 2:
             return None
         kind, c, p = ops.EM_MULTILABEL, preds.shape[1], target[0].numel() // max(preds.shape[1], 1)
+        if preds.shape[1] == 0:
+            p = math.prod(target.shape[2:])
         total_val = (n * p) if not samplewise else p
-    elif preds.ndim == target.ndim + 1 and preds.dtype in _EM_FLOAT:
+    elif preds.ndim == target.ndim + 1:
+        if preds.shape[0] != n or preds.shape[2:] != target.shape[1:]:
+            return None
         kind, c, p = ops.EM_MULTICLASS, preds.shape[1], target[0].numel()
         total_val = n if not samplewise else 1
-    elif preds.ndim == target.ndim and preds.dtype not in _EM_FLOAT:
-        kind, c, p = ops.EM_MULTILABEL, target[0].numel(), 1  # integer labels: all positions of a sample equal
+    elif preds.ndim == target.ndim:
+        if preds.shape[0] != n or preds.numel() != target.numel():
+            return None
+        # labels of any dtype (float labels compare exactly, as `preds == target` does): one unit per sample
+        kind, c, p = ops.EM_LABELS, target[0].numel(), 1
         total_val = n if not samplewise else 1
     else:
         return None
+    dev = preds.device
     if n == 0 or c == 0 or p == 0:
-        return None
+        if kind == ops.EM_MULTICLASS and c == 0 and n and p:
+            return None  # argmax over zero classes: the reference's torch body raises
+        # closed form: every vote is over zero positions / labels (vacuously correct) or there are no units
+        if kind == ops.EM_MULTILABEL:
+            per_sample = p if c == 0 else 0
+        else:
+            per_sample = 1 if (p == 0 or c == 0) else 0
+        if samplewise:
+            return (torch.full((n,), per_sample, dtype=torch.int64, device=dev),
+                    torch.tensor(total_val, device=dev))
+        if correct is None:
+            correct = torch.zeros(1, dtype=torch.int64, device=dev)
+            total = torch.zeros(1, dtype=torch.int64, device=dev)
+        if n * per_sample:
+            correct.add_(n * per_sample)
+        if total_val:
+            total.add_(total_val)
+        return correct, total
     preds, target = preds.contiguous(), target.contiguous()
     if target.dtype not in (torch.int64, torch.int32, torch.uint8, torch.bool):
         target = target.long()
     if samplewise:
         out = ops.exact_match_update(preds, target, kind, c, p, threshold, ignore_index, True, owner)
-        return out, torch.tensor(total_val, device=preds.device)
+        return out, torch.tensor(total_val, device=dev)
     if correct is None:
-        correct = torch.zeros(1, dtype=torch.int64, device=preds.device)
-        total = torch.zeros(1, dtype=torch.int64, device=preds.device)
+        correct = torch.zeros(1, dtype=torch.int64, device=dev)
+        total = torch.zeros(1, dtype=torch.int64, device=dev)
     ops.exact_match_update(preds, target, kind, c, p, threshold, ignore_index, False, owner, correct, total)
     return correct, total
 

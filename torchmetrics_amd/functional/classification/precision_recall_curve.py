@@ -33,6 +33,14 @@ def _clf_curves(preds: Tensor, target: Tensor, tmode: int, pos_label: int = 1, i
     return _sorted.split_curves(out, preds.dtype)
 
 
+def _clf_pr_curves(preds: Tensor, target: Tensor, tmode: int,
+                   ignore_index: Optional[int] = None) -> Tuple[List[Tensor], List[Tensor], List[Tensor]]:
+    """Every column's PR curve from one sorted-curve launch and one ``[S, N + 1]`` epilogue; the per-class tensors
+    are views of it (``_sorted.pr_curves``)."""
+    out = _sorted.column_stats(preds, target, tmode, 1, ignore_index, ops.EMIT_CURVE)
+    return _sorted.pr_curves(out, preds.dtype)
+
+
 def _binary_clf_curve(
     preds: Tensor,
     target: Tensor,
@@ -384,12 +392,7 @@ def _multiclass_precision_recall_curve_compute(
         thres = thresholds
         tensor_state = True
     else:
-        precision_list, recall_list, thres_list = [], [], []
-        for f, t, th in zip(*_clf_curves(state[0], state[1], ops.CLF_T_OVR)[:3]):
-            res = _pr_from_clf(f, t, th)
-            precision_list.append(res[0])
-            recall_list.append(res[1])
-            thres_list.append(res[2])
+        precision_list, recall_list, thres_list = _clf_pr_curves(state[0], state[1], ops.CLF_T_OVR)
         tensor_state = False
     if average == "macro":
         if tensor_state:
@@ -529,13 +532,7 @@ def _multilabel_precision_recall_curve_compute(
         precision, recall = _pr_from_confmat(state)
         ones = torch.ones(1, num_labels, dtype=precision.dtype, device=precision.device)
         return torch.cat([precision, ones]).T, torch.cat([recall, torch.zeros_like(ones)]).T, thresholds
-    precision_list, recall_list, thres_list = [], [], []
-    for f, t, th in zip(*_clf_curves(state[0], state[1], ops.CLF_T_ELEM, 1, ignore_index)[:3]):
-        res = _pr_from_clf(f, t, th)
-        precision_list.append(res[0])
-        recall_list.append(res[1])
-        thres_list.append(res[2])
-    return precision_list, recall_list, thres_list
+    return _clf_pr_curves(state[0], state[1], ops.CLF_T_ELEM, ignore_index)
 
 
 def _multilabel_curve_state(

@@ -21,6 +21,7 @@ from torchmetrics_amd.functional.classification.precision_recall_curve import (
     _task_dispatch,
 )
 from torchmetrics_amd import ops
+from torchmetrics_amd.functional.classification import _sorted
 from torchmetrics_amd.utilities.compute import _safe_divide
 from torchmetrics_amd.utilities.prints import rank_zero_warn
 
@@ -28,6 +29,14 @@ from torchmetrics_amd.utilities.prints import rank_zero_warn
 def _rates_from_confmat(state: Tensor) -> Tuple[Tensor, Tensor]:
     tps, fps, fns, tns = state[..., 1, 1], state[..., 0, 1], state[..., 1, 0], state[..., 0, 0]
     return _safe_divide(fps, fps + tns), _safe_divide(tps, tps + fns)
+
+
+def _clf_roc_curves(preds: Tensor, target: Tensor, tmode: int,
+                    ignore_index: Optional[int] = None) -> Tuple[List[Tensor], List[Tensor], List[Tensor]]:
+    """Every column's ROC curve from one sorted-curve launch and one ``[S, N + 1]`` epilogue; the per-class tensors
+    are views of it (``_sorted.roc_curves``)."""
+    out = _sorted.column_stats(preds, target, tmode, 1, ignore_index, ops.EMIT_CURVE)
+    return _sorted.roc_curves(out, preds.dtype, warn=lambda msg: rank_zero_warn(msg, UserWarning))
 
 
 def _binary_roc_compute(
@@ -99,13 +108,7 @@ def _multiclass_roc_compute(
         fpr, tpr, thres = fpr.flip(0).T, tpr.flip(0).T, thresholds.flip(0)
         tensor_state = True
     else:
-        fpr_list, tpr_list, thres_list = [], [], []
-        fl, tl, hl, host = _clf_curves(state[0], state[1], ops.CLF_T_OVR)
-        for f, t, th, h in zip(fl, tl, hl, host):
-            res = _roc_from_clf(f, t, th, h[1], h[0])
-            fpr_list.append(res[0])
-            tpr_list.append(res[1])
-            thres_list.append(res[2])
+        fpr_list, tpr_list, thres_list = _clf_roc_curves(state[0], state[1], ops.CLF_T_OVR)
         tensor_state = False
     if average == "macro":
         if tensor_state:
@@ -139,14 +142,7 @@ def _multilabel_roc_compute(
     if isinstance(state, Tensor) and thresholds is not None:
         fpr, tpr = _rates_from_confmat(state)
         return fpr.flip(0).T, tpr.flip(0).T, thresholds.flip(0)
-    fpr_l, tpr_l, thr_l = [], [], []
-    fl, tl, hl, host = _clf_curves(state[0], state[1], ops.CLF_T_ELEM, 1, ignore_index)
-    for f, t, th, h in zip(fl, tl, hl, host):
-        res = _roc_from_clf(f, t, th, h[1], h[0])
-        fpr_l.append(res[0])
-        tpr_l.append(res[1])
-        thr_l.append(res[2])
-    return fpr_l, tpr_l, thr_l
+    return _clf_roc_curves(state[0], state[1], ops.CLF_T_ELEM, ignore_index)
 
 
 def multilabel_roc(

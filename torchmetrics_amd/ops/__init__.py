@@ -1640,15 +1640,15 @@ def group_stats_update(preds: Tensor, target: Tensor, groups: Tensor, num_groups
         ws[0], ws[1], tp, fp, tn, fn)
 
 
-EM_MULTICLASS, EM_MULTILABEL = 0, 1
+EM_MULTICLASS, EM_MULTILABEL, EM_LABELS = 0, 1, 2
 
 
 def exact_match_update(preds: Tensor, target: Tensor, kind: int, C: int, P: int, threshold: float,
                        ignore_index: Optional[int], samplewise: bool, owner: dict,
                        correct: Optional[Tensor] = None, total: Optional[Tensor] = None) -> Optional[Tensor]:
     """Exact-match update of contiguous ROCm inputs (``csrc/classification/exact_match.hip``).  ``kind``
-    EM_MULTICLASS: preds ``[N, C, P]`` scores, target ``[N, P]``; EM_MULTILABEL: preds / target ``[N, C, P]``
-    (integer multiclass labels: ``C`` = positions, ``P`` = 1).  Global: ``correct`` / ``total`` int64 ``[1]`` states
+    EM_MULTICLASS: preds ``[N, C, P]`` scores, target ``[N, P]``; EM_MULTILABEL: preds / target ``[N, C, P]``;
+    EM_LABELS: multiclass labels of any dtype, preds / target ``[N, C]`` (``C`` = positions, ``P`` = 1).  Global: ``correct`` / ``total`` int64 ``[1]`` states
     are updated in place, returns None.  Samplewise: returns the int64 ``[N]`` per-sample counts."""
     n = target.numel() // (P if kind == EM_MULTICLASS else C * P) if P and C else 0
     ws = owner.get("_em_ws")

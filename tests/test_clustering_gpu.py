@@ -84,7 +84,7 @@ def test_dense_labels_match_unique_inverse():
     assert k == uniq.numel() and torch.equal(ids.cpu(), inv)
 
 
-@pytest.mark.parametrize("n,kp,kt", [(50, 3, 4), (5000, 7, 5), (200_000, 12, 9), (100, 1, 3)])
+@pytest.mark.parametrize("n,kp,kt", [(50, 3, 4), (5000, 7, 5), (200_000, 12, 9), (100, 1, 3), (300_000, 300, 300)])
 def test_expected_mutual_info_kernel_matches_term_sum(n, kp, kt):
     """csrc/clustering/emi.hip (log-gamma recurrence, one thread per run of terms) against the vectorised fp64 term
     sum on the host (every (i, j, n_ij) term with nine lgamma calls, as the reference)."""
@@ -97,4 +97,20 @@ def test_expected_mutual_info_kernel_matches_term_sum(n, kp, kt):
     ref = FC.expected_mutual_info_score(cont, n)
     got = FC.expected_mutual_info_score(cont.cuda(), n)
     assert got.is_cuda
+    torch.testing.assert_close(got.cpu(), ref, rtol=1e-6, atol=1e-9)
+
+
+def test_expected_mutual_info_large_skewed_table():
+    """>= 65536 cluster pairs (the tiled emi.hip path) with one giant cluster on each side: the long pair's runs are
+    dealt out inside its block; matches the vectorised fp64 term sum."""
+    from torchmetrics_amd.functional import clustering as FC
+
+    g = torch.Generator().manual_seed(11)
+    n = 100_000
+    p = torch.where(torch.rand(n, generator=g) < 0.8, 0, torch.randint(1, 400, (n,), generator=g))
+    t = torch.where(torch.rand(n, generator=g) < 0.7, 0, torch.randint(1, 250, (n,), generator=g))
+    cont = FC._mutual_info_score_update(p, t)
+    assert cont.numel() >= 65536
+    ref = FC.expected_mutual_info_score(cont, n)
+    got = FC.expected_mutual_info_score(cont.cuda(), n)
     torch.testing.assert_close(got.cpu(), ref, rtol=1e-6, atol=1e-9)

@@ -175,8 +175,9 @@ def expected_mutual_info_score(contingency: Tensor, n_samples: int) -> Tensor:
     if a.numel() == 1 or b.numel() == 1:
         return torch.tensor(0.0, device=dev)
     n = float(n_samples)
-    if contingency.is_cuda and a.numel() * b.numel() < 65536:
-        # one kernel walking every pair's range with the log-gamma recurrence (csrc/clustering/emi.hip)
+    if contingency.is_cuda:
+        # one kernel walking every pair's range with the log-gamma recurrence (csrc/clustering/emi.hip), any table
+        # size; the vectorised torch formula below is the CPU path
         return ops.expected_mutual_info(a.contiguous(), b.contiguous(), n).to(torch.float32)
     ai, bj = a[:, None].expand(-1, b.numel()).reshape(-1), b[None, :].expand(a.numel(), -1).reshape(-1)
     start = torch.clamp(ai - n + bj, min=1)

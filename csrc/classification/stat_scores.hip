@@ -952,14 +952,52 @@ int pick_grid(long long work_items, int per_block) {
 // host round trip.
 constexpr int kBinSlots = 7;
 
+// Reading B decides `round_to<scalar_t>(sigmoid(v)) > thr` -- a non-decreasing function of v, so it equals
+// `v >= cut` for the smallest float `cut` where it holds (NaN when it never does; v = NaN is false either way).
+// Every thread finds the cut once by a 32-step search over the ordered float bit patterns, with the very same
+// expression; the per-element exp / reciprocal / rounding disappear from the hot loops.
+__device__ __forceinline__ bool sigmoid_gt(float x, float thr_t, int kind) {
+  const float s = 1.f / (1.f + __expf(-x));
+  const float r = kind == 1 ? round_to<c10::BFloat16>(s) : kind == 2 ? round_to<c10::Half>(s) : s;
+  return r > thr_t;
+}
+
+__device__ __forceinline__ uint32_t ordered_key(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ float ordered_float(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
 template <typename scalar_t>
-__device__ __forceinline__ void bin_pred(scalar_t raw, float thr_t, int* flag, bool& pa, bool& pb, bool& valid) {
+__device__ __forceinline__ int round_kind() {
+  return std::is_same<scalar_t, c10::BFloat16>::value ? 1 : std::is_same<scalar_t, c10::Half>::value ? 2 : 0;
+}
+
+template <typename scalar_t>
+__device__ float sigmoid_cut(float thr_t) {
+  const int kind = round_kind<scalar_t>();
+  if (!sigmoid_gt(INFINITY, thr_t, kind)) return __uint_as_float(0x7fc00000u);  // never: NaN compares false
+  if (sigmoid_gt(-INFINITY, thr_t, kind)) return -INFINITY;
+  uint32_t lo = ordered_key(-INFINITY), hi = ordered_key(INFINITY);  // f(lo) false, f(hi) true
+  while (hi - lo > 1) {
+    const uint32_t mid = lo + ((hi - lo) >> 1);
+    if (sigmoid_gt(ordered_float(mid), thr_t, kind)) hi = mid;
+    else lo = mid;
+  }
+  return ordered_float(hi);
+}
+
+template <typename scalar_t>
+__device__ __forceinline__ void bin_pred(scalar_t raw, float thr_t, float cut, int* flag, bool& pa, bool& pb,
+                                         bool& valid) {
   valid = true;
   if constexpr (IsFloating<scalar_t>::value) {
     const float v = to_f32(raw);
     pa = v > thr_t;
-    const float s = round_to<scalar_t>(1.f / (1.f + __expf(-v)));
-    pb = s > thr_t;
+    pb = v >= cut;
   } else {
     const long long v = static_cast<long long>(raw);
     if (v != 0 && v != 1) {
@@ -994,6 +1032,7 @@ __global__ void __launch_bounds__(kBlock) bin_flat_kernel(const scalar_t* __rest
     __syncthreads();
   }
   int local_not_prob = 0;
+  const float cut = IsFloating<scalar_t>::value ? sigmoid_cut<scalar_t>(thr_t) : 0.f;
   // (i / X, i % X, (i / X) % L) are advanced incrementally: no 64-bit division per element
   const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
   const long long i_start = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -1025,7 +1064,7 @@ __global__ void __launch_bounds__(kBlock) bin_flat_kernel(const scalar_t* __rest
       raise_flag(flag, kErrTargetNotBinary);
       continue;
     }
-    bin_pred<scalar_t>(preds[i], thr_t, flag, pa, pb, valid);
+    bin_pred<scalar_t>(preds[i], thr_t, cut, flag, pa, pb, valid);
     if (!valid) continue;
     int sa, sb;
     bin_slots(tv == 1, pa, pb, sa, sb);
@@ -1132,6 +1171,7 @@ __global__ void __launch_bounds__(kVecBlock) bin_vec_kernel(const scalar_t* __re
 #pragma unroll
     for (int k = 0; k < kBinSlots; ++k) c[e][k] = 0;
   int local_not_prob = 0;
+  const float cut = sigmoid_cut<scalar_t>(thr_t);
   const u32x4* pv = reinterpret_cast<const u32x4*>(preds);
   const u32x4* tvp = reinterpret_cast<const u32x4*>(target);
   constexpr int kU = 4;
@@ -1164,7 +1204,7 @@ __global__ void __launch_bounds__(kVecBlock) bin_vec_kernel(const scalar_t* __re
           continue;
         }
         const bool pa = x > thr_t;
-        const bool pb = round_to<scalar_t>(1.f / (1.f + __expf(-x))) > thr_t;
+        const bool pb = x >= cut;
         const bool t = tv == 1;
         c[e][0] += t & pa;
         c[e][1] += !t & pa;
@@ -1211,6 +1251,7 @@ __global__ void __launch_bounds__(kBlock) bin_reg_kernel(const scalar_t* __restr
   const int label = static_cast<int>((i0 / X) % L);
   int c[kBinSlots] = {0, 0, 0, 0, 0, 0, 0};
   int local_not_prob = 0;
+  const float cut = IsFloating<scalar_t>::value ? sigmoid_cut<scalar_t>(thr_t) : 0.f;
   constexpr int kU = 4;
   for (long long base = i0; base < total; base += kU * stride) {
     long long tv[kU];
@@ -1238,7 +1279,7 @@ __global__ void __launch_bounds__(kBlock) bin_reg_kernel(const scalar_t* __restr
         continue;
       }
       bool pa, pb, valid;
-      bin_pred<scalar_t>(pv[u], thr_t, flag, pa, pb, valid);
+      bin_pred<scalar_t>(pv[u], thr_t, cut, flag, pa, pb, valid);
       if (!valid) continue;
       const bool t = tv[u] == 1;
       c[0] += t & pa;
@@ -1292,6 +1333,7 @@ __global__ void __launch_bounds__(kBlock) bin_seg_kernel(const scalar_t* __restr
   const target_t* t = target + seg * X;
   long long acc[kBinSlots] = {0, 0, 0, 0, 0, 0, 0};
   int local_not_prob = 0;
+  const float cut = IsFloating<scalar_t>::value ? sigmoid_cut<scalar_t>(thr_t) : 0.f;
   for (long long x = beg + threadIdx.x; x < end; x += blockDim.x) {
     const long long tv = static_cast<long long>(t[x]);
     const bool ignored = has_ignore && tv == ignore;
@@ -1305,7 +1347,7 @@ __global__ void __launch_bounds__(kBlock) bin_seg_kernel(const scalar_t* __restr
       continue;
     }
     bool pa, pb, valid;
-    bin_pred<scalar_t>(p[x], thr_t, flag, pa, pb, valid);
+    bin_pred<scalar_t>(p[x], thr_t, cut, flag, pa, pb, valid);
     if (!valid) continue;
     int sa, sb;
     bin_slots(tv == 1, pa, pb, sa, sb);
@@ -1931,9 +1973,36 @@ void launch_probe(at::Tensor flag) {
   hipLaunchKernelGGL(launch_probe_kernel, dim3(1), dim3(64), 0, stream(), flag.data_ptr<int>());
 }
 
+__global__ void sigmoid_cut_probe_kernel(const float* __restrict__ x, long long n, float thr_t, int kind,
+                                         int* __restrict__ out) {
+  const float cut = kind == 1 ? sigmoid_cut<c10::BFloat16>(thr_t)
+                    : kind == 2 ? sigmoid_cut<c10::Half>(thr_t) : sigmoid_cut<float>(thr_t);
+  for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<long long>(gridDim.x) * blockDim.x)
+    out[i] = (sigmoid_gt(x[i], thr_t, kind) ? 1 : 0) | (x[i] >= cut ? 2 : 0);
+}
+
+// Test probe of the reading-B cut: per value, bit 0 = the direct `round(sigmoid(x)) > thr`, bit 1 = `x >= cut`.
+// kind 0 fp32, 1 bf16, 2 fp16 rounding of the sigmoid (the threshold is rounded as bin_update rounds it).
+at::Tensor sigmoid_cut_probe(const at::Tensor& x, double threshold, int64_t kind) {
+  TM_CHECK_CUDA(x);
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous(), "sigmoid_cut_probe: contiguous fp32 values");
+  float thr_t = static_cast<float>(threshold);
+  if (kind == 1) thr_t = static_cast<float>(c10::BFloat16(thr_t));
+  if (kind == 2) thr_t = static_cast<float>(c10::Half(thr_t));
+  at::Tensor out = at::empty({x.numel()}, x.options().dtype(at::kInt));
+  if (x.numel())
+    hipLaunchKernelGGL(sigmoid_cut_probe_kernel, dim3(grid_cap((x.numel() + 255) / 256, 1024)), dim3(256), 0,
+                       stream(), x.data_ptr<float>(), static_cast<long long>(x.numel()), thr_t,
+                       static_cast<int>(kind), out.data_ptr<int>());
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return out;
+}
+
 }  // namespace tm_amd
 
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def("sigmoid_cut_probe(Tensor x, float threshold, int kind) -> Tensor");
   m.def(
       "mc_update(Tensor preds, Tensor target, Tensor(a!) out, Tensor(b!) flag, int num_classes, int ignore_index, "
       "bool has_ignore, int mode, bool samplewise) -> ()");
@@ -1955,4 +2024,5 @@ TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
   m.impl("bin_update", &tm_amd::bin_update);
   m.impl("bin_stats_finalize", &tm_amd::bin_stats_finalize);
   m.impl("bin_confmat_finalize", &tm_amd::bin_confmat_finalize);
+  m.impl("sigmoid_cut_probe", &tm_amd::sigmoid_cut_probe);
 }

@@ -13,6 +13,7 @@
 
 namespace tm_amd {
 int notprob_current(const at::Tensor& np);  // stat_scores.hip
+void bin_flush_pending(const at::Tensor& ws);  // stat_scores.hip
 namespace {
 
 constexpr int kThreads = cbody::kThreads;
@@ -147,6 +148,7 @@ void bin_stats_forward(at::Tensor ws, at::Tensor not_prob, at::Tensor tp, at::Te
               "bin_stats_forward: workspace must be int64 [L, 7]");
   const long long L = ws.numel() / kBinSlots;
   TORCH_CHECK(L >= 1 && L < (1LL << 31), "bin_stats_forward: bad label count");
+  bin_flush_pending(ws);  // bin_update may have deferred its fold to the finalize
   check_states(ws, {&tp, &fp, &tn, &fn}, L, "bin_stats_forward");
   TORCH_CHECK(kind >= 0 && kind <= 5 && average >= 0 && average <= 3, "bin_stats_forward: bad kind / average");
   TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.device() == ws.device() &&

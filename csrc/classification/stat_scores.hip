@@ -1433,6 +1433,79 @@ __global__ void __launch_bounds__(kBlock) bin_confmat_finalize_kernel(int64_t* _
   }
 }
 
+// Fold + finalize in ONE launch for an update whose per-block label histograms are still in `partials`
+// ([nrows, L * 7] int32, written by bin_vec / bin_reg / bin_flat): block = LB labels x (1024 / LB) row lanes; every
+// thread sums its rows' 7 counters for its label (4 rows in flight), waves reduce lanes of the same label by shuffles,
+// the block reduces the 16 waves in LDS, and one thread per label picks reading A / B from not_prob[slot] and writes
+// the states (or the [L, 2, 2] confusion matrices).  Any counts already folded into ws (an earlier update not yet
+// finalized) are added and ws is re-zeroed.  Replaces partials_fold_kernel + bin_*_finalize_kernel (two launches).
+template <int LB>
+__global__ void __launch_bounds__(kFoldThreads) bin_partials_finalize_kernel(
+    const int* __restrict__ part, int nrows, int L, int64_t* __restrict__ ws, int* __restrict__ not_prob, int slot,
+    bool two_slots, bool accumulate, int64_t* __restrict__ tp, int64_t* __restrict__ fp, int64_t* __restrict__ tn,
+    int64_t* __restrict__ fn, int64_t* __restrict__ confmat) {
+  constexpr int kRowLanes = kFoldThreads / LB;
+  constexpr int kW = kFoldThreads / kWave;
+  __shared__ long long red[kW][LB][kBinSlots];
+  const int lb = threadIdx.x % LB, rl = threadIdx.x / LB;
+  const int g = blockIdx.x * LB + lb;
+  const long long nbins = static_cast<long long>(L) * kBinSlots;
+  long long acc[kBinSlots] = {0, 0, 0, 0, 0, 0, 0};
+  if (g < L) {
+    const int* base = part + static_cast<long long>(g) * kBinSlots;
+    int r = rl;
+    for (; r + 3 * kRowLanes < nrows; r += 4 * kRowLanes) {
+      int v[4][kBinSlots];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < kBinSlots; ++k) v[u][k] = base[static_cast<long long>(r + u * kRowLanes) * nbins + k];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < kBinSlots; ++k) acc[k] += v[u][k];
+    }
+    for (; r < nrows; r += kRowLanes)
+#pragma unroll
+      for (int k = 0; k < kBinSlots; ++k) acc[k] += base[static_cast<long long>(r) * nbins + k];
+  }
+#pragma unroll
+  for (int k = 0; k < kBinSlots; ++k)
+#pragma unroll
+    for (int off = kWave / 2; off >= LB; off >>= 1) acc[k] += __shfl_xor(acc[k], off, kWave);
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  if (lane < LB)
+#pragma unroll
+    for (int k = 0; k < kBinSlots; ++k) red[w][lane][k] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < LB && g < L) {
+    long long c[kBinSlots];
+    int64_t* wg = ws + static_cast<long long>(g) * kBinSlots;
+#pragma unroll
+    for (int k = 0; k < kBinSlots; ++k) {
+      long long t = wg[k];
+      for (int i = 0; i < kW; ++i) t += red[i][threadIdx.x][k];
+      c[k] = t;
+      wg[k] = 0;
+    }
+    const bool use_b = not_prob[slot] != 0;
+    const long long a = use_b ? c[3] : c[0], b = use_b ? c[4] : c[1], d = use_b ? c[5] : c[2];
+    const long long e = c[6] - a - b - d;
+    if (confmat != nullptr) {
+      int64_t* m = confmat + static_cast<long long>(g) * 4;
+      m[0] += e;
+      m[1] += b;
+      m[2] += d;
+      m[3] += a;
+    } else if (accumulate) {
+      tp[g] += a; fp[g] += b; fn[g] += d; tn[g] += e;
+    } else {
+      tp[g] = a; fp[g] = b; fn[g] = d; tn[g] = e;
+    }
+  }
+  if (two_slots && blockIdx.x == 0 && threadIdx.x == 0) not_prob[slot ^ 1] = 0;
+}
+
 // reset of the per-call logit flag is ordered after the finalize (same stream) -- only for one-word flags
 __global__ void zero_int_kernel(int* p) { *p = 0; }
 
@@ -1461,6 +1534,77 @@ int notprob_current(const at::Tensor& np) {
   auto it = g_np_slot.find(np.data_ptr());
   return it == g_np_slot.end() ? 0 : it->second;
 }
+
+// Per-block label histograms of a binary / multilabel update whose fold is deferred to the finalize (keyed by the
+// workspace address): the finalize then folds AND finalizes in one launch (bin_partials_finalize_kernel).  A second
+// update on the same workspace before any finalize first folds the pending rows into ws (partials_fold_kernel).
+namespace {
+struct PendingFold {
+  at::Tensor partials;
+  at::Tensor ws;  // held: the workspace's memory cannot be freed and handed to another owner while rows are pending
+  int nrows;
+  int nbins;
+};
+std::mutex g_pf_mu;
+std::unordered_map<const void*, PendingFold> g_pending;
+
+void flush_pending(const at::Tensor& ws, hipStream_t s) {
+  PendingFold pf;
+  {
+    std::lock_guard<std::mutex> lock(g_pf_mu);
+    auto it = g_pending.find(ws.data_ptr());
+    if (it == g_pending.end()) return;
+    pf = std::move(it->second);
+    g_pending.erase(it);
+  }
+  launch_partials_fold(pf.partials.data_ptr<int>(), pf.nrows, pf.nbins, ws.data_ptr<int64_t>(), s);
+}
+
+void defer_fold(const at::Tensor& ws, at::Tensor partials, int nrows, int nbins, hipStream_t s) {
+  static const bool off = std::getenv("TM_AMD_FUSED_BIN_FINALIZE") &&
+                          std::atoi(std::getenv("TM_AMD_FUSED_BIN_FINALIZE")) == 0;
+  if (off) {
+    launch_partials_fold(partials.data_ptr<int>(), nrows, nbins, ws.data_ptr<int64_t>(), s);
+    return;
+  }
+  std::lock_guard<std::mutex> lock(g_pf_mu);
+  g_pending[ws.data_ptr()] = PendingFold{std::move(partials), ws, nrows, nbins};
+}
+
+}  // namespace
+
+// consumers of the workspace other than the two finalizers (bin_stats_forward) fold pending rows into ws first
+void bin_flush_pending(const at::Tensor& ws) { flush_pending(ws, stream()); }
+
+namespace {
+// true: the pending rows of `ws` were folded and finalized into the states (or confmat) in one launch
+bool finalize_pending(at::Tensor ws, at::Tensor not_prob, bool accumulate, int64_t* tp, int64_t* fp, int64_t* tn,
+                      int64_t* fn, int64_t* confmat, hipStream_t s) {
+  PendingFold pf;
+  {
+    std::lock_guard<std::mutex> lock(g_pf_mu);
+    auto it = g_pending.find(ws.data_ptr());
+    if (it == g_pending.end()) return false;
+    pf = std::move(it->second);
+    g_pending.erase(it);
+  }
+  const int L = pf.nbins / kBinSlots;
+  const bool two = not_prob.numel() >= 2;
+  const int slot = notprob_current(not_prob);
+  auto go = [&](auto lbc) {
+    constexpr int LB = decltype(lbc)::value;
+    hipLaunchKernelGGL((bin_partials_finalize_kernel<LB>), dim3((L + LB - 1) / LB), dim3(kFoldThreads), 0, s,
+                       pf.partials.data_ptr<int>(), pf.nrows, L, ws.data_ptr<int64_t>(), not_prob.data_ptr<int>(),
+                       slot, two, accumulate, tp, fp, tn, fn, confmat);
+  };
+  if (L == 1) go(std::integral_constant<int, 1>{});
+  else if (L <= 4) go(std::integral_constant<int, 4>{});
+  else if (L <= 16) go(std::integral_constant<int, 16>{});
+  else go(std::integral_constant<int, 64>{});
+  if (!two) hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
+  return true;
+}
+}  // namespace
 
 // ================================================================================================================
 // host launchers
@@ -1809,6 +1953,7 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
   const long long G = samplewise ? N * L : L;
   TORCH_CHECK(ws.numel() == G * kBinSlots && ws.scalar_type() == at::kLong, "bin_update: bad workspace");
   auto s = stream();
+  flush_pending(ws, s);  // an earlier update of this workspace not finalized yet: fold its rows into ws first
   int* const npw = not_prob.data_ptr<int>() + notprob_begin(not_prob);  // this update's "not probabilities" word
   TM_DISPATCH_TARGET(target.scalar_type(), "bin_update", [&] {
     const target_t* tp = reinterpret_cast<const target_t*>(target.data_ptr());
@@ -1837,7 +1982,7 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
                              has_ignore, flag.data_ptr<int>(), npw, prob_check_all,
                              partials.data_ptr<int>());
         }
-        launch_partials_fold(partials.data_ptr<int>(), grid, static_cast<int>(nbins), ws.data_ptr<int64_t>(), s);
+        defer_fold(ws, partials, grid, static_cast<int>(nbins), s);
       } else if (!samplewise && reg_grid(L * X, total) > 0 && L * kBinSlots <= kLdsBins) {
         // grid stride a multiple of L * X: a fixed label per thread (register counters)
         const long long grid = reg_grid(L * X, total);
@@ -1850,9 +1995,7 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
                            s, pp, tp, total, L, X, thr_t, ignore_index, has_ignore, ws.data_ptr<int64_t>(),
                            fold ? partials.data_ptr<int>() : nullptr, flag.data_ptr<int>(), npw,
                            prob_check_all);
-        if (fold)
-          launch_partials_fold(partials.data_ptr<int>(), static_cast<int>(grid), static_cast<int>(nbins),
-                               ws.data_ptr<int64_t>(), s);
+        if (fold) defer_fold(ws, partials, static_cast<int>(grid), static_cast<int>(nbins), s);
       } else {
         const long long nbins = L * kBinSlots;
         const bool lds_hist = !samplewise && nbins <= kLdsBins;
@@ -1867,8 +2010,7 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
                            total, L, X, thr_t, ignore_index, has_ignore, samplewise, ws.data_ptr<int64_t>(),
                            flag.data_ptr<int>(), npw, prob_check_all,
                            use_partials ? partials.data_ptr<int>() : nullptr);
-        if (use_partials)
-          launch_partials_fold(partials.data_ptr<int>(), grid, static_cast<int>(nbins), ws.data_ptr<int64_t>(), s);
+        if (use_partials) defer_fold(ws, partials, grid, static_cast<int>(nbins), s);
       }
     });
   });
@@ -1884,6 +2026,11 @@ void bin_stats_finalize(at::Tensor ws, at::Tensor not_prob, bool accumulate, at:
     TORCH_CHECK(t->device() == ws.device() && t->scalar_type() == at::kLong && t->is_contiguous() && t->numel() == G,
                 "bin_stats_finalize: states must be contiguous int64 with G elements");
   auto s = stream();
+  if (finalize_pending(ws, not_prob, accumulate, tp.data_ptr<int64_t>(), fp.data_ptr<int64_t>(),
+                       tn.data_ptr<int64_t>(), fn.data_ptr<int64_t>(), nullptr, s)) {
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+    return;
+  }
   const bool two = not_prob.numel() >= 2;  // double-buffered word: no re-arm launch
   const bool one = G <= kFinalizeOneBlock;  // one block folds and re-arms not_prob itself
   hipLaunchKernelGGL(bin_finalize_kernel, dim3(one ? 1 : grid_cap((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
@@ -1902,6 +2049,10 @@ void bin_confmat_finalize(at::Tensor ws, at::Tensor not_prob, at::Tensor confmat
   TORCH_CHECK(confmat.scalar_type() == at::kLong && confmat.is_contiguous() && confmat.numel() == 4 * G,
               "bin_confmat_finalize: confmat must be contiguous int64 [G, 2, 2]");
   auto s = stream();
+  if (finalize_pending(ws, not_prob, false, nullptr, nullptr, nullptr, nullptr, confmat.data_ptr<int64_t>(), s)) {
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+    return;
+  }
   const bool one = G <= kFinalizeOneBlock;
   const bool two = not_prob.numel() >= 2;
   hipLaunchKernelGGL(bin_confmat_finalize_kernel, dim3(one ? 1 : grid_cap((G + kBlock - 1) / kBlock)), dim3(kBlock), 0,

@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp PYTHONPATH="$GRAFT_REPO_ROOT"
 R=$GRAFT_REPO_ROOT
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_fused_update_gpu.py tests/test_fused_compute_gpu.py tests/test_stream_kernels_gpu.py tests/test_native_update.py tests/test_native_forward_gpu.py tests/test_kernels_gpu.py tests/test_sklearn_pinned_gpu.py tests/test_torchscript.py tests/test_state_arena.py tests/test_exact_match_gpu.py tests/test_curve_views.py tests/test_classification_curves.py tests/test_sigmoid_cut_gpu.py tests/test_clustering_gpu.py tests/test_classification_stats.py -m gpu > gpurun_out/r5fam_tests.log 2>&1 || { tail -40 gpurun_out/r5fam_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_fused_update_gpu.py tests/test_fused_compute_gpu.py tests/test_stream_kernels_gpu.py tests/test_native_update.py tests/test_native_forward_gpu.py tests/test_kernels_gpu.py tests/test_sklearn_pinned_gpu.py tests/test_torchscript.py tests/test_state_arena.py tests/test_exact_match_gpu.py tests/test_curve_views.py tests/test_classification_curves.py tests/test_sigmoid_cut_gpu.py tests/test_bin_fused_finalize_gpu.py tests/test_clustering_gpu.py tests/test_classification_stats.py -m gpu > gpurun_out/r5fam_tests.log 2>&1 || { tail -40 gpurun_out/r5fam_tests.log; exit 1; }
 tail -2 gpurun_out/r5fam_tests.log
 timeout -k 10 300 python3 benchmarks/bench_collection.py --sync-every-step --steps 200 --warmup 20 > gpurun_out/r5fam_coll_sync.json 2>&1 || { tail -5 gpurun_out/r5fam_coll_sync.json; exit 1; }
 tail -1 gpurun_out/r5fam_coll_sync.json | cut -c1-700

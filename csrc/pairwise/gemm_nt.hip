@@ -710,6 +710,129 @@ __global__ __launch_bounds__(TM == 256 ? 512 : 256) void gemm_nt_h16_kernel(
                                      });
 }
 
+// 256 x 256 tile, 8 waves, a 4-deep ring of 32-wide k-chunks (32 KiB per stage: 128 KiB of LDS, as the 2 x 64-wide
+// kernel above) so THREE chunks of DMA are in flight while one is multiplied -- the 2-stage kernel waits for the next
+// chunk's loads one chunk after issuing them.  Rows are 64 B: a 1 KiB global_load_lds instruction moves 16 rows, and
+// the 16-B slot of logical chunk c in row r is c ^ ((r >> 2) & 3), which keeps every ds_read_b128 lane group on 16
+// distinct slots of the 256-B bank row (rows r and r + 4 share banks unless their slots differ).
+template <int EPI, typename T>
+__global__ __launch_bounds__(512) void gemm_nt_h16_ring_kernel(const uint16_t* __restrict__ X,
+                                                               const uint16_t* __restrict__ Y, int N, int M, int D,
+                                                               long long bx, long long by, int tiles_m, EpiParams ep) {
+  constexpr int TM = 256, NT = 512, WC = 4, NA = 4, KC = 32, STAGES = 4;
+  typedef typename Mfma16<T>::v8 v8;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  uint16_t* sh = reinterpret_cast<uint16_t*>(smem);
+  constexpr int kStage = 2 * TM * KC;  // elements per stage (A then B)
+  const int batch = blockIdx.z;
+  const int32_t* gix = ep.ix ? ep.ix + (long long)batch * N : nullptr;
+  const int32_t* giy = ep.iy ? ep.iy + (long long)batch * M : nullptr;
+  if (!gix) X += batch * bx;
+  if (!giy) Y += batch * by;
+  auto xrow = [&](int i) -> const uint16_t* { return X + (long long)(gix ? gix[i] : i) * D; };
+  auto yrow = [&](int j) -> const uint16_t* { return Y + (long long)(giy ? giy[j] : j) * D; };
+  const int tiles_n = (N + TM - 1) / TM;
+  const int total = tiles_n * tiles_m;
+  const int bid = blockIdx.x;
+  const int per = (total + 7) / 8;
+  const int tile = (bid % 8) * per + bid / 8;  // XCD-aware band of row-major tiles
+  if (tile >= total) return;
+  const int ti = tile / tiles_m, tj = tile - ti * tiles_m;
+  const int row0 = ti * TM, col0 = tj * TM;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = (wave / WC) * 32 * NA, wc = (wave % WC) * 64;
+  const int h = lane >> 5, r = lane & 31;
+
+  // DMA: wave w moves rows [32 w, 32 w + 32) of both operand tiles, 16 rows per instruction (2 per operand);
+  // lane l of instruction q covers row 32 w + 16 q + l / 4, physical slot l % 4 = logical chunk (l % 4) ^ swz(row)
+  const uint16_t* srcA[2];
+  const uint16_t* srcB[2];
+  int kof[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int rr = 32 * wave + 16 * q + (lane >> 2);
+    const int c = (lane & 3) ^ ((rr >> 2) & 3);
+    kof[q] = 8 * c;
+    srcA[q] = xrow(min(row0 + rr, N - 1)) + 8 * c;
+    srcB[q] = yrow(min(col0 + rr, M - 1)) + 8 * c;
+  }
+  typedef __attribute__((address_space(3))) void lds_t;
+  typedef __attribute__((address_space(1))) void glb_t;
+  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
+  auto stage = [&](int kc) {
+    uint16_t* sa = sh + (kc % STAGES) * kStage;
+    uint16_t* sb = sa + TM * KC;
+    const int k0 = kc * KC;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const bool in = k0 + kof[q] < D;
+      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcA[q] + k0 : zero), (lds_t*)(sa + (32 * wave + 16 * q) * KC),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcB[q] + k0 : zero), (lds_t*)(sb + (32 * wave + 16 * q) * KC),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x16 acc[NA][2];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  const int swz_a = ((wr + r) >> 2) & 3;  // (32 a keeps (row >> 2) & 3)
+  const int swz_b = ((wc + r) >> 2) & 3;
+  const int nk = (D + KC - 1) / KC;
+  auto frag = [&](int buf, int s, v8* fa, v8* fb) {
+    const uint16_t* sa = sh + buf * kStage + (wr + r) * KC;
+    const uint16_t* sb = sh + buf * kStage + TM * KC + (wc + r) * KC;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) fa[a] = *reinterpret_cast<const v8*>(sa + 32 * a * KC + 8 * ((2 * s + h) ^ swz_a));
+#pragma unroll
+    for (int b = 0; b < 2; ++b) fb[b] = *reinterpret_cast<const v8*>(sb + 32 * b * KC + 8 * ((2 * s + h) ^ swz_b));
+  };
+  auto mma = [&](const v8* fa, const v8* fb) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] = Mfma16<T>::run(fa[a], fb[b], acc[a][b]);
+  };
+  // prologue: chunks 0 .. 2 in flight (4 DMA instructions per chunk and thread)
+  stage(0);
+  if (nk > 1) stage(1);
+  if (nk > 2) stage(2);
+  v8 fa0[NA], fb0[2], fa1[NA], fb1[2];
+  for (int kc = 0; kc < nk; ++kc) {
+    // chunk kc landed when at most the later chunks' DMAs are outstanding (loads retire in order)
+    const int later = min(nk - 1, kc + 2) - kc;
+    if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // every wave's part of chunk kc is in LDS, and every wave finished reading chunk kc - 1 (its fragments were
+    // consumed by MFMAs issued before this point): its buffer may take chunk kc + 3
+    __builtin_amdgcn_s_barrier();
+    if (kc + 3 < nk) stage(kc + 3);
+    const int buf = kc % STAGES;
+    frag(buf, 0, fa0, fb0);
+    frag(buf, 1, fa1, fb1);
+    mma(fa0, fb0);
+    mma(fa1, fb1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  tile_epilogue<EPI, NA, WC, TM, NT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile,
+                                     [&](int i, int j) {
+                                       const uint16_t* xr = xrow(i);
+                                       const uint16_t* yr = yrow(j);
+                                       float t = 0.f;
+                                       for (int k = 0; k < D; ++k) {
+                                         const float d = Mfma16<T>::to_f32(xr[k]) - Mfma16<T>::to_f32(yr[k]);
+                                         t = fmaf(d, d, t);
+                                       }
+                                       return t;
+                                     });
+}
+
 // The 256 x 256 kernel for large problems: D a multiple of its k-step, both sides at least one tile, enough tiles to
 // fill the chip once; TM_AMD_GEMM_BIG=0|1 forces it off / on (where it applies).
 bool big_choice(int N, int M, int D, int batches) {
@@ -791,7 +914,14 @@ void launch_h16(const at::Tensor& x, const at::Tensor& y, int batches, long long
   const size_t lds = 2ull * 2 * tm * 64 * sizeof(uint16_t);
   const auto* xp = reinterpret_cast<const uint16_t*>(x.data_ptr());
   const auto* yp = reinterpret_cast<const uint16_t*>(y.data_ptr());
-  if (big)
+  static const int ring = [] {
+    const char* e = std::getenv("TM_AMD_GEMM16_RING");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (big && ring)
+    hipLaunchKernelGGL((gemm_nt_h16_ring_kernel<EPI, T>), dim3(per * 8, 1, batches), dim3(512), lds, stream(), xp,
+                       yp, N, M, D, bx, by, tiles_m, ep);
+  else if (big)
     hipLaunchKernelGGL((gemm_nt_h16_kernel<EPI, T, 256>), dim3(per * 8, 1, batches), dim3(512), lds, stream(), xp, yp,
                        N, M, D, bx, by, tiles_m, ep);
   else

@@ -2154,6 +2154,7 @@ at::Tensor sigmoid_cut_probe(const at::Tensor& x, double threshold, int64_t kind
 
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
   m.def("sigmoid_cut_probe(Tensor x, float threshold, int kind) -> Tensor");
+  m.def("bin_flush_pending(Tensor(a!) ws) -> ()");
   m.def(
       "mc_update(Tensor preds, Tensor target, Tensor(a!) out, Tensor(b!) flag, int num_classes, int ignore_index, "
       "bool has_ignore, int mode, bool samplewise) -> ()");
@@ -2176,4 +2177,5 @@ TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
   m.impl("bin_stats_finalize", &tm_amd::bin_stats_finalize);
   m.impl("bin_confmat_finalize", &tm_amd::bin_confmat_finalize);
   m.impl("sigmoid_cut_probe", &tm_amd::sigmoid_cut_probe);
+  m.impl("bin_flush_pending", &tm_amd::bin_flush_pending);
 }

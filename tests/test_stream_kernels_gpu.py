@@ -98,6 +98,7 @@ def _bin(preds, target, L, ignore, dev, threshold=0.5):
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
     not_prob = torch.zeros(1, dtype=torch.int32, device=dev)
     ops.bin_update(preds.to(dev), target.to(dev), ws, flag, not_prob, L, threshold, ignore, False)
+    ops.bin_flush(ws)  # the fold of the per-block rows waits for a finalizer otherwise
     return ws.cpu(), int(flag.item()), int(not_prob.item())
 
 

@@ -225,7 +225,9 @@ def mc_stats_finalize(ws: Tensor, num_classes: int, micro: bool, accumulate: boo
 def bin_update(preds: Tensor, target: Tensor, ws: Tensor, flag: Tensor, not_prob: Tensor, num_labels: int,
                threshold: float, ignore_index: Optional[int], samplewise: bool = False,
                prob_check_all: bool = True) -> None:
-    """Binary / multilabel tp/fp/fn/count update for ``[N, L, ...]`` inputs into a ``[G, 7]`` workspace.
+    """Binary / multilabel tp/fp/fn/count update for ``[N, L, ...]`` inputs into a ``[G, 7]`` workspace.  On ROCm
+    the per-block partial rows may be left pending for ``bin_stats_finalize`` / ``bin_confmat_finalize`` (one fused
+    fold + finalize launch): read ``ws`` itself only after :func:`bin_flush`.
 
     ``prob_check_all=False`` excludes ignored positions from the logits-vs-probabilities decision.
     """
@@ -237,6 +239,13 @@ def bin_update(preds: Tensor, target: Tensor, ws: Tensor, flag: Tensor, not_prob
     else:
         _cpu.bin_update(preds, target, ws, flag, not_prob, num_labels, threshold, ignore_index, samplewise,
                         prob_check_all)
+
+
+def bin_flush(ws: Tensor) -> None:
+    """Fold the per-block rows a ROCm ``bin_update`` left pending for its finalizer into ``ws`` (for readers of the
+    raw workspace; the two finalizers fold and finalize in one launch themselves)."""
+    if ws.is_cuda:
+        _ops().bin_flush_pending(ws)
 
 
 def bin_confmat_finalize(ws: Tensor, not_prob: Tensor, confmat: Tensor) -> None:

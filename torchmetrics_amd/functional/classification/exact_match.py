@@ -53,20 +53,18 @@ def _exact_match_fused(
     if multilabel:
         if preds.shape != target.shape or preds.ndim < 2:
             return None
-        kind, c, p = ops.EM_MULTILABEL, preds.shape[1], target[0].numel() // max(preds.shape[1], 1)
-        if preds.shape[1] == 0:
-            p = math.prod(target.shape[2:])
+        kind, c, p = ops.EM_MULTILABEL, preds.shape[1], math.prod(target.shape[2:])
         total_val = (n * p) if not samplewise else p
     elif preds.ndim == target.ndim + 1:
         if preds.shape[0] != n or preds.shape[2:] != target.shape[1:]:
             return None
-        kind, c, p = ops.EM_MULTICLASS, preds.shape[1], target[0].numel()
+        kind, c, p = ops.EM_MULTICLASS, preds.shape[1], math.prod(target.shape[1:])
         total_val = n if not samplewise else 1
     elif preds.ndim == target.ndim:
         if preds.shape[0] != n or preds.numel() != target.numel():
             return None
         # labels of any dtype (float labels compare exactly, as `preds == target` does): one unit per sample
-        kind, c, p = ops.EM_LABELS, target[0].numel(), 1
+        kind, c, p = ops.EM_LABELS, math.prod(target.shape[1:]), 1
         total_val = n if not samplewise else 1
     else:
         return None

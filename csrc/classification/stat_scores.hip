@@ -1597,9 +1597,13 @@ bool finalize_pending(at::Tensor ws, at::Tensor not_prob, bool accumulate, int64
                        pf.partials.data_ptr<int>(), pf.nrows, L, ws.data_ptr<int64_t>(), not_prob.data_ptr<int>(),
                        slot, two, accumulate, tp, fp, tn, fn, confmat);
   };
-  if (L == 1) go(std::integral_constant<int, 1>{});
-  else if (L <= 4) go(std::integral_constant<int, 4>{});
-  else if (L <= 16) go(std::integral_constant<int, 16>{});
+  // labels per block: about 4 partial rows per thread (one batch of loads in flight), at most the label count
+  int lb = 1;
+  while (lb < 64 && lb * 2 * std::max(pf.nrows, 1) <= 4 * kFoldThreads) lb *= 2;
+  while (lb > 1 && lb / 2 >= L) lb /= 2;
+  if (lb <= 1) go(std::integral_constant<int, 1>{});
+  else if (lb <= 4) go(std::integral_constant<int, 4>{});
+  else if (lb <= 16) go(std::integral_constant<int, 16>{});
   else go(std::integral_constant<int, 64>{});
   if (!two) hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
   return true;

@@ -10,7 +10,8 @@ leaders of the families below, they are served by ``ops.mc_family_update``
   Hamming subclasses) with ``top_k=1``, ``multidim_average="global"``;
 * the confusion-matrix family (``MulticlassConfusionMatrix`` and its Jaccard / Cohen kappa / Matthews subclasses);
 * the binned multiclass PR-curve family (PR curve / ROC / AUROC / average precision with tensor thresholds, one
-  threshold set per launch, not ``average="micro"``);
+  threshold set per launch; PR curve / ROC not ``average="micro"``; AUROC / AP keep per-class curve states whatever
+  their ``average``);
 * ``MulticlassCalibrationError``.
 
 Every member must have ``ignore_index=None``, ``num_classes = C <= 64`` and the class's own ``update`` (a subclass
@@ -41,6 +42,12 @@ def _classes() -> Dict[str, type]:
             "cb": MulticlassCalibrationError}
 
 
+def _curve_wrappers() -> tuple:
+    from torchmetrics_amd.classification.precision_recall_curve import MulticlassAUROC, MulticlassAveragePrecision
+
+    return (MulticlassAUROC.update, MulticlassAveragePrecision.update)
+
+
 def _role(m: Any) -> Optional[str]:
     """The family a metric joins the fused update as, or None."""
     cls = _classes()
@@ -57,8 +64,10 @@ def _role(m: Any) -> Optional[str]:
         return None
     if isinstance(m, cls["cm"]) and t.update is cls["cm"].update:
         return "cm"
-    if isinstance(m, cls["cv"]) and t.update is cls["cv"].update:
-        if d.get("average") != "micro" and isinstance(d.get("_buffers", {}).get("thresholds"), Tensor):
+    if isinstance(m, cls["cv"]) and (t.update is cls["cv"].update or t.update in _curve_wrappers()):
+        # AUROC / AP wrap the curve update with a transient average=None (their curve state is always per class)
+        per_class = t.update is not cls["cv"].update or d.get("average") != "micro"
+        if per_class and isinstance(d.get("_buffers", {}).get("thresholds"), Tensor):
             return "cv"
         return None
     if isinstance(m, cls["cb"]) and t.update is cls["cb"].update:

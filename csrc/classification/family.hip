@@ -29,7 +29,7 @@ namespace {
 constexpr int kFamThreads = 256;
 constexpr int kFamMaxC = 64;
 constexpr int kFamMaxCons = 4;   // confusion-matrix / stat-score consumers per launch
-constexpr int kFamMaxErr = 8;    // validation words
+constexpr int kFamMaxErr = 12;   // validation words (4 + 4 consumers, a curve and a calibration member)
 constexpr int kFamMaxBlocks = 512;
 constexpr int kFoldCols = kFamThreads / kWave;  // curve columns per fold block (one wave each)
 

@@ -7,7 +7,9 @@
 // (F/classification/calibration_error.py:29-59: softmax-if-needed, top-1 confidence / correctness).  On the
 // [8192, 10] bf16 batches of config #5 that was ~10 launches per step, every one latency-bound.
 //
-// Here the batch is read ONCE by `family_rows_kernel` (one row per thread; C <= 64): it computes the row's argmax,
+// Here the batch is read ONCE by `family_rows_g_kernel` (G lanes per row, a lane per class; C <= 64; the first
+// version, `family_rows_kernel`, ran one row per thread -- 25 us for 8192 x 10 with a curve member, serial per-class
+// threshold searches at one wave per SIMD): it computes the row's argmax,
 // its softmax (rounded to the input dtype, as torch.softmax stores it), the "score outside [0, 1]" bit, and feeds a
 // per-block LDS image of everything the members need:
 //   * the C x C (target, argmax) histogram          -> confusion matrices, and tp / fp / tn / fn of the stat scores;
@@ -149,6 +151,111 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_kernel(const scalar_t
         atomicAdd(dst, 1.f);
         atomicAdd(dst + 1, cv[var]);
         atomicAdd(dst + 2, av[var]);
+      }
+    }
+  }
+  if (__any(outside) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(&blk_outside, 1);
+  if (__any(bad) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(sp.err_scratch, kErrTargetOutOfRange);
+  __syncthreads();
+  for (int i = threadIdx.x; i < sp.off_cb; i += kFamThreads)
+    if (h[i]) atomicAdd(&sp.img[i], h[i]);
+  for (int i = sp.off_cb + threadIdx.x; i < sp.part_words; i += kFamThreads)
+    if (hf[i] != 0.f) atomicAdd(reinterpret_cast<float*>(sp.img) + i, hf[i]);
+  if (threadIdx.x == 0 && blk_outside) atomicOr(&sp.outside[sp.slot], 1);
+}
+
+// The same image, G lanes per row (G = the power of two >= C, <= 64): lane c of a row's group owns class c, so the
+// per-class curve work (two threshold searches, two LDS atomics) runs in parallel across the row's lanes instead of
+// serially in one thread; the row's max / argmax come from shuffles, and its softmax denominators are summed by
+// shuffling the lanes' exponentials in class order into every lane (the order the one-thread-per-row kernel and the
+// members' own kernels use, so the rounded softmax values are the same).
+template <typename scalar_t, typename target_t, int G>
+__global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar_t* __restrict__ preds,
+                                                                    const target_t* __restrict__ target, long long N,
+                                                                    FamilySpec sp) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  int* h = smem;
+  float* hf = reinterpret_cast<float*>(smem);
+  double* thr_s = reinterpret_cast<double*>(smem + ((sp.part_words + 1) & ~1));
+  float* bnd_s = reinterpret_cast<float*>(thr_s + sp.T);
+  __shared__ int blk_outside;
+  constexpr int R = kFamThreads / G;  // rows per block step
+  const int C = sp.C, T = sp.T, nb = sp.nb;
+  for (int i = threadIdx.x; i < sp.part_words; i += kFamThreads) h[i] = 0;
+  for (int i = threadIdx.x; i < T; i += kFamThreads) thr_s[i] = sp.thr[i];
+  for (int i = threadIdx.x; i < nb; i += kFamThreads) bnd_s[i] = sp.bounds[i];
+  if (threadIdx.x == 0) blk_outside = 0;
+  __syncthreads();
+  const int c = threadIdx.x % G;
+  const int gbase = (threadIdx.x & (kWave - 1)) - c;  // the group's first lane in the wave
+  const bool has_c = c < C;
+  bool outside = false, bad = false;
+  for (long long row0 = static_cast<long long>(blockIdx.x) * R; row0 < N;
+       row0 += static_cast<long long>(gridDim.x) * R) {  // uniform across the block: shuffles see whole groups
+    const long long row = row0 + threadIdx.x / G;
+    const bool live = row < N;
+    const bool mine = live && has_c;
+    const float v = mine ? to_f32(preds[row * C + c]) : -INFINITY;
+    outside |= mine && !(v >= 0.f && v <= 1.f);
+    float mf = mine ? v : -INFINITY;  // NaN-ignoring max (fmaxf drops NaN)
+    float mx = v;
+    int mi = mine ? c : 0x7fffffff;
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) {
+      mf = fmaxf(mf, __shfl_xor(mf, off, kWave));
+      const float ov = __shfl_xor(mx, off, kWave);
+      const int oi = __shfl_xor(mi, off, kWave);
+      if (argmax_better(ov, oi, mx, mi)) mx = ov, mi = oi;
+    }
+    // softmax denominators in class order (every lane gets the same sums)
+    const float e_cal = mine ? expf(v - mx) : 0.f;
+    float s_cal = 0.f;
+    for (int k = 0; k < C; ++k) s_cal += __shfl(e_cal, gbase + k, kWave);
+    float s_cur = s_cal;
+    const bool nan_row = !(mf == mx);  // a NaN in the row: the two shifts differ (uniform within the group)
+    float e_cur = e_cal;
+    if (__any(nan_row)) {
+      e_cur = mine ? expf(v - mf) : 0.f;
+      float t2 = 0.f;
+      for (int k = 0; k < C; ++k) t2 += __shfl(e_cur, gbase + k, kWave);
+      if (nan_row) s_cur = t2;
+      else e_cur = e_cal;
+    }
+    const long long tv = live ? static_cast<long long>(target[row]) : 0;
+    const bool valid = tv >= 0 && tv < C;
+    bad |= live && c == 0 && !valid;
+    const int t = static_cast<int>(valid ? tv : 0);
+    if (live && valid && c == 0 && sp.need_cm) atomicAdd(&h[t * C + mi], 1);
+    if (mine && valid && T > 0) {
+      const double praw = static_cast<double>(v);
+      const double psoft = static_cast<double>(round_to<scalar_t>(e_cur / s_cur));
+      const int pos = c == t;
+      const int braw = bucket_of(thr_s, T, praw), bsoft = bucket_of(thr_s, T, psoft);
+      atomicAdd(&h[sp.off_cv + ((0 * (T + 1) + braw) * C + c) * 2 + pos], 1);
+      atomicAdd(&h[sp.off_cv + ((1 * (T + 1) + bsoft) * C + c) * 2 + pos], 1);
+    }
+    if (nb > 0) {
+      float sv = mine ? round_to<scalar_t>(e_cal / s_cal) : -INFINITY;
+      int si = mine ? c : 0x7fffffff;
+#pragma unroll
+      for (int off = G / 2; off > 0; off >>= 1) {
+        const float ov = __shfl_xor(sv, off, kWave);
+        const int oi = __shfl_xor(si, off, kWave);
+        if (argmax_better(ov, oi, sv, si)) sv = ov, si = oi;
+      }
+      if (live && c < 2) {  // lane 0: the raw top-1 variant, lane 1: the softmax variant
+        const float ar = mi == tv ? 1.f : 0.f, as = si == tv ? 1.f : 0.f;
+        if (c == 0) sp.cand[row] = make_float4(mx, ar, sv, as);
+        const float cvv = c == 0 ? round_to<scalar_t>(mx) : sv;
+        const float avv = c == 0 ? ar : as;
+        int b = -1;
+        for (int k = 0; k < nb; ++k) b += (bnd_s[k] <= cvv) ? 1 : 0;
+        if (b >= 0) {
+          float* dst = hf + sp.off_cb + (c * nb + b) * 3;
+          atomicAdd(dst, 1.f);
+          atomicAdd(dst + 1, cvv);
+          atomicAdd(dst + 2, avv);
+        }
       }
     }
   }
@@ -388,7 +495,20 @@ void mc_family_update(const at::Tensor& preds, const at::Tensor& target, at::Ten
   const size_t lds = static_cast<size_t>((sp.part_words + 1) & ~1) * 4 + static_cast<size_t>(sp.T) * 8 +
                      static_cast<size_t>(sp.nb) * 4;
   TORCH_CHECK(lds <= 64 * 1024, "mc_family_update: partial image exceeds 64 KiB of LDS");
-  const int nblk = static_cast<int>(std::min<long long>((N + kFamThreads - 1) / kFamThreads, kFamMaxBlocks));
+  // G lanes per row (TM_AMD_FAMILY_G=0: one thread per row); blocks capped so a hot image word takes at most that
+  // many global atomics (TM_AMD_FAMILY_BLOCKS)
+  static const int use_g = [] {
+    const char* e = std::getenv("TM_AMD_FAMILY_G");
+    return e ? std::atoi(e) : 1;
+  }();
+  static const int max_blocks = [] {
+    const char* e = std::getenv("TM_AMD_FAMILY_BLOCKS");
+    return e ? std::max(1, std::atoi(e)) : 128;
+  }();
+  const int G = C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : C <= 32 ? 32 : 64;
+  const int rows_per_blk = use_g ? kFamThreads / G : kFamThreads;
+  const int nblk = static_cast<int>(std::min<long long>((N + rows_per_blk - 1) / rows_per_blk,
+                                                        use_g ? max_blocks : kFamMaxBlocks));
   TORCH_CHECK(work.scalar_type() == at::kInt && work.is_contiguous() && work.numel() >= sp.part_words + 3,
               "mc_family_update: work scratch too small");
   TORCH_CHECK(slot == 0 || slot == 1, "mc_family_update: slot 0 / 1");
@@ -403,21 +523,28 @@ void mc_family_update(const at::Tensor& preds, const at::Tensor& target, at::Ten
   auto s = stream();
   TM_DISPATCH_TARGET(target.scalar_type(), "mc_family_update", [&] {
     const target_t* tp = reinterpret_cast<const target_t*>(target.data_ptr());
+    auto run = [&](auto tag) {
+      using scalar_t = decltype(tag);
+      const scalar_t* pp = reinterpret_cast<const scalar_t*>(preds.data_ptr());
+      auto go = [&](auto gc) {
+        constexpr int GG = decltype(gc)::value;
+        hipLaunchKernelGGL((family_rows_g_kernel<scalar_t, target_t, GG>), dim3(nblk), dim3(kFamThreads), lds, s, pp,
+                           tp, N, sp);
+      };
+      if (!use_g)
+        hipLaunchKernelGGL((family_rows_kernel<scalar_t, target_t>), dim3(nblk), dim3(kFamThreads), lds, s, pp, tp, N,
+                           sp);
+      else if (G == 4) go(std::integral_constant<int, 4>{});
+      else if (G == 8) go(std::integral_constant<int, 8>{});
+      else if (G == 16) go(std::integral_constant<int, 16>{});
+      else if (G == 32) go(std::integral_constant<int, 32>{});
+      else go(std::integral_constant<int, 64>{});
+    };
     switch (preds.scalar_type()) {
-      case at::kBFloat16:
-        hipLaunchKernelGGL((family_rows_kernel<c10::BFloat16, target_t>), dim3(nblk), dim3(kFamThreads), lds, s,
-                           reinterpret_cast<const c10::BFloat16*>(preds.data_ptr()), tp, N, sp);
-        break;
-      case at::kHalf:
-        hipLaunchKernelGGL((family_rows_kernel<c10::Half, target_t>), dim3(nblk), dim3(kFamThreads), lds, s,
-                           reinterpret_cast<const c10::Half*>(preds.data_ptr()), tp, N, sp);
-        break;
-      case at::kFloat:
-        hipLaunchKernelGGL((family_rows_kernel<float, target_t>), dim3(nblk), dim3(kFamThreads), lds, s,
-                           preds.data_ptr<float>(), tp, N, sp);
-        break;
-      default:
-        TORCH_CHECK(false, "mc_family_update: bf16 / fp16 / fp32 scores");
+      case at::kBFloat16: run(c10::BFloat16{}); break;
+      case at::kHalf: run(c10::Half{}); break;
+      case at::kFloat: run(float{}); break;
+      default: TORCH_CHECK(false, "mc_family_update: bf16 / fp16 / fp32 scores");
     }
   });
   const int r_cv = 1;

@@ -319,11 +319,11 @@ __global__ void __launch_bounds__(kBlock) moments_finalize_kernel(const double* 
 }
 
 
-// Small batches (n_rows * k <= kSmallMax, k dividing the wave): ONE 1024-thread block does the pass and the fold -- one
+// Small batches (n_rows * k <= kSmallMax, k dividing the wave): ONE 512-thread block does the pass and the fold -- one
 // launch, no partials buffer, no grid-wide fence or ticket.  Every thread keeps one column (k | 64 | 1024, so the
 // stride never changes a thread's column) and issues up to kSmallUnroll pairs' loads before accumulating them; wave
 // xor-trees then a 16-wave LDS fold give the per-column sums, and (column, destination) threads apply them.
-constexpr int kSmallThreads = 1024;
+constexpr int kSmallThreads = 512;  // 1024 capped VGPRs at 128 and spilled the fp64 accumulators to scratch
 constexpr int kSmallUnroll = 8;
 constexpr long long kSmallMax = 65536;
 

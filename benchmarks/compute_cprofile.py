@@ -1,4 +1,6 @@
-"""cProfile of the config #5 classification collection ``compute()`` on the device (host-side cost breakdown)."""
+"""cProfile of a config #5 collection step on the device (host-side cost breakdown): ``--which cls|reg`` (the
+classification or the regression collection), ``--update-only`` (no compute)."""
+import argparse
 import cProfile
 import os
 import pstats
@@ -12,15 +14,26 @@ from benchmarks.bench_collection import BATCH, NC, build  # noqa: E402
 
 
 def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--which", default="cls")
+    ap.add_argument("--update-only", action="store_true")
+    a = ap.parse_args()
     dev = torch.device("cuda")
     cls, reg = build(dev)
     g = torch.Generator().manual_seed(0)
-    logits = torch.randn(BATCH, NC, generator=g).to(dev, torch.bfloat16)
-    labels = torch.randint(0, NC, (BATCH,), generator=g).to(dev)
+    if a.which == "cls":
+        coll = cls
+        x = torch.randn(BATCH, NC, generator=g).to(dev, torch.bfloat16)
+        y = torch.randint(0, NC, (BATCH,), generator=g).to(dev)
+    else:
+        coll = reg
+        x = torch.randn(BATCH, generator=g).to(dev)
+        y = x + 0.3 * torch.randn(BATCH, generator=g).to(dev)
 
     def step():
-        cls.update(logits, labels)
-        cls.compute()
+        coll.update(x, y)
+        if not a.update_only:
+            coll.compute()
 
     for _ in range(20):
         step()
@@ -32,8 +45,8 @@ def main() -> None:
     torch.cuda.synchronize()
     pr.disable()
     st = pstats.Stats(pr)
-    st.sort_stats("tottime").print_stats(40)
-    st.sort_stats("cumtime").print_stats(40)
+    st.sort_stats("tottime").print_stats(30)
+    st.sort_stats("cumtime").print_stats(30)
 
 
 if __name__ == "__main__":

@@ -17,3 +17,8 @@ cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format cs
 cd $R && python3 tools/gpu/trace_summary.py gpurun_out/r5i2_prof --calls 110 > gpurun_out/r5i2_trace_summary.txt; head -12 gpurun_out/r5i2_trace_summary.txt; tail -1 gpurun_out/r5i2_trace_summary.txt; rm -rf gpurun_out/r5i2_prof
 timeout -k 10 300 python3 benchmarks/bench_collection.py --sync-every-step --steps 200 --warmup 20 > gpurun_out/r5i2_coll_sync.json 2>&1 || { tail -5 gpurun_out/r5i2_coll_sync.json; exit 1; }
 tail -1 gpurun_out/r5i2_coll_sync.json | cut -c1-900
+for w in cls reg; do
+  timeout -k 10 200 python3 benchmarks/compute_cprofile.py --which $w > gpurun_out/r5i2_cprof_$w.txt 2>&1 || { tail -5 gpurun_out/r5i2_cprof_$w.txt; exit 1; }
+  timeout -k 10 200 python3 benchmarks/compute_cprofile.py --which $w --update-only > gpurun_out/r5i2_cprof_${w}_upd.txt 2>&1 || { tail -5 gpurun_out/r5i2_cprof_${w}_upd.txt; exit 1; }
+done
+grep -m3 "function calls" gpurun_out/r5i2_cprof_*.txt

@@ -167,3 +167,25 @@ def test_regression_collection_update_is_one_moments_pass(monkeypatch):
         if i > 0:  # (the first update finds the compute groups member by member)
             assert n_gpu == 1, n_gpu
         _check(gr.compute(), cr.compute())
+
+
+def test_regression_collection_update_replay():
+    """After one merged step the collection replays the recorded moments call (utils/fused_moments.py): the values
+    still equal the CPU collection across steps, reset, a reconfigured member and a shape change (which fall back to
+    the members' own updates and re-record)."""
+    gr, cr = _reg().to(DEV), _reg()
+    for i in range(6):
+        _, _, x, y = _batch(80 + i, n=4096 if i != 4 else 1000)
+        gr.update(x.to(DEV), y.to(DEV))
+        cr.update(x, y)
+        _check(gr.compute(), cr.compute())
+        if i == 2:
+            rp = gr.__dict__.get("_moments_replay")
+            assert rp is not None and rp.calls >= 1 and len(rp.members) == 5
+            gr.reset()
+            cr.reset()
+    rp = gr.__dict__.get("_moments_replay")
+    assert rp is not None and rp.calls >= 1
+    # a bad shape still raises the member's error (the replay declines other shapes)
+    with pytest.raises(RuntimeError):
+        gr.update(torch.randn(10, device=DEV), torch.randn(11, device=DEV))

@@ -172,7 +172,7 @@ def test_moments_plan_merging_on_cpu(monkeypatch):
     monkeypatch.setattr(ops.MomentsPlan, "deferrable", lambda self: True)
     calls = []
     orig = ops.run_moments_plans
-    monkeypatch.setattr(ops, "run_moments_plans", lambda plans: calls.append(orig(plans)))
+    monkeypatch.setattr(ops, "run_moments_plans", lambda plans, merged_out=None: calls.append(orig(plans, merged_out)))
 
     def members():
         return {"mse": R.MeanSquaredError(), "r2": R.R2Score(), "pearson": R.PearsonCorrCoef(),

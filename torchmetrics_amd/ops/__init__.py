@@ -734,9 +734,10 @@ def states_ready(owner: dict, states: tuple, dev: int, dtypes: tuple = (torch.fl
     return ok
 
 
-def run_moments_plans(plans: "list[MomentsPlan]") -> int:
+def run_moments_plans(plans: "list[MomentsPlan]", merged_out: Optional[list] = None) -> int:
     """Execute deferred plans, merging those on identical inputs (at most one Pearson fold and 32 plain
-    destinations per launch).  Returns the number of kernel calls issued."""
+    destinations per launch).  Returns the number of kernel calls issued; ``merged_out`` receives the merged plans
+    (``utils/fused_moments.py`` records a one-call step for replay)."""
     groups: "dict[tuple, list[MomentsPlan]]" = {}
     for pl in plans:
         groups.setdefault(pl.key(), []).append(pl)
@@ -768,6 +769,8 @@ def run_moments_plans(plans: "list[MomentsPlan]") -> int:
                 merged._mask = None
             merged.run()
             calls += 1
+            if merged_out is not None:
+                merged_out.append(merged)
             members = rest
     return calls
 

@@ -178,7 +178,7 @@ def test_regression_collection_update_replay():
     still equal the CPU collection across steps, reset, a reconfigured member and a shape change (which fall back to
     the members' own updates and re-record)."""
     gr, cr = _reg().to(DEV), _reg()
-    for i in range(6):
+    for i in range(7):  # (step 4 changes the batch size: step 5 re-records, step 6 replays)
         _, _, x, y = _batch(80 + i, n=4096 if i != 4 else 1000)
         gr.update(x.to(DEV), y.to(DEV))
         cr.update(x, y)

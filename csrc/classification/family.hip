@@ -61,6 +61,8 @@ struct FamilySpec {
   int* err_scratch;
   int part_words, off_cv, off_cb;
   int need_cm;
+  int abl;  // profiling ablation (TM_AMD_FAMILY_ABLATE, default 0: results are WRONG when set): 1 no threshold
+            // searches, 2 no calibration bins, 4 no global flush, 8 no class-ordered softmax sums
 };
 
 __device__ __forceinline__ int bucket_of(const double* __restrict__ thr, int t, double p) {
@@ -157,6 +159,7 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_kernel(const scalar_t
   if (__any(outside) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(&blk_outside, 1);
   if (__any(bad) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(sp.err_scratch, kErrTargetOutOfRange);
   __syncthreads();
+  if (sp.abl & 4) return;
   for (int i = threadIdx.x; i < sp.off_cb; i += kFamThreads)
     if (h[i]) atomicAdd(&sp.img[i], h[i]);
   for (int i = sp.off_cb + threadIdx.x; i < sp.part_words; i += kFamThreads)
@@ -210,7 +213,9 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar
     // softmax denominators in class order (every lane gets the same sums)
     const float e_cal = mine ? expf(v - mx) : 0.f;
     float s_cal = 0.f;
-    for (int k = 0; k < C; ++k) s_cal += __shfl(e_cal, gbase + k, kWave);
+    if (sp.abl & 8) s_cal = 1.f;
+    else
+      for (int k = 0; k < C; ++k) s_cal += __shfl(e_cal, gbase + k, kWave);
     float s_cur = s_cal;
     const bool nan_row = !(mf == mx);  // a NaN in the row: the two shifts differ (uniform within the group)
     float e_cur = e_cal;
@@ -230,11 +235,12 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar
       const double praw = static_cast<double>(v);
       const double psoft = static_cast<double>(round_to<scalar_t>(e_cur / s_cur));
       const int pos = c == t;
-      const int braw = bucket_of(thr_s, T, praw), bsoft = bucket_of(thr_s, T, psoft);
+      const int braw = (sp.abl & 1) ? 0 : bucket_of(thr_s, T, praw);
+      const int bsoft = (sp.abl & 1) ? static_cast<int>(psoft) : bucket_of(thr_s, T, psoft);
       atomicAdd(&h[sp.off_cv + ((0 * (T + 1) + braw) * C + c) * 2 + pos], 1);
       atomicAdd(&h[sp.off_cv + ((1 * (T + 1) + bsoft) * C + c) * 2 + pos], 1);
     }
-    if (nb > 0) {
+    if (nb > 0 && !(sp.abl & 2)) {
       float sv = mine ? round_to<scalar_t>(e_cal / s_cal) : -INFINITY;
       int si = mine ? c : 0x7fffffff;
 #pragma unroll
@@ -459,6 +465,11 @@ void mc_family_update(const at::Tensor& preds, const at::Tensor& target, at::Ten
     }
   }
   sp.need_cm = sp.n_cm > 0 || sp.n_st > 0;
+  static const int abl = [] {
+    const char* e = std::getenv("TM_AMD_FAMILY_ABLATE");
+    return e ? std::atoi(e) : 0;
+  }();
+  sp.abl = abl;
   if (curve.numel() > 0) {
     sp.T = static_cast<int>(thr_sorted.numel());
     TORCH_CHECK(sp.T >= 1 && thr_sorted.scalar_type() == at::kDouble && perm.scalar_type() == at::kLong &&

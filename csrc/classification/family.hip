@@ -193,12 +193,26 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar
   const int gbase = (threadIdx.x & (kWave - 1)) - c;  // the group's first lane in the wave
   const bool has_c = c < C;
   bool outside = false, bad = false;
-  for (long long row0 = static_cast<long long>(blockIdx.x) * R; row0 < N;
-       row0 += static_cast<long long>(gridDim.x) * R) {  // uniform across the block: shuffles see whole groups
+  // 4 block steps per pass, their loads issued together (one wave per SIMD: a load per step would expose the
+  // memory latency 4 times)
+  const long long step = static_cast<long long>(gridDim.x) * R;
+  for (long long rb = static_cast<long long>(blockIdx.x) * R; rb < N; rb += 4 * step) {
+    float vv[4];
+    long long tt[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long row = rb + u * step + threadIdx.x / G;
+      vv[u] = (row < N && has_c) ? to_f32(preds[row * C + c]) : -INFINITY;
+      tt[u] = row < N ? static_cast<long long>(target[row]) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+    const long long row0 = rb + u * step;  // uniform across the block: shuffles see whole groups
+    if (row0 >= N) break;
     const long long row = row0 + threadIdx.x / G;
     const bool live = row < N;
     const bool mine = live && has_c;
-    const float v = mine ? to_f32(preds[row * C + c]) : -INFINITY;
+    const float v = vv[u];
     outside |= mine && !(v >= 0.f && v <= 1.f);
     float mf = mine ? v : -INFINITY;  // NaN-ignoring max (fmaxf drops NaN)
     float mx = v;
@@ -226,7 +240,7 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar
       if (nan_row) s_cur = t2;
       else e_cur = e_cal;
     }
-    const long long tv = live ? static_cast<long long>(target[row]) : 0;
+    const long long tv = tt[u];
     const bool valid = tv >= 0 && tv < C;
     bad |= live && c == 0 && !valid;
     const int t = static_cast<int>(valid ? tv : 0);
@@ -265,6 +279,7 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar
       }
     }
   }
+    }
   if (__any(outside) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(&blk_outside, 1);
   if (__any(bad) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(sp.err_scratch, kErrTargetOutOfRange);
   __syncthreads();

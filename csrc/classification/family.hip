@@ -62,7 +62,8 @@ struct FamilySpec {
   int part_words, off_cv, off_cb;
   int need_cm;
   int abl;  // profiling ablation (TM_AMD_FAMILY_ABLATE, default 0: results are WRONG when set): 1 no threshold
-            // searches, 2 no calibration bins, 4 no global flush, 8 no class-ordered softmax sums
+            // searches, 2 no calibration bins, 4 no global flush, 8 no class-ordered softmax sums, 16 no curve
+            // histogram at all
 };
 
 __device__ __forceinline__ int bucket_of(const double* __restrict__ thr, int t, double p) {
@@ -245,7 +246,7 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar
     bad |= live && c == 0 && !valid;
     const int t = static_cast<int>(valid ? tv : 0);
     if (live && valid && c == 0 && sp.need_cm) atomicAdd(&h[t * C + mi], 1);
-    if (mine && valid && T > 0) {
+    if (mine && valid && T > 0 && !(sp.abl & 16)) {
       const double praw = static_cast<double>(v);
       const double psoft = static_cast<double>(round_to<scalar_t>(e_cur / s_cur));
       const int pos = c == t;

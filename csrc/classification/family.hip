@@ -63,7 +63,7 @@ struct FamilySpec {
   int need_cm;
   int abl;  // profiling ablation (TM_AMD_FAMILY_ABLATE, default 0: results are WRONG when set): 1 no threshold
             // searches, 2 no calibration bins, 4 no global flush, 8 no class-ordered softmax sums, 16 no curve
-            // histogram at all
+            // histogram at all, 32 binary threshold search even on an even grid
 };
 
 __device__ __forceinline__ int bucket_of(const double* __restrict__ thr, int t, double p) {
@@ -74,6 +74,18 @@ __device__ __forceinline__ int bucket_of(const double* __restrict__ thr, int t, 
     else hi = mid;
   }
   return lo;
+}
+
+// Thresholds near an even grid (torch.linspace: the usual binned-curve argument): guess the count from the grid, then
+// step to the exact count -- one or two LDS reads instead of a log2(T)-deep chain of dependent ones.  Exact for any
+// sorted thresholds (the steps correct any guess); the grid only makes it short.
+__device__ __forceinline__ int bucket_guess(const double* __restrict__ thr, int t, double p, double t0, double inv) {
+  if (!(p == p)) return 0;  // NaN: no threshold is <= p
+  const double g = (p - t0) * inv + 1.0;
+  int b = g <= 0.0 ? 0 : (g >= static_cast<double>(t) ? t : static_cast<int>(g));
+  while (b < t && thr[b] <= p) ++b;
+  while (b > 0 && thr[b - 1] > p) --b;
+  return b;
 }
 
 template <typename scalar_t, typename target_t>
@@ -190,6 +202,14 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar
   for (int i = threadIdx.x; i < nb; i += kFamThreads) bnd_s[i] = sp.bounds[i];
   if (threadIdx.x == 0) blk_outside = 0;
   __syncthreads();
+  // thresholds on an even grid (within 1e-9 of a step): the short search
+  const double t0 = T > 0 ? thr_s[0] : 0.0, tl = T > 0 ? thr_s[T - 1] : 0.0;
+  const double inv = T > 1 && tl > t0 ? static_cast<double>(T - 1) / (tl - t0) : 0.0;
+  bool off_grid = false;
+  for (int i = threadIdx.x; i < T; i += kFamThreads)
+    off_grid |= !(fabs((thr_s[i] - t0) * inv - static_cast<double>(i)) <= 1e-9);
+  const bool on_grid = !__syncthreads_or(off_grid);  // (every thread takes part)
+  const bool grid = !(sp.abl & 32) && T > 1 && inv > 0.0 && on_grid;
   const int c = threadIdx.x % G;
   const int gbase = (threadIdx.x & (kWave - 1)) - c;  // the group's first lane in the wave
   const bool has_c = c < C;
@@ -250,8 +270,17 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar
       const double praw = static_cast<double>(v);
       const double psoft = static_cast<double>(round_to<scalar_t>(e_cur / s_cur));
       const int pos = c == t;
-      const int braw = (sp.abl & 1) ? 0 : bucket_of(thr_s, T, praw);
-      const int bsoft = (sp.abl & 1) ? static_cast<int>(psoft) : bucket_of(thr_s, T, psoft);
+      int braw, bsoft;
+      if (sp.abl & 1) {
+        braw = 0;
+        bsoft = static_cast<int>(psoft);
+      } else if (grid) {
+        braw = bucket_guess(thr_s, T, praw, t0, inv);
+        bsoft = bucket_guess(thr_s, T, psoft, t0, inv);
+      } else {
+        braw = bucket_of(thr_s, T, praw);
+        bsoft = bucket_of(thr_s, T, psoft);
+      }
       atomicAdd(&h[sp.off_cv + ((0 * (T + 1) + braw) * C + c) * 2 + pos], 1);
       atomicAdd(&h[sp.off_cv + ((1 * (T + 1) + bsoft) * C + c) * 2 + pos], 1);
     }

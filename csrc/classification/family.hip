@@ -293,34 +293,19 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar
         const int oi = __shfl_xor(si, off, kWave);
         if (argmax_better(ov, oi, sv, si)) sv = ov, si = oi;
       }
-      // lane 0: the raw top-1 variant, lane 1: the softmax variant
-      int key = -1;
-      float cvv = 0.f, avv = 0.f;
-      if (live && c < 2) {
+      if (live && c < 2) {  // lane 0: the raw top-1 variant, lane 1: the softmax variant
         const float ar = mi == tv ? 1.f : 0.f, as = si == tv ? 1.f : 0.f;
         if (c == 0) sp.cand[row] = make_float4(mx, ar, sv, as);
-        cvv = c == 0 ? round_to<scalar_t>(mx) : sv;
-        avv = c == 0 ? ar : as;
+        const float cvv = c == 0 ? round_to<scalar_t>(mx) : sv;
+        const float avv = c == 0 ? ar : as;
         int b = -1;
         for (int k = 0; k < nb; ++k) b += (bnd_s[k] <= cvv) ? 1 : 0;
-        if (b >= 0) key = c * nb + b;
-      }
-      // wave-aggregated bin adds: the rows of a wave mostly share a bin (the raw top-1 score clamps into the last
-      // one), and per-lane float atomics on one LDS word serialise -- one add per distinct bin and wave instead
-      for (;;) {
-        const unsigned long long act = __ballot(key >= 0);
-        if (act == 0) break;
-        const int lead = __ffsll(static_cast<long long>(act)) - 1;
-        const int k0 = __shfl(key, lead, kWave);
-        const bool hit = key == k0;
-        const float n1 = wave_sum(hit ? 1.f : 0.f), s1 = wave_sum(hit ? cvv : 0.f), a1 = wave_sum(hit ? avv : 0.f);
-        if ((threadIdx.x & (kWave - 1)) == lead) {
-          float* dst = hf + sp.off_cb + k0 * 3;
-          atomicAdd(dst, n1);
-          atomicAdd(dst + 1, s1);
-          atomicAdd(dst + 2, a1);
+        if (b >= 0) {
+          float* dst = hf + sp.off_cb + (c * nb + b) * 3;
+          atomicAdd(dst, 1.f);
+          atomicAdd(dst + 1, cvv);
+          atomicAdd(dst + 2, avv);
         }
-        if (hit) key = -1;
       }
     }
   }

@@ -346,7 +346,7 @@ class MetricCollection(ModuleDict):
         # (descriptor rows holding device pointers) are rebuilt on first use in the copy
         state = self.__dict__.copy()
         for k in ("_status_host", "_status_ptr", "_fused_plan", "_compute_calls", "_fused_rebuilds", "_fused_off",
-                  "_family_plan", "_moments_replay"):
+                  "_family_plan", "_moments_replay", "_word_tables"):
             state.pop(k, None)
         return state
 
@@ -402,10 +402,16 @@ class MetricCollection(ModuleDict):
             d["_status_host"] = host
             d["_status_ptr"] = int(ops._ops().mapped_device_ptr(host))
         ptr = d["_status_ptr"]
-        for i in range(0, len(words), 128):
-            chunk = words[i : i + 128]
-            table = torch.tensor([[w.data_ptr(), c] for w, c in chunk], dtype=torch.int64)
-            ops._ops().gather_words(table, ptr + 4 * i, chunk[0][0])
+        # the word table of a steady collection repeats every compute: keep the last one (a host tensor built from
+        # a Python list costs more than the gather launch)
+        key = tuple((w.data_ptr(), c) for w, c in words)
+        cached = d.get("_word_tables")
+        if cached is None or cached[0] != key:
+            tables = [torch.tensor([list(k) for k in key[i : i + 128]], dtype=torch.int64)
+                      for i in range(0, len(words), 128)]
+            cached = d["_word_tables"] = (key, tables)
+        for j, table in enumerate(cached[1]):
+            ops._ops().gather_words(table, ptr + 4 * 128 * j, words[128 * j][0])
         torch.cuda.current_stream(words[0][0].device).synchronize()
         return host[: len(words)].tolist()
 

@@ -72,6 +72,81 @@ __device__ __forceinline__ void store_out(const EpiParams& ep, long long idx, fl
   }
 }
 
+// Element-wise epilogues (STORE / COSINE / EUCLID) of the 16-bit kernels run on the TRANSPOSED accumulator: those
+// kernels issue mfma(Y fragment, X fragment), so lane r holds output row wr + 32 a + r and, for e = 4 g + q, column
+// wc + 32 b + 8 g + 4 h + q -- four consecutive columns per group.  Each group leaves as ONE vector store (4 x 16-bit =
+// 8 B, 4 x fp32 = 16 B) instead of four 2- / 4-byte stores, with a quarter of the address arithmetic.
+template <int EPI>
+__device__ __forceinline__ constexpr bool rows_in_lanes() {
+  return EPI == 0 || EPI == 1 || EPI == 2;  // kStore, kEuclid, kCosine
+}
+
+template <int EPI, int NA, int WC, typename Dist2>
+__device__ __forceinline__ void tile_epilogue_t(f32x16 (&acc)[NA][2], const EpiParams& ep, int batch, int N, int M,
+                                                int row0, int col0, Dist2 dist2) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = (wave / WC) * 32 * NA, wc = (wave % WC) * 64;
+  const int h = lane >> 5, r = lane & 31;
+  const bool vec = (ep.ldo & 3) == 0 &&
+                   ((ep.out_kind ? reinterpret_cast<uintptr_t>(ep.out16) : reinterpret_cast<uintptr_t>(ep.out)) &
+                    (ep.out_kind ? 7 : 15)) == 0;
+#pragma unroll
+  for (int a = 0; a < NA; ++a) {
+    const int i = row0 + wr + 32 * a + r;
+    if (i >= N) continue;
+    float nxi = 0.f;
+    if constexpr (EPI != 0) nxi = ep.nx[batch * (long long)N + i];
+    const long long rowbase = batch * (long long)N * ep.ldo + (long long)i * ep.ldo;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int j0 = col0 + wc + 32 * b + 8 * g + 4 * h;
+        if (j0 >= M) continue;
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = j0 + q;
+          float x = acc[a][b][4 * g + q];
+          if (j < M) {
+            if constexpr (EPI == 0) {
+              x = (ep.zero_diag && i == j) ? 0.f : x * ep.scale;
+            } else if constexpr (EPI == 2) {
+              x = (ep.zero_diag && i == j) ? 0.f : x * nxi * ep.ny[batch * (long long)M + j] * ep.scale;
+            } else {
+              const float s2 = nxi + ep.ny[batch * (long long)M + j];
+              float d2 = s2 - 2.0f * x;
+              if (d2 < s2 * (1.0f / 128.0f)) d2 = dist2(i, j);  // cancellation guard: exact difference form
+              d2 = fmaxf(d2, 0.f);
+              if (ep.zero_diag && i == j) d2 = 0.f;
+              x = ep.sqrt_out ? sqrtf(d2) : d2;
+            }
+          }
+          v[q] = x;
+        }
+        if (vec && j0 + 3 < M) {
+          if (ep.out_kind == 0) {
+            *reinterpret_cast<f32x4*>(ep.out + rowbase + j0) = f32x4{v[0], v[1], v[2], v[3]};
+          } else {
+            uint16_t u[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              u[q] = ep.out_kind == 1 ? __builtin_bit_cast(uint16_t, static_cast<__bf16>(v[q]))
+                                      : __builtin_bit_cast(uint16_t, static_cast<_Float16>(v[q]));
+            const uint2 w = make_uint2(u[0] | (static_cast<uint32_t>(u[1]) << 16),
+                                       u[2] | (static_cast<uint32_t>(u[3]) << 16));
+            *reinterpret_cast<uint2*>(ep.out16 + rowbase + j0) = w;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (j0 + q < M) store_out(ep, rowbase + j0 + q, v[q]);
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ shared epilogue
 // One implementation for every kernel of this file.  The block tile is TM x TM, NT threads = NT / 64 waves laid out as
 // (NT / 64 / WC) wave rows x WC wave columns; a wave owns NA x 2 MFMA 32 x 32 tiles: acc[a][b][e] holds
@@ -664,7 +739,12 @@ __global__ __launch_bounds__(TM == 256 ? 512 : 256) void gemm_nt_h16_kernel(
 #pragma unroll
     for (int a = 0; a < NA; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) acc[a][b] = Mfma16<T>::run(fa[a], fb[b], acc[a][b]);
+      for (int b = 0; b < 2; ++b) {
+        if constexpr (rows_in_lanes<EPI>())
+          acc[a][b] = Mfma16<T>::run(fb[b], fa[a], acc[a][b]);  // transposed tile: output rows in lanes
+        else
+          acc[a][b] = Mfma16<T>::run(fa[a], fb[b], acc[a][b]);
+      }
   };
   v8 ca[NA], cb[2], na[NA], nb[2];
   // chunk kc+1's barrier sits inside chunk kc, after its last LDS read (step 3's fragments, loaded during step 2's
@@ -697,17 +777,20 @@ __global__ __launch_bounds__(TM == 256 ? 512 : 256) void gemm_nt_h16_kernel(
     }
   }
   // (no DMA is in flight: the last chunk issued none)
-  tile_epilogue<EPI, NA, WC, TM, NT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile,
-                                     [&](int i, int j) {
-                                       const uint16_t* xr = xrow(i);
-                                       const uint16_t* yr = yrow(j);
-                                       float t = 0.f;
-                                       for (int k = 0; k < D; ++k) {
-                                         const float d = Mfma16<T>::to_f32(xr[k]) - Mfma16<T>::to_f32(yr[k]);
-                                         t = fmaf(d, d, t);
-                                       }
-                                       return t;
-                                     });
+  auto dist2 = [&](int i, int j) {
+    const uint16_t* xr = xrow(i);
+    const uint16_t* yr = yrow(j);
+    float t = 0.f;
+    for (int k = 0; k < D; ++k) {
+      const float d = Mfma16<T>::to_f32(xr[k]) - Mfma16<T>::to_f32(yr[k]);
+      t = fmaf(d, d, t);
+    }
+    return t;
+  };
+  if constexpr (rows_in_lanes<EPI>())
+    tile_epilogue_t<EPI, NA, WC>(acc, ep, batch, N, M, row0, col0, dist2);
+  else
+    tile_epilogue<EPI, NA, WC, TM, NT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile, dist2);
 }
 
 // 256 x 256 tile, 8 waves, a 4-deep ring of 32-wide k-chunks (32 KiB per stage: 128 KiB of LDS, as the 2 x 64-wide
@@ -796,7 +879,12 @@ __global__ __launch_bounds__(512) void gemm_nt_h16_ring_kernel(const uint16_t* _
 #pragma unroll
     for (int a = 0; a < NA; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) acc[a][b] = Mfma16<T>::run(fa[a], fb[b], acc[a][b]);
+      for (int b = 0; b < 2; ++b) {
+        if constexpr (rows_in_lanes<EPI>())
+          acc[a][b] = Mfma16<T>::run(fb[b], fa[a], acc[a][b]);  // transposed tile: output rows in lanes
+        else
+          acc[a][b] = Mfma16<T>::run(fa[a], fb[b], acc[a][b]);
+      }
   };
   // prologue: chunks 0 .. 2 in flight (4 DMA instructions per chunk and thread)
   stage(0);
@@ -820,17 +908,20 @@ __global__ __launch_bounds__(512) void gemm_nt_h16_ring_kernel(const uint16_t* _
     mma(fa1, fb1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
-  tile_epilogue<EPI, NA, WC, TM, NT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile,
-                                     [&](int i, int j) {
-                                       const uint16_t* xr = xrow(i);
-                                       const uint16_t* yr = yrow(j);
-                                       float t = 0.f;
-                                       for (int k = 0; k < D; ++k) {
-                                         const float d = Mfma16<T>::to_f32(xr[k]) - Mfma16<T>::to_f32(yr[k]);
-                                         t = fmaf(d, d, t);
-                                       }
-                                       return t;
-                                     });
+  auto dist2 = [&](int i, int j) {
+    const uint16_t* xr = xrow(i);
+    const uint16_t* yr = yrow(j);
+    float t = 0.f;
+    for (int k = 0; k < D; ++k) {
+      const float d = Mfma16<T>::to_f32(xr[k]) - Mfma16<T>::to_f32(yr[k]);
+      t = fmaf(d, d, t);
+    }
+    return t;
+  };
+  if constexpr (rows_in_lanes<EPI>())
+    tile_epilogue_t<EPI, NA, WC>(acc, ep, batch, N, M, row0, col0, dist2);
+  else
+    tile_epilogue<EPI, NA, WC, TM, NT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile, dist2);
 }
 
 // The 256 x 256 kernel for large problems: D a multiple of its k-step, both sides at least one tile, enough tiles to

@@ -77,15 +77,15 @@ __device__ __forceinline__ void store_out(const EpiParams& ep, long long idx, fl
 // wc + 32 b + 8 g + 4 h + q -- four consecutive columns per group.  Each group leaves as ONE vector store (4 x 16-bit =
 // 8 B, 4 x fp32 = 16 B) instead of four 2- / 4-byte stores, with a quarter of the address arithmetic.
 template <int EPI>
-__device__ __forceinline__ constexpr bool rows_in_lanes() {
+__host__ __device__ __forceinline__ constexpr bool rows_in_lanes() {
   return EPI == 0 || EPI == 1 || EPI == 2;  // kStore, kEuclid, kCosine
 }
 
-template <int EPI, int NA, int WC, typename Dist2>
-__device__ __forceinline__ void tile_epilogue_t(f32x16 (&acc)[NA][2], const EpiParams& ep, int batch, int N, int M,
+template <int EPI, int NA, int WC, typename Dist2, int NB = 2>
+__device__ __forceinline__ void tile_epilogue_t(f32x16 (&acc)[NA][NB], const EpiParams& ep, int batch, int N, int M,
                                                 int row0, int col0, Dist2 dist2) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = (wave / WC) * 32 * NA, wc = (wave % WC) * 64;
+  const int wr = (wave / WC) * 32 * NA, wc = (wave % WC) * 32 * NB;
   const int h = lane >> 5, r = lane & 31;
   const bool vec = (ep.ldo & 3) == 0 &&
                    ((ep.out_kind ? reinterpret_cast<uintptr_t>(ep.out16) : reinterpret_cast<uintptr_t>(ep.out)) &
@@ -98,7 +98,7 @@ __device__ __forceinline__ void tile_epilogue_t(f32x16 (&acc)[NA][2], const EpiP
     if constexpr (EPI != 0) nxi = ep.nx[batch * (long long)N + i];
     const long long rowbase = batch * (long long)N * ep.ldo + (long long)i * ep.ldo;
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < NB; ++b) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int j0 = col0 + wc + 32 * b + 8 * g + 4 * h;
@@ -793,6 +793,130 @@ __global__ __launch_bounds__(TM == 256 ? 512 : 256) void gemm_nt_h16_kernel(
     tile_epilogue<EPI, NA, WC, TM, NT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile, dist2);
 }
 
+// 256 x 256 tile, FOUR waves of 128 x 128 (4 x 4 MFMA 32 x 32 tiles each, 256 accumulators per lane): per k-step a
+// wave reads 8 fragments for 16 MFMAs (the 8-wave kernel: 6 for 8), and half as many waves meet at each chunk
+// barrier.  Element-wise epilogues only (transposed accumulator, rows in lanes).  Same 2-stage 64-wide k-chunk staging.
+template <int EPI, typename T>
+__global__ __launch_bounds__(256) void gemm_nt_h16_w4_kernel(const uint16_t* __restrict__ X,
+                                                             const uint16_t* __restrict__ Y, int N, int M, int D,
+                                                             long long bx, long long by, int tiles_m, EpiParams ep) {
+  constexpr int TM = 256, WC = 2, NA = 4, NB = 4, KC = 64;
+  static_assert(rows_in_lanes<EPI>(), "w4 kernel: element-wise epilogues");
+  typedef typename Mfma16<T>::v8 v8;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  uint16_t* sh = reinterpret_cast<uint16_t*>(smem);
+  constexpr int kStage = 2 * TM * KC;
+  const int batch = blockIdx.z;
+  const int32_t* gix = ep.ix ? ep.ix + (long long)batch * N : nullptr;
+  const int32_t* giy = ep.iy ? ep.iy + (long long)batch * M : nullptr;
+  if (!gix) X += batch * bx;
+  if (!giy) Y += batch * by;
+  auto xrow = [&](int i) -> const uint16_t* { return X + (long long)(gix ? gix[i] : i) * D; };
+  auto yrow = [&](int j) -> const uint16_t* { return Y + (long long)(giy ? giy[j] : j) * D; };
+  const int tiles_n = (N + TM - 1) / TM;
+  const int total = tiles_n * tiles_m;
+  const int bid = blockIdx.x;
+  const int per = (total + 7) / 8;
+  const int tile = (bid % 8) * per + bid / 8;
+  if (tile >= total) return;
+  const int ti = tile / tiles_m, tj = tile - ti * tiles_m;
+  const int row0 = ti * TM, col0 = tj * TM;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = (wave / WC) * 32 * NA, wc = (wave % WC) * 32 * NB;
+  const int h = lane >> 5, r = lane & 31;
+  // DMA: wave w moves rows [64 w, 64 w + 64) of both operand tiles, 8 rows (1 KiB) per instruction
+  const uint16_t* srcA[8];
+  const uint16_t* srcB[8];
+  int kof[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int rr = 64 * wave + 8 * q + (lane >> 3);
+    const int c = (lane & 7) ^ ((rr >> 1) & 7);
+    kof[q] = 8 * c;
+    srcA[q] = xrow(min(row0 + rr, N - 1)) + 8 * c;
+    srcB[q] = yrow(min(col0 + rr, M - 1)) + 8 * c;
+  }
+  typedef __attribute__((address_space(3))) void lds_t;
+  typedef __attribute__((address_space(1))) void glb_t;
+  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
+  auto stage = [&](int kc, int buf) {
+    uint16_t* sa = sh + buf * kStage;
+    uint16_t* sb = sa + TM * KC;
+    const int k0 = kc * KC;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const bool in = k0 + kof[q] < D;
+      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcA[q] + k0 : zero), (lds_t*)(sa + (64 * wave + 8 * q) * KC),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcB[q] + k0 : zero), (lds_t*)(sb + (64 * wave + 8 * q) * KC),
+                                       16, 0, 0);
+    }
+  };
+  f32x16 acc[NA][NB];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+  const int swz_a = ((wr + r) >> 1) & 7;
+  const int swz_b = ((wc + r) >> 1) & 7;
+  const int nk = (D + KC - 1) / KC;
+  auto frag = [&](int buf, int s, v8* fa, v8* fb) {
+    const uint16_t* sa = sh + buf * kStage + (wr + r) * KC;
+    const uint16_t* sb = sh + buf * kStage + TM * KC + (wc + r) * KC;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) fa[a] = *reinterpret_cast<const v8*>(sa + 32 * a * KC + 8 * ((2 * s + h) ^ swz_a));
+#pragma unroll
+    for (int b = 0; b < NB; ++b) fb[b] = *reinterpret_cast<const v8*>(sb + 32 * b * KC + 8 * ((2 * s + h) ^ swz_b));
+  };
+  auto mma = [&](const v8* fa, const v8* fb) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) acc[a][b] = Mfma16<T>::run(fb[b], fa[a], acc[a][b]);
+  };
+  v8 ca[NA], cb[NB], na[NA], nb[NB];
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (nk > 1) stage(1, 1);
+  frag(0, 0, ca, cb);
+  for (int kc = 0; kc < nk; ++kc) {
+    const int buf = kc & 1;
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const bool more = s4 < 3 || kc + 1 < nk;
+      if (s4 < 3) {
+        frag(buf, s4 + 1, na, nb);
+      } else if (kc + 1 < nk) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kc + 2 < nk) stage(kc + 2, buf);
+        frag(buf ^ 1, 0, na, nb);
+      }
+      mma(ca, cb);
+      if (more) {
+#pragma unroll
+        for (int a = 0; a < NA; ++a) ca[a] = na[a];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) cb[b] = nb[b];
+      }
+    }
+  }
+  auto dist2 = [&](int i, int j) {
+    const uint16_t* xr = xrow(i);
+    const uint16_t* yr = yrow(j);
+    float t = 0.f;
+    for (int k = 0; k < D; ++k) {
+      const float d = Mfma16<T>::to_f32(xr[k]) - Mfma16<T>::to_f32(yr[k]);
+      t = fmaf(d, d, t);
+    }
+    return t;
+  };
+  tile_epilogue_t<EPI, NA, WC, decltype(dist2), NB>(acc, ep, batch, N, M, row0, col0, dist2);
+}
+
 // 256 x 256 tile, 8 waves, a 4-deep ring of 32-wide k-chunks (32 KiB per stage: 128 KiB of LDS, as the 2 x 64-wide
 // kernel above) so THREE chunks of DMA are in flight while one is multiplied -- the 2-stage kernel waits for the next
 // chunk's loads one chunk after issuing them.  Rows are 64 B: a 1 KiB global_load_lds instruction moves 16 rows, and
@@ -1009,6 +1133,17 @@ void launch_h16(const at::Tensor& x, const at::Tensor& y, int batches, long long
     const char* e = std::getenv("TM_AMD_GEMM16_RING");
     return e ? std::atoi(e) : 0;
   }();
+  static const int w4 = [] {
+    const char* e = std::getenv("TM_AMD_GEMM16_W4");
+    return e ? std::atoi(e) : 0;
+  }();
+  if constexpr (rows_in_lanes<EPI>()) {
+    if (big && w4) {
+      hipLaunchKernelGGL((gemm_nt_h16_w4_kernel<EPI, T>), dim3(per * 8, 1, batches), dim3(256), lds, stream(), xp, yp,
+                         N, M, D, bx, by, tiles_m, ep);
+      return;
+    }
+  }
   if (big && ring)
     hipLaunchKernelGGL((gemm_nt_h16_ring_kernel<EPI, T>), dim3(per * 8, 1, batches), dim3(512), lds, stream(), xp,
                        yp, N, M, D, bx, by, tiles_m, ep);
@@ -1146,11 +1281,80 @@ at::Tensor gemm_nt(const at::Tensor& x, const at::Tensor& y, int64_t kind, const
   return out;
 }
 
+namespace {
+// one wave per row: fp32 sum of squares of a [rows, D] fp32 / bf16 / fp16 operand (16-byte loads when D allows),
+// then the squared norm (mode 0) or the inverse norm 1 / sqrt (mode 1) -- the epilogue factors of EUCLID / COSINE
+template <typename T>
+__global__ void __launch_bounds__(256) row_norms_kernel(const T* __restrict__ x, long long rows, int D, int mode,
+                                                        float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (static_cast<long long>(blockIdx.x) * 256 + threadIdx.x) / 64;
+  if (row >= rows) return;  // (whole waves)
+  const T* r = x + row * D;
+  float s = 0.f;
+  constexpr int kVec = 16 / sizeof(T);
+  if (D % kVec == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    for (int c = lane * kVec; c < D; c += 64 * kVec) {
+      const u32x4 w = *reinterpret_cast<const u32x4*>(r + c);
+      const T* e = reinterpret_cast<const T*>(&w);
+#pragma unroll
+      for (int k = 0; k < kVec; ++k) {
+        const float v = to_f32(e[k]);
+        s = fmaf(v, v, s);
+      }
+    }
+  } else {
+    for (int c = lane; c < D; c += 64) {
+      const float v = to_f32(r[c]);
+      s = fmaf(v, v, s);
+    }
+  }
+  s = wave_sum(s);
+  if (lane == 0) out[row] = mode ? 1.f / sqrtf(s) : s;
+}
+}  // namespace
+
+// x: [..., D] contiguous fp32 / bf16 / fp16 -> fp32 [rows]: squared row norms (mode 0) or inverse norms (mode 1)
+at::Tensor row_norms(const at::Tensor& x, int64_t mode) {
+  TM_CHECK_CUDA(x);
+  TM_CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() >= 1 && (mode == 0 || mode == 1), "row_norms: [..., D] operand, mode 0 / 1");
+  const int D = static_cast<int>(x.size(-1));
+  const long long rows = D > 0 ? x.numel() / D : 0;
+  at::Tensor out = at::empty({rows}, x.options().dtype(at::kFloat));
+  if (rows == 0) return out;
+  const dim3 grid(static_cast<unsigned>((rows + 3) / 4));
+  switch (x.scalar_type()) {
+    case at::kFloat:
+      hipLaunchKernelGGL((row_norms_kernel<float>), grid, dim3(256), 0, stream(), x.data_ptr<float>(), rows, D,
+                         static_cast<int>(mode), out.data_ptr<float>());
+      break;
+    case at::kBFloat16:
+      hipLaunchKernelGGL((row_norms_kernel<c10::BFloat16>), grid, dim3(256), 0, stream(),
+                         reinterpret_cast<const c10::BFloat16*>(x.data_ptr()), rows, D, static_cast<int>(mode),
+                         out.data_ptr<float>());
+      break;
+    case at::kHalf:
+      hipLaunchKernelGGL((row_norms_kernel<c10::Half>), grid, dim3(256), 0, stream(),
+                         reinterpret_cast<const c10::Half*>(x.data_ptr()), rows, D, static_cast<int>(mode),
+                         out.data_ptr<float>());
+      break;
+    default:
+      TORCH_CHECK(false, "row_norms: fp32 / bf16 / fp16 operand");
+  }
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return out;
+}
+
 }  // namespace tm_amd
 
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def("row_norms(Tensor x, int mode) -> Tensor");
   m.def(
       "gemm_nt(Tensor x, Tensor y, int kind, Tensor? aux_x, Tensor? aux_y, float scale, float coef, int degree, "
       "bool zero_diag, bool sqrt_out, Tensor? idx_x=None, Tensor? idx_y=None, int out_kind=0) -> Tensor");
 }
-TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) { m.impl("gemm_nt", &tm_amd::gemm_nt); }
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
+  m.impl("gemm_nt", &tm_amd::gemm_nt);
+  m.impl("row_norms", &tm_amd::row_norms);
+}

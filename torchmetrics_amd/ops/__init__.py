@@ -1391,6 +1391,15 @@ def corr_merge(stacked: Tensor) -> Tensor:
 GEMM_STORE, GEMM_EUCLID, GEMM_COSINE, GEMM_POLY_SUM, GEMM_ROW_MIN, GEMM_ROW_SUM, GEMM_ROW_COL_MAX = range(7)
 
 
+def row_norms(x: Tensor, inverse: bool = False) -> Tensor:
+    """fp32 squared row norms (or inverse norms ``1 / ||x_i||``) of a ``[..., D]`` operand, accumulated in fp32 from
+    the operand's own dtype: one wave per row on ROCm (``csrc/pairwise/gemm_nt.hip`` ``row_norms``)."""
+    if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16, torch.float16):
+        return _ops().row_norms(x.contiguous(), 1 if inverse else 0)
+    s = torch.linalg.vector_norm(x, 2, dim=-1, dtype=torch.float32).reshape(-1)
+    return 1.0 / s if inverse else s * s
+
+
 def gemm_nt(x: Tensor, y: Tensor, kind: int, aux_x: Optional[Tensor] = None, aux_y: Optional[Tensor] = None,
             scale: float = 1.0, coef: float = 0.0, degree: int = 1, zero_diagonal: bool = False,
             sqrt_out: bool = True, idx_x: Optional[Tensor] = None, idx_y: Optional[Tensor] = None,

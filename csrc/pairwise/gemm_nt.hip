@@ -104,6 +104,18 @@ __device__ __forceinline__ void tile_epilogue_t(f32x16 (&acc)[NA][NB], const Epi
         const int j0 = col0 + wc + 32 * b + 8 * g + 4 * h;
         if (j0 >= M) continue;
         float v[4];
+        float nyq[4] = {0.f, 0.f, 0.f, 0.f};  // the group's four column factors: one 16-byte load when aligned
+        if constexpr (EPI != 0) {
+          const long long o = batch * (long long)M + j0;
+          if (j0 + 3 < M && (o & 3) == 0) {
+            const f32x4 w = *reinterpret_cast<const f32x4*>(ep.ny + o);
+            nyq[0] = w[0], nyq[1] = w[1], nyq[2] = w[2], nyq[3] = w[3];
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (j0 + q < M) nyq[q] = ep.ny[o + q];
+          }
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int j = j0 + q;
@@ -112,9 +124,9 @@ __device__ __forceinline__ void tile_epilogue_t(f32x16 (&acc)[NA][NB], const Epi
             if constexpr (EPI == 0) {
               x = (ep.zero_diag && i == j) ? 0.f : x * ep.scale;
             } else if constexpr (EPI == 2) {
-              x = (ep.zero_diag && i == j) ? 0.f : x * nxi * ep.ny[batch * (long long)M + j] * ep.scale;
+              x = (ep.zero_diag && i == j) ? 0.f : x * nxi * nyq[q] * ep.scale;
             } else {
-              const float s2 = nxi + ep.ny[batch * (long long)M + j];
+              const float s2 = nxi + nyq[q];
               float d2 = s2 - 2.0f * x;
               if (d2 < s2 * (1.0f / 128.0f)) d2 = dist2(i, j);  // cancellation guard: exact difference form
               d2 = fmaxf(d2, 0.f);

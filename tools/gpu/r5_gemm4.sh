@@ -1,0 +1,12 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp PYTHONPATH="$GRAFT_REPO_ROOT"
+R=$GRAFT_REPO_ROOT
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_gemm_h16_gpu.py tests/test_pairwise.py tests/test_pairwise_precision_gpu.py -m gpu > gpurun_out/r5g4_tests.log 2>&1 || { tail -30 gpurun_out/r5g4_tests.log; exit 1; }
+tail -1 gpurun_out/r5g4_tests.log
+timeout -k 10 200 python3 benchmarks/bench_gemm16.py > gpurun_out/r5g4_bench.jsonl 2>&1 || { tail -5 gpurun_out/r5g4_bench.jsonl; exit 1; }
+grep -h shape gpurun_out/r5g4_bench.jsonl | python3 -c "
+import sys, json
+for l in sys.stdin:
+    d = json.loads(l); print(d['dtype'], d['shape'], 'store', d['store_ms'], 'blt', d['hipblaslt_ms'], 'cos', d['pairwise_cosine_ms'], 'ref', d['reference_recipe_cosine_ms'], 'rcmax', d['fused_rowcolmax_ms'], d['vendor_rowcolmax_ms'], 'poly', d['fused_polysum_ms'], d['vendor_polysum_ms'])"

@@ -934,11 +934,14 @@ __global__ __launch_bounds__(256) void gemm_nt_h16_w4_kernel(const uint16_t* __r
 // chunk's loads one chunk after issuing them.  Rows are 64 B: a 1 KiB global_load_lds instruction moves 16 rows, and
 // the 16-B slot of logical chunk c in row r is c ^ ((r >> 2) & 3), which keeps every ds_read_b128 lane group on 16
 // distinct slots of the 256-B bank row (rows r and r + 4 share banks unless their slots differ).
-template <int EPI, typename T>
+// STAGES = 2 (64 KiB of LDS): two blocks share a CU, so one block's epilogue stores and the next one's first loads
+// overlap the other block's main loop (with 128 KiB per block, every CU alternates load / compute / store phases in
+// lock-step with the whole chip).
+template <int EPI, typename T, int STAGES>
 __global__ __launch_bounds__(512) void gemm_nt_h16_ring_kernel(const uint16_t* __restrict__ X,
                                                                const uint16_t* __restrict__ Y, int N, int M, int D,
                                                                long long bx, long long by, int tiles_m, EpiParams ep) {
-  constexpr int TM = 256, NT = 512, WC = 4, NA = 4, KC = 32, STAGES = 4;
+  constexpr int TM = 256, NT = 512, WC = 4, NA = 4, KC = 32;
   typedef typename Mfma16<T>::v8 v8;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   uint16_t* sh = reinterpret_cast<uint16_t*>(smem);
@@ -1022,21 +1025,21 @@ __global__ __launch_bounds__(512) void gemm_nt_h16_ring_kernel(const uint16_t* _
           acc[a][b] = Mfma16<T>::run(fa[a], fb[b], acc[a][b]);
       }
   };
-  // prologue: chunks 0 .. 2 in flight (4 DMA instructions per chunk and thread)
-  stage(0);
-  if (nk > 1) stage(1);
-  if (nk > 2) stage(2);
+  // prologue: chunks 0 .. STAGES - 2 in flight (4 DMA instructions per chunk and thread)
+#pragma unroll
+  for (int q = 0; q < STAGES - 1; ++q)
+    if (q < nk) stage(q);
   v8 fa0[NA], fb0[2], fa1[NA], fb1[2];
   for (int kc = 0; kc < nk; ++kc) {
     // chunk kc landed when at most the later chunks' DMAs are outstanding (loads retire in order)
-    const int later = min(nk - 1, kc + 2) - kc;
+    const int later = min(nk - 1, kc + STAGES - 2) - kc;
     if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // every wave's part of chunk kc is in LDS, and every wave finished reading chunk kc - 1 (its fragments were
-    // consumed by MFMAs issued before this point): its buffer may take chunk kc + 3
+    // consumed by MFMAs issued before this point): its buffer may take chunk kc + STAGES - 1
     __builtin_amdgcn_s_barrier();
-    if (kc + 3 < nk) stage(kc + 3);
+    if (kc + STAGES - 1 < nk) stage(kc + STAGES - 1);
     const int buf = kc % STAGES;
     frag(buf, 0, fa0, fb0);
     frag(buf, 1, fa1, fb1);
@@ -1156,8 +1159,11 @@ void launch_h16(const at::Tensor& x, const at::Tensor& y, int batches, long long
       return;
     }
   }
-  if (big && ring)
-    hipLaunchKernelGGL((gemm_nt_h16_ring_kernel<EPI, T>), dim3(per * 8, 1, batches), dim3(512), lds, stream(), xp,
+  if (big && ring == 2)
+    hipLaunchKernelGGL((gemm_nt_h16_ring_kernel<EPI, T, 2>), dim3(per * 8, 1, batches), dim3(512), lds / 2, stream(),
+                       xp, yp, N, M, D, bx, by, tiles_m, ep);
+  else if (big && ring)
+    hipLaunchKernelGGL((gemm_nt_h16_ring_kernel<EPI, T, 4>), dim3(per * 8, 1, batches), dim3(512), lds, stream(), xp,
                        yp, N, M, D, bx, by, tiles_m, ep);
   else if (big)
     hipLaunchKernelGGL((gemm_nt_h16_kernel<EPI, T, 256>), dim3(per * 8, 1, batches), dim3(512), lds, stream(), xp, yp,
@@ -1221,7 +1227,13 @@ at::Tensor gemm_nt(const at::Tensor& x, const at::Tensor& y, int64_t kind, const
   TORCH_CHECK(D > 0 && N > 0 && M > 0, "gemm_nt: empty operands");
   TORCH_CHECK(static_cast<long long>(N) * M * B < (1LL << 40), "gemm_nt: output too large");
   // 16-bit operands: the 256 x 256 tile once it alone fills the chip (256 tiles), else 128 x 128
-  const bool big = h16 ? static_cast<long long>((N + 255) / 256) * ((M + 255) / 256) * B >= 256 : big_choice(N, M, D, B);
+  static const int big16_env = [] {  // TM_AMD_GEMM16_BIG=0|1 forces the 128 / 256 tile (measurement)
+    const char* e = std::getenv("TM_AMD_GEMM16_BIG");
+    return e ? std::atoi(e) : -1;
+  }();
+  const bool big16 = big16_env >= 0 ? big16_env == 1
+                                    : static_cast<long long>((N + 255) / 256) * ((M + 255) / 256) * B >= 256;
+  const bool big = h16 ? big16 : big_choice(N, M, D, B);
   const int tbm = big ? kGM : kBM, tbn = big ? kGN : kBN;
   const int tiles_n = (N + tbm - 1) / tbm, tiles_m = (M + tbn - 1) / tbn;
   const int blocks = ((tiles_n * tiles_m + 7) / 8) * 8;

@@ -48,6 +48,8 @@ def main():
             ps = timeit(lambda: ops.gemm_nt(x, y, ops.GEMM_POLY_SUM, scale=1 / d, coef=1.0, degree=3).sum())
             ps_v = timeit(lambda: ((x @ y.T).float() / d + 1.0).pow(3).sum())
             cos = timeit(lambda: tm.functional.pairwise_cosine_similarity(x, y))
+            cos_gemm = timeit(lambda: ops.gemm_nt(x, y, ops.GEMM_COSINE, ix, iy, out_dtype=dtype))
+            norms = timeit(lambda: (ops.row_norms(x, inverse=True), ops.row_norms(y, inverse=True)))
 
             def cos_ref():
                 xn = x / torch.norm(x, p=2, dim=1).unsqueeze(1)
@@ -61,7 +63,8 @@ def main():
                 "hipblaslt_ms": round(mm, 4), "hipblaslt_tflops": round(flop / mm / 1e9, 1),
                 "fused_rowcolmax_ms": round(rc, 4), "vendor_rowcolmax_ms": round(rc_v, 4),
                 "fused_polysum_ms": round(ps, 4), "vendor_polysum_ms": round(ps_v, 4),
-                "pairwise_cosine_ms": round(cos, 4), "reference_recipe_cosine_ms": round(cos_v, 4)}), flush=True)
+                "pairwise_cosine_ms": round(cos, 4), "reference_recipe_cosine_ms": round(cos_v, 4),
+                "cosine_gemm_only_ms": round(cos_gemm, 4), "row_norms_ms": round(norms, 4)}), flush=True)
             del x, y
             torch.cuda.empty_cache()
 

@@ -81,15 +81,70 @@ __host__ __device__ __forceinline__ constexpr bool rows_in_lanes() {
   return EPI == 0 || EPI == 1 || EPI == 2;  // kStore, kEuclid, kCosine
 }
 
+// interior tile of STORE / COSINE with aligned rows and no diagonal: every group is one unconditional vector store
+template <int EPI, int NA, int NB, int OK>
+__device__ __forceinline__ void tile_store_full(f32x16 (&acc)[NA][NB], const EpiParams& ep, int batch, int N, int M,
+                                                int i0, int j0w) {
+  const int h = (threadIdx.x & 63) >> 5;
+#pragma unroll
+  for (int a = 0; a < NA; ++a) {
+    const int i = i0 + 32 * a;
+    float f = ep.scale;
+    if constexpr (EPI == 2) f *= ep.nx[batch * (long long)N + i];
+    const long long rowbase = batch * (long long)N * ep.ldo + (long long)i * ep.ldo;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int j0 = j0w + 32 * b + 8 * g + 4 * h;
+        float v[4];
+        if constexpr (EPI == 2) {
+          const f32x4 w = *reinterpret_cast<const f32x4*>(ep.ny + batch * (long long)M + j0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = acc[a][b][4 * g + q] * (f * w[q]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = acc[a][b][4 * g + q] * f;
+        }
+        if constexpr (OK == 0) {
+          *reinterpret_cast<f32x4*>(ep.out + rowbase + j0) = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+          uint16_t u[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            u[q] = OK == 1 ? __builtin_bit_cast(uint16_t, static_cast<__bf16>(v[q]))
+                           : __builtin_bit_cast(uint16_t, static_cast<_Float16>(v[q]));
+          *reinterpret_cast<uint2*>(ep.out16 + rowbase + j0) =
+              make_uint2(u[0] | (static_cast<uint32_t>(u[1]) << 16), u[2] | (static_cast<uint32_t>(u[3]) << 16));
+        }
+      }
+    }
+  }
+}
+
 template <int EPI, int NA, int WC, typename Dist2, int NB = 2>
 __device__ __forceinline__ void tile_epilogue_t(f32x16 (&acc)[NA][NB], const EpiParams& ep, int batch, int N, int M,
-                                                int row0, int col0, Dist2 dist2) {
+                                                int row0, int col0, Dist2 dist2, int tile_rows = 0,
+                                                int tile_cols = 0) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = (wave / WC) * 32 * NA, wc = (wave % WC) * 32 * NB;
   const int h = lane >> 5, r = lane & 31;
   const bool vec = (ep.ldo & 3) == 0 &&
                    ((ep.out_kind ? reinterpret_cast<uintptr_t>(ep.out16) : reinterpret_cast<uintptr_t>(ep.out)) &
                     (ep.out_kind ? 7 : 15)) == 0;
+  if constexpr (EPI == 0 || EPI == 2) {
+    // (the cosine multiplies scale * nx_i first, then ny_j: the order of the general path below up to rounding)
+    const bool full = vec && !ep.zero_diag && row0 + tile_rows <= N && col0 + tile_cols <= M &&
+                      (EPI == 0 || (((batch * (long long)M) & 3) == 0 &&
+                                    (reinterpret_cast<uintptr_t>(ep.ny) & 15) == 0));
+    if (full) {
+      const int i0 = row0 + wr + r, j0w = col0 + wc;
+      if (ep.out_kind == 0) tile_store_full<EPI, NA, NB, 0>(acc, ep, batch, N, M, i0, j0w);
+      else if (ep.out_kind == 1) tile_store_full<EPI, NA, NB, 1>(acc, ep, batch, N, M, i0, j0w);
+      else tile_store_full<EPI, NA, NB, 2>(acc, ep, batch, N, M, i0, j0w);
+      return;
+    }
+  }
 #pragma unroll
   for (int a = 0; a < NA; ++a) {
     const int i = row0 + wr + 32 * a + r;
@@ -800,7 +855,7 @@ __global__ __launch_bounds__(TM == 256 ? 512 : 256) void gemm_nt_h16_kernel(
     return t;
   };
   if constexpr (rows_in_lanes<EPI>())
-    tile_epilogue_t<EPI, NA, WC>(acc, ep, batch, N, M, row0, col0, dist2);
+    tile_epilogue_t<EPI, NA, WC>(acc, ep, batch, N, M, row0, col0, dist2, TM, TM);
   else
     tile_epilogue<EPI, NA, WC, TM, NT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile, dist2);
 }
@@ -926,7 +981,7 @@ __global__ __launch_bounds__(256) void gemm_nt_h16_w4_kernel(const uint16_t* __r
     }
     return t;
   };
-  tile_epilogue_t<EPI, NA, WC, decltype(dist2), NB>(acc, ep, batch, N, M, row0, col0, dist2);
+  tile_epilogue_t<EPI, NA, WC, decltype(dist2), NB>(acc, ep, batch, N, M, row0, col0, dist2, TM, TM);
 }
 
 // 256 x 256 tile, 8 waves, a 4-deep ring of 32-wide k-chunks (32 KiB per stage: 128 KiB of LDS, as the 2 x 64-wide
@@ -1058,7 +1113,7 @@ __global__ __launch_bounds__(512) void gemm_nt_h16_ring_kernel(const uint16_t* _
     return t;
   };
   if constexpr (rows_in_lanes<EPI>())
-    tile_epilogue_t<EPI, NA, WC>(acc, ep, batch, N, M, row0, col0, dist2);
+    tile_epilogue_t<EPI, NA, WC>(acc, ep, batch, N, M, row0, col0, dist2, TM, TM);
   else
     tile_epilogue<EPI, NA, WC, TM, NT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile, dist2);
 }

@@ -1365,10 +1365,16 @@ namespace {
 // then the squared norm (mode 0) or the inverse norm 1 / sqrt (mode 1) -- the epilogue factors of EUCLID / COSINE
 template <typename T>
 __global__ void __launch_bounds__(256) row_norms_kernel(const T* __restrict__ x, long long rows, int D, int mode,
-                                                        float* __restrict__ out) {
+                                                        float* __restrict__ out, const T* __restrict__ x2,
+                                                        long long rows2, float* __restrict__ out2) {
   const int lane = threadIdx.x & 63;
-  const long long row = (static_cast<long long>(blockIdx.x) * 256 + threadIdx.x) / 64;
-  if (row >= rows) return;  // (whole waves)
+  long long row = (static_cast<long long>(blockIdx.x) * 256 + threadIdx.x) / 64;
+  if (row >= rows) {  // the second operand's rows (one launch for both sides of a GEMM)
+    row -= rows;
+    if (row >= rows2) return;  // (whole waves)
+    x = x2;
+    out = out2;
+  }
   const T* r = x + row * D;
   float s = 0.f;
   constexpr int kVec = 16 / sizeof(T);
@@ -1393,42 +1399,49 @@ __global__ void __launch_bounds__(256) row_norms_kernel(const T* __restrict__ x,
 }
 }  // namespace
 
-// x: [..., D] contiguous fp32 / bf16 / fp16 -> fp32 [rows]: squared row norms (mode 0) or inverse norms (mode 1)
-at::Tensor row_norms(const at::Tensor& x, int64_t mode) {
+// x (and optionally y): [..., D] contiguous fp32 / bf16 / fp16 of one dtype and D -> fp32 [rows] each: squared row
+// norms (mode 0) or inverse norms (mode 1), both operands in one launch
+std::vector<at::Tensor> row_norms(const at::Tensor& x, const c10::optional<at::Tensor>& y, int64_t mode) {
   TM_CHECK_CUDA(x);
   TM_CHECK_CONTIG(x);
   TORCH_CHECK(x.dim() >= 1 && (mode == 0 || mode == 1), "row_norms: [..., D] operand, mode 0 / 1");
   const int D = static_cast<int>(x.size(-1));
   const long long rows = D > 0 ? x.numel() / D : 0;
   at::Tensor out = at::empty({rows}, x.options().dtype(at::kFloat));
-  if (rows == 0) return out;
-  const dim3 grid(static_cast<unsigned>((rows + 3) / 4));
+  long long rows2 = 0;
+  at::Tensor out2;
+  if (y.has_value()) {
+    TM_SAME_DEVICE(x, (*y));
+    TM_CHECK_CONTIG((*y));
+    TORCH_CHECK(y->scalar_type() == x.scalar_type() && y->size(-1) == D, "row_norms: operands of one dtype and D");
+    rows2 = D > 0 ? y->numel() / D : 0;
+    out2 = at::empty({rows2}, x.options().dtype(at::kFloat));
+  }
+  std::vector<at::Tensor> res{out};
+  if (y.has_value()) res.push_back(out2);
+  if (rows + rows2 == 0) return res;
+  const dim3 grid(static_cast<unsigned>((rows + rows2 + 3) / 4));
+  auto go = [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL((row_norms_kernel<T>), grid, dim3(256), 0, stream(), reinterpret_cast<const T*>(x.data_ptr()),
+                       rows, D, static_cast<int>(mode), out.data_ptr<float>(),
+                       y.has_value() ? reinterpret_cast<const T*>(y->data_ptr()) : nullptr, rows2,
+                       y.has_value() ? out2.data_ptr<float>() : nullptr);
+  };
   switch (x.scalar_type()) {
-    case at::kFloat:
-      hipLaunchKernelGGL((row_norms_kernel<float>), grid, dim3(256), 0, stream(), x.data_ptr<float>(), rows, D,
-                         static_cast<int>(mode), out.data_ptr<float>());
-      break;
-    case at::kBFloat16:
-      hipLaunchKernelGGL((row_norms_kernel<c10::BFloat16>), grid, dim3(256), 0, stream(),
-                         reinterpret_cast<const c10::BFloat16*>(x.data_ptr()), rows, D, static_cast<int>(mode),
-                         out.data_ptr<float>());
-      break;
-    case at::kHalf:
-      hipLaunchKernelGGL((row_norms_kernel<c10::Half>), grid, dim3(256), 0, stream(),
-                         reinterpret_cast<const c10::Half*>(x.data_ptr()), rows, D, static_cast<int>(mode),
-                         out.data_ptr<float>());
-      break;
-    default:
-      TORCH_CHECK(false, "row_norms: fp32 / bf16 / fp16 operand");
+    case at::kFloat: go(float{}); break;
+    case at::kBFloat16: go(c10::BFloat16{}); break;
+    case at::kHalf: go(c10::Half{}); break;
+    default: TORCH_CHECK(false, "row_norms: fp32 / bf16 / fp16 operand");
   }
   C10_HIP_KERNEL_LAUNCH_CHECK();
-  return out;
+  return res;
 }
 
 }  // namespace tm_amd
 
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
-  m.def("row_norms(Tensor x, int mode) -> Tensor");
+  m.def("row_norms(Tensor x, Tensor? y, int mode) -> Tensor[]");
   m.def(
       "gemm_nt(Tensor x, Tensor y, int kind, Tensor? aux_x, Tensor? aux_y, float scale, float coef, int degree, "
       "bool zero_diag, bool sqrt_out, Tensor? idx_x=None, Tensor? idx_y=None, int out_kind=0) -> Tensor");

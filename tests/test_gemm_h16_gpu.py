@@ -114,3 +114,20 @@ def test_h16_no_upcast_kernel():
     peak_extra = torch.cuda.max_memory_allocated() - before
     assert out.dtype == torch.bfloat16
     assert peak_extra <= out.numel() * 2 + (1 << 20)  # only the bf16 output (an fp32 copy of x would be 8 MB)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("d", [512, 100, 8])
+def test_row_norms_kernel(dtype, d):
+    """csrc/pairwise/gemm_nt.hip row_norms (one wave per row, fp32 accumulation) against an fp64 torch reference;
+    two operands from one launch."""
+    g = torch.Generator().manual_seed(d)
+    x = torch.randn(1037, d, generator=g).to(dtype)
+    y = torch.randn(77, d, generator=g).to(dtype)
+    ref_x = x.double().pow(2).sum(1)
+    ref_y = y.double().pow(2).sum(1)
+    sq = ops.row_norms(x.to(DEV)).cpu().double()
+    torch.testing.assert_close(sq, ref_x, rtol=1e-5, atol=1e-6)
+    ix, iy = ops.row_norms(x.to(DEV), inverse=True, y=y.to(DEV))
+    torch.testing.assert_close(ix.cpu().double(), 1 / ref_x.sqrt(), rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(iy.cpu().double(), 1 / ref_y.sqrt(), rtol=1e-5, atol=1e-7)

@@ -171,8 +171,10 @@ def _pairwise_cosine_similarity_update(x: Tensor, y: Optional[Tensor] = None,
     x, y, zd = _check_input(x, y, zero_diagonal)
     if _mfma_ok(x) and not _vendor_gemm(x, y):
         # fp32 inverse norms read straight from the operand (one wave per row, no upcast copy)
-        ix = ops.row_norms(x, inverse=True)
-        iy = ix if y is x else ops.row_norms(y, inverse=True)
+        if y is x:
+            ix = iy = ops.row_norms(x, inverse=True)
+        else:
+            ix, iy = ops.row_norms(x, inverse=True, y=y)
         return ops.gemm_nt(x, y, ops.GEMM_COSINE, ix, iy, zero_diagonal=zd, out_dtype=x.dtype)
     xn = x / torch.linalg.vector_norm(x, 2, dim=1, keepdim=True)
     yn = xn if y is x else y / torch.linalg.vector_norm(y, 2, dim=1, keepdim=True)

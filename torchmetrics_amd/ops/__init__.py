@@ -1391,13 +1391,20 @@ def corr_merge(stacked: Tensor) -> Tensor:
 GEMM_STORE, GEMM_EUCLID, GEMM_COSINE, GEMM_POLY_SUM, GEMM_ROW_MIN, GEMM_ROW_SUM, GEMM_ROW_COL_MAX = range(7)
 
 
-def row_norms(x: Tensor, inverse: bool = False) -> Tensor:
+def row_norms(x: Tensor, inverse: bool = False, y: Optional[Tensor] = None) -> Union[Tensor, Tuple[Tensor, Tensor]]:
     """fp32 squared row norms (or inverse norms ``1 / ||x_i||``) of a ``[..., D]`` operand, accumulated in fp32 from
-    the operand's own dtype: one wave per row on ROCm (``csrc/pairwise/gemm_nt.hip`` ``row_norms``)."""
-    if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16, torch.float16):
-        return _ops().row_norms(x.contiguous(), 1 if inverse else 0)
-    s = torch.linalg.vector_norm(x, 2, dim=-1, dtype=torch.float32).reshape(-1)
-    return 1.0 / s if inverse else s * s
+    the operand's own dtype: one wave per row on ROCm (``csrc/pairwise/gemm_nt.hip`` ``row_norms``).  With ``y`` (same
+    dtype and D): both operands' norms from ONE launch, returned as a pair."""
+    if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16, torch.float16) and (
+            y is None or (y.dtype == x.dtype and y.is_cuda)):
+        res = _ops().row_norms(x.contiguous(), None if y is None else y.contiguous(), 1 if inverse else 0)
+        return res[0] if y is None else (res[0], res[1])
+
+    def one(t: Tensor) -> Tensor:
+        s = torch.linalg.vector_norm(t, 2, dim=-1, dtype=torch.float32).reshape(-1)
+        return 1.0 / s if inverse else s * s
+
+    return one(x) if y is None else (one(x), one(y))
 
 
 def gemm_nt(x: Tensor, y: Tensor, kind: int, aux_x: Optional[Tensor] = None, aux_y: Optional[Tensor] = None,

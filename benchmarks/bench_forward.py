@@ -91,6 +91,8 @@ def _time(fn, preds, target, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--ours-only", action="store_true",
+                    help="only the native forward (attributable kernel traces: no Python / reference forwards)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -103,6 +105,11 @@ def main():
     for name, (kind, make) in cases.items():
         native = make().to(dev)
         assert type(native.forward).__name__ == "NativeForward", type(native.forward)
+        if args.ours_only:
+            t_nat, _ = _time(native, preds, target, args.steps)
+            print(json.dumps({"metric": name, "batch": N, "dtype": "bf16", "steps": args.steps,
+                              "forward_us": round(t_nat, 2), "native_calls": native.forward.native_calls}), flush=True)
+            continue
         python = make().to(dev)
         python.__dict__.pop("forward")  # Metric.forward
         ref = _RefForward(kind, dev)

@@ -61,15 +61,24 @@ __global__ void __launch_bounds__(kBlock) minmax_partial_kernel(const T* __restr
   }
 }
 
+// one wave over the block partials (min / max are exact in any order; the first version walked them with one thread:
+// ~107 us for 2048 partials of dependent loads)
 __global__ void minmax_final_kernel(const int64_t* __restrict__ part, int nb, int64_t* __restrict__ out) {
-  if (threadIdx.x != 0) return;
   long long mn = LLONG_MAX, mx = LLONG_MIN;
-  for (int b = 0; b < nb; ++b) {  // fixed order
+  for (int b = threadIdx.x; b < nb; b += kWave) {
     mn = part[2 * b] < mn ? part[2 * b] : mn;
     mx = part[2 * b + 1] > mx ? part[2 * b + 1] : mx;
   }
-  out[0] = mn;
-  out[1] = mx;
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    const long long a = __shfl_xor(mn, off, kWave), b = __shfl_xor(mx, off, kWave);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if (threadIdx.x == 0) {
+    out[0] = mn;
+    out[1] = mx;
+  }
 }
 
 template <typename TT, typename TP>

@@ -9,7 +9,7 @@ prof() {
   local name=$1; shift
   cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$name -o p -- python3 "$@" > $R/gpurun_out/r5prof_$name.log 2>&1 || { tail -20 $R/gpurun_out/r5prof_$name.log; return 1; }
   cd $R && cp $(find gpurun_out/prof_$name -name "*kernel_stats.csv" | head -1) gpurun_out/r5prof_${name}_kernel_stats.csv && rm -rf gpurun_out/prof_$name
-  echo "== $name"; python3 tools/gpu/kstats.py gpurun_out/ tm_amd 2>/dev/null | head -0
+  echo "== $name"
 }
 prof clustering $R/benchmarks/bench_clustering.py --ours-only || exit 1
 prof forward $R/benchmarks/bench_forward.py --ours-only || exit 1

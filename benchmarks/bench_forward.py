@@ -76,14 +76,18 @@ class _RefForward:
         return val
 
 
-def _time(fn, preds, target, steps):
+def _time(fn, preds, target, steps, keep=True):
+    """Mean us per call; ``keep`` holds every returned value for the parity checks (for the confusion matrix that is
+    an 8 MB tensor per call: the allocator grows by steps x 8 MB inside the timed loop)."""
     vals = []
     for i in range(10):
         fn(preds[i % len(preds)], target[i % len(target)])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
-        vals.append(fn(preds[i % len(preds)], target[i % len(target)]))
+        v = fn(preds[i % len(preds)], target[i % len(target)])
+        if keep:
+            vals.append(v)
     torch.cuda.synchronize()
     return (time.perf_counter() - t0) / steps * 1e6, vals
 
@@ -106,7 +110,7 @@ def main():
         native = make().to(dev)
         assert type(native.forward).__name__ == "NativeForward", type(native.forward)
         if args.ours_only:
-            t_nat, _ = _time(native, preds, target, args.steps)
+            t_nat, _ = _time(native, preds, target, args.steps, keep=False)
             print(json.dumps({"metric": name, "batch": N, "dtype": "bf16", "steps": args.steps,
                               "forward_us": round(t_nat, 2), "native_calls": native.forward.native_calls}), flush=True)
             continue

@@ -1931,7 +1931,12 @@ long long vec_grid(const at::Tensor& preds, const at::Tensor& target, long long 
       b = r;
     }
     const long long q = m / a;
-    const long long want = std::max<long long>(1, std::min<long long>(cus, (total / VEC + kVecBlock - 1) / kVecBlock));
+    static const int mult = [] {  // blocks per CU (TM_AMD_BIN_VEC_BLOCKS_PER_CU, measurement knob; default 1)
+      const char* e = std::getenv("TM_AMD_BIN_VEC_BLOCKS_PER_CU");
+      return e ? std::max(1, std::atoi(e)) : 1;
+    }();
+    const long long want =
+        std::max<long long>(1, std::min<long long>(cus * mult, (total / VEC + kVecBlock - 1) / kVecBlock));
     const long long grid = std::max<long long>(1, (want + q / 2) / q) * q;
     return grid > 4096 ? 0 : grid;
   }

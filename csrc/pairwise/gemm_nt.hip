@@ -813,36 +813,38 @@ __global__ __launch_bounds__(TM == 256 ? 512 : 256) void gemm_nt_h16_kernel(
           acc[a][b] = Mfma16<T>::run(fa[a], fb[b], acc[a][b]);
       }
   };
-  v8 ca[NA], cb[2], na[NA], nb[2];
+  // two fragment sets used in turn: k-step s multiplies set s & 1 while set (s + 1) & 1 loads (4 k-steps per chunk,
+  // so the parity carries across chunks) -- no register copies between steps (the copying form spent ~3 v_mov per
+  // MFMA)
+  v8 fa[2][NA], fb[2][2];
   // chunk kc+1's barrier sits inside chunk kc, after its last LDS read (step 3's fragments, loaded during step 2's
   // MFMAs) and before step 3's MFMAs: the matrix pipe still holds step 2's work while the waves meet there
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (nk > 1) stage(1, 1);
-  frag(0, 0, ca, cb);
-  for (int kc = 0; kc < nk; ++kc) {
+  frag(0, 0, fa[0], fb[0]);
+  // the last chunk is peeled off (no barrier, no next fragments): the loop body has one path, so the 128
+  // accumulators are not shuffled between registers at control-flow joins
+  auto chunk = [&](int kc, auto last_c) {
+    constexpr bool kLast = decltype(last_c)::value;
     const int buf = kc & 1;
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
-      const bool more = s4 < 3 || kc + 1 < nk;
+      const int cur = s4 & 1, nxt = cur ^ 1;
       if (s4 < 3) {
-        frag(buf, s4 + 1, na, nb);
-      } else if (kc + 1 < nk) {
+        frag(buf, s4 + 1, fa[nxt], fb[nxt]);
+      } else if constexpr (!kLast) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // chunk kc+1 DMAs; chunk kc reads landed
         __builtin_amdgcn_s_barrier();
         if (kc + 2 < nk) stage(kc + 2, buf);
-        frag(buf ^ 1, 0, na, nb);
+        frag(buf ^ 1, 0, fa[nxt], fb[nxt]);
       }
-      mma(ca, cb);
-      if (more) {
-#pragma unroll
-        for (int a = 0; a < NA; ++a) ca[a] = na[a];
-#pragma unroll
-        for (int b = 0; b < 2; ++b) cb[b] = nb[b];
-      }
+      mma(fa[cur], fb[cur]);
     }
-  }
+  };
+  for (int kc = 0; kc + 1 < nk; ++kc) chunk(kc, std::false_type{});
+  chunk(nk - 1, std::true_type{});
   // (no DMA is in flight: the last chunk issued none)
   auto dist2 = [&](int i, int j) {
     const uint16_t* xr = xrow(i);

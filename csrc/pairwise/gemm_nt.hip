@@ -747,7 +747,9 @@ __global__ __launch_bounds__(TM == 256 ? 512 : 256) void gemm_nt_h16_kernel(
   if (tile >= total) return;
   const int ti = tile / tiles_m, tj = tile - ti * tiles_m;
   const int row0 = ti * TM, col0 = tj * TM;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the wave index as an SGPR value: the DMA's LDS destinations (M0) are then scalar arithmetic, not a
+  // v_readfirstlane per instruction
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = (wave / WC) * 32 * NA, wc = (wave % WC) * 64;
   const int h = lane >> 5, r = lane & 31;
 

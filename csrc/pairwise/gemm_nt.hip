@@ -723,6 +723,10 @@ struct Mfma16<_Float16> {
 
 __device__ __attribute__((aligned(16))) uint32_t g_zero_chunk[4];  // the DMA source of K padding (never written)
 
+// Measured and dropped (profiles/r05_bench_gemm16_ring_sweep_last.jsonl, r05_bench_gemm16_v2_ring*.jsonl and the
+// round-5 log): a 4-deep / 2-deep ring of 32-wide k-chunks (no faster; at 165 VGPRs two 512-thread blocks never share
+// a CU), four waves of 128 x 128 per wave (512 VGPRs, spills: 10-20 % slower), and a persistent grid-stride form that
+// overlaps a tile's stores with the next tile's DMA (within 5 %).
 template <int EPI, typename T, int TM>
 __global__ __launch_bounds__(TM == 256 ? 512 : 256) void gemm_nt_h16_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ Y, int N, int M, int D, long long bx, long long by,
@@ -864,412 +868,6 @@ __global__ __launch_bounds__(TM == 256 ? 512 : 256) void gemm_nt_h16_kernel(
     tile_epilogue<EPI, NA, WC, TM, NT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile, dist2);
 }
 
-// Persistent form of the 256 x 256 16-bit kernel for the element-wise epilogues (which need no LDS): a block walks
-// tiles grid-stride; after a tile's last MFMAs it issues the tile's vector stores and at once the next tile's first
-// two k-chunk DMAs, so the stores drain while the next tile's operands arrive (the one-tile-per-block grid runs
-// load / compute / store phases in lock-step across the chip, with a block launch between tiles).
-template <int EPI, typename T>
-__global__ __launch_bounds__(512) void gemm_nt_h16_persist_kernel(const uint16_t* __restrict__ X,
-                                                                  const uint16_t* __restrict__ Y, int N, int M, int D,
-                                                                  long long bx, long long by, int tiles_m,
-                                                                  EpiParams ep) {
-  constexpr int TM = 256, WC = 4, NA = 4, KC = 64;
-  static_assert(rows_in_lanes<EPI>(), "persistent kernel: element-wise epilogues");
-  typedef typename Mfma16<T>::v8 v8;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  uint16_t* sh = reinterpret_cast<uint16_t*>(smem);
-  constexpr int kStage = 2 * TM * KC;
-  const int batch = blockIdx.z;
-  const int32_t* gix = ep.ix ? ep.ix + (long long)batch * N : nullptr;
-  const int32_t* giy = ep.iy ? ep.iy + (long long)batch * M : nullptr;
-  if (!gix) X += batch * bx;
-  if (!giy) Y += batch * by;
-  auto xrow = [&](int i) -> const uint16_t* { return X + (long long)(gix ? gix[i] : i) * D; };
-  auto yrow = [&](int j) -> const uint16_t* { return Y + (long long)(giy ? giy[j] : j) * D; };
-  const int tiles_n = (N + TM - 1) / TM;
-  const int total = tiles_n * tiles_m;
-  const int per = (total + 7) / 8;
-  const int slots = per * 8;
-  auto tile_of = [&](int sl) { return (sl % 8) * per + sl / 8; };  // XCD-aware bands, as the one-shot grid
-  auto next_slot = [&](int sl) {
-    do sl += gridDim.x;
-    while (sl < slots && tile_of(sl) >= total);
-    return sl;
-  };
-  int slot = blockIdx.x;
-  if (slot < slots && tile_of(slot) >= total) slot = next_slot(slot);
-  if (slot >= slots) return;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = (wave / WC) * 32 * NA, wc = (wave % WC) * 64;
-  const int h = lane >> 5, r = lane & 31;
-  int kof[4], rows[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    rows[q] = 32 * wave + 8 * q + (lane >> 3);
-    kof[q] = 8 * ((lane & 7) ^ ((rows[q] >> 1) & 7));
-  }
-  const uint16_t* srcA[4];
-  const uint16_t* srcB[4];
-  auto setup = [&](int tile) {
-    const int ti = tile / tiles_m, tj = tile - ti * tiles_m;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      srcA[q] = xrow(min(ti * TM + rows[q], N - 1)) + kof[q];
-      srcB[q] = yrow(min(tj * TM + rows[q], M - 1)) + kof[q];
-    }
-  };
-  typedef __attribute__((address_space(3))) void lds_t;
-  typedef __attribute__((address_space(1))) void glb_t;
-  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
-  auto stage = [&](int kc, int buf) {
-    uint16_t* sa = sh + buf * kStage;
-    uint16_t* sb = sa + TM * KC;
-    const int k0 = kc * KC;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool in = k0 + kof[q] < D;
-      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcA[q] + k0 : zero), (lds_t*)(sa + (32 * wave + 8 * q) * KC),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcB[q] + k0 : zero), (lds_t*)(sb + (32 * wave + 8 * q) * KC),
-                                       16, 0, 0);
-    }
-  };
-  const int swz_a = ((wr + r) >> 1) & 7;
-  const int swz_b = ((wc + r) >> 1) & 7;
-  const int nk = (D + KC - 1) / KC;
-  auto frag = [&](int buf, int s, v8* fa, v8* fb) {
-    const uint16_t* sa = sh + buf * kStage + (wr + r) * KC;
-    const uint16_t* sb = sh + buf * kStage + TM * KC + (wc + r) * KC;
-#pragma unroll
-    for (int a = 0; a < NA; ++a) fa[a] = *reinterpret_cast<const v8*>(sa + 32 * a * KC + 8 * ((2 * s + h) ^ swz_a));
-#pragma unroll
-    for (int b = 0; b < 2; ++b) fb[b] = *reinterpret_cast<const v8*>(sb + 32 * b * KC + 8 * ((2 * s + h) ^ swz_b));
-  };
-  f32x16 acc[NA][2];
-  auto mma = [&](const v8* fa, const v8* fb) {
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) acc[a][b] = Mfma16<T>::run(fb[b], fa[a], acc[a][b]);
-  };
-  v8 fa[2][NA], fb[2][2];
-  auto chunk = [&](int kc, auto last_c) {
-    constexpr bool kLast = decltype(last_c)::value;
-    const int buf = kc & 1;
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      const int cur = s4 & 1, nxt = cur ^ 1;
-      if (s4 < 3) {
-        frag(buf, s4 + 1, fa[nxt], fb[nxt]);
-      } else if constexpr (!kLast) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (kc + 2 < nk) stage(kc + 2, buf);
-        frag(buf ^ 1, 0, fa[nxt], fb[nxt]);
-      }
-      mma(fa[cur], fb[cur]);
-    }
-  };
-  auto dist2 = [&](int i, int j) {
-    const uint16_t* xr = xrow(i);
-    const uint16_t* yr = yrow(j);
-    float t = 0.f;
-    for (int k = 0; k < D; ++k) {
-      const float d = Mfma16<T>::to_f32(xr[k]) - Mfma16<T>::to_f32(yr[k]);
-      t = fmaf(d, d, t);
-    }
-    return t;
-  };
-  // first tile: its two chunks in flight
-  setup(tile_of(slot));
-  stage(0, 0);
-  if (nk > 1) stage(1, 1);
-  for (;;) {
-    const int tile = tile_of(slot);
-    const int ti = tile / tiles_m, tj = tile - ti * tiles_m;
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-    // chunk 0 landed (chunk 1's 8 DMA instructions may still be in flight; older stores are done too)
-    if (nk > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    frag(0, 0, fa[0], fb[0]);
-    for (int kc = 0; kc + 1 < nk; ++kc) chunk(kc, std::false_type{});
-    chunk(nk - 1, std::true_type{});
-    const int nslot = next_slot(slot);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's LDS reads of this tile are done: both buffers may be refilled
-    tile_epilogue_t<EPI, NA, WC>(acc, ep, batch, N, M, ti * TM, tj * TM, dist2, TM, TM);
-    if (nslot >= slots) break;
-    slot = nslot;
-    setup(tile_of(slot));
-    stage(0, 0);
-    if (nk > 1) stage(1, 1);
-  }
-}
-
-// 256 x 256 tile, FOUR waves of 128 x 128 (4 x 4 MFMA 32 x 32 tiles each, 256 accumulators per lane): per k-step a
-// wave reads 8 fragments for 16 MFMAs (the 8-wave kernel: 6 for 8), and half as many waves meet at each chunk
-// barrier.  Element-wise epilogues only (transposed accumulator, rows in lanes).  Same 2-stage 64-wide k-chunk staging.
-template <int EPI, typename T>
-__global__ __launch_bounds__(256) void gemm_nt_h16_w4_kernel(const uint16_t* __restrict__ X,
-                                                             const uint16_t* __restrict__ Y, int N, int M, int D,
-                                                             long long bx, long long by, int tiles_m, EpiParams ep) {
-  constexpr int TM = 256, WC = 2, NA = 4, NB = 4, KC = 64;
-  static_assert(rows_in_lanes<EPI>(), "w4 kernel: element-wise epilogues");
-  typedef typename Mfma16<T>::v8 v8;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  uint16_t* sh = reinterpret_cast<uint16_t*>(smem);
-  constexpr int kStage = 2 * TM * KC;
-  const int batch = blockIdx.z;
-  const int32_t* gix = ep.ix ? ep.ix + (long long)batch * N : nullptr;
-  const int32_t* giy = ep.iy ? ep.iy + (long long)batch * M : nullptr;
-  if (!gix) X += batch * bx;
-  if (!giy) Y += batch * by;
-  auto xrow = [&](int i) -> const uint16_t* { return X + (long long)(gix ? gix[i] : i) * D; };
-  auto yrow = [&](int j) -> const uint16_t* { return Y + (long long)(giy ? giy[j] : j) * D; };
-  const int tiles_n = (N + TM - 1) / TM;
-  const int total = tiles_n * tiles_m;
-  const int bid = blockIdx.x;
-  const int per = (total + 7) / 8;
-  const int tile = (bid % 8) * per + bid / 8;
-  if (tile >= total) return;
-  const int ti = tile / tiles_m, tj = tile - ti * tiles_m;
-  const int row0 = ti * TM, col0 = tj * TM;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = (wave / WC) * 32 * NA, wc = (wave % WC) * 32 * NB;
-  const int h = lane >> 5, r = lane & 31;
-  // DMA: wave w moves rows [64 w, 64 w + 64) of both operand tiles, 8 rows (1 KiB) per instruction
-  const uint16_t* srcA[8];
-  const uint16_t* srcB[8];
-  int kof[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int rr = 64 * wave + 8 * q + (lane >> 3);
-    const int c = (lane & 7) ^ ((rr >> 1) & 7);
-    kof[q] = 8 * c;
-    srcA[q] = xrow(min(row0 + rr, N - 1)) + 8 * c;
-    srcB[q] = yrow(min(col0 + rr, M - 1)) + 8 * c;
-  }
-  typedef __attribute__((address_space(3))) void lds_t;
-  typedef __attribute__((address_space(1))) void glb_t;
-  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
-  auto stage = [&](int kc, int buf) {
-    uint16_t* sa = sh + buf * kStage;
-    uint16_t* sb = sa + TM * KC;
-    const int k0 = kc * KC;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const bool in = k0 + kof[q] < D;
-      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcA[q] + k0 : zero), (lds_t*)(sa + (64 * wave + 8 * q) * KC),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcB[q] + k0 : zero), (lds_t*)(sb + (64 * wave + 8 * q) * KC),
-                                       16, 0, 0);
-    }
-  };
-  f32x16 acc[NA][NB];
-#pragma unroll
-  for (int a = 0; a < NA; ++a)
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-  const int swz_a = ((wr + r) >> 1) & 7;
-  const int swz_b = ((wc + r) >> 1) & 7;
-  const int nk = (D + KC - 1) / KC;
-  auto frag = [&](int buf, int s, v8* fa, v8* fb) {
-    const uint16_t* sa = sh + buf * kStage + (wr + r) * KC;
-    const uint16_t* sb = sh + buf * kStage + TM * KC + (wc + r) * KC;
-#pragma unroll
-    for (int a = 0; a < NA; ++a) fa[a] = *reinterpret_cast<const v8*>(sa + 32 * a * KC + 8 * ((2 * s + h) ^ swz_a));
-#pragma unroll
-    for (int b = 0; b < NB; ++b) fb[b] = *reinterpret_cast<const v8*>(sb + 32 * b * KC + 8 * ((2 * s + h) ^ swz_b));
-  };
-  auto mma = [&](const v8* fa, const v8* fb) {
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-      for (int b = 0; b < NB; ++b) acc[a][b] = Mfma16<T>::run(fb[b], fa[a], acc[a][b]);
-  };
-  v8 ca[NA], cb[NB], na[NA], nb[NB];
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (nk > 1) stage(1, 1);
-  frag(0, 0, ca, cb);
-  for (int kc = 0; kc < nk; ++kc) {
-    const int buf = kc & 1;
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      const bool more = s4 < 3 || kc + 1 < nk;
-      if (s4 < 3) {
-        frag(buf, s4 + 1, na, nb);
-      } else if (kc + 1 < nk) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (kc + 2 < nk) stage(kc + 2, buf);
-        frag(buf ^ 1, 0, na, nb);
-      }
-      mma(ca, cb);
-      if (more) {
-#pragma unroll
-        for (int a = 0; a < NA; ++a) ca[a] = na[a];
-#pragma unroll
-        for (int b = 0; b < NB; ++b) cb[b] = nb[b];
-      }
-    }
-  }
-  auto dist2 = [&](int i, int j) {
-    const uint16_t* xr = xrow(i);
-    const uint16_t* yr = yrow(j);
-    float t = 0.f;
-    for (int k = 0; k < D; ++k) {
-      const float d = Mfma16<T>::to_f32(xr[k]) - Mfma16<T>::to_f32(yr[k]);
-      t = fmaf(d, d, t);
-    }
-    return t;
-  };
-  tile_epilogue_t<EPI, NA, WC, decltype(dist2), NB>(acc, ep, batch, N, M, row0, col0, dist2, TM, TM);
-}
-
-// 256 x 256 tile, 8 waves, a 4-deep ring of 32-wide k-chunks (32 KiB per stage: 128 KiB of LDS, as the 2 x 64-wide
-// kernel above) so THREE chunks of DMA are in flight while one is multiplied -- the 2-stage kernel waits for the next
-// chunk's loads one chunk after issuing them.  Rows are 64 B: a 1 KiB global_load_lds instruction moves 16 rows, and
-// the 16-B slot of logical chunk c in row r is c ^ ((r >> 2) & 3), which keeps every ds_read_b128 lane group on 16
-// distinct slots of the 256-B bank row (rows r and r + 4 share banks unless their slots differ).
-// STAGES = 2 (64 KiB of LDS): two blocks share a CU, so one block's epilogue stores and the next one's first loads
-// overlap the other block's main loop (with 128 KiB per block, every CU alternates load / compute / store phases in
-// lock-step with the whole chip).
-template <int EPI, typename T, int STAGES>
-__global__ __launch_bounds__(512) void gemm_nt_h16_ring_kernel(const uint16_t* __restrict__ X,
-                                                               const uint16_t* __restrict__ Y, int N, int M, int D,
-                                                               long long bx, long long by, int tiles_m, EpiParams ep) {
-  constexpr int TM = 256, NT = 512, WC = 4, NA = 4, KC = 32;
-  typedef typename Mfma16<T>::v8 v8;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  uint16_t* sh = reinterpret_cast<uint16_t*>(smem);
-  constexpr int kStage = 2 * TM * KC;  // elements per stage (A then B)
-  const int batch = blockIdx.z;
-  const int32_t* gix = ep.ix ? ep.ix + (long long)batch * N : nullptr;
-  const int32_t* giy = ep.iy ? ep.iy + (long long)batch * M : nullptr;
-  if (!gix) X += batch * bx;
-  if (!giy) Y += batch * by;
-  auto xrow = [&](int i) -> const uint16_t* { return X + (long long)(gix ? gix[i] : i) * D; };
-  auto yrow = [&](int j) -> const uint16_t* { return Y + (long long)(giy ? giy[j] : j) * D; };
-  const int tiles_n = (N + TM - 1) / TM;
-  const int total = tiles_n * tiles_m;
-  const int bid = blockIdx.x;
-  const int per = (total + 7) / 8;
-  const int tile = (bid % 8) * per + bid / 8;  // XCD-aware band of row-major tiles
-  if (tile >= total) return;
-  const int ti = tile / tiles_m, tj = tile - ti * tiles_m;
-  const int row0 = ti * TM, col0 = tj * TM;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = (wave / WC) * 32 * NA, wc = (wave % WC) * 64;
-  const int h = lane >> 5, r = lane & 31;
-
-  // DMA: wave w moves rows [32 w, 32 w + 32) of both operand tiles, 16 rows per instruction (2 per operand);
-  // lane l of instruction q covers row 32 w + 16 q + l / 4, physical slot l % 4 = logical chunk (l % 4) ^ swz(row)
-  const uint16_t* srcA[2];
-  const uint16_t* srcB[2];
-  int kof[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int rr = 32 * wave + 16 * q + (lane >> 2);
-    const int c = (lane & 3) ^ ((rr >> 2) & 3);
-    kof[q] = 8 * c;
-    srcA[q] = xrow(min(row0 + rr, N - 1)) + 8 * c;
-    srcB[q] = yrow(min(col0 + rr, M - 1)) + 8 * c;
-  }
-  typedef __attribute__((address_space(3))) void lds_t;
-  typedef __attribute__((address_space(1))) void glb_t;
-  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
-  auto stage = [&](int kc) {
-    uint16_t* sa = sh + (kc % STAGES) * kStage;
-    uint16_t* sb = sa + TM * KC;
-    const int k0 = kc * KC;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const bool in = k0 + kof[q] < D;
-      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcA[q] + k0 : zero), (lds_t*)(sa + (32 * wave + 16 * q) * KC),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcB[q] + k0 : zero), (lds_t*)(sb + (32 * wave + 16 * q) * KC),
-                                       16, 0, 0);
-    }
-  };
-
-  f32x16 acc[NA][2];
-#pragma unroll
-  for (int a = 0; a < NA; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-
-  const int swz_a = ((wr + r) >> 2) & 3;  // (32 a keeps (row >> 2) & 3)
-  const int swz_b = ((wc + r) >> 2) & 3;
-  const int nk = (D + KC - 1) / KC;
-  auto frag = [&](int buf, int s, v8* fa, v8* fb) {
-    const uint16_t* sa = sh + buf * kStage + (wr + r) * KC;
-    const uint16_t* sb = sh + buf * kStage + TM * KC + (wc + r) * KC;
-#pragma unroll
-    for (int a = 0; a < NA; ++a) fa[a] = *reinterpret_cast<const v8*>(sa + 32 * a * KC + 8 * ((2 * s + h) ^ swz_a));
-#pragma unroll
-    for (int b = 0; b < 2; ++b) fb[b] = *reinterpret_cast<const v8*>(sb + 32 * b * KC + 8 * ((2 * s + h) ^ swz_b));
-  };
-  auto mma = [&](const v8* fa, const v8* fb) {
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        if constexpr (rows_in_lanes<EPI>())
-          acc[a][b] = Mfma16<T>::run(fb[b], fa[a], acc[a][b]);  // transposed tile: output rows in lanes
-        else
-          acc[a][b] = Mfma16<T>::run(fa[a], fb[b], acc[a][b]);
-      }
-  };
-  // prologue: chunks 0 .. STAGES - 2 in flight (4 DMA instructions per chunk and thread)
-#pragma unroll
-  for (int q = 0; q < STAGES - 1; ++q)
-    if (q < nk) stage(q);
-  v8 fa0[NA], fb0[2], fa1[NA], fb1[2];
-  for (int kc = 0; kc < nk; ++kc) {
-    // chunk kc landed when at most the later chunks' DMAs are outstanding (loads retire in order)
-    const int later = min(nk - 1, kc + STAGES - 2) - kc;
-    if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // every wave's part of chunk kc is in LDS, and every wave finished reading chunk kc - 1 (its fragments were
-    // consumed by MFMAs issued before this point): its buffer may take chunk kc + STAGES - 1
-    __builtin_amdgcn_s_barrier();
-    if (kc + STAGES - 1 < nk) stage(kc + STAGES - 1);
-    const int buf = kc % STAGES;
-    frag(buf, 0, fa0, fb0);
-    frag(buf, 1, fa1, fb1);
-    mma(fa0, fb0);
-    mma(fa1, fb1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-  auto dist2 = [&](int i, int j) {
-    const uint16_t* xr = xrow(i);
-    const uint16_t* yr = yrow(j);
-    float t = 0.f;
-    for (int k = 0; k < D; ++k) {
-      const float d = Mfma16<T>::to_f32(xr[k]) - Mfma16<T>::to_f32(yr[k]);
-      t = fmaf(d, d, t);
-    }
-    return t;
-  };
-  if constexpr (rows_in_lanes<EPI>())
-    tile_epilogue_t<EPI, NA, WC>(acc, ep, batch, N, M, row0, col0, dist2, TM, TM);
-  else
-    tile_epilogue<EPI, NA, WC, TM, NT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile, dist2);
-}
-
 // The 256 x 256 kernel for large problems: D a multiple of its k-step, both sides at least one tile, enough tiles to
 // fill the chip once; TM_AMD_GEMM_BIG=0|1 forces it off / on (where it applies).
 bool big_choice(int N, int M, int D, int batches) {
@@ -1351,39 +949,7 @@ void launch_h16(const at::Tensor& x, const at::Tensor& y, int batches, long long
   const size_t lds = 2ull * 2 * tm * 64 * sizeof(uint16_t);
   const auto* xp = reinterpret_cast<const uint16_t*>(x.data_ptr());
   const auto* yp = reinterpret_cast<const uint16_t*>(y.data_ptr());
-  static const int ring = [] {
-    const char* e = std::getenv("TM_AMD_GEMM16_RING");
-    return e ? std::atoi(e) : 0;
-  }();
-  static const int w4 = [] {
-    const char* e = std::getenv("TM_AMD_GEMM16_W4");
-    return e ? std::atoi(e) : 0;
-  }();
-  static const int persist = [] {
-    const char* e = std::getenv("TM_AMD_GEMM16_PERSIST");
-    return e ? std::atoi(e) : 0;
-  }();
-  if constexpr (rows_in_lanes<EPI>()) {
-    if (big && persist) {
-      const int tiles = tiles_n * tiles_m;
-      const int grid = std::min(tiles, cu_count(x.get_device()) * (persist > 1 ? persist : 1));
-      hipLaunchKernelGGL((gemm_nt_h16_persist_kernel<EPI, T>), dim3(grid, 1, batches), dim3(512), lds, stream(), xp,
-                         yp, N, M, D, bx, by, tiles_m, ep);
-      return;
-    }
-    if (big && w4) {
-      hipLaunchKernelGGL((gemm_nt_h16_w4_kernel<EPI, T>), dim3(per * 8, 1, batches), dim3(256), lds, stream(), xp, yp,
-                         N, M, D, bx, by, tiles_m, ep);
-      return;
-    }
-  }
-  if (big && ring == 2)
-    hipLaunchKernelGGL((gemm_nt_h16_ring_kernel<EPI, T, 2>), dim3(per * 8, 1, batches), dim3(512), lds / 2, stream(),
-                       xp, yp, N, M, D, bx, by, tiles_m, ep);
-  else if (big && ring)
-    hipLaunchKernelGGL((gemm_nt_h16_ring_kernel<EPI, T, 4>), dim3(per * 8, 1, batches), dim3(512), lds, stream(), xp,
-                       yp, N, M, D, bx, by, tiles_m, ep);
-  else if (big)
+  if (big)
     hipLaunchKernelGGL((gemm_nt_h16_kernel<EPI, T, 256>), dim3(per * 8, 1, batches), dim3(512), lds, stream(), xp, yp,
                        N, M, D, bx, by, tiles_m, ep);
   else

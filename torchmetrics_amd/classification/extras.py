@@ -87,6 +87,7 @@ class _BinnedCalibration(Metric):
     when every rank's cache is valid (agreed with one MIN all-reduce)."""
 
     _fold_cat_lists = True  # compute() only concatenates the list states
+    _fold_every = 8  # (the bin cache serves compute(): the lists are folded every 8th batch, not at every compute)
 
     def _bounds(self, device: torch.device) -> Tensor:
         key = (self.n_bins, torch.float32, device)

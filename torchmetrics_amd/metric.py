@@ -754,6 +754,8 @@ class Metric(Module, ABC):
             self._raise_device_errors()
             state["_errors_checked_at"] = state["_update_count"]
 
+    _fold_every: int = 1  # cat-list batches pending before compute() folds them into the arena
+
     def _consolidate_cat_lists(self) -> None:
         """Replace the elements of every ``cat`` list state by their concatenation, in place (same list object).
 
@@ -775,7 +777,9 @@ class Metric(Module, ABC):
                                       tuple(a for a, fn in self._reductions.items() if fn is dim_zero_cat))
         for attr in cats[2]:
             val = d[attr] if attr in d else getattr(self, attr)
-            if isinstance(val, list) and len(val) > 1:
+            # a class whose compute() usually does not read the list (the calibration error, served by its bin cache)
+            # folds only once `_fold_every` batches are pending
+            if isinstance(val, list) and len(val) > self._fold_every:
                 val[:] = [self._fold_into_arena(attr, val)]
 
     def _fold_into_arena(self, attr: str, parts: List[Any]) -> Any:

@@ -13,8 +13,14 @@ from torchmetrics_amd import ops  # noqa: E402
 
 
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, nargs="*", default=[1024, 4096, 8192, 16384, 32768, 65536])
+    ap.add_argument("--cases", nargs="*", default=["sse", "config5", "fold_only"])
+    a = ap.parse_args()
     dev = torch.device("cuda")
-    for n in (1024, 4096, 8192, 16384, 32768, 65536):
+    for n in a.n:
         g = torch.Generator(device=dev).manual_seed(n)
         x = torch.randn(n, device=dev, generator=g)
         y = x + 0.3 * torch.randn(n, device=dev, generator=g)
@@ -32,6 +38,8 @@ def main():
         }
         row = {"n": n}
         for name, fn in cases.items():
+            if name not in a.cases:
+                continue
             for _ in range(20):
                 fn()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -18,9 +18,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, nargs="*", default=[1024, 4096, 8192, 16384, 32768, 65536])
     ap.add_argument("--cases", nargs="*", default=["sse", "config5", "fold_only"])
-    a = ap.parse_args()
+    args = ap.parse_args()
     dev = torch.device("cuda")
-    for n in a.n:
+    for n in args.n:
         g = torch.Generator(device=dev).manual_seed(n)
         x = torch.randn(n, device=dev, generator=g)
         y = x + 0.3 * torch.randn(n, device=dev, generator=g)
@@ -38,7 +38,7 @@ def main():
         }
         row = {"n": n}
         for name, fn in cases.items():
-            if name not in a.cases:
+            if name not in args.cases:
                 continue
             for _ in range(20):
                 fn()

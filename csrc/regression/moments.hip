@@ -400,6 +400,79 @@ __global__ void __launch_bounds__(kSmallThreads) moments_small_kernel(
   }
 }
 
+// Small batches on MANY blocks, still one launch and no fence: every block reduces its slice to per-column sums
+// and stores them with agent-scope (sc1) stores; after every storing wave's vmcnt(0) wait and a block barrier, one
+// lane adds 1 to the stream's ticket with an agent-scope atomic.  The block whose add returns G - 1 is last: it loads
+// all G partial rows with agent-scope (sc1) loads, sums them in block order (reproducible), applies the destinations /
+// the Pearson fold, and re-arms the ticket.  (The hand-off of MI355X_MICROARCH.md's table, first row: sc1 payload,
+// one counter, the last adder loads after its add returned, its block's other waves after a barrier.)  The single-
+// block kernel above left the chip idle but one CU: 13 us for config #5's 8192 pairs.
+constexpr int kHandoffThreads = 256;
+constexpr int kHandoffRows = 512;  // values per block (G = ceil(n / 512), at most 128 blocks)
+
+template <typename scalar_t>
+__global__ void __launch_bounds__(kHandoffThreads) moments_handoff_kernel(
+    const scalar_t* __restrict__ preds, const scalar_t* __restrict__ target, long long total, int k, int mask,
+    double eps, double pw, const float* __restrict__ shift_p, const float* __restrict__ shift_t, DestSpec spec,
+    double* __restrict__ out_sums, double* __restrict__ partial, unsigned int* __restrict__ ticket) {
+  __shared__ double wsum[kHandoffThreads / kWave][kWave][kMaxSums];  // [wave][column][sum] (k divides the wave)
+  __shared__ double tot[kWave * kMaxSums];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  constexpr int kWaves = kHandoffThreads / kWave;
+  double acc[kMaxSums];
+#pragma unroll
+  for (int q = 0; q < kMaxSums; ++q) acc[q] = 0.0;
+  const int col = tid % k;  // (block size and block offsets are multiples of k: a thread keeps its column)
+  const float sp = shift_p ? shift_p[col] : 0.f;
+  const float st = shift_t ? shift_t[col] : 0.f;
+  const long long stride = static_cast<long long>(gridDim.x) * kHandoffThreads;
+  for (long long i = static_cast<long long>(blockIdx.x) * kHandoffThreads + tid; i < total; i += stride)
+    accumulate_pair(acc, preds[i], target[i], sp, st, mask, eps, pw);
+#pragma unroll
+  for (int q = 0; q < kMaxSums; ++q) {
+    if (!((mask >> q) & 1) && q != kCOUNT) continue;  // uniform
+    double v = acc[q];
+    for (int off = kWave / 2; off >= k; off >>= 1) v += __shfl_xor(v, off, kWave);
+    if (lane < k) wsum[wid][lane][q] = v;
+  }
+  __syncthreads();
+  double* row = partial + static_cast<long long>(blockIdx.x) * k * kMaxSums;
+  for (int i = tid; i < k * kMaxSums; i += kHandoffThreads) {
+    const int c = i / kMaxSums, q = i % kMaxSums;
+    double v = 0.0;
+    if (((mask >> q) & 1) || q == kCOUNT)
+      for (int w = 0; w < kWaves; ++w) v += wsum[w][c][q];
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(row + i),
+                       static_cast<unsigned long long>(__double_as_longlong(v)), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
+  __syncthreads();
+  if (tid == 0)
+    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  // the last block: every partial row with sc1 loads, summed in block order
+  for (int i = tid; i < k * kMaxSums; i += kHandoffThreads) {
+    const int q = i % kMaxSums;
+    double v = 0.0;
+    if (((mask >> q) & 1) || q == kCOUNT)
+      for (unsigned b = 0; b < gridDim.x; ++b)
+        v += __longlong_as_double(static_cast<long long>(__hip_atomic_load(
+            reinterpret_cast<unsigned long long*>(partial + static_cast<long long>(b) * k * kMaxSums + i),
+            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+    tot[i] = v;
+    if (out_sums) out_sums[i] = v;
+  }
+  __syncthreads();
+  for (int i = tid; i < k * (spec.n + 1); i += kHandoffThreads) {
+    const int c = i / (spec.n + 1), j = i % (spec.n + 1);
+    apply_sums(tot + c * kMaxSums, c, j, spec);
+  }
+  if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+}
+
 }  // namespace
 
 // One zeroed uint32 per (device, stream), kept for the process: the last-block fold of moments_partial_kernel counts
@@ -523,8 +596,29 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
     C10_HIP_KERNEL_LAUNCH_CHECK();
     return sums;
   }
+  static const bool handoff = [] {
+    const char* e = std::getenv("TM_AMD_MOMENTS_HANDOFF");
+    return !(e && std::atoi(e) == 0);
+  }();
+  if (handoff && kWave % k == 0 && n_rows * k <= kSmallMax) {
+    // per-batch sizes of the streaming metrics (config #5: 8192 pairs): G blocks, the last one folds (no fence)
+    const long long total = n_rows * k;
+    const int G = static_cast<int>(std::min<long long>(128, std::max<long long>(1, (total + kHandoffRows - 1) /
+                                                                                       kHandoffRows)));
+    unsigned int* ticket = stream_ticket(preds.get_device(), s);
+    at::Tensor partial = at::empty({G, k, kMaxSums}, dopt);
+    TM_DISPATCH_FLOAT(preds.scalar_type(), "moments_update", [&] {
+      hipLaunchKernelGGL((moments_handoff_kernel<scalar_t>), dim3(G), dim3(kHandoffThreads), 0, s,
+                         reinterpret_cast<const scalar_t*>(preds.data_ptr()),
+                         reinterpret_cast<const scalar_t*>(target.data_ptr()), total, k, static_cast<int>(mask), eps,
+                         power, sp, st, spec, want_sums ? sums.data_ptr<double>() : nullptr, partial.data_ptr<double>(),
+                         ticket);
+    });
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+    return sums;
+  }
   if (kWave % k == 0 && n_rows * k <= kSmallMax) {
-    // per-batch sizes of the streaming metrics (config #5: 8192 pairs): ONE 1024-thread block, one launch
+    // per-batch sizes of the streaming metrics (config #5: 8192 pairs): ONE 512-thread block, one launch
     const size_t lds = static_cast<size_t>(kSmallThreads / kWave + 1) * k * kMaxSums * sizeof(double);
     TM_DISPATCH_FLOAT(preds.scalar_type(), "moments_update", [&] {
       hipLaunchKernelGGL((moments_small_kernel<scalar_t>), dim3(1), dim3(kSmallThreads), lds, s,

@@ -355,8 +355,8 @@ __global__ void __launch_bounds__(kFamThreads) family_fold_kernel(FamilySpec sp,
       const long long v = sp.img[i];
       sp.img[i] = 0;
       cmb[i] = v;
-      for (int k = 0; k < sp.n_cm; ++k)
-        if (v) sp.cm[k][i] += v;
+      for (int k = 0; k < sp.n_cm; ++k)  // no-return atomics: a plain += chained a load round trip per consumer
+        if (v) atomic_add_i64(sp.cm[k] + i, v);
     }
     __syncthreads();
     if (sp.n_st == 0) return;
@@ -386,17 +386,17 @@ __global__ void __launch_bounds__(kFamThreads) family_fold_kernel(FamilySpec sp,
     const long long n_valid = tot[3];
     for (int k = 0; k < sp.n_st; ++k) {
       if (sp.st_micro[k]) {
-        if (tid == 0) {
-          sp.st[k][0][0] += tot[0];
-          sp.st[k][1][0] += tot[1];
-          sp.st[k][2][0] += static_cast<long long>(C) * n_valid - tot[0] - tot[1] - tot[2];
-          sp.st[k][3][0] += tot[2];
+        if (tid == 0) {  // (no-return atomics: four += per consumer were 4 x n_st dependent load round trips)
+          atomic_add_i64(sp.st[k][0], tot[0]);
+          atomic_add_i64(sp.st[k][1], tot[1]);
+          atomic_add_i64(sp.st[k][2], static_cast<long long>(C) * n_valid - tot[0] - tot[1] - tot[2]);
+          atomic_add_i64(sp.st[k][3], tot[2]);
         }
       } else if (tid < C) {
-        sp.st[k][0][tid] += tp;
-        sp.st[k][1][tid] += fp;
-        sp.st[k][2][tid] += n_valid - tp - fp - fn;
-        sp.st[k][3][tid] += fn;
+        atomic_add_i64(sp.st[k][0] + tid, tp);
+        atomic_add_i64(sp.st[k][1] + tid, fp);
+        atomic_add_i64(sp.st[k][2] + tid, n_valid - tp - fp - fn);
+        atomic_add_i64(sp.st[k][3] + tid, fn);
       }
     }
     return;

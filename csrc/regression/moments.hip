@@ -76,12 +76,22 @@ __device__ __forceinline__ double ld_state(const DestSpec& spec, int j, int c) {
                              : reinterpret_cast<const double*>(spec.fptr[j])[c];
 }
 
-__device__ __forceinline__ void add_state(const DestSpec& spec, int j, int c, double inc) {
-  if (spec.fdtype[j] == 0) {
-    float* q = reinterpret_cast<float*>(spec.fptr[j]) + c;
-    *q = *q + static_cast<float>(inc);
-  } else {
-    reinterpret_cast<double*>(spec.fptr[j])[c] += inc;
+// The fold of one column: all six states are loaded before the first store (load-after-possibly-aliasing-store
+// kept the compiler from hoisting them: six dependent HBM round trips, ~1 us each, at the tail of every launch).
+__device__ __forceinline__ void pearson_fold(const DestSpec& spec, int c, double sd, double se, double sdd, double see,
+                                             double sde, double n) {
+  double old[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) old[j] = ld_state(spec, j, c);
+  const double tot = old[5] + n;
+  const double dx = sd / tot, dy = se / tot;
+  const double inc[6] = {dx, dy, sdd - dx * sd, see - dy * se, sde - dx * se, n};
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    if (spec.fdtype[j] == 0)
+      reinterpret_cast<float*>(spec.fptr[j])[c] = static_cast<float>(old[j]) + static_cast<float>(inc[j]);
+    else
+      reinterpret_cast<double*>(spec.fptr[j])[c] = old[j] + inc[j];
   }
 }
 
@@ -157,13 +167,14 @@ __global__ void __launch_bounds__(kBlock) moments_partial_kernel(const scalar_t*
     // 4-wave fold in LDS (the generic path below walks the block serially per column: ~25 us for k = 1)
     __shared__ double wred[kBlock / kWave][kWave][kMaxSums];
     const int wid = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+    for (int off = kWave / 2; off >= k; off >>= 1) {  // offsets outer: the sums' permutes overlap
 #pragma unroll
-    for (int s = 0; s < kMaxSums; ++s) {
-      if (!((mask >> s) & 1) && s != kCOUNT) continue;  // uniform: only the requested sums cross the wave
-      double v = acc[s];
-      for (int off = kWave / 2; off >= k; off >>= 1) v += __shfl_xor(v, off, kWave);
-      if (lane < k) wred[wid][lane][s] = v;
+      for (int s = 0; s < kMaxSums; ++s)  // every sum, branch-free: a per-sum branch split the batch of permutes
+        acc[s] += __shfl_xor(acc[s], off, kWave);
     }
+#pragma unroll
+    for (int s = 0; s < kMaxSums; ++s)
+      if ((((mask >> s) & 1) || s == kCOUNT) && lane < k) wred[wid][lane][s] = acc[s];
     __syncthreads();
     for (int i = threadIdx.x; i < k * kMaxSums; i += blockDim.x) {
       const int c = i / kMaxSums, s = i % kMaxSums;
@@ -230,14 +241,12 @@ __device__ void finalize_column(const double* __restrict__ partial, int nblocks,
   }
   const int wid = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
 #pragma unroll
-  for (int s = 0; s < kMaxSums; ++s) {
-    if (!((mask >> s) & 1) && s != kCOUNT) {
-      if (lane == 0) red[s][wid] = 0.0;
-      continue;
-    }
-    const double v = wave_sum(acc[s]);
-    if (lane == 0) red[s][wid] = v;
-  }
+  for (int off = kWave / 2; off > 0; off >>= 1)  // offsets outer, branch-free: the sums' permutes overlap
+#pragma unroll
+    for (int s = 0; s < kMaxSums; ++s) acc[s] += __shfl_xor(acc[s], off, kWave);
+#pragma unroll
+  for (int s = 0; s < kMaxSums; ++s)
+    if (lane == 0) red[s][wid] = (((mask >> s) & 1) || s == kCOUNT) ? acc[s] : 0.0;
   __syncthreads();
   if (threadIdx.x < kMaxSums) {
     double v = 0.0;
@@ -250,14 +259,7 @@ __device__ void finalize_column(const double* __restrict__ partial, int nblocks,
     if (threadIdx.x == kWave) {  // a lane of the second wave: the first wave's lanes own the plain dests below
       const double sd = red[kSP][0], se = red[kST][0], sdd = red[kSPP][0], see = red[kSTT][0], sde = red[kSPT][0];
       const double n = red[kCOUNT][0];
-      const double tot = ld_state(spec, 5, c) + n;
-      const double dx = sd / tot, dy = se / tot;
-      add_state(spec, 0, c, dx);
-      add_state(spec, 1, c, dy);
-      add_state(spec, 2, c, sdd - dx * sd);
-      add_state(spec, 3, c, see - dy * se);
-      add_state(spec, 4, c, sde - dx * se);
-      add_state(spec, 5, c, n);
+      pearson_fold(spec, c, sd, se, sdd, see, sde, n);
     }
   }
   if (threadIdx.x < spec.n) {
@@ -339,14 +341,73 @@ __device__ __forceinline__ void apply_sums(const double* __restrict__ v, int c, 
     }
   } else if (spec.fold == kFoldPearson) {
     const double sd = v[kSP], se = v[kST], sdd = v[kSPP], see = v[kSTT], sde = v[kSPT], n = v[kCOUNT];
-    const double tot = ld_state(spec, 5, c) + n;
-    const double dx = sd / tot, dy = se / tot;
-    add_state(spec, 0, c, dx);
-    add_state(spec, 1, c, dy);
-    add_state(spec, 2, c, sdd - dx * sd);
-    add_state(spec, 3, c, see - dy * se);
-    add_state(spec, 4, c, sde - dx * se);
-    add_state(spec, 5, c, n);
+    pearson_fold(spec, c, sd, se, sdd, see, sde, n);
+  }
+}
+
+// The same application with every load hoisted to the kernel's start: the (column, destination) item's spec fields
+// and the destination's old value(s) are loaded while the pass's own loads are in flight, so the tail is arithmetic
+// and stores.  (Applied after the sums, the field loads -- dynamically indexed kernel arguments -- then the pointer,
+// then the old value were three dependent round trips, ~1 us each, at the end of every small launch.)  Valid because
+// nothing else writes the destinations while the launch runs (one stream), and only one block applies.
+struct ApplyPre {
+  unsigned long long raw[6];  // old values, as stored (f32 in the low word / f64 / i64)
+  void* ptr;
+  int sum_id, sub_id, dtype, idx, live;
+};
+
+__device__ __forceinline__ unsigned long long ld_raw(const void* p, int dtype, int idx) {
+  if (dtype == 0) return __float_as_uint(reinterpret_cast<const float*>(p)[idx]);
+  return reinterpret_cast<const unsigned long long*>(p)[idx];
+}
+
+__device__ __forceinline__ ApplyPre apply_prefetch(int c, int j, const DestSpec& spec) {
+  ApplyPre a{};
+  if (j < spec.n) {
+    a.live = spec.per_col[j] || c == 0;
+    a.ptr = spec.ptr[j];
+    a.sum_id = spec.sum_id[j];
+    a.sub_id = spec.sub_id[j];
+    a.dtype = spec.dtype[j];
+    a.idx = spec.per_col[j] ? c : 0;
+    if (a.live) a.raw[0] = ld_raw(a.ptr, a.dtype, a.idx);
+  } else if (spec.fold == kFoldPearson) {
+    a.live = 1;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) a.raw[q] = ld_raw(spec.fptr[q], spec.fdtype[q], c);
+  }
+  return a;
+}
+
+__device__ __forceinline__ void apply_sums_pre(const double* __restrict__ v, int c, int j, const DestSpec& spec,
+                                               const ApplyPre& a) {
+  if (!a.live) return;
+  if (j < spec.n) {
+    const double x = v[a.sum_id] - (a.sub_id >= 0 ? v[a.sub_id] : 0.0);
+    const int idx = a.idx;
+    if (a.dtype == 0)
+      reinterpret_cast<float*>(a.ptr)[idx] = __uint_as_float(static_cast<unsigned>(a.raw[0])) + static_cast<float>(x);
+    else if (a.dtype == 1)
+      reinterpret_cast<double*>(a.ptr)[idx] = __longlong_as_double(static_cast<long long>(a.raw[0])) + x;
+    else
+      reinterpret_cast<int64_t*>(a.ptr)[idx] = static_cast<int64_t>(a.raw[0]) + static_cast<int64_t>(llrint(x));
+    return;
+  }
+  const double sd = v[kSP], se = v[kST], sdd = v[kSPP], see = v[kSTT], sde = v[kSPT], n = v[kCOUNT];
+  double old[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+    old[q] = spec.fdtype[q] == 0 ? static_cast<double>(__uint_as_float(static_cast<unsigned>(a.raw[q])))
+                                 : __longlong_as_double(static_cast<long long>(a.raw[q]));
+  const double tot = old[5] + n;
+  const double dx = sd / tot, dy = se / tot;
+  const double inc[6] = {dx, dy, sdd - dx * sd, see - dy * se, sde - dx * se, n};
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    if (spec.fdtype[q] == 0)
+      reinterpret_cast<float*>(spec.fptr[q])[c] = static_cast<float>(old[q]) + static_cast<float>(inc[q]);
+    else
+      reinterpret_cast<double*>(spec.fptr[q])[c] = old[q] + inc[q];
   }
 }
 
@@ -358,12 +419,20 @@ __global__ void __launch_bounds__(kSmallThreads) moments_small_kernel(
   extern __shared__ double wsum[];  // [16 waves][k][kMaxSums], then [k][kMaxSums] block totals
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
   constexpr int kWaves = kSmallThreads / kWave;
+  // measurement-only ablation (TM_AMD_MOMENTS_ABLATE, bits 27..29 of mask): 1 no pass, 2 no apply, 4 no prefetch
+  const int abl = (mask >> 27) & 7;
+  mask &= (1 << 27) - 1;
+  if (abl & 1) total = 0;
   double acc[kMaxSums];
 #pragma unroll
   for (int q = 0; q < kMaxSums; ++q) acc[q] = 0.0;
   const int col = tid % k;
   const float sp = shift_p ? shift_p[col] : 0.f;
   const float st = shift_t ? shift_t[col] : 0.f;
+  const int items = k * (spec.n + 1);
+  const bool pre = items <= kSmallThreads;  // uniform: one (column, destination) item per thread
+  ApplyPre ap{};
+  if (pre && tid < items && !(abl & 4)) ap = apply_prefetch(tid / (spec.n + 1), tid % (spec.n + 1), spec);
   for (long long base = tid; base < total; base += static_cast<long long>(kSmallThreads) * kSmallUnroll) {
     scalar_t pv[kSmallUnroll], tv[kSmallUnroll];
 #pragma unroll
@@ -376,13 +445,16 @@ __global__ void __launch_bounds__(kSmallThreads) moments_small_kernel(
     for (int u = 0; u < kSmallUnroll; ++u)
       if (base + static_cast<long long>(u) * kSmallThreads < total) accumulate_pair(acc, pv[u], tv[u], sp, st, mask, eps, pw);
   }
+  // offsets outer, sums inner: the 19 sums' ds_bpermutes of one offset are in flight together (sums outer put 6 x 19
+  // dependent ~100-cycle permutes in a row: ~5 us of the kernel at config #5's mask)
+  for (int off = kWave / 2; off >= k; off >>= 1) {
 #pragma unroll
-  for (int q = 0; q < kMaxSums; ++q) {
-    if (!((mask >> q) & 1) && q != kCOUNT) continue;  // uniform
-    double v = acc[q];
-    for (int off = kWave / 2; off >= k; off >>= 1) v += __shfl_xor(v, off, kWave);
-    if (lane < k) wsum[(wid * k + lane) * kMaxSums + q] = v;
+    for (int q = 0; q < kMaxSums; ++q)
+      acc[q] += __shfl_xor(acc[q], off, kWave);  // every sum, branch-free (a per-sum branch split the batch)
   }
+#pragma unroll
+  for (int q = 0; q < kMaxSums; ++q)
+    if ((((mask >> q) & 1) || q == kCOUNT) && lane < k) wsum[(wid * k + lane) * kMaxSums + q] = acc[q];
   __syncthreads();
   double* tot = wsum + kWaves * k * kMaxSums;
   for (int i = tid; i < k * kMaxSums; i += kSmallThreads) {
@@ -394,7 +466,12 @@ __global__ void __launch_bounds__(kSmallThreads) moments_small_kernel(
     if (out_sums) out_sums[i] = v;
   }
   __syncthreads();
-  for (int i = tid; i < k * (spec.n + 1); i += kSmallThreads) {
+  if (abl & 2) return;
+  if (pre) {
+    if (tid < items) apply_sums_pre(tot + (tid / (spec.n + 1)) * kMaxSums, tid / (spec.n + 1), tid % (spec.n + 1), spec, ap);
+    return;
+  }
+  for (int i = tid; i < items; i += kSmallThreads) {
     const int c = i / (spec.n + 1), j = i % (spec.n + 1);
     apply_sums(tot + c * kMaxSums, c, j, spec);
   }
@@ -408,41 +485,48 @@ __global__ void __launch_bounds__(kSmallThreads) moments_small_kernel(
 // one counter, the last adder loads after its add returned, its block's other waves after a barrier.)  The single-
 // block kernel above left the chip idle but one CU: 13 us for config #5's 8192 pairs.
 constexpr int kHandoffThreads = 256;
-constexpr int kHandoffRows = 512;  // values per block (G = ceil(n / 512), at most 128 blocks)
+constexpr int kHandoffRows = 512;     // values per block (G = ceil(n / 512), at most 128 blocks)
+constexpr int kHandoffMaxRows = 256;  // G * k: the last block stages every partial row in LDS (<= 39 KB)
 
 template <typename scalar_t>
 __global__ void __launch_bounds__(kHandoffThreads) moments_handoff_kernel(
     const scalar_t* __restrict__ preds, const scalar_t* __restrict__ target, long long total, int k, int mask,
     double eps, double pw, const float* __restrict__ shift_p, const float* __restrict__ shift_t, DestSpec spec,
     double* __restrict__ out_sums, double* __restrict__ partial, unsigned int* __restrict__ ticket) {
-  __shared__ double wsum[kHandoffThreads / kWave][kWave][kMaxSums];  // [wave][column][sum] (k divides the wave)
-  __shared__ double tot[kWave * kMaxSums];
+  // phase 1: [wave][column][sum]; the last block then reuses it for [G][column][sum] staged rows + [column][sum] totals
+  extern __shared__ double lds[];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
   constexpr int kWaves = kHandoffThreads / kWave;
+  const int kk = k * kMaxSums;
   double acc[kMaxSums];
 #pragma unroll
   for (int q = 0; q < kMaxSums; ++q) acc[q] = 0.0;
   const int col = tid % k;  // (block size and block offsets are multiples of k: a thread keeps its column)
   const float sp = shift_p ? shift_p[col] : 0.f;
   const float st = shift_t ? shift_t[col] : 0.f;
+  const int items = k * (spec.n + 1);
+  const bool pre = items <= kHandoffThreads;  // uniform (every block prefetches: it does not know yet who is last)
+  ApplyPre ap{};
+  if (pre && tid < items) ap = apply_prefetch(tid / (spec.n + 1), tid % (spec.n + 1), spec);
   const long long stride = static_cast<long long>(gridDim.x) * kHandoffThreads;
   for (long long i = static_cast<long long>(blockIdx.x) * kHandoffThreads + tid; i < total; i += stride)
     accumulate_pair(acc, preds[i], target[i], sp, st, mask, eps, pw);
+  for (int off = kWave / 2; off >= k; off >>= 1) {  // (offsets outer: see moments_small_kernel)
 #pragma unroll
-  for (int q = 0; q < kMaxSums; ++q) {
-    if (!((mask >> q) & 1) && q != kCOUNT) continue;  // uniform
-    double v = acc[q];
-    for (int off = kWave / 2; off >= k; off >>= 1) v += __shfl_xor(v, off, kWave);
-    if (lane < k) wsum[wid][lane][q] = v;
+    for (int q = 0; q < kMaxSums; ++q)
+      acc[q] += __shfl_xor(acc[q], off, kWave);
   }
+#pragma unroll
+  for (int q = 0; q < kMaxSums; ++q)
+    if ((((mask >> q) & 1) || q == kCOUNT) && lane < k) lds[(wid * k + lane) * kMaxSums + q] = acc[q];
   __syncthreads();
-  double* row = partial + static_cast<long long>(blockIdx.x) * k * kMaxSums;
-  for (int i = tid; i < k * kMaxSums; i += kHandoffThreads) {
+  double* row = partial + static_cast<long long>(blockIdx.x) * kk;
+  for (int i = tid; i < kk; i += kHandoffThreads) {
     const int c = i / kMaxSums, q = i % kMaxSums;
     double v = 0.0;
     if (((mask >> q) & 1) || q == kCOUNT)
-      for (int w = 0; w < kWaves; ++w) v += wsum[w][c][q];
+      for (int w = 0; w < kWaves; ++w) v += lds[(w * k + c) * kMaxSums + q];
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(row + i),
                        static_cast<unsigned long long>(__double_as_longlong(v)), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -453,22 +537,42 @@ __global__ void __launch_bounds__(kHandoffThreads) moments_handoff_kernel(
     last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  // the last block: every partial row with sc1 loads, summed in block order
-  for (int i = tid; i < k * kMaxSums; i += kHandoffThreads) {
+  // the last block: all G partial rows with coalesced, independent sc1 loads into LDS (a per-column chain of G
+  // dependent loads cost ~0.3 us per block), then per (column, sum) a block-order sum (reproducible)
+  const int nload = static_cast<int>(gridDim.x) * kk;
+  for (int base = tid; base < nload; base += 4 * kHandoffThreads) {
+    unsigned long long v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int f = base + u * kHandoffThreads;
+      v[u] = f < nload ? __hip_atomic_load(reinterpret_cast<unsigned long long*>(partial + f), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)
+                       : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int f = base + u * kHandoffThreads;
+      if (f < nload) lds[f] = __longlong_as_double(static_cast<long long>(v[u]));
+    }
+  }
+  __syncthreads();
+  double* tot = lds + nload;
+  for (int i = tid; i < kk; i += kHandoffThreads) {
     const int q = i % kMaxSums;
     double v = 0.0;
     if (((mask >> q) & 1) || q == kCOUNT)
-      for (unsigned b = 0; b < gridDim.x; ++b)
-        v += __longlong_as_double(static_cast<long long>(__hip_atomic_load(
-            reinterpret_cast<unsigned long long*>(partial + static_cast<long long>(b) * k * kMaxSums + i),
-            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+      for (unsigned b = 0; b < gridDim.x; ++b) v += lds[b * kk + i];
     tot[i] = v;
     if (out_sums) out_sums[i] = v;
   }
   __syncthreads();
-  for (int i = tid; i < k * (spec.n + 1); i += kHandoffThreads) {
-    const int c = i / (spec.n + 1), j = i % (spec.n + 1);
-    apply_sums(tot + c * kMaxSums, c, j, spec);
+  if (pre) {
+    if (tid < items) apply_sums_pre(tot + (tid / (spec.n + 1)) * kMaxSums, tid / (spec.n + 1), tid % (spec.n + 1), spec, ap);
+  } else {
+    for (int i = tid; i < items; i += kHandoffThreads) {
+      const int c = i / (spec.n + 1), j = i % (spec.n + 1);
+      apply_sums(tot + c * kMaxSums, c, j, spec);
+    }
   }
   if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
 }
@@ -596,19 +700,22 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
     C10_HIP_KERNEL_LAUNCH_CHECK();
     return sums;
   }
-  static const bool handoff = [] {
+  // TM_AMD_MOMENTS_HANDOFF: the smallest n * k taking the multi-block hand-off (0 = never)
+  static const long long handoff_min = [] {
     const char* e = std::getenv("TM_AMD_MOMENTS_HANDOFF");
-    return !(e && std::atoi(e) == 0);
+    return e ? std::atoll(e) : 8192LL;  // below: the single block (one fewer round trip)
   }();
-  if (handoff && kWave % k == 0 && n_rows * k <= kSmallMax) {
+  if (handoff_min > 0 && n_rows * k >= handoff_min && kWave % k == 0 && n_rows * k <= kSmallMax) {
     // per-batch sizes of the streaming metrics (config #5: 8192 pairs): G blocks, the last one folds (no fence)
     const long long total = n_rows * k;
-    const int G = static_cast<int>(std::min<long long>(128, std::max<long long>(1, (total + kHandoffRows - 1) /
-                                                                                       kHandoffRows)));
+    long long g = (total + kHandoffRows - 1) / kHandoffRows;
+    g = std::min<long long>(g, std::min<long long>(128, kHandoffMaxRows / k));
+    const int G = static_cast<int>(std::max<long long>(1, g));
     unsigned int* ticket = stream_ticket(preds.get_device(), s);
     at::Tensor partial = at::empty({G, k, kMaxSums}, dopt);
+    const size_t lds = static_cast<size_t>(std::max(kHandoffThreads / kWave, G + 1)) * k * kMaxSums * sizeof(double);
     TM_DISPATCH_FLOAT(preds.scalar_type(), "moments_update", [&] {
-      hipLaunchKernelGGL((moments_handoff_kernel<scalar_t>), dim3(G), dim3(kHandoffThreads), 0, s,
+      hipLaunchKernelGGL((moments_handoff_kernel<scalar_t>), dim3(G), dim3(kHandoffThreads), lds, s,
                          reinterpret_cast<const scalar_t*>(preds.data_ptr()),
                          reinterpret_cast<const scalar_t*>(target.data_ptr()), total, k, static_cast<int>(mask), eps,
                          power, sp, st, spec, want_sums ? sums.data_ptr<double>() : nullptr, partial.data_ptr<double>(),
@@ -617,14 +724,19 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
     C10_HIP_KERNEL_LAUNCH_CHECK();
     return sums;
   }
+  static const int ablate = [] {
+    const char* e = std::getenv("TM_AMD_MOMENTS_ABLATE");
+    return e ? (std::atoi(e) & 7) : 0;
+  }();
   if (kWave % k == 0 && n_rows * k <= kSmallMax) {
     // per-batch sizes of the streaming metrics (config #5: 8192 pairs): ONE 512-thread block, one launch
     const size_t lds = static_cast<size_t>(kSmallThreads / kWave + 1) * k * kMaxSums * sizeof(double);
     TM_DISPATCH_FLOAT(preds.scalar_type(), "moments_update", [&] {
       hipLaunchKernelGGL((moments_small_kernel<scalar_t>), dim3(1), dim3(kSmallThreads), lds, s,
                          reinterpret_cast<const scalar_t*>(preds.data_ptr()),
-                         reinterpret_cast<const scalar_t*>(target.data_ptr()), n_rows * k, k, static_cast<int>(mask),
-                         eps, power, sp, st, spec, want_sums ? sums.data_ptr<double>() : nullptr);
+                         reinterpret_cast<const scalar_t*>(target.data_ptr()), n_rows * k, k,
+                         static_cast<int>(mask) | (ablate << 27), eps, power, sp, st, spec,
+                         want_sums ? sums.data_ptr<double>() : nullptr);
     });
     C10_HIP_KERNEL_LAUNCH_CHECK();
     return sums;

@@ -167,11 +167,7 @@ __global__ void __launch_bounds__(kBlock) moments_partial_kernel(const scalar_t*
     // 4-wave fold in LDS (the generic path below walks the block serially per column: ~25 us for k = 1)
     __shared__ double wred[kBlock / kWave][kWave][kMaxSums];
     const int wid = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-    for (int off = kWave / 2; off >= k; off >>= 1) {  // offsets outer: the sums' permutes overlap
-#pragma unroll
-      for (int s = 0; s < kMaxSums; ++s)  // every sum, branch-free: a per-sum branch split the batch of permutes
-        acc[s] += __shfl_xor(acc[s], off, kWave);
-    }
+    wave_colsum_f64(acc, k);
 #pragma unroll
     for (int s = 0; s < kMaxSums; ++s)
       if ((((mask >> s) & 1) || s == kCOUNT) && lane < k) wred[wid][lane][s] = acc[s];
@@ -240,10 +236,7 @@ __device__ void finalize_column(const double* __restrict__ partial, int nblocks,
     for (int s = 0; s < kMaxSums; ++s) acc[s] += src[s];
   }
   const int wid = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-#pragma unroll
-  for (int off = kWave / 2; off > 0; off >>= 1)  // offsets outer, branch-free: the sums' permutes overlap
-#pragma unroll
-    for (int s = 0; s < kMaxSums; ++s) acc[s] += __shfl_xor(acc[s], off, kWave);
+  wave_colsum_f64(acc, 1);
 #pragma unroll
   for (int s = 0; s < kMaxSums; ++s)
     if (lane == 0) red[s][wid] = (((mask >> s) & 1) || s == kCOUNT) ? acc[s] : 0.0;
@@ -445,13 +438,7 @@ __global__ void __launch_bounds__(kSmallThreads) moments_small_kernel(
     for (int u = 0; u < kSmallUnroll; ++u)
       if (base + static_cast<long long>(u) * kSmallThreads < total) accumulate_pair(acc, pv[u], tv[u], sp, st, mask, eps, pw);
   }
-  // offsets outer, sums inner: the 19 sums' ds_bpermutes of one offset are in flight together (sums outer put 6 x 19
-  // dependent ~100-cycle permutes in a row: ~5 us of the kernel at config #5's mask)
-  for (int off = kWave / 2; off >= k; off >>= 1) {
-#pragma unroll
-    for (int q = 0; q < kMaxSums; ++q)
-      acc[q] += __shfl_xor(acc[q], off, kWave);  // every sum, branch-free (a per-sum branch split the batch)
-  }
+  wave_colsum_f64(acc, k);  // VALU (DPP / permlane) column sums: LDS-pipe shuffles were most of this kernel
 #pragma unroll
   for (int q = 0; q < kMaxSums; ++q)
     if ((((mask >> q) & 1) || q == kCOUNT) && lane < k) wsum[(wid * k + lane) * kMaxSums + q] = acc[q];
@@ -512,11 +499,7 @@ __global__ void __launch_bounds__(kHandoffThreads) moments_handoff_kernel(
   const long long stride = static_cast<long long>(gridDim.x) * kHandoffThreads;
   for (long long i = static_cast<long long>(blockIdx.x) * kHandoffThreads + tid; i < total; i += stride)
     accumulate_pair(acc, preds[i], target[i], sp, st, mask, eps, pw);
-  for (int off = kWave / 2; off >= k; off >>= 1) {  // (offsets outer: see moments_small_kernel)
-#pragma unroll
-    for (int q = 0; q < kMaxSums; ++q)
-      acc[q] += __shfl_xor(acc[q], off, kWave);
-  }
+  wave_colsum_f64(acc, k);
 #pragma unroll
   for (int q = 0; q < kMaxSums; ++q)
     if ((((mask >> q) & 1) || q == kCOUNT) && lane < k) lds[(wid * k + lane) * kMaxSums + q] = acc[q];

@@ -230,3 +230,25 @@ def test_moments_mid_size_last_block_fold(rows, k):
             gpu.update(p.cuda(), (p + t).cuda())
             cpu.update(p, p + t)
         torch.testing.assert_close(gpu.compute().cpu(), cpu.compute(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 16, 32, 64])
+@pytest.mark.parametrize("total", [1024, 16384, 65536])
+def test_moments_wave_column_sums(k, total):
+    """csrc/common/tm_common.h wave_colsum_f64: per-column wave sums in VALU (row_ror DPP for offsets 1..8, permlane16 /
+    permlane32 swaps for 16 / 32) for every power-of-two column count dividing the wave, through the single-block
+    (<= 8192 values) and the multi-block hand-off (> 8192) moments kernels -- against the CPU metrics."""
+    rows = total // k
+    g = torch.Generator().manual_seed(total + k)
+    shape = (rows,) if k == 1 else (rows, k)
+    kw = {} if k == 1 else {"num_outputs": k}
+    multi = {"multioutput": "raw_values"} if k > 1 else {}
+    makers = [lambda: tm.MeanSquaredError(**kw), lambda: tm.R2Score(**kw, **multi), lambda: tm.PearsonCorrCoef(**kw)]
+    for make in makers:
+        gpu, cpu = make().cuda(), make()
+        for _ in range(3):
+            p, t = torch.randn(shape, generator=g), torch.randn(shape, generator=g)
+            gpu.update(p.cuda(), (p + t).cuda())
+            cpu.update(p, p + t)
+        torch.testing.assert_close(gpu.compute().cpu(), cpu.compute(), rtol=1e-5, atol=1e-6)

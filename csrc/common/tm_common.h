@@ -95,18 +95,30 @@ struct IsFloating<c10::BFloat16> {
 };
 
 // ------------------------------------------------------------------------------------------ wave reductions
+// Whole-wave sums through the device library's wave reductions (DPP row shifts + readlane, inactive lanes count as
+// zero, the result is wave-uniform): VALU work.  A __shfl_xor tree is six dependent ds_bpermutes (twice for 64-bit
+// values) through the LDS pipe -- ~100 cycles each in a latency-bound tail and ~8 clk of LDS issue per wave.
+extern "C" __device__ __attribute__((const)) float __ockl_wfred_add_f32(float);
+extern "C" __device__ __attribute__((const)) double __ockl_wfred_add_f64(double);
+extern "C" __device__ __attribute__((const)) int __ockl_wfred_add_i32(int);
+extern "C" __device__ __attribute__((const)) unsigned int __ockl_wfred_add_u32(unsigned int);
+extern "C" __device__ __attribute__((const)) long long __ockl_wfred_add_i64(long long);
+extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_add_u64(unsigned long long);
+
+__device__ __forceinline__ float wave_sum_impl(float v) { return __ockl_wfred_add_f32(v); }
+__device__ __forceinline__ double wave_sum_impl(double v) { return __ockl_wfred_add_f64(v); }
+__device__ __forceinline__ int wave_sum_impl(int v) { return __ockl_wfred_add_i32(v); }
+__device__ __forceinline__ unsigned int wave_sum_impl(unsigned int v) { return __ockl_wfred_add_u32(v); }
+__device__ __forceinline__ long long wave_sum_impl(long long v) { return __ockl_wfred_add_i64(v); }
+__device__ __forceinline__ long wave_sum_impl(long v) { return __ockl_wfred_add_i64(v); }
+__device__ __forceinline__ unsigned long long wave_sum_impl(unsigned long long v) { return __ockl_wfred_add_u64(v); }
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
-  return v;
+  return wave_sum_impl(v);
 }
 
-__device__ __forceinline__ long long wave_sum_ll(long long v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
-  return v;
-}
+__device__ __forceinline__ long long wave_sum_ll(long long v) { return __ockl_wfred_add_i64(v); }
 
 // ---------------------------------------------------------------------- VALU-only f64 column sums in a wave
 // v[s] summed over the lanes of this wave that share (lane mod k), k a power of two dividing 64 (k = 1: the whole

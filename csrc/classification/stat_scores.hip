@@ -1008,6 +1008,65 @@ __device__ __forceinline__ void bin_pred(scalar_t raw, float thr_t, float cut, i
   }
 }
 
+// Branch-free element step of the binary counters: six raw counts (t & pa, pa, t & pb, pb, t, valid) -- the 7 slots
+// (tp / fp / fn under both probability readings + count) follow from them in bin_to_slots.  The per-element
+// `continue`s of the earlier form (ignored, non-binary target / pred) made every element its own exec-masked basic
+// block: ~86 instructions per element in bin_vec_kernel, VALU / SALU-bound at 2.7 TB/s.  Flag bits are collected in
+// registers and raised once per wave.
+struct BinAcc {
+  int a = 0, p = 0, b = 0, q = 0, t = 0, n = 0;
+  int not_prob = 0, bad_t = 0, bad_p = 0;
+};
+
+template <typename scalar_t, typename target_t>
+__device__ __forceinline__ void bin_step(BinAcc& c, scalar_t raw, target_t traw, float thr_t, float cut,
+                                         long long ignore, bool has_ignore, bool prob_check_all) {
+  const long long tv = static_cast<long long>(traw);
+  const bool ignored = has_ignore && tv == ignore;
+  const bool tbin = static_cast<unsigned long long>(tv) <= 1ull;
+  c.bad_t |= !ignored && !tbin;
+  bool pa, pb, pvalid;
+  if constexpr (IsFloating<scalar_t>::value) {
+    const float v = to_f32(raw);
+    pa = v > thr_t;
+    pb = v >= cut;
+    pvalid = true;
+    c.not_prob |= !(v >= 0.f && v <= 1.f) && (prob_check_all || !ignored);
+  } else {
+    const long long pv = static_cast<long long>(raw);
+    pvalid = static_cast<unsigned long long>(pv) <= 1ull;
+    c.bad_p |= !ignored && tbin && !pvalid;
+    pa = pb = pv == 1;
+  }
+  const int valid = !ignored && tbin && pvalid;
+  const int t = valid & (tv == 1);
+  const int ia = valid & pa, ib = valid & pb;
+  c.a += t & ia;
+  c.p += ia;
+  c.b += t & ib;
+  c.q += ib;
+  c.t += t;
+  c.n += valid;
+}
+
+__device__ __forceinline__ void bin_to_slots(const BinAcc& c, int (&s)[kBinSlots]) {
+  s[0] = c.a;
+  s[1] = c.p - c.a;
+  s[2] = c.t - c.a;
+  s[3] = c.b;
+  s[4] = c.q - c.b;
+  s[5] = c.t - c.b;
+  s[6] = c.n;
+}
+
+// the flags an accumulation saw, raised once per wave (call with every lane of the wave)
+__device__ __forceinline__ void bin_raise(const BinAcc& c, int* flag, int* not_prob) {
+  const bool lead = (threadIdx.x & (kWave - 1)) == 0;
+  if (__any(c.bad_t) && lead) raise_flag(flag, kErrTargetNotBinary);
+  if (__any(c.bad_p) && lead) raise_flag(flag, kErrPredsNotBinary);
+  if (not_prob != nullptr && __any(c.not_prob) && lead) atomicOr(not_prob, 1);
+}
+
 __device__ __forceinline__ void bin_slots(bool t, bool pa, bool pb, int& sa, int& sb) {
   // tp=0 fp=1 fn=2 (tn implicit); -1 = tn
   sa = t ? (pa ? 0 : 2) : (pa ? 1 : -1);
@@ -1165,12 +1224,7 @@ __global__ void __launch_bounds__(kVecBlock) bin_vec_kernel(const scalar_t* __re
   const long long S = static_cast<long long>(gridDim.x) * kVecBlock;
   const long long v0 = static_cast<long long>(blockIdx.x) * kVecBlock + threadIdx.x;
   const int l0 = static_cast<int>((v0 * VEC) % L);
-  int c[VEC][kBinSlots];
-#pragma unroll
-  for (int e = 0; e < VEC; ++e)
-#pragma unroll
-    for (int k = 0; k < kBinSlots; ++k) c[e][k] = 0;
-  int local_not_prob = 0;
+  BinAcc c[VEC];
   const float cut = sigmoid_cut<scalar_t>(thr_t);
   const u32x4* pv = reinterpret_cast<const u32x4*>(preds);
   const u32x4* tvp = reinterpret_cast<const u32x4*>(target);
@@ -1193,35 +1247,24 @@ __global__ void __launch_bounds__(kVecBlock) bin_vec_kernel(const scalar_t* __re
       const scalar_t* pe = reinterpret_cast<const scalar_t*>(&praw[u]);
       const target_t* te = reinterpret_cast<const target_t*>(&traw[u][0]);
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) {
-        const long long tv = static_cast<long long>(te[e]);
-        const bool ignored = has_ignore && tv == ignore;
-        const float x = to_f32(pe[e]);
-        if (!(x >= 0.f && x <= 1.f) && (prob_check_all || !ignored)) local_not_prob = 1;
-        if (ignored) continue;
-        if (tv != 0 && tv != 1) {
-          raise_flag(flag, kErrTargetNotBinary);
-          continue;
-        }
-        const bool pa = x > thr_t;
-        const bool pb = x >= cut;
-        const bool t = tv == 1;
-        c[e][0] += t & pa;
-        c[e][1] += !t & pa;
-        c[e][2] += t & !pa;
-        c[e][3] += t & pb;
-        c[e][4] += !t & pb;
-        c[e][5] += t & !pb;
-        c[e][6] += 1;
-      }
+      for (int e = 0; e < VEC; ++e) bin_step(c[e], pe[e], te[e], thr_t, cut, ignore, has_ignore, prob_check_all);
     }
   }
-  if (__any(local_not_prob) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(not_prob, 1);
+  BinAcc any;
 #pragma unroll
-  for (int e = 0; e < VEC; ++e)
+  for (int e = 0; e < VEC; ++e) {
+    any.bad_t |= c[e].bad_t;
+    any.not_prob |= c[e].not_prob;
+  }
+  bin_raise(any, flag, not_prob);
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    int sl[kBinSlots];
+    bin_to_slots(c[e], sl);
 #pragma unroll
     for (int k = 0; k < kBinSlots; ++k)
-      if (c[e][k]) atomicAdd(&lds[(l0 + e) * kBinSlots + k], c[e][k]);
+      if (sl[k]) atomicAdd(&lds[(l0 + e) * kBinSlots + k], sl[k]);
+  }
   __syncthreads();
   int* row = partials + static_cast<long long>(blockIdx.x) * nbins;
   for (int b = threadIdx.x; b < nbins; b += kVecBlock) row[b] = lds[b];
@@ -1249,51 +1292,27 @@ __global__ void __launch_bounds__(kBlock) bin_reg_kernel(const scalar_t* __restr
   const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
   const long long i0 = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int label = static_cast<int>((i0 / X) % L);
-  int c[kBinSlots] = {0, 0, 0, 0, 0, 0, 0};
-  int local_not_prob = 0;
+  BinAcc acc;
   const float cut = IsFloating<scalar_t>::value ? sigmoid_cut<scalar_t>(thr_t) : 0.f;
   constexpr int kU = 4;
   for (long long base = i0; base < total; base += kU * stride) {
-    long long tv[kU];
+    target_t tv[kU];
     scalar_t pv[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const long long i = base + u * stride;
       if (i < total) {
-        tv[u] = static_cast<long long>(target[i]);
+        tv[u] = target[i];
         pv[u] = preds[i];
       }
     }
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const long long i = base + u * stride;
-      if (i >= total) break;
-      const bool ignored = has_ignore && tv[u] == ignore;
-      if constexpr (IsFloating<scalar_t>::value) {
-        const float v = to_f32(pv[u]);
-        if (!(v >= 0.f && v <= 1.f) && (prob_check_all || !ignored)) local_not_prob = 1;
-      }
-      if (ignored) continue;
-      if (tv[u] != 0 && tv[u] != 1) {
-        raise_flag(flag, kErrTargetNotBinary);
-        continue;
-      }
-      bool pa, pb, valid;
-      bin_pred<scalar_t>(pv[u], thr_t, cut, flag, pa, pb, valid);
-      if (!valid) continue;
-      const bool t = tv[u] == 1;
-      c[0] += t & pa;
-      c[1] += !t & pa;
-      c[2] += t & !pa;
-      c[3] += t & pb;
-      c[4] += !t & pb;
-      c[5] += t & !pb;
-      c[6] += 1;
-    }
+    for (int u = 0; u < kU; ++u)
+      if (base + u * stride < total) bin_step(acc, pv[u], tv[u], thr_t, cut, ignore, has_ignore, prob_check_all);
   }
-  if (IsFloating<scalar_t>::value) {
-    if (__any(local_not_prob) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(not_prob, 1);
-  }
+  bin_raise(acc, flag, IsFloating<scalar_t>::value ? not_prob : nullptr);
+  int c[kBinSlots];
+  bin_to_slots(acc, c);
   if (L * X == 1) {  // one label in the whole grid: reduce across the wave first
 #pragma unroll
     for (int k = 0; k < kBinSlots; ++k) {
@@ -1469,10 +1488,7 @@ __global__ void __launch_bounds__(kFoldThreads) bin_partials_finalize_kernel(
 #pragma unroll
       for (int k = 0; k < kBinSlots; ++k) acc[k] += base[static_cast<long long>(r) * nbins + k];
   }
-#pragma unroll
-  for (int k = 0; k < kBinSlots; ++k)
-#pragma unroll
-    for (int off = kWave / 2; off >= LB; off >>= 1) acc[k] += __shfl_xor(acc[k], off, kWave);
+  wave_colsum64(acc, LB);  // lanes of one label: DPP / permlane (VALU), not 7 x 6 x 2 ds_bpermutes
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   if (lane < LB)
 #pragma unroll

@@ -125,63 +125,78 @@ __device__ __forceinline__ long long wave_sum_ll(long long v) { return __ockl_wf
 // wave): row_ror DPP moves for offsets 1..8, the gfx950 permlane16 / permlane32 swaps for 16 / 32 -- no LDS.  Every
 // lane ends with its residue class's sum (so lane c < k holds column c).  ds_bpermute shuffles cost the LDS pipe
 // ~8 clk each: 19 sums x 6 offsets x 2 halves x 8 waves of them were ~6 us of a 512-thread moments launch.
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double x) {
-  const long long b = __double_as_longlong(x);
-  const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(b), CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(b >> 32), CTRL, 0xf, 0xf, false);
-  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+template <typename T>
+__device__ __forceinline__ long long bits64(T x) {
+  static_assert(sizeof(T) == 8, "64-bit values");
+  return __builtin_bit_cast(long long, x);
 }
 
-__device__ __forceinline__ double join_f64(unsigned lo, unsigned hi) {
-  return __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+template <int CTRL, typename T>
+__device__ __forceinline__ T dpp64(T x) {
+  const long long b = bits64(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(b), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(b >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(T, (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+
+template <typename T>
+__device__ __forceinline__ T join64(unsigned lo, unsigned hi) {
+  return __builtin_bit_cast(T, static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
 }
 
 // x[lane] + x[lane ^ 16] (the same sum, in the same order, in both lanes)
-__device__ __forceinline__ double xor16_sum_f64(double x) {
-  const long long b = __double_as_longlong(x);
+template <typename T>
+__device__ __forceinline__ T xor16_sum64(T x) {
+  const long long b = bits64(x);
   const unsigned lo = static_cast<unsigned>(b), hi = static_cast<unsigned>(b >> 32);
   const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // [0]: even rows' values, [1]: odd rows'
   const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-  return join_f64(l[0], h[0]) + join_f64(l[1], h[1]);
+  return join64<T>(l[0], h[0]) + join64<T>(l[1], h[1]);
 }
 
 // x[lane] + x[lane ^ 32]
-__device__ __forceinline__ double xor32_sum_f64(double x) {
-  const long long b = __double_as_longlong(x);
+template <typename T>
+__device__ __forceinline__ T xor32_sum64(T x) {
+  const long long b = bits64(x);
   const unsigned lo = static_cast<unsigned>(b), hi = static_cast<unsigned>(b >> 32);
   const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);  // [0]: lanes 0-31's values, [1]: 32-63's
   const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-  return join_f64(l[0], h[0]) + join_f64(l[1], h[1]);
+  return join64<T>(l[0], h[0]) + join64<T>(l[1], h[1]);
+}
+
+// T = double or long long; call with every lane of the wave active
+template <typename T, int NS>
+__device__ __forceinline__ void wave_colsum64(T (&v)[NS], int k) {
+  // offsets below k would mix columns; the branches are uniform (and fold away for a constant k)
+  if (k <= 1) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) v[s] += dpp64<0x121>(v[s]);  // row_ror:1
+  }
+  if (k <= 2) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) v[s] += dpp64<0x122>(v[s]);  // row_ror:2
+  }
+  if (k <= 4) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) v[s] += dpp64<0x124>(v[s]);  // row_ror:4
+  }
+  if (k <= 8) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) v[s] += dpp64<0x128>(v[s]);  // row_ror:8
+  }
+  if (k <= 16) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) v[s] = xor16_sum64(v[s]);
+  }
+  if (k <= 32) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) v[s] = xor32_sum64(v[s]);
+  }
 }
 
 template <int NS>
 __device__ __forceinline__ void wave_colsum_f64(double (&v)[NS], int k) {
-  // offsets below k would mix columns; the branches are uniform
-  if (k <= 1) {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) v[s] += dpp_f64<0x121>(v[s]);  // row_ror:1
-  }
-  if (k <= 2) {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) v[s] += dpp_f64<0x122>(v[s]);  // row_ror:2
-  }
-  if (k <= 4) {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) v[s] += dpp_f64<0x124>(v[s]);  // row_ror:4
-  }
-  if (k <= 8) {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) v[s] += dpp_f64<0x128>(v[s]);  // row_ror:8
-  }
-  if (k <= 16) {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) v[s] = xor16_sum_f64(v[s]);
-  }
-  if (k <= 32) {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) v[s] = xor32_sum_f64(v[s]);
-  }
+  wave_colsum64(v, k);
 }
 
 // argmax combine with torch.argmax semantics: NaN wins, then larger value, then smaller index

@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(kThreads) calib_bins_kernel(const float* __res
       if (bs[mid] <= x) lo = mid + 1;
       else hi = mid;
     }
-    const int b = lo - 1;
+    const int b = x != x ? nb - 1 : lo - 1;  // NaN: past every bound, as torch.bucketize(right=True) sorts it
     if (b < 0) {  // below the first boundary: index -1, which index_add rejects in the reference
       oob = true;
       continue;
@@ -84,6 +84,7 @@ __global__ void __launch_bounds__(kThreads) calib_bins_private_kernel(const floa
     const float x = conf[e];
     int b = -1;
     for (int k = 0; k < nb; ++k) b += (bs[k] <= x) ? 1 : 0;  // #{bounds <= x} - 1 (ascending bounds)
+    if (x != x) b = nb - 1;  // NaN: torch.bucketize(right=True) sorts it past every bound (the reference's last bin)
     if (b < 0) {
       oob = true;
       continue;

@@ -25,6 +25,8 @@
 // the whole classification group, whatever the number of members.
 #include "common/tm_common.h"
 
+#include <utility>
+
 namespace tm_amd {
 namespace {
 
@@ -161,6 +163,7 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_kernel(const scalar_t
       for (int var = 0; var < 2; ++var) {
         int b = -1;
         for (int k = 0; k < nb; ++k) b += (bnd_s[k] <= cv[var]) ? 1 : 0;
+        if (cv[var] != cv[var]) b = nb - 1;  // NaN: past every bound (torch.bucketize), the reference's last bin
         if (b < 0) continue;
         float* dst = hf + sp.off_cb + (var * nb + b) * 3;
         atomicAdd(dst, 1.f);
@@ -178,6 +181,67 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_kernel(const scalar_t
   for (int i = sp.off_cb + threadIdx.x; i < sp.part_words; i += kFamThreads)
     if (hf[i] != 0.f) atomicAdd(reinterpret_cast<float*>(sp.img) + i, hf[i]);
   if (threadIdx.x == 0 && blk_outside) atomicOr(&sp.outside[sp.slot], 1);
+}
+
+// ---- VALU (DPP) group exchanges for G <= 16 lanes per row: a row group never straddles a 16-lane DPP row.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __int_as_float(dpp_i32<CTRL>(__float_as_int(x)));
+}
+
+// a butterfly partner at distance 1, 2, 4, 8 once the smaller distances are reduced: quad_perm [1,0,3,2] / [2,3,0,1],
+// then row_half_mirror / row_mirror (they pair the already-uniform halves)
+template <int STEP>
+constexpr int kGroupXor = STEP == 1 ? 0xB1 : STEP == 2 ? 0x4E : STEP == 4 ? 0x141 : 0x140;
+
+template <int G, int STEP = 1>
+__device__ __forceinline__ void group_max_argmax(float& mf, float& mx, int& mi) {
+  if constexpr (STEP < G) {
+    mf = fmaxf(mf, dpp_f32<kGroupXor<STEP>>(mf));
+    const float ov = dpp_f32<kGroupXor<STEP>>(mx);
+    const int oi = dpp_i32<kGroupXor<STEP>>(mi);
+    if (argmax_better(ov, oi, mx, mi)) mx = ov, mi = oi;
+    group_max_argmax<G, STEP * 2>(mf, mx, mi);
+  }
+}
+
+template <int G, int STEP = 1>
+__device__ __forceinline__ void group_argmax(float& v, int& i) {
+  if constexpr (STEP < G) {
+    const float ov = dpp_f32<kGroupXor<STEP>>(v);
+    const int oi = dpp_i32<kGroupXor<STEP>>(i);
+    if (argmax_better(ov, oi, v, i)) v = ov, i = oi;
+    group_argmax<G, STEP * 2>(v, i);
+  }
+}
+
+// lane K of this lane's G-group, broadcast (row_newbcast: lane n of each 16-lane row; quad_perm inside quads)
+template <int G, int K>
+__device__ __forceinline__ float group_bcast(float x) {
+  if constexpr (G == 16) {
+    return dpp_f32<0x150 + K>(x);
+  } else if constexpr (G == 8) {
+    const float a = dpp_f32<0x150 + K>(x), b = dpp_f32<0x158 + K>(x);
+    return (threadIdx.x & 8) ? b : a;
+  } else if constexpr (G == 4) {
+    return dpp_f32<K | (K << 2) | (K << 4) | (K << 6)>(x);
+  } else {
+    static_assert(G == 2, "G <= 16");
+    return dpp_f32<K | (K << 2) | ((2 + K) << 4) | ((2 + K) << 6)>(x);
+  }
+}
+
+// sum of the group's lanes 0 .. C-1 in class order (the reference's softmax denominator order): bit-identical to the
+// serial loop over __shfl broadcasts
+template <int G, int... Ks>
+__device__ __forceinline__ float class_order_sum(float e, int C, std::integer_sequence<int, Ks...>) {
+  float s = 0.f;
+  ((Ks < C ? (s += group_bcast<G, Ks>(e), 0) : 0), ...);
+  return s;
 }
 
 // The same image, G lanes per row (G = the power of two >= C, <= 64): lane c of a row's group owns class c, so the
@@ -238,26 +302,37 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar
     float mf = mine ? v : -INFINITY;  // NaN-ignoring max (fmaxf drops NaN)
     float mx = v;
     int mi = mine ? c : 0x7fffffff;
+    if constexpr (G <= 16) {
+      group_max_argmax<G>(mf, mx, mi);  // DPP (VALU): a ds_bpermute butterfly was ~100 cycles per dependent step
+    } else {
 #pragma unroll
-    for (int off = G / 2; off > 0; off >>= 1) {
-      mf = fmaxf(mf, __shfl_xor(mf, off, kWave));
-      const float ov = __shfl_xor(mx, off, kWave);
-      const int oi = __shfl_xor(mi, off, kWave);
-      if (argmax_better(ov, oi, mx, mi)) mx = ov, mi = oi;
+      for (int off = G / 2; off > 0; off >>= 1) {
+        mf = fmaxf(mf, __shfl_xor(mf, off, kWave));
+        const float ov = __shfl_xor(mx, off, kWave);
+        const int oi = __shfl_xor(mi, off, kWave);
+        if (argmax_better(ov, oi, mx, mi)) mx = ov, mi = oi;
+      }
     }
     // softmax denominators in class order (every lane gets the same sums)
+    auto order_sum = [&](float e) {
+      if constexpr (G <= 16) {
+        return class_order_sum<G>(e, C, std::make_integer_sequence<int, G>{});
+      } else {
+        float t = 0.f;
+        for (int k = 0; k < C; ++k) t += __shfl(e, gbase + k, kWave);
+        return t;
+      }
+    };
     const float e_cal = mine ? expf(v - mx) : 0.f;
     float s_cal = 0.f;
     if (sp.abl & 8) s_cal = 1.f;
-    else
-      for (int k = 0; k < C; ++k) s_cal += __shfl(e_cal, gbase + k, kWave);
+    else s_cal = order_sum(e_cal);
     float s_cur = s_cal;
     const bool nan_row = !(mf == mx);  // a NaN in the row: the two shifts differ (uniform within the group)
     float e_cur = e_cal;
     if (__any(nan_row)) {
       e_cur = mine ? expf(v - mf) : 0.f;
-      float t2 = 0.f;
-      for (int k = 0; k < C; ++k) t2 += __shfl(e_cur, gbase + k, kWave);
+      const float t2 = order_sum(e_cur);
       if (nan_row) s_cur = t2;
       else e_cur = e_cal;
     }
@@ -287,11 +362,15 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar
     if (nb > 0 && !(sp.abl & 2)) {
       float sv = mine ? round_to<scalar_t>(e_cal / s_cal) : -INFINITY;
       int si = mine ? c : 0x7fffffff;
+      if constexpr (G <= 16) {
+        group_argmax<G>(sv, si);
+      } else {
 #pragma unroll
-      for (int off = G / 2; off > 0; off >>= 1) {
-        const float ov = __shfl_xor(sv, off, kWave);
-        const int oi = __shfl_xor(si, off, kWave);
-        if (argmax_better(ov, oi, sv, si)) sv = ov, si = oi;
+        for (int off = G / 2; off > 0; off >>= 1) {
+          const float ov = __shfl_xor(sv, off, kWave);
+          const int oi = __shfl_xor(si, off, kWave);
+          if (argmax_better(ov, oi, sv, si)) sv = ov, si = oi;
+        }
       }
       if (live && c < 2) {  // lane 0: the raw top-1 variant, lane 1: the softmax variant
         const float ar = mi == tv ? 1.f : 0.f, as = si == tv ? 1.f : 0.f;
@@ -300,6 +379,7 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar
         const float avv = c == 0 ? ar : as;
         int b = -1;
         for (int k = 0; k < nb; ++k) b += (bnd_s[k] <= cvv) ? 1 : 0;
+        if (cvv != cvv) b = nb - 1;  // NaN: past every bound (torch.bucketize), the reference's last bin
         if (b >= 0) {
           float* dst = hf + sp.off_cb + (c * nb + b) * 3;
           atomicAdd(dst, 1.f);

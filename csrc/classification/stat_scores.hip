@@ -1018,12 +1018,18 @@ struct BinAcc {
   int not_prob = 0, bad_t = 0, bad_p = 0;
 };
 
-template <typename scalar_t, typename target_t>
+// kIgn: an ignore_index is set (else the compare is compiled out); kProb: check "probabilities" per element here (the
+// vector kernel instead tracks a packed ordinal range, see OrdRange)
+template <bool kIgn = true, bool kProb = true, typename scalar_t, typename target_t>
 __device__ __forceinline__ void bin_step(BinAcc& c, scalar_t raw, target_t traw, float thr_t, float cut,
                                          long long ignore, bool has_ignore, bool prob_check_all) {
   const long long tv = static_cast<long long>(traw);
-  const bool ignored = has_ignore && tv == ignore;
-  const bool tbin = static_cast<unsigned long long>(tv) <= 1ull;
+  const bool ignored = kIgn && has_ignore && tv == ignore;
+  bool tbin;
+  if constexpr (sizeof(target_t) <= 4)
+    tbin = static_cast<uint32_t>(static_cast<int32_t>(traw)) <= 1u;  // 32-bit compare for narrow targets
+  else
+    tbin = static_cast<unsigned long long>(tv) <= 1ull;
   c.bad_t |= !ignored && !tbin;
   bool pa, pb, pvalid;
   if constexpr (IsFloating<scalar_t>::value) {
@@ -1031,7 +1037,7 @@ __device__ __forceinline__ void bin_step(BinAcc& c, scalar_t raw, target_t traw,
     pa = v > thr_t;
     pb = v >= cut;
     pvalid = true;
-    c.not_prob |= !(v >= 0.f && v <= 1.f) && (prob_check_all || !ignored);
+    if constexpr (kProb) c.not_prob |= !(v >= 0.f && v <= 1.f) && (prob_check_all || !ignored);
   } else {
     const long long pv = static_cast<long long>(raw);
     pvalid = static_cast<unsigned long long>(pv) <= 1ull;
@@ -1039,7 +1045,11 @@ __device__ __forceinline__ void bin_step(BinAcc& c, scalar_t raw, target_t traw,
     pa = pb = pv == 1;
   }
   const int valid = !ignored && tbin && pvalid;
-  const int t = valid & (tv == 1);
+  int t;
+  if constexpr (sizeof(target_t) <= 4)
+    t = valid & (static_cast<int32_t>(traw) == 1);
+  else
+    t = valid & (tv == 1);
   const int ia = valid & pa, ib = valid & pb;
   c.a += t & ia;
   c.p += ia;
@@ -1209,6 +1219,51 @@ void launch_partials_fold(const int* part, int nrows, int nbins, int64_t* ws, hi
 // row of `partials`, which partials_fold_kernel folds into the workspace.
 constexpr int kVecBlock = 512;
 
+// "Are all scores in [0, 1]?" over whole 16-byte vectors: the order-preserving ordinal of each value (sign-magnitude
+// float bits u -> u ^ ((u >>a msb) | msb), NaNs land beyond +-inf) folded into a running min / max (packed 16-bit
+// min / max for bf16 / fp16: 2 values per instruction).  In range iff min >= ord(-0) and max <= ord(1).  Replaces
+// four compares / selects per element when every position counts (no ignore_index, or prob_check_all).
+template <typename scalar_t>
+struct OrdRange;
+template <>
+struct OrdRange<float> {
+  uint32_t lo = 0xffffffffu, hi = 0u;
+  __device__ __forceinline__ void add(const u32x4& v) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t w = v[k];
+      const uint32_t o = w ^ (static_cast<uint32_t>(static_cast<int32_t>(w) >> 31) | 0x80000000u);
+      lo = o < lo ? o : lo;
+      hi = o > hi ? o : hi;
+    }
+  }
+  __device__ __forceinline__ bool ok() const { return lo >= 0x7fffffffu && hi <= 0xbf800000u; }
+};
+template <typename scalar_t>
+struct OrdRange16 {
+  u16x2 lo = {0xffff, 0xffff}, hi = {0, 0};
+  __device__ __forceinline__ void add(const u32x4& v) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t w = v[k];
+      const s16x2 sw = __builtin_bit_cast(s16x2, w);
+      const uint32_t sgn = __builtin_bit_cast(uint32_t, static_cast<s16x2>(sw >> (s16x2){15, 15}));
+      const u16x2 o = __builtin_bit_cast(u16x2, w ^ (sgn | 0x80008000u));
+      lo = __builtin_elementwise_min(lo, o);
+      hi = __builtin_elementwise_max(hi, o);
+    }
+  }
+  __device__ __forceinline__ bool ok() const {
+    constexpr uint32_t one = std::is_same<scalar_t, c10::BFloat16>::value ? 0xbf80u : 0xbc00u;  // ord(1.0)
+    const uint32_t l = lo.x < lo.y ? lo.x : lo.y, h = hi.x > hi.y ? hi.x : hi.y;
+    return l >= 0x7fffu && h <= one;
+  }
+};
+template <>
+struct OrdRange<c10::BFloat16> : OrdRange16<c10::BFloat16> {};
+template <>
+struct OrdRange<c10::Half> : OrdRange16<c10::Half> {};
+
 template <typename scalar_t, typename target_t, int VEC>
 __global__ void __launch_bounds__(kVecBlock) bin_vec_kernel(const scalar_t* __restrict__ preds,
                                                             const target_t* __restrict__ target, long long nvec,
@@ -1229,26 +1284,38 @@ __global__ void __launch_bounds__(kVecBlock) bin_vec_kernel(const scalar_t* __re
   const u32x4* pv = reinterpret_cast<const u32x4*>(preds);
   const u32x4* tvp = reinterpret_cast<const u32x4*>(target);
   constexpr int kU = 4;
-  for (long long base = v0; base < nvec; base += kU * S) {
-    u32x4 praw[kU];
-    u32x4 traw[kU][kTChunks];
+  OrdRange<scalar_t> range;
+  auto walk = [&](auto ign) {  // ign: std::integral_constant<bool, has_ignore> (wave-uniform, two instantiations)
+    constexpr bool kIgn = decltype(ign)::value;
+    for (long long base = v0; base < nvec; base += kU * S) {
+      u32x4 praw[kU];
+      u32x4 traw[kU][kTChunks];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const long long v = base + u * S;
-      if (v < nvec) {
-        praw[u] = __builtin_nontemporal_load(pv + v);
+      for (int u = 0; u < kU; ++u) {
+        const long long v = base + u * S;
+        if (v < nvec) {
+          praw[u] = __builtin_nontemporal_load(pv + v);
 #pragma unroll
-        for (int j = 0; j < kTChunks; ++j) traw[u][j] = __builtin_nontemporal_load(tvp + v * kTChunks + j);
+          for (int j = 0; j < kTChunks; ++j) traw[u][j] = __builtin_nontemporal_load(tvp + v * kTChunks + j);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (base + u * S >= nvec) break;
+        const scalar_t* pe = reinterpret_cast<const scalar_t*>(&praw[u]);
+        const target_t* te = reinterpret_cast<const target_t*>(&traw[u][0]);
+        if constexpr (!kIgn) range.add(praw[u]);  // every position counts for the probability check
+#pragma unroll
+        for (int e = 0; e < VEC; ++e)
+          bin_step<kIgn, kIgn>(c[e], pe[e], te[e], thr_t, cut, ignore, has_ignore, prob_check_all);
       }
     }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      if (base + u * S >= nvec) break;
-      const scalar_t* pe = reinterpret_cast<const scalar_t*>(&praw[u]);
-      const target_t* te = reinterpret_cast<const target_t*>(&traw[u][0]);
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) bin_step(c[e], pe[e], te[e], thr_t, cut, ignore, has_ignore, prob_check_all);
-    }
+  };
+  if (has_ignore) {
+    walk(std::true_type{});
+  } else {
+    walk(std::false_type{});
+    c[0].not_prob |= !range.ok();
   }
   BinAcc any;
 #pragma unroll
@@ -2001,7 +2068,7 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
                                                              cu_count(preds.get_device())));
         const long long nbins = L * kBinSlots;
         at::Tensor partials = at::empty({static_cast<long long>(grid) * nbins}, ws.options().dtype(at::kInt));
-        if constexpr (VEC * sizeof(scalar_t) == 16) {
+        if constexpr (VEC * sizeof(scalar_t) == 16 && IsFloating<scalar_t>::value && sizeof(scalar_t) <= 4) {
           hipLaunchKernelGGL((bin_vec_kernel<scalar_t, target_t, VEC>), dim3(grid), dim3(kVecBlock),
                              nbins * sizeof(int), s, pp, tp, total / VEC, static_cast<int>(L), thr_t, ignore_index,
                              has_ignore, flag.data_ptr<int>(), npw, prob_check_all,

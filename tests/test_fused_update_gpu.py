@@ -108,3 +108,33 @@ def test_fused_update_falls_back_off_path():
     g.update(p.to(DEV), t.to(DEV))
     c.update(p, t)
     _check(g.compute(), c.compute())
+
+
+@pytest.mark.parametrize("nc", [2, 3, 5, 8, 13, 16, 17, 33])
+@pytest.mark.parametrize("nan_rows", [False, True])
+def test_fused_update_group_widths(nc, nan_rows):
+    """family_rows_g_kernel's group exchanges: DPP butterflies / row broadcasts for G <= 16 lanes per row (G = 2, 4,
+    8, 16), ds_bpermute shuffles above (32, 64) -- every class count against the CPU collection, with NaN rows (the
+    NaN-ignoring max differs from the argmax max there)."""
+    g, c = _cls(nc=nc).to(DEV), _cls(nc=nc)
+    for i, n in enumerate([4096, 333]):
+        p, t = _batch(40 + i, n, nc=nc)
+        if nan_rows:
+            p[::97, nc // 2] = float("nan")
+        g.update(p.to(DEV), t.to(DEV))
+        c.update(p, t)
+    _check(g.compute(), c.compute())
+    assert _plan(g) is not None and _plan(g).calls >= 1
+
+
+@pytest.mark.parametrize("n_bins", [15, 40])
+def test_calibration_error_nan_rows_standalone(n_bins):
+    """NaN confidences land in the last bin, where torch.bucketize(right=True) puts them in the reference
+    (calib_bins_private_kernel for <= 16 bounds, calib_bins_kernel above)."""
+    g_m, c_m = C.MulticlassCalibrationError(5, n_bins=n_bins).to(DEV), C.MulticlassCalibrationError(5, n_bins=n_bins)
+    for i in range(2):
+        p, t = _batch(70 + i, 2000, nc=5)
+        p[::13, 2] = float("nan")
+        g_m.update(p.to(DEV), t.to(DEV))
+        c_m.update(p, t)
+    torch.testing.assert_close(g_m.compute().cpu(), c_m.compute(), atol=1e-5, rtol=1e-5, equal_nan=True)

@@ -144,3 +144,26 @@ def test_multilabel_module_values_on_vec_path():
     ref = tm.MultilabelF1Score(L)
     ref.update(p, t)
     torch.testing.assert_close(m.compute().cpu(), ref.compute())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("odd", ["none", "neg_zero", "one", "above_one", "tiny_negative", "nan", "neg_nan", "inf"])
+def test_multilabel_vec_probability_range_edges(dtype, odd):
+    """bin_vec_kernel decides "all scores in [0, 1]" from a packed ordinal min / max (OrdRange): -0.0 and 1.0 are in
+    range; anything above 1, below -0.0, NaN of either sign or inf is not -- the same reading as the CPU path."""
+    N, L = 2048, 128
+    g = torch.Generator().manual_seed(17)
+    preds = torch.rand(N, L, generator=g).to(dtype)
+    target = torch.randint(0, 2, (N, L), generator=g)
+    val = {"none": None, "neg_zero": -0.0, "one": 1.0, "above_one": 1.0078125, "tiny_negative": -1e-3,
+           "nan": float("nan"), "neg_nan": -float("nan"), "inf": float("inf")}[odd]
+    if val is not None:
+        preds[N // 2, L // 3] = val
+        if odd == "neg_nan":
+            bits = preds.view(torch.int16 if dtype != torch.float32 else torch.int32)
+            bits[N // 2, L // 3] |= (-32768 if dtype != torch.float32 else -(2 ** 31))
+    gg = _bin(preds, target, L, None, DEV)
+    cc = _bin(preds, target, L, None, "cpu")
+    assert gg[2] == cc[2]  # the probabilities / logits decision
+    if odd not in ("nan", "neg_nan"):
+        assert torch.equal(gg[0], cc[0])

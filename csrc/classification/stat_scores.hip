@@ -254,9 +254,11 @@ __global__ void __launch_bounds__(kOrdBlock) mc_argmax_ord16_kernel(const scalar
                                                                  long long tn_all = 0) {
   static_assert(sizeof(scalar_t) == 2, "16-bit floats only");
   if constexpr (kMode == kMcStatsDirect) {
-    // every class gains a true negative per row of the batch; the rows' own classes give theirs back below
-    if (blockIdx.x == 0)
-      for (int c = threadIdx.x; c < C; c += blockDim.x) atomic_add_i64(tn_st + c, tn_all);
+    // every class gains a true negative per row of the batch; the rows' own classes give theirs back below (spread
+    // over the grid's first threads: one add each, no block starts its rows behind C / 512 rounds of them)
+    for (long long c = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; c < C;
+         c += static_cast<long long>(gridDim.x) * blockDim.x)
+      atomic_add_i64(tn_st + c, tn_all);
   }
   const int lane = threadIdx.x & (kWave - 1);
   const long long nwaves = static_cast<long long>(gridDim.x) * (blockDim.x / kWave);

@@ -1821,7 +1821,12 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
               if constexpr (sizeof(scalar_t) == 2) {
                 if (!ord16_off) {
                   const long long want16 = (N + kOrdBlock / kWave - 1) / (kOrdBlock / kWave);  // one row per wave
-                  const int grid16 = static_cast<int>(std::min<long long>(want16, static_cast<long long>(cus) * 4));
+                  static const int per_cu = [] {  // blocks per CU (TM_AMD_ORD16_BLOCKS_PER_CU: measurement knob)
+                    const char* e = std::getenv("TM_AMD_ORD16_BLOCKS_PER_CU");
+                    return e ? std::max(1, std::atoi(e)) : 4;
+                  }();
+                  const int grid16 =
+                      static_cast<int>(std::min<long long>(want16, static_cast<long long>(cus) * per_cu));
                   if (mode == kMcConfmat)
                     hipLaunchKernelGGL((mc_argmax_ord16_kernel<scalar_t, target_t, P, kMcConfmat>), dim3(grid16),
                                        dim3(kOrdBlock), 0, s, pp, tp, N, C, ignore_index, has_ignore, outp, flagp);

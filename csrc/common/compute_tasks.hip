@@ -44,8 +44,12 @@ __global__ void __launch_bounds__(cbody::kThreads) compute_tasks_kernel(TaskTabl
   extern __shared__ double dyn[];
   __shared__ double red[cbody::kThreads / kWave];
   const int b = blockIdx.x;
-  int ti = 0;
-  while (ti + 1 < tab.n && tab.first[ti + 1] <= b) ++ti;
+  // the block's task: every lane loads one block prefix (one round trip), a ballot counts the tasks starting at or
+  // before this block.  (A serial scan of the prefixes was up to n dependent kernel-argument loads, ~0.3-1 us each
+  // from a kernel-argument buffer the host has just written: 1.7-12 us per launch in config #5's traces.)
+  const int lane = threadIdx.x & (kWave - 1);
+  const bool starts = lane < tab.n && tab.first[lane] <= b;
+  const int ti = __builtin_amdgcn_readfirstlane(__popcll(__ballot(starts)) - 1);
   const Task& t = tab.t[ti];
   const int local = b - tab.first[ti];
   switch (t.type) {

@@ -1271,7 +1271,8 @@ __global__ void __launch_bounds__(kVecBlock) bin_vec_kernel(const scalar_t* __re
                                                             const target_t* __restrict__ target, long long nvec,
                                                             int L, float thr_t, long long ignore, bool has_ignore,
                                                             int* __restrict__ flag, int* __restrict__ not_prob,
-                                                            bool prob_check_all, int* __restrict__ partials) {
+                                                            bool prob_check_all, int* __restrict__ partials,
+                                                            int64_t* __restrict__ ws) {
   static_assert(VEC * sizeof(scalar_t) == 16, "one 16-byte vector of preds per step");
   constexpr int kTChunks = (VEC * sizeof(target_t) + 15) / 16;  // 16-byte chunks of the matching targets
   extern __shared__ __attribute__((aligned(16))) int lds[];
@@ -1335,6 +1336,13 @@ __global__ void __launch_bounds__(kVecBlock) bin_vec_kernel(const scalar_t* __re
       if (sl[k]) atomicAdd(&lds[(l0 + e) * kBinSlots + k], sl[k]);
   }
   __syncthreads();
+  if (partials == nullptr) {  // TM_AMD_BIN_VEC_ATOMIC: each block adds its histogram straight into ws (no fold launch)
+    for (int b = threadIdx.x; b < nbins; b += kVecBlock) {
+      const int v = lds[b];
+      if (v) atomic_add_i64(ws + b, v);
+    }
+    return;
+  }
   int* row = partials + static_cast<long long>(blockIdx.x) * nbins;
   for (int b = threadIdx.x; b < nbins; b += kVecBlock) row[b] = lds[b];
 }
@@ -2074,14 +2082,21 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
         const int grid = static_cast<int>(vec_grid<scalar_t>(preds, target, L, X, samplewise, total,
                                                              cu_count(preds.get_device())));
         const long long nbins = L * kBinSlots;
-        at::Tensor partials = at::empty({static_cast<long long>(grid) * nbins}, ws.options().dtype(at::kInt));
+        // measurement knob, off by default: block histograms by int64 atomics into ws (no fold launch) measured
+        // 19.1 vs 19.2 us for MultilabelAccuracy(100) and 39.1 vs 33.2 us for MultilabelF1Score(1000)
+        static const bool atomic_flush = [] {
+          const char* e = std::getenv("TM_AMD_BIN_VEC_ATOMIC");
+          return e && std::atoi(e) != 0;
+        }();
+        at::Tensor partials;
+        if (!atomic_flush) partials = at::empty({static_cast<long long>(grid) * nbins}, ws.options().dtype(at::kInt));
         if constexpr (VEC * sizeof(scalar_t) == 16 && IsFloating<scalar_t>::value && sizeof(scalar_t) <= 4) {
           hipLaunchKernelGGL((bin_vec_kernel<scalar_t, target_t, VEC>), dim3(grid), dim3(kVecBlock),
                              nbins * sizeof(int), s, pp, tp, total / VEC, static_cast<int>(L), thr_t, ignore_index,
                              has_ignore, flag.data_ptr<int>(), npw, prob_check_all,
-                             partials.data_ptr<int>());
+                             atomic_flush ? nullptr : partials.data_ptr<int>(), ws.data_ptr<int64_t>());
         }
-        defer_fold(ws, partials, grid, static_cast<int>(nbins), s);
+        if (!atomic_flush) defer_fold(ws, partials, grid, static_cast<int>(nbins), s);
       } else if (!samplewise && reg_grid(L * X, total) > 0 && L * kBinSlots <= kLdsBins) {
         // grid stride a multiple of L * X: a fixed label per thread (register counters)
         const long long grid = reg_grid(L * X, total);

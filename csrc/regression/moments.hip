@@ -691,7 +691,11 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
   if (handoff_min > 0 && n_rows * k >= handoff_min && kWave % k == 0 && n_rows * k <= kSmallMax) {
     // per-batch sizes of the streaming metrics (config #5: 8192 pairs): G blocks, the last one folds (no fence)
     const long long total = n_rows * k;
-    long long g = (total + kHandoffRows - 1) / kHandoffRows;
+    static const long long per_block = [] {  // values per block (TM_AMD_MOMENTS_ROWS: measurement knob)
+      const char* e = std::getenv("TM_AMD_MOMENTS_ROWS");
+      return e ? std::max(64LL, std::atoll(e)) : static_cast<long long>(kHandoffRows);
+    }();
+    long long g = (total + per_block - 1) / per_block;
     g = std::min<long long>(g, std::min<long long>(128, kHandoffMaxRows / k));
     const int G = static_cast<int>(std::max<long long>(1, g));
     unsigned int* ticket = stream_ticket(preds.get_device(), s);

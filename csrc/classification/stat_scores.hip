@@ -1266,7 +1266,7 @@ struct OrdRange<c10::BFloat16> : OrdRange16<c10::BFloat16> {};
 template <>
 struct OrdRange<c10::Half> : OrdRange16<c10::Half> {};
 
-template <typename scalar_t, typename target_t, int VEC>
+template <typename scalar_t, typename target_t, int VEC, int kU = 4>
 __global__ void __launch_bounds__(kVecBlock) bin_vec_kernel(const scalar_t* __restrict__ preds,
                                                             const target_t* __restrict__ target, long long nvec,
                                                             int L, float thr_t, long long ignore, bool has_ignore,
@@ -1286,7 +1286,6 @@ __global__ void __launch_bounds__(kVecBlock) bin_vec_kernel(const scalar_t* __re
   const float cut = sigmoid_cut<scalar_t>(thr_t);
   const u32x4* pv = reinterpret_cast<const u32x4*>(preds);
   const u32x4* tvp = reinterpret_cast<const u32x4*>(target);
-  constexpr int kU = 4;
   OrdRange<scalar_t> range;
   auto walk = [&](auto ign) {  // ign: std::integral_constant<bool, has_ignore> (wave-uniform, two instantiations)
     constexpr bool kIgn = decltype(ign)::value;
@@ -2091,7 +2090,15 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
         at::Tensor partials;
         if (!atomic_flush) partials = at::empty({static_cast<long long>(grid) * nbins}, ws.options().dtype(at::kInt));
         if constexpr (VEC * sizeof(scalar_t) == 16 && IsFloating<scalar_t>::value && sizeof(scalar_t) <= 4) {
-          hipLaunchKernelGGL((bin_vec_kernel<scalar_t, target_t, VEC>), dim3(grid), dim3(kVecBlock),
+          // vectors in flight per thread (TM_AMD_BIN_VEC_U: 4 or 8, measurement knob; 8 measured 19.5-19.6 vs
+          // 19.3-19.5 us at MultilabelAccuracy(100), 33.9-34.0 vs 33.3 us at MultilabelF1Score(1000): 4 stays)
+          static const int unroll = [] {
+            const char* e = std::getenv("TM_AMD_BIN_VEC_U");
+            return e && std::atoi(e) == 8 ? 8 : 4;
+          }();
+          auto vec_kernel = unroll == 8 ? bin_vec_kernel<scalar_t, target_t, VEC, 8>
+                                        : bin_vec_kernel<scalar_t, target_t, VEC, 4>;
+          hipLaunchKernelGGL(vec_kernel, dim3(grid), dim3(kVecBlock),
                              nbins * sizeof(int), s, pp, tp, total / VEC, static_cast<int>(L), thr_t, ignore_index,
                              has_ignore, flag.data_ptr<int>(), npw, prob_check_all,
                              atomic_flush ? nullptr : partials.data_ptr<int>(), ws.data_ptr<int64_t>());

@@ -716,7 +716,7 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
     return e ? (std::atoi(e) & 7) : 0;
   }();
   if (kWave % k == 0 && n_rows * k <= kSmallMax) {
-    // small per-batch sizes (below the hand-off threshold, or k not a power of two): ONE 512-thread block, one launch
+    // small per-batch sizes (below the hand-off threshold above): ONE 512-thread block, one launch
     const size_t lds = static_cast<size_t>(kSmallThreads / kWave + 1) * k * kMaxSums * sizeof(double);
     TM_DISPATCH_FLOAT(preds.scalar_type(), "moments_update", [&] {
       hipLaunchKernelGGL((moments_small_kernel<scalar_t>), dim3(1), dim3(kSmallThreads), lds, s,

@@ -592,7 +592,7 @@ bool forward_allowed(PyObject* st) {
 // its storage by nothing but the metric's own states on it and their view base (a packed arena's buffer).
 // why (optional): 1 no _defaults, 2 a state missing / not a tensor, 3 a Python reference besides the dict (detail: the
 // refcount), 4 no storage, 5 more than 16 tensors on the storage, 6 other tensors on the storage (detail: use count
-// * 100 + allowed), 7 the view base held from Python (detail: its refcount)
+// * 100 + allowed), 7 the view base held from Python (detail: its refcount), 8 a free-threaded CPython build
 template <typename Keys>
 bool states_unobserved_why(PyObject* st, const Keys& keys, int* why, long long* detail) {
   auto fail = [&](int w, long long d) {
@@ -600,6 +600,11 @@ bool states_unobserved_why(PyObject* st, const Keys& keys, int* why, long long* 
     if (detail != nullptr) *detail = d;
     return false;
   };
+#ifdef Py_GIL_DISABLED
+  // free-threaded CPython: biased reference counts make Py_REFCNT an approximation of the owners, not an exact count
+  // (8): never merge in place there -- the reference's out-of-place forward runs instead
+  return fail(8, 0);
+#endif
   PyObject* defaults = PyDict_GetItem(st, g_k_defaults);
   if (defaults == nullptr || !PyDict_Check(defaults)) return fail(1, 0);
   for (PyObject* key : keys) {
@@ -662,7 +667,11 @@ PyObject* sole_ref(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
     if (PyErr_Occurred()) return nullptr;
     Py_RETURN_FALSE;
   }
+#ifdef Py_GIL_DISABLED
+  Py_RETURN_FALSE;  // (see states_unobserved_why: no exact count on a free-threaded build)
+#else
   return PyBool_FromLong(THPVariable_Check(o) && Py_REFCNT(o) == 1);
+#endif
 }
 
 // _states_unobserved(state_dict, keys) -> (ok, why, detail): the forward's aliasing test on its own (tests, diagnostics)

@@ -164,6 +164,13 @@ void mc_calibration_update(const at::Tensor& preds, const at::Tensor& target, at
   if (M == 0) return;
   auto s = stream();
   int* np = notprob.data_ptr<int>();
+  // inside a hipGraph capture the host parity would be frozen: word 0 is zeroed before and re-armed after the select
+  // on every replay, so the graph leaves both words zero for eager updates around it (the caller keeps its parity)
+  const bool captured = stream_capturing(s);
+  if (captured) {
+    slot = 0;
+    launch_zero_words(np, 2, s);
+  }
   float4* cp = reinterpret_cast<float4*>(cand.data_ptr<float>());
   TM_DISPATCH_TARGET(target.scalar_type(), "mc_calibration_update", [&] {
     const target_t* tp = reinterpret_cast<const target_t*>(target.data_ptr());
@@ -183,6 +190,7 @@ void mc_calibration_update(const at::Tensor& preds, const at::Tensor& target, at
                          np + (1 - slot), conf.data_ptr<float>(), acc.data_ptr<float>());
     });
   });
+  if (captured) launch_zero_words(np, 2, s);
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 

@@ -667,6 +667,13 @@ void mc_family_update(const at::Tensor& preds, const at::Tensor& target, at::Ten
     sp.cand = reinterpret_cast<float4*>(cand.data_ptr<float>());
   }
   auto s = stream();
+  // inside a hipGraph capture the host parity would be frozen into the graph: word 0 is zeroed before the rows pass
+  // and re-armed after the fold on every replay (both words end zero, so eager updates around the graph keep theirs)
+  const bool captured = stream_capturing(s);
+  if (captured) {
+    sp.slot = 0;
+    launch_zero_words(sp.outside, 2, s);
+  }
   TM_DISPATCH_TARGET(target.scalar_type(), "mc_family_update", [&] {
     const target_t* tp = reinterpret_cast<const target_t*>(target.data_ptr());
     auto run = [&](auto tag) {
@@ -700,6 +707,7 @@ void mc_family_update(const at::Tensor& preds, const at::Tensor& target, at::Ten
   const int r_bins = r_sel + n_sel;
   const int grid = r_bins + (sp.nb > 0 ? 1 : 0);
   hipLaunchKernelGGL(family_fold_kernel, dim3(grid), dim3(kFamThreads), 0, s, sp, N, r_cv, r_sel, n_sel, r_bins);
+  if (captured) launch_zero_words(sp.outside, 2, s);
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 

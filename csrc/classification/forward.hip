@@ -12,7 +12,7 @@
 #include "common/compute_bodies.h"
 
 namespace tm_amd {
-int notprob_current(const at::Tensor& np);  // stat_scores.hip
+NpView notprob_view(const at::Tensor& np, hipStream_t s);  // stat_scores.hip
 void bin_flush_pending(const at::Tensor& ws);  // stat_scores.hip
 namespace {
 
@@ -154,11 +154,11 @@ void bin_stats_forward(at::Tensor ws, at::Tensor not_prob, at::Tensor tp, at::Te
   TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.device() == ws.device() &&
                   out.numel() == (average == 3 ? L : 1),
               "bin_stats_forward: bad output");
+  const NpView nv = notprob_view(not_prob, stream());
   hipLaunchKernelGGL(bin_stats_forward_kernel, dim3(1), dim3(kThreads), 0, stream(), ws.data_ptr<int64_t>(),
                      static_cast<int>(L), not_prob.data_ptr<int>(), tp.data_ptr<int64_t>(), fp.data_ptr<int64_t>(),
                      tn.data_ptr<int64_t>(), fn.data_ptr<int64_t>(), static_cast<int>(kind), static_cast<int>(average),
-                     static_cast<float>(beta * beta), out.data_ptr<float>(), notprob_current(not_prob),
-                     not_prob.numel() >= 2);
+                     static_cast<float>(beta * beta), out.data_ptr<float>(), nv.slot, nv.two);
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 

@@ -1627,6 +1627,15 @@ int notprob_current(const at::Tensor& np) {
   return it == g_np_slot.end() ? 0 : it->second;
 }
 
+// The reader's view of the word pair: (slot, double-buffered).  While the stream is being captured into a hipGraph the
+// host parity would be frozen into the graph, so captured work uses the one-word protocol on word 0 instead: bin_update
+// zeroes both words first and the finalize re-arms word 0 after reading it, on every replay.  Eager updates around the
+// graph keep their parity: the graph leaves both words zero.
+NpView notprob_view(const at::Tensor& np, hipStream_t s) {
+  if (np.numel() < 2 || stream_capturing(s)) return NpView{0, false};
+  return NpView{notprob_current(np), true};
+}
+
 // Per-block label histograms of a binary / multilabel update whose fold is deferred to the finalize (keyed by the
 // workspace address): the finalize then folds AND finalizes in one launch (bin_partials_finalize_kernel).  A second
 // update on the same workspace before any finalize first folds the pending rows into ws (partials_fold_kernel).
@@ -1681,8 +1690,9 @@ bool finalize_pending(at::Tensor ws, at::Tensor not_prob, bool accumulate, int64
     g_pending.erase(it);
   }
   const int L = pf.nbins / kBinSlots;
-  const bool two = not_prob.numel() >= 2;
-  const int slot = notprob_current(not_prob);
+  const NpView nv = notprob_view(not_prob, s);
+  const bool two = nv.two;
+  const int slot = nv.slot;
   auto go = [&](auto lbc) {
     constexpr int LB = decltype(lbc)::value;
     hipLaunchKernelGGL((bin_partials_finalize_kernel<LB>), dim3((L + LB - 1) / LB), dim3(kFoldThreads), 0, s,
@@ -2067,7 +2077,10 @@ void bin_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor ws
   TORCH_CHECK(ws.numel() == G * kBinSlots && ws.scalar_type() == at::kLong, "bin_update: bad workspace");
   auto s = stream();
   flush_pending(ws, s);  // an earlier update of this workspace not finalized yet: fold its rows into ws first
-  int* const npw = not_prob.data_ptr<int>() + notprob_begin(not_prob);  // this update's "not probabilities" word
+  const bool captured = not_prob.numel() >= 2 && stream_capturing(s);
+  if (captured) launch_zero_words(not_prob.data_ptr<int>(), 2, s);  // one-word protocol inside a graph
+  // this update's "not probabilities" word
+  int* const npw = not_prob.data_ptr<int>() + (captured ? 0 : notprob_begin(not_prob));
   TM_DISPATCH_TARGET(target.scalar_type(), "bin_update", [&] {
     const target_t* tp = reinterpret_cast<const target_t*>(target.data_ptr());
     TM_DISPATCH_PREDS(preds.scalar_type(), "bin_update", [&] {
@@ -2159,12 +2172,12 @@ void bin_stats_finalize(at::Tensor ws, at::Tensor not_prob, bool accumulate, at:
     C10_HIP_KERNEL_LAUNCH_CHECK();
     return;
   }
-  const bool two = not_prob.numel() >= 2;  // double-buffered word: no re-arm launch
+  const NpView nv = notprob_view(not_prob, s);
+  const bool two = nv.two;                  // double-buffered word: no re-arm launch
   const bool one = G <= kFinalizeOneBlock;  // one block folds and re-arms not_prob itself
   hipLaunchKernelGGL(bin_finalize_kernel, dim3(one ? 1 : grid_cap((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                      ws.data_ptr<int64_t>(), G, not_prob.data_ptr<int>(), accumulate, tp.data_ptr<int64_t>(),
-                     fp.data_ptr<int64_t>(), tn.data_ptr<int64_t>(), fn.data_ptr<int64_t>(), one && !two,
-                     notprob_current(not_prob), two);
+                     fp.data_ptr<int64_t>(), tn.data_ptr<int64_t>(), fn.data_ptr<int64_t>(), one && !two, nv.slot, two);
   if (!one && !two) hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
@@ -2182,10 +2195,11 @@ void bin_confmat_finalize(at::Tensor ws, at::Tensor not_prob, at::Tensor confmat
     return;
   }
   const bool one = G <= kFinalizeOneBlock;
-  const bool two = not_prob.numel() >= 2;
+  const NpView nv = notprob_view(not_prob, s);
+  const bool two = nv.two;
   hipLaunchKernelGGL(bin_confmat_finalize_kernel, dim3(one ? 1 : grid_cap((G + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                      s, ws.data_ptr<int64_t>(), G, not_prob.data_ptr<int>(), confmat.data_ptr<int64_t>(),
-                     one && !two, notprob_current(not_prob), two);
+                     one && !two, nv.slot, two);
   if (!one && !two) hipLaunchKernelGGL(zero_int_kernel, dim3(1), dim3(1), 0, s, not_prob.data_ptr<int>());
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }

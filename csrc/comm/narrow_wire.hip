@@ -170,13 +170,47 @@ at::Tensor narrow_decode(const at::Tensor& wire, int64_t n, at::ScalarType out_d
   return out;
 }
 
+// Optimistic static-shape gather (parallel/sync.py ``_gather_static``): every rank sends its fixed-shape
+// ``None`` / callable-reduction states at their configured shapes plus one signature element (1 = every state had
+// that shape and dtype, 0 = not) in ONE all_gather with no shape header.  This one-thread-per-rank check ORs `bit`
+// into the caller's validation word when any rank's signature (the last column of the gathered [W, L + 1] buffer) is
+// not 1; compute() reads the word anyway and re-syncs with the header in that (rare) case.
+namespace {
+template <typename T>
+__global__ void static_sig_check_kernel(const T* __restrict__ g, int world, long long row, int* __restrict__ word,
+                                        int bit) {
+  const int r = threadIdx.x;
+  const bool bad = r < world && static_cast<double>(g[static_cast<long long>(r) * row + row - 1]) != 1.0;
+  if (__any(bad) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(word, bit);
+}
+}  // namespace
+
+void static_gather_check(const at::Tensor& gathered, at::Tensor word, int64_t bit) {
+  TM_CHECK_CUDA(gathered);
+  TM_SAME_DEVICE(gathered, word);
+  TM_CHECK_CONTIG(gathered);
+  TORCH_CHECK(gathered.dim() == 2 && gathered.size(1) >= 1, "static_gather_check: gathered must be [W, L + 1]");
+  TORCH_CHECK(word.scalar_type() == at::kInt && word.numel() >= 1, "static_gather_check: word must be int32");
+  const int world = static_cast<int>(gathered.size(0));
+  TORCH_CHECK(world >= 1 && world <= 1024, "static_gather_check: 1 <= W <= 1024");
+  const long long row = gathered.size(1);
+  const int threads = (world + kWave - 1) / kWave * kWave;
+  AT_DISPATCH_ALL_TYPES_AND2(at::kHalf, at::kBFloat16, gathered.scalar_type(), "static_gather_check", [&] {
+    hipLaunchKernelGGL((static_sig_check_kernel<scalar_t>), dim3(1), dim3(threads), 0, stream(),
+                       gathered.data_ptr<scalar_t>(), world, row, word.data_ptr<int>(), static_cast<int>(bit));
+  });
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
   m.def("narrow_encode(Tensor src, int code, int world) -> Tensor");
   m.def("narrow_decode(Tensor wire, int n, ScalarType out_dtype, Tensor? word, int bit) -> Tensor");
+  m.def("static_gather_check(Tensor gathered, Tensor(a!) word, int bit) -> ()");
 }
 TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
   m.impl("narrow_encode", &narrow_encode);
   m.impl("narrow_decode", &narrow_decode);
+  m.impl("static_gather_check", &static_gather_check);
 }
 
 }  // namespace tm_amd

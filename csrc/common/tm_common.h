@@ -232,6 +232,31 @@ inline int grid_cap(long long blocks, int cap = 256 * 16) {
 
 inline hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
 
+// True while `s` is being captured into a hipGraph.  The double-buffered "scores are not probabilities" words pick
+// their slot from a host-side update parity, which a captured graph would freeze at the capture-time value (one slot
+// read and never re-armed on replay): under capture the launchers use slot 0 and re-arm it inside the captured work.
+inline bool stream_capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
+}
+
+// which word of a binary / multilabel "not probabilities" pair a reader uses, and whether the pair is double-buffered
+// (stat_scores.hip notprob_view)
+struct NpView {
+  int slot;
+  bool two;
+};
+
+// zero n (<= 64) int words: the captured-mode re-arm of a decision word buffer (one copy per translation unit)
+namespace {
+__global__ void zero_words_kernel(int* __restrict__ p, int n) {
+  if (static_cast<int>(threadIdx.x) < n) p[threadIdx.x] = 0;
+}
+}  // namespace
+inline void launch_zero_words(int* p, int n, hipStream_t s) {
+  hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, s, p, n);
+}
+
 // CU count of a device, queried once per device (hipDeviceGetAttribute costs host time on every call).
 inline int cu_count(int device) {
   static int cache[64] = {0};

@@ -479,7 +479,7 @@ template <typename scalar_t>
 __global__ void __launch_bounds__(kHandoffThreads) moments_handoff_kernel(
     const scalar_t* __restrict__ preds, const scalar_t* __restrict__ target, long long total, int k, int mask,
     double eps, double pw, const float* __restrict__ shift_p, const float* __restrict__ shift_t, DestSpec spec,
-    double* __restrict__ out_sums, double* __restrict__ partial, unsigned int* __restrict__ ticket) {
+    double* __restrict__ out_sums, double* __restrict__ partial, unsigned int* __restrict__ ticket, bool fenced) {
   // phase 1: [wave][column][sum]; the last block then reuses it for [G][column][sum] staged rows + [column][sum] totals
   extern __shared__ double lds[];
   __shared__ int last;
@@ -514,12 +514,27 @@ __global__ void __launch_bounds__(kHandoffThreads) moments_handoff_kernel(
                        static_cast<unsigned long long>(__double_as_longlong(v)), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
+  // Memory-model note.  The hand-off is the "sc1 payload" form of MI355X_MICROARCH.md (Valid forms): EVERY
+  // store of the partial rows is an agent-scope (sc1, write-through) atomic store drained by `s_waitcnt vmcnt(0)`
+  // before the block's barrier and ticket add, and EVERY load of them in the last block is an agent-scope (sc1)
+  // atomic load -- no L1 / non-coherent L2 copy is ever read, so no release / acquire fence (buffer_wbl2 / buffer_inv
+  // sc1, ~1.7 us each on gfx950) is needed on this ISA.  It is NOT ordered by the C++/HIP memory model alone (relaxed
+  // stores vs a relaxed ticket): `fenced` (TM_AMD_MOMENTS_FENCED=1) adds the model's agent-scope release before the
+  // ticket and acquire after it, for measurement and for any other target; tests/test_moments_handoff_gpu.py
+  // checks every sum under uneven load on gfx950 with the fence-free default.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
   __syncthreads();
-  if (tid == 0)
-    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  if (tid == 0) {
+    if (fenced) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    } else {
+      last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    }
+  }
   __syncthreads();
   if (!last) return;
+  if (fenced) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // the last block: all G partial rows with coalesced, independent sc1 loads into LDS (a per-column chain of G
   // dependent loads cost ~0.3 us per block), then per (column, sum) a block-order sum (reproducible)
   const int nload = static_cast<int>(gridDim.x) * kk;
@@ -699,6 +714,10 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
     g = std::min<long long>(g, std::min<long long>(128, kHandoffMaxRows / k));
     const int G = static_cast<int>(std::max<long long>(1, g));
     unsigned int* ticket = stream_ticket(preds.get_device(), s);
+    static const bool fenced = [] {
+      const char* e = std::getenv("TM_AMD_MOMENTS_FENCED");
+      return e && std::atoi(e) != 0;
+    }();
     at::Tensor partial = at::empty({G, k, kMaxSums}, dopt);
     const size_t lds = static_cast<size_t>(std::max(kHandoffThreads / kWave, G + 1)) * k * kMaxSums * sizeof(double);
     TM_DISPATCH_FLOAT(preds.scalar_type(), "moments_update", [&] {
@@ -706,7 +725,7 @@ at::Tensor moments_update(const at::Tensor& preds, const at::Tensor& target, int
                          reinterpret_cast<const scalar_t*>(preds.data_ptr()),
                          reinterpret_cast<const scalar_t*>(target.data_ptr()), total, k, static_cast<int>(mask), eps,
                          power, sp, st, spec, want_sums ? sums.data_ptr<double>() : nullptr, partial.data_ptr<double>(),
-                         ticket);
+                         ticket, fenced);
     });
     C10_HIP_KERNEL_LAUNCH_CHECK();
     return sums;

@@ -121,3 +121,20 @@ def test_degenerate_shapes_closed_form(no_torch_body):
         m.update(preds.to(DEV), target.to(DEV))
         correct = torch.cat(m.correct) if isinstance(m.correct, list) else m.correct
         assert int(correct.sum()) == exp_c and int(m.total.sum()) == exp_t, (preds.shape, ml, avg)
+
+
+@pytest.mark.parametrize("samplewise", [False, True])
+def test_float_target_compared_exactly(samplewise):
+    """A floating target is compared as-is: target 1.5 matches preds 1.5 and nothing else, as the
+    reference's ``preds == target`` does -- the labels kernel would truncate it, so those batches take the torch
+    body."""
+    target = torch.tensor([[1.5, 2.0], [0.0, 1.0], [1.5, 1.5], [2.0, 0.5]])
+    preds = torch.tensor([[1.5, 2.0], [0.0, 1.0], [1.0, 1.5], [2.0, 0.0]])
+    avg = "samplewise" if samplewise else "global"
+    exp = _ref_multiclass(preds, target, None, samplewise)
+    assert float(exp.sum()) == 2.0 if samplewise else float(exp) == 0.5
+    got = multiclass_exact_match(preds.to(DEV), target.to(DEV), 3, avg, validate_args=False)
+    torch.testing.assert_close(got.cpu().float(), exp)
+    m = tm.MulticlassExactMatch(3, multidim_average=avg, validate_args=False).to(DEV)
+    m.update(preds.to(DEV), target.to(DEV))
+    torch.testing.assert_close(m.compute().cpu().float(), exp)

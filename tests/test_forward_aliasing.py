@@ -60,3 +60,38 @@ def test_packed_arena_states():
     assert _probe(a.__dict__, keys)[:2] == (False, 7)
     del b
     assert _probe(a.__dict__, keys)[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("how", ["attribute", "metric_state", "compute", "state_dict_keep_vars", "arena_view"])
+def test_held_state_never_changes_under_native_forward(how):
+    """The reference's reduce-state forward (``S/metric.py:329-352``) re-binds fresh state tensors, so a state object
+    the user holds keeps its value.  The ROCm native forward merges in place only when nothing outside holds a state;
+    whichever way a state was handed out -- an attribute read, ``metric_state``, a ``compute()`` result that IS the
+    state, ``state_dict(keep_vars=True)`` or a view -- the held object must not change, and the metric's own states
+    and batch values must equal a CPU run."""
+    dev = "cuda"
+    g = torch.Generator().manual_seed(2)
+    batches = [(torch.randn(257, 6, generator=g), torch.randint(0, 6, (257,), generator=g)) for _ in range(4)]
+    for make in (lambda: tm.MulticlassConfusionMatrix(6), lambda: tm.classification.MulticlassAccuracy(6)):
+        m, ref = make().to(dev), make()
+        m.persistent(True)
+        for i, (p, t) in enumerate(batches):
+            attr = "confmat" if hasattr(m, "confmat") else "tp"
+            if how == "attribute":
+                held = getattr(m, attr)
+            elif how == "metric_state":
+                held = m.metric_state[attr]
+            elif how == "compute":
+                held = m.compute() if i else getattr(m, attr)
+            elif how == "state_dict_keep_vars":
+                held = m.state_dict(keep_vars=True)[attr]
+            else:
+                held = getattr(m, attr)[1:]
+            snap = held.clone()
+            out = m(p.to(dev), t.to(dev))
+            ref_out = ref(p, t)
+            assert torch.equal(held, snap), f"{how}: a held state changed under forward (batch {i})"
+            torch.testing.assert_close(out.cpu(), ref_out)
+            del held
+        torch.testing.assert_close(m.compute().cpu(), ref.compute())

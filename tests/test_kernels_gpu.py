@@ -381,6 +381,60 @@ def test_graphed_update_matches_eager():
         GraphedUpdate(C.MulticlassCalibrationError(10).to(DEV), batches[0][0], batches[0][1])
 
 
+@pytest.mark.parametrize("n", [64, 4096, 70000])
+def test_graphed_update_decides_logits_per_batch(n):
+    """The 'scores are not probabilities' decision is per batch under graph replay too: batches that
+    alternate between logits and probabilities, replayed from one captured graph and interleaved with eager updates
+    of the same metric, equal eager-only updates -- binary / multilabel stat scores, the binary confusion matrix and
+    the fused multiclass family (binned AUROC / AP soften logits only)."""
+    import torchmetrics_amd as tm
+    from torchmetrics_amd import classification as C
+    from torchmetrics_amd.utils.graphs import GraphedUpdate
+
+    g = torch.Generator().manual_seed(3)
+
+    def batch(kind, logits):
+        if kind == "bin":
+            p = torch.randn(n, generator=g) * 3 if logits else torch.rand(n, generator=g)
+            return p.to(DEV), torch.randint(0, 2, (n,), generator=g).to(DEV)
+        if kind == "ml":
+            p = torch.randn(n, 5, generator=g) * 3 if logits else torch.rand(n, 5, generator=g)
+            return p.to(DEV), torch.randint(0, 2, (n, 5), generator=g).to(DEV)
+        p = torch.randn(n, 6, generator=g) * 3 if logits else torch.softmax(torch.randn(n, 6, generator=g), 1)
+        return p.to(DEV, torch.bfloat16), torch.randint(0, 6, (n,), generator=g).to(DEV)
+
+    makers = {
+        "bin": lambda: [C.BinaryAccuracy(), C.BinaryF1Score(), C.BinaryConfusionMatrix()],
+        "ml": lambda: [C.MultilabelF1Score(5, average="macro"), C.MultilabelAccuracy(5, average=None)],
+        "mc": lambda: [tm.MetricCollection({
+            "acc": C.MulticlassAccuracy(6), "cm": C.MulticlassConfusionMatrix(6),
+            "auroc": C.MulticlassAUROC(6, thresholds=20), "ap": C.MulticlassAveragePrecision(6, thresholds=20)},
+            compute_groups=True)],
+    }
+    pattern = [True, False, False, True, False, True, True, False]
+    for kind, make in makers.items():
+        eager = [m.to(DEV) for m in make()]
+        graphed = [m.to(DEV) for m in make()]
+        first = batch(kind, True)
+        runners = [GraphedUpdate(m, *first) for m in graphed]
+        for i, logits in enumerate(pattern):
+            p, t = batch(kind, logits)
+            for m in eager:
+                m.update(p, t)
+            for m, r in zip(graphed, runners):
+                if i % 3 == 2:
+                    m.update(p, t)  # eager update of the graphed metric between replays
+                else:
+                    r(p, t)
+        for a, b in zip(graphed, eager):
+            ra, rb = a.compute(), b.compute()
+            if isinstance(rb, dict):
+                for k in rb:
+                    torch.testing.assert_close(ra[k], rb[k], msg=f"{kind}/{k}")
+            else:
+                torch.testing.assert_close(ra, rb, msg=kind)
+
+
 # ------------------------------------------------------------------ fused regression compute (regression_compute.hip)
 def _reg_cases():
     g = torch.Generator().manual_seed(7)

@@ -6,7 +6,7 @@ syncs are interchangeable.  Deliberate difference: ``BinaryGroupStatRates`` / ``
 statistics by group *id* (the reference enumerates the groups present in each batch, which misattributes counts when
 a batch lacks a group).
 """
-from typing import Any, Dict, Optional, Type
+from typing import Any, Dict, Optional, Tuple, Type
 
 import torch
 from torch import Tensor
@@ -68,7 +68,7 @@ from torchmetrics_amd.functional.classification.stat_scores import (
 from torchmetrics_amd.functional.classification.stat_scores import _sink_flag
 from torchmetrics_amd.metric import Metric
 from torchmetrics_amd.utilities.checks import _check_same_shape
-from torchmetrics_amd.utilities.data import dim_zero_cat
+from torchmetrics_amd.utilities.data import dim_zero_cat, dim_zero_sum
 from torchmetrics_amd.utilities.enums import ClassificationTaskNoBinary, ClassificationTaskNoMultilabel
 from torchmetrics_amd.utilities.prints import rank_zero_warn
 
@@ -83,8 +83,13 @@ class _BinnedCalibration(Metric):
     concatenates and bucketizes the whole history on each compute; with a compute per step that is O(steps²)).  The
     cache is trusted only while it covers exactly the samples in the list states (host-side element counts, no sync):
     anything else -- a forward() state merge, a loaded state dict, CPU states -- re-bins from the lists once and
-    re-seeds the cache.  Under DDP the ranks all-reduce the bins (3 (n_bins+1) floats) instead of gathering the lists
-    when every rank's cache is valid (agreed with one MIN all-reduce)."""
+    re-seeds the cache.
+
+    Under DDP, ``sync()`` / ``sync_context`` gather the list states like the reference (``S/metric.py:427-457``: after
+    a sync they are the global lists).  The sync that only serves ``compute()`` sends the bins instead: every rank
+    offers its local ``[n_bins + 1, 3]`` bins (the cache, or one binning pass over its lists when the cache does not
+    cover them) as an fp64 SUM state -- one bucket of the metric's / collection's single engine call, no agreement
+    round, no host read -- and compute() folds the global bins."""
 
     _fold_cat_lists = True  # compute() only concatenates the list states
     _fold_every = 8  # (the bin cache serves compute(): the lists are folded every 8th batch, not at every compute)
@@ -143,23 +148,38 @@ class _BinnedCalibration(Metric):
         self.__dict__.pop("_bin_cache", None)
         return super()._apply(fn, exclude_state)
 
-    def _sync_dist(self, dist_sync_fn: Optional[Any] = None, process_group: Optional[Any] = None) -> None:
-        import torch.distributed as dist
-
+    def _local_bins(self) -> Tensor:
+        """This rank's (count, Σconf, Σacc) bins over every sample in its list states: the cache when it covers them,
+        else one binning pass (re-seeding the cache on ROCm f32); always available, so every rank takes the same
+        sync plan."""
         cache = self._valid_cache()
-        if dist_sync_fn is None and dist.is_available() and dist.is_initialized():
-            group = process_group or self.process_group
-            dev = cache[0].device if cache is not None else (
-                torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl"
-                else torch.device("cpu"))
-            ok = torch.tensor([1 if cache is not None else 0], dtype=torch.int32, device=dev)
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
-            if int(ok.item()) == 1:
-                bins = cache[0].clone()
-                dist.all_reduce(bins, group=group)
-                self.__dict__["_bin_synced"] = bins
-                return
-        super()._sync_dist(dist_sync_fn, process_group)
+        if cache is not None:
+            return cache[0]
+        conf = dim_zero_cat(self.confidences) if self._list_numel() else None
+        if conf is None:
+            return torch.zeros(self.n_bins + 1, 3, dtype=torch.float64, device=self.device)
+        acc = dim_zero_cat(self.accuracies)
+        if conf.is_cuda and conf.dtype == torch.float32 and self.n_bins + 1 <= 4096 and not self.compute_on_cpu:
+            cache = [torch.zeros(self.n_bins + 1, 3, dtype=torch.float32, device=conf.device), conf.numel(),
+                     self.confidences]
+            ops.calibration_bins_into(conf.contiguous(), acc.float().contiguous(), self._bounds(conf.device),
+                                      cache[0])
+            self.__dict__["_bin_cache"] = cache
+            return cache[0]
+        bounds = torch.linspace(0, 1, self.n_bins + 1, dtype=conf.dtype, device=conf.device)
+        idx = torch.bucketize(conf, bounds, right=True) - 1
+        src = torch.stack([torch.ones_like(conf), conf, acc.to(conf.dtype)], dim=1)
+        return torch.zeros(self.n_bins + 1, 3, dtype=conf.dtype, device=conf.device).index_add_(0, idx, src)
+
+    def _compute_sync_override(self) -> Optional[Tuple[Dict[str, Tensor], Dict[str, Any]]]:
+        return {"bins\0": self._local_bins().to(torch.float64)}, {"bins\0": dim_zero_sum}
+
+    def _compute_sync_finish(self, synced: Dict[str, Any]) -> None:
+        c = self.confidences
+        first = c if isinstance(c, Tensor) else (c[0] if c else None)
+        # the global bins in the lists' dtype (the reference's compute runs in the confidences' dtype)
+        dt = first.dtype if first is not None and first.is_floating_point() else torch.float32
+        self.__dict__["_bin_synced"] = synced["bins\0"].to(torch.float32 if synced["bins\0"].is_cuda else dt)
 
     def compute(self) -> Tensor:
         bins = self.__dict__.pop("_bin_synced", None)
@@ -179,9 +199,15 @@ class _BinnedCalibration(Metric):
                 bins = cache[0]
             else:
                 return _ce_compute(conf, acc, self.n_bins, norm=self.norm)
-        if self.norm in ("l1", "max"):
+        if self.norm in ("l1", "max") and bins.is_cuda:
             return ops.calibration_error_from_bins(bins, self.norm)
         count = bins[:, 0]
+        if self.norm in ("l1", "max"):
+            acc_bin = torch.nan_to_num(bins[:, 2] / count)
+            conf_bin = torch.nan_to_num(bins[:, 1] / count)
+            if self.norm == "l1":
+                return torch.sum(torch.abs(acc_bin - conf_bin) * (count / count.sum()))
+            return torch.max(torch.abs(acc_bin - conf_bin))
         acc_bin = torch.nan_to_num(bins[:, 2] / count)
         conf_bin = torch.nan_to_num(bins[:, 1] / count)
         ce = torch.sum(torch.pow(acc_bin - conf_bin, 2) * (count / count.sum()))

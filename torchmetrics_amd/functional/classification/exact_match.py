@@ -43,10 +43,14 @@ def _exact_match_fused(
     """ROCm path (``csrc/classification/exact_match.hip``) on the unformatted inputs: argmax / sigmoid-or-not /
     threshold / ignore / all-positions vote in one pass.  Global with ``correct`` / ``total`` given: the states are
     updated in place.  Returns ``(correct, total)`` as the torch update would, or None (the caller's torch body runs)
-    only for CPU tensors and shapes the reference's validation rejects (``validate_args=False`` with mismatched
-    shapes, an argmax over zero classes).  Every ROCm input the reference accepts runs here: scores, integer and
-    float labels, ``ignore_index``, empty batches and zero-size position dims (those two in closed form)."""
+    for CPU tensors, floating-point targets and shapes the reference's validation rejects (``validate_args=False``
+    with mismatched shapes, an argmax over zero classes).  A floating target is compared as-is by the reference
+    (``preds == target``: 1.5 matches only 1.5); the kernel compares integer labels, so those batches keep the torch
+    body rather than truncating the target.  Every other ROCm input runs here: scores, integer / float label preds,
+    ``ignore_index``, empty batches and zero-size position dims (those two in closed form)."""
     if not (preds.is_cuda and target.is_cuda and preds.device == target.device) or target.ndim < 1:
+        return None
+    if target.is_floating_point():
         return None
     n = target.shape[0]
     samplewise = multidim_average == "samplewise"
@@ -63,7 +67,7 @@ def _exact_match_fused(
     elif preds.ndim == target.ndim:
         if preds.shape[0] != n or preds.numel() != target.numel():
             return None
-        # labels of any dtype (float labels compare exactly, as `preds == target` does): one unit per sample
+        # labels (integer target; float preds compare exactly, as `preds == target` does): one unit per sample
         kind, c, p = ops.EM_LABELS, math.prod(target.shape[1:]), 1
         total_val = n if not samplewise else 1
     else:
@@ -90,7 +94,7 @@ def _exact_match_fused(
         return correct, total
     preds, target = preds.contiguous(), target.contiguous()
     if target.dtype not in (torch.int64, torch.int32, torch.uint8, torch.bool):
-        target = target.long()
+        target = target.long()  # int8 / int16 labels: widened exactly
     if samplewise:
         out = ops.exact_match_update(preds, target, kind, c, p, threshold, ignore_index, True, owner)
         return out, torch.tensor(total_val, device=dev)

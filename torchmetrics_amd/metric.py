@@ -54,6 +54,9 @@ _REDUCTION_BY_NAME = {
     "cat": dim_zero_cat,
 }
 
+# reductions the engine all-reduces (everything else that is a tensor state is gathered)
+_ENGINE_REDUCE_FNS = (dim_zero_sum, dim_zero_mean, dim_zero_max, dim_zero_min)
+
 _NULL_CTX = nullcontext()
 
 _CONST_ATTRS = (
@@ -472,8 +475,46 @@ class Metric(Module, ABC):
             setattr(self, attr, merged)
 
     # ------------------------------------------------------------------------------------------------------- sync
+    def _static_gather_spec(self) -> Dict[str, Tuple[Tuple[int, ...], torch.dtype, Tuple[str, str]]]:
+        """``{state: (configured shape, dtype, ident)}`` of the tensor states with a ``None`` / callable reduction:
+        their ``add_state`` default fixes their shape on every rank, so the engine gathers them without the shape
+        header (``parallel/sync.py`` static gather; a state that left that shape is caught by a signature)."""
+        d = self.__dict__
+        cached = d.get("_static_spec")
+        if cached is not None and cached[0] == len(self._defaults):
+            return cached[1]
+        spec = {}
+        for attr, default in self._defaults.items():
+            fn = self._reductions.get(attr)
+            if isinstance(default, Tensor) and fn is not dim_zero_cat and (
+                    fn is None or (callable(fn) and fn not in _ENGINE_REDUCE_FNS)):
+                spec[attr] = (tuple(default.shape), default.dtype, (type(self).__qualname__, attr))
+        d["_static_spec"] = (len(self._defaults), spec)
+        return spec
+
+    def _compute_sync_override(self) -> Optional[Tuple[Dict[str, Tensor], Dict[str, Callable]]]:
+        """States to sync INSTEAD of the metric's own when the sync only serves this ``compute()`` (``None``: the
+        states themselves).  A metric whose compute needs less than its states (calibration error: its bins, not the
+        sample lists) overrides this and :meth:`_compute_sync_finish`; ``sync()`` / ``sync_context`` always sync the
+        real states (reference contract, ``S/metric.py:427-457``)."""
+        return None
+
+    def _compute_sync_finish(self, synced: Dict[str, Any]) -> None:
+        """Receives the synced override states of :meth:`_compute_sync_override` (this metric and every member of
+        its compute group)."""
+
     def _sync_dist(self, dist_sync_fn: Optional[Callable] = None, process_group: Optional[Any] = None) -> None:
         group = process_group or self.process_group
+        if dist_sync_fn is None and self.__dict__.get("_in_compute"):
+            override = self._compute_sync_override()
+            if override is not None:
+                dev = next((v.device for v in override[0].values() if isinstance(v, Tensor) and v.is_cuda), None)
+                err = self._device_error_buffer(dev) if dev is not None else None
+                synced = sync_state_dicts([override], group=group, err_word=err, narrow_word=err)[0]
+                self._compute_sync_finish(synced)
+                if err is not None:
+                    self.__dict__["_sync_word_pending"] = True
+                return
         packed = self._packed_sync_plan(group) if dist_sync_fn is None and self._packed_sync_states else {}
         states = {attr: getattr(self, attr) for attr in self._reductions if attr not in packed}
         if dist_sync_fn is None:
@@ -496,7 +537,8 @@ class Metric(Module, ABC):
             err = self._device_error_buffer(dev) if dev is not None else None
             # inside compute() a narrow-wire overflow is reported in the same word (no host read in the sync)
             narrow = err if self.__dict__.get("_defer_narrow") else None
-            synced = sync_state_dicts([(states, reductions)], group=group, err_word=err, narrow_word=narrow)[0]
+            synced = sync_state_dicts([(states, reductions, self._static_gather_spec())], group=group, err_word=err,
+                                      narrow_word=narrow)[0]
             for attr in packed:
                 flat, sizes, n = synced.pop(attr + "\0flat"), synced.pop(attr + "\0sizes"), synced.pop(attr + "\0n")
                 setattr(self, attr, [])
@@ -995,8 +1037,9 @@ class Metric(Module, ABC):
             local[attr] = (flat, sizes)
             ok.append(1 if (flat is not None and flat.ndim >= 1) or not sizes else 0)
         dev = next((f.device for f, _ in local.values() if f is not None), self.device)
-        backend = torch.distributed.get_backend(group)
-        flag_dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+        from torchmetrics_amd.parallel.sync import _device_comm
+
+        flag_dev = torch.device("cuda", torch.cuda.current_device()) if _device_comm(group) else torch.device("cpu")
         flags = torch.tensor(ok, dtype=torch.int32, device=flag_dev)
         torch.distributed.all_reduce(flags, op=torch.distributed.ReduceOp.MIN, group=group)
         del dev

@@ -590,7 +590,8 @@ def mc_calibration_update(preds: Tensor, target: Tensor, ws: CalibrationWorkspac
         if flag is None:
             flag = _EMPTY_FLAG[key] = torch.empty(0, dtype=torch.int32, device=dev)
     (_fast_mod or _fast()).mc_calibration_update(preds, target, ws.cand, conf, acc, ws.notprob, ws.slot, flag)
-    ws.slot ^= 1
+    if not torch.cuda.is_current_stream_capturing():  # captured: the kernel side runs the one-word protocol
+        ws.slot ^= 1
     return conf, acc
 
 
@@ -1474,6 +1475,9 @@ def gemm_row_col_max(x: Tensor, y: Tensor, scale: float = 1.0) -> "tuple[Tensor,
 
 
 # ------------------------------------------------------------------------------------------------------------ text
+_LEV_WAVES = 4  # waves (pairs) per block of csrc/text/levenshtein.hip (kWavesPerBlock)
+
+
 def levenshtein(pred: Tensor, poff: Tensor, ref: Tensor, roff: Tensor, ins: int = 1, dele: int = 1, sub: int = 1,
                 use_beam: bool = False, max_ref_len: Optional[int] = None) -> Tensor:
     """Batched edit distances ``[B]`` (int64) of int32 token-id sequences packed with int64 offsets
@@ -1481,7 +1485,17 @@ def levenshtein(pred: Tensor, poff: Tensor, ref: Tensor, roff: Tensor, ins: int 
     multithreaded host DP when the library is loaded, else the Python DP of :mod:`ops._cpu`."""
     out = torch.empty(poff.numel() - 1, dtype=torch.int64, device=pred.device)
     if max_ref_len is None:
-        max_ref_len = int((roff[1:] - roff[:-1]).max().item()) if roff.numel() > 1 else 0
+        # the LDS rows are sized by the longest reference: the packed length bounds it with no device read (the
+        # in-package callers pass the tokeniser's host-side maximum); only a bound too large for LDS reads the offsets
+        bound = ref.numel()
+        if roff.numel() <= 1:
+            max_ref_len = 0
+        elif not roff.is_cuda:
+            max_ref_len = int((roff[1:] - roff[:-1]).max())
+        elif _LEV_WAVES * 2 * (bound + 1) * 4 <= 160 * 1024:
+            max_ref_len = bound
+        else:
+            max_ref_len = int((roff[1:] - roff[:-1]).max().item())
     args = (pred.int().contiguous(), poff.long().contiguous(), ref.int().contiguous(), roff.long().contiguous(), out,
             int(ins), int(dele), int(sub), bool(use_beam), int(max_ref_len))
     if pred.is_cuda or native_available():
@@ -1773,6 +1787,15 @@ def narrow_encode(src: Tensor, code: int, world: int) -> Tensor:
     if src.is_cuda:
         return _ops().narrow_encode(src.contiguous(), int(code), int(world))
     return _cpu.narrow_encode(src, int(code), int(world))
+
+
+def static_gather_check(gathered: Tensor, word: Tensor, bit: int) -> None:
+    """``word |= bit`` (on the device) when a rank's signature -- the last column of the gathered ``[W, L + 1]``
+    static-shape bucket -- is not 1 (``csrc/comm/narrow_wire.hip``); CPU buckets are checked on the host."""
+    if gathered.is_cuda:
+        _ops().static_gather_check(gathered, word, int(bit))
+    elif bool((gathered[:, -1] != 1).any()):
+        word.bitwise_or_(int(bit))
 
 
 def narrow_decode(wire: Tensor, n: int, out_dtype: torch.dtype, word: Optional[Tensor], bit: int) -> Tensor:

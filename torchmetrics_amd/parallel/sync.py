@@ -18,6 +18,8 @@ This engine keeps the exact *result* semantics but changes the communication pla
   host read: the verdict lands in the metric's validation word.
 * **one-shot path** -- on RCCL, reduce buckets of <= 256 KiB (every classification / regression state) skip the
   ring: one peer-read kernel over xGMI (:mod:`torchmetrics_amd.parallel.oneshot`).
+* **static gather** -- tensor states with ``None`` / callable reductions at their configured shapes: one signed
+  ``all_gather`` per dtype, no shape header, no host read (:func:`_gather_static`).
 * **gather bucket** -- ``cat``, ``None`` and custom-callable states. One fixed-size metadata header per rank (element
   counts, dtype codes and shapes: one ``all_gather``, one device->host copy), then ONE ``all_gather`` of the packed
   payload per dtype, padded only to the largest rank's payload (not per-dimension to the max shape).  Partially-empty list states do not hang (the
@@ -70,7 +72,7 @@ _DTYPE_CODES = [
 ]
 
 _stats = {"all_reduce": 0, "oneshot_all_reduce": 0, "all_gather": 0, "meta_all_gather": 0, "bytes": 0,
-          "narrow_all_reduce": 0, "narrow_retry": 0}
+          "narrow_all_reduce": 0, "narrow_retry": 0, "static_all_gather": 0, "static_retry": 0}
 
 
 def comm_stats(reset: bool = False) -> Dict[str, int]:
@@ -95,6 +97,16 @@ def _is_nccl(group: Optional[Any]) -> bool:
         return dist.get_backend(group) == "nccl"
     except Exception:
         return False
+
+
+# Tests on the one-GPU box run several ranks on one device over gloo (RCCL refuses two ranks per device): this keeps
+# the engine's metadata / gather buffers on the GPU as on RCCL, so the device-side branches (deferred signature and
+# narrow checks in the validation word) run there too; gloo moves CUDA tensors itself.
+_FORCE_DEVICE_COMM = False
+
+
+def _device_comm(group: Optional[Any]) -> bool:
+    return _FORCE_DEVICE_COMM or _is_nccl(group)
 
 
 def _reduce_kind(fn: Any) -> Optional[str]:
@@ -186,11 +198,108 @@ def _narrow_bucket(src: Tensor, world: int, group: Optional[Any], word: Optional
 
 
 def narrow_resolve(word: Tensor) -> None:
-    """After ``word`` showed ``NARROW_RETRY``: move every bucket of its last sync whose check failed one width up (the
-    caller then re-syncs; every rank sees the same summed slots, so every rank does the same)."""
+    """After ``word`` showed ``NARROW_RETRY``: move every bucket of its last sync whose check failed one width up, and
+    send every static-shape gather bucket whose signature failed through the shape header from now on (the caller then
+    re-syncs; every rank sees the same summed slots / gathered signatures, so every rank does the same)."""
     for key, slots in _NARROW_PENDING.pop(id(word), []):
         big, neg = (int(v) for v in slots.tolist())
         _escalate(key, big, neg)
+    for keys, sig in _STATIC_PENDING.pop(id(word), []):
+        if bool((sig != 1).any()):
+            _STATIC_OFF.update(keys)
+            _stats["static_retry"] += 1
+
+
+# ---- optimistic static-shape gather ----------------------------------------------------------------------------
+# Tensor states with a ``None`` / callable reduction (Pearson's six running moments, PSNR's min / max target) have
+# the shape their metric's configuration gave them in ``add_state`` on every rank.  Instead of the shape header (one
+# all_gather plus a device->host read per sync), each rank sends them at that configured shape with ONE signature
+# element (1: every state of the bucket had its configured shape and dtype; 0: not -- zeros are sent in its place, so
+# the message size is still the agreed one) in one all_gather.  The signatures are checked on the device into the
+# caller's validation word (``NARROW_RETRY``: compute() reads the word anyway); on a failed check every rank moves
+# those states to the header path (``_STATIC_OFF``) and syncs again.  ``TORCHMETRICS_AMD_STATIC_GATHER=0`` disables it.
+_STATIC_OFF: set = set()
+_STATIC_PENDING: Dict[int, List[Tuple[List[Any], Tensor]]] = {}
+_SIG: Dict[Tuple[torch.dtype, torch.device, bool], Tensor] = {}
+
+
+def _static_enabled() -> bool:
+    import os
+
+    return os.environ.get("TORCHMETRICS_AMD_STATIC_GATHER", "1") not in ("0", "false", "False")
+
+
+def _static_key(group: Optional[Any], spec: Tuple[Any, ...]) -> Tuple[Any, ...]:
+    ranks = None if group is None or group is dist.group.WORLD else tuple(dist.get_process_group_ranks(group))
+    return (ranks,) + tuple(spec)
+
+
+def _signature(dtype: torch.dtype, device: torch.device, ok: bool) -> Tensor:
+    key = (dtype, device, ok)
+    t = _SIG.get(key)
+    if t is None:
+        t = _SIG[key] = torch.full((1,), 1 if ok else 0, dtype=dtype, device=device)
+    return t
+
+
+class _StaticItem:
+    __slots__ = ("key", "val", "fn", "shape", "dtype", "skey")
+
+    def __init__(self, key: Tuple[int, str], val: Tensor, fn: Any, shape: Tuple[int, ...], dtype: torch.dtype,
+                 skey: Tuple[Any, ...]) -> None:
+        self.key, self.val, self.fn, self.shape, self.dtype, self.skey = key, val, fn, shape, dtype, skey
+
+
+def _gather_static(items: List[_StaticItem], world: int, group: Optional[Any], word: Optional[Tensor],
+                   results: List[Dict[str, State]]) -> "List[_GatherItem]":
+    """One signed all_gather per dtype of the static-shape items; returns the items that must take the header path
+    now (a failed signature checked on the host: CPU buckets, or no validation word to defer the check into)."""
+    from torchmetrics_amd.utils.validation import NARROW_RETRY
+
+    by_dtype: Dict[torch.dtype, List[_StaticItem]] = {}
+    for it in items:
+        by_dtype.setdefault(it.dtype, []).append(it)
+    dev = torch.device("cuda", torch.cuda.current_device()) if _device_comm(group) else torch.device("cpu")
+    fallback: List[_GatherItem] = []
+    for dt, its in by_dtype.items():
+        wire = _WIRE_DTYPE.get(dt, dt)
+        parts, ok = [], True
+        for it in its:
+            v = it.val
+            if tuple(v.shape) == it.shape and v.dtype == dt:
+                parts.append(v.reshape(-1))
+            else:
+                ok = False
+                parts.append(torch.zeros(math.prod(it.shape), dtype=dt, device=dev))
+        parts.append(_signature(dt, dev, ok))
+        local = torch.cat([p if p.device == dev else p.to(dev) for p in parts])
+        if wire != dt:
+            local = local.to(wire)
+        allbuf = _all_gather_flat(local, world, group)  # [W, L + 1]
+        _stats["static_all_gather"] += 1
+        keys = [it.skey for it in its]
+        if allbuf.device.type != "cuda" or word is None or word.device != allbuf.device:
+            if bool((allbuf[:, -1] != 1).any()):  # (a host tensor, or no word to defer into: read now)
+                _STATIC_OFF.update(keys)
+                _stats["static_retry"] += 1
+                fallback += [_GatherItem(it.key, False, [it.val.contiguous()], it.fn) for it in its]
+                continue
+        else:
+            ops.static_gather_check(allbuf, word, NARROW_RETRY)
+            _STATIC_PENDING.setdefault(id(word), []).append((keys, allbuf[:, -1]))
+        if wire != dt:
+            allbuf = allbuf.to(dt)
+        target = its[0].val.device
+        if allbuf.device != target:
+            allbuf = allbuf.to(target)
+        off = 0
+        for it in its:
+            n = math.prod(it.shape)
+            stacked = allbuf[:, off : off + n].reshape((world,) + it.shape)
+            off += n
+            mi, name = it.key
+            results[mi][name] = stacked if it.fn is None else it.fn(stacked)
+    return fallback
 
 
 def _narrow_enabled() -> bool:
@@ -240,7 +349,10 @@ def sync_state_dicts(
 
     Args:
         entries: one ``(states, reductions)`` pair per metric; ``reductions[name]`` is the metric's
-            ``dist_reduce_fx`` after string resolution (``dim_zero_sum`` ...), ``None`` or a callable.
+            ``dist_reduce_fx`` after string resolution (``dim_zero_sum`` ...), ``None`` or a callable.  An optional
+            third element maps tensor states with a ``None`` / callable reduction to their configured
+            ``(shape, dtype, ident)`` (``Metric._static_gather_spec``): those go through the signed static-shape
+            gather instead of the shape header.
         group: process group (``None`` = WORLD).
         err_word: int32 device word (the metric's / collection's deferred-validation word).  One-shot buckets OR
             ``ONESHOT_FAILED`` into it on failure and the CALLER must read it before using the results (``compute()``
@@ -253,7 +365,7 @@ def sync_state_dicts(
         One dict of synced states per entry.
     """
     if _prof.ENABLED:
-        with _prof.range(f"tm.sync/{sum(len(r) for _, r in entries)} states"):
+        with _prof.range(f"tm.sync/{sum(len(e[1]) for e in entries)} states"):
             return _sync_state_dicts(entries, group, err_word, narrow_word)
     return _sync_state_dicts(entries, group, err_word, narrow_word)
 
@@ -270,7 +382,11 @@ def _sync_state_dicts(
     # ---- classify ---------------------------------------------------------------------------------------------
     reduce_buckets: Dict[Tuple[str, torch.dtype, torch.device], List[Tuple[Tuple[int, str], Tensor]]] = {}
     gather_items: List[_GatherItem] = []
-    for mi, (states, reductions) in enumerate(entries):
+    static_items: List[_StaticItem] = []
+    static_on = world > 1 and _static_enabled()
+    for mi, entry in enumerate(entries):
+        states, reductions = entry[0], entry[1]
+        static = entry[2] if static_on and len(entry) > 2 else None
         for name, fn in reductions.items():
             val = states[name]
             kind = _reduce_kind(fn)
@@ -278,6 +394,12 @@ def _sync_state_dicts(
                 reduce_buckets.setdefault((kind, val.dtype, val.device), []).append(((mi, name), val))
                 continue
             if isinstance(val, Tensor):
+                spec = static.get(name) if static else None
+                if spec is not None and fn is not dim_zero_cat:
+                    skey = _static_key(group, spec)
+                    if skey not in _STATIC_OFF:
+                        static_items.append(_StaticItem((mi, name), val, fn, tuple(spec[0]), spec[1], skey))
+                        continue
                 gather_items.append(_GatherItem((mi, name), False, [val.contiguous()], fn))
             else:
                 elems = list(val)
@@ -288,6 +410,7 @@ def _sync_state_dicts(
     # ---- reduce bucket: one all_reduce per (op, dtype, device) ------------------------------------------------
     if narrow_word is not None:
         _NARROW_PENDING.pop(id(narrow_word), None)
+        _STATIC_PENDING.pop(id(narrow_word), None)
     for (kind, dtype, _device), members in reduce_buckets.items():
         wire = _WIRE_DTYPE.get(dtype, dtype)
         span = members[0][1].reshape(-1) if len(members) == 1 else contiguous_span([t for _, t in members])
@@ -320,6 +443,9 @@ def _sync_state_dicts(
                 piece = piece.to(dtype)
             results[mi][name] = piece
 
+    if static_items:
+        with _prof.range(f"tm.sync.static/{len(static_items)} states") if _prof.ENABLED else _NULL_CTX:
+            gather_items += _gather_static(static_items, world, group, narrow_word, results)
     if gather_items:
         with _prof.range(f"tm.sync.gather/{len(gather_items)} states") if _prof.ENABLED else _NULL_CTX:
             gathered = _gather_items(gather_items, world, group)
@@ -446,7 +572,7 @@ def _gather_items(items: List[_GatherItem], world: int, group: Optional[Any]) ->
 
 
 def _comm_device(items: List[_GatherItem], group: Optional[Any]) -> torch.device:
-    if _is_nccl(group):
+    if _device_comm(group):
         return torch.device("cuda", torch.cuda.current_device())
     return torch.device("cpu")
 

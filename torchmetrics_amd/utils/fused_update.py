@@ -187,7 +187,8 @@ class FamilyPlan:
         ops._fast().mc_family_update(preds, target, cm, st, micro, curve if curve is not None else empty, thr, perm,
                                      conf, acc, bounds, bins, err, self.work, self.slot,
                                      self.cand if cb is not None else empty)
-        self.slot ^= 1
+        if not torch.cuda.is_current_stream_capturing():  # captured: the kernel side runs the one-word protocol
+            self.slot ^= 1
         self.calls += 1
         for m in self.metrics:
             d = m.__dict__

@@ -15,14 +15,13 @@
 //   * the C x C (target, argmax) histogram          -> confusion matrices, and tp / fp / tn / fn of the stat scores;
 //   * per-class threshold-bucket histograms, for the raw scores AND for the softmax (the batch-wide softmax decision
 //     is only known when every block is done) -> the [T, C, 2, 2] binned-curve state;
-//   * top-1 (confidence, correct) candidates of both variants per row, and their (count, Σconf, Σacc) bins -> the
-//     calibration error's list states and its bin cache.
-// Each block adds its (non-zero) image words into one batch image in global memory (integer atomics: exact; the
-// calibration float bins in arrival order) and ORs its outside bit into the batch's decision word;
-// `family_fold_kernel` (one launch, blocks by role) reads the batch image once, adds it into every member's state,
-// selects the calibration outputs, publishes the target-range bit into every member's validation word, and re-zeroes
-// the image for the next update (the decision word is double-buffered by update parity).  Two launches per step for
-// the whole classification group, whatever the number of members.
+//   * top-1 (confidence, correct) candidates of both variants per row -> the calibration error's list states.
+// Each block adds its (non-zero) image words into one batch image in global memory (integer atomics: exact) and ORs
+// its outside bit into the batch's decision word; `family_fold_kernel` (one launch, blocks by role) reads the batch
+// image once, adds it into every member's state, selects the calibration outputs and bins the kept variant into the
+// metric's (count, Σconf, Σacc) cache (float atomics, arrival order), publishes the target-range bit into every
+// member's validation word, and re-zeroes the image for the next update (the decision word is double-buffered by
+// update parity).  Two launches per step for the whole classification group, whatever the number of members.
 #include "common/tm_common.h"
 
 #include <utility>
@@ -30,12 +29,14 @@
 namespace tm_amd {
 namespace {
 
-constexpr int kFamThreads = 256;
+constexpr int kFamThreads = 256;      // fold kernel
+constexpr int kFamRowThreads = 1024;  // rows kernel: 16 waves per block -- config #5's 8192 rows are ONE block step on
+                                      // 128 blocks (256-thread blocks ran 4 dependent steps per wave: 20.4 us vs ...)
 constexpr int kFamMaxC = 64;
 constexpr int kFamMaxCons = 4;   // confusion-matrix / stat-score consumers per launch
 constexpr int kFamMaxErr = 12;   // validation words (4 + 4 consumers, a curve and a calibration member)
-constexpr int kFamMaxBlocks = 512;
 constexpr int kFoldCols = kFamThreads / kWave;  // curve columns per fold block (one wave each)
+constexpr int kFoldMaxBins = 512;               // calibration bins binned in a fold block's LDS (more: global atomics)
 
 struct FamilySpec {
   int C;
@@ -56,7 +57,7 @@ struct FamilySpec {
   int n_err;
   int* err[kFamMaxErr];
   // scratch (zero on entry, re-zeroed by the fold)
-  int* img;                                // batch image: [C*C cm][2][T+1][C][2] curve][2][nb][3] calib (f32)]
+  int* img;                                // batch image: [C*C cm][2][T+1][C][2] curve]
   int* outside;                            // [2] decision words, by update parity
   int slot;
   float4* cand;                            // [N]
@@ -64,8 +65,8 @@ struct FamilySpec {
   int part_words, off_cv, off_cb;
   int need_cm;
   int abl;  // profiling ablation (TM_AMD_FAMILY_ABLATE, default 0: results are WRONG when set): 1 no threshold
-            // searches, 2 no calibration bins, 4 no global flush, 8 no class-ordered softmax sums, 16 no curve
-            // histogram at all, 32 binary threshold search even on an even grid
+            // searches, 8 no class-ordered softmax sums, 16 no curve histogram at all, 32 binary threshold search even
+            // on an even grid
 };
 
 __device__ __forceinline__ int bucket_of(const double* __restrict__ thr, int t, double p) {
@@ -88,99 +89,6 @@ __device__ __forceinline__ int bucket_guess(const double* __restrict__ thr, int 
   while (b < t && thr[b] <= p) ++b;
   while (b > 0 && thr[b - 1] > p) --b;
   return b;
-}
-
-template <typename scalar_t, typename target_t>
-__global__ void __launch_bounds__(kFamThreads) family_rows_kernel(const scalar_t* __restrict__ preds,
-                                                                  const target_t* __restrict__ target, long long N,
-                                                                  FamilySpec sp) {
-  extern __shared__ __attribute__((aligned(16))) int smem[];
-  int* h = smem;                                                 // this block's partial row
-  float* hf = reinterpret_cast<float*>(smem);                    // (the calibration bins are floats)
-  double* thr_s = reinterpret_cast<double*>(smem + ((sp.part_words + 1) & ~1));
-  float* bnd_s = reinterpret_cast<float*>(thr_s + sp.T);
-  __shared__ int blk_outside;
-  const int C = sp.C, T = sp.T, nb = sp.nb;
-  for (int i = threadIdx.x; i < sp.part_words; i += kFamThreads) h[i] = 0;
-  for (int i = threadIdx.x; i < T; i += kFamThreads) thr_s[i] = sp.thr[i];
-  for (int i = threadIdx.x; i < nb; i += kFamThreads) bnd_s[i] = sp.bounds[i];
-  if (threadIdx.x == 0) blk_outside = 0;
-  __syncthreads();
-  bool outside = false, bad = false;
-  for (long long row = static_cast<long long>(blockIdx.x) * kFamThreads + threadIdx.x; row < N;
-       row += static_cast<long long>(gridDim.x) * kFamThreads) {
-    const scalar_t* r = preds + row * C;
-    float mx = -INFINITY, mf = -INFINITY;  // argmax max (NaN wins) / NaN-ignoring max (the curve's softmax shift)
-    int mi = 0x7fffffff;
-    for (int c = 0; c < C; ++c) {
-      const float v = to_f32(r[c]);
-      outside |= !(v >= 0.f && v <= 1.f);
-      mf = fmaxf(mf, v);
-      if (argmax_better(v, c, mx, mi)) {
-        mx = v;
-        mi = c;
-      }
-    }
-    float s_cal = 0.f;
-    for (int c = 0; c < C; ++c) s_cal += expf(to_f32(r[c]) - mx);
-    float s_cur = s_cal;
-    if (!(mf == mx)) {  // a NaN in the row: the two shifts differ
-      s_cur = 0.f;
-      for (int c = 0; c < C; ++c) s_cur += expf(to_f32(r[c]) - mf);
-    }
-    const long long tv = static_cast<long long>(target[row]);
-    const bool valid = tv >= 0 && tv < C;
-    bad |= !valid;
-    const int t = static_cast<int>(valid ? tv : 0);
-    if (valid && sp.need_cm) atomicAdd(&h[t * C + mi], 1);
-    if (valid && T > 0) {
-      for (int c = 0; c < C; ++c) {
-        const float x = to_f32(r[c]);
-        const double praw = static_cast<double>(x);
-        const double psoft = static_cast<double>(round_to<scalar_t>(expf(x - mf) / s_cur));
-        const int pos = c == t;
-        const int braw = bucket_of(thr_s, T, praw), bsoft = bucket_of(thr_s, T, psoft);
-        atomicAdd(&h[sp.off_cv + ((0 * (T + 1) + braw) * C + c) * 2 + pos], 1);
-        atomicAdd(&h[sp.off_cv + ((1 * (T + 1) + bsoft) * C + c) * 2 + pos], 1);
-      }
-    }
-    if (nb > 0) {
-      float sv = -INFINITY;
-      int si = 0x7fffffff;
-      for (int c = 0; c < C; ++c) {
-        const float p = round_to<scalar_t>(expf(to_f32(r[c]) - mx) / s_cal);
-        if (argmax_better(p, c, sv, si)) {
-          sv = p;
-          si = c;
-        }
-      }
-      const float ar = mi == tv ? 1.f : 0.f, as = si == tv ? 1.f : 0.f;
-      sp.cand[row] = make_float4(mx, ar, sv, as);
-      // (count, Σconf, Σacc) bins of both variants: bin = #{bounds <= conf} - 1
-      const float cv[2] = {round_to<scalar_t>(mx), sv};
-      const float av[2] = {ar, as};
-#pragma unroll
-      for (int var = 0; var < 2; ++var) {
-        int b = -1;
-        for (int k = 0; k < nb; ++k) b += (bnd_s[k] <= cv[var]) ? 1 : 0;
-        if (cv[var] != cv[var]) b = nb - 1;  // NaN: past every bound (torch.bucketize), the reference's last bin
-        if (b < 0) continue;
-        float* dst = hf + sp.off_cb + (var * nb + b) * 3;
-        atomicAdd(dst, 1.f);
-        atomicAdd(dst + 1, cv[var]);
-        atomicAdd(dst + 2, av[var]);
-      }
-    }
-  }
-  if (__any(outside) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(&blk_outside, 1);
-  if (__any(bad) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(sp.err_scratch, kErrTargetOutOfRange);
-  __syncthreads();
-  if (sp.abl & 4) return;
-  for (int i = threadIdx.x; i < sp.off_cb; i += kFamThreads)
-    if (h[i]) atomicAdd(&sp.img[i], h[i]);
-  for (int i = sp.off_cb + threadIdx.x; i < sp.part_words; i += kFamThreads)
-    if (hf[i] != 0.f) atomicAdd(reinterpret_cast<float*>(sp.img) + i, hf[i]);
-  if (threadIdx.x == 0 && blk_outside) atomicOr(&sp.outside[sp.slot], 1);
 }
 
 // ---- VALU (DPP) group exchanges for G <= 16 lanes per row: a row group never straddles a 16-lane DPP row.
@@ -250,32 +158,27 @@ __device__ __forceinline__ float class_order_sum(float e, int C, std::integer_se
 // shuffling the lanes' exponentials in class order into every lane (the order the one-thread-per-row kernel and the
 // members' own kernels use, so the rounded softmax values are the same).
 template <typename scalar_t, typename target_t, int G>
-__global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar_t* __restrict__ preds,
+__global__ void __launch_bounds__(kFamRowThreads) family_rows_g_kernel(const scalar_t* __restrict__ preds,
                                                                     const target_t* __restrict__ target, long long N,
                                                                     FamilySpec sp) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
   int* h = smem;
-  float* hf = reinterpret_cast<float*>(smem);
   double* thr_s = reinterpret_cast<double*>(smem + ((sp.part_words + 1) & ~1));
-  float* bnd_s = reinterpret_cast<float*>(thr_s + sp.T);
   __shared__ int blk_outside;
-  constexpr int R = kFamThreads / G;  // rows per block step
+  constexpr int R = kFamRowThreads / G;  // rows per block step
   const int C = sp.C, T = sp.T, nb = sp.nb;
-  for (int i = threadIdx.x; i < sp.part_words; i += kFamThreads) h[i] = 0;
-  for (int i = threadIdx.x; i < T; i += kFamThreads) thr_s[i] = sp.thr[i];
-  for (int i = threadIdx.x; i < nb; i += kFamThreads) bnd_s[i] = sp.bounds[i];
+  for (int i = threadIdx.x; i < sp.part_words; i += kFamRowThreads) h[i] = 0;
+  for (int i = threadIdx.x; i < T; i += kFamRowThreads) thr_s[i] = sp.thr[i];
   if (threadIdx.x == 0) blk_outside = 0;
   __syncthreads();
   // thresholds on an even grid (within 1e-9 of a step): the short search
   const double t0 = T > 0 ? thr_s[0] : 0.0, tl = T > 0 ? thr_s[T - 1] : 0.0;
   const double inv = T > 1 && tl > t0 ? static_cast<double>(T - 1) / (tl - t0) : 0.0;
   bool off_grid = false;
-  for (int i = threadIdx.x; i < T; i += kFamThreads)
+  for (int i = threadIdx.x; i < T; i += kFamRowThreads)
     off_grid |= !(fabs((thr_s[i] - t0) * inv - static_cast<double>(i)) <= 1e-9);
   const bool on_grid = !__syncthreads_or(off_grid);  // (every thread takes part)
   const bool grid = !(sp.abl & 32) && T > 1 && inv > 0.0 && on_grid;
-  const float b_lo = nb > 0 ? bnd_s[0] : 0.f;
-  const float b_inv = nb > 1 && bnd_s[nb - 1] > b_lo ? static_cast<float>(nb - 1) / (bnd_s[nb - 1] - b_lo) : 0.f;
   const int c = threadIdx.x % G;
   const int gbase = (threadIdx.x & (kWave - 1)) - c;  // the group's first lane in the wave
   const bool has_c = c < C;
@@ -361,7 +264,7 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar
       atomicAdd(&h[sp.off_cv + ((0 * (T + 1) + braw) * C + c) * 2 + pos], 1);
       atomicAdd(&h[sp.off_cv + ((1 * (T + 1) + bsoft) * C + c) * 2 + pos], 1);
     }
-    if (nb > 0 && !(sp.abl & 2)) {
+    if (nb > 0) {
       float sv = mine ? round_to<scalar_t>(e_cal / s_cal) : -INFINITY;
       int si = mine ? c : 0x7fffffff;
       if constexpr (G <= 16) {
@@ -374,39 +277,16 @@ __global__ void __launch_bounds__(kFamThreads) family_rows_g_kernel(const scalar
           if (argmax_better(ov, oi, sv, si)) sv = ov, si = oi;
         }
       }
-      if (live && c < 2) {  // lane 0: the raw top-1 variant, lane 1: the softmax variant
-        const float ar = mi == tv ? 1.f : 0.f, as = si == tv ? 1.f : 0.f;
-        if (c == 0) sp.cand[row] = make_float4(mx, ar, sv, as);
-        const float cvv = c == 0 ? round_to<scalar_t>(mx) : sv;
-        const float avv = c == 0 ? ar : as;
-        // b = #{bounds <= conf} - 1: a guess from the bounds' even grid (linspace), then exact steps (any sorted
-        // bounds) -- the linear scan was nb dependent LDS reads per row (~6 us of this kernel at 15 bins)
-        int b;
-        if (cvv != cvv) {
-          b = nb - 1;  // NaN: past every bound (torch.bucketize), the reference's last bin
-        } else {
-          const float g = (cvv - b_lo) * b_inv;
-          b = g < 0.f ? -1 : (g >= static_cast<float>(nb - 1) ? nb - 1 : static_cast<int>(g));
-          while (b + 1 < nb && bnd_s[b + 1] <= cvv) ++b;
-          while (b >= 0 && bnd_s[b] > cvv) --b;
-        }
-        if (b >= 0) {
-          float* dst = hf + sp.off_cb + (c * nb + b) * 3;
-          atomicAdd(dst, 1.f);
-          atomicAdd(dst + 1, cvv);
-          atomicAdd(dst + 2, avv);
-        }
-      }
+      // both top-1 candidates of the row; the fold keeps the variant the batch-wide decision picks and bins it
+      if (live && c == 0) sp.cand[row] = make_float4(mx, mi == tv ? 1.f : 0.f, sv, si == tv ? 1.f : 0.f);
     }
   }
     }
   if (__any(outside) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(&blk_outside, 1);
   if (__any(bad) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(sp.err_scratch, kErrTargetOutOfRange);
   __syncthreads();
-  for (int i = threadIdx.x; i < sp.off_cb; i += kFamThreads)
+  for (int i = threadIdx.x; i < sp.part_words; i += kFamRowThreads)
     if (h[i]) atomicAdd(&sp.img[i], h[i]);
-  for (int i = sp.off_cb + threadIdx.x; i < sp.part_words; i += kFamThreads)
-    if (hf[i] != 0.f) atomicAdd(reinterpret_cast<float*>(sp.img) + i, hf[i]);
   if (threadIdx.x == 0 && blk_outside) atomicOr(&sp.outside[sp.slot], 1);
 }
 
@@ -424,7 +304,7 @@ __device__ __forceinline__ long long wave_incl_scan_ll(long long v) {
 // wave per class column), then the calibration select blocks (rows), then one calibration-bins block.  Every image
 // word is read, and re-zeroed, by exactly one block.
 __global__ void __launch_bounds__(kFamThreads) family_fold_kernel(FamilySpec sp, long long N, int r_cv, int r_sel,
-                                                                  int n_sel, int r_bins) {
+                                                                  int n_sel) {
   __shared__ long long cmb[kFamMaxC * kFamMaxC];
   __shared__ long long red[4][kFamThreads / kWave];
   const int C = sp.C, T = sp.T, nb = sp.nb;
@@ -535,21 +415,52 @@ __global__ void __launch_bounds__(kFamThreads) family_fold_kernel(FamilySpec sp,
     return;
   }
   if (bid >= r_sel && bid < r_sel + n_sel) {
+    // the calibration member's outputs: the variant the batch-wide decision picked, and its (count, sum conf,
+    // sum acc) bins into the metric's cache -- per block in LDS, then one float atomic per non-zero word (binning
+    // only the kept variant here halved the rows kernel's calibration work; it bins no discarded candidate)
+    __shared__ float bsh[kFoldMaxBins * 3];
+    __shared__ float bnd[kFoldMaxBins];
+    const bool do_bins = sp.bins != nullptr && nb > 0;
+    const bool lds_bins = nb <= kFoldMaxBins;
+    if (do_bins && lds_bins) {
+      for (int i = tid; i < nb * 3; i += kFamThreads) bsh[i] = 0.f;
+      for (int i = tid; i < nb; i += kFamThreads) bnd[i] = sp.bounds[i];
+      __syncthreads();
+    }
+    const float* bb = lds_bins ? bnd : sp.bounds;
+    float* bins = lds_bins ? bsh : sp.bins;
+    const float b_lo = do_bins ? bb[0] : 0.f;
+    const float b_inv = do_bins && nb > 1 && bb[nb - 1] > b_lo ? static_cast<float>(nb - 1) / (bb[nb - 1] - b_lo)
+                                                               : 0.f;
     for (long long i = static_cast<long long>(bid - r_sel) * kFamThreads + tid; i < N;
          i += static_cast<long long>(n_sel) * kFamThreads) {
       const float4 c = sp.cand[i];
-      sp.conf[i] = var ? c.z : c.x;
-      sp.acc[i] = var ? c.w : c.y;
+      const float cv = var ? c.z : c.x, av = var ? c.w : c.y;
+      sp.conf[i] = cv;
+      sp.acc[i] = av;
+      if (do_bins) {
+        // b = #{bounds <= conf} - 1: a guess from the bounds' even grid (linspace), then exact steps (any sorted
+        // bounds); NaN: past every bound (torch.bucketize), the reference's last bin
+        int b;
+        if (cv != cv) {
+          b = nb - 1;
+        } else {
+          const float g = (cv - b_lo) * b_inv;
+          b = g < 0.f ? -1 : (g >= static_cast<float>(nb - 1) ? nb - 1 : static_cast<int>(g));
+          while (b + 1 < nb && bb[b + 1] <= cv) ++b;
+          while (b >= 0 && bb[b] > cv) --b;
+        }
+        if (b >= 0) {
+          atomicAdd(bins + b * 3, 1.f);
+          atomicAdd(bins + b * 3 + 1, cv);
+          atomicAdd(bins + b * 3 + 2, av);
+        }
+      }
     }
-    return;
-  }
-  if (bid == r_bins) {
-    float* f = reinterpret_cast<float*>(sp.img) + sp.off_cb;
-    for (int i = tid; i < nb * 3; i += kFamThreads) {
-      const float v = f[var * nb * 3 + i];
-      if (sp.bins != nullptr && v != 0.f) sp.bins[i] += v;
-      f[i] = 0.f;
-      f[nb * 3 + i] = 0.f;
+    if (do_bins && lds_bins) {
+      __syncthreads();
+      for (int i = tid; i < nb * 3; i += kFamThreads)
+        if (bsh[i] != 0.f) atomicAdd(sp.bins + i, bsh[i]);
     }
   }
 }
@@ -637,24 +548,17 @@ void mc_family_update(const at::Tensor& preds, const at::Tensor& target, at::Ten
   if (N == 0) return;
   sp.off_cv = sp.need_cm ? C * C : 0;
   sp.off_cb = sp.off_cv + (sp.T > 0 ? 2 * (sp.T + 1) * C * 2 : 0);
-  sp.part_words = sp.off_cb + 2 * sp.nb * 3;
-  const size_t lds = static_cast<size_t>((sp.part_words + 1) & ~1) * 4 + static_cast<size_t>(sp.T) * 8 +
-                     static_cast<size_t>(sp.nb) * 4;
+  sp.part_words = sp.off_cb;  // (the calibration bins are binned by the fold, from the kept variant)
+  const size_t lds = static_cast<size_t>((sp.part_words + 1) & ~1) * 4 + static_cast<size_t>(sp.T) * 8;
   TORCH_CHECK(lds <= 64 * 1024, "mc_family_update: partial image exceeds 64 KiB of LDS");
-  // G lanes per row (TM_AMD_FAMILY_G=0: one thread per row); blocks capped so a hot image word takes at most that
-  // many global atomics (TM_AMD_FAMILY_BLOCKS)
-  static const int use_g = [] {
-    const char* e = std::getenv("TM_AMD_FAMILY_G");
-    return e ? std::atoi(e) : 1;
-  }();
+  // G lanes per row; blocks capped so a hot image word takes at most that many global atomics (TM_AMD_FAMILY_BLOCKS)
   static const int max_blocks = [] {
     const char* e = std::getenv("TM_AMD_FAMILY_BLOCKS");
     return e ? std::max(1, std::atoi(e)) : 128;
   }();
   const int G = C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : C <= 32 ? 32 : 64;
-  const int rows_per_blk = use_g ? kFamThreads / G : kFamThreads;
-  const int nblk = static_cast<int>(std::min<long long>((N + rows_per_blk - 1) / rows_per_blk,
-                                                        use_g ? max_blocks : kFamMaxBlocks));
+  const int rows_per_blk = kFamRowThreads / G;
+  const int nblk = static_cast<int>(std::min<long long>((N + rows_per_blk - 1) / rows_per_blk, max_blocks));
   TORCH_CHECK(work.scalar_type() == at::kInt && work.is_contiguous() && work.numel() >= sp.part_words + 3,
               "mc_family_update: work scratch too small");
   TORCH_CHECK(slot == 0 || slot == 1, "mc_family_update: slot 0 / 1");
@@ -681,13 +585,10 @@ void mc_family_update(const at::Tensor& preds, const at::Tensor& target, at::Ten
       const scalar_t* pp = reinterpret_cast<const scalar_t*>(preds.data_ptr());
       auto go = [&](auto gc) {
         constexpr int GG = decltype(gc)::value;
-        hipLaunchKernelGGL((family_rows_g_kernel<scalar_t, target_t, GG>), dim3(nblk), dim3(kFamThreads), lds, s, pp,
-                           tp, N, sp);
+        hipLaunchKernelGGL((family_rows_g_kernel<scalar_t, target_t, GG>), dim3(nblk), dim3(kFamRowThreads), lds, s,
+                           pp, tp, N, sp);
       };
-      if (!use_g)
-        hipLaunchKernelGGL((family_rows_kernel<scalar_t, target_t>), dim3(nblk), dim3(kFamThreads), lds, s, pp, tp, N,
-                           sp);
-      else if (G == 4) go(std::integral_constant<int, 4>{});
+      if (G == 4) go(std::integral_constant<int, 4>{});
       else if (G == 8) go(std::integral_constant<int, 8>{});
       else if (G == 16) go(std::integral_constant<int, 16>{});
       else if (G == 32) go(std::integral_constant<int, 32>{});
@@ -704,16 +605,16 @@ void mc_family_update(const at::Tensor& preds, const at::Tensor& target, at::Ten
   const int n_cv = sp.T > 0 ? (C + kFoldCols - 1) / kFoldCols : 0;
   const int r_sel = r_cv + n_cv;
   const int n_sel = sp.nb > 0 ? static_cast<int>(std::min<long long>((N + kFamThreads - 1) / kFamThreads, 256)) : 0;
-  const int r_bins = r_sel + n_sel;
-  const int grid = r_bins + (sp.nb > 0 ? 1 : 0);
-  hipLaunchKernelGGL(family_fold_kernel, dim3(grid), dim3(kFamThreads), 0, s, sp, N, r_cv, r_sel, n_sel, r_bins);
+  const int grid = r_sel + n_sel;
+  hipLaunchKernelGGL(family_fold_kernel, dim3(grid), dim3(kFamThreads), 0, s, sp, N, r_cv, r_sel, n_sel);
   if (captured) launch_zero_words(sp.outside, 2, s);
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }
 
 // int32 words the scratch `work` must hold
 int64_t mc_family_work_words(int64_t C, bool need_cm, int64_t T, int64_t nb) {
-  return (need_cm ? C * C : 0) + (T > 0 ? 2 * (T + 1) * C * 2 : 0) + 2 * nb * 3 + 3;
+  (void)nb;
+  return (need_cm ? C * C : 0) + (T > 0 ? 2 * (T + 1) * C * 2 : 0) + 3;
 }
 
 }  // namespace tm_amd

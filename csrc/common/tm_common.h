@@ -199,6 +199,18 @@ __device__ __forceinline__ void wave_colsum_f64(double (&v)[NS], int k) {
   wave_colsum64(v, k);
 }
 
+// the same over the sums whose bit is set in `use` only (a wave-uniform mask: unused sums skip their 6 exchange steps)
+template <int NS>
+__device__ __forceinline__ void wave_colsum_f64_masked(double (&v)[NS], int k, int use) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (!((use >> s) & 1)) continue;
+    double one[1] = {v[s]};
+    wave_colsum64(one, k);
+    v[s] = one[0];
+  }
+}
+
 // argmax combine with torch.argmax semantics: NaN wins, then larger value, then smaller index
 __device__ __forceinline__ bool argmax_better(float va, int ia, float vb, int ib) {
   const bool na = va != va, nb = vb != vb;

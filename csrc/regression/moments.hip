@@ -438,7 +438,8 @@ __global__ void __launch_bounds__(kSmallThreads) moments_small_kernel(
     for (int u = 0; u < kSmallUnroll; ++u)
       if (base + static_cast<long long>(u) * kSmallThreads < total) accumulate_pair(acc, pv[u], tv[u], sp, st, mask, eps, pw);
   }
-  wave_colsum_f64(acc, k);  // VALU (DPP / permlane) column sums: LDS-pipe shuffles were most of this kernel
+  // VALU (DPP / permlane) column sums of the requested sums: LDS-pipe shuffles were most of this kernel
+  wave_colsum_f64_masked(acc, k, (mask & ((1 << kMaxSums) - 1)) | (1 << kCOUNT));
 #pragma unroll
   for (int q = 0; q < kMaxSums; ++q)
     if ((((mask >> q) & 1) || q == kCOUNT) && lane < k) wsum[(wid * k + lane) * kMaxSums + q] = acc[q];
@@ -499,7 +500,7 @@ __global__ void __launch_bounds__(kHandoffThreads) moments_handoff_kernel(
   const long long stride = static_cast<long long>(gridDim.x) * kHandoffThreads;
   for (long long i = static_cast<long long>(blockIdx.x) * kHandoffThreads + tid; i < total; i += stride)
     accumulate_pair(acc, preds[i], target[i], sp, st, mask, eps, pw);
-  wave_colsum_f64(acc, k);
+  wave_colsum_f64_masked(acc, k, mask | (1 << kCOUNT));  // the requested sums only (config #5: 8 of 19)
 #pragma unroll
   for (int q = 0; q < kMaxSums; ++q)
     if ((((mask >> q) & 1) || q == kCOUNT) && lane < k) lds[(wid * k + lane) * kMaxSums + q] = acc[q];

@@ -28,6 +28,7 @@ from torchmetrics_amd.detection._coco_eval import (
     cat_states,
     coco_evaluate,
     coco_summarize,
+    summarize_all,
     image_sizes,
     per_class_stats,
 )
@@ -249,6 +250,15 @@ class MeanAveragePrecision(Metric):
 
     # ----------------------------------------------------------------------------------------------- compute
     def _get_classes(self) -> List[int]:
+        memo = self.__dict__.get("_packed_memo")
+        if memo is not None and "classes" in memo:  # (one unique + host read per compute(), not one per use)
+            return memo["classes"]
+        out = self._get_classes_uncached()
+        if memo is not None:
+            memo["classes"] = out
+        return out
+
+    def _get_classes_uncached(self) -> List[int]:
         dev = self._state_device()
         parts = [cat_states(self._packed(n), dev).reshape(-1).long() for n in ("detection_labels", "groundtruth_labels")]
         labels = torch.cat(parts)
@@ -321,7 +331,12 @@ class MeanAveragePrecision(Metric):
             # pycocotools takes mAP at a hard-coded 100 detections (-1 without that threshold); faster-coco-eval
             # uses the largest threshold
             legacy = 100 if self.backend == "pycocotools" else None
-            stats = coco_summarize(ev, self.iou_thresholds, mdt, map_max_det=legacy).to(torch.float32).cpu()
+            ev_cls = None
+            if self.class_metrics:
+                ev_cls = self._evaluate(i_type, micro=False) if self.average == "micro" else ev
+            # the summary and the per-class numbers cross to the host in ONE transfer
+            stats, mp, mr = summarize_all(ev, self.iou_thresholds, mdt, map_max_det=legacy, class_ev=ev_cls)
+            stats = stats.to(torch.float32)
             names = ["map", "map_50", "map_75", "map_small", "map_medium", "map_large", f"mar_{mdt[0]}",
                      f"mar_{mdt[1]}", f"mar_{mdt[2]}", "mar_small", "mar_medium", "mar_large"]
             result.update({f"{prefix}{k}": stats[i] for i, k in enumerate(names)})
@@ -333,9 +348,7 @@ class MeanAveragePrecision(Metric):
                     f"{prefix}scores": ev["scores"].float().cpu(),
                 })
             if self.class_metrics:
-                ev_cls = self._evaluate(i_type, micro=False) if self.average == "micro" else ev
-                mp, mr = per_class_stats(ev_cls, mdt, map_max_det=legacy)
-                map_pc, mar_pc = mp.to(torch.float32).cpu(), mr.to(torch.float32).cpu()
+                map_pc, mar_pc = mp.to(torch.float32), mr.to(torch.float32)
             else:
                 map_pc = torch.tensor([-1.0], dtype=torch.float32)
                 mar_pc = torch.tensor([-1.0], dtype=torch.float32)

@@ -1302,7 +1302,7 @@ def coco_accumulate(tp_all: Tensor, fp_all: Tensor, rank_s: Tensor, score_s: Ten
     tpb = (tp_all.reshape(T * A, n).to(torch.int64) << shifts).sum(0)
     fpb = (fp_all.reshape(T * A, n).to(torch.int64) << shifts).sum(0)
     seg = torch.zeros(K + 1, dtype=torch.int64, device=tp_all.device)
-    torch.cumsum(torch.bincount(cls_s, minlength=K), 0, out=seg[1:])
+    torch.cumsum(histogram(cls_s, K), 0, out=seg[1:])  # (sentinel category K, sorted last: skipped)
     _ops().coco_accumulate(tpb, fpb, rank_s.to(torch.int64).contiguous(), score_s.to(torch.float64).contiguous(), seg,
                            npig.contiguous(), r_thr.contiguous(), torch.tensor(list(max_dets), dtype=torch.int64),
                            int(T), precision, recall, scores)

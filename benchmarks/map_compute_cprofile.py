@@ -31,6 +31,7 @@ def main():
     pr.disable()
     st = pstats.Stats(pr)
     st.sort_stats("tottime").print_stats(35)
+    st.sort_stats("cumtime").print_stats(45)
 
 
 if __name__ == "__main__":

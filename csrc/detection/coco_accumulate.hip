@@ -143,7 +143,46 @@ __global__ void __launch_bounds__(kAccThreads) coco_accumulate_kernel(const int6
   }
 }
 
+// per detection: bit q (= t * A + a) of tpb / fpb set when the detection is a true / false positive of
+// (threshold t, area a) -- matched / unmatched and not ignored; reads the matcher's [T * A, D] flags coalesced
+__global__ void __launch_bounds__(256) coco_pack_kernel(const uint8_t* __restrict__ match,
+                                                        const uint8_t* __restrict__ ig, long long D, int TA,
+                                                        int64_t* __restrict__ tpb, int64_t* __restrict__ fpb) {
+  const long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= D) return;
+  long long tp = 0, fp = 0;
+  for (int q = 0; q < TA; ++q) {
+    const long long e = static_cast<long long>(q) * D + i;
+    if (ig[e]) continue;
+    if (match[e]) tp |= 1LL << q;
+    else fp |= 1LL << q;
+  }
+  tpb[i] = tp;
+  fpb[i] = fp;
+}
+
 }  // namespace
+
+// match / ig uint8 [T, A, D] (coco_match's outputs) -> packed true / false positive bits int64 [D] each
+std::tuple<at::Tensor, at::Tensor> coco_pack_bits(const at::Tensor& match, const at::Tensor& ig) {
+  TM_CHECK_CUDA(match);
+  TM_SAME_DEVICE(match, ig);
+  TM_CHECK_CONTIG(match);
+  TM_CHECK_CONTIG(ig);
+  TORCH_CHECK(match.scalar_type() == at::kByte && ig.scalar_type() == at::kByte && match.dim() == 3 &&
+                  ig.sizes() == match.sizes(),
+              "coco_pack_bits: uint8 [T, A, D] flags");
+  const long long TA = match.size(0) * match.size(1), D = match.size(2);
+  TORCH_CHECK(TA <= 63, "coco_pack_bits: T * A <= 63");
+  at::Tensor tpb = at::empty({D}, match.options().dtype(at::kLong));
+  at::Tensor fpb = at::empty({D}, match.options().dtype(at::kLong));
+  if (D > 0)
+    hipLaunchKernelGGL(coco_pack_kernel, dim3(static_cast<unsigned>((D + 255) / 256)), dim3(256), 0, stream(),
+                       match.data_ptr<uint8_t>(), ig.data_ptr<uint8_t>(), D, static_cast<int>(TA),
+                       tpb.data_ptr<int64_t>(), fpb.data_ptr<int64_t>());
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return {tpb, fpb};
+}
 
 // tpb / fpb int64 [D]: per detection (sorted by category, then score) bit t * A + a set for a true / false positive of
 // (IoU threshold t, area range a); rank int64 [D] (rank within its image and category); score fp64 [D]; seg int64
@@ -202,10 +241,14 @@ void coco_accumulate(const at::Tensor& tpb, const at::Tensor& fpb, const at::Ten
 }
 
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def("coco_pack_bits(Tensor match, Tensor ig) -> (Tensor, Tensor)");
   m.def(
       "coco_accumulate(Tensor tpb, Tensor fpb, Tensor rank, Tensor score, Tensor seg, Tensor npig, Tensor r_thr, "
       "Tensor max_dets, int T, Tensor(a!) precision, Tensor(b!) recall, Tensor(c!) scores) -> ()");
 }
-TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) { m.impl("coco_accumulate", &coco_accumulate); }
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
+  m.impl("coco_pack_bits", &coco_pack_bits);
+  m.impl("coco_accumulate", &coco_accumulate);
+}
 
 }  // namespace tm_amd

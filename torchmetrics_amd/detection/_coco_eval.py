@@ -5,13 +5,15 @@ Behavioural reference: pycocotools ``COCOeval`` as driven by ``S/detection/mean_
 (category, area, max-dets) precision / recall accumulation, the 12-number summary).
 
 MI355X design: every step is a batched device computation over *all* images and categories at once --
-(1) two stable sorts group detections by (image, category) in score order and truncate to the largest max-dets;
-(2) the ``coco_match`` HIP kernel runs every (group, area range, IoU threshold) greedy matching problem in its own
-thread; (3) accumulation: on ROCm one kernel thread per (category, IoU threshold, area, max-dets) walks the
-category's score-sorted detections forward (counts, recall, threshold positions) and backward (exact precision
-envelope), ``csrc/detection/coco_accumulate.hip``; elsewhere a segmented cumulative sum over detections sorted by
-(category, score) for all thresholds / areas at once, a segmented reverse running-max for the envelope and one
-``searchsorted`` + scatter per max-dets; (4) the summary is masked means.  The host only sees the final numbers.
+(1) one radix sort of (group, descending score) keys groups detections by (image, category) in score order, device
+histograms give the group sizes (the largest max-dets value truncates each group in place: no compaction, no host
+sync); (2) the ``coco_match`` HIP kernel runs every (group, area range, IoU threshold) greedy matching problem in its
+own thread; (3) accumulation: on ROCm the matcher's flags are packed into true / false positive bit words and one
+wave per (category, IoU threshold, area, max-dets) sweeps the category's score-sorted detections with ballot counts
+and a suffix-max envelope, ``csrc/detection/coco_accumulate.hip``; elsewhere a segmented cumulative sum over
+detections sorted by (category, score) for all thresholds / areas at once, a segmented reverse running-max for the
+envelope and one ``searchsorted`` + scatter per max-dets; (4) the summary is four masked reductions crossing to the
+host in one transfer.
 """
 from typing import Dict, List, Optional, Sequence, Tuple, Union
 
@@ -32,6 +34,25 @@ def _segment_starts(sorted_keys: Tensor) -> Tensor:
     if n > 1:
         start[1:] = sorted_keys[1:] != sorted_keys[:-1]
     return torch.where(start, idx, torch.zeros_like(idx)).cummax(0).values
+
+
+def _desc_key32(x: Tensor) -> Tensor:
+    """int64 in [0, 2^32): larger for smaller ``x``, ties equal -- the f32 bit pattern made order-preserving (sign
+    flip for positives, full flip for negatives) and reversed; -0 is +0 and NaN sorts last, as in
+    ``argsort(-x)``."""
+    xf = x.float() + 0.0  # (-0.0 + 0.0 = +0.0)
+    b = xf.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    ordered = torch.where(b >= 0x80000000, 0xFFFFFFFF - b, b | 0x80000000)  # ascending in x
+    return torch.where(torch.isnan(xf), 0xFFFFFFFF, 0xFFFFFFFF - ordered)
+
+
+def _group_score_order(group: Tensor, score: Tensor, desc32: Optional[Tensor]) -> Tensor:
+    """Permutation sorting by (group ascending, score descending), ties in input order (stable) -- what
+    ``argsort(-score, stable)`` then ``argsort(group[.], stable)`` give."""
+    if desc32 is not None and group.numel() < (1 << 31):
+        return torch.sort((group << 32) | desc32, stable=True).indices
+    order = torch.argsort(-score, stable=True)
+    return order[torch.argsort(group[order], stable=True)]
 
 
 class Packed:
@@ -138,7 +159,11 @@ def coco_evaluate(
         d_box, g_box = flat(det_boxes, torch.float64, (4,)), flat(gt_boxes, torch.float64, (4,))
         d_area = d_box[:, 2] * d_box[:, 3]
         g_mask_area = g_box[:, 2] * g_box[:, 3]
-    d_score = flat(det_scores, torch.float64)
+    d_score_raw = cat_states(det_scores, dev)
+    d_score = d_score_raw.to(torch.float64)
+    # descending-score sort keys: 32-bit scores (the usual f32 / f16 / bf16) map to an order-preserving uint32, so
+    # (group, -score) is ONE int64 radix key per sort instead of two stable sorts; fp64 scores keep the two sorts
+    desc32 = _desc_key32(d_score_raw) if d_score_raw.dtype in (torch.float32, torch.float16, torch.bfloat16) else None
     g_crowd_all = flat(gt_crowds, torch.long).clamp(0, 1).to(torch.uint8)
     g_area_in = flat(gt_areas, torch.float64)
     g_area = torch.where(g_area_in > 0, g_area_in, g_mask_area)
@@ -150,8 +175,7 @@ def coco_evaluate(
 
     # (1) detections grouped by (image, category), score-descending (stable); each group's first max_dets[-1] are
     # matched (the rest keep their slots, with a rank the accumulation skips)
-    order = torch.argsort(-d_score, stable=True)
-    order = order[torch.argsort(d_group[order], stable=True)]
+    order = _group_score_order(d_group, d_score, desc32)
     grp_s = d_group[order]
     det_cnt_all = ops.histogram(grp_s, n_groups)  # (sentinel keys skipped)
     det_start = torch.cumsum(det_cnt_all, 0) - det_cnt_all
@@ -180,12 +204,8 @@ def coco_evaluate(
     # sentinel detections sort into a last category K that no kernel reads
     cls_k = torch.where(valid_s, d_cls[order], K)
     score_k = d_score[order]
-    o = torch.argsort(-score_k, stable=True)
-    o = o[torch.argsort(cls_k[o], stable=True)]
+    o = _group_score_order(cls_k, score_k, desc32[order] if desc32 is not None else None)
     cls_s, rank_s, score_s = cls_k[o], rank[o], score_k[o]
-    match = dt_match[..., o].bool()
-    ig = dt_ig[..., o].bool()
-    tp_all, fp_all = match & ~ig, ~match & ~ig  # [T, A, D]
     g_ig = (g_crowd.bool()[None, :] | (g_area[None, :] < areas[:, :1]) | (g_area[None, :] > areas[:, 1:]))  # [A, G]
     # non-ignored ground truths per (area, category): one device histogram (an fp64 index_add here serialised on
     # 80 addresses: 0.37 ms)
@@ -194,10 +214,13 @@ def coco_evaluate(
     has_gt = npig > 0
     n = cls_s.numel()
     # ROCm: one wave per (category, threshold, area, max-dets), csrc/detection/coco_accumulate.hip
-    done = bool(n) and ops.coco_accumulate(tp_all, fp_all, rank_s, score_s, cls_s, npig, r_thr, max_dets, precision,
-                                           recall, scores_out)
+    done = bool(n) and ops.coco_accumulate(dt_match, dt_ig, o, rank_s, score_s, cls_s, npig, r_thr, max_dets,
+                                           precision, recall, scores_out)
     if n and not done:
         # (the batched torch path) the sentinel detections go: every segment below is a real category
+        match = dt_match[..., o].bool()
+        ig = dt_ig[..., o].bool()
+        tp_all, fp_all = match & ~ig, ~match & ~ig  # [T, A, D]
         sel = cls_s < K
         cls_s, rank_s, score_s = cls_s[sel], rank_s[sel], score_s[sel]
         tp_all, fp_all = tp_all[..., sel], fp_all[..., sel]

@@ -1288,20 +1288,22 @@ def coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, g
                            iou_pre, iou_off)
 
 
-def coco_accumulate(tp_all: Tensor, fp_all: Tensor, rank_s: Tensor, score_s: Tensor, cls_s: Tensor, npig: Tensor,
-                    r_thr: Tensor, max_dets: Sequence[int], precision: Tensor, recall: Tensor, scores: Tensor) -> bool:
+def coco_accumulate(dt_match: Tensor, dt_ig: Tensor, o: Tensor, rank_s: Tensor, score_s: Tensor, cls_s: Tensor,
+                    npig: Tensor, r_thr: Tensor, max_dets: Sequence[int], precision: Tensor, recall: Tensor,
+                    scores: Tensor) -> bool:
     """COCO accumulation of every (category, IoU threshold, area, max-dets) in one launch
-    (``csrc/detection/coco_accumulate.hip``).  ``tp_all`` / ``fp_all`` bool ``[T, A, D]`` over detections sorted by
-    (category, score); fills ``precision`` / ``scores`` ``[T, R, K, A, M]`` and ``recall`` ``[T, K, A, M]`` in place.
-    Returns False (nothing written) where the kernel does not apply: CPU, T * A > 63 or more than 8 max-dets values."""
-    T, A, n = tp_all.shape
+    (``csrc/detection/coco_accumulate.hip``).  ``dt_match`` / ``dt_ig`` uint8 ``[T, A, D]`` from :func:`coco_match`,
+    ``o`` the permutation to detections sorted by (category, score) (``cls_s`` / ``rank_s`` / ``score_s`` already in
+    that order; category ``K`` = sentinel, skipped); fills ``precision`` / ``scores`` ``[T, R, K, A, M]`` and
+    ``recall`` ``[T, K, A, M]`` in place.  Returns False (nothing written) where the kernel does not apply: CPU,
+    T * A > 63 or more than 8 max-dets values."""
+    T, A, n = dt_match.shape
     K = npig.shape[1]
-    if not tp_all.is_cuda or T * A > 63 or len(max_dets) > 8 or n == 0:
+    if not dt_match.is_cuda or T * A > 63 or len(max_dets) > 8 or n == 0:
         return False
-    shifts = torch.arange(T * A, device=tp_all.device, dtype=torch.int64)[:, None]
-    tpb = (tp_all.reshape(T * A, n).to(torch.int64) << shifts).sum(0)
-    fpb = (fp_all.reshape(T * A, n).to(torch.int64) << shifts).sum(0)
-    seg = torch.zeros(K + 1, dtype=torch.int64, device=tp_all.device)
+    tpb, fpb = _ops().coco_pack_bits(dt_match.contiguous(), dt_ig.contiguous())  # (matcher order, coalesced)
+    tpb, fpb = tpb[o], fpb[o]
+    seg = torch.zeros(K + 1, dtype=torch.int64, device=dt_match.device)
     torch.cumsum(histogram(cls_s, K), 0, out=seg[1:])  # (sentinel category K, sorted last: skipped)
     _ops().coco_accumulate(tpb, fpb, rank_s.to(torch.int64).contiguous(), score_s.to(torch.float64).contiguous(), seg,
                            npig.contiguous(), r_thr.contiguous(), torch.tensor(list(max_dets), dtype=torch.int64),

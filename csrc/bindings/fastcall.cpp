@@ -44,6 +44,7 @@ void stat_reduce(const at::Tensor& tp, const at::Tensor& fp, const at::Tensor& t
                  at::Tensor out, int64_t kind, int64_t average, bool multilabel, double beta);
 void launch_probe(at::Tensor flag);
 int64_t read_word_sync(const at::Tensor& word);
+std::vector<int64_t> read_words(const at::Tensor& words, const at::Tensor& anchor, int64_t spin_us);
 bool mc_stats_direct(const at::Tensor& preds, const at::Tensor& target, at::Tensor tp, at::Tensor fp, at::Tensor tn,
                      at::Tensor fn, at::Tensor flag, int64_t num_classes);
 void mc_family_update(const at::Tensor& preds, const at::Tensor& target, at::TensorList cm, at::TensorList st,
@@ -1216,7 +1217,41 @@ PyObject* read_word(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   return PyLong_FromLongLong(v);
 }
 
+// read_words(table: CPU int64 [n, 2], anchor: Tensor, spin_us: int) -> list[int]: every status word of a collection
+// compute() through one gather kernel + a sequence-number spin on mapped host memory (compute_tasks.hip), the GIL
+// released while it waits
+PyObject* read_words_fc(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 3 || !THPVariable_Check(args[0]) || !THPVariable_Check(args[1]) || !PyLong_Check(args[2])) {
+    PyErr_SetString(PyExc_TypeError, "read_words(table: Tensor, anchor: Tensor, spin_us: int)");
+    return nullptr;
+  }
+  const at::Tensor table = THPVariable_Unpack(args[0]);
+  const at::Tensor anchor = THPVariable_Unpack(args[1]);
+  const int64_t spin = PyLong_AsLongLong(args[2]);
+  std::vector<int64_t> v;
+  std::string err;
+  Py_BEGIN_ALLOW_THREADS
+  try {
+    v = tm_amd::read_words(table, anchor, spin);
+  } catch (const c10::Error& e) {
+    err = e.what_without_backtrace();
+  } catch (const std::exception& e) {
+    err = e.what();
+  }
+  Py_END_ALLOW_THREADS
+  if (!err.empty()) {
+    PyErr_SetString(PyExc_RuntimeError, err.c_str());
+    return nullptr;
+  }
+  PyObject* out = PyList_New(static_cast<Py_ssize_t>(v.size()));
+  if (out == nullptr) return nullptr;
+  for (size_t i = 0; i < v.size(); ++i) PyList_SET_ITEM(out, static_cast<Py_ssize_t>(i), PyLong_FromLongLong(v[i]));
+  return out;
+}
+
 PyMethodDef kFactoryMethods[] = {
+    {"read_words", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&read_words_fc)), METH_FASTCALL,
+     "every status word of a collection compute() in one gather kernel + a sequence spin on mapped host memory"},
     {"read_word", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&read_word)), METH_FASTCALL,
      "an int32 device word read through mapped host memory after a stream sync"},
     {"stats_updater", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(&make_stats_updater)),

@@ -8,7 +8,10 @@
 // Descriptors travel by value in the kernel arguments (no device table to keep alive; capturable into a HIP graph).
 #include "common/compute_bodies.h"
 
+#include <atomic>
+#include <chrono>
 #include <mutex>
+#include <vector>
 
 namespace tm_amd {
 namespace {
@@ -125,6 +128,28 @@ __global__ void __launch_bounds__(kMaxWords) gather_words_kernel(WordTable tab, 
   __threadfence_system();
 }
 
+// read_words: the gather above, then a sequence number stored after every word is visible to the host (each storing
+// lane's system-scope fence, the block barrier, then lane 0's store)
+__global__ void __launch_bounds__(kMaxWords) gather_words_seq_kernel(WordTable tab, int* __restrict__ dst,
+                                                                      int* __restrict__ seq, int seq_val) {
+  const int i = threadIdx.x;
+  if (i < tab.n) {
+    int v = 0;
+    switch (tab.code[i]) {
+      case 0: v = *static_cast<const int*>(tab.p[i]); break;
+      case 1: v = *static_cast<const float*>(tab.p[i]) != 0.f ? 1 : 0; break;
+      case 2: v = *static_cast<const double*>(tab.p[i]) != 0.0 ? 1 : 0; break;
+      case 3: v = *static_cast<const int64_t*>(tab.p[i]) != 0 ? 1 : 0; break;
+      default: v = *static_cast<const uint8_t*>(tab.p[i]) != 0 ? 1 : 0; break;
+    }
+    dst[i] = v;
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (i == 0) *reinterpret_cast<volatile int*>(seq) = seq_val;
+  __threadfence_system();
+}
+
 // one word of device memory copied into mapped host memory (vector store by lane 0) -- read_word_sync
 __global__ void __launch_bounds__(64) publish_word_kernel(const int* __restrict__ src, int* __restrict__ dst) {
   if (threadIdx.x == 0) dst[0] = src[0];
@@ -186,6 +211,68 @@ void gather_words(const at::Tensor& words, int64_t dst, const at::Tensor& anchor
   }
   hipLaunchKernelGGL(gather_words_kernel, dim3(1), dim3(kMaxWords), 0, stream(), tab, reinterpret_cast<int*>(dst));
   C10_HIP_KERNEL_LAUNCH_CHECK();
+}
+
+// Every status word of a collection compute() in ONE native call: the gather kernel stores the words and then a
+// sequence number into mapped pinned host memory; the host spins on the sequence number (the kernel is the last
+// work of the stream, typically landing within a few us) instead of a hipStreamSynchronize round trip, and falls
+// back to that sync after `spin_us` (a busy queue ahead of it).  words: CPU int64 [n, 2] (pointer, code) rows as for
+// gather_words; anchor: a tensor on the device (device + current stream).  The caller releases the GIL.
+std::vector<int64_t> read_words(const at::Tensor& words, const at::Tensor& anchor, int64_t spin_us) {
+  TM_CHECK_CUDA(anchor);
+  TORCH_CHECK(!words.is_cuda() && words.scalar_type() == at::kLong && words.dim() == 2 && words.size(1) == 2,
+              "read_words: words must be a CPU int64 [n, 2] table");
+  const int n = static_cast<int>(words.size(0));
+  TORCH_CHECK(n >= 1 && n <= kMaxWords, "read_words: 1..", kMaxWords, " words");
+  const int dev = anchor.get_device();
+  TORCH_CHECK(dev >= 0 && dev < 64, "read_words: device index");
+  static std::mutex mu;
+  static int* host[64] = {};
+  static int* mapped[64] = {};
+  static int counter[64] = {};
+  std::lock_guard<std::mutex> lock(mu);  // one buffer per device: serialise readers of one device
+  if (host[dev] == nullptr) {
+    int* h = nullptr;
+    TORCH_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h), (kMaxWords + 64) * sizeof(int),
+                              hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess,
+                "read_words: pinned allocation failed");
+    void* d = nullptr;
+    TORCH_CHECK(hipHostGetDevicePointer(&d, h, 0) == hipSuccess, "read_words: unmapped pinned memory");
+    host[dev] = h;
+    mapped[dev] = static_cast<int*>(d);
+    h[kMaxWords] = 0;
+  }
+  const at::Tensor w = words.contiguous();
+  const int64_t* r = w.data_ptr<int64_t>();
+  WordTable tab{};
+  tab.n = n;
+  for (int k = 0; k < n; ++k) {
+    tab.p[k] = reinterpret_cast<const void*>(r[2 * k]);
+    tab.code[k] = static_cast<int>(r[2 * k + 1]);
+    TORCH_CHECK(tab.p[k] != nullptr && tab.code[k] >= 0 && tab.code[k] <= 4, "read_words: bad word ", k);
+  }
+  int seq_val = counter[dev] = (counter[dev] % 0x3fffffff) + 1;
+  volatile int* seq = host[dev] + kMaxWords;
+  hipStream_t s = stream();
+  hipLaunchKernelGGL(gather_words_seq_kernel, dim3(1), dim3(kMaxWords), 0, s, tab, mapped[dev], mapped[dev] + kMaxWords,
+                     seq_val);
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  const auto t0 = std::chrono::steady_clock::now();
+  bool seen = false;
+  while (true) {
+    if (*seq == seq_val) {
+      seen = true;
+      break;
+    }
+    if (std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count() >
+        spin_us)
+      break;
+  }
+  if (!seen) TORCH_CHECK(hipStreamSynchronize(s) == hipSuccess, "read_words: stream synchronisation failed");
+  std::atomic_thread_fence(std::memory_order_acquire);
+  std::vector<int64_t> out(n);
+  for (int k = 0; k < n; ++k) out[k] = static_cast<volatile int*>(host[dev])[k];
+  return out;
 }
 
 // device-side address of pinned host memory (kernels write it directly)

@@ -193,3 +193,32 @@ def test_regression_collection_update_replay():
     # a bad shape still raises the member's error (the replay declines other shapes)
     with pytest.raises(RuntimeError):
         gr.update(torch.randn(10, device=DEV), torch.randn(11, device=DEV))
+
+
+def test_dropped_results_reuse_the_output_buffer_held_ones_never_change():
+    """A per-step compute() whose results were dropped reuses the plan's output buffer (no view construction); a kept
+    result, a kept VIEW of a result and a member's cached compute() value each force a fresh buffer instead, so no
+    handed-out tensor ever changes (utils/fused_compute.py CollectionPlan.run)."""
+    gc, cc = _cls().to(DEV), _cls()
+    ptrs = []
+    kept, kept_view, snap, snap_view = None, None, None, None
+    for i in range(8):
+        p, t, _, _ = _batch(i)
+        gc.update(p.to(DEV), t.to(DEV))
+        cc.update(p, t)
+        res = gc.compute()
+        _check(res, cc.compute())
+        ptrs.append(res["acc"].data_ptr())
+        if i == 3:
+            kept, snap = res["f1"], res["f1"].clone()
+        if i == 5:
+            kept_view, snap_view = res["mcc"].reshape(-1)[0:1], res["mcc"].reshape(-1)[0:1].clone()
+        del res
+    assert ptrs[2] == ptrs[1], "dropped results: the buffer is reused"
+    assert ptrs[4] != ptrs[3], "a kept result forces a fresh buffer"
+    assert ptrs[6] != ptrs[5], "a kept view of a result forces a fresh buffer"
+    assert torch.equal(kept, snap) and torch.equal(kept_view, snap_view)
+    # a second compute() without an update returns the members' cached values: the buffer holding them stays
+    a = gc.compute()
+    b = gc.compute()
+    assert torch.equal(a["acc"], b["acc"])

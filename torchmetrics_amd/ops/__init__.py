@@ -123,6 +123,20 @@ def read_word(word: Tensor) -> int:
     return int(word.reshape(-1)[0].item())
 
 
+READ_WORDS_SPIN_US = 2000  # how long read_words spins before a blocking stream sync (a busy queue ahead of it)
+
+
+def read_words(table: Tensor, anchor: Tensor) -> Optional[List[int]]:
+    """Every word of ``table`` (CPU int64 ``[n <= 128, 2]`` rows of (device pointer, code), see
+    ``csrc/common/compute_tasks.hip`` read_words) through one gather kernel into mapped host memory and a spin on the
+    sequence number it stores after them; None without the native module (the caller takes the gather + sync)."""
+    mod = _fast_mod if _fast_mod is not None else (_fast() if native_available() else None)
+    fn = getattr(mod, "read_words", None) if mod is not None else None
+    if fn is None or not anchor.is_cuda:
+        return None
+    return fn(table, anchor, READ_WORDS_SPIN_US)
+
+
 def sole_ref(d: dict, key: Any) -> bool:
     """Whether ``d[key]`` is a tensor whose Python object is referenced by ``d`` alone (``_sole_ref`` in
     ``csrc/bindings/fastcall.cpp``: the exact strong-reference count, read from C).  Without the native module:

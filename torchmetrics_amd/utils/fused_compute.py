@@ -23,7 +23,9 @@ The plan is rebuilt when the collection's members change (``add_metrics``), when
 device / dtype changes (``Metric._cfg_version``), or when a state's shape / dtype no longer matches the recording.
 ``TORCHMETRICS_AMD_FUSED_COMPUTE=0`` turns it off.
 """
+import operator
 import os
+import sys
 import warnings
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -66,6 +68,8 @@ class CollectionPlan:
         self._seen: Optional[Tuple[Any, ...]] = None  # the state objects valid() last checked in full
         self._last_ptrs: Optional[Tuple[int, ...]] = None
         self._same = False
+        self._reuse: Optional["_Outputs"] = None
+        self._ver_keys: Optional[tuple] = None
         self._build(members)
 
     # ------------------------------------------------------------------------------------------------- record
@@ -226,13 +230,18 @@ class CollectionPlan:
 
     # ------------------------------------------------------------------------------------------------- replay
     def valid(self) -> bool:
-        for f in self.fused:
-            if f.metric.__dict__.get("_cfg_version", 0) != f.version:
+        ver = self._ver_keys
+        if ver is None:
+            ver = self._ver_keys = ([f.metric.__dict__ for f in self.fused], [f.version for f in self.fused],
+                                    [(m.__dict__, a) for m, a, _, _ in self.state_sig])
+        for d, v in zip(ver[0], ver[1]):
+            if d.get("_cfg_version", 0) != v:
                 return False
         # the same state objects as at the last full check (the common case: states updated in place): valid, and
         # their memory has not moved (run() keeps the pointers it patched last time)
-        cur = tuple(m.__dict__.get(a) for m, a, _, _ in self.state_sig)
-        if self._seen is not None and len(cur) == len(self._seen) and all(x is y for x, y in zip(cur, self._seen)):
+        cur = [d.get(a) for d, a in ver[2]]
+        seen = self._seen
+        if seen is not None and len(cur) == len(seen) and all(map(operator.is_, cur, seen)):
             self._same = True
             return True
         self._same = False
@@ -243,31 +252,66 @@ class CollectionPlan:
         return True
 
     def run(self) -> Tuple[Dict[str, Any], Dict[str, List[Tuple[Tensor, str, Any]]]]:
-        """One launch for every fused member: ``({key: result}, {key: deferred checks})``."""
+        """One launch for every fused member: ``({key: result}, {key: deferred checks})``.
+
+        The output buffer and the result views of the last run are reused when nothing outside this plan still
+        refers to them (every view object back at the reference count it had when built, and no other tensor on
+        the buffer's storage): a per-step ``compute()`` whose results were logged and dropped then costs one launch
+        and no view construction (13 ``as_strided`` views were ~20 us of host time per compute of config #5).  A
+        result the caller kept -- or a member's cached ``compute()`` value -- makes the plan build a fresh buffer, so
+        a handed-out result never changes."""
         flat = self.flat_np
         if not (self._same and self._last_ptrs is not None):
             ptrs = tuple(m.__dict__[a].data_ptr() for m, a in self.in_pairs)
             if ptrs != self._last_ptrs:  # states moved (reset, sync, .to()): re-point the input slots
                 flat[self.in_idx] = np.asarray(ptrs, dtype=np.int64)[self.slot_pair] + self.in_off
                 self._last_ptrs = ptrs
-        raw = torch.empty(self.out_bytes_total, dtype=torch.uint8, device=self.device)
-        flat[self.out_idx] = self.out_rel + raw.data_ptr()
-        bufs = {dt: raw[off : off + nb].view(dt) for dt, off, nb in self.out_layout}
-        mx = 32
+        c = self._reuse
+        if c is None or not c.idle():
+            raw = torch.empty(self.out_bytes_total, dtype=torch.uint8, device=self.device)
+            flat[self.out_idx] = self.out_rel + raw.data_ptr()
+            bufs = {dt: raw[off : off + nb].view(dt) for dt, off, nb in self.out_layout}
+            strided = torch.as_strided
+            leaves: List[List[Tensor]] = []
+            checks: Dict[str, List[Tuple[Tensor, str, Any]]] = {}
+            for f in self.fused:
+                # (as_strided offsets count from the shared storage's start: add each dtype view's own offset)
+                leaves.append([strided(bufs[dt], shape, stride, bufs[dt].storage_offset() + off)
+                               for dt, off, shape, stride in f.leaves])
+                if f.checks:
+                    checks[f.key] = [(bufs[dt][off : off + 1], msg, exc) for dt, off, msg, exc in f.checks]
+            c = self._reuse = _Outputs(raw, bufs, leaves, checks)
         tasks = ops._ops().compute_tasks
+        mx = 32
         for i in range(0, self.rows.shape[0], mx):
-            tasks(self.rows[i : i + mx], raw, self.lds)
-        results: Dict[str, Any] = {}
-        checks: Dict[str, List[Tuple[Tensor, str, Any]]] = {}
-        strided = torch.as_strided
-        for f in self.fused:
-            # (as_strided offsets count from the shared storage's start: add each dtype view's own offset)
-            leaves = [strided(bufs[dt], shape, stride, bufs[dt].storage_offset() + off)
-                      for dt, off, shape, stride in f.leaves]
-            results[f.key] = _rebuild(f.spec, leaves)
-            if f.checks:
-                checks[f.key] = [(bufs[dt][off : off + 1], msg, exc) for dt, off, msg, exc in f.checks]
-        return results, checks
+            tasks(self.rows[i : i + mx], c.raw, self.lds)
+        results = {f.key: _rebuild(f.spec, lv) for f, lv in zip(self.fused, c.leaves)}
+        return results, c.checks
+
+
+class _Outputs:
+    """One run's output buffer and the views handed out from it, with the reference counts they have while only
+    the plan holds them (see :meth:`CollectionPlan.run`)."""
+
+    __slots__ = ("raw", "bufs", "leaves", "checks", "storage", "use", "rc")
+
+    def __init__(self, raw: Tensor, bufs: Dict[torch.dtype, Tensor], leaves: List[List[Tensor]],
+                 checks: Dict[str, List[Tuple[Tensor, str, Any]]]) -> None:
+        self.raw, self.bufs, self.leaves, self.checks = raw, bufs, leaves, checks
+        self.storage = raw.untyped_storage()
+        self.use = torch._C._storage_Use_Count(self.storage._cdata)
+        # (counted the way idle() counts: the list's reference + the call's argument, no loop variable / zip tuple)
+        self.rc = [[sys.getrefcount(lv[i]) for i in range(len(lv))] for lv in leaves]
+
+    def idle(self) -> bool:
+        if torch._C._storage_Use_Count(self.storage._cdata) != self.use:
+            return False  # another tensor on the buffer (a view of a result, a check slice kept alive ...)
+        getrc = sys.getrefcount
+        for lv, rc in zip(self.leaves, self.rc):
+            for i in range(len(lv)):
+                if getrc(lv[i]) != rc[i]:
+                    return False  # a result (or a member's cached compute() value) is still held
+        return True
 
 
 def _squeeze(v: Any) -> Any:

@@ -727,7 +727,11 @@ __device__ __attribute__((aligned(16))) uint32_t g_zero_chunk[4];  // the DMA so
 // round-5 log): a 4-deep / 2-deep ring of 32-wide k-chunks (no faster; at 165 VGPRs two 512-thread blocks never share
 // a CU), four waves of 128 x 128 per wave (512 VGPRs, spills: 10-20 % slower), and a persistent grid-stride form that
 // overlaps a tile's stores with the next tile's DMA (within 5 %).
-template <int EPI, typename T, int TM>
+// GRAN: bytes per DMA lane.  16 (the fast form) needs 16-byte aligned rows (D % 8 == 0, 16-byte aligned bases);
+// rows of any other width are staged in place into the SAME swizzled LDS layout, the K tail zero-filled element by
+// element -- no padded copy and no fp32 upcast of the operands: 4-byte DMA lanes for even widths (4x the
+// instructions), register staging of whole 16-byte slots for odd ones (GRAN 2).
+template <int EPI, typename T, int TM, int GRAN = 16>
 __global__ __launch_bounds__(TM == 256 ? 512 : 256) void gemm_nt_h16_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ Y, int N, int M, int D, long long bx, long long by,
     int tiles_m, EpiParams ep) {
@@ -778,13 +782,54 @@ __global__ __launch_bounds__(TM == 256 ? 512 : 256) void gemm_nt_h16_kernel(
     uint16_t* sa = sh + buf * kStage;
     uint16_t* sb = sa + TM * KC;
     const int k0 = kc * KC;
+    if constexpr (GRAN == 16) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool in = k0 + kof[q] < D;
-      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcA[q] + k0 : zero), (lds_t*)(sa + (32 * wave + 8 * q) * KC),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcB[q] + k0 : zero), (lds_t*)(sb + (32 * wave + 8 * q) * KC),
-                                       16, 0, 0);
+      for (int q = 0; q < 4; ++q) {
+        const bool in = k0 + kof[q] < D;
+        __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcA[q] + k0 : zero), (lds_t*)(sa + (32 * wave + 8 * q) * KC),
+                                         16, 0, 0);
+        __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcB[q] + k0 : zero), (lds_t*)(sb + (32 * wave + 8 * q) * KC),
+                                         16, 0, 0);
+      }
+    } else if constexpr (GRAN == 2) {
+      // odd widths: 2-byte rows.  The LDS-DMA forms below 4 bytes do not pack lanes 2 bytes apart, so these rows
+      // are register-staged: each lane assembles whole 16-byte slots (8 elements, element-wise K bound) and writes
+      // them to their swizzled LDS place; the barrier protocol is unchanged (the writes land before the barrier
+      // that precedes the reads)
+      constexpr int kSlots = TM * (KC / 8) / NT;  // slots per thread and operand
+#pragma unroll
+      for (int v = 0; v < kSlots; ++v) {
+        const int id = tid + v * NT;
+        const int rr = id >> 3, slot = id & 7;
+        const int k = k0 + 8 * (slot ^ ((rr >> 1) & 7));
+        const uint16_t* pa = xrow(min(row0 + rr, N - 1)) + k;
+        const uint16_t* pb = yrow(min(col0 + rr, M - 1)) + k;
+        uint16_t ea[8], eb[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bool in = k + e < D;
+          ea[e] = in ? pa[e] : uint16_t(0);
+          eb[e] = in ? pb[e] : uint16_t(0);
+        }
+        *reinterpret_cast<uint4*>(sa + rr * KC + 8 * slot) = __builtin_bit_cast(uint4, ea);
+        *reinterpret_cast<uint4*>(sb + rr * KC + 8 * slot) = __builtin_bit_cast(uint4, eb);
+      }
+    } else {
+      // E elements per lane, LPR lanes per 64-element LDS row, RPI rows per instruction: lane l of instruction q
+      // fills element slot (l % LPR) * E of row 32 w + RPI q + l / LPR, i.e. logical chunk slot ^ swizzle(row)
+      constexpr int E = GRAN / 2, LPR = KC / E, RPI = 64 / LPR;
+      const int le = (lane % LPR) * E;
+      const int slot = le >> 3, within = le & 7;
+#pragma unroll 4
+      for (int q = 0; q < 32 / RPI; ++q) {
+        const int rr = 32 * wave + RPI * q + lane / LPR;
+        const int k = k0 + 8 * (slot ^ ((rr >> 1) & 7)) + within;
+        const bool in = k < D;  // (E = 2 only with D even: k and k + 1 are both inside or both past D)
+        const uint16_t* pa = in ? xrow(min(row0 + rr, N - 1)) + k : zero;
+        const uint16_t* pb = in ? yrow(min(col0 + rr, M - 1)) + k : zero;
+        __builtin_amdgcn_global_load_lds((glb_t*)pa, (lds_t*)(sa + (32 * wave + RPI * q) * KC), 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((glb_t*)pb, (lds_t*)(sb + (32 * wave + RPI * q) * KC), 4, 0, 0);
+      }
     }
   };
 
@@ -943,6 +988,23 @@ void launch(const at::Tensor& x, const at::Tensor& y, int batches, long long bx,
 template <int EPI, typename T>
 void launch_h16(const at::Tensor& x, const at::Tensor& y, int batches, long long bx, long long by, int N, int M, int D,
                 const EpiParams& ep, bool big) {
+  // DMA granularity from the rows' alignment (D and the base addresses): 16-byte rows take the fast form
+  const uintptr_t align = reinterpret_cast<uintptr_t>(x.data_ptr()) | reinterpret_cast<uintptr_t>(y.data_ptr());
+  const int gran = (D % 8 == 0 && align % 16 == 0) ? 16 : ((D % 2 == 0 && align % 4 == 0) ? 4 : 2);
+  if (gran != 16) {  // (odd widths: the 128 x 128 tile)
+    const int tiles_n = (N + 127) / 128, tiles_m = (M + 127) / 128;
+    const int per = (tiles_n * tiles_m + 7) / 8;
+    const size_t lds = 2ull * 2 * 128 * 64 * sizeof(uint16_t);
+    const auto* xp = reinterpret_cast<const uint16_t*>(x.data_ptr());
+    const auto* yp = reinterpret_cast<const uint16_t*>(y.data_ptr());
+    if (gran == 4)
+      hipLaunchKernelGGL((gemm_nt_h16_kernel<EPI, T, 128, 4>), dim3(per * 8, 1, batches), dim3(256), lds, stream(),
+                         xp, yp, N, M, D, bx, by, tiles_m, ep);
+    else
+      hipLaunchKernelGGL((gemm_nt_h16_kernel<EPI, T, 128, 2>), dim3(per * 8, 1, batches), dim3(256), lds, stream(),
+                         xp, yp, N, M, D, bx, by, tiles_m, ep);
+    return;
+  }
   const int tm = big ? 256 : 128;
   const int tiles_n = (N + tm - 1) / tm, tiles_m = (M + tm - 1) / tm;
   const int per = (tiles_n * tiles_m + 7) / 8;
@@ -1005,9 +1067,11 @@ at::Tensor gemm_nt(const at::Tensor& x, const at::Tensor& y, int64_t kind, const
     ep.iy = idx_y->data_ptr<int32_t>();
   }
   TORCH_CHECK(y.size(-1) == D, "gemm_nt: inner dimension mismatch");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
-              "gemm_nt: 16-byte aligned operands");
-  TORCH_CHECK(D % (h16 ? 8 : 4) == 0, "gemm_nt: D must be a multiple of 16 bytes (4 fp32 / 8 16-bit elements)");
+  // fp32 operands: 16-byte rows (the fp32 kernels' vector staging); 16-bit operands: any width / 2-byte alignment
+  // (launch_h16 picks the DMA granularity)
+  TORCH_CHECK(h16 || (reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+                      reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0 && D % 4 == 0),
+              "gemm_nt: fp32 operands need 16-byte aligned rows (D % 4 == 0)");
   TORCH_CHECK(D > 0 && N > 0 && M > 0, "gemm_nt: empty operands");
   TORCH_CHECK(static_cast<long long>(N) * M * B < (1LL << 40), "gemm_nt: output too large");
   // 16-bit operands: the 256 x 256 tile once it alone fills the chip (256 tiles), else 128 x 128
@@ -1015,8 +1079,11 @@ at::Tensor gemm_nt(const at::Tensor& x, const at::Tensor& y, int64_t kind, const
     const char* e = std::getenv("TM_AMD_GEMM16_BIG");
     return e ? std::atoi(e) : -1;
   }();
-  const bool big16 = big16_env >= 0 ? big16_env == 1
-                                    : static_cast<long long>((N + 255) / 256) * ((M + 255) / 256) * B >= 256;
+  // (rows that are not 16-byte aligned run the 128 x 128 tile with narrower DMA lanes: launch_h16)
+  const bool rows16 = D % 8 == 0 && ((reinterpret_cast<uintptr_t>(x.data_ptr()) |
+                                      reinterpret_cast<uintptr_t>(y.data_ptr())) % 16) == 0;
+  const bool big16 = rows16 && (big16_env >= 0 ? big16_env == 1
+                                               : static_cast<long long>((N + 255) / 256) * ((M + 255) / 256) * B >= 256);
   const bool big = h16 ? big16 : big_choice(N, M, D, B);
   const int tbm = big ? kGM : kBM, tbn = big ? kGN : kBN;
   const int tiles_n = (N + tbm - 1) / tbm, tiles_m = (M + tbn - 1) / tbn;

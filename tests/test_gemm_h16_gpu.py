@@ -131,3 +131,43 @@ def test_row_norms_kernel(dtype, d):
     ix, iy = ops.row_norms(x.to(DEV), inverse=True, y=y.to(DEV))
     torch.testing.assert_close(ix.cpu().double(), 1 / ref_x.sqrt(), rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(iy.cpu().double(), 1 / ref_y.sqrt(), rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("n,m,d,shift", [(300, 200, 100, 0), (257, 131, 77, 0), (300, 200, 72, 1), (129, 65, 5, 0),
+                                         (1000, 600, 130, 3), (64, 64, 1, 0)])
+def test_h16_any_width_and_alignment_stays_16bit(dtype, n, m, d, shift):
+    """Rows that are not 16-byte aligned (D % 8 != 0, or a base address off by ``shift`` elements) run the 16-bit
+    kernel with narrower DMA lanes and in-kernel K padding (csrc/pairwise/gemm_nt.hip GRAN): no fp32 upcast copy, the
+    same results as an fp64 GEMM of the 16-bit values, for the element-wise and the reduction epilogues."""
+    x, y = _xy(n, m, d, dtype, 5)
+    bx = torch.zeros(n * d + shift, dtype=dtype)
+    by = torch.zeros(m * d + shift, dtype=dtype)
+    bx[shift:] = x.reshape(-1)
+    by[shift:] = y.reshape(-1)
+    xd = bx.to(DEV)[shift:].view(n, d)
+    yd = by.to(DEV)[shift:].view(m, d)
+    assert xd.is_contiguous() and (shift == 0 or xd.data_ptr() % 16 != 0)
+    calls = []
+    real_float = torch.Tensor.float
+
+    def spy(self, *a, **k):
+        if self.is_cuda and self.dtype == dtype and self.dim() >= 2:
+            calls.append(tuple(self.shape))
+        return real_float(self, *a, **k)
+
+    torch.Tensor.float = spy
+    try:
+        out = ops.gemm_nt(xd, yd, ops.GEMM_STORE)
+        rows, cols = ops.gemm_row_col_max(xd[None], yd[None])
+    finally:
+        torch.Tensor.float = real_float
+    assert not calls, f"operands upcast to fp32: {calls}"
+    dot = x.double() @ y.double().T
+    torch.testing.assert_close(out.cpu().double(), dot, **_tol(d))
+    torch.testing.assert_close(rows[0].cpu().double(), dot.max(1).values, **_tol(d))
+    torch.testing.assert_close(cols[0].cpu().double(), dot.max(0).values, **_tol(d))
+    xx, yy = x.double(), y.double()
+    nx, ny = (xx * xx).sum(1), (yy * yy).sum(1)
+    e = ops.gemm_nt(xd, yd, ops.GEMM_EUCLID, nx.float().to(DEV), ny.float().to(DEV))
+    torch.testing.assert_close(e.cpu().double(), torch.cdist(xx, yy), rtol=1e-4, atol=1e-4)

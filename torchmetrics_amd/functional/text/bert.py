@@ -79,12 +79,18 @@ def _greedy_match(pe: Tensor, te: Tensor, pw: Tensor, tw: Tensor) -> Tuple[Tenso
     if pe.is_cuda and not (pe.requires_grad or te.requires_grad) and n * nl * p * r > 0:
         # ROCm: no [N, L, P, R] tensor -- sentence-length pairs (<= 128 tokens a side) on the per-pair 64 x 64
         # super-tile kernel, longer ones on the 128 x 128 MFMA GEMM with the row / column max epilogue
-        x = pe.reshape(n * nl, p, d).float().contiguous()
-        y = te.reshape(n * nl, r, d).float().contiguous()
+        # 16-bit embeddings (a bf16 / fp16 model: the reference's einsum runs in that dtype) stay 16-bit: the 16-bit
+        # matrix cores, no fp32 upcast pass
+        h16 = pe.dtype in (torch.bfloat16, torch.float16) and te.dtype == pe.dtype
+        x = pe.reshape(n * nl, p, d)
+        y = te.reshape(n * nl, r, d)
+        x, y = (x.contiguous(), y.contiguous()) if h16 else (x.float().contiguous(), y.float().contiguous())
         if p <= 128 and r <= 128:
             rmax, cmax = ops.bert_rowcol_max(x, y)
-        elif d % 4 == 0:
+        elif h16 or d % 4 == 0:
             rmax, cmax = ops.gemm_row_col_max(x, y)
+            if h16:  # (the similarities in the embeddings' dtype, as the bert_rowcol_max path rounds them)
+                rmax, cmax = rmax.to(pe.dtype).float(), cmax.to(pe.dtype).float()
         else:
             rmax = cmax = None
     else:

@@ -1442,12 +1442,11 @@ def gemm_nt(x: Tensor, y: Tensor, kind: int, aux_x: Optional[Tensor] = None, aux
     in the epilogue (no separate cast pass).
     """
     if x.is_cuda:
-        h16 = (x.dtype in (torch.bfloat16, torch.float16) and y.dtype == x.dtype and x.shape[-1] % 8 == 0
-               and x.shape[-1] > 0)
+        # 16-bit operands of any width and alignment stay 16-bit (rows that are not 16-byte aligned are staged with
+        # narrower DMA lanes in the kernel, csrc/pairwise/gemm_nt.hip GRAN): only mixed / other dtypes go to fp32
+        h16 = x.dtype in (torch.bfloat16, torch.float16) and y.dtype == x.dtype and x.shape[-1] > 0
         if h16:
             x, y = x.contiguous(), y.contiguous()
-            if x.data_ptr() % 16 or y.data_ptr() % 16:
-                h16 = False
         if not h16:
             x = x.float().contiguous()
             y = y.float().contiguous()
@@ -1467,7 +1466,8 @@ def gemm_nt(x: Tensor, y: Tensor, kind: int, aux_x: Optional[Tensor] = None, aux
 
 def bert_rowcol_max(x: Tensor, y: Tensor) -> "tuple[Tensor, Tensor]":
     """Row / column maxima of ``x[b] @ y[b]^T`` for token sets of at most 128 per side (``csrc/text/bert_match.hip``,
-    one block per pair, 64 x 64 MFMA super-tiles).  x ``[B, P, D]``, y ``[B, R, D]`` fp32."""
+    one block per pair, 64 x 64 MFMA super-tiles).  x ``[B, P, D]``, y ``[B, R, D]`` fp32, or bf16 / fp16 on the
+    16-bit matrix cores (fp32 accumulate, maxima rounded to the input dtype); fp32 ``[B, P]`` / ``[B, R]`` out."""
     b, p, _ = x.shape
     r = y.shape[1]
     rmax = torch.empty(b, p, dtype=torch.float32, device=x.device)

@@ -38,7 +38,7 @@ def main():
         ms_batch = timed(lambda: ops.dgemm([a, b], [b, a], [c, c2], alpha=[1.0, 1.0], beta=[0.5, 0.5], cin=[a, b]))
         ms_ref = timed(lambda: torch.matmul(a, b, out=c2))
         for impl, ms, f in (("ours", ms_ours, flops), ("ours_batched2", ms_batch, 2 * flops), ("torch_matmul", ms_ref, flops)):
-            print(json.dumps({"d": d, "impl": impl, "waves": os.environ.get("TM_AMD_DGEMM_WAVES", "8"), "ms": round(ms, 4), "tflops": round(f / ms / 1e9, 2),
+            print(json.dumps({"d": d, "impl": impl, "variant": os.environ.get("TM_AMD_DGEMM_VARIANT", "auto"), "ms": round(ms, 4), "tflops": round(f / ms / 1e9, 2),
                               "rel_err_vs_torch": err if impl == "ours" else None}), flush=True)
 
 

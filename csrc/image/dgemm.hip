@@ -7,10 +7,12 @@
 // dgemm_nn_kernel: C_p = alpha_p * A_p B_p + beta_p * Cin_p + diag_p * I for up to kMaxBatch problems of one shape in
 // ONE launch (the Newton-Schulz update Y' = a Y W + b Y and Z' = a W Z + b Z are two GEMMs sharing W: batching them
 // gives 2 tiles per CU instead of 1 at D = 2048).  Row-major operands, M x K times K x N.
-//   * 128 x 128 C tile per block, 4 waves as 2 x 2, each wave 64 x 64 = 4 x 4 v_mfma_f64_16x16x4_f64 accumulators.
-//   * K chunk of 16, two LDS stages; chunk c+1 staged while chunk c is consumed, chunk c+2 in flight in registers.
+//   * C tile per block 128 x 128 (8 waves as 2 x 4, 64 x 32 each) once the grid covers every CU, else 64 x 64 (4 waves
+//     of 32 x 32, four blocks per CU: D = 1024 runs at 30 instead of 14 TFLOP/s); see the note at the kernel.
+//   * K chunk of 16, two LDS stages; chunk c+1 staged while chunk c is consumed, chunk c+2 in flight in registers;
+//     within a chunk the operands of k-step s+1 are read from LDS while the MFMAs of step s issue.
 //     A is stored m-major (row stride 17 doubles: the 16 rows a wave reads at one k land on distinct banks), B k-major
-//     (row stride 144 doubles: consecutive k rows start 32 banks apart).
+//     (row stride kTN + 16 doubles: consecutive k rows start 32 banks apart).
 //   * XCD-aware tile order: block b runs on XCD b % 8 (observed dispatch), so the tile id is remapped to give each XCD
 //     a contiguous range of tile ids, and tile ids walk groups of 4 tile rows column by column: the 32 tiles one XCD
 //     holds at D = 2048 are a 4 x 8 patch (A panels read by 8 tiles, B panels by 4, out of that XCD's L2).
@@ -32,7 +34,6 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 constexpr int kT = 128;        // C tile edge
 constexpr int kKC = 16;        // K chunk
 constexpr int kAStride = kKC + 1;
-constexpr int kBStride = kT + 16;
 constexpr int kMaxBatch = 2;
 constexpr int kGroupRows = 4;  // tile-row group of the L2-friendly order
 
@@ -63,20 +64,30 @@ __device__ __forceinline__ void tile_of(int t, int nti, int ntj, int& ti, int& t
   ti = g * kGroupRows + r % rows_in_group;
 }
 
-// kWC waves across the tile's columns (2 or 4), 2 down its rows: 4 waves (64 x 64 per wave, 16 accumulators) or 8
-// waves (64 x 32 per wave, 8 accumulators: two waves per SIMD at one block per CU, so one wave's LDS waits and barrier
-// hide under the other's MFMAs).
+// C tile kTM x kTN per block, kWR x kWC waves, each wave (kTM / kWR) x (kTN / kWC) as 16 x 16 f64 MFMA tiles:
+//   * 128 x 128, 2 x 4 waves of 64 x 32 (8 accumulators; two waves per SIMD at one block per CU);
+//   * 64 x 64, 2 x 2 waves of 32 x 32 (4 accumulators, 38 KB of LDS): four blocks per CU, for grids smaller than the
+//     CU count.
+//   Measured at D = 2048 (profiles/r06_dgemm_pmc_*.txt, SQ_VALU_MFMA_BUSY_CYCLES over SIMD cycles): 128 x 128 / 8 waves
+//   keeps the f64 pipe 75-79 % busy, 64 x 64 / 4 blocks per CU 73 %, Tensile's MT64x64x16 90 % at a higher clock; at
+//   D = 4096 ours is within 3-6 % of Tensile (profiles/r06_bench_dgemm.jsonl).
 // kBT: B given as [N, K] row-major (C = A B^T), staged like A and transposed into the k-major LDS slab.
-template <int kWC, bool kBT>
-__global__ void __launch_bounds__(128 * kWC, 2)
+template <int kTM, int kTN, int kWR, int kWC, int kOcc, bool kBT, bool kPipeLds = true>
+__global__ void __launch_bounds__(kWave * kWR * kWC, kOcc)
     dgemm_nn_kernel(GemmBatch batch, int nprob, int M, int N, int K, bool vec_ok) {
-  constexpr int kThr = 128 * kWC;
-  constexpr int kQ = 4 / (kWC / 2);           // 16-col MFMA tiles per wave (4 or 2)
-  constexpr int kPerA = kT * kKC / kThr;      // A doubles staged per thread (8 or 4)
-  constexpr int kPerB = kKC * kT / kThr;      // B doubles staged per thread
-  __shared__ __attribute__((aligned(16))) double As[2][kT * kAStride];
-  __shared__ __attribute__((aligned(16))) double Bs[2][kKC * kBStride];
-  const int nti = (M + kT - 1) / kT, ntj = (N + kT - 1) / kT;
+  constexpr int kThr = kWave * kWR * kWC;
+  constexpr int kWaveRows = kTM / kWR;
+  constexpr int kMW = kWaveRows / 16;         // 16-row MFMA tiles per wave
+  constexpr int kWaveCols = kTN / kWC;
+  constexpr int kQ = kWaveCols / 16;          // 16-col MFMA tiles per wave (4 or 2)
+  constexpr int kPerA = kTM * kKC / kThr;     // A doubles staged per thread
+  constexpr int kPerB = kKC * kTN / kThr;     // B doubles staged per thread
+  constexpr int kBStr = kTN + 16;             // consecutive k rows of the B slab start 32 banks apart
+  static_assert(kMW >= 1 && kQ >= 1 && kPerA % 2 == 0 && kPerB % 2 == 0 && kTM * kKC == kThr * kPerA &&
+                    kKC * kTN == kThr * kPerB, "dgemm tile shape");
+  __shared__ __attribute__((aligned(16))) double As[2][kTM * kAStride];
+  __shared__ __attribute__((aligned(16))) double Bs[2][kKC * kBStr];
+  const int nti = (M + kTM - 1) / kTM, ntj = (N + kTN - 1) / kTN;
   const int per = nti * ntj;
   const int total = per * nprob;
   // XCD-aware remap: contiguous tile ids per XCD (when the grid divides evenly over 8 XCDs)
@@ -88,16 +99,15 @@ __global__ void __launch_bounds__(128 * kWC, 2)
   const GemmProblem& pr = batch.p[pi];
   const double* __restrict__ A = pr.a;
   const double* __restrict__ B = pr.b;
-  const int i0 = ti * kT, j0 = tj * kT;
+  const int i0 = ti * kTM, j0 = tj * kTN;
 
   const int tid = threadIdx.x;
   const int wave = tid / kWave, lane = tid & (kWave - 1);
   const int wr = wave / kWC, wc = wave % kWC;
-  constexpr int kWaveCols = kT / kWC;
-  // staging: A chunk 128 rows x 16 k (thread: one row, kPerA consecutive k); B chunk 16 k x 128 cols (thread: one k
+  // staging: A chunk kTM rows x 16 k (thread: one row, kPerA consecutive k); B chunk 16 k x kTN cols (thread: one k
   // row, kPerB consecutive cols)
   constexpr int kAThrPerRow = kKC / kPerA;
-  constexpr int kBThrPerRow = kT / kPerB;
+  constexpr int kBThrPerRow = kTN / kPerB;
   const int ar = tid / kAThrPerRow, ak = (tid % kAThrPerRow) * kPerA;
   const int bk = tid / kBThrPerRow, bc = (tid % kBThrPerRow) * kPerB;
   constexpr int kBTThrPerRow = kKC / kPerB;  // kBT: thread -> one B row (output column), kPerB consecutive k
@@ -162,17 +172,17 @@ __global__ void __launch_bounds__(128 * kWC, 2)
     for (int e = 0; e < kPerA; ++e) a[e] = ra[e];
     if constexpr (kBT) {
 #pragma unroll
-      for (int e = 0; e < kPerB; ++e) Bs[s][(btk + e) * kBStride + btn] = rb[e];
+      for (int e = 0; e < kPerB; ++e) Bs[s][(btk + e) * kBStr + btn] = rb[e];
     } else {
-      double* b = &Bs[s][bk * kBStride + bc];
+      double* b = &Bs[s][bk * kBStr + bc];
 #pragma unroll
       for (int e = 0; e < kPerB; ++e) b[e] = rb[e];
     }
   };
 
-  f64x4 acc[4][kQ];
+  f64x4 acc[kMW][kQ];
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
+  for (int m = 0; m < kMW; ++m)
 #pragma unroll
     for (int q = 0; q < kQ; ++q) acc[m][q] = f64x4{0.0, 0.0, 0.0, 0.0};
 
@@ -185,18 +195,31 @@ __global__ void __launch_bounds__(128 * kWC, 2)
   for (int c = 0; c < chunks; ++c) {
     const double* as = As[s];
     const double* bs = Bs[s];
+    // operands of k-step ks + 1 are read while the MFMAs of k-step ks issue (two register sets), so a wave never
+    // waits on LDS between its own MFMAs; the scheduling barriers keep the compiler from sinking the reads back
+    double av[2][kMW], bv[2][kQ];
+    auto rd = [&](int buf, int ks) {
+      const int k = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int m = 0; m < kMW; ++m) av[buf][m] = as[(wr * kWaveRows + m * 16 + (lane & 15)) * kAStride + k];
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) bv[buf][q] = bs[k * kBStr + wc * kWaveCols + q * 16 + (lane & 15)];
+    };
+    rd(0, 0);
 #pragma unroll
     for (int ks = 0; ks < kKC / 4; ++ks) {
-      const int k = ks * 4 + (lane >> 4);
-      double av[4], bv[kQ];
+      if (kPipeLds) {
+        if (ks + 1 < kKC / 4) rd((ks + 1) & 1, ks + 1);
+        __builtin_amdgcn_sched_barrier(0);
+      } else if (ks > 0) {
+        rd(ks & 1, ks);
+      }
 #pragma unroll
-      for (int m = 0; m < 4; ++m) av[m] = as[(wr * 64 + m * 16 + (lane & 15)) * kAStride + k];
+      for (int m = 0; m < kMW; ++m)
 #pragma unroll
-      for (int q = 0; q < kQ; ++q) bv[q] = bs[k * kBStride + wc * kWaveCols + q * 16 + (lane & 15)];
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int q = 0; q < kQ; ++q) acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], bv[q], acc[m][q], 0, 0, 0);
+        for (int q = 0; q < kQ; ++q)
+          acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks & 1][m], bv[ks & 1][q], acc[m][q], 0, 0, 0);
+      if (kPipeLds) __builtin_amdgcn_sched_barrier(0);
     }
     if (c + 1 < chunks) {
       store(s ^ 1);  // the other stage was released by the previous iteration's barrier
@@ -209,29 +232,49 @@ __global__ void __launch_bounds__(128 * kWC, 2)
   double* __restrict__ C = pr.c;
   const double* __restrict__ Cin = pr.cin;
   const double alpha = pr.alpha, beta = pr.beta, dg = pr.diag;
+  const bool euclid = pr.out32 != nullptr;
+  const int col0 = j0 + wc * kWaveCols + (lane & 15);
+  // one 16-row slice of accumulators at a time: its Cin values (or norms) are loaded together, all in flight at once,
+  // before any of its stores -- not one dependent load per element
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
+  for (int m = 0; m < kMW; ++m) {
+    const int row0 = i0 + wr * kWaveRows + m * 16 + (lane >> 4);
+    double cv[kQ][4];
+    double rv[4], colv[kQ];
 #pragma unroll
     for (int q = 0; q < kQ; ++q)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = i0 + wr * 64 + m * 16 + (lane >> 4) + 4 * r;
-        const int col = j0 + wc * kWaveCols + q * 16 + (lane & 15);
+        const int row = row0 + 4 * r, col = col0 + q * 16;
+        cv[q][r] = (!euclid && Cin != nullptr && row < M && col < N) ? Cin[static_cast<long long>(row) * N + col] : 0.0;
+      }
+    if (euclid) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rv[r] = row0 + 4 * r < M ? pr.rowv[row0 + 4 * r] : 0.0;
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) colv[q] = col0 + q * 16 < N ? pr.colv[col0 + q * 16] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < kQ; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + 4 * r, col = col0 + q * 16;
         if (row < M && col < N) {
           const long long e = static_cast<long long>(row) * N + col;
           double v = alpha * acc[m][q][r];
-          if (pr.out32 != nullptr) {
-            float d2 = static_cast<float>(v + pr.rowv[row] + pr.colv[col]);
+          if (euclid) {
+            float d2 = static_cast<float>(v + rv[r] + colv[q]);
             d2 = d2 > 0.f ? d2 : 0.f;
             if (pr.zero_diag && row == col) d2 = 0.f;
             pr.out32[e] = pr.sqrt_out ? sqrtf(d2) : d2;
             continue;
           }
-          if (Cin != nullptr) v += beta * Cin[e];
+          if (Cin != nullptr) v += beta * cv[q][r];
           if (row == col) v += dg;
           C[e] = v;
         }
       }
+  }
 }
 
 // ----------------------------------------------------------------------------------------------- power iteration
@@ -386,15 +429,41 @@ void dgemm_nn(at::TensorList a, at::TensorList b, at::TensorList c, at::TensorLi
              reinterpret_cast<uintptr_t>(gb.p[i].b) % 16 == 0;
   }
   if (M == 0 || N == 0) return;
-  const int tiles = ((M + kT - 1) / kT) * ((N + kT - 1) / kT) * np;
-  static const int waves = [] {
-    const char* e = std::getenv("TM_AMD_DGEMM_WAVES");  // tuning knob: 4 or 8 waves per 128 x 128 tile
-    return e ? std::atoi(e) : 8;
+  static const int variant = [] {
+    // tuning knob: 8 = 128 x 128 tile / 8 waves, 4 = 128 x 128 / 4 waves, 64 = 128 x 64 / 4 waves, 44 = 64 x 64 / 4
+    // waves; 0 = by shape
+    const char* e = std::getenv("TM_AMD_DGEMM_VARIANT");
+    return e ? std::atoi(e) : 0;
   }();
-  if (waves == 4) {
-    hipLaunchKernelGGL((dgemm_nn_kernel<2, false>), dim3(tiles), dim3(256), 0, stream(), gb, np, M, N, K, vec_ok);
-  } else {
-    hipLaunchKernelGGL((dgemm_nn_kernel<4, false>), dim3(tiles), dim3(512), 0, stream(), gb, np, M, N, K, vec_ok);
+  // by shape: 128 x 128 tiles once they cover every CU (MFMA busy 79 % vs 73 % for 64 x 64 at D = 2048), 64 x 64
+  // below that (D = 1024: 29 vs 14 TFLOP/s)
+  const int t128 = ((M + kT - 1) / kT) * ((N + kT - 1) / kT) * np;
+  const int v = variant != 0 ? variant : (t128 < cu_count(a[0].get_device()) ? 44 : 8);
+  auto grid = [&](int tm, int tn) { return dim3(((M + tm - 1) / tm) * ((N + tn - 1) / tn) * np); };
+  auto s = stream();
+  switch (v) {
+    case 44:
+      hipLaunchKernelGGL((dgemm_nn_kernel<64, 64, 2, 2, 4, false>), grid(64, 64), dim3(256), 0, s, gb, np, M, N, K, vec_ok);
+      break;
+    case -44:
+      hipLaunchKernelGGL((dgemm_nn_kernel<64, 64, 2, 2, 4, false, false>), grid(64, 64), dim3(256), 0, s, gb, np, M, N, K,
+                         vec_ok);
+      break;
+    case 64:
+      hipLaunchKernelGGL((dgemm_nn_kernel<128, 64, 2, 2, 2, false>), grid(128, 64), dim3(256), 0, s, gb, np, M, N, K,
+                         vec_ok);
+      break;
+    case 4:
+      hipLaunchKernelGGL((dgemm_nn_kernel<128, 128, 2, 2, 2, false>), grid(128, 128), dim3(256), 0, s, gb, np, M, N, K,
+                         vec_ok);
+      break;
+    case -8:
+      hipLaunchKernelGGL((dgemm_nn_kernel<128, 128, 2, 4, 2, false, false>), grid(128, 128), dim3(512), 0, s, gb, np, M, N,
+                         K, vec_ok);
+      break;
+    default:
+      hipLaunchKernelGGL((dgemm_nn_kernel<128, 128, 2, 4, 2, false>), grid(128, 128), dim3(512), 0, s, gb, np, M, N, K,
+                         vec_ok);
   }
 }
 
@@ -424,7 +493,7 @@ void euclid_f64(const at::Tensor& x, const at::Tensor& y, const at::Tensor& nx, 
   const bool vec_ok = K % 2 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
                       reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0;
   const int tiles = ((M + kT - 1) / kT) * ((N + kT - 1) / kT);
-  hipLaunchKernelGGL((dgemm_nn_kernel<4, true>), dim3(tiles), dim3(512), 0, stream(), gb, 1, M, N, K, vec_ok);
+  hipLaunchKernelGGL((dgemm_nn_kernel<128, 128, 2, 4, 2, true>), dim3(tiles), dim3(512), 0, stream(), gb, 1, M, N, K, vec_ok);
 }
 
 // One power-iteration step (see dgemv4_resid_kernel); returns nothing, writes w_out [d, 4] and part_out [blocks, 4].

@@ -9,10 +9,12 @@
 // kernel reduces the split-K partials in a fixed order (bitwise reproducible) and adds them into both triangles of
 // the state, transposing the mirrored block through LDS so both writes are coalesced.
 //
-// Per block: 128 x 128 C tile, 4 waves as 2 x 2, each 64 x 64 = 4 x 4 MFMA 16x16 accumulators (f64x4).  K chunk = 32
-// samples, two LDS stages: chunk c+1 is written into the other stage while chunk c is consumed, chunk c+2 is in
-// flight in registers, one barrier per chunk.  LDS rows are padded to 144 elements (≡ 16 mod 32 words for b32 reads,
-// ≡ 32 mod 64 for b64 reads) so the 4 k-rows read by one wave land on disjoint banks.
+// Per block: 128 x 128 C tile, 8 waves as 2 x 4, each 64 x 32 = 4 x 2 MFMA 16x16 accumulators (f64x4): two waves per
+// SIMD, so one wave's LDS waits and the chunk barrier hide under the other's MFMAs (the 4-wave 64 x 64 layout ran the
+// f64 pipe ~8 % less busy, csrc/image/dgemm.hip).  K chunk = 32 samples, two LDS stages: chunk c+1 is written into the
+// other stage while chunk c is consumed, chunk c+2 is in flight in registers, one barrier per chunk; inside a chunk the
+// operands of k-step s+1 are read while the MFMAs of step s issue.  LDS rows are padded to 144 elements (≡ 16 mod 32
+// words for b32 reads, ≡ 32 mod 64 for b64 reads) so the 4 k-rows read by one wave land on disjoint banks.
 //
 // Numerics: products and sums are fp64 exactly as in the reference (inputs are exactly representable in fp64).
 #include <cstdlib>
@@ -27,8 +29,10 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 constexpr int kTile = 128;          // C tile edge
 constexpr int kKC = 32;             // samples per K chunk (8 MFMA k-steps of 4)
 constexpr int kLdsRow = kTile + 16; // padded LDS row (elements)
-constexpr int kThreads = 256;       // 4 waves, 2 x 2 over the tile, 64 x 64 each
-constexpr int kColsPerThread = 16;  // each thread stages 16 consecutive columns of one sample row per panel
+constexpr int kThreads = 512;       // 8 waves, 2 x 4 over the tile, 64 x 32 each
+constexpr int kColsPerThread = 8;   // each thread stages 8 consecutive columns of one sample row per panel
+constexpr int kThrPerRow = kTile / kColsPerThread;  // 16 threads stage one sample row
+static_assert(kThrPerRow * kKC == kThreads, "staging covers the chunk exactly");
 
 // LDS element type: fp32 for every input narrower than or equal to fp32 (exact), fp64 for fp64 inputs
 template <typename T>
@@ -61,13 +65,14 @@ __device__ __forceinline__ void tile_coords(int t, int ntile, int& ti, int& tj) 
   tj = row + rem;
 }
 
-// Loads 16 consecutive features (columns c0..c0+15 of sample row `row`) in storage type, 16-byte loads when possible.
+// Loads kColsPerThread consecutive features (columns c0..c0+15 of sample row `row`) in storage type, 16-byte loads when possible.
 template <typename scalar_t>
-__device__ __forceinline__ void load16(const scalar_t* __restrict__ x, long long n, int d, long long row, int c0,
+__device__ __forceinline__ void load_cols(const scalar_t* __restrict__ x, long long n, int d, long long row, int c0,
                                        bool vec_ok, scalar_t (&out)[kColsPerThread]) {
   if (row < n && vec_ok && c0 + kColsPerThread <= d) {
     const scalar_t* p = x + row * d + c0;
     constexpr int kPer = 16 / sizeof(scalar_t);  // elements per 16-byte load
+    static_assert(kColsPerThread % kPer == 0, "whole 16-byte loads");
 #pragma unroll
     for (int v = 0; v < kColsPerThread / kPer; ++v) {
       const u32x4 raw = *reinterpret_cast<const u32x4*>(p + v * kPer);
@@ -103,23 +108,23 @@ __global__ void __launch_bounds__(kThreads, 2)
   const long long c_end = min(chunks, c_beg + per);
 
   const int tid = threadIdx.x;
-  const int lr = tid / 8;                    // sample row (0..31) staged by this thread
-  const int lc = (tid % 8) * kColsPerThread; // first of 16 panel columns staged by this thread
+  const int lr = tid / kThrPerRow;                     // sample row (0..31) staged by this thread
+  const int lc = (tid % kThrPerRow) * kColsPerThread;  // first of its panel columns
   const int wave = tid / kWave, lane = tid & (kWave - 1);
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave >> 2, wc = wave & 3;             // wave tile: rows wr*64.., cols wc*32..
 
-  f64x4 acc[4][4];
+  f64x4 acc[4][2];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int b = 0; b < 2; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
   double colsum = 0.0;  // diagonal tiles: threads 0..127 own one column's running sum
 
   scalar_t ra[kColsPerThread], rb[kColsPerThread];
   auto load = [&](long long chunk) {
     const long long row = chunk * kKC + lr;
-    load16(x, n, d, row, i0 + lc, vec_ok, ra);
-    if (!diag) load16(x, n, d, row, j0 + lc, vec_ok, rb);
+    load_cols(x, n, d, row, i0 + lc, vec_ok, ra);
+    if (!diag) load_cols(x, n, d, row, j0 + lc, vec_ok, rb);
   };
   auto store = [&](int stage) {
     st_t* a = lds + (stage * 2) * kPanel + lr * kLdsRow + lc;
@@ -146,18 +151,26 @@ __global__ void __launch_bounds__(kThreads, 2)
 #pragma unroll 8
       for (int r = 0; r < kKC; ++r) colsum += static_cast<double>(As[r * kLdsRow + tid]);
     }
-#pragma unroll 2
-    for (int ks = 0; ks < kKC / 4; ++ks) {
+    st_t av[2][4], bv[2][2];  // stage type in registers: widened right at the MFMA
+    auto rd = [&](int buf, int ks) {
       const int k = ks * 4 + (lane >> 4);
-      double av[4], bv[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) av[m] = static_cast<double>(As[k * kLdsRow + wr * 64 + m * 16 + (lane & 15)]);
+      for (int m = 0; m < 4; ++m) av[buf][m] = As[k * kLdsRow + wr * 64 + m * 16 + (lane & 15)];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) bv[q] = static_cast<double>(Bs[k * kLdsRow + wc * 64 + q * 16 + (lane & 15)]);
+      for (int q = 0; q < 2; ++q) bv[buf][q] = Bs[k * kLdsRow + wc * 32 + q * 16 + (lane & 15)];
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < kKC / 4; ++ks) {
+      if (ks + 1 < kKC / 4) rd((ks + 1) & 1, ks + 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m], bv[q], acc[m][q], 0, 0, 0);
+        for (int q = 0; q < 2; ++q)
+          acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(static_cast<double>(av[ks & 1][m]),
+                                                           static_cast<double>(bv[ks & 1][q]), acc[m][q], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (c + 1 < c_end) {
       store(stage ^ 1);                    // the other stage was released by the previous iteration's barrier
@@ -172,11 +185,11 @@ __global__ void __launch_bounds__(kThreads, 2)
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = wr * 64 + m * 16 + (lane >> 4) + 4 * r;  // f64 MFMA C/D layout
-        const int col = wc * 64 + q * 16 + (lane & 15);
+        const int col = wc * 32 + q * 16 + (lane & 15);
         out[row * kTile + col] = acc[m][q][r];
       }
   if (diag && tid < kTile) {

@@ -25,7 +25,7 @@ def _tol(d):
 
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("n,m,d", [(300, 200, 72), (128, 128, 64), (1000, 777, 200), (4100, 4097, 96),
-                                   (4096, 4096, 8)])
+                                   (4096, 4096, 8), (4097, 4096, 520)])
 def test_h16_store(dtype, n, m, d):
     x, y = _xy(n, m, d, dtype)
     out = ops.gemm_nt(x.to(DEV), y.to(DEV), ops.GEMM_STORE, scale=0.5)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes over benchmarks/dgemm_pmc_driver.py (ours single / batched pair vs Tensile at D = 2048), one pass per run.
+# Two PMC passes over a benchmarks/*_pmc_driver.py (DRIVER=..., default the fp64 GEMM one), one pass per run.
 #   bash tools/gpu/dgemm_pmc.sh <name>
 set -o pipefail
 mkdir -p gpurun_out
@@ -11,7 +11,7 @@ P2="TCC_HIT_sum TCC_MISS_sum SQ_INSTS_LDS SQ_INSTS_VALU SQ_WAVES GRBM_COUNT"
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  cd /tmp && timeout -s KILL 90 rocprofv3 --pmc $P -d $R/gpurun_out/${N}_p$i -o p --output-format csv -- python3 $R/benchmarks/dgemm_pmc_driver.py ${2:-2048} > $R/gpurun_out/${N}_p$i.log 2>&1 || { tail -20 $R/gpurun_out/${N}_p$i.log; exit 1; }
+  cd /tmp && timeout -s KILL 90 rocprofv3 --pmc $P -d $R/gpurun_out/${N}_p$i -o p --output-format csv -- python3 $R/benchmarks/${DRIVER:-dgemm_pmc_driver.py} $ARGS > $R/gpurun_out/${N}_p$i.log 2>&1 || { tail -20 $R/gpurun_out/${N}_p$i.log; exit 1; }
   cd $R && f=$(find gpurun_out/${N}_p$i -name "*counter_collection.csv" | head -1) && cp $f gpurun_out/${N}_p$i.csv && rm -rf gpurun_out/${N}_p$i
 done
 python3 tools/gpu/pmc_summary.py gpurun_out/${N}_p1.csv gpurun_out/${N}_p2.csv

@@ -1,4 +1,4 @@
-"""Timing of the 16-bit GEMM store path at two shapes under TM_AMD_GEMM16_PP (main-loop variants and timing probes)."""
+"""Timing of the 16-bit GEMM store path at two shapes (kept for the round-6 loop probes: profiles/r06_gemm16_loop_probes.txt)."""
 import sys, os, time, json, torch
 sys.path.insert(0, os.environ["GRAFT_REPO_ROOT"])
 from torchmetrics_amd import ops

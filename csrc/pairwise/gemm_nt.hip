@@ -727,6 +727,11 @@ __device__ __attribute__((aligned(16))) uint32_t g_zero_chunk[4];  // the DMA so
 // round-5 log): a 4-deep / 2-deep ring of 32-wide k-chunks (no faster; at 165 VGPRs two 512-thread blocks never share
 // a CU), four waves of 128 x 128 per wave (512 VGPRs, spills: 10-20 % slower), and a persistent grid-stride form that
 // overlaps a tile's stores with the next tile's DMA (within 5 %).
+// Round 6 (profiles/r06_gemm16_loop_probes.txt, r06_bench_gemm16_pingpong.jsonl): a phased "ping-pong" loop after
+// cdna_hip_programming.md §5 (32-deep K pieces through a 4-slot LDS ring, counted vmcnt across barriers, the two wave rows
+// one barrier apart so one wave per SIMD issues MFMAs while the other reads) ran 925-960 TFLOP/s at 4096^2 x 2048 against
+// 951-961 for this loop; its timing probes put the ceiling in the MFMA-and-barrier skeleton itself (no DMA: 1193, no DMA
+// and no barriers: 1222), not in the staging.
 // GRAN: bytes per DMA lane.  16 (the fast form) needs 16-byte aligned rows (D % 8 == 0, 16-byte aligned bases);
 // rows of any other width are staged in place into the SAME swizzled LDS layout, the K tail zero-filled element by
 // element -- no padded copy and no fp32 upcast of the operands: 4-byte DMA lanes for even widths (4x the
@@ -913,191 +918,6 @@ __global__ __launch_bounds__(TM == 256 ? 512 : 256) void gemm_nt_h16_kernel(
     tile_epilogue<EPI, NA, WC, TM, NT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile, dist2);
 }
 
-// ------------------------------------------------------------------------------- 16-bit, ping-pong main loop
-// The 256 x 256 16-bit GEMM with its main loop split into phases (cdna_hip_programming.md §5, the 8-phase template,
-// adapted): the same 8 waves (2 wave rows x 4 wave columns, 128 x 64 per wave, acc[4][2] of 32x32x16 MFMAs -- so the
-// epilogues above apply unchanged), but
-//   * K is staged in PIECES of 32 elements (A and B, 256 rows x 64 B each) through a ring of 4 LDS slots (128 KB):
-//     piece j + 3 is issued by LDS-DMA while piece j is read, and each wave waits only for the oldest piece it needs
-//     (a counted `s_waitcnt vmcnt(8)`, never 0 in the loop), so two pieces stay in flight across every barrier;
-//   * a phase is one 16-deep k-step: 6 fragment reads, a barrier, then 8 MFMAs between two barriers with raised
-//     priority; the wave row 1 runs one barrier behind wave row 0 (one extra barrier at the start), so in every
-//     inter-barrier segment one wave of each SIMD issues MFMAs while the other reads its next fragments and DMAs;
-//   * slot layout [256 rows][4 x 16 B], logical chunk c of row r at c ^ ((r >> 2) & 3): the 16 lanes of a ds_read_b128
-//     group hit 16 distinct 16-byte bank slots (the DMA writes lane-linear; the swizzle is on its SOURCE address).
-// Hazards, by segment (barrier-separated; row 0 reads phase f in segment 2f + 1, row 1 in 2f + 2, MFMAs one segment
-// later): piece j + 3 overwrites piece j - 1, whose last reads (phase 2j - 1) row 1 retires at the start of segment 4j + 1,
-// and is issued in phase 2j + 1 (segments 4j + 3 / 4j + 4); the wait for piece j + 1 sits in that same phase, before the
-// barrier that precedes its first read (phase 2j + 2: segments 4j + 5 / 4j + 6) by either wave row.
-// 16-byte rows only (D % 8 == 0, 16-byte aligned bases); the K tail past D reads the zero block.
-template <int EPI, typename T, int kProbe = 0>
-__global__ __launch_bounds__(512) void gemm_nt_h16_pp_kernel(const uint16_t* __restrict__ X,
-                                                             const uint16_t* __restrict__ Y, int N, int M, int D,
-                                                             long long bx, long long by, int tiles_m, EpiParams ep,
-                                                             int sg_shift) {
-  constexpr int TM = 256, NT = 512, WC = 4, NA = 4, PK = 32;  // PK: K elements per piece
-  constexpr int kSlot = 2 * TM * PK;                          // elements per ring slot (A then B)
-  typedef typename Mfma16<T>::v8 v8;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  uint16_t* sh = reinterpret_cast<uint16_t*>(smem);
-  const int batch = blockIdx.z;
-  const int32_t* gix = ep.ix ? ep.ix + (long long)batch * N : nullptr;
-  const int32_t* giy = ep.iy ? ep.iy + (long long)batch * M : nullptr;
-  if (!gix) X += batch * bx;
-  if (!giy) Y += batch * by;
-  auto xrow = [&](int i) -> const uint16_t* { return X + (long long)(gix ? gix[i] : i) * D; };
-  auto yrow = [&](int j) -> const uint16_t* { return Y + (long long)(giy ? giy[j] : j) * D; };
-  const int tiles_n = (N + TM - 1) / TM;
-  const int total = tiles_n * tiles_m;
-  const int bid = blockIdx.x;
-  const int per = (total + 7) / 8;
-  const int tile = (bid % 8) * per + bid / 8;
-  if (tile >= total) return;  // (the whole block: no barrier is left waiting)
-  const int ti = tile / tiles_m, tj = tile - ti * tiles_m;
-  const int row0 = ti * TM, col0 = tj * TM;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = (wave >> sg_shift) & 1;  // stagger group: 0 leads, 1 runs one barrier behind
-  const int wr = (wave / WC) * 32 * NA, wc = (wave % WC) * 64;
-  const int h = lane >> 5, r = lane & 31;
-
-  // DMA: wave w moves rows [32 w, 32 w + 32) of both operands of a piece, 16 rows (1 KiB) per instruction: lane l of
-  // instruction q fills row 32 w + 16 q + l / 4, physical chunk l % 4 = logical chunk (l % 4) ^ ((row >> 2) & 3)
-  const uint16_t* srcA[2];
-  const uint16_t* srcB[2];
-  int kof[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int rr = 32 * wave + 16 * q + (lane >> 2);
-    const int c = (lane & 3) ^ ((rr >> 2) & 3);
-    kof[q] = 8 * c;
-    srcA[q] = xrow(min(row0 + rr, N - 1)) + 8 * c;
-    srcB[q] = yrow(min(col0 + rr, M - 1)) + 8 * c;
-  }
-  typedef __attribute__((address_space(3))) void lds_t;
-  typedef __attribute__((address_space(1))) void glb_t;
-  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_zero_chunk);
-  const int np = (D + PK - 1) / PK;  // pieces
-  auto issue = [&](int j) {  // 4 DMA instructions per wave
-    uint16_t* sa = sh + (j & 3) * kSlot;
-    uint16_t* sb = sa + TM * PK;
-    const int k0 = j * PK;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const bool in = k0 + kof[q] < D;
-      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcA[q] + k0 : zero), (lds_t*)(sa + (32 * wave + 16 * q) * PK), 16,
-                                       0, 0);
-      __builtin_amdgcn_global_load_lds((glb_t*)(in ? srcB[q] + k0 : zero), (lds_t*)(sb + (32 * wave + 16 * q) * PK), 16,
-                                       0, 0);
-    }
-  };
-  // keep the newest n pieces in flight (n = 0, 1, 2), retire the rest
-  auto wait_pieces = [&](int n) {
-    if (n >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-
-  f32x16 acc[NA][2];
-#pragma unroll
-  for (int a = 0; a < NA; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-
-  const int swz_a = ((wr + r) >> 2) & 3;  // (32 a keeps (row >> 2) & 3)
-  const int swz_b = ((wc + r) >> 2) & 3;
-  // fragments of k-step s (0, 1) of piece j: logical chunk 2 s + h of rows wr + 32 a + r / wc + 32 b + r
-  auto frag = [&](int j, int s, v8* fa, v8* fb) {
-    const uint16_t* sa = sh + (j & 3) * kSlot + (wr + r) * PK;
-    const uint16_t* sb = sh + (j & 3) * kSlot + TM * PK + (wc + r) * PK;
-#pragma unroll
-    for (int a = 0; a < NA; ++a) fa[a] = *reinterpret_cast<const v8*>(sa + 32 * a * PK + 8 * ((2 * s + h) ^ swz_a));
-#pragma unroll
-    for (int b = 0; b < 2; ++b) fb[b] = *reinterpret_cast<const v8*>(sb + 32 * b * PK + 8 * ((2 * s + h) ^ swz_b));
-  };
-  // timing probes (wrong results): 1 = 16x16x32 MFMAs of the same cycles, 2 = no DMA in the loop, 3 = DMA never waited
-  constexpr bool kProbe16 = kProbe == 1;
-  f32x4 probe[NA][2][2];
-  if constexpr (kProbe16) {
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) probe[a][b][0] = probe[a][b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  auto mma = [&](const v8* fa, const v8* fb) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        if constexpr (kProbe16) {
-          probe[a][b][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], probe[a][b][0], 0, 0, 0);
-          probe[a][b][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], probe[a][b][1], 0, 0, 0);
-        } else if constexpr (rows_in_lanes<EPI>()) {
-          acc[a][b] = Mfma16<T>::run(fb[b], fa[a], acc[a][b]);
-        } else {
-          acc[a][b] = Mfma16<T>::run(fa[a], fb[b], acc[a][b]);
-        }
-      }
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto barrier = [] {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  // prologue: pieces 0..2 in flight, piece 0 retired and visible
-  for (int j = 0; j < 3 && j < np; ++j) issue(j);
-  wait_pieces(min(np, 3) - 1);
-  barrier();
-  if (grp == 1) barrier();  // the stagger
-  v8 fa[2][NA], fb[2][2];
-  for (int j = 0; j < np; ++j) {
-    // phase 2j: k-step 0 of piece j
-    frag(j, 0, fa[0], fb[0]);
-    barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    mma(fa[0], fb[0]);
-    barrier();
-    // phase 2j + 1: k-step 1 of piece j, DMA of piece j + 3 (its slot held piece j - 1: free, see above), and the wait
-    // for piece j + 1
-    frag(j, 1, fa[1], fb[1]);
-    if (kProbe != 2 && j + 3 < np) issue(j + 3);
-    if (kProbe != 3) wait_pieces(min(np, j + 4) - (j + 2));
-    barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    mma(fa[1], fb[1]);
-    barrier();
-  }
-  if (grp == 0) barrier();  // balance the stagger: both rows have passed the same number of barriers
-  if constexpr (kProbe16) {
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[a][b][e] = probe[a][b][0][e] + probe[a][b][1][e];
-  }
-  auto dist2 = [&](int i, int j) {
-    const uint16_t* xr = xrow(i);
-    const uint16_t* yr = yrow(j);
-    float t = 0.f;
-    for (int k = 0; k < D; ++k) {
-      const float d = Mfma16<T>::to_f32(xr[k]) - Mfma16<T>::to_f32(yr[k]);
-      t = fmaf(d, d, t);
-    }
-    return t;
-  };
-  if constexpr (rows_in_lanes<EPI>())
-    tile_epilogue_t<EPI, NA, WC>(acc, ep, batch, N, M, row0, col0, dist2, TM, TM);
-  else
-    tile_epilogue<EPI, NA, WC, TM, NT>(acc, smem, ep, batch, N, M, row0, col0, ti, tj, tiles_n, tile, dist2);
-}
-
 // The 256 x 256 kernel for large problems: D a multiple of its k-step, both sides at least one tile, enough tiles to
 // fill the chip once; TM_AMD_GEMM_BIG=0|1 forces it off / on (where it applies).
 bool big_choice(int N, int M, int D, int batches) {
@@ -1196,24 +1016,7 @@ void launch_h16(const at::Tensor& x, const at::Tensor& y, int batches, long long
   const size_t lds = 2ull * 2 * tm * 64 * sizeof(uint16_t);
   const auto* xp = reinterpret_cast<const uint16_t*>(x.data_ptr());
   const auto* yp = reinterpret_cast<const uint16_t*>(y.data_ptr());
-  static const int sg_shift = [] {  // TM_AMD_GEMM16_SG: stagger group = (wave >> SG) & 1 (measurement knob)
-    const char* e = std::getenv("TM_AMD_GEMM16_SG");
-    return e ? std::atoi(e) : 2;
-  }();
-  static const int pp = [] {  // TM_AMD_GEMM16_PP=0: the one-barrier-per-chunk loop (A/B knob); 2-4: timing probes
-    const char* e = std::getenv("TM_AMD_GEMM16_PP");
-    return e ? std::atoi(e) : 1;
-  }();
-  if (big && pp >= 2 && pp <= 4 && EPI == kStore) {
-    auto k = pp == 2 ? gemm_nt_h16_pp_kernel<EPI, T, 1> : pp == 3 ? gemm_nt_h16_pp_kernel<EPI, T, 2>
-                                                                   : gemm_nt_h16_pp_kernel<EPI, T, 3>;
-    hipLaunchKernelGGL(k, dim3(per * 8, 1, batches), dim3(512), lds, stream(), xp, yp, N, M, D, bx, by, tiles_m, ep,
-                       sg_shift);
-  }
-  else if (big && pp)
-    hipLaunchKernelGGL((gemm_nt_h16_pp_kernel<EPI, T>), dim3(per * 8, 1, batches), dim3(512), lds, stream(), xp, yp, N,
-                       M, D, bx, by, tiles_m, ep, sg_shift);
-  else if (big)
+  if (big)
     hipLaunchKernelGGL((gemm_nt_h16_kernel<EPI, T, 256>), dim3(per * 8, 1, batches), dim3(512), lds, stream(), xp, yp,
                        N, M, D, bx, by, tiles_m, ep);
   else

@@ -509,6 +509,36 @@ def test_coco_accumulate_kernel_matches_torch_path(monkeypatch):
         assert torch.equal(fused[key], ref[key]), key
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("backend,mdt", [("faster_coco_eval", [1, 7, 50]), ("pycocotools", [1, 7, 50]),
+                                         ("pycocotools", [1, 10, 100])])
+@pytest.mark.parametrize("average", ["macro", "micro"])
+def test_coco_summary_kernel_matches_torch_reductions(monkeypatch, backend, mdt, average):
+    """The one-launch summary (coco_summary_kernel: masked precision / recall sums per (t, a, m) and the per-class
+    numbers) gives the same summary and per-class values as the masked torch reductions it replaced, including the
+    legacy mAP at a max-dets value that is absent (-1) and micro averaging (a second, per-class evaluation)."""
+    from benchmarks.bench_map import make_data
+    from torchmetrics_amd import ops
+    from torchmetrics_amd.detection import MeanAveragePrecision
+
+    dev = torch.device("cuda", 0)
+    preds, target = make_data(64, dev, seed=5)
+
+    def run():
+        m = MeanAveragePrecision(class_metrics=True, max_detection_thresholds=mdt, backend=backend,
+                                 average=average).to(dev)
+        m.update(preds[:32], target[:32])
+        m.update(preds[32:], target[32:])
+        return m.compute()
+
+    fused = run()
+    monkeypatch.setattr(ops, "coco_summary", lambda *a, **k: None)
+    ref = run()
+    assert fused.keys() == ref.keys()
+    for key in fused:
+        torch.testing.assert_close(fused[key].double(), ref[key].double(), rtol=1e-6, atol=1e-7, msg=key)
+
+
 def _ddp_map_packed(rank, world, preds, target):
     """The per-image states cross the engine flat (Metric._packed_sync_plan); rank 1 holds one image more than rank 0
     and updates twice; after compute() the local (chunked, unbuilt) states are back; the synced order is element-major

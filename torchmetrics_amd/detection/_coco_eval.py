@@ -125,9 +125,11 @@ def coco_evaluate(
     r_thr = torch.tensor(list(rec_thresholds), dtype=torch.float64, device=dev)
     areas = torch.tensor(AREA_RANGES, dtype=torch.float64, device=dev)
     T, R, A, M, K = t_thr.numel(), r_thr.numel(), areas.shape[0], len(max_dets), classes.numel()
-    precision = torch.full((T, R, K, A, M), -1.0, dtype=torch.float64, device=dev)
-    recall = torch.full((T, K, A, M), -1.0, dtype=torch.float64, device=dev)
-    scores_out = torch.full((T, R, K, A, M), -1.0, dtype=torch.float64, device=dev)
+    # (every entry is written below: by the accumulation kernel, which also writes -1 for categories without a
+    # non-ignored ground truth, or by the torch path and the final mask)
+    precision = torch.empty((T, R, K, A, M), dtype=torch.float64, device=dev)
+    recall = torch.empty((T, K, A, M), dtype=torch.float64, device=dev)
+    scores_out = torch.empty((T, R, K, A, M), dtype=torch.float64, device=dev)
     if K == 0:
         return {"precision": precision, "recall": recall, "scores": scores_out}
 
@@ -277,11 +279,13 @@ def coco_evaluate(
         precision.zero_()
         scores_out.zero_()
         recall.zero_()
-    # categories without any non-ignored ground truth stay at -1 (pycocotools skips them)
-    missing = ~has_gt.T  # [K, A]
-    precision.masked_fill_(missing[None, None, :, :, None], -1.0)
-    scores_out.masked_fill_(missing[None, None, :, :, None], -1.0)
-    recall.masked_fill_(missing[None, :, :, None], -1.0)
+    if not done:
+        # categories without any non-ignored ground truth stay at -1 (pycocotools skips them; the kernel writes these
+        # itself)
+        missing = ~has_gt.T  # [K, A]
+        precision.masked_fill_(missing[None, None, :, :, None], -1.0)
+        scores_out.masked_fill_(missing[None, None, :, :, None], -1.0)
+        recall.masked_fill_(missing[None, :, :, None], -1.0)
     return {"precision": precision, "recall": recall, "scores": scores_out}
 
 
@@ -355,10 +359,41 @@ def per_class_stats(ev: Dict[str, Tensor], max_dets: Optional[Sequence[int]] = N
     return mp, mr
 
 
+def _summary_kernel(ev: Dict[str, Tensor], max_dets: Sequence[int], map_max_det: Optional[int],
+                    class_ev: Optional[Dict[str, Tensor]]) -> Optional[Tuple[Tuple[Tensor, ...], Tensor, Tensor]]:
+    """ROCm: the masked sums and the per-class numbers from ONE summary launch and one host transfer."""
+    prec, rec = ev["precision"], ev["recall"]
+    cev = class_ev if class_ev is not None else ev
+    m_ap = len(max_dets) - 1
+    if map_max_det is not None:
+        m_ap = list(max_dets).index(map_max_det) if map_max_det in max_dets else -1
+    vec = ops.coco_summary(prec, rec, cev["precision"], cev["recall"], m_ap)
+    if vec is None:
+        return None
+    T, _, K, A, M = prec.shape
+    v = vec.cpu()
+    tam, tk, nb = T * A * M, T * K, (K + 3) // 4
+    sp, cp = (v[i * nb * tam:(i + 1) * nb * tam].reshape(T, nb, A, M).sum(1) for i in range(2))
+    base = 2 * nb * tam
+    sr, cr = (v[base + i * tam:base + (i + 1) * tam].reshape(T, A, M) for i in range(2))
+    base += 2 * tam
+    mps, mpc, mrs, mrc = (v[base + i * tk:base + (i + 1) * tk].reshape(T, K).sum(0) for i in range(4))
+    mp = torch.where(mpc > 0, mps / mpc.clamp(min=1), torch.full_like(mps, -1.0))
+    if m_ap < 0:
+        mp = torch.full_like(mps, -1.0)
+    mr = torch.where(mrc > 0, mrs / mrc.clamp(min=1), torch.full_like(mrs, -1.0))
+    return (sp, cp, sr, cr), mp, mr
+
+
 def summarize_all(ev: Dict[str, Tensor], iou_thresholds: Sequence[float], max_dets: Sequence[int],
                   map_max_det: Optional[int] = None, class_ev: Optional[Dict[str, Tensor]] = None
                   ) -> Tuple[Tensor, Optional[Tensor], Optional[Tensor]]:
     """The summary numbers and (``class_ev`` given) the per-class mAP / mAR with ONE device->host transfer."""
+    fused = _summary_kernel(ev, max_dets, map_max_det, class_ev)
+    if fused is not None:
+        host, mp, mr = fused
+        stats = coco_summarize(ev, iou_thresholds, max_dets, map_max_det, host=host)
+        return (stats, None, None) if class_ev is None else (stats, mp, mr)
     parts = list(_masked_sums(ev))
     if class_ev is not None:
         parts += list(per_class_stats(class_ev, max_dets, map_max_det))

@@ -1325,6 +1325,18 @@ def coco_accumulate(dt_match: Tensor, dt_ig: Tensor, o: Tensor, rank_s: Tensor, 
     return True
 
 
+def coco_summary(prec: Tensor, rec: Tensor, cprec: Tensor, crec: Tensor, m_ap: int) -> Optional[Tensor]:
+    """Every sum COCO's summary and per-class numbers need, in one launch (``csrc/detection/coco_accumulate.hip``
+    coco_summary_kernel): an fp64 vector ``[psp, pcp]`` (``[T, ceil(K / 4), A*M]``: partial sums / counts of the defined
+    precision entries per group of 4 categories), ``[sr, cr]`` (``[T, A*M]``: recall over K), then
+    ``[mps, mpc, mrs, mrc]`` (``[T, K]``: per-category precision at (area 0, max-dets ``m_ap``; ``m_ap < 0``: zeros)
+    and recall at (area 0, last max-dets)).  None where the kernel does not apply (CPU tensors, A * M > 32)."""
+    T, R, K, A, M = prec.shape
+    if not prec.is_cuda or A * M > 32:
+        return None
+    return _ops().coco_summary(prec.contiguous(), rec.contiguous(), cprec.contiguous(), crec.contiguous(), int(m_ap))
+
+
 def panoptic_tables(pcode: Tensor, tcode: Tensor) -> List[Tensor]:
     """Per-image pixel areas of predicted segments, target segments and segment pairs from int32 ``[B, P]`` segment
     codes (``csrc/detection/panoptic.hip``: LDS hash tables, one block per image).  Returns pair keys (int64:

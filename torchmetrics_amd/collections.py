@@ -11,6 +11,8 @@ classification+regression collection that is one ``all_reduce`` per (op, dtype) 
 collectives in total.  Every member's ``compute()`` still returns the synced value and local states are restored
 afterwards, exactly like the per-metric path.
 """
+import operator
+from itertools import repeat
 from collections import OrderedDict
 from copy import deepcopy
 from typing import Any, Dict, Hashable, Iterable, Iterator, List, Optional, Sequence, Tuple, Union
@@ -82,8 +84,9 @@ class MetricCollection(ModuleDict):
             # then merged into one kernel pass for the whole collection (ops.run_moments_plans)
             sink: list = []
             submitted: list = []
+            modules = self._modules
             for name in names:
-                m0 = getattr(self, name)
+                m0 = modules[name]
                 if (done and id(m0) in done) or (replayed and id(m0) in replayed):
                     continue
                 d = m0.__dict__
@@ -124,7 +127,7 @@ class MetricCollection(ModuleDict):
         if _validation.STRICT or not rp.run(args[0], args[1]):
             self.__dict__["_moments_replay"] = None
             return None
-        return {id(m) for m in rp.members}
+        return rp.member_ids
 
     def _fused_update(self, names: List[str], args: tuple, kwargs: dict) -> Optional[set]:
         """Run the fused few-class multiclass update (utils/fused_update.py) for the leaders it serves; returns the
@@ -146,7 +149,7 @@ class MetricCollection(ModuleDict):
         plan = entry[1]
         if not plan.ok or not plan.run(args[0], args[1]):
             return None
-        return {id(m) for m in plan.metrics}
+        return plan.metric_ids
 
     def _merge_compute_groups(self) -> None:
         """Merge groups whose leaders hold identical states (O(M^2) pairwise, once)."""
@@ -186,6 +189,22 @@ class MetricCollection(ModuleDict):
         # called by every items() / values() / [] access: plain attributes go straight to __dict__ (they live there;
         # nn.Module.__setattr__ costs ~1 us per call), states through setattr only when a reference is stale
         d = self.__dict__
+        if not d["_state_is_copy"] and not copy:
+            # steady state: every follower already holds its leader's state objects -- one C-speed identity pass over
+            # flattened (leader, follower, state) lists built once per groups object (the per-state walk below was
+            # ~6 us per compute() of config #5)
+            groups = d.get("_groups")
+            fast = d.get("_ref_fast")
+            if fast is None or fast[0] is not groups:
+                fast = d["_ref_fast"] = (groups, *self._ref_fast_lists())
+            _, lead_d, foll_d, names, pairs = fast
+            lv = list(map(dict.get, lead_d, names))
+            if not any(map(operator.is_, lv, repeat(None))) and all(map(operator.is_, map(dict.get, foll_d, names), lv)):
+                for d0, di in pairs:
+                    di["_update_count"] = d0["_update_count"]
+                    if d0["_computed"] is None:
+                        di["_computed"] = None
+                return
         if not d["_state_is_copy"]:
             modules = self._modules
             for cg in self._groups.values():
@@ -211,6 +230,28 @@ class MetricCollection(ModuleDict):
                     elif d0["_computed"] is None:
                         di["_computed"] = None
         d["_state_is_copy"] = copy
+
+    def _ref_fast_lists(self) -> Tuple[List[dict], List[dict], List[str], List[Tuple[dict, dict]]]:
+        """(leader dicts, follower dicts, state names) flattened over every (follower, state) of the compute groups,
+        and the (leader dict, follower dict) pairs."""
+        lead_d: List[dict] = []
+        foll_d: List[dict] = []
+        names: List[str] = []
+        pairs: List[Tuple[dict, dict]] = []
+        modules = self._modules
+        for cg in self._groups.values():
+            if len(cg) == 1 or any(n not in modules for n in cg):
+                continue
+            d0 = modules[cg[0]].__dict__
+            states = list(modules[cg[0]]._defaults)
+            for name in cg[1:]:
+                di = modules[name].__dict__
+                pairs.append((d0, di))
+                for st in states:
+                    lead_d.append(d0)
+                    foll_d.append(di)
+                    names.append(st)
+        return lead_d, foll_d, names, pairs
 
     def compute(self) -> Dict[str, Any]:
         if _prof.ENABLED:
@@ -369,7 +410,7 @@ class MetricCollection(ModuleDict):
         # (descriptor rows holding device pointers) are rebuilt on first use in the copy
         state = self.__dict__.copy()
         for k in ("_status_host", "_status_ptr", "_fused_plan", "_compute_calls", "_fused_rebuilds", "_fused_off",
-                  "_family_plan", "_moments_replay", "_word_tables", "_word_table1"):
+                  "_family_plan", "_moments_replay", "_word_tables", "_word_table1", "_ref_fast"):
             state.pop(k, None)
         return state
 

@@ -44,6 +44,7 @@ class MomentsReplay:
 
     def __init__(self, members: List[Any], plan: "ops.MomentsPlan", preds: Tensor, target: Tensor) -> None:
         self.members = members
+        self.member_ids = frozenset(id(x) for x in self.members)
         self.versions = tuple(m.__dict__.get("_cfg_version", 0) for m in members)
         self.states = [(m.__dict__, tuple((k, m.__dict__.get(k)) for k in m._defaults)) for m in members]
         self.shape, self.dtype, self.device = preds.shape, preds.dtype, preds.device

@@ -20,6 +20,7 @@ states moved or replaced -- takes the members' own updates, which raise the refe
 does what each member's update does: the states accumulate in place, list states get their new elements, the
 validation words get the device-side target-range bit, and ``_update_count`` / ``_computed`` are maintained.
 """
+import operator
 from typing import Any, Dict, List, Optional, Tuple
 
 import torch
@@ -100,6 +101,7 @@ class FamilyPlan:
         self.C = C
         self.roles = roles
         self.metrics = [m for r in ("st", "cm", "cv", "cb") for m in roles[r]]
+        self.metric_ids = frozenset(id(m) for m in self.metrics)
         self.versions = tuple(m.__dict__.get("_cfg_version", 0) for m in self.metrics)
         self.ok = C is not None and len(self.metrics) >= 2  # one member alone keeps its own (native) update
         T = roles["cv"][0].thresholds.numel() if roles["cv"] else 0
@@ -118,7 +120,12 @@ class FamilyPlan:
         keys += [(m.__dict__, a) for m in roles["st"] for a in ("tp", "fp", "tn", "fn")]
         keys += [(m.__dict__, "confmat") for m in roles["cv"]]
         keys += [(m.__dict__, "_device_errors") for m in self.metrics]
+        if roles["cv"]:  # the threshold buffer the cached (thresholds, permutation) pair was built from
+            keys.append((roles["cv"][0].__dict__["_buffers"], "thresholds"))
         self._state_keys = keys
+        # the same pairs as two parallel lists: map(dict.get, dicts, names) walks them at C speed
+        self._sk_dicts = [d for d, _ in keys]
+        self._sk_names = [a for _, a in keys]
         self._state_cache: Optional[tuple] = None
 
     def valid(self, members: List[Tuple[str, Any]]) -> bool:
@@ -165,18 +172,25 @@ class FamilyPlan:
         dev = preds.device
         # the consumers' state objects as of the last run: unchanged (updated in place, the common case) -> the
         # checked argument lists are reused (a per-call walk of ~40 state checks was ~8 us of host time)
-        cur = tuple(d[a] if a in d else None for d, a in self._state_keys)
+        cur = list(map(dict.get, self._sk_dicts, self._sk_names))
         hit = self._state_cache
-        if hit is not None and hit[0] == dev and len(hit[1]) == len(cur) and all(
-                x is y for x, y in zip(hit[1], cur)):
-            cm, st, micro, curve, err = hit[2]
+        if hit is not None and hit[0] == dev and all(map(operator.is_, hit[1], cur)):
+            cm, st, micro, curve, err, thr, perm, bounds = hit[2]
         else:
             states = self._states(dev)
             if states is None:
                 return False
             cm, st, micro, curve = states
             err = [m._device_error_buffer(dev) for m in self.metrics if m.validate_args]
-            self._state_cache = (dev, cur, (cm, st, micro, curve, err))
+            thr = perm = bounds = _empty(dev)
+            if curve is not None:
+                m = self.roles["cv"][0]
+                thr, perm, _, _ = m._cws.get(m.thresholds.to(dev), C)
+            if self.roles["cb"]:
+                bounds = self.roles["cb"][0]._bounds(dev)
+            # (re-read: _device_error_buffer may have just created a word)
+            cur = list(map(dict.get, self._sk_dicts, self._sk_names))
+            self._state_cache = (dev, cur, (cm, st, micro, curve, err, thr, perm, bounds))
         preds, target = preds.contiguous(), target.contiguous()
         n = preds.shape[0]
         if self.work is None or self.work.device != dev:
@@ -184,17 +198,12 @@ class FamilyPlan:
             self.work = torch.zeros(words, dtype=torch.int32, device=dev)  # zero once: every fold re-zeroes it
             self.slot = 0
         empty = _empty(dev)
-        thr = perm = empty
-        if curve is not None:
-            m = self.roles["cv"][0]
-            thr, perm, _, _ = m._cws.get(m.thresholds.to(dev), C)
-        conf = acc = bounds = bins = empty
+        conf = acc = bins = empty
         cb = self.roles["cb"][0] if self.roles["cb"] else None
         cache = None
         if cb is not None:
             conf = torch.empty(n, dtype=torch.float32, device=dev)
             acc = torch.empty(n, dtype=torch.float32, device=dev)
-            bounds = cb._bounds(dev)
             if self.cand is None or self.cand.device != dev or self.cand.numel() < 4 * n:
                 self.cand = torch.empty(4 * max(n, 1024), dtype=torch.float32, device=dev)
             cache = _calibration_cache(cb, dev)

@@ -73,7 +73,13 @@ class MetricCollection(ModuleDict):
     def update(self, *args: Any, **kwargs: Any) -> None:
         """Update every metric (only the first member of each compute group once groups are known)."""
         if self._groups_checked or not self._enable_compute_groups:
-            names = [cg[0] for cg in self._groups.values()] if self._groups_checked else list(self._modules.keys())
+            d = self.__dict__
+            nc = d.get("_names_cache")
+            if nc is None or nc[0] is not d["_groups"] or nc[1] != self._groups_checked:
+                names = [cg[0] for cg in self._groups.values()] if self._groups_checked else list(self._modules.keys())
+                nc = d["_names_cache"] = (d["_groups"], self._groups_checked, names,
+                                          tuple(id(self._modules[n]) for n in names))
+            names = nc[2]
             # few-class multiclass leaders on the same (preds, target): ONE fused pass for all of them
             # (utils/fused_update.py, csrc/classification/family.hip)
             done = self._fused_update(names, args, kwargs)
@@ -141,7 +147,8 @@ class MetricCollection(ModuleDict):
             return None
 
         d = self.__dict__
-        ident = tuple(id(self._modules[n]) for n in names)
+        nc = d.get("_names_cache")
+        ident = nc[3] if nc is not None and nc[2] is names else tuple(id(self._modules[n]) for n in names)
         entry = d.get("_family_plan")
         if entry is None or entry[0] != ident or not entry[1].valid(None):
             entry = (ident, _fu.FamilyPlan([(n, self._modules[n]) for n in names]))
@@ -410,7 +417,8 @@ class MetricCollection(ModuleDict):
         # (descriptor rows holding device pointers) are rebuilt on first use in the copy
         state = self.__dict__.copy()
         for k in ("_status_host", "_status_ptr", "_fused_plan", "_compute_calls", "_fused_rebuilds", "_fused_off",
-                  "_family_plan", "_moments_replay", "_word_tables", "_word_table1", "_ref_fast"):
+                  "_family_plan", "_moments_replay", "_word_tables", "_word_table1", "_ref_fast",
+                  "_names_cache", "_ident_cache"):
             state.pop(k, None)
         return state
 
@@ -425,7 +433,11 @@ class MetricCollection(ModuleDict):
         d["_compute_calls"] = calls + 1
         if calls == 0 or d.get("_fused_off") or not _fc.enabled():
             return {}, {}
-        ident = tuple(id(m) for _, m in members)
+        ic = d.get("_ident_cache")
+        if ic is None or ic[0] is not d.get("_groups") or len(ic[1]) != len(members) or not all(
+                map(operator.is_, ic[2], (m for _, m in members))):
+            ic = d["_ident_cache"] = (d.get("_groups"), tuple(id(m) for _, m in members), [m for _, m in members])
+        ident = ic[1]
         plan = d.get("_fused_plan")
         if plan is None or plan[0] != ident or not plan[1].valid():
             rebuilds = d.get("_fused_rebuilds", 0)
@@ -462,14 +474,20 @@ class MetricCollection(ModuleDict):
         words in ONE native call that spins on a sequence number the kernel stores after the words (no stream-sync
         round trip, ``ops.read_words``), else the gather launch(es) + a stream sync."""
         d = self.__dict__
-        key = tuple((w.data_ptr(), c) for w, c in words)
         if len(words) <= 128:
+            # the same word tensors as last time (the steady state): their table is reused without re-reading any
+            # data_ptr (a word tensor's storage does not move)
             cached = d.get("_word_table1")
-            if cached is None or cached[0] != key:
-                cached = d["_word_table1"] = (key, torch.tensor([list(k) for k in key], dtype=torch.int64))
+            if (cached is None or len(cached[2]) != len(words)
+                    or not all(map(operator.is_, cached[2], (w for w, _ in words)))
+                    or cached[3] != [c for _, c in words]):
+                key = tuple((w.data_ptr(), c) for w, c in words)
+                cached = d["_word_table1"] = (key, torch.tensor([list(k) for k in key], dtype=torch.int64),
+                                              [w for w, _ in words], [c for _, c in words])
             fast = ops.read_words(cached[1], words[0][0])
             if fast is not None:
                 return fast
+        key = tuple((w.data_ptr(), c) for w, c in words)
         host = d.get("_status_host")
         if host is None or host.numel() < len(words):
             host = torch.zeros(max(128, len(words)), dtype=torch.int32, pin_memory=True)
@@ -505,11 +523,21 @@ class MetricCollection(ModuleDict):
                 fused, fchecks = self._fused_compute(members)
                 local = not fused or not _engine_dist_available()
                 with _deferred.defer() as dfr:
+                    items = dfr.items
+                    take = self._take_fused
                     for k, m in members:
                         val = fused.get(k) if fused else None
                         if val is not None and (local or m.__dict__["_is_synced"]):
-                            result[k] = self._take_fused(m, val)
-                            dfr.items.extend(fchecks.get(k, ()))
+                            md = m.__dict__
+                            # (the common case of _take_fused inline: no cached value, updated, cache on)
+                            if md["_computed"] is None and md["_update_count"] and md["compute_with_cache"]:
+                                md["_computed"] = val
+                                result[k] = val
+                            else:
+                                result[k] = take(m, val)
+                            chk = fchecks.get(k)
+                            if chk:
+                                items.extend(chk)
                         else:
                             result[k] = m.compute()
                 return self._finish_device_checks(plan, dfr.items)

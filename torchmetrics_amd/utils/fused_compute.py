@@ -280,24 +280,26 @@ class CollectionPlan:
                                for dt, off, shape, stride in f.leaves])
                 if f.checks:
                     checks[f.key] = [(bufs[dt][off : off + 1], msg, exc) for dt, off, msg, exc in f.checks]
-            c = self._reuse = _Outputs(raw, bufs, leaves, checks)
+            # the results too are built once per buffer: reused with it (a results mapping or container held outside
+            # holds its leaves, so idle() sees it)
+            results = {f.key: _rebuild(f.spec, lv) for f, lv in zip(self.fused, leaves)}
+            c = self._reuse = _Outputs(raw, bufs, leaves, checks, results)
         tasks = ops._ops().compute_tasks
         mx = 32
         for i in range(0, self.rows.shape[0], mx):
             tasks(self.rows[i : i + mx], c.raw, self.lds)
-        results = {f.key: _rebuild(f.spec, lv) for f, lv in zip(self.fused, c.leaves)}
-        return results, c.checks
+        return c.results, c.checks
 
 
 class _Outputs:
     """One run's output buffer and the views handed out from it, with the reference counts they have while only
     the plan holds them (see :meth:`CollectionPlan.run`)."""
 
-    __slots__ = ("raw", "bufs", "leaves", "checks", "storage", "use", "rc")
+    __slots__ = ("raw", "bufs", "leaves", "checks", "results", "storage", "use", "rc")
 
     def __init__(self, raw: Tensor, bufs: Dict[torch.dtype, Tensor], leaves: List[List[Tensor]],
-                 checks: Dict[str, List[Tuple[Tensor, str, Any]]]) -> None:
-        self.raw, self.bufs, self.leaves, self.checks = raw, bufs, leaves, checks
+                 checks: Dict[str, List[Tuple[Tensor, str, Any]]], results: Dict[str, Any]) -> None:
+        self.raw, self.bufs, self.leaves, self.checks, self.results = raw, bufs, leaves, checks, results
         self.storage = raw.untyped_storage()
         self.use = torch._C._storage_Use_Count(self.storage._cdata)
         # (counted the way idle() counts: the list's reference + the call's argument, no loop variable / zip tuple)

@@ -381,7 +381,10 @@ class MetricCollection(ModuleDict):
         if not words:
             return False
         dev = words[0][0].device
-        if any(w.device != dev for w, _ in words):
+        cached = self.__dict__.get("_word_table1")
+        same = (cached is not None and len(cached[2]) == len(words)
+                and all(map(operator.is_, cached[2], (w for w, _ in words))))  # (checked on one device before)
+        if not same and any(w.device != dev for w, _ in words):
             codes = [int(w.reshape(-1)[0].item()) if c == 0 else int(w.reshape(-1)[0].item() != 0)
                      for w, c in words]  # (several devices: rare, read each)
         else:

@@ -233,13 +233,13 @@ class CollectionPlan:
         ver = self._ver_keys
         if ver is None:
             ver = self._ver_keys = ([f.metric.__dict__ for f in self.fused], [f.version for f in self.fused],
-                                    [(m.__dict__, a) for m, a, _, _ in self.state_sig])
+                                    [m.__dict__ for m, _, _, _ in self.state_sig], [a for _, a, _, _ in self.state_sig])
         for d, v in zip(ver[0], ver[1]):
             if d.get("_cfg_version", 0) != v:
                 return False
         # the same state objects as at the last full check (the common case: states updated in place): valid, and
         # their memory has not moved (run() keeps the pointers it patched last time)
-        cur = [d.get(a) for d, a in ver[2]]
+        cur = list(map(dict.get, ver[2], ver[3]))
         seen = self._seen
         if seen is not None and len(cur) == len(seen) and all(map(operator.is_, cur, seen)):
             self._same = True

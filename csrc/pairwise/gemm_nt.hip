@@ -732,6 +732,10 @@ __device__ __attribute__((aligned(16))) uint32_t g_zero_chunk[4];  // the DMA so
 // one barrier apart so one wave per SIMD issues MFMAs while the other reads) ran 925-960 TFLOP/s at 4096^2 x 2048 against
 // 951-961 for this loop; its timing probes put the ceiling in the MFMA-and-barrier skeleton itself (no DMA: 1193, no DMA
 // and no barriers: 1222), not in the staging.
+// Also measured and dropped in round 6 (profiles/r06_bench_gemm16_w4_variant.jsonl): the library's own shape at this
+// tile, four waves of 128 x 128 (acc[4][4], 512 registers per lane, no spill; half the LDS reads per MFMA): 903 vs 956
+// TFLOP/s at 4096^2 x 2048, slower on every shape -- one wave per SIMD leaves the chunk barrier and the first fragment
+// reads after it exposed.
 // GRAN: bytes per DMA lane.  16 (the fast form) needs 16-byte aligned rows (D % 8 == 0, 16-byte aligned bases);
 // rows of any other width are staged in place into the SAME swizzled LDS layout, the K tail zero-filled element by
 // element -- no padded copy and no fp32 upcast of the operands: 4-byte DMA lanes for even widths (4x the

@@ -700,15 +700,74 @@ __device__ __forceinline__ int row_argmax_ord16(const unsigned char* __restrict_
   return static_cast<int>(0xffffu - (best & 0xffffu));
 }
 
+// Add one C x C (target, prediction) histogram held in LDS to its destination: the confusion matrix (kMcConfmat), the
+// stats workspace [tp | fp | fn | -] (kMcStats), or the four int64 states (kMcStatsDirect: out = tp; tn gets the
+// histogram's rows minus tp + fp + fn).  Every output is linear in the histogram, so per-block or per-group
+// histograms add up to the batch's.  `red`: >= C long longs of LDS scratch (not aliasing `hist`).  Block-uniform.
+template <typename count_t>
+__device__ __forceinline__ void flush_hist(const count_t* hist, int C, int mode, int64_t* __restrict__ out,
+                                           int64_t* __restrict__ fp_s, int64_t* __restrict__ tn_s,
+                                           int64_t* __restrict__ fn_s, long long* red) {
+  if (mode == kMcConfmat) {
+    for (int b = threadIdx.x; b < C * C; b += kBlock) {
+      const long long v = hist[b];
+      if (v) atomic_add_i64(out + b, v);
+    }
+    return;
+  }
+  const int c = threadIdx.x;  // C <= kTileMaxC < kBlock: one thread per class
+  long long tp = 0, row = 0, col = 0;
+  if (c < C) {
+    tp = hist[c * C + c];
+    for (int j = 0; j < C; ++j) {
+      row += hist[c * C + j];  // target c
+      col += hist[j * C + c];  // predicted c
+    }
+  }
+  if (mode == kMcStats) {
+    if (c < C) {
+      if (tp) atomic_add_i64(out + c, tp);
+      if (col - tp) atomic_add_i64(out + C + c, col - tp);
+      if (row - tp) atomic_add_i64(out + 2LL * C + c, row - tp);
+    }
+    return;
+  }
+  if (c < C) red[c] = row;
+  __syncthreads();
+  if (c < C) {
+    long long rows = 0;
+    for (int j = 0; j < C; ++j) rows += red[j];
+    if (tp) atomic_add_i64(out + c, tp);
+    if (col - tp) atomic_add_i64(fp_s + c, col - tp);
+    if (row - tp) atomic_add_i64(fn_s + c, row - tp);
+    if (rows - row - col + tp) atomic_add_i64(tn_s + c, rows - row - col + tp);
+  }
+}
+
+// Group hand-off of the tile kernel (tickets != nullptr): block b belongs to group b % ngroups (with blocks dispatched
+// round-robin over the XCDs, a group of 8 is one XCD's blocks); it stores its histogram to its partials row, and the
+// LAST block of each group to finish sums the group's rows and flushes them with flush_hist -- ngroups x (C^2 or 4C)
+// atomics instead of one per block, and no fold / finalize launch.  Only for C^2 <= 256 bins (the folder's loads stay
+// one round: 8 x 256 / C^2 rows per group); measured (1 M x 10 bf16): 9.9 us tile + 4.7 us fold kernel + finalize ->
+// 14.1 us in one launch (groups of 32 blocks, two load rounds: 17.9 us; per-block int64 flush: 26.8 us).  Memory model: the "sc1 payload" hand-off of
+// moments_handoff_kernel (agent-scope stores drained by vmcnt(0) before the barrier and the agent-scope ticket add;
+// agent-scope loads in the last block); the last block re-arms its ticket word.
+constexpr int kGroupLoads = 8;       // member rows per folding thread: a group's rows are ONE round of loads
+constexpr int kGroupMaxBlocks = 16;  // blocks per ticket word
+
 template <typename scalar_t, typename target_t, int NW>
 __global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t* __restrict__ preds,
                                                                  const target_t* __restrict__ target, long long N,
                                                                  int C, int R, long long ignore, bool has_ignore,
                                                                  int mode, int64_t* __restrict__ out,
-                                                                 int* __restrict__ part, int* __restrict__ flag) {
+                                                                 int* __restrict__ part, int* __restrict__ flag,
+                                                                 unsigned int* __restrict__ tickets, int ngroups,
+                                                                 int64_t* __restrict__ fp_s, int64_t* __restrict__ tn_s,
+                                                                 int64_t* __restrict__ fn_s) {
   // dynamic LDS: the C x C histogram (padded to 16 B), then the logits tile (+ 256 B: row_argmax_regs reads up to
   // NW + 1 dwords from the last row's start) -- a 10-class block takes 33 KiB, so 4 blocks fit a CU
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int last;
   const int ncm = C * C;
   int* hist = reinterpret_cast<int*>(smem);
   unsigned char* tile_raw = smem + ((ncm * 4 + 15) & ~15);
@@ -789,26 +848,64 @@ __global__ void __launch_bounds__(kBlock) mc_fewbins_tile_kernel(const scalar_t*
     }
   }
   __syncthreads();
-  if (part != nullptr) {  // this block's histogram, plain stores: fewbins_fold_kernel sums the blocks
+  if (tickets != nullptr) {
+    const int g = static_cast<int>(blockIdx.x % ngroups);
+    const int gsize = static_cast<int>((gridDim.x - g + ngroups - 1) / ngroups);
+    int* dst = part + static_cast<long long>(blockIdx.x) * ncm;
+    for (int b = threadIdx.x; b < ncm; b += kBlock)
+      __hip_atomic_store(dst + b, hist[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
+    __syncthreads();
+    if (threadIdx.x == 0)
+      last = __hip_atomic_fetch_add(tickets + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             static_cast<unsigned>(gsize - 1);
+    __syncthreads();
+    if (!last) return;
+    // the group's rows g, g + ngroups, ...: per bin, tpb threads each sum every tpb-th member row (independent loads,
+    // 8 in flight), then the tpb partial sums are combined in LDS (the tile area is free now)
+    long long* psum = reinterpret_cast<long long*>(tile_raw);                     // [tpb][ncm] when ncm <= kBlock
+    long long* tot = ncm <= kBlock ? psum + kBlock : psum;                        // [ncm]
+    long long* red = reinterpret_cast<long long*>(hist);                          // >= C long longs (C >= 2)
+    const int tpb = ncm <= kBlock ? kBlock / ncm : 1;
+    for (int b0 = 0; b0 < ncm; b0 += kBlock / tpb) {
+      const int b = b0 + (threadIdx.x % (kBlock / tpb)), j = threadIdx.x / (kBlock / tpb);
+      long long s = 0;
+      if (b < ncm && j < tpb) {
+        for (int m = j; m < gsize; m += 8 * tpb) {
+          int v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int mm = m + u * tpb;
+            v[u] = mm < gsize ? __hip_atomic_load(part + static_cast<long long>(g + mm * ngroups) * ncm + b,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : 0;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) s += v[u];
+        }
+      }
+      if (tpb == 1) {
+        if (b < ncm) tot[b] = s;
+      } else if (b < ncm && j < tpb) {
+        psum[j * ncm + b] = s;
+      }
+    }
+    if (tpb > 1) {
+      __syncthreads();
+      for (int b = threadIdx.x; b < ncm; b += kBlock) {
+        long long s = 0;
+        for (int j = 0; j < tpb; ++j) s += psum[j * ncm + b];
+        tot[b] = s;
+      }
+    }
+    __syncthreads();
+    flush_hist(tot, C, mode, out, fp_s, tn_s, fn_s, red);
+    if (threadIdx.x == 0) __hip_atomic_store(tickets + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+  } else if (part != nullptr) {  // this block's histogram, plain stores: fewbins_fold_kernel sums the blocks
     int* dst = part + static_cast<long long>(blockIdx.x) * ncm;
     for (int b = threadIdx.x; b < ncm; b += kBlock) dst[b] = hist[b];
-  } else if (mode == kMcConfmat) {
-    for (int b = threadIdx.x; b < ncm; b += kBlock) {
-      const int v = hist[b];
-      if (v) atomic_add_i64(out + b, v);
-    }
-  } else {  // stats workspace [tp | fp | fn | -]
-    for (int c = threadIdx.x; c < C; c += kBlock) {
-      const int tp = hist[c * C + c];
-      int row = 0, col = 0;
-      for (int j = 0; j < C; ++j) {
-        row += hist[c * C + j];
-        col += hist[j * C + c];
-      }
-      if (tp) atomic_add_i64(out + c, tp);
-      if (col - tp) atomic_add_i64(out + C + c, col - tp);
-      if (row - tp) atomic_add_i64(out + 2LL * C + c, row - tp);
-    }
+  } else {  // per-block flush (a few blocks)
+    flush_hist(hist, C, mode, out, fp_s, tn_s, fn_s, reinterpret_cast<long long*>(tile_raw));
   }
 }
 
@@ -1601,6 +1698,88 @@ __global__ void __launch_bounds__(kFoldThreads) bin_partials_finalize_kernel(
 // reset of the per-call logit flag is ordered after the finalize (same stream) -- only for one-word flags
 __global__ void zero_int_kernel(int* p) { *p = 0; }
 
+int fewbins_tile_per_cu() {  // blocks per CU of the tiled kernel; 0 = off
+  static const int v = [] {
+    const char* e = std::getenv("TM_AMD_FEWBINS_TILE");
+    return e ? std::atoi(e) : 3;  // measured (1 M x 10 bf16, fold path): 3 / CU 10.4 us, 2 / CU 12.0
+  }();
+  return v;
+}
+
+// rows per thread per tile: as many as fit 32 KiB of logits (at most kTileRows; TM_AMD_FEWBINS_R caps it)
+long long fewbins_tile_rows(int C, size_t elem) {
+  static const int r_cap = [] {
+    const char* e = std::getenv("TM_AMD_FEWBINS_R");
+    return e ? std::max(1, std::min(kTileRows, std::atoi(e))) : kTileRows;
+  }();
+  // (fewer rows per tile -- more blocks for a small batch -- measured slower: every block adds a histogram)
+  return std::min<long long>(r_cap, (kTileChunks * 16LL) / (static_cast<long long>(C) * static_cast<long long>(elem)));
+}
+
+// short rows (<= 128 B, <= 64 classes, X == 1, 16-byte aligned logits): the tiled kernel with its C x C LDS histogram
+bool fewbins_tile_fits(const void* preds, int C, size_t elem) {
+  return fewbins_tile_per_cu() > 0 && C >= 2 && C <= kTileMaxC && fewbins_tile_rows(C, elem) >= 1 &&
+         reinterpret_cast<uintptr_t>(preds) % 16 == 0;
+}
+
+// The tiled few-class kernel and how its blocks' histograms reach the destination (mode: kMcConfmat -> out = the
+// matrix; kMcStats -> out = the stats workspace; kMcStatsDirect -> out = tp, fp_s / tn_s / fn_s = the other states):
+//   * <= kFoldMinBlocks blocks: per-block atomics;
+//   * C^2 <= 256: the group hand-off inside the one launch;
+//   * else: partials + fewbins_fold_kernel (TM_AMD_FEWBINS_FUSED=0 forces this for the confusion matrix and the
+//     workspace: the round-5 form, for A/B; kMcStatsDirect keeps the hand-off -- the fold has no state destinations).
+template <typename scalar_t, typename target_t>
+void fewbins_tile_launch(const scalar_t* pp, const target_t* tp, long long N, int C, long long ignore_index,
+                         bool has_ignore, int mode, int64_t* outp, int64_t* fp_s, int64_t* tn_s, int64_t* fn_s,
+                         int* flagp, const at::Tensor& preds, hipStream_t s) {
+  const long long R = fewbins_tile_rows(C, sizeof(scalar_t));
+  const long long ntiles = (N + kBlock * R - 1) / (kBlock * R);
+  const int tgrid = static_cast<int>(
+      std::min<long long>(ntiles, static_cast<long long>(cu_count(preds.get_device())) * fewbins_tile_per_cu()));
+  static const bool fused_on = [] {
+    const char* e = std::getenv("TM_AMD_FEWBINS_FUSED");
+    return !e || std::atoi(e) != 0;
+  }();
+  static const int group_env = [] {  // measurement knob: blocks per hand-off group (0: per-block atomic flush)
+    const char* e = std::getenv("TM_AMD_FEWBINS_GROUP");
+    return e ? std::max(0, std::atoi(e)) : -1;
+  }();
+  const int ncm = C * C;
+  // a few blocks (small batches) flush with atomics: neither a fold launch nor a hand-off tail pays for them
+  const bool few = tgrid <= kFoldMinBlocks || group_env == 0;
+  const bool handoff = !few && ncm <= kBlock && (fused_on || mode == kMcStatsDirect);
+  const bool fold = !few && !handoff;
+  // one round of loads in the folder (kGroupLoads rows per bin-thread, 256 / C^2 threads per bin), and at most
+  // kGroupMaxBlocks ticket adds per word: the adds to one address serialise (C = 2 in ONE group of 512 blocks: 16.7 us
+  // against the fold launch's 13.7)
+  const int gsize = group_env > 0 ? group_env : std::min(kGroupMaxBlocks, kGroupLoads * (kBlock / std::max(ncm, 1)));
+  const int ngroups = handoff ? std::min(kStreamTickets - 1, (tgrid + gsize - 1) / gsize) : 0;
+  unsigned int* tickets = handoff ? stream_ticket(preds.get_device(), s) + 1 : nullptr;
+  at::Tensor part;
+  if (handoff || fold) part = at::empty({static_cast<long long>(tgrid) * ncm}, preds.options().dtype(at::kInt));
+  int* partp = (handoff || fold) ? part.data_ptr<int>() : nullptr;
+  const size_t smem = static_cast<size_t>((ncm * 4 + 15) & ~15) + kTileChunks * kBlock * 16 + 256;
+  // dwords per row for the register argmax: 8 (rows <= 32 B) or 32 (<= 128 B); 8-byte scores read LDS
+  const long long rbytes = static_cast<long long>(C) * sizeof(scalar_t);
+  auto launch_tile = [&](auto nw_tag) {
+    constexpr int NW = decltype(nw_tag)::value;
+    hipLaunchKernelGGL((mc_fewbins_tile_kernel<scalar_t, target_t, NW>), dim3(tgrid), dim3(kBlock), smem, s, pp, tp,
+                       N, C, static_cast<int>(R), ignore_index, has_ignore, mode, outp, partp, flagp, tickets, ngroups,
+                       fp_s, tn_s, fn_s);
+    if (fold)
+      hipLaunchKernelGGL(fewbins_fold_kernel,
+                         dim3((ncm + kWave - 1) / kWave,
+                              (tgrid + kFoldThreads / kWave * kFoldRows - 1) / (kFoldThreads / kWave * kFoldRows)),
+                         dim3(kFoldThreads), 0, s, partp, tgrid, C, mode, outp);
+  };
+  if constexpr (sizeof(scalar_t) == 2 || sizeof(scalar_t) == 4) {
+    if (rbytes <= 32) launch_tile(std::integral_constant<int, 8>{});
+    else launch_tile(std::integral_constant<int, 32>{});
+  } else {
+    launch_tile(std::integral_constant<int, 0>{});
+  }
+}
+
 }  // namespace
 
 // The "scores are not probabilities" word of the binary / multilabel path, double-buffered by update parity when the
@@ -1770,54 +1949,9 @@ void mc_update(const at::Tensor& preds, const at::Tensor& target, at::Tensor out
       const scalar_t* pp = reinterpret_cast<const scalar_t*>(preds.data_ptr());
       if constexpr (IsFloating<scalar_t>::value) {
         const bool vec = (C * sizeof(scalar_t)) % 16 == 0 && (reinterpret_cast<uintptr_t>(pp) % 16) == 0;
-        static const int tile_grid = [] {
-          const char* e = std::getenv("TM_AMD_FEWBINS_TILE");  // blocks per CU of the tiled kernel; 0 = off
-          return e ? std::atoi(e) : 3;  // measured (1 M x 10 bf16, fold path): 3 / CU 10.4 us, 2 / CU 12.0
-        }();
-        // rows per thread per tile: as many as fit 32 KiB of logits (at most kTileRows; TM_AMD_FEWBINS_R caps it)
-        static const int r_cap = [] {
-          const char* e = std::getenv("TM_AMD_FEWBINS_R");
-          return e ? std::max(1, std::min(kTileRows, std::atoi(e))) : kTileRows;
-        }();
-        // (fewer rows per tile -- more blocks for a small batch -- measured slower: every block adds a histogram)
-        const long long R = std::min<long long>(r_cap, (kTileChunks * 16LL) / (static_cast<long long>(C) * sizeof(scalar_t)));
-        // short rows (<= 128 B, <= 64 classes): the tiled kernel with its C x C LDS histogram
-        const bool tile_rows = tile_grid > 0 && !samplewise && X == 1 && C <= kTileMaxC && R >= 1 &&
-                               reinterpret_cast<uintptr_t>(pp) % 16 == 0;
-        if (tile_rows) {
-          const long long ntiles = (N + kBlock * R - 1) / (kBlock * R);
-          const int tgrid = static_cast<int>(
-              std::min<long long>(ntiles, static_cast<long long>(cu_count(preds.get_device())) * tile_grid));
-          // dwords per row for the register argmax: 8 (rows <= 32 B) or 32 (<= 128 B); 8-byte scores read LDS
-          const long long rbytes = static_cast<long long>(C) * sizeof(scalar_t);
-          static const bool fold_on = [] {
-            const char* e = std::getenv("TM_AMD_FEWBINS_FOLD");  // 0: per-block global-atomic flush (A/B)
-            return !e || std::atoi(e) != 0;
-          }();
-          const int ncm = C * C;
-          // a few blocks (small batches) flush with atomics: the fold's extra launch would cost more than their chains
-          const bool fold = fold_on && tgrid > kFoldMinBlocks;
-          at::Tensor part;
-          if (fold) part = at::empty({static_cast<long long>(tgrid) * ncm}, preds.options().dtype(at::kInt));
-          int* partp = fold ? part.data_ptr<int>() : nullptr;
-          const size_t smem = static_cast<size_t>((ncm * 4 + 15) & ~15) + kTileChunks * kBlock * 16 + 256;
-          auto launch_tile = [&](auto nw_tag) {
-            constexpr int NW = decltype(nw_tag)::value;
-            hipLaunchKernelGGL((mc_fewbins_tile_kernel<scalar_t, target_t, NW>), dim3(tgrid), dim3(kBlock), smem, s,
-                               pp, tp, N, C, static_cast<int>(R), ignore_index, has_ignore, static_cast<int>(mode),
-                               outp, partp, flagp);
-            if (fold)
-              hipLaunchKernelGGL(fewbins_fold_kernel,
-                                 dim3((ncm + kWave - 1) / kWave,
-                                      (tgrid + kFoldThreads / kWave * kFoldRows - 1) / (kFoldThreads / kWave * kFoldRows)),
-                                 dim3(kFoldThreads), 0, s, partp, tgrid, C, static_cast<int>(mode), outp);
-          };
-          if constexpr (sizeof(scalar_t) == 2 || sizeof(scalar_t) == 4) {
-            if (rbytes <= 32) launch_tile(std::integral_constant<int, 8>{});
-            else launch_tile(std::integral_constant<int, 32>{});
-          } else {
-            launch_tile(std::integral_constant<int, 0>{});
-          }
+        if (!samplewise && X == 1 && fewbins_tile_fits(pp, C, sizeof(scalar_t))) {
+          fewbins_tile_launch(pp, tp, N, C, ignore_index, has_ignore, static_cast<int>(mode), outp, nullptr, nullptr,
+                              nullptr, flagp, preds, s);
         } else if (X == 1 && C >= 32 && vec) {
           // rows of <= 16 lanes x 8 loads x 16 B go 16 lanes per row; longer rows use the whole wave per row
           const long long row_bytes = static_cast<long long>(C) * sizeof(scalar_t);
@@ -1939,18 +2073,40 @@ bool mc_stats_direct(const at::Tensor& preds, const at::Tensor& target, at::Tens
   const long long C = num_classes;
   if (!preds.is_cuda() || preds.dim() != 2 || target.dim() != 1 || preds.size(1) != C || preds.size(0) != target.size(0))
     return false;
-  if (preds.scalar_type() != at::kBFloat16 && preds.scalar_type() != at::kHalf) return false;
+  const bool f32 = preds.scalar_type() == at::kFloat;
+  if (preds.scalar_type() != at::kBFloat16 && preds.scalar_type() != at::kHalf && !f32) return false;
   if (target.scalar_type() != at::kLong && target.scalar_type() != at::kInt) return false;
   if (!preds.is_contiguous() || !target.is_contiguous() || reinterpret_cast<uintptr_t>(preds.data_ptr()) % 16 != 0)
     return false;
-  const long long row_bytes = C * 2;
-  if (row_bytes % 16 != 0 || row_bytes < 1024 || row_bytes > 4 * 1024) return false;
   for (const at::Tensor* t : {&tp, &fp, &tn, &fn})
     if (!t->is_cuda() || t->get_device() != preds.get_device() || t->scalar_type() != at::kLong ||
         !t->is_contiguous() || t->numel() != C)
       return false;
   static const bool off = std::getenv("TM_AMD_MC_STATS_DIRECT") && std::atoi(std::getenv("TM_AMD_MC_STATS_DIRECT")) == 0;
   if (off) return false;
+  // few classes (C <= 16): the tiled kernel, its group hand-off flushing straight into the states
+  if (C * C <= kBlock && fewbins_tile_fits(preds.data_ptr(), static_cast<int>(C), preds.element_size())) {
+    const long long N = preds.size(0);
+    if (N == 0) return true;
+    auto s = stream();
+    TM_DISPATCH_TARGET(target.scalar_type(), "mc_stats_direct", [&] {
+      const target_t* tg = reinterpret_cast<const target_t*>(target.data_ptr());
+      auto go = [&](auto scalar_tag) {
+        using scalar_t = decltype(scalar_tag);
+        fewbins_tile_launch(reinterpret_cast<const scalar_t*>(preds.data_ptr()), tg, N, static_cast<int>(C), 0LL,
+                            false, kMcStatsDirect, tp.data_ptr<int64_t>(), fp.data_ptr<int64_t>(),
+                            tn.data_ptr<int64_t>(), fn.data_ptr<int64_t>(), flag.data_ptr<int>(), preds, s);
+      };
+      if (preds.scalar_type() == at::kBFloat16) go(c10::BFloat16{});
+      else if (preds.scalar_type() == at::kHalf) go(c10::Half{});
+      else go(float{});
+    });
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+    return true;
+  }
+  if (f32) return false;
+  const long long row_bytes = C * 2;
+  if (row_bytes % 16 != 0 || row_bytes < 1024 || row_bytes > 4 * 1024) return false;
   const long long N = preds.size(0);
   if (N == 0) return true;
   auto s = stream();

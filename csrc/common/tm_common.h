@@ -269,6 +269,13 @@ inline void launch_zero_words(int* p, int n, hipStream_t s) {
   hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, s, p, n);
 }
 
+// kStreamTickets zeroed uint32 words per (device, stream), kept for the process (csrc/regression/moments.hip): the
+// last-block hand-offs count finished blocks in them and every kernel re-arms (zeroes) the words it used before it
+// ends, so consecutive launches on a stream -- which never overlap -- share them.  Word 0: the moments kernels;
+// words 1..127: the few-class tile kernel's hand-off groups (stat_scores.hip).
+constexpr int kStreamTickets = 128;
+unsigned int* stream_ticket(int device, hipStream_t s);
+
 // CU count of a device, queried once per device (hipDeviceGetAttribute costs host time on every call).
 inline int cu_count(int device) {
   static int cache[64] = {0};

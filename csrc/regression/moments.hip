@@ -578,9 +578,9 @@ __global__ void __launch_bounds__(kHandoffThreads) moments_handoff_kernel(
 
 }  // namespace
 
-// One zeroed uint32 per (device, stream), kept for the process: the last-block fold of moments_partial_kernel counts
-// finished blocks in it and resets it, so consecutive launches on a stream reuse it (launches on one stream never
-// overlap).
+// kStreamTickets zeroed uint32 words per (device, stream), kept for the process (tm_common.h): the last-block folds
+// of moments_partial_kernel / moments_handoff_kernel count finished blocks in word 0 and reset it, so consecutive
+// launches on a stream reuse it (launches on one stream never overlap).
 unsigned int* stream_ticket(int device, hipStream_t s) {
   static std::mutex mu;
   // never destroyed: the tensors must not be freed after the runtime has shut down at process exit
@@ -589,7 +589,8 @@ unsigned int* stream_ticket(int device, hipStream_t s) {
   auto key = std::make_pair(device, s);
   auto it = tickets->find(key);
   if (it == tickets->end())
-    it = tickets->emplace(key, at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, device))).first;
+    it = tickets->emplace(key, at::zeros({kStreamTickets}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, device)))
+             .first;
   return reinterpret_cast<unsigned int*>(it->second.data_ptr<int>());
 }
 

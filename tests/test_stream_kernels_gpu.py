@@ -167,3 +167,32 @@ def test_multilabel_vec_probability_range_edges(dtype, odd):
     assert gg[2] == cc[2]  # the probabilities / logits decision
     if odd not in ("nan", "neg_nan"):
         assert torch.equal(gg[0], cc[0])
+
+
+@pytest.mark.parametrize("dtype,C", [(torch.bfloat16, 2), (torch.bfloat16, 10), (torch.float16, 17),
+                                     (torch.bfloat16, 64), (torch.float32, 10), (torch.float32, 31)])
+@pytest.mark.parametrize("N", [1, 255, 3000, 100_003, 1 << 22])
+def test_fewbins_group_handoff_states(dtype, C, N):
+    """Few-class multiclass stats straight into the tp / fp / tn / fn states in one launch (mc_stats_direct ->
+    mc_fewbins_tile_kernel's group hand-off: the last block of each group sums its partial rows and adds them to the
+    states; tickets re-armed by the kernel): repeated updates of different batches, then the confusion matrix (same
+    hand-off, matrix destination), equal to the CPU module."""
+    import torchmetrics_amd as tm
+
+    g = torch.Generator().manual_seed(C * 7 + N % 1013)
+    ms = tm.MulticlassStatScores(C, average="none").to(DEV)
+    cm = tm.MulticlassConfusionMatrix(C).to(DEV)
+    rs, rc = tm.MulticlassStatScores(C, average="none"), tm.MulticlassConfusionMatrix(C)
+    for i in range(3):
+        p = torch.randn(N, C, generator=g).to(dtype)
+        t = torch.randint(0, C, (N,), generator=g)
+        if i == 1:
+            p[::3] = 0.0  # ties: first index
+        ms.update(p.to(DEV), t.to(DEV))
+        cm.update(p.to(DEV), t.to(DEV))
+        rs.update(p.float(), t)
+        rc.update(p.float(), t)
+    for k in ("tp", "fp", "tn", "fn"):
+        assert torch.equal(getattr(ms, k).cpu(), getattr(rs, k)), k
+    assert torch.equal(ms.compute().cpu(), rs.compute())
+    assert torch.equal(cm.compute().cpu(), rc.compute())

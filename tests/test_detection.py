@@ -510,6 +510,56 @@ def test_coco_accumulate_kernel_matches_torch_path(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("score_dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("average", ["macro", "micro"])
+@pytest.mark.parametrize("variant", ["plain", "int32_labels_no_area", "big_images"])
+def test_coco_prepare_kernel_matches_aten_grouping(monkeypatch, score_dtype, average, variant):
+    """The one-launch grouping stage (csrc/detection/coco_prepare.hip: per-image LDS ranking into (image, category,
+    score) order, group tables, non-ignored ground-truth histogram) gives bit-identical precision / recall / scores and
+    summary to the ATen grouping path (sorts, histograms, gathers): score ties, crowds, areas absent (box area used),
+    int32 labels, empty images, images larger than a block (> 256 detections) and micro averaging (labels outside the
+    category axis)."""
+    from torchmetrics_amd.detection import _coco_eval
+
+    dev = torch.device("cuda", 0)
+    big = variant == "big_images"
+    preds, target = _random_coco(11, n_img=10, n_cls=5, max_gt=40 if big else 8, max_det=700 if big else 15)
+    preds[3] = {"boxes": torch.zeros(0, 4), "scores": torch.zeros(0), "labels": torch.zeros(0, dtype=torch.long)}
+    target[5] = {"boxes": torch.zeros(0, 4), "labels": torch.zeros(0, dtype=torch.long),
+                 "iscrowd": torch.zeros(0, dtype=torch.long)}
+    for p in preds:
+        p["scores"] = p["scores"].to(score_dtype)
+        if variant == "int32_labels_no_area":
+            p["labels"] = p["labels"].int()
+    for t in target:
+        if variant == "int32_labels_no_area":
+            t["labels"] = t["labels"].int()
+        else:
+            t["area"] = torch.where(torch.rand(t["labels"].numel()) < 0.3, torch.zeros(t["labels"].numel()),
+                                    torch.rand(t["labels"].numel()) * 9000)
+    mdt = [1, 10, 300] if big else [1, 7, 50]
+
+    def run():
+        m = MeanAveragePrecision(class_metrics=True, extended_summary=True, max_detection_thresholds=mdt,
+                                 average=average).to(dev)
+        m.update(_to(preds[:6], dev), _to(target[:6], dev))
+        m.update(_to(preds[6:], dev), _to(target[6:], dev))
+        return m.compute()
+
+    calls = []
+    real = ops.coco_prepare
+    monkeypatch.setattr(ops, "coco_prepare", lambda *a: calls.append(1) or real(*a))
+    fused = run()
+    assert calls, "the prepared path did not run"
+    monkeypatch.setattr(_coco_eval, "PREP_MAX_PER_IMAGE", -1)
+    ref = run()
+    for key in ref:
+        if key == "ious":
+            continue
+        assert torch.equal(fused[key], ref[key]), key
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("backend,mdt", [("faster_coco_eval", [1, 7, 50]), ("pycocotools", [1, 7, 50]),
                                          ("pycocotools", [1, 10, 100])])
 @pytest.mark.parametrize("average", ["macro", "micro"])

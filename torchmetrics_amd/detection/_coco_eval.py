@@ -23,7 +23,34 @@ from torch import Tensor
 from torchmetrics_amd import ops
 
 AREA_RANGES = ((0.0, 1e5**2), (0.0, 32.0**2), (32.0**2, 96.0**2), (96.0**2, 1e5**2))
+
+# device copies of the configuration constants (IoU / recall thresholds, area ranges), made once per (device, values):
+# a ``torch.tensor(..., device=dev)`` from host memory is a synchronous copy that drains the stream, so three of them
+# per compute() kept the host from running ahead of the device
+_CONST: Dict[Tuple[torch.device, Tuple[float, ...]], Tensor] = {}
+
+
+def _device_const(values: Sequence, dev: torch.device) -> Tensor:
+    key = (dev, tuple(float(v) for v in values))
+    t = _CONST.get(key)
+    if t is None:
+        if len(_CONST) > 64:
+            _CONST.clear()
+        t = _CONST[key] = torch.tensor(key[1], dtype=torch.float64, device=dev)
+    return t
+
+
+def _to_device_async(values: List[int], dev: torch.device) -> Tensor:
+    """int64 host values on ``dev`` without draining the stream: a pinned staging buffer and a non-blocking copy (a
+    pageable source makes the copy wait for the device's queue)."""
+    t = torch.tensor(values, dtype=torch.long)
+    if dev.type == "cpu":
+        return t
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
 AREA_LABELS = ("all", "small", "medium", "large")
+PREP_MAX_PER_IMAGE = 2048  # csrc/detection/coco_prepare.hip kPrepMaxPerImage
 
 
 def _segment_starts(sorted_keys: Tensor) -> Tensor:
@@ -121,9 +148,9 @@ def coco_evaluate(
     """
     dev = classes.device
     n_img = len(det_labels)
-    t_thr = torch.tensor(list(iou_thresholds), dtype=torch.float64, device=dev)
-    r_thr = torch.tensor(list(rec_thresholds), dtype=torch.float64, device=dev)
-    areas = torch.tensor(AREA_RANGES, dtype=torch.float64, device=dev)
+    t_thr = _device_const(iou_thresholds, dev)
+    r_thr = _device_const(rec_thresholds, dev)
+    areas = _device_const([a for r in AREA_RANGES for a in r], dev).reshape(-1, 2)
     T, R, A, M, K = t_thr.numel(), r_thr.numel(), areas.shape[0], len(max_dets), classes.numel()
     # (every entry is written below: by the accumulation kernel, which also writes -1 for categories without a
     # non-ignored ground truth, or by the torch path and the final mask)
@@ -142,11 +169,15 @@ def coco_evaluate(
     # group starts (no segmented cummax), and the image index expansion with a host-known output size.
     d_sizes, g_sizes = image_sizes(det_labels), image_sizes(gt_labels)
     n_det, n_gt = int(sum(d_sizes)), int(sum(g_sizes))
+    if det_rle is None and dev.type == "cuda":
+        fast = _evaluate_prepared(det_boxes, det_scores, det_labels, gt_boxes, gt_labels, gt_crowds, gt_areas, d_sizes,
+                                  g_sizes, classes, t_thr, r_thr, areas, max_dets, precision, recall, scores_out)
+        if fast:
+            return {"precision": precision, "recall": recall, "scores": scores_out}
     img_ids = torch.arange(n_img, device=dev)
-    d_img = torch.repeat_interleave(img_ids, torch.tensor(d_sizes, dtype=torch.long).to(dev, non_blocking=True),
-                                    output_size=n_det)
-    g_img = torch.repeat_interleave(img_ids, torch.tensor(g_sizes, dtype=torch.long).to(dev, non_blocking=True),
-                                    output_size=n_gt)
+    sizes_dev = _to_device_async(list(d_sizes) + list(g_sizes), dev)  # one pinned, non-blocking copy for both
+    d_img = torch.repeat_interleave(img_ids, sizes_dev[:n_img], output_size=n_det)
+    g_img = torch.repeat_interleave(img_ids, sizes_dev[n_img:], output_size=n_gt)
     d_lab, g_lab = flat(det_labels, torch.long), flat(gt_labels, torch.long)
     d_cls = torch.searchsorted(classes, d_lab).clamp(max=K - 1)
     g_cls = torch.searchsorted(classes, g_lab).clamp(max=K - 1)
@@ -287,6 +318,63 @@ def coco_evaluate(
         scores_out.masked_fill_(missing[None, None, :, :, None], -1.0)
         recall.masked_fill_(missing[None, :, :, None], -1.0)
     return {"precision": precision, "recall": recall, "scores": scores_out}
+
+
+def _evaluate_prepared(det_boxes, det_scores, det_labels, gt_boxes, gt_labels, gt_crowds, gt_areas,
+                       d_sizes: List[int], g_sizes: List[int], classes: Tensor, t_thr: Tensor, r_thr: Tensor,
+                       areas: Tensor, max_dets: Sequence[int], precision: Tensor, recall: Tensor,
+                       scores_out: Tensor) -> bool:
+    """ROCm bbox path: the grouping stage in ONE launch (``ops.coco_prepare``: per image, every detection / ground
+    truth ranks itself against the image's (category, score) keys in LDS and writes itself into matcher order, with
+    the group starts / counts and the non-ignored ground-truth histogram), then the matcher, ONE (category, score)
+    sort and the accumulation kernel.  The same arrays as the ATen grouping below, but ~35 launches instead of ~160
+    (compute() was host-bound on them).  False (nothing written) where it does not apply: fp64 scores, images of more
+    than ``PREP_MAX_PER_IMAGE`` annotations, non-integer labels / crowds."""
+    dev = classes.device
+    n_img = len(d_sizes)
+    if n_img == 0 or max(max(d_sizes, default=0), max(g_sizes, default=0)) > PREP_MAX_PER_IMAGE:
+        return False
+    d_lab = cat_states(det_labels, dev).reshape(-1)
+    g_lab = cat_states(gt_labels, dev).reshape(-1)
+    d_score = cat_states(det_scores, dev).reshape(-1)
+    g_crowd = cat_states(gt_crowds, dev).reshape(-1)
+    g_area = cat_states(gt_areas, dev).reshape(-1)
+    d_box = cat_states(det_boxes, dev, (4,))
+    g_box = cat_states(gt_boxes, dev, (4,))
+    ints, floats = (torch.int64, torch.int32, torch.int16, torch.uint8, torch.bool), \
+        (torch.float32, torch.float64, torch.float16, torch.bfloat16)
+    if g_area.dtype in ints:  # (no "area" key: the zero defaults carry the labels' dtype)
+        g_area = g_area.to(torch.float64)
+    if d_score.dtype not in floats[:1] + floats[2:] or any(t.dtype not in ints for t in (d_lab, g_lab, g_crowd)) or \
+            any(t.dtype not in floats for t in (d_box, g_box, g_area)):
+        return False
+    off = [0] * (2 * (n_img + 1))
+    acc = 0
+    for i, v in enumerate(d_sizes):
+        acc += v
+        off[i + 1] = acc
+    acc = 0
+    for i, v in enumerate(g_sizes):
+        acc += v
+        off[n_img + 2 + i] = acc
+    K, A = classes.numel(), areas.shape[0]
+    G = n_img * K
+    (tables, d_box_s, d_area_s, rank_v, cls_k, score_k, key2, g_box_s, g_area_s,
+     g_crowd_s) = ops.coco_prepare(classes, _to_device_async(off, dev), d_lab.contiguous(), d_score.contiguous(),
+                                   d_box.contiguous(), g_lab.contiguous(), g_box.contiguous(), g_crowd.contiguous(),
+                                   g_area.contiguous(), areas.reshape(-1), n_img, int(max_dets[-1]),
+                                   max(max(d_sizes, default=0), max(g_sizes, default=0)))
+    dt_match, dt_ig = ops.coco_match(d_box_s, d_area_s, g_box_s, g_area_s, g_crowd_s, tables[:G], tables[G:2 * G],
+                                     tables[2 * G:3 * G], tables[3 * G:4 * G], areas.reshape(-1), t_thr, None, None)
+    npig = tables[4 * G:].reshape(A, K).to(torch.float64)
+    # (3) accumulate: detections of each category in score order (ties: image, then rank -- the prepared order);
+    # categories not on the K axis carry index K and sort last
+    o = torch.sort(key2, stable=True).indices
+    cls_s, rank_s, score_s = cls_k[o], rank_v[o], score_k[o]
+    # (where the accumulation kernel does not apply -- T * A > 63, more than 8 max-dets values, no detections -- the
+    # caller's ATen path runs from the start)
+    return ops.coco_accumulate(dt_match, dt_ig, o, rank_s, score_s, cls_s, npig, r_thr, max_dets, precision, recall,
+                               scores_out)
 
 
 def _masked_mean(s: Tensor) -> Tensor:

@@ -259,10 +259,25 @@ class MeanAveragePrecision(Metric):
         return out
 
     def _get_classes_uncached(self) -> List[int]:
+        return self._classes_both()[0]
+
+    def _classes_both(self) -> Tuple[List[int], Optional[Tensor]]:
+        """The sorted category ids present: the host list (the K axis) and the device tensor ``unique()`` produced
+        (kept, instead of copying the list back: a host-to-device copy drains the stream)."""
+        memo = self.__dict__.get("_packed_memo")
+        if memo is not None and "classes_both" in memo:
+            return memo["classes_both"]
         dev = self._state_device()
         parts = [cat_states(self._packed(n), dev).reshape(-1).long() for n in ("detection_labels", "groundtruth_labels")]
         labels = torch.cat(parts)
-        return labels.unique().cpu().tolist() if labels.numel() else []
+        if labels.numel():
+            u = labels.unique()
+            out = (u.cpu().tolist(), u)
+        else:
+            out = ([], None)
+        if memo is not None:
+            memo["classes_both"] = out
+        return out
 
     def _state_device(self) -> torch.device:
         for name in ("detection_labels", "groundtruth_labels"):
@@ -281,7 +296,9 @@ class MeanAveragePrecision(Metric):
 
     def _evaluate(self, i_type: str, micro: bool) -> Dict[str, Tensor]:
         dev = self._state_device()
-        classes = torch.tensor(self._get_classes(), dtype=torch.long, device=dev)
+        host_cls, dev_cls = self._classes_both()
+        classes = dev_cls if dev_cls is not None and dev_cls.device == dev else \
+            torch.tensor(host_cls, dtype=torch.long, device=dev)
 
         def relabel(xs):
             if not micro:

@@ -1302,6 +1302,16 @@ def coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, g
                            iou_pre, iou_off)
 
 
+def coco_prepare(classes: Tensor, off: Tensor, d_lab: Tensor, d_score: Tensor, d_box: Tensor, g_lab: Tensor,
+                 g_box: Tensor, g_crowd: Tensor, g_area: Tensor, areas: Tensor, n_img: int, max_det: int,
+                 max_per_image: int) -> List[Tensor]:
+    """COCO grouping stage in one launch (``csrc/detection/coco_prepare.hip``): detections and ground truths in
+    (image, category, score) matcher order with the group tables and the non-ignored ground-truth histogram.  Returns
+    ``[tables int32 [4 G + A K], d_box, d_area, rank, cls, score, key2, g_box, g_area, g_crowd]`` (see the kernel)."""
+    return _ops().coco_prepare(classes, off, d_lab, d_score, d_box, g_lab, g_box, g_crowd, g_area, areas, int(n_img),
+                               int(max_det), int(max_per_image))
+
+
 def coco_accumulate(dt_match: Tensor, dt_ig: Tensor, o: Tensor, rank_s: Tensor, score_s: Tensor, cls_s: Tensor,
                     npig: Tensor, r_thr: Tensor, max_dets: Sequence[int], precision: Tensor, recall: Tensor,
                     scores: Tensor) -> bool:

@@ -161,6 +161,37 @@ __global__ void __launch_bounds__(256) coco_pack_kernel(const uint8_t* __restric
   fpb[i] = fp;
 }
 
+// coco_pack_kernel in accumulation order, fused with the gathers around it: sorted position i takes detection
+// j = o[i] (o: the (category, score) sort permutation of the matcher-order arrays) -- its true / false positive bit
+// words, rank and score -- and the category segment starts seg [K + 1] (seg[c] = first position whose category is
+// >= c; category K = not on the axis, sorted last) come from the boundaries between neighbours.  One launch instead
+// of pack + five gathers + histogram + scan.
+__global__ void __launch_bounds__(256) coco_pack_sorted_kernel(
+    const uint8_t* __restrict__ match, const uint8_t* __restrict__ ig, const int64_t* __restrict__ o,
+    const int64_t* __restrict__ rank_v, const double* __restrict__ score_v, const int64_t* __restrict__ cls_v,
+    long long D, int TA, int K, int64_t* __restrict__ tpb, int64_t* __restrict__ fpb, int64_t* __restrict__ rank_s,
+    double* __restrict__ score_s, int64_t* __restrict__ seg) {
+  const long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= D) return;
+  const long long j = o[i];
+  long long tp = 0, fp = 0;
+  for (int q = 0; q < TA; ++q) {
+    const long long e = static_cast<long long>(q) * D + j;
+    if (ig[e]) continue;
+    if (match[e]) tp |= 1LL << q;
+    else fp |= 1LL << q;
+  }
+  tpb[i] = tp;
+  fpb[i] = fp;
+  rank_s[i] = rank_v[j];
+  score_s[i] = score_v[j];
+  const long long c = cls_v[j];
+  const long long cp = i > 0 ? cls_v[o[i - 1]] : -1;
+  for (long long x = cp + 1; x <= c && x <= K; ++x) seg[x] = i;
+  if (i == D - 1)
+    for (long long x = c + 1; x <= K; ++x) seg[x] = D;
+}
+
 // ------------------------------------------------------------------------------------------------ summary
 // Every number COCOeval.summarize and the per-class mAP / mAR need, from precision [T, R, K, A, M] and recall
 // [T, K, A, M], in ONE launch (it replaced ~10 masked-reduction launches over the 7.7 MB precision tensor plus a
@@ -303,6 +334,43 @@ std::tuple<at::Tensor, at::Tensor> coco_pack_bits(const at::Tensor& match, const
   return {tpb, fpb};
 }
 
+// match / ig uint8 [T, A, D] in matcher order, o int64 [D] the accumulation order, rank / cls int64 and score fp64 [D]
+// in matcher order -> (tpb, fpb, rank, score) in accumulation order and seg int64 [K + 1]
+std::vector<at::Tensor> coco_pack_sorted(const at::Tensor& match, const at::Tensor& ig, const at::Tensor& o,
+                                         const at::Tensor& rank, const at::Tensor& score, const at::Tensor& cls,
+                                         int64_t K) {
+  TM_CHECK_CUDA(match);
+  for (const at::Tensor* x : {&ig, &o, &rank, &score, &cls}) {
+    TM_SAME_DEVICE(match, *x);
+    TM_CHECK_CONTIG(*x);
+  }
+  TM_CHECK_CONTIG(match);
+  TORCH_CHECK(match.scalar_type() == at::kByte && ig.scalar_type() == at::kByte && match.dim() == 3 &&
+                  ig.sizes() == match.sizes(),
+              "coco_pack_sorted: uint8 [T, A, D] flags");
+  const long long TA = match.size(0) * match.size(1), D = match.size(2);
+  TORCH_CHECK(TA <= 63, "coco_pack_sorted: T * A <= 63");
+  TORCH_CHECK(o.scalar_type() == at::kLong && rank.scalar_type() == at::kLong && cls.scalar_type() == at::kLong &&
+                  score.scalar_type() == at::kDouble && o.numel() == D && rank.numel() == D && cls.numel() == D &&
+                  score.numel() == D,
+              "coco_pack_sorted: o / rank / cls int64 [D], score fp64 [D]");
+  auto l = match.options().dtype(at::kLong);
+  at::Tensor tpb = at::empty({D}, l), fpb = at::empty({D}, l), rank_s = at::empty({D}, l);
+  at::Tensor score_s = at::empty({D}, match.options().dtype(at::kDouble));
+  at::Tensor seg = at::empty({K + 1}, l);
+  if (D == 0) {
+    seg.zero_();
+  } else {
+    hipLaunchKernelGGL(coco_pack_sorted_kernel, dim3(static_cast<unsigned>((D + 255) / 256)), dim3(256), 0, stream(),
+                       match.data_ptr<uint8_t>(), ig.data_ptr<uint8_t>(), o.data_ptr<int64_t>(),
+                       rank.data_ptr<int64_t>(), score.data_ptr<double>(), cls.data_ptr<int64_t>(), D,
+                       static_cast<int>(TA), static_cast<int>(K), tpb.data_ptr<int64_t>(), fpb.data_ptr<int64_t>(),
+                       rank_s.data_ptr<int64_t>(), score_s.data_ptr<double>(), seg.data_ptr<int64_t>());
+    C10_HIP_KERNEL_LAUNCH_CHECK();
+  }
+  return {tpb, fpb, rank_s, score_s, seg};
+}
+
 // tpb / fpb int64 [D]: per detection (sorted by category, then score) bit t * A + a set for a true / false positive of
 // (IoU threshold t, area range a); rank int64 [D] (rank within its image and category); score fp64 [D]; seg int64
 // [K + 1]; npig fp64 [A, K]; r_thr fp64 [R]; max_dets int64 [M] (CPU); outputs fp64 precision / scores [T, R, K, A, M],
@@ -393,6 +461,7 @@ at::Tensor coco_summary(const at::Tensor& prec, const at::Tensor& rec, const at:
 
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
   m.def("coco_pack_bits(Tensor match, Tensor ig) -> (Tensor, Tensor)");
+  m.def("coco_pack_sorted(Tensor match, Tensor ig, Tensor o, Tensor rank, Tensor score, Tensor cls, int K) -> Tensor[]");
   m.def("coco_summary(Tensor prec, Tensor rec, Tensor cprec, Tensor crec, int m_ap) -> Tensor");
   m.def(
       "coco_accumulate(Tensor tpb, Tensor fpb, Tensor rank, Tensor score, Tensor seg, Tensor npig, Tensor r_thr, "
@@ -400,6 +469,7 @@ TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
 }
 TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
   m.impl("coco_pack_bits", &coco_pack_bits);
+  m.impl("coco_pack_sorted", &coco_pack_sorted);
   m.impl("coco_accumulate", &coco_accumulate);
   m.impl("coco_summary", &coco_summary);
 }

@@ -504,6 +504,7 @@ def test_coco_accumulate_kernel_matches_torch_path(monkeypatch):
 
     fused = run()
     monkeypatch.setattr(ops, "coco_accumulate", lambda *a, **k: False)
+    monkeypatch.setattr(ops, "coco_accumulate_sorted", lambda *a, **k: False)
     ref = run()
     for key in ("precision", "recall", "scores", "map", "map_per_class", "mar_50_per_class", "mar_small"):
         assert torch.equal(fused[key], ref[key]), key

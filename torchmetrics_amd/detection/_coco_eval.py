@@ -15,6 +15,7 @@ detections sorted by (category, score) for all thresholds / areas at once, a seg
 envelope and one ``searchsorted`` + scatter per max-dets; (4) the summary is four masked reductions crossing to the
 host in one transfer.
 """
+from itertools import accumulate
 from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import torch
@@ -332,7 +333,8 @@ def _evaluate_prepared(det_boxes, det_scores, det_labels, gt_boxes, gt_labels, g
     than ``PREP_MAX_PER_IMAGE`` annotations, non-integer labels / crowds."""
     dev = classes.device
     n_img = len(d_sizes)
-    if n_img == 0 or max(max(d_sizes, default=0), max(g_sizes, default=0)) > PREP_MAX_PER_IMAGE:
+    biggest = max(max(d_sizes, default=0), max(g_sizes, default=0))
+    if n_img == 0 or biggest > PREP_MAX_PER_IMAGE:
         return False
     d_lab = cat_states(det_labels, dev).reshape(-1)
     g_lab = cat_states(gt_labels, dev).reshape(-1)
@@ -348,33 +350,23 @@ def _evaluate_prepared(det_boxes, det_scores, det_labels, gt_boxes, gt_labels, g
     if d_score.dtype not in floats[:1] + floats[2:] or any(t.dtype not in ints for t in (d_lab, g_lab, g_crowd)) or \
             any(t.dtype not in floats for t in (d_box, g_box, g_area)):
         return False
-    off = [0] * (2 * (n_img + 1))
-    acc = 0
-    for i, v in enumerate(d_sizes):
-        acc += v
-        off[i + 1] = acc
-    acc = 0
-    for i, v in enumerate(g_sizes):
-        acc += v
-        off[n_img + 2 + i] = acc
+    off = [0, *accumulate(d_sizes), 0, *accumulate(g_sizes)]
     K, A = classes.numel(), areas.shape[0]
     G = n_img * K
     (tables, d_box_s, d_area_s, rank_v, cls_k, score_k, key2, g_box_s, g_area_s,
      g_crowd_s) = ops.coco_prepare(classes, _to_device_async(off, dev), d_lab.contiguous(), d_score.contiguous(),
                                    d_box.contiguous(), g_lab.contiguous(), g_box.contiguous(), g_crowd.contiguous(),
-                                   g_area.contiguous(), areas.reshape(-1), n_img, int(max_dets[-1]),
-                                   max(max(d_sizes, default=0), max(g_sizes, default=0)))
+                                   g_area.contiguous(), areas.reshape(-1), n_img, int(max_dets[-1]), biggest)
     dt_match, dt_ig = ops.coco_match(d_box_s, d_area_s, g_box_s, g_area_s, g_crowd_s, tables[:G], tables[G:2 * G],
                                      tables[2 * G:3 * G], tables[3 * G:4 * G], areas.reshape(-1), t_thr, None, None)
     npig = tables[4 * G:].reshape(A, K).to(torch.float64)
     # (3) accumulate: detections of each category in score order (ties: image, then rank -- the prepared order);
     # categories not on the K axis carry index K and sort last
     o = torch.sort(key2, stable=True).indices
-    cls_s, rank_s, score_s = cls_k[o], rank_v[o], score_k[o]
     # (where the accumulation kernel does not apply -- T * A > 63, more than 8 max-dets values, no detections -- the
     # caller's ATen path runs from the start)
-    return ops.coco_accumulate(dt_match, dt_ig, o, rank_s, score_s, cls_s, npig, r_thr, max_dets, precision, recall,
-                               scores_out)
+    return ops.coco_accumulate_sorted(dt_match, dt_ig, o, rank_v, score_k, cls_k, npig, r_thr, max_dets, precision,
+                                      recall, scores_out)
 
 
 def _masked_mean(s: Tensor) -> Tensor:

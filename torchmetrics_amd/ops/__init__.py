@@ -1335,6 +1335,24 @@ def coco_accumulate(dt_match: Tensor, dt_ig: Tensor, o: Tensor, rank_s: Tensor, 
     return True
 
 
+def coco_accumulate_sorted(dt_match: Tensor, dt_ig: Tensor, o: Tensor, rank_v: Tensor, score_v: Tensor,
+                           cls_v: Tensor, npig: Tensor, r_thr: Tensor, max_dets: Sequence[int], precision: Tensor,
+                           recall: Tensor, scores: Tensor) -> bool:
+    """:func:`coco_accumulate` from matcher-order ``rank_v`` / ``score_v`` / ``cls_v`` and the accumulation order ``o``:
+    the bit packing, the gathers and the category segments in ONE launch (``coco_pack_sorted``), then the
+    accumulation kernel.  False (nothing written) where the kernel does not apply."""
+    T, A, n = dt_match.shape
+    K = npig.shape[1]
+    if not dt_match.is_cuda or T * A > 63 or len(max_dets) > 8 or n == 0:
+        return False
+    tpb, fpb, rank_s, score_s, seg = _ops().coco_pack_sorted(dt_match.contiguous(), dt_ig.contiguous(), o.contiguous(),
+                                                             rank_v.contiguous(), score_v.contiguous(),
+                                                             cls_v.contiguous(), int(K))
+    _ops().coco_accumulate(tpb, fpb, rank_s, score_s, seg, npig.contiguous(), r_thr.contiguous(),
+                           torch.tensor(list(max_dets), dtype=torch.int64), int(T), precision, recall, scores)
+    return True
+
+
 def coco_summary(prec: Tensor, rec: Tensor, cprec: Tensor, crec: Tensor, m_ap: int) -> Optional[Tensor]:
     """Every sum COCO's summary and per-class numbers need, in one launch (``csrc/detection/coco_accumulate.hip``
     coco_summary_kernel): an fp64 vector ``[psp, pcp]`` (``[T, ceil(K / 4), A*M]``: partial sums / counts of the defined

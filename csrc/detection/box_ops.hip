@@ -365,9 +365,13 @@ std::tuple<at::Tensor, at::Tensor> coco_match(const at::Tensor& dbox, const at::
   const int groups = static_cast<int>(det_start.numel());
   const int num_area = static_cast<int>(area_rng.numel() / 2), num_thr = static_cast<int>(iou_thr.numel());
   auto opts = dbox.options().dtype(at::kByte);
-  at::Tensor dt_match = at::zeros({num_thr, num_area, num_det}, opts);
-  at::Tensor dt_ig = at::zeros({num_thr, num_area, num_det}, opts);
-  at::Tensor used = at::zeros({static_cast<long long>(num_thr) * num_area * std::max(num_gt, 1)}, opts);
+  // the two flag arrays and the matcher's "ground truth used" scratch from ONE zero-filled allocation (one fill
+  // launch instead of three: compute() is launch-bound)
+  const long long tad = static_cast<long long>(num_thr) * num_area * num_det;
+  at::Tensor zbuf = at::zeros({2 * tad + static_cast<long long>(num_thr) * num_area * std::max(num_gt, 1)}, opts);
+  at::Tensor dt_match = zbuf.narrow(0, 0, tad).view({num_thr, num_area, num_det});
+  at::Tensor dt_ig = zbuf.narrow(0, tad, tad).view({num_thr, num_area, num_det});
+  at::Tensor used = zbuf.narrow(0, 2 * tad, zbuf.numel() - 2 * tad);
   const bool pre = iou_pre.has_value() && iou_pre->defined();
   if (pre) {
     TORCH_CHECK(iou_off.has_value() && iou_off->scalar_type() == at::kLong && iou_off->numel() == groups,

@@ -173,6 +173,64 @@ __global__ void __launch_bounds__(kPrepThreads) coco_prepare_kernel(PrepArgs a) 
   }
 }
 
+// Sorted distinct values of two integer label arrays in [0, kUniqRange), in ONE single-block launch (the K axis of
+// every COCO evaluation: torch.unique was a radix sort + merges + a partition, ~15 launches): an LDS bitmap of the
+// range, then a block scan of the words' popcounts writes the values in order.  out int64 [1 + kUniqMax]: out[0] =
+// the count, or -1 when a value is outside the range, -2 when more than kUniqMax values are distinct (the caller
+// falls back to torch.unique).
+constexpr int kUniqRange = 1 << 16;
+constexpr int kUniqMax = 4096;
+constexpr int kUniqThreads = 1024;
+
+__global__ void __launch_bounds__(kUniqThreads) small_unique_kernel(const void* __restrict__ a, int acode,
+                                                                    long long na, const void* __restrict__ b,
+                                                                    int bcode, long long nb,
+                                                                    int64_t* __restrict__ out) {
+  constexpr int kWords = kUniqRange / 32;
+  constexpr int kPer = kWords / kUniqThreads;  // bitmap words per thread in the compaction
+  __shared__ uint32_t bits[kWords];
+  __shared__ int scan[kUniqThreads];
+  __shared__ int bad;
+  const int tid = threadIdx.x;
+  for (int w = tid; w < kWords; w += kUniqThreads) bits[w] = 0u;
+  if (tid == 0) bad = 0;
+  __syncthreads();
+  for (long long i = tid; i < na + nb; i += kUniqThreads) {
+    const long long v = i < na ? ld_i(a, acode, i) : ld_i(b, bcode, i - na);
+    if (v < 0 || v >= kUniqRange) bad = 1;
+    else atomicOr(&bits[v >> 5], 1u << (v & 31));
+  }
+  __syncthreads();
+  if (bad) {
+    if (tid == 0) out[0] = -1;
+    return;
+  }
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) cnt += __popc(bits[tid * kPer + k]);
+  scan[tid] = cnt;
+  __syncthreads();
+  for (int off = 1; off < kUniqThreads; off <<= 1) {  // inclusive Hillis-Steele scan of the popcounts
+    const int v = tid >= off ? scan[tid - off] : 0;
+    __syncthreads();
+    scan[tid] += v;
+    __syncthreads();
+  }
+  const int total = scan[kUniqThreads - 1];
+  if (tid == 0) out[0] = total > kUniqMax ? -2 : total;
+  if (total > kUniqMax) return;
+  int pos = scan[tid] - cnt;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    uint32_t w = bits[tid * kPer + k];
+    while (w) {
+      const int bit = __ffs(w) - 1;
+      w &= w - 1;
+      out[1 + pos++] = static_cast<long long>(tid * kPer + k) * 32 + bit;
+    }
+  }
+}
+
 int float_code(const at::Tensor& t) {
   switch (t.scalar_type()) {
     case at::kFloat: return kF32;
@@ -274,12 +332,29 @@ std::vector<at::Tensor> coco_prepare(const at::Tensor& classes, const at::Tensor
   return {tables, o_dbox, o_darea, o_rank, o_cls, o_score, o_key2, o_gbox, o_garea, o_gcrowd};
 }
 
+// a, b: integer label arrays on one device -> int64 [1 + kUniqMax] (see small_unique_kernel)
+at::Tensor small_unique(const at::Tensor& a, const at::Tensor& b) {
+  TM_CHECK_CUDA(a);
+  TM_SAME_DEVICE(a, b);
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous(), "small_unique: contiguous inputs expected");
+  at::Tensor out = at::empty({1 + kUniqMax}, a.options().dtype(at::kLong));
+  hipLaunchKernelGGL(small_unique_kernel, dim3(1), dim3(kUniqThreads), 0, stream(), a.data_ptr(), int_code(a),
+                     static_cast<long long>(a.numel()), b.data_ptr(), int_code(b), static_cast<long long>(b.numel()),
+                     out.data_ptr<int64_t>());
+  C10_HIP_KERNEL_LAUNCH_CHECK();
+  return out;
+}
+
 TORCH_LIBRARY_FRAGMENT(tm_amd, m) {
+  m.def("small_unique(Tensor a, Tensor b) -> Tensor");
   m.def(
       "coco_prepare(Tensor classes, Tensor off, Tensor d_lab, Tensor d_score, Tensor d_box, Tensor g_lab, "
       "Tensor g_box, Tensor g_crowd, Tensor g_area, Tensor areas, int n_img, int max_det, int max_per_image) "
       "-> Tensor[]");
 }
-TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) { m.impl("coco_prepare", &coco_prepare); }
+TORCH_LIBRARY_IMPL(tm_amd, CUDA, m) {
+  m.impl("coco_prepare", &coco_prepare);
+  m.impl("small_unique", &small_unique);
+}
 
 }  // namespace tm_amd

@@ -696,3 +696,27 @@ def test_map_native_pack_declines_irregular_batches():
         MeanAveragePrecision().to(dev).update(short, t)
     cpu = [{k: v.cpu() for k, v in d.items()} for d in p]
     assert ops.map_pack(cpu, [{k: v.cpu() for k, v in d.items()} for d in t], 1) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt_a,dt_b", [(torch.int64, torch.int64), (torch.int32, torch.int64), (torch.uint8, torch.int16)])
+def test_small_unique_kernel_matches_torch_unique(dt_a, dt_b):
+    """ops.small_unique (one-block LDS bitmap + scan, csrc/detection/coco_prepare.hip) equals torch.unique of the
+    concatenation; values outside [0, 65536) or more than 4096 distinct values decline (None)."""
+    g = torch.Generator().manual_seed(7)
+    hi_a = 200 if dt_a == torch.uint8 else 60000
+    a = torch.randint(0, hi_a, (70_000,), generator=g).to(dt_a)
+    b = torch.randint(0, 3000, (513,), generator=g).to(dt_b)
+    b[:5] = torch.tensor([0, 1, 2, 2, 2999], dtype=dt_b)
+    a_small = a[:3000]
+    ref = torch.unique(torch.cat([a_small.long(), b.long()]))
+    got = ops.small_unique(a_small.cuda(), b.cuda())
+    assert got is not None
+    assert got[0] == ref.tolist() and torch.equal(got[1].cpu(), ref)
+    if dt_a != torch.uint8:
+        assert ops.small_unique(a.cuda(), b.cuda()) is None  # > 4096 distinct values
+    neg = b.clone()
+    neg[7] = -1 if dt_b != torch.uint8 else 0
+    if dt_b != torch.uint8:
+        assert ops.small_unique(a_small.cuda(), neg.cuda()) is None  # outside the range
+    assert ops.small_unique(a_small, b) is None  # CPU

@@ -268,13 +268,18 @@ class MeanAveragePrecision(Metric):
         if memo is not None and "classes_both" in memo:
             return memo["classes_both"]
         dev = self._state_device()
-        parts = [cat_states(self._packed(n), dev).reshape(-1).long() for n in ("detection_labels", "groundtruth_labels")]
-        labels = torch.cat(parts)
-        if labels.numel():
-            u = labels.unique()
-            out = (u.cpu().tolist(), u)
+        parts = [cat_states(self._packed(n), dev).reshape(-1) for n in ("detection_labels", "groundtruth_labels")]
+        # ROCm: one bitmap launch (labels in [0, 65536)); else torch.unique of the concatenation
+        fast = ops.small_unique(parts[0], parts[1]) if parts[0].numel() + parts[1].numel() else None
+        if fast is not None:
+            out = fast
         else:
-            out = ([], None)
+            labels = torch.cat([p.long() for p in parts])
+            if labels.numel():
+                u = labels.unique()
+                out = (u.cpu().tolist(), u)
+            else:
+                out = ([], None)
         if memo is not None:
             memo["classes_both"] = out
         return out

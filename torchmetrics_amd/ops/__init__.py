@@ -1302,6 +1302,20 @@ def coco_match(dbox, darea, gbox, garea, gcrowd, det_start, det_cnt, gt_start, g
                            iou_pre, iou_off)
 
 
+def small_unique(a: Tensor, b: Tensor) -> Optional[Tuple[List[int], Tensor]]:
+    """Sorted distinct values of two integer label tensors (ROCm, values in [0, 65536), at most 4096 of them) with ONE
+    launch and one device->host copy (``csrc/detection/coco_prepare.hip`` small_unique_kernel): ``(host list, device
+    int64 tensor)``; None where it does not apply (the caller takes ``torch.unique``)."""
+    if not a.is_cuda or a.dtype.is_floating_point or b.dtype.is_floating_point or b.device != a.device:
+        return None
+    out = _ops().small_unique(a.reshape(-1).contiguous(), b.reshape(-1).contiguous())
+    host = out.cpu()
+    n = int(host[0])
+    if n < 0:
+        return None
+    return host[1:1 + n].tolist(), out[1:1 + n]
+
+
 def coco_prepare(classes: Tensor, off: Tensor, d_lab: Tensor, d_score: Tensor, d_box: Tensor, g_lab: Tensor,
                  g_box: Tensor, g_crowd: Tensor, g_area: Tensor, areas: Tensor, n_img: int, max_det: int,
                  max_per_image: int) -> List[Tensor]:

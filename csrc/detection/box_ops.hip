@@ -209,6 +209,10 @@ __global__ void __launch_bounds__(256) coco_match_kernel(
   const double thr = min(iou_thr[t], 1.0 - 1e-10);
   const long long plane_d = static_cast<long long>(t * num_area + a) * num_det;
   uint8_t* used = gt_used + static_cast<long long>(t * num_area + a) * num_gt;
+  // groups of <= 64 ground truths (the usual case) keep the "already matched" flags in a register bitmask: no global
+  // store -> load round trip between consecutive detections of the greedy loop
+  const bool small = gn <= 64;
+  unsigned long long used_bits = 0ull;
   for (int k = 0; k < dn; ++k) {
     const int di = d0 + k;
     const double* db = dbox + 4LL * di;
@@ -220,7 +224,7 @@ __global__ void __launch_bounds__(256) coco_match_kernel(
       const int gi = g0 + j;
       const bool crowd = gcrowd[gi] != 0;
       const bool ig = crowd || garea[gi] < lo || garea[gi] > hi;
-      if (ig || used[gi]) continue;
+      if (ig || (small ? ((used_bits >> j) & 1ull) != 0 : used[gi] != 0)) continue;
       const double v = iou_pre ? iou_pre[iou_off[grp] + static_cast<long long>(k) * gn + j]
                                : coco_iou(db, gbox + 4LL * gi, false);
       if (v < best) continue;
@@ -232,7 +236,8 @@ __global__ void __launch_bounds__(256) coco_match_kernel(
         const int gi = g0 + j;
         const bool crowd = gcrowd[gi] != 0;
         const bool ig = crowd || garea[gi] < lo || garea[gi] > hi;
-        if (!ig || (used[gi] && !crowd)) continue;
+        const bool u = small ? ((used_bits >> j) & 1ull) != 0 : used[gi] != 0;
+        if (!ig || (u && !crowd)) continue;
         const double v = iou_pre ? iou_pre[iou_off[grp] + static_cast<long long>(k) * gn + j]
                                  : coco_iou(db, gbox + 4LL * gi, crowd);
         if (v < best) continue;
@@ -242,7 +247,8 @@ __global__ void __launch_bounds__(256) coco_match_kernel(
       }
     }
     if (m >= 0) {
-      used[m] = 1;
+      if (small) used_bits |= 1ull << (m - g0);
+      else used[m] = 1;
       dt_match[plane_d + di] = 1;
       dt_ig[plane_d + di] = m_ig ? 1 : 0;
     } else {
